@@ -1,0 +1,28 @@
+// `peasoup` command-line entry point (src/pipeline_multi.cu:262-419 main()).
+#include <iostream>
+
+#include "psoup/cli.hpp"
+#include "psoup/common.hpp"
+#include "psoup/pipeline.hpp"
+
+int main(int argc, char** argv) {
+  psoup::CmdLineOptions args;
+  bool exit_now = false;
+  if (!psoup::parse_cmdline(args, argc, argv, &exit_now)) {
+    std::cerr << "Failed to parse command line arguments." << std::endl;
+    return 1;
+  }
+  if (exit_now) return 0;
+  try {
+    psoup::PipelineResult res = psoup::run_pipeline(args);
+    psoup::write_outputs(args, res);
+    if (args.verbose || args.progress_bar) {
+      std::cout << "Wrote " << res.candidates.size() << " candidates to " << args.outdir << std::endl;
+      std::cout << "DMxaccel trials/s: " << res.performance["dm_accel_trials_per_sec"] << std::endl;
+    }
+  } catch (const std::exception& e) {
+    std::cerr << "peasoup: error: " << e.what() << std::endl;
+    return 2;
+  }
+  return 0;
+}

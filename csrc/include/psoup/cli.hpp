@@ -1,0 +1,81 @@
+// Command-line options.
+//
+// Parity: include/utils/cmdline.hpp:6-209 (CmdLineOptions + TCLAP parser with
+// 25 options and their defaults; -h/--help and --version "1.0" come from
+// TCLAP) and src/coincidencer.cpp:31-98 (coincidencer options).  The parser
+// is a small in-repo replacement for the vendored TCLAP (no vendoring).
+// Extra MI355X options are long-only and default to the reference behaviour
+// except where noted.
+#pragma once
+
+#include <string>
+#include <vector>
+
+namespace psoup {
+
+struct CmdLineOptions {
+  std::string infilename;
+  std::string outdir;
+  std::string killfilename;
+  std::string zapfilename;
+  int max_num_threads = 14;
+  int limit = 1000;
+  unsigned int size = 0;
+  float dm_start = 0.0f;
+  float dm_end = 100.0f;
+  float dm_tol = 1.10f;
+  float dm_pulse_width = 64.0f;
+  float acc_start = 0.0f;
+  float acc_end = 0.0f;
+  float acc_tol = 1.10f;
+  float acc_pulse_width = 64.0f;
+  float boundary_5_freq = 0.05f;
+  float boundary_25_freq = 0.5f;
+  int nharmonics = 4;
+  int npdmp = 0;
+  float min_snr = 9.0f;
+  float min_freq = 0.1f;
+  float max_freq = 1100.0f;
+  int max_harm = 16;
+  float freq_tol = 0.0001f;
+  bool verbose = false;
+  bool progress_bar = false;
+
+  // ---- MI355X-native extensions (long options only) ----
+  std::string accel_convention = "legacy";  // legacy | reference
+  std::string dedisp_kernel = "auto";       // auto | mfma | direct
+  int accel_batch = 0;                      // 0 = auto (sized for HBM)
+  bool use_boundaries = false;              // honour --boundary_* (reference ignores them)
+  std::string checkpoint_dir;               // per-DM candidate spill + resume
+  std::string trace_json;                   // optional per-stage JSON trace
+  int fault_after_dms = -1;                 // fault injection (testing)
+};
+
+// Returns false on a parse error (message printed to stderr).  Sets
+// *exit_now (and returns true) for --help / --version.
+bool parse_cmdline(CmdLineOptions& args, int argc, const char* const* argv, bool* exit_now = nullptr);
+bool parse_cmdline(CmdLineOptions& args, const std::vector<std::string>& argv, bool* exit_now = nullptr);
+std::string cmdline_usage();
+
+// Default outdir: "./%Y-%m-%d-%H:%M_peasoup/" in UTC (cmdline.hpp:53-59).
+std::string default_outdir();
+
+struct CoincidencerOptions {
+  std::vector<std::string> filterbanks;
+  std::string samp_outfilename = "rfi.eb_mask";
+  std::string spec_outfilename = "birdies.txt";
+  float boundary_5_freq = 0.05f;
+  float boundary_25_freq = 0.5f;
+  int nharmonics = 4;
+  float threshold = 4.0f;
+  int beam_threshold = 4;
+  float min_freq = 0.1f;
+  float max_freq = 1100.0f;
+  int max_harm = 16;
+  float freq_tol = 0.0001f;
+  bool verbose = false;
+};
+bool parse_coincidencer_cmdline(CoincidencerOptions& args, int argc, const char* const* argv,
+                                bool* exit_now = nullptr);
+
+}  // namespace psoup

@@ -1,0 +1,290 @@
+// L0 platform layer: error propagation, RAII device/pinned buffers, timers,
+// roctx ranges and rank-prefixed logging.
+//
+// Parity notes (reference -> here):
+//   include/utils/exceptions.hpp:13-153  ErrorChecker (syncs after EVERY call)
+//       -> PSOUP_HIP_CHECK / PSOUP_ROCFFT_CHECK: throw with file:line + rank
+//          context and never synchronise; PSOUP_DEBUG_SYNC=1 restores the
+//          sync-after-launch behaviour for debugging.
+//   include/utils/utils.hpp:20-80  Utils::device_malloc/h2dcpy/...
+//       -> DeviceBuffer<T>/PinnedBuffer<T> (RAII, async copies on a stream).
+//   include/utils/stopwatch.hpp:9-142  Stopwatch (gettimeofday, seconds)
+//       -> Stopwatch (steady_clock, seconds, accumulating) + GpuTimer.
+//   include/utils/nvtx.hpp:1-24  PUSH/POP_NVTX_RANGE -> RoctxRange (roctx).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace psoup {
+
+// ---------------------------------------------------------------- errors ----
+class Error : public std::runtime_error {
+ public:
+  explicit Error(const std::string& msg) : std::runtime_error(msg) {}
+};
+
+int log_rank();                 // rank used as log prefix (-1 = none)
+void set_log_rank(int rank);
+bool debug_sync_enabled();      // PSOUP_DEBUG_SYNC env var
+
+[[noreturn]] void throw_error(const std::string& what, const char* file, int line);
+
+#define PSOUP_THROW(msg)                                                   \
+  do {                                                                     \
+    std::ostringstream _psoup_os;                                          \
+    _psoup_os << msg;                                                      \
+    ::psoup::throw_error(_psoup_os.str(), __FILE__, __LINE__);             \
+  } while (0)
+
+#define PSOUP_CHECK(cond, msg)                                             \
+  do {                                                                     \
+    if (!(cond)) PSOUP_THROW("check failed: " #cond ": " << msg);          \
+  } while (0)
+
+#define PSOUP_HIP_CHECK(expr)                                              \
+  do {                                                                     \
+    hipError_t _psoup_e = (expr);                                          \
+    if (_psoup_e != hipSuccess)                                            \
+      PSOUP_THROW("HIP error " << hipGetErrorName(_psoup_e) << " ("        \
+                               << hipGetErrorString(_psoup_e)              \
+                               << ") in " #expr);                          \
+  } while (0)
+
+// Called after each kernel launch: catches launch-configuration errors
+// without a device sync; in debug mode also synchronises the stream so the
+// faulting kernel is named.
+void post_launch_check(const char* kernel, hipStream_t stream);
+
+// ---------------------------------------------------------------- logging ---
+enum class LogLevel { Quiet = 0, Info = 1, Verbose = 2 };
+void set_log_level(LogLevel lvl);
+LogLevel log_level();
+void log_info(const std::string& msg);
+void log_verbose(const std::string& msg);
+
+// ---------------------------------------------------------------- buffers ---
+template <class T>
+class DeviceBuffer {
+ public:
+  DeviceBuffer() = default;
+  explicit DeviceBuffer(size_t n) { resize(n); }
+  ~DeviceBuffer() { release(); }
+  DeviceBuffer(const DeviceBuffer&) = delete;
+  DeviceBuffer& operator=(const DeviceBuffer&) = delete;
+  DeviceBuffer(DeviceBuffer&& o) noexcept : ptr_(o.ptr_), n_(o.n_), cap_(o.cap_) {
+    o.ptr_ = nullptr;
+    o.n_ = o.cap_ = 0;
+  }
+  DeviceBuffer& operator=(DeviceBuffer&& o) noexcept {
+    if (this != &o) {
+      release();
+      ptr_ = o.ptr_;
+      n_ = o.n_;
+      cap_ = o.cap_;
+      o.ptr_ = nullptr;
+      o.n_ = o.cap_ = 0;
+    }
+    return *this;
+  }
+  // Grows (never shrinks) the allocation; contents are not preserved.
+  void resize(size_t n) {
+    if (n <= cap_) {
+      n_ = n;
+      return;
+    }
+    release();
+    if (n > 0) PSOUP_HIP_CHECK(hipMalloc(reinterpret_cast<void**>(&ptr_), n * sizeof(T)));
+    n_ = cap_ = n;
+  }
+  void release() {
+    if (ptr_) (void)hipFree(ptr_);
+    ptr_ = nullptr;
+    n_ = cap_ = 0;
+  }
+  void zero_async(hipStream_t s) {
+    if (n_) PSOUP_HIP_CHECK(hipMemsetAsync(ptr_, 0, n_ * sizeof(T), s));
+  }
+  T* data() const { return ptr_; }
+  size_t size() const { return n_; }
+  size_t bytes() const { return n_ * sizeof(T); }
+
+ private:
+  T* ptr_ = nullptr;
+  size_t n_ = 0;
+  size_t cap_ = 0;
+};
+
+template <class T>
+class PinnedBuffer {
+ public:
+  PinnedBuffer() = default;
+  explicit PinnedBuffer(size_t n) { resize(n); }
+  ~PinnedBuffer() { release(); }
+  PinnedBuffer(const PinnedBuffer&) = delete;
+  PinnedBuffer& operator=(const PinnedBuffer&) = delete;
+  void resize(size_t n) {
+    if (n <= cap_) {
+      n_ = n;
+      return;
+    }
+    release();
+    if (n > 0) PSOUP_HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&ptr_), n * sizeof(T), hipHostMallocDefault));
+    n_ = cap_ = n;
+  }
+  void release() {
+    if (ptr_) (void)hipHostFree(ptr_);
+    ptr_ = nullptr;
+    n_ = cap_ = 0;
+  }
+  T* data() const { return ptr_; }
+  size_t size() const { return n_; }
+  T& operator[](size_t i) { return ptr_[i]; }
+  const T& operator[](size_t i) const { return ptr_[i]; }
+
+ private:
+  T* ptr_ = nullptr;
+  size_t n_ = 0;
+  size_t cap_ = 0;
+};
+
+// RAII stream / event owners.
+class Stream {
+ public:
+  Stream() { PSOUP_HIP_CHECK(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking)); }
+  ~Stream() {
+    if (s_) (void)hipStreamDestroy(s_);
+  }
+  Stream(const Stream&) = delete;
+  Stream& operator=(const Stream&) = delete;
+  hipStream_t get() const { return s_; }
+
+ private:
+  hipStream_t s_ = nullptr;
+};
+
+class Event {
+ public:
+  explicit Event(bool timing = false) {
+    PSOUP_HIP_CHECK(hipEventCreateWithFlags(&e_, timing ? hipEventDefault : hipEventDisableTiming));
+  }
+  ~Event() {
+    if (e_) (void)hipEventDestroy(e_);
+  }
+  Event(const Event&) = delete;
+  Event& operator=(const Event&) = delete;
+  void record(hipStream_t s) { PSOUP_HIP_CHECK(hipEventRecord(e_, s)); }
+  void sync() { PSOUP_HIP_CHECK(hipEventSynchronize(e_)); }
+  hipEvent_t get() const { return e_; }
+
+ private:
+  hipEvent_t e_ = nullptr;
+};
+
+// ---------------------------------------------------------------- timers ----
+// Accumulating wall-clock stopwatch; get_time() returns SECONDS (the
+// reference's Stopwatch::getTime also returns seconds despite its comment).
+class Stopwatch {
+ public:
+  void start() {
+    t0_ = clock::now();
+    running_ = true;
+  }
+  void stop() {
+    if (running_) acc_ += std::chrono::duration<double>(clock::now() - t0_).count();
+    running_ = false;
+  }
+  void reset() {
+    acc_ = 0.0;
+    running_ = false;
+  }
+  double get_time() const {
+    double t = acc_;
+    if (running_) t += std::chrono::duration<double>(clock::now() - t0_).count();
+    return t;
+  }
+
+ private:
+  using clock = std::chrono::steady_clock;
+  clock::time_point t0_{};
+  double acc_ = 0.0;
+  bool running_ = false;
+};
+
+// GPU-side interval timer (hipEvent pair), accumulates milliseconds.
+class GpuTimer {
+ public:
+  GpuTimer() : a_(true), b_(true) {}
+  void start(hipStream_t s) { a_.record(s); }
+  void stop(hipStream_t s) {
+    b_.record(s);
+    pending_ = true;
+  }
+  double elapsed_ms() {
+    if (pending_) {
+      b_.sync();
+      float ms = 0.f;
+      PSOUP_HIP_CHECK(hipEventElapsedTime(&ms, a_.get(), b_.get()));
+      acc_ += ms;
+      pending_ = false;
+    }
+    return acc_;
+  }
+
+ private:
+  Event a_, b_;
+  bool pending_ = false;
+  double acc_ = 0.0;
+};
+
+// --------------------------------------------------------------- roctx ------
+// Named ranges visible in rocprofv3 --marker-trace (same names as the
+// reference's NVTX ranges: "Dedisperse", "DM-Loop", "Acceleration-Loop",
+// "Harmonic summing").
+class RoctxRange {
+ public:
+  explicit RoctxRange(const char* name);
+  ~RoctxRange();
+  RoctxRange(const RoctxRange&) = delete;
+  RoctxRange& operator=(const RoctxRange&) = delete;
+
+ private:
+  bool active_;
+};
+
+void roctx_push(const char* name);
+void roctx_pop();
+
+// ---------------------------------------------------------------- device ----
+struct DeviceInfo {
+  int id = 0;
+  std::string name;
+  std::string arch;  // gcnArchName, e.g. gfx950:sramecc+:xnack-
+  int major = 0;
+  int minor = 0;
+  int multiprocessors = 0;
+  size_t total_mem = 0;
+};
+int device_count();
+DeviceInfo device_info(int device);
+int runtime_version();
+int driver_version();
+
+// Largest power of two STRICTLY less than val (reference utils.hpp:12-18:
+// `while (n*2 < val) n *= 2`), so an exact 2^k input yields 2^(k-1).
+inline uint64_t prev_power_of_two(uint64_t val) {
+  uint64_t n = 1;
+  while (n * 2 < val) n *= 2;
+  return n;
+}
+
+}  // namespace psoup

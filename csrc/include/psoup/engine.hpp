@@ -1,0 +1,260 @@
+// Per-GPU engine: resident filterbank, dedispersion, whitening, batched
+// acceleration search, candidate folding, coincidence masks.
+//
+// Parity (reference -> here):
+//   Dedisperser (dedisperser.hpp:12-114, external dedisp)  -> DeviceFilterbank + Dedisperser
+//   Worker::start (pipeline_multi.cu:100-252), one accel trial at a time with a
+//     device sync after every kernel                       -> SearchEngine::search_trial
+//     (whitening fused into 5 kernels; K accelerations per batched rocFFT;
+//      fused harmonic-sum/peak kernel; peak lists copied on a second stream
+//      while the next batch computes; host clustering/distillation overlapped)
+//   Dereddener/Zapper/SpectrumFormer                       -> Whitener
+//   MultiFolder/TimeSeriesFolder/FoldOptimiser (folder.hpp) -> FoldEngine
+//   Coincidencer (coincidencer.hpp)                         -> beam_indicator + coincidence
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "psoup/candidates.hpp"
+#include "psoup/common.hpp"
+#include "psoup/fft.hpp"
+#include "psoup/kernels.hpp"
+#include "psoup/plan.hpp"
+#include "psoup/sigproc.hpp"
+
+namespace psoup {
+
+enum class DedispKernel { Auto = 0, Direct = 1, Mfma = 2 };
+DedispKernel parse_dedisp_kernel(const std::string& s);
+
+// Geometry shared by every rank: DM list, delays, killmask, output length.
+struct DedispGeometry {
+  int nchans = 0;
+  int nbits = 0;
+  double tsamp = 0, fch1 = 0, foff = 0;
+  uint64_t nsamps = 0;
+  std::vector<float> dm_list;
+  std::vector<float> delays;
+  std::vector<int> killmask;
+  int max_delay = 0;
+  uint64_t out_nsamps = 0;
+  float out_scale = 1.f;
+  int bias = 0;
+  int nactive = 0;
+  static DedispGeometry make(const SigprocHeader& hdr, uint64_t nsamps, const std::vector<float>& dm_list,
+                             const std::vector<int>& killmask);
+  // int32 [ndm][nchans] sample offsets for DMs [d0, d1)
+  std::vector<int32_t> offsets(int d0, int d1) const;
+};
+
+// Channel-major int8 filterbank resident in HBM.
+class DeviceFilterbank {
+ public:
+  DeviceFilterbank(const DedispGeometry& g, hipStream_t stream);
+  // Packed (SIGPROC layout) bytes already on this device (e.g. after an RCCL broadcast).
+  void load_packed_device(const uint8_t* d_packed);
+  // Packed bytes in host memory (H2D in chunks through pinned staging).
+  void load_packed_host(const uint8_t* h_packed);
+  const int8_t* data() const { return chan_.data(); }
+  uint64_t stride() const { return stride_; }
+  const DedispGeometry& geometry() const { return g_; }
+
+ private:
+  DedispGeometry g_;
+  hipStream_t stream_;
+  uint64_t stride_;
+  DeviceBuffer<int8_t> chan_;
+};
+
+class Dedisperser {
+ public:
+  Dedisperser(const DeviceFilterbank& fb, hipStream_t stream);
+  // DM trials [d0, d1) -> out[(d-d0)*out_stride + t], t < out_nsamps
+  void run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispKernel kind = DedispKernel::Auto);
+  static uint64_t row_stride(uint64_t out_nsamps) { return (out_nsamps + 255) / 256 * 256; }
+
+ private:
+  const DeviceFilterbank& fb_;
+  hipStream_t stream_;
+  DeviceBuffer<int32_t> d_offsets_, d_kill_, d_active_, d_steps_, d_nsteps_;
+  DeviceBuffer<int8_t> d_deltas_;
+};
+
+struct SearchParams {
+  uint64_t fft_size = 0;
+  float tsamp = 0.f;
+  float min_snr = 9.f;
+  float min_freq = 0.1f;
+  float max_freq = 1100.f;
+  int nharmonics = 4;
+  float freq_tol = 0.0001f;
+  int max_harm = 16;
+  float boundary_5_freq = 0.05f;
+  float boundary_25_freq = 0.5f;
+  std::vector<float> zap_freqs, zap_widths;
+  int accel_batch = 0;          // 0 = auto
+  size_t batch_bytes = 3ull << 30;  // auto-batch HBM budget
+  int min_gap = 30;
+};
+
+// Running-median whitening of one N-point series, in place.
+class Whitener {
+ public:
+  Whitener(uint64_t n, float tsamp, hipStream_t stream);
+  // trial u8[nsamps] -> d_series f32[n] (pad with mean / truncate)
+  void load_trial(const uint8_t* d_trial, uint64_t nsamps, float* d_series);
+  // R2C, running median, deredden (+zap), [interbin stats], C2R in place.
+  void whiten(float* d_series, const uint32_t* d_zapmask, bool with_stats, float boundary5, float boundary25);
+  // Forward spectrum of the (whitened) series is left in spectrum() until the next call.
+  float2* spectrum() const { return fser_.data(); }
+  const float* stats() const { return stats_.data(); }  // {mean, rms, std} of the interbin spectrum
+  uint64_t n() const { return n_; }
+  uint64_t nbins() const { return n_ / 2 + 1; }
+  float bin_width() const { return bin_width_; }
+  FftPlan& r2c() { return *r2c_; }
+  FftPlan& c2r() { return *c2r_; }
+
+ private:
+  uint64_t n_;
+  float tsamp_, bin_width_;
+  hipStream_t stream_;
+  std::unique_ptr<FftPlan> r2c_, c2r_;
+  DeviceBuffer<float2> fser_;
+  DeviceBuffer<float> m5_, m25_, m125_;
+  DeviceBuffer<double> partials_;
+  DeviceBuffer<float> stats_;
+  DeviceBuffer<unsigned long long> sum_;
+};
+
+struct SearchCounters {
+  uint64_t dm_trials = 0;
+  uint64_t accel_trials = 0;
+  uint64_t peaks = 0;
+  uint64_t overflows = 0;
+  double whiten_s = 0, accel_s = 0, host_s = 0;
+};
+
+class SearchEngine {
+ public:
+  SearchEngine(const SearchParams& p, hipStream_t stream);
+  ~SearchEngine();
+  // Full Worker::start body for one DM trial (pipeline_multi.cu:147-243):
+  // returns the acceleration-distilled candidates of this DM.
+  CandidateList search_trial(const uint8_t* d_trial, uint64_t nsamps, float dm, int dm_idx,
+                             const std::vector<float>& accs);
+  const SearchParams& params() const { return p_; }
+  const SearchCounters& counters() const { return ctr_; }
+  void reset_counters() { ctr_ = SearchCounters(); }
+  int batch_size() const { return K_; }
+  float tobs() const { return tobs_; }
+  // Debug access to the whitened series of the last trial.
+  const float* whitened() const { return tim_.data(); }
+  const Whitener& whitener() const { return *wh_; }
+
+ private:
+  struct Slot {
+    DeviceBuffer<kern::PeakRecord> d_peaks;
+    DeviceBuffer<uint32_t> d_count;
+    PinnedBuffer<kern::PeakRecord> h_peaks;
+    PinnedBuffer<uint32_t> h_count;
+    std::unique_ptr<Event> done, copied;
+    int first = 0, count = 0;
+  };
+  void ensure_batch_buffers();
+  FftPlan& batch_plan(int count);
+  void launch_batch(Slot& s, int first, int count);
+  void grow_capacity(uint32_t need);
+  void process_slot(Slot& s, float dm, int dm_idx, const std::vector<float>& accs, CandidateList& out);
+
+  SearchParams p_;
+  hipStream_t stream_;
+  Stream copy_stream_;
+  uint64_t n_, nb_;
+  float bin_width_, tobs_;
+  int nlev_;
+  int K_;
+  uint32_t cap_;
+  kern::HarmParams hp_{};
+  std::vector<PeakBounds> bounds_;
+  int hi_ = 0;
+  std::unique_ptr<Whitener> wh_;
+  DeviceBuffer<float> tim_;
+  DeviceBuffer<uint32_t> zapmask_;
+  bool zap_ = false;
+  DeviceBuffer<float> res_;
+  DeviceBuffer<float2> spec_;
+  DeviceBuffer<float> P_;
+  DeviceBuffer<double> af_;
+  std::vector<double> af_host_;
+  std::map<int, std::unique_ptr<FftPlan>> plans_;
+  Slot slots_[2];
+  SearchCounters ctr_;
+  HarmonicDistiller harm_;
+  AccelerationDistiller accd_;
+  // host scratch
+  std::vector<uint32_t> seg_count_, seg_off_;
+  std::vector<kern::PeakRecord> sorted_;
+};
+
+// Zap mask for an FFT size (birdiezapper.hpp / kernels.cu:1036-1069 semantics).
+std::vector<uint32_t> build_zap_mask(const std::vector<float>& freqs, const std::vector<float>& widths,
+                                     float bin_width, uint64_t nbins);
+
+// Host part of FoldOptimiser::calculate_sn (folder.hpp:140-183); the
+// negative modulo the reference invokes for bin < nbins/2 is made a proper
+// circular index.
+void fold_calculate_sn(const float* prof, int bin, int width, int nbins, float* sn1, float* sn2);
+
+struct FoldResult {
+  float folded_snr = 0.f;
+  double opt_period = 0.0;
+  int opt_width = 0;
+  int opt_bin = 0;
+  std::vector<float> fold;  // [nints][nbins]
+  std::vector<float> prof;
+};
+
+class FoldEngine {
+ public:
+  static constexpr int kNbins = 64;
+  static constexpr int kNints = 16;
+  FoldEngine(uint64_t nsamps, float tsamp, hipStream_t stream);
+  // Fold + optimise candidates (period, acc) of one DM trial.
+  std::vector<FoldResult> fold_trial(const uint8_t* d_trial, uint64_t trial_nsamps, const std::vector<double>& periods,
+                                     const std::vector<float>& accs);
+  // Fold + optimise candidates on an already-whitened series (testing).
+  std::vector<FoldResult> fold_series(const float* d_series, const std::vector<double>& periods,
+                                      const std::vector<float>& accs);
+  uint64_t nsamps() const { return n_; }
+
+ private:
+  uint64_t n_;
+  float tsamp_;
+  hipStream_t stream_;
+  std::unique_ptr<Whitener> wh_;
+  DeviceBuffer<float> tim_;
+  DeviceBuffer<float2> shift_table_;
+  DeviceBuffer<kern::FoldJob> jobs_;
+  DeviceBuffer<float> psum_, folds_, opt_fold_, opt_prof_, opt_val_;
+  DeviceBuffer<int32_t> pcount_, opt_int_;
+  int chunk_ = 4096;
+};
+
+// Multi-beam coincidencer helpers (coincidencer.cpp:124-200): normalise a
+// beam (time series and spectrum) and add its indicator (x > thresh) into
+// uint8 count arrays.
+struct BeamProducts {
+  DeviceBuffer<float> series;    // normalised whitened time series [n]
+  DeviceBuffer<float> spectrum;  // normalised interbinned spectrum [n/2+1]
+};
+void coincidencer_beam(const uint8_t* d_trial, uint64_t n, float tsamp, BeamProducts& out, hipStream_t stream);
+// Write text outputs (coincidencer.hpp:42-80).
+void write_samp_mask(const std::vector<float>& mask, const std::string& filename);
+void write_birdie_list(const std::vector<float>& mask, float bin_width, const std::string& filename);
+
+}  // namespace psoup

@@ -1,0 +1,155 @@
+// Host-side launchers for every hand-written HIP kernel (gfx950 / CDNA4).
+// All launchers are asynchronous on the given stream and never synchronise.
+//
+// Reference kernel map (src/kernels.cu):
+//   K29 conversion_kernel, K9/K10 GPU_mean/GPU_fill   -> u8_sum + u8_to_f32_pad
+//   K2 power_series / K3 bin_interbin / K4 normalise  -> form_amplitude,
+//        form_interbin, normalise; fused into whiten_* and interbin_normalise_batch
+//   K22/K23 median_scrunch5 + linear_stretch + K24 divide_c_by_f + K25 zap
+//                                                      -> median5_amp, median5,
+//                                                         deredden_zap (fused)
+//   K8/K9 GPU_rms/GPU_mean                            -> interbin_stats (fused
+//                                                         single-pass partials)
+//   K5/K6 resample_kernel(II)                         -> resample_batch, resample_v1
+//   K1 harmonic_sum + K7 device_find_peaks            -> harmonic_peaks_batch
+//   K13 fold_time_series                              -> fold_accumulate + fold_reduce
+//   K14-K21 fold optimiser chain                      -> fold_optimise (one fused kernel)
+//   K26 coincidence_kernel                            -> coincidence_*
+//   K27/K28 conjugate / cuCmulf_inplace               -> conjugate, cmul_inplace
+//   dedisp (external library)                         -> unpack_transpose,
+//                                                        dedisperse_direct, dedisperse_mfma
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+namespace psoup {
+namespace kern {
+
+// ---------------------------------------------------------------- records ---
+struct PeakRecord {
+  uint32_t seg;  // batch_item * 8 + level
+  int32_t idx;
+  float snr;
+};
+static_assert(sizeof(PeakRecord) == 12, "PeakRecord layout");
+
+constexpr int kMaxHarmLevels = 5;  // 2,4,8,16,32 harmonics (kernels.cu:42-96)
+
+// --------------------------------------------------------- unpack/dedisp ----
+// packed time-major SIGPROC data (nbits in {1,2,4,8}, LSB-first) ->
+// channel-major int8 rows: out[c*out_stride + t] = value - bias.
+void unpack_transpose(const uint8_t* packed, uint64_t nsamps, int nchans, int nbits, int8_t* out,
+                      uint64_t out_stride, int bias, hipStream_t s);
+
+// Direct (VALU) brute-force dedispersion, exact integer sums.
+//   out[d*out_stride + t] = clip(scale * (sum_{c: kill[c]} (x[c][t + off(c,d)] + bias)))
+// for d in [0, ndm), t in [0, out_nsamps).  offsets: int32 [ndm][nchans].
+void dedisperse_direct(const int8_t* chan_major, uint64_t chan_stride, int nchans, const int32_t* offsets,
+                       const int32_t* killmask, int ndm, uint64_t out_nsamps, uint8_t* out, uint64_t out_stride,
+                       float scale, int bias, int nactive, hipStream_t s);
+
+// MFMA dedispersion (v_mfma_i32_32x32x32_i8 over one-hot shift matrices),
+// bit-identical to dedisperse_direct.  The host builds, per tile of 32 DMs,
+// the list of (channel, 16-sample shift block) pairs (two per MFMA step) and
+// the per-lane one-hot positions; see dedisperse.hip.
+struct MfmaDedispPlan {
+  int ntiles = 0;
+  int max_steps = 0;
+  std::vector<int32_t> steps;   // [ntiles][max_steps][4] = {c0, sb0, c1, sb1}
+  std::vector<int8_t> deltas;   // [ntiles][max_steps][64] one-hot position per lane, -1 = none
+  std::vector<int32_t> nsteps;  // [ntiles]
+};
+// offsets: host int32 [ndm][nchans]; killmask: host [nchans] (0 = killed)
+void build_mfma_dedisp_plan(const int32_t* offsets, int ndm, int nchans, const int32_t* killmask,
+                            MfmaDedispPlan& plan);
+// Reads up to 560 bytes past out_nsamps + max offset in each channel row.
+void dedisperse_mfma(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_steps, const int8_t* d_deltas,
+                     const int32_t* d_nsteps, int ntiles, int max_steps, int ndm, uint64_t out_nsamps, uint8_t* out,
+                     uint64_t out_stride, float scale, int bias_total, hipStream_t s);
+
+// ------------------------------------------------------------ time series ---
+void u8_sum(const uint8_t* in, uint64_t n, unsigned long long* sum, hipStream_t s);
+// out[i] = i < nvalid ? in[i] : (float)(sum / nvalid)
+void u8_to_f32_pad(const uint8_t* in, uint64_t nvalid, float* out, uint64_t n, const unsigned long long* sum,
+                   hipStream_t s);
+void f32_stats(const float* x, uint64_t n, double* partials, int npartials, float* stats_out, hipStream_t s);
+
+// ----------------------------------------------------------------- spectra --
+void form_amplitude(const float2* X, uint64_t nbins, float* out, hipStream_t s);
+void form_interbin(const float2* X, uint64_t nbins, float* out, hipStream_t s);
+// x = (x - mean)/sigma ; mean/sigma either host scalars or device pointer
+// (stats = {mean, rms, std}) scaled by `scale`.
+void normalise(float* x, uint64_t n, float mean, float sigma, hipStream_t s);
+void normalise_dev(float* x, uint64_t n, const float* stats, float scale, hipStream_t s);
+
+// running median (Dereddener::calculate_median): out_count = count/5
+void median5_amp(const float2* X, uint64_t nbins, float* out, hipStream_t s);
+void median5(const float* in, uint64_t count, float* out, hipStream_t s);
+// X[k] /= median(k) (k<5 -> 0), then zapped bins -> 1+0i. median(k) is the
+// piecewise linear stretch of m5/m25/m125 at boundaries pos5/pos25.
+void deredden_zap(float2* X, uint64_t nbins, const float* m5, uint64_t n5, const float* m25, uint64_t n25,
+                  const float* m125, uint64_t n125, int64_t pos5, int64_t pos25, const uint32_t* zapmask,
+                  hipStream_t s);
+// P = interbin(X); per-block partial sums of P and P^2 -> stats {mean,rms,std}
+void interbin_stats(const float2* X, uint64_t nbins, float* P, double* partials, int npartials, float* stats,
+                    hipStream_t s);
+
+// ------------------------------------------------------------- resampling ---
+// out[k][i] = in[clamp(rint(i + i*af_k*(i - n)))], af_k = acc_k*tsamp/(2c)
+void resample_batch(const float* in, uint64_t n, float* out, uint64_t out_stride, const double* af, int K,
+                    hipStream_t s);
+// out[i] = in[clamp(rint(i + af*((i-n/2)^2 - (n/2)^2)))]
+void resample_v1(const float* in, uint64_t n, float* out, double af, hipStream_t s);
+
+// ----------------------------------------------------- search hot path ------
+// P[k][i] = (interbin(X[k])[i] - stats.mean*nscale) / (stats.std*nscale), i < nbins_out
+void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride, float* P, uint64_t pstride,
+                              int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s);
+
+struct HarmParams {
+  int nlevels;             // number of harmonic-sum levels (0..5)
+  int start[6];            // per level search range [start, end)
+  int end[6];
+  float thresh;
+  uint32_t capacity;       // PeakRecord capacity of `out`
+};
+// Fused incoherent harmonic sum + threshold + compaction: never writes the
+// summed spectra.  Records land unordered; count may exceed capacity (then
+// the caller re-runs with a bigger buffer).
+void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
+                          PeakRecord* out, uint32_t* count, hipStream_t s);
+// Debug/test: materialise level-h sums [nlevels][nbins] for one spectrum.
+void harmonic_sums(const float* P, uint64_t nbins, int nlevels, float* out, hipStream_t s);
+
+// ------------------------------------------------------------------ folding --
+struct FoldJob {
+  double tsamp_by_period;  // tsamp / period
+  double af;               // acc*tsamp/(2c) for the v1 resampler
+};
+// Partial fold sums: partial[(job*nints + subint)*nchunk + chunk][nbins] (sum),
+// counts likewise.  n = samples in the (whitened) series.
+void fold_accumulate(const float* in, uint64_t n, const FoldJob* jobs, int njobs, int nbins, int nints,
+                     int chunk, float* psum, int32_t* pcount, hipStream_t s);
+void fold_reduce(const float* psum, const int32_t* pcount, int njobs, int nbins, int nints, int nchunk,
+                 float* fold, hipStream_t s);
+// Shift-phase table [nshift][nints][nbins] complex (FoldOptimiser shift array)
+void fold_shift_table(float2* table, int nbins, int nints, hipStream_t s);
+// One workgroup per fold: shift/collapse/template search.  opt_int = {template, shift, bin}
+void fold_optimise(const float* folds, int nfold, const float2* shift_table, float* opt_fold, float* opt_prof,
+                   int32_t* opt_int, float* opt_val, hipStream_t s);
+
+// ------------------------------------------------------------- coincidence --
+// counts[i] += (x[i] > thresh)   (uint8 counts)
+void count_above(const float* x, uint64_t n, float thresh, uint8_t* counts, hipStream_t s);
+// mask[i] = counts[i] < beam_thresh
+void coincidence_mask(const uint8_t* counts, uint64_t n, int beam_thresh, float* mask, hipStream_t s);
+
+// ------------------------------------------------------------- correlation --
+void conjugate(float2* x, uint64_t n, hipStream_t s);
+void cmul_inplace(const float2* x, float2* y, uint64_t n, hipStream_t s);
+
+}  // namespace kern
+}  // namespace psoup

@@ -1,0 +1,243 @@
+// Brute-force incoherent dedispersion (replaces the external dedisp library
+// called from include/transforms/dedisperser.hpp:98-113).
+//
+// Input: channel-major int8 rows x[c][t] = raw - bias (unpack_transpose).
+// Output: DM-major uint8 trials, out[d][t] = (uint8) clamp(scale * S, 0, 255),
+//   S = sum over unkilled channels of raw[c][t + off(c,d)], off = (int)(dm*delay[c] + 0.5)
+// scale = 192 / (in_range * nchans) (= 255/(in_range*nchans) * 3*1024/255/16,
+// dedisp's 8-bit output scaling; exactly 1.0 for 2-bit x 64 channels).
+//
+// Two kernels produce bit-identical output:
+//   dedisperse_direct_kernel  VALU reference: one thread = 4 samples of 1 DM.
+//   dedisperse_mfma_kernel    v_mfma_i32_32x32x32_i8: the DM sum is a GEMM of
+//     shifted data (A: 32 samples x 32 (channel,shift) pairs) with a one-hot
+//     selection matrix (B: 32 (channel,shift) pairs x 32 DMs); see below.
+#include <algorithm>
+#include <utility>
+#include <vector>
+
+#include "device_common.hpp"
+#include "psoup/kernels.hpp"
+
+namespace psoup {
+namespace kern {
+
+namespace {
+
+__device__ __forceinline__ uint8_t scale_out(int sum, float scale) {
+  float v = static_cast<float>(sum) * scale;
+  v = fminf(fmaxf(v, 0.f), 255.f);
+  return static_cast<uint8_t>(v);
+}
+
+__global__ void __launch_bounds__(256) dedisperse_direct_kernel(const int8_t* __restrict__ x, uint64_t stride,
+                                                                int nchans, const int32_t* __restrict__ offsets,
+                                                                const int32_t* __restrict__ kill,
+                                                                uint64_t out_nsamps, uint8_t* __restrict__ out,
+                                                                uint64_t out_stride, float scale, int bias_total) {
+  const int d = blockIdx.y;
+  const uint64_t t = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) * 4;
+  if (t >= out_nsamps) return;
+  const int32_t* off = offsets + static_cast<uint64_t>(d) * nchans;
+  int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  const bool full = t + 4 <= out_nsamps;
+  for (int c = 0; c < nchans; ++c) {
+    if (!kill[c]) continue;
+    const int8_t* p = x + static_cast<uint64_t>(c) * stride + t + off[c];
+    if (full) {
+      s0 += p[0];
+      s1 += p[1];
+      s2 += p[2];
+      s3 += p[3];
+    } else {
+      s0 += p[0];
+      if (t + 1 < out_nsamps) s1 += p[1];
+      if (t + 2 < out_nsamps) s2 += p[2];
+      if (t + 3 < out_nsamps) s3 += p[3];
+    }
+  }
+  uint8_t* o = out + static_cast<uint64_t>(d) * out_stride + t;
+  o[0] = scale_out(s0 + bias_total, scale);
+  if (t + 1 < out_nsamps) o[1] = scale_out(s1 + bias_total, scale);
+  if (t + 2 < out_nsamps) o[2] = scale_out(s2 + bias_total, scale);
+  if (t + 3 < out_nsamps) o[3] = scale_out(s3 + bias_total, scale);
+}
+
+
+// ------------------------------------------------------------------ MFMA ----
+// out[t][d] = sum_k A[t][k] * B[k][d] with k = (channel c, shift j in a block of
+// 16 consecutive shifts starting at sb):
+//   A[t][(c,j)] = x[c][t + sb + j]               (16 consecutive bytes per lane)
+//   B[(c,j)][d] = (off(c,d) - sb == j)           (one-hot, built from a delta byte)
+// One v_mfma_i32_32x32x32_i8 covers two (c, sb) blocks (lane half h = block h)
+// for 32 samples x 32 DMs; a wave owns 4 such sample tiles (128 samples) so
+// each one-hot B fragment is reused 4x.  Workgroup = 4 waves = 512 samples of
+// one 32-DM tile.  Exact int32 accumulation => identical to the VALU kernel.
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v16i __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+constexpr int kMfmaWaveTiles = 4;                       // 32-sample tiles per wave
+constexpr int kMfmaWgSamples = 4 * 32 * kMfmaWaveTiles;  // 512
+
+__global__ void __launch_bounds__(256) dedisperse_mfma_kernel(
+    const int8_t* __restrict__ x, uint64_t stride, const int4* __restrict__ steps, const int8_t* __restrict__ deltas,
+    const int32_t* __restrict__ nsteps, int max_steps, int ndm, uint64_t out_nsamps, uint8_t* __restrict__ out,
+    uint64_t out_stride, float scale, int bias_total, uint64_t ntime_tiles) {
+  const int tile = blockIdx.x;  // DM tile (fastest: concurrent WGs share the x window in L2)
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int ns = nsteps[tile];
+  const int4* st = steps + static_cast<uint64_t>(tile) * max_steps;
+  const int8_t* dl = deltas + static_cast<uint64_t>(tile) * max_steps * 64;
+  for (uint64_t tt = blockIdx.y; tt < ntime_tiles; tt += gridDim.y) {
+    const uint64_t t0 = tt * kMfmaWgSamples + static_cast<uint64_t>(wave) * (32 * kMfmaWaveTiles);
+    v16i acc[kMfmaWaveTiles];
+#pragma unroll
+    for (int m = 0; m < kMfmaWaveTiles; ++m)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[m][e] = 0;
+    for (int s = 0; s < ns; ++s) {
+      const int4 stp = st[s];
+      const int c = h ? stp.z : stp.x;
+      const int sb = h ? stp.w : stp.y;
+      const int delta = dl[s * 64 + lane];
+      v4i b;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        b[q] = (delta >= 0 && (delta >> 2) == q) ? (1 << ((delta & 3) * 8)) : 0;
+      const int8_t* row = x + static_cast<uint64_t>(c) * stride;
+#pragma unroll
+      for (int m = 0; m < kMfmaWaveTiles; ++m) {
+        const uint64_t a0 = t0 + m * 32 + r + static_cast<int64_t>(sb);
+        const uint64_t al = a0 & ~3ull;
+        const int sh = static_cast<int>(a0 & 3ull);
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(row + al);
+        const u32x4_a4 w = *reinterpret_cast<const u32x4_a4*>(p);
+        const uint32_t w4 = p[4];
+        v4i a;
+        a[0] = static_cast<int>(__builtin_amdgcn_alignbyte(w[1], w[0], sh));
+        a[1] = static_cast<int>(__builtin_amdgcn_alignbyte(w[2], w[1], sh));
+        a[2] = static_cast<int>(__builtin_amdgcn_alignbyte(w[3], w[2], sh));
+        a[3] = static_cast<int>(__builtin_amdgcn_alignbyte(w4, w[3], sh));
+        acc[m] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc[m], 0, 0, 0);
+      }
+    }
+    // C/D layout (32x32): col = lane&31 (DM), row = (reg&3) + 8*(reg>>2) + 4*(lane>>5) (sample)
+    const int d = tile * 32 + r;
+    if (d < ndm) {
+      uint8_t* o = out + static_cast<uint64_t>(d) * out_stride;
+#pragma unroll
+      for (int m = 0; m < kMfmaWaveTiles; ++m) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const uint64_t t = t0 + m * 32 + 8 * g + 4 * h;
+          uint32_t packed = 0;
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            packed |= static_cast<uint32_t>(scale_out(acc[m][4 * g + e] + bias_total, scale)) << (8 * e);
+          if (t + 4 <= out_nsamps) {
+            *reinterpret_cast<uint32_t*>(o + t) = packed;
+          } else {
+            for (int e = 0; e < 4; ++e)
+              if (t + e < out_nsamps) o[t + e] = static_cast<uint8_t>(packed >> (8 * e));
+          }
+        }
+      }
+    }
+  }
+}
+
+}  // namespace
+
+void dedisperse_direct(const int8_t* chan_major, uint64_t chan_stride, int nchans, const int32_t* offsets,
+                       const int32_t* killmask, int ndm, uint64_t out_nsamps, uint8_t* out, uint64_t out_stride,
+                       float scale, int bias, int nactive, hipStream_t s) {
+  if (ndm <= 0 || out_nsamps == 0) return;
+  PSOUP_CHECK(ndm <= 65535, "too many DMs per launch");
+  uint64_t gx = (out_nsamps + 1023) / 1024;
+  dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(ndm));
+  dedisperse_direct_kernel<<<grid, 256, 0, s>>>(chan_major, chan_stride, nchans, offsets, killmask, out_nsamps,
+                                                 out, out_stride, scale, bias * nactive);
+  post_launch_check("dedisperse_direct_kernel", s);
+}
+
+
+void build_mfma_dedisp_plan(const int32_t* offsets, int ndm, int nchans, const int32_t* killmask,
+                            MfmaDedispPlan& plan) {
+  const int ntiles = (ndm + 31) / 32;
+  plan.ntiles = ntiles;
+  std::vector<std::vector<int32_t>> tsteps(static_cast<size_t>(ntiles));
+  std::vector<std::vector<int8_t>> tdeltas(static_cast<size_t>(ntiles));
+  int max_steps = 1;
+  for (int T = 0; T < ntiles; ++T) {
+    auto off = [&](int dd, int c) {
+      int d = std::min(T * 32 + dd, ndm - 1);  // pad the last tile with the last DM
+      return offsets[static_cast<size_t>(d) * nchans + c];
+    };
+    std::vector<std::pair<int, int>> blocks;
+    for (int c = 0; c < nchans; ++c) {
+      if (killmask && !killmask[c]) continue;
+      int smin = off(0, c), smax = off(0, c);
+      for (int dd = 1; dd < 32; ++dd) {
+        smin = std::min(smin, off(dd, c));
+        smax = std::max(smax, off(dd, c));
+      }
+      PSOUP_CHECK(smin >= 0, "negative dispersion offset (foff > 0 is not supported)");
+      for (int sb = smin; sb <= smax; sb += 16) blocks.emplace_back(c, sb);
+    }
+    if (blocks.size() % 2) blocks.push_back(std::make_pair(-1, -1));  // dummy half (zero one-hot)
+    const int nst = static_cast<int>(blocks.size() / 2);
+    auto& S = tsteps[T];
+    auto& D = tdeltas[T];
+    S.resize(static_cast<size_t>(nst) * 4);
+    D.resize(static_cast<size_t>(nst) * 64);
+    for (int s = 0; s < nst; ++s) {
+      for (int hh = 0; hh < 2; ++hh) {
+        auto blk = blocks[2 * s + hh];
+        const bool dummy = blk.first < 0;
+        const int c = dummy ? blocks[2 * s].first : blk.first;
+        const int sb = dummy ? blocks[2 * s].second : blk.second;
+        S[4 * s + 2 * hh] = c;
+        S[4 * s + 2 * hh + 1] = sb;
+        for (int rr = 0; rr < 32; ++rr) {
+          int delta = -1;
+          if (!dummy && T * 32 + rr < ndm) {
+            const int dv = off(rr, c) - sb;
+            if (dv >= 0 && dv < 16) delta = dv;
+          }
+          D[static_cast<size_t>(s) * 64 + hh * 32 + rr] = static_cast<int8_t>(delta);
+        }
+      }
+    }
+    max_steps = std::max(max_steps, nst);
+  }
+  plan.max_steps = max_steps;
+  plan.steps.assign(static_cast<size_t>(ntiles) * max_steps * 4, 0);
+  plan.deltas.assign(static_cast<size_t>(ntiles) * max_steps * 64, static_cast<int8_t>(-1));
+  plan.nsteps.assign(static_cast<size_t>(ntiles), 0);
+  for (int T = 0; T < ntiles; ++T) {
+    const int nst = static_cast<int>(tsteps[T].size() / 4);
+    plan.nsteps[T] = nst;
+    std::copy(tsteps[T].begin(), tsteps[T].end(), plan.steps.begin() + static_cast<size_t>(T) * max_steps * 4);
+    std::copy(tdeltas[T].begin(), tdeltas[T].end(), plan.deltas.begin() + static_cast<size_t>(T) * max_steps * 64);
+  }
+}
+
+void dedisperse_mfma(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_steps, const int8_t* d_deltas,
+                     const int32_t* d_nsteps, int ntiles, int max_steps, int ndm, uint64_t out_nsamps, uint8_t* out,
+                     uint64_t out_stride, float scale, int bias_total, hipStream_t s) {
+  if (ndm <= 0 || out_nsamps == 0) return;
+  PSOUP_CHECK(ntiles <= 65535, "too many DM tiles");
+  const uint64_t ntt = (out_nsamps + kMfmaWgSamples - 1) / kMfmaWgSamples;
+  dim3 grid(static_cast<unsigned>(ntiles), static_cast<unsigned>(std::min<uint64_t>(ntt, 65535)));
+  dedisperse_mfma_kernel<<<grid, 256, 0, s>>>(chan_major, chan_stride, reinterpret_cast<const int4*>(d_steps),
+                                               d_deltas, d_nsteps, max_steps, ndm, out_nsamps, out, out_stride, scale,
+                                               bias_total, ntt);
+  post_launch_check("dedisperse_mfma_kernel", s);
+}
+
+}  // namespace kern
+}  // namespace psoup

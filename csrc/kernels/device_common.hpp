@@ -1,0 +1,119 @@
+// Shared device helpers for the gfx950 kernels (64-lane wavefronts).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "psoup/common.hpp"
+
+namespace psoup {
+namespace kern {
+namespace dev {
+
+constexpr int kWave = 64;
+
+// Memory-bound launches: enough blocks to fill 256 CUs x 8, grid-stride the rest.
+inline unsigned grid_for(uint64_t work_items, unsigned block, unsigned cap = 2048) {
+  uint64_t g = (work_items + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return static_cast<unsigned>(g);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, kWave);
+  return v;
+}
+
+// Block-wide sum; `scratch` must hold blockDim.x/64 elements. Result valid
+// in every thread.
+template <class T>
+__device__ __forceinline__ T block_sum(T v, T* scratch) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  const int nw = (blockDim.x + kWave - 1) / kWave;
+  v = wave_sum(v);
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  T r = T(0);
+  for (int i = 0; i < nw; ++i) r += scratch[i];
+  __syncthreads();
+  return r;
+}
+
+// Exact median of five (any correct network gives the identical value).
+__device__ __forceinline__ float median5(float a, float b, float c, float d, float e) {
+  float t;
+#define PS_SORT2(x, y) \
+  t = fminf(x, y);     \
+  y = fmaxf(x, y);     \
+  x = t;
+  PS_SORT2(a, b);
+  PS_SORT2(d, e);
+  PS_SORT2(a, d);  // a = min of 4 (excluded)
+  PS_SORT2(b, e);  // e = max of 4 (excluded)
+  // median of {b, c, d}
+  PS_SORT2(b, c);
+  PS_SORT2(c, d);
+  PS_SORT2(b, c);
+#undef PS_SORT2
+  return c;
+}
+
+__device__ __forceinline__ float median3(float a, float b, float c) {
+  return fmaxf(fminf(a, b), fminf(fmaxf(a, b), c));
+}
+
+__device__ __forceinline__ float median4(float a, float b, float c, float d) {
+  // mean of the two middle values
+  float lo1 = fminf(a, b), hi1 = fmaxf(a, b);
+  float lo2 = fminf(c, d), hi2 = fmaxf(c, d);
+  float mid_lo = fmaxf(lo1, lo2);
+  float mid_hi = fminf(hi1, hi2);
+  return 0.5f * (mid_lo + mid_hi);
+}
+
+// cuCdivf as in CUDA's cuComplex.h (scaled division) for a real divisor,
+// so dereddening reproduces the reference's rounding.
+__device__ __forceinline__ float2 cdiv_real(float2 x, float f) {
+  float s = fabsf(f);
+  float oos = 1.0f / s;
+  float ars = x.x * oos;
+  float ais = x.y * oos;
+  float brs = f * oos;
+  float s2 = brs * brs;
+  float oos2 = 1.0f / s2;
+  return make_float2((ars * brs) * oos2, (ais * brs) * oos2);
+}
+
+// Amplitude |X| exactly as power_series_kernel (z * rsqrt(z)), 0 for z == 0.
+__device__ __forceinline__ float amplitude(float2 x) {
+  float z = x.x * x.x + x.y * x.y;
+  return z > 0.f ? z * rsqrtf(z) : 0.f;
+}
+
+// Interbinned amplitude, bin_interbin_series_kernel semantics.
+__device__ __forceinline__ float interbin(float2 x, float2 xl) {
+  float ampsq = x.x * x.x + x.y * x.y;
+  float dre = x.x - xl.x, dim = x.y - xl.y;
+  float ampsq_diff = static_cast<float>(0.5 * static_cast<double>(dre * dre + dim * dim));
+  return sqrtf(fmaxf(ampsq, ampsq_diff));
+}
+
+}  // namespace dev
+}  // namespace kern
+}  // namespace psoup

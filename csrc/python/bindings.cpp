@@ -1,0 +1,609 @@
+// pybind11 bindings of the native core (module peasoup_amd._C).
+// Device memory crosses the boundary as raw addresses (torch tensors'
+// data_ptr()) and streams as hipStream_t handles (torch.cuda.Stream.cuda_stream),
+// so no torch headers are needed and the extension builds in seconds.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "psoup/candidates.hpp"
+#include "psoup/cli.hpp"
+#include "psoup/common.hpp"
+#include "psoup/engine.hpp"
+#include "psoup/fft.hpp"
+#include "psoup/kernels.hpp"
+#include "psoup/output.hpp"
+#include "psoup/pipeline.hpp"
+#include "psoup/plan.hpp"
+#include "psoup/sigproc.hpp"
+
+namespace py = pybind11;
+using namespace psoup;
+
+namespace {
+
+template <class T>
+T* P(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+py::dict header_to_dict(const SigprocHeader& h) {
+  py::dict d;
+  d["source_name"] = h.source_name;
+  d["rawdatafile"] = h.rawdatafile;
+  d["az_start"] = h.az_start;
+  d["za_start"] = h.za_start;
+  d["src_raj"] = h.src_raj;
+  d["src_dej"] = h.src_dej;
+  d["tstart"] = h.tstart;
+  d["tsamp"] = h.tsamp;
+  d["period"] = h.period;
+  d["fch1"] = h.fch1;
+  d["foff"] = h.foff;
+  d["nchans"] = h.nchans;
+  d["telescope_id"] = h.telescope_id;
+  d["machine_id"] = h.machine_id;
+  d["data_type"] = h.data_type;
+  d["ibeam"] = h.ibeam;
+  d["nbeams"] = h.nbeams;
+  d["nbits"] = h.nbits;
+  d["barycentric"] = h.barycentric;
+  d["pulsarcentric"] = h.pulsarcentric;
+  d["nbins"] = h.nbins;
+  d["nsamples"] = h.nsamples;
+  d["nifs"] = h.nifs;
+  d["npuls"] = h.npuls;
+  d["refdm"] = h.refdm;
+  d["signed"] = static_cast<int>(h.signed_data);
+  d["size"] = h.size;
+  return d;
+}
+
+SigprocHeader dict_to_header(const py::dict& d) {
+  SigprocHeader h;
+  auto gd = [&](const char* k, double& v) {
+    if (d.contains(k)) {
+      v = d[k].cast<double>();
+      h.keys_present.push_back(k);
+    }
+  };
+  auto gi = [&](const char* k, int& v) {
+    if (d.contains(k)) {
+      v = d[k].cast<int>();
+      h.keys_present.push_back(k);
+    }
+  };
+  if (d.contains("source_name")) h.source_name = d["source_name"].cast<std::string>();
+  if (d.contains("rawdatafile")) h.rawdatafile = d["rawdatafile"].cast<std::string>();
+  gd("az_start", h.az_start);
+  gd("za_start", h.za_start);
+  gd("src_raj", h.src_raj);
+  gd("src_dej", h.src_dej);
+  gd("tstart", h.tstart);
+  gd("tsamp", h.tsamp);
+  gd("period", h.period);
+  gd("fch1", h.fch1);
+  gd("foff", h.foff);
+  gi("nchans", h.nchans);
+  gi("telescope_id", h.telescope_id);
+  gi("machine_id", h.machine_id);
+  gi("data_type", h.data_type);
+  gi("ibeam", h.ibeam);
+  gi("nbeams", h.nbeams);
+  gi("nbits", h.nbits);
+  gi("barycentric", h.barycentric);
+  gi("pulsarcentric", h.pulsarcentric);
+  gi("nbins", h.nbins);
+  gi("nsamples", h.nsamples);
+  gi("nifs", h.nifs);
+  gi("npuls", h.npuls);
+  gd("refdm", h.refdm);
+  if (d.contains("signed")) {
+    h.signed_data = static_cast<unsigned char>(d["signed"].cast<int>());
+    h.keys_present.push_back("signed");
+  }
+  return h;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "peasoup_amd native core (C++/HIP for gfx950)";
+  py::register_exception<psoup::Error>(m, "NativeError", PyExc_RuntimeError);
+
+  // ------------------------------------------------------------ platform --
+  m.def("device_count", &device_count);
+  m.def("device_info", [](int d) {
+    DeviceInfo i = device_info(d);
+    py::dict r;
+    r["id"] = i.id;
+    r["name"] = i.name;
+    r["arch"] = i.arch;
+    r["major"] = i.major;
+    r["minor"] = i.minor;
+    r["multiprocessors"] = i.multiprocessors;
+    r["total_mem"] = i.total_mem;
+    return r;
+  });
+  m.def("runtime_version", &runtime_version);
+  m.def("driver_version", &driver_version);
+  m.def("set_log_rank", &set_log_rank);
+  m.def("set_log_level", [](int l) { set_log_level(static_cast<LogLevel>(l)); });
+  m.def("prev_power_of_two", &prev_power_of_two);
+  m.def("roctx_push", [](const std::string& name) { roctx_push(name.c_str()); });
+  m.def("roctx_pop", &roctx_pop);
+
+  // ---------------------------------------------------------------- io ----
+  m.def("read_header", [](const std::string& f) { return header_to_dict(read_header_file(f)); });
+  m.def("read_killfile", [](const std::string& f, int nchans) {
+    bool ok = true;
+    auto v = read_killfile(f, nchans, &ok);
+    return py::make_tuple(v, ok);
+  });
+  m.def("read_zapfile", [](const std::string& f) {
+    std::vector<float> a, b;
+    read_zapfile(f, a, b);
+    return py::make_tuple(a, b);
+  });
+  m.def("write_filterbank", [](const std::string& f, const py::dict& hdr, py::array_t<uint8_t, py::array::c_style> data) {
+    SigprocHeader h = dict_to_header(hdr);
+    std::vector<uint8_t> v(data.data(), data.data() + data.size());
+    Filterbank fb = Filterbank::from_memory(h, std::move(v));
+    fb.write(f);
+  });
+  m.def("read_tim", [](const std::string& f) {
+    TimeSeriesFile t = read_tim(f);
+    return py::make_tuple(header_to_dict(t.header), py::array_t<float>(t.data.size(), t.data.data()));
+  });
+  m.def("write_tim", [](const std::string& f, const py::dict& hdr, const std::vector<float>& data) {
+    write_tim(f, dict_to_header(hdr), data);
+  });
+
+  py::class_<Filterbank>(m, "Filterbank")
+      .def_static("from_file", &Filterbank::from_file)
+      .def_property_readonly("header", [](const Filterbank& fb) { return header_to_dict(fb.header()); })
+      .def_property_readonly("nsamps", &Filterbank::nsamps)
+      .def_property_readonly("nchans", &Filterbank::nchans)
+      .def_property_readonly("nbits", &Filterbank::nbits)
+      .def_property_readonly("tsamp", &Filterbank::tsamp)
+      .def_property_readonly("fch1", &Filterbank::fch1)
+      .def_property_readonly("foff", &Filterbank::foff)
+      .def_property_readonly("data_bytes", &Filterbank::data_bytes)
+      .def_property_readonly("data_address", [](const Filterbank& fb) { return reinterpret_cast<uintptr_t>(fb.data()); })
+      .def("cfreq", &Filterbank::cfreq)
+      .def("data", [](const Filterbank& fb) {
+        // zero-copy read-only view of the mmapped data block
+        py::array_t<uint8_t> a({static_cast<py::ssize_t>(fb.data_bytes())}, {1}, fb.data(), py::cast(fb));
+        py::detail::array_proxy(a.ptr())->flags &= ~py::detail::npy_api::NPY_ARRAY_WRITEABLE_;
+        return a;
+      });
+
+  // -------------------------------------------------------------- plans ---
+  m.def("generate_dm_list", &generate_dm_list, py::arg("dm_start"), py::arg("dm_end"), py::arg("tsamp"),
+        py::arg("pulse_width_us"), py::arg("fch1"), py::arg("foff"), py::arg("nchans"), py::arg("tol"));
+  m.def("generate_delay_table", &generate_delay_table);
+  m.def("compute_max_delay", &compute_max_delay);
+  py::enum_<AccelConvention>(m, "AccelConvention")
+      .value("Legacy", AccelConvention::Legacy)
+      .value("Reference", AccelConvention::Reference);
+  py::class_<AccelPlan>(m, "AccelPlan")
+      .def(py::init<float, float, float, float, uint64_t, float, float, float, AccelConvention>(), py::arg("acc_lo"),
+           py::arg("acc_hi"), py::arg("tol"), py::arg("pulse_width"), py::arg("nsamps"), py::arg("tsamp"),
+           py::arg("cfreq"), py::arg("bw"), py::arg("convention") = AccelConvention::Legacy)
+      .def("generate", &AccelPlan::generate)
+      .def("step", &AccelPlan::step);
+
+  // --------------------------------------------------------- candidates ---
+  py::class_<Candidate>(m, "Candidate")
+      .def(py::init<>())
+      .def(py::init<float, int, float, int, float, float>(), py::arg("dm"), py::arg("dm_idx"), py::arg("acc"),
+           py::arg("nh"), py::arg("snr"), py::arg("freq"))
+      .def_readwrite("dm", &Candidate::dm)
+      .def_readwrite("dm_idx", &Candidate::dm_idx)
+      .def_readwrite("acc", &Candidate::acc)
+      .def_readwrite("nh", &Candidate::nh)
+      .def_readwrite("snr", &Candidate::snr)
+      .def_readwrite("freq", &Candidate::freq)
+      .def_readwrite("folded_snr", &Candidate::folded_snr)
+      .def_readwrite("opt_period", &Candidate::opt_period)
+      .def_readwrite("is_adjacent", &Candidate::is_adjacent)
+      .def_readwrite("is_physical", &Candidate::is_physical)
+      .def_readwrite("ddm_count_ratio", &Candidate::ddm_count_ratio)
+      .def_readwrite("ddm_snr_ratio", &Candidate::ddm_snr_ratio)
+      .def_readwrite("assoc", &Candidate::assoc)
+      .def_readwrite("fold", &Candidate::fold)
+      .def_readwrite("nbins", &Candidate::nbins)
+      .def_readwrite("nints", &Candidate::nints)
+      .def("count_assoc", &Candidate::count_assoc)
+      .def("print", &Candidate::print)
+      .def("pods", [](const Candidate& c) {
+        std::vector<CandidatePOD> v;
+        c.collect_candidates(v);
+        py::list out;
+        for (auto& p : v) out.append(py::make_tuple(p.dm, p.dm_idx, p.acc, p.nh, p.snr, p.freq));
+        return out;
+      })
+      .def("__repr__", [](const Candidate& c) {
+        char b[256];
+        std::snprintf(b, sizeof b, "<Candidate P=%.9f dm=%.3f acc=%.2f nh=%d snr=%.2f fsnr=%.2f nassoc=%d>",
+                      1.0 / c.freq, c.dm, c.acc, c.nh, c.snr, c.folded_snr, c.count_assoc());
+        return std::string(b);
+      });
+  py::class_<HarmonicDistiller>(m, "HarmonicDistiller")
+      .def(py::init<float, float, bool, bool>(), py::arg("tol"), py::arg("max_harm"), py::arg("keep_related"),
+           py::arg("fractional_harms") = true)
+      .def("distill", &HarmonicDistiller::distill);
+  py::class_<AccelerationDistiller>(m, "AccelerationDistiller")
+      .def(py::init<float, float, bool>(), py::arg("tobs"), py::arg("tol"), py::arg("keep_related"))
+      .def("distill", &AccelerationDistiller::distill);
+  py::class_<DMDistiller>(m, "DMDistiller")
+      .def(py::init<float, bool>(), py::arg("tol"), py::arg("keep_related"))
+      .def("distill", &DMDistiller::distill);
+  py::class_<CandidateScorer>(m, "CandidateScorer")
+      .def(py::init<float, float, float, float>(), py::arg("tsamp"), py::arg("cfreq"), py::arg("foff"), py::arg("bw"))
+      .def("score_all", [](const CandidateScorer& s, CandidateList c) {
+        s.score_all(c);
+        return c;
+      });
+  m.def("identify_unique_peaks", [](const std::vector<int>& idxs, const std::vector<float>& snrs, int min_gap) {
+    std::vector<int> pi;
+    std::vector<float> ps;
+    identify_unique_peaks(idxs.data(), snrs.data(), std::min(idxs.size(), snrs.size()), min_gap, pi, ps);
+    return py::make_tuple(pi, ps);
+  });
+  m.def("peak_bounds", [](int nbins, float bin_width, int nh, float min_freq, float max_freq) {
+    PeakBounds b = peak_bounds(nbins, bin_width, nh, min_freq, max_freq);
+    return py::make_tuple(b.start_idx, b.end_idx, b.factor);
+  });
+  m.def("sort_by_folded_snr", [](CandidateList c) {
+    sort_by_folded_snr(c);
+    return c;
+  });
+  m.def("serialize_candidates", [](const CandidateList& c) {
+    auto v = serialize_candidates(c);
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+  });
+  m.def("deserialize_candidates", [](py::buffer b) {
+    py::buffer_info info = b.request();
+    return deserialize_candidates(static_cast<const uint8_t*>(info.ptr), static_cast<size_t>(info.size * info.itemsize));
+  });
+  m.def("deserialize_candidates_at", [](uintptr_t addr, size_t n) {
+    return deserialize_candidates(reinterpret_cast<const uint8_t*>(addr), n);
+  });
+
+  // ----------------------------------------------------------------- cli --
+  py::class_<CmdLineOptions>(m, "CmdLineOptions")
+      .def(py::init<>())
+      .def_readwrite("infilename", &CmdLineOptions::infilename)
+      .def_readwrite("outdir", &CmdLineOptions::outdir)
+      .def_readwrite("killfilename", &CmdLineOptions::killfilename)
+      .def_readwrite("zapfilename", &CmdLineOptions::zapfilename)
+      .def_readwrite("max_num_threads", &CmdLineOptions::max_num_threads)
+      .def_readwrite("limit", &CmdLineOptions::limit)
+      .def_readwrite("size", &CmdLineOptions::size)
+      .def_readwrite("dm_start", &CmdLineOptions::dm_start)
+      .def_readwrite("dm_end", &CmdLineOptions::dm_end)
+      .def_readwrite("dm_tol", &CmdLineOptions::dm_tol)
+      .def_readwrite("dm_pulse_width", &CmdLineOptions::dm_pulse_width)
+      .def_readwrite("acc_start", &CmdLineOptions::acc_start)
+      .def_readwrite("acc_end", &CmdLineOptions::acc_end)
+      .def_readwrite("acc_tol", &CmdLineOptions::acc_tol)
+      .def_readwrite("acc_pulse_width", &CmdLineOptions::acc_pulse_width)
+      .def_readwrite("boundary_5_freq", &CmdLineOptions::boundary_5_freq)
+      .def_readwrite("boundary_25_freq", &CmdLineOptions::boundary_25_freq)
+      .def_readwrite("nharmonics", &CmdLineOptions::nharmonics)
+      .def_readwrite("npdmp", &CmdLineOptions::npdmp)
+      .def_readwrite("min_snr", &CmdLineOptions::min_snr)
+      .def_readwrite("min_freq", &CmdLineOptions::min_freq)
+      .def_readwrite("max_freq", &CmdLineOptions::max_freq)
+      .def_readwrite("max_harm", &CmdLineOptions::max_harm)
+      .def_readwrite("freq_tol", &CmdLineOptions::freq_tol)
+      .def_readwrite("verbose", &CmdLineOptions::verbose)
+      .def_readwrite("progress_bar", &CmdLineOptions::progress_bar)
+      .def_readwrite("accel_convention", &CmdLineOptions::accel_convention)
+      .def_readwrite("dedisp_kernel", &CmdLineOptions::dedisp_kernel)
+      .def_readwrite("accel_batch", &CmdLineOptions::accel_batch)
+      .def_readwrite("use_boundaries", &CmdLineOptions::use_boundaries)
+      .def_readwrite("checkpoint_dir", &CmdLineOptions::checkpoint_dir)
+      .def_readwrite("trace_json", &CmdLineOptions::trace_json)
+      .def_readwrite("fault_after_dms", &CmdLineOptions::fault_after_dms);
+  m.def("parse_cmdline", [](const std::vector<std::string>& argv) {
+    CmdLineOptions a;
+    bool exit_now = false;
+    bool ok = parse_cmdline(a, argv, &exit_now);
+    return py::make_tuple(ok, exit_now, a);
+  });
+  m.def("cmdline_usage", &cmdline_usage);
+  m.def("default_outdir", &default_outdir);
+  py::class_<CoincidencerOptions>(m, "CoincidencerOptions")
+      .def(py::init<>())
+      .def_readwrite("filterbanks", &CoincidencerOptions::filterbanks)
+      .def_readwrite("samp_outfilename", &CoincidencerOptions::samp_outfilename)
+      .def_readwrite("spec_outfilename", &CoincidencerOptions::spec_outfilename)
+      .def_readwrite("threshold", &CoincidencerOptions::threshold)
+      .def_readwrite("beam_threshold", &CoincidencerOptions::beam_threshold)
+      .def_readwrite("nharmonics", &CoincidencerOptions::nharmonics)
+      .def_readwrite("verbose", &CoincidencerOptions::verbose);
+  m.def("parse_coincidencer_cmdline", [](const std::vector<std::string>& argv) {
+    CoincidencerOptions a;
+    bool exit_now = false;
+    std::vector<const char*> cv;
+    for (auto& s : argv) cv.push_back(s.c_str());
+    bool ok = parse_coincidencer_cmdline(a, static_cast<int>(cv.size()), cv.data(), &exit_now);
+    return py::make_tuple(ok, exit_now, a);
+  });
+
+  // -------------------------------------------------------------- output --
+  m.def("xml_fmt_float", [](float v) { return xml::fmt(v); });
+  m.def("xml_fmt_double", [](double v) { return xml::fmt(v); });
+  m.def("write_candidates_binary", [](const std::string& outdir, const CandidateList& c, const std::string& fname) {
+    CandidateFileWriter w(outdir);
+    w.write_binary(c, fname);
+    std::map<unsigned, long> bm = w.byte_mapping;
+    return bm;
+  });
+  m.def(
+      "write_overview",
+      [](const std::string& path, const CmdLineOptions& args, const py::object& header_file, const std::vector<float>& dms,
+         const std::vector<float>& accs, const std::vector<int>& devices, const CandidateList& cands,
+         const std::map<unsigned, long>& byte_map, const std::map<std::string, double>& timers,
+         const std::map<std::string, double>& perf) {
+        OverviewWriter ow;
+        ow.add_misc_info();
+        if (py::isinstance<py::str>(header_file)) ow.add_header(header_file.cast<std::string>());
+        else ow.add_header(dict_to_header(header_file.cast<py::dict>()));
+        ow.add_search_parameters(args);
+        ow.add_dm_list(dms);
+        ow.add_acc_list(accs);
+        if (!devices.empty()) ow.add_gpu_info(devices);
+        ow.add_candidates(cands, byte_map);
+        ow.add_timing_info(timers);
+        if (!perf.empty()) ow.add_performance(perf);
+        ow.to_file(path);
+      },
+      py::arg("path"), py::arg("args"), py::arg("header"), py::arg("dms"), py::arg("accs"), py::arg("devices"),
+      py::arg("cands"), py::arg("byte_map"), py::arg("timers"), py::arg("perf"));
+
+  // ------------------------------------------------------------- kernels --
+  py::module_ k = m.def_submodule("kernels", "raw HIP kernel launchers (addresses + stream handles)");
+  k.def("unpack_transpose", [](uintptr_t packed, uint64_t nsamps, int nchans, int nbits, uintptr_t out,
+                               uint64_t out_stride, int bias, uintptr_t s) {
+    kern::unpack_transpose(P<const uint8_t>(packed), nsamps, nchans, nbits, P<int8_t>(out), out_stride, bias, S(s));
+  });
+  k.def("dedisperse_direct", [](uintptr_t x, uint64_t stride, int nchans, uintptr_t offsets, uintptr_t kill, int ndm,
+                                uint64_t out_nsamps, uintptr_t out, uint64_t out_stride, float scale, int bias,
+                                int nactive, uintptr_t s) {
+    kern::dedisperse_direct(P<const int8_t>(x), stride, nchans, P<const int32_t>(offsets), P<const int32_t>(kill), ndm,
+                            out_nsamps, P<uint8_t>(out), out_stride, scale, bias, nactive, S(s));
+  });
+  k.def("u8_to_f32_pad", [](uintptr_t in, uint64_t nvalid, uintptr_t out, uint64_t n, uintptr_t sum, uintptr_t s) {
+    kern::u8_sum(P<const uint8_t>(in), nvalid, P<unsigned long long>(sum), S(s));
+    kern::u8_to_f32_pad(P<const uint8_t>(in), nvalid, P<float>(out), n, P<const unsigned long long>(sum), S(s));
+  });
+  k.def("f32_stats", [](uintptr_t x, uint64_t n, uintptr_t partials, int np, uintptr_t stats, uintptr_t s) {
+    kern::f32_stats(P<const float>(x), n, P<double>(partials), np, P<float>(stats), S(s));
+  });
+  k.def("form_amplitude", [](uintptr_t X, uint64_t nb, uintptr_t out, uintptr_t s) {
+    kern::form_amplitude(P<const float2>(X), nb, P<float>(out), S(s));
+  });
+  k.def("form_interbin", [](uintptr_t X, uint64_t nb, uintptr_t out, uintptr_t s) {
+    kern::form_interbin(P<const float2>(X), nb, P<float>(out), S(s));
+  });
+  k.def("normalise", [](uintptr_t x, uint64_t n, float mean, float sigma, uintptr_t s) {
+    kern::normalise(P<float>(x), n, mean, sigma, S(s));
+  });
+  k.def("median5_amp", [](uintptr_t X, uint64_t nb, uintptr_t out, uintptr_t s) {
+    kern::median5_amp(P<const float2>(X), nb, P<float>(out), S(s));
+  });
+  k.def("median5", [](uintptr_t in, uint64_t count, uintptr_t out, uintptr_t s) {
+    kern::median5(P<const float>(in), count, P<float>(out), S(s));
+  });
+  k.def("deredden_zap", [](uintptr_t X, uint64_t nb, uintptr_t m5, uint64_t n5, uintptr_t m25, uint64_t n25,
+                           uintptr_t m125, uint64_t n125, int64_t pos5, int64_t pos25, uintptr_t zap, uintptr_t s) {
+    kern::deredden_zap(P<float2>(X), nb, P<const float>(m5), n5, P<const float>(m25), n25, P<const float>(m125), n125,
+                       pos5, pos25, P<const uint32_t>(zap), S(s));
+  });
+  k.def("interbin_stats", [](uintptr_t X, uint64_t nb, uintptr_t Pout, uintptr_t partials, int np, uintptr_t stats,
+                             uintptr_t s) {
+    kern::interbin_stats(P<const float2>(X), nb, P<float>(Pout), P<double>(partials), np, P<float>(stats), S(s));
+  });
+  k.def("resample_batch", [](uintptr_t in, uint64_t n, uintptr_t out, uint64_t ostride, uintptr_t af, int K,
+                             uintptr_t s) {
+    kern::resample_batch(P<const float>(in), n, P<float>(out), ostride, P<const double>(af), K, S(s));
+  });
+  k.def("resample_v1", [](uintptr_t in, uint64_t n, uintptr_t out, double af, uintptr_t s) {
+    kern::resample_v1(P<const float>(in), n, P<float>(out), af, S(s));
+  });
+  k.def("interbin_normalise_batch", [](uintptr_t X, uint64_t nb, uint64_t xstride, uintptr_t Pout, uint64_t pstride,
+                                       int K, uint64_t nbo, uintptr_t stats, float nscale, uintptr_t s) {
+    kern::interbin_normalise_batch(P<const float2>(X), nb, xstride, P<float>(Pout), pstride, K, nbo,
+                                   P<const float>(stats), nscale, S(s));
+  });
+  k.def("harmonic_peaks_batch", [](uintptr_t Pin, uint64_t nb, uint64_t pstride, int K, int nlevels,
+                                   const std::vector<int>& start, const std::vector<int>& end, float thresh,
+                                   uint32_t capacity, uintptr_t out, uintptr_t count, uintptr_t s) {
+    kern::HarmParams hp{};
+    hp.nlevels = nlevels;
+    for (int i = 0; i < 6; ++i) {
+      hp.start[i] = i < static_cast<int>(start.size()) ? start[i] : 0;
+      hp.end[i] = i < static_cast<int>(end.size()) ? end[i] : 0;
+    }
+    hp.thresh = thresh;
+    hp.capacity = capacity;
+    kern::harmonic_peaks_batch(P<const float>(Pin), nb, pstride, K, hp, P<kern::PeakRecord>(out), P<uint32_t>(count),
+                               S(s));
+  });
+  k.def("harmonic_sums", [](uintptr_t Pin, uint64_t nb, int nlevels, uintptr_t out, uintptr_t s) {
+    kern::harmonic_sums(P<const float>(Pin), nb, nlevels, P<float>(out), S(s));
+  });
+  k.def("fold_shift_table", [](uintptr_t table, int nbins, int nints, uintptr_t s) {
+    kern::fold_shift_table(P<float2>(table), nbins, nints, S(s));
+  });
+  k.def("fold_optimise", [](uintptr_t folds, int nfold, uintptr_t table, uintptr_t opt_fold, uintptr_t opt_prof,
+                            uintptr_t opt_int, uintptr_t opt_val, uintptr_t s) {
+    kern::fold_optimise(P<const float>(folds), nfold, P<const float2>(table), P<float>(opt_fold), P<float>(opt_prof),
+                        P<int32_t>(opt_int), P<float>(opt_val), S(s));
+  });
+  k.def("count_above", [](uintptr_t x, uint64_t n, float thresh, uintptr_t counts, uintptr_t s) {
+    kern::count_above(P<const float>(x), n, thresh, P<uint8_t>(counts), S(s));
+  });
+  k.def("coincidence_mask", [](uintptr_t counts, uint64_t n, int beam_thresh, uintptr_t mask, uintptr_t s) {
+    kern::coincidence_mask(P<const uint8_t>(counts), n, beam_thresh, P<float>(mask), S(s));
+  });
+  k.def("conjugate", [](uintptr_t x, uint64_t n, uintptr_t s) { kern::conjugate(P<float2>(x), n, S(s)); });
+  k.def("cmul_inplace", [](uintptr_t x, uintptr_t y, uint64_t n, uintptr_t s) {
+    kern::cmul_inplace(P<const float2>(x), P<float2>(y), n, S(s));
+  });
+
+  // ------------------------------------------------------------- fft ------
+  py::enum_<FftType>(m, "FftType")
+      .value("R2C", FftType::R2C)
+      .value("C2R", FftType::C2R)
+      .value("C2C_FWD", FftType::C2C_FWD)
+      .value("C2C_INV", FftType::C2C_INV);
+  py::class_<FftPlan>(m, "FftPlan")
+      .def(py::init<FftType, uint64_t, uint64_t, uint64_t, uint64_t, bool>(), py::arg("type"), py::arg("n"),
+           py::arg("batch") = 1, py::arg("in_dist") = 0, py::arg("out_dist") = 0, py::arg("inplace") = false)
+      .def("execute", [](FftPlan& p, uintptr_t in, uintptr_t out, uintptr_t s) { p.execute(P<void>(in), P<void>(out), S(s)); })
+      .def_property_readonly("work_bytes", &FftPlan::work_bytes);
+
+  // ------------------------------------------------------------- engine ---
+  py::enum_<DedispKernel>(m, "DedispKernel")
+      .value("Auto", DedispKernel::Auto)
+      .value("Direct", DedispKernel::Direct)
+      .value("Mfma", DedispKernel::Mfma);
+  py::class_<DedispGeometry>(m, "DedispGeometry")
+      .def_static("make", [](const py::dict& hdr, uint64_t nsamps, const std::vector<float>& dms,
+                             const std::vector<int>& kill) { return DedispGeometry::make(dict_to_header(hdr), nsamps, dms, kill); })
+      .def_readonly("nchans", &DedispGeometry::nchans)
+      .def_readonly("nbits", &DedispGeometry::nbits)
+      .def_readonly("nsamps", &DedispGeometry::nsamps)
+      .def_readonly("dm_list", &DedispGeometry::dm_list)
+      .def_readonly("delays", &DedispGeometry::delays)
+      .def_readonly("killmask", &DedispGeometry::killmask)
+      .def_readonly("max_delay", &DedispGeometry::max_delay)
+      .def_readonly("out_nsamps", &DedispGeometry::out_nsamps)
+      .def_readonly("out_scale", &DedispGeometry::out_scale)
+      .def_readonly("bias", &DedispGeometry::bias)
+      .def_readonly("nactive", &DedispGeometry::nactive)
+      .def("offsets", &DedispGeometry::offsets);
+  py::class_<DeviceFilterbank>(m, "DeviceFilterbank")
+      .def(py::init([](const DedispGeometry& g, uintptr_t s) { return new DeviceFilterbank(g, S(s)); }),
+           py::keep_alive<1, 2>())
+      .def("load_packed_device", [](DeviceFilterbank& f, uintptr_t p) { f.load_packed_device(P<const uint8_t>(p)); })
+      .def("load_packed_host", [](DeviceFilterbank& f, uintptr_t p) { f.load_packed_host(P<const uint8_t>(p)); },
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("data_address", [](const DeviceFilterbank& f) { return reinterpret_cast<uintptr_t>(f.data()); })
+      .def_property_readonly("stride", &DeviceFilterbank::stride);
+  py::class_<Dedisperser>(m, "Dedisperser")
+      .def(py::init([](const DeviceFilterbank& fb, uintptr_t s) { return new Dedisperser(fb, S(s)); }),
+           py::keep_alive<1, 2>())
+      .def("run", [](Dedisperser& d, int d0, int d1, uintptr_t out, uint64_t ostride, DedispKernel k) {
+        d.run(d0, d1, P<uint8_t>(out), ostride, k);
+      }, py::call_guard<py::gil_scoped_release>())
+      .def_static("row_stride", &Dedisperser::row_stride);
+
+  py::class_<SearchParams>(m, "SearchParams")
+      .def(py::init<>())
+      .def_readwrite("fft_size", &SearchParams::fft_size)
+      .def_readwrite("tsamp", &SearchParams::tsamp)
+      .def_readwrite("min_snr", &SearchParams::min_snr)
+      .def_readwrite("min_freq", &SearchParams::min_freq)
+      .def_readwrite("max_freq", &SearchParams::max_freq)
+      .def_readwrite("nharmonics", &SearchParams::nharmonics)
+      .def_readwrite("freq_tol", &SearchParams::freq_tol)
+      .def_readwrite("max_harm", &SearchParams::max_harm)
+      .def_readwrite("boundary_5_freq", &SearchParams::boundary_5_freq)
+      .def_readwrite("boundary_25_freq", &SearchParams::boundary_25_freq)
+      .def_readwrite("zap_freqs", &SearchParams::zap_freqs)
+      .def_readwrite("zap_widths", &SearchParams::zap_widths)
+      .def_readwrite("accel_batch", &SearchParams::accel_batch)
+      .def_readwrite("batch_bytes", &SearchParams::batch_bytes)
+      .def_readwrite("min_gap", &SearchParams::min_gap);
+  py::class_<SearchEngine>(m, "SearchEngine")
+      .def(py::init([](const SearchParams& p, uintptr_t s) { return new SearchEngine(p, S(s)); }))
+      .def("search_trial", [](SearchEngine& e, uintptr_t trial, uint64_t nsamps, float dm, int dm_idx,
+                              const std::vector<float>& accs) {
+        return e.search_trial(P<const uint8_t>(trial), nsamps, dm, dm_idx, accs);
+      }, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("batch_size", &SearchEngine::batch_size)
+      .def_property_readonly("tobs", &SearchEngine::tobs)
+      .def_property_readonly("whitened_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.whitened()); })
+      .def_property_readonly("stats_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.whitener().stats()); })
+      .def("counters", [](const SearchEngine& e) {
+        const SearchCounters& c = e.counters();
+        py::dict d;
+        d["dm_trials"] = c.dm_trials;
+        d["accel_trials"] = c.accel_trials;
+        d["peaks"] = c.peaks;
+        d["overflows"] = c.overflows;
+        d["accel_s"] = c.accel_s;
+        d["host_s"] = c.host_s;
+        return d;
+      })
+      .def("reset_counters", &SearchEngine::reset_counters);
+  m.def("build_zap_mask", &build_zap_mask);
+  m.def("fold_calculate_sn", [](const std::vector<float>& prof, int bin, int width) {
+    float a = 0, b = 0;
+    fold_calculate_sn(prof.data(), bin, width, static_cast<int>(prof.size()), &a, &b);
+    return py::make_tuple(a, b);
+  });
+  py::class_<FoldResult>(m, "FoldResult")
+      .def_readonly("folded_snr", &FoldResult::folded_snr)
+      .def_readonly("opt_period", &FoldResult::opt_period)
+      .def_readonly("opt_width", &FoldResult::opt_width)
+      .def_readonly("opt_bin", &FoldResult::opt_bin)
+      .def_readonly("fold", &FoldResult::fold)
+      .def_readonly("prof", &FoldResult::prof);
+  py::class_<FoldEngine>(m, "FoldEngine")
+      .def(py::init([](uint64_t n, float tsamp, uintptr_t s) { return new FoldEngine(n, tsamp, S(s)); }))
+      .def("fold_trial", [](FoldEngine& f, uintptr_t trial, uint64_t nsamps, const std::vector<double>& periods,
+                            const std::vector<float>& accs) { return f.fold_trial(P<const uint8_t>(trial), nsamps, periods, accs); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("fold_series", [](FoldEngine& f, uintptr_t series, const std::vector<double>& periods,
+                             const std::vector<float>& accs) { return f.fold_series(P<const float>(series), periods, accs); },
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("nsamps", &FoldEngine::nsamps);
+  m.def("coincidencer_beam", [](uintptr_t trial, uint64_t n, float tsamp, uintptr_t series_out, uintptr_t spec_out,
+                                uintptr_t s) {
+    BeamProducts bp;
+    coincidencer_beam(P<const uint8_t>(trial), n, tsamp, bp, S(s));
+    PSOUP_HIP_CHECK(hipMemcpyAsync(P<float>(series_out), bp.series.data(), n * 4, hipMemcpyDeviceToDevice, S(s)));
+    PSOUP_HIP_CHECK(hipMemcpyAsync(P<float>(spec_out), bp.spectrum.data(), (n / 2 + 1) * 4, hipMemcpyDeviceToDevice, S(s)));
+    PSOUP_HIP_CHECK(hipStreamSynchronize(S(s)));
+  });
+  m.def("write_samp_mask", &write_samp_mask);
+  m.def("write_birdie_list", &write_birdie_list);
+
+  // ----------------------------------------------------------- pipeline ---
+  m.def("run_pipeline_native", [](const CmdLineOptions& args) {
+    PipelineResult r;
+    {
+      py::gil_scoped_release nogil;
+      r = run_pipeline(args);
+      write_outputs(args, r);
+    }
+    py::dict d;
+    d["candidates"] = r.candidates;
+    d["timers"] = r.timers;
+    d["performance"] = r.performance;
+    d["dm_list"] = r.setup.dm_list;
+    d["fft_size"] = r.setup.fft_size;
+    return d;
+  });
+  m.def("accel_list_for", [](const CmdLineOptions& args, const py::dict& hdr, float dm) {
+    SearchSetup s = make_search_setup(args, dict_to_header(hdr));
+    return s.accel_plan.generate(dm);
+  });
+  m.def("global_distill_and_score", [](CandidateList c, const CmdLineOptions& args, const py::dict& hdr) {
+    SearchSetup s = make_search_setup(args, dict_to_header(hdr));
+    return global_distill_and_score(std::move(c), args, s);
+  });
+  m.def("search_params_from_args", [](const CmdLineOptions& args, const py::dict& hdr) {
+    SearchSetup s = make_search_setup(args, dict_to_header(hdr));
+    return py::make_tuple(s.search, s.dm_list, s.killmask, s.fft_size, s.cfreq);
+  });
+}

@@ -1,0 +1,332 @@
+#include "psoup/candidates.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "psoup/common.hpp"
+
+namespace psoup {
+
+static constexpr double kSpeedOfLight = 299792458.0;
+
+int Candidate::count_assoc() const {
+  int count = 0;
+  for (const auto& a : assoc) {
+    count++;
+    count += a.count_assoc();
+  }
+  return count;
+}
+
+void Candidate::collect_candidates(std::vector<CandidatePOD>& out) const {
+  out.push_back(pod());
+  for (const auto& a : assoc) a.collect_candidates(out);
+}
+
+void Candidate::set_fold(const float* ar, int nbins_, int nints_) {
+  nbins = nbins_;
+  nints = nints_;
+  fold.assign(ar, ar + static_cast<size_t>(nbins_) * nints_);
+}
+
+std::string Candidate::print() const {
+  char buf[512];
+  std::snprintf(buf, sizeof(buf), "%.15f\t%.15f\t%.15f\t%.2f\t%.2f\t%d\t%.1f\t%.1f\t%d\t%d\t%.4f\t%.4f\t%d\n",
+                1.0 / freq, opt_period, static_cast<double>(freq), static_cast<double>(dm),
+                static_cast<double>(acc), nh, static_cast<double>(snr), static_cast<double>(folded_snr),
+                static_cast<int>(is_adjacent), static_cast<int>(is_physical),
+                static_cast<double>(ddm_count_ratio), static_cast<double>(ddm_snr_ratio),
+                static_cast<int>(assoc.size()));
+  std::string s(buf);
+  for (const auto& a : assoc) s += a.print();
+  return s;
+}
+
+namespace {
+
+// BaseDistiller::distill (distiller.hpp:27-59) with a pluggable condition.
+template <class Cond>
+CandidateList base_distill(CandidateList cands, Cond&& condition) {
+  const size_t size = cands.size();
+  std::vector<char> unique(size, 1);
+  // std::sort (not stable_sort) on purpose: with the same input order it breaks
+  // S/N ties exactly as the reference's libstdc++ introsort does.
+  std::sort(cands.begin(), cands.end(), [](const Candidate& a, const Candidate& b) { return a.snr > b.snr; });
+  size_t start = 0;
+  while (true) {
+    long idx = -1;
+    for (size_t ii = start; ii < size; ++ii) {
+      if (unique[ii]) {
+        start = ii + 1;
+        idx = static_cast<long>(ii);
+        break;
+      }
+    }
+    if (idx < 0) break;
+    condition(cands, static_cast<size_t>(idx), unique);
+  }
+  CandidateList out;
+  for (size_t ii = 0; ii < size; ++ii)
+    if (unique[ii]) out.push_back(std::move(cands[ii]));
+  return out;
+}
+
+}  // namespace
+
+CandidateList HarmonicDistiller::distill(CandidateList cands) const {
+  const double upper_tol = 1 + tol_;
+  const double lower_tol = 1 - tol_;
+  const float max_harm = max_harm_;
+  const bool keep = keep_related_, frac = fractional_;
+  return base_distill(std::move(cands), [&](CandidateList& c, size_t idx, std::vector<char>& unique) {
+    const double fundi_freq = c[idx].freq;
+    const size_t size = c.size();
+    for (size_t ii = idx + 1; ii < size; ++ii) {
+      const double freq = c[ii].freq;
+      const int nh = c[ii].nh;
+      const float max_denominator = frac ? static_cast<float>(std::pow(2.0, nh)) : 1.f;
+      for (int jj = 1; jj <= max_harm; ++jj) {
+        for (int kk = 1; kk <= max_denominator; ++kk) {
+          const double ratio = kk * freq / (jj * fundi_freq);
+          if (ratio > lower_tol && ratio < upper_tol) {
+            if (keep) c[idx].append(c[ii]);
+            unique[ii] = 0;
+          }
+        }
+      }
+    }
+  });
+}
+
+AccelerationDistiller::AccelerationDistiller(float tobs, float tol, bool keep_related)
+    : tobs_(tobs), tol_(tol), keep_related_(keep_related) {
+  tobs_over_c_ = tobs_ / kSpeedOfLight;
+}
+
+CandidateList AccelerationDistiller::distill(CandidateList cands) const {
+  const double toc = tobs_over_c_;
+  const float tol = tol_;
+  const bool keep = keep_related_;
+  return base_distill(std::move(cands), [&](CandidateList& c, size_t idx, std::vector<char>& unique) {
+    const double fundi_freq = c[idx].freq;
+    const double fundi_acc = c[idx].acc;
+    const double edge = fundi_freq * tol;
+    const size_t size = c.size();
+    for (size_t ii = idx + 1; ii < size; ++ii) {
+      const double delta_acc = fundi_acc - c[ii].acc;
+      // correct_for_acceleration returns float (distiller.hpp:120-122).
+      const double acc_freq = static_cast<float>(fundi_freq + delta_acc * fundi_freq * toc);
+      const double f = c[ii].freq;
+      bool related;
+      if (acc_freq > fundi_freq)
+        related = (f > fundi_freq - edge && f < acc_freq + edge);
+      else
+        related = (f < fundi_freq + edge && f > acc_freq - edge);
+      if (related) {
+        if (keep) c[idx].append(c[ii]);
+        unique[ii] = 0;
+      }
+    }
+  });
+}
+
+CandidateList DMDistiller::distill(CandidateList cands) const {
+  const double upper_tol = 1 + tol_;
+  const double lower_tol = 1 - tol_;
+  const bool keep = keep_related_;
+  return base_distill(std::move(cands), [&](CandidateList& c, size_t idx, std::vector<char>& unique) {
+    const double fundi_freq = c[idx].freq;
+    const size_t size = c.size();
+    for (size_t ii = idx + 1; ii < size; ++ii) {
+      const double ratio = c[ii].freq / fundi_freq;
+      if (ratio > lower_tol && ratio < upper_tol) {
+        if (keep) c[idx].append(c[ii]);
+        unique[ii] = 0;
+      }
+    }
+  });
+}
+
+CandidateScorer::CandidateScorer(float tsamp, float cfreq, float foff, float bw)
+    : tsamp_(tsamp), cfreq_(cfreq), foff_(foff) {
+  float ftop = static_cast<float>(cfreq + bw / 2.0);
+  float fbottom = static_cast<float>(cfreq - bw / 2.0);
+  tdm_chan_partial_ = static_cast<float>(8300.0 * foff / std::pow(cfreq, 3.0));
+  tdm_band_partial_ = static_cast<float>(4150.0 * (1.0 / std::pow(fbottom, 2) - 1.0 / std::pow(ftop, 2)));
+}
+
+void CandidateScorer::score(Candidate& cand) const {
+  cand.is_physical = 1.0 / cand.freq > cand.dm * tdm_chan_partial_;
+  {
+    const int idx = cand.dm_idx;
+    bool adjacent = false, unique = true;
+    for (const auto& a : cand.assoc) {
+      if (a.dm_idx != idx) unique = false;
+      if (a.dm_idx == idx + 1 || a.dm_idx == idx - 1) {
+        adjacent = true;
+        break;
+      }
+    }
+    cand.is_adjacent = adjacent || unique;
+  }
+  {
+    int inside_count = 1, total_count = 1;
+    float inside_snr = cand.snr, total_snr = cand.snr;
+    float ddm = static_cast<float>(1.0 / (cand.freq * tdm_band_partial_));
+    for (const auto& a : cand.assoc) {
+      total_count++;
+      total_snr += a.snr;
+      if (std::fabs(cand.dm - a.dm) <= ddm) {
+        inside_count++;
+        inside_snr += a.snr;
+      }
+    }
+    cand.ddm_count_ratio = static_cast<float>(inside_count) / total_count;
+    cand.ddm_snr_ratio = inside_snr / total_snr;
+  }
+}
+
+void CandidateScorer::score_all(CandidateList& cands) const {
+  for (auto& c : cands) score(c);
+}
+
+void identify_unique_peaks(const int* idxs, const float* snrs, size_t count, int min_gap,
+                           std::vector<int>& peak_idxs, std::vector<float>& peak_snrs) {
+  size_t ii = 0;
+  while (ii < count) {
+    float cpeak = snrs[ii];
+    int cpeakidx = idxs[ii];
+    int lastidx = idxs[ii];
+    ii++;
+    while (ii < count && (idxs[ii] - lastidx) < min_gap) {
+      if (snrs[ii] > cpeak) {
+        cpeak = snrs[ii];
+        cpeakidx = idxs[ii];
+        lastidx = idxs[ii];
+      }
+      ii++;
+    }
+    peak_idxs.push_back(cpeakidx);
+    peak_snrs.push_back(cpeak);
+  }
+}
+
+PeakBounds peak_bounds(int size, float bin_width, int nh, float min_freq, float max_freq) {
+  PeakBounds b;
+  const float nyquist = bin_width * size;
+  const int orig_size = static_cast<int>(2.0 * (size - 1.0));
+  const double p2 = std::pow(2.0, nh);
+  const int max_bin = static_cast<int>((max_freq / bin_width) * p2);
+  b.start_idx = static_cast<int>(orig_size * (min_freq / nyquist) * p2);
+  b.end_idx = std::min(size, max_bin);
+  b.factor = 1.0 / size * nyquist / std::pow(2.0, static_cast<float>(nh));
+  if (b.start_idx < 0) b.start_idx = 0;
+  return b;
+}
+
+void sort_by_folded_snr(CandidateList& cands) {
+  std::stable_sort(cands.begin(), cands.end(), [](const Candidate& x, const Candidate& y) {
+    return std::max(x.snr, x.folded_snr) > std::max(y.snr, y.folded_snr);
+  });
+}
+
+// ------------------------------------------------------------ serialise ----
+namespace {
+#pragma pack(push, 1)
+struct NodeRec {
+  float dm;
+  int32_t dm_idx;
+  float acc;
+  int32_t nh;
+  float snr;
+  float freq;
+  float folded_snr;
+  double opt_period;
+  uint8_t is_adjacent;
+  uint8_t is_physical;
+  float ddm_count_ratio;
+  float ddm_snr_ratio;
+  int32_t nbins;
+  int32_t nints;
+  int32_t nfold;
+  int32_t nassoc;
+};
+#pragma pack(pop)
+
+void put(std::vector<uint8_t>& out, const void* p, size_t n) {
+  const uint8_t* b = static_cast<const uint8_t*>(p);
+  out.insert(out.end(), b, b + n);
+}
+
+void ser_node(const Candidate& c, std::vector<uint8_t>& out) {
+  NodeRec r{c.dm, c.dm_idx, c.acc, c.nh, c.snr, c.freq, c.folded_snr, c.opt_period,
+            static_cast<uint8_t>(c.is_adjacent), static_cast<uint8_t>(c.is_physical), c.ddm_count_ratio,
+            c.ddm_snr_ratio, c.nbins, c.nints, static_cast<int32_t>(c.fold.size()),
+            static_cast<int32_t>(c.assoc.size())};
+  put(out, &r, sizeof(r));
+  if (!c.fold.empty()) put(out, c.fold.data(), c.fold.size() * sizeof(float));
+  for (const auto& a : c.assoc) ser_node(a, out);
+}
+
+struct Reader {
+  const uint8_t* p;
+  size_t n, off = 0;
+  void get(void* dst, size_t k) {
+    PSOUP_CHECK(off + k <= n, "truncated candidate stream");
+    std::memcpy(dst, p + off, k);
+    off += k;
+  }
+};
+
+Candidate de_node(Reader& r, int depth) {
+  PSOUP_CHECK(depth < 64, "candidate tree too deep");
+  NodeRec rec;
+  r.get(&rec, sizeof(rec));
+  Candidate c(rec.dm, rec.dm_idx, rec.acc, rec.nh, rec.snr, rec.freq);
+  c.folded_snr = rec.folded_snr;
+  c.opt_period = rec.opt_period;
+  c.is_adjacent = rec.is_adjacent != 0;
+  c.is_physical = rec.is_physical != 0;
+  c.ddm_count_ratio = rec.ddm_count_ratio;
+  c.ddm_snr_ratio = rec.ddm_snr_ratio;
+  c.nbins = rec.nbins;
+  c.nints = rec.nints;
+  PSOUP_CHECK(rec.nfold >= 0 && rec.nassoc >= 0, "corrupt candidate record");
+  if (rec.nfold > 0) {
+    c.fold.resize(static_cast<size_t>(rec.nfold));
+    r.get(c.fold.data(), c.fold.size() * sizeof(float));
+  }
+  c.assoc.reserve(static_cast<size_t>(rec.nassoc));
+  for (int i = 0; i < rec.nassoc; ++i) c.assoc.push_back(de_node(r, depth + 1));
+  return c;
+}
+}  // namespace
+
+std::vector<uint8_t> serialize_candidates(const CandidateList& cands) {
+  std::vector<uint8_t> out;
+  uint32_t magic = 0x50534F43u;  // "PSOC"
+  int64_t n = static_cast<int64_t>(cands.size());
+  put(out, &magic, 4);
+  put(out, &n, 8);
+  for (const auto& c : cands) ser_node(c, out);
+  return out;
+}
+
+CandidateList deserialize_candidates(const uint8_t* data, size_t nbytes) {
+  CandidateList out;
+  if (nbytes == 0) return out;
+  Reader r{data, nbytes};
+  uint32_t magic = 0;
+  int64_t n = 0;
+  r.get(&magic, 4);
+  PSOUP_CHECK(magic == 0x50534F43u, "bad candidate stream magic");
+  r.get(&n, 8);
+  PSOUP_CHECK(n >= 0, "bad candidate count");
+  out.reserve(static_cast<size_t>(n));
+  for (int64_t i = 0; i < n; ++i) out.push_back(de_node(r, 0));
+  return out;
+}
+
+}  // namespace psoup

@@ -1,0 +1,109 @@
+#include "psoup/common.hpp"
+
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include <atomic>
+#include <cstring>
+#include <iostream>
+#include <mutex>
+
+namespace psoup {
+
+namespace {
+std::atomic<int> g_rank{-1};
+std::atomic<int> g_level{static_cast<int>(LogLevel::Info)};
+std::mutex g_log_mutex;
+
+std::string prefix() {
+  int r = g_rank.load();
+  if (r < 0) return "";
+  return "[rank " + std::to_string(r) + "] ";
+}
+}  // namespace
+
+int log_rank() { return g_rank.load(); }
+void set_log_rank(int rank) { g_rank.store(rank); }
+
+bool debug_sync_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("PSOUP_DEBUG_SYNC");
+    return v && std::strcmp(v, "0") != 0;
+  }();
+  return on;
+}
+
+void throw_error(const std::string& what, const char* file, int line) {
+  std::ostringstream os;
+  os << prefix() << what << " [" << file << ":" << line << "]";
+  throw Error(os.str());
+}
+
+void post_launch_check(const char* kernel, hipStream_t stream) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess)
+    PSOUP_THROW("launch of " << kernel << " failed: " << hipGetErrorName(e) << " ("
+                             << hipGetErrorString(e) << ")");
+  if (debug_sync_enabled()) {
+    e = hipStreamSynchronize(stream);
+    if (e != hipSuccess)
+      PSOUP_THROW("kernel " << kernel << " faulted: " << hipGetErrorName(e) << " ("
+                            << hipGetErrorString(e) << ")");
+  }
+}
+
+void set_log_level(LogLevel lvl) { g_level.store(static_cast<int>(lvl)); }
+LogLevel log_level() { return static_cast<LogLevel>(g_level.load()); }
+
+void log_info(const std::string& msg) {
+  if (g_level.load() < static_cast<int>(LogLevel::Info)) return;
+  std::lock_guard<std::mutex> lk(g_log_mutex);
+  std::cout << prefix() << msg << std::endl;
+}
+
+void log_verbose(const std::string& msg) {
+  if (g_level.load() < static_cast<int>(LogLevel::Verbose)) return;
+  std::lock_guard<std::mutex> lk(g_log_mutex);
+  std::cout << prefix() << msg << std::endl;
+}
+
+RoctxRange::RoctxRange(const char* name) : active_(true) { roctxRangePushA(name); }
+RoctxRange::~RoctxRange() {
+  if (active_) roctxRangePop();
+}
+
+void roctx_push(const char* name) { roctxRangePushA(name); }
+void roctx_pop() { roctxRangePop(); }
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+DeviceInfo device_info(int device) {
+  hipDeviceProp_t p;
+  PSOUP_HIP_CHECK(hipGetDeviceProperties(&p, device));
+  DeviceInfo d;
+  d.id = device;
+  d.name = p.name;
+  d.arch = p.gcnArchName;
+  d.major = p.major;
+  d.minor = p.minor;
+  d.multiprocessors = p.multiProcessorCount;
+  d.total_mem = p.totalGlobalMem;
+  return d;
+}
+
+int runtime_version() {
+  int v = 0;
+  (void)hipRuntimeGetVersion(&v);
+  return v;
+}
+
+int driver_version() {
+  int v = 0;
+  (void)hipDriverGetVersion(&v);
+  return v;
+}
+
+}  // namespace psoup

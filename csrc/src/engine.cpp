@@ -1,0 +1,586 @@
+#include "psoup/engine.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <fstream>
+#include <numeric>
+
+namespace psoup {
+
+static constexpr double kC = 299792458.0;
+
+DedispKernel parse_dedisp_kernel(const std::string& s) {
+  if (s == "auto") return DedispKernel::Auto;
+  if (s == "direct") return DedispKernel::Direct;
+  if (s == "mfma") return DedispKernel::Mfma;
+  PSOUP_THROW("unknown dedispersion kernel '" << s << "' (auto|direct|mfma)");
+}
+
+// ------------------------------------------------------------ geometry ------
+DedispGeometry DedispGeometry::make(const SigprocHeader& hdr, uint64_t nsamps, const std::vector<float>& dm_list,
+                                    const std::vector<int>& killmask) {
+  DedispGeometry g;
+  g.nchans = hdr.nchans;
+  g.nbits = hdr.nbits;
+  g.tsamp = hdr.tsamp;
+  g.fch1 = hdr.fch1;
+  g.foff = hdr.foff;
+  g.nsamps = nsamps;
+  g.dm_list = dm_list;
+  g.delays = generate_delay_table(g.nchans, g.tsamp, g.fch1, g.foff);
+  g.killmask = killmask.empty() ? std::vector<int>(static_cast<size_t>(g.nchans), 1) : killmask;
+  PSOUP_CHECK(static_cast<int>(g.killmask.size()) == g.nchans, "killmask size != nchans");
+  g.max_delay = compute_max_delay(g.dm_list, g.delays);
+  PSOUP_CHECK(static_cast<uint64_t>(g.max_delay) < nsamps,
+              "max dispersion delay (" << g.max_delay << " samples) exceeds the observation (" << nsamps << ")");
+  g.out_nsamps = nsamps - static_cast<uint64_t>(g.max_delay);
+  const double in_range = static_cast<double>((1 << g.nbits) - 1);
+  g.out_scale = static_cast<float>(192.0 / (in_range * g.nchans));
+  g.bias = (g.nbits == 8) ? 128 : 0;
+  g.nactive = 0;
+  for (int k : g.killmask) g.nactive += (k != 0);
+  return g;
+}
+
+std::vector<int32_t> DedispGeometry::offsets(int d0, int d1) const {
+  std::vector<int32_t> o(static_cast<size_t>(d1 - d0) * nchans);
+  for (int d = d0; d < d1; ++d)
+    for (int c = 0; c < nchans; ++c)
+      o[static_cast<size_t>(d - d0) * nchans + c] = dm_delay_samples(dm_list[d], delays[c]);
+  return o;
+}
+
+// -------------------------------------------------------- device filterbank -
+DeviceFilterbank::DeviceFilterbank(const DedispGeometry& g, hipStream_t stream) : g_(g), stream_(stream) {
+  // rows padded so the MFMA kernel's over-reads (<= 560 B past the last
+  // output sample + its offset) stay inside the row; one spare row at the end
+  stride_ = (g_.nsamps + 1024 + 255) / 256 * 256;
+  chan_.resize(stride_ * static_cast<uint64_t>(g_.nchans + 1));
+  chan_.zero_async(stream_);
+}
+
+void DeviceFilterbank::load_packed_device(const uint8_t* d_packed) {
+  kern::unpack_transpose(d_packed, g_.nsamps, g_.nchans, g_.nbits, chan_.data(), stride_, g_.bias, stream_);
+}
+
+void DeviceFilterbank::load_packed_host(const uint8_t* h_packed) {
+  const uint64_t bytes = g_.nsamps * static_cast<uint64_t>(g_.nchans) * g_.nbits / 8;
+  // Chunked: H2D through two pinned staging buffers, unpack each chunk.
+  const uint64_t bps = static_cast<uint64_t>(g_.nchans) * g_.nbits / 8;
+  uint64_t chunk_samps = std::max<uint64_t>(256, ((64ull << 20) / bps) / 256 * 256);
+  PinnedBuffer<uint8_t> stage[2];
+  DeviceBuffer<uint8_t> dstage[2];
+  Event ev[2];
+  for (int i = 0; i < 2; ++i) {
+    stage[i].resize(chunk_samps * bps);
+    dstage[i].resize(chunk_samps * bps);
+  }
+  int slot = 0;
+  bool used[2] = {false, false};
+  for (uint64_t t0 = 0; t0 < g_.nsamps; t0 += chunk_samps) {
+    const uint64_t ns = std::min(chunk_samps, g_.nsamps - t0);
+    if (used[slot]) ev[slot].sync();
+    std::memcpy(stage[slot].data(), h_packed + t0 * bps, ns * bps);
+    PSOUP_HIP_CHECK(hipMemcpyAsync(dstage[slot].data(), stage[slot].data(), ns * bps, hipMemcpyHostToDevice, stream_));
+    kern::unpack_transpose(dstage[slot].data(), ns, g_.nchans, g_.nbits, chan_.data() + t0, stride_, g_.bias, stream_);
+    ev[slot].record(stream_);
+    used[slot] = true;
+    slot ^= 1;
+  }
+  (void)bytes;
+  PSOUP_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+Dedisperser::Dedisperser(const DeviceFilterbank& fb, hipStream_t stream) : fb_(fb), stream_(stream) {
+  const auto& g = fb_.geometry();
+  std::vector<int32_t> kill(g.killmask.begin(), g.killmask.end());
+  std::vector<int32_t> active;
+  for (int c = 0; c < g.nchans; ++c)
+    if (g.killmask[c]) active.push_back(c);
+  d_kill_.resize(kill.size());
+  PSOUP_HIP_CHECK(hipMemcpy(d_kill_.data(), kill.data(), kill.size() * 4, hipMemcpyHostToDevice));
+  d_active_.resize(std::max<size_t>(1, active.size()));
+  if (!active.empty())
+    PSOUP_HIP_CHECK(hipMemcpy(d_active_.data(), active.data(), active.size() * 4, hipMemcpyHostToDevice));
+}
+
+void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispKernel kind) {
+  const auto& g = fb_.geometry();
+  PSOUP_CHECK(d0 >= 0 && d1 <= static_cast<int>(g.dm_list.size()) && d0 <= d1, "bad DM range");
+  if (d0 == d1) return;
+  RoctxRange r("Dedisperse");
+  if (kind == DedispKernel::Auto) kind = DedispKernel::Mfma;
+  const int ndm = d1 - d0;
+  if (kind == DedispKernel::Mfma) {
+    std::vector<int32_t> offs = g.offsets(d0, d1);
+    std::vector<int32_t> kill(g.killmask.begin(), g.killmask.end());
+    kern::MfmaDedispPlan plan;
+    kern::build_mfma_dedisp_plan(offs.data(), ndm, g.nchans, kill.data(), plan);
+    d_steps_.resize(plan.steps.size());
+    d_deltas_.resize(plan.deltas.size());
+    d_nsteps_.resize(plan.nsteps.size());
+    PSOUP_HIP_CHECK(hipMemcpyAsync(d_steps_.data(), plan.steps.data(), plan.steps.size() * 4, hipMemcpyHostToDevice,
+                                   stream_));
+    PSOUP_HIP_CHECK(hipMemcpyAsync(d_deltas_.data(), plan.deltas.data(), plan.deltas.size(), hipMemcpyHostToDevice,
+                                   stream_));
+    PSOUP_HIP_CHECK(hipMemcpyAsync(d_nsteps_.data(), plan.nsteps.data(), plan.nsteps.size() * 4,
+                                   hipMemcpyHostToDevice, stream_));
+    PSOUP_HIP_CHECK(hipStreamSynchronize(stream_));  // host tables may go out of scope
+    kern::dedisperse_mfma(fb_.data(), fb_.stride(), d_steps_.data(), d_deltas_.data(), d_nsteps_.data(), plan.ntiles,
+                          plan.max_steps, ndm, g.out_nsamps, out, out_stride, g.out_scale, g.bias * g.nactive,
+                          stream_);
+  } else {
+    std::vector<int32_t> offs = g.offsets(d0, d1);
+    d_offsets_.resize(offs.size());
+    PSOUP_HIP_CHECK(hipMemcpyAsync(d_offsets_.data(), offs.data(), offs.size() * 4, hipMemcpyHostToDevice, stream_));
+    PSOUP_HIP_CHECK(hipStreamSynchronize(stream_));
+    kern::dedisperse_direct(fb_.data(), fb_.stride(), g.nchans, d_offsets_.data(), d_kill_.data(), ndm, g.out_nsamps,
+                            out, out_stride, g.out_scale, g.bias, g.nactive, stream_);
+  }
+}
+
+// ---------------------------------------------------------------- whitener --
+Whitener::Whitener(uint64_t n, float tsamp, hipStream_t stream) : n_(n), tsamp_(tsamp), stream_(stream) {
+  PSOUP_CHECK(n >= 250, "series too short for the running median (need >= 250 samples)");
+  float tobs = static_cast<float>(static_cast<float>(n) * tsamp);
+  bin_width_ = static_cast<float>(1.0 / tobs);
+  const uint64_t nb = nbins();
+  r2c_ = std::make_unique<FftPlan>(FftType::R2C, n, 1);
+  c2r_ = std::make_unique<FftPlan>(FftType::C2R, n, 1);
+  fser_.resize(nb);
+  m5_.resize(nb / 5);
+  m25_.resize(std::max<uint64_t>(1, nb / 5 / 5));
+  m125_.resize(std::max<uint64_t>(1, nb / 5 / 5 / 5));
+  partials_.resize(2 * 1024);
+  stats_.resize(4);
+  sum_.resize(1);
+}
+
+void Whitener::load_trial(const uint8_t* d_trial, uint64_t nsamps, float* d_series) {
+  const uint64_t nvalid = std::min(nsamps, n_);
+  kern::u8_sum(d_trial, nvalid, sum_.data(), stream_);
+  kern::u8_to_f32_pad(d_trial, nvalid, d_series, n_, sum_.data(), stream_);
+}
+
+void Whitener::whiten(float* d_series, const uint32_t* d_zapmask, bool with_stats, float boundary5, float boundary25) {
+  const uint64_t nb = nbins();
+  r2c_->execute(d_series, fser_.data(), stream_);
+  const uint64_t n5 = nb / 5, n25 = n5 / 5, n125 = n25 / 5;
+  kern::median5_amp(fser_.data(), nb, m5_.data(), stream_);
+  kern::median5(m5_.data(), n5, m25_.data(), stream_);
+  kern::median5(m25_.data(), n25, m125_.data(), stream_);
+  const int64_t pos5 = static_cast<int64_t>(static_cast<int>(boundary5 / bin_width_));
+  const int64_t pos25 = static_cast<int64_t>(static_cast<int>(boundary25 / bin_width_));
+  kern::deredden_zap(fser_.data(), nb, m5_.data(), n5, m25_.data(), std::max<uint64_t>(1, n25), m125_.data(),
+                     std::max<uint64_t>(1, n125), pos5, pos25, d_zapmask, stream_);
+  if (with_stats) kern::interbin_stats(fser_.data(), nb, nullptr, partials_.data(), 1024, stats_.data(), stream_);
+  c2r_->execute(fser_.data(), d_series, stream_);
+}
+
+std::vector<uint32_t> build_zap_mask(const std::vector<float>& freqs, const std::vector<float>& widths,
+                                     float bin_width, uint64_t nbins) {
+  std::vector<uint32_t> mask((nbins + 31) / 32, 0u);
+  for (size_t i = 0; i < freqs.size() && i < widths.size(); ++i) {
+    const float f = freqs[i], w = widths[i];
+    long low = static_cast<long>(std::floor((f - w) / bin_width));
+    long high = static_cast<long>(std::ceil((f + w) / bin_width));
+    if (low < 0) low = 0;
+    if (low >= static_cast<long>(nbins)) continue;
+    if (high >= static_cast<long>(nbins)) high = static_cast<long>(nbins) - 1;
+    for (long k = low; k < high; ++k) mask[static_cast<size_t>(k) >> 5] |= 1u << (k & 31);
+  }
+  return mask;
+}
+
+// ----------------------------------------------------------- search engine --
+SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
+    : p_(p),
+      stream_(stream),
+      harm_(p.freq_tol, static_cast<float>(p.max_harm), false, true),
+      accd_(static_cast<float>(static_cast<float>(p.fft_size) * p.tsamp), p.freq_tol, true) {
+  PSOUP_CHECK(p_.fft_size >= 250, "fft_size too small");
+  n_ = p_.fft_size;
+  nb_ = n_ / 2 + 1;
+  tobs_ = static_cast<float>(static_cast<float>(n_) * p_.tsamp);
+  bin_width_ = static_cast<float>(1.0 / tobs_);
+  nlev_ = std::min(std::max(p_.nharmonics, 0), kern::kMaxHarmLevels);
+  if (p_.nharmonics > kern::kMaxHarmLevels)
+    log_info("warning: nharmonics > 5 is capped at 5 (32 harmonics), as the reference kernel only writes 5 levels");
+  wh_ = std::make_unique<Whitener>(n_, p_.tsamp, stream_);
+  tim_.resize(n_);
+  if (!p_.zap_freqs.empty()) {
+    auto mask = build_zap_mask(p_.zap_freqs, p_.zap_widths, bin_width_, nb_);
+    zapmask_.resize(mask.size());
+    PSOUP_HIP_CHECK(hipMemcpy(zapmask_.data(), mask.data(), mask.size() * 4, hipMemcpyHostToDevice));
+    zap_ = true;
+  }
+  bounds_.clear();
+  hp_.nlevels = nlev_;
+  hp_.thresh = p_.min_snr;
+  hi_ = 0;
+  for (int h = 0; h <= 5; ++h) {
+    if (h <= nlev_) {
+      PeakBounds b = peak_bounds(static_cast<int>(nb_), bin_width_, h, p_.min_freq, p_.max_freq);
+      bounds_.push_back(b);
+      hp_.start[h] = b.start_idx;
+      hp_.end[h] = std::max(b.start_idx, b.end_idx);
+      hi_ = std::max(hi_, hp_.end[h]);
+    } else {
+      hp_.start[h] = hp_.end[h] = 0;
+    }
+  }
+  // batch size
+  if (p_.accel_batch > 0) {
+    K_ = p_.accel_batch;
+  } else {
+    const size_t per = n_ * 4 + nb_ * 8 + static_cast<size_t>(hi_) * 4;
+    K_ = static_cast<int>(std::max<size_t>(1, p_.batch_bytes / per));
+    K_ = std::min(K_, 256);
+    if (K_ >= 16) K_ = K_ / 8 * 8;
+  }
+  cap_ = static_cast<uint32_t>(std::max<uint64_t>(1u << 16, static_cast<uint64_t>(K_) * 4096));
+  for (auto& s : slots_) {
+    s.done = std::make_unique<Event>();
+    s.copied = std::make_unique<Event>();
+    s.d_count.resize(1);
+    s.h_count.resize(1);
+  }
+  grow_capacity(cap_);
+}
+
+SearchEngine::~SearchEngine() {
+  (void)hipStreamSynchronize(stream_);
+  (void)hipStreamSynchronize(copy_stream_.get());
+}
+
+void SearchEngine::grow_capacity(uint32_t need) {
+  cap_ = std::max(cap_, need);
+  for (auto& s : slots_) {
+    s.d_peaks.resize(cap_);
+    s.h_peaks.resize(cap_);
+  }
+  hp_.capacity = cap_;
+}
+
+void SearchEngine::ensure_batch_buffers() {
+  if (res_.size() >= static_cast<uint64_t>(K_) * n_) return;
+  res_.resize(static_cast<uint64_t>(K_) * n_);
+  spec_.resize(static_cast<uint64_t>(K_) * nb_);
+  P_.resize(static_cast<uint64_t>(K_) * std::max<uint64_t>(1, static_cast<uint64_t>(hi_)));
+}
+
+FftPlan& SearchEngine::batch_plan(int count) {
+  auto it = plans_.find(count);
+  if (it != plans_.end()) return *it->second;
+  auto plan = std::make_unique<FftPlan>(FftType::R2C, n_, static_cast<uint64_t>(count), n_, nb_);
+  FftPlan& ref = *plan;
+  plans_[count] = std::move(plan);
+  return ref;
+}
+
+void SearchEngine::launch_batch(Slot& s, int first, int count) {
+  s.first = first;
+  s.count = count;
+  kern::resample_batch(tim_.data(), n_, res_.data(), n_, af_.data() + first, count, stream_);
+  batch_plan(count).execute(res_.data(), spec_.data(), stream_);
+  const uint64_t pst = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
+  kern::interbin_normalise_batch(spec_.data(), nb_, nb_, P_.data(), pst, count, static_cast<uint64_t>(hi_),
+                                 wh_->stats(), static_cast<float>(n_), stream_);
+  PSOUP_HIP_CHECK(hipMemsetAsync(s.d_count.data(), 0, sizeof(uint32_t), stream_));
+  {
+    RoctxRange r("Harmonic summing");
+    kern::harmonic_peaks_batch(P_.data(), nb_, pst, count, hp_, s.d_peaks.data(), s.d_count.data(), stream_);
+  }
+  PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_count.data(), s.d_count.data(), sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  s.done->record(stream_);
+}
+
+void SearchEngine::process_slot(Slot& s, float dm, int dm_idx, const std::vector<float>& accs, CandidateList& out) {
+  const uint32_t cnt = std::min(s.h_count[0], cap_);
+  ctr_.peaks += cnt;
+  const int L = nlev_ + 1;
+  const int nseg = s.count * 8;
+  seg_count_.assign(static_cast<size_t>(nseg) + 1, 0);
+  for (uint32_t i = 0; i < cnt; ++i) seg_count_[s.h_peaks[i].seg]++;
+  seg_off_.assign(static_cast<size_t>(nseg) + 1, 0);
+  for (int i = 0; i < nseg; ++i) seg_off_[i + 1] = seg_off_[i] + seg_count_[i];
+  sorted_.resize(cnt);
+  {
+    std::vector<uint32_t> fill(seg_off_.begin(), seg_off_.end() - 1);
+    for (uint32_t i = 0; i < cnt; ++i) sorted_[fill[s.h_peaks[i].seg]++] = s.h_peaks[i];
+  }
+  std::vector<int> idxs, pidx;
+  std::vector<float> snrs, psnr;
+  for (int k = 0; k < s.count; ++k) {
+    const float acc = accs[static_cast<size_t>(s.first + k)];
+    CandidateList trial;
+    for (int h = 0; h < L; ++h) {
+      const int seg = k * 8 + h;
+      const uint32_t a = seg_off_[seg], b = seg_off_[seg + 1];
+      if (a == b) continue;
+      std::sort(sorted_.begin() + a, sorted_.begin() + b,
+                [](const kern::PeakRecord& x, const kern::PeakRecord& y) { return x.idx < y.idx; });
+      idxs.resize(b - a);
+      snrs.resize(b - a);
+      for (uint32_t i = a; i < b; ++i) {
+        idxs[i - a] = sorted_[i].idx;
+        snrs[i - a] = sorted_[i].snr;
+      }
+      pidx.clear();
+      psnr.clear();
+      identify_unique_peaks(idxs.data(), snrs.data(), idxs.size(), p_.min_gap, pidx, psnr);
+      const double factor = bounds_[static_cast<size_t>(h)].factor;
+      for (size_t i = 0; i < pidx.size(); ++i)
+        trial.emplace_back(dm, dm_idx, acc, h, psnr[i], static_cast<float>(pidx[i] * factor));
+    }
+    if (!trial.empty()) {
+      CandidateList d = harm_.distill(std::move(trial));
+      for (auto& c : d) out.push_back(std::move(c));
+    }
+  }
+}
+
+CandidateList SearchEngine::search_trial(const uint8_t* d_trial, uint64_t nsamps, float dm, int dm_idx,
+                                         const std::vector<float>& accs) {
+  RoctxRange dm_range("DM-Loop");
+  Stopwatch sw;
+  sw.start();
+  wh_->load_trial(d_trial, nsamps, tim_.data());
+  wh_->whiten(tim_.data(), zap_ ? zapmask_.data() : nullptr, true, p_.boundary_5_freq, p_.boundary_25_freq);
+  ctr_.dm_trials++;
+  const int nacc = static_cast<int>(accs.size());
+  CandidateList accel_trial_cands;
+  if (nacc == 0) return accel_trial_cands;
+  // acceleration factors (double, as device_resampleII)
+  {
+    // previous DM's batches have all retired (their events were waited on), so
+    // the host staging vector and af_ may be rewritten here
+    af_host_.resize(static_cast<size_t>(nacc));
+    for (int i = 0; i < nacc; ++i) af_host_[i] = (static_cast<double>(accs[i]) * p_.tsamp) / (2 * kC);
+    af_.resize(af_host_.size());
+    PSOUP_HIP_CHECK(hipMemcpyAsync(af_.data(), af_host_.data(), af_host_.size() * sizeof(double),
+                                   hipMemcpyHostToDevice, stream_));
+  }
+  ensure_batch_buffers();
+  RoctxRange acc_range("Acceleration-Loop");
+  std::deque<int> inflight;  // slot indices
+  int next = 0, slot = 0;
+  auto issue = [&](int sl) {
+    const int c = std::min(K_, nacc - next);
+    launch_batch(slots_[sl], next, c);
+    inflight.push_back(sl);
+    next += c;
+  };
+  while (inflight.size() < 2 && next < nacc) {
+    issue(slot);
+    slot ^= 1;
+  }
+  Stopwatch host;
+  while (!inflight.empty()) {
+    const int sl = inflight.front();
+    Slot& s = slots_[sl];
+    s.done->sync();
+    uint32_t cnt = s.h_count[0];
+    if (cnt > cap_) {
+      // Peak buffer overflow: drain, grow, recompute every in-flight batch.
+      ctr_.overflows++;
+      PSOUP_HIP_CHECK(hipStreamSynchronize(stream_));
+      uint32_t need = cnt;
+      for (int q : inflight) need = std::max(need, slots_[q].h_count[0]);
+      grow_capacity(need + need / 2 + 1024);
+      for (int q : inflight) launch_batch(slots_[q], slots_[q].first, slots_[q].count);
+      continue;
+    }
+    inflight.pop_front();
+    if (cnt > 0)
+      PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_peaks.data(), s.d_peaks.data(), cnt * sizeof(kern::PeakRecord),
+                                     hipMemcpyDeviceToHost, copy_stream_.get()));
+    s.copied->record(copy_stream_.get());
+    // the next batch that reuses this slot must wait for the copy-out
+    PSOUP_HIP_CHECK(hipStreamWaitEvent(stream_, s.copied->get(), 0));
+    if (next < nacc) issue(sl);
+    s.copied->sync();
+    host.start();
+    process_slot(s, dm, dm_idx, accs, accel_trial_cands);
+    host.stop();
+    ctr_.accel_trials += static_cast<uint64_t>(s.count);
+  }
+  ctr_.host_s += host.get_time();
+  CandidateList dm_cands = accd_.distill(std::move(accel_trial_cands));
+  sw.stop();
+  ctr_.accel_s += sw.get_time();
+  return dm_cands;
+}
+
+// ---------------------------------------------------------------- folding ---
+void fold_calculate_sn(const float* prof, int bin, int width, int nbins, float* sn1, float* sn2) {
+  const int edge = static_cast<int>(width * 0.3 + 0.5);
+  const int width_by_2 = static_cast<int>(width / 2.0 + 0.5);
+  std::vector<float> on_pulse, off_pulse, rprof;
+  for (int ii = 0; ii < nbins; ++ii) {
+    int jj = ((bin - nbins / 2 + ii) % nbins + nbins) % nbins;
+    rprof.push_back(prof[jj]);
+  }
+  bin = nbins / 2 - 1;
+  const int upper_edge = bin + (width_by_2 + edge);
+  const int lower_edge = bin - (width_by_2 + edge);
+  for (int ii = 0; ii < nbins; ++ii) {
+    if (ii <= upper_edge && ii >= lower_edge) on_pulse.push_back(rprof[ii]);
+    else off_pulse.push_back(rprof[ii]);
+  }
+  auto mean_of = [](const std::vector<float>& v) -> float {
+    if (v.empty()) return std::nanf("");
+    double a = 0.0;  // std::accumulate(..., 0.0) accumulates in double
+    for (float x : v) a += x;
+    return static_cast<float>(a / v.size());
+  };
+  const float on_mean = mean_of(on_pulse);
+  const float off_mean = mean_of(off_pulse);
+  float acc = 0;
+  for (float x : off_pulse) acc = static_cast<float>(acc + std::pow(x - off_mean, 2.0));
+  const float off_std = std::sqrt(acc / off_pulse.size());
+  *sn1 = static_cast<float>((on_mean - off_mean) * std::sqrt(static_cast<double>(width)) / off_std);
+  double tot = 0.0;
+  for (int ii = 0; ii < nbins; ++ii) {
+    float v = rprof[ii] - off_mean;
+    v = v / off_std;
+    tot += v;
+  }
+  *sn2 = static_cast<float>(tot / std::sqrt(static_cast<double>(width)));
+  if (*sn1 > 99999) *sn1 = 0.0f;
+  if (*sn2 > 99999) *sn2 = 0.0f;
+}
+
+FoldEngine::FoldEngine(uint64_t nsamps, float tsamp, hipStream_t stream) : n_(nsamps), tsamp_(tsamp), stream_(stream) {
+  PSOUP_CHECK(n_ >= 1024, "fold series too short");
+  wh_ = std::make_unique<Whitener>(n_, tsamp_, stream_);
+  tim_.resize(n_);
+  shift_table_.resize(static_cast<uint64_t>(kNbins) * kNbins * kNints);
+  kern::fold_shift_table(shift_table_.data(), kNbins, kNints, stream_);
+  chunk_ = static_cast<int>(std::min<uint64_t>(4096, n_ / kNints));
+}
+
+std::vector<FoldResult> FoldEngine::fold_trial(const uint8_t* d_trial, uint64_t trial_nsamps,
+                                               const std::vector<double>& periods, const std::vector<float>& accs) {
+  wh_->load_trial(d_trial, trial_nsamps, tim_.data());
+  wh_->whiten(tim_.data(), nullptr, false, 0.05f, 0.5f);
+  return fold_series(tim_.data(), periods, accs);
+}
+
+std::vector<FoldResult> FoldEngine::fold_series(const float* d_series, const std::vector<double>& periods,
+                                                const std::vector<float>& accs) {
+  const int nj = static_cast<int>(periods.size());
+  std::vector<FoldResult> res(static_cast<size_t>(nj));
+  if (nj == 0) return res;
+  std::vector<kern::FoldJob> jobs(static_cast<size_t>(nj));
+  for (int i = 0; i < nj; ++i) {
+    jobs[i].tsamp_by_period = static_cast<double>(tsamp_) / periods[i];
+    jobs[i].af = (static_cast<double>(accs[i]) * tsamp_) / (2 * kC);
+  }
+  const uint64_t nps = n_ / kNints;
+  const int nchunk = static_cast<int>((nps + chunk_ - 1) / chunk_);
+  jobs_.resize(jobs.size());
+  PSOUP_HIP_CHECK(hipMemcpyAsync(jobs_.data(), jobs.data(), jobs.size() * sizeof(kern::FoldJob), hipMemcpyHostToDevice,
+                                 stream_));
+  const size_t nfold = static_cast<size_t>(nj) * kNints * kNbins;
+  psum_.resize(nfold * nchunk);
+  pcount_.resize(nfold * nchunk);
+  folds_.resize(nfold);
+  opt_fold_.resize(nfold);
+  opt_prof_.resize(static_cast<size_t>(nj) * kNbins);
+  opt_int_.resize(static_cast<size_t>(nj) * 3);
+  opt_val_.resize(static_cast<size_t>(nj));
+  kern::fold_accumulate(d_series, n_, jobs_.data(), nj, kNbins, kNints, chunk_, psum_.data(), pcount_.data(), stream_);
+  kern::fold_reduce(psum_.data(), pcount_.data(), nj, kNbins, kNints, nchunk, folds_.data(), stream_);
+  kern::fold_optimise(folds_.data(), nj, shift_table_.data(), opt_fold_.data(), opt_prof_.data(), opt_int_.data(),
+                      opt_val_.data(), stream_);
+  std::vector<float> h_fold(nfold), h_prof(static_cast<size_t>(nj) * kNbins);
+  std::vector<int32_t> h_int(static_cast<size_t>(nj) * 3);
+  PSOUP_HIP_CHECK(hipMemcpyAsync(h_fold.data(), opt_fold_.data(), nfold * 4, hipMemcpyDeviceToHost, stream_));
+  PSOUP_HIP_CHECK(hipMemcpyAsync(h_prof.data(), opt_prof_.data(), h_prof.size() * 4, hipMemcpyDeviceToHost, stream_));
+  PSOUP_HIP_CHECK(hipMemcpyAsync(h_int.data(), opt_int_.data(), h_int.size() * 4, hipMemcpyDeviceToHost, stream_));
+  PSOUP_HIP_CHECK(hipStreamSynchronize(stream_));
+  const float tobs = static_cast<float>(static_cast<double>(n_) * tsamp_);
+  for (int i = 0; i < nj; ++i) {
+    FoldResult& r = res[i];
+    const int opt_template = h_int[3 * i + 0];
+    const int opt_shift = h_int[3 * i + 1];
+    const int opt_bin = h_int[3 * i + 2] - opt_template / 2;
+    float sn1 = 0, sn2 = 0;
+    fold_calculate_sn(h_prof.data() + static_cast<size_t>(i) * kNbins, opt_bin, opt_template, kNbins, &sn1, &sn2);
+    r.folded_snr = std::max(sn1, sn2);
+    const double p = periods[i];
+    // FoldedSubints::get_opt_period returns float (folded.hpp)
+    r.opt_period = static_cast<float>(p * ((((32.0 - opt_shift) * p) / (kNbins * tobs)) + 1));
+    r.opt_width = opt_template + 1;
+    r.opt_bin = opt_bin;
+    r.fold.assign(h_fold.begin() + static_cast<long>(i) * kNints * kNbins,
+                  h_fold.begin() + static_cast<long>(i + 1) * kNints * kNbins);
+    r.prof.assign(h_prof.begin() + static_cast<long>(i) * kNbins, h_prof.begin() + static_cast<long>(i + 1) * kNbins);
+  }
+  return res;
+}
+
+// ------------------------------------------------------------ coincidencer --
+void coincidencer_beam(const uint8_t* d_trial, uint64_t n, float tsamp, BeamProducts& out, hipStream_t stream) {
+  Whitener wh(n, tsamp, stream);
+  out.series.resize(n);
+  out.spectrum.resize(wh.nbins());
+  wh.load_trial(d_trial, n, out.series.data());
+  // whiten without the C2R so the dereddened spectrum can be formed first
+  const uint64_t nb = wh.nbins();
+  wh.r2c().execute(out.series.data(), wh.spectrum(), stream);
+  DeviceBuffer<float> m5(nb / 5), m25(std::max<uint64_t>(1, nb / 25)), m125(std::max<uint64_t>(1, nb / 125));
+  const uint64_t n5 = nb / 5, n25 = n5 / 5, n125 = n25 / 5;
+  kern::median5_amp(wh.spectrum(), nb, m5.data(), stream);
+  kern::median5(m5.data(), n5, m25.data(), stream);
+  kern::median5(m25.data(), n25, m125.data(), stream);
+  const float bw = wh.bin_width();
+  kern::deredden_zap(wh.spectrum(), nb, m5.data(), n5, m25.data(), std::max<uint64_t>(1, n25), m125.data(),
+                     std::max<uint64_t>(1, n125), static_cast<int>(0.05f / bw), static_cast<int>(0.5f / bw), nullptr,
+                     stream);
+  DeviceBuffer<double> partials(2 * 1024);
+  DeviceBuffer<float> st(4);
+  kern::interbin_stats(wh.spectrum(), nb, out.spectrum.data(), partials.data(), 1024, st.data(), stream);
+  kern::normalise_dev(out.spectrum.data(), nb, st.data(), 1.0f, stream);
+  wh.c2r().execute(wh.spectrum(), out.series.data(), stream);
+  kern::f32_stats(out.series.data(), n, partials.data(), 1024, st.data(), stream);
+  kern::normalise_dev(out.series.data(), n, st.data(), 1.0f, stream);
+  PSOUP_HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+void write_samp_mask(const std::vector<float>& mask, const std::string& filename) {
+  FILE* fo = std::fopen(filename.c_str(), "w");
+  if (!fo) PSOUP_THROW("cannot write " << filename);
+  std::fprintf(fo, "#0 1\n");
+  for (float v : mask) std::fprintf(fo, "%d\n", static_cast<int>(v));
+  std::fclose(fo);
+}
+
+void write_birdie_list(const std::vector<float>& mask, float bin_width, const std::string& filename) {
+  std::vector<std::pair<float, float>> birdies;
+  const long size = static_cast<long>(mask.size());
+  long ii = 0;
+  while (ii < size) {
+    if (mask[ii] == 0) {
+      int count = 0;
+      while (ii < size && mask[ii] == 0) {
+        count++;
+        ii++;
+      }
+      birdies.emplace_back(static_cast<float>(((ii - 1) - (count / 2.0)) * bin_width),
+                           static_cast<float>(count * bin_width));
+    } else {
+      ii++;
+    }
+  }
+  FILE* fo = std::fopen(filename.c_str(), "w");
+  if (!fo) PSOUP_THROW("cannot write " << filename);
+  for (const auto& b : birdies) std::fprintf(fo, "%.9f\t%.6f\n", b.first, b.second);
+  std::fclose(fo);
+}
+
+}  // namespace psoup

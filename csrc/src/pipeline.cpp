@@ -1,0 +1,368 @@
+#include "psoup/pipeline.hpp"
+
+#include <sys/stat.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <fstream>
+#include <iostream>
+#include <mutex>
+#include <sstream>
+#include <thread>
+
+#include "psoup/output.hpp"
+
+namespace psoup {
+
+SearchSetup make_search_setup(const CmdLineOptions& args, const SigprocHeader& hdr) {
+  SearchSetup s;
+  s.header = hdr;
+  s.nsamps = static_cast<uint64_t>(hdr.nsamples);
+  s.dm_list = generate_dm_list(args.dm_start, args.dm_end, hdr.tsamp, args.dm_pulse_width, hdr.fch1, hdr.foff,
+                               hdr.nchans, args.dm_tol);
+  s.killmask = std::vector<int>(static_cast<size_t>(hdr.nchans), 1);
+  if (!args.killfilename.empty()) s.killmask = read_killfile(args.killfilename, hdr.nchans);
+  s.fft_size = args.size == 0 ? prev_power_of_two(s.nsamps) : args.size;
+  // cfreq as Filterbank::get_cfreq (float arithmetic)
+  {
+    float fch1 = static_cast<float>(hdr.fch1), foff = static_cast<float>(hdr.foff);
+    float nch = static_cast<float>(static_cast<unsigned>(hdr.nchans));
+    s.cfreq = foff < 0 ? fch1 + foff * nch / 2 : fch1 - foff * nch / 2;
+  }
+  s.accel_plan = AccelPlan(args.acc_start, args.acc_end, args.acc_tol, args.acc_pulse_width, s.fft_size,
+                           static_cast<float>(hdr.tsamp), s.cfreq, static_cast<float>(hdr.foff),
+                           parse_accel_convention(args.accel_convention));
+  SearchParams& p = s.search;
+  p.fft_size = s.fft_size;
+  p.tsamp = static_cast<float>(hdr.tsamp);
+  p.min_snr = args.min_snr;
+  p.min_freq = args.min_freq;
+  p.max_freq = args.max_freq;
+  p.nharmonics = args.nharmonics;
+  p.freq_tol = args.freq_tol;
+  p.max_harm = args.max_harm;
+  // The reference never passes --boundary_* to the dereddener (pipeline_multi.cu:182).
+  p.boundary_5_freq = args.use_boundaries ? args.boundary_5_freq : 0.05f;
+  p.boundary_25_freq = args.use_boundaries ? args.boundary_25_freq : 0.5f;
+  if (!args.zapfilename.empty()) read_zapfile(args.zapfilename, p.zap_freqs, p.zap_widths);
+  p.accel_batch = args.accel_batch;
+  s.dedisp_kernel = parse_dedisp_kernel(args.dedisp_kernel);
+  return s;
+}
+
+CandidateList global_distill_and_score(CandidateList cands, const CmdLineOptions& args, const SearchSetup& s) {
+  DMDistiller dm_still(args.freq_tol, true);
+  HarmonicDistiller harm_still(args.freq_tol, static_cast<float>(args.max_harm), true, false);
+  cands = dm_still.distill(std::move(cands));
+  cands = harm_still.distill(std::move(cands));
+  CandidateScorer scorer(static_cast<float>(s.header.tsamp), s.cfreq, static_cast<float>(s.header.foff),
+                         static_cast<float>(std::fabs(s.header.foff) * s.header.nchans));
+  scorer.score_all(cands);
+  return cands;
+}
+
+std::map<int, std::vector<int>> select_fold_candidates(const CandidateList& cands, int n) {
+  std::map<int, std::vector<int>> m;
+  const int count = std::min(n, static_cast<int>(cands.size()));
+  for (int i = 0; i < count; ++i) {
+    const float p = static_cast<float>(1.0 / cands[i].freq);
+    if (p > 0.001f && p < 10.00f) m[cands[i].dm_idx].push_back(i);
+  }
+  return m;
+}
+
+// ---------------------------------------------------------------- progress --
+struct ProgressBar::Impl {
+  std::string title;
+  std::atomic<double> frac{0.0};
+  std::atomic<bool> running{false};
+  std::thread th;
+  Stopwatch sw;
+};
+
+ProgressBar::ProgressBar(std::string title) : impl_(new Impl) { impl_->title = std::move(title); }
+ProgressBar::~ProgressBar() {
+  stop();
+  delete impl_;
+}
+void ProgressBar::start() {
+  if (impl_->running.exchange(true)) return;
+  impl_->sw.start();
+  impl_->th = std::thread([this] {
+    while (impl_->running.load()) {
+      double f = impl_->frac.load();
+      double el = impl_->sw.get_time();
+      double eta = f > 0 ? el / f - el : 0.0;
+      int w = 40, fill = static_cast<int>(f * w);
+      std::fprintf(stderr, "\r%s [%s%s] %5.1f%%  ETA %6.1f s", impl_->title.c_str(), std::string(fill, '=').c_str(),
+                   std::string(w - fill, ' ').c_str(), 100 * f, eta);
+      std::fflush(stderr);
+      std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    }
+  });
+}
+void ProgressBar::set(double f) { impl_->frac.store(f); }
+void ProgressBar::stop() {
+  if (!impl_->running.exchange(false)) return;
+  if (impl_->th.joinable()) impl_->th.join();
+  std::fprintf(stderr, "\r%s complete (%.2f s)%40s\n", impl_->title.c_str(), impl_->sw.get_time(), "");
+}
+
+// ---------------------------------------------------------------- pipeline --
+namespace {
+
+std::string chunk_file(const std::string& dir, int d0, int d1) {
+  std::ostringstream os;
+  os << dir << "/dm_" << d0 << "_" << d1 << ".psoc";
+  return os.str();
+}
+
+bool load_chunk(const std::string& path, CandidateList& out) {
+  std::ifstream in(path, std::ios::binary);
+  if (!in) return false;
+  std::vector<uint8_t> buf((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+  try {
+    CandidateList c = deserialize_candidates(buf.data(), buf.size());
+    for (auto& x : c) out.push_back(std::move(x));
+    return true;
+  } catch (const std::exception&) {
+    return false;
+  }
+}
+
+void save_chunk(const std::string& path, const CandidateList& c) {
+  std::vector<uint8_t> buf = serialize_candidates(c);
+  std::string tmp = path + ".tmp";
+  {
+    std::ofstream out(tmp, std::ios::binary);
+    out.write(reinterpret_cast<const char*>(buf.data()), static_cast<std::streamsize>(buf.size()));
+  }
+  std::rename(tmp.c_str(), path.c_str());
+}
+
+struct Shared {
+  const CmdLineOptions* args;
+  const SearchSetup* setup;
+  const Filterbank* fb;
+  std::atomic<int> next_dm{0};
+  int chunk = 8;
+  int ndm = 0;
+  std::mutex mu;
+  CandidateList cands;
+  std::atomic<uint64_t> accel_trials{0};
+  std::atomic<int> done_dms{0};
+  std::vector<double> dedisp_s, search_s;
+  std::exception_ptr error;
+  ProgressBar* progress = nullptr;
+};
+
+}  // namespace
+
+PipelineResult run_pipeline(const CmdLineOptions& args) {
+  PipelineResult res;
+  Stopwatch t_total, t_read, t_dedisp, t_search, t_fold;
+  t_total.start();
+  if (args.verbose) set_log_level(LogLevel::Verbose);
+
+  t_read.start();
+  Filterbank fb = Filterbank::from_file(args.infilename);
+  t_read.stop();
+
+  SearchSetup setup = make_search_setup(args, fb.header());
+  res.setup = setup;
+  const int ndev_avail = device_count();
+  PSOUP_CHECK(ndev_avail > 0, "no HIP devices visible");
+  const int ngpu = std::max(1, std::min(ndev_avail, args.max_num_threads));
+  for (int i = 0; i < ngpu; ++i) res.devices.push_back(i);
+  log_verbose("Using " + std::to_string(ngpu) + " GPU(s); " + std::to_string(setup.dm_list.size()) + " DM trials; fft " +
+              std::to_string(setup.fft_size));
+
+  DedispGeometry geom = DedispGeometry::make(fb.header(), fb.nsamps(), setup.dm_list, setup.killmask);
+  if (!args.checkpoint_dir.empty()) make_dirs(args.checkpoint_dir);
+
+  Shared sh;
+  sh.args = &args;
+  sh.setup = &setup;
+  sh.fb = &fb;
+  sh.ndm = static_cast<int>(setup.dm_list.size());
+  sh.chunk = std::max(1, std::min(32, sh.ndm / (4 * ngpu) + 1));
+  sh.dedisp_s.assign(static_cast<size_t>(ngpu), 0.0);
+  sh.search_s.assign(static_cast<size_t>(ngpu), 0.0);
+  ProgressBar progress("Searching DM trials");
+  if (args.progress_bar) {
+    sh.progress = &progress;
+    progress.start();
+  }
+
+  // Per-device resident state is kept for the folding stage.
+  struct DevState {
+    std::unique_ptr<Stream> stream;
+    std::unique_ptr<DeviceFilterbank> dfb;
+    std::unique_ptr<Dedisperser> dd;
+  };
+  std::vector<DevState> devs(static_cast<size_t>(ngpu));
+
+  t_search.start();
+  auto worker = [&](int dev) {
+    try {
+      PSOUP_HIP_CHECK(hipSetDevice(dev));
+      DevState& ds = devs[static_cast<size_t>(dev)];
+      ds.stream = std::make_unique<Stream>();
+      hipStream_t st = ds.stream->get();
+      Stopwatch wd, ws;
+      wd.start();
+      ds.dfb = std::make_unique<DeviceFilterbank>(geom, st);
+      ds.dfb->load_packed_host(fb.data());
+      ds.dd = std::make_unique<Dedisperser>(*ds.dfb, st);
+      wd.stop();
+      SearchEngine engine(setup.search, st);
+      const uint64_t rstride = Dedisperser::row_stride(geom.out_nsamps);
+      DeviceBuffer<uint8_t> trials(rstride * static_cast<uint64_t>(sh.chunk));
+      int processed = 0;
+      while (true) {
+        const int d0 = sh.next_dm.fetch_add(sh.chunk);
+        if (d0 >= sh.ndm) break;
+        const int d1 = std::min(sh.ndm, d0 + sh.chunk);
+        CandidateList local;
+        const std::string ck = args.checkpoint_dir.empty() ? "" : chunk_file(args.checkpoint_dir, d0, d1);
+        if (!ck.empty() && load_chunk(ck, local)) {
+          log_verbose("resumed DMs [" + std::to_string(d0) + "," + std::to_string(d1) + ") from checkpoint");
+        } else {
+          wd.start();
+          ds.dd->run(d0, d1, trials.data(), rstride, setup.dedisp_kernel);
+          PSOUP_HIP_CHECK(hipStreamSynchronize(st));
+          wd.stop();
+          ws.start();
+          for (int d = d0; d < d1; ++d) {
+            if (args.fault_after_dms >= 0 && processed >= args.fault_after_dms)
+              PSOUP_THROW("fault injection: device " << dev << " aborting after " << processed << " DM trials");
+            const float dm = setup.dm_list[static_cast<size_t>(d)];
+            std::vector<float> accs = setup.accel_plan.generate(dm);
+            log_verbose("Searching " + std::to_string(accs.size()) + " acceleration trials for DM " +
+                        std::to_string(dm));
+            CandidateList c = engine.search_trial(trials.data() + static_cast<uint64_t>(d - d0) * rstride,
+                                                  geom.out_nsamps, dm, d, accs);
+            sh.accel_trials += accs.size();
+            for (auto& x : c) local.push_back(std::move(x));
+            processed++;
+          }
+          ws.stop();
+          if (!ck.empty()) save_chunk(ck, local);
+        }
+        {
+          std::lock_guard<std::mutex> lk(sh.mu);
+          for (auto& x : local) sh.cands.push_back(std::move(x));
+        }
+        int done = sh.done_dms.fetch_add(d1 - d0) + (d1 - d0);
+        if (sh.progress) sh.progress->set(static_cast<double>(done) / sh.ndm);
+      }
+      sh.dedisp_s[static_cast<size_t>(dev)] = wd.get_time();
+      sh.search_s[static_cast<size_t>(dev)] = ws.get_time();
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(sh.mu);
+      if (!sh.error) sh.error = std::current_exception();
+      sh.next_dm.store(sh.ndm + 1000000);  // drain the queue
+    }
+  };
+  std::vector<std::thread> threads;
+  for (int d = 0; d < ngpu; ++d) threads.emplace_back(worker, d);
+  for (auto& t : threads) t.join();
+  t_search.stop();
+  if (args.progress_bar) progress.stop();
+  if (sh.error) std::rethrow_exception(sh.error);
+
+  // Concatenation order of the reference depends on thread timing; sort by
+  // DM index first so the global distillation is deterministic.
+  std::stable_sort(sh.cands.begin(), sh.cands.end(),
+                   [](const Candidate& a, const Candidate& b) { return a.dm_idx < b.dm_idx; });
+  CandidateList cands = global_distill_and_score(std::move(sh.cands), args, setup);
+
+  // ---- folding (distributed over the devices by DM)
+  t_fold.start();
+  if (args.npdmp > 0 && !cands.empty()) {
+    auto groups = select_fold_candidates(cands, args.npdmp);
+    const uint64_t fold_n = prev_power_of_two(geom.out_nsamps);
+    std::vector<std::pair<int, std::vector<int>>> glist(groups.begin(), groups.end());
+    std::vector<std::thread> fth;
+    std::exception_ptr ferr;
+    std::mutex fmu;
+    for (int dev = 0; dev < ngpu; ++dev) {
+      fth.emplace_back([&, dev] {
+        try {
+          PSOUP_HIP_CHECK(hipSetDevice(dev));
+          DevState& ds = devs[static_cast<size_t>(dev)];
+          hipStream_t st = ds.stream->get();
+          FoldEngine fe(fold_n, static_cast<float>(geom.tsamp), st);
+          const uint64_t rstride = Dedisperser::row_stride(geom.out_nsamps);
+          DeviceBuffer<uint8_t> trial(rstride);
+          for (size_t g = static_cast<size_t>(dev); g < glist.size(); g += static_cast<size_t>(ngpu)) {
+            const int dm_idx = glist[g].first;
+            ds.dd->run(dm_idx, dm_idx + 1, trial.data(), rstride, setup.dedisp_kernel);
+            std::vector<double> periods;
+            std::vector<float> accs;
+            for (int ci : glist[g].second) {
+              periods.push_back(static_cast<double>(static_cast<float>(1.0 / cands[ci].freq)));
+              accs.push_back(cands[ci].acc);
+            }
+            auto fr = fe.fold_trial(trial.data(), geom.out_nsamps, periods, accs);
+            for (size_t k = 0; k < fr.size(); ++k) {
+              Candidate& c = cands[static_cast<size_t>(glist[g].second[k])];
+              c.folded_snr = fr[k].folded_snr;
+              c.set_fold(fr[k].fold.data(), FoldEngine::kNbins, FoldEngine::kNints);
+              c.opt_period = fr[k].opt_period;
+            }
+          }
+        } catch (...) {
+          std::lock_guard<std::mutex> lk(fmu);
+          if (!ferr) ferr = std::current_exception();
+        }
+      });
+    }
+    for (auto& t : fth) t.join();
+    if (ferr) std::rethrow_exception(ferr);
+    sort_by_folded_snr(cands);
+  }
+  t_fold.stop();
+
+  const size_t new_size = std::min(static_cast<size_t>(std::max(args.limit, 0)), cands.size());
+  cands.resize(new_size);
+  res.candidates = std::move(cands);
+
+  double dmax = 0, smax = 0;
+  for (int d = 0; d < ngpu; ++d) {
+    dmax = std::max(dmax, sh.dedisp_s[static_cast<size_t>(d)]);
+    smax = std::max(smax, sh.search_s[static_cast<size_t>(d)]);
+  }
+  t_total.stop();
+  res.timers["reading"] = t_read.get_time();
+  res.timers["dedispersion"] = dmax;
+  res.timers["searching"] = t_search.get_time();
+  res.timers["folding"] = t_fold.get_time();
+  res.timers["total"] = t_total.get_time();
+  const double trials = static_cast<double>(sh.accel_trials.load());
+  res.performance["dm_accel_trials"] = trials;
+  res.performance["dm_accel_trials_per_sec"] = t_search.get_time() > 0 ? trials / t_search.get_time() : 0.0;
+  res.performance["search_kernel_seconds_max_device"] = smax;
+  return res;
+}
+
+void write_outputs(const CmdLineOptions& args, const PipelineResult& res) {
+  CandidateFileWriter cf(args.outdir);
+  cf.write_binary(res.candidates, "candidates.peasoup");
+  OverviewWriter ow;
+  ow.add_misc_info();
+  ow.add_header(args.infilename);
+  ow.add_search_parameters(args);
+  ow.add_dm_list(res.setup.dm_list);
+  ow.add_acc_list(res.setup.accel_plan.generate(0.0f));
+  ow.add_gpu_info(res.devices);
+  ow.add_candidates(res.candidates, cf.byte_mapping);
+  ow.add_timing_info(res.timers);
+  ow.add_performance(res.performance);
+  ow.to_file(args.outdir + "/overview.xml");
+}
+
+}  // namespace psoup

@@ -1,0 +1,31 @@
+"""peasoup_amd: MI355X-native pulsar acceleration search (peasoup capabilities).
+
+C++/HIP core (``peasoup_amd._C``) for gfx950 + a PyTorch-ROCm facing Python
+layer.  ``torch`` is imported first so that the extension binds to the HIP
+runtime torch already loaded (one runtime per process).
+"""
+from __future__ import annotations
+
+import torch  # noqa: F401  (must precede _C: share torch's HIP runtime)
+
+__version__ = "0.1.0"
+
+try:
+    from . import _C  # noqa: F401
+except ImportError as exc:  # pragma: no cover - exercised only when unbuilt
+    raise ImportError(
+        "peasoup_amd native extension is not built; run `python -m peasoup_amd._build` "
+        f"(hipcc/gfx950) first: {exc}"
+    ) from exc
+
+NativeError = _C.NativeError
+
+
+def native_library_path() -> str:
+    """Filesystem path of the loaded native extension."""
+    return _C.__file__
+
+
+def gpu_available() -> bool:
+    """True when a HIP device is visible to this process."""
+    return torch.cuda.is_available() and torch.cuda.device_count() > 0
