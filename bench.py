@@ -1,0 +1,166 @@
+#!/usr/bin/env python3
+"""Headline benchmark: DM x acceleration trials/s on 2^23-sample series with
+an 8-harmonic sum (-n 3), one process per MI355X (torchrun for N > 1).
+
+One step (per rank, weak scaling -- fixed work per GPU):
+  * dedisperse this rank's DM shard (``--dms-per-gpu`` trials) from the
+    resident 1024-channel 2-bit filterbank with the MFMA dedispersion kernel,
+  * whiten each trial and search +-500 m/s^2 (legacy acceleration-plan
+    convention: ~684 trials per DM at 2^23 x 64 us) with an 8-harmonic sum:
+    batched resampling -> batched rocFFT R2C -> fused interbin/normalise ->
+    fused harmonic-sum + peak compaction -> host clustering + distillation,
+  * gather every rank's candidates to all ranks over RCCL and run the global
+    DM/harmonic distillation + scoring.
+The synthetic filterbank (uniform 2-bit noise, random seed) is generated on
+rank 0's GPU and RCCL-broadcast to the others outside the timed region.
+
+Prints ONE JSON line on rank 0.  Reference number: BASELINE.md has no
+published 2^23 figure; the N*log N extrapolation of the golden-run search
+throughput (573 trials/s at 2^17 on 2x Tesla C2070) is ~6.6 trials/s, used
+for vs_baseline.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+BASELINE_TRIALS_PER_S = 6.6  # 573 trials/s @2^17 scaled by N log N to 2^23 (2x C2070)
+
+
+def parse():
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--log2n", type=int, default=23, help="FFT length = 2^log2n")
+    p.add_argument("--nchans", type=int, default=1024)
+    p.add_argument("--nbits", type=int, default=2)
+    p.add_argument("--tsamp", type=float, default=64e-6)
+    p.add_argument("--dms-per-gpu", type=int, default=2)
+    p.add_argument("--acc", type=float, default=500.0, help="search +-acc m/s^2")
+    p.add_argument("--nharmonics", type=int, default=3)
+    p.add_argument("--accel-batch", type=int, default=0)
+    p.add_argument("--dedisp-kernel", default="mfma", choices=["mfma", "direct"])
+    p.add_argument("--seed", type=int, default=1234)
+    return p.parse_args()
+
+
+def main() -> int:
+    a = parse()
+    from peasoup_amd import _C
+    from peasoup_amd.models.search import RankSearcher
+    from peasoup_amd.parallel import dist as pdist
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus != world_env and world_env == 1 and a.gpus > 1:
+        print("bench.py: for --gpus > 1 launch with torch.distributed.run (one rank per GPU)", file=sys.stderr)
+        return 2
+    ctx = pdist.init()
+    dev = ctx.device
+    assert dev.type == "cuda", "bench.py needs a GPU"
+
+    n = 1 << a.log2n
+    fch1, foff = 1550.0, -400.0 / a.nchans
+    # DM list: enough trials for every rank's shard (Levin spacing, tol 1.1, 64 us)
+    args = _C.CmdLineOptions()
+    args.infilename = "synthetic"
+    args.outdir = "/tmp/peasoup_bench"
+    args.dm_start = 0.0
+    need = a.dms_per_gpu * ctx.world_size
+    dm_end = 5.0
+    while True:
+        dms = _C.generate_dm_list(0.0, dm_end, a.tsamp, 64.0, fch1, foff, a.nchans, 1.1)
+        if len(dms) > need:
+            break
+        dm_end *= 1.5
+    args.dm_end = dm_end
+    args.acc_start, args.acc_end = -a.acc, a.acc
+    args.nharmonics = a.nharmonics
+    args.size = n
+    args.accel_batch = a.accel_batch
+    args.dedisp_kernel = a.dedisp_kernel
+    delays = _C.generate_delay_table(a.nchans, a.tsamp, fch1, foff)
+    max_delay = _C.compute_max_delay(dms, delays)
+    nsamps = n + max_delay + 4096
+    header = {"source_name": "synthetic noise", "tsamp": a.tsamp, "fch1": fch1, "foff": foff,
+              "nchans": a.nchans, "nbits": a.nbits, "nifs": 1, "data_type": 1, "tstart": 60000.0,
+              "nsamples": nsamps}
+    nbytes = nsamps * a.nchans * a.nbits // 8
+
+    # ---- synthetic filterbank on rank 0's GPU, RCCL broadcast to the others
+    packed = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    if ctx.is_root:
+        g = torch.Generator(device=dev)
+        g.manual_seed(a.seed)
+        packed.random_(0, 256, generator=g)  # every 2-bit field uniform on {0..3}
+    pdist.broadcast_bytes(packed, nbytes)
+    rs = RankSearcher(args, header, packed, nsamps)
+    del packed
+    torch.cuda.empty_cache()
+
+    shard = range(ctx.rank * a.dms_per_gpu, (ctx.rank + 1) * a.dms_per_gpu)
+    trials_per_step_local = sum(len(rs.accel_list(rs.dm_list[d])) for d in shard)
+    trials_per_step = trials_per_step_local * ctx.world_size  # identical shards sizes
+
+    def step():
+        local = rs.search(shard, chunk=a.dms_per_gpu)
+        blobs = pdist.gather_bytes(_C.serialize_candidates(local), dst=None)
+        cands = []
+        for b in blobs:
+            cands.extend(_C.deserialize_candidates(b))
+        cands.sort(key=lambda c: c.dm_idx)
+        return _C.global_distill_and_score(cands, args, rs.header)
+
+    for _ in range(a.warmup):
+        step()
+    pdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ncands = 0
+    for _ in range(a.steps):
+        ncands = len(step())
+    torch.cuda.synchronize()
+    pdist.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = pdist.all_reduce_max_float(elapsed)
+    ms_per_step = 1e3 * elapsed / a.steps
+    value = trials_per_step * a.steps / elapsed
+    if ctx.is_root:
+        out = {
+            "metric": "DM×accel trials/sec, 2^23-sample series, 8-harmonic sum",
+            "value": round(value, 2),
+            "unit": "trials/s",
+            "n_gpus": ctx.world_size,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_TRIALS_PER_S, 2),
+            "dtype": "fp32",
+            "data": "synthetic (uniform 2-bit noise filterbank, random seed)",
+            "config": {
+                "model": f"peasoup accel search: 2^{a.log2n}-pt series, +-{a.acc:g} m/s^2 (legacy plan), "
+                         f"{1 << a.nharmonics}-harmonic sum, {a.nchans}-ch {a.nbits}-bit filterbank, "
+                         f"MFMA dedispersion",
+                "global_batch": trials_per_step,
+                "seq_len": n,
+                "parallelism": f"dm{ctx.world_size}",
+                "dms_per_gpu": a.dms_per_gpu,
+                "accel_trials_per_dm": trials_per_step_local // a.dms_per_gpu,
+                "accel_batch": rs.engine.batch_size,
+                "candidates_after_distill": ncands,
+            },
+        }
+        print(json.dumps(out), flush=True)
+    pdist.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

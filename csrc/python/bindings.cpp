@@ -598,6 +598,9 @@ PYBIND11_MODULE(_C, m) {
     SearchSetup s = make_search_setup(args, dict_to_header(hdr));
     return s.accel_plan.generate(dm);
   });
+  m.def("accel_plan_from_args", [](const CmdLineOptions& args, const py::dict& hdr) {
+    return make_search_setup(args, dict_to_header(hdr)).accel_plan;
+  });
   m.def("global_distill_and_score", [](CandidateList c, const CmdLineOptions& args, const py::dict& hdr) {
     SearchSetup s = make_search_setup(args, dict_to_header(hdr));
     return global_distill_and_score(std::move(c), args, s);

@@ -227,7 +227,7 @@ PeakBounds peak_bounds(int size, float bin_width, int nh, float min_freq, float 
 }
 
 void sort_by_folded_snr(CandidateList& cands) {
-  std::stable_sort(cands.begin(), cands.end(), [](const Candidate& x, const Candidate& y) {
+  std::sort(cands.begin(), cands.end(), [](const Candidate& x, const Candidate& y) {
     return std::max(x.snr, x.folded_snr) > std::max(y.snr, y.folded_snr);
   });
 }

@@ -1,0 +1,285 @@
+"""Distributed peasoup search: one process per GPU, RCCL collectives.
+
+Flow per rank (SURVEY.md §7.1 distribution model):
+
+1. rank 0 reads the ``.fil`` (mmap) and copies the packed bytes to its GPU;
+   an RCCL broadcast over xGMI replicates them (``broadcast_bytes``), and
+   every rank unpacks them into a channel-major int8 filterbank resident in
+   HBM (``DeviceFilterbank``).
+2. each rank owns a contiguous DM shard balanced by acceleration-trial count
+   (``shard_range``); it dedisperses chunks of that shard on the MFMA
+   dedispersion kernel straight into HBM and runs the native
+   ``SearchEngine`` (whitening + batched acceleration search) on each trial.
+3. per-rank candidate trees are serialised and gathered to rank 0 over RCCL
+   (``gather_bytes``); rank 0 runs the global DM / harmonic distillation and
+   scoring.
+4. fold jobs are grouped by DM and spread round-robin over the ranks (each
+   holds the whole filterbank, so any rank can re-dedisperse any DM); results
+   are gathered to rank 0, which writes ``candidates.peasoup`` and
+   ``overview.xml``.
+
+Reference: src/pipeline_multi.cu:100-419 (Worker, DMDispenser, main) and
+include/transforms/folder.hpp:337-442 (MultiFolder).
+"""
+from __future__ import annotations
+
+import os
+import struct
+import time
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import torch
+
+from .. import _C
+from ..parallel import dist as pdist
+from ..utils.timing import Stopwatch, roctx_range
+
+
+@dataclass
+class SearchResult:
+    candidates: list
+    timers: Dict[str, float]
+    performance: Dict[str, float]
+    dm_list: List[float]
+    acc_list0: List[float]
+    devices: List[int]
+    header: dict
+    args: object = None
+    accel_trials: int = 0
+
+
+def _stream_handle() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+class RankSearcher:
+    """Per-rank search state: resident filterbank, dedisperser, engine."""
+
+    def __init__(self, args, header: dict, packed: Optional[torch.Tensor], nsamps: int,
+                 killmask: Optional[Sequence[int]] = None):
+        self.ctx = pdist.context()
+        self.args = args
+        self.header = dict(header)
+        self.header["nsamples"] = int(nsamps)
+        params, dm_list, kill, fft_size, cfreq = _C.search_params_from_args(args, self.header)
+        if killmask is not None:
+            kill = list(killmask)
+        self.params = params
+        self.dm_list = list(dm_list)
+        self.fft_size = int(fft_size)
+        self.cfreq = cfreq
+        self.geom = _C.DedispGeometry.make(self.header, int(nsamps), self.dm_list, list(kill))
+        self.stream = _stream_handle()
+        self.dfb = _C.DeviceFilterbank(self.geom, self.stream)
+        if packed is not None:
+            self.load_packed(packed)
+        self.dedisperser = _C.Dedisperser(self.dfb, self.stream)
+        self.engine = _C.SearchEngine(self.params, self.stream)
+        self.kernel = _C.DedispKernel.Mfma if args.dedisp_kernel in ("auto", "mfma") else _C.DedispKernel.Direct
+        self.row_stride = _C.Dedisperser.row_stride(self.geom.out_nsamps)
+        self.accel_plan = _C.accel_plan_from_args(args, self.header)
+        self._trials: Optional[torch.Tensor] = None
+
+    def load_packed(self, packed: torch.Tensor) -> None:
+        if packed.is_cuda:
+            self.dfb.load_packed_device(packed.data_ptr())
+        else:
+            self.dfb.load_packed_host(packed.data_ptr())
+
+    def accel_list(self, dm: float) -> List[float]:
+        return self.accel_plan.generate(float(dm))
+
+    def dedisperse(self, d0: int, d1: int) -> torch.Tensor:
+        n = d1 - d0
+        need = n * self.row_stride
+        if self._trials is None or self._trials.numel() < need:
+            self._trials = torch.empty(need, dtype=torch.uint8, device=self.ctx.device)
+        self.dedisperser.run(d0, d1, self._trials.data_ptr(), self.row_stride, self.kernel)
+        return self._trials
+
+    def search(self, dm_indices: Sequence[int], chunk: int = 16, timers: Optional[Dict[str, Stopwatch]] = None,
+               progress=None) -> list:
+        cands: list = []
+        idx = list(dm_indices)
+        t_dd = timers.get("dedispersion") if timers else None
+        t_s = timers.get("searching") if timers else None
+        ntrials = 0
+        for c0 in range(0, len(idx), chunk):
+            block = idx[c0:c0 + chunk]
+            d0, d1 = block[0], block[-1] + 1
+            assert d1 - d0 == len(block), "DM shard must be contiguous"
+            if t_dd:
+                t_dd.start()
+            with roctx_range("Dedisperse"):
+                trials = self.dedisperse(d0, d1)
+            if t_dd:
+                torch.cuda.current_stream().synchronize()
+                t_dd.stop()
+            if t_s:
+                t_s.start()
+            for k, d in enumerate(block):
+                dm = self.dm_list[d]
+                accs = self.accel_list(dm)
+                ntrials += len(accs)
+                addr = trials.data_ptr() + k * self.row_stride
+                cands.extend(self.engine.search_trial(addr, self.geom.out_nsamps, dm, d, accs))
+                if progress is not None:
+                    progress(1)
+            if t_s:
+                t_s.stop()
+        self.accel_trials = ntrials
+        return cands
+
+    def fold(self, groups: Dict[int, List[int]], cands: list) -> Dict[int, tuple]:
+        """Fold candidates (index -> (folded_snr, opt_period, fold)) for the DM groups given."""
+        out: Dict[int, tuple] = {}
+        if not groups:
+            return out
+        n = _C.prev_power_of_two(self.geom.out_nsamps)
+        fe = _C.FoldEngine(n, float(self.header["tsamp"]), self.stream)
+        for dm_idx, members in sorted(groups.items()):
+            trials = self.dedisperse(dm_idx, dm_idx + 1)
+            periods = [float(struct.unpack("f", struct.pack("f", 1.0 / cands[i].freq))[0]) for i in members]
+            accs = [cands[i].acc for i in members]
+            res = fe.fold_trial(trials.data_ptr(), self.geom.out_nsamps, periods, accs)
+            for i, r in zip(members, res):
+                out[i] = (r.folded_snr, r.opt_period, list(r.fold))
+        return out
+
+
+def _encode_fold_results(res: Dict[int, tuple]) -> bytes:
+    parts = [struct.pack("<i", len(res))]
+    for i, (snr, per, fold) in res.items():
+        parts.append(struct.pack("<ifdi", i, snr, per, len(fold)))
+        parts.append(struct.pack(f"<{len(fold)}f", *fold))
+    return b"".join(parts)
+
+
+def _decode_fold_results(b: bytes) -> Dict[int, tuple]:
+    out: Dict[int, tuple] = {}
+    (n,) = struct.unpack_from("<i", b, 0)
+    off = 4
+    for _ in range(n):
+        i, snr, per, nf = struct.unpack_from("<ifdi", b, off)
+        off += struct.calcsize("<ifdi")
+        fold = list(struct.unpack_from(f"<{nf}f", b, off))
+        off += 4 * nf
+        out[i] = (snr, per, fold)
+    return out
+
+
+def load_packed_for_rank(infilename: str, ctx: pdist.DistContext):
+    """Rank 0 reads the filterbank; the packed bytes are RCCL-broadcast to
+    every rank's GPU.  Returns (header, packed_tensor_on_device, nsamps)."""
+    header = None
+    packed = None
+    if ctx.is_root:
+        fb = _C.Filterbank.from_file(infilename)
+        header = fb.header
+        nbytes = int(fb.data_bytes)
+        hdr_bytes = repr(header).encode()
+    else:
+        hdr_bytes = None
+    hdr_bytes = pdist.broadcast_object_bytes(hdr_bytes)
+    if header is None:
+        import ast
+
+        header = ast.literal_eval(hdr_bytes.decode())
+    nsamps = int(header["nsamples"])
+    nbytes = nsamps * int(header["nchans"]) * int(header["nbits"]) // 8
+    if ctx.device.type == "cuda":
+        packed = torch.empty(nbytes, dtype=torch.uint8, device=ctx.device)
+        if ctx.is_root:
+            host = torch.from_numpy(fb.data())[:nbytes]
+            packed.copy_(host, non_blocking=False)
+        if ctx.distributed:
+            pdist.broadcast_bytes(packed, nbytes)
+    else:
+        packed = torch.from_numpy(fb.data()[:nbytes].copy()) if ctx.is_root else None
+    return header, packed, nsamps
+
+
+def run_search(args, write: bool = True) -> Optional[SearchResult]:
+    """Full distributed search (torchrun: one rank per GPU).  Returns the
+    result on rank 0 (None elsewhere)."""
+    ctx = pdist.init()
+    timers = {k: Stopwatch() for k in ("reading", "dedispersion", "searching", "folding", "total")}
+    timers["total"].start()
+    timers["reading"].start()
+    header, packed, nsamps = load_packed_for_rank(args.infilename, ctx)
+    timers["reading"].stop()
+
+    rs = RankSearcher(args, header, packed, nsamps)
+    del packed
+    ndm = len(rs.dm_list)
+    weights = [len(rs.accel_list(d)) for d in rs.dm_list]
+    shard = pdist.shard_range(ndm, ctx.world_size, ctx.rank, weights)
+    pdist.barrier()
+    t0 = time.perf_counter()
+    local = rs.search(shard, timers=timers)
+    torch.cuda.synchronize()
+    search_wall = time.perf_counter() - t0
+    local_trials = sum(weights[i] for i in shard)
+
+    # ---- candidate gather (RCCL) + global distillation on rank 0
+    blobs = pdist.gather_bytes(_C.serialize_candidates(local), dst=None)
+    total_trials = sum(weights)
+    cands = []
+    for b in blobs:
+        cands.extend(_C.deserialize_candidates(b))
+    cands.sort(key=lambda c: c.dm_idx)
+    cands = _C.global_distill_and_score(cands, args, rs.header)
+    search_wall = pdist.all_reduce_max_float(search_wall)
+
+    # ---- distributed folding (all ranks hold identical `cands`)
+    timers["folding"].start()
+    if args.npdmp > 0 and cands:
+        groups = {}
+        count = min(args.npdmp, len(cands))
+        for i in range(count):
+            p = float(struct.unpack("f", struct.pack("f", 1.0 / cands[i].freq))[0])
+            if 0.001 < p < 10.0:
+                groups.setdefault(cands[i].dm_idx, []).append(i)
+        keys = sorted(groups)
+        mine = {k: groups[k] for j, k in enumerate(keys) if j % ctx.world_size == ctx.rank}
+        res = rs.fold(mine, cands)
+        parts = pdist.gather_bytes(_encode_fold_results(res), dst=0)
+        if ctx.is_root:
+            for p in parts:
+                for i, (snr, per, fold) in _decode_fold_results(p).items():
+                    c = cands[i]
+                    c.folded_snr = snr
+                    c.opt_period = per
+                    c.fold = fold
+                    c.nbins, c.nints = 64, 16
+                    cands[i] = c
+            cands = _C.sort_by_folded_snr(cands)
+    timers["folding"].stop()
+    if not ctx.is_root:
+        timers["total"].stop()
+        return None
+    cands = cands[: max(0, args.limit)]
+    timers["total"].stop()
+    perf = {
+        "dm_accel_trials": float(total_trials),
+        "dm_accel_trials_per_sec": total_trials / search_wall if search_wall > 0 else 0.0,
+        "ranks": float(ctx.world_size),
+    }
+    tdict = {k: v.get_time() for k, v in timers.items()}
+    acc0 = rs.accel_list(0.0)
+    res = SearchResult(cands, tdict, perf, rs.dm_list, acc0, list(range(ctx.world_size)) if ctx.device.type == "cuda" else [],
+                       rs.header, args, total_trials)
+    if write:
+        write_outputs(args, res)
+    return res
+
+
+def write_outputs(args, res: SearchResult) -> None:
+    os.makedirs(args.outdir, exist_ok=True)
+    bm = _C.write_candidates_binary(args.outdir, res.candidates, "candidates.peasoup")
+    devices = [torch.cuda.current_device()] if res.devices else []
+    if len(res.devices) > 1:
+        devices = list(range(min(len(res.devices), torch.cuda.device_count())))
+    _C.write_overview(os.path.join(args.outdir, "overview.xml"), args, args.infilename, res.dm_list, res.acc_list0,
+                      devices, res.candidates, bm, res.timers, res.performance)
