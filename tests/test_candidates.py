@@ -1,0 +1,182 @@
+"""Distillers, scorer, peak clustering, serialisation vs pure-Python oracles."""
+import math
+import random
+
+import numpy as np
+import pytest
+
+from peasoup_amd.utils import reference as ref
+
+
+class Cand:
+    def __init__(self, dm, dm_idx, acc, nh, snr, freq):
+        self.dm, self.dm_idx, self.acc, self.nh, self.snr, self.freq = dm, dm_idx, acc, nh, snr, freq
+        self.assoc = []
+
+
+def py_distill(cands, cond):
+    cands = sorted(cands, key=lambda c: -c.snr)
+    uniq = [True] * len(cands)
+    start = 0
+    while True:
+        idx = -1
+        for ii in range(start, len(cands)):
+            if uniq[ii]:
+                start, idx = ii + 1, ii
+                break
+        if idx < 0:
+            break
+        cond(cands, idx, uniq)
+    return [c for c, u in zip(cands, uniq) if u]
+
+
+def f32(x):
+    return float(np.float32(x))
+
+
+def harm_cond(tol, max_harm, keep, frac):
+    def cond(c, idx, uniq):
+        f0 = c[idx].freq
+        for ii in range(idx + 1, len(c)):
+            maxd = 2.0 ** c[ii].nh if frac else 1
+            for jj in range(1, int(max_harm) + 1):
+                kk = 1
+                while kk <= maxd:
+                    r = kk * c[ii].freq / (jj * f0)
+                    if 1 - f32(tol) < r < 1 + f32(tol):
+                        if keep:
+                            c[idx].assoc.append(c[ii])
+                        uniq[ii] = False
+                    kk += 1
+    return cond
+
+
+def acc_cond(tobs, tol, keep):
+    toc = f32(tobs) / 299792458.0
+
+    def cond(c, idx, uniq):
+        f0, a0 = c[idx].freq, c[idx].acc
+        edge = f0 * f32(tol)
+        for ii in range(idx + 1, len(c)):
+            af = f32(f0 + (a0 - c[ii].acc) * f0 * toc)
+            f = c[ii].freq
+            rel = (f0 - edge < f < af + edge) if af > f0 else (af - edge < f < f0 + edge)
+            if rel:
+                if keep:
+                    c[idx].assoc.append(c[ii])
+                uniq[ii] = False
+    return cond
+
+
+def dm_cond(tol, keep):
+    def cond(c, idx, uniq):
+        for ii in range(idx + 1, len(c)):
+            r = c[ii].freq / c[idx].freq
+            if 1 - f32(tol) < r < 1 + f32(tol):
+                if keep:
+                    c[idx].assoc.append(c[ii])
+                uniq[ii] = False
+    return cond
+
+
+def random_cands(rng, n, base_freqs=(4.0, 7.3, 11.1)):
+    out = []
+    for _ in range(n):
+        f0 = rng.choice(base_freqs)
+        h = rng.choice([1, 2, 3, 0.5, 0.25, 1.5])
+        f = f32(f0 * h * (1 + rng.uniform(-2e-5, 2e-5)))
+        out.append((f32(rng.uniform(0, 100)), rng.randrange(0, 50), f32(rng.uniform(-50, 50)), rng.randrange(0, 5),
+                    f32(rng.uniform(9, 60)), f))
+    return out
+
+
+def to_native(C, tuples):
+    return [C.Candidate(*t) for t in tuples]
+
+
+def sig(c):
+    return (round(c.snr, 5), round(c.freq, 7), c.nh, c.dm_idx, round(c.acc, 4))
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_harmonic_distiller_matches_python(C, seed):
+    rng = random.Random(seed)
+    tup = random_cands(rng, 120)
+    for keep, frac in ((False, True), (True, False), (True, True)):
+        nat = C.HarmonicDistiller(1e-4, 16, keep, frac).distill(to_native(C, tup))
+        py = py_distill([Cand(*t) for t in tup], harm_cond(1e-4, 16, keep, frac))
+        assert [sig(c) for c in nat] == [sig(c) for c in py]
+        if keep:
+            assert [c.count_assoc() for c in nat] == [len(c.assoc) for c in py]
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_acceleration_and_dm_distillers_match_python(C, seed):
+    rng = random.Random(seed)
+    tup = random_cands(rng, 150)
+    nat = C.AccelerationDistiller(41.94304, 1e-4, True).distill(to_native(C, tup))
+    py = py_distill([Cand(*t) for t in tup], acc_cond(41.94304, 1e-4, True))
+    assert [sig(c) for c in nat] == [sig(c) for c in py]
+    assert [c.count_assoc() for c in nat] == [len(c.assoc) for c in py]
+    nat = C.DMDistiller(1e-4, True).distill(to_native(C, tup))
+    py = py_distill([Cand(*t) for t in tup], dm_cond(1e-4, True))
+    assert [sig(c) for c in nat] == [sig(c) for c in py]
+
+
+def test_keep_related_appends_once_per_match(C):
+    # candidate at 2x the fundamental matches jj=2,kk=1 and jj=4,kk=2 (nh=1 -> 2 denominators)
+    c = [C.Candidate(10, 1, 0, 1, 50.0, 1.0), C.Candidate(10, 1, 0, 1, 20.0, 2.0)]
+    out = C.HarmonicDistiller(1e-4, 16, True, True).distill(c)
+    assert len(out) == 1 and out[0].count_assoc() == 2
+
+
+def test_scorer(C):
+    cands = [C.Candidate(20.0, 6, 0.0, 4, 80.0, 4.0)]
+    a1 = C.Candidate(23.0, 7, 0.0, 3, 70.0, 4.0)
+    a2 = C.Candidate(100.0, 30, 0.0, 3, 10.0, 4.0)
+    cands[0].assoc = [a1, a2]
+    s = C.CandidateScorer(0.00032, 1475.12, -1.09, 1.09 * 64).score_all(cands)[0]
+    assert s.is_physical  # always true for foff < 0
+    assert s.is_adjacent  # has dm_idx + 1
+    ftop, fbot = 1475.12 + 1.09 * 32, 1475.12 - 1.09 * 32
+    ddm = 1.0 / (4.0 * 4150.0 * (1 / fbot ** 2 - 1 / ftop ** 2))
+    inside = 1 + (abs(20 - 23) <= ddm) + (abs(20 - 100) <= ddm)
+    assert s.ddm_count_ratio == pytest.approx(inside / 3)
+    lone = C.CandidateScorer(0.00032, 1475.12, -1.09, 69.76).score_all([C.Candidate(1, 3, 0, 0, 9, 2)])[0]
+    assert lone.is_adjacent and lone.ddm_count_ratio == 1.0
+
+
+def test_identify_unique_peaks(C):
+    rng = np.random.default_rng(5)
+    idx = np.sort(rng.choice(100000, 2000, replace=False)).astype(np.int32)
+    snr = rng.uniform(9, 30, size=2000).astype(np.float32)
+    pi, ps = C.identify_unique_peaks(list(idx), list(snr), 30)
+    exp = ref.unique_peaks(idx, snr, 30)
+    assert list(zip(pi, ps)) == [(a, pytest.approx(b)) for a, b in exp]
+    # gap measured from the last MAXIMUM: 0(10) 20(5) 45(4) -> one cluster? 45-0 >= 30 -> split
+    pi, ps = C.identify_unique_peaks([0, 20, 45], [10.0, 5.0, 4.0], 30)
+    assert pi == [0, 45]
+
+
+def test_peak_bounds_match_reference(C):
+    for nb, bw, nh in ((65537, 0.0238, 0), (65537, 0.0238, 3), (4194305, 0.00186, 3)):
+        s, e, f = C.peak_bounds(nb, bw, nh, 0.1, 1100.0)
+        rs, re_, rf = ref.peak_bounds(nb, bw, nh, 0.1, 1100.0)
+        assert (s, e) == (rs, re_) and f == pytest.approx(rf, rel=1e-12)
+
+
+def test_serialisation_roundtrip(C):
+    a = C.Candidate(1.5, 2, -3.0, 4, 55.5, 3.25)
+    a.folded_snr = 12.5
+    a.opt_period = 0.3077
+    a.fold = [float(i) for i in range(64 * 16)]
+    a.nbins, a.nints = 64, 16
+    b = C.Candidate(2.5, 3, 1.0, 1, 22.0, 6.5)
+    b.assoc = [C.Candidate(3.5, 4, 0.0, 0, 11.0, 13.0)]
+    a.assoc = [b]
+    blob = C.serialize_candidates([a, b])
+    back = C.deserialize_candidates(blob)
+    assert len(back) == 2 and back[0].count_assoc() == 2 and back[0].fold == a.fold
+    assert back[0].opt_period == a.opt_period and back[0].assoc[0].assoc[0].freq == 13.0
+    assert [p[5] for p in back[0].pods()] == [3.25, 6.5, 13.0]
+    assert C.deserialize_candidates(C.serialize_candidates([])) == []

@@ -1,0 +1,102 @@
+"""SIGPROC I/O, DM list, delay table and acceleration plan parity (CPU)."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import TUTORIAL, DATA
+from peasoup_amd.utils import sigproc
+
+
+def test_tutorial_header_native_and_python(C):
+    h = C.read_header(TUTORIAL)
+    p = sigproc.read_header(TUTORIAL)
+    assert h["nchans"] == 64 and h["nbits"] == 2 and h["nsamples"] == 187520
+    assert h["tsamp"] == pytest.approx(0.00032) and h["fch1"] == 1510.0 and h["foff"] == pytest.approx(-1.09)
+    assert h["size"] == 244 == p["size"]
+    for k in ("nchans", "nbits", "nsamples", "tsamp", "fch1", "foff", "tstart", "source_name", "signed"):
+        assert h[k] == p[k], k
+    fb = C.Filterbank.from_file(TUTORIAL)
+    assert fb.nsamps == 187520 and fb.data_bytes == 187520 * 16
+    assert fb.cfreq() == pytest.approx(1475.12, abs=1e-3)
+
+
+def test_filterbank_roundtrip(C, tmp_path):
+    rng = np.random.default_rng(0)
+    for nbits in (1, 2, 4, 8):
+        vals = rng.integers(0, 1 << nbits, size=(300, 16), dtype=np.uint8)
+        hdr = {"nchans": 16, "nbits": nbits, "tsamp": 1e-4, "fch1": 1400.0, "foff": -0.5, "nifs": 1,
+               "source_name": "rt", "tstart": 55000.5}
+        p = str(tmp_path / f"x{nbits}.fil")
+        sigproc.write_filterbank(p, hdr, vals)
+        back = sigproc.read_filterbank(p)
+        assert np.array_equal(back.data, vals)
+        nh = C.read_header(p)
+        assert nh["nsamples"] == 300 and nh["nbits"] == nbits and nh["source_name"] == "rt"
+        # native writer -> python reader
+        p2 = str(tmp_path / f"y{nbits}.fil")
+        C.write_filterbank(p2, hdr, sigproc.pack_samples(vals, nbits))
+        assert np.array_equal(sigproc.read_filterbank(p2).data, vals)
+
+
+def test_tim_roundtrip(C, tmp_path):
+    x = np.linspace(-3, 3, 1000).astype(np.float32)
+    p = str(tmp_path / "a.tim")
+    C.write_tim(p, {"tsamp": 6.4e-5, "fch1": 1400.0, "source_name": "t"}, list(x))
+    h, d = C.read_tim(p)
+    assert h["nsamples"] == 1000 and np.allclose(d, x)
+    h2, d2 = sigproc.read_tim(p)
+    assert np.array_equal(d2, x)
+
+
+def test_killfile_zapfile(C, tmp_path):
+    k = tmp_path / "kill.txt"
+    k.write_text("\n".join(["1"] * 60 + ["0"] * 4) + "\n")
+    mask, ok = C.read_killfile(str(k), 64)
+    assert ok and mask[:60] == [1] * 60 and mask[60:] == [0] * 4
+    mask, ok = C.read_killfile(str(k), 128)  # wrong size: warning + all ones
+    assert not ok and mask == [1] * 128
+    f, w = C.read_zapfile(os.path.join(DATA, "default_zaplist.txt"))
+    assert f == pytest.approx([50, 100, 150, 200, 250]) and w == pytest.approx([0.1, 0.15, 0.15, 0.15, 0.15])
+
+
+def test_dm_list_matches_golden_bit_for_bit(C, golden):
+    dms = C.generate_dm_list(0.0, 250.0, 0.00032, 64.0, 1510.0, -1.09, 64, 1.1)
+    ref = golden.dm_list
+    assert len(dms) == len(ref) == 59
+    # golden values are float32 printed with 15 significant digits
+    assert [C.xml_fmt_float(d) for d in dms] == [
+        t.text for t in golden.root.find("dedispersion_trials").findall("trial")]
+
+
+def test_delay_table_and_max_delay(C):
+    from peasoup_amd.utils import reference as ref
+
+    d = C.generate_delay_table(64, 0.00032, 1510.0, -1.09)
+    assert np.allclose(d, ref.delay_table(64, 0.00032, 1510.0, -1.09))
+    dms = C.generate_dm_list(0.0, 250.0, 0.00032, 64.0, 1510.0, -1.09, 64, 1.1)
+    assert C.compute_max_delay(dms, d) == 140
+    g = C.DedispGeometry.make(C.read_header(TUTORIAL), 187520, dms, [])
+    assert g.out_nsamps == 187380 and g.out_scale == 1.0 and g.nactive == 64
+
+
+def test_accel_plan_conventions(C):
+    cf = C.Filterbank.from_file(TUTORIAL).cfreq()
+    legacy = C.AccelPlan(-5, 5, 1.1, 64.0, 131072, 0.00032, cf, -1.09)
+    assert legacy.generate(0.0) == [0.0, -5.0, 5.0]  # golden overview.xml:124-128
+    assert legacy.step(0.0) == pytest.approx(239.9, rel=1e-3)
+    cur = C.AccelPlan(-5, 5, 1.1, 64.0, 131072, 0.00032, cf, -1.09, C.AccelConvention.Reference)
+    lst = cur.generate(0.0)
+    assert len(lst) == 44 and lst[0] == 0.0 and lst[1] == -5.0 and lst[-1] == 5.0
+    assert cur.step(0.0) == pytest.approx(0.2399, rel=1e-3)
+    # 2^23 x 64 us, +-500
+    big = C.AccelPlan(-500, 500, 1.1, 64.0, 1 << 23, 64e-6, 1400.0, -0.39)
+    assert big.step(0.0) == pytest.approx(1.464, rel=2e-3)
+    assert 680 <= len(big.generate(0.0)) <= 690
+    assert C.AccelPlan(0, 0, 1.1, 64.0, 1024, 1e-4, 1400.0, -1).generate(3.0) == [0.0]
+
+
+def test_prev_power_of_two_strictly_less(C):
+    assert C.prev_power_of_two(187520) == 131072
+    assert C.prev_power_of_two(1 << 23) == 1 << 22  # exact power -> half (utils.hpp:12-18)
+    assert C.prev_power_of_two((1 << 23) + 1) == 1 << 23

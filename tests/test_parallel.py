@@ -1,0 +1,87 @@
+"""Multi-process collectives on the gloo backend (world_size 2, CPU)."""
+import os
+import socket
+import sys
+
+import pytest
+import torch.multiprocessing as mp
+
+from peasoup_amd.parallel import dist as pdist
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    try:
+        import torch
+
+        import peasoup_amd
+        from peasoup_amd import _C
+
+        ctx = pdist.init(backend="gloo")
+        assert ctx.world_size == world and ctx.rank == rank
+        # candidate gather: each rank serialises a different tree
+        c = _C.Candidate(1.0 + rank, rank, 0.0, rank, 10.0 + rank, 2.0 + rank)
+        c.assoc = [_C.Candidate(5.0, 7, 1.0, 1, 3.0, 4.0)] * (rank + 1)
+        blobs = pdist.gather_bytes(_C.serialize_candidates([c]), dst=0)
+        res = {}
+        if rank == 0:
+            got = [_C.deserialize_candidates(b)[0] for b in blobs]
+            res["gather"] = [(g.dm_idx, g.count_assoc()) for g in got]
+        # broadcast of a byte buffer (filterbank broadcast path)
+        buf = torch.arange(1000, dtype=torch.int64).to(torch.uint8) if rank == 0 else None
+        out = pdist.broadcast_bytes(buf, 1000)
+        res["bcast"] = int(out.to(torch.int64).sum())
+        s = pdist.broadcast_object_bytes(b"hello-header" if rank == 0 else None)
+        res["obj"] = s
+        t = torch.full((8,), rank + 1, dtype=torch.uint8)
+        pdist.all_reduce_sum(t)
+        res["allreduce"] = int(t[0])
+        res["max"] = pdist.all_reduce_max_float(float(rank))
+        pdist.barrier()
+        q.put((rank, res))
+        pdist.shutdown()
+    except Exception as e:  # pragma: no cover
+        import traceback
+
+        q.put((rank, {"error": traceback.format_exc()}))
+
+
+def test_gloo_collectives_world2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(2):
+        assert "error" not in out[r], out[r].get("error")
+    assert out[0]["gather"] == [(0, 1), (1, 2)]
+    assert out[0]["bcast"] == out[1]["bcast"] == sum(i % 256 for i in range(1000))
+    assert out[1]["obj"] == b"hello-header"
+    assert out[0]["allreduce"] == out[1]["allreduce"] == 3
+    assert out[0]["max"] == out[1]["max"] == 1.0
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_shard_range_partitions(world):
+    n = 59
+    shards = [pdist.shard_range(n, world, r) for r in range(world)]
+    assert sum(len(s) for s in shards) == n
+    assert [i for s in shards for i in s] == list(range(n))
+    w = [1.0 + (i % 7) for i in range(n)]
+    shards = [pdist.shard_range(n, world, r, w) for r in range(world)]
+    assert [i for s in shards for i in s] == list(range(n))
+    loads = [sum(w[i] for i in s) for s in shards]
+    assert max(loads) - min(loads) <= max(w) + 1e-9
