@@ -533,6 +533,12 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("tobs", &SearchEngine::tobs)
       .def_property_readonly("whitened_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.whitened()); })
       .def_property_readonly("stats_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.whitener().stats()); })
+      .def("copy_whitened", [](const SearchEngine& e, uintptr_t dst) {
+        PSOUP_HIP_CHECK(hipMemcpy(P<void>(dst), e.whitened(), e.params().fft_size * sizeof(float), hipMemcpyDeviceToDevice));
+      })
+      .def("copy_stats", [](const SearchEngine& e, uintptr_t dst) {
+        PSOUP_HIP_CHECK(hipMemcpy(P<void>(dst), e.whitener().stats(), 3 * sizeof(float), hipMemcpyDeviceToDevice));
+      })
       .def("counters", [](const SearchEngine& e) {
         const SearchCounters& c = e.counters();
         py::dict d;

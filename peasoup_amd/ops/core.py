@@ -1,0 +1,283 @@
+"""Op implementations (see package docstring)."""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from .. import _C
+
+K = _C.kernels
+
+
+def _s() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _check(t: torch.Tensor, dtype: torch.dtype, name: str) -> None:
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a HIP (cuda) tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def _cplx_ptr(t: torch.Tensor) -> int:
+    _check(t, torch.complex64, "complex tensor")
+    return t.data_ptr()
+
+
+# ------------------------------------------------------------------ dedisp --
+def unpack_transpose(packed: torch.Tensor, nsamps: int, nchans: int, nbits: int, bias: int = 0,
+                     stride: Optional[int] = None) -> torch.Tensor:
+    """Packed SIGPROC bytes -> int8 [nchans, stride] (value - bias)."""
+    _check(packed, torch.uint8, "packed")
+    stride = stride or nsamps
+    out = torch.zeros((nchans, stride), dtype=torch.int8, device=packed.device)
+    K.unpack_transpose(packed.data_ptr(), nsamps, nchans, nbits, out.data_ptr(), stride, bias, _s())
+    return out
+
+
+def dedisperse(chan_major: torch.Tensor, offsets: torch.Tensor, out_nsamps: int, scale: float, bias: int = 0,
+               killmask: Optional[torch.Tensor] = None, kernel: str = "direct") -> torch.Tensor:
+    """Brute-force dedispersion of an int8 [nchans, stride] block.
+
+    offsets: int32 [ndm, nchans] sample delays.  Returns uint8 [ndm, out_nsamps].
+    kernel: "direct" (VALU) or "mfma" (v_mfma_i32_32x32x32_i8 one-hot GEMM).
+    """
+    _check(chan_major, torch.int8, "chan_major")
+    nchans, stride = chan_major.shape
+    ndm = offsets.shape[0]
+    dev = chan_major.device
+    kill = killmask if killmask is not None else torch.ones(nchans, dtype=torch.int32, device=dev)
+    nactive = int(kill.ne(0).sum())
+    out = torch.empty((ndm, out_nsamps), dtype=torch.uint8, device=dev)
+    if kernel == "direct":
+        offs = offsets.to(dev, torch.int32).contiguous()
+        K.dedisperse_direct(chan_major.data_ptr(), stride, nchans, offs.data_ptr(), kill.to(dev, torch.int32).contiguous().data_ptr(),
+                            ndm, out_nsamps, out.data_ptr(), out_nsamps, float(scale), int(bias), nactive, _s())
+        return out
+    raise ValueError("mfma dedispersion is driven through _C.Dedisperser (needs padded rows)")
+
+
+# ------------------------------------------------------------ time series --
+def convert_pad(trial: torch.Tensor, n: int) -> torch.Tensor:
+    """uint8 trial -> float32[n]: copy (truncate) or pad with the trial mean."""
+    _check(trial, torch.uint8, "trial")
+    out = torch.empty(n, dtype=torch.float32, device=trial.device)
+    tmp = torch.zeros(1, dtype=torch.int64, device=trial.device)
+    K.u8_to_f32_pad(trial.data_ptr(), min(trial.numel(), n), out.data_ptr(), n, tmp.data_ptr(), _s())
+    return out
+
+
+# ------------------------------------------------------------------ FFT -----
+class FFTPlanCache:
+    """rocFFT plan cache keyed by (type, n, batch)."""
+
+    _plans: Dict[Tuple, object] = {}
+
+    @classmethod
+    def get(cls, kind: str, n: int, batch: int = 1):
+        key = (kind, n, batch, torch.cuda.current_device())
+        p = cls._plans.get(key)
+        if p is None:
+            t = {"r2c": _C.FftType.R2C, "c2r": _C.FftType.C2R, "c2c_fwd": _C.FftType.C2C_FWD,
+                 "c2c_inv": _C.FftType.C2C_INV}[kind]
+            p = _C.FftPlan(t, n, batch)
+            cls._plans[key] = p
+        return p
+
+
+def rfft(x: torch.Tensor) -> torch.Tensor:
+    """Unnormalised real-to-complex FFT over the last dim (rocFFT)."""
+    _check(x, torch.float32, "x")
+    n = x.shape[-1]
+    batch = x.numel() // n
+    out = torch.empty(x.shape[:-1] + (n // 2 + 1,), dtype=torch.complex64, device=x.device)
+    FFTPlanCache.get("r2c", n, batch).execute(x.data_ptr(), out.data_ptr(), _s())
+    return out
+
+
+def irfft(X: torch.Tensor, n: int) -> torch.Tensor:
+    """Unnormalised complex-to-real inverse FFT (cuFFT/rocFFT convention: x*n)."""
+    Xc = X.contiguous().clone()  # C2R may overwrite its input
+    batch = Xc.numel() // (n // 2 + 1)
+    out = torch.empty(X.shape[:-1] + (n,), dtype=torch.float32, device=X.device)
+    FFTPlanCache.get("c2r", n, batch).execute(_cplx_ptr(Xc), out.data_ptr(), _s())
+    return out
+
+
+# --------------------------------------------------------------- spectra ----
+def form_amplitude(X: torch.Tensor) -> torch.Tensor:
+    out = torch.empty(X.numel(), dtype=torch.float32, device=X.device)
+    K.form_amplitude(_cplx_ptr(X), X.numel(), out.data_ptr(), _s())
+    return out
+
+
+def form_interbin(X: torch.Tensor) -> torch.Tensor:
+    out = torch.empty(X.numel(), dtype=torch.float32, device=X.device)
+    K.form_interbin(_cplx_ptr(X), X.numel(), out.data_ptr(), _s())
+    return out
+
+
+def normalise(x: torch.Tensor, mean: float, sigma: float) -> torch.Tensor:
+    _check(x, torch.float32, "x")
+    K.normalise(x.data_ptr(), x.numel(), float(mean), float(sigma), _s())
+    return x
+
+
+def median_scrunch5(x: torch.Tensor, from_complex: bool = False) -> torch.Tensor:
+    n = x.numel()
+    out = torch.empty(max(1, n // 5), dtype=torch.float32, device=x.device)
+    if from_complex:
+        K.median5_amp(_cplx_ptr(x), n, out.data_ptr(), _s())
+    else:
+        _check(x, torch.float32, "x")
+        K.median5(x.data_ptr(), n, out.data_ptr(), _s())
+    return out
+
+
+def running_median(X: torch.Tensor):
+    """The three median scrunches of Dereddener::calculate_median."""
+    m5 = median_scrunch5(X, from_complex=True)
+    m25 = median_scrunch5(m5)
+    m125 = median_scrunch5(m25)
+    return m5, m25, m125
+
+
+def deredden(X: torch.Tensor, bin_width: float, zapmask: Optional[torch.Tensor] = None,
+             boundary5: float = 0.05, boundary25: float = 0.5) -> torch.Tensor:
+    """In place: X /= running median (bins < 5 -> 0), zapped bins -> 1+0i."""
+    nb = X.numel()
+    m5, m25, m125 = running_median(X)
+    pos5 = int(float(torch.tensor(boundary5, dtype=torch.float32) / torch.tensor(bin_width, dtype=torch.float32)))
+    pos25 = int(float(torch.tensor(boundary25, dtype=torch.float32) / torch.tensor(bin_width, dtype=torch.float32)))
+    zp = 0
+    if zapmask is not None:
+        _check(zapmask, torch.int32, "zapmask")
+        zp = zapmask.data_ptr()
+    K.deredden_zap(_cplx_ptr(X), nb, m5.data_ptr(), nb // 5, m25.data_ptr(), max(1, nb // 25), m125.data_ptr(),
+                   max(1, nb // 125), pos5, pos25, zp, _s())
+    return X
+
+
+def interbin_stats(X: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Interbinned spectrum + device stats {mean, rms, std}."""
+    P = torch.empty(X.numel(), dtype=torch.float32, device=X.device)
+    partials = torch.empty(2048, dtype=torch.float64, device=X.device)
+    st = torch.empty(4, dtype=torch.float32, device=X.device)
+    K.interbin_stats(_cplx_ptr(X), X.numel(), P.data_ptr(), partials.data_ptr(), 1024, st.data_ptr(), _s())
+    return P, st
+
+
+def interbin_normalise(X: torch.Tensor, stats: torch.Tensor, nscale: float, nbins_out: Optional[int] = None):
+    """Batched: X complex [K, B] -> (interbin(X) - mean*nscale)/(std*nscale)."""
+    Kb, nb = X.shape
+    nbo = nbins_out or nb
+    P = torch.empty((Kb, nbo), dtype=torch.float32, device=X.device)
+    K.interbin_normalise_batch(_cplx_ptr(X), nb, nb, P.data_ptr(), nbo, Kb, nbo, stats.data_ptr(), float(nscale), _s())
+    return P
+
+
+# ---------------------------------------------------------- acceleration ---
+def resample(x: torch.Tensor, accels: Sequence[float], tsamp: float) -> torch.Tensor:
+    """Batched time-domain acceleration resampling (resampleII semantics)."""
+    _check(x, torch.float32, "x")
+    n = x.numel()
+    af = torch.tensor([(float(torch.tensor(a, dtype=torch.float32)) * float(torch.tensor(tsamp, dtype=torch.float32)))
+                       / (2 * 299792458.0) for a in accels], dtype=torch.float64, device=x.device)
+    stride = (n + 3) // 4 * 4
+    out = torch.empty((len(accels), stride), dtype=torch.float32, device=x.device)
+    K.resample_batch(x.data_ptr(), n, out.data_ptr(), stride, af.data_ptr(), len(accels), _s())
+    return out[:, :n]
+
+
+def resample_v1(x: torch.Tensor, accel: float, tsamp: float) -> torch.Tensor:
+    _check(x, torch.float32, "x")
+    af = (float(torch.tensor(accel, dtype=torch.float32)) * float(torch.tensor(tsamp, dtype=torch.float32))) / (2 * 299792458.0)
+    out = torch.empty_like(x)
+    K.resample_v1(x.data_ptr(), x.numel(), out.data_ptr(), af, _s())
+    return out
+
+
+def harmonic_sums(P: torch.Tensor, nlevels: int) -> torch.Tensor:
+    """Materialised harmonic sums [nlevels, n] (debug/test path)."""
+    _check(P, torch.float32, "P")
+    out = torch.empty((max(1, nlevels), P.numel()), dtype=torch.float32, device=P.device)
+    K.harmonic_sums(P.data_ptr(), P.numel(), nlevels, out.data_ptr(), _s())
+    return out[:nlevels]
+
+
+def harmonic_peaks(P: torch.Tensor, nlevels: int, starts: Sequence[int], ends: Sequence[int], thresh: float,
+                   capacity: int = 1 << 20):
+    """Fused harmonic sum + threshold: P [K, n] -> records (trial, level, idx, snr)
+    as int64/float32 tensors sorted by (trial, level, idx)."""
+    _check(P, torch.float32, "P")
+    Kb, n = P.shape
+    rec = torch.empty((capacity, 3), dtype=torch.int32, device=P.device)
+    cnt = torch.zeros(1, dtype=torch.int32, device=P.device)
+    K.harmonic_peaks_batch(P.data_ptr(), n, n, Kb, nlevels, list(starts), list(ends), float(thresh), capacity,
+                           rec.data_ptr(), cnt.data_ptr(), _s())
+    c = int(cnt.item())
+    if c > capacity:
+        return harmonic_peaks(P, nlevels, starts, ends, thresh, capacity=c + 1024)
+    r = rec[:c]
+    seg = r[:, 0].to(torch.int64)
+    idx = r[:, 1].to(torch.int64)
+    snr = r[:, 2].view(torch.float32)
+    order = torch.argsort(seg * (1 << 32) + idx)
+    return seg[order] // 8, seg[order] % 8, idx[order], snr[order]
+
+
+# --------------------------------------------------------------- folding ----
+def fold_series(series: torch.Tensor, periods: Sequence[float], accels: Sequence[float], tsamp: float):
+    """Fold + optimise a whitened series for several (period, accel) pairs.
+    Returns native FoldResult objects (folded_snr, opt_period, fold[16*64], ...)."""
+    _check(series, torch.float32, "series")
+    fe = _C.FoldEngine(series.numel(), float(tsamp), _s())
+    return fe.fold_series(series.data_ptr(), [float(p) for p in periods], [float(a) for a in accels])
+
+
+def fold_optimise(folds: torch.Tensor):
+    """Fused fold optimiser on [nfold, 16, 64] folds -> (opt_int[nfold,3], opt_fold, opt_prof)."""
+    _check(folds, torch.float32, "folds")
+    nf = folds.shape[0]
+    dev = folds.device
+    table = torch.empty((64, 16, 64), dtype=torch.complex64, device=dev)
+    K.fold_shift_table(table.data_ptr(), 64, 16, _s())
+    of = torch.empty_like(folds)
+    op = torch.empty((nf, 64), dtype=torch.float32, device=dev)
+    oi = torch.empty((nf, 3), dtype=torch.int32, device=dev)
+    ov = torch.empty(nf, dtype=torch.float32, device=dev)
+    K.fold_optimise(folds.data_ptr(), nf, table.data_ptr(), of.data_ptr(), op.data_ptr(), oi.data_ptr(), ov.data_ptr(), _s())
+    return oi, of, op
+
+
+# ----------------------------------------------------------- coincidence ----
+def coincidence_counts(x: torch.Tensor, thresh: float, counts: Optional[torch.Tensor] = None) -> torch.Tensor:
+    _check(x, torch.float32, "x")
+    if counts is None:
+        counts = torch.zeros(x.numel(), dtype=torch.uint8, device=x.device)
+    K.count_above(x.data_ptr(), x.numel(), float(thresh), counts.data_ptr(), _s())
+    return counts
+
+
+def coincidence_mask(counts: torch.Tensor, beam_thresh: int) -> torch.Tensor:
+    _check(counts, torch.uint8, "counts")
+    mask = torch.empty(counts.numel(), dtype=torch.float32, device=counts.device)
+    K.coincidence_mask(counts.data_ptr(), counts.numel(), int(beam_thresh), mask.data_ptr(), _s())
+    return mask
+
+
+# ----------------------------------------------------------- correlation ----
+def conjugate(x: torch.Tensor) -> torch.Tensor:
+    K.conjugate(_cplx_ptr(x), x.numel(), _s())
+    return x
+
+
+def cmul_(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """y <- x * y (complex, in place)."""
+    K.cmul_inplace(_cplx_ptr(x), _cplx_ptr(y), y.numel(), _s())
+    return y

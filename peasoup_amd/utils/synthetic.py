@@ -4,7 +4,7 @@ Used by the tests and benchmarks (there is no network access to real data).
 The generator produces quantised Gaussian noise plus a dispersed periodic
 pulse train whose arrival times follow the same dispersion law the pipeline
 searches for (delay_c = 4.15e3 * DM * (1/f_c^2 - 1/f_1^2) s), optionally with
-a constant line-of-sight acceleration (phase = (t + a t^2/(2c)) / P).
+a constant line-of-sight acceleration (phase = (t - a t^2/(2c)) / P, a > 0 away).
 """
 from __future__ import annotations
 
@@ -55,7 +55,9 @@ def generate(nsamps: int, header: Dict, pulsars=(), seed: int = 0, chunk: int = 
         for p in pulsars:
             delay = 4.15e3 * p.dm * (1.0 / freqs ** 2 - 1.0 / fch1 ** 2)  # seconds
             te = t - delay[None, :]
-            ph = (te + p.accel * te * te / (2 * C_LIGHT)) / p.period + p.phase
+            # +ve acceleration = away from the observer (distiller.hpp:164):
+            # the apparent spin frequency drifts down
+            ph = (te - p.accel * te * te / (2 * C_LIGHT)) / p.period + p.phase
             ph = ph - np.floor(ph)
             d = np.minimum(ph, 1.0 - ph)
             w = p.duty / 2.3548

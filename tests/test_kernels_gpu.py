@@ -1,0 +1,262 @@
+"""HIP kernel numerics vs the NumPy float32 references (MI355X)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from peasoup_amd.utils import reference as ref
+from peasoup_amd.utils import sigproc, synthetic
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def test_single_hip_runtime_loaded():
+    import peasoup_amd  # noqa: F401
+
+    libs = {l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l}
+    assert len(libs) == 1, libs
+
+
+@pytest.mark.parametrize("nbits", [1, 2, 4, 8])
+def test_unpack_transpose(nbits):
+    from peasoup_amd import ops
+
+    rng = np.random.default_rng(nbits)
+    nsamps, nchans = 1000, 96 if nbits != 1 else 64
+    vals = rng.integers(0, 1 << nbits, size=(nsamps, nchans), dtype=np.uint8)
+    packed = torch.from_numpy(sigproc.pack_samples(vals, nbits)).to(dev)
+    bias = 128 if nbits == 8 else 0
+    out = ops.unpack_transpose(packed, nsamps, nchans, nbits, bias=bias, stride=1024)
+    exp = (vals.T.astype(np.int16) - bias).astype(np.int8)
+    assert np.array_equal(out[:, :nsamps].cpu().numpy(), exp)
+
+
+def _geometry(C, nchans=64, nbits=2, nsamps=6000, dm_end=200.0, tsamp=0.00032, fch1=1510.0, foff=-1.09):
+    hdr = synthetic.make_header(nchans=nchans, nbits=nbits, tsamp=tsamp, fch1=fch1, foff=foff, nsamples=nsamps)
+    dms = C.generate_dm_list(0.0, dm_end, tsamp, 64.0, fch1, foff, nchans, 1.1)
+    return hdr, dms
+
+
+@pytest.mark.parametrize("nbits,nchans,kill", [(2, 64, False), (8, 128, True), (4, 64, True)])
+def test_dedisperse_direct_and_mfma_bit_exact(C, nbits, nchans, kill):
+    rng = np.random.default_rng(7)
+    hdr, dms = _geometry(C, nchans=nchans, nbits=nbits, nsamps=5000, dm_end=150.0)
+    vals = rng.integers(0, 1 << nbits, size=(5000, nchans), dtype=np.uint8)
+    killmask = [int(rng.random() > 0.2) for _ in range(nchans)] if kill else []
+    g = C.DedispGeometry.make(hdr, 5000, dms, killmask)
+    s = torch.cuda.current_stream().cuda_stream
+    dfb = C.DeviceFilterbank(g, s)
+    packed = torch.from_numpy(sigproc.pack_samples(vals, nbits)).to(dev)
+    dfb.load_packed_device(packed.data_ptr())
+    dd = C.Dedisperser(dfb, s)
+    ndm = len(dms)
+    stride = C.Dedisperser.row_stride(g.out_nsamps)
+    outs = {}
+    for k in (C.DedispKernel.Direct, C.DedispKernel.Mfma):
+        o = torch.zeros(ndm * stride, dtype=torch.uint8, device=dev)
+        dd.run(0, ndm, o.data_ptr(), stride, k)
+        outs[k] = o.view(ndm, stride)[:, : g.out_nsamps].cpu().numpy()
+    offs = np.array(g.offsets(0, ndm), dtype=np.int32).reshape(ndm, nchans)
+    exp = ref.dedisperse(vals, offs, nbits, killmask or None, g.out_nsamps)
+    assert np.array_equal(outs[C.DedispKernel.Direct], exp)
+    assert np.array_equal(outs[C.DedispKernel.Mfma], exp)
+    # sub-range (DM offset inside a tile)
+    o = torch.zeros(5 * stride, dtype=torch.uint8, device=dev)
+    dd.run(3, 8, o.data_ptr(), stride, C.DedispKernel.Mfma)
+    assert np.array_equal(o.view(5, stride)[:, : g.out_nsamps].cpu().numpy(), exp[3:8])
+
+
+def test_convert_pad_and_truncate():
+    from peasoup_amd import ops
+
+    u = torch.randint(0, 256, (1000,), dtype=torch.uint8, device=dev)
+    x = ops.convert_pad(u, 1536)
+    exp = ref.convert_pad(u.cpu().numpy(), 1536)
+    assert np.allclose(x.cpu().numpy(), exp)
+    x = ops.convert_pad(u, 512)
+    assert np.array_equal(x.cpu().numpy(), u[:512].cpu().numpy().astype(np.float32))
+
+
+def test_spectrum_forms_and_running_median():
+    from peasoup_amd import ops
+
+    rng = np.random.default_rng(3)
+    n = 1 << 16
+    x = rng.standard_normal(n).astype(np.float32) + np.linspace(0, 5, n, dtype=np.float32)
+    X = ops.rfft(torch.from_numpy(x).to(dev))
+    Xn = X.cpu().numpy()
+    assert np.allclose(Xn, np.fft.rfft(x.astype(np.float64)), rtol=1e-4, atol=1e-2)
+    assert np.allclose(ops.form_amplitude(X).cpu().numpy(), ref.amplitude(Xn), rtol=1e-5, atol=1e-5)
+    assert np.allclose(ops.form_interbin(X).cpu().numpy(), ref.interbin(Xn), rtol=1e-5, atol=1e-5)
+    m5, m25, m125 = ops.running_median(X)
+    amp = ref.amplitude(Xn)
+    assert np.allclose(m5.cpu().numpy(), ref.median_scrunch5(amp), rtol=1e-6)
+    assert np.allclose(m25.cpu().numpy(), ref.median_scrunch5(ref.median_scrunch5(amp)), rtol=1e-6)
+    bw = float(np.float32(1.0 / np.float32(n * np.float32(0.00032))))
+    zm = ref.zap_mask([10.0, 50.0], [0.3, 0.5], bw, len(Xn))
+    bits = np.zeros((len(Xn) + 31) // 32, np.uint32)
+    for k in np.nonzero(zm)[0]:
+        bits[k >> 5] |= np.uint32(1 << (k & 31))
+    zt = torch.from_numpy(bits.view(np.int32)).to(dev)
+    Xd = ops.deredden(X.clone(), bw, zt).cpu().numpy()
+    exp = ref.deredden(Xn, ref.running_median(amp, bw), zm)
+    assert np.allclose(Xd, exp, rtol=2e-5, atol=1e-6)
+    import peasoup_amd._C as C
+
+    assert np.array_equal(np.array(C.build_zap_mask([10.0, 50.0], [0.3, 0.5], bw, len(Xn)), dtype=np.uint32), bits)
+    P, st = ops.interbin_stats(torch.from_numpy(exp).to(dev))
+    mean, rms, std = ref.stats(ref.interbin(exp))
+    assert st[0].item() == pytest.approx(mean, rel=1e-5) and st[2].item() == pytest.approx(std, rel=1e-4)
+
+
+def test_whitening_engine_matches_reference(C):
+    """Whitener path of SearchEngine (convert/pad, R2C, median, deredden, zap, C2R)."""
+    rng = np.random.default_rng(11)
+    nsamps, n = 100000, 1 << 17
+    trial = rng.integers(60, 200, size=nsamps, dtype=np.uint8)
+    p = C.SearchParams()
+    p.fft_size, p.tsamp = n, 0.00032
+    p.zap_freqs, p.zap_widths = [50.0], [0.15]
+    s = torch.cuda.current_stream().cuda_stream
+    eng = C.SearchEngine(p, s)
+    t = torch.from_numpy(trial).to(dev)
+    eng.search_trial(t.data_ptr(), nsamps, 0.0, 0, [0.0])
+    torch.cuda.synchronize()
+    w = torch.empty(n, dtype=torch.float32, device=dev)
+    stt = torch.empty(3, dtype=torch.float32, device=dev)
+    eng.copy_whitened(w.data_ptr())
+    eng.copy_stats(stt.data_ptr())
+    bw = float(np.float32(1.0 / np.float32(np.float32(n) * np.float32(0.00032))))
+    zm = ref.zap_mask([50.0], [0.15], bw, n // 2 + 1)
+    exp, st = ref.whiten(trial, n, 0.00032, zm)
+    got = w.cpu().numpy()
+    scale = np.abs(exp).max()
+    assert np.abs(got - exp).max() / scale < 2e-5
+    assert stt[0].item() == pytest.approx(st[0], rel=1e-4) and stt[2].item() == pytest.approx(st[2], rel=1e-3)
+
+
+def test_resample_batch_and_v1():
+    from peasoup_amd import ops
+
+    n = 1 << 18
+    x = torch.arange(n, dtype=torch.float32, device=dev) % 451  # resampling_test.cpp sawtooth
+    accs = [-500.0, -125.5, 0.0, 125.5, 499.0]
+    tsamp = 64e-6
+    out = ops.resample(x, accs, tsamp).cpu().numpy()
+    xn = x.cpu().numpy()
+    for k, a in enumerate(accs):
+        exp = ref.resample_ii(xn, ref.accel_factor(a, tsamp))
+        assert np.array_equal(out[k], exp), a
+    v1 = ops.resample_v1(x, 125.5, tsamp).cpu().numpy()
+    assert np.array_equal(v1, ref.resample_v1(xn, ref.accel_factor(125.5, tsamp)))
+    # resample (II) and v1 agree up to index rounding ties (reference resampling_test.cpp)
+    ii = ref.resample_ii(xn, ref.accel_factor(125.5, tsamp))
+    assert np.mean(ii != v1) < 1e-3
+
+
+@pytest.mark.parametrize("nlevels", [1, 2, 3, 4, 5])
+def test_harmonic_sums_exact(nlevels):
+    from peasoup_amd import ops
+
+    rng = np.random.default_rng(nlevels)
+    P = rng.standard_normal(200003).astype(np.float32)
+    got = ops.harmonic_sums(torch.from_numpy(P).to(dev), nlevels).cpu().numpy()
+    exp = ref.harmonic_sums(P, nlevels)
+    for h in range(nlevels):
+        assert np.array_equal(got[h], exp[h]), h
+
+
+def test_harmonic_peaks_matches_threshold_of_sums():
+    from peasoup_amd import ops
+
+    rng = np.random.default_rng(2)
+    n, Kb, nlev = 120001, 3, 4
+    P = rng.standard_normal((Kb, n)).astype(np.float32) * 2.5
+    starts = [17, 30, 60, 120, 240]
+    ends = [n - 5, n - 100, n, n, n - 1]
+    trial, level, idx, snr = ops.harmonic_peaks(torch.from_numpy(P).to(dev), nlev, starts, ends, 9.0)
+    got = set(zip(trial.tolist(), level.tolist(), idx.tolist()))
+    exp = set()
+    for k in range(Kb):
+        levels = [P[k]] + ref.harmonic_sums(P[k], nlev)
+        for h, L in enumerate(levels):
+            sel = np.nonzero(L[starts[h]:ends[h]] > 9.0)[0] + starts[h]
+            exp |= {(k, h, int(i)) for i in sel}
+    assert got == exp and len(exp) > 50
+
+
+def test_interbin_normalise_batch():
+    from peasoup_amd import ops
+
+    rng = np.random.default_rng(4)
+    X = (rng.standard_normal((3, 5001)) + 1j * rng.standard_normal((3, 5001))).astype(np.complex64)
+    st = torch.tensor([1.5, 2.0, 0.75, 0.0], dtype=torch.float32, device=dev)
+    P = ops.interbin_normalise(torch.from_numpy(X).to(dev), st, 16.0).cpu().numpy()
+    mean, sd = np.float32(1.5) * np.float32(16.0), np.float32(0.75) * np.float32(16.0)
+    for k in range(3):
+        assert np.allclose(P[k], (ref.interbin(X[k]) - mean) / sd, rtol=1e-6, atol=1e-6)
+
+
+def test_fold_optimise_matches_fft_reference():
+    from peasoup_amd import ops
+
+    rng = np.random.default_rng(9)
+    folds = rng.standard_normal((6, 16, 64)).astype(np.float32)
+    # add a drifting narrow pulse to some folds
+    for f in range(3):
+        for i in range(16):
+            folds[f, i, (20 + (i * (f + 1)) // 4) % 64] += 8.0
+    oi, of, op = ops.fold_optimise(torch.from_numpy(folds).to(dev))
+    oi, of, op = oi.cpu().numpy(), of.cpu().numpy(), op.cpu().numpy()
+    for f in range(6):
+        t, s, j, ofold, oprof = ref.fold_optimise(folds[f])
+        if f < 3:
+            assert (oi[f, 0], oi[f, 1], oi[f, 2]) == (t, s, j)
+            assert np.allclose(of[f], ofold, rtol=1e-3, atol=1e-2)
+            assert np.allclose(op[f], oprof, rtol=1e-3, atol=1e-2)
+
+
+def test_fold_series_against_reference(C):
+    from peasoup_amd import ops
+
+    n, tsamp, period = 1 << 18, 0.00032, 0.2513
+    t = np.arange(n) * tsamp
+    ph = (t / period) % 1.0
+    x = (np.exp(-0.5 * ((ph - 0.3) / 0.02) ** 2) * 5 + np.random.default_rng(1).standard_normal(n)).astype(np.float32)
+    res = ops.fold_series(torch.from_numpy(x).to(dev), [period], [0.0], tsamp)[0]
+    fold_ref = ref.fold_series(x, period, float(np.float32(tsamp)))  # the folder's tsamp is float32
+    t_, s_, j_, ofold, oprof = ref.fold_optimise(fold_ref)
+    assert res.opt_width == t_ + 1
+    sn1, sn2 = ref.calculate_sn(oprof, j_ - t_ // 2, t_)
+    # float32 fold sums in a different order than the double-precision oracle
+    assert res.folded_snr == pytest.approx(max(sn1, sn2), rel=1e-2)
+    assert np.allclose(np.array(res.fold).reshape(16, 64), ofold, rtol=2e-3, atol=2e-2)
+
+
+def test_calculate_sn_host(C):
+    rng = np.random.default_rng(6)
+    prof = rng.standard_normal(64).astype(np.float32)
+    prof[40:44] += 10
+    for b, w in ((41, 3), (5, 7), (60, 1)):
+        a, c = C.fold_calculate_sn(list(prof), b, w)
+        ea, ec = ref.calculate_sn(prof, b, w)
+        assert a == pytest.approx(ea, rel=1e-5) and c == pytest.approx(ec, rel=1e-5)
+
+
+def test_coincidence_and_correlation_ops():
+    from peasoup_amd import ops
+
+    rng = np.random.default_rng(8)
+    beams = [rng.standard_normal(10000).astype(np.float32) * 3 for _ in range(5)]
+    counts = None
+    for b in beams:
+        counts = ops.coincidence_counts(torch.from_numpy(b).to(dev), 4.0, counts)
+    mask = ops.coincidence_mask(counts, 2).cpu().numpy()
+    assert np.array_equal(mask, ref.coincidence_mask(beams, 4.0, 2))
+    x = torch.from_numpy((rng.standard_normal(999) + 1j * rng.standard_normal(999)).astype(np.complex64)).to(dev)
+    y = torch.from_numpy((rng.standard_normal(999) + 1j * rng.standard_normal(999)).astype(np.complex64)).to(dev)
+    exp = np.conj(x.cpu().numpy()) * y.cpu().numpy()
+    ops.cmul_(ops.conjugate(x), y)
+    assert np.allclose(y.cpu().numpy(), exp, rtol=1e-5, atol=1e-5)

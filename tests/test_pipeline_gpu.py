@@ -1,0 +1,113 @@
+"""End-to-end pipeline on MI355X: golden tutorial.fil parity, injected
+accelerated pulsars, checkpoint/resume and fault propagation."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN_XML, REPO, TUTORIAL
+from peasoup_amd.utils.outputs import CandidateFileParser, OverviewFile, PeasoupOutput
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN_ARGS = ["--dm_end", "250", "--acc_start", "-5", "--acc_end", "5", "-n", "4", "--npdmp", "10"]
+
+
+def _compare_with_golden(out_dir):
+    g = OverviewFile(GOLDEN_XML)
+    o = OverviewFile(os.path.join(out_dir, "overview.xml"))
+    assert o.dm_list == g.dm_list
+    assert o.acc_list == g.acc_list
+    for i in range(len(g)):
+        gc, oc = g.get_candidate(i), o.get_candidate(i)
+        assert oc["period"] == pytest.approx(gc["period"], rel=1e-7), i
+        assert oc["opt_period"] == pytest.approx(gc["opt_period"], rel=1e-6), i
+        assert oc["dm"] == pytest.approx(gc["dm"], rel=1e-7), i
+        assert oc["nh"] == gc["nh"], i
+        assert oc["snr"] == pytest.approx(gc["snr"], rel=1e-5), i
+        assert oc["folded_snr"] == pytest.approx(gc["folded_snr"], rel=2e-2), i
+        assert oc["nassoc"] == gc["nassoc"], i
+        assert oc["byte_offset"] == gc["byte_offset"], i
+        assert (oc["is_adjacent"], oc["is_physical"]) == (gc["is_adjacent"], gc["is_physical"]), i
+    # 0 and +-5 m/s^2 resample bit-identically at 2^17 x 320 us (max shift
+    # 0.01 sample), so the credited acceleration of these exact S/N ties is an
+    # artefact of sort order (the golden run used 2 GPU threads, so its
+    # concatenation order was timing dependent): only the plan values are checked.
+    assert all(o.get_candidate(i)["acc"] in (0.0, -5.0, 5.0) for i in range(len(g)))
+    recs = CandidateFileParser(os.path.join(out_dir, "candidates.peasoup")).records()
+    assert all(r[1] is not None and r[1].shape == (16, 64) for r in recs[:10])
+
+
+def test_cli_golden_tutorial(tmp_path):
+    exe = os.path.join(REPO, "bin", "peasoup")
+    r = subprocess.run([exe, "-i", TUTORIAL, "-o", str(tmp_path)] + GOLDEN_ARGS, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr
+    _compare_with_golden(str(tmp_path))
+    o = OverviewFile(os.path.join(str(tmp_path), "overview.xml"))
+    assert set(o.execution_times) == {"dedispersion", "folding", "reading", "searching", "total"}
+
+
+def test_python_run_search_golden(C, tmp_path):
+    from peasoup_amd.models.search import run_search
+
+    ok, _, args = C.parse_cmdline(["peasoup", "-i", TUTORIAL, "-o", str(tmp_path)] + GOLDEN_ARGS)
+    res = run_search(args)
+    assert res is not None and res.accel_trials == 59 * 3
+    _compare_with_golden(str(tmp_path))
+
+
+def test_direct_and_mfma_dedispersion_give_identical_search(C, tmp_path):
+    outs = []
+    for k in ("direct", "mfma"):
+        d = tmp_path / k
+        r = subprocess.run([os.path.join(REPO, "bin", "peasoup"), "-i", TUTORIAL, "-o", str(d), "--dedisp_kernel", k,
+                            "--dm_end", "100", "-n", "3"], capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr
+        outs.append(open(d / "candidates.peasoup", "rb").read())
+    assert outs[0] == outs[1]
+
+
+def test_checkpoint_resume_and_fault_injection(tmp_path):
+    exe = os.path.join(REPO, "bin", "peasoup")
+    ck = tmp_path / "ck"
+    base = [exe, "-i", TUTORIAL, "--dm_end", "250", "-n", "4", "--checkpoint_dir", str(ck)]
+    r = subprocess.run(base + ["-o", str(tmp_path / "a"), "--fault_after_dms", "20"], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode != 0 and "fault injection" in r.stderr
+    done = list(ck.glob("*.psoc"))
+    assert 0 < len(done)
+    r = subprocess.run(base + ["-o", str(tmp_path / "b")], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr
+    r2 = subprocess.run([exe, "-i", TUTORIAL, "--dm_end", "250", "-n", "4", "-o", str(tmp_path / "c")],
+                        capture_output=True, text=True, timeout=600)
+    assert r2.returncode == 0
+    assert open(tmp_path / "b" / "candidates.peasoup", "rb").read() == open(tmp_path / "c" / "candidates.peasoup",
+                                                                            "rb").read()
+
+
+def test_injected_accelerated_pulsar_is_found(C, tmp_path):
+    """A binary pulsar (a = 60 m/s^2) in synthetic noise is recovered at the
+    right DM/acceleration and beats its zero-acceleration detection."""
+    from peasoup_amd.models.search import run_search
+    from peasoup_amd.utils import synthetic
+
+    hdr = synthetic.make_header(nchans=64, nbits=2, tsamp=256e-6, fch1=1400.0, foff=-2.0)
+    nsamps = (1 << 20) + 2000
+    psr = synthetic.PulsarSpec(period=0.0123, dm=40.0, duty=0.08, amplitude=0.08, accel=60.0)
+    fil = str(tmp_path / "psr.fil")
+    synthetic.write(fil, nsamps, hdr, [psr], seed=3)
+    ok, _, args = C.parse_cmdline(["peasoup", "-i", fil, "-o", str(tmp_path / "out"), "--dm_start", "30",
+                                   "--dm_end", "50", "--acc_start", "-100", "--acc_end", "100", "-n", "3",
+                                   "--npdmp", "3", "--fft_size", str(1 << 20)])
+    res = run_search(args)
+    best = res.candidates[0]
+    f0 = 1.0 / psr.period
+    ratio = best.freq / f0
+    assert min(abs(ratio - h) for h in (0.5, 1.0, 2.0)) < 2e-3, (best.freq, f0)
+    assert abs(best.dm - 40.0) < 6.0
+    assert abs(best.acc - 60.0) < 25.0
+    assert best.folded_snr > 8.0
