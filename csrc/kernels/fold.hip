@@ -33,16 +33,16 @@ __global__ void __launch_bounds__(256) fold_accumulate_kernel(const float* __res
                                                               int nints, int chunk, int nchunk,
                                                               float* __restrict__ psum,
                                                               int32_t* __restrict__ pcount) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* lsum = reinterpret_cast<float*>(smem);
-  int* lcnt = reinterpret_cast<int*>(smem + sizeof(float) * nbins);
+  // Deterministic accumulation: every thread owns one float slot per bin
+  // (slot[bin][thread]); a fixed-order reduction follows.  Float LDS
+  // atomics would make folds (and the folded S/N) vary run to run.
+  __shared__ float slot[kNb * 256];
+  __shared__ int lcnt[kNb];
   const int job = blockIdx.z;
   const int subint = blockIdx.y;
   const int ch = blockIdx.x;
-  for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
-    lsum[b] = 0.f;
-    lcnt[b] = 0;
-  }
+  for (int b = 0; b < nbins; ++b) slot[b * 256 + threadIdx.x] = 0.f;
+  for (int b = threadIdx.x; b < nbins; b += blockDim.x) lcnt[b] = 0;
   __syncthreads();
   const FoldJob J = jobs[job];
   const uint64_t nps = n / nints;
@@ -68,7 +68,7 @@ __global__ void __launch_bounds__(256) fold_accumulate_kernel(const float* __res
     float v = in[src];
     if (b != cur) {
       if (cur >= 0) {
-        atomicAdd(&lsum[cur], rs);
+        slot[cur * 256 + threadIdx.x] += rs;
         atomicAdd(&lcnt[cur], rc);
       }
       cur = b;
@@ -79,13 +79,20 @@ __global__ void __launch_bounds__(256) fold_accumulate_kernel(const float* __res
     rc++;
   }
   if (cur >= 0) {
-    atomicAdd(&lsum[cur], rs);
+    slot[cur * 256 + threadIdx.x] += rs;
     atomicAdd(&lcnt[cur], rc);
   }
   __syncthreads();
+  // 4 threads per bin, 64 slots each, then a fixed-order combine
+  const int b = threadIdx.x >> 2, q = threadIdx.x & 3;
+  float s = 0.f;
+  if (b < nbins)
+    for (int k = 0; k < 64; ++k) s += slot[b * 256 + q * 64 + k];
+  s += __shfl_xor(s, 1, 64);
+  s += __shfl_xor(s, 2, 64);
   const uint64_t o = ((static_cast<uint64_t>(job) * nints + subint) * nchunk + ch) * nbins;
-  for (int b = threadIdx.x; b < nbins; b += blockDim.x) {
-    psum[o + b] = lsum[b];
+  if (b < nbins && q == 0) {
+    psum[o + b] = s;
     pcount[o + b] = lcnt[b];
   }
 }
@@ -261,8 +268,8 @@ void fold_accumulate(const float* in, uint64_t n, const FoldJob* jobs, int njobs
   const uint64_t nps = n / nints;
   const int nchunk = static_cast<int>((nps + chunk - 1) / chunk);
   dim3 grid(static_cast<unsigned>(nchunk), static_cast<unsigned>(nints), static_cast<unsigned>(njobs));
-  size_t lds = (sizeof(float) + sizeof(int)) * static_cast<size_t>(nbins);
-  fold_accumulate_kernel<<<grid, 256, lds, s>>>(in, n, jobs, nbins, nints, chunk, nchunk, psum, pcount);
+  PSOUP_CHECK(nbins >= 1 && nbins <= kNb, "fold_accumulate supports up to 64 bins");
+  fold_accumulate_kernel<<<grid, 256, 0, s>>>(in, n, jobs, nbins, nints, chunk, nchunk, psum, pcount);
   post_launch_check("fold_accumulate_kernel", s);
 }
 

@@ -126,7 +126,13 @@ def broadcast_bytes(buf: Optional[torch.Tensor], nbytes: int, src: int = 0) -> t
     piece = 1 << 30
     flat = buf.view(-1)
     for off in range(0, nbytes, piece):
-        dist.broadcast(flat[off:min(nbytes, off + piece)], src=src)
+        part = flat[off:min(nbytes, off + piece)]
+        if part.is_cuda and ctx.backend != "nccl":  # gloo: stage through host memory
+            h = part.cpu()
+            dist.broadcast(h, src=src)
+            part.copy_(h)
+        else:
+            dist.broadcast(part, src=src)
     return buf
 
 
