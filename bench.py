@@ -45,6 +45,7 @@ def parse():
     p.add_argument("--acc", type=float, default=500.0, help="search +-acc m/s^2")
     p.add_argument("--nharmonics", type=int, default=3)
     p.add_argument("--accel-batch", type=int, default=0)
+    p.add_argument("--fft-mode", type=int, default=1, help="0: rocFFT R2C; 1: C2C(N/2) + fused r2c post")
     p.add_argument("--dedisp-kernel", default="mfma", choices=["mfma", "direct"])
     p.add_argument("--seed", type=int, default=1234)
     return p.parse_args()
@@ -99,7 +100,7 @@ def main() -> int:
         g.manual_seed(a.seed)
         packed.random_(0, 256, generator=g)  # every 2-bit field uniform on {0..3}
     pdist.broadcast_bytes(packed, nbytes)
-    rs = RankSearcher(args, header, packed, nsamps)
+    rs = RankSearcher(args, header, packed, nsamps, fft_mode=a.fft_mode)
     del packed
     torch.cuda.empty_cache()
 

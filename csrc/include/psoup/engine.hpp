@@ -100,6 +100,10 @@ struct SearchParams {
   int accel_batch = 0;          // 0 = auto
   size_t batch_bytes = 3ull << 30;  // auto-batch HBM budget
   int min_gap = 30;
+  // Acceleration-trial FFT path: 0 = rocFFT R2C of N points; 1 = rocFFT C2C
+  // of N/2 points with the real-FFT post-processing fused into the interbin
+  // kernel (default, N even).
+  int fft_mode = 1;
 };
 
 // Running-median whitening of one N-point series, in place.
@@ -186,6 +190,7 @@ class SearchEngine {
   DeviceBuffer<float> tim_;
   DeviceBuffer<uint32_t> zapmask_;
   bool zap_ = false;
+  bool c2c_ = true;
   DeviceBuffer<float> res_;
   DeviceBuffer<float2> spec_;
   DeviceBuffer<float> P_;

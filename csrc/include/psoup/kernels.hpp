@@ -109,6 +109,11 @@ void resample_v1(const float* in, uint64_t n, float* out, double af, hipStream_t
 void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride, float* P, uint64_t pstride,
                               int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s);
 
+// Same output from the M = N/2 point complex FFT Z[K][M] of the packed real
+// series (real-FFT post-processing fused in; saves the separate r2c pass).
+void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride, float* P, uint64_t pstride, int K,
+                                  uint64_t nbins_out, const float* stats, float nscale, hipStream_t s);
+
 struct HarmParams {
   int nlevels;             // number of harmonic-sum levels (0..5)
   int start[6];            // per level search range [start, end)

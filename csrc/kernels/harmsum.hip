@@ -44,6 +44,46 @@ __global__ void __launch_bounds__(256) interbin_normalise_batch_kernel(const flo
   }
 }
 
+// Real-input FFT recovered from an M = N/2 point complex FFT of the packed
+// series z[m] = x[2m] + i x[2m+1]:
+//   X[k] = (Z[k] + conj Z[M-k])/2 - i/2 e^{-2 pi i k/N} (Z[k] - conj Z[M-k]),  k = 0..M
+// (indices mod M).  Replaces rocFFT's separate r2c post-processing pass.
+__device__ __forceinline__ float2 r2c_bin(const float2* __restrict__ z, uint64_t M, uint64_t k) {
+  const uint64_t a = (k == M) ? 0 : k;
+  const uint64_t b = (k == 0) ? 0 : M - k;
+  const float2 za = z[a], zb = z[b];
+  const float ex = 0.5f * (za.x + zb.x), ey = 0.5f * (za.y - zb.y);
+  const float dx = 0.5f * (za.x - zb.x), dy = 0.5f * (za.y + zb.y);
+  const float ox = dy, oy = -dx;  // -i * d
+  float s, c;
+  sincospif(-static_cast<float>(k) / static_cast<float>(M), &s, &c);
+  return make_float2(ex + c * ox - s * oy, ey + c * oy + s * ox);
+}
+
+__global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
+    const float2* __restrict__ Z, uint64_t M, uint64_t zstride, float* __restrict__ P, uint64_t pstride,
+    uint64_t nbins_out, const float* __restrict__ stats, float nscale) {
+  __shared__ float2 X[257];
+  const int kk = blockIdx.y;
+  const float2* z = Z + static_cast<uint64_t>(kk) * zstride;
+  float* p = P + static_cast<uint64_t>(kk) * pstride;
+  const float mean = stats[0] * nscale;
+  const float sigma = stats[2] * nscale;
+  for (uint64_t k0 = static_cast<uint64_t>(blockIdx.x) * 256; k0 < nbins_out; k0 += static_cast<uint64_t>(gridDim.x) * 256) {
+    const uint64_t k = k0 + threadIdx.x;
+    X[threadIdx.x + 1] = (k <= M) ? r2c_bin(z, M, k) : make_float2(0.f, 0.f);
+    if (threadIdx.x == 0) X[0] = (k0 > 0) ? r2c_bin(z, M, k0 - 1) : make_float2(0.f, 0.f);
+    __syncthreads();
+    if (k < nbins_out) {
+      float v = dev::interbin(X[threadIdx.x + 1], X[threadIdx.x]);
+      v -= mean;
+      v /= sigma;
+      p[k] = v;
+    }
+    __syncthreads();
+  }
+}
+
 __device__ __forceinline__ void emit(bool pred, uint32_t seg, int idx, float snr, PeakRecord* __restrict__ out,
                                      uint32_t* __restrict__ count, uint32_t capacity) {
   const unsigned long long mask = __ballot(pred);
@@ -146,6 +186,16 @@ void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride,
   dim3 grid(dev::grid_for(nbins_out, 256, 1024), static_cast<unsigned>(K));
   interbin_normalise_batch_kernel<<<grid, 256, 0, s>>>(X, xstride, P, pstride, nbins_out, stats, nscale);
   post_launch_check("interbin_normalise_batch_kernel", s);
+}
+
+void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride, float* P, uint64_t pstride, int K,
+                                  uint64_t nbins_out, const float* stats, float nscale, hipStream_t s) {
+  PSOUP_CHECK(K >= 1 && K <= 65535, "bad batch");
+  PSOUP_CHECK(nbins_out <= M + 1, "nbins_out beyond the spectrum");
+  if (nbins_out == 0) return;
+  dim3 grid(dev::grid_for(nbins_out, 256, 1024), static_cast<unsigned>(K));
+  r2c_interbin_normalise_batch_kernel<<<grid, 256, 0, s>>>(Z, M, zstride, P, pstride, nbins_out, stats, nscale);
+  post_launch_check("r2c_interbin_normalise_batch_kernel", s);
 }
 
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,

@@ -422,6 +422,12 @@ PYBIND11_MODULE(_C, m) {
     kern::interbin_normalise_batch(P<const float2>(X), nb, xstride, P<float>(Pout), pstride, K, nbo,
                                    P<const float>(stats), nscale, S(s));
   });
+  k.def("r2c_interbin_normalise_batch", [](uintptr_t Z, uint64_t M, uint64_t zstride, uintptr_t Pout,
+                                           uint64_t pstride, int K, uint64_t nbo, uintptr_t stats, float nscale,
+                                           uintptr_t s) {
+    kern::r2c_interbin_normalise_batch(P<const float2>(Z), M, zstride, P<float>(Pout), pstride, K, nbo,
+                                       P<const float>(stats), nscale, S(s));
+  });
   k.def("harmonic_peaks_batch", [](uintptr_t Pin, uint64_t nb, uint64_t pstride, int K, int nlevels,
                                    const std::vector<int>& start, const std::vector<int>& end, float thresh,
                                    uint32_t capacity, uintptr_t out, uintptr_t count, uintptr_t s) {
@@ -522,7 +528,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("zap_widths", &SearchParams::zap_widths)
       .def_readwrite("accel_batch", &SearchParams::accel_batch)
       .def_readwrite("batch_bytes", &SearchParams::batch_bytes)
-      .def_readwrite("min_gap", &SearchParams::min_gap);
+      .def_readwrite("min_gap", &SearchParams::min_gap)
+      .def_readwrite("fft_mode", &SearchParams::fft_mode);
   py::class_<SearchEngine>(m, "SearchEngine")
       .def(py::init([](const SearchParams& p, uintptr_t s) { return new SearchEngine(p, S(s)); }))
       .def("search_trial", [](SearchEngine& e, uintptr_t trial, uint64_t nsamps, float dm, int dm_idx,

@@ -211,6 +211,7 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     log_info("warning: nharmonics > 5 is capped at 5 (32 harmonics), as the reference kernel only writes 5 levels");
   wh_ = std::make_unique<Whitener>(n_, p_.tsamp, stream_);
   tim_.resize(n_);
+  c2c_ = (p_.fft_mode == 1) && (n_ % 2 == 0);
   if (!p_.zap_freqs.empty()) {
     auto mask = build_zap_mask(p_.zap_freqs, p_.zap_widths, bin_width_, nb_);
     zapmask_.resize(mask.size());
@@ -275,7 +276,11 @@ void SearchEngine::ensure_batch_buffers() {
 FftPlan& SearchEngine::batch_plan(int count) {
   auto it = plans_.find(count);
   if (it != plans_.end()) return *it->second;
-  auto plan = std::make_unique<FftPlan>(FftType::R2C, n_, static_cast<uint64_t>(count), n_, nb_);
+  std::unique_ptr<FftPlan> plan;
+  if (c2c_)  // N/2-point complex FFT of the packed real series (post-processing fused downstream)
+    plan = std::make_unique<FftPlan>(FftType::C2C_FWD, n_ / 2, static_cast<uint64_t>(count), n_ / 2, nb_);
+  else
+    plan = std::make_unique<FftPlan>(FftType::R2C, n_, static_cast<uint64_t>(count), n_, nb_);
   FftPlan& ref = *plan;
   plans_[count] = std::move(plan);
   return ref;
@@ -287,8 +292,12 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
   kern::resample_batch(tim_.data(), n_, res_.data(), n_, af_.data() + first, count, stream_);
   batch_plan(count).execute(res_.data(), spec_.data(), stream_);
   const uint64_t pst = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
-  kern::interbin_normalise_batch(spec_.data(), nb_, nb_, P_.data(), pst, count, static_cast<uint64_t>(hi_),
-                                 wh_->stats(), static_cast<float>(n_), stream_);
+  if (c2c_)
+    kern::r2c_interbin_normalise_batch(spec_.data(), n_ / 2, nb_, P_.data(), pst, count, static_cast<uint64_t>(hi_),
+                                       wh_->stats(), static_cast<float>(n_), stream_);
+  else
+    kern::interbin_normalise_batch(spec_.data(), nb_, nb_, P_.data(), pst, count, static_cast<uint64_t>(hi_),
+                                   wh_->stats(), static_cast<float>(n_), stream_);
   PSOUP_HIP_CHECK(hipMemsetAsync(s.d_count.data(), 0, sizeof(uint32_t), stream_));
   {
     RoctxRange r("Harmonic summing");

@@ -57,7 +57,7 @@ class RankSearcher:
     """Per-rank search state: resident filterbank, dedisperser, engine."""
 
     def __init__(self, args, header: dict, packed: Optional[torch.Tensor], nsamps: int,
-                 killmask: Optional[Sequence[int]] = None):
+                 killmask: Optional[Sequence[int]] = None, fft_mode: Optional[int] = None):
         self.ctx = pdist.context()
         self.args = args
         self.header = dict(header)
@@ -65,6 +65,8 @@ class RankSearcher:
         params, dm_list, kill, fft_size, cfreq = _C.search_params_from_args(args, self.header)
         if killmask is not None:
             kill = list(killmask)
+        if fft_mode is not None:
+            params.fft_mode = int(fft_mode)
         self.params = params
         self.dm_list = list(dm_list)
         self.fft_size = int(fft_size)

@@ -25,6 +25,7 @@ from .core import (  # noqa: F401
     irfft,
     median_scrunch5,
     normalise,
+    r2c_interbin_normalise,
     resample,
     resample_v1,
     rfft,

@@ -181,6 +181,23 @@ def interbin_normalise(X: torch.Tensor, stats: torch.Tensor, nscale: float, nbin
     return P
 
 
+def r2c_interbin_normalise(x: torch.Tensor, stats: torch.Tensor, nscale: float,
+                           nbins_out: Optional[int] = None) -> torch.Tensor:
+    """Batched real series x [K, N] (N even) -> same output as
+    ``interbin_normalise(rfft(x))`` but via an N/2-point complex FFT of the
+    packed series with the real-FFT post-processing fused into the kernel."""
+    _check(x, torch.float32, "x")
+    Kb, n = x.shape
+    assert n % 2 == 0
+    M = n // 2
+    Z = torch.fft.fft(torch.view_as_complex(x.contiguous().view(Kb, M, 2)), dim=-1).contiguous()
+    nbo = nbins_out or (M + 1)
+    P = torch.empty((Kb, nbo), dtype=torch.float32, device=x.device)
+    K.r2c_interbin_normalise_batch(_cplx_ptr(Z), M, M, P.data_ptr(), nbo, Kb, nbo, stats.data_ptr(),
+                                   float(nscale), _s())
+    return P
+
+
 # ---------------------------------------------------------- acceleration ---
 def resample(x: torch.Tensor, accels: Sequence[float], tsamp: float) -> torch.Tensor:
     """Batched time-domain acceleration resampling (resampleII semantics)."""

@@ -199,6 +199,22 @@ def test_interbin_normalise_batch():
         assert np.allclose(P[k], (ref.interbin(X[k]) - mean) / sd, rtol=1e-6, atol=1e-6)
 
 
+def test_r2c_interbin_normalise_batch():
+    """Fused real-FFT post-processing (N/2-point complex FFT) vs numpy rfft."""
+    from peasoup_amd import ops
+
+    rng = np.random.default_rng(5)
+    n = 1 << 14
+    x = rng.standard_normal((3, n)).astype(np.float32)
+    st = torch.tensor([1.5, 2.0, 0.75, 0.0], dtype=torch.float32, device=dev)
+    P = ops.r2c_interbin_normalise(torch.from_numpy(x).to(dev), st, 1.0).cpu().numpy()
+    assert P.shape == (3, n // 2 + 1)
+    for k in range(3):
+        X = np.fft.rfft(x[k].astype(np.float64))
+        exp = (ref.interbin(X.astype(np.complex64)) - 1.5) / 0.75
+        assert np.allclose(P[k], exp, rtol=1e-4, atol=2e-3), np.abs(P[k] - exp).max()
+
+
 def test_fold_optimise_matches_fft_reference():
     from peasoup_amd import ops
 
