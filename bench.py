@@ -45,7 +45,8 @@ def parse():
     p.add_argument("--acc", type=float, default=500.0, help="search +-acc m/s^2")
     p.add_argument("--nharmonics", type=int, default=3)
     p.add_argument("--accel-batch", type=int, default=0)
-    p.add_argument("--fft-mode", type=int, default=1, help="0: rocFFT R2C; 1: C2C(N/2) + fused r2c post")
+    p.add_argument("--fft-mode", type=int, default=2,
+                   help="2: fused resample + four-step FFT; 1: rocFFT C2C(N/2) + fused r2c post; 0: rocFFT R2C")
     p.add_argument("--dedisp-kernel", default="mfma", choices=["mfma", "direct"])
     p.add_argument("--seed", type=int, default=1234)
     return p.parse_args()
@@ -84,6 +85,7 @@ def main() -> int:
     args.nharmonics = a.nharmonics
     args.size = n
     args.accel_batch = a.accel_batch
+    args.fft_mode = a.fft_mode
     args.dedisp_kernel = a.dedisp_kernel
     delays = _C.generate_delay_table(a.nchans, a.tsamp, fch1, foff)
     max_delay = _C.compute_max_delay(dms, delays)
@@ -100,7 +102,7 @@ def main() -> int:
         g.manual_seed(a.seed)
         packed.random_(0, 256, generator=g)  # every 2-bit field uniform on {0..3}
     pdist.broadcast_bytes(packed, nbytes)
-    rs = RankSearcher(args, header, packed, nsamps, fft_mode=a.fft_mode)
+    rs = RankSearcher(args, header, packed, nsamps)
     del packed
     torch.cuda.empty_cache()
 
@@ -155,6 +157,7 @@ def main() -> int:
                 "dms_per_gpu": a.dms_per_gpu,
                 "accel_trials_per_dm": trials_per_step_local // a.dms_per_gpu,
                 "accel_batch": rs.engine.batch_size,
+                "fft_mode": rs.engine.fft_mode,
                 "candidates_after_distill": ncands,
             },
         }

@@ -102,8 +102,9 @@ struct SearchParams {
   int min_gap = 30;
   // Acceleration-trial FFT path: 0 = rocFFT R2C of N points; 1 = rocFFT C2C
   // of N/2 points with the real-FFT post-processing fused into the interbin
-  // kernel (default, N even).
-  int fft_mode = 1;
+  // kernel; 2 = resample fused into a two-pass four-step FFT (fft4step.hip,
+  // default; falls back to 1 when N/2 is not N1*N2 with N1,N2 in 128..4096).
+  int fft_mode = 2;
 };
 
 // Running-median whitening of one N-point series, in place.
@@ -155,6 +156,7 @@ class SearchEngine {
   const SearchCounters& counters() const { return ctr_; }
   void reset_counters() { ctr_ = SearchCounters(); }
   int batch_size() const { return K_; }
+  int fft_mode() const { return mode_; }
   float tobs() const { return tobs_; }
   // Debug access to the whitened series of the last trial.
   const float* whitened() const { return tim_.data(); }
@@ -190,7 +192,10 @@ class SearchEngine {
   DeviceBuffer<float> tim_;
   DeviceBuffer<uint32_t> zapmask_;
   bool zap_ = false;
-  bool c2c_ = true;
+  int mode_ = 2;        // effective fft_mode
+  int f4_n1_ = 0, f4_n2_ = 0;
+  DeviceBuffer<float2> f4_tab_;
+  uint64_t xs_ = 0;     // per-trial stride of spec_ (complex)
   DeviceBuffer<float> res_;
   DeviceBuffer<float2> spec_;
   DeviceBuffer<float> P_;

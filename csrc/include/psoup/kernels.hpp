@@ -114,6 +114,19 @@ void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride,
 void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride, float* P, uint64_t pstride, int K,
                                   uint64_t nbins_out, const float* stats, float nscale, hipStream_t s);
 
+// Fused resample + four-step FFT (fft4step.hip).  M = N/2 = N1*N2 with
+// N1, N2 powers of two in [128, 4096]; fft4_factor picks N2 <= N1 <= 2 N2.
+bool fft4_factor(uint64_t M, int* N1, int* N2);
+// Twiddle tables (upload once per plan): see fft4step.hip for the layout.
+std::vector<float2> fft4_tables(int N1, int N2);
+// Pass A: Y[k][k2*N1 + i] = W_M^{i k2} sum_j z_k[N1 j + i] W_N2^{j k2}, where
+// z_k[m] = x_k[2m] + i x_k[2m+1] and x_k = resampleII(in, af[k]); n = 2M.
+void fft4_resample_colpass(const float* in, uint64_t n, const double* af, int K, float2* Y, uint64_t ystride,
+                           int N1, int N2, const float2* tables, hipStream_t s);
+// Pass B: X[k][k2 + N2 k1] = sum_i Y[k][k2*N1 + i] W_N1^{i k1}  (= FFT_M(z_k)).
+void fft4_rowpass(const float2* Y, uint64_t ystride, float2* X, uint64_t xstride, int K, int N1, int N2,
+                  const float2* tables, hipStream_t s);
+
 struct HarmParams {
   int nlevels;             // number of harmonic-sum levels (0..5)
   int start[6];            // per level search range [start, end)

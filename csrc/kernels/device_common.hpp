@@ -114,6 +114,18 @@ __device__ __forceinline__ float interbin(float2 x, float2 xl) {
   return sqrtf(fmaxf(ampsq, ampsq_diff));
 }
 
+// resampleII read index (kernels.cu:338-379) in double precision, clamped
+// to [0, nmax].  Shared by the resampler and the fused four-step FFT so both
+// paths pick bit-identical samples.
+__device__ __forceinline__ uint64_t accel_index_ii(double af, double size, uint64_t id, uint64_t nmax) {
+  const double d = static_cast<double>(id);
+  const double r = d + d * af * (d - size);
+  double rr = rint(r);
+  if (rr < 0.0) rr = 0.0;
+  const uint64_t j = static_cast<uint64_t>(rr);
+  return j > nmax ? nmax : j;
+}
+
 }  // namespace dev
 }  // namespace kern
 }  // namespace psoup

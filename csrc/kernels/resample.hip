@@ -12,15 +12,6 @@ namespace kern {
 
 namespace {
 
-__device__ __forceinline__ uint64_t accel_index_ii(double af, double size, uint64_t id, uint64_t nmax) {
-  double d = static_cast<double>(id);
-  double r = d + d * af * (d - size);
-  double rr = rint(r);
-  if (rr < 0.0) rr = 0.0;
-  uint64_t j = static_cast<uint64_t>(rr);
-  return j > nmax ? nmax : j;
-}
-
 __global__ void __launch_bounds__(256) resample_batch_kernel(const float* __restrict__ in, uint64_t n,
                                                              float* __restrict__ out, uint64_t out_stride,
                                                              const double* __restrict__ afs) {
@@ -33,14 +24,14 @@ __global__ void __launch_bounds__(256) resample_batch_kernel(const float* __rest
   for (uint64_t v = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; v < n4; v += stride) {
     uint64_t i = v * 4;
     float4 r;
-    r.x = in[accel_index_ii(af, size, i, n - 1)];
-    r.y = in[accel_index_ii(af, size, i + 1, n - 1)];
-    r.z = in[accel_index_ii(af, size, i + 2, n - 1)];
-    r.w = in[accel_index_ii(af, size, i + 3, n - 1)];
+    r.x = in[dev::accel_index_ii(af, size, i, n - 1)];
+    r.y = in[dev::accel_index_ii(af, size, i + 1, n - 1)];
+    r.z = in[dev::accel_index_ii(af, size, i + 2, n - 1)];
+    r.w = in[dev::accel_index_ii(af, size, i + 3, n - 1)];
     reinterpret_cast<float4*>(o)[v] = r;
   }
   for (uint64_t i = n4 * 4 + blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n; i += stride)
-    o[i] = in[accel_index_ii(af, size, i, n - 1)];
+    o[i] = in[dev::accel_index_ii(af, size, i, n - 1)];
 }
 
 __global__ void __launch_bounds__(256) resample_v1_kernel(const float* __restrict__ in, uint64_t n,

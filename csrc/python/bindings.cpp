@@ -306,6 +306,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("accel_convention", &CmdLineOptions::accel_convention)
       .def_readwrite("dedisp_kernel", &CmdLineOptions::dedisp_kernel)
       .def_readwrite("accel_batch", &CmdLineOptions::accel_batch)
+      .def_readwrite("fft_mode", &CmdLineOptions::fft_mode)
       .def_readwrite("use_boundaries", &CmdLineOptions::use_boundaries)
       .def_readwrite("checkpoint_dir", &CmdLineOptions::checkpoint_dir)
       .def_readwrite("trace_json", &CmdLineOptions::trace_json)
@@ -428,6 +429,26 @@ PYBIND11_MODULE(_C, m) {
     kern::r2c_interbin_normalise_batch(P<const float2>(Z), M, zstride, P<float>(Pout), pstride, K, nbo,
                                        P<const float>(stats), nscale, S(s));
   });
+  k.def("fft4_factor", [](uint64_t M) {
+    int n1 = 0, n2 = 0;
+    bool ok = kern::fft4_factor(M, &n1, &n2);
+    return py::make_tuple(ok, n1, n2);
+  });
+  k.def("fft4_tables", [](int n1, int n2) {
+    auto t = kern::fft4_tables(n1, n2);
+    py::array_t<float> a({static_cast<py::ssize_t>(t.size()), static_cast<py::ssize_t>(2)});
+    std::memcpy(a.mutable_data(), t.data(), t.size() * sizeof(float2));
+    return a;
+  });
+  k.def("fft4_resample_colpass", [](uintptr_t in, uint64_t n, uintptr_t af, int K, uintptr_t Y, uint64_t ystride,
+                                    int n1, int n2, uintptr_t tab, uintptr_t s) {
+    kern::fft4_resample_colpass(P<const float>(in), n, P<const double>(af), K, P<float2>(Y), ystride, n1, n2,
+                                P<const float2>(tab), S(s));
+  });
+  k.def("fft4_rowpass", [](uintptr_t Y, uint64_t ystride, uintptr_t X, uint64_t xstride, int K, int n1, int n2,
+                           uintptr_t tab, uintptr_t s) {
+    kern::fft4_rowpass(P<const float2>(Y), ystride, P<float2>(X), xstride, K, n1, n2, P<const float2>(tab), S(s));
+  });
   k.def("harmonic_peaks_batch", [](uintptr_t Pin, uint64_t nb, uint64_t pstride, int K, int nlevels,
                                    const std::vector<int>& start, const std::vector<int>& end, float thresh,
                                    uint32_t capacity, uintptr_t out, uintptr_t count, uintptr_t s) {
@@ -537,6 +558,7 @@ PYBIND11_MODULE(_C, m) {
         return e.search_trial(P<const uint8_t>(trial), nsamps, dm, dm_idx, accs);
       }, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("batch_size", &SearchEngine::batch_size)
+      .def_property_readonly("fft_mode", &SearchEngine::fft_mode)
       .def_property_readonly("tobs", &SearchEngine::tobs)
       .def_property_readonly("whitened_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.whitened()); })
       .def_property_readonly("stats_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.whitener().stats()); })

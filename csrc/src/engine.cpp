@@ -211,7 +211,14 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     log_info("warning: nharmonics > 5 is capped at 5 (32 harmonics), as the reference kernel only writes 5 levels");
   wh_ = std::make_unique<Whitener>(n_, p_.tsamp, stream_);
   tim_.resize(n_);
-  c2c_ = (p_.fft_mode == 1) && (n_ % 2 == 0);
+  mode_ = (n_ % 2 == 0) ? std::min(std::max(p_.fft_mode, 0), 2) : 0;
+  if (mode_ == 2 && !kern::fft4_factor(n_ / 2, &f4_n1_, &f4_n2_)) mode_ = 1;
+  if (mode_ == 2) {
+    auto tab = kern::fft4_tables(f4_n1_, f4_n2_);
+    f4_tab_.resize(tab.size());
+    PSOUP_HIP_CHECK(hipMemcpy(f4_tab_.data(), tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice));
+  }
+  xs_ = mode_ == 2 ? (n_ / 2 + 8) : nb_;
   if (!p_.zap_freqs.empty()) {
     auto mask = build_zap_mask(p_.zap_freqs, p_.zap_widths, bin_width_, nb_);
     zapmask_.resize(mask.size());
@@ -269,7 +276,7 @@ void SearchEngine::grow_capacity(uint32_t need) {
 void SearchEngine::ensure_batch_buffers() {
   if (res_.size() >= static_cast<uint64_t>(K_) * n_) return;
   res_.resize(static_cast<uint64_t>(K_) * n_);
-  spec_.resize(static_cast<uint64_t>(K_) * nb_);
+  spec_.resize(static_cast<uint64_t>(K_) * xs_);
   P_.resize(static_cast<uint64_t>(K_) * std::max<uint64_t>(1, static_cast<uint64_t>(hi_)));
 }
 
@@ -277,7 +284,7 @@ FftPlan& SearchEngine::batch_plan(int count) {
   auto it = plans_.find(count);
   if (it != plans_.end()) return *it->second;
   std::unique_ptr<FftPlan> plan;
-  if (c2c_)  // N/2-point complex FFT of the packed real series (post-processing fused downstream)
+  if (mode_ == 1)  // N/2-point complex FFT of the packed real series (post-processing fused downstream)
     plan = std::make_unique<FftPlan>(FftType::C2C_FWD, n_ / 2, static_cast<uint64_t>(count), n_ / 2, nb_);
   else
     plan = std::make_unique<FftPlan>(FftType::R2C, n_, static_cast<uint64_t>(count), n_, nb_);
@@ -289,11 +296,19 @@ FftPlan& SearchEngine::batch_plan(int count) {
 void SearchEngine::launch_batch(Slot& s, int first, int count) {
   s.first = first;
   s.count = count;
-  kern::resample_batch(tim_.data(), n_, res_.data(), n_, af_.data() + first, count, stream_);
-  batch_plan(count).execute(res_.data(), spec_.data(), stream_);
+  if (mode_ == 2) {
+    // res_ holds the K four-step intermediates Y (complex, M per trial)
+    float2* Y = reinterpret_cast<float2*>(res_.data());
+    kern::fft4_resample_colpass(tim_.data(), n_, af_.data() + first, count, Y, n_ / 2, f4_n1_, f4_n2_,
+                                f4_tab_.data(), stream_);
+    kern::fft4_rowpass(Y, n_ / 2, spec_.data(), xs_, count, f4_n1_, f4_n2_, f4_tab_.data(), stream_);
+  } else {
+    kern::resample_batch(tim_.data(), n_, res_.data(), n_, af_.data() + first, count, stream_);
+    batch_plan(count).execute(res_.data(), spec_.data(), stream_);
+  }
   const uint64_t pst = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
-  if (c2c_)
-    kern::r2c_interbin_normalise_batch(spec_.data(), n_ / 2, nb_, P_.data(), pst, count, static_cast<uint64_t>(hi_),
+  if (mode_ >= 1)
+    kern::r2c_interbin_normalise_batch(spec_.data(), n_ / 2, xs_, P_.data(), pst, count, static_cast<uint64_t>(hi_),
                                        wh_->stats(), static_cast<float>(n_), stream_);
   else
     kern::interbin_normalise_batch(spec_.data(), nb_, nb_, P_.data(), pst, count, static_cast<uint64_t>(hi_),

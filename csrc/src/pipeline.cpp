@@ -49,6 +49,7 @@ SearchSetup make_search_setup(const CmdLineOptions& args, const SigprocHeader& h
   p.boundary_25_freq = args.use_boundaries ? args.boundary_25_freq : 0.5f;
   if (!args.zapfilename.empty()) read_zapfile(args.zapfilename, p.zap_freqs, p.zap_widths);
   p.accel_batch = args.accel_batch;
+  p.fft_mode = args.fft_mode;
   s.dedisp_kernel = parse_dedisp_kernel(args.dedisp_kernel);
   return s;
 }

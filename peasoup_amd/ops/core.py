@@ -211,6 +211,31 @@ def resample(x: torch.Tensor, accels: Sequence[float], tsamp: float) -> torch.Te
     return out[:, :n]
 
 
+def _accel_factors(accels: Sequence[float], tsamp: float, device) -> torch.Tensor:
+    return torch.tensor([(float(torch.tensor(a, dtype=torch.float32)) * float(torch.tensor(tsamp, dtype=torch.float32)))
+                         / (2 * 299792458.0) for a in accels], dtype=torch.float64, device=device)
+
+
+def fft4_resample_spectrum(x: torch.Tensor, accels: Sequence[float], tsamp: float) -> torch.Tensor:
+    """Fused resample + four-step FFT: returns Z [K, N/2] complex64 with
+    Z[k] = FFT_{N/2}(z_k), z_k[m] = r_k[2m] + i r_k[2m+1], r_k = resample(x, accels[k])."""
+    _check(x, torch.float32, "x")
+    n = x.numel()
+    ok, n1, n2 = K.fft4_factor(n // 2)
+    if not ok or n % 2:
+        raise ValueError(f"fft4: unsupported length {n}")
+    M = n // 2
+    tab = torch.from_numpy(K.fft4_tables(n1, n2)).to(x.device)
+    af = _accel_factors(accels, tsamp, x.device)
+    Kb = len(accels)
+    Y = torch.empty((Kb, M, 2), dtype=torch.float32, device=x.device)
+    Z = torch.empty((Kb, M, 2), dtype=torch.float32, device=x.device)
+    K.fft4_resample_colpass(x.data_ptr(), n, af.data_ptr(), Kb, Y.data_ptr(), M, n1, n2, tab.data_ptr(), _s())
+    K.fft4_rowpass(Y.data_ptr(), M, Z.data_ptr(), M, Kb, n1, n2, tab.data_ptr(), _s())
+    torch.cuda.current_stream().synchronize()  # keep `tab`/`Y` alive until the passes ran
+    return torch.view_as_complex(Z)
+
+
 def resample_v1(x: torch.Tensor, accel: float, tsamp: float) -> torch.Tensor:
     _check(x, torch.float32, "x")
     af = (float(torch.tensor(accel, dtype=torch.float32)) * float(torch.tensor(tsamp, dtype=torch.float32))) / (2 * 299792458.0)

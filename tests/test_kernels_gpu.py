@@ -215,6 +215,26 @@ def test_r2c_interbin_normalise_batch():
         assert np.allclose(P[k], exp, rtol=1e-4, atol=2e-3), np.abs(P[k] - exp).max()
 
 
+@pytest.mark.parametrize("log2n", [15, 17, 20, 23])
+def test_fft4_resample_spectrum_matches_numpy(log2n):
+    """Fused resample + four-step FFT vs (bit-exact GPU resample) + numpy fp64 FFT."""
+    from peasoup_amd import ops
+
+    rng = np.random.default_rng(log2n)
+    n = 1 << log2n
+    x = torch.from_numpy(rng.standard_normal(n).astype(np.float32)).to(dev)
+    accs = [-480.0, 0.0, 37.5, 500.0] if log2n < 23 else [-500.0, 250.0]
+    Z = ops.fft4_resample_spectrum(x, accs, 64e-6).cpu().numpy()
+    R = ops.resample(x, accs, 64e-6).cpu().numpy().astype(np.float64)
+    for k in range(len(accs)):
+        z = R[k, 0::2] + 1j * R[k, 1::2]
+        ref_Z = np.fft.fft(z)
+        err = np.abs(Z[k] - ref_Z)
+        scale = np.sqrt(np.mean(np.abs(ref_Z) ** 2))
+        assert err.max() / scale < 5e-5, (k, err.max() / scale)
+        assert np.sqrt(np.mean(err ** 2)) / scale < 5e-6
+
+
 def test_fold_optimise_matches_fft_reference():
     from peasoup_amd import ops
 

@@ -111,3 +111,28 @@ def test_injected_accelerated_pulsar_is_found(C, tmp_path):
     assert abs(best.dm - 40.0) < 6.0
     assert abs(best.acc - 60.0) < 25.0
     assert best.folded_snr > 8.0
+
+
+def test_fft_modes_agree(C, tmp_path):
+    """The fused four-step FFT (default), rocFFT C2C(N/2) and rocFFT R2C paths
+    give the same candidates (S/N to FFT rounding)."""
+    from peasoup_amd.utils.outputs import OverviewFile
+
+    res = {}
+    for mode in (0, 1, 2):
+        d = tmp_path / f"m{mode}"
+        r = subprocess.run([os.path.join(REPO, "bin", "peasoup"), "-i", TUTORIAL, "-o", str(d), "--fft_mode", str(mode),
+                            "--dm_end", "120", "-n", "4", "--npdmp", "0", "--acc_start", "-50", "--acc_end", "50"],
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr
+        res[mode] = OverviewFile(os.path.join(str(d), "overview.xml"))
+    n = len(res[0])
+    assert n > 10
+    for mode in (1, 2):
+        o = res[mode]
+        assert len(o) == n
+        for i in range(n):
+            a, b = res[0].get_candidate(i), o.get_candidate(i)
+            assert b["period"] == pytest.approx(a["period"], rel=1e-7), (mode, i)
+            assert b["dm"] == a["dm"] and b["nh"] == a["nh"], (mode, i)
+            assert b["snr"] == pytest.approx(a["snr"], rel=1e-4), (mode, i)
