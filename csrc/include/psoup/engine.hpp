@@ -193,8 +193,9 @@ class SearchEngine {
   DeviceBuffer<uint32_t> zapmask_;
   bool zap_ = false;
   int mode_ = 2;        // effective fft_mode
-  int f4_n1_ = 0, f4_n2_ = 0;
+  kern::Fft4Geom f4_;
   DeviceBuffer<float2> f4_tab_;
+  DeviceBuffer<float> f4_in_;  // padded whitened series read by the fused FFT
   uint64_t xs_ = 0;     // per-trial stride of spec_ (complex)
   DeviceBuffer<float> res_;
   DeviceBuffer<float2> spec_;

@@ -109,23 +109,49 @@ void resample_v1(const float* in, uint64_t n, float* out, double af, hipStream_t
 void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride, float* P, uint64_t pstride,
                               int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s);
 
-// Same output from the M = N/2 point complex FFT Z[K][M] of the packed real
+// Same output from the M = N/2 point complex FFT Z[K] of the packed real
 // series (real-FFT post-processing fused in; saves the separate r2c pass).
-void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride, float* P, uint64_t pstride, int K,
-                                  uint64_t nbins_out, const float* stats, float nscale, hipStream_t s);
+// Bin k of Z[k] lives at (k >> log2_row)*row_pitch + (k & (2^log2_row - 1))
+// (log2_row = log2 M, row_pitch = M for a plain array).  Each thread forms
+// the bin pair (k, M-k) from one pair of loads.
+void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t row_pitch,
+                                  float* P, uint64_t pstride, int K, uint64_t nbins_out, const float* stats,
+                                  float nscale, hipStream_t s);
 
-// Fused resample + four-step FFT (fft4step.hip).  M = N/2 = N1*N2 with
-// N1, N2 powers of two in [128, 4096]; fft4_factor picks N2 <= N1 <= 2 N2.
-bool fft4_factor(uint64_t M, int* N1, int* N2);
+// Fused resample + four-step FFT (fft4step.hip).  M = N/2 = n1*n2 with
+// n1, n2 powers of two in [128, 4096], n2 <= n1 <= 2 n2.  Intermediates use
+// padded row pitches (power-of-two strides would camp on one memory channel):
+//   Y[k][k2*ypitch + i]  (pass A output),  X[k][k1*xpitch + k2] = FFT_M(z_k)[k2 + n2 k1].
+struct Fft4Geom {
+  int n1 = 0, n2 = 0;
+  uint64_t ypitch = 0, ystride = 0;  // complex
+  uint64_t xpitch = 0, xstride = 0;  // complex
+  int log2_xrow = 0;                 // log2(n2): X index of bin k = (k >> log2_xrow)*xpitch + (k & (n2-1))
+  uint64_t inpitch = 0, insize = 0;  // floats: padded input copy
+  bool ok = false;
+};
+Fft4Geom fft4_geometry(uint64_t M);
 // Twiddle tables (upload once per plan): see fft4step.hip for the layout.
-std::vector<float2> fft4_tables(int N1, int N2);
-// Pass A: Y[k][k2*N1 + i] = W_M^{i k2} sum_j z_k[N1 j + i] W_N2^{j k2}, where
+std::vector<float2> fft4_tables(const Fft4Geom& g);
+// Padded copy of the (whitened) input series read by pass A; insize floats.
+void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& g, hipStream_t s);
+// Pass A: Y[k][k2][i] = W_M^{i k2} sum_j z_k[n1 j + i] W_n2^{j k2}, where
 // z_k[m] = x_k[2m] + i x_k[2m+1] and x_k = resampleII(in, af[k]); n = 2M.
-void fft4_resample_colpass(const float* in, uint64_t n, const double* af, int K, float2* Y, uint64_t ystride,
-                           int N1, int N2, const float2* tables, hipStream_t s);
-// Pass B: X[k][k2 + N2 k1] = sum_i Y[k][k2*N1 + i] W_N1^{i k1}  (= FFT_M(z_k)).
-void fft4_rowpass(const float2* Y, uint64_t ystride, float2* X, uint64_t xstride, int K, int N1, int N2,
-                  const float2* tables, hipStream_t s);
+void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
+                           const Fft4Geom& g, const float2* tables, hipStream_t s);
+// Pass B: X[k][k1][k2] = sum_i Y[k][k2][i] W_n1^{i k1}.
+void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, hipStream_t s);
+// Tuning switches (process-wide, for measurement): kernel shape and store policy.
+enum Fft4Flags : int {
+  kFft4Cpt8 = 1,         // 8 transforms per thread, one thread group (64-byte segments)
+  kFft4NoRemap = 2,      // plain block order (no XCD-contiguous remap)
+  kFft4NtStores = 4,     // nontemporal stores
+  kFft4SkipCompute = 8,  // timing only: memory traffic without the FFT
+  kFft4Wide = 16,        // 16 transforms per workgroup (128-byte segments, one workgroup per CU)
+  kFft4TrialSlow = 32,   // block order: column/row block fastest, trial slowest (write locality)
+};
+void fft4_set_flags(int flags);
+int fft4_flags();
 
 struct HarmParams {
   int nlevels;             // number of harmonic-sum levels (0..5)

@@ -117,9 +117,10 @@ __device__ __forceinline__ float interbin(float2 x, float2 xl) {
 // resampleII read index (kernels.cu:338-379) in double precision, clamped
 // to [0, nmax].  Shared by the resampler and the fused four-step FFT so both
 // paths pick bit-identical samples.
+__device__ __forceinline__ double accel_pos_ii(double af, double size, double d) { return d + d * af * (d - size); }
+
 __device__ __forceinline__ uint64_t accel_index_ii(double af, double size, uint64_t id, uint64_t nmax) {
-  const double d = static_cast<double>(id);
-  const double r = d + d * af * (d - size);
+  const double r = accel_pos_ii(af, size, static_cast<double>(id));
   double rr = rint(r);
   if (rr < 0.0) rr = 0.0;
   const uint64_t j = static_cast<uint64_t>(rr);

@@ -14,14 +14,18 @@
 //   pass B (rows, length N1): DFT over i of row k2, write X[k2 + N2 k1]
 //     in natural order.
 //
-// Each workgroup transforms 8 adjacent columns (pass A) or rows (pass B) at
-// once, so every global access is one 64-byte vector per lane (8 complex
-// values), and every thread owns the same 8 points of each of the 8
-// transforms: 64 complex values in VGPRs.  The transforms are Stockham
-// radix-8 (+ a final radix-4/2 stage) with LDS exchanges between stages, in
-// channel groups sized to keep LDS at 72 KiB so two workgroups share a CU.
-// Twiddles come from small host-built tables (double-precision), not
-// per-thread transcendental evaluation.
+// A workgroup transforms 8 adjacent columns (pass A) or rows (pass B), so
+// every global row segment it touches is 64 bytes (8 complex values); it runs
+// as two halves of L/8 threads, each half owning 4 of the 8 transforms and
+// each thread 8 points of each of its 4 transforms (32 complex values in
+// VGPRs).  The two halves write the two 32-byte halves of every 64-byte
+// segment at the same time, so L2 merges them into whole lines.  Transforms
+// are Stockham radix-8 (+ a final radix-4/2 stage) with LDS exchanges between
+// stages; LDS stays at 72 KiB per workgroup so two workgroups (16 waves)
+// share a CU.  Twiddles come from small host-built tables (double precision).
+// Block ids are remapped so that each XCD (blockIdx % 8 under round-robin
+// dispatch) works on a contiguous range of (column block, trial) pairs: the
+// trials of one column block, whose resampled reads overlap, share one L2.
 #include "device_common.hpp"
 #include "psoup/kernels.hpp"
 
@@ -32,20 +36,30 @@ namespace kern {
 
 namespace {
 
-constexpr int kCh = 8;   // transforms per workgroup -> 64-byte vectors per lane
-constexpr int kPts = 8;  // points per thread per transform
+constexpr int kPts = 8;     // points per thread per transform
 constexpr int kSplit = 11;  // W_M^a = hi[a >> kSplit] * lo[a & (2^kSplit - 1)]
+constexpr int kLdsBudget = 73728;  // bytes per workgroup: two workgroups per CU
 
-template <int L>
+// CPT = transforms per thread, SUB = thread groups per workgroup; the
+// workgroup covers CH = CPT*SUB adjacent columns/rows (8: 64-byte row
+// segments, two workgroups per CU; 16: 128-byte segments, one per CU).
+template <int L, int CPT, int SUB>
 struct Cfg {
-  static constexpr int T = L / kPts;                                // threads per workgroup
-  static constexpr int CG = L >= 4096 ? 2 : (L >= 2048 ? 4 : 8);    // channels per LDS exchange
-  static constexpr int PAD = L + L / 8;                             // padded floats per channel plane
-  static constexpr int LDS_FLOATS = 2 * CG * PAD;
+  static constexpr int CH = CPT * SUB;
+  static constexpr int T = L / kPts;                     // threads per group
+  static constexpr int THREADS = T * SUB;
+  static constexpr int PAD = L + L / 8;                  // padded floats per channel plane
+  static constexpr int BUDGET = CH >= 16 ? 2 * kLdsBudget : kLdsBudget;
+  static constexpr int CG0 = BUDGET / (SUB * 2 * PAD * 4);
+  static constexpr int CG = CG0 >= CPT ? CPT : (CG0 >= 4 ? 4 : (CG0 >= 2 ? 2 : 1));  // channels per exchange round
+  static constexpr int GROUP_FLOATS = 2 * CG * PAD;
+  static constexpr int LDS_FLOATS = SUB * GROUP_FLOATS;
 };
 
-using Vec = float2[kCh][kPts];
+template <int CPT>
+using Vec = float2[CPT][kPts];
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned 16-byte load
+typedef float f4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int lds_pad(int x) { return x + (x >> 3); }
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
@@ -88,8 +102,8 @@ __device__ __forceinline__ void fft8(float2& a0, float2& a1, float2& a2, float2&
 // One Stockham iteration's arithmetic (Govindaraju et al. formulation): for
 // virtual thread j' = t + b*T, points v[b + r*B] = data[j' + r*L/R] are
 // twiddled by W_{Ns R}^{r (j' mod Ns)} and transformed in place.
-template <int L, int Ns, int R>
-__device__ __forceinline__ void stage_compute(Vec& v, int t, const float2* __restrict__ twL) {
+template <int L, int CPT, int Ns, int R>
+__device__ __forceinline__ void stage_compute(Vec<CPT>& v, int t, const float2* __restrict__ twL) {
   constexpr int T = L / kPts, B = kPts / R;
 #pragma unroll
   for (int b = 0; b < B; ++b) {
@@ -100,11 +114,11 @@ __device__ __forceinline__ void stage_compute(Vec& v, int t, const float2* __res
       for (int r = 1; r < R; ++r) {
         const float2 w = twL[r * jm * scale];
 #pragma unroll
-        for (int c = 0; c < kCh; ++c) v[c][b + r * B] = cmul(v[c][b + r * B], w);
+        for (int c = 0; c < CPT; ++c) v[c][b + r * B] = cmul(v[c][b + r * B], w);
       }
     }
 #pragma unroll
-    for (int c = 0; c < kCh; ++c) {
+    for (int c = 0; c < CPT; ++c) {
       if constexpr (R == 8)
         fft8(v[c][b], v[c][b + B], v[c][b + 2 * B], v[c][b + 3 * B], v[c][b + 4 * B], v[c][b + 5 * B],
              v[c][b + 6 * B], v[c][b + 7 * B]);
@@ -118,13 +132,13 @@ __device__ __forceinline__ void stage_compute(Vec& v, int t, const float2* __res
 
 // Scatter to the Stockham destination (j'/Ns)*Ns*R + j' mod Ns + r*Ns, then
 // gather back in the uniform pattern t + q*T.
-template <int L, int Ns, int R>
-__device__ __forceinline__ void exchange(Vec& v, float* __restrict__ lds, int t) {
-  constexpr int T = L / kPts, B = kPts / R, CG = Cfg<L>::CG, PAD = Cfg<L>::PAD;
+template <int L, int CPT, int CG, int Ns, int R>
+__device__ __forceinline__ void exchange(Vec<CPT>& v, float* __restrict__ lds, int t) {
+  constexpr int T = L / kPts, B = kPts / R, PAD = L + L / 8;
   float* re = lds;
   float* im = lds + CG * PAD;
 #pragma unroll
-  for (int g = 0; g < kCh; g += CG) {
+  for (int g = 0; g < CPT; g += CG) {
 #pragma unroll
     for (int b = 0; b < B; ++b) {
       const int j = t + b * T;
@@ -150,50 +164,53 @@ __device__ __forceinline__ void exchange(Vec& v, float* __restrict__ lds, int t)
   }
 }
 
-// Full forward DFT of length L on the 8 channels; input and output both in
-// the pattern v[c][q] <-> element t + q*T.
-template <int L, int Ns>
-__device__ __forceinline__ void fft_stages(Vec& v, float* __restrict__ lds, int t, const float2* __restrict__ twL) {
+// Full forward DFT of length L on the thread's CPT channels (lds = its group's
+// region); input and output both in the pattern v[c][q] <-> element t + q*T.
+template <int L, int CPT, int CG, int Ns>
+__device__ __forceinline__ void fft_stages(Vec<CPT>& v, float* __restrict__ lds, int t,
+                                           const float2* __restrict__ twL) {
   constexpr int R = (L / Ns >= 8) ? 8 : L / Ns;
-  stage_compute<L, Ns, R>(v, t, twL);
+  stage_compute<L, CPT, Ns, R>(v, t, twL);
   if constexpr (Ns * R < L) {
-    exchange<L, Ns, R>(v, lds, t);
-    fft_stages<L, Ns * R>(v, lds, t, twL);
+    exchange<L, CPT, CG, Ns, R>(v, lds, t);
+    fft_stages<L, CPT, CG, Ns * R>(v, lds, t, twL);
   }
 }
 
-// Sixteen consecutive resampled samples x[p0 .. p0+15].  The read index
-// drifts by < 1 sample per 16 for any physical acceleration, so they come
-// from one 20-float window (five dword-aligned 16-byte loads); lanes where
-// that does not hold (series edges, extreme drift) gather per sample.
-__device__ __forceinline__ void load_resampled16(const float* __restrict__ in, uint64_t n, double af, double size,
-                                                 uint64_t p0, float (&x)[16]) {
-  uint32_t e[16];
-  const uint64_t i0 = dev::accel_index_ii(af, size, p0, n - 1);
-  const int64_t w0 = static_cast<int64_t>(i0) - 1;
-  bool fast = (w0 >= 0) && (static_cast<uint64_t>(w0) + 20 <= n);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const uint64_t idx = i == 0 ? i0 : dev::accel_index_ii(af, size, p0 + i, n - 1);
-    e[i] = static_cast<uint32_t>(static_cast<int64_t>(idx) - (w0 + i));
-    fast = fast && (e[i] <= 2u);
-  }
+// S consecutive resampled samples x[p0 .. p0+S-1].  The read index is
+// evaluated exactly (the resampleII formula, as resample_batch) at both ends
+// of the span; when the shift idx(p) - p is the same at both ends, the
+// shift function is monotone on the span (the parabola's vertex n/2 is not
+// inside) and both ends round with a margin, every sample in between has
+// that same shift and the S values are one contiguous load of
+// the padded input (S = 16: 64 bytes).  Otherwise (a shift step inside the span, series edges)
+// each sample is indexed exactly and gathered from the plain series.
+template <int S>  // S = samples per span, a multiple of 4
+__device__ __forceinline__ void load_resampled(const float* __restrict__ in, const float* __restrict__ in_pad,
+                                               uint64_t n, int log2row, uint64_t inpitch, double af, double size,
+                                               uint64_t p0, float (&x)[S]) {
+  const double d0 = static_cast<double>(p0), d1 = static_cast<double>(p0 + S - 1);
+  const double r0 = dev::accel_pos_ii(af, size, d0), r1 = dev::accel_pos_ii(af, size, d1);
+  const double q0 = rint(r0), q1 = rint(r1);
+  const double vertex = 0.5 * size;
+  const bool fast = (q1 - q0 == static_cast<double>(S - 1)) && (0.5 - fabs(r0 - q0) > 1e-7) &&
+                    (0.5 - fabs(r1 - q1) > 1e-7) && q0 >= 0.0 && q1 <= static_cast<double>(n - 1) &&
+                    !(d0 < vertex && vertex < d1);
   if (fast) {
-    float w[20];
-    const f4u* src = reinterpret_cast<const f4u*>(in + w0);
+    const uint64_t i0 = static_cast<uint64_t>(q0);
+    const uint64_t a = (i0 >> log2row) * inpitch + (i0 & ((uint64_t(1) << log2row) - 1));
+    const f4u* src = reinterpret_cast<const f4u*>(in_pad + a);
 #pragma unroll
-    for (int u = 0; u < 5; ++u) {
-      const f4u q = src[u];
-      w[4 * u] = q.x;
-      w[4 * u + 1] = q.y;
-      w[4 * u + 2] = q.z;
-      w[4 * u + 3] = q.w;
+    for (int u = 0; u < S / 4; ++u) {
+      const f4u w = src[u];
+      x[4 * u] = w.x;
+      x[4 * u + 1] = w.y;
+      x[4 * u + 2] = w.z;
+      x[4 * u + 3] = w.w;
     }
-#pragma unroll
-    for (int i = 0; i < 16; ++i) x[i] = e[i] == 0 ? w[i] : (e[i] == 1 ? w[i + 1] : w[i + 2]);
   } else {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) x[i] = in[w0 + i + static_cast<int64_t>(static_cast<int32_t>(e[i]))];
+    for (int i = 0; i < S; ++i) x[i] = in[dev::accel_index_ii(af, size, p0 + i, n - 1)];
   }
 }
 
@@ -216,143 +233,242 @@ __device__ __forceinline__ float2 twiddle_M(uint32_t a, const float2* __restrict
   return cmul(hi[a >> kSplit], lo[a & ((1u << kSplit) - 1)]);
 }
 
-// Pass A.  grid.x = (N1/8) * K, trial fastest so the K workgroups of one
-// column block run together and share the input window in L2.
-template <int L>
-__global__ void __launch_bounds__(Cfg<L>::T) fft4_colpass_kernel(const float* __restrict__ in, uint64_t n,
-                                                                  const double* __restrict__ afs, int K,
-                                                                  float2* __restrict__ Y, uint64_t ystride, int N1,
-                                                                  const float2* __restrict__ tab) {
-  __shared__ float lds[Cfg<L>::LDS_FLOATS];
-  constexpr int T = Cfg<L>::T;
-  const int t = threadIdx.x;
-  const int k = blockIdx.x % K;
-  const int i0 = (blockIdx.x / K) * kCh;
-  const TableOffsets to = table_offsets(N1, L);
-  const double af = afs[k];
-  const double size = static_cast<double>(n);
-  Vec v;
+template <int CPT>
+__device__ __forceinline__ void store_row(float2* __restrict__ dst, const Vec<CPT>& v, int q, bool nt) {
+  f4v* d = reinterpret_cast<f4v*>(dst);
 #pragma unroll
-  for (int q = 0; q < kPts; ++q) {
-    const uint64_t j = t + q * T;
-    float x[16];
-    load_resampled16(in, n, af, size, 2 * (static_cast<uint64_t>(N1) * j + i0), x);
-#pragma unroll
-    for (int c = 0; c < kCh; ++c) v[c][q] = make_float2(x[2 * c], x[2 * c + 1]);
-  }
-  fft_stages<L, 1>(v, lds, t, tab + to.n2);
-  const uint32_t mask = static_cast<uint32_t>(N1) * L - 1;
-  float2* y = Y + static_cast<uint64_t>(k) * ystride + i0;
-#pragma unroll
-  for (int q = 0; q < kPts; ++q) {
-    const uint32_t k2 = t + q * T;
-    float2 w = twiddle_M((static_cast<uint32_t>(i0) * k2) & mask, tab + to.lo, tab + to.hi);
-    const float2 step = twiddle_M(k2, tab + to.lo, tab + to.hi);
-#pragma unroll
-    for (int c = 0; c < kCh; ++c) {
-      v[c][q] = cmul(v[c][q], w);
-      w = cmul(w, step);
-    }
-    float4* dst = reinterpret_cast<float4*>(y + static_cast<uint64_t>(k2) * N1);
-#pragma unroll
-    for (int c = 0; c < kCh; c += 2) dst[c / 2] = make_float4(v[c][q].x, v[c][q].y, v[c + 1][q].x, v[c + 1][q].y);
+  for (int c = 0; c < CPT; c += 2) {
+    const f4v val = {v[c][q].x, v[c][q].y, v[c + 1][q].x, v[c + 1][q].y};
+    if (nt)
+      __builtin_nontemporal_store(val, d + c / 2);
+    else
+      d[c / 2] = val;
   }
 }
 
-// Pass B.  grid.x = (N2/8) * K.
-template <int L>
-__global__ void __launch_bounds__(Cfg<L>::T) fft4_rowpass_kernel(const float2* __restrict__ Y, uint64_t ystride,
-                                                                  float2* __restrict__ X, uint64_t xstride, int K,
-                                                                  int N2, const float2* __restrict__ tab) {
-  __shared__ float lds[Cfg<L>::LDS_FLOATS];
-  constexpr int T = Cfg<L>::T;
-  const int t = threadIdx.x;
-  const int k = blockIdx.x % K;
-  const int r0 = (blockIdx.x / K) * kCh;
-  const TableOffsets to = table_offsets(L, N2);
-  const float2* y = Y + static_cast<uint64_t>(k) * ystride + static_cast<uint64_t>(r0) * L;
-  Vec v;
-#pragma unroll
-  for (int c = 0; c < kCh; ++c)
-#pragma unroll
-    for (int q = 0; q < kPts; ++q) v[c][q] = y[static_cast<uint64_t>(c) * L + t + q * T];
-  fft_stages<L, 1>(v, lds, t, tab + to.n1);
-  float2* x = X + static_cast<uint64_t>(k) * xstride + r0;
+// XCD-aware block order (remap = true): logical block
+// b' = (b % 8) * (nblocks / 8) + b / 8, so each XCD's share of the grid is one
+// contiguous logical range (nblocks is a multiple of 8).
+__device__ __forceinline__ uint32_t logical_block(uint32_t nblocks, bool remap) {
+  const uint32_t b = blockIdx.x;
+  return remap ? (b & 7u) * (nblocks >> 3) + (b >> 3) : b;
+}
+
+// Input copy with rows of 2*N1 floats at a pitch of 2*N1 + 32 (the pad holds
+// the next row's head, so a span starting in a row is contiguous).  Pass A's
+// lanes read rows 2*N1 floats apart; the odd pitch spreads them over memory
+// channels instead of one.
+__global__ void __launch_bounds__(256) fft4_pad_input_kernel(const float* __restrict__ in, uint64_t n,
+                                                             float* __restrict__ out, uint64_t rowlen,
+                                                             uint64_t pitch, uint64_t total) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t u = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; u < total; u += stride) {
+    const uint64_t row = u / pitch, r = u - row * pitch;
+    const uint64_t src = row * rowlen + r;
+    out[u] = src < n ? in[src] : 0.f;
+  }
+}
+
+// Pass A.  Logical block = column block * K + trial (trial fastest).
+template <int L, int CPT, int SUB>
+__global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2)) fft4_colpass_kernel(
+    const float* __restrict__ in, const float* __restrict__ in_pad, uint64_t n, const double* __restrict__ afs, int K,
+    float2* __restrict__ Y, Fft4Geom g, const float2* __restrict__ tab, int flags) {
+  using C = Cfg<L, CPT, SUB>;
+  __shared__ float lds[C::LDS_FLOATS];
+  constexpr int T = C::T;
+  const int grp = threadIdx.x / T;
+  const int t = threadIdx.x - grp * T;
+  const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
+  const int N1 = g.n1;
+  const uint32_t nbt = static_cast<uint32_t>(N1 / C::CH);  // blocks per trial
+  const bool tslow = flags & kFft4TrialSlow;
+  const int k = static_cast<int>(tslow ? lb / nbt : lb % static_cast<uint32_t>(K));
+  const int c0 = static_cast<int>(tslow ? lb % nbt : lb / static_cast<uint32_t>(K)) * C::CH + grp * CPT;
+  const int log2row = __builtin_ctz(static_cast<unsigned>(2 * N1));
+  const TableOffsets to = table_offsets(N1, L);
+  const double af = afs[k];
+  const double size = static_cast<double>(n);
+  Vec<CPT> v;
 #pragma unroll
   for (int q = 0; q < kPts; ++q) {
-    const uint64_t k1 = t + q * T;
-    float4* dst = reinterpret_cast<float4*>(x + k1 * N2);
+    const uint64_t j = t + q * T;
+    float x[2 * CPT];
+    load_resampled<2 * CPT>(in, in_pad, n, log2row, g.inpitch, af, size, 2 * (static_cast<uint64_t>(N1) * j + c0), x);
 #pragma unroll
-    for (int c = 0; c < kCh; c += 2) dst[c / 2] = make_float4(v[c][q].x, v[c][q].y, v[c + 1][q].x, v[c + 1][q].y);
+    for (int c = 0; c < CPT; ++c) v[c][q] = make_float2(x[2 * c], x[2 * c + 1]);
   }
+  if (!(flags & kFft4SkipCompute)) fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n2);
+  const uint32_t mask = static_cast<uint32_t>(N1) * L - 1;
+  float2* y = Y + static_cast<uint64_t>(k) * g.ystride + c0;
+  const bool nt = flags & kFft4NtStores;
+#pragma unroll
+  for (int q = 0; q < kPts; ++q) {
+    const uint32_t k2 = t + q * T;
+    float2 w = twiddle_M((static_cast<uint32_t>(c0) * k2) & mask, tab + to.lo, tab + to.hi);
+    const float2 step = twiddle_M(k2, tab + to.lo, tab + to.hi);
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+      v[c][q] = cmul(v[c][q], w);
+      w = cmul(w, step);
+    }
+    store_row<CPT>(y + static_cast<uint64_t>(k2) * g.ypitch, v, q, nt);
+  }
+}
+
+// Pass B.  Logical block = row block * K + trial.
+template <int L, int CPT, int SUB>
+__global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2)) fft4_rowpass_kernel(
+    const float2* __restrict__ Y, float2* __restrict__ X, int K, Fft4Geom g, const float2* __restrict__ tab,
+    int flags) {
+  using C = Cfg<L, CPT, SUB>;
+  __shared__ float lds[C::LDS_FLOATS];
+  constexpr int T = C::T;
+  const int grp = threadIdx.x / T;
+  const int t = threadIdx.x - grp * T;
+  const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
+  const uint32_t nbt = static_cast<uint32_t>(g.n2 / C::CH);  // blocks per trial
+  const bool tslow = flags & kFft4TrialSlow;
+  const int k = static_cast<int>(tslow ? lb / nbt : lb % static_cast<uint32_t>(K));
+  const int r0 = static_cast<int>(tslow ? lb % nbt : lb / static_cast<uint32_t>(K)) * C::CH + grp * CPT;
+  const TableOffsets to = table_offsets(L, g.n2);
+  const float2* y = Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(r0) * g.ypitch;
+  Vec<CPT> v;
+#pragma unroll
+  for (int c = 0; c < CPT; ++c)
+#pragma unroll
+    for (int q = 0; q < kPts; ++q) v[c][q] = y[static_cast<uint64_t>(c) * g.ypitch + t + q * T];
+  if (!(flags & kFft4SkipCompute)) fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n1);
+  float2* x = X + static_cast<uint64_t>(k) * g.xstride + r0;
+  const bool nt = flags & kFft4NtStores;
+#pragma unroll
+  for (int q = 0; q < kPts; ++q) store_row<CPT>(x + static_cast<uint64_t>(t + q * T) * g.xpitch, v, q, nt);
 }
 
 bool supported_len(int L) { return L >= 128 && L <= 4096 && (L & (L - 1)) == 0; }
 
 }  // namespace
 
-bool fft4_factor(uint64_t M, int* N1, int* N2) {
-  if (M == 0 || (M & (M - 1)) != 0) return false;
+Fft4Geom fft4_geometry(uint64_t M) {
+  Fft4Geom g;
+  if (M == 0 || (M & (M - 1)) != 0) return g;
   int lg = 0;
   while ((uint64_t(1) << lg) < M) ++lg;
   const int a = lg / 2, b = lg - a;  // N2 = 2^a <= N1 = 2^b
-  if (!supported_len(1 << a) || !supported_len(1 << b)) return false;
-  if (N1) *N1 = 1 << b;
-  if (N2) *N2 = 1 << a;
-  return true;
+  if (!supported_len(1 << a) || !supported_len(1 << b)) return g;
+  g.n1 = 1 << b;
+  g.n2 = 1 << a;
+  g.ypitch = static_cast<uint64_t>(g.n1) + 8;
+  g.ystride = g.ypitch * g.n2;
+  g.xpitch = static_cast<uint64_t>(g.n2) + 8;
+  g.xstride = g.xpitch * g.n1;
+  g.log2_xrow = a;
+  g.inpitch = 2 * static_cast<uint64_t>(g.n1) + 32;
+  g.insize = g.inpitch * g.n2;
+  g.ok = true;
+  return g;
 }
 
-std::vector<float2> fft4_tables(int N1, int N2) {
-  const TableOffsets o = table_offsets(N1, N2);
-  const double M = static_cast<double>(N1) * N2;
+std::vector<float2> fft4_tables(const Fft4Geom& g) {
+  const TableOffsets o = table_offsets(g.n1, g.n2);
+  const double M = static_cast<double>(g.n1) * g.n2;
   std::vector<float2> t(o.total);
   auto w = [](double num, double den) {
     const double a = -2.0 * M_PI * num / den;
     return make_float2(static_cast<float>(std::cos(a)), static_cast<float>(std::sin(a)));
   };
-  for (int m = 0; m < N2; ++m) t[o.n2 + m] = w(m, N2);
-  for (int m = 0; m < N1; ++m) t[o.n1 + m] = w(m, N1);
+  for (int m = 0; m < g.n2; ++m) t[o.n2 + m] = w(m, g.n2);
+  for (int m = 0; m < g.n1; ++m) t[o.n1 + m] = w(m, g.n1);
   for (uint64_t m = 0; m < (1u << kSplit); ++m) t[o.lo + m] = w(static_cast<double>(m), M);
   for (uint64_t m = 0; m < (o.total - o.hi); ++m) t[o.hi + m] = w(static_cast<double>(m << kSplit), M);
   return t;
 }
 
-void fft4_resample_colpass(const float* in, uint64_t n, const double* af, int K, float2* Y, uint64_t ystride, int N1,
-                           int N2, const float2* tables, hipStream_t s) {
-  PSOUP_CHECK(K >= 1 && n == 2ull * N1 * N2 && supported_len(N1) && supported_len(N2),
-              "fft4 colpass: bad geometry n=" << n << " N1=" << N1 << " N2=" << N2 << " K=" << K);
-  PSOUP_CHECK(ystride % 8 == 0 && ystride >= static_cast<uint64_t>(N1) * N2 &&
-                  (reinterpret_cast<uintptr_t>(Y) & 63) == 0,
-              "fft4 colpass: Y alignment/stride");
-  const uint64_t nblocks = static_cast<uint64_t>(N1 / kCh) * K;
-  PSOUP_CHECK(nblocks < (1ull << 31), "fft4 colpass: grid too large");
-  const dim3 grid(static_cast<unsigned>(nblocks));
-  switch (N2) {
-    case 128: fft4_colpass_kernel<128><<<grid, Cfg<128>::T, 0, s>>>(in, n, af, K, Y, ystride, N1, tables); break;
-    case 256: fft4_colpass_kernel<256><<<grid, Cfg<256>::T, 0, s>>>(in, n, af, K, Y, ystride, N1, tables); break;
-    case 512: fft4_colpass_kernel<512><<<grid, Cfg<512>::T, 0, s>>>(in, n, af, K, Y, ystride, N1, tables); break;
-    case 1024: fft4_colpass_kernel<1024><<<grid, Cfg<1024>::T, 0, s>>>(in, n, af, K, Y, ystride, N1, tables); break;
-    case 2048: fft4_colpass_kernel<2048><<<grid, Cfg<2048>::T, 0, s>>>(in, n, af, K, Y, ystride, N1, tables); break;
-    default: fft4_colpass_kernel<4096><<<grid, Cfg<4096>::T, 0, s>>>(in, n, af, K, Y, ystride, N1, tables); break;
+void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& g, hipStream_t s) {
+  PSOUP_CHECK(g.ok && n == 2ull * g.n1 * g.n2, "fft4 pad: bad geometry");
+  fft4_pad_input_kernel<<<dev::grid_for(g.insize, 256, 4096), 256, 0, s>>>(in, n, in_pad, 2ull * g.n1, g.inpitch,
+                                                                          g.insize);
+  post_launch_check("fft4_pad_input_kernel", s);
+}
+
+namespace {
+int g_fft4_flags = 0;
+
+template <int CPT, int SUB>
+void launch_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
+                    const Fft4Geom& g, const float2* tables, dim3 grid, int flags, hipStream_t s) {
+  switch (g.n2) {
+#define PS_CASE(LL)                                                                                       \
+  case LL:                                                                                                \
+    if constexpr (Cfg<LL, CPT, SUB>::THREADS <= 1024)                                                     \
+      fft4_colpass_kernel<LL, CPT, SUB><<<grid, Cfg<LL, CPT, SUB>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g, \
+                                                                                      tables, flags);     \
+    else                                                                                                  \
+      PSOUP_THROW("fft4: workgroup too large");                                                           \
+    break;
+    PS_CASE(128) PS_CASE(256) PS_CASE(512) PS_CASE(1024) PS_CASE(2048) PS_CASE(4096)
+#undef PS_CASE
+    default: PSOUP_THROW("fft4: unsupported column length " << g.n2);
   }
+}
+
+template <int CPT, int SUB>
+void launch_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, dim3 grid, int flags,
+                    hipStream_t s) {
+  switch (g.n1) {
+#define PS_CASE(LL)                                                                                    \
+  case LL:                                                                                             \
+    if constexpr (Cfg<LL, CPT, SUB>::THREADS <= 1024)                                                  \
+      fft4_rowpass_kernel<LL, CPT, SUB><<<grid, Cfg<LL, CPT, SUB>::THREADS, 0, s>>>(Y, X, K, g, tables, flags); \
+    else                                                                                               \
+      PSOUP_THROW("fft4: workgroup too large");                                                        \
+    break;
+    PS_CASE(128) PS_CASE(256) PS_CASE(512) PS_CASE(1024) PS_CASE(2048) PS_CASE(4096)
+#undef PS_CASE
+    default: PSOUP_THROW("fft4: unsupported row length " << g.n1);
+  }
+}
+}  // namespace
+
+void fft4_set_flags(int flags) { g_fft4_flags = flags; }
+int fft4_flags() { return g_fft4_flags; }
+
+void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
+                           const Fft4Geom& g, const float2* tables, hipStream_t s) {
+  PSOUP_CHECK(g.ok && K >= 1 && n == 2ull * g.n1 * g.n2, "fft4 colpass: bad geometry n=" << n << " K=" << K);
+  PSOUP_CHECK((reinterpret_cast<uintptr_t>(Y) & 63) == 0, "fft4 colpass: Y alignment");
+  const int f = g_fft4_flags;
+  const int ch = (f & kFft4Wide) ? 16 : 8;
+  const uint64_t nblocks = static_cast<uint64_t>(g.n1 / ch) * K;
+  PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 8 == 0, "fft4 colpass: grid");
+  const dim3 grid(static_cast<unsigned>(nblocks));
+  if ((f & kFft4Wide) && (f & kFft4Cpt8))
+    launch_colpass<8, 2>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  else if (f & kFft4Wide)
+    launch_colpass<4, 4>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  else if (f & kFft4Cpt8)
+    launch_colpass<8, 1>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  else
+    launch_colpass<4, 2>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   post_launch_check("fft4_colpass_kernel", s);
 }
 
-void fft4_rowpass(const float2* Y, uint64_t ystride, float2* X, uint64_t xstride, int K, int N1, int N2,
-                  const float2* tables, hipStream_t s) {
-  PSOUP_CHECK(K >= 1 && supported_len(N1) && supported_len(N2), "fft4 rowpass: bad geometry");
-  PSOUP_CHECK(xstride % 8 == 0 && xstride >= static_cast<uint64_t>(N1) * N2 &&
-                  (reinterpret_cast<uintptr_t>(X) & 63) == 0,
-              "fft4 rowpass: X alignment/stride");
-  const dim3 grid(static_cast<unsigned>(static_cast<uint64_t>(N2 / kCh) * K));
-  switch (N1) {
-    case 128: fft4_rowpass_kernel<128><<<grid, Cfg<128>::T, 0, s>>>(Y, ystride, X, xstride, K, N2, tables); break;
-    case 256: fft4_rowpass_kernel<256><<<grid, Cfg<256>::T, 0, s>>>(Y, ystride, X, xstride, K, N2, tables); break;
-    case 512: fft4_rowpass_kernel<512><<<grid, Cfg<512>::T, 0, s>>>(Y, ystride, X, xstride, K, N2, tables); break;
-    case 1024: fft4_rowpass_kernel<1024><<<grid, Cfg<1024>::T, 0, s>>>(Y, ystride, X, xstride, K, N2, tables); break;
-    case 2048: fft4_rowpass_kernel<2048><<<grid, Cfg<2048>::T, 0, s>>>(Y, ystride, X, xstride, K, N2, tables); break;
-    default: fft4_rowpass_kernel<4096><<<grid, Cfg<4096>::T, 0, s>>>(Y, ystride, X, xstride, K, N2, tables); break;
-  }
+void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, hipStream_t s) {
+  PSOUP_CHECK(g.ok && K >= 1, "fft4 rowpass: bad geometry");
+  PSOUP_CHECK((reinterpret_cast<uintptr_t>(X) & 63) == 0, "fft4 rowpass: X alignment");
+  const int f = g_fft4_flags;
+  const int ch = (f & kFft4Wide) ? 16 : 8;
+  const uint64_t nblocks = static_cast<uint64_t>(g.n2 / ch) * K;
+  PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 8 == 0, "fft4 rowpass: grid");
+  const dim3 grid(static_cast<unsigned>(nblocks));
+  if ((f & kFft4Wide) && (f & kFft4Cpt8))
+    launch_rowpass<8, 2>(Y, X, K, g, tables, grid, f, s);
+  else if (f & kFft4Wide)
+    launch_rowpass<4, 4>(Y, X, K, g, tables, grid, f, s);
+  else if (f & kFft4Cpt8)
+    launch_rowpass<8, 1>(Y, X, K, g, tables, grid, f, s);
+  else
+    launch_rowpass<4, 2>(Y, X, K, g, tables, grid, f, s);
   post_launch_check("fft4_rowpass_kernel", s);
 }
 

@@ -47,11 +47,9 @@ __global__ void __launch_bounds__(256) interbin_normalise_batch_kernel(const flo
 // Real-input FFT recovered from an M = N/2 point complex FFT of the packed
 // series z[m] = x[2m] + i x[2m+1]:
 //   X[k] = (Z[k] + conj Z[M-k])/2 - i/2 e^{-2 pi i k/N} (Z[k] - conj Z[M-k]),  k = 0..M
-// (indices mod M).  Replaces rocFFT's separate r2c post-processing pass.
-__device__ __forceinline__ float2 r2c_bin(const float2* __restrict__ z, uint64_t M, uint64_t k) {
-  const uint64_t a = (k == M) ? 0 : k;
-  const uint64_t b = (k == 0) ? 0 : M - k;
-  const float2 za = z[a], zb = z[b];
+// (indices mod M); za = Z[k mod M], zb = Z[(M-k) mod M].  Replaces rocFFT's
+// separate r2c post-processing pass.
+__device__ __forceinline__ float2 r2c_combine(float2 za, float2 zb, uint64_t k, uint64_t M) {
   const float ex = 0.5f * (za.x + zb.x), ey = 0.5f * (za.y - zb.y);
   const float dx = 0.5f * (za.x - zb.x), dy = 0.5f * (za.y + zb.y);
   const float ox = dy, oy = -dx;  // -i * d
@@ -60,25 +58,50 @@ __device__ __forceinline__ float2 r2c_bin(const float2* __restrict__ z, uint64_t
   return make_float2(ex + c * ox - s * oy, ey + c * oy + s * ox);
 }
 
+__device__ __forceinline__ uint64_t zaddr(uint64_t k, int log2_row, uint64_t pitch) {
+  return (k >> log2_row) * pitch + (k & ((uint64_t(1) << log2_row) - 1));
+}
+
+// One workgroup per tile of 256 bins k in [k0, k0+256), k <= M/2: both the
+// ascending bins k and their mirrors M-k come from the same loads
+// Z[k], Z[M-k]; one halo bin each side feeds the interbin neighbour.
 __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
-    const float2* __restrict__ Z, uint64_t M, uint64_t zstride, float* __restrict__ P, uint64_t pstride,
-    uint64_t nbins_out, const float* __restrict__ stats, float nscale) {
-  __shared__ float2 X[257];
+    const float2* __restrict__ Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t pitch, float* __restrict__ P,
+    uint64_t pstride, uint64_t nbins_out, const float* __restrict__ stats, float nscale) {
+  __shared__ float2 A[258];  // A[u] = X[k0 - 1 + u]
+  __shared__ float2 D[258];  // D[u] = X[M - (k0 - 1 + u)]
   const int kk = blockIdx.y;
+  const int t = threadIdx.x;
   const float2* z = Z + static_cast<uint64_t>(kk) * zstride;
   float* p = P + static_cast<uint64_t>(kk) * pstride;
   const float mean = stats[0] * nscale;
   const float sigma = stats[2] * nscale;
-  for (uint64_t k0 = static_cast<uint64_t>(blockIdx.x) * 256; k0 < nbins_out; k0 += static_cast<uint64_t>(gridDim.x) * 256) {
-    const uint64_t k = k0 + threadIdx.x;
-    X[threadIdx.x + 1] = (k <= M) ? r2c_bin(z, M, k) : make_float2(0.f, 0.f);
-    if (threadIdx.x == 0) X[0] = (k0 > 0) ? r2c_bin(z, M, k0 - 1) : make_float2(0.f, 0.f);
+  const uint64_t half = M / 2;
+  auto pair = [&](int64_t k, int u) {
+    if (k < 0 || static_cast<uint64_t>(k) > half + 1) {
+      A[u] = D[u] = make_float2(0.f, 0.f);
+      return;
+    }
+    const uint64_t uk = static_cast<uint64_t>(k);
+    const uint64_t a = uk & (M - 1), b = (M - uk) & (M - 1);
+    const float2 za = z[zaddr(a, log2_row, pitch)], zb = z[zaddr(b, log2_row, pitch)];
+    A[u] = r2c_combine(za, zb, uk, M);
+    D[u] = r2c_combine(zb, za, M - uk, M);
+  };
+  for (uint64_t k0 = static_cast<uint64_t>(blockIdx.x) * 256; k0 <= half;
+       k0 += static_cast<uint64_t>(gridDim.x) * 256) {
+    pair(static_cast<int64_t>(k0 + t), t + 1);
+    if (t == 0) pair(static_cast<int64_t>(k0) - 1, 0);
+    if (t == 1) pair(static_cast<int64_t>(k0 + 256), 257);
     __syncthreads();
-    if (k < nbins_out) {
-      float v = dev::interbin(X[threadIdx.x + 1], X[threadIdx.x]);
-      v -= mean;
-      v /= sigma;
-      p[k] = v;
+    const uint64_t k = k0 + t;
+    if (k <= half) {
+      if (k < nbins_out) {
+        const float2 xl = k > 0 ? A[t] : make_float2(0.f, 0.f);
+        p[k] = (dev::interbin(A[t + 1], xl) - mean) / sigma;
+      }
+      const uint64_t j = M - k;  // mirrored bin (> M/2), neighbour X[j-1] = D[t+2]
+      if (j > half && j < nbins_out) p[j] = (dev::interbin(D[t + 1], D[t + 2]) - mean) / sigma;
     }
     __syncthreads();
   }
@@ -188,13 +211,17 @@ void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride,
   post_launch_check("interbin_normalise_batch_kernel", s);
 }
 
-void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride, float* P, uint64_t pstride, int K,
-                                  uint64_t nbins_out, const float* stats, float nscale, hipStream_t s) {
+void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t row_pitch,
+                                  float* P, uint64_t pstride, int K, uint64_t nbins_out, const float* stats,
+                                  float nscale, hipStream_t s) {
   PSOUP_CHECK(K >= 1 && K <= 65535, "bad batch");
+  PSOUP_CHECK(M >= 2 && (M & (M - 1)) == 0, "r2c: M must be a power of two");
   PSOUP_CHECK(nbins_out <= M + 1, "nbins_out beyond the spectrum");
+  PSOUP_CHECK(log2_row >= 0 && log2_row < 63 && (uint64_t(1) << log2_row) <= M, "r2c: bad row layout");
   if (nbins_out == 0) return;
-  dim3 grid(dev::grid_for(nbins_out, 256, 1024), static_cast<unsigned>(K));
-  r2c_interbin_normalise_batch_kernel<<<grid, 256, 0, s>>>(Z, M, zstride, P, pstride, nbins_out, stats, nscale);
+  dim3 grid(dev::grid_for(M / 2 + 1, 256, 2048), static_cast<unsigned>(K));
+  r2c_interbin_normalise_batch_kernel<<<grid, 256, 0, s>>>(Z, M, zstride, log2_row, row_pitch, P, pstride, nbins_out,
+                                                           stats, nscale);
   post_launch_check("r2c_interbin_normalise_batch_kernel", s);
 }
 

@@ -423,31 +423,42 @@ PYBIND11_MODULE(_C, m) {
     kern::interbin_normalise_batch(P<const float2>(X), nb, xstride, P<float>(Pout), pstride, K, nbo,
                                    P<const float>(stats), nscale, S(s));
   });
-  k.def("r2c_interbin_normalise_batch", [](uintptr_t Z, uint64_t M, uint64_t zstride, uintptr_t Pout,
-                                           uint64_t pstride, int K, uint64_t nbo, uintptr_t stats, float nscale,
-                                           uintptr_t s) {
-    kern::r2c_interbin_normalise_batch(P<const float2>(Z), M, zstride, P<float>(Pout), pstride, K, nbo,
-                                       P<const float>(stats), nscale, S(s));
+  k.def("r2c_interbin_normalise_batch", [](uintptr_t Z, uint64_t M, uint64_t zstride, int log2_row,
+                                           uint64_t row_pitch, uintptr_t Pout, uint64_t pstride, int K, uint64_t nbo,
+                                           uintptr_t stats, float nscale, uintptr_t s) {
+    kern::r2c_interbin_normalise_batch(P<const float2>(Z), M, zstride, log2_row, row_pitch, P<float>(Pout), pstride,
+                                       K, nbo, P<const float>(stats), nscale, S(s));
   });
-  k.def("fft4_factor", [](uint64_t M) {
-    int n1 = 0, n2 = 0;
-    bool ok = kern::fft4_factor(M, &n1, &n2);
-    return py::make_tuple(ok, n1, n2);
-  });
-  k.def("fft4_tables", [](int n1, int n2) {
-    auto t = kern::fft4_tables(n1, n2);
+  py::class_<kern::Fft4Geom>(k, "Fft4Geom")
+      .def_readonly("ok", &kern::Fft4Geom::ok)
+      .def_readonly("n1", &kern::Fft4Geom::n1)
+      .def_readonly("n2", &kern::Fft4Geom::n2)
+      .def_readonly("ypitch", &kern::Fft4Geom::ypitch)
+      .def_readonly("ystride", &kern::Fft4Geom::ystride)
+      .def_readonly("xpitch", &kern::Fft4Geom::xpitch)
+      .def_readonly("xstride", &kern::Fft4Geom::xstride)
+      .def_readonly("log2_xrow", &kern::Fft4Geom::log2_xrow)
+      .def_readonly("inpitch", &kern::Fft4Geom::inpitch)
+      .def_readonly("insize", &kern::Fft4Geom::insize);
+  k.def("fft4_geometry", &kern::fft4_geometry);
+  k.def("fft4_set_flags", &kern::fft4_set_flags);
+  k.def("fft4_flags", &kern::fft4_flags);
+  k.def("fft4_tables", [](const kern::Fft4Geom& g) {
+    auto t = kern::fft4_tables(g);
     py::array_t<float> a({static_cast<py::ssize_t>(t.size()), static_cast<py::ssize_t>(2)});
     std::memcpy(a.mutable_data(), t.data(), t.size() * sizeof(float2));
     return a;
   });
-  k.def("fft4_resample_colpass", [](uintptr_t in, uint64_t n, uintptr_t af, int K, uintptr_t Y, uint64_t ystride,
-                                    int n1, int n2, uintptr_t tab, uintptr_t s) {
-    kern::fft4_resample_colpass(P<const float>(in), n, P<const double>(af), K, P<float2>(Y), ystride, n1, n2,
-                                P<const float2>(tab), S(s));
+  k.def("fft4_pad_input", [](uintptr_t in, uint64_t n, uintptr_t out, const kern::Fft4Geom& g, uintptr_t s) {
+    kern::fft4_pad_input(P<const float>(in), n, P<float>(out), g, S(s));
   });
-  k.def("fft4_rowpass", [](uintptr_t Y, uint64_t ystride, uintptr_t X, uint64_t xstride, int K, int n1, int n2,
-                           uintptr_t tab, uintptr_t s) {
-    kern::fft4_rowpass(P<const float2>(Y), ystride, P<float2>(X), xstride, K, n1, n2, P<const float2>(tab), S(s));
+  k.def("fft4_resample_colpass", [](uintptr_t in, uintptr_t in_pad, uint64_t n, uintptr_t af, int K, uintptr_t Y,
+                                    const kern::Fft4Geom& g, uintptr_t tab, uintptr_t s) {
+    kern::fft4_resample_colpass(P<const float>(in), P<const float>(in_pad), n, P<const double>(af), K, P<float2>(Y),
+                                g, P<const float2>(tab), S(s));
+  });
+  k.def("fft4_rowpass", [](uintptr_t Y, uintptr_t X, int K, const kern::Fft4Geom& g, uintptr_t tab, uintptr_t s) {
+    kern::fft4_rowpass(P<const float2>(Y), P<float2>(X), K, g, P<const float2>(tab), S(s));
   });
   k.def("harmonic_peaks_batch", [](uintptr_t Pin, uint64_t nb, uint64_t pstride, int K, int nlevels,
                                    const std::vector<int>& start, const std::vector<int>& end, float thresh,

@@ -196,6 +196,12 @@ std::vector<uint32_t> build_zap_mask(const std::vector<float>& freqs, const std:
 }
 
 // ----------------------------------------------------------- search engine --
+static int ilog2(uint64_t v) {
+  int l = 0;
+  while ((uint64_t(1) << (l + 1)) <= v) ++l;
+  return l;
+}
+
 SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     : p_(p),
       stream_(stream),
@@ -212,13 +218,15 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   wh_ = std::make_unique<Whitener>(n_, p_.tsamp, stream_);
   tim_.resize(n_);
   mode_ = (n_ % 2 == 0) ? std::min(std::max(p_.fft_mode, 0), 2) : 0;
-  if (mode_ == 2 && !kern::fft4_factor(n_ / 2, &f4_n1_, &f4_n2_)) mode_ = 1;
+  if (mode_ == 2) f4_ = kern::fft4_geometry(n_ / 2);
+  if (mode_ == 2 && !f4_.ok) mode_ = 1;
   if (mode_ == 2) {
-    auto tab = kern::fft4_tables(f4_n1_, f4_n2_);
+    auto tab = kern::fft4_tables(f4_);
     f4_tab_.resize(tab.size());
     PSOUP_HIP_CHECK(hipMemcpy(f4_tab_.data(), tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice));
+    f4_in_.resize(f4_.insize);
   }
-  xs_ = mode_ == 2 ? (n_ / 2 + 8) : nb_;
+  xs_ = mode_ == 2 ? f4_.xstride : nb_;
   if (!p_.zap_freqs.empty()) {
     auto mask = build_zap_mask(p_.zap_freqs, p_.zap_widths, bin_width_, nb_);
     zapmask_.resize(mask.size());
@@ -274,8 +282,9 @@ void SearchEngine::grow_capacity(uint32_t need) {
 }
 
 void SearchEngine::ensure_batch_buffers() {
-  if (res_.size() >= static_cast<uint64_t>(K_) * n_) return;
-  res_.resize(static_cast<uint64_t>(K_) * n_);
+  const uint64_t rs = mode_ == 2 ? 2 * f4_.ystride : n_;  // floats per trial
+  if (res_.size() >= static_cast<uint64_t>(K_) * rs) return;
+  res_.resize(static_cast<uint64_t>(K_) * rs);
   spec_.resize(static_cast<uint64_t>(K_) * xs_);
   P_.resize(static_cast<uint64_t>(K_) * std::max<uint64_t>(1, static_cast<uint64_t>(hi_)));
 }
@@ -299,16 +308,18 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
   if (mode_ == 2) {
     // res_ holds the K four-step intermediates Y (complex, M per trial)
     float2* Y = reinterpret_cast<float2*>(res_.data());
-    kern::fft4_resample_colpass(tim_.data(), n_, af_.data() + first, count, Y, n_ / 2, f4_n1_, f4_n2_,
-                                f4_tab_.data(), stream_);
-    kern::fft4_rowpass(Y, n_ / 2, spec_.data(), xs_, count, f4_n1_, f4_n2_, f4_tab_.data(), stream_);
+    kern::fft4_resample_colpass(tim_.data(), f4_in_.data(), n_, af_.data() + first, count, Y, f4_, f4_tab_.data(),
+                                stream_);
+    kern::fft4_rowpass(Y, spec_.data(), count, f4_, f4_tab_.data(), stream_);
   } else {
     kern::resample_batch(tim_.data(), n_, res_.data(), n_, af_.data() + first, count, stream_);
     batch_plan(count).execute(res_.data(), spec_.data(), stream_);
   }
   const uint64_t pst = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
+  const int zrow_log2 = mode_ == 2 ? f4_.log2_xrow : ilog2(n_ / 2);
+  const uint64_t zrow_pitch = mode_ == 2 ? f4_.xpitch : n_ / 2;
   if (mode_ >= 1)
-    kern::r2c_interbin_normalise_batch(spec_.data(), n_ / 2, xs_, P_.data(), pst, count, static_cast<uint64_t>(hi_),
+    kern::r2c_interbin_normalise_batch(spec_.data(), n_ / 2, xs_, zrow_log2, zrow_pitch, P_.data(), pst, count, static_cast<uint64_t>(hi_),
                                        wh_->stats(), static_cast<float>(n_), stream_);
   else
     kern::interbin_normalise_batch(spec_.data(), nb_, nb_, P_.data(), pst, count, static_cast<uint64_t>(hi_),
@@ -374,6 +385,7 @@ CandidateList SearchEngine::search_trial(const uint8_t* d_trial, uint64_t nsamps
   sw.start();
   wh_->load_trial(d_trial, nsamps, tim_.data());
   wh_->whiten(tim_.data(), zap_ ? zapmask_.data() : nullptr, true, p_.boundary_5_freq, p_.boundary_25_freq);
+  if (mode_ == 2) kern::fft4_pad_input(tim_.data(), n_, f4_in_.data(), f4_, stream_);
   ctr_.dm_trials++;
   const int nacc = static_cast<int>(accs.size());
   CandidateList accel_trial_cands;

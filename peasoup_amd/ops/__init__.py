@@ -14,6 +14,7 @@ from .core import (  # noqa: F401
     convert_pad,
     dedisperse,
     deredden,
+    fft4_resample_interbin,
     fft4_resample_spectrum,
     fold_optimise,
     fold_series,

@@ -193,8 +193,8 @@ def r2c_interbin_normalise(x: torch.Tensor, stats: torch.Tensor, nscale: float,
     Z = torch.fft.fft(torch.view_as_complex(x.contiguous().view(Kb, M, 2)), dim=-1).contiguous()
     nbo = nbins_out or (M + 1)
     P = torch.empty((Kb, nbo), dtype=torch.float32, device=x.device)
-    K.r2c_interbin_normalise_batch(_cplx_ptr(Z), M, M, P.data_ptr(), nbo, Kb, nbo, stats.data_ptr(),
-                                   float(nscale), _s())
+    K.r2c_interbin_normalise_batch(_cplx_ptr(Z), M, M, M.bit_length() - 1, M, P.data_ptr(), nbo, Kb, nbo,
+                                   stats.data_ptr(), float(nscale), _s())
     return P
 
 
@@ -216,24 +216,45 @@ def _accel_factors(accels: Sequence[float], tsamp: float, device) -> torch.Tenso
                          / (2 * 299792458.0) for a in accels], dtype=torch.float64, device=device)
 
 
+def _fft4_padded(x: torch.Tensor, accels: Sequence[float], tsamp: float):
+    _check(x, torch.float32, "x")
+    n = x.numel()
+    g = K.fft4_geometry(n // 2)
+    if not g.ok or n % 2:
+        raise ValueError(f"fft4: unsupported length {n}")
+    tab = torch.from_numpy(K.fft4_tables(g)).to(x.device)
+    af = _accel_factors(accels, tsamp, x.device)
+    Kb = len(accels)
+    xp = torch.empty(g.insize, dtype=torch.float32, device=x.device)
+    Y = torch.empty((Kb, g.ystride, 2), dtype=torch.float32, device=x.device)
+    X = torch.empty((Kb, g.xstride, 2), dtype=torch.float32, device=x.device)
+    K.fft4_pad_input(x.data_ptr(), n, xp.data_ptr(), g, _s())
+    K.fft4_resample_colpass(x.data_ptr(), xp.data_ptr(), n, af.data_ptr(), Kb, Y.data_ptr(), g, tab.data_ptr(), _s())
+    K.fft4_rowpass(Y.data_ptr(), X.data_ptr(), Kb, g, tab.data_ptr(), _s())
+    return g, X
+
+
 def fft4_resample_spectrum(x: torch.Tensor, accels: Sequence[float], tsamp: float) -> torch.Tensor:
     """Fused resample + four-step FFT: returns Z [K, N/2] complex64 with
     Z[k] = FFT_{N/2}(z_k), z_k[m] = r_k[2m] + i r_k[2m+1], r_k = resample(x, accels[k])."""
-    _check(x, torch.float32, "x")
-    n = x.numel()
-    ok, n1, n2 = K.fft4_factor(n // 2)
-    if not ok or n % 2:
-        raise ValueError(f"fft4: unsupported length {n}")
-    M = n // 2
-    tab = torch.from_numpy(K.fft4_tables(n1, n2)).to(x.device)
-    af = _accel_factors(accels, tsamp, x.device)
-    Kb = len(accels)
-    Y = torch.empty((Kb, M, 2), dtype=torch.float32, device=x.device)
-    Z = torch.empty((Kb, M, 2), dtype=torch.float32, device=x.device)
-    K.fft4_resample_colpass(x.data_ptr(), n, af.data_ptr(), Kb, Y.data_ptr(), M, n1, n2, tab.data_ptr(), _s())
-    K.fft4_rowpass(Y.data_ptr(), M, Z.data_ptr(), M, Kb, n1, n2, tab.data_ptr(), _s())
-    torch.cuda.current_stream().synchronize()  # keep `tab`/`Y` alive until the passes ran
-    return torch.view_as_complex(Z)
+    g, X = _fft4_padded(x, accels, tsamp)
+    Kb = X.shape[0]
+    Z = X.view(Kb, g.n1, g.xpitch, 2)[:, :, : g.n2].reshape(Kb, g.n1 * g.n2, 2)
+    return torch.view_as_complex(Z.contiguous())
+
+
+def fft4_resample_interbin(x: torch.Tensor, accels: Sequence[float], tsamp: float, stats: torch.Tensor,
+                           nscale: float) -> torch.Tensor:
+    """The search hot path of fft_mode 2: fused resample + four-step FFT, then
+    the paired real-FFT post-processing + interbin + normalise on the padded
+    spectrum layout.  Returns P [K, N/2 + 1]."""
+    g, X = _fft4_padded(x, accels, tsamp)
+    Kb = X.shape[0]
+    M = g.n1 * g.n2
+    P = torch.empty((Kb, M + 1), dtype=torch.float32, device=x.device)
+    K.r2c_interbin_normalise_batch(X.data_ptr(), M, g.xstride, g.log2_xrow, g.xpitch, P.data_ptr(), M + 1, Kb, M + 1,
+                                   stats.data_ptr(), float(nscale), _s())
+    return P
 
 
 def resample_v1(x: torch.Tensor, accel: float, tsamp: float) -> torch.Tensor:

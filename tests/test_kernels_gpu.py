@@ -296,3 +296,22 @@ def test_coincidence_and_correlation_ops():
     exp = np.conj(x.cpu().numpy()) * y.cpu().numpy()
     ops.cmul_(ops.conjugate(x), y)
     assert np.allclose(y.cpu().numpy(), exp, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("log2n", [16, 21])
+def test_fft4_interbin_path_matches_rocfft_path(log2n):
+    """fft_mode 2 hot path (padded spectrum layout) == resample + C2C + r2c post."""
+    from peasoup_amd import ops
+
+    rng = np.random.default_rng(100 + log2n)
+    n = 1 << log2n
+    x = torch.from_numpy(rng.standard_normal(n).astype(np.float32)).to(dev)
+    accs = [-300.0, 0.0, 410.0]
+    st = torch.tensor([1.0, 2.0, 0.5, 0.0], dtype=torch.float32, device=dev)
+    P2 = ops.fft4_resample_interbin(x, accs, 64e-6, st, float(n)).cpu().numpy()
+    R = ops.resample(x, accs, 64e-6).contiguous()
+    P1 = ops.r2c_interbin_normalise(R, st, float(n)).cpu().numpy()
+    assert P2.shape == P1.shape == (3, n // 2 + 1)
+    scale = np.abs(P1).max()
+    assert np.abs(P2 - P1).max() / scale < 1e-4
+    assert np.sqrt(np.mean((P2 - P1) ** 2)) / np.sqrt(np.mean(P1 ** 2)) < 1e-5

@@ -1,0 +1,103 @@
+#!/usr/bin/env python3
+"""Per-kernel microbenchmark of the acceleration-search hot path at the
+headline size (2^23-point series, K trials per batch), with HIP-event timing.
+
+    python tools/kbench.py [--log2n 23] [--K 32] [--reps 10] [--flags 0,1,2,4]
+
+Prints one line per (kernel, variant): time per launch, per trial, and the
+effective HBM bandwidth of the bytes the kernel must move.
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from peasoup_amd import _C  # noqa: E402
+
+K_ = _C.kernels
+
+
+def timeit(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / reps  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--log2n", type=int, default=23)
+    ap.add_argument("--K", type=int, default=32)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--flags", default="0,1,2,4,5")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    n = 1 << a.log2n
+    M = n // 2
+    K = a.K
+    s = torch.cuda.current_stream().cuda_stream
+    g = K_.fft4_geometry(M)
+    assert g.ok
+    x = torch.randn(n, device=dev)
+    tab = torch.from_numpy(K_.fft4_tables(g)).to(dev)
+    tsamp = 64e-6
+    accs = np.linspace(-500, 500, K)
+    af = torch.tensor([a_ * tsamp / (2 * 299792458.0) for a_ in accs], dtype=torch.float64, device=dev)
+    xp = torch.empty(g.insize, device=dev)
+    Y = torch.empty(K * g.ystride * 2, device=dev)
+    X = torch.empty(K * g.xstride * 2, device=dev)
+    P = torch.empty(K * (M + 1), device=dev)
+    st = torch.tensor([1.0, 2.0, 0.5, 0.0], device=dev)
+    GB = 1e9
+    rows = []
+
+    def report(name, us, nbytes):
+        rows.append((name, us))
+        print(f"{name:44s} {us:9.1f} us/launch {us / K:8.2f} us/trial {nbytes / (us * 1e-6) / GB:8.0f} GB/s",
+              flush=True)
+
+    big = torch.empty(K * M * 2, device=dev)
+    big2 = torch.empty_like(big)
+    report("torch copy (K*M complex)", timeit(lambda: big2.copy_(big), a.reps), 2 * big.numel() * 4)
+    del big, big2
+    K_.fft4_pad_input(x.data_ptr(), n, xp.data_ptr(), g, s)
+    report("pad_input", timeit(lambda: K_.fft4_pad_input(x.data_ptr(), n, xp.data_ptr(), g, s), a.reps) * K,
+           2 * 4 * n)
+    for f in [int(v) for v in a.flags.split(",")]:
+        K_.fft4_set_flags(f)
+        tc = timeit(lambda: K_.fft4_resample_colpass(x.data_ptr(), xp.data_ptr(), n, af.data_ptr(), K, Y.data_ptr(), g,
+                                                     tab.data_ptr(), s), a.reps)
+        report(f"colpass flags={f}", tc, K * 8 * M)
+        tr = timeit(lambda: K_.fft4_rowpass(Y.data_ptr(), X.data_ptr(), K, g, tab.data_ptr(), s), a.reps)
+        report(f"rowpass flags={f}", tr, K * 16 * M)
+    K_.fft4_set_flags(0)
+    tz = timeit(lambda: K_.r2c_interbin_normalise_batch(X.data_ptr(), M, g.xstride, g.log2_xrow, g.xpitch, P.data_ptr(),
+                                                        M + 1, K, M + 1, st.data_ptr(), float(n), s), a.reps)
+    report("r2c_interbin_normalise", tz, K * (8 * M + 4 * M))
+    # harmonic peaks on normal noise (threshold 9 -> few peaks)
+    P.normal_()
+    nb = M + 1
+    cap = 1 << 20
+    out = torch.empty(cap * 3, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    starts = [1, 2, 4, 8, 16]
+    ends = [nb] * 5
+
+    def harm():
+        cnt.zero_()
+        K_.harmonic_peaks_batch(P.data_ptr(), nb, nb, K, 3, starts, ends, 9.0, cap, out.data_ptr(), cnt.data_ptr(), s)
+
+    th = timeit(harm, a.reps)
+    report("harmonic_peaks (3 levels)", th, K * 4 * M)
+
+
+if __name__ == "__main__":
+    main()
