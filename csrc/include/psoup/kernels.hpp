@@ -111,12 +111,12 @@ void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride,
 
 // Same output from the M = N/2 point complex FFT Z[K] of the packed real
 // series (real-FFT post-processing fused in; saves the separate r2c pass).
-// Bin k of Z[k] lives at (k >> log2_row)*row_pitch + (k & (2^log2_row - 1))
-// (log2_row = log2 M, row_pitch = M for a plain array).  Each thread forms
-// the bin pair (k, M-k) from one pair of loads.
+// Bin k = k2 + 2^log2_row * k1 of Z lives at (k2 >> 3)*blk_pitch + k1*row_pitch + (k2 & 7)
+// (plain array: log2_row = log2 M, row_pitch = M, blk_pitch = 8).  Each
+// thread forms the bin pair (k, M-k) from one pair of loads.
 void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t row_pitch,
-                                  float* P, uint64_t pstride, int K, uint64_t nbins_out, const float* stats,
-                                  float nscale, hipStream_t s);
+                                  uint64_t blk_pitch, float* P, uint64_t pstride, int K, uint64_t nbins_out,
+                                  const float* stats, float nscale, hipStream_t s);
 
 // Fused resample + four-step FFT (fft4step.hip).  M = N/2 = n1*n2 with
 // n1, n2 powers of two in [128, 4096], n2 <= n1 <= 2 n2.  Intermediates use
@@ -149,6 +149,9 @@ enum Fft4Flags : int {
   kFft4SkipCompute = 8,  // timing only: memory traffic without the FFT
   kFft4Wide = 16,        // 16 transforms per workgroup (128-byte segments, one workgroup per CU)
   kFft4TrialSlow = 32,   // block order: column/row block fastest, trial slowest (write locality)
+  kFft4SkipLoad = 64,    // timing only: synthetic inputs instead of global loads
+  kFft4SkipStore = 128,  // timing only: no global stores
+  kFft4Blocked = 256,    // blocked Y/X layouts: every lane stores 64 contiguous bytes (CPT 8 only)
 };
 void fft4_set_flags(int flags);
 int fft4_flags();

@@ -294,7 +294,13 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
   for (int q = 0; q < kPts; ++q) {
     const uint64_t j = t + q * T;
     float x[2 * CPT];
-    load_resampled<2 * CPT>(in, in_pad, n, log2row, g.inpitch, af, size, 2 * (static_cast<uint64_t>(N1) * j + c0), x);
+    if (flags & kFft4SkipLoad) {
+#pragma unroll
+      for (int e = 0; e < 2 * CPT; ++e) x[e] = static_cast<float>(j + e);
+    } else {
+      load_resampled<2 * CPT>(in, in_pad, n, log2row, g.inpitch, af, size, 2 * (static_cast<uint64_t>(N1) * j + c0),
+                              x);
+    }
 #pragma unroll
     for (int c = 0; c < CPT; ++c) v[c][q] = make_float2(x[2 * c], x[2 * c + 1]);
   }
@@ -312,7 +318,10 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
       v[c][q] = cmul(v[c][q], w);
       w = cmul(w, step);
     }
-    store_row<CPT>(y + static_cast<uint64_t>(k2) * g.ypitch, v, q, nt);
+    float2* dst = (flags & kFft4Blocked)
+                      ? Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(c0) * g.n2 + k2 * CPT
+                      : y + static_cast<uint64_t>(k2) * g.ypitch;
+    if (!(flags & kFft4SkipStore) || v[0][q].x == 1234.5f) store_row<CPT>(dst, v, q, nt);
   }
 }
 
@@ -333,16 +342,29 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
   const int r0 = static_cast<int>(tslow ? lb % nbt : lb / static_cast<uint32_t>(K)) * C::CH + grp * CPT;
   const TableOffsets to = table_offsets(L, g.n2);
   const float2* y = Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(r0) * g.ypitch;
+  const float2* yb = Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(r0) * CPT;
+  const bool blocked = flags & kFft4Blocked;
   Vec<CPT> v;
 #pragma unroll
   for (int c = 0; c < CPT; ++c)
 #pragma unroll
-    for (int q = 0; q < kPts; ++q) v[c][q] = y[static_cast<uint64_t>(c) * g.ypitch + t + q * T];
+    for (int q = 0; q < kPts; ++q) {
+      const uint32_t i = t + q * T;
+      v[c][q] = (flags & kFft4SkipLoad)
+                    ? make_float2(static_cast<float>(t + q), static_cast<float>(c))
+                    : (blocked ? yb[static_cast<uint64_t>(i / CPT) * (CPT * g.n2) + c * CPT + (i % CPT)]
+                               : y[static_cast<uint64_t>(c) * g.ypitch + i]);
+    }
   if (!(flags & kFft4SkipCompute)) fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n1);
   float2* x = X + static_cast<uint64_t>(k) * g.xstride + r0;
   const bool nt = flags & kFft4NtStores;
 #pragma unroll
-  for (int q = 0; q < kPts; ++q) store_row<CPT>(x + static_cast<uint64_t>(t + q * T) * g.xpitch, v, q, nt);
+  for (int q = 0; q < kPts; ++q)
+    if (!(flags & kFft4SkipStore) || v[0][q].x == 1234.5f)
+      store_row<CPT>(blocked ? X + static_cast<uint64_t>(k) * g.xstride + static_cast<uint64_t>(r0) * L +
+                                   static_cast<uint64_t>(t + q * T) * CPT
+                             : x + static_cast<uint64_t>(t + q * T) * g.xpitch,
+                     v, q, nt);
 }
 
 bool supported_len(int L) { return L >= 128 && L <= 4096 && (L & (L - 1)) == 0; }
@@ -392,7 +414,7 @@ void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& 
 }
 
 namespace {
-int g_fft4_flags = 0;
+int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked;  // fastest measured shape (tools/kbench.py)
 
 template <int CPT, int SUB>
 void launch_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,

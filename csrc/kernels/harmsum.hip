@@ -49,24 +49,27 @@ __global__ void __launch_bounds__(256) interbin_normalise_batch_kernel(const flo
 //   X[k] = (Z[k] + conj Z[M-k])/2 - i/2 e^{-2 pi i k/N} (Z[k] - conj Z[M-k]),  k = 0..M
 // (indices mod M); za = Z[k mod M], zb = Z[(M-k) mod M].  Replaces rocFFT's
 // separate r2c post-processing pass.
-__device__ __forceinline__ float2 r2c_combine(float2 za, float2 zb, uint64_t k, uint64_t M) {
+// (c, s) = (cos, sin) of -pi k / M.
+__device__ __forceinline__ float2 r2c_combine(float2 za, float2 zb, float c, float s) {
   const float ex = 0.5f * (za.x + zb.x), ey = 0.5f * (za.y - zb.y);
   const float dx = 0.5f * (za.x - zb.x), dy = 0.5f * (za.y + zb.y);
   const float ox = dy, oy = -dx;  // -i * d
-  float s, c;
-  sincospif(-static_cast<float>(k) / static_cast<float>(M), &s, &c);
   return make_float2(ex + c * ox - s * oy, ey + c * oy + s * ox);
 }
 
-__device__ __forceinline__ uint64_t zaddr(uint64_t k, int log2_row, uint64_t pitch) {
-  return (k >> log2_row) * pitch + (k & ((uint64_t(1) << log2_row) - 1));
+// Address of bin k = k2 + 2^log2_row * k1 in a (possibly blocked) layout:
+// (k2 >> 3) * blk + k1 * pitch + (k2 & 7).
+__device__ __forceinline__ uint64_t zaddr(uint64_t k, int log2_row, uint64_t pitch, uint64_t blk) {
+  const uint64_t k2 = k & ((uint64_t(1) << log2_row) - 1);
+  return (k2 >> 3) * blk + (k >> log2_row) * pitch + (k2 & 7);
 }
 
 // One workgroup per tile of 256 bins k in [k0, k0+256), k <= M/2: both the
 // ascending bins k and their mirrors M-k come from the same loads
 // Z[k], Z[M-k]; one halo bin each side feeds the interbin neighbour.
 __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
-    const float2* __restrict__ Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t pitch, float* __restrict__ P,
+    const float2* __restrict__ Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t pitch, uint64_t blk,
+    float* __restrict__ P,
     uint64_t pstride, uint64_t nbins_out, const float* __restrict__ stats, float nscale) {
   __shared__ float2 A[258];  // A[u] = X[k0 - 1 + u]
   __shared__ float2 D[258];  // D[u] = X[M - (k0 - 1 + u)]
@@ -84,9 +87,11 @@ __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
     }
     const uint64_t uk = static_cast<uint64_t>(k);
     const uint64_t a = uk & (M - 1), b = (M - uk) & (M - 1);
-    const float2 za = z[zaddr(a, log2_row, pitch)], zb = z[zaddr(b, log2_row, pitch)];
-    A[u] = r2c_combine(za, zb, uk, M);
-    D[u] = r2c_combine(zb, za, M - uk, M);
+    const float2 za = z[zaddr(a, log2_row, pitch, blk)], zb = z[zaddr(b, log2_row, pitch, blk)];
+    float sn, cs;
+    sincospif(-static_cast<float>(uk) / static_cast<float>(M), &sn, &cs);
+    A[u] = r2c_combine(za, zb, cs, sn);
+    D[u] = r2c_combine(zb, za, -cs, sn);  // angle -pi (M-k)/M = -pi + pi k/M
   };
   for (uint64_t k0 = static_cast<uint64_t>(blockIdx.x) * 256; k0 <= half;
        k0 += static_cast<uint64_t>(gridDim.x) * 256) {
@@ -123,56 +128,122 @@ __device__ __forceinline__ void emit(bool pred, uint32_t seg, int idx, float snr
   }
 }
 
+// LDS-staged fused harmonic sum.  A workgroup owns a tile of B = 256*BPT
+// bins [b0, b0+B) of one trial.  Every gather the tile needs -- level h,
+// odd numerator m: P[(i*m + 2^(h-1)) >> h] -- falls in one contiguous
+// range of length ~B*m/2^h, so the tile first copies the fundamental and
+// each of those ranges into LDS with coalesced loads (they are L2-hot:
+// neighbouring tiles need overlapping ranges), then every thread sums its
+// bins from LDS.  Even numerators repeat the previous level's terms and
+// are not re-read (as in the reference recurrence).
+template <int NLEV>
+struct HarmTile {
+  static constexpr int BPT = NLEV <= 3 ? 8 : (NLEV == 4 ? 4 : 2);
+  static constexpr int B = 256 * BPT;
+  static constexpr int NREG = 1 << NLEV;  // fundamental + sum_{h=1..NLEV} 2^(h-1) ranges
+  static constexpr int maxlen(int h, int m) { return h == 0 ? B : (((B - 1) * m) >> h) + 2; }
+  static constexpr int region(int h, int m) { return h == 0 ? 0 : (1 << (h - 1)) + (m - 1) / 2; }
+  static constexpr int offset(int r) {
+    int off = 0;
+    for (int h = 0; h <= NLEV; ++h)
+      for (int m = 1; m < (h == 0 ? 2 : (1 << h)); m += 2) {
+        if (region(h, m) == r) return off;
+        off += maxlen(h, m);
+      }
+    return off;
+  }
+  static constexpr int TOTAL = offset(NREG);
+  static constexpr int iters() {
+    int n = 0;
+    for (int h = 0; h <= NLEV; ++h)
+      for (int m = 1; m < (h == 0 ? 2 : (1 << h)); m += 2) n += (maxlen(h, m) + 255) / 256;
+    return n;
+  }
+  static constexpr int ITERS = iters();
+};
+
 template <int NLEV>
 __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __restrict__ P, uint64_t pstride,
                                                              int lo, int hi, HarmParams hp,
                                                              PeakRecord* __restrict__ out,
                                                              uint32_t* __restrict__ count) {
+  using Tl = HarmTile<NLEV>;
+  constexpr int B = Tl::B;
+  __shared__ float lds[Tl::TOTAL];
   const int k = blockIdx.y;
   const float* p = P + static_cast<uint64_t>(k) * pstride;
+  const int t = threadIdx.x;
+  const int b0 = lo + static_cast<int>(blockIdx.x) * B;
+  const int last = hi - 1;
+  // ---- stage the fundamental and every gather range: all loads are issued
+  // before the first LDS store (fixed trip counts), so they overlap.
+  float tmp[Tl::ITERS];
+  {
+    int it = 0;
+#pragma unroll
+    for (int h = 0; h <= NLEV; ++h) {
+#pragma unroll
+      for (int m = 1; m < (h == 0 ? 2 : (1 << h)); m += 2) {
+        const int half = h == 0 ? 0 : (1 << (h - 1));
+        const int r0 = (b0 * m + half) >> h;
+#pragma unroll
+        for (int e = 0; e < (Tl::maxlen(h, m) + 255) / 256; ++e) tmp[it++] = p[min(r0 + t + 256 * e, last)];
+      }
+    }
+  }
+  {
+    int it = 0;
+#pragma unroll
+    for (int h = 0; h <= NLEV; ++h) {
+#pragma unroll
+      for (int m = 1; m < (h == 0 ? 2 : (1 << h)); m += 2) {
+        float* dst = lds + Tl::offset(Tl::region(h, m));
+#pragma unroll
+        for (int e = 0; e < (Tl::maxlen(h, m) + 255) / 256; ++e, ++it)
+          if (t + 256 * e < Tl::maxlen(h, m)) dst[t + 256 * e] = tmp[it];
+      }
+    }
+  }
+  __syncthreads();
   const float thr = hp.thresh;
   const uint32_t seg0 = static_cast<uint32_t>(k) * 8u;
-  const int stride = gridDim.x * blockDim.x;
-  for (int base = lo + blockIdx.x * blockDim.x; base < hi; base += stride) {
-    const int i = base + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < Tl::BPT; ++u) {
+    const int i = b0 + t + u * 256;
     const bool valid = i < hi;
-    const int ii = valid ? i : lo;
-    float val = p[ii];
-    emit(valid && ii >= hp.start[0] && ii < hp.end[0] && val > thr, seg0, ii, val, out, count, hp.capacity);
+    float val = lds[t + u * 256];
+    emit(valid && i >= hp.start[0] && i < hp.end[0] && val > thr, seg0, i, val, out, count, hp.capacity);
+#define PS_TERM(h, m) lds[Tl::offset(Tl::region(h, m)) + (((i * (m) + (1 << ((h) - 1))) >> (h)) - ((b0 * (m) + (1 << ((h) - 1))) >> (h)))]
     if constexpr (NLEV >= 1) {
-      const long long li = ii;
-      val += p[(li + 1) >> 1];
-      float o = static_cast<float>(static_cast<double>(val) * c_level_scale[1]);
-      emit(valid && ii >= hp.start[1] && ii < hp.end[1] && o > thr, seg0 + 1, ii, o, out, count, hp.capacity);
+      val += PS_TERM(1, 1);
+      const float o = static_cast<float>(static_cast<double>(val) * c_level_scale[1]);
+      emit(valid && i >= hp.start[1] && i < hp.end[1] && o > thr, seg0 + 1, i, o, out, count, hp.capacity);
     }
     if constexpr (NLEV >= 2) {
-      const long long li = ii;
-      val += p[(li * 3 + 2) >> 2];
-      val += p[(li * 1 + 2) >> 2];
-      float o = static_cast<float>(static_cast<double>(val) * c_level_scale[2]);
-      emit(valid && ii >= hp.start[2] && ii < hp.end[2] && o > thr, seg0 + 2, ii, o, out, count, hp.capacity);
+      val += PS_TERM(2, 3);  // reference order: 3/4 before 1/4
+      val += PS_TERM(2, 1);
+      const float o = static_cast<float>(static_cast<double>(val) * c_level_scale[2]);
+      emit(valid && i >= hp.start[2] && i < hp.end[2] && o > thr, seg0 + 2, i, o, out, count, hp.capacity);
     }
     if constexpr (NLEV >= 3) {
-      const long long li = ii;
 #pragma unroll
-      for (int m = 1; m < 8; m += 2) val += p[(li * m + 4) >> 3];
-      float o = static_cast<float>(static_cast<double>(val) * c_level_scale[3]);
-      emit(valid && ii >= hp.start[3] && ii < hp.end[3] && o > thr, seg0 + 3, ii, o, out, count, hp.capacity);
+      for (int m = 1; m < 8; m += 2) val += PS_TERM(3, m);
+      const float o = static_cast<float>(static_cast<double>(val) * c_level_scale[3]);
+      emit(valid && i >= hp.start[3] && i < hp.end[3] && o > thr, seg0 + 3, i, o, out, count, hp.capacity);
     }
     if constexpr (NLEV >= 4) {
-      const long long li = ii;
 #pragma unroll
-      for (int m = 1; m < 16; m += 2) val += p[(li * m + 8) >> 4];
-      float o = static_cast<float>(static_cast<double>(val) * c_level_scale[4]);
-      emit(valid && ii >= hp.start[4] && ii < hp.end[4] && o > thr, seg0 + 4, ii, o, out, count, hp.capacity);
+      for (int m = 1; m < 16; m += 2) val += PS_TERM(4, m);
+      const float o = static_cast<float>(static_cast<double>(val) * c_level_scale[4]);
+      emit(valid && i >= hp.start[4] && i < hp.end[4] && o > thr, seg0 + 4, i, o, out, count, hp.capacity);
     }
     if constexpr (NLEV >= 5) {
-      const long long li = ii;
 #pragma unroll
-      for (int m = 1; m < 32; m += 2) val += p[(li * m + 16) >> 5];
-      float o = static_cast<float>(static_cast<double>(val) * c_level_scale[5]);
-      emit(valid && ii >= hp.start[5] && ii < hp.end[5] && o > thr, seg0 + 5, ii, o, out, count, hp.capacity);
+      for (int m = 1; m < 32; m += 2) val += PS_TERM(5, m);
+      const float o = static_cast<float>(static_cast<double>(val) * c_level_scale[5]);
+      emit(valid && i >= hp.start[5] && i < hp.end[5] && o > thr, seg0 + 5, i, o, out, count, hp.capacity);
     }
+#undef PS_TERM
   }
 }
 
@@ -212,16 +283,17 @@ void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride,
 }
 
 void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t row_pitch,
-                                  float* P, uint64_t pstride, int K, uint64_t nbins_out, const float* stats,
-                                  float nscale, hipStream_t s) {
+                                  uint64_t blk_pitch, float* P, uint64_t pstride, int K, uint64_t nbins_out,
+                                  const float* stats, float nscale, hipStream_t s) {
   PSOUP_CHECK(K >= 1 && K <= 65535, "bad batch");
   PSOUP_CHECK(M >= 2 && (M & (M - 1)) == 0, "r2c: M must be a power of two");
   PSOUP_CHECK(nbins_out <= M + 1, "nbins_out beyond the spectrum");
   PSOUP_CHECK(log2_row >= 0 && log2_row < 63 && (uint64_t(1) << log2_row) <= M, "r2c: bad row layout");
   if (nbins_out == 0) return;
   dim3 grid(dev::grid_for(M / 2 + 1, 256, 2048), static_cast<unsigned>(K));
-  r2c_interbin_normalise_batch_kernel<<<grid, 256, 0, s>>>(Z, M, zstride, log2_row, row_pitch, P, pstride, nbins_out,
-                                                           stats, nscale);
+  PSOUP_CHECK(log2_row >= 3 || blk_pitch == 8, "r2c: blocked layout needs rows of >= 8 bins");
+  r2c_interbin_normalise_batch_kernel<<<grid, 256, 0, s>>>(Z, M, zstride, log2_row, row_pitch, blk_pitch, P, pstride,
+                                                           nbins_out, stats, nscale);
   post_launch_check("r2c_interbin_normalise_batch_kernel", s);
 }
 
@@ -238,14 +310,16 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
   }
   PSOUP_CHECK(hi <= static_cast<int>(nbins), "search range beyond spectrum");
   if (hi <= lo) return;
-  dim3 grid(dev::grid_for(static_cast<uint64_t>(hi - lo), 256, 1024), static_cast<unsigned>(K));
+  PSOUP_CHECK(static_cast<int64_t>(hi) * 32 < (int64_t(1) << 31), "spectrum too long for the int32 gather math");
+  auto grid_of = [&](int B) {
+    return dim3(static_cast<unsigned>((hi - lo + B - 1) / B), static_cast<unsigned>(K));
+  };
   switch (hp.nlevels) {
-    case 0: harmonic_peaks_kernel<0><<<grid, 256, 0, s>>>(P, pstride, lo, hi, hp, out, count); break;
-    case 1: harmonic_peaks_kernel<1><<<grid, 256, 0, s>>>(P, pstride, lo, hi, hp, out, count); break;
-    case 2: harmonic_peaks_kernel<2><<<grid, 256, 0, s>>>(P, pstride, lo, hi, hp, out, count); break;
-    case 3: harmonic_peaks_kernel<3><<<grid, 256, 0, s>>>(P, pstride, lo, hi, hp, out, count); break;
-    case 4: harmonic_peaks_kernel<4><<<grid, 256, 0, s>>>(P, pstride, lo, hi, hp, out, count); break;
-    default: harmonic_peaks_kernel<5><<<grid, 256, 0, s>>>(P, pstride, lo, hi, hp, out, count); break;
+#define PS_CASE(NL) \
+  case NL: harmonic_peaks_kernel<NL><<<grid_of(HarmTile<NL>::B), 256, 0, s>>>(P, pstride, lo, hi, hp, out, count); break;
+    PS_CASE(0) PS_CASE(1) PS_CASE(2) PS_CASE(3) PS_CASE(4)
+#undef PS_CASE
+    default: harmonic_peaks_kernel<5><<<grid_of(HarmTile<5>::B), 256, 0, s>>>(P, pstride, lo, hi, hp, out, count); break;
   }
   post_launch_check("harmonic_peaks_kernel", s);
 }

@@ -424,10 +424,10 @@ PYBIND11_MODULE(_C, m) {
                                    P<const float>(stats), nscale, S(s));
   });
   k.def("r2c_interbin_normalise_batch", [](uintptr_t Z, uint64_t M, uint64_t zstride, int log2_row,
-                                           uint64_t row_pitch, uintptr_t Pout, uint64_t pstride, int K, uint64_t nbo,
-                                           uintptr_t stats, float nscale, uintptr_t s) {
-    kern::r2c_interbin_normalise_batch(P<const float2>(Z), M, zstride, log2_row, row_pitch, P<float>(Pout), pstride,
-                                       K, nbo, P<const float>(stats), nscale, S(s));
+                                           uint64_t row_pitch, uint64_t blk_pitch, uintptr_t Pout, uint64_t pstride,
+                                           int K, uint64_t nbo, uintptr_t stats, float nscale, uintptr_t s) {
+    kern::r2c_interbin_normalise_batch(P<const float2>(Z), M, zstride, log2_row, row_pitch, blk_pitch, P<float>(Pout),
+                                       pstride, K, nbo, P<const float>(stats), nscale, S(s));
   });
   py::class_<kern::Fft4Geom>(k, "Fft4Geom")
       .def_readonly("ok", &kern::Fft4Geom::ok)

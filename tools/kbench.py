@@ -78,10 +78,13 @@ def main():
         report(f"colpass flags={f}", tc, K * 8 * M)
         tr = timeit(lambda: K_.fft4_rowpass(Y.data_ptr(), X.data_ptr(), K, g, tab.data_ptr(), s), a.reps)
         report(f"rowpass flags={f}", tr, K * 16 * M)
+    for blocked in (False, True):
+        row, blk = (8, 8 * g.n1) if blocked else (g.xpitch, 8)
+        tz = timeit(lambda: K_.r2c_interbin_normalise_batch(X.data_ptr(), M, g.xstride, g.log2_xrow, row, blk,
+                                                            P.data_ptr(), M + 1, K, M + 1, st.data_ptr(), float(n), s),
+                    a.reps)
+        report(f"r2c_interbin_normalise blocked={blocked}", tz, K * (8 * M + 4 * M))
     K_.fft4_set_flags(0)
-    tz = timeit(lambda: K_.r2c_interbin_normalise_batch(X.data_ptr(), M, g.xstride, g.log2_xrow, g.xpitch, P.data_ptr(),
-                                                        M + 1, K, M + 1, st.data_ptr(), float(n), s), a.reps)
-    report("r2c_interbin_normalise", tz, K * (8 * M + 4 * M))
     # harmonic peaks on normal noise (threshold 9 -> few peaks)
     P.normal_()
     nb = M + 1
