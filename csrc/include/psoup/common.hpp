@@ -167,6 +167,7 @@ class Stream {
   Stream(const Stream&) = delete;
   Stream& operator=(const Stream&) = delete;
   hipStream_t get() const { return s_; }
+  void sync() const { PSOUP_HIP_CHECK(hipStreamSynchronize(s_)); }
 
  private:
   hipStream_t s_ = nullptr;

@@ -1,0 +1,217 @@
+// Native host-side unit tests for the C++ core (no GPU needed).  Built as
+// `bin/psoup_unit_tests`; the sanitizer build (`python -m peasoup_amd._build
+// --sanitize address|undefined|thread`) compiles these sources and the host
+// components they exercise with -fsanitize=..., since GPU
+// ASan is not available on the MI355X pool.
+//
+// usage: psoup_unit_tests [repo_root]   (repo_root locates the tutorial .fil)
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "psoup/candidates.hpp"
+#include "psoup/cli.hpp"
+#include "psoup/common.hpp"
+#include "psoup/output.hpp"
+#include "psoup/plan.hpp"
+#include "psoup/sigproc.hpp"
+
+using namespace psoup;
+
+namespace {
+
+int g_fail = 0, g_pass = 0;
+std::string g_root = ".";
+
+#define CHECK(cond)                                                                      \
+  do {                                                                                   \
+    if (!(cond)) {                                                                       \
+      std::cerr << "  FAILED " << __FILE__ << ":" << __LINE__ << ": " #cond << "\n";     \
+      ++g_fail;                                                                          \
+      return;                                                                            \
+    }                                                                                    \
+  } while (0)
+
+struct Case {
+  const char* name;
+  std::function<void()> fn;
+};
+
+void t_prev_power_of_two() {
+  CHECK(prev_power_of_two(187520) == 131072);
+  CHECK(prev_power_of_two(1u << 23) == (1u << 22));  // strictly less (utils.hpp:12-18)
+  CHECK(prev_power_of_two(1000) == 512);
+}
+
+void t_accel_plan_conventions() {
+  AccelPlan legacy(-5, 5, 1.1f, 64.f, 131072, 0.00032f, 1367.5f, -1.09f);
+  auto l = legacy.generate(0.f);
+  CHECK(l.size() == 3 && l[0] == 0.f && l[1] == -5.f && l[2] == 5.f);
+  AccelPlan cur(-5, 5, 1.1f, 64.f, 131072, 0.00032f, 1367.5f, -1.09f, AccelConvention::Reference);
+  CHECK(cur.generate(0.f).size() == 44);
+  AccelPlan big(-500, 500, 1.1f, 64.f, 1u << 23, 64e-6f, 1400.f, -0.39f);
+  const size_t nb = big.generate(0.f).size();
+  CHECK(nb >= 680 && nb <= 690);
+  CHECK(AccelPlan(0, 0, 1.1f, 64.f, 1024, 1e-4f, 1400.f, -1.f).generate(3.f) == std::vector<float>{0.f});
+}
+
+void t_dm_list_tutorial() {
+  SigprocHeader h = read_header_file(g_root + "/tests/data/tutorial.fil");
+  auto dms = generate_dm_list(0.f, 250.f, h.tsamp, 64.0, h.fch1, h.foff, h.nchans, 1.1f);
+  CHECK(dms.size() == 59);  // golden overview.xml dedispersion_trials
+  CHECK(dms.front() == 0.f);
+  for (size_t i = 1; i < dms.size(); ++i) CHECK(dms[i] > dms[i - 1]);
+  auto delays = generate_delay_table(h.nchans, h.tsamp, h.fch1, h.foff);
+  CHECK(compute_max_delay(dms, delays) == 140);
+}
+
+void t_cli_parse() {
+  CmdLineOptions a;
+  bool exit_now = false;
+  std::vector<std::string> argv = {"peasoup", "-i", "x.fil", "--dm_end", "250", "-n", "3", "--acc_start=-5",
+                                   "--acc_end", "5", "-vp", "--fft_mode", "1", "--npdmp", "10"};
+  CHECK(parse_cmdline(a, argv, &exit_now));
+  CHECK(!exit_now && a.infilename == "x.fil" && a.dm_end == 250.f && a.nharmonics == 3);
+  CHECK(a.acc_start == -5.f && a.acc_end == 5.f && a.verbose && a.progress_bar && a.fft_mode == 1 && a.npdmp == 10);
+  CmdLineOptions b;
+  CHECK(!parse_cmdline(b, std::vector<std::string>{"peasoup", "--dm_end", "1"}, &exit_now));  // -i required
+  CHECK(!parse_cmdline(b, std::vector<std::string>{"peasoup", "-i", "f", "--bogus", "1"}, &exit_now));
+}
+
+void t_xml_format() {
+  CHECK(xml::fmt(0.1) == "0.1");
+  CHECK(xml::fmt(1.0 / 3.0) == "0.333333333333333");
+  xml::Element e("cand");
+  e.add_attribute("id", 3);
+  e.add_attribute("name", std::string("a<b&c"));
+  e.append(xml::Element("period", 0.25));
+  const std::string s = e.to_string();
+  CHECK(s.find("id='3'") != std::string::npos);
+  CHECK(s.find("a&lt;b&amp;c") != std::string::npos);
+  CHECK(s.find("<period>0.25</period>") != std::string::npos);
+}
+
+CandidateList synth_cands() {
+  CandidateList c;
+  c.emplace_back(10.f, 3, 0.f, 2, 20.f, 4.0f);
+  c.emplace_back(10.f, 3, 0.f, 1, 12.f, 8.0f);        // 2nd harmonic of the first
+  c.emplace_back(10.f, 3, 0.f, 1, 11.f, 2.0f);        // subharmonic
+  c.emplace_back(10.f, 3, 0.f, 1, 15.f, 4.7312f);     // unrelated
+  c.emplace_back(12.f, 4, 5.f, 1, 9.5f, 4.00001f);    // same signal, neighbour DM
+  return c;
+}
+
+void t_distillers() {
+  HarmonicDistiller hd(0.0001f, 16.f, true, true);
+  auto out = hd.distill(synth_cands());
+  CHECK(out.size() == 2);
+  CHECK(out[0].snr == 20.f && out[0].count_assoc() >= 2);
+  DMDistiller dd(0.0001f, true);
+  auto out2 = dd.distill(synth_cands());
+  CHECK(out2.size() < 5);
+  AccelerationDistiller ad(537.f, 0.0001f, true);
+  CHECK(!ad.distill(synth_cands()).empty());
+}
+
+void t_serialise_roundtrip() {
+  CandidateList c = synth_cands();
+  c[0].append(c[1]);
+  c[0].assoc[0].append(c[2]);
+  auto bytes = serialize_candidates(c);
+  auto back = deserialize_candidates(bytes.data(), bytes.size());
+  CHECK(back.size() == c.size());
+  CHECK(back[0].count_assoc() == c[0].count_assoc());
+  CHECK(back[3].freq == c[3].freq && back[4].dm_idx == 4);
+  bool threw = false;
+  try {
+    deserialize_candidates(bytes.data(), bytes.size() / 2);
+  } catch (const std::exception&) {
+    threw = true;
+  }
+  CHECK(threw);
+}
+
+void t_sigproc_roundtrip() {
+  SigprocHeader h;
+  h.source_name = "unit";
+  h.nchans = 16;
+  h.nbits = 8;
+  h.tsamp = 1e-4;
+  h.fch1 = 1500;
+  h.foff = -1;
+  h.nsamples = 7;
+  h.nifs = 1;
+  h.keys_present = {"source_name", "nchans", "nbits", "tsamp", "fch1", "foff", "nsamples", "nifs"};
+  std::stringstream ss;
+  write_header(ss, h);
+  SigprocHeader r;
+  ss.seekg(0);
+  CHECK(read_header(ss, r));
+  CHECK(r.source_name == "unit" && r.nchans == 16 && r.nbits == 8 && r.tsamp == 1e-4 && r.fch1 == 1500 &&
+        r.foff == -1 && r.nsamples == 7);
+}
+
+void t_peaks_and_bounds() {
+  // identify_unique_peaks: clusters separated by < min_gap merge (peakfinder.hpp:24-55)
+  const int idx[] = {100, 101, 105, 200, 260, 261};
+  const float snr[] = {9.5f, 12.f, 10.f, 11.f, 9.1f, 9.2f};
+  std::vector<int> oi;
+  std::vector<float> os;
+  identify_unique_peaks(idx, snr, 6, 30, oi, os);
+  CHECK(oi.size() == 3 && oi[0] == 101 && oi[1] == 200 && oi[2] == 261);
+  PeakBounds b = peak_bounds(65537, 0.0238f, 3, 0.1f, 1100.f);
+  CHECK(b.start_idx > 0 && b.end_idx == 65537);
+}
+
+void t_threads_shared_readonly() {
+  // The per-GPU worker threads share the AccelPlan and DM list read-only
+  // (SURVEY.md §5.2); hammer that under TSan/ASan builds.
+  AccelPlan plan(-500, 500, 1.1f, 64.f, 1u << 20, 64e-6f, 1400.f, -0.39f);
+  std::vector<size_t> counts(8);
+  std::vector<std::thread> th;
+  for (int t = 0; t < 8; ++t)
+    th.emplace_back([&, t] {
+      size_t n = 0;
+      for (int k = 0; k < 50; ++k) n += plan.generate(static_cast<float>(k)).size();
+      counts[static_cast<size_t>(t)] = n;
+    });
+  for (auto& x : th) x.join();
+  for (size_t c : counts) CHECK(c == counts[0] && c > 0);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc > 1) g_root = argv[1];
+  std::vector<Case> cases = {
+      {"prev_power_of_two", t_prev_power_of_two},
+      {"accel_plan_conventions", t_accel_plan_conventions},
+      {"dm_list_tutorial", t_dm_list_tutorial},
+      {"cli_parse", t_cli_parse},
+      {"xml_format", t_xml_format},
+      {"distillers", t_distillers},
+      {"serialise_roundtrip", t_serialise_roundtrip},
+      {"sigproc_roundtrip", t_sigproc_roundtrip},
+      {"peaks_and_bounds", t_peaks_and_bounds},
+      {"threads_shared_readonly", t_threads_shared_readonly},
+  };
+  for (auto& c : cases) {
+    const int before = g_fail;
+    try {
+      c.fn();
+    } catch (const std::exception& e) {
+      std::cerr << "  EXCEPTION in " << c.name << ": " << e.what() << "\n";
+      ++g_fail;
+    }
+    if (g_fail == before) ++g_pass;
+    std::cout << (g_fail == before ? "[ OK ] " : "[FAIL] ") << c.name << "\n";
+  }
+  std::cout << g_pass << " passed, " << g_fail << " failed\n";
+  return g_fail == 0 ? 0 : 1;
+}
