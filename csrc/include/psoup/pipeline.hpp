@@ -71,7 +71,14 @@ struct PipelineResult {
   std::map<std::string, double> performance;
   std::vector<int> devices;
   SearchSetup setup;
+  // per device: dedispersion_s, search_s, dm_trials, accel_trials, peaks,
+  // peak_overflows, accel_loop_s, host_distill_s, fft_mode, accel_batch
+  std::vector<std::map<std::string, double>> device_stats;
 };
+
+// Per-stage JSON trace (--trace_json): timers, performance, per-device
+// counters and the search configuration.
+std::string trace_json(const CmdLineOptions& args, const PipelineResult& res);
 
 // Runs the whole search in this process on `ndevices` GPUs (threads).
 PipelineResult run_pipeline(const CmdLineOptions& args);

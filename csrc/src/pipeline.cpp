@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <condition_variable>
 #include <cstdio>
 #include <fstream>
@@ -156,6 +157,7 @@ struct Shared {
   std::atomic<uint64_t> accel_trials{0};
   std::atomic<int> done_dms{0};
   std::vector<double> dedisp_s, search_s;
+  std::vector<std::map<std::string, double>> dev_stats;
   std::exception_ptr error;
   ProgressBar* progress = nullptr;
 };
@@ -191,6 +193,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   sh.ndm = static_cast<int>(setup.dm_list.size());
   sh.chunk = std::max(1, std::min(32, sh.ndm / (4 * ngpu) + 1));
   sh.dedisp_s.assign(static_cast<size_t>(ngpu), 0.0);
+  sh.dev_stats.assign(static_cast<size_t>(ngpu), {});
   sh.search_s.assign(static_cast<size_t>(ngpu), 0.0);
   ProgressBar progress("Searching DM trials");
   if (args.progress_bar) {
@@ -262,6 +265,18 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
       }
       sh.dedisp_s[static_cast<size_t>(dev)] = wd.get_time();
       sh.search_s[static_cast<size_t>(dev)] = ws.get_time();
+      const SearchCounters& c = engine.counters();
+      auto& st_map = sh.dev_stats[static_cast<size_t>(dev)];
+      st_map["dedispersion_s"] = wd.get_time();
+      st_map["search_s"] = ws.get_time();
+      st_map["dm_trials"] = static_cast<double>(c.dm_trials);
+      st_map["accel_trials"] = static_cast<double>(c.accel_trials);
+      st_map["peaks"] = static_cast<double>(c.peaks);
+      st_map["peak_overflows"] = static_cast<double>(c.overflows);
+      st_map["accel_loop_s"] = c.accel_s;
+      st_map["host_distill_s"] = c.host_s;
+      st_map["fft_mode"] = engine.fft_mode();
+      st_map["accel_batch"] = engine.batch_size();
     } catch (...) {
       std::lock_guard<std::mutex> lk(sh.mu);
       if (!sh.error) sh.error = std::current_exception();
@@ -347,7 +362,62 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   res.performance["dm_accel_trials"] = trials;
   res.performance["dm_accel_trials_per_sec"] = t_search.get_time() > 0 ? trials / t_search.get_time() : 0.0;
   res.performance["search_kernel_seconds_max_device"] = smax;
+  res.device_stats = sh.dev_stats;
   return res;
+}
+
+namespace {
+std::string json_num(double v) {
+  if (!std::isfinite(v)) return "null";
+  char buf[64];
+  std::snprintf(buf, sizeof(buf), "%.17g", v);
+  return buf;
+}
+std::string json_str(const std::string& s) {
+  std::string o = "\"";
+  for (char ch : s) {
+    if (ch == '"' || ch == '\\') o += '\\';
+    if (static_cast<unsigned char>(ch) < 0x20) {
+      char b[8];
+      std::snprintf(b, sizeof(b), "\\u%04x", ch);
+      o += b;
+      continue;
+    }
+    o += ch;
+  }
+  return o + "\"";
+}
+std::string json_map(const std::map<std::string, double>& m) {
+  std::string o = "{";
+  bool first = true;
+  for (const auto& kv : m) {
+    o += (first ? "" : ", ") + json_str(kv.first) + ": " + json_num(kv.second);
+    first = false;
+  }
+  return o + "}";
+}
+}  // namespace
+
+std::string trace_json(const CmdLineOptions& args, const PipelineResult& res) {
+  std::string o = "{\n";
+  o += "  \"input\": " + json_str(args.infilename) + ",\n";
+  o += "  \"config\": {\"fft_size\": " + json_num(static_cast<double>(res.setup.search.fft_size)) +
+       ", \"nharmonics\": " + json_num(args.nharmonics) + ", \"ndm\": " +
+       json_num(static_cast<double>(res.setup.dm_list.size())) + ", \"acc_start\": " + json_num(args.acc_start) +
+       ", \"acc_end\": " + json_num(args.acc_end) + ", \"accel_convention\": " + json_str(args.accel_convention) +
+       ", \"dedisp_kernel\": " + json_str(args.dedisp_kernel) + ", \"fft_mode\": " + json_num(args.fft_mode) +
+       "},\n";
+  o += "  \"timers_s\": " + json_map(res.timers) + ",\n";
+  o += "  \"performance\": " + json_map(res.performance) + ",\n";
+  o += "  \"devices\": [";
+  for (size_t d = 0; d < res.device_stats.size(); ++d) {
+    auto m = res.device_stats[d];
+    m["device"] = d < res.devices.size() ? res.devices[d] : static_cast<double>(d);
+    o += (d ? ",\n    " : "\n    ") + json_map(m);
+  }
+  o += "\n  ],\n";
+  o += "  \"candidates\": " + json_num(static_cast<double>(res.candidates.size())) + "\n}\n";
+  return o;
 }
 
 void write_outputs(const CmdLineOptions& args, const PipelineResult& res) {
@@ -364,6 +434,11 @@ void write_outputs(const CmdLineOptions& args, const PipelineResult& res) {
   ow.add_timing_info(res.timers);
   ow.add_performance(res.performance);
   ow.to_file(args.outdir + "/overview.xml");
+  if (!args.trace_json.empty()) {
+    std::ofstream f(args.trace_json);
+    if (!f) PSOUP_THROW("cannot write trace file " << args.trace_json);
+    f << trace_json(args, res);
+  }
 }
 
 }  // namespace psoup

@@ -23,6 +23,7 @@ include/transforms/folder.hpp:337-442 (MultiFolder).
 """
 from __future__ import annotations
 
+import json
 import os
 import struct
 import time
@@ -47,6 +48,7 @@ class SearchResult:
     header: dict
     args: object = None
     accel_trials: int = 0
+    rank_stats: list = field(default_factory=list)
 
 
 def _stream_handle() -> int:
@@ -223,6 +225,11 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     torch.cuda.synchronize()
     search_wall = time.perf_counter() - t0
     local_trials = sum(weights[i] for i in shard)
+    rank_stats = dict(rs.engine.counters())
+    rank_stats.update({"rank": ctx.rank, "search_s": search_wall, "accel_trials_planned": local_trials,
+                       "fft_mode": rs.engine.fft_mode, "accel_batch": rs.engine.batch_size,
+                       "dedispersion_s": timers["dedispersion"].get_time(), "searching_s": timers["searching"].get_time()})
+    all_stats = pdist.gather_bytes(json.dumps(rank_stats).encode(), dst=0)
 
     # ---- candidate gather (RCCL) + global distillation on rank 0
     blobs = pdist.gather_bytes(_C.serialize_candidates(local), dst=None)
@@ -272,13 +279,32 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     acc0 = rs.accel_list(0.0)
     res = SearchResult(cands, tdict, perf, rs.dm_list, acc0, list(range(ctx.world_size)) if ctx.device.type == "cuda" else [],
                        rs.header, args, total_trials)
+    res.rank_stats = [json.loads(b.decode()) for b in all_stats] if all_stats else []
     if write:
         write_outputs(args, res)
     return res
 
 
+def trace_dict(args, res: SearchResult) -> dict:
+    """The --trace_json document (same layout as the native CLI's)."""
+    return {
+        "input": args.infilename,
+        "config": {"fft_size": int(args.size) or None, "nharmonics": args.nharmonics, "ndm": len(res.dm_list),
+                   "acc_start": args.acc_start, "acc_end": args.acc_end,
+                   "accel_convention": args.accel_convention, "dedisp_kernel": args.dedisp_kernel,
+                   "fft_mode": args.fft_mode},
+        "timers_s": res.timers,
+        "performance": res.performance,
+        "devices": res.rank_stats,
+        "candidates": len(res.candidates),
+    }
+
+
 def write_outputs(args, res: SearchResult) -> None:
     os.makedirs(args.outdir, exist_ok=True)
+    if getattr(args, "trace_json", ""):
+        with open(args.trace_json, "w") as f:
+            json.dump(trace_dict(args, res), f, indent=2)
     bm = _C.write_candidates_binary(args.outdir, res.candidates, "candidates.peasoup")
     devices = [torch.cuda.current_device()] if res.devices else []
     if len(res.devices) > 1:

@@ -136,3 +136,29 @@ def test_fft_modes_agree(C, tmp_path):
             assert b["period"] == pytest.approx(a["period"], rel=1e-7), (mode, i)
             assert b["dm"] == a["dm"] and b["nh"] == a["nh"], (mode, i)
             assert b["snr"] == pytest.approx(a["snr"], rel=1e-4), (mode, i)
+
+
+def test_trace_json_cli_and_python(C, tmp_path):
+    """--trace_json: per-stage timers, performance and per-device counters
+    (SURVEY.md §5.1/§5.5), from the native CLI and the Python driver."""
+    import json
+
+    from peasoup_amd.models.search import run_search
+
+    tj = tmp_path / "cli_trace.json"
+    r = subprocess.run([os.path.join(REPO, "bin", "peasoup"), "-i", TUTORIAL, "-o", str(tmp_path / "cli"),
+                        "--dm_end", "60", "-n", "3", "--trace_json", str(tj)], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(tj.read_text())
+    assert set(d["timers_s"]) == {"dedispersion", "folding", "reading", "searching", "total"}
+    assert d["performance"]["dm_accel_trials_per_sec"] > 0
+    dev = d["devices"][0]
+    assert dev["accel_trials"] == d["performance"]["dm_accel_trials"] and dev["fft_mode"] == 2
+    tp = tmp_path / "py_trace.json"
+    ok, _, args = C.parse_cmdline(["peasoup", "-i", TUTORIAL, "-o", str(tmp_path / "py"), "--dm_end", "60", "-n", "3",
+                                   "--trace_json", str(tp)])
+    run_search(args)
+    d2 = json.loads(tp.read_text())
+    assert d2["devices"][0]["accel_trials"] == d["performance"]["dm_accel_trials"]
+    assert d2["config"]["ndm"] == d["config"]["ndm"]
