@@ -85,3 +85,55 @@ def test_shard_range_partitions(world):
     assert [i for s in shards for i in s] == list(range(n))
     loads = [sum(w[i] for i in s) for s in shards]
     assert max(loads) - min(loads) <= max(w) + 1e-9
+
+
+def _timeshard_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    try:
+        import numpy as np
+        import torch
+
+        from peasoup_amd import _C
+        from peasoup_amd.parallel import timeshard
+        from peasoup_amd.utils import reference as ref
+        from peasoup_amd.utils import sigproc, synthetic
+
+        pdist.init(backend="gloo")
+        nchans, nbits, nsamps = 32, 2, 3000
+        hdr = synthetic.make_header(nchans=nchans, nbits=nbits, tsamp=0.00032, fch1=1510.0, foff=-2.0,
+                                    nsamples=nsamps)
+        dms = _C.generate_dm_list(0.0, 120.0, 0.00032, 64.0, 1510.0, -2.0, nchans, 1.1)
+        vals = np.random.default_rng(5).integers(0, 4, size=(nsamps, nchans), dtype=np.uint8)
+        packed = sigproc.pack_samples(vals, nbits)
+        plan = timeshard.make_plan(hdr, nsamps, dms, world)
+        own = torch.from_numpy(timeshard.slice_packed(packed, plan, rank).copy())
+        mine = timeshard.time_sharded_dedisperse(own, plan, timeshard.reference_dedisperser(hdr, dms))
+        offs = ref.dm_offsets(dms, ref.delay_table(nchans, 0.00032, 1510.0, -2.0))
+        full = ref.dedisperse(vals, offs, nbits, None, plan.out_nsamps)
+        s = plan.dm_shards[rank]
+        q.put((rank, {"ok": bool(np.array_equal(mine.numpy(), full[s.start:s.stop])), "shape": tuple(mine.shape),
+                      "max_delay": plan.max_delay}))
+        pdist.shutdown()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, {"error": traceback.format_exc()}))
+
+
+def test_time_sharded_dedispersion_gloo_world3():
+    """Halo exchange + all-to-all corner turn == whole-observation dedispersion."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_timeshard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in out[r], out[r].get("error")
+        assert out[r]["ok"], out[r]
+    assert out[0]["max_delay"] > 0
