@@ -7,6 +7,16 @@ torchrun-compatible, one-process-per-GPU program:
 Flags are identical to the native ``bin/peasoup`` (include/utils/cmdline.hpp).
 A single process uses one GPU; the native CLI's ``-t`` thread-per-GPU mode
 remains available in ``bin/peasoup``.
+
+Failure handling: a failing rank prints its error with its
+rank and exits immediately, so torchrun tears the group down instead of
+letting the peers hang in a collective.  Elastic recovery is torchrun's
+restart plus resume:
+
+    python -m torch.distributed.run --max-restarts 3 ... -m peasoup_amd ... --checkpoint_dir ck/
+
+re-runs the group after a failure and every rank skips the DM chunks whose
+spill files (``ck/dm_<d0>_<d1>.psoc``) already exist.
 """
 from __future__ import annotations
 
@@ -28,7 +38,23 @@ def main(argv=None) -> int:
         return 0
     if args.verbose:
         _C.set_log_level(2)
-    res = run_search(args)
+    try:
+        res = run_search(args)
+    except BaseException as e:  # noqa: BLE001 - any failure must tear the job down
+        # A failed rank must not leave its peers blocked in a collective: report
+        # with rank context and exit hard, which destroys this rank's RCCL
+        # communicator (the ncclCommAbort equivalent) and makes torchrun stop
+        # -- or, with --max-restarts, restart -- the worker group.  A restart
+        # with --checkpoint_dir resumes from the per-DM spill files.
+        import os
+        import traceback
+
+        rank = os.environ.get("RANK", "0")
+        print(f"[rank {rank}] peasoup failed: {e}", file=sys.stderr)
+        traceback.print_exc()
+        sys.stderr.flush()
+        sys.stdout.flush()
+        os._exit(1)
     if res is not None and (args.verbose or args.progress_bar):
         print(f"Wrote {len(res.candidates)} candidates to {args.outdir}; "
               f"{res.performance['dm_accel_trials_per_sec']:.1f} DMxaccel trials/s over {int(res.performance['ranks'])} rank(s)")

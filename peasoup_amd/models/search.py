@@ -27,6 +27,7 @@ import json
 import os
 import struct
 import time
+import warnings
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence
 
@@ -109,10 +110,23 @@ class RankSearcher:
         t_dd = timers.get("dedispersion") if timers else None
         t_s = timers.get("searching") if timers else None
         ntrials = 0
+        ckdir = getattr(self.args, "checkpoint_dir", "") or ""
+        fault_after = int(getattr(self.args, "fault_after_dms", -1))
+        processed = 0
         for c0 in range(0, len(idx), chunk):
             block = idx[c0:c0 + chunk]
             d0, d1 = block[0], block[-1] + 1
             assert d1 - d0 == len(block), "DM shard must be contiguous"
+            ck = os.path.join(ckdir, f"dm_{d0}_{d1}.psoc") if ckdir else ""
+            if ck and os.path.exists(ck):
+                # resume: same spill format as the native pipeline (CandidatePOD trees)
+                with open(ck, "rb") as f:
+                    cands.extend(_C.deserialize_candidates(f.read()))
+                ntrials += sum(len(self.accel_list(self.dm_list[d])) for d in block)
+                if progress is not None:
+                    progress(len(block))
+                continue
+            chunk_cands: list = []
             if t_dd:
                 t_dd.start()
             with roctx_range("Dedisperse"):
@@ -123,15 +137,25 @@ class RankSearcher:
             if t_s:
                 t_s.start()
             for k, d in enumerate(block):
+                if 0 <= fault_after <= processed:
+                    raise RuntimeError(f"fault injection: rank {self.ctx.rank} aborting after {processed} DM trials")
                 dm = self.dm_list[d]
                 accs = self.accel_list(dm)
                 ntrials += len(accs)
                 addr = trials.data_ptr() + k * self.row_stride
-                cands.extend(self.engine.search_trial(addr, self.geom.out_nsamps, dm, d, accs))
+                chunk_cands.extend(self.engine.search_trial(addr, self.geom.out_nsamps, dm, d, accs))
+                processed += 1
                 if progress is not None:
                     progress(1)
             if t_s:
                 t_s.stop()
+            if ck:
+                os.makedirs(ckdir, exist_ok=True)
+                tmp = ck + f".tmp{self.ctx.rank}"
+                with open(tmp, "wb") as f:
+                    f.write(_C.serialize_candidates(chunk_cands))
+                os.replace(tmp, ck)
+            cands.extend(chunk_cands)
         self.accel_trials = ntrials
         return cands
 
@@ -195,7 +219,9 @@ def load_packed_for_rank(infilename: str, ctx: pdist.DistContext):
     if ctx.device.type == "cuda":
         packed = torch.empty(nbytes, dtype=torch.uint8, device=ctx.device)
         if ctx.is_root:
-            host = torch.from_numpy(fb.data())[:nbytes]
+            with warnings.catch_warnings():  # read-only mmap view, only copied to the device
+                warnings.simplefilter("ignore", UserWarning)
+                host = torch.from_numpy(fb.data())[:nbytes]
             packed.copy_(host, non_blocking=False)
         if ctx.distributed:
             pdist.broadcast_bytes(packed, nbytes)

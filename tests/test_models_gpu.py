@@ -151,3 +151,28 @@ def test_time_shard_native_windows_match_whole(C):
         ext = torch.from_numpy(packed[lo:hi].copy()).cuda()
         got = fn(ext, w.stop + plan.max_delay - w.start, len(w)).cpu().numpy()
         assert np.array_equal(got, full[:, w.start:w.stop]), r
+
+
+def test_python_entry_fault_then_resume(tmp_path):
+    """python -m peasoup_amd: an injected fault exits non-zero with rank
+    context; a re-run with the same --checkpoint_dir resumes from the spill
+    files and matches a clean run byte for byte."""
+    import subprocess
+    import sys
+
+    from conftest import REPO, TUTORIAL
+
+    ck = tmp_path / "ck"
+    base = [sys.executable, "-m", "peasoup_amd", "-i", TUTORIAL, "--dm_end", "120", "-n", "3"]
+    env = dict(os.environ, PYTHONPATH=REPO)
+    r = subprocess.run(base + ["-o", str(tmp_path / "a"), "--checkpoint_dir", str(ck), "--fault_after_dms", "20"],
+                       capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
+    assert r.returncode != 0 and "[rank 0] peasoup failed: fault injection" in r.stderr
+    assert len(list(ck.glob("dm_*.psoc"))) >= 1
+    r = subprocess.run(base + ["-o", str(tmp_path / "b"), "--checkpoint_dir", str(ck)], capture_output=True, text=True,
+                       timeout=600, env=env, cwd=REPO)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run(base + ["-o", str(tmp_path / "c")], capture_output=True, text=True, timeout=600, env=env,
+                       cwd=REPO)
+    assert r.returncode == 0, r.stderr
+    assert (tmp_path / "b" / "candidates.peasoup").read_bytes() == (tmp_path / "c" / "candidates.peasoup").read_bytes()
