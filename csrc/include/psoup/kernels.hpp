@@ -111,12 +111,14 @@ void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride,
 
 // Same output from the M = N/2 point complex FFT Z[K] of the packed real
 // series (real-FFT post-processing fused in; saves the separate r2c pass).
-// Bin k = k2 + 2^log2_row * k1 of Z lives at (k2 >> 3)*blk_pitch + k1*row_pitch + (k2 & 7)
-// (plain array: log2_row = log2 M, row_pitch = M, blk_pitch = 8).  Each
-// thread forms the bin pair (k, M-k) from one pair of loads.
+// Bin k = k2 + 2^log2_row * k1 of Z lives at
+// (k2 >> log2_blk)*blk_pitch + k1*row_pitch + (k2 & (2^log2_blk - 1))
+// (plain array: log2_row = log2 M, row_pitch = M, log2_blk = 3, blk_pitch = 8;
+// see fft4_x_layout for the fused FFT's layouts).  Each thread forms the bin
+// pair (k, M-k) from one pair of loads.
 void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t row_pitch,
-                                  uint64_t blk_pitch, float* P, uint64_t pstride, int K, uint64_t nbins_out,
-                                  const float* stats, float nscale, hipStream_t s);
+                                  uint64_t blk_pitch, int log2_blk, float* P, uint64_t pstride, int K,
+                                  uint64_t nbins_out, const float* stats, float nscale, hipStream_t s);
 
 // Fused resample + four-step FFT (fft4step.hip).  M = N/2 = n1*n2 with
 // n1, n2 powers of two in [128, 4096], n2 <= n1 <= 2 n2.  Intermediates use
@@ -141,17 +143,24 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
                            const Fft4Geom& g, const float2* tables, hipStream_t s);
 // Pass B: X[k][k1][k2] = sum_i Y[k][k2][i] W_n1^{i k1}.
 void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, hipStream_t s);
+// Spectrum layout of fft4_rowpass under the current flags, as r2c parameters.
+struct Fft4XLayout {
+  int log2_row;
+  uint64_t row_pitch, blk_pitch;
+  int log2_blk;
+};
+Fft4XLayout fft4_x_layout(const Fft4Geom& g);
 // Tuning switches (process-wide, for measurement): kernel shape and store policy.
 enum Fft4Flags : int {
-  kFft4Cpt8 = 1,         // 8 transforms per thread, one thread group (64-byte segments)
+  kFft4Cpt8 = 1,         // 8 transforms per thread, one thread group (else 4 per thread, two groups)
   kFft4NoRemap = 2,      // plain block order (no XCD-contiguous remap)
   kFft4NtStores = 4,     // nontemporal stores
   kFft4SkipCompute = 8,  // timing only: memory traffic without the FFT
-  kFft4Wide = 16,        // 16 transforms per workgroup (128-byte segments, one workgroup per CU)
   kFft4TrialSlow = 32,   // block order: column/row block fastest, trial slowest (write locality)
-  kFft4SkipLoad = 64,    // timing only: synthetic inputs instead of global loads
+  kFft4SkipLoad = 64,    // timing only: synthetic inputs instead of global loads (blocked CPT-8 kernel)
   kFft4SkipStore = 128,  // timing only: no global stores
-  kFft4Blocked = 256,    // blocked Y/X layouts: every lane stores 64 contiguous bytes (CPT 8 only)
+  kFft4Blocked = 256,    // blocked Y/X layouts: every lane stores its transforms' values contiguously
+  kFft4Ch4 = 16,         // with kFft4Blocked: pass B runs 4 transforms per workgroup (4 waves/SIMD)
 };
 void fft4_set_flags(int flags);
 int fft4_flags();

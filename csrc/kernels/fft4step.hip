@@ -45,11 +45,12 @@ constexpr int kLdsBudget = 73728;  // bytes per workgroup: two workgroups per CU
 // segments, two workgroups per CU; 16: 128-byte segments, one per CU).
 template <int L, int CPT, int SUB>
 struct Cfg {
-  static constexpr int CH = CPT * SUB;
+  static constexpr int CH = CPT * SUB;  // transforms per workgroup (blocked layout width when SUB == 1)
+  static_assert(CH == 8 || (CH == 4 && SUB == 1), "workgroups cover 8 (or, blocked, 4) transforms");
   static constexpr int T = L / kPts;                     // threads per group
   static constexpr int THREADS = T * SUB;
   static constexpr int PAD = L + L / 8;                  // padded floats per channel plane
-  static constexpr int BUDGET = CH >= 16 ? 2 * kLdsBudget : kLdsBudget;
+  static constexpr int BUDGET = CH == 4 ? kLdsBudget / 2 : kLdsBudget;  // CH 4: four workgroups per CU
   static constexpr int CG0 = BUDGET / (SUB * 2 * PAD * 4);
   static constexpr int CG = CG0 >= CPT ? CPT : (CG0 >= 4 ? 4 : (CG0 >= 2 ? 2 : 1));  // channels per exchange round
   static constexpr int GROUP_FLOATS = 2 * CG * PAD;
@@ -134,9 +135,8 @@ __device__ __forceinline__ void stage_compute(Vec<CPT>& v, int t, const float2* 
 // gather back in the uniform pattern t + q*T.
 template <int L, int CPT, int CG, int Ns, int R>
 __device__ __forceinline__ void exchange(Vec<CPT>& v, float* __restrict__ lds, int t) {
-  constexpr int T = L / kPts, B = kPts / R, PAD = L + L / 8;
-  float* re = lds;
-  float* im = lds + CG * PAD;
+  constexpr int T = L / kPts, B = kPts / R, PAD = L + L / 8;  // PAD in complex elements
+  float2* buf = reinterpret_cast<float2*>(lds);                   // 8-byte ds_write_b64 / ds_read_b64
 #pragma unroll
   for (int g = 0; g < CPT; g += CG) {
 #pragma unroll
@@ -147,10 +147,7 @@ __device__ __forceinline__ void exchange(Vec<CPT>& v, float* __restrict__ lds, i
       for (int r = 0; r < R; ++r) {
         const int idx = lds_pad(base + r * Ns);
 #pragma unroll
-        for (int cc = 0; cc < CG; ++cc) {
-          re[cc * PAD + idx] = v[g + cc][b + r * B].x;
-          im[cc * PAD + idx] = v[g + cc][b + r * B].y;
-        }
+        for (int cc = 0; cc < CG; ++cc) buf[cc * PAD + idx] = v[g + cc][b + r * B];
       }
     }
     __syncthreads();
@@ -158,7 +155,7 @@ __device__ __forceinline__ void exchange(Vec<CPT>& v, float* __restrict__ lds, i
     for (int q = 0; q < kPts; ++q) {
       const int idx = lds_pad(t + q * T);
 #pragma unroll
-      for (int cc = 0; cc < CG; ++cc) v[g + cc][q] = make_float2(re[cc * PAD + idx], im[cc * PAD + idx]);
+      for (int cc = 0; cc < CG; ++cc) v[g + cc][q] = buf[cc * PAD + idx];
     }
     __syncthreads();
   }
@@ -269,13 +266,18 @@ __global__ void __launch_bounds__(256) fft4_pad_input_kernel(const float* __rest
   }
 }
 
+// Kernel variants: MODE bit 0 = blocked Y/X layouts (CPT 8), bit 1 = timing
+// build honouring the kFft4Skip* flags (tools/kbench.py only).
+constexpr int kModeBlocked = 1, kModeTiming = 2;
+
 // Pass A.  Logical block = column block * K + trial (trial fastest).
-template <int L, int CPT, int SUB>
+template <int L, int CPT, int SUB, int MODE>
 __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2)) fft4_colpass_kernel(
     const float* __restrict__ in, const float* __restrict__ in_pad, uint64_t n, const double* __restrict__ afs, int K,
     float2* __restrict__ Y, Fft4Geom g, const float2* __restrict__ tab, int flags) {
   using C = Cfg<L, CPT, SUB>;
-  __shared__ float lds[C::LDS_FLOATS];
+  constexpr bool kBlocked = MODE & kModeBlocked, kTiming = MODE & kModeTiming;
+  __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   constexpr int T = C::T;
   const int grp = threadIdx.x / T;
   const int t = threadIdx.x - grp * T;
@@ -294,7 +296,7 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
   for (int q = 0; q < kPts; ++q) {
     const uint64_t j = t + q * T;
     float x[2 * CPT];
-    if (flags & kFft4SkipLoad) {
+    if (kTiming && (flags & kFft4SkipLoad)) {
 #pragma unroll
       for (int e = 0; e < 2 * CPT; ++e) x[e] = static_cast<float>(j + e);
     } else {
@@ -304,9 +306,10 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
 #pragma unroll
     for (int c = 0; c < CPT; ++c) v[c][q] = make_float2(x[2 * c], x[2 * c + 1]);
   }
-  if (!(flags & kFft4SkipCompute)) fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n2);
+  if (!kTiming || !(flags & kFft4SkipCompute))
+    fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n2);
   const uint32_t mask = static_cast<uint32_t>(N1) * L - 1;
-  float2* y = Y + static_cast<uint64_t>(k) * g.ystride + c0;
+  float2* yk = Y + static_cast<uint64_t>(k) * g.ystride;
   const bool nt = flags & kFft4NtStores;
 #pragma unroll
   for (int q = 0; q < kPts; ++q) {
@@ -318,20 +321,21 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
       v[c][q] = cmul(v[c][q], w);
       w = cmul(w, step);
     }
-    float2* dst = (flags & kFft4Blocked)
-                      ? Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(c0) * g.n2 + k2 * CPT
-                      : y + static_cast<uint64_t>(k2) * g.ypitch;
-    if (!(flags & kFft4SkipStore) || v[0][q].x == 1234.5f) store_row<CPT>(dst, v, q, nt);
+    // blocked: Y_b[c0/8][k2][c] (each lane 64 contiguous bytes); else Y[k2][i] at pitch ypitch
+    float2* dst = kBlocked ? yk + static_cast<uint64_t>(c0) * g.n2 + k2 * CPT
+                           : yk + static_cast<uint64_t>(k2) * g.ypitch + c0;
+    if (!kTiming || !(flags & kFft4SkipStore) || v[0][q].x == 1234.5f) store_row<CPT>(dst, v, q, nt);
   }
 }
 
 // Pass B.  Logical block = row block * K + trial.
-template <int L, int CPT, int SUB>
+template <int L, int CPT, int SUB, int MODE>
 __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2)) fft4_rowpass_kernel(
     const float2* __restrict__ Y, float2* __restrict__ X, int K, Fft4Geom g, const float2* __restrict__ tab,
     int flags) {
   using C = Cfg<L, CPT, SUB>;
-  __shared__ float lds[C::LDS_FLOATS];
+  constexpr bool kBlocked = MODE & kModeBlocked, kTiming = MODE & kModeTiming;
+  __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   constexpr int T = C::T;
   const int grp = threadIdx.x / T;
   const int t = threadIdx.x - grp * T;
@@ -341,30 +345,32 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
   const int k = static_cast<int>(tslow ? lb / nbt : lb % static_cast<uint32_t>(K));
   const int r0 = static_cast<int>(tslow ? lb % nbt : lb / static_cast<uint32_t>(K)) * C::CH + grp * CPT;
   const TableOffsets to = table_offsets(L, g.n2);
-  const float2* y = Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(r0) * g.ypitch;
-  const float2* yb = Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(r0) * CPT;
-  const bool blocked = flags & kFft4Blocked;
+  const float2* yk = Y + static_cast<uint64_t>(k) * g.ystride;
   Vec<CPT> v;
 #pragma unroll
   for (int c = 0; c < CPT; ++c)
 #pragma unroll
     for (int q = 0; q < kPts; ++q) {
       const uint32_t i = t + q * T;
-      v[c][q] = (flags & kFft4SkipLoad)
-                    ? make_float2(static_cast<float>(t + q), static_cast<float>(c))
-                    : (blocked ? yb[static_cast<uint64_t>(i / CPT) * (CPT * g.n2) + c * CPT + (i % CPT)]
-                               : y[static_cast<uint64_t>(c) * g.ypitch + i]);
+      if (kTiming && (flags & kFft4SkipLoad))
+        v[c][q] = make_float2(static_cast<float>(t + q), static_cast<float>(c));
+      else if (kBlocked)  // Y_b[i/8][r0 + c][i%8] (pass A always writes 8-wide blocks)
+        v[c][q] = yk[static_cast<uint64_t>(i / 8) * (8 * g.n2) + (r0 + c) * 8 + (i % 8)];
+      else
+        v[c][q] = yk[static_cast<uint64_t>(r0 + c) * g.ypitch + i];
     }
-  if (!(flags & kFft4SkipCompute)) fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n1);
-  float2* x = X + static_cast<uint64_t>(k) * g.xstride + r0;
+  if (!kTiming || !(flags & kFft4SkipCompute))
+    fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n1);
+  float2* xk = X + static_cast<uint64_t>(k) * g.xstride;
   const bool nt = flags & kFft4NtStores;
 #pragma unroll
-  for (int q = 0; q < kPts; ++q)
-    if (!(flags & kFft4SkipStore) || v[0][q].x == 1234.5f)
-      store_row<CPT>(blocked ? X + static_cast<uint64_t>(k) * g.xstride + static_cast<uint64_t>(r0) * L +
-                                   static_cast<uint64_t>(t + q * T) * CPT
-                             : x + static_cast<uint64_t>(t + q * T) * g.xpitch,
-                     v, q, nt);
+  for (int q = 0; q < kPts; ++q) {
+    const uint64_t k1 = t + q * T;
+    // blocked: X_b[r0/8][k1][r0%8 + c] (8-wide blocks; a 4-transform workgroup
+    // writes one 32-byte half); else X[k1][k2] at pitch xpitch
+    float2* dst = kBlocked ? xk + static_cast<uint64_t>(r0 / 8) * (8 * L) + k1 * 8 + (r0 % 8) : xk + k1 * g.xpitch + r0;
+    if (!kTiming || !(flags & kFft4SkipStore) || v[0][q].x == 1234.5f) store_row<CPT>(dst, v, q, nt);
+  }
 }
 
 bool supported_len(int L) { return L >= 128 && L <= 4096 && (L & (L - 1)) == 0; }
@@ -414,19 +420,16 @@ void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& 
 }
 
 namespace {
-int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked;  // fastest measured shape (tools/kbench.py)
+int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4Ch4;  // fastest measured shape (tools/kbench.py)
 
-template <int CPT, int SUB>
+template <int CPT, int SUB, int MODE>
 void launch_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
                     const Fft4Geom& g, const float2* tables, dim3 grid, int flags, hipStream_t s) {
   switch (g.n2) {
-#define PS_CASE(LL)                                                                                       \
-  case LL:                                                                                                \
-    if constexpr (Cfg<LL, CPT, SUB>::THREADS <= 1024)                                                     \
-      fft4_colpass_kernel<LL, CPT, SUB><<<grid, Cfg<LL, CPT, SUB>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g, \
-                                                                                      tables, flags);     \
-    else                                                                                                  \
-      PSOUP_THROW("fft4: workgroup too large");                                                           \
+#define PS_CASE(LL)                                                                                          \
+  case LL:                                                                                                   \
+    fft4_colpass_kernel<LL, CPT, SUB, MODE><<<grid, Cfg<LL, CPT, SUB>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g, \
+                                                                                       tables, flags);       \
     break;
     PS_CASE(128) PS_CASE(256) PS_CASE(512) PS_CASE(1024) PS_CASE(2048) PS_CASE(4096)
 #undef PS_CASE
@@ -434,25 +437,30 @@ void launch_colpass(const float* in, const float* in_pad, uint64_t n, const doub
   }
 }
 
-template <int CPT, int SUB>
+template <int CPT, int SUB, int MODE>
 void launch_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, dim3 grid, int flags,
                     hipStream_t s) {
   switch (g.n1) {
-#define PS_CASE(LL)                                                                                    \
-  case LL:                                                                                             \
-    if constexpr (Cfg<LL, CPT, SUB>::THREADS <= 1024)                                                  \
-      fft4_rowpass_kernel<LL, CPT, SUB><<<grid, Cfg<LL, CPT, SUB>::THREADS, 0, s>>>(Y, X, K, g, tables, flags); \
-    else                                                                                               \
-      PSOUP_THROW("fft4: workgroup too large");                                                        \
+#define PS_CASE(LL)                                                                                             \
+  case LL:                                                                                                      \
+    fft4_rowpass_kernel<LL, CPT, SUB, MODE><<<grid, Cfg<LL, CPT, SUB>::THREADS, 0, s>>>(Y, X, K, g, tables, flags); \
     break;
     PS_CASE(128) PS_CASE(256) PS_CASE(512) PS_CASE(1024) PS_CASE(2048) PS_CASE(4096)
 #undef PS_CASE
     default: PSOUP_THROW("fft4: unsupported row length " << g.n1);
   }
 }
+
+constexpr int kTimingFlags = kFft4SkipLoad | kFft4SkipStore | kFft4SkipCompute;
 }  // namespace
 
 void fft4_set_flags(int flags) { g_fft4_flags = flags; }
+
+Fft4XLayout fft4_x_layout(const Fft4Geom& g) {
+  const int f = g_fft4_flags;
+  if ((f & kFft4Blocked) && (f & (kFft4Cpt8 | kFft4Ch4))) return {g.log2_xrow, 8, 8ull * g.n1, 3};
+  return {g.log2_xrow, g.xpitch, 8, 3};
+}
 int fft4_flags() { return g_fft4_flags; }
 
 void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
@@ -460,18 +468,19 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   PSOUP_CHECK(g.ok && K >= 1 && n == 2ull * g.n1 * g.n2, "fft4 colpass: bad geometry n=" << n << " K=" << K);
   PSOUP_CHECK((reinterpret_cast<uintptr_t>(Y) & 63) == 0, "fft4 colpass: Y alignment");
   const int f = g_fft4_flags;
-  const int ch = (f & kFft4Wide) ? 16 : 8;
-  const uint64_t nblocks = static_cast<uint64_t>(g.n1 / ch) * K;
+  const uint64_t nblocks = static_cast<uint64_t>(g.n1 / 8) * K;
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 8 == 0, "fft4 colpass: grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
-  if ((f & kFft4Wide) && (f & kFft4Cpt8))
-    launch_colpass<8, 2>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
-  else if (f & kFft4Wide)
-    launch_colpass<4, 4>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  if ((f & kFft4Blocked) && (f & kFft4Ch4) && !(f & kTimingFlags))  // Y stays 8-wide; only pass B narrows
+    launch_colpass<8, 1, kModeBlocked>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  else if (f & kTimingFlags)
+    launch_colpass<8, 1, kModeBlocked | kModeTiming>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  else if ((f & kFft4Cpt8) && (f & kFft4Blocked))
+    launch_colpass<8, 1, kModeBlocked>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   else if (f & kFft4Cpt8)
-    launch_colpass<8, 1>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+    launch_colpass<8, 1, 0>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   else
-    launch_colpass<4, 2>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+    launch_colpass<4, 2, 0>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   post_launch_check("fft4_colpass_kernel", s);
 }
 
@@ -479,18 +488,20 @@ void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const fl
   PSOUP_CHECK(g.ok && K >= 1, "fft4 rowpass: bad geometry");
   PSOUP_CHECK((reinterpret_cast<uintptr_t>(X) & 63) == 0, "fft4 rowpass: X alignment");
   const int f = g_fft4_flags;
-  const int ch = (f & kFft4Wide) ? 16 : 8;
+  const int ch = ((f & kFft4Blocked) && (f & kFft4Ch4) && !(f & kTimingFlags)) ? 4 : 8;
   const uint64_t nblocks = static_cast<uint64_t>(g.n2 / ch) * K;
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 8 == 0, "fft4 rowpass: grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
-  if ((f & kFft4Wide) && (f & kFft4Cpt8))
-    launch_rowpass<8, 2>(Y, X, K, g, tables, grid, f, s);
-  else if (f & kFft4Wide)
-    launch_rowpass<4, 4>(Y, X, K, g, tables, grid, f, s);
+  if (ch == 4)
+    launch_rowpass<4, 1, kModeBlocked>(Y, X, K, g, tables, grid, f, s);
+  else if (f & kTimingFlags)
+    launch_rowpass<8, 1, kModeBlocked | kModeTiming>(Y, X, K, g, tables, grid, f, s);
+  else if ((f & kFft4Cpt8) && (f & kFft4Blocked))
+    launch_rowpass<8, 1, kModeBlocked>(Y, X, K, g, tables, grid, f, s);
   else if (f & kFft4Cpt8)
-    launch_rowpass<8, 1>(Y, X, K, g, tables, grid, f, s);
+    launch_rowpass<8, 1, 0>(Y, X, K, g, tables, grid, f, s);
   else
-    launch_rowpass<4, 2>(Y, X, K, g, tables, grid, f, s);
+    launch_rowpass<4, 2, 0>(Y, X, K, g, tables, grid, f, s);
   post_launch_check("fft4_rowpass_kernel", s);
 }
 

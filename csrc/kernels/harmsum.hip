@@ -58,21 +58,27 @@ __device__ __forceinline__ float2 r2c_combine(float2 za, float2 zb, float c, flo
 }
 
 // Address of bin k = k2 + 2^log2_row * k1 in a (possibly blocked) layout:
-// (k2 >> 3) * blk + k1 * pitch + (k2 & 7).
-__device__ __forceinline__ uint64_t zaddr(uint64_t k, int log2_row, uint64_t pitch, uint64_t blk) {
+// (k2 >> lw) * blk + k1 * pitch + (k2 & (2^lw - 1)).
+__device__ __forceinline__ uint64_t zaddr(uint64_t k, int log2_row, uint64_t pitch, uint64_t blk, int lw) {
   const uint64_t k2 = k & ((uint64_t(1) << log2_row) - 1);
-  return (k2 >> 3) * blk + (k >> log2_row) * pitch + (k2 & 7);
+  return (k2 >> lw) * blk + (k >> log2_row) * pitch + (k2 & ((uint64_t(1) << lw) - 1));
 }
 
-// One workgroup per tile of 256 bins k in [k0, k0+256), k <= M/2: both the
-// ascending bins k and their mirrors M-k come from the same loads
-// Z[k], Z[M-k]; one halo bin each side feeds the interbin neighbour.
+// One workgroup per tile of 1024 bins k in [k0, k0+1024), k <= M/2, four
+// bins per thread 256 apart (so every load instruction reads 64 consecutive
+// bins, whatever the spectrum layout): both the ascending bins k and their
+// mirrors M-k come from the same pair of loads Z[k], Z[M-k] (all eight loads
+// of a thread are issued before any is used); one halo bin each side feeds
+// the interbin neighbour.  One sincospi per thread: the twiddles of the other
+// three bins are W^k * W^(256u), precomputed per block.
+constexpr int kR2cBpt = 4;
+constexpr int kR2cTile = 256 * kR2cBpt;
+
 __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
-    const float2* __restrict__ Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t pitch, uint64_t blk,
-    float* __restrict__ P,
-    uint64_t pstride, uint64_t nbins_out, const float* __restrict__ stats, float nscale) {
-  __shared__ float2 A[258];  // A[u] = X[k0 - 1 + u]
-  __shared__ float2 D[258];  // D[u] = X[M - (k0 - 1 + u)]
+    const float2* __restrict__ Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t pitch, uint64_t blk, int lw,
+    float* __restrict__ P, uint64_t pstride, uint64_t nbins_out, const float* __restrict__ stats, float nscale) {
+  __shared__ float2 A[kR2cTile + 2];  // A[u] = X[k0 - 1 + u]
+  __shared__ float2 D[kR2cTile + 2];  // D[u] = X[M - (k0 - 1 + u)]
   const int kk = blockIdx.y;
   const int t = threadIdx.x;
   const float2* z = Z + static_cast<uint64_t>(kk) * zstride;
@@ -80,33 +86,58 @@ __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
   const float mean = stats[0] * nscale;
   const float sigma = stats[2] * nscale;
   const uint64_t half = M / 2;
-  auto pair = [&](int64_t k, int u) {
+  float2 wu[kR2cBpt];  // W^(256 u), W = e^{-i pi / M}
+#pragma unroll
+  for (int u = 0; u < kR2cBpt; ++u)
+    sincospif(-static_cast<float>(256 * u) / static_cast<float>(M), &wu[u].y, &wu[u].x);
+  auto halo = [&](int64_t k, int u) {
     if (k < 0 || static_cast<uint64_t>(k) > half + 1) {
       A[u] = D[u] = make_float2(0.f, 0.f);
       return;
     }
     const uint64_t uk = static_cast<uint64_t>(k);
-    const uint64_t a = uk & (M - 1), b = (M - uk) & (M - 1);
-    const float2 za = z[zaddr(a, log2_row, pitch, blk)], zb = z[zaddr(b, log2_row, pitch, blk)];
+    const float2 za = z[zaddr(uk & (M - 1), log2_row, pitch, blk, lw)];
+    const float2 zb = z[zaddr((M - uk) & (M - 1), log2_row, pitch, blk, lw)];
     float sn, cs;
     sincospif(-static_cast<float>(uk) / static_cast<float>(M), &sn, &cs);
     A[u] = r2c_combine(za, zb, cs, sn);
     D[u] = r2c_combine(zb, za, -cs, sn);  // angle -pi (M-k)/M = -pi + pi k/M
   };
-  for (uint64_t k0 = static_cast<uint64_t>(blockIdx.x) * 256; k0 <= half;
-       k0 += static_cast<uint64_t>(gridDim.x) * 256) {
-    pair(static_cast<int64_t>(k0 + t), t + 1);
-    if (t == 0) pair(static_cast<int64_t>(k0) - 1, 0);
-    if (t == 1) pair(static_cast<int64_t>(k0 + 256), 257);
+  for (uint64_t k0 = static_cast<uint64_t>(blockIdx.x) * kR2cTile; k0 <= half;
+       k0 += static_cast<uint64_t>(gridDim.x) * kR2cTile) {
+    const uint64_t kb = k0 + static_cast<uint64_t>(t);
+    float2 za[kR2cBpt], zb[kR2cBpt];
+#pragma unroll
+    for (int u = 0; u < kR2cBpt; ++u) {
+      const uint64_t k = kb + 256 * u;
+      const bool ok = k <= half + 1;
+      za[u] = ok ? z[zaddr(k & (M - 1), log2_row, pitch, blk, lw)] : make_float2(0.f, 0.f);
+      zb[u] = ok ? z[zaddr((M - k) & (M - 1), log2_row, pitch, blk, lw)] : make_float2(0.f, 0.f);
+    }
+    if (t == 0) halo(static_cast<int64_t>(k0) - 1, 0);
+    if (t == 1) halo(static_cast<int64_t>(k0 + kR2cTile), kR2cTile + 1);
+    float sn, cs;
+    sincospif(-static_cast<float>(kb) / static_cast<float>(M), &sn, &cs);
+#pragma unroll
+    for (int u = 0; u < kR2cBpt; ++u) {
+      const float c = cs * wu[u].x - sn * wu[u].y, s = cs * wu[u].y + sn * wu[u].x;  // W^(kb+256u)
+      const int slot = t + 256 * u + 1;
+      A[slot] = r2c_combine(za[u], zb[u], c, s);
+      D[slot] = r2c_combine(zb[u], za[u], -c, s);
+    }
     __syncthreads();
-    const uint64_t k = k0 + t;
-    if (k <= half) {
-      if (k < nbins_out) {
-        const float2 xl = k > 0 ? A[t] : make_float2(0.f, 0.f);
-        p[k] = (dev::interbin(A[t + 1], xl) - mean) / sigma;
+#pragma unroll
+    for (int u = 0; u < kR2cBpt; ++u) {
+      const uint64_t k = kb + 256 * u;
+      const int slot = t + 256 * u + 1;
+      if (k <= half) {
+        if (k < nbins_out) {
+          const float2 xl = k > 0 ? A[slot - 1] : make_float2(0.f, 0.f);
+          p[k] = (dev::interbin(A[slot], xl) - mean) / sigma;
+        }
+        const uint64_t j = M - k;  // mirrored bin (> M/2), neighbour X[j-1] = D[slot+1]
+        if (j > half && j < nbins_out) p[j] = (dev::interbin(D[slot], D[slot + 1]) - mean) / sigma;
       }
-      const uint64_t j = M - k;  // mirrored bin (> M/2), neighbour X[j-1] = D[t+2]
-      if (j > half && j < nbins_out) p[j] = (dev::interbin(D[t + 1], D[t + 2]) - mean) / sigma;
     }
     __syncthreads();
   }
@@ -283,17 +314,17 @@ void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride,
 }
 
 void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t row_pitch,
-                                  uint64_t blk_pitch, float* P, uint64_t pstride, int K, uint64_t nbins_out,
-                                  const float* stats, float nscale, hipStream_t s) {
+                                  uint64_t blk_pitch, int log2_blk, float* P, uint64_t pstride, int K,
+                                  uint64_t nbins_out, const float* stats, float nscale, hipStream_t s) {
   PSOUP_CHECK(K >= 1 && K <= 65535, "bad batch");
   PSOUP_CHECK(M >= 2 && (M & (M - 1)) == 0, "r2c: M must be a power of two");
   PSOUP_CHECK(nbins_out <= M + 1, "nbins_out beyond the spectrum");
   PSOUP_CHECK(log2_row >= 0 && log2_row < 63 && (uint64_t(1) << log2_row) <= M, "r2c: bad row layout");
   if (nbins_out == 0) return;
-  dim3 grid(dev::grid_for(M / 2 + 1, 256, 2048), static_cast<unsigned>(K));
-  PSOUP_CHECK(log2_row >= 3 || blk_pitch == 8, "r2c: blocked layout needs rows of >= 8 bins");
-  r2c_interbin_normalise_batch_kernel<<<grid, 256, 0, s>>>(Z, M, zstride, log2_row, row_pitch, blk_pitch, P, pstride,
-                                                           nbins_out, stats, nscale);
+  dim3 grid(dev::grid_for((M / 2 + 1 + kR2cBpt - 1) / kR2cBpt, 256, 2048), static_cast<unsigned>(K));
+  PSOUP_CHECK(log2_blk >= 0 && log2_blk <= log2_row, "r2c: bad block layout");
+  r2c_interbin_normalise_batch_kernel<<<grid, 256, 0, s>>>(Z, M, zstride, log2_row, row_pitch, blk_pitch, log2_blk, P,
+                                                           pstride, nbins_out, stats, nscale);
   post_launch_check("r2c_interbin_normalise_batch_kernel", s);
 }
 

@@ -424,10 +424,15 @@ PYBIND11_MODULE(_C, m) {
                                    P<const float>(stats), nscale, S(s));
   });
   k.def("r2c_interbin_normalise_batch", [](uintptr_t Z, uint64_t M, uint64_t zstride, int log2_row,
-                                           uint64_t row_pitch, uint64_t blk_pitch, uintptr_t Pout, uint64_t pstride,
-                                           int K, uint64_t nbo, uintptr_t stats, float nscale, uintptr_t s) {
-    kern::r2c_interbin_normalise_batch(P<const float2>(Z), M, zstride, log2_row, row_pitch, blk_pitch, P<float>(Pout),
-                                       pstride, K, nbo, P<const float>(stats), nscale, S(s));
+                                           uint64_t row_pitch, uint64_t blk_pitch, int log2_blk, uintptr_t Pout,
+                                           uint64_t pstride, int K, uint64_t nbo, uintptr_t stats, float nscale,
+                                           uintptr_t s) {
+    kern::r2c_interbin_normalise_batch(P<const float2>(Z), M, zstride, log2_row, row_pitch, blk_pitch, log2_blk,
+                                       P<float>(Pout), pstride, K, nbo, P<const float>(stats), nscale, S(s));
+  });
+  k.def("fft4_x_layout", [](const kern::Fft4Geom& g) {
+    kern::Fft4XLayout l = kern::fft4_x_layout(g);
+    return py::make_tuple(l.log2_row, l.row_pitch, l.blk_pitch, l.log2_blk);
   });
   py::class_<kern::Fft4Geom>(k, "Fft4Geom")
       .def_readonly("ok", &kern::Fft4Geom::ok)

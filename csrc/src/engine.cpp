@@ -316,12 +316,11 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
     batch_plan(count).execute(res_.data(), spec_.data(), stream_);
   }
   const uint64_t pst = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
-  const int zrow_log2 = mode_ == 2 ? f4_.log2_xrow : ilog2(n_ / 2);
-  const bool blocked = mode_ == 2 && (kern::fft4_flags() & kern::kFft4Blocked);
-  const uint64_t zrow_pitch = mode_ == 2 ? (blocked ? 8 : f4_.xpitch) : n_ / 2;
-  const uint64_t zblk_pitch = blocked ? 8ull * f4_.n1 : 8;
+  const kern::Fft4XLayout xl =
+      mode_ == 2 ? kern::fft4_x_layout(f4_) : kern::Fft4XLayout{ilog2(n_ / 2), n_ / 2, 8, 3};
   if (mode_ >= 1)
-    kern::r2c_interbin_normalise_batch(spec_.data(), n_ / 2, xs_, zrow_log2, zrow_pitch, zblk_pitch, P_.data(), pst, count, static_cast<uint64_t>(hi_),
+    kern::r2c_interbin_normalise_batch(spec_.data(), n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch,
+                                       xl.log2_blk, P_.data(), pst, count, static_cast<uint64_t>(hi_),
                                        wh_->stats(), static_cast<float>(n_), stream_);
   else
     kern::interbin_normalise_batch(spec_.data(), nb_, nb_, P_.data(), pst, count, static_cast<uint64_t>(hi_),

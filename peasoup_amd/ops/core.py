@@ -193,7 +193,7 @@ def r2c_interbin_normalise(x: torch.Tensor, stats: torch.Tensor, nscale: float,
     Z = torch.fft.fft(torch.view_as_complex(x.contiguous().view(Kb, M, 2)), dim=-1).contiguous()
     nbo = nbins_out or (M + 1)
     P = torch.empty((Kb, nbo), dtype=torch.float32, device=x.device)
-    K.r2c_interbin_normalise_batch(_cplx_ptr(Z), M, M, M.bit_length() - 1, M, 8, P.data_ptr(), nbo, Kb, nbo,
+    K.r2c_interbin_normalise_batch(_cplx_ptr(Z), M, M, M.bit_length() - 1, M, 8, 3, P.data_ptr(), nbo, Kb, nbo,
                                    stats.data_ptr(), float(nscale), _s())
     return P
 
@@ -235,11 +235,9 @@ def _fft4_padded(x: torch.Tensor, accels: Sequence[float], tsamp: float):
 
 
 def fft4_x_layout(g):
-    """(log2_row, row_pitch, blk_pitch) of the fused FFT's spectrum layout
-    under the current kernel flags (blocked or padded natural order)."""
-    if K.fft4_flags() & 256:  # kFft4Blocked
-        return g.log2_xrow, 8, 8 * g.n1
-    return g.log2_xrow, g.xpitch, 8
+    """(log2_row, row_pitch, blk_pitch, log2_blk) of the fused FFT's spectrum
+    layout under the current kernel flags (blocked or padded natural order)."""
+    return K.fft4_x_layout(g)
 
 
 def fft4_resample_spectrum(x: torch.Tensor, accels: Sequence[float], tsamp: float) -> torch.Tensor:
@@ -248,10 +246,10 @@ def fft4_resample_spectrum(x: torch.Tensor, accels: Sequence[float], tsamp: floa
     g, X = _fft4_padded(x, accels, tsamp)
     Kb = X.shape[0]
     M = g.n1 * g.n2
-    log2_row, row, blk = fft4_x_layout(g)
+    log2_row, row, blk, lw = fft4_x_layout(g)
     k = torch.arange(M, device=x.device, dtype=torch.int64)
     k2 = k & (g.n2 - 1)
-    addr = (k2 >> 3) * blk + (k >> log2_row) * row + (k2 & 7)
+    addr = (k2 >> lw) * blk + (k >> log2_row) * row + (k2 & ((1 << lw) - 1))
     Xc = torch.view_as_complex(X)  # [K, xstride]
     return Xc[:, addr].contiguous()
 
@@ -264,9 +262,9 @@ def fft4_resample_interbin(x: torch.Tensor, accels: Sequence[float], tsamp: floa
     g, X = _fft4_padded(x, accels, tsamp)
     Kb = X.shape[0]
     M = g.n1 * g.n2
-    log2_row, row, blk = fft4_x_layout(g)
+    log2_row, row, blk, lw = fft4_x_layout(g)
     P = torch.empty((Kb, M + 1), dtype=torch.float32, device=x.device)
-    K.r2c_interbin_normalise_batch(X.data_ptr(), M, g.xstride, log2_row, row, blk, P.data_ptr(), M + 1, Kb, M + 1,
+    K.r2c_interbin_normalise_batch(X.data_ptr(), M, g.xstride, log2_row, row, blk, lw, P.data_ptr(), M + 1, Kb, M + 1,
                                    stats.data_ptr(), float(nscale), _s())
     return P
 

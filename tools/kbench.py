@@ -78,12 +78,12 @@ def main():
         report(f"colpass flags={f}", tc, K * 8 * M)
         tr = timeit(lambda: K_.fft4_rowpass(Y.data_ptr(), X.data_ptr(), K, g, tab.data_ptr(), s), a.reps)
         report(f"rowpass flags={f}", tr, K * 16 * M)
-    for blocked in (False, True):
-        row, blk = (8, 8 * g.n1) if blocked else (g.xpitch, 8)
-        tz = timeit(lambda: K_.r2c_interbin_normalise_batch(X.data_ptr(), M, g.xstride, g.log2_xrow, row, blk,
+    for blk_w in (0, 4, 8):
+        row, blk, lw = (g.xpitch, 8, 3) if blk_w == 0 else (blk_w, blk_w * g.n1, blk_w.bit_length() - 1)
+        tz = timeit(lambda: K_.r2c_interbin_normalise_batch(X.data_ptr(), M, g.xstride, g.log2_xrow, row, blk, lw,
                                                             P.data_ptr(), M + 1, K, M + 1, st.data_ptr(), float(n), s),
                     a.reps)
-        report(f"r2c_interbin_normalise blocked={blocked}", tz, K * (8 * M + 4 * M))
+        report(f"r2c_interbin_normalise block={blk_w}", tz, K * (8 * M + 4 * M))
     K_.fft4_set_flags(0)
     # harmonic peaks on normal noise (threshold 9 -> few peaks)
     P.normal_()
