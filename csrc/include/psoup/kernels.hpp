@@ -161,6 +161,7 @@ enum Fft4Flags : int {
   kFft4SkipStore = 128,  // timing only: no global stores
   kFft4Blocked = 256,    // blocked Y/X layouts: every lane stores its transforms' values contiguously
   kFft4Ch4 = 16,         // with kFft4Blocked: pass B runs 4 transforms per workgroup (4 waves/SIMD)
+  kFft4TileY = 1024,     // with kFft4Blocked: 8x8-tiled Y between the passes (16-byte pass-B loads)
 };
 void fft4_set_flags(int flags);
 int fft4_flags();

@@ -268,7 +268,10 @@ __global__ void __launch_bounds__(256) fft4_pad_input_kernel(const float* __rest
 
 // Kernel variants: MODE bit 0 = blocked Y/X layouts (CPT 8), bit 1 = timing
 // build honouring the kFft4Skip* flags (tools/kbench.py only).
-constexpr int kModeBlocked = 1, kModeTiming = 2;
+// bit 2 = tiled Y (pass A -> pass B): Y_t[i/8][k2/8][i%8][k2%8], so a pass-B
+// lane reads its rows' values as contiguous 16-byte vectors and eight lanes
+// cover 512 contiguous bytes.
+constexpr int kModeBlocked = 1, kModeTiming = 2, kModeTileY = 4;
 
 // Pass A.  Logical block = column block * K + trial (trial fastest).
 template <int L, int CPT, int SUB, int MODE>
@@ -276,7 +279,8 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
     const float* __restrict__ in, const float* __restrict__ in_pad, uint64_t n, const double* __restrict__ afs, int K,
     float2* __restrict__ Y, Fft4Geom g, const float2* __restrict__ tab, int flags) {
   using C = Cfg<L, CPT, SUB>;
-  constexpr bool kBlocked = MODE & kModeBlocked, kTiming = MODE & kModeTiming;
+  constexpr bool kBlocked = MODE & kModeBlocked, kTiming = MODE & kModeTiming, kTileY = MODE & kModeTileY;
+  static_assert(!kTileY || (CPT == 8 && SUB == 1), "tiled Y needs 8 transforms per thread");
   __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   constexpr int T = C::T;
   const int grp = threadIdx.x / T;
@@ -321,10 +325,16 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
       v[c][q] = cmul(v[c][q], w);
       w = cmul(w, step);
     }
-    // blocked: Y_b[c0/8][k2][c] (each lane 64 contiguous bytes); else Y[k2][i] at pitch ypitch
-    float2* dst = kBlocked ? yk + static_cast<uint64_t>(c0) * g.n2 + k2 * CPT
-                           : yk + static_cast<uint64_t>(k2) * g.ypitch + c0;
-    if (!kTiming || !(flags & kFft4SkipStore) || v[0][q].x == 1234.5f) store_row<CPT>(dst, v, q, nt);
+    if constexpr (kTileY) {
+      float2* dst = yk + static_cast<uint64_t>(c0) * g.n2 + (k2 >> 3) * 64 + (k2 & 7);
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) dst[c * 8] = v[c][q];
+    } else {
+      // blocked: Y_b[c0/8][k2][c] (each lane 64 contiguous bytes); else Y[k2][i] at pitch ypitch
+      float2* dst = kBlocked ? yk + static_cast<uint64_t>(c0) * g.n2 + k2 * CPT
+                             : yk + static_cast<uint64_t>(k2) * g.ypitch + c0;
+      if (!kTiming || !(flags & kFft4SkipStore) || v[0][q].x == 1234.5f) store_row<CPT>(dst, v, q, nt);
+    }
   }
 }
 
@@ -334,7 +344,7 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
     const float2* __restrict__ Y, float2* __restrict__ X, int K, Fft4Geom g, const float2* __restrict__ tab,
     int flags) {
   using C = Cfg<L, CPT, SUB>;
-  constexpr bool kBlocked = MODE & kModeBlocked, kTiming = MODE & kModeTiming;
+  constexpr bool kBlocked = MODE & kModeBlocked, kTiming = MODE & kModeTiming, kTileY = MODE & kModeTileY;
   __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   constexpr int T = C::T;
   const int grp = threadIdx.x / T;
@@ -347,6 +357,20 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
   const TableOffsets to = table_offsets(L, g.n2);
   const float2* yk = Y + static_cast<uint64_t>(k) * g.ystride;
   Vec<CPT> v;
+  if constexpr (kTileY) {
+#pragma unroll
+    for (int q = 0; q < kPts; ++q) {
+      const uint32_t i = t + q * T;
+      const float4* src = reinterpret_cast<const float4*>(yk + static_cast<uint64_t>(i >> 3) * (8 * g.n2) +
+                                                          (r0 >> 3) * 64 + (i & 7) * 8 + (r0 & 7));
+#pragma unroll
+      for (int c2 = 0; c2 < CPT / 2; ++c2) {
+        const float4 w = src[c2];
+        v[2 * c2][q] = make_float2(w.x, w.y);
+        v[2 * c2 + 1][q] = make_float2(w.z, w.w);
+      }
+    }
+  } else
 #pragma unroll
   for (int c = 0; c < CPT; ++c)
 #pragma unroll
@@ -420,7 +444,7 @@ void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& 
 }
 
 namespace {
-int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4Ch4;  // fastest measured shape (tools/kbench.py)
+int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4TileY;  // fastest measured shape (tools/kbench.py)
 
 template <int CPT, int SUB, int MODE>
 void launch_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
@@ -471,7 +495,9 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   const uint64_t nblocks = static_cast<uint64_t>(g.n1 / 8) * K;
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 8 == 0, "fft4 colpass: grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
-  if ((f & kFft4Blocked) && (f & kFft4Ch4) && !(f & kTimingFlags))  // Y stays 8-wide; only pass B narrows
+  if ((f & kFft4Blocked) && (f & kFft4TileY) && !(f & kTimingFlags))
+    launch_colpass<8, 1, kModeBlocked | kModeTileY>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  else if ((f & kFft4Blocked) && (f & kFft4Ch4) && !(f & kTimingFlags))  // Y stays 8-wide; only pass B narrows
     launch_colpass<8, 1, kModeBlocked>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   else if (f & kTimingFlags)
     launch_colpass<8, 1, kModeBlocked | kModeTiming>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
@@ -492,7 +518,12 @@ void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const fl
   const uint64_t nblocks = static_cast<uint64_t>(g.n2 / ch) * K;
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 8 == 0, "fft4 rowpass: grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
-  if (ch == 4)
+  const bool tiley = (f & kFft4Blocked) && (f & kFft4TileY) && !(f & kTimingFlags);
+  if (ch == 4 && tiley)
+    launch_rowpass<4, 1, kModeBlocked | kModeTileY>(Y, X, K, g, tables, grid, f, s);
+  else if (tiley)
+    launch_rowpass<8, 1, kModeBlocked | kModeTileY>(Y, X, K, g, tables, grid, f, s);
+  else if (ch == 4)
     launch_rowpass<4, 1, kModeBlocked>(Y, X, K, g, tables, grid, f, s);
   else if (f & kTimingFlags)
     launch_rowpass<8, 1, kModeBlocked | kModeTiming>(Y, X, K, g, tables, grid, f, s);
