@@ -120,6 +120,11 @@ void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride,
                                   uint64_t blk_pitch, int log2_blk, float* P, uint64_t pstride, int K,
                                   uint64_t nbins_out, const float* stats, float nscale, hipStream_t s);
 
+// Same output from the 8x8-tiled spectrum of fft4 pass B (kFft4TileX):
+// bin k = k2 + n2*k1 at X[k2/8][k1/8][k2%8][k1%8]; 64-byte loads per thread.
+void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstride, float* P, uint64_t pstride,
+                                  int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s);
+
 // Fused resample + four-step FFT (fft4step.hip).  M = N/2 = n1*n2 with
 // n1, n2 powers of two in [128, 4096], n2 <= n1 <= 2 n2.  Intermediates use
 // padded row pitches (power-of-two strides would camp on one memory channel):
@@ -148,6 +153,7 @@ struct Fft4XLayout {
   int log2_row;
   uint64_t row_pitch, blk_pitch;
   int log2_blk;
+  bool tiled;  // kFft4TileX: use r2c_interbin_normalise_tiled
 };
 Fft4XLayout fft4_x_layout(const Fft4Geom& g);
 // Tuning switches (process-wide, for measurement): kernel shape and store policy.
@@ -162,6 +168,7 @@ enum Fft4Flags : int {
   kFft4Blocked = 256,    // blocked Y/X layouts: every lane stores its transforms' values contiguously
   kFft4Ch4 = 16,         // with kFft4Blocked: pass B runs 4 transforms per workgroup (4 waves/SIMD)
   kFft4TileY = 1024,     // with kFft4Blocked: 8x8-tiled Y between the passes (16-byte pass-B loads)
+  kFft4TileX = 2048,     // with kFft4TileY: 8x8-tiled spectrum X (coalesced pass-B stores; tiled r2c)
 };
 void fft4_set_flags(int flags);
 int fft4_flags();

@@ -271,7 +271,8 @@ __global__ void __launch_bounds__(256) fft4_pad_input_kernel(const float* __rest
 // bit 2 = tiled Y (pass A -> pass B): Y_t[i/8][k2/8][i%8][k2%8], so a pass-B
 // lane reads its rows' values as contiguous 16-byte vectors and eight lanes
 // cover 512 contiguous bytes.
-constexpr int kModeBlocked = 1, kModeTiming = 2, kModeTileY = 4;
+// bit 3 = tiled X: X_t[k2/8][k1/8][k2%8][k1%8] (read by r2c_interbin_normalise_tiled).
+constexpr int kModeBlocked = 1, kModeTiming = 2, kModeTileY = 4, kModeTileX = 8;
 
 // Pass A.  Logical block = column block * K + trial (trial fastest).
 template <int L, int CPT, int SUB, int MODE>
@@ -387,6 +388,16 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
     fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n1);
   float2* xk = X + static_cast<uint64_t>(k) * g.xstride;
   const bool nt = flags & kFft4NtStores;
+  if constexpr ((MODE & kModeTileX) != 0) {
+#pragma unroll
+    for (int q = 0; q < kPts; ++q) {
+      const uint64_t k1 = t + q * T;
+      float2* dst = xk + static_cast<uint64_t>(r0 >> 3) * (8 * L) + (k1 >> 3) * 64 + (r0 & 7) * 8 + (k1 & 7);
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) dst[c * 8] = v[c][q];
+    }
+    return;
+  }
 #pragma unroll
   for (int q = 0; q < kPts; ++q) {
     const uint64_t k1 = t + q * T;
@@ -444,7 +455,7 @@ void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& 
 }
 
 namespace {
-int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4TileY;  // fastest measured shape (tools/kbench.py)
+int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4TileY | kFft4TileX;  // fastest measured (tools/kbench.py)
 
 template <int CPT, int SUB, int MODE>
 void launch_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
@@ -480,10 +491,17 @@ constexpr int kTimingFlags = kFft4SkipLoad | kFft4SkipStore | kFft4SkipCompute;
 
 void fft4_set_flags(int flags) { g_fft4_flags = flags; }
 
+// The tiled spectrum needs 8 x 256 r2c tiles: n2 >= 256, n1 >= 16.
+bool tiled_x(const Fft4Geom& g, int f) {
+  return (f & kFft4Blocked) && (f & kFft4TileY) && (f & kFft4TileX) && !(f & kTimingFlags) && g.n2 >= 256 &&
+         g.n1 >= 16;
+}
+
 Fft4XLayout fft4_x_layout(const Fft4Geom& g) {
   const int f = g_fft4_flags;
-  if ((f & kFft4Blocked) && (f & (kFft4Cpt8 | kFft4Ch4))) return {g.log2_xrow, 8, 8ull * g.n1, 3};
-  return {g.log2_xrow, g.xpitch, 8, 3};
+  if (tiled_x(g, f)) return {g.log2_xrow, 0, 0, 3, true};
+  if ((f & kFft4Blocked) && (f & (kFft4Cpt8 | kFft4Ch4))) return {g.log2_xrow, 8, 8ull * g.n1, 3, false};
+  return {g.log2_xrow, g.xpitch, 8, 3, false};
 }
 int fft4_flags() { return g_fft4_flags; }
 
@@ -519,7 +537,9 @@ void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const fl
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 8 == 0, "fft4 rowpass: grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
   const bool tiley = (f & kFft4Blocked) && (f & kFft4TileY) && !(f & kTimingFlags);
-  if (ch == 4 && tiley)
+  if (tiley && tiled_x(g, f))
+    launch_rowpass<8, 1, kModeBlocked | kModeTileY | kModeTileX>(Y, X, K, g, tables, grid, f, s);
+  else if (ch == 4 && tiley)
     launch_rowpass<4, 1, kModeBlocked | kModeTileY>(Y, X, K, g, tables, grid, f, s);
   else if (tiley)
     launch_rowpass<8, 1, kModeBlocked | kModeTileY>(Y, X, K, g, tables, grid, f, s);

@@ -143,6 +143,105 @@ __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
   }
 }
 
+// Tiled spectrum layout written by fft4 pass B (kFft4TileX):
+// bin k = k2 + n2*k1 at X_t[k2/8][k1/8][k2%8][k1%8]; a (k2-octet, k1-octet)
+// pair is one contiguous 512-byte chunk.
+__device__ __forceinline__ uint64_t taddr(uint64_t k, int log2_n2, uint64_t n1) {
+  const uint64_t k2 = k & ((uint64_t(1) << log2_n2) - 1), k1 = k >> log2_n2;
+  return (k2 >> 3) * (8 * n1) + (k1 >> 3) * 64 + (k2 & 7) * 8 + (k1 & 7);
+}
+
+// One workgroup per tile of 8 rows k1 in [g0, g0+8) (g0 < n1/2) x 256
+// columns k2 in [c0, c0+256): thread t owns column c0+t of all 8 rows, so its
+// 8 bins are 64 contiguous bytes of X_t (4 x 16-byte loads) and so are their
+// mirrors M-k = (n2-k2) + n2*(n1-1-k1) (reversed).  Rows k1 < n1/2 produce
+// every bin below M/2 and, as mirrors, every bin above it; bin M/2 is done by
+// block (0,0).  P rows are written coalesced in natural order.
+__global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* __restrict__ Z, int log2_n2,
+                                                                 uint64_t n1, uint64_t zstride,
+                                                                 float* __restrict__ P, uint64_t pstride,
+                                                                 uint64_t nbins_out, const float* __restrict__ stats,
+                                                                 float nscale) {
+  __shared__ float2 A[8][258];  // A[r][u] = X[(g0+r)*n2 + c0 - 1 + u]
+  __shared__ float2 D[8][258];  // D[r][u] = X[M - ((g0+r)*n2 + c0 - 1 + u)]
+  const uint64_t n2 = uint64_t(1) << log2_n2;
+  const uint64_t M = n1 * n2, half = M / 2;
+  const int kk = blockIdx.z;
+  const int t = threadIdx.x;
+  const float2* z = Z + static_cast<uint64_t>(kk) * zstride;
+  float* p = P + static_cast<uint64_t>(kk) * pstride;
+  const float mean = stats[0] * nscale;
+  const float sigma = stats[2] * nscale;
+  const uint64_t g0 = static_cast<uint64_t>(blockIdx.y) * 8;
+  const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * 256;
+  auto xbin = [&](uint64_t k, float2& xa, float2& xm) {  // generic: X[k] and X[M-k]
+    const float2 za = z[taddr(k & (M - 1), log2_n2, n1)];
+    const float2 zb = z[taddr((M - k) & (M - 1), log2_n2, n1)];
+    float sn, cs;
+    sincospif(-static_cast<float>(k) / static_cast<float>(M), &sn, &cs);
+    xa = r2c_combine(za, zb, cs, sn);
+    xm = r2c_combine(zb, za, -cs, sn);
+  };
+  const uint64_t k2 = c0 + t;
+  if (k2 == 0) {
+    // column 0 pairs row k1 with row n1 - k1 (not n1 - 1 - k1)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) xbin((g0 + r) * n2, A[r][t + 1], D[r][t + 1]);
+  } else {
+    const float4* sa = reinterpret_cast<const float4*>(z + (k2 >> 3) * (8 * n1) + (g0 >> 3) * 64 + (k2 & 7) * 8);
+    const uint64_t m2 = n2 - k2, m1 = n1 - 8 - g0;  // mirror column, first mirror row (rows reversed)
+    const float4* sb = reinterpret_cast<const float4*>(z + (m2 >> 3) * (8 * n1) + (m1 >> 3) * 64 + (m2 & 7) * 8);
+    float2 za[8], zb[8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 a = sa[u], b = sb[u];
+      za[2 * u] = make_float2(a.x, a.y);
+      za[2 * u + 1] = make_float2(a.z, a.w);
+      zb[7 - 2 * u] = make_float2(b.x, b.y);
+      zb[6 - 2 * u] = make_float2(b.z, b.w);
+    }
+    float sn, cs;
+    sincospif(-static_cast<float>(g0 * n2 + k2) / static_cast<float>(M), &sn, &cs);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      float ws, wc;  // W^(r n2): exact angle r / n1
+      sincospif(-static_cast<float>(r) / static_cast<float>(n1), &ws, &wc);
+      const float c = cs * wc - sn * ws, sv = cs * ws + sn * wc;
+      A[r][t + 1] = r2c_combine(za[r], zb[r], c, sv);
+      D[r][t + 1] = r2c_combine(zb[r], za[r], -c, sv);
+    }
+  }
+  if (t < 8) {  // halos: column c0-1 (ascending neighbour) and c0+256 (mirror neighbour) of row t
+    const uint64_t row = (g0 + t) * n2 + c0;
+    float2 xa, xm;
+    if (row > 0) {
+      xbin(row - 1, xa, xm);
+      A[t][0] = xa;
+    } else {
+      A[t][0] = make_float2(0.f, 0.f);
+    }
+    xbin(row + 256, xa, xm);
+    D[t][257] = xm;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    const uint64_t k = (g0 + r) * n2 + k2;
+    if (k < nbins_out) {
+      const float2 xl = k > 0 ? A[r][t] : make_float2(0.f, 0.f);
+      p[k] = (dev::interbin(A[r][t + 1], xl) - mean) / sigma;
+    }
+    const uint64_t j = M - k;  // > M/2 for every k in the ascending rows
+    if (j < nbins_out) p[j] = (dev::interbin(D[r][t + 1], D[r][t + 2]) - mean) / sigma;
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && half < nbins_out) {  // bin M/2 (row n1/2, column 0)
+    float2 xa, xm, la, lm;
+    xbin(half, xa, xm);
+    xbin(half - 1, la, lm);
+    p[half] = (dev::interbin(xa, la) - mean) / sigma;
+  }
+}
+
 __device__ __forceinline__ void emit(bool pred, uint32_t seg, int idx, float snr, PeakRecord* __restrict__ out,
                                      uint32_t* __restrict__ count, uint32_t capacity) {
   const unsigned long long mask = __ballot(pred);
@@ -326,6 +425,21 @@ void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride,
   r2c_interbin_normalise_batch_kernel<<<grid, 256, 0, s>>>(Z, M, zstride, log2_row, row_pitch, blk_pitch, log2_blk, P,
                                                            pstride, nbins_out, stats, nscale);
   post_launch_check("r2c_interbin_normalise_batch_kernel", s);
+}
+
+void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstride, float* P, uint64_t pstride,
+                                  int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s) {
+  PSOUP_CHECK(K >= 1 && K <= 65535, "bad batch");
+  PSOUP_CHECK(n1 >= 16 && n2 >= 256 && (n1 & (n1 - 1)) == 0 && (n2 & (n2 - 1)) == 0, "r2c tiled: bad geometry");
+  PSOUP_CHECK(nbins_out <= static_cast<uint64_t>(n1) * n2 + 1, "nbins_out beyond the spectrum");
+  PSOUP_CHECK((reinterpret_cast<uintptr_t>(X) & 15) == 0 && xstride % 2 == 0, "r2c tiled: alignment");
+  if (nbins_out == 0) return;
+  int lg = 0;
+  while ((1 << lg) < n2) ++lg;
+  dim3 grid(static_cast<unsigned>(n2 / 256), static_cast<unsigned>(n1 / 2 / 8), static_cast<unsigned>(K));
+  r2c_interbin_tiled_kernel<<<grid, 256, 0, s>>>(X, lg, static_cast<uint64_t>(n1), xstride, P, pstride, nbins_out,
+                                                 stats, nscale);
+  post_launch_check("r2c_interbin_tiled_kernel", s);
 }
 
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,

@@ -432,7 +432,13 @@ PYBIND11_MODULE(_C, m) {
   });
   k.def("fft4_x_layout", [](const kern::Fft4Geom& g) {
     kern::Fft4XLayout l = kern::fft4_x_layout(g);
-    return py::make_tuple(l.log2_row, l.row_pitch, l.blk_pitch, l.log2_blk);
+    return py::make_tuple(l.log2_row, l.row_pitch, l.blk_pitch, l.log2_blk, l.tiled);
+  });
+  k.def("r2c_interbin_normalise_tiled", [](uintptr_t X, int n1, int n2, uint64_t xstride, uintptr_t Pout,
+                                           uint64_t pstride, int K, uint64_t nbo, uintptr_t stats, float nscale,
+                                           uintptr_t s) {
+    kern::r2c_interbin_normalise_tiled(P<const float2>(X), n1, n2, xstride, P<float>(Pout), pstride, K, nbo,
+                                       P<const float>(stats), nscale, S(s));
   });
   py::class_<kern::Fft4Geom>(k, "Fft4Geom")
       .def_readonly("ok", &kern::Fft4Geom::ok)

@@ -317,8 +317,11 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
   }
   const uint64_t pst = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
   const kern::Fft4XLayout xl =
-      mode_ == 2 ? kern::fft4_x_layout(f4_) : kern::Fft4XLayout{ilog2(n_ / 2), n_ / 2, 8, 3};
-  if (mode_ >= 1)
+      mode_ == 2 ? kern::fft4_x_layout(f4_) : kern::Fft4XLayout{ilog2(n_ / 2), n_ / 2, 8, 3, false};
+  if (mode_ == 2 && xl.tiled)
+    kern::r2c_interbin_normalise_tiled(spec_.data(), f4_.n1, f4_.n2, xs_, P_.data(), pst, count,
+                                       static_cast<uint64_t>(hi_), wh_->stats(), static_cast<float>(n_), stream_);
+  else if (mode_ >= 1)
     kern::r2c_interbin_normalise_batch(spec_.data(), n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch,
                                        xl.log2_blk, P_.data(), pst, count, static_cast<uint64_t>(hi_),
                                        wh_->stats(), static_cast<float>(n_), stream_);

@@ -235,8 +235,8 @@ def _fft4_padded(x: torch.Tensor, accels: Sequence[float], tsamp: float):
 
 
 def fft4_x_layout(g):
-    """(log2_row, row_pitch, blk_pitch, log2_blk) of the fused FFT's spectrum
-    layout under the current kernel flags (blocked or padded natural order)."""
+    """(log2_row, row_pitch, blk_pitch, log2_blk, tiled) of the fused FFT's
+    spectrum layout under the current kernel flags."""
     return K.fft4_x_layout(g)
 
 
@@ -246,10 +246,14 @@ def fft4_resample_spectrum(x: torch.Tensor, accels: Sequence[float], tsamp: floa
     g, X = _fft4_padded(x, accels, tsamp)
     Kb = X.shape[0]
     M = g.n1 * g.n2
-    log2_row, row, blk, lw = fft4_x_layout(g)
+    log2_row, row, blk, lw, tiled = fft4_x_layout(g)
     k = torch.arange(M, device=x.device, dtype=torch.int64)
     k2 = k & (g.n2 - 1)
-    addr = (k2 >> lw) * blk + (k >> log2_row) * row + (k2 & ((1 << lw) - 1))
+    k1 = k >> log2_row
+    if tiled:
+        addr = (k2 >> 3) * (8 * g.n1) + (k1 >> 3) * 64 + (k2 & 7) * 8 + (k1 & 7)
+    else:
+        addr = (k2 >> lw) * blk + k1 * row + (k2 & ((1 << lw) - 1))
     Xc = torch.view_as_complex(X)  # [K, xstride]
     return Xc[:, addr].contiguous()
 
@@ -262,10 +266,14 @@ def fft4_resample_interbin(x: torch.Tensor, accels: Sequence[float], tsamp: floa
     g, X = _fft4_padded(x, accels, tsamp)
     Kb = X.shape[0]
     M = g.n1 * g.n2
-    log2_row, row, blk, lw = fft4_x_layout(g)
+    log2_row, row, blk, lw, tiled = fft4_x_layout(g)
     P = torch.empty((Kb, M + 1), dtype=torch.float32, device=x.device)
-    K.r2c_interbin_normalise_batch(X.data_ptr(), M, g.xstride, log2_row, row, blk, lw, P.data_ptr(), M + 1, Kb, M + 1,
-                                   stats.data_ptr(), float(nscale), _s())
+    if tiled:
+        K.r2c_interbin_normalise_tiled(X.data_ptr(), g.n1, g.n2, g.xstride, P.data_ptr(), M + 1, Kb, M + 1,
+                                       stats.data_ptr(), float(nscale), _s())
+    else:
+        K.r2c_interbin_normalise_batch(X.data_ptr(), M, g.xstride, log2_row, row, blk, lw, P.data_ptr(), M + 1, Kb,
+                                       M + 1, stats.data_ptr(), float(nscale), _s())
     return P
 
 

@@ -84,6 +84,9 @@ def main():
                                                             P.data_ptr(), M + 1, K, M + 1, st.data_ptr(), float(n), s),
                     a.reps)
         report(f"r2c_interbin_normalise block={blk_w}", tz, K * (8 * M + 4 * M))
+    tz = timeit(lambda: K_.r2c_interbin_normalise_tiled(X.data_ptr(), g.n1, g.n2, g.xstride, P.data_ptr(), M + 1, K,
+                                                        M + 1, st.data_ptr(), float(n), s), a.reps)
+    report("r2c_interbin_normalise tiled", tz, K * (8 * M + 4 * M))
     K_.fft4_set_flags(0)
     # harmonic peaks on normal noise (threshold 9 -> few peaks)
     P.normal_()
