@@ -270,27 +270,31 @@ template <int NLEV>
 struct HarmTile {
   static constexpr int BPT = NLEV <= 3 ? 8 : (NLEV == 4 ? 4 : 2);
   static constexpr int B = 256 * BPT;
-  static constexpr int NREG = 1 << NLEV;  // fundamental + sum_{h=1..NLEV} 2^(h-1) ranges
+  static constexpr int NREG = 1 << NLEV;  // (fundamental) + sum_{h=1..NLEV} 2^(h-1) gather ranges
   static constexpr int maxlen(int h, int m) { return h == 0 ? B : (((B - 1) * m) >> h) + 2; }
+  static constexpr int chunks(int h, int m) { return (maxlen(h, m) + 3) / 4; }  // 16-byte chunks
   static constexpr int region(int h, int m) { return h == 0 ? 0 : (1 << (h - 1)) + (m - 1) / 2; }
+  // LDS offset (floats, multiple of 4) of gather range r >= 1; the fundamental stays in registers
   static constexpr int offset(int r) {
     int off = 0;
-    for (int h = 0; h <= NLEV; ++h)
-      for (int m = 1; m < (h == 0 ? 2 : (1 << h)); m += 2) {
+    for (int h = 1; h <= NLEV; ++h)
+      for (int m = 1; m < (1 << h); m += 2) {
         if (region(h, m) == r) return off;
-        off += maxlen(h, m);
+        off += 4 * chunks(h, m);
       }
     return off;
   }
-  static constexpr int TOTAL = offset(NREG);
-  static constexpr int iters() {
+  static constexpr int TOTAL = offset(NREG) > 0 ? offset(NREG) : 4;
+  static constexpr int iters() {  // 16-byte staging loads per thread
     int n = 0;
-    for (int h = 0; h <= NLEV; ++h)
-      for (int m = 1; m < (h == 0 ? 2 : (1 << h)); m += 2) n += (maxlen(h, m) + 255) / 256;
+    for (int h = 1; h <= NLEV; ++h)
+      for (int m = 1; m < (1 << h); m += 2) n += (chunks(h, m) + 255) / 256;
     return n;
   }
-  static constexpr int ITERS = iters();
+  static constexpr int ITERS = iters() > 0 ? iters() : 1;
 };
+
+typedef float f4u_h __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned 16-byte load
 
 template <int NLEV>
 __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __restrict__ P, uint64_t pstride,
@@ -299,38 +303,51 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
                                                              uint32_t* __restrict__ count) {
   using Tl = HarmTile<NLEV>;
   constexpr int B = Tl::B;
-  __shared__ float lds[Tl::TOTAL];
+  __shared__ __attribute__((aligned(16))) float lds[Tl::TOTAL];
   const int k = blockIdx.y;
   const float* p = P + static_cast<uint64_t>(k) * pstride;
   const int t = threadIdx.x;
   const int b0 = lo + static_cast<int>(blockIdx.x) * B;
   const int last = hi - 1;
-  // ---- stage the fundamental and every gather range: all loads are issued
-  // before the first LDS store (fixed trip counts), so they overlap.
-  float tmp[Tl::ITERS];
+  // ---- fundamental straight into registers (coalesced)
+  float fund[Tl::BPT];
+#pragma unroll
+  for (int u = 0; u < Tl::BPT; ++u) fund[u] = p[min(b0 + t + 256 * u, last)];
+  // ---- stage every gather range in 16-byte chunks: all loads are issued
+  // before the first LDS store (fixed trip counts).  Only values at indices
+  // < hi are ever used; chunks reaching past `last` are gathered per element.
+  f4u_h tmp[Tl::ITERS];
   {
     int it = 0;
 #pragma unroll
-    for (int h = 0; h <= NLEV; ++h) {
+    for (int h = 1; h <= NLEV; ++h) {
 #pragma unroll
-      for (int m = 1; m < (h == 0 ? 2 : (1 << h)); m += 2) {
-        const int half = h == 0 ? 0 : (1 << (h - 1));
+      for (int m = 1; m < (1 << h); m += 2) {
+        const int half = 1 << (h - 1);
         const int r0 = (b0 * m + half) >> h;
 #pragma unroll
-        for (int e = 0; e < (Tl::maxlen(h, m) + 255) / 256; ++e) tmp[it++] = p[min(r0 + t + 256 * e, last)];
+        for (int e = 0; e < (Tl::chunks(h, m) + 255) / 256; ++e, ++it) {
+          const int a = r0 + 4 * (t + 256 * e);
+          if (a + 3 <= last) {
+            tmp[it] = *reinterpret_cast<const f4u_h*>(p + a);
+          } else {
+            tmp[it] = f4u_h{p[min(a, last)], p[min(a + 1, last)], p[min(a + 2, last)], p[min(a + 3, last)]};
+          }
+        }
       }
     }
   }
   {
     int it = 0;
 #pragma unroll
-    for (int h = 0; h <= NLEV; ++h) {
+    for (int h = 1; h <= NLEV; ++h) {
 #pragma unroll
-      for (int m = 1; m < (h == 0 ? 2 : (1 << h)); m += 2) {
-        float* dst = lds + Tl::offset(Tl::region(h, m));
+      for (int m = 1; m < (1 << h); m += 2) {
+        float4* dst = reinterpret_cast<float4*>(lds + Tl::offset(Tl::region(h, m)));
 #pragma unroll
-        for (int e = 0; e < (Tl::maxlen(h, m) + 255) / 256; ++e, ++it)
-          if (t + 256 * e < Tl::maxlen(h, m)) dst[t + 256 * e] = tmp[it];
+        for (int e = 0; e < (Tl::chunks(h, m) + 255) / 256; ++e, ++it)
+          if (t + 256 * e < Tl::chunks(h, m))
+            dst[t + 256 * e] = make_float4(tmp[it].x, tmp[it].y, tmp[it].z, tmp[it].w);
       }
     }
   }
@@ -341,39 +358,45 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
   for (int u = 0; u < Tl::BPT; ++u) {
     const int i = b0 + t + u * 256;
     const bool valid = i < hi;
-    float val = lds[t + u * 256];
-    emit(valid && i >= hp.start[0] && i < hp.end[0] && val > thr, seg0, i, val, out, count, hp.capacity);
+    float val = fund[u];  // fundamental P[i]
+    float o[NLEV + 1];
+    o[0] = val;
 #define PS_TERM(h, m) lds[Tl::offset(Tl::region(h, m)) + (((i * (m) + (1 << ((h) - 1))) >> (h)) - ((b0 * (m) + (1 << ((h) - 1))) >> (h)))]
     if constexpr (NLEV >= 1) {
       val += PS_TERM(1, 1);
-      const float o = static_cast<float>(static_cast<double>(val) * c_level_scale[1]);
-      emit(valid && i >= hp.start[1] && i < hp.end[1] && o > thr, seg0 + 1, i, o, out, count, hp.capacity);
+      o[1] = static_cast<float>(static_cast<double>(val) * c_level_scale[1]);
     }
     if constexpr (NLEV >= 2) {
       val += PS_TERM(2, 3);  // reference order: 3/4 before 1/4
       val += PS_TERM(2, 1);
-      const float o = static_cast<float>(static_cast<double>(val) * c_level_scale[2]);
-      emit(valid && i >= hp.start[2] && i < hp.end[2] && o > thr, seg0 + 2, i, o, out, count, hp.capacity);
+      o[2] = static_cast<float>(static_cast<double>(val) * c_level_scale[2]);
     }
     if constexpr (NLEV >= 3) {
 #pragma unroll
       for (int m = 1; m < 8; m += 2) val += PS_TERM(3, m);
-      const float o = static_cast<float>(static_cast<double>(val) * c_level_scale[3]);
-      emit(valid && i >= hp.start[3] && i < hp.end[3] && o > thr, seg0 + 3, i, o, out, count, hp.capacity);
+      o[3] = static_cast<float>(static_cast<double>(val) * c_level_scale[3]);
     }
     if constexpr (NLEV >= 4) {
 #pragma unroll
       for (int m = 1; m < 16; m += 2) val += PS_TERM(4, m);
-      const float o = static_cast<float>(static_cast<double>(val) * c_level_scale[4]);
-      emit(valid && i >= hp.start[4] && i < hp.end[4] && o > thr, seg0 + 4, i, o, out, count, hp.capacity);
+      o[4] = static_cast<float>(static_cast<double>(val) * c_level_scale[4]);
     }
     if constexpr (NLEV >= 5) {
 #pragma unroll
       for (int m = 1; m < 32; m += 2) val += PS_TERM(5, m);
-      const float o = static_cast<float>(static_cast<double>(val) * c_level_scale[5]);
-      emit(valid && i >= hp.start[5] && i < hp.end[5] && o > thr, seg0 + 5, i, o, out, count, hp.capacity);
+      o[5] = static_cast<float>(static_cast<double>(val) * c_level_scale[5]);
     }
 #undef PS_TERM
+    bool pred[NLEV + 1];
+    bool any = false;
+#pragma unroll
+    for (int h = 0; h <= NLEV; ++h) {
+      pred[h] = valid && i >= hp.start[h] && i < hp.end[h] && o[h] > thr;
+      any = any || pred[h];
+    }
+    if (__ballot(any) == 0ull) continue;  // one ballot per bin group in the (usual) no-peak case
+#pragma unroll
+    for (int h = 0; h <= NLEV; ++h) emit(pred[h], seg0 + h, i, o[h], out, count, hp.capacity);
   }
 }
 
