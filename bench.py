@@ -3,12 +3,14 @@
 an 8-harmonic sum (-n 3), one process per MI355X (torchrun for N > 1).
 
 One step (per rank, weak scaling -- fixed work per GPU):
-  * dedisperse this rank's DM shard (``--dms-per-gpu`` trials) from the
+  * dedisperse this rank's DM shard (``--dms-per-gpu`` trials, default 8, one
+    chunk -- the production pipeline dedisperses 16-DM chunks) from the
     resident 1024-channel 2-bit filterbank with the MFMA dedispersion kernel,
   * whiten each trial and search +-500 m/s^2 (legacy acceleration-plan
     convention: ~684 trials per DM at 2^23 x 64 us) with an 8-harmonic sum:
-    batched resampling -> batched rocFFT R2C -> fused interbin/normalise ->
-    fused harmonic-sum + peak compaction -> host clustering + distillation,
+    fused resample + two-pass four-step FFT -> paired real-FFT post-processing
+    + interbin/normalise -> LDS-staged harmonic sum + peak compaction -> host
+    clustering + distillation (overlapped with the next batch),
   * gather every rank's candidates to all ranks over RCCL and run the global
     DM/harmonic distillation + scoring.
 The synthetic filterbank (uniform 2-bit noise, random seed) is generated on
@@ -41,7 +43,8 @@ def parse():
     p.add_argument("--nchans", type=int, default=1024)
     p.add_argument("--nbits", type=int, default=2)
     p.add_argument("--tsamp", type=float, default=64e-6)
-    p.add_argument("--dms-per-gpu", type=int, default=2)
+    p.add_argument("--dms-per-gpu", type=int, default=8,
+                   help="DM trials per GPU per step (dedispersed as one chunk, as the pipeline does)")
     p.add_argument("--acc", type=float, default=500.0, help="search +-acc m/s^2")
     p.add_argument("--nharmonics", type=int, default=3)
     p.add_argument("--accel-batch", type=int, default=0)
