@@ -111,4 +111,22 @@ std::vector<int> read_killfile(const std::string& filename, int nchans, bool* ok
 // (the reference would read out of bounds on such lines).
 void read_zapfile(const std::string& filename, std::vector<float>& freqs, std::vector<float>& widths);
 
+// PSRDADA ASCII header (the first 4096 bytes of a .dada file), with the
+// field set and parse semantics of DadaHeader::fromfile (header.hpp:52-161):
+// first occurrence of "KEY " anywhere in the header, BW read as an integer,
+// nsamples = payload bytes / nchan / nant / npol / 2.
+constexpr size_t kDadaHeaderSize = 4096;
+struct DadaHeader {
+  float header_version = 0.f;
+  unsigned header_size = 0;
+  double bw = 0, freq = 0;
+  unsigned nant = 0, nchan = 0, ndim = 0, npol = 0, nbit = 0;
+  double tsamp = 0, osamp_ratio = 0;
+  std::string source_name, ra, dec, proc_file, mode, observer, pid, telescope, instrument, utc_start;
+  size_t obs_offset = 0, dsb = 0, filesize = 0, dada_filesize = 0, nsamples = 0, bytes_per_sec = 0;
+  unsigned ant_id = 0, file_no = 0;
+};
+DadaHeader parse_dada_header(const std::string& text, size_t payload_bytes);
+DadaHeader read_dada_header(const std::string& filename);
+
 }  // namespace psoup

@@ -148,6 +148,40 @@ PYBIND11_MODULE(_C, m) {
     read_zapfile(f, a, b);
     return py::make_tuple(a, b);
   });
+  m.def("read_dada_header", [](const std::string& f) {
+    DadaHeader h = read_dada_header(f);
+    py::dict d;
+    d["header_version"] = h.header_version;
+    d["header_size"] = h.header_size;
+    d["bw"] = h.bw;
+    d["freq"] = h.freq;
+    d["nant"] = h.nant;
+    d["nchan"] = h.nchan;
+    d["ndim"] = h.ndim;
+    d["npol"] = h.npol;
+    d["nbit"] = h.nbit;
+    d["tsamp"] = h.tsamp;
+    d["osamp_ratio"] = h.osamp_ratio;
+    d["source_name"] = h.source_name;
+    d["ra"] = h.ra;
+    d["dec"] = h.dec;
+    d["proc_file"] = h.proc_file;
+    d["mode"] = h.mode;
+    d["observer"] = h.observer;
+    d["pid"] = h.pid;
+    d["obs_offset"] = h.obs_offset;
+    d["telescope"] = h.telescope;
+    d["instrument"] = h.instrument;
+    d["dsb"] = h.dsb;
+    d["filesize"] = h.filesize;
+    d["dada_filesize"] = h.dada_filesize;
+    d["nsamples"] = h.nsamples;
+    d["bytes_per_sec"] = h.bytes_per_sec;
+    d["utc_start"] = h.utc_start;
+    d["ant_id"] = h.ant_id;
+    d["file_no"] = h.file_no;
+    return d;
+  });
   m.def("write_filterbank", [](const std::string& f, const py::dict& hdr, py::array_t<uint8_t, py::array::c_style> data) {
     SigprocHeader h = dict_to_header(hdr);
     std::vector<uint8_t> v(data.data(), data.data() + data.size());

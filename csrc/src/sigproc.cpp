@@ -305,4 +305,66 @@ void read_zapfile(const std::string& filename, std::vector<float>& freqs, std::v
   }
 }
 
+// ------------------------------------------------------------------ DADA ---
+namespace {
+std::string dada_value(const std::string& text, const std::string& key) {
+  const size_t pos = text.find(key + " ");
+  if (pos == std::string::npos) return "";
+  std::istringstream is(text.substr(pos + key.size() + 1));
+  std::string v;
+  is >> v;
+  return v;
+}
+}  // namespace
+
+DadaHeader parse_dada_header(const std::string& text, size_t payload_bytes) {
+  DadaHeader h;
+  auto s = [&](const char* k) { return dada_value(text, k); };
+  auto i = [&](const char* k) { return std::atoi(s(k).c_str()); };
+  auto f = [&](const char* k) { return std::atof(s(k).c_str()); };
+  h.filesize = payload_bytes;
+  h.header_version = static_cast<float>(f("HDR_VERSION"));
+  h.header_size = static_cast<unsigned>(i("HDR_SIZE"));
+  h.bw = i("BW");  // integer parse, as the reference
+  h.freq = f("FREQ");
+  h.nant = static_cast<unsigned>(i("NANT"));
+  h.nchan = static_cast<unsigned>(i("NCHAN"));
+  h.ndim = static_cast<unsigned>(i("NDIM"));
+  h.npol = static_cast<unsigned>(i("NPOL"));
+  h.nbit = static_cast<unsigned>(i("NBIT"));
+  h.tsamp = f("TSAMP");
+  h.osamp_ratio = f("OSAMP_RATIO");
+  h.source_name = s("SOURCE");
+  h.ra = s("RA");
+  h.dec = s("DEC");
+  h.proc_file = s("PROC_FILE");
+  h.mode = s("MODE");
+  h.observer = s("OBSERVER");
+  h.pid = s("PID");
+  h.obs_offset = static_cast<size_t>(i("OBS_OFFSET"));
+  h.telescope = s("TELESCOPE");
+  h.instrument = s("INSTRUMENT");
+  h.dsb = static_cast<size_t>(i("DSB"));
+  h.dada_filesize = static_cast<size_t>(i("FILE_SIZE"));
+  const double denom = static_cast<double>(h.nchan) * h.nant * h.npol * 2.0;
+  h.nsamples = denom > 0 ? static_cast<size_t>(static_cast<double>(payload_bytes) / denom) : 0;
+  h.bytes_per_sec = static_cast<size_t>(i("BYTES_PER_SECOND"));
+  h.utc_start = s("UTC_START");
+  h.ant_id = static_cast<unsigned>(i("ANT_ID"));
+  h.file_no = static_cast<unsigned>(i("FILE_NUMBER"));
+  return h;
+}
+
+DadaHeader read_dada_header(const std::string& filename) {
+  std::ifstream in(filename, std::ios::binary);
+  if (!in) PSOUP_THROW("cannot open DADA file " << filename);
+  std::string buf(kDadaHeaderSize, '\0');
+  in.read(&buf[0], static_cast<std::streamsize>(kDadaHeaderSize));
+  const size_t got = static_cast<size_t>(in.gcount());
+  buf.resize(got);
+  in.seekg(0, std::ios::end);
+  const size_t total = static_cast<size_t>(in.tellg());
+  return parse_dada_header(buf, total > kDadaHeaderSize ? total - kDadaHeaderSize : 0);
+}
+
 }  // namespace psoup

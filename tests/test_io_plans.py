@@ -100,3 +100,28 @@ def test_prev_power_of_two_strictly_less(C):
     assert C.prev_power_of_two(187520) == 131072
     assert C.prev_power_of_two(1 << 23) == 1 << 22  # exact power -> half (utils.hpp:12-18)
     assert C.prev_power_of_two((1 << 23) + 1) == 1 << 23
+
+
+def test_dada_header_and_channel_extraction(C, tmp_path):
+    """PSRDADA header parse (DadaHeader semantics: BW as integer, nsamples
+    from the payload size) and channel extraction for the correlator."""
+    import numpy as np
+
+    from peasoup_amd.utils import dada
+
+    nant, nchan, npol, n = 3, 4, 2, 500
+    rng = np.random.default_rng(1)
+    payload = rng.integers(-20, 20, size=(n, nant, nchan, npol, 2), dtype=np.int8)
+    hdr = {"HDR_VERSION": 1.0, "HDR_SIZE": 4096, "BW": 16.75, "FREQ": 1400.5, "NANT": nant, "NCHAN": nchan,
+           "NDIM": 2, "NPOL": npol, "NBIT": 8, "TSAMP": 0.064, "SOURCE": "J0000+0000", "UTC_START": "2026-10-16-00:00:00",
+           "ANT_ID": 7, "FILE_NUMBER": 2}
+    path = str(tmp_path / "x.dada")
+    dada.write(path, hdr, payload)
+    h = C.read_dada_header(path)
+    assert h["nant"] == nant and h["nchan"] == nchan and h["npol"] == npol and h["nbit"] == 8
+    assert h["bw"] == 16.0 and h["freq"] == 1400.5 and h["tsamp"] == 0.064
+    assert h["source_name"] == "J0000+0000" and h["ant_id"] == 7 and h["file_no"] == 2
+    assert h["filesize"] == payload.nbytes and h["nsamples"] == n
+    arr = dada.extract_channel(path, channel=2, size=100, offset=10, pol=1)
+    assert arr.shape == (nant, 200)
+    assert np.array_equal(arr[1].reshape(100, 2), payload[10:110, 1, 2, 1, :])

@@ -176,3 +176,29 @@ def test_python_entry_fault_then_resume(tmp_path):
                        cwd=REPO)
     assert r.returncode == 0, r.stderr
     assert (tmp_path / "b" / "candidates.peasoup").read_bytes() == (tmp_path / "c" / "candidates.peasoup").read_bytes()
+
+
+def test_accmap_tool_finds_injected_delay(tmp_path):
+    """tools/peasoup_accmap.py on a synthetic DADA file with a known lag."""
+    import json
+    import subprocess
+    import sys
+
+    import numpy as np
+
+    from conftest import REPO
+    from peasoup_amd.utils import dada
+
+    rng = np.random.default_rng(3)
+    n, nant, nchan, lag = 1 << 14, 2, 2, 37
+    base = rng.integers(-40, 40, size=(n + lag, 2), dtype=np.int8)
+    payload = np.zeros((n, nant, nchan, 1, 2), dtype=np.int8)
+    payload[:, 0, 1, 0, :] = base[lag:lag + n]
+    payload[:, 1, 1, 0, :] = base[:n]
+    path = str(tmp_path / "v.dada")
+    dada.write(path, {"HDR_SIZE": 4096, "NANT": nant, "NCHAN": nchan, "NPOL": 1, "NDIM": 2, "NBIT": 8}, payload)
+    r = subprocess.run([sys.executable, os.path.join(REPO, "tools", "peasoup_accmap.py"), path, "--channel", "1",
+                        "--size", str(n), "--max-delay", "128"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert abs(d["delays"]["0-1"]) == lag
