@@ -169,6 +169,8 @@ enum Fft4Flags : int {
   kFft4Ch4 = 16,         // with kFft4Blocked: pass B runs 4 transforms per workgroup (4 waves/SIMD)
   kFft4TileY = 1024,     // with kFft4Blocked: 8x8-tiled Y between the passes (16-byte pass-B loads)
   kFft4TileX = 2048,     // with kFft4TileY: 8x8-tiled spectrum X (coalesced pass-B stores; tiled r2c)
+  kFft4PairXcd = 4096,   // pass A: adjacent column blocks of a trial on one XCD (shared input lines)
+  kFft4GroupXcd = 8192,  // pass A: 8 trials x 2 adjacent column blocks per XCD group (needs K % 8 == 0)
 };
 void fft4_set_flags(int flags);
 int fft4_flags();

@@ -290,8 +290,24 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
   const int N1 = g.n1;
   const uint32_t nbt = static_cast<uint32_t>(N1 / C::CH);  // blocks per trial
   const bool tslow = flags & kFft4TrialSlow;
-  const int k = static_cast<int>(tslow ? lb / nbt : lb % static_cast<uint32_t>(K));
-  const int c0 = static_cast<int>(tslow ? lb % nbt : lb / static_cast<uint32_t>(K)) * C::CH + grp * CPT;
+  int k = static_cast<int>(tslow ? lb / nbt : lb % static_cast<uint32_t>(K));
+  int c0 = static_cast<int>(tslow ? lb % nbt : lb / static_cast<uint32_t>(K)) * C::CH + grp * CPT;
+  if ((flags & kFft4GroupXcd) && (K & 7) == 0) {
+    // 8 consecutive trials x column blocks 2p, 2p+1 (16 workgroups reading
+    // nearly the same input lines) share one XCD, in consecutive slots
+    const uint32_t b = blockIdx.x;
+    const uint32_t G = ((b >> 7) << 3) | (b & 7u), w = (b >> 3) & 15u;
+    const uint32_t kg = static_cast<uint32_t>(K) >> 3;
+    k = static_cast<int>(8 * (G % kg) + (w & 7u));
+    c0 = static_cast<int>(2 * (G / kg) + (w >> 3)) * C::CH + grp * CPT;
+  } else if (flags & kFft4PairXcd) {
+    // column blocks 2p and 2p+1 of a trial (the two 64-byte halves of every
+    // input line) run on the same XCD, 8 dispatch slots apart
+    const uint32_t b = blockIdx.x;
+    const uint32_t s = (b >> 3) & 1u, u = ((b >> 4) << 3) | (b & 7u);
+    k = static_cast<int>(u % static_cast<uint32_t>(K));
+    c0 = static_cast<int>(2 * (u / static_cast<uint32_t>(K)) + s) * C::CH + grp * CPT;
+  }
   const int log2row = __builtin_ctz(static_cast<unsigned>(2 * N1));
   const TableOffsets to = table_offsets(N1, L);
   const double af = afs[k];
@@ -455,7 +471,8 @@ void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& 
 }
 
 namespace {
-int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4TileY | kFft4TileX;  // fastest measured (tools/kbench.py)
+int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4TileY | kFft4TileX | kFft4PairXcd |
+                   kFft4GroupXcd;  // fastest measured (tools/kbench.py)
 
 template <int CPT, int SUB, int MODE>
 void launch_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
@@ -511,7 +528,8 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   PSOUP_CHECK((reinterpret_cast<uintptr_t>(Y) & 63) == 0, "fft4 colpass: Y alignment");
   const int f = g_fft4_flags;
   const uint64_t nblocks = static_cast<uint64_t>(g.n1 / 8) * K;
-  PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 8 == 0, "fft4 colpass: grid");
+  PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 16 == 0, "fft4 colpass: grid");
+  PSOUP_CHECK(!(f & kFft4GroupXcd) || (K & 7) != 0 || nblocks % 128 == 0, "fft4 colpass: group grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
   if ((f & kFft4Blocked) && (f & kFft4TileY) && !(f & kTimingFlags))
     launch_colpass<8, 1, kModeBlocked | kModeTileY>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);

@@ -215,7 +215,7 @@ def test_r2c_interbin_normalise_batch():
         assert np.allclose(P[k], exp, rtol=1e-4, atol=2e-3), np.abs(P[k] - exp).max()
 
 
-FFT4_FLAG_SETS = [None, 0, 1, 259, 274, 1299, 1283, 3331]  # None = library default; 3331 = tiled Y and X
+FFT4_FLAG_SETS = [None, 0, 1, 259, 274, 1299, 3331, 7427]  # None = default (15619); 3331 = tiled Y and X
 
 
 @pytest.fixture(params=FFT4_FLAG_SETS)
