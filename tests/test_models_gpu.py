@@ -91,9 +91,10 @@ def _free_port():
     return p
 
 
-def test_two_rank_search_equals_single_rank(tmp_path):
+@pytest.mark.parametrize("world", [2, 4])
+def test_multi_rank_search_equals_single_rank(tmp_path, world):
     """DM sharding + RCCL-style gather + distributed folding reproduce the
-    single-process result (gloo transport, both ranks on one GPU)."""
+    single-process result (gloo transport, all ranks on one GPU)."""
     port = _free_port()
     script = (
         "import os,sys; sys.path.insert(0, %r)\n"
@@ -106,9 +107,9 @@ def test_two_rank_search_equals_single_rank(tmp_path):
         "pdist.shutdown()\n" % (REPO, TUTORIAL))
     f = tmp_path / "run.py"
     f.write_text(script)
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world))
     procs = []
-    for r in range(2):
+    for r in range(world):
         e = dict(env, RANK=str(r), LOCAL_RANK="0")
         procs.append(subprocess.Popen([sys.executable, str(f), str(tmp_path / "dist")], env=e, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))

@@ -55,23 +55,25 @@ def _worker(rank, world, port, q):
         q.put((rank, {"error": traceback.format_exc()}))
 
 
-def test_gloo_collectives_world2():
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_gloo_collectives(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     out = dict(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
-    for r in range(2):
+    for r in range(world):
         assert "error" not in out[r], out[r].get("error")
-    assert out[0]["gather"] == [(0, 1), (1, 2)]
-    assert out[0]["bcast"] == out[1]["bcast"] == sum(i % 256 for i in range(1000))
-    assert out[1]["obj"] == b"hello-header"
-    assert out[0]["allreduce"] == out[1]["allreduce"] == 3
-    assert out[0]["max"] == out[1]["max"] == 1.0
+    assert out[0]["gather"] == [(r, r + 1) for r in range(world)]
+    for r in range(world):
+        assert out[r]["bcast"] == sum(i % 256 for i in range(1000))
+        assert out[r]["obj"] == b"hello-header"
+        assert out[r]["allreduce"] == world * (world + 1) // 2
+        assert out[r]["max"] == float(world - 1)
 
 
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
@@ -121,9 +123,9 @@ def _timeshard_worker(rank, world, port, q):
         q.put((rank, {"error": traceback.format_exc()}))
 
 
-def test_time_sharded_dedispersion_gloo_world3():
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_time_sharded_dedispersion_gloo(world):
     """Halo exchange + all-to-all corner turn == whole-observation dedispersion."""
-    world = 3
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
