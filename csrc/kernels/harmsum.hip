@@ -354,6 +354,9 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
   __syncthreads();
   const float thr = hp.thresh;
   const uint32_t seg0 = static_cast<uint32_t>(k) * 8u;
+  bool inner = true;  // block-uniform: the whole tile lies inside every level's search range
+#pragma unroll
+  for (int h = 0; h <= NLEV; ++h) inner = inner && b0 >= hp.start[h] && b0 + B <= hp.end[h];
 #pragma unroll
   for (int u = 0; u < Tl::BPT; ++u) {
     const int i = b0 + t + u * 256;
@@ -369,7 +372,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
     if constexpr (NLEV >= 2) {
       val += PS_TERM(2, 3);  // reference order: 3/4 before 1/4
       val += PS_TERM(2, 1);
-      o[2] = static_cast<float>(static_cast<double>(val) * c_level_scale[2]);
+      o[2] = val * 0.5f;  // == (float)((double)val * 0.5): exact scaling
     }
     if constexpr (NLEV >= 3) {
 #pragma unroll
@@ -379,7 +382,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
     if constexpr (NLEV >= 4) {
 #pragma unroll
       for (int m = 1; m < 16; m += 2) val += PS_TERM(4, m);
-      o[4] = static_cast<float>(static_cast<double>(val) * c_level_scale[4]);
+      o[4] = val * 0.25f;  // exact
     }
     if constexpr (NLEV >= 5) {
 #pragma unroll
@@ -391,7 +394,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
     bool any = false;
 #pragma unroll
     for (int h = 0; h <= NLEV; ++h) {
-      pred[h] = valid && i >= hp.start[h] && i < hp.end[h] && o[h] > thr;
+      pred[h] = valid && (inner || (i >= hp.start[h] && i < hp.end[h])) && o[h] > thr;
       any = any || pred[h];
     }
     if (__ballot(any) == 0ull) continue;  // one ballot per bin group in the (usual) no-peak case
