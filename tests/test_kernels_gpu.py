@@ -229,18 +229,18 @@ def fft4_flags(request):
     C.kernels.fft4_set_flags(old)
 
 
-@pytest.mark.parametrize("log2n", [15, 17, 20, 23])
+@pytest.mark.parametrize("log2n", [15, 17, 20, 23, 25])
 def test_fft4_resample_spectrum_matches_numpy(log2n, fft4_flags):
     """Fused resample + four-step FFT vs (bit-exact GPU resample) + numpy fp64 FFT."""
     from peasoup_amd import ops
 
-    if log2n == 23 and fft4_flags not in (None, 0):
-        pytest.skip("2^23 checked with the default kernel shape only")
+    if log2n >= 23 and fft4_flags is not None:
+        pytest.skip("2^23 and 2^25 checked with the default kernel shape only")
 
     rng = np.random.default_rng(log2n)
     n = 1 << log2n
     x = torch.from_numpy(rng.standard_normal(n).astype(np.float32)).to(dev)
-    accs = [-480.0, 0.0, 37.5, 500.0] if log2n < 23 else [-500.0, 250.0]
+    accs = [-480.0, 0.0, 37.5, 500.0] if log2n < 23 else ([-500.0, 250.0] if log2n == 23 else [310.0])
     Z = ops.fft4_resample_spectrum(x, accs, 64e-6).cpu().numpy()
     R = ops.resample(x, accs, 64e-6).cpu().numpy().astype(np.float64)
     for k in range(len(accs)):
