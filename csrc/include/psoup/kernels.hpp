@@ -187,6 +187,8 @@ struct HarmParams {
 // the caller re-runs with a bigger buffer).
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
                           PeakRecord* out, uint32_t* count, hipStream_t s);
+// Tuning: bit 0 = XCD-per-trial block order (default on).
+void harmonic_set_flags(int flags);
 // Debug/test: materialise level-h sums [nlevels][nbins] for one spectrum.
 void harmonic_sums(const float* P, uint64_t nbins, int nlevels, float* out, hipStream_t s);
 

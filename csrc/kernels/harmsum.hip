@@ -296,18 +296,32 @@ struct HarmTile {
 
 typedef float f4u_h __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned 16-byte load
 
+// Block order: with xcd_trials (K % 8 == 0) XCD x (blockIdx % 8 under
+// round-robin dispatch) runs trials x, x+8, ... and each trial's tiles in
+// increasing order, so the recently streamed part of that trial's spectrum
+// -- where the high-numerator gather ranges lie -- is in the XCD's own L2.
 template <int NLEV>
 __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __restrict__ P, uint64_t pstride,
                                                              int lo, int hi, HarmParams hp,
                                                              PeakRecord* __restrict__ out,
-                                                             uint32_t* __restrict__ count) {
+                                                             uint32_t* __restrict__ count, int ntiles,
+                                                             int xcd_trials) {
   using Tl = HarmTile<NLEV>;
   constexpr int B = Tl::B;
   __shared__ __attribute__((aligned(16))) float lds[Tl::TOTAL];
-  const int k = blockIdx.y;
+  const uint32_t bid = blockIdx.x;
+  int k, tile;
+  if (xcd_trials) {
+    const uint32_t slot = bid >> 3;
+    k = static_cast<int>((slot / ntiles) * 8 + (bid & 7u));
+    tile = static_cast<int>(slot % ntiles);
+  } else {
+    k = static_cast<int>(bid / ntiles);
+    tile = static_cast<int>(bid % ntiles);
+  }
   const float* p = P + static_cast<uint64_t>(k) * pstride;
   const int t = threadIdx.x;
-  const int b0 = lo + static_cast<int>(blockIdx.x) * B;
+  const int b0 = lo + tile * B;
   const int last = hi - 1;
   // ---- fundamental straight into registers (coalesced)
   float fund[Tl::BPT];
@@ -468,6 +482,11 @@ void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstr
   post_launch_check("r2c_interbin_tiled_kernel", s);
 }
 
+namespace {
+int g_harm_flags = 1;  // bit 0: XCD-per-trial block order
+}  // namespace
+void harmonic_set_flags(int flags) { g_harm_flags = flags; }
+
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
                           PeakRecord* out, uint32_t* count, hipStream_t s) {
   PSOUP_CHECK(hp.nlevels >= 0 && hp.nlevels <= kMaxHarmLevels, "nlevels out of range");
@@ -482,15 +501,21 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
   PSOUP_CHECK(hi <= static_cast<int>(nbins), "search range beyond spectrum");
   if (hi <= lo) return;
   PSOUP_CHECK(static_cast<int64_t>(hi) * 32 < (int64_t(1) << 31), "spectrum too long for the int32 gather math");
-  auto grid_of = [&](int B) {
-    return dim3(static_cast<unsigned>((hi - lo + B - 1) / B), static_cast<unsigned>(K));
-  };
+  const int xcd = (g_harm_flags & 1) && (K % 8 == 0);
+  auto ntiles_of = [&](int B) { return (hi - lo + B - 1) / B; };
   switch (hp.nlevels) {
-#define PS_CASE(NL) \
-  case NL: harmonic_peaks_kernel<NL><<<grid_of(HarmTile<NL>::B), 256, 0, s>>>(P, pstride, lo, hi, hp, out, count); break;
+#define PS_CASE(NL)                                                                                           \
+  case NL: {                                                                                                  \
+    const int nt = ntiles_of(HarmTile<NL>::B);                                                                \
+    PSOUP_CHECK(static_cast<int64_t>(nt) * K < (int64_t(1) << 31), "harmonic grid too large");               \
+    harmonic_peaks_kernel<NL><<<dim3(static_cast<unsigned>(nt * K)), 256, 0, s>>>(P, pstride, lo, hi, hp, out,  \
+                                                                                  count, nt, xcd);             \
+    break;                                                                                                    \
+  }
     PS_CASE(0) PS_CASE(1) PS_CASE(2) PS_CASE(3) PS_CASE(4)
+    default:
+      PS_CASE(5)
 #undef PS_CASE
-    default: harmonic_peaks_kernel<5><<<grid_of(HarmTile<5>::B), 256, 0, s>>>(P, pstride, lo, hi, hp, out, count); break;
   }
   post_launch_check("harmonic_peaks_kernel", s);
 }

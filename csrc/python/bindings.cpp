@@ -522,6 +522,7 @@ PYBIND11_MODULE(_C, m) {
   k.def("harmonic_sums", [](uintptr_t Pin, uint64_t nb, int nlevels, uintptr_t out, uintptr_t s) {
     kern::harmonic_sums(P<const float>(Pin), nb, nlevels, P<float>(out), S(s));
   });
+  k.def("harmonic_set_flags", &kern::harmonic_set_flags);
   k.def("fold_shift_table", [](uintptr_t table, int nbins, int nints, uintptr_t s) {
     kern::fold_shift_table(P<float2>(table), nbins, nints, S(s));
   });

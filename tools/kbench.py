@@ -101,8 +101,11 @@ def main():
         cnt.zero_()
         K_.harmonic_peaks_batch(P.data_ptr(), nb, nb, K, 3, starts, ends, 9.0, cap, out.data_ptr(), cnt.data_ptr(), s)
 
-    th = timeit(harm, a.reps)
-    report("harmonic_peaks (3 levels)", th, K * 4 * M)
+    for hf in (0, 1):
+        K_.harmonic_set_flags(hf)
+        th = timeit(harm, a.reps)
+        report(f"harmonic_peaks (3 levels) xcd={hf}", th, K * 4 * M)
+    K_.harmonic_set_flags(1)
 
 
 if __name__ == "__main__":
