@@ -48,6 +48,8 @@ def parse():
     p.add_argument("--acc", type=float, default=500.0, help="search +-acc m/s^2")
     p.add_argument("--nharmonics", type=int, default=3)
     p.add_argument("--accel-batch", type=int, default=0)
+    p.add_argument("--sub-batch", type=int, default=-1,
+                   help="trials per sub-batch on two alternating streams (0 = off, -1 = auto: half a batch)")
     p.add_argument("--fft-mode", type=int, default=2,
                    help="2: fused resample + four-step FFT; 1: rocFFT C2C(N/2) + fused r2c post; 0: rocFFT R2C")
     p.add_argument("--dedisp-kernel", default="mfma", choices=["mfma", "direct"])
@@ -88,6 +90,7 @@ def main() -> int:
     args.nharmonics = a.nharmonics
     args.size = n
     args.accel_batch = a.accel_batch
+    args.sub_batch = a.sub_batch
     args.fft_mode = a.fft_mode
     args.dedisp_kernel = a.dedisp_kernel
     delays = _C.generate_delay_table(a.nchans, a.tsamp, fch1, foff)
@@ -160,6 +163,7 @@ def main() -> int:
                 "dms_per_gpu": a.dms_per_gpu,
                 "accel_trials_per_dm": trials_per_step_local // a.dms_per_gpu,
                 "accel_batch": rs.engine.batch_size,
+                "sub_batch": rs.engine.sub_batch,
                 "fft_mode": rs.engine.fft_mode,
                 "candidates_after_distill": ncands,
             },

@@ -98,7 +98,8 @@ struct SearchParams {
   float boundary_25_freq = 0.5f;
   std::vector<float> zap_freqs, zap_widths;
   int accel_batch = 0;          // 0 = auto
-  size_t batch_bytes = 3ull << 30;  // auto-batch HBM budget
+  int sub_batch = -1;           // fused-FFT trials per sub-batch on alternating streams (0 = off, -1 = auto)
+  size_t batch_bytes = 6ull << 30;  // auto-batch HBM budget (64 trials of 2^23)
   int min_gap = 30;
   // Acceleration-trial FFT path: 0 = rocFFT R2C of N points; 1 = rocFFT C2C
   // of N/2 points with the real-FFT post-processing fused into the interbin
@@ -156,6 +157,7 @@ class SearchEngine {
   const SearchCounters& counters() const { return ctr_; }
   void reset_counters() { ctr_ = SearchCounters(); }
   int batch_size() const { return K_; }
+  int sub_batch() const { return sub_; }
   int fft_mode() const { return mode_; }
   float tobs() const { return tobs_; }
   // Debug access to the whitened series of the last trial.
@@ -180,6 +182,9 @@ class SearchEngine {
   SearchParams p_;
   hipStream_t stream_;
   Stream copy_stream_;
+  Stream aux_stream_;              // second compute stream of the sub-batch pipeline
+  Event fork_, join_;
+  int sub_ = 0;                    // effective sub-batch size (0 = whole batch on stream_)
   uint64_t n_, nb_;
   float bin_width_, tobs_;
   int nlev_;

@@ -181,6 +181,7 @@ struct HarmParams {
   int end[6];
   float thresh;
   uint32_t capacity;       // PeakRecord capacity of `out`
+  uint32_t trial_base = 0; // added to the batch item of every record (sub-batch launches)
 };
 // Fused incoherent harmonic sum + threshold + compaction: never writes the
 // summed spectra.  Records land unordered; count may exceed capacity (then

@@ -367,7 +367,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
   }
   __syncthreads();
   const float thr = hp.thresh;
-  const uint32_t seg0 = static_cast<uint32_t>(k) * 8u;
+  const uint32_t seg0 = (static_cast<uint32_t>(k) + hp.trial_base) * 8u;
   bool inner = true;  // block-uniform: the whole tile lies inside every level's search range
 #pragma unroll
   for (int h = 0; h <= NLEV; ++h) inner = inner && b0 >= hp.start[h] && b0 + B <= hp.end[h];

@@ -340,6 +340,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("accel_convention", &CmdLineOptions::accel_convention)
       .def_readwrite("dedisp_kernel", &CmdLineOptions::dedisp_kernel)
       .def_readwrite("accel_batch", &CmdLineOptions::accel_batch)
+      .def_readwrite("sub_batch", &CmdLineOptions::sub_batch)
       .def_readwrite("fft_mode", &CmdLineOptions::fft_mode)
       .def_readwrite("use_boundaries", &CmdLineOptions::use_boundaries)
       .def_readwrite("checkpoint_dir", &CmdLineOptions::checkpoint_dir)
@@ -605,6 +606,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("zap_freqs", &SearchParams::zap_freqs)
       .def_readwrite("zap_widths", &SearchParams::zap_widths)
       .def_readwrite("accel_batch", &SearchParams::accel_batch)
+      .def_readwrite("sub_batch", &SearchParams::sub_batch)
       .def_readwrite("batch_bytes", &SearchParams::batch_bytes)
       .def_readwrite("min_gap", &SearchParams::min_gap)
       .def_readwrite("fft_mode", &SearchParams::fft_mode);
@@ -615,6 +617,7 @@ PYBIND11_MODULE(_C, m) {
         return e.search_trial(P<const uint8_t>(trial), nsamps, dm, dm_idx, accs);
       }, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("batch_size", &SearchEngine::batch_size)
+      .def_property_readonly("sub_batch", &SearchEngine::sub_batch)
       .def_property_readonly("fft_mode", &SearchEngine::fft_mode)
       .def_property_readonly("tobs", &SearchEngine::tobs)
       .def_property_readonly("whitened_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.whitened()); })

@@ -228,6 +228,8 @@ static std::vector<Spec> peasoup_specs(CmdLineOptions& a) {
             a.accel_convention),
       val_s("", "dedisp_kernel", "Dedispersion kernel: auto | mfma | direct", a.dedisp_kernel),
       val_n("", "accel_batch", "Acceleration trials per batched FFT (0 = auto)", a.accel_batch),
+      val_n("", "sub_batch", "Fused-FFT trials per sub-batch on two alternating streams (0 = off, -1 = auto)",
+            a.sub_batch),
       val_n("", "fft_mode", "Accel-trial FFT: 2 = fused resample + four-step FFT (default), 1 = rocFFT C2C(N/2), 0 = rocFFT R2C",
             a.fft_mode),
       sw("", "use_boundaries", "Honour --boundary_* in the running median (reference ignores them)",

@@ -255,8 +255,13 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     const size_t per = n_ * 4 + nb_ * 8 + static_cast<size_t>(hi_) * 4;
     K_ = static_cast<int>(std::max<size_t>(1, p_.batch_bytes / per));
     K_ = std::min(K_, 256);
-    if (K_ >= 16) K_ = K_ / 8 * 8;
+    if (K_ >= 32) K_ = K_ / 16 * 16;  // halves stay multiples of 8 (XCD-grouped kernels)
+    else if (K_ >= 16) K_ = K_ / 8 * 8;
   }
+  // Auto: two half-batches on alternating streams (+4-5% at 2^23: the
+  // tail of one sub-batch's kernels overlaps the head of the other's).
+  sub_ = mode_ != 2 ? 0 : p_.sub_batch >= 0 ? p_.sub_batch : (K_ >= 16 ? K_ / 2 : 0);
+  if (sub_ >= K_) sub_ = 0;
   cap_ = static_cast<uint32_t>(std::max<uint64_t>(1u << 16, static_cast<uint64_t>(K_) * 4096));
   for (auto& s : slots_) {
     s.done = std::make_unique<Event>();
@@ -305,33 +310,56 @@ FftPlan& SearchEngine::batch_plan(int count) {
 void SearchEngine::launch_batch(Slot& s, int first, int count) {
   s.first = first;
   s.count = count;
-  if (mode_ == 2) {
-    // res_ holds the K four-step intermediates Y (complex, M per trial)
-    float2* Y = reinterpret_cast<float2*>(res_.data());
-    kern::fft4_resample_colpass(tim_.data(), f4_in_.data(), n_, af_.data() + first, count, Y, f4_, f4_tab_.data(),
-                                stream_);
-    kern::fft4_rowpass(Y, spec_.data(), count, f4_, f4_tab_.data(), stream_);
-  } else {
-    kern::resample_batch(tim_.data(), n_, res_.data(), n_, af_.data() + first, count, stream_);
-    batch_plan(count).execute(res_.data(), spec_.data(), stream_);
-  }
   const uint64_t pst = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
   const kern::Fft4XLayout xl =
       mode_ == 2 ? kern::fft4_x_layout(f4_) : kern::Fft4XLayout{ilog2(n_ / 2), n_ / 2, 8, 3, false};
-  if (mode_ == 2 && xl.tiled)
-    kern::r2c_interbin_normalise_tiled(spec_.data(), f4_.n1, f4_.n2, xs_, P_.data(), pst, count,
-                                       static_cast<uint64_t>(hi_), wh_->stats(), static_cast<float>(n_), stream_);
-  else if (mode_ >= 1)
-    kern::r2c_interbin_normalise_batch(spec_.data(), n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch,
-                                       xl.log2_blk, P_.data(), pst, count, static_cast<uint64_t>(hi_),
-                                       wh_->stats(), static_cast<float>(n_), stream_);
-  else
-    kern::interbin_normalise_batch(spec_.data(), nb_, nb_, P_.data(), pst, count, static_cast<uint64_t>(hi_),
-                                   wh_->stats(), static_cast<float>(n_), stream_);
   PSOUP_HIP_CHECK(hipMemsetAsync(s.d_count.data(), 0, sizeof(uint32_t), stream_));
-  {
+  // Trials [b, b + c) of the batch: spectrum, power spectrum, harmonic peaks.
+  auto run = [&](int b, int c, hipStream_t st) {
+    float* P = P_.data() + static_cast<uint64_t>(b) * pst;
+    if (mode_ == 2) {
+      // res_ holds the four-step intermediates Y (complex, ystride per trial)
+      float2* Y = reinterpret_cast<float2*>(res_.data()) + static_cast<uint64_t>(b) * f4_.ystride;
+      float2* X = spec_.data() + static_cast<uint64_t>(b) * xs_;
+      kern::fft4_resample_colpass(tim_.data(), f4_in_.data(), n_, af_.data() + first + b, c, Y, f4_,
+                                  f4_tab_.data(), st);
+      kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st);
+      if (xl.tiled)
+        kern::r2c_interbin_normalise_tiled(X, f4_.n1, f4_.n2, xs_, P, pst, c, static_cast<uint64_t>(hi_),
+                                           wh_->stats(), static_cast<float>(n_), st);
+      else
+        kern::r2c_interbin_normalise_batch(X, n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch, xl.log2_blk,
+                                           P, pst, c, static_cast<uint64_t>(hi_), wh_->stats(),
+                                           static_cast<float>(n_), st);
+    } else {
+      kern::resample_batch(tim_.data(), n_, res_.data(), n_, af_.data() + first, c, st);
+      batch_plan(c).execute(res_.data(), spec_.data(), st);
+      if (mode_ == 1)
+        kern::r2c_interbin_normalise_batch(spec_.data(), n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch,
+                                           xl.log2_blk, P, pst, c, static_cast<uint64_t>(hi_), wh_->stats(),
+                                           static_cast<float>(n_), st);
+      else
+        kern::interbin_normalise_batch(spec_.data(), nb_, nb_, P, pst, c, static_cast<uint64_t>(hi_),
+                                       wh_->stats(), static_cast<float>(n_), st);
+    }
     RoctxRange r("Harmonic summing");
-    kern::harmonic_peaks_batch(P_.data(), nb_, pst, count, hp_, s.d_peaks.data(), s.d_count.data(), stream_);
+    kern::HarmParams hp = hp_;
+    hp.trial_base = static_cast<uint32_t>(b);
+    kern::harmonic_peaks_batch(P, nb_, pst, c, hp, s.d_peaks.data(), s.d_count.data(), st);
+  };
+  if (sub_ > 0 && count > sub_) {
+    // Sub-batch pipeline: consecutive sub-batches alternate between two
+    // streams, so one sub-batch's four kernels run while the other's are in
+    // flight and each intermediate (Y, X, P) is re-read soon after it was
+    // written, while it is still resident in the 256 MB Infinity Cache.
+    fork_.record(stream_);
+    PSOUP_HIP_CHECK(hipStreamWaitEvent(aux_stream_.get(), fork_.get(), 0));
+    for (int b = 0, j = 0; b < count; b += sub_, ++j)
+      run(b, std::min(sub_, count - b), (j & 1) ? aux_stream_.get() : stream_);
+    join_.record(aux_stream_.get());
+    PSOUP_HIP_CHECK(hipStreamWaitEvent(stream_, join_.get(), 0));
+  } else {
+    run(0, count, stream_);
   }
   PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_count.data(), s.d_count.data(), sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   s.done->record(stream_);

@@ -50,6 +50,7 @@ SearchSetup make_search_setup(const CmdLineOptions& args, const SigprocHeader& h
   p.boundary_25_freq = args.use_boundaries ? args.boundary_25_freq : 0.5f;
   if (!args.zapfilename.empty()) read_zapfile(args.zapfilename, p.zap_freqs, p.zap_widths);
   p.accel_batch = args.accel_batch;
+  p.sub_batch = args.sub_batch;
   p.fft_mode = args.fft_mode;
   s.dedisp_kernel = parse_dedisp_kernel(args.dedisp_kernel);
   return s;
@@ -277,6 +278,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
       st_map["host_distill_s"] = c.host_s;
       st_map["fft_mode"] = engine.fft_mode();
       st_map["accel_batch"] = engine.batch_size();
+      st_map["sub_batch"] = engine.sub_batch();
     } catch (...) {
       std::lock_guard<std::mutex> lk(sh.mu);
       if (!sh.error) sh.error = std::current_exception();

@@ -254,6 +254,7 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     rank_stats = dict(rs.engine.counters())
     rank_stats.update({"rank": ctx.rank, "search_s": search_wall, "accel_trials_planned": local_trials,
                        "fft_mode": rs.engine.fft_mode, "accel_batch": rs.engine.batch_size,
+                       "sub_batch": rs.engine.sub_batch,
                        "dedispersion_s": timers["dedispersion"].get_time(), "searching_s": timers["searching"].get_time()})
     all_stats = pdist.gather_bytes(json.dumps(rank_stats).encode(), dst=0)
 

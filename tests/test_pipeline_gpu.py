@@ -138,6 +138,22 @@ def test_fft_modes_agree(C, tmp_path):
             assert b["snr"] == pytest.approx(a["snr"], rel=1e-4), (mode, i)
 
 
+def test_sub_batch_pipeline_identical(C, tmp_path):
+    """Sub-batches on two alternating streams (--sub_batch) produce exactly
+    the candidates of whole-batch launches, including an uneven split."""
+    out = {}
+    for sb in (0, 2, 3):
+        d = tmp_path / f"sb{sb}"
+        r = subprocess.run([os.path.join(REPO, "bin", "peasoup"), "-i", TUTORIAL, "-o", str(d), "--accel_batch", "8",
+                            "--sub_batch", str(sb), "--dm_end", "120", "-n", "4", "--npdmp", "0",
+                            "--acc_start", "-50", "--acc_end", "50"], capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr
+        with open(d / "candidates.peasoup", "rb") as f:
+            out[sb] = f.read()
+    assert len(out[0]) > 1000
+    assert out[2] == out[0] and out[3] == out[0]
+
+
 def test_trace_json_cli_and_python(C, tmp_path):
     """--trace_json: per-stage timers, performance and per-device counters
     (SURVEY.md §5.1/§5.5), from the native CLI and the Python driver."""
