@@ -14,7 +14,7 @@ try:
     from . import _C  # noqa: F401
 except ImportError as exc:  # pragma: no cover - exercised only when unbuilt
     raise ImportError(
-        "peasoup_amd native extension is not built; run `python -m peasoup_amd._build` "
+        "peasoup_amd native extension is not built; run `python peasoup_amd/_build.py` "
         f"(hipcc/gfx950) first: {exc}"
     ) from exc
 

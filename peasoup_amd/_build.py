@@ -5,7 +5,7 @@ Builds ``peasoup_amd/_C*.so`` (pybind11 extension) and the ``bin/peasoup``,
 executables from ``csrc/``.  The artefacts stay in the repository tree so they
 travel with the source snapshot to a GPU box.
 
-``python -m peasoup_amd._build --sanitize address`` (or ``undefined`` /
+``python peasoup_amd/_build.py --sanitize address`` (or ``undefined`` /
 ``thread``) builds only the host unit tests under that sanitizer into
 ``build-<sanitizer>/`` -> ``bin/psoup_unit_tests_<sanitizer>``.
 """

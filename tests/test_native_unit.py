@@ -19,7 +19,7 @@ def _run(exe):
 def test_native_unit_tests():
     exe = os.path.join(REPO, "bin", "psoup_unit_tests")
     if not os.path.exists(exe):
-        pytest.skip("native build missing (python -m peasoup_amd._build)")
+        pytest.skip("native build missing (python peasoup_amd/_build.py)")
     _run(exe)
 
 
