@@ -146,8 +146,20 @@ void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& 
 // z_k[m] = x_k[2m] + i x_k[2m+1] and x_k = resampleII(in, af[k]); n = 2M.
 void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
                            const Fft4Geom& g, const float2* tables, hipStream_t s);
-// Pass B: X[k][k1][k2] = sum_i Y[k][k2][i] W_n1^{i k1}.
-void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, hipStream_t s);
+// Pass B: X[k][k1][k2] = sum_i Y[k][k2][i] W_n1^{i k1}.  With the tiled
+// spectrum layout and nbins_out > 0, only the k1 rows that
+// r2c_interbin_normalise_tiled reads for bins < nbins_out are stored (the
+// search needs bins below max_freq only: ~14% of the spectrum at 2^23).
+void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, hipStream_t s,
+                  uint64_t nbins_out = 0);
+// Row-octet blocks (8 rows k1 each) r2c_interbin_normalise_tiled runs for
+// bins < nbins_out; it reads spectrum rows k1 <= 8*ny and k1 >= n1 - 8*ny.
+inline uint32_t r2c_tiled_row_blocks(uint64_t nbins_out, int n1, int n2) {
+  const uint64_t full = static_cast<uint64_t>(n1) / 16;
+  if (nbins_out == 0) return static_cast<uint32_t>(full);
+  const uint64_t ny = (nbins_out - 1) / (8ull * static_cast<uint64_t>(n2)) + 1;
+  return static_cast<uint32_t>(ny < full ? ny : full);
+}
 // Spectrum layout of fft4_rowpass under the current flags, as r2c parameters.
 struct Fft4XLayout {
   int log2_row;
@@ -171,6 +183,7 @@ enum Fft4Flags : int {
   kFft4TileX = 2048,     // with kFft4TileY: 8x8-tiled spectrum X (coalesced pass-B stores; tiled r2c)
   kFft4PairXcd = 4096,   // pass A: adjacent column blocks of a trial on one XCD (shared input lines)
   kFft4GroupXcd = 8192,  // pass A: 8 trials x 2 adjacent column blocks per XCD group (needs K % 8 == 0)
+  kFft4Sub2 = 16384,     // tiled paths: two thread groups x 4 transforms per workgroup (fewer VGPRs, 4 waves/SIMD)
 };
 void fft4_set_flags(int flags);
 int fft4_flags();

@@ -110,7 +110,9 @@ __device__ __forceinline__ float amplitude(float2 x) {
 __device__ __forceinline__ float interbin(float2 x, float2 xl) {
   float ampsq = x.x * x.x + x.y * x.y;
   float dre = x.x - xl.x, dim = x.y - xl.y;
-  float ampsq_diff = static_cast<float>(0.5 * static_cast<double>(dre * dre + dim * dim));
+  // 0.5 * (double) then rounding to float == the float product by 0.5f:
+  // scaling by a power of two is exact (denormals are kept in both)
+  float ampsq_diff = (dre * dre + dim * dim) * 0.5f;
   return sqrtf(fmaxf(ampsq, ampsq_diff));
 }
 

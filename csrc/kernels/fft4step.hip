@@ -276,12 +276,12 @@ constexpr int kModeBlocked = 1, kModeTiming = 2, kModeTileY = 4, kModeTileX = 8;
 
 // Pass A.  Logical block = column block * K + trial (trial fastest).
 template <int L, int CPT, int SUB, int MODE>
-__global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2)) fft4_colpass_kernel(
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::THREADS), amdgpu_waves_per_eu((CPT == 4 ? 4 : 2)))) fft4_colpass_kernel(
     const float* __restrict__ in, const float* __restrict__ in_pad, uint64_t n, const double* __restrict__ afs, int K,
     float2* __restrict__ Y, Fft4Geom g, const float2* __restrict__ tab, int flags) {
   using C = Cfg<L, CPT, SUB>;
   constexpr bool kBlocked = MODE & kModeBlocked, kTiming = MODE & kModeTiming, kTileY = MODE & kModeTileY;
-  static_assert(!kTileY || (CPT == 8 && SUB == 1), "tiled Y needs 8 transforms per thread");
+  static_assert(!kTileY || C::CH == 8, "tiled Y needs 8 transforms per workgroup");
   __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   constexpr int T = C::T;
   const int grp = threadIdx.x / T;
@@ -343,7 +343,8 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
       w = cmul(w, step);
     }
     if constexpr (kTileY) {
-      float2* dst = yk + static_cast<uint64_t>(c0) * g.n2 + (k2 >> 3) * 64 + (k2 & 7);
+      // c0 & 7 != 0 when two thread groups share one 8-column tile (SUB 2)
+      float2* dst = yk + static_cast<uint64_t>(c0 & ~7) * g.n2 + (k2 >> 3) * 64 + (c0 & 7) * 8 + (k2 & 7);
 #pragma unroll
       for (int c = 0; c < CPT; ++c) dst[c * 8] = v[c][q];
     } else {
@@ -357,9 +358,9 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
 
 // Pass B.  Logical block = row block * K + trial.
 template <int L, int CPT, int SUB, int MODE>
-__global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2)) fft4_rowpass_kernel(
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::THREADS), amdgpu_waves_per_eu((CPT == 4 ? 4 : 2)))) fft4_rowpass_kernel(
     const float2* __restrict__ Y, float2* __restrict__ X, int K, Fft4Geom g, const float2* __restrict__ tab,
-    int flags) {
+    int flags, uint32_t keep_oct) {
   using C = Cfg<L, CPT, SUB>;
   constexpr bool kBlocked = MODE & kModeBlocked, kTiming = MODE & kModeTiming, kTileY = MODE & kModeTileY;
   __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
@@ -405,9 +406,15 @@ __global__ void __launch_bounds__((Cfg<L, CPT, SUB>::THREADS), (CPT == 4 ? 4 : 2
   float2* xk = X + static_cast<uint64_t>(k) * g.xstride;
   const bool nt = flags & kFft4NtStores;
   if constexpr ((MODE & kModeTileX) != 0) {
+    // keep_oct > 0: only k1 octets [0, keep_oct) and [L/8 - keep_oct, L/8)
+    // are ever read (bins below the search limit and their mirrors); a wave's
+    // 64 lanes cover 8 whole octets, so the predicate is wave-uniform.
+    const uint32_t hi_oct = L / 8 - keep_oct;
 #pragma unroll
     for (int q = 0; q < kPts; ++q) {
       const uint64_t k1 = t + q * T;
+      const uint32_t oct = static_cast<uint32_t>(k1 >> 3);
+      if (keep_oct != 0 && oct >= keep_oct && oct < hi_oct) continue;
       float2* dst = xk + static_cast<uint64_t>(r0 >> 3) * (8 * L) + (k1 >> 3) * 64 + (r0 & 7) * 8 + (k1 & 7);
 #pragma unroll
       for (int c = 0; c < CPT; ++c) dst[c * 8] = v[c][q];
@@ -491,11 +498,12 @@ void launch_colpass(const float* in, const float* in_pad, uint64_t n, const doub
 
 template <int CPT, int SUB, int MODE>
 void launch_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, dim3 grid, int flags,
-                    hipStream_t s) {
+                    hipStream_t s, uint32_t keep_oct = 0) {
   switch (g.n1) {
 #define PS_CASE(LL)                                                                                             \
   case LL:                                                                                                      \
-    fft4_rowpass_kernel<LL, CPT, SUB, MODE><<<grid, Cfg<LL, CPT, SUB>::THREADS, 0, s>>>(Y, X, K, g, tables, flags); \
+    fft4_rowpass_kernel<LL, CPT, SUB, MODE><<<grid, Cfg<LL, CPT, SUB>::THREADS, 0, s>>>(Y, X, K, g, tables, flags, \
+                                                                                        keep_oct);             \
     break;
     PS_CASE(128) PS_CASE(256) PS_CASE(512) PS_CASE(1024) PS_CASE(2048) PS_CASE(4096)
 #undef PS_CASE
@@ -531,7 +539,9 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 16 == 0, "fft4 colpass: grid");
   PSOUP_CHECK(!(f & kFft4GroupXcd) || (K & 7) != 0 || nblocks % 128 == 0, "fft4 colpass: group grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
-  if ((f & kFft4Blocked) && (f & kFft4TileY) && !(f & kTimingFlags))
+  if ((f & kFft4Blocked) && (f & kFft4TileY) && (f & kFft4Sub2) && !(f & kTimingFlags))
+    launch_colpass<4, 2, kModeBlocked | kModeTileY>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  else if ((f & kFft4Blocked) && (f & kFft4TileY) && !(f & kTimingFlags))
     launch_colpass<8, 1, kModeBlocked | kModeTileY>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   else if ((f & kFft4Blocked) && (f & kFft4Ch4) && !(f & kTimingFlags))  // Y stays 8-wide; only pass B narrows
     launch_colpass<8, 1, kModeBlocked>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
@@ -546,7 +556,8 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   post_launch_check("fft4_colpass_kernel", s);
 }
 
-void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, hipStream_t s) {
+void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, hipStream_t s,
+                  uint64_t nbins_out) {
   PSOUP_CHECK(g.ok && K >= 1, "fft4 rowpass: bad geometry");
   PSOUP_CHECK((reinterpret_cast<uintptr_t>(X) & 63) == 0, "fft4 rowpass: X alignment");
   const int f = g_fft4_flags;
@@ -555,8 +566,18 @@ void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const fl
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 8 == 0, "fft4 rowpass: grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
   const bool tiley = (f & kFft4Blocked) && (f & kFft4TileY) && !(f & kTimingFlags);
-  if (tiley && tiled_x(g, f))
-    launch_rowpass<8, 1, kModeBlocked | kModeTileY | kModeTileX>(Y, X, K, g, tables, grid, f, s);
+  if (tiley && tiled_x(g, f)) {
+    // rows r2c_interbin_normalise_tiled reads: octets [0, ny] and [n1/8 - ny, n1/8)
+    uint32_t keep = 0;
+    if (nbins_out > 0) {
+      const uint32_t ny = r2c_tiled_row_blocks(nbins_out, g.n1, g.n2);
+      if (2 * (ny + 1) < static_cast<uint32_t>(g.n1 / 8)) keep = ny + 1;
+    }
+    if (f & kFft4Sub2)
+      launch_rowpass<4, 2, kModeBlocked | kModeTileY | kModeTileX>(Y, X, K, g, tables, grid, f, s, keep);
+    else
+      launch_rowpass<8, 1, kModeBlocked | kModeTileY | kModeTileX>(Y, X, K, g, tables, grid, f, s, keep);
+  }
   else if (ch == 4 && tiley)
     launch_rowpass<4, 1, kModeBlocked | kModeTileY>(Y, X, K, g, tables, grid, f, s);
   else if (tiley)

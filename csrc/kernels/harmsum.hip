@@ -16,6 +16,8 @@
 #include "device_common.hpp"
 #include "psoup/kernels.hpp"
 
+#include <cmath>
+
 namespace psoup {
 namespace kern {
 
@@ -157,11 +159,16 @@ __device__ __forceinline__ uint64_t taddr(uint64_t k, int log2_n2, uint64_t n1) 
 // mirrors M-k = (n2-k2) + n2*(n1-1-k1) (reversed).  Rows k1 < n1/2 produce
 // every bin below M/2 and, as mirrors, every bin above it; bin M/2 is done by
 // block (0,0).  P rows are written coalesced in natural order.
+// Row twiddles W^(r n2) = e^{-i pi r / n1}, r = 0..7 (kernel argument: SGPRs)
+struct RowTw8 {
+  float c[8], s[8];
+};
+
 __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* __restrict__ Z, int log2_n2,
                                                                  uint64_t n1, uint64_t zstride,
                                                                  float* __restrict__ P, uint64_t pstride,
                                                                  uint64_t nbins_out, const float* __restrict__ stats,
-                                                                 float nscale) {
+                                                                 float nscale, RowTw8 rtw) {
   __shared__ float2 A[8][258];  // A[r][u] = X[(g0+r)*n2 + c0 - 1 + u]
   __shared__ float2 D[8][258];  // D[r][u] = X[M - ((g0+r)*n2 + c0 - 1 + u)]
   const uint64_t n2 = uint64_t(1) << log2_n2;
@@ -204,8 +211,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* _
     sincospif(-static_cast<float>(g0 * n2 + k2) / static_cast<float>(M), &sn, &cs);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      float ws, wc;  // W^(r n2): exact angle r / n1
-      sincospif(-static_cast<float>(r) / static_cast<float>(n1), &ws, &wc);
+      const float ws = rtw.s[r], wc = rtw.c[r];  // W^(r n2)
       const float c = cs * wc - sn * ws, sv = cs * ws + sn * wc;
       A[r][t + 1] = r2c_combine(za[r], zb[r], c, sv);
       D[r][t + 1] = r2c_combine(zb[r], za[r], -c, sv);
@@ -370,15 +376,46 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
   const uint32_t seg0 = (static_cast<uint32_t>(k) + hp.trial_base) * 8u;
   bool inner = true;  // block-uniform: the whole tile lies inside every level's search range
 #pragma unroll
-  for (int h = 0; h <= NLEV; ++h) inner = inner && b0 >= hp.start[h] && b0 + B <= hp.end[h];
+  for (int h = 0; h <= NLEV; ++h) inner = inner & (b0 >= hp.start[h]) & (b0 + B <= hp.end[h]);
+  // Gather offsets are affine in u: for i = i0 + 256u,
+  // (i*m + 2^(h-1)) >> h = ((i0*m + 2^(h-1)) >> h) + u*(m << (8-h)) exactly
+  // (256m is a multiple of 2^h), so each term's LDS address is formed once per
+  // thread and the per-bin reads use immediate offsets.
+  const int i0 = b0 + t;
+  int lo_h[NLEV + 1], hi_h[NLEV + 1];
+#pragma unroll
+  for (int h = 0; h <= NLEV; ++h) {
+    lo_h[h] = hp.start[h];
+    hi_h[h] = hp.end[h];
+  }
+#define PS_BASE(h, m) (Tl::offset(Tl::region(h, m)) + (((i0 * (m) + (1 << ((h) - 1))) >> (h)) - ((b0 * (m) + (1 << ((h) - 1))) >> (h))))
+  int base[Tl::NREG];
+  if constexpr (NLEV >= 1) base[1] = PS_BASE(1, 1);
+  if constexpr (NLEV >= 2) {
+    base[2] = PS_BASE(2, 1);
+    base[3] = PS_BASE(2, 3);
+  }
+  if constexpr (NLEV >= 3) {
+#pragma unroll
+    for (int m = 1; m < 8; m += 2) base[4 + m / 2] = PS_BASE(3, m);
+  }
+  if constexpr (NLEV >= 4) {
+#pragma unroll
+    for (int m = 1; m < 16; m += 2) base[8 + m / 2] = PS_BASE(4, m);
+  }
+  if constexpr (NLEV >= 5) {
+#pragma unroll
+    for (int m = 1; m < 32; m += 2) base[16 + m / 2] = PS_BASE(5, m);
+  }
+#undef PS_BASE
 #pragma unroll
   for (int u = 0; u < Tl::BPT; ++u) {
-    const int i = b0 + t + u * 256;
+    const int i = i0 + u * 256;
     const bool valid = i < hi;
     float val = fund[u];  // fundamental P[i]
     float o[NLEV + 1];
     o[0] = val;
-#define PS_TERM(h, m) lds[Tl::offset(Tl::region(h, m)) + (((i * (m) + (1 << ((h) - 1))) >> (h)) - ((b0 * (m) + (1 << ((h) - 1))) >> (h)))]
+#define PS_TERM(h, m) lds[base[(1 << ((h) - 1)) + (m) / 2] + u * ((m) << (8 - (h)))]
     if constexpr (NLEV >= 1) {
       val += PS_TERM(1, 1);
       o[1] = static_cast<float>(static_cast<double>(val) * c_level_scale[1]);
@@ -404,12 +441,15 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
       o[5] = static_cast<float>(static_cast<double>(val) * c_level_scale[5]);
     }
 #undef PS_TERM
+    // branch-free predicates (bitwise, no short-circuit: the compiler would
+    // otherwise emit an exec-mask branch per level and bin)
     bool pred[NLEV + 1];
     bool any = false;
 #pragma unroll
     for (int h = 0; h <= NLEV; ++h) {
-      pred[h] = valid && (inner || (i >= hp.start[h] && i < hp.end[h])) && o[h] > thr;
-      any = any || pred[h];
+      const bool in_range = inner | ((i >= lo_h[h]) & (i < hi_h[h]));
+      pred[h] = valid & in_range & (o[h] > thr);
+      any = any | pred[h];
     }
     if (__ballot(any) == 0ull) continue;  // one ballot per bin group in the (usual) no-peak case
 #pragma unroll
@@ -476,9 +516,16 @@ void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstr
   if (nbins_out == 0) return;
   int lg = 0;
   while ((1 << lg) < n2) ++lg;
-  dim3 grid(static_cast<unsigned>(n2 / 256), static_cast<unsigned>(n1 / 2 / 8), static_cast<unsigned>(K));
+  // row blocks beyond the last one holding a bin < nbins_out write nothing
+  dim3 grid(static_cast<unsigned>(n2 / 256), r2c_tiled_row_blocks(nbins_out, n1, n2), static_cast<unsigned>(K));
+  RowTw8 rtw;
+  for (int r = 0; r < 8; ++r) {
+    const double a = -M_PI * r / static_cast<double>(n1);
+    rtw.c[r] = static_cast<float>(std::cos(a));
+    rtw.s[r] = static_cast<float>(std::sin(a));
+  }
   r2c_interbin_tiled_kernel<<<grid, 256, 0, s>>>(X, lg, static_cast<uint64_t>(n1), xstride, P, pstride, nbins_out,
-                                                 stats, nscale);
+                                                 stats, nscale, rtw);
   post_launch_check("r2c_interbin_tiled_kernel", s);
 }
 

@@ -503,9 +503,13 @@ PYBIND11_MODULE(_C, m) {
     kern::fft4_resample_colpass(P<const float>(in), P<const float>(in_pad), n, P<const double>(af), K, P<float2>(Y),
                                 g, P<const float2>(tab), S(s));
   });
-  k.def("fft4_rowpass", [](uintptr_t Y, uintptr_t X, int K, const kern::Fft4Geom& g, uintptr_t tab, uintptr_t s) {
-    kern::fft4_rowpass(P<const float2>(Y), P<float2>(X), K, g, P<const float2>(tab), S(s));
-  });
+  k.def(
+      "fft4_rowpass",
+      [](uintptr_t Y, uintptr_t X, int K, const kern::Fft4Geom& g, uintptr_t tab, uintptr_t s, uint64_t nbins_out) {
+        kern::fft4_rowpass(P<const float2>(Y), P<float2>(X), K, g, P<const float2>(tab), S(s), nbins_out);
+      },
+      py::arg("Y"), py::arg("X"), py::arg("K"), py::arg("g"), py::arg("tab"), py::arg("s"), py::arg("nbins_out") = 0);
+  k.def("r2c_tiled_row_blocks", &kern::r2c_tiled_row_blocks);
   k.def("harmonic_peaks_batch", [](uintptr_t Pin, uint64_t nb, uint64_t pstride, int K, int nlevels,
                                    const std::vector<int>& start, const std::vector<int>& end, float thresh,
                                    uint32_t capacity, uintptr_t out, uintptr_t count, uintptr_t s) {

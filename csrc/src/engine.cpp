@@ -323,7 +323,7 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
       float2* X = spec_.data() + static_cast<uint64_t>(b) * xs_;
       kern::fft4_resample_colpass(tim_.data(), f4_in_.data(), n_, af_.data() + first + b, c, Y, f4_,
                                   f4_tab_.data(), st);
-      kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st);
+      kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st, static_cast<uint64_t>(hi_));
       if (xl.tiled)
         kern::r2c_interbin_normalise_tiled(X, f4_.n1, f4_.n2, xs_, P, pst, c, static_cast<uint64_t>(hi_),
                                            wh_->stats(), static_cast<float>(n_), st);

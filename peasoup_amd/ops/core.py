@@ -216,7 +216,7 @@ def _accel_factors(accels: Sequence[float], tsamp: float, device) -> torch.Tenso
                          / (2 * 299792458.0) for a in accels], dtype=torch.float64, device=device)
 
 
-def _fft4_padded(x: torch.Tensor, accels: Sequence[float], tsamp: float):
+def _fft4_padded(x: torch.Tensor, accels: Sequence[float], tsamp: float, nbins_out: int = 0):
     _check(x, torch.float32, "x")
     n = x.numel()
     g = K.fft4_geometry(n // 2)
@@ -230,7 +230,7 @@ def _fft4_padded(x: torch.Tensor, accels: Sequence[float], tsamp: float):
     X = torch.empty((Kb, g.xstride, 2), dtype=torch.float32, device=x.device)
     K.fft4_pad_input(x.data_ptr(), n, xp.data_ptr(), g, _s())
     K.fft4_resample_colpass(x.data_ptr(), xp.data_ptr(), n, af.data_ptr(), Kb, Y.data_ptr(), g, tab.data_ptr(), _s())
-    K.fft4_rowpass(Y.data_ptr(), X.data_ptr(), Kb, g, tab.data_ptr(), _s())
+    K.fft4_rowpass(Y.data_ptr(), X.data_ptr(), Kb, g, tab.data_ptr(), _s(), nbins_out)
     return g, X
 
 
@@ -259,21 +259,24 @@ def fft4_resample_spectrum(x: torch.Tensor, accels: Sequence[float], tsamp: floa
 
 
 def fft4_resample_interbin(x: torch.Tensor, accels: Sequence[float], tsamp: float, stats: torch.Tensor,
-                           nscale: float) -> torch.Tensor:
+                           nscale: float, nbins_out: int | None = None) -> torch.Tensor:
     """The search hot path of fft_mode 2: fused resample + four-step FFT, then
     the paired real-FFT post-processing + interbin + normalise on the fused
-    FFT's spectrum layout.  Returns P [K, N/2 + 1]."""
-    g, X = _fft4_padded(x, accels, tsamp)
+    FFT's spectrum layout.  Returns P [K, N/2 + 1]; with ``nbins_out`` only
+    bins below it are formed (pass B then stores only the spectrum rows the
+    r2c step reads, as the search engine does) and the rest stay zero."""
+    M = (x.numel()) // 2
+    nbo = M + 1 if nbins_out is None else int(nbins_out)
+    g, X = _fft4_padded(x, accels, tsamp, nbins_out=0 if nbins_out is None else nbo)
     Kb = X.shape[0]
-    M = g.n1 * g.n2
     log2_row, row, blk, lw, tiled = fft4_x_layout(g)
-    P = torch.empty((Kb, M + 1), dtype=torch.float32, device=x.device)
+    P = torch.zeros((Kb, M + 1), dtype=torch.float32, device=x.device)
     if tiled:
-        K.r2c_interbin_normalise_tiled(X.data_ptr(), g.n1, g.n2, g.xstride, P.data_ptr(), M + 1, Kb, M + 1,
+        K.r2c_interbin_normalise_tiled(X.data_ptr(), g.n1, g.n2, g.xstride, P.data_ptr(), M + 1, Kb, nbo,
                                        stats.data_ptr(), float(nscale), _s())
     else:
         K.r2c_interbin_normalise_batch(X.data_ptr(), M, g.xstride, log2_row, row, blk, lw, P.data_ptr(), M + 1, Kb,
-                                       M + 1, stats.data_ptr(), float(nscale), _s())
+                                       nbo, stats.data_ptr(), float(nscale), _s())
     return P
 
 

@@ -215,7 +215,7 @@ def test_r2c_interbin_normalise_batch():
         assert np.allclose(P[k], exp, rtol=1e-4, atol=2e-3), np.abs(P[k] - exp).max()
 
 
-FFT4_FLAG_SETS = [None, 0, 1, 259, 274, 1299, 3331, 7427]  # None = default (15619); 3331 = tiled Y and X
+FFT4_FLAG_SETS = [None, 0, 1, 259, 274, 1299, 3331, 7427, 32003]  # None = default; 3331 = tiled Y and X; 32003 = + Sub2
 
 
 @pytest.fixture(params=FFT4_FLAG_SETS)
@@ -332,3 +332,21 @@ def test_fft4_interbin_path_matches_rocfft_path(log2n, fft4_flags):
     scale = np.abs(P1).max()
     assert np.abs(P2 - P1).max() / scale < 1e-4
     assert np.sqrt(np.mean((P2 - P1) ** 2)) / np.sqrt(np.mean(P1 ** 2)) < 1e-5
+
+
+@pytest.mark.parametrize("log2n,frac", [(21, 0.1), (21, 0.37), (23, 0.1408), (21, 0.499)])
+def test_fft4_pruned_spectrum_rows_match_full(log2n, frac):
+    """Search path: pass B stores only the spectrum rows the tiled r2c reads
+    for bins < nbins_out; those bins are bit-identical to the unpruned path."""
+    from peasoup_amd import ops
+
+    rng = np.random.default_rng(7 + log2n)
+    n = 1 << log2n
+    x = torch.from_numpy(rng.standard_normal(n).astype(np.float32)).to(dev)
+    accs = [-250.0, 0.0, 120.0, 499.0, -499.0, 3.0, 7.0, -1.0]
+    st = torch.tensor([1.0, 2.0, 0.5, 0.0], dtype=torch.float32, device=dev)
+    nbo = int(frac * n)
+    full = ops.fft4_resample_interbin(x, accs, 64e-6, st, float(n))
+    pruned = ops.fft4_resample_interbin(x, accs, 64e-6, st, float(n), nbins_out=nbo)
+    assert torch.equal(full[:, :nbo], pruned[:, :nbo])
+    assert torch.count_nonzero(pruned[:, nbo:]) == 0

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Full GPU check: gpu tests, smoke(), one bench, rocprofv3 kernel stats of the bench.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 240 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo TESTS_FAIL; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -2 gpurun_out/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo SMOKE_FAIL; tail -30 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
+timeout -k 10 400 python bench.py "$@" > gpurun_out/bench.log 2>&1 || { echo BENCH_FAIL; tail -30 gpurun_out/bench.log; exit 1; }
+tail -1 gpurun_out/bench.log
+bash tools/gpu_prof.sh prof "$@"
