@@ -306,12 +306,20 @@ typedef float f4u_h __attribute__((ext_vector_type(4), aligned(4)));  // dword-a
 // round-robin dispatch) runs trials x, x+8, ... and each trial's tiles in
 // increasing order, so the recently streamed part of that trial's spectrum
 // -- where the high-numerator gather ranges lie -- is in the XCD's own L2.
+// Conservative pre-thresholds on the unscaled running sums: o_h > thresh
+// implies sum_h > lo[h] (lo[h] sits a relative 1e-5 below thresh / scale_h),
+// so a bin group whose sums all stay at or below lo[] cannot hold a peak and
+// skips the exact double-scaled levels and range checks.
+struct HarmPre {
+  float lo[6];
+};
+
 template <int NLEV>
 __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __restrict__ P, uint64_t pstride,
                                                              int lo, int hi, HarmParams hp,
                                                              PeakRecord* __restrict__ out,
                                                              uint32_t* __restrict__ count, int ntiles,
-                                                             int xcd_trials) {
+                                                             int xcd_trials, HarmPre pre) {
   using Tl = HarmTile<NLEV>;
   constexpr int B = Tl::B;
   __shared__ __attribute__((aligned(16))) float lds[Tl::TOTAL];
@@ -413,36 +421,50 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
     const int i = i0 + u * 256;
     const bool valid = i < hi;
     float val = fund[u];  // fundamental P[i]
-    float o[NLEV + 1];
-    o[0] = val;
+    float sum[NLEV + 1];  // unscaled running sum after each level
+    sum[0] = val;
 #define PS_TERM(h, m) lds[base[(1 << ((h) - 1)) + (m) / 2] + u * ((m) << (8 - (h)))]
     if constexpr (NLEV >= 1) {
       val += PS_TERM(1, 1);
-      o[1] = static_cast<float>(static_cast<double>(val) * c_level_scale[1]);
+      sum[1] = val;
     }
     if constexpr (NLEV >= 2) {
       val += PS_TERM(2, 3);  // reference order: 3/4 before 1/4
       val += PS_TERM(2, 1);
-      o[2] = val * 0.5f;  // == (float)((double)val * 0.5): exact scaling
+      sum[2] = val;
     }
     if constexpr (NLEV >= 3) {
 #pragma unroll
       for (int m = 1; m < 8; m += 2) val += PS_TERM(3, m);
-      o[3] = static_cast<float>(static_cast<double>(val) * c_level_scale[3]);
+      sum[3] = val;
     }
     if constexpr (NLEV >= 4) {
 #pragma unroll
       for (int m = 1; m < 16; m += 2) val += PS_TERM(4, m);
-      o[4] = val * 0.25f;  // exact
+      sum[4] = val;
     }
     if constexpr (NLEV >= 5) {
 #pragma unroll
       for (int m = 1; m < 32; m += 2) val += PS_TERM(5, m);
-      o[5] = static_cast<float>(static_cast<double>(val) * c_level_scale[5]);
+      sum[5] = val;
     }
 #undef PS_TERM
-    // branch-free predicates (bitwise, no short-circuit: the compiler would
-    // otherwise emit an exec-mask branch per level and bin)
+    bool cand = false;
+#pragma unroll
+    for (int h = 0; h <= NLEV; ++h) cand = cand | (sum[h] > pre.lo[h]);
+    if (__ballot(cand) == 0ull) continue;  // the usual no-peak case: one compare per level
+    // exact levels: each scaled by the double constant rsqrt(2^h) before rounding to float
+    float o[NLEV + 1];
+#pragma unroll
+    for (int h = 0; h <= NLEV; ++h) {
+      if (h == 2)
+        o[h] = sum[h] * 0.5f;  // == (float)((double)sum * 0.5): exact scaling
+      else if (h == 4)
+        o[h] = sum[h] * 0.25f;
+      else
+        o[h] = h == 0 ? sum[0] : static_cast<float>(static_cast<double>(sum[h]) * c_level_scale[h]);
+    }
+    // branch-free predicates (bitwise, no short-circuit)
     bool pred[NLEV + 1];
     bool any = false;
 #pragma unroll
@@ -549,6 +571,20 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
   if (hi <= lo) return;
   PSOUP_CHECK(static_cast<int64_t>(hi) * 32 < (int64_t(1) << 31), "spectrum too long for the int32 gather math");
   const int xcd = (g_harm_flags & 1) && (K % 8 == 0);
+  HarmPre pre;
+  {
+    static const double scale[6] = {1.0, 0.70710678118654752440, 0.5, 0.35355339059327376220, 0.25,
+                                    0.17677669529663688110};
+    for (int h = 0; h < 6; ++h) {
+      const double t = static_cast<double>(hp.thresh) / scale[h];
+      // rounding to float and the double product can move o_h by < 2^-23
+      // relative; 1e-5 relative margin (and an absolute one near 0) is safe
+      const double lo = t - std::fabs(t) * 1e-5 - 1e-30;
+      float f = static_cast<float>(lo);
+      if (static_cast<double>(f) > lo) f = std::nextafter(f, -INFINITY);
+      pre.lo[h] = (g_harm_flags & 2) ? -INFINITY : f;  // bit 1: disable the pre-threshold (testing)
+    }
+  }
   auto ntiles_of = [&](int B) { return (hi - lo + B - 1) / B; };
   switch (hp.nlevels) {
 #define PS_CASE(NL)                                                                                           \
@@ -556,7 +592,7 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
     const int nt = ntiles_of(HarmTile<NL>::B);                                                                \
     PSOUP_CHECK(static_cast<int64_t>(nt) * K < (int64_t(1) << 31), "harmonic grid too large");               \
     harmonic_peaks_kernel<NL><<<dim3(static_cast<unsigned>(nt * K)), 256, 0, s>>>(P, pstride, lo, hi, hp, out,  \
-                                                                                  count, nt, xcd);             \
+                                                                                  count, nt, xcd, pre);        \
     break;                                                                                                    \
   }
     PS_CASE(0) PS_CASE(1) PS_CASE(2) PS_CASE(3) PS_CASE(4)

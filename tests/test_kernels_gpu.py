@@ -350,3 +350,35 @@ def test_fft4_pruned_spectrum_rows_match_full(log2n, frac):
     pruned = ops.fft4_resample_interbin(x, accs, 64e-6, st, float(n), nbins_out=nbo)
     assert torch.equal(full[:, :nbo], pruned[:, :nbo])
     assert torch.count_nonzero(pruned[:, nbo:]) == 0
+
+
+@pytest.mark.parametrize("nlev,thresh", [(1, 6.0), (3, 9.0), (3, 11.5), (5, 10.0)])
+def test_harmonic_prethreshold_is_exact(nlev, thresh):
+    """The conservative unscaled pre-threshold (fast no-peak path) never drops a
+    peak: records equal the exact-path records and the threshold of the
+    reference sums."""
+    import peasoup_amd._C as C
+    from peasoup_amd import ops
+
+    rng = np.random.default_rng(40 + nlev)
+    n, Kb = 70001, 8
+    P = rng.standard_normal((Kb, n)).astype(np.float32) * 3.0
+    starts = [3, 5, 9, 17, 33, 65]
+    ends = [n] * 6
+    Pt = torch.from_numpy(P).to(dev)
+    runs = []
+    try:
+        for flags in (1, 3):  # bit 1 disables the pre-threshold
+            C.kernels.harmonic_set_flags(flags)
+            trial, level, idx, snr = ops.harmonic_peaks(Pt, nlev, starts, ends, thresh)
+            runs.append(sorted(zip(trial.tolist(), level.tolist(), idx.tolist(), snr.tolist())))
+    finally:
+        C.kernels.harmonic_set_flags(1)
+    assert runs[0] == runs[1] and len(runs[0]) > 20
+    exp = set()
+    for k in range(Kb):
+        levels = [P[k]] + ref.harmonic_sums(P[k], nlev)
+        for h, L in enumerate(levels):
+            sel = np.nonzero(L[starts[h]:ends[h]] > thresh)[0] + starts[h]
+            exp |= {(k, h, int(i)) for i in sel}
+    assert {r[:3] for r in runs[0]} == exp
