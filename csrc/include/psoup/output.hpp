@@ -99,12 +99,23 @@ class CandidateFileWriter {
   explicit CandidateFileWriter(std::string outdir);
   // Returns false (after perror) when the file cannot be opened.
   bool write_binary(const CandidateList& cands, const std::string& filename);
+  // One file per candidate, cand_%04d_<P %.5f>_<DM %.1f>_<acc %.1f>.peasoup, same
+  // record format (output_stats.hpp:272-307 write_binaries); fills `filenames`
+  // with the absolute paths.  Returns false (after perror) on the first failure.
+  bool write_binaries(const CandidateList& cands);
   std::map<unsigned, long> byte_mapping;
+  std::map<unsigned, std::string> filenames;
   const std::string& outdir() const { return outdir_; }
 
  private:
   std::string outdir_;
 };
+
+// Text candidate dumps (candidates.hpp:120-150): one Candidate::print file per
+// candidate (cand_%04d_..., CandidateCollection::generate_candidate_binaries)
+// and a single annotated listing (write_candidate_file).
+bool write_candidate_text_files(const CandidateList& cands, const std::string& outdir);
+bool write_candidate_file(const CandidateList& cands, const std::string& path);
 
 // Recursive mkdir -p (0777 & ~umask); returns false on failure.
 bool make_dirs(const std::string& path);

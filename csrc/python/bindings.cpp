@@ -381,6 +381,14 @@ PYBIND11_MODULE(_C, m) {
     std::map<unsigned, long> bm = w.byte_mapping;
     return bm;
   });
+  m.def("write_candidates_binaries", [](const std::string& outdir, const CandidateList& c) {
+    CandidateFileWriter w(outdir);
+    if (!w.write_binaries(c)) throw std::runtime_error("write_binaries failed in " + outdir);
+    std::map<unsigned, std::string> names = w.filenames;
+    return names;
+  });
+  m.def("write_candidate_text_files", &write_candidate_text_files);
+  m.def("write_candidate_file", &write_candidate_file);
   m.def(
       "write_overview",
       [](const std::string& path, const CmdLineOptions& args, const py::object& header_file, const std::vector<float>& dms,

@@ -1,3 +1,5 @@
+#include <climits>
+#include <cstdlib>
 #include "psoup/output.hpp"
 
 #include <sys/stat.h>
@@ -278,6 +280,80 @@ bool CandidateFileWriter::write_binary(const CandidateList& cands, const std::st
     int32_t ndets = static_cast<int32_t>(dets.size());
     std::fwrite(&ndets, sizeof(int32_t), 1, fo);
     std::fwrite(dets.data(), sizeof(CandidatePOD), dets.size(), fo);
+  }
+  std::fclose(fo);
+  return true;
+}
+
+namespace {
+std::string cand_filename(size_t i, const Candidate& c) {
+  char buf[160];
+  std::snprintf(buf, sizeof(buf), "cand_%04d_%.5f_%.1f_%.1f.peasoup", static_cast<int>(i), 1.0 / c.freq, c.dm,
+                c.acc);
+  return buf;
+}
+
+void write_record(FILE* fo, const Candidate& c, std::vector<CandidatePOD>& dets) {
+  if (!c.fold.empty()) {
+    std::fwrite("FOLD", 1, 4, fo);
+    int32_t nb = c.nbins, ni = c.nints;
+    std::fwrite(&nb, sizeof(int32_t), 1, fo);
+    std::fwrite(&ni, sizeof(int32_t), 1, fo);
+    std::fwrite(c.fold.data(), sizeof(float), static_cast<size_t>(nb) * ni, fo);
+  }
+  dets.clear();
+  c.collect_candidates(dets);
+  int32_t ndets = static_cast<int32_t>(dets.size());
+  std::fwrite(&ndets, sizeof(int32_t), 1, fo);
+  std::fwrite(dets.data(), sizeof(CandidatePOD), dets.size(), fo);
+}
+}  // namespace
+
+bool CandidateFileWriter::write_binaries(const CandidateList& cands) {
+  filenames.clear();
+  std::vector<CandidatePOD> dets;
+  for (size_t i = 0; i < cands.size(); ++i) {
+    const std::string path = outdir_ + "/" + cand_filename(i, cands[i]);
+    FILE* fo = std::fopen(path.c_str(), "wb");
+    if (!fo) {
+      perror(path.c_str());
+      return false;
+    }
+    write_record(fo, cands[i], dets);
+    std::fclose(fo);
+    char real[PATH_MAX];
+    filenames[static_cast<unsigned>(i)] = realpath(path.c_str(), real) ? std::string(real) : path;
+  }
+  return true;
+}
+
+bool write_candidate_text_files(const CandidateList& cands, const std::string& outdir) {
+  if (!make_dirs(outdir)) return false;
+  for (size_t i = 0; i < cands.size(); ++i) {
+    const std::string path = outdir + "/" + cand_filename(i, cands[i]);
+    FILE* fo = std::fopen(path.c_str(), "w");
+    if (!fo) {
+      perror(path.c_str());
+      return false;
+    }
+    const std::string txt = cands[i].print();
+    std::fwrite(txt.data(), 1, txt.size(), fo);
+    std::fclose(fo);
+  }
+  return true;
+}
+
+bool write_candidate_file(const CandidateList& cands, const std::string& path) {
+  FILE* fo = std::fopen(path.c_str(), "w");
+  if (!fo) {
+    perror(path.c_str());
+    return false;
+  }
+  std::fprintf(fo, "#Period...Optimal period...Frequency...DM...Acceleration...Harmonic number...S/N...Folded S/N\n");
+  for (size_t i = 0; i < cands.size(); ++i) {
+    std::fprintf(fo, "#Candidate %d\n", static_cast<int>(i));
+    const std::string txt = cands[i].print();
+    std::fwrite(txt.data(), 1, txt.size(), fo);
   }
   std::fclose(fo);
   return true;

@@ -107,3 +107,30 @@ def test_coincidencer_cli(C):
 def test_radec_to_str():
     assert radec_to_str(123456.78) == "12:34:56.7800"
     assert radec_to_str(-12345.5) == "-1:23:45.5000"  # "%02d" of -1, as peasoup_tools.py
+
+
+def test_per_candidate_binaries_and_text_files(C, tmp_path):
+    """write_binaries (output_stats.hpp:272-307): one cand_%04d_P_DM_acc.peasoup
+    per candidate with the same record format; text dumps (candidates.hpp:120-150)."""
+    cands = [_cand(C, i) for i in range(3)]
+    names = C.write_candidates_binaries(str(tmp_path / "bins"), cands)
+    assert sorted(names) == [0, 1, 2]
+    for i, c in enumerate(cands):
+        base = "cand_%04d_%.5f_%.1f_%.1f.peasoup" % (i, 1.0 / np.float32(4.0 + i), np.float32(10.0 + i),
+                                                   np.float32(-1.5 * i))
+        assert os.path.basename(names[i]) == base and os.path.isabs(names[i])
+        recs = CandidateFileParser(names[i]).records()
+        assert len(recs) == 1
+        off, fold, hits = recs[0]
+        assert off == 0 and len(hits) == 2
+        assert (fold is not None) == (i % 2 == 0)
+        assert hits[0]["snr"] == pytest.approx(50.0 - i) and hits[1]["dm_idx"] == i + 1
+    assert C.write_candidate_text_files(cands, str(tmp_path / "txt"))
+    txt = sorted(os.listdir(tmp_path / "txt"))
+    assert len(txt) == 3
+    first = open(tmp_path / "txt" / txt[0]).read().splitlines()
+    assert len(first) == 2 and len(first[0].split("\t")) == 13
+    assert C.write_candidate_file(cands, str(tmp_path / "candidates.txt"))
+    lines = open(tmp_path / "candidates.txt").read().splitlines()
+    assert lines[0].startswith("#Period...Optimal period") and lines[1] == "#Candidate 0"
+    assert sum(1 for ln in lines if ln.startswith("#Candidate")) == 3
