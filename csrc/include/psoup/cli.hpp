@@ -80,4 +80,32 @@ struct CoincidencerOptions {
 bool parse_coincidencer_cmdline(CoincidencerOptions& args, int argc, const char* const* argv,
                                 bool* exit_now = nullptr);
 
+// FFA pipeline options (include/utils/cmdline.hpp:35-50 FFACmdLineOptions,
+// :211-292 read_ffa_cmdline_options): same flags and defaults.
+struct FfaCmdLineOptions {
+  std::string infilename;
+  std::string outfilename;
+  std::string killfilename;
+  int max_num_threads = 14;
+  unsigned int nstreams = 16;
+  float dm_start = 0.0f;
+  float dm_end = 100.0f;
+  float dm_tol = 1.10f;
+  float dm_pulse_width = 64.0f;
+  float p_start = 0.8f;
+  float p_end = 20.0f;
+  float min_dc = 0.001f;
+  bool verbose = false;
+  bool progress_bar = false;
+  // MI355X-native extensions (long options only)
+  float min_snr = 7.0f;
+  int nbins = 0;
+  int limit = 1000;
+  double cluster_tol = 2.0;
+  std::string dedisp_kernel = "auto";
+};
+// "%Y-%m-%d-%H:%M_ffaster.output" in UTC (cmdline.hpp:61-67).
+std::string default_ffa_output_filename();
+bool parse_ffa_cmdline(FfaCmdLineOptions& args, const std::vector<std::string>& argv, bool* exit_now = nullptr);
+
 }  // namespace psoup

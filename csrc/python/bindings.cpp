@@ -12,6 +12,7 @@
 #include "psoup/cli.hpp"
 #include "psoup/common.hpp"
 #include "psoup/engine.hpp"
+#include "psoup/ffa.hpp"
 #include "psoup/fft.hpp"
 #include "psoup/kernels.hpp"
 #include "psoup/output.hpp"
@@ -109,6 +110,8 @@ SigprocHeader dict_to_header(const py::dict& d) {
 }
 
 }  // namespace
+
+void bind_ffa(py::module_& m);  // bind_ffa.cpp
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "peasoup_amd native core (C++/HIP for gfx950)";
@@ -412,6 +415,8 @@ PYBIND11_MODULE(_C, m) {
       py::arg("cands"), py::arg("byte_map"), py::arg("timers"), py::arg("perf"));
 
   // ------------------------------------------------------------- kernels --
+  bind_ffa(m);
+
   py::module_ k = m.def_submodule("kernels", "raw HIP kernel launchers (addresses + stream handles)");
   k.def("unpack_transpose", [](uintptr_t packed, uint64_t nsamps, int nchans, int nbits, uintptr_t out,
                                uint64_t out_stride, int bias, uintptr_t s) {
@@ -536,6 +541,12 @@ PYBIND11_MODULE(_C, m) {
     kern::harmonic_sums(P<const float>(Pin), nb, nlevels, P<float>(out), S(s));
   });
   k.def("harmonic_set_flags", &kern::harmonic_set_flags);
+  k.def("ffa_downsample", [](uintptr_t x, uint64_t n, double f, uintptr_t out, uint64_t nout, uintptr_t s) {
+    kern::ffa_downsample(P<const float>(x), n, f, P<float>(out), nout, S(s));
+  });
+  k.def("ffa_detrend", [](uintptr_t in, uint64_t n, uint64_t window, uintptr_t means, uintptr_t out, uintptr_t s) {
+    kern::ffa_detrend(P<const uint8_t>(in), n, window, P<float>(means), P<float>(out), S(s));
+  });
   k.def("fold_shift_table", [](uintptr_t table, int nbins, int nints, uintptr_t s) {
     kern::fold_shift_table(P<float2>(table), nbins, nints, S(s));
   });

@@ -282,4 +282,38 @@ bool parse_coincidencer_cmdline(CoincidencerOptions& a, int argc, const char* co
   return true;
 }
 
+std::string default_ffa_output_filename() {
+  char buf[128];
+  std::time_t t = std::time(nullptr);
+  std::strftime(buf, sizeof(buf), "%Y-%m-%d-%H:%M_ffaster.output", std::gmtime(&t));
+  return std::string(buf);
+}
+
+bool parse_ffa_cmdline(FfaCmdLineOptions& a, const std::vector<std::string>& argv, bool* exit_now) {
+  a.outfilename = default_ffa_output_filename();
+  std::vector<Spec> specs = {
+      val_s("i", "inputfile", "File to process (.fil)", a.infilename, true),
+      val_s("o", "outfilename", "The output filename", a.outfilename),
+      val_s("k", "killfile", "Channel mask file", a.killfilename),
+      val_n("t", "num_threads", "The number of GPUs to use", a.max_num_threads),
+      val_u("", "nstreams", "The number of CUDA streams to use", a.nstreams),
+      val_n("", "dm_start", "First DM to dedisperse to", a.dm_start),
+      val_n("", "dm_end", "Last DM to dedisperse to", a.dm_end),
+      val_n("", "dm_tol", "DM smearing tolerance (1.11=10%)", a.dm_tol),
+      val_n("", "dm_pulse_width", "Minimum pulse width for which dm_tol is valid", a.dm_pulse_width),
+      val_n("", "p_start", "Start period for FFA search", a.p_start),
+      val_n("", "p_end", "End period for FFA search", a.p_end),
+      val_n("", "min_dc", "Minimum duty cycle", a.min_dc),
+      sw("v", "verbose", "verbose mode", a.verbose),
+      sw("p", "progress_bar", "Enable progress bar for DM search", a.progress_bar),
+      // MI355X-native extensions
+      val_n("m", "min_snr", "Minimum boxcar S/N of a folded profile", a.min_snr),
+      val_n("", "bins", "Base bins per period (periods span [bins, 2 bins)); 0 = from --min_dc", a.nbins),
+      val_n("", "limit", "Upper limit on the number of candidates written", a.limit),
+      val_n("", "cluster_tol", "Peak clustering tolerance in units of 1/T_obs", a.cluster_tol),
+      val_s("", "dedisp_kernel", "Dedispersion kernel: auto | mfma | direct", a.dedisp_kernel),
+  };
+  return run_parser(specs, argv, "Peasoup/FFAster extension - a GPU FFA pulsar search pipeline", nullptr, exit_now);
+}
+
 }  // namespace psoup

@@ -316,3 +316,63 @@ def coincidence_mask(arrays: Sequence[np.ndarray], thresh: float, beam_thresh: i
     for a in arrays:
         cnt += (a > np.float32(thresh))
     return (cnt < beam_thresh).astype(np.float32)
+
+
+# ----------------------------------------------------------------- FFA ------
+def ffa_transform(X: np.ndarray) -> np.ndarray:
+    """Radix-2 FFA (Staelin) of an [m, P] fold matrix, m a power of two:
+    out[s] = H[s//2] + roll(T[s//2], -((s+1)//2)) over the two transformed
+    halves; row s is the fold at period P + s/(m-1) bins (ffa.hip convention).
+    Evaluated in float64 (the oracle)."""
+    X = np.asarray(X, dtype=np.float64)
+    m = X.shape[0]
+    if m == 1:
+        return X.copy()
+    h = m // 2
+    H, T = ffa_transform(X[:h]), ffa_transform(X[h:])
+    out = np.empty_like(X)
+    for s in range(m):
+        j = s // 2
+        out[s] = H[j] + np.roll(T[j], -((s + 1) // 2))
+    return out
+
+
+def ffa_fold_matrix(ds: np.ndarray, P: int) -> np.ndarray:
+    """[m2, P]: floor(len/P) rows of the series, zero rows up to a power of two."""
+    m = len(ds) // P
+    m2 = 1 << int(np.ceil(np.log2(max(1, m))))
+    X = np.zeros((m2, P), dtype=np.float64)
+    X[:m] = np.asarray(ds[: m * P], dtype=np.float64).reshape(m, P)
+    return X
+
+
+def boxcar_best_snr(profile: np.ndarray, widths, var: float) -> float:
+    """Max over widths and circular phases of boxcar_sum / sqrt(w var)."""
+    p = np.asarray(profile, dtype=np.float64)
+    P = len(p)
+    ext = np.concatenate([p, p])
+    c = np.concatenate([[0.0], np.cumsum(ext)])
+    best = -np.inf
+    for w in widths:
+        if w >= P:
+            break
+        s = (c[w: w + P] - c[:P]).max()
+        best = max(best, s / np.sqrt(w * var))
+    return best
+
+
+def ffa_downsample(x: np.ndarray, f: float) -> np.ndarray:
+    """Piecewise-constant integration over [j f, (j+1) f)."""
+    x = np.asarray(x, dtype=np.float64)
+    n = len(x)
+    nout = int(np.floor(n / f))
+    c = np.concatenate([[0.0], np.cumsum(x)])
+
+    def integ(t):
+        i = np.minimum(np.floor(t).astype(np.int64), n)
+        frac = t - i
+        return c[i] + np.where(i < n, x[np.minimum(i, n - 1)] * frac, 0.0)
+
+    j = np.arange(nout + 1, dtype=np.float64) * f
+    I = integ(j)
+    return I[1:] - I[:-1]
