@@ -112,15 +112,16 @@ void bind_ffa(py::module_& m) {
       .def_property_readonly("peaks", &FfaEngine::peaks);
 
   py::class_<FfaResult>(m, "FfaResult")
-      .def_readonly("candidates", &FfaResult::candidates)
-      .def_readonly("dm_list", &FfaResult::dm_list)
-      .def_readonly("devices", &FfaResult::devices)
-      .def_readonly("timers", &FfaResult::timers)
-      .def_readonly("nsamps", &FfaResult::nsamps)
-      .def_readonly("tobs", &FfaResult::tobs)
-      .def_readonly("nb0", &FfaResult::nb0)
-      .def_readonly("profiles", &FfaResult::profiles)
-      .def_readonly("peaks", &FfaResult::peaks);
+      .def(py::init<>())
+      .def_readwrite("candidates", &FfaResult::candidates)
+      .def_readwrite("dm_list", &FfaResult::dm_list)
+      .def_readwrite("devices", &FfaResult::devices)
+      .def_readwrite("timers", &FfaResult::timers)
+      .def_readwrite("nsamps", &FfaResult::nsamps)
+      .def_readwrite("tobs", &FfaResult::tobs)
+      .def_readwrite("nb0", &FfaResult::nb0)
+      .def_readwrite("profiles", &FfaResult::profiles)
+      .def_readwrite("peaks", &FfaResult::peaks);
   m.def("run_ffa_pipeline", [](const FfaCmdLineOptions& a) {
     py::gil_scoped_release nogil;
     return run_ffa_pipeline(a);

@@ -1,4 +1,5 @@
-"""``python -m peasoup_amd [peasoup flags]`` -- the peasoup CLI as a
+"""``python -m peasoup_amd [peasoup flags]`` (or ``python -m peasoup_amd ffa
+[ffaster flags]`` for the FFA search) -- the peasoup CLI as a
 torchrun-compatible, one-process-per-GPU program:
 
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \\
@@ -29,6 +30,8 @@ def main(argv=None) -> int:
     from .parallel import dist as pdist
 
     argv = list(sys.argv if argv is None else argv)
+    if len(argv) > 1 and argv[1] == "ffa":
+        return _main_ffa(["ffaster"] + argv[2:])
     argv[0] = "peasoup"
     ok, exit_now, args = _C.parse_cmdline(argv)
     if not ok:
@@ -58,6 +61,33 @@ def main(argv=None) -> int:
     if res is not None and (args.verbose or args.progress_bar):
         print(f"Wrote {len(res.candidates)} candidates to {args.outdir}; "
               f"{res.performance['dm_accel_trials_per_sec']:.1f} DMxaccel trials/s over {int(res.performance['ranks'])} rank(s)")
+    pdist.shutdown()
+    return 0
+
+
+def _main_ffa(argv) -> int:
+    from . import _C
+    from .models.ffa import run_ffa_search
+    from .parallel import dist as pdist
+
+    ok, exit_now, args = _C.parse_ffa_cmdline(argv)
+    if not ok:
+        print("Failed to parse command line arguments.", file=sys.stderr)
+        return 1
+    if exit_now:
+        return 0
+    try:
+        res = run_ffa_search(args)
+    except BaseException as e:  # noqa: BLE001 - same teardown policy as the search
+        import os
+        import traceback
+
+        print(f"[rank {os.environ.get('RANK', '0')}] ffa failed: {e}", file=sys.stderr)
+        traceback.print_exc()
+        sys.stderr.flush()
+        os._exit(1)
+    if res is not None and args.verbose:
+        print(f"Wrote {len(res.candidates)} FFA candidates to {args.outfilename}")
     pdist.shutdown()
     return 0
 

@@ -154,3 +154,49 @@ def test_ffa_detrend_removes_linear_trend():
     y = out.cpu().numpy()
     mid = slice(w, n - w)
     assert abs(np.polyfit(t[mid], y[mid], 1)[0]) < 1e-5 and abs(y[mid].mean()) < 0.2
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.gpu
+def test_ffa_two_rank_search_equals_native_pipeline(tmp_path):
+    """DM-sharded FFA (2 ranks, gloo transport, one GPU) + gather + cross-DM
+    clustering == the native thread-per-GPU pipeline's candidates."""
+    import sys
+
+    hdr = synthetic.make_header(nchans=32, nbits=2, tsamp=1e-3)
+    path = str(tmp_path / "d.fil")
+    synthetic.write(path, 1 << 16, hdr, [synthetic.PulsarSpec(period=0.6321, dm=15.0, duty=0.03, amplitude=0.5)],
+                    seed=4)
+    flags = ["-i", path, "--dm_end", "40", "--p_start", "0.3", "--p_end", "2.0", "--min_dc", "0.02", "-t", "1"]
+    script = (
+        "import os,sys; sys.path.insert(0, %r)\n"
+        "from peasoup_amd.parallel import dist as pdist\n"
+        "pdist.init(backend='gloo')\n"
+        "from peasoup_amd import __main__ as m\n"
+        "raise SystemExit(m.main(['x', 'ffa'] + sys.argv[1:]))\n" % REPO)
+    f = tmp_path / "run.py"
+    f.write_text(script)
+    port = _free_port()
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="2")
+    out = str(tmp_path / "dist.txt")
+    procs = [subprocess.Popen([sys.executable, str(f)] + flags + ["-o", out], env=dict(env, RANK=str(r), LOCAL_RANK="0"),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(2)]
+    for p in procs:
+        _, err = p.communicate(timeout=300)
+        assert p.returncode == 0, err[-3000:]
+    ok, _, a = C.parse_ffa_cmdline(["ffaster"] + flags + ["-o", str(tmp_path / "native.txt")])
+    res = C.run_ffa_pipeline(a)
+    rows = [ln.split() for ln in open(out) if not ln.startswith("#")]
+    assert len(rows) == len(res.candidates) > 0
+    for row, c in zip(rows, res.candidates):
+        assert float(row[1]) == pytest.approx(c.period, rel=1e-9) and int(row[4]) == c.dm_idx
+        assert float(row[5]) == pytest.approx(c.snr, abs=1e-3)
