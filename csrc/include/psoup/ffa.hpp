@@ -46,14 +46,21 @@ struct FfaPeak {
 static_assert(sizeof(FfaPeak) == 16, "FfaPeak layout");
 
 // Block means over `window` samples, x = in - (linear trend between block
-// centres).  block_means: ceil(n / window) floats.
-void ffa_detrend(const uint8_t* in, uint64_t n, uint64_t window, float* block_means, float* out, hipStream_t s);
+// centres).  sums / block_means: ceil(n / window) elements (< 65536).
+void ffa_detrend(const uint8_t* in, uint64_t n, uint64_t window, unsigned long long* sums, float* block_means,
+                 float* out, hipStream_t s);
 // out[j] = integral of x over [j f, (j+1) f), j < nout <= n / f (f >= 1).
 void ffa_downsample(const float* x, uint64_t n, double f, float* out, uint64_t nout, hipStream_t s);
-// Folded FFA planes of every period of a chunk (arena layout from FfaPeriod);
-// the result of period i lies in arena1 iff its number of global stages
-// (log2m2 - LDS stages) is odd -- ffa_snr resolves that.
+// Folded FFA planes of every period of a chunk (arena layout from FfaPeriod):
+// the first min(4, log2m2) stages on LDS-resident row blocks (when the
+// chunk's longest period fits), the rest as ping-pong passes of two stages.
 bool ffa_uses_lds(int max_p);
+// True when period pp's result lies in the second arena: an odd number of
+// global passes, ceil((log2m2 - LDS stages) / 2).
+__host__ __device__ inline bool ffa_result_in_second(const FfaPeriod& pp, int lds_stages) {
+  const int g = pp.log2m2 - (pp.log2m2 < lds_stages ? pp.log2m2 : lds_stages);
+  return (((g + 1) / 2) & 1) != 0;
+}
 void ffa_transform(const float* ds, const FfaPeriod* d_periods, int nper, int max_m2, int max_log2m2, int max_p,
                    float* arena0, float* arena1, hipStream_t s);
 // Best boxcar S/N of every folded profile; records above sp.thresh are
@@ -135,6 +142,7 @@ class FfaEngine {
   hipStream_t stream_;
   std::vector<FfaOctave> plan_;
   DeviceBuffer<float> x_, ds_, means_, a0_, a1_;
+  DeviceBuffer<unsigned long long> sums_;
   DeviceBuffer<double> partials_;
   DeviceBuffer<float> stats_;
   DeviceBuffer<kern::FfaPeak> d_peaks_;

@@ -26,20 +26,34 @@
 #include "device_common.hpp"
 #include "psoup/ffa.hpp"
 
+#include <algorithm>
+
 namespace psoup {
 namespace kern {
 
 namespace {
 
-__global__ void __launch_bounds__(256) block_means_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t w,
-                                                          float* __restrict__ means) {
-  __shared__ double scratch[4];
-  const uint64_t b0 = static_cast<uint64_t>(blockIdx.x) * w;
+// Exact per-block byte sums: blockIdx.y = trend block, x splits it.
+__global__ void __launch_bounds__(256) block_sums_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t w,
+                                                         unsigned long long* __restrict__ sums) {
+  __shared__ unsigned long long scratch[4];
+  const uint64_t b0 = static_cast<uint64_t>(blockIdx.y) * w;
   const uint64_t b1 = b0 + w < n ? b0 + w : n;
-  double acc = 0.0;
-  for (uint64_t i = b0 + threadIdx.x; i < b1; i += blockDim.x) acc += in[i];
+  unsigned long long acc = 0;
+  for (uint64_t i = b0 + blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < b1;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    acc += in[i];
   acc = dev::block_sum(acc, scratch);
-  if (threadIdx.x == 0) means[blockIdx.x] = static_cast<float>(acc / static_cast<double>(b1 - b0));
+  if (threadIdx.x == 0 && acc) atomicAdd(&sums[blockIdx.y], acc);
+}
+
+__global__ void block_means_kernel(const unsigned long long* __restrict__ sums, uint64_t n, uint64_t w, int nblk,
+                                   float* __restrict__ means) {
+  for (int b = blockIdx.x * blockDim.x + threadIdx.x; b < nblk; b += gridDim.x * blockDim.x) {
+    const uint64_t b0 = static_cast<uint64_t>(b) * w;
+    const uint64_t cnt = (b0 + w < n ? b0 + w : n) - b0;
+    means[b] = static_cast<float>(static_cast<double>(sums[b]) / static_cast<double>(cnt));
+  }
 }
 
 // x[i] = in[i] - trend(i); trend is linear between block centres (flat
@@ -100,66 +114,111 @@ __global__ void __launch_bounds__(256) fill_kernel(const float* __restrict__ ds,
 constexpr int kLdsLog2 = 4;
 constexpr int kLdsRows = 1 << kLdsLog2;
 constexpr int kLdsFloats = 16384;  // 64 KiB: 16 rows x 1024 bins
+constexpr int kMaxProfile = 2048;
+constexpr int kMaxProfileLds = kMaxProfile;
 
-__global__ void __launch_bounds__(256) stages_lds_kernel(const FfaPeriod* __restrict__ per, float* __restrict__ arena,
-                                                         int maxp_lds) {
+// 1024 threads = 16 rows x 64 bin lanes: thread (r, c) owns row r, bins
+// c, c+64, ...; no per-element division, every thread busy whatever P is.
+__global__ void __launch_bounds__(1024) stages_lds_kernel(const FfaPeriod* __restrict__ per, float* __restrict__ arena,
+                                                          int maxp_lds) {
   __shared__ float buf[2][kLdsFloats];
   const FfaPeriod pp = per[blockIdx.y];
   const int L = pp.log2m2 < kLdsLog2 ? pp.log2m2 : kLdsLog2;
   const int rows = 1 << L;
   const int P = pp.p;
   if (P > maxp_lds || L == 0) return;
+  const int r = threadIdx.x >> 6, c = threadIdx.x & 63;
+  const bool live = r < rows;
   for (int blk = blockIdx.x; blk * rows < pp.m2; blk += gridDim.x) {
     float* g = arena + pp.offset + static_cast<uint64_t>(blk) * rows * P;
-    for (int e = threadIdx.x; e < rows * P; e += blockDim.x) buf[0][e] = g[e];
+    if (live)
+      for (int b = c; b < P; b += 64) buf[0][r * P + b] = g[r * P + b];
     __syncthreads();
     int cur = 0;
     for (int st = 0; st < L; ++st) {
       const int m = 2 << st, h = m >> 1;
-      const float* src = buf[cur];
-      float* dst = buf[cur ^ 1];
-      for (int e = threadIdx.x; e < rows * P; e += blockDim.x) {
-        const int s = e / P, b = e - s * P;
-        const int base = (s / m) * m, so = s - base;
+      if (live) {
+        const float* src = buf[cur];
+        float* dst = buf[cur ^ 1];
+        const int base = r & ~(m - 1), so = r & (m - 1);
         const int j = so >> 1, sh = ((so + 1) >> 1) % P;
-        int bt = b + sh;
-        bt -= (bt >= P) ? P : 0;
-        dst[e] = src[(base + j) * P + b] + src[(base + h + j) * P + bt];
+        const float* hrow = src + (base + j) * P;
+        const float* trow = src + (base + h + j) * P;
+        for (int b = c; b < P; b += 64) {
+          int bt = b + sh;
+          bt -= (bt >= P) ? P : 0;
+          dst[r * P + b] = hrow[b] + trow[bt];
+        }
       }
       __syncthreads();
       cur ^= 1;
     }
-    for (int e = threadIdx.x; e < rows * P; e += blockDim.x) g[e] = buf[cur][e];
+    if (live)
+      for (int b = c; b < P; b += 64) g[r * P + b] = buf[cur][r * P + b];
     __syncthreads();
   }
 }
 
-// One global stage (ping-pong between in and out) for periods with
-// stage < log2 M2.  blockIdx.y = period, x strides the rows.
-__global__ void __launch_bounds__(256) stage_kernel(const FfaPeriod* __restrict__ per, const float* __restrict__ in,
-                                                    float* __restrict__ out, int stage) {
+// One global ping-pong pass covering stages st and st+1 (radix 4: rows
+// i, q+i, 2q+i, 3q+i of a 4q block -> rows 4i..4i+3, q = 2^st), or stage st
+// alone when it is the period's last (radix 2).  Sums are formed in the
+// radix-2 order, (X0 + X1[+a]) + (X2[+c] + X3[+d]).  The group's input rows
+// are staged in LDS and read back with the circular shifts.
+__global__ void __launch_bounds__(256) pass_kernel(const FfaPeriod* __restrict__ per, const float* __restrict__ in,
+                                                   float* __restrict__ out, int st) {
+  __shared__ float rows[4][kMaxProfileLds];
   const FfaPeriod pp = per[blockIdx.y];
-  if (stage >= pp.log2m2) return;
+  if (st >= pp.log2m2) return;
   const int P = pp.p;
-  const int m = 2 << stage, h = m >> 1;
+  const bool r4 = st + 1 < pp.log2m2;
+  const int q = 1 << st;
+  const int ngroups = r4 ? pp.m2 >> 2 : pp.m2 >> 1;
   const float* src = in + pp.offset;
   float* dst = out + pp.offset;
-  for (int s = blockIdx.x; s < pp.m2; s += gridDim.x) {
-    const int base = (s / m) * m, so = s - base;
-    const int j = so >> 1, sh = ((so + 1) >> 1) % P;  // M2/2 may exceed P
-    const float* hrow = src + static_cast<uint64_t>(base + j) * P;
-    const float* trow = src + static_cast<uint64_t>(base + h + j) * P;
-    float* orow = dst + static_cast<uint64_t>(s) * P;
-    for (int b = threadIdx.x; b < P; b += blockDim.x) {
-      int bt = b + sh;
-      bt -= (bt >= P) ? P : 0;
-      orow[b] = hrow[b] + trow[bt];
+  for (int g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    if (r4) {
+      const int blk = g >> st, i = g & (q - 1);
+      const int base = blk * 4 * q;
+      for (int k = 0; k < 4; ++k) {
+        const float* rsrc = src + static_cast<uint64_t>(base + k * q + i) * P;
+        for (int b = threadIdx.x; b < P; b += blockDim.x) rows[k][b] = rsrc[b];
+      }
+      __syncthreads();
+      // out[4i+u][b] = (X0[b] + X1[b+a_u]) + (X2[b+c_u] + X3[b+d_u])
+      const int a0 = i % P, a1 = (i + 1) % P;
+      const int c0 = (2 * i) % P, c1 = (2 * i + 1) % P, c2 = (2 * i + 2) % P;
+      const int d0 = (3 * i) % P, d1 = (3 * i + 1) % P, d2 = (3 * i + 2) % P, d3 = (3 * i + 3) % P;
+      auto wrap = [P](int x) { return x >= P ? x - P : x; };
+      float* o = dst + static_cast<uint64_t>(base + 4 * i) * P;
+      for (int b = threadIdx.x; b < P; b += blockDim.x) {
+        const float x0 = rows[0][b];
+        const float l0 = x0 + rows[1][wrap(b + a0)], l1 = x0 + rows[1][wrap(b + a1)];
+        o[b] = l0 + (rows[2][wrap(b + c0)] + rows[3][wrap(b + d0)]);
+        o[P + b] = l0 + (rows[2][wrap(b + c1)] + rows[3][wrap(b + d1)]);
+        o[2 * P + b] = l1 + (rows[2][wrap(b + c1)] + rows[3][wrap(b + d2)]);
+        o[3 * P + b] = l1 + (rows[2][wrap(b + c2)] + rows[3][wrap(b + d3)]);
+      }
+      __syncthreads();
+    } else {
+      const int blk = g >> st, j = g & (q - 1);
+      const int base = blk * 2 * q;
+      const float* hrow = src + static_cast<uint64_t>(base + j) * P;
+      const float* trow = src + static_cast<uint64_t>(base + q + j) * P;
+      const int s0 = j % P, s1 = (j + 1) % P;
+      float* o = dst + static_cast<uint64_t>(base + 2 * j) * P;
+      for (int b = threadIdx.x; b < P; b += blockDim.x) {
+        const float hv = hrow[b];
+        int t0 = b + s0, t1 = b + s1;
+        t0 -= t0 >= P ? P : 0;
+        t1 -= t1 >= P ? P : 0;
+        o[b] = hv + trow[t0];
+        o[P + b] = hv + trow[t1];
+      }
     }
   }
 }
 
 // One wavefront per profile: circular prefix sums, boxcar S/N ladder.
-constexpr int kMaxProfile = 2048;
 
 __global__ void __launch_bounds__(256) snr_kernel(const FfaPeriod* __restrict__ per, const float* __restrict__ a0,
                                                   const float* __restrict__ a1, int lds_stages, FfaSnrParams sp,
@@ -173,29 +232,28 @@ __global__ void __launch_bounds__(256) snr_kernel(const FfaPeriod* __restrict__ 
   const int s = active ? s0 : pp.m2 - 1;
   const int P = pp.p;
   // the result sits in a1 after an odd number of global ping-pong stages
-  const int gstages = pp.log2m2 - (pp.log2m2 < lds_stages ? pp.log2m2 : lds_stages);
-  const float* prof = ((gstages & 1) ? a1 : a0) + pp.offset + static_cast<uint64_t>(s) * P;
+  const float* prof = (ffa_result_in_second(pp, lds_stages) ? a1 : a0) + pp.offset + static_cast<uint64_t>(s) * P;
   float* C = pre[wave];
   // contiguous chunk per lane, exclusive scan of chunk sums across the wave
-  const int chunk = (P + 63) / 64;
-  const int b0 = lane * chunk;
-  float part = 0.f;
-  for (int b = b0; b < b0 + chunk && b < P; ++b) part += prof[b];
-  float incl = part;
-#pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const float v = __shfl_up(incl, off, 64);
-    if (lane >= off) incl += v;
-  }
-  float run = incl - part;
+  // prefix sums over the profile viewed as rows of 64: coalesced loads, a
+  // 64-lane inclusive scan per row plus the running carry (conflict-free LDS)
   if (lane == 0) C[0] = 0.f;
-  for (int b = b0; b < b0 + chunk && b < P; ++b) {
-    run += prof[b];
-    C[b + 1] = run;
+  float carry = 0.f;
+  for (int b0 = 0; b0 < P; b0 += 64) {
+    const int b = b0 + lane;
+    float v = b < P ? prof[b] : 0.f;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const float u = __shfl_up(v, off, 64);
+      if (lane >= off) v += u;
+    }
+    if (b < P) C[b + 1] = carry + v;
+    carry += __shfl(v, 63, 64);
   }
   __syncthreads();  // prefix sums are wave-local; all four waves reach this barrier
   const float total = C[P];
   const float var = static_cast<float>(pp.m) * sp.var_per_bin;
+  // per-lane best over (width, phase), one wave reduction at the end
   float best = -1e30f;
   int best_w = 0;
   for (int wi = 0; wi < sp.nwidths; ++wi) {
@@ -207,12 +265,19 @@ __global__ void __launch_bounds__(256) snr_kernel(const FfaPeriod* __restrict__ 
       const float sum = e <= P ? C[e] - C[ph] : total - C[ph] + C[e - P];
       mx = fmaxf(mx, sum);
     }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
     const float snr = mx * rsqrtf(static_cast<float>(w) * var);
     if (snr > best) {
       best = snr;
       best_w = w;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float ob = __shfl_xor(best, off, 64);
+    const int ow = __shfl_xor(best_w, off, 64);
+    if (ob > best || (ob == best && ow < best_w)) {  // ties: narrowest width (deterministic)
+      best = ob;
+      best_w = ow;
     }
   }
   if (lane == 0 && active) {
@@ -226,11 +291,17 @@ __global__ void __launch_bounds__(256) snr_kernel(const FfaPeriod* __restrict__ 
 
 }  // namespace
 
-void ffa_detrend(const uint8_t* in, uint64_t n, uint64_t window, float* block_means, float* out, hipStream_t s) {
+void ffa_detrend(const uint8_t* in, uint64_t n, uint64_t window, unsigned long long* sums, float* block_means,
+                 float* out, hipStream_t s) {
   PSOUP_CHECK(n > 0 && window > 0, "ffa_detrend: empty input");
   const uint64_t nblk = (n + window - 1) / window;
-  PSOUP_CHECK(nblk < (1ull << 31), "ffa_detrend: too many blocks");
-  block_means_kernel<<<static_cast<unsigned>(nblk), 256, 0, s>>>(in, n, window, block_means);
+  PSOUP_CHECK(nblk < 65536, "ffa_detrend: too many trend blocks");
+  PSOUP_HIP_CHECK(hipMemsetAsync(sums, 0, nblk * sizeof(unsigned long long), s));
+  const unsigned splits = dev::grid_for(window, 256 * 16, 256);
+  block_sums_kernel<<<dim3(splits, static_cast<unsigned>(nblk)), 256, 0, s>>>(in, n, window, sums);
+  post_launch_check("ffa block_sums_kernel", s);
+  block_means_kernel<<<dev::grid_for(nblk, 256, 64), 256, 0, s>>>(sums, n, window, static_cast<int>(nblk),
+                                                                 block_means);
   post_launch_check("ffa block_means_kernel", s);
   detrend_kernel<<<dev::grid_for(n, 256, 4096), 256, 0, s>>>(in, n, window, block_means, static_cast<int>(nblk), out);
   post_launch_check("ffa detrend_kernel", s);
@@ -257,15 +328,18 @@ void ffa_transform(const float* ds, const FfaPeriod* d_periods, int nper, int ma
   int first = 0;
   if (ffa_uses_lds(max_p)) {
     const int nb = (max_m2 + kLdsRows - 1) / kLdsRows;
-    stages_lds_kernel<<<dim3(static_cast<unsigned>(nb < 4096 ? nb : 4096), nper), 256, 0, s>>>(d_periods, arena0,
-                                                                                                kLdsFloats / kLdsRows);
+    stages_lds_kernel<<<dim3(static_cast<unsigned>(nb < 4096 ? nb : 4096), nper), 1024, 0, s>>>(d_periods, arena0,
+                                                                                                 kLdsFloats / kLdsRows);
     post_launch_check("ffa stages_lds_kernel", s);
     first = kLdsLog2;
   }
   float* bufs[2] = {arena0, arena1};
-  for (int st = first, k = 0; st < max_log2m2; ++st, ++k)
-    stage_kernel<<<dim3(gx, nper), 256, 0, s>>>(d_periods, bufs[k & 1], bufs[(k + 1) & 1], st);
-  if (max_log2m2 > first) post_launch_check("ffa stage_kernel", s);
+  // radix-4 passes (two stages each); a period with one stage left does it
+  // as a radix-2 group in the same pass
+  const unsigned gp = static_cast<unsigned>(std::max(1, std::min(max_m2 / 2, 4096)));
+  for (int st = first, k = 0; st < max_log2m2; st += 2, ++k)
+    pass_kernel<<<dim3(gp, nper), 256, 0, s>>>(d_periods, bufs[k & 1], bufs[(k + 1) & 1], st);
+  if (max_log2m2 > first) post_launch_check("ffa pass_kernel", s);
 }
 
 void ffa_snr(const FfaPeriod* d_periods, int nper, int max_m2, int max_p, const float* arena0, const float* arena1,

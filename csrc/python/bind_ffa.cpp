@@ -184,8 +184,7 @@ void bind_ffa(py::module_& m) {
         const bool lds = kern::ffa_uses_lds(max_p);
         py::list out;
         for (const auto& fp : tab) {
-          const int lds_st = lds ? std::min(fp.log2m2, 4) : 0;
-          const bool in1 = ((fp.log2m2 - lds_st) & 1) != 0;
+          const bool in1 = kern::ffa_result_in_second(fp, lds ? 4 : 0);
           const float* src = (in1 ? h1.data() : h0.data()) + fp.offset;
           py::array_t<float> plane({fp.m2, fp.p});
           std::copy(src, src + static_cast<size_t>(fp.m2) * fp.p, plane.mutable_data());

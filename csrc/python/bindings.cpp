@@ -544,8 +544,10 @@ PYBIND11_MODULE(_C, m) {
   k.def("ffa_downsample", [](uintptr_t x, uint64_t n, double f, uintptr_t out, uint64_t nout, uintptr_t s) {
     kern::ffa_downsample(P<const float>(x), n, f, P<float>(out), nout, S(s));
   });
-  k.def("ffa_detrend", [](uintptr_t in, uint64_t n, uint64_t window, uintptr_t means, uintptr_t out, uintptr_t s) {
-    kern::ffa_detrend(P<const uint8_t>(in), n, window, P<float>(means), P<float>(out), S(s));
+  k.def("ffa_detrend", [](uintptr_t in, uint64_t n, uint64_t window, uintptr_t sums, uintptr_t means, uintptr_t out,
+                          uintptr_t s) {
+    kern::ffa_detrend(P<const uint8_t>(in), n, window, P<unsigned long long>(sums), P<float>(means), P<float>(out),
+                      S(s));
   });
   k.def("fold_shift_table", [](uintptr_t table, int nbins, int nints, uintptr_t s) {
     kern::fold_shift_table(P<float2>(table), nbins, nints, S(s));

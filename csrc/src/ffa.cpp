@@ -135,10 +135,10 @@ FfaEngine::FfaEngine(const FfaParams& p, uint64_t nsamps, hipStream_t stream) : 
   uint64_t window = static_cast<uint64_t>(std::ceil((p_.detrend_s > 0 ? p_.detrend_s : 3.0 * p_.p_end) / p_.tsamp));
   window = std::min<uint64_t>(std::max<uint64_t>(window, 64), n_);
   means_.resize((n_ + window - 1) / window);
+  sums_.resize((n_ + window - 1) / window);
   partials_.resize(2 * 1024);
   stats_.resize(4);
-  d_count_.resize(1);
-  d_peaks_.resize(cap_);
+  cap_ = 1u << 14;
   const std::vector<int> w = ffa_widths(ffa_base_bins(p_));
   snr_.nwidths = static_cast<int32_t>(w.size());
   for (size_t i = 0; i < w.size(); ++i) snr_.widths[i] = w[i];
@@ -151,37 +151,54 @@ FfaCandidateList FfaEngine::search(const uint8_t* d_trial, float dm, int dm_idx)
   hipStream_t s = stream_;
   uint64_t window = static_cast<uint64_t>(std::ceil((p_.detrend_s > 0 ? p_.detrend_s : 3.0 * p_.p_end) / p_.tsamp));
   window = std::min<uint64_t>(std::max<uint64_t>(window, 64), n_);
-  kern::ffa_detrend(d_trial, n_, window, means_.data(), x_.data(), s);
+  kern::ffa_detrend(d_trial, n_, window, sums_.data(), means_.data(), x_.data(), s);
   kern::f32_stats(x_.data(), n_, partials_.data(), 1024, stats_.data(), s);
   kern::normalise_dev(x_.data(), n_, stats_.data(), 1.0f, s);
+  // Every chunk of every octave is issued back to back (one S/N record
+  // buffer and counter per chunk); the host synchronises once per DM.  A
+  // record-buffer overflow (rare) grows the buffers and reruns the DM.
+  size_t nchunks = 0;
+  for (const auto& oc : plan_) nchunks += oc.chunks.size();
+  std::vector<uint32_t> counts(nchunks);
+  for (int attempt = 0; attempt < 3; ++attempt) {
+    if (d_peaks_.size() < nchunks * cap_) d_peaks_.resize(nchunks * cap_);
+    if (d_count_.size() < nchunks) d_count_.resize(nchunks);
+    PSOUP_HIP_CHECK(hipMemsetAsync(d_count_.data(), 0, nchunks * sizeof(uint32_t), s));
+    size_t t = 0;
+    for (size_t o = 0; o < plan_.size(); ++o) {
+      const FfaOctave& oc = plan_[o];
+      kern::ffa_downsample(x_.data(), n_, oc.factor, ds_.data(), oc.nds, s);
+      kern::FfaSnrParams sp = snr_;
+      sp.var_per_bin = static_cast<float>(oc.factor);
+      for (const FfaChunk& ch : oc.chunks) {
+        const kern::FfaPeriod* dper = tables_[t].data();
+        const int nper = static_cast<int>(ch.periods.size());
+        kern::ffa_transform(ds_.data(), dper, nper, ch.max_m2, ch.max_log2m2, ch.max_p, a0_.data(), a1_.data(), s);
+        kern::ffa_snr(dper, nper, ch.max_m2, ch.max_p, a0_.data(), a1_.data(), sp, d_peaks_.data() + t * cap_,
+                      d_count_.data() + t, cap_, nullptr, s);
+        ++t;
+      }
+    }
+    PSOUP_HIP_CHECK(hipMemcpyAsync(counts.data(), d_count_.data(), nchunks * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    PSOUP_HIP_CHECK(hipStreamSynchronize(s));
+    const uint32_t mx = nchunks ? *std::max_element(counts.begin(), counts.end()) : 0;
+    if (mx <= cap_) break;
+    PSOUP_CHECK(attempt < 2, "ffa: peak buffer overflow persists");
+    cap_ = mx + mx / 4;
+  }
   FfaCandidateList raw;
   size_t t = 0;
   for (size_t o = 0; o < plan_.size(); ++o) {
     const FfaOctave& oc = plan_[o];
-    kern::ffa_downsample(x_.data(), n_, oc.factor, ds_.data(), oc.nds, s);
-    kern::FfaSnrParams sp = snr_;
-    sp.var_per_bin = static_cast<float>(oc.factor);
+    const double bin_s = oc.factor * p_.tsamp;
     for (const FfaChunk& ch : oc.chunks) {
-      const kern::FfaPeriod* dper = tables_[t++].data();
-      const int nper = static_cast<int>(ch.periods.size());
-      kern::ffa_transform(ds_.data(), dper, nper, ch.max_m2, ch.max_log2m2, ch.max_p, a0_.data(), a1_.data(), s);
-      uint32_t cnt = 0;
-      for (int attempt = 0; attempt < 2; ++attempt) {
-        PSOUP_HIP_CHECK(hipMemsetAsync(d_count_.data(), 0, sizeof(uint32_t), s));
-        kern::ffa_snr(dper, nper, ch.max_m2, ch.max_p, a0_.data(), a1_.data(), sp, d_peaks_.data(), d_count_.data(),
-                      cap_, nullptr, s);
-        PSOUP_HIP_CHECK(hipMemcpyAsync(&cnt, d_count_.data(), sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        PSOUP_HIP_CHECK(hipStreamSynchronize(s));
-        if (cnt <= cap_) break;
-        cap_ = cnt + cnt / 4;  // grow and recompute this chunk's S/N pass
-        d_peaks_.resize(cap_);
-      }
+      const uint32_t cnt = counts[t];
       nprof_ += ch.nprof;
       npeaks_ += cnt;
       h_peaks_.resize(cnt);
       if (cnt)
-        PSOUP_HIP_CHECK(hipMemcpy(h_peaks_.data(), d_peaks_.data(), cnt * sizeof(kern::FfaPeak), hipMemcpyDeviceToHost));
-      const double bin_s = oc.factor * p_.tsamp;
+        PSOUP_HIP_CHECK(hipMemcpy(h_peaks_.data(), d_peaks_.data() + t * cap_, cnt * sizeof(kern::FfaPeak),
+                                  hipMemcpyDeviceToHost));
       for (const auto& pk : h_peaks_) {
         const kern::FfaPeriod& fp = ch.periods[static_cast<size_t>(pk.period_idx)];
         const double pbins = fp.m2 > 1 ? fp.p + static_cast<double>(pk.drift) / (fp.m2 - 1) : fp.p;
@@ -195,6 +212,7 @@ FfaCandidateList FfaEngine::search(const uint8_t* d_trial, float dm, int dm_idx)
         c.octave = static_cast<int>(o);
         raw.push_back(c);
       }
+      ++t;
     }
   }
   return ffa_cluster(std::move(raw), p_.cluster_tol / tobs());

@@ -148,7 +148,9 @@ def test_ffa_detrend_removes_linear_trend():
     xt = torch.from_numpy(u8).cuda()
     out = torch.empty(n, device="cuda")
     means = torch.empty((n + w - 1) // w, device="cuda")
-    C.kernels.ffa_detrend(xt.data_ptr(), n, w, means.data_ptr(), out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    sums = torch.empty((n + w - 1) // w, dtype=torch.int64, device="cuda")
+    C.kernels.ffa_detrend(xt.data_ptr(), n, w, sums.data_ptr(), means.data_ptr(), out.data_ptr(),
+                          torch.cuda.current_stream().cuda_stream)
     exp_means = np.array([u8[i:i + w].mean() for i in range(0, n, w)])
     np.testing.assert_allclose(means.cpu().numpy(), exp_means, rtol=1e-5)
     y = out.cpu().numpy()
