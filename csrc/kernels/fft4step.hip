@@ -243,6 +243,56 @@ __device__ __forceinline__ void store_row(float2* __restrict__ dst, const Vec<CP
   }
 }
 
+// Tiled-layout store of a workgroup's 8 transforms x L points, staged
+// through LDS so that every global store instruction writes 4 KiB of
+// contiguous memory (the workgroup's output is one contiguous 8 L complex
+// region: [L/8][8 transforms][8]).  Direct per-lane stores of that layout
+// write 64-byte pieces 512 bytes apart and run at ~60% of the contiguous
+// write bandwidth.  Two halves of 4 L complex (64 KiB at L = 2048) fit the
+// 72 KiB LDS budget; one complex of padding per 64 spreads the 8-byte LDS
+// writes over the banks.  keep_oct > 0 skips the octets outside
+// [0, keep_oct) u [L/8 - keep_oct, L/8) (see the pruned pass-B stores).
+template <int L>
+__device__ __forceinline__ void store_tiled_staged(const Vec<8>& v, float* __restrict__ lds, int t,
+                                                   float2* __restrict__ region, uint32_t keep_oct, bool nt) {
+  constexpr int T = L / kPts;
+  constexpr int PARTS = L > 1024 ? L / 1024 : 1;  // 64 KiB (8192 complex) per part
+  constexpr int QP = kPts / PARTS;                 // q values per part
+  constexpr int PART = 8 * L / PARTS;              // complex per part
+  static_assert((PART + PART / 64) * 2 <= kLdsBudget / 4, "staging does not fit the LDS budget");
+  float2* buf = reinterpret_cast<float2*>(lds);
+  auto pad = [](int x) { return x + (x >> 6); };
+  const uint32_t hi_oct = L / 8 - keep_oct;
+#pragma unroll
+  for (int h = 0; h < PARTS; ++h) {
+    __syncthreads();  // LDS is free (FFT exchanges / previous part done)
+#pragma unroll
+    for (int qq = 0; qq < QP; ++qq) {
+      const int k = t + (QP * h + qq) * T;  // point index of this thread's values
+      const int pos = (k >> 3) * 64 + (k & 7) - h * PART;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) buf[pad(pos + c * 8)] = v[c][QP * h + qq];
+    }
+    __syncthreads();
+    float2* out = region + static_cast<uint64_t>(h) * PART;
+#pragma unroll
+    for (int j = 0; j < PART / (2 * T); ++j) {
+      const int idx = 2 * (j * T + t);  // two complex per lane (16 bytes)
+      if (keep_oct != 0) {
+        const uint32_t oct = static_cast<uint32_t>((h * PART + idx) >> 6);
+        if (oct >= keep_oct && oct < hi_oct) continue;
+      }
+      const float2 a = buf[pad(idx)], b = buf[pad(idx + 1)];
+      const f4v val = {a.x, a.y, b.x, b.y};
+      f4v* d = reinterpret_cast<f4v*>(out + idx);
+      if (nt)
+        __builtin_nontemporal_store(val, d);
+      else
+        *d = val;
+    }
+  }
+}
+
 // XCD-aware block order (remap = true): logical block
 // b' = (b % 8) * (nblocks / 8) + b / 8, so each XCD's share of the grid is one
 // contiguous logical range (nblocks is a multiple of 8).
@@ -273,6 +323,7 @@ __global__ void __launch_bounds__(256) fft4_pad_input_kernel(const float* __rest
 // cover 512 contiguous bytes.
 // bit 3 = tiled X: X_t[k2/8][k1/8][k2%8][k1%8] (read by r2c_interbin_normalise_tiled).
 constexpr int kModeBlocked = 1, kModeTiming = 2, kModeTileY = 4, kModeTileX = 8;
+constexpr int kModeStaged = 16;  // LDS-staged contiguous stores of the tiled layouts
 
 // Pass A.  Logical block = column block * K + trial (trial fastest).
 template <int L, int CPT, int SUB, int MODE>
@@ -332,6 +383,23 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
   const uint32_t mask = static_cast<uint32_t>(N1) * L - 1;
   float2* yk = Y + static_cast<uint64_t>(k) * g.ystride;
   const bool nt = flags & kFft4NtStores;
+  if constexpr (kTileY && CPT == 8 && SUB == 1 && (MODE & kModeStaged) != 0) {
+    {
+#pragma unroll
+      for (int q = 0; q < kPts; ++q) {
+        const uint32_t k2 = t + q * T;
+        float2 w = twiddle_M((static_cast<uint32_t>(c0) * k2) & mask, tab + to.lo, tab + to.hi);
+        const float2 step = twiddle_M(k2, tab + to.lo, tab + to.hi);
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) {
+          v[c][q] = cmul(v[c][q], w);
+          w = cmul(w, step);
+        }
+      }
+      store_tiled_staged<L>(v, lds, t, yk + static_cast<uint64_t>(c0) * g.n2, 0, nt);
+      return;
+    }
+  }
 #pragma unroll
   for (int q = 0; q < kPts; ++q) {
     const uint32_t k2 = t + q * T;
@@ -405,6 +473,12 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
     fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n1);
   float2* xk = X + static_cast<uint64_t>(k) * g.xstride;
   const bool nt = flags & kFft4NtStores;
+  if constexpr ((MODE & kModeTileX) != 0 && CPT == 8 && SUB == 1 && (MODE & kModeStaged) != 0) {
+    {
+      store_tiled_staged<L>(v, lds, t, xk + static_cast<uint64_t>(r0 >> 3) * (8 * L), keep_oct, nt);
+      return;
+    }
+  }
   if constexpr ((MODE & kModeTileX) != 0) {
     // keep_oct > 0: only k1 octets [0, keep_oct) and [L/8 - keep_oct, L/8)
     // are ever read (bins below the search limit and their mirrors); a wave's
@@ -541,6 +615,8 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   const dim3 grid(static_cast<unsigned>(nblocks));
   if ((f & kFft4Blocked) && (f & kFft4TileY) && (f & kFft4Sub2) && !(f & kTimingFlags))
     launch_colpass<4, 2, kModeBlocked | kModeTileY>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  else if ((f & kFft4Blocked) && (f & kFft4TileY) && (f & kFft4StagedStores) && !(f & kTimingFlags))
+    launch_colpass<8, 1, kModeBlocked | kModeTileY | kModeStaged>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   else if ((f & kFft4Blocked) && (f & kFft4TileY) && !(f & kTimingFlags))
     launch_colpass<8, 1, kModeBlocked | kModeTileY>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   else if ((f & kFft4Blocked) && (f & kFft4Ch4) && !(f & kTimingFlags))  // Y stays 8-wide; only pass B narrows
@@ -575,6 +651,9 @@ void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const fl
     }
     if (f & kFft4Sub2)
       launch_rowpass<4, 2, kModeBlocked | kModeTileY | kModeTileX>(Y, X, K, g, tables, grid, f, s, keep);
+    else if (f & kFft4StagedStores)
+      launch_rowpass<8, 1, kModeBlocked | kModeTileY | kModeTileX | kModeStaged>(Y, X, K, g, tables, grid, f, s,
+                                                                                   keep);
     else
       launch_rowpass<8, 1, kModeBlocked | kModeTileY | kModeTileX>(Y, X, K, g, tables, grid, f, s, keep);
   }
