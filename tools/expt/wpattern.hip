@@ -3,6 +3,7 @@
 // P[k1*n2 + k2] for all k1: 28-32 byte chunks 8 KB apart) vs contiguous writes.
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 constexpr int N1 = 2048, N2 = 2048;
@@ -45,8 +46,21 @@ __global__ void __launch_bounds__(512) wchunk(float* P, int K, int nb) {
   }
 }
 
-int main() {
-  const int K = 32;
+__global__ void __launch_bounds__(256) rcontig(const float4* __restrict__ P, size_t n4, float* out) {
+  float4 acc = make_float4(0, 0, 0, 0);
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256) {
+    float4 v = P[i];
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  if (acc.x + acc.y + acc.z + acc.w == 1234.5f) out[0] = acc.x;
+}
+__global__ void __launch_bounds__(256) wcontig4(float4* __restrict__ P, size_t n4) {
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256)
+    P[i] = make_float4(1.f, 2.f, 3.f, (float)i);
+}
+
+int main(int argc, char** argv) {
+  const int K = argc > 1 ? atoi(argv[1]) : 32;
   float* P;
   const size_t per = (size_t)N1 * N2 + 64;
   hipMalloc(&P, per * K * sizeof(float));
@@ -65,6 +79,14 @@ int main() {
     const double us = ms * 1e3 / 10 / K;
     printf("%-28s %8.2f us/trial  %7.0f GB/s\n", name, us, N1 * (double)N2 * 4 / (us * 1e-6) / 1e9);
   };
+  {
+    const size_t n4 = per * K / 4;
+    float* o;
+    hipMalloc(&o, 64);
+    time("read-only float4 (grid 8192)", [&] { rcontig<<<8192, 256>>>((const float4*)P, n4, o); });
+    time("write-only float4 (grid 8192)", [&] { wcontig4<<<8192, 256>>>((float4*)P, n4); });
+    time("write-only float4 (grid 2048)", [&] { wcontig4<<<2048, 256>>>((float4*)P, n4); });
+  }
   const int nbc = (N1 * N2) / (16 * N1);
   time("contiguous", [&] { wcontig<<<nbc * K, 512>>>(P, K); });
   const int nb7 = (N2 / 2 + 6) / 7;
