@@ -16,6 +16,11 @@
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <condition_variable>
+#include <exception>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -287,5 +292,30 @@ inline uint64_t prev_power_of_two(uint64_t val) {
   while (n * 2 < val) n *= 2;
   return n;
 }
+
+// Small fixed-size host worker pool for data-parallel host stages (peak
+// clustering / harmonic distillation of a trial batch).  parallel_for(n, fn)
+// runs fn(i) for i in [0, n) over the workers plus the calling thread and
+// returns when all are done; exceptions are rethrown in the caller.
+class HostPool {
+ public:
+  explicit HostPool(int workers);
+  ~HostPool();
+  HostPool(const HostPool&) = delete;
+  HostPool& operator=(const HostPool&) = delete;
+  int size() const { return static_cast<int>(threads_.size()) + 1; }
+  void parallel_for(int n, const std::function<void(int)>& fn);
+
+ private:
+  void loop();
+  std::vector<std::thread> threads_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(int)>* job_ = nullptr;
+  int n_ = 0, next_ = 0, active_ = 0;
+  uint64_t generation_ = 0;
+  bool stop_ = false;
+  std::exception_ptr err_;
+};
 
 }  // namespace psoup

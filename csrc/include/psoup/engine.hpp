@@ -99,6 +99,7 @@ struct SearchParams {
   std::vector<float> zap_freqs, zap_widths;
   int accel_batch = 0;          // 0 = auto
   int sub_batch = -1;           // fused-FFT trials per sub-batch on alternating streams (0 = off, -1 = auto)
+  int host_threads = -1;        // host workers clustering/distilling peak-heavy batches (-1 = auto, 0/1 = serial)
   size_t batch_bytes = 6ull << 30;  // auto-batch HBM budget (64 trials of 2^23)
   int min_gap = 30;
   // Acceleration-trial FFT path: 0 = rocFFT R2C of N points; 1 = rocFFT C2C
@@ -215,6 +216,7 @@ class SearchEngine {
   // host scratch
   std::vector<uint32_t> seg_count_, seg_off_;
   std::vector<kern::PeakRecord> sorted_;
+  std::unique_ptr<HostPool> pool_;  // null: serial host processing
 };
 
 // Zap mask for an FFT size (birdiezapper.hpp / kernels.cu:1036-1069 semantics).

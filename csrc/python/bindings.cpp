@@ -621,6 +621,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("fft_size", &SearchParams::fft_size)
       .def_readwrite("tsamp", &SearchParams::tsamp)
       .def_readwrite("min_snr", &SearchParams::min_snr)
+      .def_readwrite("host_threads", &SearchParams::host_threads)
       .def_readwrite("min_freq", &SearchParams::min_freq)
       .def_readwrite("max_freq", &SearchParams::max_freq)
       .def_readwrite("nharmonics", &SearchParams::nharmonics)

@@ -106,4 +106,74 @@ int driver_version() {
   return v;
 }
 
+HostPool::HostPool(int workers) {
+  for (int i = 0; i < workers; ++i) threads_.emplace_back([this] { loop(); });
+}
+
+HostPool::~HostPool() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : threads_) t.join();
+}
+
+void HostPool::loop() {
+  uint64_t seen = 0;
+  std::unique_lock<std::mutex> lk(mu_);
+  while (true) {
+    cv_.wait(lk, [&] { return stop_ || generation_ != seen; });
+    if (stop_) return;
+    seen = generation_;
+    ++active_;
+    while (next_ < n_) {
+      const int i = next_++;
+      lk.unlock();
+      try {
+        (*job_)(i);
+      } catch (...) {
+        lk.lock();
+        if (!err_) err_ = std::current_exception();
+        lk.unlock();
+      }
+      lk.lock();
+    }
+    if (--active_ == 0) done_cv_.notify_all();
+  }
+}
+
+void HostPool::parallel_for(int n, const std::function<void(int)>& fn) {
+  if (n <= 0) return;
+  if (threads_.empty() || n == 1) {
+    for (int i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  std::unique_lock<std::mutex> lk(mu_);
+  job_ = &fn;
+  n_ = n;
+  next_ = 0;
+  err_ = nullptr;
+  ++generation_;
+  ++active_;  // the caller works too
+  cv_.notify_all();
+  while (next_ < n_) {
+    const int i = next_++;
+    lk.unlock();
+    try {
+      fn(i);
+    } catch (...) {
+      lk.lock();
+      if (!err_) err_ = std::current_exception();
+      lk.unlock();
+    }
+    lk.lock();
+  }
+  --active_;
+  done_cv_.wait(lk, [&] { return active_ == 0; });
+  job_ = nullptr;
+  n_ = 0;
+  if (err_) std::rethrow_exception(err_);
+}
+
 }  // namespace psoup

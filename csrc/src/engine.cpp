@@ -1,5 +1,7 @@
 #include "psoup/engine.hpp"
 
+#include <thread>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
@@ -270,6 +272,9 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     s.h_count.resize(1);
   }
   grow_capacity(cap_);
+  int ht = p_.host_threads;
+  if (ht < 0) ht = static_cast<int>(std::min(4u, std::max(1u, std::thread::hardware_concurrency() / 4)));
+  if (ht > 1) pool_ = std::make_unique<HostPool>(ht - 1);
 }
 
 SearchEngine::~SearchEngine() {
@@ -379,34 +384,53 @@ void SearchEngine::process_slot(Slot& s, float dm, int dm_idx, const std::vector
     std::vector<uint32_t> fill(seg_off_.begin(), seg_off_.end() - 1);
     for (uint32_t i = 0; i < cnt; ++i) sorted_[fill[s.h_peaks[i].seg]++] = s.h_peaks[i];
   }
-  std::vector<int> idxs, pidx;
-  std::vector<float> snrs, psnr;
-  for (int k = 0; k < s.count; ++k) {
-    const float acc = accs[static_cast<size_t>(s.first + k)];
-    CandidateList trial;
-    for (int h = 0; h < L; ++h) {
-      const int seg = k * 8 + h;
-      const uint32_t a = seg_off_[seg], b = seg_off_[seg + 1];
-      if (a == b) continue;
-      std::sort(sorted_.begin() + a, sorted_.begin() + b,
-                [](const kern::PeakRecord& x, const kern::PeakRecord& y) { return x.idx < y.idx; });
-      idxs.resize(b - a);
-      snrs.resize(b - a);
-      for (uint32_t i = a; i < b; ++i) {
-        idxs[i - a] = sorted_[i].idx;
-        snrs[i - a] = sorted_[i].snr;
+  // Per-trial clustering + harmonic distillation.  Trials own disjoint
+  // segments of sorted_, so peak-heavy batches (RFI) are spread over the
+  // host pool; results are concatenated in trial order (deterministic).
+  auto trial_range = [&](int k0, int k1, CandidateList& dst) {
+    std::vector<int> idxs, pidx;
+    std::vector<float> snrs, psnr;
+    for (int k = k0; k < k1; ++k) {
+      const float acc = accs[static_cast<size_t>(s.first + k)];
+      CandidateList trial;
+      for (int h = 0; h < L; ++h) {
+        const int seg = k * 8 + h;
+        const uint32_t a = seg_off_[seg], b = seg_off_[seg + 1];
+        if (a == b) continue;
+        std::sort(sorted_.begin() + a, sorted_.begin() + b,
+                  [](const kern::PeakRecord& x, const kern::PeakRecord& y) { return x.idx < y.idx; });
+        idxs.resize(b - a);
+        snrs.resize(b - a);
+        for (uint32_t i = a; i < b; ++i) {
+          idxs[i - a] = sorted_[i].idx;
+          snrs[i - a] = sorted_[i].snr;
+        }
+        pidx.clear();
+        psnr.clear();
+        identify_unique_peaks(idxs.data(), snrs.data(), idxs.size(), p_.min_gap, pidx, psnr);
+        const double factor = bounds_[static_cast<size_t>(h)].factor;
+        for (size_t i = 0; i < pidx.size(); ++i)
+          trial.emplace_back(dm, dm_idx, acc, h, psnr[i], static_cast<float>(pidx[i] * factor));
       }
-      pidx.clear();
-      psnr.clear();
-      identify_unique_peaks(idxs.data(), snrs.data(), idxs.size(), p_.min_gap, pidx, psnr);
-      const double factor = bounds_[static_cast<size_t>(h)].factor;
-      for (size_t i = 0; i < pidx.size(); ++i)
-        trial.emplace_back(dm, dm_idx, acc, h, psnr[i], static_cast<float>(pidx[i] * factor));
+      if (!trial.empty()) {
+        CandidateList d = harm_.distill(std::move(trial));
+        for (auto& c : d) dst.push_back(std::move(c));
+      }
     }
-    if (!trial.empty()) {
-      CandidateList d = harm_.distill(std::move(trial));
-      for (auto& c : d) out.push_back(std::move(c));
-    }
+  };
+  constexpr uint32_t kParallelPeaks = 8192;  // below this the serial loop is cheaper
+  if (pool_ && cnt >= kParallelPeaks && s.count > 1) {
+    const int nparts = std::min(s.count, 4 * pool_->size());
+    std::vector<CandidateList> parts(static_cast<size_t>(nparts));
+    pool_->parallel_for(nparts, [&](int j) {
+      const int k0 = static_cast<int>(static_cast<int64_t>(s.count) * j / nparts);
+      const int k1 = static_cast<int>(static_cast<int64_t>(s.count) * (j + 1) / nparts);
+      trial_range(k0, k1, parts[static_cast<size_t>(j)]);
+    });
+    for (auto& part : parts)
+      for (auto& c : part) out.push_back(std::move(c));
+  } else {
+    trial_range(0, s.count, out);
   }
 }
 

@@ -11,6 +11,7 @@
 #include <functional>
 #include <iostream>
 #include <sstream>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
@@ -185,6 +186,32 @@ void t_threads_shared_readonly() {
   for (size_t c : counts) CHECK(c == counts[0] && c > 0);
 }
 
+// HostPool (engine host stages): every index runs exactly once per call,
+// repeated generations reuse the workers, exceptions reach the caller
+// (exercised under TSan by the sanitizer build).
+void t_host_pool() {
+  HostPool pool(5);
+  CHECK(pool.size() == 6);
+  for (int rep = 0; rep < 50; ++rep) {
+    const int n = 1 + (rep * 37) % 200;
+    std::vector<int> hits(static_cast<size_t>(n), 0);
+    pool.parallel_for(n, [&](int i) { hits[static_cast<size_t>(i)] += 1; });
+    for (int h : hits) CHECK(h == 1);
+  }
+  bool thrown = false;
+  try {
+    pool.parallel_for(64, [](int i) {
+      if (i == 17) throw std::runtime_error("boom");
+    });
+  } catch (const std::runtime_error&) {
+    thrown = true;
+  }
+  CHECK(thrown);
+  std::vector<int> again(10, 0);
+  pool.parallel_for(10, [&](int i) { again[static_cast<size_t>(i)] = i; });
+  for (int i = 0; i < 10; ++i) CHECK(again[static_cast<size_t>(i)] == i);
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -200,6 +227,7 @@ int main(int argc, char** argv) {
       {"sigproc_roundtrip", t_sigproc_roundtrip},
       {"peaks_and_bounds", t_peaks_and_bounds},
       {"threads_shared_readonly", t_threads_shared_readonly},
+      {"host_pool", t_host_pool},
   };
   for (auto& c : cases) {
     const int before = g_fail;

@@ -382,3 +382,26 @@ def test_harmonic_prethreshold_is_exact(nlev, thresh):
             sel = np.nonzero(L[starts[h]:ends[h]] > thresh)[0] + starts[h]
             exp |= {(k, h, int(i)) for i in sel}
     assert {r[:3] for r in runs[0]} == exp
+
+
+def test_parallel_host_distillation_is_deterministic(C):
+    """Peak-heavy batches (low threshold: tens of thousands of records) are
+    clustered/distilled on the host pool; candidates equal the serial path."""
+    rng = np.random.default_rng(21)
+    nsamps, n = 200000, 1 << 17
+    t = (np.arange(nsamps) * 0.00032) / 0.0731
+    trial = np.clip(rng.normal(128, 6, nsamps) + 9.0 * ((t % 1.0) < 0.03), 0, 255).astype(np.uint8)
+    tt = torch.from_numpy(trial).to(dev)
+    accs = [float(a) for a in np.linspace(-40, 40, 48)]
+    s = torch.cuda.current_stream().cuda_stream
+    runs = []
+    for ht in (1, 6):
+        p = C.SearchParams()
+        p.fft_size, p.tsamp, p.nharmonics, p.min_snr = n, 0.00032, 3, 2.5
+        p.host_threads = ht
+        eng = C.SearchEngine(p, s)
+        cands = eng.search_trial(tt.data_ptr(), nsamps, 5.0, 0, accs)
+        torch.cuda.synchronize()
+        assert eng.counters()["peaks"] > 8192 * 2  # the parallel branch is taken
+        runs.append([(c.acc, c.nh, c.snr, c.freq, len(c.assoc)) for c in cands])
+    assert runs[0] == runs[1] and len(runs[0]) > 0
