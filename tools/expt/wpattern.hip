@@ -59,6 +59,26 @@ __global__ void __launch_bounds__(256) wcontig4(float4* __restrict__ P, size_t n
     P[i] = make_float4(1.f, 2.f, 3.f, (float)i);
 }
 
+// write-only with occupancy limited by dynamic LDS (lds_bytes per WG)
+__global__ void __launch_bounds__(256) wocc(float4* __restrict__ P, size_t n4) {
+  extern __shared__ float pad[];
+  if (threadIdx.x == 1023) pad[0] = 0.f;  // never true; keeps the allocation
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n4; i += (size_t)gridDim.x * 256)
+    P[i] = make_float4(1.f, 2.f, 3.f, (float)i);
+}
+// same, but each thread writes 32 x 16 B in one burst at the end (FFT-like)
+__global__ void __launch_bounds__(256) wburst(float4* __restrict__ P, size_t n4) {
+  extern __shared__ float pad[];
+  if (threadIdx.x == 1023) pad[0] = 0.f;
+  const size_t per = 256 * 32;
+  const size_t nblk = n4 / per;
+  for (size_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+    float4* d = P + b * per;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) d[j * 256 + threadIdx.x] = make_float4(1.f, 2.f, 3.f, (float)j);
+  }
+}
+
 int main(int argc, char** argv) {
   const int K = argc > 1 ? atoi(argv[1]) : 32;
   float* P;
@@ -86,6 +106,17 @@ int main(int argc, char** argv) {
     time("read-only float4 (grid 8192)", [&] { rcontig<<<8192, 256>>>((const float4*)P, n4, o); });
     time("write-only float4 (grid 8192)", [&] { wcontig4<<<8192, 256>>>((float4*)P, n4); });
     time("write-only float4 (grid 2048)", [&] { wcontig4<<<2048, 256>>>((float4*)P, n4); });
+  }
+  {
+    const size_t n4 = per * K / 4;
+    for (int wgs : {1, 2, 4, 8}) {
+      const size_t lds = 160 * 1024 / wgs - 1024;
+      char name[64];
+      snprintf(name, sizeof(name), "write-only, %d WG/CU", wgs);
+      time(name, [&] { wocc<<<256 * wgs, 256, lds>>>((float4*)P, n4); });
+      snprintf(name, sizeof(name), "write burst, %d WG/CU", wgs);
+      time(name, [&] { wburst<<<256 * wgs, 256, lds>>>((float4*)P, n4); });
+    }
   }
   const int nbc = (N1 * N2) / (16 * N1);
   time("contiguous", [&] { wcontig<<<nbc * K, 512>>>(P, K); });
