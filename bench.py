@@ -53,6 +53,7 @@ def parse():
     p.add_argument("--fft-mode", type=int, default=2,
                    help="2: fused resample + four-step FFT; 1: rocFFT C2C(N/2) + fused r2c post; 0: rocFFT R2C")
     p.add_argument("--dedisp-kernel", default="mfma", choices=["mfma", "direct"])
+    p.add_argument("--fft4-flags", type=int, default=-1, help="fused-FFT kernel variant flags (tuning; -1 = default)")
     p.add_argument("--seed", type=int, default=1234)
     return p.parse_args()
 
@@ -69,6 +70,8 @@ def main() -> int:
         return 2
     ctx = pdist.init()
     dev = ctx.device
+    if a.fft4_flags >= 0:
+        _C.kernels.fft4_set_flags(a.fft4_flags)
     assert dev.type == "cuda", "bench.py needs a GPU"
 
     n = 1 << a.log2n

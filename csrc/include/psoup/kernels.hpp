@@ -185,6 +185,7 @@ enum Fft4Flags : int {
   kFft4GroupXcd = 8192,  // pass A: 8 trials x 2 adjacent column blocks per XCD group (needs K % 8 == 0)
   kFft4Sub2 = 16384,     // tiled paths: two thread groups x 4 transforms per workgroup (fewer VGPRs, 4 waves/SIMD)
   kFft4StagedStores = 32768,  // tiled paths: LDS-staged stores, 4 KiB contiguous per store instruction
+  kFft4UniformTw = 65536,     // pass A: four-step twiddles as per-thread x workgroup-uniform (SGPR) factors
 };
 void fft4_set_flags(int flags);
 int fft4_flags();

@@ -400,11 +400,36 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
       return;
     }
   }
+  // Four-step twiddles W^{(c0+c) k2}, k2 = t + qT: w0 = W^{c0 k2}, step =
+  // W^{k2}.  kFft4UniformTw: both split into a per-thread factor (W^{c0 t},
+  // W^t: one pair of table lookups) times a workgroup-uniform factor
+  // (W^{c0 q T}, W^{q T}: computed in lanes 0..7, read back with readlane
+  // into SGPRs) instead of four table lookups per q.
+  const bool utw = flags & kFft4UniformTw;
+  float2 bt0 = make_float2(1.f, 0.f), bts = make_float2(1.f, 0.f), u0 = bt0, us = bt0;
+  if (utw) {
+    bt0 = twiddle_M((static_cast<uint32_t>(c0) * static_cast<uint32_t>(t)) & mask, tab + to.lo, tab + to.hi);
+    bts = twiddle_M(static_cast<uint32_t>(t), tab + to.lo, tab + to.hi);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t qT = (lane & 7u) * static_cast<uint32_t>(T);
+    u0 = twiddle_M((static_cast<uint32_t>(c0) * qT) & mask, tab + to.lo, tab + to.hi);
+    us = twiddle_M(qT & mask, tab + to.lo, tab + to.hi);
+  }
 #pragma unroll
   for (int q = 0; q < kPts; ++q) {
     const uint32_t k2 = t + q * T;
-    float2 w = twiddle_M((static_cast<uint32_t>(c0) * k2) & mask, tab + to.lo, tab + to.hi);
-    const float2 step = twiddle_M(k2, tab + to.lo, tab + to.hi);
+    float2 w, step;
+    if (utw) {
+      const float2 ua = make_float2(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(u0.x), q)),
+                                    __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u0.y), q)));
+      const float2 ub = make_float2(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(us.x), q)),
+                                    __int_as_float(__builtin_amdgcn_readlane(__float_as_int(us.y), q)));
+      w = cmul(bt0, ua);
+      step = cmul(bts, ub);
+    } else {
+      w = twiddle_M((static_cast<uint32_t>(c0) * k2) & mask, tab + to.lo, tab + to.hi);
+      step = twiddle_M(k2, tab + to.lo, tab + to.hi);
+    }
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
       v[c][q] = cmul(v[c][q], w);
@@ -553,7 +578,7 @@ void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& 
 
 namespace {
 int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4TileY | kFft4TileX | kFft4PairXcd |
-                   kFft4GroupXcd;  // fastest measured (tools/kbench.py)
+                   kFft4GroupXcd | kFft4UniformTw;  // fastest measured (tools/kbench.py)
 
 template <int CPT, int SUB, int MODE>
 void launch_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,

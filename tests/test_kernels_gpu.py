@@ -215,7 +215,7 @@ def test_r2c_interbin_normalise_batch():
         assert np.allclose(P[k], exp, rtol=1e-4, atol=2e-3), np.abs(P[k] - exp).max()
 
 
-FFT4_FLAG_SETS = [None, 0, 1, 259, 274, 1299, 3331, 7427, 32003, 48387]  # None = default; 3331 = tiled Y and X; 32003 = + Sub2
+FFT4_FLAG_SETS = [None, 0, 1, 259, 274, 1299, 3331, 7427, 15619, 32003, 48387]  # None = default (81155: tiled Y and X + uniform pass-A twiddles); 32003 = + Sub2
 
 
 @pytest.fixture(params=FFT4_FLAG_SETS)
