@@ -111,11 +111,24 @@ __device__ __forceinline__ void stage_compute(Vec<CPT>& v, int t, const float2* 
     if constexpr (Ns > 1) {
       const int jm = (t + b * T) & (Ns - 1);
       constexpr int scale = L / (Ns * R);
+      // W^{r jm scale}, r < R: two table reads (w1, w4) and short products
+      // (at most two multiplications deep) instead of R-1 table reads
+      float2 w[R];
+      w[1] = twL[jm * scale];
+      if constexpr (R >= 4) {
+        w[2] = cmul(w[1], w[1]);
+        w[3] = cmul(w[2], w[1]);
+      }
+      if constexpr (R == 8) {
+        w[4] = twL[4 * jm * scale];
+        w[5] = cmul(w[4], w[1]);
+        w[6] = cmul(w[4], w[2]);
+        w[7] = cmul(w[4], w[3]);
+      }
 #pragma unroll
       for (int r = 1; r < R; ++r) {
-        const float2 w = twL[r * jm * scale];
 #pragma unroll
-        for (int c = 0; c < CPT; ++c) v[c][b + r * B] = cmul(v[c][b + r * B], w);
+        for (int c = 0; c < CPT; ++c) v[c][b + r * B] = cmul(v[c][b + r * B], w[r]);
       }
     }
 #pragma unroll
