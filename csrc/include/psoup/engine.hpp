@@ -178,7 +178,10 @@ class SearchEngine {
   FftPlan& batch_plan(int count);
   void launch_batch(Slot& s, int first, int count);
   void grow_capacity(uint32_t need);
-  void process_slot(Slot& s, float dm, int dm_idx, const std::vector<float>& accs, CandidateList& out);
+  // first/count/npeaks are the batch's values captured before the slot was
+  // re-issued (launch_batch overwrites Slot::first/count/h_count)
+  void process_slot(Slot& s, int first, int count, uint32_t npeaks, float dm, int dm_idx,
+                    const std::vector<float>& accs, CandidateList& out);
 
   SearchParams p_;
   hipStream_t stream_;

@@ -370,13 +370,18 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
   s.done->record(stream_);
 }
 
-void SearchEngine::process_slot(Slot& s, float dm, int dm_idx, const std::vector<float>& accs, CandidateList& out) {
-  const uint32_t cnt = std::min(s.h_count[0], cap_);
+void SearchEngine::process_slot(Slot& s, int first, int count, uint32_t npeaks, float dm, int dm_idx,
+                                const std::vector<float>& accs, CandidateList& out) {
+  const uint32_t cnt = std::min(npeaks, cap_);
   ctr_.peaks += cnt;
   const int L = nlev_ + 1;
-  const int nseg = s.count * 8;
+  const int nseg = count * 8;
   seg_count_.assign(static_cast<size_t>(nseg) + 1, 0);
-  for (uint32_t i = 0; i < cnt; ++i) seg_count_[s.h_peaks[i].seg]++;
+  for (uint32_t i = 0; i < cnt; ++i) {
+    const uint32_t seg = s.h_peaks[i].seg;
+    PSOUP_CHECK(seg < static_cast<uint32_t>(nseg), "peak record outside its batch (segment " << seg << ")");
+    seg_count_[seg]++;
+  }
   seg_off_.assign(static_cast<size_t>(nseg) + 1, 0);
   for (int i = 0; i < nseg; ++i) seg_off_[i + 1] = seg_off_[i] + seg_count_[i];
   sorted_.resize(cnt);
@@ -391,7 +396,7 @@ void SearchEngine::process_slot(Slot& s, float dm, int dm_idx, const std::vector
     std::vector<int> idxs, pidx;
     std::vector<float> snrs, psnr;
     for (int k = k0; k < k1; ++k) {
-      const float acc = accs[static_cast<size_t>(s.first + k)];
+      const float acc = accs[static_cast<size_t>(first + k)];
       CandidateList trial;
       for (int h = 0; h < L; ++h) {
         const int seg = k * 8 + h;
@@ -419,18 +424,18 @@ void SearchEngine::process_slot(Slot& s, float dm, int dm_idx, const std::vector
     }
   };
   constexpr uint32_t kParallelPeaks = 8192;  // below this the serial loop is cheaper
-  if (pool_ && cnt >= kParallelPeaks && s.count > 1) {
-    const int nparts = std::min(s.count, 4 * pool_->size());
+  if (pool_ && cnt >= kParallelPeaks && count > 1) {
+    const int nparts = std::min(count, 4 * pool_->size());
     std::vector<CandidateList> parts(static_cast<size_t>(nparts));
     pool_->parallel_for(nparts, [&](int j) {
-      const int k0 = static_cast<int>(static_cast<int64_t>(s.count) * j / nparts);
-      const int k1 = static_cast<int>(static_cast<int64_t>(s.count) * (j + 1) / nparts);
+      const int k0 = static_cast<int>(static_cast<int64_t>(count) * j / nparts);
+      const int k1 = static_cast<int>(static_cast<int64_t>(count) * (j + 1) / nparts);
       trial_range(k0, k1, parts[static_cast<size_t>(j)]);
     });
     for (auto& part : parts)
       for (auto& c : part) out.push_back(std::move(c));
   } else {
-    trial_range(0, s.count, out);
+    trial_range(0, count, out);
   }
 }
 
@@ -487,6 +492,9 @@ CandidateList SearchEngine::search_trial(const uint8_t* d_trial, uint64_t nsamps
       continue;
     }
     inflight.pop_front();
+    // The batch's identity: the slot is re-issued below (launch_batch
+    // overwrites first/count/h_count) before its records are processed.
+    const int b_first = s.first, b_count = s.count;
     if (cnt > 0)
       PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_peaks.data(), s.d_peaks.data(), cnt * sizeof(kern::PeakRecord),
                                      hipMemcpyDeviceToHost, copy_stream_.get()));
@@ -496,9 +504,9 @@ CandidateList SearchEngine::search_trial(const uint8_t* d_trial, uint64_t nsamps
     if (next < nacc) issue(sl);
     s.copied->sync();
     host.start();
-    process_slot(s, dm, dm_idx, accs, accel_trial_cands);
+    process_slot(s, b_first, b_count, cnt, dm, dm_idx, accs, accel_trial_cands);
     host.stop();
-    ctr_.accel_trials += static_cast<uint64_t>(s.count);
+    ctr_.accel_trials += static_cast<uint64_t>(b_count);
   }
   ctr_.host_s += host.get_time();
   CandidateList dm_cands = accd_.distill(std::move(accel_trial_cands));

@@ -405,3 +405,35 @@ def test_parallel_host_distillation_is_deterministic(C):
         assert eng.counters()["peaks"] > 8192 * 2  # the parallel branch is taken
         runs.append([(c.acc, c.nh, c.snr, c.freq, len(c.assoc)) for c in cands])
     assert runs[0] == runs[1] and len(runs[0]) > 0
+
+
+@pytest.mark.parametrize("batch,sub", [(4, 0), (7, 0), (16, 8), (64, 32)])
+def test_results_independent_of_accel_batching(C, batch, sub):
+    """Regression: with more acceleration trials than two batches the slots
+    are re-issued before their peak records are processed (and the last
+    batch is partial); candidates (incl. their accelerations) must not depend
+    on the batch size or sub-batching."""
+    rng = np.random.default_rng(33)
+    nsamps, n = 1100000, 1 << 20
+    tsamp = 64e-6
+    t = np.arange(nsamps) * tsamp
+    # accelerated pulsar (synthetic.py convention): phase = (t - a t^2 / 2c) / P;
+    # over 67 s the drift is ~1.2 turns, so the acceleration is measurable
+    a_true = 310.0
+    ph = ((t - a_true * t * t / (2 * 299792458.0)) / 0.002) % 1.0
+    trial = np.clip(rng.normal(128, 6, nsamps) + 2.0 * (np.minimum(ph, 1 - ph) < 0.04), 0, 255).astype(np.uint8)
+    tt = torch.from_numpy(trial).to(dev)
+    accs = [float(a) for a in np.linspace(-500, 500, 101)]
+    s = torch.cuda.current_stream().cuda_stream
+    runs = []
+    for b, sb in ((200, 0), (batch, sub)):
+        p = C.SearchParams()
+        p.fft_size, p.tsamp, p.nharmonics, p.min_snr = n, tsamp, 3, 6.0
+        p.accel_batch, p.sub_batch = b, sb
+        eng = C.SearchEngine(p, s)
+        cands = eng.search_trial(tt.data_ptr(), nsamps, 1.0, 0, accs)
+        torch.cuda.synchronize()
+        runs.append(sorted((c.acc, c.nh, c.snr, c.freq) for c in cands))
+    assert runs[0] == runs[1] and len(runs[0]) > 0
+    best = max(runs[1], key=lambda r: r[2])
+    assert abs(best[0] - a_true) <= 30.0, best
