@@ -213,6 +213,7 @@ class Stopwatch {
     acc_ = 0.0;
     running_ = false;
   }
+  void add(double seconds) { acc_ += seconds; }  // externally measured interval (e.g. GPU events)
   double get_time() const {
     double t = acc_;
     if (running_) t += std::chrono::duration<double>(clock::now() - t0_).count();

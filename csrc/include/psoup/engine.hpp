@@ -74,15 +74,26 @@ class DeviceFilterbank {
 class Dedisperser {
  public:
   Dedisperser(const DeviceFilterbank& fb, hipStream_t stream);
-  // DM trials [d0, d1) -> out[(d-d0)*out_stride + t], t < out_nsamps
-  void run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispKernel kind = DedispKernel::Auto);
+  // DM trials [d0, d1) -> out[(d-d0)*out_stride + t], t < out_nsamps, on
+  // stream s (nullptr = the constructor's stream).  MFMA runs made of whole
+  // kTileDms-DM tiles (d0 and d1 multiples of it, or d1 = the list's end) use
+  // the resident whole-DM-list plan (built on first use, one upload) and never
+  // block the host; other ranges build a plan for [d0, d1) and wait for its
+  // upload.
+  void run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispKernel kind = DedispKernel::Auto,
+           hipStream_t s = nullptr);
   static uint64_t row_stride(uint64_t out_nsamps) { return (out_nsamps + 255) / 256 * 256; }
+  static constexpr int kTileDms = 32;  // DMs per MFMA tile
 
  private:
+  void build_resident_plan();
   const DeviceFilterbank& fb_;
   hipStream_t stream_;
-  DeviceBuffer<int32_t> d_offsets_, d_kill_, d_active_, d_steps_, d_nsteps_;
+  DeviceBuffer<int32_t> d_offsets_, d_kill_, d_active_, d_steps_, d_tile_info_;
   DeviceBuffer<int8_t> d_deltas_;
+  bool resident_ = false;
+  DeviceBuffer<int32_t> r_steps_, r_tile_info_;
+  DeviceBuffer<int8_t> r_deltas_;
 };
 
 struct SearchParams {

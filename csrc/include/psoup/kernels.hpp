@@ -57,17 +57,17 @@ void dedisperse_direct(const int8_t* chan_major, uint64_t chan_stride, int nchan
 // the per-lane one-hot positions; see dedisperse.hip.
 struct MfmaDedispPlan {
   int ntiles = 0;
-  int max_steps = 0;
-  std::vector<int32_t> steps;   // [ntiles][max_steps][4] = {c0, sb0, c1, sb1}
-  std::vector<int8_t> deltas;   // [ntiles][max_steps][64] one-hot position per lane, -1 = none
-  std::vector<int32_t> nsteps;  // [ntiles]
+  int max_steps = 0;               // longest tile (informational)
+  std::vector<int32_t> steps;      // [total steps][4] = {c0, sb0, c1, sb1}, tiles back to back
+  std::vector<int8_t> deltas;      // [total steps][64] one-hot position per lane, -1 = none
+  std::vector<int32_t> tile_info;  // [ntiles][2] = {first step, step count}
 };
 // offsets: host int32 [ndm][nchans]; killmask: host [nchans] (0 = killed)
 void build_mfma_dedisp_plan(const int32_t* offsets, int ndm, int nchans, const int32_t* killmask,
                             MfmaDedispPlan& plan);
 // Reads up to 560 bytes past out_nsamps + max offset in each channel row.
 void dedisperse_mfma(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_steps, const int8_t* d_deltas,
-                     const int32_t* d_nsteps, int ntiles, int max_steps, int ndm, uint64_t out_nsamps, uint8_t* out,
+                     const int32_t* d_tile_info, int ntiles, int ndm, uint64_t out_nsamps, uint8_t* out,
                      uint64_t out_stride, float scale, int bias_total, hipStream_t s);
 
 // ------------------------------------------------------------ time series ---

@@ -82,16 +82,17 @@ constexpr int kMfmaWgSamples = 4 * 32 * kMfmaWaveTiles;  // 512
 
 __global__ void __launch_bounds__(256) dedisperse_mfma_kernel(
     const int8_t* __restrict__ x, uint64_t stride, const int4* __restrict__ steps, const int8_t* __restrict__ deltas,
-    const int32_t* __restrict__ nsteps, int max_steps, int ndm, uint64_t out_nsamps, uint8_t* __restrict__ out,
+    const int2* __restrict__ tile_info, int ndm, uint64_t out_nsamps, uint8_t* __restrict__ out,
     uint64_t out_stride, float scale, int bias_total, uint64_t ntime_tiles) {
   const int tile = blockIdx.x;  // DM tile (fastest: concurrent WGs share the x window in L2)
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
   const int r = lane & 31;
   const int h = lane >> 5;
-  const int ns = nsteps[tile];
-  const int4* st = steps + static_cast<uint64_t>(tile) * max_steps;
-  const int8_t* dl = deltas + static_cast<uint64_t>(tile) * max_steps * 64;
+  const int2 ti = tile_info[tile];  // {first step, step count}: ragged per-tile step lists
+  const int ns = ti.y;
+  const int4* st = steps + ti.x;
+  const int8_t* dl = deltas + static_cast<uint64_t>(ti.x) * 64;
   for (uint64_t tt = blockIdx.y; tt < ntime_tiles; tt += gridDim.y) {
     const uint64_t t0 = tt * kMfmaWgSamples + static_cast<uint64_t>(wave) * (32 * kMfmaWaveTiles);
     v16i acc[kMfmaWaveTiles];
@@ -215,26 +216,33 @@ void build_mfma_dedisp_plan(const int32_t* offsets, int ndm, int nchans, const i
     max_steps = std::max(max_steps, nst);
   }
   plan.max_steps = max_steps;
-  plan.steps.assign(static_cast<size_t>(ntiles) * max_steps * 4, 0);
-  plan.deltas.assign(static_cast<size_t>(ntiles) * max_steps * 64, static_cast<int8_t>(-1));
-  plan.nsteps.assign(static_cast<size_t>(ntiles), 0);
+  size_t total = 0;
+  for (const auto& S : tsteps) total += S.size() / 4;
+  plan.steps.assign(total * 4, 0);
+  plan.deltas.assign(total * 64, static_cast<int8_t>(-1));
+  plan.tile_info.assign(static_cast<size_t>(ntiles) * 2, 0);
+  size_t at = 0;
   for (int T = 0; T < ntiles; ++T) {
-    const int nst = static_cast<int>(tsteps[T].size() / 4);
-    plan.nsteps[T] = nst;
-    std::copy(tsteps[T].begin(), tsteps[T].end(), plan.steps.begin() + static_cast<size_t>(T) * max_steps * 4);
-    std::copy(tdeltas[T].begin(), tdeltas[T].end(), plan.deltas.begin() + static_cast<size_t>(T) * max_steps * 64);
+    const size_t nst = tsteps[T].size() / 4;
+    PSOUP_CHECK(at + nst < (1ull << 31), "MFMA dedispersion plan too large");
+    plan.tile_info[2 * T] = static_cast<int32_t>(at);
+    plan.tile_info[2 * T + 1] = static_cast<int32_t>(nst);
+    std::copy(tsteps[T].begin(), tsteps[T].end(), plan.steps.begin() + at * 4);
+    std::copy(tdeltas[T].begin(), tdeltas[T].end(), plan.deltas.begin() + at * 64);
+    at += nst;
   }
 }
 
 void dedisperse_mfma(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_steps, const int8_t* d_deltas,
-                     const int32_t* d_nsteps, int ntiles, int max_steps, int ndm, uint64_t out_nsamps, uint8_t* out,
+                     const int32_t* d_tile_info, int ntiles, int ndm, uint64_t out_nsamps, uint8_t* out,
                      uint64_t out_stride, float scale, int bias_total, hipStream_t s) {
   if (ndm <= 0 || out_nsamps == 0) return;
   PSOUP_CHECK(ntiles <= 65535, "too many DM tiles");
   const uint64_t ntt = (out_nsamps + kMfmaWgSamples - 1) / kMfmaWgSamples;
   dim3 grid(static_cast<unsigned>(ntiles), static_cast<unsigned>(std::min<uint64_t>(ntt, 65535)));
   dedisperse_mfma_kernel<<<grid, 256, 0, s>>>(chan_major, chan_stride, reinterpret_cast<const int4*>(d_steps),
-                                               d_deltas, d_nsteps, max_steps, ndm, out_nsamps, out, out_stride, scale,
+                                               d_deltas, reinterpret_cast<const int2*>(d_tile_info), ndm, out_nsamps,
+                                               out, out_stride, scale,
                                                bias_total, ntt);
   post_launch_check("dedisperse_mfma_kernel", s);
 }

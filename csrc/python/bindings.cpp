@@ -608,13 +608,35 @@ PYBIND11_MODULE(_C, m) {
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("data_address", [](const DeviceFilterbank& f) { return reinterpret_cast<uintptr_t>(f.data()); })
       .def_property_readonly("stride", &DeviceFilterbank::stride);
+  // Native stream / event handles: ordering between the engine's stream and a
+  // side stream is expressed with these (HIP semantics end to end) rather than
+  // through torch's stream objects.
+  py::class_<Stream>(m, "GpuStream")
+      .def(py::init<>())
+      .def_property_readonly("handle", [](const Stream& s) { return reinterpret_cast<uintptr_t>(s.get()); })
+      .def("synchronize", &Stream::sync, py::call_guard<py::gil_scoped_release>());
+  m.def("stream_synchronize", [](uintptr_t s) { PSOUP_HIP_CHECK(hipStreamSynchronize(S(s))); },
+        py::call_guard<py::gil_scoped_release>());
+  py::class_<Event>(m, "GpuEvent")
+      .def(py::init<bool>(), py::arg("timing") = false)
+      .def("record", [](Event& e, uintptr_t s) { e.record(S(s)); })
+      .def("wait", [](Event& e, uintptr_t s) { PSOUP_HIP_CHECK(hipStreamWaitEvent(S(s), e.get(), 0)); },
+           py::arg("stream"), "make `stream` wait for the last record of this event")
+      .def("synchronize", &Event::sync, py::call_guard<py::gil_scoped_release>())
+      .def("elapsed_ms", [](const Event& a, const Event& b) {
+        float ms = 0.f;
+        PSOUP_HIP_CHECK(hipEventElapsedTime(&ms, a.get(), b.get()));
+        return ms;
+      });
   py::class_<Dedisperser>(m, "Dedisperser")
       .def(py::init([](const DeviceFilterbank& fb, uintptr_t s) { return new Dedisperser(fb, S(s)); }),
            py::keep_alive<1, 2>())
-      .def("run", [](Dedisperser& d, int d0, int d1, uintptr_t out, uint64_t ostride, DedispKernel k) {
-        d.run(d0, d1, P<uint8_t>(out), ostride, k);
-      }, py::call_guard<py::gil_scoped_release>())
-      .def_static("row_stride", &Dedisperser::row_stride);
+      .def("run", [](Dedisperser& d, int d0, int d1, uintptr_t out, uint64_t ostride, DedispKernel k, uintptr_t s) {
+        d.run(d0, d1, P<uint8_t>(out), ostride, k, S(s));
+      }, py::arg("d0"), py::arg("d1"), py::arg("out"), py::arg("out_stride"), py::arg("kind") = DedispKernel::Auto,
+           py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>())
+      .def_static("row_stride", &Dedisperser::row_stride)
+      .def_property_readonly_static("tile_dms", [](py::object) { return Dedisperser::kTileDms; });
 
   py::class_<SearchParams>(m, "SearchParams")
       .def(py::init<>())

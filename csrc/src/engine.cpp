@@ -109,38 +109,62 @@ Dedisperser::Dedisperser(const DeviceFilterbank& fb, hipStream_t stream) : fb_(f
     PSOUP_HIP_CHECK(hipMemcpy(d_active_.data(), active.data(), active.size() * 4, hipMemcpyHostToDevice));
 }
 
-void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispKernel kind) {
+void Dedisperser::build_resident_plan() {
+  const auto& g = fb_.geometry();
+  const int ndm = static_cast<int>(g.dm_list.size());
+  std::vector<int32_t> offs = g.offsets(0, ndm);
+  std::vector<int32_t> kill(g.killmask.begin(), g.killmask.end());
+  kern::MfmaDedispPlan plan;
+  kern::build_mfma_dedisp_plan(offs.data(), ndm, g.nchans, kill.data(), plan);
+  r_steps_.resize(plan.steps.size());
+  r_deltas_.resize(plan.deltas.size());
+  r_tile_info_.resize(plan.tile_info.size());
+  PSOUP_HIP_CHECK(hipMemcpy(r_steps_.data(), plan.steps.data(), plan.steps.size() * 4, hipMemcpyHostToDevice));
+  PSOUP_HIP_CHECK(hipMemcpy(r_deltas_.data(), plan.deltas.data(), plan.deltas.size(), hipMemcpyHostToDevice));
+  PSOUP_HIP_CHECK(
+      hipMemcpy(r_tile_info_.data(), plan.tile_info.data(), plan.tile_info.size() * 4, hipMemcpyHostToDevice));
+  resident_ = true;
+}
+
+void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispKernel kind, hipStream_t s) {
   const auto& g = fb_.geometry();
   PSOUP_CHECK(d0 >= 0 && d1 <= static_cast<int>(g.dm_list.size()) && d0 <= d1, "bad DM range");
   if (d0 == d1) return;
+  if (!s) s = stream_;
   RoctxRange r("Dedisperse");
   if (kind == DedispKernel::Auto) kind = DedispKernel::Mfma;
   const int ndm = d1 - d0;
-  if (kind == DedispKernel::Mfma) {
+  const int ntiles = (ndm + kTileDms - 1) / kTileDms;
+  const int ndm_all = static_cast<int>(g.dm_list.size());
+  if (kind == DedispKernel::Mfma && d0 % kTileDms == 0 && (d1 % kTileDms == 0 || d1 == ndm_all)) {
+    // whole tiles of the resident plan cover exactly these DMs
+    if (!resident_) build_resident_plan();
+    kern::dedisperse_mfma(fb_.data(), fb_.stride(), r_steps_.data(), r_deltas_.data(),
+                          r_tile_info_.data() + 2 * (d0 / kTileDms), ntiles, ndm, g.out_nsamps, out, out_stride,
+                          g.out_scale, g.bias * g.nactive, s);
+  } else if (kind == DedispKernel::Mfma) {
     std::vector<int32_t> offs = g.offsets(d0, d1);
     std::vector<int32_t> kill(g.killmask.begin(), g.killmask.end());
     kern::MfmaDedispPlan plan;
     kern::build_mfma_dedisp_plan(offs.data(), ndm, g.nchans, kill.data(), plan);
+    PSOUP_CHECK(plan.ntiles == ntiles, "MFMA plan tile count");
     d_steps_.resize(plan.steps.size());
     d_deltas_.resize(plan.deltas.size());
-    d_nsteps_.resize(plan.nsteps.size());
-    PSOUP_HIP_CHECK(hipMemcpyAsync(d_steps_.data(), plan.steps.data(), plan.steps.size() * 4, hipMemcpyHostToDevice,
-                                   stream_));
-    PSOUP_HIP_CHECK(hipMemcpyAsync(d_deltas_.data(), plan.deltas.data(), plan.deltas.size(), hipMemcpyHostToDevice,
-                                   stream_));
-    PSOUP_HIP_CHECK(hipMemcpyAsync(d_nsteps_.data(), plan.nsteps.data(), plan.nsteps.size() * 4,
-                                   hipMemcpyHostToDevice, stream_));
-    PSOUP_HIP_CHECK(hipStreamSynchronize(stream_));  // host tables may go out of scope
-    kern::dedisperse_mfma(fb_.data(), fb_.stride(), d_steps_.data(), d_deltas_.data(), d_nsteps_.data(), plan.ntiles,
-                          plan.max_steps, ndm, g.out_nsamps, out, out_stride, g.out_scale, g.bias * g.nactive,
-                          stream_);
+    d_tile_info_.resize(plan.tile_info.size());
+    PSOUP_HIP_CHECK(hipMemcpyAsync(d_steps_.data(), plan.steps.data(), plan.steps.size() * 4, hipMemcpyHostToDevice, s));
+    PSOUP_HIP_CHECK(hipMemcpyAsync(d_deltas_.data(), plan.deltas.data(), plan.deltas.size(), hipMemcpyHostToDevice, s));
+    PSOUP_HIP_CHECK(hipMemcpyAsync(d_tile_info_.data(), plan.tile_info.data(), plan.tile_info.size() * 4,
+                                   hipMemcpyHostToDevice, s));
+    PSOUP_HIP_CHECK(hipStreamSynchronize(s));  // host tables go out of scope
+    kern::dedisperse_mfma(fb_.data(), fb_.stride(), d_steps_.data(), d_deltas_.data(), d_tile_info_.data(), ntiles,
+                          ndm, g.out_nsamps, out, out_stride, g.out_scale, g.bias * g.nactive, s);
   } else {
     std::vector<int32_t> offs = g.offsets(d0, d1);
     d_offsets_.resize(offs.size());
-    PSOUP_HIP_CHECK(hipMemcpyAsync(d_offsets_.data(), offs.data(), offs.size() * 4, hipMemcpyHostToDevice, stream_));
-    PSOUP_HIP_CHECK(hipStreamSynchronize(stream_));
+    PSOUP_HIP_CHECK(hipMemcpyAsync(d_offsets_.data(), offs.data(), offs.size() * 4, hipMemcpyHostToDevice, s));
+    PSOUP_HIP_CHECK(hipStreamSynchronize(s));
     kern::dedisperse_direct(fb_.data(), fb_.stride(), g.nchans, d_offsets_.data(), d_kill_.data(), ndm, g.out_nsamps,
-                            out, out_stride, g.out_scale, g.bias, g.nactive, stream_);
+                            out, out_stride, g.out_scale, g.bias, g.nactive, s);
   }
 }
 

@@ -225,21 +225,45 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
       wd.stop();
       SearchEngine engine(setup.search, st);
       const uint64_t rstride = Dedisperser::row_stride(geom.out_nsamps);
-      DeviceBuffer<uint8_t> trials(rstride * static_cast<uint64_t>(sh.chunk));
-      int processed = 0;
-      while (true) {
-        const int d0 = sh.next_dm.fetch_add(sh.chunk);
-        if (d0 >= sh.ndm) break;
+      // Double-buffered: the next chunk is dedispersed on a side stream while
+      // this one is searched; the search stream waits on an event.
+      Stream dstream;
+      DeviceBuffer<uint8_t> trials[2] = {DeviceBuffer<uint8_t>(rstride * static_cast<uint64_t>(sh.chunk)),
+                                         DeviceBuffer<uint8_t>(rstride * static_cast<uint64_t>(sh.chunk))};
+      Event ready[2] = {Event(true), Event(true)}, began[2] = {Event(true), Event(true)}, freed[2];
+      bool pending[2] = {false, false}, used[2] = {false, false};
+      double dd_ms = 0.0;
+      auto ck_of = [&](int d0) {
         const int d1 = std::min(sh.ndm, d0 + sh.chunk);
+        return args.checkpoint_dir.empty() ? std::string() : chunk_file(args.checkpoint_dir, d0, d1);
+      };
+      auto resumable = [&](const std::string& ck) {
+        if (ck.empty()) return false;
+        std::ifstream f(ck, std::ios::binary);
+        return static_cast<bool>(f);
+      };
+      auto issue = [&](int d0, int k) {
+        const int d1 = std::min(sh.ndm, d0 + sh.chunk);
+        if (used[k]) PSOUP_HIP_CHECK(hipStreamWaitEvent(dstream.get(), freed[k].get(), 0));
+        began[k].record(dstream.get());
+        ds.dd->run(d0, d1, trials[k].data(), rstride, setup.dedisp_kernel, dstream.get());
+        ready[k].record(dstream.get());
+        pending[k] = true;
+      };
+      int processed = 0, k = 0;
+      int cur = sh.next_dm.fetch_add(sh.chunk);
+      if (cur < sh.ndm && !resumable(ck_of(cur))) issue(cur, k);
+      while (cur < sh.ndm) {
+        const int d0 = cur, d1 = std::min(sh.ndm, d0 + sh.chunk);
+        const std::string ck = ck_of(d0);
+        const int nxt = sh.next_dm.fetch_add(sh.chunk);
+        if (nxt < sh.ndm && !resumable(ck_of(nxt))) issue(nxt, k ^ 1);
         CandidateList local;
-        const std::string ck = args.checkpoint_dir.empty() ? "" : chunk_file(args.checkpoint_dir, d0, d1);
-        if (!ck.empty() && load_chunk(ck, local)) {
+        if (!pending[k] && load_chunk(ck, local)) {
           log_verbose("resumed DMs [" + std::to_string(d0) + "," + std::to_string(d1) + ") from checkpoint");
         } else {
-          wd.start();
-          ds.dd->run(d0, d1, trials.data(), rstride, setup.dedisp_kernel);
-          PSOUP_HIP_CHECK(hipStreamSynchronize(st));
-          wd.stop();
+          if (!pending[k]) issue(d0, k);  // unreadable checkpoint: recompute
+          PSOUP_HIP_CHECK(hipStreamWaitEvent(st, ready[k].get(), 0));
           ws.start();
           for (int d = d0; d < d1; ++d) {
             if (args.fault_after_dms >= 0 && processed >= args.fault_after_dms)
@@ -248,13 +272,19 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
             std::vector<float> accs = setup.accel_plan.generate(dm);
             log_verbose("Searching " + std::to_string(accs.size()) + " acceleration trials for DM " +
                         std::to_string(dm));
-            CandidateList c = engine.search_trial(trials.data() + static_cast<uint64_t>(d - d0) * rstride,
+            CandidateList c = engine.search_trial(trials[k].data() + static_cast<uint64_t>(d - d0) * rstride,
                                                   geom.out_nsamps, dm, d, accs);
             sh.accel_trials += accs.size();
             for (auto& x : c) local.push_back(std::move(x));
             processed++;
           }
           ws.stop();
+          freed[k].record(st);
+          used[k] = true;
+          pending[k] = false;
+          float ms = 0.f;
+          PSOUP_HIP_CHECK(hipEventElapsedTime(&ms, began[k].get(), ready[k].get()));
+          dd_ms += ms;
           if (!ck.empty()) save_chunk(ck, local);
         }
         {
@@ -263,7 +293,12 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
         }
         int done = sh.done_dms.fetch_add(d1 - d0) + (d1 - d0);
         if (sh.progress) sh.progress->set(static_cast<double>(done) / sh.ndm);
+        cur = nxt;
+        k ^= 1;
       }
+      PSOUP_HIP_CHECK(hipStreamSynchronize(dstream.get()));
+      PSOUP_HIP_CHECK(hipStreamSynchronize(st));
+      wd.add(dd_ms * 1e-3);  // GPU time of the (overlapped) dedispersion kernels
       sh.dedisp_s[static_cast<size_t>(dev)] = wd.get_time();
       sh.search_s[static_cast<size_t>(dev)] = ws.get_time();
       const SearchCounters& c = engine.counters();

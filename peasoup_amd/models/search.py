@@ -52,8 +52,18 @@ class SearchResult:
     rank_stats: list = field(default_factory=list)
 
 
-def _stream_handle() -> int:
-    return torch.cuda.current_stream().cuda_stream
+_SYNC_DEDISP = os.environ.get("PSOUP_SYNC_DEDISP", "0") == "1"  # debug: no dedispersion/search overlap
+
+
+_ENGINE_STREAMS: Dict[int, object] = {}  # device index -> _C.GpuStream, alive for the process
+
+
+def _engine_stream(device: torch.device) -> int:
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    if idx not in _ENGINE_STREAMS:
+        with torch.cuda.device(idx):
+            _ENGINE_STREAMS[idx] = _C.GpuStream()
+    return _ENGINE_STREAMS[idx].handle
 
 
 class RankSearcher:
@@ -75,7 +85,10 @@ class RankSearcher:
         self.fft_size = int(fft_size)
         self.cfreq = cfreq
         self.geom = _C.DedispGeometry.make(self.header, int(nsamps), self.dm_list, list(kill))
-        self.stream = _stream_handle()
+        # the engine, dedisperser and folder share one explicit non-blocking
+        # stream; torch work that produced `packed` is drained first
+        self.stream = _engine_stream(self.ctx.device)
+        torch.cuda.synchronize(self.ctx.device)
         self.dfb = _C.DeviceFilterbank(self.geom, self.stream)
         if packed is not None:
             self.load_packed(packed)
@@ -103,52 +116,104 @@ class RankSearcher:
         self.dedisperser.run(d0, d1, self._trials.data_ptr(), self.row_stride, self.kernel)
         return self._trials
 
-    def search(self, dm_indices: Sequence[int], chunk: int = 16, timers: Optional[Dict[str, Stopwatch]] = None,
+    @staticmethod
+    def chunk_ranges(idx: Sequence[int], chunk: int) -> List[tuple]:
+        """Contiguous [d0, d1) blocks of ``idx`` cut at multiples of ``chunk``
+        (itself a multiple of the MFMA tile), so every block but a shard's
+        first starts on a tile of the resident dedispersion plan."""
+        idx = list(idx)
+        if not idx:
+            return []
+        lo, hi = idx[0], idx[-1] + 1
+        assert hi - lo == len(idx), "DM shard must be contiguous"
+        out = []
+        d0 = lo
+        while d0 < hi:
+            d1 = min(hi, (d0 // chunk + 1) * chunk)
+            out.append((d0, d1))
+            d0 = d1
+        return out
+
+    def search(self, dm_indices: Sequence[int], chunk: int = 32, timers: Optional[Dict[str, Stopwatch]] = None,
                progress=None) -> list:
+        """Dedisperse + search ``dm_indices`` chunk by chunk.  Chunk k+1 is
+        dedispersed on a side stream into the other half of a double buffer
+        while chunk k is searched (the reference dedisperses the whole DM
+        list up front, pipeline.cu:325-359); the search stream waits on an
+        event, never the host.  ``timers['dedispersion']`` accumulates the
+        dedispersion kernels' GPU time (overlapped), ``timers['searching']``
+        the wall time of the search loop."""
+        tile = int(_C.Dedisperser.tile_dms)
+        chunk = max(tile, (int(chunk) + tile - 1) // tile * tile)
+        blocks = self.chunk_ranges(dm_indices, chunk)
         cands: list = []
-        idx = list(dm_indices)
         t_dd = timers.get("dedispersion") if timers else None
         t_s = timers.get("searching") if timers else None
         ntrials = 0
         ckdir = getattr(self.args, "checkpoint_dir", "") or ""
         fault_after = int(getattr(self.args, "fault_after_dms", -1))
         processed = 0
-        for c0 in range(0, len(idx), chunk):
-            block = idx[c0:c0 + chunk]
-            d0, d1 = block[0], block[-1] + 1
-            assert d1 - d0 == len(block), "DM shard must be contiguous"
-            ck = os.path.join(ckdir, f"dm_{d0}_{d1}.psoc") if ckdir else ""
-            if ck and os.path.exists(ck):
+        ck_of = [os.path.join(ckdir, f"dm_{d0}_{d1}.psoc") if ckdir else "" for d0, d1 in blocks]
+        todo = [i for i, ck in enumerate(ck_of) if not (ck and os.path.exists(ck))]
+        dev = self.ctx.device
+        side = _C.GpuStream()
+        nbuf = min(2, len(todo))
+        bufs = [torch.empty(chunk * self.row_stride, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
+        freed = [None] * nbuf      # event: search stream finished with the buffer
+        issued = {}                # block index -> (buffer, ready event, start event)
+
+        def issue(j: int) -> None:
+            k = len(issued) % nbuf
+            d0, d1 = blocks[j]
+            start, ready = _C.GpuEvent(True), _C.GpuEvent(True)
+            if freed[k] is not None:
+                freed[k].wait(side.handle)
+            start.record(side.handle)
+            with roctx_range("Dedisperse"):
+                self.dedisperser.run(d0, d1, bufs[k].data_ptr(), self.row_stride, self.kernel, side.handle)
+            ready.record(side.handle)
+            if _SYNC_DEDISP:
+                ready.synchronize()
+            issued[j] = (k, ready, start)
+
+        dd_events = []
+        if todo:
+            issue(todo[0])
+        if t_s:
+            t_s.start()
+        nxt = 1  # next entry of todo to dedisperse
+        for i in range(len(blocks)):
+            d0, d1 = blocks[i]
+            ck = ck_of[i]
+            if i not in issued:
                 # resume: same spill format as the native pipeline (CandidatePOD trees)
                 with open(ck, "rb") as f:
                     cands.extend(_C.deserialize_candidates(f.read()))
-                ntrials += sum(len(self.accel_list(self.dm_list[d])) for d in block)
+                ntrials += sum(len(self.accel_list(self.dm_list[d])) for d in range(d0, d1))
                 if progress is not None:
-                    progress(len(block))
+                    progress(d1 - d0)
                 continue
+            k, ready, start = issued[i]
+            if nxt < len(todo):
+                issue(todo[nxt])  # overlaps the search below
+                nxt += 1
+            ready.wait(self.stream)
+            dd_events.append((start, ready))
             chunk_cands: list = []
-            if t_dd:
-                t_dd.start()
-            with roctx_range("Dedisperse"):
-                trials = self.dedisperse(d0, d1)
-            if t_dd:
-                torch.cuda.current_stream().synchronize()
-                t_dd.stop()
-            if t_s:
-                t_s.start()
-            for k, d in enumerate(block):
+            for d in range(d0, d1):
                 if 0 <= fault_after <= processed:
                     raise RuntimeError(f"fault injection: rank {self.ctx.rank} aborting after {processed} DM trials")
                 dm = self.dm_list[d]
                 accs = self.accel_list(dm)
                 ntrials += len(accs)
-                addr = trials.data_ptr() + k * self.row_stride
+                addr = bufs[k].data_ptr() + (d - d0) * self.row_stride
                 chunk_cands.extend(self.engine.search_trial(addr, self.geom.out_nsamps, dm, d, accs))
                 processed += 1
                 if progress is not None:
                     progress(1)
-            if t_s:
-                t_s.stop()
+            ev = _C.GpuEvent()
+            ev.record(self.stream)
+            freed[k] = ev
             if ck:
                 os.makedirs(ckdir, exist_ok=True)
                 tmp = ck + f".tmp{self.ctx.rank}"
@@ -156,6 +221,12 @@ class RankSearcher:
                     f.write(_C.serialize_candidates(chunk_cands))
                 os.replace(tmp, ck)
             cands.extend(chunk_cands)
+        side.synchronize()
+        _C.stream_synchronize(self.stream)
+        if t_s:
+            t_s.stop()
+        if t_dd and dd_events:
+            t_dd.add(sum(a.elapsed_ms(b) for a, b in dd_events) * 1e-3)
         self.accel_trials = ntrials
         return cands
 

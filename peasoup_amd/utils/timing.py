@@ -21,6 +21,10 @@ class Stopwatch:
             self._acc += time.perf_counter() - self._t0
             self._t0 = None
 
+    def add(self, seconds: float) -> None:
+        """Accumulate an externally measured interval (e.g. GPU event time)."""
+        self._acc += float(seconds)
+
     def reset(self) -> None:
         self._acc = 0.0
         self._t0 = None

@@ -68,6 +68,34 @@ def test_dedisperse_direct_and_mfma_bit_exact(C, nbits, nchans, kill):
     assert np.array_equal(o.view(5, stride)[:, : g.out_nsamps].cpu().numpy(), exp[3:8])
 
 
+def test_mfma_resident_plan_ranges_and_side_stream(C):
+    """Whole-tile ranges use the resident plan (ragged per-tile step lists),
+    other ranges a per-call plan; both bit-exact, also on a side stream."""
+    rng = np.random.default_rng(11)
+    nchans, nsamps = 64, 6000
+    hdr, dms = _geometry(C, nchans=nchans, nbits=2, nsamps=nsamps, dm_end=900.0)
+    ndm = len(dms)
+    assert ndm > 70, ndm
+    vals = rng.integers(0, 4, size=(nsamps, nchans), dtype=np.uint8)
+    g = C.DedispGeometry.make(hdr, nsamps, dms, [])
+    s = torch.cuda.current_stream().cuda_stream
+    dfb = C.DeviceFilterbank(g, s)
+    dfb.load_packed_device(torch.from_numpy(sigproc.pack_samples(vals, 2)).to(dev).data_ptr())
+    dd = C.Dedisperser(dfb, s)
+    stride = C.Dedisperser.row_stride(g.out_nsamps)
+    offs = np.array(g.offsets(0, ndm), dtype=np.int32).reshape(ndm, nchans)
+    exp = ref.dedisperse(vals, offs, 2, None, g.out_nsamps)
+    T = C.Dedisperser.tile_dms
+    side = torch.cuda.Stream()
+    for d0, d1 in [(0, T), (T, 2 * T), (2 * T, ndm), (0, ndm), (T, T + 5), (5, 2 * T), (ndm - 3, ndm)]:
+        o = torch.zeros((d1 - d0) * stride, dtype=torch.uint8, device=dev)
+        side.wait_stream(torch.cuda.current_stream())
+        dd.run(d0, d1, o.data_ptr(), stride, C.DedispKernel.Mfma, side.cuda_stream)
+        side.synchronize()
+        got = o.view(d1 - d0, stride)[:, : g.out_nsamps].cpu().numpy()
+        assert np.array_equal(got, exp[d0:d1]), (d0, d1)
+
+
 def test_convert_pad_and_truncate():
     from peasoup_amd import ops
 

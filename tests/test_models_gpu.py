@@ -166,7 +166,7 @@ def test_python_entry_fault_then_resume(tmp_path):
     ck = tmp_path / "ck"
     base = [sys.executable, "-m", "peasoup_amd", "-i", TUTORIAL, "--dm_end", "120", "-n", "3"]
     env = dict(os.environ, PYTHONPATH=REPO)
-    r = subprocess.run(base + ["-o", str(tmp_path / "a"), "--checkpoint_dir", str(ck), "--fault_after_dms", "20"],
+    r = subprocess.run(base + ["-o", str(tmp_path / "a"), "--checkpoint_dir", str(ck), "--fault_after_dms", "33"],
                        capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
     assert r.returncode != 0 and "[rank 0] peasoup failed: fault injection" in r.stderr
     assert len(list(ck.glob("dm_*.psoc"))) >= 1
