@@ -29,7 +29,7 @@
 
 namespace psoup {
 
-enum class DedispKernel { Auto = 0, Direct = 1, Mfma = 2 };
+enum class DedispKernel { Auto = 0, Direct = 1, Mfma = 2, Valu = 3 };
 DedispKernel parse_dedisp_kernel(const std::string& s);
 
 // Geometry shared by every rank: DM list, delays, killmask, output length.
@@ -84,15 +84,23 @@ class Dedisperser {
            hipStream_t s = nullptr);
   static uint64_t row_stride(uint64_t out_nsamps) { return (out_nsamps + 255) / 256 * 256; }
   static constexpr int kTileDms = 32;  // DMs per MFMA tile
+  // Auto's choice for [d0, d1): one-hot MFMA while the tiles' offset spread is
+  // narrow (few 16-shift blocks per channel), packed-byte VALU once it is wide.
+  DedispKernel choose(int d0, int d1);
+  // resident-plan MFMA steps per (tile, active channel) over [d0, d1)'s tiles
+  double mfma_steps_per_channel(int d0, int d1);
 
  private:
   void build_resident_plan();
+  void build_valu_tables();
   const DeviceFilterbank& fb_;
   hipStream_t stream_;
   DeviceBuffer<int32_t> d_offsets_, d_kill_, d_active_, d_steps_, d_tile_info_;
   DeviceBuffer<int8_t> d_deltas_;
-  bool resident_ = false;
-  DeviceBuffer<int32_t> r_steps_, r_tile_info_;
+  bool resident_ = false, valu_ready_ = false;
+  std::vector<int32_t> h_tile_steps_;  // resident plan: MFMA steps per tile
+  int ldo_ = 0;                        // columns of r_offT_
+  DeviceBuffer<int32_t> r_steps_, r_tile_info_, r_offT_;
   DeviceBuffer<int8_t> r_deltas_;
 };
 

@@ -70,6 +70,14 @@ void dedisperse_mfma(const int8_t* chan_major, uint64_t chan_stride, const int32
                      const int32_t* d_tile_info, int ntiles, int ndm, uint64_t out_nsamps, uint8_t* out,
                      uint64_t out_stride, float scale, int bias_total, hipStream_t s);
 
+// Packed-byte VALU dedispersion (wide-spread DM tiles), bit-identical to
+// dedisperse_direct.  d_offT: int32 [nactive][ldo] offsets of active channel
+// ci for DM column d_base + k (k < ndm rounded up to the workgroup's DM count,
+// padded columns must hold valid offsets); d_active: active channel indices.
+void dedisperse_valu(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_active, int nactive,
+                     const int32_t* d_offT, int ldo, int d_base, int ndm, uint64_t out_nsamps, uint8_t* out,
+                     uint64_t out_stride, float scale, int nbits, int bias, hipStream_t s);
+
 // ------------------------------------------------------------ time series ---
 void u8_sum(const uint8_t* in, uint64_t n, unsigned long long* sum, hipStream_t s);
 // out[i] = i < nvalid ? in[i] : (float)(sum / nvalid)

@@ -151,6 +151,141 @@ __global__ void __launch_bounds__(256) dedisperse_mfma_kernel(
   }
 }
 
+
+// ------------------------------------------------------------------ VALU ----
+// Packed-byte kernel for wide DM tiles (offset spread across the tile >> 16
+// samples, where the one-hot MFMA GEMM is mostly zeros).  Workgroup = 4 waves
+// = 4*DPT DMs x 1024 samples; lane = 16 consecutive samples, wave = DPT DMs.
+// Channel-outer / DM-inner: one channel's window (1024 + spread bytes) is
+// re-read by the workgroup's DMs straight from L1.  Per channel and DM a lane
+// loads 20 bytes (dwordx4 + dword at the dword-aligned offset) and v_perm
+// picks the even / odd bytes at the wave-uniform misalignment into two 16-bit
+// lanes, so one 32-bit add accumulates two samples.  Sums are of raw
+// (unbiased) bytes: x ^ 0x80 restores raw for bias-128 8-bit data.  16-bit
+// lanes hold max_raw * nactive <= 65535 (WIDE = false, nbits <= 4 at <= 4369
+// channels); otherwise they are flushed to 32-bit sums every 256 channels.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+template <int DPT, bool WIDE, bool XOR>
+__global__ void __launch_bounds__(256) dedisperse_valu_kernel(
+    const int8_t* __restrict__ x, uint64_t stride, const int32_t* __restrict__ active, int nactive,
+    const int32_t* __restrict__ offT, int ldo, int d_base, int ndm, uint64_t out_nsamps, uint8_t* __restrict__ out,
+    uint64_t out_stride, float scale) {
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int dm0 = blockIdx.x * (4 * DPT) + wave * DPT;  // relative to d_base
+  const uint64_t tb = static_cast<uint64_t>(blockIdx.y) * 1024;  // workgroup's first sample
+  const uint32_t lo = static_cast<uint32_t>(lane) * 16;          // lane's byte offset from tb
+  const uint64_t t = tb + lo;
+  uint32_t pk[DPT][8];
+  int wide[WIDE ? DPT : 1][WIDE ? 16 : 1];
+#pragma unroll
+  for (int j = 0; j < DPT; ++j)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) pk[j][q] = 0;
+  if constexpr (WIDE) {
+#pragma unroll
+    for (int j = 0; j < DPT; ++j)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) wide[j][q] = 0;
+  }
+  auto flush = [&]() {
+    if constexpr (WIDE) {
+#pragma unroll
+      for (int j = 0; j < DPT; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          wide[j][4 * i + 0] += pk[j][2 * i] & 0xFFFF;
+          wide[j][4 * i + 2] += pk[j][2 * i] >> 16;
+          wide[j][4 * i + 1] += pk[j][2 * i + 1] & 0xFFFF;
+          wide[j][4 * i + 3] += pk[j][2 * i + 1] >> 16;
+          pk[j][2 * i] = 0;
+          pk[j][2 * i + 1] = 0;
+        }
+    }
+  };
+  // Two register sets of 20-byte windows (A: even channels, B: odd): the next
+  // channel's DPT loads are in flight while this one's are accumulated.
+  u32x4 wa[DPT], wb[DPT];
+  uint32_t wa4[DPT], wb4[DPT];
+  uint32_t sha[DPT], shb[DPT];
+  auto load = [&](int ci, u32x4* w, uint32_t* w4, uint32_t* sh) {
+    // uniform row base (SGPRs) + 32-bit lane offset
+    const int8_t* row = x + static_cast<uint64_t>(active[ci]) * stride + tb;
+    const int32_t* o = offT + static_cast<uint64_t>(ci) * ldo + d_base + dm0;
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      const int off = o[j];
+      const int8_t* rb = row + (off & ~3);
+      w[j] = *reinterpret_cast<const u32x4_a4*>(rb + lo);
+      w4[j] = *reinterpret_cast<const uint32_t*>(rb + lo + 16);
+      sh[j] = static_cast<uint32_t>(off & 3);
+    }
+  };
+  auto accumulate = [&](u32x4* w, uint32_t* w4, const uint32_t* sh) {
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      if constexpr (XOR) {
+        w[j] ^= 0x80808080u;
+        w4[j] ^= 0x80808080u;
+      }
+      const uint32_t selE = 0x0C000C00u | sh[j] | ((sh[j] + 2) << 16);  // bytes sh, sh+2 -> 16-bit lanes
+      const uint32_t selO = selE + 0x00010001u;                        // bytes sh+1, sh+3
+      pk[j][0] += __builtin_amdgcn_perm(w[j][1], w[j][0], selE);
+      pk[j][1] += __builtin_amdgcn_perm(w[j][1], w[j][0], selO);
+      pk[j][2] += __builtin_amdgcn_perm(w[j][2], w[j][1], selE);
+      pk[j][3] += __builtin_amdgcn_perm(w[j][2], w[j][1], selO);
+      pk[j][4] += __builtin_amdgcn_perm(w[j][3], w[j][2], selE);
+      pk[j][5] += __builtin_amdgcn_perm(w[j][3], w[j][2], selO);
+      pk[j][6] += __builtin_amdgcn_perm(w4[j], w[j][3], selE);
+      pk[j][7] += __builtin_amdgcn_perm(w4[j], w[j][3], selO);
+    }
+  };
+  load(0, wa, wa4, sha);
+  int ci = 0;
+  for (; ci + 1 < nactive; ci += 2) {
+    load(ci + 1, wb, wb4, shb);
+    accumulate(wa, wa4, sha);
+    if (WIDE && (ci & 255) == 255) flush();
+    load(min(ci + 2, nactive - 1), wa, wa4, sha);  // branch-free (a spare reload at the end)
+    accumulate(wb, wb4, shb);
+    if (WIDE && ((ci + 1) & 255) == 255) flush();
+  }
+  if (ci < nactive) accumulate(wa, wa4, sha);  // odd count: A holds the last channel
+  flush();
+  if (t >= out_nsamps) return;
+#pragma unroll
+  for (int j = 0; j < DPT; ++j) {
+    const int d = dm0 + j;
+    if (d >= ndm) break;
+    uint32_t ob[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int s4[4];
+      if constexpr (WIDE) {
+        s4[0] = wide[j][4 * i];
+        s4[1] = wide[j][4 * i + 1];
+        s4[2] = wide[j][4 * i + 2];
+        s4[3] = wide[j][4 * i + 3];
+      } else {
+        s4[0] = static_cast<int>(pk[j][2 * i] & 0xFFFF);
+        s4[1] = static_cast<int>(pk[j][2 * i + 1] & 0xFFFF);
+        s4[2] = static_cast<int>(pk[j][2 * i] >> 16);
+        s4[3] = static_cast<int>(pk[j][2 * i + 1] >> 16);
+      }
+      ob[i] = static_cast<uint32_t>(scale_out(s4[0], scale)) | (static_cast<uint32_t>(scale_out(s4[1], scale)) << 8) |
+              (static_cast<uint32_t>(scale_out(s4[2], scale)) << 16) |
+              (static_cast<uint32_t>(scale_out(s4[3], scale)) << 24);
+    }
+    uint8_t* orow = out + static_cast<uint64_t>(d) * out_stride + t;
+    if (t + 16 <= out_nsamps) {
+      *reinterpret_cast<u32x4*>(orow) = u32x4{ob[0], ob[1], ob[2], ob[3]};
+    } else {
+      for (uint64_t e = 0; t + e < out_nsamps; ++e) orow[e] = static_cast<uint8_t>(ob[e >> 2] >> (8 * (e & 3)));
+    }
+  }
+}
+
 }  // namespace
 
 void dedisperse_direct(const int8_t* chan_major, uint64_t chan_stride, int nchans, const int32_t* offsets,
@@ -245,6 +380,37 @@ void dedisperse_mfma(const int8_t* chan_major, uint64_t chan_stride, const int32
                                                out, out_stride, scale,
                                                bias_total, ntt);
   post_launch_check("dedisperse_mfma_kernel", s);
+}
+
+void dedisperse_valu(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_active, int nactive,
+                     const int32_t* d_offT, int ldo, int d_base, int ndm, uint64_t out_nsamps, uint8_t* out,
+                     uint64_t out_stride, float scale, int nbits, int bias, hipStream_t s) {
+  if (ndm <= 0 || out_nsamps == 0 || nactive <= 0) return;
+  PSOUP_CHECK(bias == 0 || bias == 128, "dedisperse_valu: bias must be 0 or 128");
+  PSOUP_CHECK((chan_stride & 3) == 0 && (out_stride & 15) == 0, "dedisperse_valu: stride alignment");
+  const uint64_t max_raw = (1ull << std::min(nbits, 8)) - 1;
+  const bool wide = max_raw * static_cast<uint64_t>(nactive) > 65535;
+  const int dpt = wide ? 4 : 8;
+  const uint64_t ty = (out_nsamps + 1023) / 1024;
+  PSOUP_CHECK(ty <= 0x7FFFFFFF, "dedisperse_valu: series too long");
+  dim3 grid(static_cast<unsigned>((ndm + 4 * dpt - 1) / (4 * dpt)), static_cast<unsigned>(ty));
+  PSOUP_CHECK(d_base + static_cast<int>(grid.x) * 4 * dpt <= ldo, "dedisperse_valu: offset table too narrow");
+#define PSOUP_VALU_LAUNCH(D, W, X)                                                                            \
+  dedisperse_valu_kernel<D, W, X><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive, d_offT, ldo, \
+                                                       d_base, ndm, out_nsamps, out, out_stride, scale)
+  if (wide) {
+    if (bias == 128)
+      PSOUP_VALU_LAUNCH(4, true, true);
+    else
+      PSOUP_VALU_LAUNCH(4, true, false);
+  } else {
+    if (bias == 128)
+      PSOUP_VALU_LAUNCH(8, false, true);
+    else
+      PSOUP_VALU_LAUNCH(8, false, false);
+  }
+#undef PSOUP_VALU_LAUNCH
+  post_launch_check("dedisperse_valu_kernel", s);
 }
 
 }  // namespace kern

@@ -584,7 +584,8 @@ PYBIND11_MODULE(_C, m) {
   py::enum_<DedispKernel>(m, "DedispKernel")
       .value("Auto", DedispKernel::Auto)
       .value("Direct", DedispKernel::Direct)
-      .value("Mfma", DedispKernel::Mfma);
+      .value("Mfma", DedispKernel::Mfma)
+      .value("Valu", DedispKernel::Valu);
   py::class_<DedispGeometry>(m, "DedispGeometry")
       .def_static("make", [](const py::dict& hdr, uint64_t nsamps, const std::vector<float>& dms,
                              const std::vector<int>& kill) { return DedispGeometry::make(dict_to_header(hdr), nsamps, dms, kill); })
@@ -636,6 +637,8 @@ PYBIND11_MODULE(_C, m) {
       }, py::arg("d0"), py::arg("d1"), py::arg("out"), py::arg("out_stride"), py::arg("kind") = DedispKernel::Auto,
            py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>())
       .def_static("row_stride", &Dedisperser::row_stride)
+      .def("choose", &Dedisperser::choose, py::arg("d0"), py::arg("d1"))
+      .def("mfma_steps_per_channel", &Dedisperser::mfma_steps_per_channel, py::arg("d0"), py::arg("d1"))
       .def_property_readonly_static("tile_dms", [](py::object) { return Dedisperser::kTileDms; });
 
   py::class_<SearchParams>(m, "SearchParams")

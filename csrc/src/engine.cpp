@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <fstream>
@@ -18,7 +19,8 @@ DedispKernel parse_dedisp_kernel(const std::string& s) {
   if (s == "auto") return DedispKernel::Auto;
   if (s == "direct") return DedispKernel::Direct;
   if (s == "mfma") return DedispKernel::Mfma;
-  PSOUP_THROW("unknown dedispersion kernel '" << s << "' (auto|direct|mfma)");
+  if (s == "valu") return DedispKernel::Valu;
+  PSOUP_THROW("unknown dedispersion kernel '" << s << "' (auto|direct|mfma|valu)");
 }
 
 // ------------------------------------------------------------ geometry ------
@@ -123,7 +125,54 @@ void Dedisperser::build_resident_plan() {
   PSOUP_HIP_CHECK(hipMemcpy(r_deltas_.data(), plan.deltas.data(), plan.deltas.size(), hipMemcpyHostToDevice));
   PSOUP_HIP_CHECK(
       hipMemcpy(r_tile_info_.data(), plan.tile_info.data(), plan.tile_info.size() * 4, hipMemcpyHostToDevice));
+  h_tile_steps_.resize(static_cast<size_t>(plan.ntiles));
+  for (int T = 0; T < plan.ntiles; ++T) h_tile_steps_[T] = plan.tile_info[2 * T + 1];
   resident_ = true;
+}
+
+void Dedisperser::build_valu_tables() {
+  // offsets transposed to [active channel][DM], columns padded (with the last
+  // DM) past the last workgroup of any range
+  const auto& g = fb_.geometry();
+  const int ndm = static_cast<int>(g.dm_list.size());
+  std::vector<int32_t> offs = g.offsets(0, ndm);
+  std::vector<int> active;
+  for (int c = 0; c < g.nchans; ++c)
+    if (g.killmask[c]) active.push_back(c);
+  ldo_ = (ndm + kTileDms - 1) / kTileDms * kTileDms + kTileDms;
+  std::vector<int32_t> t(static_cast<size_t>(std::max<size_t>(1, active.size())) * ldo_, 0);
+  for (size_t ci = 0; ci < active.size(); ++ci)
+    for (int d = 0; d < ldo_; ++d)
+      t[ci * ldo_ + d] = offs[static_cast<size_t>(std::min(d, ndm - 1)) * g.nchans + active[ci]];
+  r_offT_.resize(t.size());
+  PSOUP_HIP_CHECK(hipMemcpy(r_offT_.data(), t.data(), t.size() * 4, hipMemcpyHostToDevice));
+  valu_ready_ = true;
+}
+
+static double valu_ratio() {
+  // MFMA steps per (tile, active channel) above which the VALU kernel is
+  // faster (calibrated on MI355X with tools/dedisp_bench.py)
+  static const double r = [] {
+    const char* e = std::getenv("PSOUP_DEDISP_VALU_RATIO");
+    return e ? std::atof(e) : 1.85;
+  }();
+  return r;
+}
+
+double Dedisperser::mfma_steps_per_channel(int d0, int d1) {
+  const auto& g = fb_.geometry();
+  PSOUP_CHECK(d0 >= 0 && d0 < d1 && d1 <= static_cast<int>(g.dm_list.size()), "bad DM range");
+  if (!resident_) build_resident_plan();
+  double steps = 0;
+  const int t0 = d0 / kTileDms, t1 = (d1 - 1) / kTileDms;
+  for (int T = t0; T <= t1; ++T) steps += h_tile_steps_[static_cast<size_t>(T)];
+  return steps / ((t1 - t0 + 1) * static_cast<double>(std::max(1, g.nactive)));
+}
+
+DedispKernel Dedisperser::choose(int d0, int d1) {
+  const auto& g = fb_.geometry();
+  if (g.nactive == 0 || d0 >= d1) return DedispKernel::Mfma;
+  return mfma_steps_per_channel(d0, d1) > valu_ratio() ? DedispKernel::Valu : DedispKernel::Mfma;
 }
 
 void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispKernel kind, hipStream_t s) {
@@ -132,8 +181,15 @@ void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispK
   if (d0 == d1) return;
   if (!s) s = stream_;
   RoctxRange r("Dedisperse");
-  if (kind == DedispKernel::Auto) kind = DedispKernel::Mfma;
+  if (kind == DedispKernel::Auto) kind = choose(d0, d1);
+  if (kind == DedispKernel::Valu && g.nactive == 0) kind = DedispKernel::Direct;
   const int ndm = d1 - d0;
+  if (kind == DedispKernel::Valu) {
+    if (!valu_ready_) build_valu_tables();
+    kern::dedisperse_valu(fb_.data(), fb_.stride(), d_active_.data(), g.nactive, r_offT_.data(), ldo_, d0, ndm,
+                          g.out_nsamps, out, out_stride, g.out_scale, g.nbits, g.bias, s);
+    return;
+  }
   const int ntiles = (ndm + kTileDms - 1) / kTileDms;
   const int ndm_all = static_cast<int>(g.dm_list.size());
   if (kind == DedispKernel::Mfma && d0 % kTileDms == 0 && (d1 % kTileDms == 0 || d1 == ndm_all)) {

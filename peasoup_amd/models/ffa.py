@@ -65,7 +65,8 @@ class RankFfa:
             else:
                 self.dfb.load_packed_host(packed.data_ptr())
         self.dedisperser = _C.Dedisperser(self.dfb, self.stream)
-        self.kernel = _C.DedispKernel.Mfma if args.dedisp_kernel in ("auto", "mfma") else _C.DedispKernel.Direct
+        self.kernel = {"auto": _C.DedispKernel.Auto, "mfma": _C.DedispKernel.Mfma, "valu": _C.DedispKernel.Valu,
+                       "direct": _C.DedispKernel.Direct}[args.dedisp_kernel]
         self.params = _C.ffa_params_from(args, float(header["tsamp"]))
         self.engine = _C.FfaEngine(self.params, int(self.geom.out_nsamps), self.stream)
         self.row_stride = _C.Dedisperser.row_stride(self.geom.out_nsamps)

@@ -94,7 +94,8 @@ class RankSearcher:
             self.load_packed(packed)
         self.dedisperser = _C.Dedisperser(self.dfb, self.stream)
         self.engine = _C.SearchEngine(self.params, self.stream)
-        self.kernel = _C.DedispKernel.Mfma if args.dedisp_kernel in ("auto", "mfma") else _C.DedispKernel.Direct
+        self.kernel = {"auto": _C.DedispKernel.Auto, "mfma": _C.DedispKernel.Mfma, "valu": _C.DedispKernel.Valu,
+                       "direct": _C.DedispKernel.Direct}[args.dedisp_kernel]
         self.row_stride = _C.Dedisperser.row_stride(self.geom.out_nsamps)
         self.accel_plan = _C.accel_plan_from_args(args, self.header)
         self._trials: Optional[torch.Tensor] = None

@@ -39,8 +39,11 @@ def _geometry(C, nchans=64, nbits=2, nsamps=6000, dm_end=200.0, tsamp=0.00032, f
     return hdr, dms
 
 
-@pytest.mark.parametrize("nbits,nchans,kill", [(2, 64, False), (8, 128, True), (4, 64, True)])
-def test_dedisperse_direct_and_mfma_bit_exact(C, nbits, nchans, kill):
+@pytest.mark.parametrize("nbits,nchans,kill", [(2, 64, False), (8, 128, True), (4, 64, True), (1, 64, False),
+                                               (8, 384, True)])
+def test_dedisperse_direct_mfma_valu_bit_exact(C, nbits, nchans, kill):
+    """Direct, one-hot MFMA and packed-byte VALU kernels vs the NumPy
+    reference; (8, 384) exercises the VALU kernel's 32-bit flush path."""
     rng = np.random.default_rng(7)
     hdr, dms = _geometry(C, nchans=nchans, nbits=nbits, nsamps=5000, dm_end=150.0)
     vals = rng.integers(0, 1 << nbits, size=(5000, nchans), dtype=np.uint8)
@@ -54,18 +57,20 @@ def test_dedisperse_direct_and_mfma_bit_exact(C, nbits, nchans, kill):
     ndm = len(dms)
     stride = C.Dedisperser.row_stride(g.out_nsamps)
     outs = {}
-    for k in (C.DedispKernel.Direct, C.DedispKernel.Mfma):
+    kinds = (C.DedispKernel.Direct, C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto)
+    for k in kinds:
         o = torch.zeros(ndm * stride, dtype=torch.uint8, device=dev)
         dd.run(0, ndm, o.data_ptr(), stride, k)
         outs[k] = o.view(ndm, stride)[:, : g.out_nsamps].cpu().numpy()
     offs = np.array(g.offsets(0, ndm), dtype=np.int32).reshape(ndm, nchans)
     exp = ref.dedisperse(vals, offs, nbits, killmask or None, g.out_nsamps)
-    assert np.array_equal(outs[C.DedispKernel.Direct], exp)
-    assert np.array_equal(outs[C.DedispKernel.Mfma], exp)
+    for k in kinds:
+        assert np.array_equal(outs[k], exp), k
     # sub-range (DM offset inside a tile)
-    o = torch.zeros(5 * stride, dtype=torch.uint8, device=dev)
-    dd.run(3, 8, o.data_ptr(), stride, C.DedispKernel.Mfma)
-    assert np.array_equal(o.view(5, stride)[:, : g.out_nsamps].cpu().numpy(), exp[3:8])
+    for k in (C.DedispKernel.Mfma, C.DedispKernel.Valu):
+        o = torch.zeros(5 * stride, dtype=torch.uint8, device=dev)
+        dd.run(3, 8, o.data_ptr(), stride, k)
+        assert np.array_equal(o.view(5, stride)[:, : g.out_nsamps].cpu().numpy(), exp[3:8]), k
 
 
 def test_mfma_resident_plan_ranges_and_side_stream(C):
@@ -89,11 +94,13 @@ def test_mfma_resident_plan_ranges_and_side_stream(C):
     side = torch.cuda.Stream()
     for d0, d1 in [(0, T), (T, 2 * T), (2 * T, ndm), (0, ndm), (T, T + 5), (5, 2 * T), (ndm - 3, ndm)]:
         o = torch.zeros((d1 - d0) * stride, dtype=torch.uint8, device=dev)
-        side.wait_stream(torch.cuda.current_stream())
-        dd.run(d0, d1, o.data_ptr(), stride, C.DedispKernel.Mfma, side.cuda_stream)
-        side.synchronize()
-        got = o.view(d1 - d0, stride)[:, : g.out_nsamps].cpu().numpy()
-        assert np.array_equal(got, exp[d0:d1]), (d0, d1)
+        for k in (C.DedispKernel.Mfma, C.DedispKernel.Valu):
+            o.zero_()
+            side.wait_stream(torch.cuda.current_stream())
+            dd.run(d0, d1, o.data_ptr(), stride, k, side.cuda_stream)
+            side.synchronize()
+            got = o.view(d1 - d0, stride)[:, : g.out_nsamps].cpu().numpy()
+            assert np.array_equal(got, exp[d0:d1]), (d0, d1, k)
 
 
 def test_convert_pad_and_truncate():
