@@ -45,6 +45,7 @@ struct CmdLineOptions {
   std::string accel_convention = "legacy";  // legacy | reference
   std::string dedisp_kernel = "auto";       // auto | mfma | direct
   int accel_batch = 0;                      // 0 = auto (sized for HBM)
+  int engines_per_gpu = 0;                  // search engines (streams + host threads) per GPU, 0 = auto
   int sub_batch = -1;                       // -1 = auto
   int fft_mode = 2;                         // see SearchParams::fft_mode
   bool use_boundaries = false;              // honour --boundary_* (reference ignores them)

@@ -179,6 +179,7 @@ class SearchEngine {
   int batch_size() const { return K_; }
   int sub_batch() const { return sub_; }
   int fft_mode() const { return mode_; }
+  hipStream_t stream() const { return stream_; }
   float tobs() const { return tobs_; }
   // Debug access to the whitened series of the last trial.
   const float* whitened() const { return tim_.data(); }

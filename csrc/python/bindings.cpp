@@ -343,6 +343,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("accel_convention", &CmdLineOptions::accel_convention)
       .def_readwrite("dedisp_kernel", &CmdLineOptions::dedisp_kernel)
       .def_readwrite("accel_batch", &CmdLineOptions::accel_batch)
+      .def_readwrite("engines_per_gpu", &CmdLineOptions::engines_per_gpu)
       .def_readwrite("sub_batch", &CmdLineOptions::sub_batch)
       .def_readwrite("fft_mode", &CmdLineOptions::fft_mode)
       .def_readwrite("use_boundaries", &CmdLineOptions::use_boundaries)
@@ -670,6 +671,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("batch_size", &SearchEngine::batch_size)
       .def_property_readonly("sub_batch", &SearchEngine::sub_batch)
       .def_property_readonly("fft_mode", &SearchEngine::fft_mode)
+      .def_property_readonly("stream", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.stream()); })
       .def_property_readonly("tobs", &SearchEngine::tobs)
       .def_property_readonly("whitened_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.whitened()); })
       .def_property_readonly("stats_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.whitener().stats()); })

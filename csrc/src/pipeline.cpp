@@ -8,6 +8,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <iostream>
 #include <mutex>
@@ -210,19 +211,59 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   };
   std::vector<DevState> devs(static_cast<size_t>(ngpu));
 
+  // Search engines per GPU: each has its own stream, dedispersion side stream
+  // and host thread, and pulls DM chunks from the shared queue, so one
+  // engine's small per-DM kernels and host distillation overlap another's.
+  int neng = args.engines_per_gpu;
+  if (const char* e = std::getenv("PSOUP_ENGINES")) neng = std::max(neng, std::atoi(e));
+  if (neng <= 0) {
+    size_t mx = 0;
+    for (float dm : setup.dm_list) mx = std::max(mx, setup.accel_plan.generate(dm).size());
+    neng = mx < 128 ? 3 : 1;
+  }
+  res.performance["engines_per_gpu"] = neng;
+
   t_search.start();
-  auto worker = [&](int dev) {
+  // phase 1: resident filterbank per device
+  {
+    std::vector<std::thread> lth;
+    for (int dev = 0; dev < ngpu; ++dev)
+      lth.emplace_back([&, dev] {
+        try {
+          PSOUP_HIP_CHECK(hipSetDevice(dev));
+          DevState& ds = devs[static_cast<size_t>(dev)];
+          Stopwatch wl;
+          wl.start();
+          ds.stream = std::make_unique<Stream>();
+          ds.dfb = std::make_unique<DeviceFilterbank>(geom, ds.stream->get());
+          ds.dfb->load_packed_host(fb.data());
+          ds.dd = std::make_unique<Dedisperser>(*ds.dfb, ds.stream->get());
+          PSOUP_HIP_CHECK(hipStreamSynchronize(ds.stream->get()));
+          wl.stop();
+          std::lock_guard<std::mutex> lk(sh.mu);
+          sh.dev_stats[static_cast<size_t>(dev)]["load_s"] = wl.get_time();
+        } catch (...) {
+          std::lock_guard<std::mutex> lk(sh.mu);
+          if (!sh.error) sh.error = std::current_exception();
+        }
+      });
+    for (auto& t : lth) t.join();
+    if (sh.error) std::rethrow_exception(sh.error);
+  }
+  // phase 2: neng engines per device
+  auto worker = [&](int dev, int slot) {
     try {
       PSOUP_HIP_CHECK(hipSetDevice(dev));
       DevState& ds = devs[static_cast<size_t>(dev)];
-      ds.stream = std::make_unique<Stream>();
-      hipStream_t st = ds.stream->get();
+      std::unique_ptr<Stream> own_stream;
+      std::unique_ptr<Dedisperser> own_dd;
+      if (slot > 0) {
+        own_stream = std::make_unique<Stream>();
+        own_dd = std::make_unique<Dedisperser>(*ds.dfb, own_stream->get());
+      }
+      hipStream_t st = slot > 0 ? own_stream->get() : ds.stream->get();
+      Dedisperser* dd = slot > 0 ? own_dd.get() : ds.dd.get();
       Stopwatch wd, ws;
-      wd.start();
-      ds.dfb = std::make_unique<DeviceFilterbank>(geom, st);
-      ds.dfb->load_packed_host(fb.data());
-      ds.dd = std::make_unique<Dedisperser>(*ds.dfb, st);
-      wd.stop();
       SearchEngine engine(setup.search, st);
       const uint64_t rstride = Dedisperser::row_stride(geom.out_nsamps);
       // Double-buffered: the next chunk is dedispersed on a side stream while
@@ -246,7 +287,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
         const int d1 = std::min(sh.ndm, d0 + sh.chunk);
         if (used[k]) PSOUP_HIP_CHECK(hipStreamWaitEvent(dstream.get(), freed[k].get(), 0));
         began[k].record(dstream.get());
-        ds.dd->run(d0, d1, trials[k].data(), rstride, setup.dedisp_kernel, dstream.get());
+        dd->run(d0, d1, trials[k].data(), rstride, setup.dedisp_kernel, dstream.get());
         ready[k].record(dstream.get());
         pending[k] = true;
       };
@@ -299,18 +340,19 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
       PSOUP_HIP_CHECK(hipStreamSynchronize(dstream.get()));
       PSOUP_HIP_CHECK(hipStreamSynchronize(st));
       wd.add(dd_ms * 1e-3);  // GPU time of the (overlapped) dedispersion kernels
-      sh.dedisp_s[static_cast<size_t>(dev)] = wd.get_time();
-      sh.search_s[static_cast<size_t>(dev)] = ws.get_time();
       const SearchCounters& c = engine.counters();
+      std::lock_guard<std::mutex> lk(sh.mu);
+      sh.dedisp_s[static_cast<size_t>(dev)] += wd.get_time();
+      sh.search_s[static_cast<size_t>(dev)] += ws.get_time();
       auto& st_map = sh.dev_stats[static_cast<size_t>(dev)];
-      st_map["dedispersion_s"] = wd.get_time();
-      st_map["search_s"] = ws.get_time();
-      st_map["dm_trials"] = static_cast<double>(c.dm_trials);
-      st_map["accel_trials"] = static_cast<double>(c.accel_trials);
-      st_map["peaks"] = static_cast<double>(c.peaks);
-      st_map["peak_overflows"] = static_cast<double>(c.overflows);
-      st_map["accel_loop_s"] = c.accel_s;
-      st_map["host_distill_s"] = c.host_s;
+      st_map["dedispersion_s"] += wd.get_time();  // summed over the device's engines
+      st_map["search_s"] += ws.get_time();
+      st_map["dm_trials"] += static_cast<double>(c.dm_trials);
+      st_map["accel_trials"] += static_cast<double>(c.accel_trials);
+      st_map["peaks"] += static_cast<double>(c.peaks);
+      st_map["peak_overflows"] += static_cast<double>(c.overflows);
+      st_map["accel_loop_s"] += c.accel_s;
+      st_map["host_distill_s"] += c.host_s;
       st_map["fft_mode"] = engine.fft_mode();
       st_map["accel_batch"] = engine.batch_size();
       st_map["sub_batch"] = engine.sub_batch();
@@ -321,7 +363,8 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     }
   };
   std::vector<std::thread> threads;
-  for (int d = 0; d < ngpu; ++d) threads.emplace_back(worker, d);
+  for (int d = 0; d < ngpu; ++d)
+    for (int e = 0; e < neng; ++e) threads.emplace_back(worker, d, e);
   for (auto& t : threads) t.join();
   t_search.stop();
   if (args.progress_bar) progress.stop();

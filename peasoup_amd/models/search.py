@@ -23,9 +23,11 @@ include/transforms/folder.hpp:337-442 (MultiFolder).
 """
 from __future__ import annotations
 
+import concurrent.futures
 import json
 import os
 import struct
+import threading
 import time
 import warnings
 from dataclasses import dataclass, field
@@ -55,15 +57,28 @@ class SearchResult:
 _SYNC_DEDISP = os.environ.get("PSOUP_SYNC_DEDISP", "0") == "1"  # debug: no dedispersion/search overlap
 
 
-_ENGINE_STREAMS: Dict[int, object] = {}  # device index -> _C.GpuStream, alive for the process
+_ENGINE_STREAMS: Dict[tuple, object] = {}  # (device index, slot) -> _C.GpuStream, alive for the process
 
 
-def _engine_stream(device: torch.device) -> int:
+def _engine_stream(device: torch.device, slot: int = 0) -> int:
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    if idx not in _ENGINE_STREAMS:
+    if (idx, slot) not in _ENGINE_STREAMS:
         with torch.cuda.device(idx):
-            _ENGINE_STREAMS[idx] = _C.GpuStream()
-    return _ENGINE_STREAMS[idx].handle
+            _ENGINE_STREAMS[(idx, slot)] = _C.GpuStream()
+    return _ENGINE_STREAMS[(idx, slot)].handle
+
+
+def engines_per_gpu(args, max_trials_per_dm: int) -> int:
+    """Search engines per GPU (each on its own stream, fed by its own host
+    thread): DM trials of a chunk are dealt round-robin so one engine's small
+    per-DM kernels (whitening, short acceleration batches) and host
+    distillation overlap the others'.  Auto: 3 when DMs carry fewer than 128
+    acceleration trials (config 4: 1.6x the search throughput), else 1 (long
+    batches already fill the GPU; a second engine costs ~2% at 684 trials)."""
+    v = int(os.environ.get("PSOUP_ENGINES", "0") or 0) or int(getattr(args, "engines_per_gpu", 0) or 0)
+    if v <= 0:
+        v = 3 if max_trials_per_dm < 128 else 1
+    return max(1, v)
 
 
 class RankSearcher:
@@ -98,6 +113,10 @@ class RankSearcher:
                        "direct": _C.DedispKernel.Direct}[args.dedisp_kernel]
         self.row_stride = _C.Dedisperser.row_stride(self.geom.out_nsamps)
         self.accel_plan = _C.accel_plan_from_args(args, self.header)
+        max_trials = max((len(self.accel_list(d)) for d in self.dm_list), default=0)
+        self.engines = [self.engine] + [_C.SearchEngine(self.params, _engine_stream(self.ctx.device, i))
+                                        for i in range(1, engines_per_gpu(args, max_trials))]
+        self._pool = None
         self._trials: Optional[torch.Tensor] = None
 
     def load_packed(self, packed: torch.Tensor) -> None:
@@ -167,8 +186,8 @@ class RankSearcher:
             k = len(issued) % nbuf
             d0, d1 = blocks[j]
             start, ready = _C.GpuEvent(True), _C.GpuEvent(True)
-            if freed[k] is not None:
-                freed[k].wait(side.handle)
+            for ev in freed[k] or ():
+                ev.wait(side.handle)
             start.record(side.handle)
             with roctx_range("Dedisperse"):
                 self.dedisperser.run(d0, d1, bufs[k].data_ptr(), self.row_stride, self.kernel, side.handle)
@@ -178,6 +197,7 @@ class RankSearcher:
             issued[j] = (k, ready, start)
 
         dd_events = []
+        lock = threading.Lock()
         if todo:
             issue(todo[0])
         if t_s:
@@ -198,23 +218,45 @@ class RankSearcher:
             if nxt < len(todo):
                 issue(todo[nxt])  # overlaps the search below
                 nxt += 1
-            ready.wait(self.stream)
+            for e in self.engines:
+                ready.wait(e.stream)
             dd_events.append((start, ready))
+            per_dm: Dict[int, list] = {}
+
+            def run_dms(e, dms):
+                nonlocal processed, ntrials
+                for d in dms:
+                    with lock:
+                        if 0 <= fault_after <= processed:
+                            raise RuntimeError(f"fault injection: rank {self.ctx.rank} aborting after "
+                                               f"{processed} DM trials")
+                        processed += 1
+                    dm = self.dm_list[d]
+                    accs = self.accel_list(dm)
+                    addr = bufs[k].data_ptr() + (d - d0) * self.row_stride
+                    per_dm[d] = e.search_trial(addr, self.geom.out_nsamps, dm, d, accs)
+                    with lock:
+                        ntrials += len(accs)
+                        if progress is not None:
+                            progress(1)
+
+            ne = len(self.engines)
+            if ne == 1:
+                run_dms(self.engine, range(d0, d1))
+            else:
+                futs = [self._executor().submit(run_dms, e, range(d0 + j, d1, ne))
+                        for j, e in enumerate(self.engines)]
+                for f in futs:
+                    f.result()
             chunk_cands: list = []
             for d in range(d0, d1):
-                if 0 <= fault_after <= processed:
-                    raise RuntimeError(f"fault injection: rank {self.ctx.rank} aborting after {processed} DM trials")
-                dm = self.dm_list[d]
-                accs = self.accel_list(dm)
-                ntrials += len(accs)
-                addr = bufs[k].data_ptr() + (d - d0) * self.row_stride
-                chunk_cands.extend(self.engine.search_trial(addr, self.geom.out_nsamps, dm, d, accs))
-                processed += 1
-                if progress is not None:
-                    progress(1)
-            ev = _C.GpuEvent()
-            ev.record(self.stream)
-            freed[k] = ev
+                chunk_cands.extend(per_dm[d])
+            evs = []
+            for e in self.engines:
+                ev = _C.GpuEvent()
+                ev.record(e.stream)
+                evs.append(ev)
+            freed[k] = evs
             if ck:
                 os.makedirs(ckdir, exist_ok=True)
                 tmp = ck + f".tmp{self.ctx.rank}"
@@ -223,13 +265,27 @@ class RankSearcher:
                 os.replace(tmp, ck)
             cands.extend(chunk_cands)
         side.synchronize()
-        _C.stream_synchronize(self.stream)
+        for e in self.engines:
+            _C.stream_synchronize(e.stream)
         if t_s:
             t_s.stop()
         if t_dd and dd_events:
             t_dd.add(sum(a.elapsed_ms(b) for a, b in dd_events) * 1e-3)
         self.accel_trials = ntrials
         return cands
+
+    def _executor(self):
+        if self._pool is None:
+            self._pool = concurrent.futures.ThreadPoolExecutor(len(self.engines), thread_name_prefix="psoup-eng")
+        return self._pool
+
+    def counters(self) -> Dict[str, float]:
+        """Engine counters summed over this rank's engines."""
+        out: Dict[str, float] = {}
+        for e in self.engines:
+            for key, v in dict(e.counters()).items():
+                out[key] = out.get(key, 0) + v
+        return out
 
     def fold(self, groups: Dict[int, List[int]], cands: list) -> Dict[int, tuple]:
         """Fold candidates (index -> (folded_snr, opt_period, fold)) for the DM groups given."""
@@ -323,7 +379,7 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     torch.cuda.synchronize()
     search_wall = time.perf_counter() - t0
     local_trials = sum(weights[i] for i in shard)
-    rank_stats = dict(rs.engine.counters())
+    rank_stats = rs.counters()
     rank_stats.update({"rank": ctx.rank, "search_s": search_wall, "accel_trials_planned": local_trials,
                        "fft_mode": rs.engine.fft_mode, "accel_batch": rs.engine.batch_size,
                        "sub_batch": rs.engine.sub_batch,

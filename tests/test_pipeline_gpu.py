@@ -178,3 +178,25 @@ def test_trace_json_cli_and_python(C, tmp_path):
     d2 = json.loads(tp.read_text())
     assert d2["devices"][0]["accel_trials"] == d["performance"]["dm_accel_trials"]
     assert d2["config"]["ndm"] == d["config"]["ndm"]
+
+
+def test_engines_per_gpu_do_not_change_results(tmp_path):
+    """1 vs 3 search engines per GPU (native CLI and Python driver): the
+    candidate files are byte-identical."""
+    exe = os.path.join(REPO, "bin", "peasoup")
+    outs = []
+    for n in (1, 3):
+        d = tmp_path / f"cli{n}"
+        r = subprocess.run([exe, "-i", TUTORIAL, "-o", str(d), "--engines_per_gpu", str(n)] + GOLDEN_ARGS,
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr
+        outs.append((d / "candidates.peasoup").read_bytes())
+    for n in (1, 3):
+        d = tmp_path / f"py{n}"
+        env = dict(os.environ, PYTHONPATH=REPO)
+        r = subprocess.run([sys.executable, "-m", "peasoup_amd", "-i", TUTORIAL, "-o", str(d), "--engines_per_gpu",
+                            str(n)] + GOLDEN_ARGS, capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
+        assert r.returncode == 0, r.stderr
+        outs.append((d / "candidates.peasoup").read_bytes())
+    assert outs[0] == outs[1]
+    assert outs[2] == outs[3]
