@@ -131,25 +131,50 @@ struct SearchParams {
 // Running-median whitening of one N-point series, in place.
 class Whitener {
  public:
-  Whitener(uint64_t n, float tsamp, hipStream_t stream);
+  // allow_fft4: run the N-point real transforms on the four-step FFT passes
+  // (K = 1) when the geometry allows; otherwise (or when false) rocFFT.
+  Whitener(uint64_t n, float tsamp, hipStream_t stream, bool allow_fft4 = true);
   // trial u8[nsamps] -> d_series f32[n] (pad with mean / truncate)
   void load_trial(const uint8_t* d_trial, uint64_t nsamps, float* d_series);
   // R2C, running median, deredden (+zap), [interbin stats], C2R in place.
   void whiten(float* d_series, const uint32_t* d_zapmask, bool with_stats, float boundary5, float boundary25);
+  // load_trial + whiten (with stats) for `count` trials in one batch: trial b
+  // at d_trials + b*row_stride -> d_out + b*out_stride, its interbin stats
+  // {mean, rms, std} at d_stats + 4b.  The forward and inverse transforms run
+  // as one K = count four-step FFT each (rocFFT per trial without fft4).
+  void whiten_batch(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count, float* d_out,
+                    uint64_t out_stride, const uint32_t* d_zapmask, float* d_stats, float boundary5,
+                    float boundary25);
+  // device bytes whiten_batch holds per trial of its largest batch
+  uint64_t batch_bytes_per_trial() const;
+  // Unnormalised N-point R2C (n/2+1 bins) and C2R, as rocFFT's.
+  void forward(const float* d_series, float2* d_spec);
+  void inverse(const float2* d_spec, float* d_series);
   // Forward spectrum of the (whitened) series is left in spectrum() until the next call.
   float2* spectrum() const { return fser_.data(); }
   const float* stats() const { return stats_.data(); }  // {mean, rms, std} of the interbin spectrum
   uint64_t n() const { return n_; }
   uint64_t nbins() const { return n_ / 2 + 1; }
   float bin_width() const { return bin_width_; }
-  FftPlan& r2c() { return *r2c_; }
-  FftPlan& c2r() { return *c2r_; }
+  bool uses_fft4() const { return f4_; }
 
  private:
+  FftPlan& r2c();
+  FftPlan& c2r();
   uint64_t n_;
   float tsamp_, bin_width_;
   hipStream_t stream_;
-  std::unique_ptr<FftPlan> r2c_, c2r_;
+  std::unique_ptr<FftPlan> r2c_, c2r_;  // rocFFT, created on first use
+  void ensure_batch(int count);
+  void dered_stats(float2* spec, const uint32_t* d_zapmask, float* d_stats, float boundary5, float boundary25);
+  bool f4_ = false;
+  kern::Fft4Geom g4_;
+  int bcap_ = 0;  // trials the fft4 batch buffers hold
+  DeviceBuffer<float2> tab4_, y4_, x4_, tmp4_;
+  DeviceBuffer<float> in4_;
+  DeviceBuffer<double> af0_;
+  DeviceBuffer<float2> bspec_;
+  DeviceBuffer<unsigned long long> bsum_;
   DeviceBuffer<float2> fser_;
   DeviceBuffer<float> m5_, m25_, m125_;
   DeviceBuffer<double> partials_;
@@ -173,6 +198,12 @@ class SearchEngine {
   // returns the acceleration-distilled candidates of this DM.
   CandidateList search_trial(const uint8_t* d_trial, uint64_t nsamps, float dm, int dm_idx,
                              const std::vector<float>& accs);
+  // Batched front end: whiten `count` (<= max_prepare()) trials at d_trials +
+  // b*row_stride in one batch, then search each with search_prepared(b, ...).
+  // search_trial = prepare(trial, 0, nsamps, 1) + search_prepared(0, ...).
+  void prepare(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count);
+  CandidateList search_prepared(int b, float dm, int dm_idx, const std::vector<float>& accs);
+  int max_prepare() const { return max_prep_; }
   const SearchParams& params() const { return p_; }
   const SearchCounters& counters() const { return ctr_; }
   void reset_counters() { ctr_ = SearchCounters(); }
@@ -181,8 +212,9 @@ class SearchEngine {
   int fft_mode() const { return mode_; }
   hipStream_t stream() const { return stream_; }
   float tobs() const { return tobs_; }
-  // Debug access to the whitened series of the last trial.
-  const float* whitened() const { return tim_.data(); }
+  // Debug access to the whitened series / interbin stats of the last searched trial.
+  const float* whitened() const { return cur_tim_; }
+  const float* trial_stats() const { return cur_stats_; }
   const Whitener& whitener() const { return *wh_; }
 
  private:
@@ -218,13 +250,18 @@ class SearchEngine {
   std::vector<PeakBounds> bounds_;
   int hi_ = 0;
   std::unique_ptr<Whitener> wh_;
-  DeviceBuffer<float> tim_;
+  DeviceBuffer<float> tim_;    // whitened series of the prepared trials [max_prep_][n_]
+  DeviceBuffer<float> wstats_; // their interbin stats [max_prep_][4]
+  int prepared_ = 0, max_prep_ = 1;
+  const float* cur_tim_ = nullptr;  // trial being searched
+  const float* cur_pad_ = nullptr;
+  const float* cur_stats_ = nullptr;
   DeviceBuffer<uint32_t> zapmask_;
   bool zap_ = false;
   int mode_ = 2;        // effective fft_mode
   kern::Fft4Geom f4_;
   DeviceBuffer<float2> f4_tab_;
-  DeviceBuffer<float> f4_in_;  // padded whitened series read by the fused FFT
+  DeviceBuffer<float> f4_in_;  // padded whitened series read by the fused FFT [max_prep_][insize]
   uint64_t xs_ = 0;     // per-trial stride of spec_ (complex)
   DeviceBuffer<float> res_;
   DeviceBuffer<float2> spec_;
@@ -278,7 +315,12 @@ class FoldEngine {
   float tsamp_;
   hipStream_t stream_;
   std::unique_ptr<Whitener> wh_;
-  DeviceBuffer<float> tim_;
+  DeviceBuffer<float> tim_;    // whitened series of the prepared trials [max_prep_][n_]
+  DeviceBuffer<float> wstats_; // their interbin stats [max_prep_][4]
+  int prepared_ = 0, max_prep_ = 1;
+  const float* cur_tim_ = nullptr;  // trial being searched
+  const float* cur_pad_ = nullptr;
+  const float* cur_stats_ = nullptr;
   DeviceBuffer<float2> shift_table_;
   DeviceBuffer<kern::FoldJob> jobs_;
   DeviceBuffer<float> psum_, folds_, opt_fold_, opt_prof_, opt_val_;

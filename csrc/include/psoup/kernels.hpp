@@ -79,10 +79,12 @@ void dedisperse_valu(const int8_t* chan_major, uint64_t chan_stride, const int32
                      uint64_t out_stride, float scale, int nbits, int bias, hipStream_t s);
 
 // ------------------------------------------------------------ time series ---
-void u8_sum(const uint8_t* in, uint64_t n, unsigned long long* sum, hipStream_t s);
+// count > 1: rows b at in + b*in_stride, sums sum[b], outputs out + b*out_stride.
+void u8_sum(const uint8_t* in, uint64_t n, unsigned long long* sum, hipStream_t s, int count = 1,
+            uint64_t in_stride = 0);
 // out[i] = i < nvalid ? in[i] : (float)(sum / nvalid)
 void u8_to_f32_pad(const uint8_t* in, uint64_t nvalid, float* out, uint64_t n, const unsigned long long* sum,
-                   hipStream_t s);
+                   hipStream_t s, int count = 1, uint64_t in_stride = 0, uint64_t out_stride = 0);
 void f32_stats(const float* x, uint64_t n, double* partials, int npartials, float* stats_out, hipStream_t s);
 
 // ----------------------------------------------------------------- spectra --
@@ -144,12 +146,17 @@ struct Fft4Geom {
   int log2_xrow = 0;                 // log2(n2): X index of bin k = (k >> log2_xrow)*xpitch + (k & (n2-1))
   uint64_t inpitch = 0, insize = 0;  // floats: padded input copy
   bool ok = false;
+  // Pass A input per trial k: in + k*in_tstride, in_pad + k*pad_tstride
+  // (0 = every trial resamples the same series; the batched whitener sets n, insize).
+  uint64_t in_tstride = 0, pad_tstride = 0;
 };
 Fft4Geom fft4_geometry(uint64_t M);
 // Twiddle tables (upload once per plan): see fft4step.hip for the layout.
 std::vector<float2> fft4_tables(const Fft4Geom& g);
 // Padded copy of the (whitened) input series read by pass A; insize floats.
-void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& g, hipStream_t s);
+// count > 1: series b at in + b*in_stride -> in_pad + b*g.insize.
+void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& g, hipStream_t s, int count = 1,
+                    uint64_t in_stride = 0);
 // Pass A: Y[k][k2][i] = W_M^{i k2} sum_j z_k[n1 j + i] W_n2^{j k2}, where
 // z_k[m] = x_k[2m] + i x_k[2m+1] and x_k = resampleII(in, af[k]); n = 2M.
 void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
@@ -176,6 +183,37 @@ struct Fft4XLayout {
   bool tiled;  // kFft4TileX: use r2c_interbin_normalise_tiled
 };
 Fft4XLayout fft4_x_layout(const Fft4Geom& g);
+// Whitening real FFTs on the four-step passes (K = 1): spectrum layout of
+// fft4_rowpass as kernel arguments; natural-order half spectrum <-> pass data.
+struct XLayoutArgs {
+  int tiled;           // kFft4TileX layout (taddr) else blocked/natural (zaddr)
+  int log2_row;        // tiled: log2(n2)
+  uint64_t n1;         // tiled
+  uint64_t row_pitch, blk_pitch;
+  int log2_blk;
+};
+inline XLayoutArgs xlayout_args(const Fft4Geom& g, const Fft4XLayout& l) {
+  XLayoutArgs a{};
+  a.tiled = l.tiled ? 1 : 0;
+  a.log2_row = l.tiled ? g.log2_xrow : l.log2_row;
+  a.n1 = static_cast<uint64_t>(g.n1);
+  a.row_pitch = l.row_pitch;
+  a.blk_pitch = l.blk_pitch;
+  a.log2_blk = l.log2_blk;
+  return a;
+}
+// X[k] (k = 0..M, natural) of the N = 2M real series whose half-length FFT Z
+// (layout L) fft4_rowpass produced.
+// Batched (count transforms): Z + b*zstride -> X + b*xstride (and likewise below).
+void fft4_r2c_half(const float2* Z, uint64_t M, const XLayoutArgs& L, float2* X, hipStream_t s, int count = 1,
+                   uint64_t zstride = 0, uint64_t xstride = 0);
+// Natural-order M complex values whose forward FFT is the conjugate of the
+// unnormalised C2R of X[0..M] (as pairs x[2m] + i x[2m+1]).
+void fft4_c2r_pre(const float2* X, uint64_t M, float2* out, hipStream_t s, int count = 1, uint64_t xstride = 0,
+                  uint64_t ostride = 0);
+// x[2m] + i x[2m+1] = conj(Z[m]) (Z in layout L): the N-point unnormalised C2R.
+void fft4_c2r_post(const float2* Z, uint64_t M, const XLayoutArgs& L, float* x, hipStream_t s, int count = 1,
+                   uint64_t zstride = 0, uint64_t ostride = 0);
 // Tuning switches (process-wide, for measurement): kernel shape and store policy.
 enum Fft4Flags : int {
   kFft4Cpt8 = 1,         // 8 transforms per thread, one thread group (else 4 per thread, two groups)

@@ -320,7 +320,9 @@ __device__ __forceinline__ uint32_t logical_block(uint32_t nblocks, bool remap) 
 // channels instead of one.
 __global__ void __launch_bounds__(256) fft4_pad_input_kernel(const float* __restrict__ in, uint64_t n,
                                                              float* __restrict__ out, uint64_t rowlen,
-                                                             uint64_t pitch, uint64_t total) {
+                                                             uint64_t pitch, uint64_t total, uint64_t in_stride) {
+  in += blockIdx.y * in_stride;
+  out += blockIdx.y * total;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t u = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; u < total; u += stride) {
     const uint64_t row = u / pitch, r = u - row * pitch;
@@ -385,8 +387,9 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
 #pragma unroll
       for (int e = 0; e < 2 * CPT; ++e) x[e] = static_cast<float>(j + e);
     } else {
-      load_resampled<2 * CPT>(in, in_pad, n, log2row, g.inpitch, af, size, 2 * (static_cast<uint64_t>(N1) * j + c0),
-                              x);
+      load_resampled<2 * CPT>(in + static_cast<uint64_t>(k) * g.in_tstride,
+                              in_pad + static_cast<uint64_t>(k) * g.pad_tstride, n, log2row, g.inpitch, af, size,
+                              2 * (static_cast<uint64_t>(N1) * j + c0), x);
     }
 #pragma unroll
     for (int c = 0; c < CPT; ++c) v[c][q] = make_float2(x[2 * c], x[2 * c + 1]);
@@ -582,10 +585,11 @@ std::vector<float2> fft4_tables(const Fft4Geom& g) {
   return t;
 }
 
-void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& g, hipStream_t s) {
-  PSOUP_CHECK(g.ok && n == 2ull * g.n1 * g.n2, "fft4 pad: bad geometry");
-  fft4_pad_input_kernel<<<dev::grid_for(g.insize, 256, 4096), 256, 0, s>>>(in, n, in_pad, 2ull * g.n1, g.inpitch,
-                                                                          g.insize);
+void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& g, hipStream_t s, int count,
+                    uint64_t in_stride) {
+  PSOUP_CHECK(count >= 1 && count <= 65535, "fft4_pad_input: bad count");
+  const dim3 grid(dev::grid_for(g.insize, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
+  fft4_pad_input_kernel<<<grid, 256, 0, s>>>(in, n, in_pad, 2ull * g.n1, g.inpitch, g.insize, in_stride);
   post_launch_check("fft4_pad_input_kernel", s);
 }
 

@@ -502,6 +502,59 @@ __global__ void __launch_bounds__(256) harmonic_sums_kernel(const float* __restr
   }
 }
 
+// ------------------------------------------------ whitening real FFTs ----
+// The whitener's N-point real transforms on the four-step passes (K = 1):
+//   forward: z[m] = x[2m] + i x[2m+1] -> Z = FFT_M(z) (passes A+B, spectrum
+//            layout L) -> X[k] = r2c_combine(Z[k], Z[M-k]), k = 0..M, natural;
+//   inverse: Z'[k] = conj((X[k] + conj X[M-k]) + i W^k (X[k] - conj X[M-k])),
+//            W = e^{2 pi i/N}; passes A+B give FFT_M(Z') = conj(N-unnormalised
+//            IFFT_M), so x[2m] + i x[2m+1] = conj(out[m]) (rocFFT C2R scale).
+__device__ __forceinline__ uint64_t xaddr(uint64_t k, const XLayoutArgs& L) {
+  return L.tiled ? taddr(k, L.log2_row, L.n1) : zaddr(k, L.log2_row, L.row_pitch, L.blk_pitch, L.log2_blk);
+}
+
+__global__ void __launch_bounds__(256) r2c_half_kernel(const float2* __restrict__ Z, uint64_t M, XLayoutArgs L,
+                                                       float2* __restrict__ X, uint64_t zstride, uint64_t xstride) {
+  Z += blockIdx.y * zstride;
+  X += blockIdx.y * xstride;
+  for (uint64_t k = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; k <= M;
+       k += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const float2 za = Z[xaddr(k & (M - 1), L)];
+    const float2 zb = Z[xaddr((M - k) & (M - 1), L)];
+    float sn, cs;
+    sincospif(-static_cast<float>(k) / static_cast<float>(M), &sn, &cs);
+    X[k] = r2c_combine(za, zb, cs, sn);
+  }
+}
+
+__global__ void __launch_bounds__(256) c2r_pre_kernel(const float2* __restrict__ X, uint64_t M,
+                                                      float2* __restrict__ out, uint64_t xstride, uint64_t ostride) {
+  X += blockIdx.y * xstride;
+  out += blockIdx.y * ostride;
+  for (uint64_t k = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; k < M;
+       k += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const float2 a = X[k], b = X[M - k];
+    const float ex = a.x + b.x, ey = a.y - b.y;  // X[k] + conj X[M-k]
+    const float dx = a.x - b.x, dy = a.y + b.y;  // X[k] - conj X[M-k]
+    float sn, cs;
+    sincospif(static_cast<float>(k) / static_cast<float>(M), &sn, &cs);
+    const float wx = cs * dx - sn * dy, wy = cs * dy + sn * dx;  // W^k d
+    // e + i (W^k d), conjugated
+    out[k] = make_float2(ex - wy, -(ey + wx));
+  }
+}
+
+__global__ void __launch_bounds__(256) c2r_post_kernel(const float2* __restrict__ Z, uint64_t M, XLayoutArgs L,
+                                                       float2* __restrict__ x, uint64_t zstride, uint64_t ostride) {
+  Z += blockIdx.y * zstride;
+  x += blockIdx.y * ostride;
+  for (uint64_t m = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; m < M;
+       m += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const float2 v = Z[xaddr(m, L)];
+    x[m] = make_float2(v.x, -v.y);
+  }
+}
+
 }  // namespace
 
 void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride, float* P, uint64_t pstride,
@@ -549,6 +602,33 @@ void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstr
   r2c_interbin_tiled_kernel<<<grid, 256, 0, s>>>(X, lg, static_cast<uint64_t>(n1), xstride, P, pstride, nbins_out,
                                                  stats, nscale, rtw);
   post_launch_check("r2c_interbin_tiled_kernel", s);
+}
+
+void fft4_r2c_half(const float2* Z, uint64_t M, const XLayoutArgs& L, float2* X, hipStream_t s, int count,
+                   uint64_t zstride, uint64_t xstride) {
+  PSOUP_CHECK(M >= 2 && (M & (M - 1)) == 0, "r2c_half: M must be a power of two");
+  PSOUP_CHECK(count >= 1 && count <= 65535, "r2c_half: bad count");
+  const dim3 grid(dev::grid_for(M + 1, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
+  r2c_half_kernel<<<grid, 256, 0, s>>>(Z, M, L, X, zstride, xstride);
+  post_launch_check("r2c_half_kernel", s);
+}
+
+void fft4_c2r_pre(const float2* X, uint64_t M, float2* out, hipStream_t s, int count, uint64_t xstride,
+                  uint64_t ostride) {
+  PSOUP_CHECK(M >= 2, "c2r_pre: bad size");
+  PSOUP_CHECK(count >= 1 && count <= 65535, "c2r_pre: bad count");
+  const dim3 grid(dev::grid_for(M, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
+  c2r_pre_kernel<<<grid, 256, 0, s>>>(X, M, out, xstride, ostride);
+  post_launch_check("c2r_pre_kernel", s);
+}
+
+void fft4_c2r_post(const float2* Z, uint64_t M, const XLayoutArgs& L, float* x, hipStream_t s, int count,
+                   uint64_t zstride, uint64_t ostride) {
+  PSOUP_CHECK((reinterpret_cast<uintptr_t>(x) & 7) == 0 && ostride % 2 == 0, "c2r_post: output alignment");
+  PSOUP_CHECK(count >= 1 && count <= 65535, "c2r_post: bad count");
+  const dim3 grid(dev::grid_for(M, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
+  c2r_post_kernel<<<grid, 256, 0, s>>>(Z, M, L, reinterpret_cast<float2*>(x), zstride, ostride / 2);
+  post_launch_check("c2r_post_kernel", s);
 }
 
 namespace {

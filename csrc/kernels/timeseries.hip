@@ -11,7 +11,9 @@ namespace kern {
 namespace {
 
 __global__ void __launch_bounds__(256) u8_sum_kernel(const uint8_t* __restrict__ in, uint64_t n,
-                                                     unsigned long long* __restrict__ sum) {
+                                                     unsigned long long* __restrict__ sum, uint64_t in_stride) {
+  in += blockIdx.y * in_stride;
+  sum += blockIdx.y;
   __shared__ unsigned long long scratch[4];
   unsigned long long acc = 0;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
@@ -41,7 +43,11 @@ __global__ void __launch_bounds__(256) u8_sum_kernel(const uint8_t* __restrict__
 
 __global__ void __launch_bounds__(256) u8_to_f32_pad_kernel(const uint8_t* __restrict__ in, uint64_t nvalid,
                                                             float* __restrict__ out, uint64_t n,
-                                                            const unsigned long long* __restrict__ sum) {
+                                                            const unsigned long long* __restrict__ sum,
+                                                            uint64_t in_stride, uint64_t out_stride) {
+  in += blockIdx.y * in_stride;
+  out += blockIdx.y * out_stride;
+  sum += blockIdx.y;
   const float mean = nvalid ? static_cast<float>(static_cast<double>(*sum) / static_cast<double>(nvalid)) : 0.f;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   // 4 samples per thread per step
@@ -110,19 +116,21 @@ __global__ void __launch_bounds__(256) stats_finalize_kernel(const double* __res
   }
 }
 
-void u8_sum(const uint8_t* in, uint64_t n, unsigned long long* sum, hipStream_t s) {
-  PSOUP_HIP_CHECK(hipMemsetAsync(sum, 0, sizeof(unsigned long long), s));
+void u8_sum(const uint8_t* in, uint64_t n, unsigned long long* sum, hipStream_t s, int count, uint64_t in_stride) {
+  PSOUP_CHECK(count >= 1 && count <= 65535, "u8_sum: bad count");
+  PSOUP_HIP_CHECK(hipMemsetAsync(sum, 0, sizeof(unsigned long long) * count, s));
   if (n == 0) return;
-  unsigned grid = dev::grid_for(n / 16 + 1, 256, 1024);
-  u8_sum_kernel<<<grid, 256, 0, s>>>(in, n, sum);
+  const dim3 grid(dev::grid_for(n / 16 + 1, 256, count > 1 ? 256 : 1024), static_cast<unsigned>(count));
+  u8_sum_kernel<<<grid, 256, 0, s>>>(in, n, sum, in_stride);
   post_launch_check("u8_sum_kernel", s);
 }
 
 void u8_to_f32_pad(const uint8_t* in, uint64_t nvalid, float* out, uint64_t n, const unsigned long long* sum,
-                   hipStream_t s) {
-  PSOUP_CHECK((reinterpret_cast<uintptr_t>(out) & 15) == 0, "output must be 16-byte aligned");
-  unsigned grid = dev::grid_for(n / 4 + 1, 256);
-  u8_to_f32_pad_kernel<<<grid, 256, 0, s>>>(in, nvalid, out, n, sum);
+                   hipStream_t s, int count, uint64_t in_stride, uint64_t out_stride) {
+  PSOUP_CHECK((reinterpret_cast<uintptr_t>(out) & 15) == 0 && out_stride % 4 == 0, "output must be 16-byte aligned");
+  PSOUP_CHECK(count >= 1 && count <= 65535, "u8_to_f32_pad: bad count");
+  const dim3 grid(dev::grid_for(n / 4 + 1, 256, count > 1 ? 1024 : 2048), static_cast<unsigned>(count));
+  u8_to_f32_pad_kernel<<<grid, 256, 0, s>>>(in, nvalid, out, n, sum, in_stride, out_stride);
   post_launch_check("u8_to_f32_pad_kernel", s);
 }
 

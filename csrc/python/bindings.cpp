@@ -642,6 +642,15 @@ PYBIND11_MODULE(_C, m) {
       .def("mfma_steps_per_channel", &Dedisperser::mfma_steps_per_channel, py::arg("d0"), py::arg("d1"))
       .def_property_readonly_static("tile_dms", [](py::object) { return Dedisperser::kTileDms; });
 
+  py::class_<Whitener>(m, "Whitener")
+      .def(py::init([](uint64_t n, float tsamp, uintptr_t s, bool f4) { return new Whitener(n, tsamp, S(s), f4); }),
+           py::arg("n"), py::arg("tsamp"), py::arg("stream"), py::arg("allow_fft4") = true)
+      .def("forward", [](Whitener& w, uintptr_t x, uintptr_t X) { w.forward(P<const float>(x), P<float2>(X)); })
+      .def("inverse", [](Whitener& w, uintptr_t X, uintptr_t x) { w.inverse(P<const float2>(X), P<float>(x)); })
+      .def("whiten", [](Whitener& w, uintptr_t x, bool stats) { w.whiten(P<float>(x), nullptr, stats, 0.05f, 0.5f); },
+           py::arg("series"), py::arg("with_stats") = true)
+      .def_property_readonly("uses_fft4", &Whitener::uses_fft4)
+      .def_property_readonly("nbins", &Whitener::nbins);
   py::class_<SearchParams>(m, "SearchParams")
       .def(py::init<>())
       .def_readwrite("fft_size", &SearchParams::fft_size)
@@ -668,18 +677,26 @@ PYBIND11_MODULE(_C, m) {
                               const std::vector<float>& accs) {
         return e.search_trial(P<const uint8_t>(trial), nsamps, dm, dm_idx, accs);
       }, py::call_guard<py::gil_scoped_release>())
+      .def("prepare", [](SearchEngine& e, uintptr_t trials, uint64_t row_stride, uint64_t nsamps, int count) {
+        e.prepare(P<const uint8_t>(trials), row_stride, nsamps, count);
+      }, py::arg("trials"), py::arg("row_stride"), py::arg("nsamps"), py::arg("count"),
+         py::call_guard<py::gil_scoped_release>())
+      .def("search_prepared", [](SearchEngine& e, int b, float dm, int dm_idx, const std::vector<float>& accs) {
+        return e.search_prepared(b, dm, dm_idx, accs);
+      }, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("max_prepare", &SearchEngine::max_prepare)
       .def_property_readonly("batch_size", &SearchEngine::batch_size)
       .def_property_readonly("sub_batch", &SearchEngine::sub_batch)
       .def_property_readonly("fft_mode", &SearchEngine::fft_mode)
       .def_property_readonly("stream", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.stream()); })
       .def_property_readonly("tobs", &SearchEngine::tobs)
       .def_property_readonly("whitened_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.whitened()); })
-      .def_property_readonly("stats_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.whitener().stats()); })
+      .def_property_readonly("stats_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.trial_stats()); })
       .def("copy_whitened", [](const SearchEngine& e, uintptr_t dst) {
         PSOUP_HIP_CHECK(hipMemcpy(P<void>(dst), e.whitened(), e.params().fft_size * sizeof(float), hipMemcpyDeviceToDevice));
       })
       .def("copy_stats", [](const SearchEngine& e, uintptr_t dst) {
-        PSOUP_HIP_CHECK(hipMemcpy(P<void>(dst), e.whitener().stats(), 3 * sizeof(float), hipMemcpyDeviceToDevice));
+        PSOUP_HIP_CHECK(hipMemcpy(P<void>(dst), e.trial_stats(), 3 * sizeof(float), hipMemcpyDeviceToDevice));
       })
       .def("counters", [](const SearchEngine& e) {
         const SearchCounters& c = e.counters();

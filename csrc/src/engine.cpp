@@ -225,13 +225,23 @@ void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispK
 }
 
 // ---------------------------------------------------------------- whitener --
-Whitener::Whitener(uint64_t n, float tsamp, hipStream_t stream) : n_(n), tsamp_(tsamp), stream_(stream) {
+Whitener::Whitener(uint64_t n, float tsamp, hipStream_t stream, bool allow_fft4)
+    : n_(n), tsamp_(tsamp), stream_(stream) {
   PSOUP_CHECK(n >= 250, "series too short for the running median (need >= 250 samples)");
   float tobs = static_cast<float>(static_cast<float>(n) * tsamp);
   bin_width_ = static_cast<float>(1.0 / tobs);
   const uint64_t nb = nbins();
-  r2c_ = std::make_unique<FftPlan>(FftType::R2C, n, 1);
-  c2r_ = std::make_unique<FftPlan>(FftType::C2R, n, 1);
+  if (allow_fft4 && n % 2 == 0) {
+    g4_ = kern::fft4_geometry(n / 2);
+    // single-transform grids of both passes need n1/8 % 16 == 0 and n2/8 % 8 == 0
+    f4_ = g4_.ok && g4_.n1 >= 128 && g4_.n2 >= 64;
+  }
+  if (f4_) {
+    auto tab = kern::fft4_tables(g4_);
+    tab4_.resize(tab.size());
+    PSOUP_HIP_CHECK(hipMemcpy(tab4_.data(), tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice));
+    ensure_batch(1);
+  }
   fser_.resize(nb);
   m5_.resize(nb / 5);
   m25_.resize(std::max<uint64_t>(1, nb / 5 / 5));
@@ -241,25 +251,124 @@ Whitener::Whitener(uint64_t n, float tsamp, hipStream_t stream) : n_(n), tsamp_(
   sum_.resize(1);
 }
 
+FftPlan& Whitener::r2c() {
+  if (!r2c_) r2c_ = std::make_unique<FftPlan>(FftType::R2C, n_, 1);
+  return *r2c_;
+}
+
+FftPlan& Whitener::c2r() {
+  if (!c2r_) c2r_ = std::make_unique<FftPlan>(FftType::C2R, n_, 1);
+  return *c2r_;
+}
+
+void Whitener::forward(const float* d_series, float2* d_spec) {
+  if (!f4_) {
+    r2c().execute(const_cast<float*>(d_series), d_spec, stream_);
+    return;
+  }
+  const uint64_t M = n_ / 2;
+  kern::fft4_pad_input(d_series, n_, in4_.data(), g4_, stream_);
+  kern::fft4_resample_colpass(d_series, in4_.data(), n_, af0_.data(), 1, y4_.data(), g4_, tab4_.data(), stream_);
+  kern::fft4_rowpass(y4_.data(), x4_.data(), 1, g4_, tab4_.data(), stream_);
+  kern::fft4_r2c_half(x4_.data(), M, kern::xlayout_args(g4_, kern::fft4_x_layout(g4_)), d_spec, stream_);
+}
+
+void Whitener::inverse(const float2* d_spec, float* d_series) {
+  if (!f4_) {
+    c2r().execute(const_cast<float2*>(d_spec), d_series, stream_);
+    return;
+  }
+  const uint64_t M = n_ / 2;
+  kern::fft4_c2r_pre(d_spec, M, tmp4_.data(), stream_);
+  const float* t = reinterpret_cast<const float*>(tmp4_.data());
+  kern::fft4_pad_input(t, n_, in4_.data(), g4_, stream_);
+  kern::fft4_resample_colpass(t, in4_.data(), n_, af0_.data(), 1, y4_.data(), g4_, tab4_.data(), stream_);
+  kern::fft4_rowpass(y4_.data(), x4_.data(), 1, g4_, tab4_.data(), stream_);
+  kern::fft4_c2r_post(x4_.data(), M, kern::xlayout_args(g4_, kern::fft4_x_layout(g4_)), d_series, stream_);
+}
+
 void Whitener::load_trial(const uint8_t* d_trial, uint64_t nsamps, float* d_series) {
   const uint64_t nvalid = std::min(nsamps, n_);
   kern::u8_sum(d_trial, nvalid, sum_.data(), stream_);
   kern::u8_to_f32_pad(d_trial, nvalid, d_series, n_, sum_.data(), stream_);
 }
 
-void Whitener::whiten(float* d_series, const uint32_t* d_zapmask, bool with_stats, float boundary5, float boundary25) {
+void Whitener::dered_stats(float2* spec, const uint32_t* d_zapmask, float* d_stats, float boundary5,
+                           float boundary25) {
   const uint64_t nb = nbins();
-  r2c_->execute(d_series, fser_.data(), stream_);
   const uint64_t n5 = nb / 5, n25 = n5 / 5, n125 = n25 / 5;
-  kern::median5_amp(fser_.data(), nb, m5_.data(), stream_);
+  kern::median5_amp(spec, nb, m5_.data(), stream_);
   kern::median5(m5_.data(), n5, m25_.data(), stream_);
   kern::median5(m25_.data(), n25, m125_.data(), stream_);
   const int64_t pos5 = static_cast<int64_t>(static_cast<int>(boundary5 / bin_width_));
   const int64_t pos25 = static_cast<int64_t>(static_cast<int>(boundary25 / bin_width_));
-  kern::deredden_zap(fser_.data(), nb, m5_.data(), n5, m25_.data(), std::max<uint64_t>(1, n25), m125_.data(),
+  kern::deredden_zap(spec, nb, m5_.data(), n5, m25_.data(), std::max<uint64_t>(1, n25), m125_.data(),
                      std::max<uint64_t>(1, n125), pos5, pos25, d_zapmask, stream_);
-  if (with_stats) kern::interbin_stats(fser_.data(), nb, nullptr, partials_.data(), 1024, stats_.data(), stream_);
-  c2r_->execute(fser_.data(), d_series, stream_);
+  if (d_stats) kern::interbin_stats(spec, nb, nullptr, partials_.data(), 1024, d_stats, stream_);
+}
+
+void Whitener::whiten(float* d_series, const uint32_t* d_zapmask, bool with_stats, float boundary5, float boundary25) {
+  forward(d_series, fser_.data());
+  dered_stats(fser_.data(), d_zapmask, with_stats ? stats_.data() : nullptr, boundary5, boundary25);
+  inverse(fser_.data(), d_series);
+}
+
+uint64_t Whitener::batch_bytes_per_trial() const {
+  if (!f4_) return 0;
+  return g4_.ystride * 8 + g4_.xstride * 8 + nbins() * 8 + (n_ / 2) * 8 + g4_.insize * 4;
+}
+
+void Whitener::ensure_batch(int count) {
+  if (count <= bcap_) return;
+  y4_.resize(g4_.ystride * count);
+  x4_.resize(g4_.xstride * count);
+  tmp4_.resize((n_ / 2) * count);
+  in4_.resize(g4_.insize * count);
+  bspec_.resize(nbins() * count);
+  bsum_.resize(static_cast<uint64_t>(count));
+  af0_.resize(static_cast<uint64_t>(count));
+  af0_.zero_async(stream_);
+  bcap_ = count;
+}
+
+void Whitener::whiten_batch(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count, float* d_out,
+                            uint64_t out_stride, const uint32_t* d_zapmask, float* d_stats, float boundary5,
+                            float boundary25) {
+  PSOUP_CHECK(count >= 1, "whiten_batch: empty batch");
+  if (!f4_) {
+    for (int b = 0; b < count; ++b) {
+      float* x = d_out + static_cast<uint64_t>(b) * out_stride;
+      load_trial(d_trials + static_cast<uint64_t>(b) * row_stride, nsamps, x);
+      forward(x, fser_.data());
+      dered_stats(fser_.data(), d_zapmask, d_stats + 4 * b, boundary5, boundary25);
+      inverse(fser_.data(), x);
+    }
+    return;
+  }
+  ensure_batch(count);
+  const uint64_t M = n_ / 2, nb = nbins();
+  const uint64_t nvalid = std::min(nsamps, n_);
+  const kern::XLayoutArgs L = kern::xlayout_args(g4_, kern::fft4_x_layout(g4_));
+  kern::u8_sum(d_trials, nvalid, bsum_.data(), stream_, count, row_stride);
+  kern::u8_to_f32_pad(d_trials, nvalid, d_out, n_, bsum_.data(), stream_, count, row_stride, out_stride);
+  // forward: K = count transforms, trial b reading series b
+  kern::Fft4Geom g = g4_;
+  g.in_tstride = out_stride;
+  g.pad_tstride = g4_.insize;
+  kern::fft4_pad_input(d_out, n_, in4_.data(), g4_, stream_, count, out_stride);
+  kern::fft4_resample_colpass(d_out, in4_.data(), n_, af0_.data(), count, y4_.data(), g, tab4_.data(), stream_);
+  kern::fft4_rowpass(y4_.data(), x4_.data(), count, g4_, tab4_.data(), stream_);
+  kern::fft4_r2c_half(x4_.data(), M, L, bspec_.data(), stream_, count, g4_.xstride, nb);
+  for (int b = 0; b < count; ++b)
+    dered_stats(bspec_.data() + static_cast<uint64_t>(b) * nb, d_zapmask, d_stats + 4 * b, boundary5, boundary25);
+  // inverse
+  kern::fft4_c2r_pre(bspec_.data(), M, tmp4_.data(), stream_, count, nb, M);
+  const float* t = reinterpret_cast<const float*>(tmp4_.data());
+  g.in_tstride = n_;
+  kern::fft4_pad_input(t, n_, in4_.data(), g4_, stream_, count, n_);
+  kern::fft4_resample_colpass(t, in4_.data(), n_, af0_.data(), count, y4_.data(), g, tab4_.data(), stream_);
+  kern::fft4_rowpass(y4_.data(), x4_.data(), count, g4_, tab4_.data(), stream_);
+  kern::fft4_c2r_post(x4_.data(), M, L, d_out, stream_, count, g4_.xstride, out_stride);
 }
 
 std::vector<uint32_t> build_zap_mask(const std::vector<float>& freqs, const std::vector<float>& widths,
@@ -297,8 +406,17 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   nlev_ = std::min(std::max(p_.nharmonics, 0), kern::kMaxHarmLevels);
   if (p_.nharmonics > kern::kMaxHarmLevels)
     log_info("warning: nharmonics > 5 is capped at 5 (32 harmonics), as the reference kernel only writes 5 levels");
-  wh_ = std::make_unique<Whitener>(n_, p_.tsamp, stream_);
+  // A/B knobs: PSOUP_WHITEN_ROCFFT=1 whitens with rocFFT, PSOUP_PREPARE_MAX caps the whitening batch
+  const char* wr = std::getenv("PSOUP_WHITEN_ROCFFT");
+  wh_ = std::make_unique<Whitener>(n_, p_.tsamp, stream_, p_.fft_mode == 2 && !(wr && std::atoi(wr) == 1));
+  {
+    // whitening batch: up to 3 GB of per-trial whitening state (>= 1 trial)
+    const uint64_t per = wh_->batch_bytes_per_trial() + n_ * 4 + (p_.fft_mode == 2 ? n_ * 4 + 4096 : 0);
+    max_prep_ = per ? static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(64, (3ull << 30) / per))) : 1;
+    if (const char* pm = std::getenv("PSOUP_PREPARE_MAX")) max_prep_ = std::max(1, std::min(max_prep_, std::atoi(pm)));
+  }
   tim_.resize(n_);
+  wstats_.resize(4 * static_cast<uint64_t>(max_prep_));
   mode_ = (n_ % 2 == 0) ? std::min(std::max(p_.fft_mode, 0), 2) : 0;
   if (mode_ == 2) f4_ = kern::fft4_geometry(n_ / 2);
   if (mode_ == 2 && !f4_.ok) mode_ = 1;
@@ -406,26 +524,26 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
       // res_ holds the four-step intermediates Y (complex, ystride per trial)
       float2* Y = reinterpret_cast<float2*>(res_.data()) + static_cast<uint64_t>(b) * f4_.ystride;
       float2* X = spec_.data() + static_cast<uint64_t>(b) * xs_;
-      kern::fft4_resample_colpass(tim_.data(), f4_in_.data(), n_, af_.data() + first + b, c, Y, f4_,
+      kern::fft4_resample_colpass(cur_tim_, cur_pad_, n_, af_.data() + first + b, c, Y, f4_,
                                   f4_tab_.data(), st);
       kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st, static_cast<uint64_t>(hi_));
       if (xl.tiled)
         kern::r2c_interbin_normalise_tiled(X, f4_.n1, f4_.n2, xs_, P, pst, c, static_cast<uint64_t>(hi_),
-                                           wh_->stats(), static_cast<float>(n_), st);
+                                           cur_stats_, static_cast<float>(n_), st);
       else
         kern::r2c_interbin_normalise_batch(X, n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch, xl.log2_blk,
-                                           P, pst, c, static_cast<uint64_t>(hi_), wh_->stats(),
+                                           P, pst, c, static_cast<uint64_t>(hi_), cur_stats_,
                                            static_cast<float>(n_), st);
     } else {
-      kern::resample_batch(tim_.data(), n_, res_.data(), n_, af_.data() + first, c, st);
+      kern::resample_batch(cur_tim_, n_, res_.data(), n_, af_.data() + first, c, st);
       batch_plan(c).execute(res_.data(), spec_.data(), st);
       if (mode_ == 1)
         kern::r2c_interbin_normalise_batch(spec_.data(), n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch,
-                                           xl.log2_blk, P, pst, c, static_cast<uint64_t>(hi_), wh_->stats(),
+                                           xl.log2_blk, P, pst, c, static_cast<uint64_t>(hi_), cur_stats_,
                                            static_cast<float>(n_), st);
       else
         kern::interbin_normalise_batch(spec_.data(), nb_, nb_, P, pst, c, static_cast<uint64_t>(hi_),
-                                       wh_->stats(), static_cast<float>(n_), st);
+                                       cur_stats_, static_cast<float>(n_), st);
     }
     RoctxRange r("Harmonic summing");
     kern::HarmParams hp = hp_;
@@ -519,14 +637,35 @@ void SearchEngine::process_slot(Slot& s, int first, int count, uint32_t npeaks, 
   }
 }
 
+void SearchEngine::prepare(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count) {
+  PSOUP_CHECK(count >= 1 && count <= max_prep_, "prepare: count " << count << " outside [1, " << max_prep_ << "]");
+  RoctxRange r("Whitening");
+  // the previous batch's searches have retired (search_prepared waits on every
+  // acceleration batch), so the buffers may be rewritten
+  tim_.resize(n_ * static_cast<uint64_t>(count));
+  wh_->whiten_batch(d_trials, row_stride, nsamps, count, tim_.data(), n_, zap_ ? zapmask_.data() : nullptr,
+                    wstats_.data(), p_.boundary_5_freq, p_.boundary_25_freq);
+  if (mode_ == 2) {
+    f4_in_.resize(f4_.insize * static_cast<uint64_t>(count));
+    kern::fft4_pad_input(tim_.data(), n_, f4_in_.data(), f4_, stream_, count, n_);
+  }
+  prepared_ = count;
+}
+
 CandidateList SearchEngine::search_trial(const uint8_t* d_trial, uint64_t nsamps, float dm, int dm_idx,
                                          const std::vector<float>& accs) {
+  prepare(d_trial, 0, nsamps, 1);
+  return search_prepared(0, dm, dm_idx, accs);
+}
+
+CandidateList SearchEngine::search_prepared(int b, float dm, int dm_idx, const std::vector<float>& accs) {
+  PSOUP_CHECK(b >= 0 && b < prepared_, "search_prepared: trial " << b << " was not prepared");
   RoctxRange dm_range("DM-Loop");
   Stopwatch sw;
   sw.start();
-  wh_->load_trial(d_trial, nsamps, tim_.data());
-  wh_->whiten(tim_.data(), zap_ ? zapmask_.data() : nullptr, true, p_.boundary_5_freq, p_.boundary_25_freq);
-  if (mode_ == 2) kern::fft4_pad_input(tim_.data(), n_, f4_in_.data(), f4_, stream_);
+  cur_tim_ = tim_.data() + static_cast<uint64_t>(b) * n_;
+  cur_pad_ = mode_ == 2 ? f4_in_.data() + static_cast<uint64_t>(b) * f4_.insize : nullptr;
+  cur_stats_ = wstats_.data() + 4 * static_cast<uint64_t>(b);
   ctr_.dm_trials++;
   const int nacc = static_cast<int>(accs.size());
   CandidateList accel_trial_cands;
@@ -712,7 +851,7 @@ void coincidencer_beam(const uint8_t* d_trial, uint64_t n, float tsamp, BeamProd
   wh.load_trial(d_trial, n, out.series.data());
   // whiten without the C2R so the dereddened spectrum can be formed first
   const uint64_t nb = wh.nbins();
-  wh.r2c().execute(out.series.data(), wh.spectrum(), stream);
+  wh.forward(out.series.data(), wh.spectrum());
   DeviceBuffer<float> m5(nb / 5), m25(std::max<uint64_t>(1, nb / 25)), m125(std::max<uint64_t>(1, nb / 125));
   const uint64_t n5 = nb / 5, n25 = n5 / 5, n125 = n25 / 5;
   kern::median5_amp(wh.spectrum(), nb, m5.data(), stream);
@@ -726,7 +865,7 @@ void coincidencer_beam(const uint8_t* d_trial, uint64_t n, float tsamp, BeamProd
   DeviceBuffer<float> st(4);
   kern::interbin_stats(wh.spectrum(), nb, out.spectrum.data(), partials.data(), 1024, st.data(), stream);
   kern::normalise_dev(out.spectrum.data(), nb, st.data(), 1.0f, stream);
-  wh.c2r().execute(wh.spectrum(), out.series.data(), stream);
+  wh.inverse(wh.spectrum(), out.series.data());
   kern::f32_stats(out.series.data(), n, partials.data(), 1024, st.data(), stream);
   kern::normalise_dev(out.series.data(), n, st.data(), 1.0f, stream);
   PSOUP_HIP_CHECK(hipStreamSynchronize(stream));

@@ -306,18 +306,23 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
           if (!pending[k]) issue(d0, k);  // unreadable checkpoint: recompute
           PSOUP_HIP_CHECK(hipStreamWaitEvent(st, ready[k].get(), 0));
           ws.start();
-          for (int d = d0; d < d1; ++d) {
-            if (args.fault_after_dms >= 0 && processed >= args.fault_after_dms)
-              PSOUP_THROW("fault injection: device " << dev << " aborting after " << processed << " DM trials");
-            const float dm = setup.dm_list[static_cast<size_t>(d)];
-            std::vector<float> accs = setup.accel_plan.generate(dm);
-            log_verbose("Searching " + std::to_string(accs.size()) + " acceleration trials for DM " +
-                        std::to_string(dm));
-            CandidateList c = engine.search_trial(trials[k].data() + static_cast<uint64_t>(d - d0) * rstride,
-                                                  geom.out_nsamps, dm, d, accs);
-            sh.accel_trials += accs.size();
-            for (auto& x : c) local.push_back(std::move(x));
-            processed++;
+          // whiten the chunk's trials in batches of up to max_prepare, then search each
+          for (int p0 = d0; p0 < d1; p0 += engine.max_prepare()) {
+            const int cnt = std::min(engine.max_prepare(), d1 - p0);
+            engine.prepare(trials[k].data() + static_cast<uint64_t>(p0 - d0) * rstride, rstride, geom.out_nsamps,
+                           cnt);
+            for (int d = p0; d < p0 + cnt; ++d) {
+              if (args.fault_after_dms >= 0 && processed >= args.fault_after_dms)
+                PSOUP_THROW("fault injection: device " << dev << " aborting after " << processed << " DM trials");
+              const float dm = setup.dm_list[static_cast<size_t>(d)];
+              std::vector<float> accs = setup.accel_plan.generate(dm);
+              log_verbose("Searching " + std::to_string(accs.size()) + " acceleration trials for DM " +
+                          std::to_string(dm));
+              CandidateList c = engine.search_prepared(d - p0, dm, d, accs);
+              sh.accel_trials += accs.size();
+              for (auto& x : c) local.push_back(std::move(x));
+              processed++;
+            }
           }
           ws.stop();
           freed[k].record(st);

@@ -224,21 +224,28 @@ class RankSearcher:
             per_dm: Dict[int, list] = {}
 
             def run_dms(e, dms):
+                # this engine's DMs are every ne-th row of the chunk: whitened
+                # as batches of up to max_prepare, then searched one by one
                 nonlocal processed, ntrials
-                for d in dms:
-                    with lock:
-                        if 0 <= fault_after <= processed:
-                            raise RuntimeError(f"fault injection: rank {self.ctx.rank} aborting after "
-                                               f"{processed} DM trials")
-                        processed += 1
-                    dm = self.dm_list[d]
-                    accs = self.accel_list(dm)
-                    addr = bufs[k].data_ptr() + (d - d0) * self.row_stride
-                    per_dm[d] = e.search_trial(addr, self.geom.out_nsamps, dm, d, accs)
-                    with lock:
-                        ntrials += len(accs)
-                        if progress is not None:
-                            progress(1)
+                dms = list(dms)
+                step = (dms[1] - dms[0]) if len(dms) > 1 else 1
+                for p0 in range(0, len(dms), e.max_prepare):
+                    part = dms[p0:p0 + e.max_prepare]
+                    e.prepare(bufs[k].data_ptr() + (part[0] - d0) * self.row_stride, step * self.row_stride,
+                              self.geom.out_nsamps, len(part))
+                    for b, d in enumerate(part):
+                        with lock:
+                            if 0 <= fault_after <= processed:
+                                raise RuntimeError(f"fault injection: rank {self.ctx.rank} aborting after "
+                                                   f"{processed} DM trials")
+                            processed += 1
+                        dm = self.dm_list[d]
+                        accs = self.accel_list(dm)
+                        per_dm[d] = e.search_prepared(b, dm, d, accs)
+                        with lock:
+                            ntrials += len(accs)
+                            if progress is not None:
+                                progress(1)
 
             ne = len(self.engines)
             if ne == 1:

@@ -472,3 +472,64 @@ def test_results_independent_of_accel_batching(C, batch, sub):
     assert runs[0] == runs[1] and len(runs[0]) > 0
     best = max(runs[1], key=lambda r: r[2])
     assert abs(best[0] - a_true) <= 30.0, best
+
+
+@pytest.mark.parametrize("log2n", [17, 20, 23])
+def test_whitener_real_ffts_on_fft4_match_numpy(C, log2n):
+    """Whitener R2C/C2R on the four-step passes (K = 1) vs NumPy fp64 and the
+    rocFFT fallback: unnormalised like rocFFT (C2R(R2C(x)) = N x)."""
+    n = 1 << log2n
+    rng = np.random.default_rng(log2n)
+    x = rng.standard_normal(n).astype(np.float32)
+    s = torch.cuda.current_stream().cuda_stream
+    xs = torch.from_numpy(x).to(dev)
+    ref_spec = np.fft.rfft(x.astype(np.float64))
+    scale = np.abs(ref_spec).max()
+    outs = {}
+    for f4 in (True, False):
+        w = C.Whitener(n, 64e-6, s, f4)
+        assert w.uses_fft4 == f4
+        X = torch.empty(n // 2 + 1, dtype=torch.complex64, device=dev)
+        w.forward(xs.data_ptr(), X.data_ptr())
+        torch.cuda.synchronize()
+        Xn = X.cpu().numpy()
+        y = torch.empty(n, dtype=torch.float32, device=dev)
+        w.inverse(X.data_ptr(), y.data_ptr())  # (rocFFT's out-of-place C2R may overwrite X)
+        torch.cuda.synchronize()
+        assert np.abs(Xn - ref_spec).max() < 2e-6 * scale * log2n, f4
+        assert np.allclose(y.cpu().numpy() / n, x, atol=2e-5 * log2n), f4
+        outs[f4] = Xn
+    assert np.abs(outs[True] - outs[False]).max() < 2e-6 * scale * log2n
+
+
+def test_batched_whitening_matches_single_trial(C):
+    """SearchEngine.prepare(count) + search_prepared(b) (one K = count
+    four-step FFT pair for the whitening) gives the candidates, whitened
+    series and stats of search_trial on each trial alone."""
+    rng = np.random.default_rng(5)
+    n, nsamps, count = 1 << 18, (1 << 18) + 300, 5
+    rs = 1 << 19
+    t = np.arange(nsamps) * 64e-6
+    rows = np.zeros((count, rs), dtype=np.uint8)
+    for b in range(count):
+        x = rng.normal(128, 10, nsamps) + 25 * (((t / (0.0213 * (1 + 0.1 * b))) % 1.0) < 0.03)
+        rows[b, :nsamps] = np.clip(np.rint(x), 0, 255).astype(np.uint8)
+    d = torch.from_numpy(rows).to(dev)
+    p = C.SearchParams()
+    p.fft_size, p.tsamp, p.nharmonics = n, 64e-6, 3
+    s = torch.cuda.current_stream().cuda_stream
+    e1, e2 = C.SearchEngine(p, s), C.SearchEngine(p, s)
+    assert e2.max_prepare >= count
+    accs = [-20.0, 0.0, 35.0]
+    e2.prepare(d.data_ptr(), rs, nsamps, count)
+    key = lambda c: (round(c.freq, 7), c.acc, c.nh, c.snr)  # noqa: E731
+    for b in range(count):
+        single = e1.search_trial(d.data_ptr() + b * rs, nsamps, 10.0, b, accs)
+        w1 = torch.empty(n, dtype=torch.float32, device=dev)
+        e1.copy_whitened(w1.data_ptr())
+        batched = e2.search_prepared(b, 10.0, b, accs)
+        w2 = torch.empty(n, dtype=torch.float32, device=dev)
+        e2.copy_whitened(w2.data_ptr())
+        assert torch.equal(w1, w2), b
+        assert sorted(map(key, single)) == sorted(map(key, batched)), b
+        assert len(single) > 0
