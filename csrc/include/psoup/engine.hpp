@@ -203,6 +203,18 @@ class SearchEngine {
   // search_trial = prepare(trial, 0, nsamps, 1) + search_prepared(0, ...).
   void prepare(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count);
   CandidateList search_prepared(int b, float dm, int dm_idx, const std::vector<float>& accs);
+  // Several prepared DMs at once: their acceleration trials are concatenated
+  // and cut into batches of K regardless of DM boundaries (a batch's trials
+  // may resample different series), so short trial lists still fill batches
+  // and the slot pipeline does not drain between DMs.  Returns one
+  // acceleration-distilled list per job, identical to search_prepared's.
+  struct Job {
+    int b;  // prepared series
+    float dm;
+    int dm_idx;
+    std::vector<float> accs;
+  };
+  std::vector<CandidateList> search_prepared_many(const std::vector<Job>& jobs);
   int max_prepare() const { return max_prep_; }
   const SearchParams& params() const { return p_; }
   const SearchCounters& counters() const { return ctr_; }
@@ -232,8 +244,13 @@ class SearchEngine {
   void grow_capacity(uint32_t need);
   // first/count/npeaks are the batch's values captured before the slot was
   // re-issued (launch_batch overwrites Slot::first/count/h_count)
-  void process_slot(Slot& s, int first, int count, uint32_t npeaks, float dm, int dm_idx,
-                    const std::vector<float>& accs, CandidateList& out);
+  void process_slot(Slot& s, int first, int count, uint32_t npeaks, std::vector<CandidateList>& out_by_job);
+  // flat trial list of the current search_prepared_many call
+  const std::vector<Job>* jobs_ = nullptr;
+  std::vector<int> flat_job_;
+  std::vector<float> flat_acc_;
+  std::vector<uint32_t> flat_src_;
+  DeviceBuffer<uint32_t> d_src_;
 
   SearchParams p_;
   hipStream_t stream_;

@@ -128,12 +128,16 @@ void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride,
 // pair (k, M-k) from one pair of loads.
 void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t row_pitch,
                                   uint64_t blk_pitch, int log2_blk, float* P, uint64_t pstride, int K,
-                                  uint64_t nbins_out, const float* stats, float nscale, hipStream_t s);
+                                  uint64_t nbins_out, const float* stats, float nscale, hipStream_t s,
+                                  const uint32_t* tsrc = nullptr);
 
 // Same output from the 8x8-tiled spectrum of fft4 pass B (kFft4TileX):
 // bin k = k2 + n2*k1 at X[k2/8][k1/8][k2%8][k1%8]; 64-byte loads per thread.
+// tsrc (device, optional): trial k normalises with stats + 4*tsrc[k] (batches
+// mixing trials of several prepared series).
 void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstride, float* P, uint64_t pstride,
-                                  int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s);
+                                  int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s,
+                                  const uint32_t* tsrc = nullptr);
 
 // Fused resample + four-step FFT (fft4step.hip).  M = N/2 = n1*n2 with
 // n1, n2 powers of two in [128, 4096], n2 <= n1 <= 2 n2.  Intermediates use
@@ -149,6 +153,8 @@ struct Fft4Geom {
   // Pass A input per trial k: in + k*in_tstride, in_pad + k*pad_tstride
   // (0 = every trial resamples the same series; the batched whitener sets n, insize).
   uint64_t in_tstride = 0, pad_tstride = 0;
+  // optional device map trial -> series index (else trial k reads series k)
+  const uint32_t* tsrc = nullptr;
 };
 Fft4Geom fft4_geometry(uint64_t M);
 // Twiddle tables (upload once per plan): see fft4step.hip for the layout.

@@ -377,6 +377,7 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
   const int log2row = __builtin_ctz(static_cast<unsigned>(2 * N1));
   const TableOffsets to = table_offsets(N1, L);
   const double af = afs[k];
+  const uint64_t src = g.tsrc ? g.tsrc[k] : static_cast<uint64_t>(k);  // series this trial resamples
   const double size = static_cast<double>(n);
   Vec<CPT> v;
 #pragma unroll
@@ -387,9 +388,8 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
 #pragma unroll
       for (int e = 0; e < 2 * CPT; ++e) x[e] = static_cast<float>(j + e);
     } else {
-      load_resampled<2 * CPT>(in + static_cast<uint64_t>(k) * g.in_tstride,
-                              in_pad + static_cast<uint64_t>(k) * g.pad_tstride, n, log2row, g.inpitch, af, size,
-                              2 * (static_cast<uint64_t>(N1) * j + c0), x);
+      load_resampled<2 * CPT>(in + src * g.in_tstride, in_pad + src * g.pad_tstride, n, log2row, g.inpitch, af,
+                              size, 2 * (static_cast<uint64_t>(N1) * j + c0), x);
     }
 #pragma unroll
     for (int c = 0; c < CPT; ++c) v[c][q] = make_float2(x[2 * c], x[2 * c + 1]);

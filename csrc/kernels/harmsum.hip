@@ -78,13 +78,15 @@ constexpr int kR2cTile = 256 * kR2cBpt;
 
 __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
     const float2* __restrict__ Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t pitch, uint64_t blk, int lw,
-    float* __restrict__ P, uint64_t pstride, uint64_t nbins_out, const float* __restrict__ stats, float nscale) {
+    float* __restrict__ P, uint64_t pstride, uint64_t nbins_out, const float* __restrict__ stats, float nscale,
+    const uint32_t* __restrict__ tsrc) {
   __shared__ float2 A[kR2cTile + 2];  // A[u] = X[k0 - 1 + u]
   __shared__ float2 D[kR2cTile + 2];  // D[u] = X[M - (k0 - 1 + u)]
   const int kk = blockIdx.y;
   const int t = threadIdx.x;
   const float2* z = Z + static_cast<uint64_t>(kk) * zstride;
   float* p = P + static_cast<uint64_t>(kk) * pstride;
+  if (tsrc) stats += 4 * tsrc[kk];  // multi-series batch: this trial's whitening stats
   const float mean = stats[0] * nscale;
   const float sigma = stats[2] * nscale;
   const uint64_t half = M / 2;
@@ -168,7 +170,8 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* _
                                                                  uint64_t n1, uint64_t zstride,
                                                                  float* __restrict__ P, uint64_t pstride,
                                                                  uint64_t nbins_out, const float* __restrict__ stats,
-                                                                 float nscale, RowTw8 rtw) {
+                                                                 float nscale, RowTw8 rtw,
+                                                                 const uint32_t* __restrict__ tsrc) {
   __shared__ float2 A[8][258];  // A[r][u] = X[(g0+r)*n2 + c0 - 1 + u]
   __shared__ float2 D[8][258];  // D[r][u] = X[M - ((g0+r)*n2 + c0 - 1 + u)]
   const uint64_t n2 = uint64_t(1) << log2_n2;
@@ -177,6 +180,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* _
   const int t = threadIdx.x;
   const float2* z = Z + static_cast<uint64_t>(kk) * zstride;
   float* p = P + static_cast<uint64_t>(kk) * pstride;
+  if (tsrc) stats += 4 * tsrc[kk];  // multi-series batch: this trial's whitening stats
   const float mean = stats[0] * nscale;
   const float sigma = stats[2] * nscale;
   const uint64_t g0 = static_cast<uint64_t>(blockIdx.y) * 8;
@@ -569,7 +573,8 @@ void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride,
 
 void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride, int log2_row, uint64_t row_pitch,
                                   uint64_t blk_pitch, int log2_blk, float* P, uint64_t pstride, int K,
-                                  uint64_t nbins_out, const float* stats, float nscale, hipStream_t s) {
+                                  uint64_t nbins_out, const float* stats, float nscale, hipStream_t s,
+                                  const uint32_t* tsrc) {
   PSOUP_CHECK(K >= 1 && K <= 65535, "bad batch");
   PSOUP_CHECK(M >= 2 && (M & (M - 1)) == 0, "r2c: M must be a power of two");
   PSOUP_CHECK(nbins_out <= M + 1, "nbins_out beyond the spectrum");
@@ -578,12 +583,13 @@ void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride,
   dim3 grid(dev::grid_for((M / 2 + 1 + kR2cBpt - 1) / kR2cBpt, 256, 2048), static_cast<unsigned>(K));
   PSOUP_CHECK(log2_blk >= 0 && log2_blk <= log2_row, "r2c: bad block layout");
   r2c_interbin_normalise_batch_kernel<<<grid, 256, 0, s>>>(Z, M, zstride, log2_row, row_pitch, blk_pitch, log2_blk, P,
-                                                           pstride, nbins_out, stats, nscale);
+                                                           pstride, nbins_out, stats, nscale, tsrc);
   post_launch_check("r2c_interbin_normalise_batch_kernel", s);
 }
 
 void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstride, float* P, uint64_t pstride,
-                                  int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s) {
+                                  int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s,
+                                  const uint32_t* tsrc) {
   PSOUP_CHECK(K >= 1 && K <= 65535, "bad batch");
   PSOUP_CHECK(n1 >= 16 && n2 >= 256 && (n1 & (n1 - 1)) == 0 && (n2 & (n2 - 1)) == 0, "r2c tiled: bad geometry");
   PSOUP_CHECK(nbins_out <= static_cast<uint64_t>(n1) * n2 + 1, "nbins_out beyond the spectrum");
@@ -600,7 +606,7 @@ void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstr
     rtw.s[r] = static_cast<float>(std::sin(a));
   }
   r2c_interbin_tiled_kernel<<<grid, 256, 0, s>>>(X, lg, static_cast<uint64_t>(n1), xstride, P, pstride, nbins_out,
-                                                 stats, nscale, rtw);
+                                                 stats, nscale, rtw, tsrc);
   post_launch_check("r2c_interbin_tiled_kernel", s);
 }
 

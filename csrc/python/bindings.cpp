@@ -684,6 +684,13 @@ PYBIND11_MODULE(_C, m) {
       .def("search_prepared", [](SearchEngine& e, int b, float dm, int dm_idx, const std::vector<float>& accs) {
         return e.search_prepared(b, dm, dm_idx, accs);
       }, py::call_guard<py::gil_scoped_release>())
+      .def("search_prepared_many", [](SearchEngine& e, const std::vector<std::tuple<int, float, int, std::vector<float>>>& jobs) {
+        std::vector<SearchEngine::Job> js;
+        js.reserve(jobs.size());
+        for (const auto& j : jobs) js.push_back(SearchEngine::Job{std::get<0>(j), std::get<1>(j), std::get<2>(j), std::get<3>(j)});
+        return e.search_prepared_many(js);
+      }, py::arg("jobs"), py::call_guard<py::gil_scoped_release>(),
+         "jobs: [(prepared index, dm, dm_idx, accs)] -> one candidate list per job")
       .def_property_readonly("max_prepare", &SearchEngine::max_prepare)
       .def_property_readonly("batch_size", &SearchEngine::batch_size)
       .def_property_readonly("sub_batch", &SearchEngine::sub_batch)

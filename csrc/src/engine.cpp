@@ -524,16 +524,23 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
       // res_ holds the four-step intermediates Y (complex, ystride per trial)
       float2* Y = reinterpret_cast<float2*>(res_.data()) + static_cast<uint64_t>(b) * f4_.ystride;
       float2* X = spec_.data() + static_cast<uint64_t>(b) * xs_;
-      kern::fft4_resample_colpass(cur_tim_, cur_pad_, n_, af_.data() + first + b, c, Y, f4_,
-                                  f4_tab_.data(), st);
+      // trial first+b+i resamples prepared series d_src_[first+b+i] and is
+      // normalised with that series' whitening stats
+      const uint32_t* src = d_src_.data() + first + b;
+      kern::Fft4Geom g = f4_;
+      g.in_tstride = n_;
+      g.pad_tstride = f4_.insize;
+      g.tsrc = src;
+      kern::fft4_resample_colpass(tim_.data(), f4_in_.data(), n_, af_.data() + first + b, c, Y, g, f4_tab_.data(),
+                                  st);
       kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st, static_cast<uint64_t>(hi_));
       if (xl.tiled)
         kern::r2c_interbin_normalise_tiled(X, f4_.n1, f4_.n2, xs_, P, pst, c, static_cast<uint64_t>(hi_),
-                                           cur_stats_, static_cast<float>(n_), st);
+                                           wstats_.data(), static_cast<float>(n_), st, src);
       else
         kern::r2c_interbin_normalise_batch(X, n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch, xl.log2_blk,
-                                           P, pst, c, static_cast<uint64_t>(hi_), cur_stats_,
-                                           static_cast<float>(n_), st);
+                                           P, pst, c, static_cast<uint64_t>(hi_), wstats_.data(),
+                                           static_cast<float>(n_), st, src);
     } else {
       kern::resample_batch(cur_tim_, n_, res_.data(), n_, af_.data() + first, c, st);
       batch_plan(c).execute(res_.data(), spec_.data(), st);
@@ -568,8 +575,8 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
   s.done->record(stream_);
 }
 
-void SearchEngine::process_slot(Slot& s, int first, int count, uint32_t npeaks, float dm, int dm_idx,
-                                const std::vector<float>& accs, CandidateList& out) {
+void SearchEngine::process_slot(Slot& s, int first, int count, uint32_t npeaks,
+                                std::vector<CandidateList>& out_by_job) {
   const uint32_t cnt = std::min(npeaks, cap_);
   ctr_.peaks += cnt;
   const int L = nlev_ + 1;
@@ -590,11 +597,17 @@ void SearchEngine::process_slot(Slot& s, int first, int count, uint32_t npeaks, 
   // Per-trial clustering + harmonic distillation.  Trials own disjoint
   // segments of sorted_, so peak-heavy batches (RFI) are spread over the
   // host pool; results are concatenated in trial order (deterministic).
-  auto trial_range = [&](int k0, int k1, CandidateList& dst) {
+  // per-trial results, appended to their jobs' lists in trial order below
+  std::vector<CandidateList> per_trial(static_cast<size_t>(count));
+  auto trial_range = [&](int k0, int k1) {
     std::vector<int> idxs, pidx;
     std::vector<float> snrs, psnr;
     for (int k = k0; k < k1; ++k) {
-      const float acc = accs[static_cast<size_t>(first + k)];
+      const size_t ft = static_cast<size_t>(first + k);
+      const float acc = flat_acc_[ft];
+      const Job& job = (*jobs_)[static_cast<size_t>(flat_job_[ft])];
+      const float dm = job.dm;
+      const int dm_idx = job.dm_idx;
       CandidateList trial;
       for (int h = 0; h < L; ++h) {
         const int seg = k * 8 + h;
@@ -615,25 +628,23 @@ void SearchEngine::process_slot(Slot& s, int first, int count, uint32_t npeaks, 
         for (size_t i = 0; i < pidx.size(); ++i)
           trial.emplace_back(dm, dm_idx, acc, h, psnr[i], static_cast<float>(pidx[i] * factor));
       }
-      if (!trial.empty()) {
-        CandidateList d = harm_.distill(std::move(trial));
-        for (auto& c : d) dst.push_back(std::move(c));
-      }
+      if (!trial.empty()) per_trial[static_cast<size_t>(k)] = harm_.distill(std::move(trial));
     }
   };
   constexpr uint32_t kParallelPeaks = 8192;  // below this the serial loop is cheaper
   if (pool_ && cnt >= kParallelPeaks && count > 1) {
     const int nparts = std::min(count, 4 * pool_->size());
-    std::vector<CandidateList> parts(static_cast<size_t>(nparts));
     pool_->parallel_for(nparts, [&](int j) {
       const int k0 = static_cast<int>(static_cast<int64_t>(count) * j / nparts);
       const int k1 = static_cast<int>(static_cast<int64_t>(count) * (j + 1) / nparts);
-      trial_range(k0, k1, parts[static_cast<size_t>(j)]);
+      trial_range(k0, k1);
     });
-    for (auto& part : parts)
-      for (auto& c : part) out.push_back(std::move(c));
   } else {
-    trial_range(0, count, out);
+    trial_range(0, count);
+  }
+  for (int k = 0; k < count; ++k) {
+    CandidateList& dst = out_by_job[static_cast<size_t>(flat_job_[static_cast<size_t>(first + k)])];
+    for (auto& c : per_trial[static_cast<size_t>(k)]) dst.push_back(std::move(c));
   }
 }
 
@@ -659,38 +670,68 @@ CandidateList SearchEngine::search_trial(const uint8_t* d_trial, uint64_t nsamps
 }
 
 CandidateList SearchEngine::search_prepared(int b, float dm, int dm_idx, const std::vector<float>& accs) {
-  PSOUP_CHECK(b >= 0 && b < prepared_, "search_prepared: trial " << b << " was not prepared");
+  std::vector<Job> jobs(1);
+  jobs[0] = Job{b, dm, dm_idx, accs};
+  return std::move(search_prepared_many(jobs)[0]);
+}
+
+std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<Job>& jobs) {
   RoctxRange dm_range("DM-Loop");
   Stopwatch sw;
   sw.start();
-  cur_tim_ = tim_.data() + static_cast<uint64_t>(b) * n_;
-  cur_pad_ = mode_ == 2 ? f4_in_.data() + static_cast<uint64_t>(b) * f4_.insize : nullptr;
-  cur_stats_ = wstats_.data() + 4 * static_cast<uint64_t>(b);
-  ctr_.dm_trials++;
-  const int nacc = static_cast<int>(accs.size());
-  CandidateList accel_trial_cands;
-  if (nacc == 0) return accel_trial_cands;
-  // acceleration factors (double, as device_resampleII)
-  {
-    // previous DM's batches have all retired (their events were waited on), so
-    // the host staging vector and af_ may be rewritten here
-    af_host_.resize(static_cast<size_t>(nacc));
-    for (int i = 0; i < nacc; ++i) af_host_[i] = (static_cast<double>(accs[i]) * p_.tsamp) / (2 * kC);
-    af_.resize(af_host_.size());
-    PSOUP_HIP_CHECK(hipMemcpyAsync(af_.data(), af_host_.data(), af_host_.size() * sizeof(double),
-                                   hipMemcpyHostToDevice, stream_));
+  const int njobs = static_cast<int>(jobs.size());
+  std::vector<CandidateList> by_job(static_cast<size_t>(njobs));
+  if (njobs == 0) return by_job;
+  if (mode_ != 2 && njobs > 1) {
+    // the rocFFT paths resample one series per batch: one job at a time
+    for (int j = 0; j < njobs; ++j) {
+      const Job& jb = jobs[static_cast<size_t>(j)];
+      by_job[static_cast<size_t>(j)] = search_prepared(jb.b, jb.dm, jb.dm_idx, jb.accs);
+    }
+    return by_job;
   }
+  // flat trial list: job j's trials in order, jobs in order
+  flat_job_.clear();
+  flat_acc_.clear();
+  flat_src_.clear();
+  af_host_.clear();
+  for (int j = 0; j < njobs; ++j) {
+    const Job& jb = jobs[static_cast<size_t>(j)];
+    PSOUP_CHECK(jb.b >= 0 && jb.b < prepared_, "search_prepared: trial " << jb.b << " was not prepared");
+    for (float a : jb.accs) {
+      flat_job_.push_back(j);
+      flat_acc_.push_back(a);
+      flat_src_.push_back(static_cast<uint32_t>(jb.b));
+      af_host_.push_back((static_cast<double>(a) * p_.tsamp) / (2 * kC));
+    }
+  }
+  ctr_.dm_trials += static_cast<uint64_t>(njobs);
+  const Job& j0 = jobs[0];
+  cur_tim_ = tim_.data() + static_cast<uint64_t>(j0.b) * n_;
+  cur_pad_ = mode_ == 2 ? f4_in_.data() + static_cast<uint64_t>(j0.b) * f4_.insize : nullptr;
+  cur_stats_ = wstats_.data() + 4 * static_cast<uint64_t>(j0.b);
+  const int ntr = static_cast<int>(flat_acc_.size());
+  if (ntr == 0) return by_job;
+  jobs_ = &jobs;
+  // previous batches have all retired (their events were waited on), so the
+  // device copies of the trial tables may be rewritten
+  af_.resize(af_host_.size());
+  d_src_.resize(flat_src_.size());
+  PSOUP_HIP_CHECK(hipMemcpyAsync(af_.data(), af_host_.data(), af_host_.size() * sizeof(double),
+                                 hipMemcpyHostToDevice, stream_));
+  PSOUP_HIP_CHECK(hipMemcpyAsync(d_src_.data(), flat_src_.data(), flat_src_.size() * sizeof(uint32_t),
+                                 hipMemcpyHostToDevice, stream_));
   ensure_batch_buffers();
   RoctxRange acc_range("Acceleration-Loop");
   std::deque<int> inflight;  // slot indices
   int next = 0, slot = 0;
   auto issue = [&](int sl) {
-    const int c = std::min(K_, nacc - next);
+    const int c = std::min(K_, ntr - next);
     launch_batch(slots_[sl], next, c);
     inflight.push_back(sl);
     next += c;
   };
-  while (inflight.size() < 2 && next < nacc) {
+  while (inflight.size() < 2 && next < ntr) {
     issue(slot);
     slot ^= 1;
   }
@@ -720,18 +761,20 @@ CandidateList SearchEngine::search_prepared(int b, float dm, int dm_idx, const s
     s.copied->record(copy_stream_.get());
     // the next batch that reuses this slot must wait for the copy-out
     PSOUP_HIP_CHECK(hipStreamWaitEvent(stream_, s.copied->get(), 0));
-    if (next < nacc) issue(sl);
+    if (next < ntr) issue(sl);
     s.copied->sync();
     host.start();
-    process_slot(s, b_first, b_count, cnt, dm, dm_idx, accs, accel_trial_cands);
+    process_slot(s, b_first, b_count, cnt, by_job);
     host.stop();
     ctr_.accel_trials += static_cast<uint64_t>(b_count);
   }
   ctr_.host_s += host.get_time();
-  CandidateList dm_cands = accd_.distill(std::move(accel_trial_cands));
+  std::vector<CandidateList> out(static_cast<size_t>(njobs));
+  for (int j = 0; j < njobs; ++j) out[static_cast<size_t>(j)] = accd_.distill(std::move(by_job[static_cast<size_t>(j)]));
+  jobs_ = nullptr;
   sw.stop();
   ctr_.accel_s += sw.get_time();
-  return dm_cands;
+  return out;
 }
 
 // ---------------------------------------------------------------- folding ---

@@ -309,20 +309,23 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
           // whiten the chunk's trials in batches of up to max_prepare, then search each
           for (int p0 = d0; p0 < d1; p0 += engine.max_prepare()) {
             const int cnt = std::min(engine.max_prepare(), d1 - p0);
+            if (args.fault_after_dms >= 0 && processed + cnt > args.fault_after_dms)
+              PSOUP_THROW("fault injection: device " << dev << " aborting after " << processed << " DM trials");
             engine.prepare(trials[k].data() + static_cast<uint64_t>(p0 - d0) * rstride, rstride, geom.out_nsamps,
                            cnt);
+            std::vector<SearchEngine::Job> jobs;
             for (int d = p0; d < p0 + cnt; ++d) {
-              if (args.fault_after_dms >= 0 && processed >= args.fault_after_dms)
-                PSOUP_THROW("fault injection: device " << dev << " aborting after " << processed << " DM trials");
               const float dm = setup.dm_list[static_cast<size_t>(d)];
-              std::vector<float> accs = setup.accel_plan.generate(dm);
-              log_verbose("Searching " + std::to_string(accs.size()) + " acceleration trials for DM " +
+              jobs.push_back(SearchEngine::Job{d - p0, dm, d, setup.accel_plan.generate(dm)});
+              log_verbose("Searching " + std::to_string(jobs.back().accs.size()) + " acceleration trials for DM " +
                           std::to_string(dm));
-              CandidateList c = engine.search_prepared(d - p0, dm, d, accs);
-              sh.accel_trials += accs.size();
-              for (auto& x : c) local.push_back(std::move(x));
-              processed++;
+              sh.accel_trials += jobs.back().accs.size();
             }
+            // one flat trial list over the chunk's DMs (batches span DM boundaries)
+            std::vector<CandidateList> res = engine.search_prepared_many(jobs);
+            for (auto& c : res)
+              for (auto& x : c) local.push_back(std::move(x));
+            processed += cnt;
           }
           ws.stop();
           freed[k].record(st);

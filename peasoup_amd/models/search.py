@@ -231,17 +231,17 @@ class RankSearcher:
                 step = (dms[1] - dms[0]) if len(dms) > 1 else 1
                 for p0 in range(0, len(dms), e.max_prepare):
                     part = dms[p0:p0 + e.max_prepare]
+                    with lock:
+                        if 0 <= fault_after < processed + len(part):
+                            raise RuntimeError(f"fault injection: rank {self.ctx.rank} aborting after "
+                                               f"{processed} DM trials")
+                        processed += len(part)
                     e.prepare(bufs[k].data_ptr() + (part[0] - d0) * self.row_stride, step * self.row_stride,
                               self.geom.out_nsamps, len(part))
-                    for b, d in enumerate(part):
-                        with lock:
-                            if 0 <= fault_after <= processed:
-                                raise RuntimeError(f"fault injection: rank {self.ctx.rank} aborting after "
-                                                   f"{processed} DM trials")
-                            processed += 1
-                        dm = self.dm_list[d]
-                        accs = self.accel_list(dm)
-                        per_dm[d] = e.search_prepared(b, dm, d, accs)
+                    jobs = [(b, self.dm_list[d], d, self.accel_list(self.dm_list[d])) for b, d in enumerate(part)]
+                    # one flat trial list over the part's DMs (batches span DM boundaries)
+                    for (b, dm, d, accs), c in zip(jobs, e.search_prepared_many(jobs)):
+                        per_dm[d] = c
                         with lock:
                             ntrials += len(accs)
                             if progress is not None:
