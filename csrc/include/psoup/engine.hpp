@@ -100,7 +100,8 @@ class Dedisperser {
   bool resident_ = false, valu_ready_ = false;
   std::vector<int32_t> h_tile_steps_;  // resident plan: MFMA steps per tile
   int ldo_ = 0;                        // columns of r_offT_
-  DeviceBuffer<int32_t> r_steps_, r_tile_info_, r_offT_;
+  std::vector<int32_t> h_tile_win_;    // LDS kernel: largest channel window per 32-DM tile (bytes)
+  DeviceBuffer<int32_t> r_steps_, r_tile_info_, r_offT_, r_wmin_;
   DeviceBuffer<int8_t> r_deltas_;
 };
 

@@ -78,6 +78,16 @@ void dedisperse_valu(const int8_t* chan_major, uint64_t chan_stride, const int32
                      const int32_t* d_offT, int ldo, int d_base, int ndm, uint64_t out_nsamps, uint8_t* out,
                      uint64_t out_stride, float scale, int nbits, int bias, hipStream_t s);
 
+// LDS-staged packed-byte kernel: same contract as dedisperse_valu for ranges
+// starting on a 32-DM tile, plus d_wmin [tile][nactive] = each tile's
+// smallest offset per channel rounded down to 16 and max_window = the largest
+// (tile, channel) window 1024 + (max offset - wmin) + 32 bytes.
+bool dedisperse_lds_fits(int nbits, int nactive, int max_window);
+void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_active, int nactive,
+                    const int32_t* d_offT, int ldo, int d_base, int ndm, const int32_t* d_wmin, int max_window,
+                    uint64_t out_nsamps, uint8_t* out, uint64_t out_stride, float scale, int nbits, int bias,
+                    hipStream_t s);
+
 // ------------------------------------------------------------ time series ---
 // count > 1: rows b at in + b*in_stride, sums sum[b], outputs out + b*out_stride.
 void u8_sum(const uint8_t* in, uint64_t n, unsigned long long* sum, hipStream_t s, int count = 1,

@@ -13,6 +13,7 @@
 //     shifted data (A: 32 samples x 32 (channel,shift) pairs) with a one-hot
 //     selection matrix (B: 32 (channel,shift) pairs x 32 DMs); see below.
 #include <algorithm>
+#include <cstdlib>
 #include <utility>
 #include <vector>
 
@@ -286,6 +287,133 @@ __global__ void __launch_bounds__(256) dedisperse_valu_kernel(
   }
 }
 
+
+// LDS-staged variant of the packed-byte kernel (narrow sample: nbits <= 4).
+// Per channel the workgroup (32 DMs x 1024 samples) stages the channel's
+// window -- from the tile's smallest offset, 16-byte aligned, 1024 + spread
+// + 32 bytes -- once, with aligned dwordx4 loads one channel ahead (double
+// buffer, one barrier per channel); each lane then reads its 32 bytes per DM
+// as two conflict-free ds_read_b128 and picks 5 words at the wave-uniform
+// word offset (uniform branch) before the same v_perm/add accumulation.
+// wmin[tile][ci]: the window start (relative to the sample) of tile and channel.
+constexpr int kLdsWinWords = 2048;  // 8 KiB per buffer
+
+template <int Q>
+__device__ __forceinline__ void lds_accumulate(const uint32_t* w, uint32_t sh, uint32_t (&pk)[8]) {
+  const uint32_t selE = 0x0C000C00u | sh | ((sh + 2) << 16);
+  const uint32_t selO = selE + 0x00010001u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pk[2 * i] += __builtin_amdgcn_perm(w[Q + i + 1], w[Q + i], selE);
+    pk[2 * i + 1] += __builtin_amdgcn_perm(w[Q + i + 1], w[Q + i], selO);
+  }
+}
+
+template <bool XOR, int PASSES, bool UNALIGNED, int DPT>
+__global__ void __launch_bounds__(256) dedisperse_lds_kernel(
+    const int8_t* __restrict__ x, uint64_t stride, const int32_t* __restrict__ active, int nactive,
+    const int32_t* __restrict__ offT, int ldo, int d_base, int ndm, const int32_t* __restrict__ wmin,
+    uint64_t out_nsamps, uint8_t* __restrict__ out, uint64_t out_stride, float scale, int win_chunks) {
+  __shared__ __attribute__((aligned(16))) uint32_t win[2][kLdsWinWords];
+  // workgroup = 4*DPT DMs (DPT = 8: one 32-DM tile; 4: half a tile, more
+  // workgroups per CU to hide the channel-window loads)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int dm0 = blockIdx.x * (4 * DPT) + wave * DPT;  // relative to d_base
+  const int tile = (blockIdx.x * 4 * DPT) / 32;
+  const uint64_t tb = static_cast<uint64_t>(blockIdx.y) * 1024;
+  const uint64_t t = tb + static_cast<uint64_t>(lane) * 16;
+  const int32_t* wm = wmin + static_cast<uint64_t>(d_base / 32 + tile) * nactive;
+  uint32_t pk[DPT][8];
+#pragma unroll
+  for (int j = 0; j < DPT; ++j)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) pk[j][q] = 0;
+  u32x4 r[PASSES];
+  // every thread stages 16 bytes per pass (predicating the loads to the
+  // launch's largest window measured slower: 2.57 vs 2.2 ms per 32-DM chunk)
+  (void)win_chunks;
+  auto gload = [&](int ci) {
+    const int8_t* row = x + static_cast<uint64_t>(active[ci]) * stride + tb + wm[ci];
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p)
+      r[p] = *reinterpret_cast<const u32x4*>(row + 4096 * p + 16 * threadIdx.x);
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int p = 0; p < PASSES; ++p) {
+      if constexpr (XOR) r[p] ^= 0x80808080u;
+      *reinterpret_cast<u32x4*>(&win[buf][1024 * p + 4 * threadIdx.x]) = r[p];
+    }
+  };
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int ci = 0; ci < nactive; ++ci) {
+    const int buf = ci & 1;
+    if (ci + 1 < nactive) gload(ci + 1);  // in flight during this channel's sums
+    const int w0 = wm[ci];
+    const int32_t* o = offT + static_cast<uint64_t>(ci) * ldo + d_base + dm0;
+    // all DPT windows' LDS reads first (latency overlapped), then the sums
+    int rel[DPT];
+    uint32_t w[DPT][8];
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      rel[j] = o[j] - w0;  // >= 0, wave-uniform
+      if constexpr (UNALIGNED) {
+        // each lane's 20 bytes from the dword holding its first sample
+        // (dword-aligned ds_read_b128 + ds_read_b32); v_perm does the byte shift
+        const uint32_t* src = &win[buf][4 * lane + (rel[j] >> 2)];
+        const u32x4 a = *reinterpret_cast<const u32x4_a4*>(src);
+        w[j][0] = a[0]; w[j][1] = a[1]; w[j][2] = a[2]; w[j][3] = a[3];
+        w[j][4] = src[4];
+      } else {
+        const uint32_t* src = &win[buf][4 * lane + ((rel[j] >> 4) << 2)];
+        const u32x4 a = *reinterpret_cast<const u32x4*>(src);
+        const u32x4 b = *reinterpret_cast<const u32x4*>(src + 4);
+        w[j][0] = a[0]; w[j][1] = a[1]; w[j][2] = a[2]; w[j][3] = a[3];
+        w[j][4] = b[0]; w[j][5] = b[1]; w[j][6] = b[2]; w[j][7] = b[3];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < DPT; ++j) {
+      const uint32_t sh = static_cast<uint32_t>(rel[j] & 3);
+      if constexpr (UNALIGNED) {
+        lds_accumulate<0>(w[j], sh, pk[j]);
+      } else {
+        switch ((rel[j] >> 2) & 3) {  // uniform
+          case 0: lds_accumulate<0>(w[j], sh, pk[j]); break;
+          case 1: lds_accumulate<1>(w[j], sh, pk[j]); break;
+          case 2: lds_accumulate<2>(w[j], sh, pk[j]); break;
+          default: lds_accumulate<3>(w[j], sh, pk[j]); break;
+        }
+      }
+    }
+    if (ci + 1 < nactive) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  if (t >= out_nsamps) return;
+#pragma unroll
+  for (int j = 0; j < DPT; ++j) {
+    const int d = dm0 + j;
+    if (d >= ndm) break;
+    uint32_t ob[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int s0 = static_cast<int>(pk[j][2 * i] & 0xFFFF), s2 = static_cast<int>(pk[j][2 * i] >> 16);
+      const int s1 = static_cast<int>(pk[j][2 * i + 1] & 0xFFFF), s3 = static_cast<int>(pk[j][2 * i + 1] >> 16);
+      ob[i] = static_cast<uint32_t>(scale_out(s0, scale)) | (static_cast<uint32_t>(scale_out(s1, scale)) << 8) |
+              (static_cast<uint32_t>(scale_out(s2, scale)) << 16) | (static_cast<uint32_t>(scale_out(s3, scale)) << 24);
+    }
+    uint8_t* orow = out + static_cast<uint64_t>(d) * out_stride + t;
+    if (t + 16 <= out_nsamps) {
+      *reinterpret_cast<u32x4*>(orow) = u32x4{ob[0], ob[1], ob[2], ob[3]};
+    } else {
+      for (uint64_t e = 0; t + e < out_nsamps; ++e) orow[e] = static_cast<uint8_t>(ob[e >> 2] >> (8 * (e & 3)));
+    }
+  }
+}
+
 }  // namespace
 
 void dedisperse_direct(const int8_t* chan_major, uint64_t chan_stride, int nchans, const int32_t* offsets,
@@ -411,6 +539,60 @@ void dedisperse_valu(const int8_t* chan_major, uint64_t chan_stride, const int32
   }
 #undef PSOUP_VALU_LAUNCH
   post_launch_check("dedisperse_valu_kernel", s);
+}
+
+bool dedisperse_lds_fits(int nbits, int nactive, int max_window) {
+  const uint64_t max_raw = (1ull << std::min(nbits, 8)) - 1;
+  return max_raw * static_cast<uint64_t>(nactive) <= 65535 && max_window <= 4 * kLdsWinWords;
+}
+
+void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_active, int nactive,
+                    const int32_t* d_offT, int ldo, int d_base, int ndm, const int32_t* d_wmin, int max_window,
+                    uint64_t out_nsamps, uint8_t* out, uint64_t out_stride, float scale, int nbits, int bias,
+                    hipStream_t s) {
+  if (ndm <= 0 || out_nsamps == 0 || nactive <= 0) return;
+  PSOUP_CHECK(d_base % 32 == 0, "dedisperse_lds: range must start on a 32-DM tile");
+  PSOUP_CHECK(dedisperse_lds_fits(nbits, nactive, max_window), "dedisperse_lds: window or sums too large");
+  PSOUP_CHECK((chan_stride & 15) == 0 && (out_stride & 15) == 0, "dedisperse_lds: stride alignment");
+  const uint64_t ty = (out_nsamps + 1023) / 1024;
+  PSOUP_CHECK(ty <= 65535, "dedisperse_lds: series too long for the grid");
+  static const int dpt = [] {
+    const char* e = std::getenv("PSOUP_DEDISP_LDS_DPT");  // A/B knob: DMs per wave, 8 or 4
+    return e && std::atoi(e) == 8 ? 8 : 4;  // 4: 141 ms vs 173 ms for the config-4 DM list
+  }();
+  dim3 grid(static_cast<unsigned>((ndm + 4 * dpt - 1) / (4 * dpt)), static_cast<unsigned>(ty));
+  PSOUP_CHECK(d_base + static_cast<int>(grid.x) * 4 * dpt <= ldo, "dedisperse_lds: offset table too narrow");
+  const bool two = max_window > 4096;
+  const bool xr = bias == 128;
+  // LDS read form: 1 = two 16-byte-aligned b128 + uniform word-select branch
+  // (default, 172 ms for the 2026-DM config-4 list), 2 = one dword-aligned
+  // (split) b128 + b32 per DM (214 ms)
+  static const int form = [] {
+    const char* e = std::getenv("PSOUP_DEDISP_LDS_FORM");
+    return e ? std::atoi(e) : 1;
+  }();
+#define PSOUP_LDS_LAUNCH(X, P, U)                                                                          \
+  if (dpt == 4)                                                                                               \
+    dedisperse_lds_kernel<X, P, U, 4><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive, d_offT, \
+                                                           ldo, d_base, ndm, d_wmin, out_nsamps, out, out_stride, \
+                                                           scale, (max_window + 15) / 16);                    \
+  else                                                                                                        \
+    dedisperse_lds_kernel<X, P, U, 8><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive, d_offT, \
+                                                           ldo, d_base, ndm, d_wmin, out_nsamps, out, out_stride, \
+                                                           scale, (max_window + 15) / 16)
+#define PSOUP_LDS_LAUNCH_U(X, P)   \
+  if (form == 1)                   \
+    PSOUP_LDS_LAUNCH(X, P, false); \
+  else                             \
+    PSOUP_LDS_LAUNCH(X, P, true)
+  if (xr) {
+    if (two) { PSOUP_LDS_LAUNCH_U(true, 2); } else { PSOUP_LDS_LAUNCH_U(true, 1); }
+  } else {
+    if (two) { PSOUP_LDS_LAUNCH_U(false, 2); } else { PSOUP_LDS_LAUNCH_U(false, 1); }
+  }
+#undef PSOUP_LDS_LAUNCH_U
+#undef PSOUP_LDS_LAUNCH
+  post_launch_check("dedisperse_lds_kernel", s);
 }
 
 }  // namespace kern

@@ -146,6 +146,25 @@ void Dedisperser::build_valu_tables() {
       t[ci * ldo_ + d] = offs[static_cast<size_t>(std::min(d, ndm - 1)) * g.nchans + active[ci]];
   r_offT_.resize(t.size());
   PSOUP_HIP_CHECK(hipMemcpy(r_offT_.data(), t.data(), t.size() * 4, hipMemcpyHostToDevice));
+  // LDS kernel windows: per 32-DM tile and channel, the smallest offset
+  // (rounded down to 16 bytes) and the window length it must stage
+  const int ntiles = ldo_ / kTileDms;
+  const size_t na = std::max<size_t>(1, active.size());
+  std::vector<int32_t> wmin(static_cast<size_t>(ntiles) * na, 0);
+  h_tile_win_.assign(static_cast<size_t>(ntiles), 0);
+  for (int T = 0; T < ntiles; ++T)
+    for (size_t ci = 0; ci < active.size(); ++ci) {
+      int lo = t[ci * ldo_ + T * kTileDms], hi = lo;
+      for (int k = 1; k < kTileDms; ++k) {
+        lo = std::min(lo, t[ci * ldo_ + T * kTileDms + k]);
+        hi = std::max(hi, t[ci * ldo_ + T * kTileDms + k]);
+      }
+      const int w0 = lo & ~15;
+      wmin[static_cast<size_t>(T) * na + ci] = w0;
+      h_tile_win_[static_cast<size_t>(T)] = std::max(h_tile_win_[static_cast<size_t>(T)], 1024 + (hi - w0) + 32);
+    }
+  r_wmin_.resize(wmin.size());
+  PSOUP_HIP_CHECK(hipMemcpy(r_wmin_.data(), wmin.data(), wmin.size() * 4, hipMemcpyHostToDevice));
   valu_ready_ = true;
 }
 
@@ -172,7 +191,14 @@ double Dedisperser::mfma_steps_per_channel(int d0, int d1) {
 DedispKernel Dedisperser::choose(int d0, int d1) {
   const auto& g = fb_.geometry();
   if (g.nactive == 0 || d0 >= d1) return DedispKernel::Mfma;
-  return mfma_steps_per_channel(d0, d1) > valu_ratio() ? DedispKernel::Valu : DedispKernel::Mfma;
+  // the LDS-staged packed-byte kernel (tile-aligned ranges, narrow samples)
+  // beats the MFMA plan from ~1.0 steps per channel, the global-load one from 1.85
+  if (!valu_ready_) build_valu_tables();
+  int win = 0;
+  for (int T = d0 / kTileDms; T <= (d1 - 1) / kTileDms; ++T) win = std::max(win, h_tile_win_[static_cast<size_t>(T)]);
+  const bool lds = d0 % kTileDms == 0 && kern::dedisperse_lds_fits(g.nbits, g.nactive, win);
+  const double ratio = lds ? valu_ratio() * (1.0 / 1.85) : valu_ratio();
+  return mfma_steps_per_channel(d0, d1) > ratio ? DedispKernel::Valu : DedispKernel::Mfma;
 }
 
 void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispKernel kind, hipStream_t s) {
@@ -186,8 +212,18 @@ void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispK
   const int ndm = d1 - d0;
   if (kind == DedispKernel::Valu) {
     if (!valu_ready_) build_valu_tables();
-    kern::dedisperse_valu(fb_.data(), fb_.stride(), d_active_.data(), g.nactive, r_offT_.data(), ldo_, d0, ndm,
-                          g.out_nsamps, out, out_stride, g.out_scale, g.nbits, g.bias, s);
+    static const bool lds_on = [] {
+      const char* e = std::getenv("PSOUP_DEDISP_LDS");  // A/B knob: 0 = global-load kernel only
+      return !(e && std::atoi(e) == 0);
+    }();
+    int win = 0;
+    for (int T = d0 / kTileDms; T <= (d1 - 1) / kTileDms; ++T) win = std::max(win, h_tile_win_[static_cast<size_t>(T)]);
+    if (lds_on && d0 % kTileDms == 0 && kern::dedisperse_lds_fits(g.nbits, g.nactive, win))
+      kern::dedisperse_lds(fb_.data(), fb_.stride(), d_active_.data(), g.nactive, r_offT_.data(), ldo_, d0, ndm,
+                           r_wmin_.data(), win, g.out_nsamps, out, out_stride, g.out_scale, g.nbits, g.bias, s);
+    else
+      kern::dedisperse_valu(fb_.data(), fb_.stride(), d_active_.data(), g.nactive, r_offT_.data(), ldo_, d0, ndm,
+                            g.out_nsamps, out, out_stride, g.out_scale, g.nbits, g.bias, s);
     return;
   }
   const int ntiles = (ndm + kTileDms - 1) / kTileDms;
