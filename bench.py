@@ -5,7 +5,8 @@ an 8-harmonic sum (-n 3), one process per MI355X (torchrun for N > 1).
 One step (per rank, weak scaling -- fixed work per GPU):
   * dedisperse this rank's DM shard (``--dms-per-gpu`` trials, default 8, one
     chunk -- the production pipeline dedisperses 16-DM chunks) from the
-    resident 1024-channel 2-bit filterbank with the MFMA dedispersion kernel,
+    resident 1024-channel 2-bit filterbank (Auto kernel choice: one-hot MFMA at
+    these low DMs, packed-byte VALU/LDS for wide tiles),
   * whiten each trial and search +-500 m/s^2 (legacy acceleration-plan
     convention: ~684 trials per DM at 2^23 x 64 us) with an 8-harmonic sum:
     fused resample + two-pass four-step FFT -> paired real-FFT post-processing
@@ -159,7 +160,7 @@ def main() -> int:
             "config": {
                 "model": f"peasoup accel search: 2^{a.log2n}-pt series, +-{a.acc:g} m/s^2 (legacy plan), "
                          f"{1 << a.nharmonics}-harmonic sum, {a.nchans}-ch {a.nbits}-bit filterbank, "
-                         f"MFMA dedispersion",
+                         f"auto dedispersion kernel",
                 "global_batch": trials_per_step,
                 "seq_len": n,
                 "parallelism": f"dm{ctx.world_size}",
