@@ -58,7 +58,8 @@ def init(backend: Optional[str] = None, timeout_s: float = 1800.0) -> DistContex
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     has_gpu = torch.cuda.is_available() and torch.cuda.device_count() > 0
     if backend is None:
-        backend = "nccl" if has_gpu else "gloo"
+        # PSOUP_DIST_BACKEND=gloo rehearses multi-rank runs with several ranks on one GPU
+        backend = os.environ.get("PSOUP_DIST_BACKEND") or ("nccl" if has_gpu else "gloo")
     device = torch.device("cpu")
     if has_gpu and backend == "nccl":
         ndev = torch.cuda.device_count()
