@@ -38,7 +38,12 @@ namespace {
 
 constexpr int kPts = 8;     // points per thread per transform
 constexpr int kSplit = 11;  // W_M^a = hi[a >> kSplit] * lo[a & (2^kSplit - 1)]
-constexpr int kLdsBudget = 73728;  // bytes per workgroup: two workgroups per CU
+constexpr int kLdsBudget = 74752;  // bytes per workgroup: two workgroups per CU
+// Channel planes in the exchange buffer are kChanPad complex elements apart
+// beyond the padded length: with a plane stride that is a multiple of 64
+// elements the compiler pairs two channels' accesses into ds_read2st64_b64 /
+// ds_write2st64_b64, which run at half the LDS rate of two ds_read_b64.
+constexpr int kChanPad = 8;
 
 // CPT = transforms per thread, SUB = thread groups per workgroup; the
 // workgroup covers CH = CPT*SUB adjacent columns/rows (8: 64-byte row
@@ -49,7 +54,7 @@ struct Cfg {
   static_assert(CH == 8 || (CH == 4 && SUB == 1), "workgroups cover 8 (or, blocked, 4) transforms");
   static constexpr int T = L / kPts;                     // threads per group
   static constexpr int THREADS = T * SUB;
-  static constexpr int PAD = L + L / 8;                  // padded floats per channel plane
+  static constexpr int PAD = L + L / 8 + kChanPad;       // complex elements per channel plane
   static constexpr int BUDGET = CH == 4 ? kLdsBudget / 2 : kLdsBudget;  // CH 4: four workgroups per CU
   static constexpr int CG0 = BUDGET / (SUB * 2 * PAD * 4);
   static constexpr int CG = CG0 >= CPT ? CPT : (CG0 >= 4 ? 4 : (CG0 >= 2 ? 2 : 1));  // channels per exchange round
@@ -148,7 +153,7 @@ __device__ __forceinline__ void stage_compute(Vec<CPT>& v, int t, const float2* 
 // gather back in the uniform pattern t + q*T.
 template <int L, int CPT, int CG, int Ns, int R>
 __device__ __forceinline__ void exchange(Vec<CPT>& v, float* __restrict__ lds, int t) {
-  constexpr int T = L / kPts, B = kPts / R, PAD = L + L / 8;  // PAD in complex elements
+  constexpr int T = L / kPts, B = kPts / R, PAD = L + L / 8 + kChanPad;  // plane stride, complex elements
   float2* buf = reinterpret_cast<float2*>(lds);                   // 8-byte ds_write_b64 / ds_read_b64
 #pragma unroll
   for (int g = 0; g < CPT; g += CG) {
