@@ -72,12 +72,13 @@ class RankFfa:
         self.row_stride = _C.Dedisperser.row_stride(self.geom.out_nsamps)
         self._trials: Optional[torch.Tensor] = None
 
-    def search(self, dm_indices, chunk: int = 16) -> list:
-        idx = list(dm_indices)
+    def search(self, dm_indices, chunk: int = 32) -> list:
+        from .search import RankSearcher
+
         out: list = []
-        for c0 in range(0, len(idx), chunk):
-            block = idx[c0:c0 + chunk]
-            d0, d1 = block[0], block[-1] + 1
+        # chunks cut at multiples of the dedispersion tile (resident plans)
+        for d0, d1 in RankSearcher.chunk_ranges(dm_indices, chunk):
+            block = range(d0, d1)
             need = (d1 - d0) * self.row_stride
             if self._trials is None or self._trials.numel() < need:
                 self._trials = torch.empty(need, dtype=torch.uint8, device=self.ctx.device)
