@@ -106,16 +106,21 @@ void normalise(float* x, uint64_t n, float mean, float sigma, hipStream_t s);
 void normalise_dev(float* x, uint64_t n, const float* stats, float scale, hipStream_t s);
 
 // running median (Dereddener::calculate_median): out_count = count/5
-void median5_amp(const float2* X, uint64_t nbins, float* out, hipStream_t s);
-void median5(const float* in, uint64_t count, float* out, hipStream_t s);
+// batch > 1: item b at X + b*xstride / in + b*istride -> out + b*ostride
+void median5_amp(const float2* X, uint64_t nbins, float* out, hipStream_t s, int batch = 1, uint64_t xstride = 0,
+                 uint64_t ostride = 0);
+void median5(const float* in, uint64_t count, float* out, hipStream_t s, int batch = 1, uint64_t istride = 0,
+             uint64_t ostride = 0);
 // X[k] /= median(k) (k<5 -> 0), then zapped bins -> 1+0i. median(k) is the
 // piecewise linear stretch of m5/m25/m125 at boundaries pos5/pos25.
 void deredden_zap(float2* X, uint64_t nbins, const float* m5, uint64_t n5, const float* m25, uint64_t n25,
                   const float* m125, uint64_t n125, int64_t pos5, int64_t pos25, const uint32_t* zapmask,
-                  hipStream_t s);
+                  hipStream_t s, int batch = 1, uint64_t xstride = 0, uint64_t mstride = 0);
 // P = interbin(X); per-block partial sums of P and P^2 -> stats {mean,rms,std}
+// batch > 1 (P == nullptr): item b's spectrum at X + b*xstride, partials at
+// partials + 2*npartials*b, stats at stats + 4*b
 void interbin_stats(const float2* X, uint64_t nbins, float* P, double* partials, int npartials, float* stats,
-                    hipStream_t s);
+                    hipStream_t s, int batch = 1, uint64_t xstride = 0);
 
 // ------------------------------------------------------------- resampling ---
 // out[k][i] = in[clamp(rint(i + i*af_k*(i - n)))], af_k = acc_k*tsamp/(2c)

@@ -12,7 +12,7 @@ namespace psoup {
 namespace kern {
 
 __global__ void stats_finalize_kernel(const double* __restrict__ partials, int npart, uint64_t n,
-                                      float* __restrict__ stats);
+                                      float* __restrict__ stats, int pstride);
 
 namespace {
 
@@ -57,7 +57,10 @@ __global__ void __launch_bounds__(256) normalise_dev_kernel(float* __restrict__ 
 }
 
 __global__ void __launch_bounds__(256) median5_amp_kernel(const float2* __restrict__ X, uint64_t nout,
-                                                          float* __restrict__ out) {
+                                                          float* __restrict__ out, uint64_t xstride,
+                                                          uint64_t ostride) {
+  X += blockIdx.y * xstride;
+  out += blockIdx.y * ostride;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < nout; i += stride) {
     const float2* p = X + 5 * i;
@@ -67,7 +70,9 @@ __global__ void __launch_bounds__(256) median5_amp_kernel(const float2* __restri
 }
 
 __global__ void __launch_bounds__(256) median5_kernel(const float* __restrict__ in, uint64_t nout,
-                                                      float* __restrict__ out) {
+                                                      float* __restrict__ out, uint64_t istride, uint64_t ostride) {
+  in += blockIdx.y * istride;
+  out += blockIdx.y * ostride;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < nout; i += stride) {
     const float* p = in + 5 * i;
@@ -75,8 +80,11 @@ __global__ void __launch_bounds__(256) median5_kernel(const float* __restrict__ 
   }
 }
 
-__global__ void median_small_kernel(const float* __restrict__ in, int count, float* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+__global__ void median_small_kernel(const float* __restrict__ in, int count, float* __restrict__ out,
+                                    uint64_t istride, uint64_t ostride) {
+  if (threadIdx.x != 0) return;
+  in += blockIdx.x * istride;
+  out += blockIdx.x * ostride;
   float r;
   if (count == 1) r = in[0];
   else if (count == 2) r = 0.5f * (in[0] + in[1]);
@@ -102,7 +110,12 @@ __global__ void __launch_bounds__(256) deredden_zap_kernel(float2* __restrict__ 
                                                            const float* __restrict__ m25, uint64_t n25,
                                                            float step25, const float* __restrict__ m125,
                                                            uint64_t n125, float step125, int64_t pos5,
-                                                           int64_t pos25, const uint32_t* __restrict__ zapmask) {
+                                                           int64_t pos25, const uint32_t* __restrict__ zapmask,
+                                                           uint64_t xstride, uint64_t mstride) {
+  X += blockIdx.y * xstride;  // batch item blockIdx.y: its spectrum and medians
+  m5 += blockIdx.y * mstride;
+  m25 += blockIdx.y * mstride;
+  m125 += blockIdx.y * mstride;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t k = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; k < nbins; k += stride) {
     float2 x;
@@ -122,8 +135,11 @@ __global__ void __launch_bounds__(256) deredden_zap_kernel(float2* __restrict__ 
 
 __global__ void __launch_bounds__(256) interbin_moments_kernel(const float2* __restrict__ X, uint64_t nbins,
                                                                float* __restrict__ P,
-                                                               double* __restrict__ partials) {
+                                                               double* __restrict__ partials, uint64_t xstride,
+                                                               int pstride) {
   __shared__ double scratch[4];
+  X += blockIdx.y * xstride;
+  partials += static_cast<uint64_t>(blockIdx.y) * pstride;
   double s = 0.0, s2 = 0.0;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < nbins; i += stride) {
@@ -168,41 +184,53 @@ void normalise_dev(float* x, uint64_t n, const float* stats, float scale, hipStr
   post_launch_check("normalise_dev_kernel", s);
 }
 
-void median5_amp(const float2* X, uint64_t nbins, float* out, hipStream_t s) {
+void median5_amp(const float2* X, uint64_t nbins, float* out, hipStream_t s, int batch, uint64_t xstride,
+                 uint64_t ostride) {
   uint64_t nout = nbins / 5;
   if (nout == 0) PSOUP_THROW("median5_amp needs >= 5 bins");
-  median5_amp_kernel<<<dev::grid_for(nout, 256), 256, 0, s>>>(X, nout, out);
+  PSOUP_CHECK(batch >= 1 && batch <= 65535, "median5_amp: bad batch");
+  const dim3 grid(dev::grid_for(nout, 256, batch > 1 ? 512 : 2048), static_cast<unsigned>(batch));
+  median5_amp_kernel<<<grid, 256, 0, s>>>(X, nout, out, xstride, ostride);
   post_launch_check("median5_amp_kernel", s);
 }
 
-void median5(const float* in, uint64_t count, float* out, hipStream_t s) {
+void median5(const float* in, uint64_t count, float* out, hipStream_t s, int batch, uint64_t istride,
+             uint64_t ostride) {
   if (count == 0) return;
+  PSOUP_CHECK(batch >= 1 && batch <= 65535, "median5: bad batch");
   if (count < 5) {
-    median_small_kernel<<<1, 64, 0, s>>>(in, static_cast<int>(count), out);
+    median_small_kernel<<<static_cast<unsigned>(batch), 64, 0, s>>>(in, static_cast<int>(count), out, istride,
+                                                                     ostride);
     post_launch_check("median_small_kernel", s);
     return;
   }
   uint64_t nout = count / 5;
-  median5_kernel<<<dev::grid_for(nout, 256), 256, 0, s>>>(in, nout, out);
+  const dim3 grid(dev::grid_for(nout, 256, batch > 1 ? 512 : 2048), static_cast<unsigned>(batch));
+  median5_kernel<<<grid, 256, 0, s>>>(in, nout, out, istride, ostride);
   post_launch_check("median5_kernel", s);
 }
 
 void deredden_zap(float2* X, uint64_t nbins, const float* m5, uint64_t n5, const float* m25, uint64_t n25,
                   const float* m125, uint64_t n125, int64_t pos5, int64_t pos25, const uint32_t* zapmask,
-                  hipStream_t s) {
+                  hipStream_t s, int batch, uint64_t xstride, uint64_t mstride) {
   PSOUP_CHECK(n5 >= 1 && n25 >= 1 && n125 >= 1, "running median needs >= 125 bins");
-  deredden_zap_kernel<<<dev::grid_for(nbins, 256), 256, 0, s>>>(
-      X, nbins, m5, n5, stretch_step(n5, nbins), m25, n25, stretch_step(n25, nbins), m125, n125,
-      stretch_step(n125, nbins), pos5, pos25, zapmask);
+  PSOUP_CHECK(batch >= 1 && batch <= 65535, "deredden_zap: bad batch");
+  const dim3 grid(dev::grid_for(nbins, 256, batch > 1 ? 512 : 2048), static_cast<unsigned>(batch));
+  deredden_zap_kernel<<<grid, 256, 0, s>>>(X, nbins, m5, n5, stretch_step(n5, nbins), m25, n25,
+                                           stretch_step(n25, nbins), m125, n125, stretch_step(n125, nbins), pos5,
+                                           pos25, zapmask, xstride, mstride);
   post_launch_check("deredden_zap_kernel", s);
 }
 
 void interbin_stats(const float2* X, uint64_t nbins, float* P, double* partials, int npartials, float* stats,
-                    hipStream_t s) {
-  unsigned grid = dev::grid_for(nbins, 256, static_cast<unsigned>(npartials));
-  interbin_moments_kernel<<<grid, 256, 0, s>>>(X, nbins, P, partials);
+                    hipStream_t s, int batch, uint64_t xstride) {
+  PSOUP_CHECK(batch >= 1 && batch <= 65535 && (batch == 1 || P == nullptr), "interbin_stats: bad batch");
+  const unsigned gx = dev::grid_for(nbins, 256, static_cast<unsigned>(npartials));
+  interbin_moments_kernel<<<dim3(gx, static_cast<unsigned>(batch)), 256, 0, s>>>(X, nbins, P, partials, xstride,
+                                                                                 2 * npartials);
   post_launch_check("interbin_moments_kernel", s);
-  stats_finalize_kernel<<<1, 256, 0, s>>>(partials, static_cast<int>(grid), nbins, stats);
+  stats_finalize_kernel<<<static_cast<unsigned>(batch), 256, 0, s>>>(partials, static_cast<int>(gx), nbins, stats,
+                                                                      2 * npartials);
   post_launch_check("stats_finalize_kernel", s);
 }
 

@@ -96,8 +96,10 @@ __global__ void __launch_bounds__(256) f32_moments_kernel(const float* __restric
 // Final reduction shared with spectrum.hip: stats = {mean, rms, std} as the
 // reference's stats::stats (float mean/rms, std = sqrt(rms^2 - mean^2)).
 __global__ void __launch_bounds__(256) stats_finalize_kernel(const double* __restrict__ partials, int npart,
-                                                             uint64_t n, float* __restrict__ stats) {
+                                                             uint64_t n, float* __restrict__ stats, int pstride) {
   __shared__ double scratch[4];
+  partials += static_cast<uint64_t>(blockIdx.x) * pstride;  // batch item blockIdx.x
+  stats += 4 * blockIdx.x;
   double s = 0.0, s2 = 0.0;
   for (int i = threadIdx.x; i < npart; i += blockDim.x) {
     s += partials[2 * i];
@@ -139,7 +141,7 @@ void f32_stats(const float* x, uint64_t n, double* partials, int npartials, floa
   unsigned grid = dev::grid_for(n, 256, static_cast<unsigned>(npartials));
   f32_moments_kernel<<<grid, 256, 0, s>>>(x, n, partials);
   post_launch_check("f32_moments_kernel", s);
-  stats_finalize_kernel<<<1, 256, 0, s>>>(partials, static_cast<int>(grid), n, stats_out);
+  stats_finalize_kernel<<<1, 256, 0, s>>>(partials, static_cast<int>(grid), n, stats_out, 0);
   post_launch_check("stats_finalize_kernel", s);
 }
 

@@ -272,12 +272,6 @@ Whitener::Whitener(uint64_t n, float tsamp, hipStream_t stream, bool allow_fft4)
     // single-transform grids of both passes need n1/8 % 16 == 0 and n2/8 % 8 == 0
     f4_ = g4_.ok && g4_.n1 >= 128 && g4_.n2 >= 64;
   }
-  if (f4_) {
-    auto tab = kern::fft4_tables(g4_);
-    tab4_.resize(tab.size());
-    PSOUP_HIP_CHECK(hipMemcpy(tab4_.data(), tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice));
-    ensure_batch(1);
-  }
   fser_.resize(nb);
   m5_.resize(nb / 5);
   m25_.resize(std::max<uint64_t>(1, nb / 5 / 5));
@@ -285,6 +279,12 @@ Whitener::Whitener(uint64_t n, float tsamp, hipStream_t stream, bool allow_fft4)
   partials_.resize(2 * 1024);
   stats_.resize(4);
   sum_.resize(1);
+  if (f4_) {
+    auto tab = kern::fft4_tables(g4_);
+    tab4_.resize(tab.size());
+    PSOUP_HIP_CHECK(hipMemcpy(tab4_.data(), tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice));
+    ensure_batch(1);
+  }
 }
 
 FftPlan& Whitener::r2c() {
@@ -351,7 +351,8 @@ void Whitener::whiten(float* d_series, const uint32_t* d_zapmask, bool with_stat
 
 uint64_t Whitener::batch_bytes_per_trial() const {
   if (!f4_) return 0;
-  return g4_.ystride * 8 + g4_.xstride * 8 + nbins() * 8 + (n_ / 2) * 8 + g4_.insize * 4;
+  return g4_.ystride * 8 + g4_.xstride * 8 + nbins() * 8 + (n_ / 2) * 8 + g4_.insize * 4 +
+         3 * (nbins() / 5 + 1) * 4 + 2 * 1024 * 8;
 }
 
 void Whitener::ensure_batch(int count) {
@@ -362,6 +363,12 @@ void Whitener::ensure_batch(int count) {
   in4_.resize(g4_.insize * count);
   bspec_.resize(nbins() * count);
   bsum_.resize(static_cast<uint64_t>(count));
+  // running medians / stats partials of every batch item (stride: n5)
+  const uint64_t ms = std::max<uint64_t>(1, nbins() / 5);
+  m5_.resize(ms * count);
+  m25_.resize(ms * count);
+  m125_.resize(ms * count);
+  partials_.resize(2 * 1024 * static_cast<uint64_t>(count));
   af0_.resize(static_cast<uint64_t>(count));
   af0_.zero_async(stream_);
   bcap_ = count;
@@ -395,8 +402,18 @@ void Whitener::whiten_batch(const uint8_t* d_trials, uint64_t row_stride, uint64
   kern::fft4_resample_colpass(d_out, in4_.data(), n_, af0_.data(), count, y4_.data(), g, tab4_.data(), stream_);
   kern::fft4_rowpass(y4_.data(), x4_.data(), count, g4_, tab4_.data(), stream_);
   kern::fft4_r2c_half(x4_.data(), M, L, bspec_.data(), stream_, count, g4_.xstride, nb);
-  for (int b = 0; b < count; ++b)
-    dered_stats(bspec_.data() + static_cast<uint64_t>(b) * nb, d_zapmask, d_stats + 4 * b, boundary5, boundary25);
+  {
+    // running median, dereddening + zapping and interbin stats of all items
+    const uint64_t n5 = nb / 5, n25 = n5 / 5, n125 = n25 / 5, ms = std::max<uint64_t>(1, n5);
+    kern::median5_amp(bspec_.data(), nb, m5_.data(), stream_, count, nb, ms);
+    kern::median5(m5_.data(), n5, m25_.data(), stream_, count, ms, ms);
+    kern::median5(m25_.data(), n25, m125_.data(), stream_, count, ms, ms);
+    const int64_t pos5 = static_cast<int64_t>(static_cast<int>(boundary5 / bin_width_));
+    const int64_t pos25 = static_cast<int64_t>(static_cast<int>(boundary25 / bin_width_));
+    kern::deredden_zap(bspec_.data(), nb, m5_.data(), n5, m25_.data(), std::max<uint64_t>(1, n25), m125_.data(),
+                       std::max<uint64_t>(1, n125), pos5, pos25, d_zapmask, stream_, count, nb, ms);
+    kern::interbin_stats(bspec_.data(), nb, nullptr, partials_.data(), 1024, d_stats, stream_, count, nb);
+  }
   // inverse
   kern::fft4_c2r_pre(bspec_.data(), M, tmp4_.data(), stream_, count, nb, M);
   const float* t = reinterpret_cast<const float*>(tmp4_.data());
