@@ -217,14 +217,17 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   int neng = args.engines_per_gpu;
   if (const char* e = std::getenv("PSOUP_ENGINES")) neng = std::max(neng, std::atoi(e));
   if (neng <= 0) {
-    size_t mx = 0;
-    for (float dm : setup.dm_list) mx = std::max(mx, setup.accel_plan.generate(dm).size());
-    neng = mx < 128 ? 3 : 1;
+    // Each engine here pulls whole chunks (up to 32 DMs, whitened and searched
+    // as one flat trial list), which already fills the GPU: measured on the
+    // 2026-DM config 4, 1 engine 0.50 s vs 3 engines 0.54 s.  (The Python
+    // driver deals one chunk's DMs round-robin to 3 engines instead: 0.37 s.)
+    neng = 1;
   }
   res.performance["engines_per_gpu"] = neng;
 
-  t_search.start();
-  // phase 1: resident filterbank per device
+  // phase 1: resident filterbank per device (host-to-device upload + unpack,
+  // timed as part of "reading")
+  t_read.start();
   {
     std::vector<std::thread> lth;
     for (int dev = 0; dev < ngpu; ++dev)
@@ -250,6 +253,8 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     for (auto& t : lth) t.join();
     if (sh.error) std::rethrow_exception(sh.error);
   }
+  t_read.stop();
+  t_search.start();
   // phase 2: neng engines per device
   auto worker = [&](int dev, int slot) {
     try {

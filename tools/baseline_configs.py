@@ -157,6 +157,20 @@ def config45(a, npdmp, cfg):
             "--acc_end", "500", "-n", "3", "--npdmp", str(npdmp), "--limit", "1000"]
     ok, _, args = _C.parse_cmdline(argv)
     assert ok
+    if a.native:
+        # the native C++ pipeline (bin/peasoup, one host thread per GPU + engines)
+        import subprocess
+
+        trace = os.path.join(a.workdir, f"trace_cfg{cfg}.json")
+        t0 = time.perf_counter()
+        r = subprocess.run([os.path.join(REPO, "bin", "peasoup")] + argv[1:] + ["--trace_json", trace],
+                           capture_output=True, text=True)
+        wall = time.perf_counter() - t0
+        assert r.returncode == 0, r.stderr[-2000:]
+        tr = json.load(open(trace))
+        return {"config": cfg, "desc": "native bin/peasoup, same data and options", "log2n": a.log2n,
+                "wall_s": round(wall, 3), "timers_s": {k: round(v, 3) for k, v in tr.get("timers_s", {}).items()},
+                "performance": tr.get("performance", {})}
     t0 = time.perf_counter()
     res = run_search(args)
     wall = time.perf_counter() - t0
@@ -193,6 +207,7 @@ def main():
     ap.add_argument("--log2n", type=int, default=20)
     ap.add_argument("--workdir", default=os.path.join(REPO, "gpurun_out", "configs"))
     ap.add_argument("--out", default="")
+    ap.add_argument("--native", action="store_true", help="configs 4/5 through bin/peasoup instead of Python")
     a = ap.parse_args()
     os.makedirs(a.workdir, exist_ok=True)
     ctx = pdist.init()
