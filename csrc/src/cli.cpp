@@ -229,8 +229,8 @@ static std::vector<Spec> peasoup_specs(CmdLineOptions& a) {
       val_s("", "dedisp_kernel", "Dedispersion kernel: auto | mfma | valu | direct", a.dedisp_kernel),
       val_n("", "accel_batch", "Acceleration trials per batched FFT (0 = auto)", a.accel_batch),
       val_n("", "engines_per_gpu",
-            "Search engines per GPU, each on its own stream and host thread (0 = auto: Python driver 3 when DMs "
-            "have < 128 acceleration trials, else 1; native pipeline 1)",
+            "Search engines per GPU, each on its own stream and host thread, dealt every N-th DM of a chunk "
+            "(0 = auto: Python driver 3 when DMs have < 128 acceleration trials, else 1; native pipeline 1)",
             a.engines_per_gpu),
       val_n("", "sub_batch", "Fused-FFT trials per sub-batch on two alternating streams (0 = off, -1 = auto)",
             a.sub_batch),

@@ -161,6 +161,7 @@ struct Shared {
   std::vector<double> dedisp_s, search_s;
   std::vector<std::map<std::string, double>> dev_stats;
   std::exception_ptr error;
+  std::atomic<bool> abort{false};
   ProgressBar* progress = nullptr;
 };
 
@@ -217,10 +218,8 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   int neng = args.engines_per_gpu;
   if (const char* e = std::getenv("PSOUP_ENGINES")) neng = std::max(neng, std::atoi(e));
   if (neng <= 0) {
-    // Each engine here pulls whole chunks (up to 32 DMs, whitened and searched
-    // as one flat trial list), which already fills the GPU: measured on the
-    // 2026-DM config 4, 1 engine 0.50 s vs 3 engines 0.54 s.  (The Python
-    // driver deals one chunk's DMs round-robin to 3 engines instead: 0.37 s.)
+    // measured on the 2026-DM config 4 (13 trials per DM): 1 engine 0.52 s,
+    // 3 engines 0.56 s of search here (the Python driver gains from 3)
     neng = 1;
   }
   res.performance["engines_per_gpu"] = neng;
@@ -255,111 +254,188 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   }
   t_read.stop();
   t_search.start();
-  // phase 2: neng engines per device
+  // phase 2, per device: a feeder thread dedisperses DM chunks (one ahead,
+  // double-buffered, on its own stream) and publishes them; each of the
+  // device's neng engine threads searches every neng-th DM row of each chunk
+  // (whitened and searched as one flat trial list), so all engines work on the
+  // same chunk and the feeder reuses a buffer once every engine released it.
+  struct Pub {
+    int d0 = 0, d1 = 0;
+    bool resumed = false;
+    int pending = 0;
+    CandidateList cands;
+  };
+  struct DevSched {
+    std::mutex mu;
+    std::condition_variable cv;
+    Pub pub[2];
+    long published = 0;
+    bool done = false;
+    std::atomic<int> processed{0};
+    std::unique_ptr<Stream> dstream;
+    std::unique_ptr<DeviceBuffer<uint8_t>> trials[2];
+    Event ready[2] = {Event(true), Event(true)}, began[2] = {Event(true), Event(true)};
+    std::vector<std::unique_ptr<Event>> freed[2];
+    bool used[2] = {false, false};
+    double dd_ms = 0.0;
+  };
+  std::vector<std::unique_ptr<DevSched>> scheds;
+  const uint64_t rstride = Dedisperser::row_stride(geom.out_nsamps);
+  for (int d = 0; d < ngpu; ++d) {
+    PSOUP_HIP_CHECK(hipSetDevice(d));
+    auto sc = std::make_unique<DevSched>();
+    sc->dstream = std::make_unique<Stream>();
+    for (int k = 0; k < 2; ++k) {
+      sc->trials[k] = std::make_unique<DeviceBuffer<uint8_t>>(rstride * static_cast<uint64_t>(sh.chunk));
+      for (int e = 0; e < neng; ++e) sc->freed[k].push_back(std::make_unique<Event>());
+    }
+    scheds.push_back(std::move(sc));
+  }
+  auto fail = [&](int dev) {
+    {
+      std::lock_guard<std::mutex> lk(sh.mu);
+      if (!sh.error) sh.error = std::current_exception();
+      sh.next_dm.store(sh.ndm + 1000000);  // drain the queue
+    }
+    sh.abort.store(true);
+    for (auto& sc : scheds) {
+      std::lock_guard<std::mutex> lk(sc->mu);
+      sc->cv.notify_all();
+    }
+    (void)dev;
+  };
+  auto feeder = [&](int dev) {
+    DevSched& sc = *scheds[static_cast<size_t>(dev)];
+    try {
+      PSOUP_HIP_CHECK(hipSetDevice(dev));
+      DevState& ds = devs[static_cast<size_t>(dev)];
+      hipStream_t dst = sc.dstream->get();
+      int k = 0;
+      while (!sh.abort.load()) {
+        const int d0 = sh.next_dm.fetch_add(sh.chunk);
+        if (d0 >= sh.ndm) break;
+        const int d1 = std::min(sh.ndm, d0 + sh.chunk);
+        {
+          std::unique_lock<std::mutex> lk(sc.mu);
+          sc.cv.wait(lk, [&] { return sc.pub[k].pending == 0 || sh.abort.load(); });
+        }
+        if (sh.abort.load()) break;
+        Pub& p = sc.pub[k];
+        p.d0 = d0;
+        p.d1 = d1;
+        p.cands.clear();
+        const std::string ck = args.checkpoint_dir.empty() ? std::string() : chunk_file(args.checkpoint_dir, d0, d1);
+        p.resumed = !ck.empty() && load_chunk(ck, p.cands);
+        if (p.resumed) {
+          log_verbose("resumed DMs [" + std::to_string(d0) + "," + std::to_string(d1) + ") from checkpoint");
+        } else {
+          if (sc.used[k])
+            for (auto& ev : sc.freed[k]) PSOUP_HIP_CHECK(hipStreamWaitEvent(dst, ev->get(), 0));
+          sc.began[k].record(dst);
+          ds.dd->run(d0, d1, sc.trials[k]->data(), rstride, setup.dedisp_kernel, dst);
+          sc.ready[k].record(dst);
+          sc.used[k] = true;
+        }
+        {
+          std::lock_guard<std::mutex> lk(sc.mu);
+          p.pending = neng;
+          sc.published++;
+        }
+        sc.cv.notify_all();
+        k ^= 1;
+      }
+    } catch (...) {
+      fail(dev);
+    }
+    std::lock_guard<std::mutex> lk(sc.mu);
+    sc.done = true;
+    sc.cv.notify_all();
+  };
   auto worker = [&](int dev, int slot) {
+    DevSched& sc = *scheds[static_cast<size_t>(dev)];
     try {
       PSOUP_HIP_CHECK(hipSetDevice(dev));
       DevState& ds = devs[static_cast<size_t>(dev)];
       std::unique_ptr<Stream> own_stream;
-      std::unique_ptr<Dedisperser> own_dd;
-      if (slot > 0) {
-        own_stream = std::make_unique<Stream>();
-        own_dd = std::make_unique<Dedisperser>(*ds.dfb, own_stream->get());
-      }
+      if (slot > 0) own_stream = std::make_unique<Stream>();
       hipStream_t st = slot > 0 ? own_stream->get() : ds.stream->get();
-      Dedisperser* dd = slot > 0 ? own_dd.get() : ds.dd.get();
-      Stopwatch wd, ws;
+      Stopwatch ws;
       SearchEngine engine(setup.search, st);
-      const uint64_t rstride = Dedisperser::row_stride(geom.out_nsamps);
-      // Double-buffered: the next chunk is dedispersed on a side stream while
-      // this one is searched; the search stream waits on an event.
-      Stream dstream;
-      DeviceBuffer<uint8_t> trials[2] = {DeviceBuffer<uint8_t>(rstride * static_cast<uint64_t>(sh.chunk)),
-                                         DeviceBuffer<uint8_t>(rstride * static_cast<uint64_t>(sh.chunk))};
-      Event ready[2] = {Event(true), Event(true)}, began[2] = {Event(true), Event(true)}, freed[2];
-      bool pending[2] = {false, false}, used[2] = {false, false};
-      double dd_ms = 0.0;
-      auto ck_of = [&](int d0) {
-        const int d1 = std::min(sh.ndm, d0 + sh.chunk);
-        return args.checkpoint_dir.empty() ? std::string() : chunk_file(args.checkpoint_dir, d0, d1);
-      };
-      auto resumable = [&](const std::string& ck) {
-        if (ck.empty()) return false;
-        std::ifstream f(ck, std::ios::binary);
-        return static_cast<bool>(f);
-      };
-      auto issue = [&](int d0, int k) {
-        const int d1 = std::min(sh.ndm, d0 + sh.chunk);
-        if (used[k]) PSOUP_HIP_CHECK(hipStreamWaitEvent(dstream.get(), freed[k].get(), 0));
-        began[k].record(dstream.get());
-        dd->run(d0, d1, trials[k].data(), rstride, setup.dedisp_kernel, dstream.get());
-        ready[k].record(dstream.get());
-        pending[k] = true;
-      };
-      int processed = 0, k = 0;
-      int cur = sh.next_dm.fetch_add(sh.chunk);
-      if (cur < sh.ndm && !resumable(ck_of(cur))) issue(cur, k);
-      while (cur < sh.ndm) {
-        const int d0 = cur, d1 = std::min(sh.ndm, d0 + sh.chunk);
-        const std::string ck = ck_of(d0);
-        const int nxt = sh.next_dm.fetch_add(sh.chunk);
-        if (nxt < sh.ndm && !resumable(ck_of(nxt))) issue(nxt, k ^ 1);
+      for (long g = 0;; ++g) {
+        {
+          std::unique_lock<std::mutex> lk(sc.mu);
+          sc.cv.wait(lk, [&] { return sc.published > g || sc.done || sh.abort.load(); });
+          if (sh.abort.load() || sc.published <= g) break;
+        }
+        const int k = static_cast<int>(g & 1);
+        Pub& p = sc.pub[k];
         CandidateList local;
-        if (!pending[k] && load_chunk(ck, local)) {
-          log_verbose("resumed DMs [" + std::to_string(d0) + "," + std::to_string(d1) + ") from checkpoint");
-        } else {
-          if (!pending[k]) issue(d0, k);  // unreadable checkpoint: recompute
-          PSOUP_HIP_CHECK(hipStreamWaitEvent(st, ready[k].get(), 0));
+        if (!p.resumed) {
+          PSOUP_HIP_CHECK(hipStreamWaitEvent(st, sc.ready[k].get(), 0));
           ws.start();
-          // whiten the chunk's trials in batches of up to max_prepare, then search each
-          for (int p0 = d0; p0 < d1; p0 += engine.max_prepare()) {
-            const int cnt = std::min(engine.max_prepare(), d1 - p0);
-            if (args.fault_after_dms >= 0 && processed + cnt > args.fault_after_dms)
-              PSOUP_THROW("fault injection: device " << dev << " aborting after " << processed << " DM trials");
-            engine.prepare(trials[k].data() + static_cast<uint64_t>(p0 - d0) * rstride, rstride, geom.out_nsamps,
-                           cnt);
+          std::vector<int> rows;
+          for (int d = p.d0 + slot; d < p.d1; d += neng) rows.push_back(d);
+          for (size_t r0 = 0; r0 < rows.size(); r0 += static_cast<size_t>(engine.max_prepare())) {
+            const int cnt = static_cast<int>(std::min(rows.size() - r0, static_cast<size_t>(engine.max_prepare())));
+            const int before = sc.processed.fetch_add(cnt);
+            if (args.fault_after_dms >= 0 && before + cnt > args.fault_after_dms)
+              PSOUP_THROW("fault injection: device " << dev << " aborting after " << before << " DM trials");
+            engine.prepare(sc.trials[k]->data() + static_cast<uint64_t>(rows[r0] - p.d0) * rstride,
+                           static_cast<uint64_t>(neng) * rstride, geom.out_nsamps, cnt);
             std::vector<SearchEngine::Job> jobs;
-            for (int d = p0; d < p0 + cnt; ++d) {
+            for (int i = 0; i < cnt; ++i) {
+              const int d = rows[r0 + static_cast<size_t>(i)];
               const float dm = setup.dm_list[static_cast<size_t>(d)];
-              jobs.push_back(SearchEngine::Job{d - p0, dm, d, setup.accel_plan.generate(dm)});
+              jobs.push_back(SearchEngine::Job{i, dm, d, setup.accel_plan.generate(dm)});
               log_verbose("Searching " + std::to_string(jobs.back().accs.size()) + " acceleration trials for DM " +
                           std::to_string(dm));
               sh.accel_trials += jobs.back().accs.size();
             }
-            // one flat trial list over the chunk's DMs (batches span DM boundaries)
+            // one flat trial list over these DMs (batches span DM boundaries)
             std::vector<CandidateList> res = engine.search_prepared_many(jobs);
             for (auto& c : res)
               for (auto& x : c) local.push_back(std::move(x));
-            processed += cnt;
           }
           ws.stop();
-          freed[k].record(st);
-          used[k] = true;
-          pending[k] = false;
-          float ms = 0.f;
-          PSOUP_HIP_CHECK(hipEventElapsedTime(&ms, began[k].get(), ready[k].get()));
-          dd_ms += ms;
-          if (!ck.empty()) save_chunk(ck, local);
+          sc.freed[k][static_cast<size_t>(slot)]->record(st);
         }
+        bool last = false;
         {
-          std::lock_guard<std::mutex> lk(sh.mu);
-          for (auto& x : local) sh.cands.push_back(std::move(x));
+          // the last engine keeps pending at 1 until the chunk is handed over,
+          // so the feeder cannot refill this slot while p.cands is read
+          std::lock_guard<std::mutex> lk(sc.mu);
+          for (auto& x : local) p.cands.push_back(std::move(x));
+          last = p.pending == 1;
+          if (!last) --p.pending;
         }
-        int done = sh.done_dms.fetch_add(d1 - d0) + (d1 - d0);
-        if (sh.progress) sh.progress->set(static_cast<double>(done) / sh.ndm);
-        cur = nxt;
-        k ^= 1;
+        if (last) {
+          // every engine is done with this chunk: checkpoint and hand over
+          if (!p.resumed) {
+            float ms = 0.f;
+            PSOUP_HIP_CHECK(hipEventElapsedTime(&ms, sc.began[k].get(), sc.ready[k].get()));
+            sc.dd_ms += ms;
+            std::stable_sort(p.cands.begin(), p.cands.end(),
+                             [](const Candidate& a, const Candidate& b) { return a.dm_idx < b.dm_idx; });
+            if (!args.checkpoint_dir.empty()) save_chunk(chunk_file(args.checkpoint_dir, p.d0, p.d1), p.cands);
+          }
+          {
+            std::lock_guard<std::mutex> lk(sh.mu);
+            for (auto& x : p.cands) sh.cands.push_back(x);
+          }
+          const int done = sh.done_dms.fetch_add(p.d1 - p.d0) + (p.d1 - p.d0);
+          if (sh.progress) sh.progress->set(static_cast<double>(done) / sh.ndm);
+          std::lock_guard<std::mutex> lk(sc.mu);
+          p.cands.clear();
+          p.pending = 0;
+          sc.cv.notify_all();
+        }
       }
-      PSOUP_HIP_CHECK(hipStreamSynchronize(dstream.get()));
       PSOUP_HIP_CHECK(hipStreamSynchronize(st));
-      wd.add(dd_ms * 1e-3);  // GPU time of the (overlapped) dedispersion kernels
       const SearchCounters& c = engine.counters();
       std::lock_guard<std::mutex> lk(sh.mu);
-      sh.dedisp_s[static_cast<size_t>(dev)] += wd.get_time();
       sh.search_s[static_cast<size_t>(dev)] += ws.get_time();
       auto& st_map = sh.dev_stats[static_cast<size_t>(dev)];
-      st_map["dedispersion_s"] += wd.get_time();  // summed over the device's engines
-      st_map["search_s"] += ws.get_time();
+      st_map["search_s"] += ws.get_time();  // summed over the device's engines
       st_map["dm_trials"] += static_cast<double>(c.dm_trials);
       st_map["accel_trials"] += static_cast<double>(c.accel_trials);
       st_map["peaks"] += static_cast<double>(c.peaks);
@@ -370,15 +446,22 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
       st_map["accel_batch"] = engine.batch_size();
       st_map["sub_batch"] = engine.sub_batch();
     } catch (...) {
-      std::lock_guard<std::mutex> lk(sh.mu);
-      if (!sh.error) sh.error = std::current_exception();
-      sh.next_dm.store(sh.ndm + 1000000);  // drain the queue
+      fail(dev);
     }
   };
   std::vector<std::thread> threads;
-  for (int d = 0; d < ngpu; ++d)
+  for (int d = 0; d < ngpu; ++d) {
+    threads.emplace_back(feeder, d);
     for (int e = 0; e < neng; ++e) threads.emplace_back(worker, d, e);
+  }
   for (auto& t : threads) t.join();
+  for (int d = 0; d < ngpu; ++d) {
+    PSOUP_HIP_CHECK(hipSetDevice(d));
+    scheds[static_cast<size_t>(d)]->dstream->sync();
+    const double dd = scheds[static_cast<size_t>(d)]->dd_ms * 1e-3;  // GPU time of the (overlapped) kernels
+    sh.dedisp_s[static_cast<size_t>(d)] = dd;
+    sh.dev_stats[static_cast<size_t>(d)]["dedispersion_s"] = dd;
+  }
   t_search.stop();
   if (args.progress_bar) progress.stop();
   if (sh.error) std::rethrow_exception(sh.error);
