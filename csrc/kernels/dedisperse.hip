@@ -296,7 +296,7 @@ __global__ void __launch_bounds__(256) dedisperse_valu_kernel(
 // as two conflict-free ds_read_b128 and picks 5 words at the wave-uniform
 // word offset (uniform branch) before the same v_perm/add accumulation.
 // wmin[tile][ci]: the window start (relative to the sample) of tile and channel.
-constexpr int kLdsWinWords = 2048;  // 8 KiB per buffer
+constexpr int kLdsWinWords = 2048;  // largest staged window: 8 KiB (two 4 KiB passes)
 
 template <int Q>
 __device__ __forceinline__ void lds_accumulate(const uint32_t* w, uint32_t sh, uint32_t (&pk)[8]) {
@@ -309,12 +309,14 @@ __device__ __forceinline__ void lds_accumulate(const uint32_t* w, uint32_t sh, u
   }
 }
 
-template <bool XOR, int PASSES, bool UNALIGNED, int DPT>
+template <bool XOR, int PASSES, int DPT, int CPB>
 __global__ void __launch_bounds__(256) dedisperse_lds_kernel(
     const int8_t* __restrict__ x, uint64_t stride, const int32_t* __restrict__ active, int nactive,
     const int32_t* __restrict__ offT, int ldo, int d_base, int ndm, const int32_t* __restrict__ wmin,
-    uint64_t out_nsamps, uint8_t* __restrict__ out, uint64_t out_stride, float scale, int win_chunks) {
-  __shared__ __attribute__((aligned(16))) uint32_t win[2][kLdsWinWords];
+    uint64_t out_nsamps, uint8_t* __restrict__ out, uint64_t out_stride, float scale) {
+  // CPB channels' windows per LDS buffer (one barrier per CPB channels),
+  // double-buffered; each window is PASSES x 4 KiB
+  __shared__ __attribute__((aligned(16))) uint32_t win[2][CPB * PASSES * 1024];
   // workgroup = 4*DPT DMs (DPT = 8: one 32-DM tile; 4: half a tile, more
   // workgroups per CU to hide the channel-window loads)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -329,67 +331,66 @@ __global__ void __launch_bounds__(256) dedisperse_lds_kernel(
   for (int j = 0; j < DPT; ++j)
 #pragma unroll
     for (int q = 0; q < 8; ++q) pk[j][q] = 0;
-  u32x4 r[PASSES];
-  // every thread stages 16 bytes per pass (predicating the loads to the
-  // launch's largest window measured slower: 2.57 vs 2.2 ms per 32-DM chunk)
-  (void)win_chunks;
-  auto gload = [&](int ci) {
-    const int8_t* row = x + static_cast<uint64_t>(active[ci]) * stride + tb + wm[ci];
+  u32x4 r[CPB][PASSES];
+  // every thread stages 16 bytes per pass and channel (predicating the loads
+  // to the launch's largest window measured slower: 2.57 vs 2.2 ms per chunk)
+  auto gload = [&](int c0) {
 #pragma unroll
-    for (int p = 0; p < PASSES; ++p)
-      r[p] = *reinterpret_cast<const u32x4*>(row + 4096 * p + 16 * threadIdx.x);
+    for (int q = 0; q < CPB; ++q) {
+      const int ci = min(c0 + q, nactive - 1);  // past the end: a harmless reload
+      const int8_t* row = x + static_cast<uint64_t>(active[ci]) * stride + tb + wm[ci];
+#pragma unroll
+      for (int p = 0; p < PASSES; ++p)
+        r[q][p] = *reinterpret_cast<const u32x4*>(row + 4096 * p + 16 * threadIdx.x);
+    }
   };
   auto lstore = [&](int buf) {
 #pragma unroll
-    for (int p = 0; p < PASSES; ++p) {
-      if constexpr (XOR) r[p] ^= 0x80808080u;
-      *reinterpret_cast<u32x4*>(&win[buf][1024 * p + 4 * threadIdx.x]) = r[p];
-    }
+    for (int q = 0; q < CPB; ++q)
+#pragma unroll
+      for (int p = 0; p < PASSES; ++p) {
+        if constexpr (XOR) r[q][p] ^= 0x80808080u;
+        *reinterpret_cast<u32x4*>(&win[buf][(q * PASSES + p) * 1024 + 4 * threadIdx.x]) = r[q][p];
+      }
   };
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int ci = 0; ci < nactive; ++ci) {
-    const int buf = ci & 1;
-    if (ci + 1 < nactive) gload(ci + 1);  // in flight during this channel's sums
+  auto compute = [&](int ci, const uint32_t* wbase) {
     const int w0 = wm[ci];
     const int32_t* o = offT + static_cast<uint64_t>(ci) * ldo + d_base + dm0;
-    // all DPT windows' LDS reads first (latency overlapped), then the sums
+    // all DPT windows' LDS reads first (latency overlapped), then the sums:
+    // two 16-byte-aligned ds_read_b128 per DM, words picked at the
+    // wave-uniform offset (a dword-aligned b128 + b32 form measured slower)
     int rel[DPT];
     uint32_t w[DPT][8];
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
       rel[j] = o[j] - w0;  // >= 0, wave-uniform
-      if constexpr (UNALIGNED) {
-        // each lane's 20 bytes from the dword holding its first sample
-        // (dword-aligned ds_read_b128 + ds_read_b32); v_perm does the byte shift
-        const uint32_t* src = &win[buf][4 * lane + (rel[j] >> 2)];
-        const u32x4 a = *reinterpret_cast<const u32x4_a4*>(src);
-        w[j][0] = a[0]; w[j][1] = a[1]; w[j][2] = a[2]; w[j][3] = a[3];
-        w[j][4] = src[4];
-      } else {
-        const uint32_t* src = &win[buf][4 * lane + ((rel[j] >> 4) << 2)];
-        const u32x4 a = *reinterpret_cast<const u32x4*>(src);
-        const u32x4 b = *reinterpret_cast<const u32x4*>(src + 4);
-        w[j][0] = a[0]; w[j][1] = a[1]; w[j][2] = a[2]; w[j][3] = a[3];
-        w[j][4] = b[0]; w[j][5] = b[1]; w[j][6] = b[2]; w[j][7] = b[3];
-      }
+      const uint32_t* src = wbase + 4 * lane + ((rel[j] >> 4) << 2);
+      const u32x4 a = *reinterpret_cast<const u32x4*>(src);
+      const u32x4 b = *reinterpret_cast<const u32x4*>(src + 4);
+      w[j][0] = a[0]; w[j][1] = a[1]; w[j][2] = a[2]; w[j][3] = a[3];
+      w[j][4] = b[0]; w[j][5] = b[1]; w[j][6] = b[2]; w[j][7] = b[3];
     }
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
       const uint32_t sh = static_cast<uint32_t>(rel[j] & 3);
-      if constexpr (UNALIGNED) {
-        lds_accumulate<0>(w[j], sh, pk[j]);
-      } else {
-        switch ((rel[j] >> 2) & 3) {  // uniform
-          case 0: lds_accumulate<0>(w[j], sh, pk[j]); break;
-          case 1: lds_accumulate<1>(w[j], sh, pk[j]); break;
-          case 2: lds_accumulate<2>(w[j], sh, pk[j]); break;
-          default: lds_accumulate<3>(w[j], sh, pk[j]); break;
-        }
+      switch ((rel[j] >> 2) & 3) {  // uniform
+        case 0: lds_accumulate<0>(w[j], sh, pk[j]); break;
+        case 1: lds_accumulate<1>(w[j], sh, pk[j]); break;
+        case 2: lds_accumulate<2>(w[j], sh, pk[j]); break;
+        default: lds_accumulate<3>(w[j], sh, pk[j]); break;
       }
     }
-    if (ci + 1 < nactive) lstore(buf ^ 1);
+  };
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int c0 = 0, it = 0; c0 < nactive; c0 += CPB, ++it) {
+    const int buf = it & 1;
+    if (c0 + CPB < nactive) gload(c0 + CPB);  // in flight during these channels' sums
+#pragma unroll 1
+    for (int q = 0; q < CPB; ++q)
+      if (c0 + q < nactive) compute(c0 + q, &win[buf][q * PASSES * 1024]);
+    if (c0 + CPB < nactive) lstore(buf ^ 1);
     __syncthreads();
   }
   if (t >= out_nsamps) return;
@@ -557,40 +558,44 @@ void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_
   const uint64_t ty = (out_nsamps + 1023) / 1024;
   PSOUP_CHECK(ty <= 65535, "dedisperse_lds: series too long for the grid");
   static const int dpt = [] {
-    const char* e = std::getenv("PSOUP_DEDISP_LDS_DPT");  // A/B knob: DMs per wave, 8 or 4
-    return e && std::atoi(e) == 8 ? 8 : 4;  // 4: 141 ms vs 173 ms for the config-4 DM list
+    const char* e = std::getenv("PSOUP_DEDISP_LDS_DPT");  // A/B knob: DMs per wave, 8, 4 or 2
+    const int v = e ? std::atoi(e) : 4;  // 4: 141 ms vs 173 ms (8) for the config-4 DM list
+    return v == 8 || v == 2 ? v : 4;
   }();
   dim3 grid(static_cast<unsigned>((ndm + 4 * dpt - 1) / (4 * dpt)), static_cast<unsigned>(ty));
   PSOUP_CHECK(d_base + static_cast<int>(grid.x) * 4 * dpt <= ldo, "dedisperse_lds: offset table too narrow");
   const bool two = max_window > 4096;
   const bool xr = bias == 128;
-  // LDS read form: 1 = two 16-byte-aligned b128 + uniform word-select branch
-  // (default, 172 ms for the 2026-DM config-4 list), 2 = one dword-aligned
-  // (split) b128 + b32 per DM (214 ms)
-  static const int form = [] {
-    const char* e = std::getenv("PSOUP_DEDISP_LDS_FORM");
-    return e ? std::atoi(e) : 1;
+  // channels per barrier (A/B knob PSOUP_DEDISP_LDS_CPB = 1, 2 or 4; one-pass windows only)
+  static const int cpb = [] {
+    const char* e = std::getenv("PSOUP_DEDISP_LDS_CPB");
+    const int v = e ? std::atoi(e) : 1;  // 1: 140 ms, 2: 153 ms, 4: 185 ms (fewer workgroups per CU)
+    return v == 2 || v == 4 ? v : 1;
   }();
-#define PSOUP_LDS_LAUNCH(X, P, U)                                                                          \
-  if (dpt == 4)                                                                                               \
-    dedisperse_lds_kernel<X, P, U, 4><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive, d_offT, \
-                                                           ldo, d_base, ndm, d_wmin, out_nsamps, out, out_stride, \
-                                                           scale, (max_window + 15) / 16);                    \
-  else                                                                                                        \
-    dedisperse_lds_kernel<X, P, U, 8><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive, d_offT, \
-                                                           ldo, d_base, ndm, d_wmin, out_nsamps, out, out_stride, \
-                                                           scale, (max_window + 15) / 16)
-#define PSOUP_LDS_LAUNCH_U(X, P)   \
-  if (form == 1)                   \
-    PSOUP_LDS_LAUNCH(X, P, false); \
-  else                             \
-    PSOUP_LDS_LAUNCH(X, P, true)
-  if (xr) {
-    if (two) { PSOUP_LDS_LAUNCH_U(true, 2); } else { PSOUP_LDS_LAUNCH_U(true, 1); }
-  } else {
-    if (two) { PSOUP_LDS_LAUNCH_U(false, 2); } else { PSOUP_LDS_LAUNCH_U(false, 1); }
+#define PSOUP_LDS_LAUNCH(X, P, D, C)                                                                           \
+  dedisperse_lds_kernel<X, P, D, C><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive, d_offT, ldo, \
+                                                         d_base, ndm, d_wmin, out_nsamps, out, out_stride, scale)
+#define PSOUP_LDS_ONE(X)                                      \
+  if (two) {                                                  \
+    if (dpt == 8) PSOUP_LDS_LAUNCH(X, 2, 8, 1);               \
+    else PSOUP_LDS_LAUNCH(X, 2, 4, 1);                        \
+  } else if (dpt == 8) {                                      \
+    PSOUP_LDS_LAUNCH(X, 1, 8, 1);                             \
+  } else if (dpt == 2) {                                      \
+    PSOUP_LDS_LAUNCH(X, 1, 2, 1);                             \
+  } else if (cpb == 1) {                                      \
+    PSOUP_LDS_LAUNCH(X, 1, 4, 1);                             \
+  } else if (cpb == 2) {                                      \
+    PSOUP_LDS_LAUNCH(X, 1, 4, 2);                             \
+  } else {                                                    \
+    PSOUP_LDS_LAUNCH(X, 1, 4, 4);                             \
   }
-#undef PSOUP_LDS_LAUNCH_U
+  if (xr) {
+    PSOUP_LDS_ONE(true)
+  } else {
+    PSOUP_LDS_ONE(false)
+  }
+#undef PSOUP_LDS_ONE
 #undef PSOUP_LDS_LAUNCH
   post_launch_check("dedisperse_lds_kernel", s);
 }
