@@ -533,3 +533,32 @@ def test_batched_whitening_matches_single_trial(C):
         assert torch.equal(w1, w2), b
         assert sorted(map(key, single)) == sorted(map(key, batched)), b
         assert len(single) > 0
+
+
+def test_flat_multi_dm_batches_match_per_dm_search(C):
+    """search_prepared_many: the trials of several DMs concatenated and cut
+    into K-trial batches across DM boundaries (per-trial series index and
+    whitening stats) give each DM exactly the candidates of its own search."""
+    rng = np.random.default_rng(9)
+    n, nsamps, count = 1 << 18, (1 << 18) + 300, 5
+    rs = 1 << 19
+    t = np.arange(nsamps) * 64e-6
+    rows = np.zeros((count, rs), dtype=np.uint8)
+    for b in range(count):
+        x = rng.normal(128, 10, nsamps) + 25 * (((t / (0.0171 * (1 + 0.13 * b))) % 1.0) < 0.03)
+        rows[b, :nsamps] = np.clip(np.rint(x), 0, 255).astype(np.uint8)
+    d = torch.from_numpy(rows).to(dev)
+    p = C.SearchParams()
+    p.fft_size, p.tsamp, p.nharmonics, p.accel_batch = n, 64e-6, 3, 16
+    s = torch.cuda.current_stream().cuda_stream
+    e1, e2 = C.SearchEngine(p, s), C.SearchEngine(p, s)
+    acc_lists = [list(np.linspace(-40, 40, k)) for k in (3, 37, 1, 16, 10)]
+    e2.prepare(d.data_ptr(), rs, nsamps, count)
+    many = e2.search_prepared_many([(b, 5.0 + b, b, acc_lists[b]) for b in range(count)])
+    key = lambda c: (c.dm_idx, round(c.freq, 7), c.acc, c.nh, c.snr)  # noqa: E731
+    total = 0
+    for b in range(count):
+        single = e1.search_trial(d.data_ptr() + b * rs, nsamps, 5.0 + b, b, acc_lists[b])
+        assert sorted(map(key, single)) == sorted(map(key, many[b])), b
+        total += len(single)
+    assert total > 0
