@@ -209,6 +209,8 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     std::unique_ptr<Stream> stream;
     std::unique_ptr<DeviceFilterbank> dfb;
     std::unique_ptr<Dedisperser> dd;
+    std::vector<std::unique_ptr<Stream>> estreams;       // engines 1.. (engine 0 uses `stream`)
+    std::vector<std::unique_ptr<SearchEngine>> engines;  // built with the resident data, outside the search timer
   };
   std::vector<DevState> devs(static_cast<size_t>(ngpu));
 
@@ -240,6 +242,11 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
           ds.dfb = std::make_unique<DeviceFilterbank>(geom, ds.stream->get());
           ds.dfb->load_packed_host(fb.data());
           ds.dd = std::make_unique<Dedisperser>(*ds.dfb, ds.stream->get());
+          for (int e = 0; e < neng; ++e) {
+            if (e > 0) ds.estreams.push_back(std::make_unique<Stream>());
+            ds.engines.push_back(std::make_unique<SearchEngine>(
+                setup.search, e > 0 ? ds.estreams.back()->get() : ds.stream->get()));
+          }
           PSOUP_HIP_CHECK(hipStreamSynchronize(ds.stream->get()));
           wl.stop();
           std::lock_guard<std::mutex> lk(sh.mu);
@@ -356,11 +363,9 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     try {
       PSOUP_HIP_CHECK(hipSetDevice(dev));
       DevState& ds = devs[static_cast<size_t>(dev)];
-      std::unique_ptr<Stream> own_stream;
-      if (slot > 0) own_stream = std::make_unique<Stream>();
-      hipStream_t st = slot > 0 ? own_stream->get() : ds.stream->get();
+      SearchEngine& engine = *ds.engines[static_cast<size_t>(slot)];
+      hipStream_t st = engine.stream();
       Stopwatch ws;
-      SearchEngine engine(setup.search, st);
       for (long g = 0;; ++g) {
         {
           std::unique_lock<std::mutex> lk(sc.mu);
