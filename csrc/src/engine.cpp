@@ -511,9 +511,16 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     if (K_ >= 32) K_ = K_ / 16 * 16;  // halves stay multiples of 8 (XCD-grouped kernels)
     else if (K_ >= 16) K_ = K_ / 8 * 8;
   }
-  // Auto: two half-batches on alternating streams (+4-5% at 2^23: the
-  // tail of one sub-batch's kernels overlaps the head of the other's).
-  sub_ = mode_ != 2 ? 0 : p_.sub_batch >= 0 ? p_.sub_batch : (K_ >= 16 ? K_ / 2 : 0);
+  // Auto: sub-batches on alternating streams (+4-5% at 2^23: the tail of
+  // one sub-batch's kernels overlaps the head of the other's), half a batch
+  // but at most 2^28 samples (32 trials of 2^23: at K = 256, sub-batches of
+  // 16/32/64/128 measured 20.81k/20.84k/20.71k/20.47k trials/s same-box).
+  int sub_auto = 0;
+  if (K_ >= 16) {
+    const int cap = static_cast<int>(std::max<uint64_t>(8, (uint64_t(1) << 28) / n_)) / 8 * 8;
+    sub_auto = std::min(K_ / 2, cap);
+  }
+  sub_ = mode_ != 2 ? 0 : p_.sub_batch >= 0 ? p_.sub_batch : sub_auto;
   if (sub_ >= K_) sub_ = 0;
   cap_ = static_cast<uint32_t>(std::max<uint64_t>(1u << 16, static_cast<uint64_t>(K_) * 4096));
   for (auto& s : slots_) {
