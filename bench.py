@@ -48,12 +48,13 @@ def parse():
                    help="DM trials per GPU per step (dedispersed as one chunk, as the pipeline does)")
     p.add_argument("--acc", type=float, default=500.0, help="search +-acc m/s^2")
     p.add_argument("--nharmonics", type=int, default=3)
-    p.add_argument("--accel-batch", type=int, default=0)
+    p.add_argument("--accel-batch", type=int, default=0,
+                   help="acceleration trials per batch (0 = auto: 256 at 2^23 within a 24 GiB budget)")
     p.add_argument("--sub-batch", type=int, default=-1,
-                   help="trials per sub-batch on two alternating streams (0 = off, -1 = auto: half a batch)")
+                   help="trials per sub-batch on two alternating streams (0 = off, -1 = auto: half a batch, at most 2^28 samples)")
     p.add_argument("--fft-mode", type=int, default=2,
                    help="2: fused resample + four-step FFT; 1: rocFFT C2C(N/2) + fused r2c post; 0: rocFFT R2C")
-    p.add_argument("--dedisp-kernel", default="mfma", choices=["mfma", "direct"])
+    p.add_argument("--dedisp-kernel", default="auto", choices=["auto", "mfma", "valu", "direct"])
     p.add_argument("--fft4-flags", type=int, default=-1, help="fused-FFT kernel variant flags (tuning; -1 = default)")
     p.add_argument("--seed", type=int, default=1234)
     return p.parse_args()
@@ -160,7 +161,7 @@ def main() -> int:
             "config": {
                 "model": f"peasoup accel search: 2^{a.log2n}-pt series, +-{a.acc:g} m/s^2 (legacy plan), "
                          f"{1 << a.nharmonics}-harmonic sum, {a.nchans}-ch {a.nbits}-bit filterbank, "
-                         f"auto dedispersion kernel",
+                         f"{a.dedisp_kernel} dedispersion kernel",
                 "global_batch": trials_per_step,
                 "seq_len": n,
                 "parallelism": f"dm{ctx.world_size}",
