@@ -785,8 +785,25 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
   RoctxRange acc_range("Acceleration-Loop");
   std::deque<int> inflight;  // slot indices
   int next = 0, slot = 0;
+  // Short trial lists (one DM at 2^23: 685 trials) keep at least
+  // PSOUP_MIN_BATCHES (default 8) batches in the two-slot pipeline so host
+  // clustering still overlaps the GPU, but never fall below the batch the
+  // 6 GiB budget gives (K_small: 64 at 2^23, 256 at 2^20).
+  int kc = K_;
+  {
+    static const int min_batches = [] {
+      const char* e = std::getenv("PSOUP_MIN_BATCHES");
+      return e ? std::max(1, std::atoi(e)) : 8;
+    }();
+    if (p_.accel_batch <= 0 && ntr < min_batches * K_) {
+      const uint64_t per = n_ * 4 + nb_ * 8 + static_cast<uint64_t>(hi_) * 4;
+      const int k_small = static_cast<int>(std::max<uint64_t>(16, std::min<uint64_t>(256, (6ull << 30) / per)));
+      const int even = (ntr + min_batches - 1) / min_batches;
+      kc = std::min(K_, std::max(k_small, (even + 7) / 8 * 8));
+    }
+  }
   auto issue = [&](int sl) {
-    const int c = std::min(K_, ntr - next);
+    const int c = std::min(kc, ntr - next);
     launch_batch(slots_[sl], next, c);
     inflight.push_back(sl);
     next += c;
