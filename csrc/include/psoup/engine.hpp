@@ -121,6 +121,13 @@ struct SearchParams {
   int sub_batch = -1;           // fused-FFT trials per sub-batch on alternating streams (0 = off, -1 = auto)
   int host_threads = -1;        // host workers clustering/distilling peak-heavy batches (-1 = auto, 0/1 = serial)
   size_t batch_bytes = 24ull << 30;  // auto-batch HBM budget (256 trials of 2^23; same-box A/B vs 64: +1.8%)
+  // Engines sharing the device: the auto budget is also capped at 70% of the
+  // device's free memory divided by this count.
+  int engines_per_device = 1;
+  // Auto batching of short trial lists: lists shorter than min_batches full
+  // batches are cut into min_batches even batches (multiples of 8), but never
+  // below the batch a quarter of the budget gives.
+  int min_batches = 8;
   int min_gap = 30;
   // Acceleration-trial FFT path: 0 = rocFFT R2C of N points; 1 = rocFFT C2C
   // of N/2 points with the real-FFT post-processing fused into the interbin
@@ -221,6 +228,7 @@ class SearchEngine {
   const SearchCounters& counters() const { return ctr_; }
   void reset_counters() { ctr_ = SearchCounters(); }
   int batch_size() const { return K_; }
+  int last_batch() const { return last_kc_; }  // batch size of the last search_prepared_many call
   int sub_batch() const { return sub_; }
   int fft_mode() const { return mode_; }
   hipStream_t stream() const { return stream_; }
@@ -239,7 +247,7 @@ class SearchEngine {
     std::unique_ptr<Event> done, copied;
     int first = 0, count = 0;
   };
-  void ensure_batch_buffers();
+  void ensure_batch_buffers(int k);
   FftPlan& batch_plan(int count);
   void launch_batch(Slot& s, int first, int count);
   void grow_capacity(uint32_t need);
@@ -263,6 +271,9 @@ class SearchEngine {
   float bin_width_, tobs_;
   int nlev_;
   int K_;
+  int k_small_ = 1;     // auto short-list batch floor
+  int last_kc_ = 0;
+  int buf_k_ = 0;       // trials the batch buffers hold
   uint32_t cap_;
   kern::HarmParams hp_{};
   std::vector<PeakBounds> bounds_;

@@ -9,6 +9,7 @@
 #include <cstring>
 
 #include "psoup/candidates.hpp"
+#include "psoup/checkpoint.hpp"
 #include "psoup/cli.hpp"
 #include "psoup/common.hpp"
 #include "psoup/engine.hpp"
@@ -669,6 +670,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("accel_batch", &SearchParams::accel_batch)
       .def_readwrite("sub_batch", &SearchParams::sub_batch)
       .def_readwrite("batch_bytes", &SearchParams::batch_bytes)
+      .def_readwrite("engines_per_device", &SearchParams::engines_per_device)
+      .def_readwrite("min_batches", &SearchParams::min_batches)
       .def_readwrite("min_gap", &SearchParams::min_gap)
       .def_readwrite("fft_mode", &SearchParams::fft_mode);
   py::class_<SearchEngine>(m, "SearchEngine")
@@ -693,6 +696,7 @@ PYBIND11_MODULE(_C, m) {
          "jobs: [(prepared index, dm, dm_idx, accs)] -> one candidate list per job")
       .def_property_readonly("max_prepare", &SearchEngine::max_prepare)
       .def_property_readonly("batch_size", &SearchEngine::batch_size)
+      .def_property_readonly("last_batch", &SearchEngine::last_batch)
       .def_property_readonly("sub_batch", &SearchEngine::sub_batch)
       .def_property_readonly("fft_mode", &SearchEngine::fft_mode)
       .def_property_readonly("stream", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.stream()); })
@@ -777,6 +781,23 @@ PYBIND11_MODULE(_C, m) {
     SearchSetup s = make_search_setup(args, dict_to_header(hdr));
     return global_distill_and_score(std::move(c), args, s);
   });
+  // ----------------------------------------------------- checkpoint/resume --
+  m.def("checkpoint_identity", [](const CmdLineOptions& args, const py::dict& hdr) {
+    RunIdentity id = make_run_identity(args, dict_to_header(hdr));
+    return py::make_tuple(id.key, id.text);
+  });
+  m.def("prepare_checkpoint_dir", [](const std::string& dir, const CmdLineOptions& args, const py::dict& hdr) {
+    RunIdentity id = make_run_identity(args, dict_to_header(hdr));
+    prepare_checkpoint_dir(dir, id);
+    return id.key;
+  });
+  m.def("spill_path", &spill_path);
+  m.def("load_spill", [](const std::string& path, uint64_t key) {
+    CandidateList c;
+    SpillStatus st = load_spill(path, key, c);
+    return py::make_tuple(std::string(spill_status_name(st)), c);
+  });
+  m.def("save_spill", &save_spill, py::arg("path"), py::arg("key"), py::arg("cands"));
   m.def("search_params_from_args", [](const CmdLineOptions& args, const py::dict& hdr) {
     SearchSetup s = make_search_setup(args, dict_to_header(hdr));
     return py::make_tuple(s.search, s.dm_list, s.killmask, s.fft_size, s.cfreq);

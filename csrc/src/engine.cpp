@@ -502,14 +502,21 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     }
   }
   // batch size
-  if (p_.accel_batch > 0) {
-    K_ = p_.accel_batch;
-  } else {
-    const size_t per = n_ * 4 + nb_ * 8 + static_cast<size_t>(hi_) * 4;
-    K_ = static_cast<int>(std::max<size_t>(1, p_.batch_bytes / per));
-    K_ = std::min(K_, 256);
-    if (K_ >= 32) K_ = K_ / 16 * 16;  // halves stay multiples of 8 (XCD-grouped kernels)
-    else if (K_ >= 16) K_ = K_ / 8 * 8;
+  {
+    // auto budget: capped by the device's free memory shared among its engines
+    size_t budget = p_.batch_bytes;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
+      budget = std::min(budget, free_b / 10 * 7 / static_cast<size_t>(std::max(1, p_.engines_per_device)));
+    const size_t per = n_ * 4 + nb_ * 8 + static_cast<size_t>(hi_) * 4;  // Y/res + X/spec + P per trial
+    auto round_batch = [](size_t k) {
+      int K = static_cast<int>(std::min<size_t>(256, std::max<size_t>(1, k)));
+      if (K >= 32) K = K / 16 * 16;  // halves stay multiples of 8 (XCD-grouped kernels)
+      else if (K >= 16) K = K / 8 * 8;
+      return K;
+    };
+    K_ = p_.accel_batch > 0 ? p_.accel_batch : round_batch(budget / per);
+    k_small_ = std::min(K_, std::max(16, round_batch(budget / 4 / per)));
   }
   // Auto: sub-batches on alternating streams (+4-5% at 2^23: the tail of
   // one sub-batch's kernels overlaps the head of the other's), half a batch
@@ -549,12 +556,15 @@ void SearchEngine::grow_capacity(uint32_t need) {
   hp_.capacity = cap_;
 }
 
-void SearchEngine::ensure_batch_buffers() {
+void SearchEngine::ensure_batch_buffers(int k) {
+  // sized for the largest batch actually launched (a short trial list never
+  // allocates a whole K_-trial batch)
+  if (k <= buf_k_) return;
+  buf_k_ = k;
   const uint64_t rs = mode_ == 2 ? 2 * f4_.ystride : n_;  // floats per trial
-  if (res_.size() >= static_cast<uint64_t>(K_) * rs) return;
-  res_.resize(static_cast<uint64_t>(K_) * rs);
-  spec_.resize(static_cast<uint64_t>(K_) * xs_);
-  P_.resize(static_cast<uint64_t>(K_) * std::max<uint64_t>(1, static_cast<uint64_t>(hi_)));
+  res_.resize(static_cast<uint64_t>(k) * rs);
+  spec_.resize(static_cast<uint64_t>(k) * xs_);
+  P_.resize(static_cast<uint64_t>(k) * std::max<uint64_t>(1, static_cast<uint64_t>(hi_)));
 }
 
 FftPlan& SearchEngine::batch_plan(int count) {
@@ -781,27 +791,28 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
                                  hipMemcpyHostToDevice, stream_));
   PSOUP_HIP_CHECK(hipMemcpyAsync(d_src_.data(), flat_src_.data(), flat_src_.size() * sizeof(uint32_t),
                                  hipMemcpyHostToDevice, stream_));
-  ensure_batch_buffers();
   RoctxRange acc_range("Acceleration-Loop");
   std::deque<int> inflight;  // slot indices
   int next = 0, slot = 0;
-  // Short trial lists (one DM at 2^23: 685 trials) keep at least
-  // PSOUP_MIN_BATCHES (default 8) batches in the two-slot pipeline so host
-  // clustering still overlaps the GPU, but never fall below the batch the
-  // 6 GiB budget gives (K_small: 64 at 2^23, 256 at 2^20).
+  // Short trial lists (one DM at 2^23: 685 trials) keep at least min_batches
+  // (default 8, env PSOUP_MIN_BATCHES) batches in the two-slot pipeline so
+  // host clustering still overlaps the GPU, but never fall below k_small_
+  // (the batch a quarter of the budget gives: 64 at 2^23 with the default
+  // 24 GiB, rounded like K_).
   int kc = K_;
   {
-    static const int min_batches = [] {
+    static const int env_min_batches = [] {
       const char* e = std::getenv("PSOUP_MIN_BATCHES");
-      return e ? std::max(1, std::atoi(e)) : 8;
+      return e ? std::max(1, std::atoi(e)) : 0;
     }();
+    const int min_batches = env_min_batches > 0 ? env_min_batches : std::max(1, p_.min_batches);
     if (p_.accel_batch <= 0 && ntr < min_batches * K_) {
-      const uint64_t per = n_ * 4 + nb_ * 8 + static_cast<uint64_t>(hi_) * 4;
-      const int k_small = static_cast<int>(std::max<uint64_t>(16, std::min<uint64_t>(256, (6ull << 30) / per)));
       const int even = (ntr + min_batches - 1) / min_batches;
-      kc = std::min(K_, std::max(k_small, (even + 7) / 8 * 8));
+      kc = std::min(K_, std::max(k_small_, (even + 7) / 8 * 8));
     }
   }
+  last_kc_ = kc;
+  ensure_batch_buffers(std::min(kc, ntr));
   auto issue = [&](int sl) {
     const int c = std::min(kc, ntr - next);
     launch_batch(slots_[sl], next, c);

@@ -15,6 +15,7 @@
 #include <sstream>
 #include <thread>
 
+#include "psoup/checkpoint.hpp"
 #include "psoup/output.hpp"
 
 namespace psoup {
@@ -118,35 +119,6 @@ void ProgressBar::stop() {
 // ---------------------------------------------------------------- pipeline --
 namespace {
 
-std::string chunk_file(const std::string& dir, int d0, int d1) {
-  std::ostringstream os;
-  os << dir << "/dm_" << d0 << "_" << d1 << ".psoc";
-  return os.str();
-}
-
-bool load_chunk(const std::string& path, CandidateList& out) {
-  std::ifstream in(path, std::ios::binary);
-  if (!in) return false;
-  std::vector<uint8_t> buf((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
-  try {
-    CandidateList c = deserialize_candidates(buf.data(), buf.size());
-    for (auto& x : c) out.push_back(std::move(x));
-    return true;
-  } catch (const std::exception&) {
-    return false;
-  }
-}
-
-void save_chunk(const std::string& path, const CandidateList& c) {
-  std::vector<uint8_t> buf = serialize_candidates(c);
-  std::string tmp = path + ".tmp";
-  {
-    std::ofstream out(tmp, std::ios::binary);
-    out.write(reinterpret_cast<const char*>(buf.data()), static_cast<std::streamsize>(buf.size()));
-  }
-  std::rename(tmp.c_str(), path.c_str());
-}
-
 struct Shared {
   const CmdLineOptions* args;
   const SearchSetup* setup;
@@ -187,7 +159,11 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
               std::to_string(setup.fft_size));
 
   DedispGeometry geom = DedispGeometry::make(fb.header(), fb.nsamps(), setup.dm_list, setup.killmask);
-  if (!args.checkpoint_dir.empty()) make_dirs(args.checkpoint_dir);
+  RunIdentity ckid;
+  if (!args.checkpoint_dir.empty()) {
+    ckid = make_run_identity(args, fb.header());
+    prepare_checkpoint_dir(args.checkpoint_dir, ckid);
+  }
 
   Shared sh;
   sh.args = &args;
@@ -225,6 +201,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     neng = 1;
   }
   res.performance["engines_per_gpu"] = neng;
+  setup.search.engines_per_device = neng;  // the auto batch budget is shared among them
 
   // phase 1: resident filterbank per device (host-to-device upload + unpack,
   // timed as part of "reading")
@@ -331,11 +308,16 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
         p.d0 = d0;
         p.d1 = d1;
         p.cands.clear();
-        const std::string ck = args.checkpoint_dir.empty() ? std::string() : chunk_file(args.checkpoint_dir, d0, d1);
-        p.resumed = !ck.empty() && load_chunk(ck, p.cands);
+        const std::string ck = args.checkpoint_dir.empty() ? std::string() : spill_path(args.checkpoint_dir, d0, d1);
+        const SpillStatus st = ck.empty() ? SpillStatus::Missing : load_spill(ck, ckid.key, p.cands);
+        p.resumed = st == SpillStatus::Loaded;
         if (p.resumed) {
           log_verbose("resumed DMs [" + std::to_string(d0) + "," + std::to_string(d1) + ") from checkpoint");
         } else {
+          if (st != SpillStatus::Missing)
+            log_info("checkpoint spill " + ck + " is " + spill_status_name(st) + "; recomputing DMs [" +
+                     std::to_string(d0) + "," + std::to_string(d1) + ")");
+          p.cands.clear();
           if (sc.used[k])
             for (auto& ev : sc.freed[k]) PSOUP_HIP_CHECK(hipStreamWaitEvent(dst, ev->get(), 0));
           sc.began[k].record(dst);
@@ -421,7 +403,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
             sc.dd_ms += ms;
             std::stable_sort(p.cands.begin(), p.cands.end(),
                              [](const Candidate& a, const Candidate& b) { return a.dm_idx < b.dm_idx; });
-            if (!args.checkpoint_dir.empty()) save_chunk(chunk_file(args.checkpoint_dir, p.d0, p.d1), p.cands);
+            if (!args.checkpoint_dir.empty()) save_spill(spill_path(args.checkpoint_dir, p.d0, p.d1), ckid.key, p.cands);
           }
           {
             std::lock_guard<std::mutex> lk(sh.mu);

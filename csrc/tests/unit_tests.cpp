@@ -5,6 +5,8 @@
 // ASan is not available on the MI355X pool.
 //
 // usage: psoup_unit_tests [repo_root]   (repo_root locates the tutorial .fil)
+#include <unistd.h>
+
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -17,6 +19,7 @@
 #include <vector>
 
 #include "psoup/candidates.hpp"
+#include "psoup/checkpoint.hpp"
 #include "psoup/cli.hpp"
 #include "psoup/common.hpp"
 #include "psoup/output.hpp"
@@ -214,6 +217,45 @@ void t_host_pool() {
 
 }  // namespace
 
+// Checkpoint spills: keyed, integrity-checked, atomic; concurrent writers of
+// different chunks (the native pipeline's engines) leave only whole files.
+void t_checkpoint_spills() {
+  char tmpl[] = "/tmp/psoup_ck_XXXXXX";
+  char* dir = ::mkdtemp(tmpl);
+  CHECK(dir != nullptr);
+  const std::string d = dir;
+  CmdLineOptions a;
+  a.infilename = g_root + "/tests/data/tutorial.fil";
+  SigprocHeader h = read_header_file(a.infilename);
+  const RunIdentity id = make_run_identity(a, h);
+  prepare_checkpoint_dir(d, id);
+  CandidateList c = synth_cands();
+  std::vector<std::thread> th;
+  for (int i = 0; i < 4; ++i) th.emplace_back([&, i] { save_spill(spill_path(d, 8 * i, 8 * i + 8), id.key, c); });
+  for (auto& t : th) t.join();
+  for (int i = 0; i < 4; ++i) {
+    CandidateList back;
+    CHECK(load_spill(spill_path(d, 8 * i, 8 * i + 8), id.key, back) == SpillStatus::Loaded);
+    CHECK(back.size() == c.size() && back[3].freq == c[3].freq);
+    CandidateList none;
+    CHECK(load_spill(spill_path(d, 8 * i, 8 * i + 8), id.key + 1, none) == SpillStatus::Mismatch && none.empty());
+  }
+  CandidateList none;
+  CHECK(load_spill(spill_path(d, 99, 100), id.key, none) == SpillStatus::Missing);
+  a.nharmonics = 3;
+  CHECK(make_run_identity(a, h).key != id.key);
+  bool threw = false;
+  try {
+    save_spill(d + "/missing_subdir/x.psoc", id.key, c);
+  } catch (const std::exception&) {
+    threw = true;
+  }
+  CHECK(threw);
+  for (int i = 0; i < 4; ++i) std::remove(spill_path(d, 8 * i, 8 * i + 8).c_str());
+  std::remove((d + "/manifest.txt").c_str());
+  ::rmdir(d.c_str());
+}
+
 int main(int argc, char** argv) {
   if (argc > 1) g_root = argv[1];
   std::vector<Case> cases = {
@@ -228,6 +270,7 @@ int main(int argc, char** argv) {
       {"peaks_and_bounds", t_peaks_and_bounds},
       {"threads_shared_readonly", t_threads_shared_readonly},
       {"host_pool", t_host_pool},
+      {"checkpoint_spills", t_checkpoint_spills},
   };
   for (auto& c : cases) {
     const int before = g_fail;

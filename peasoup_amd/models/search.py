@@ -108,14 +108,16 @@ class RankSearcher:
         if packed is not None:
             self.load_packed(packed)
         self.dedisperser = _C.Dedisperser(self.dfb, self.stream)
-        self.engine = _C.SearchEngine(self.params, self.stream)
         self.kernel = {"auto": _C.DedispKernel.Auto, "mfma": _C.DedispKernel.Mfma, "valu": _C.DedispKernel.Valu,
                        "direct": _C.DedispKernel.Direct}[args.dedisp_kernel]
         self.row_stride = _C.Dedisperser.row_stride(self.geom.out_nsamps)
         self.accel_plan = _C.accel_plan_from_args(args, self.header)
         max_trials = max((len(self.accel_list(d)) for d in self.dm_list), default=0)
+        neng = engines_per_gpu(args, max_trials)
+        self.params.engines_per_device = neng  # the auto batch budget is shared among them
+        self.engine = _C.SearchEngine(self.params, self.stream)
         self.engines = [self.engine] + [_C.SearchEngine(self.params, _engine_stream(self.ctx.device, i))
-                                        for i in range(1, engines_per_gpu(args, max_trials))]
+                                        for i in range(1, neng)]
         self._pool = None
         self._trials: Optional[torch.Tensor] = None
 
@@ -173,8 +175,20 @@ class RankSearcher:
         ckdir = getattr(self.args, "checkpoint_dir", "") or ""
         fault_after = int(getattr(self.args, "fault_after_dms", -1))
         processed = 0
-        ck_of = [os.path.join(ckdir, f"dm_{d0}_{d1}.psoc") if ckdir else "" for d0, d1 in blocks]
-        todo = [i for i, ck in enumerate(ck_of) if not (ck and os.path.exists(ck))]
+        ck_of = [_C.spill_path(ckdir, d0, d1) if ckdir else "" for d0, d1 in blocks]
+        resumed: Dict[int, list] = {}
+        ckey = 0
+        if ckdir:
+            # spills are bound to this run's identity (input, header, options):
+            # a spill of another run, or a corrupt/truncated one, is recomputed
+            ckey = _C.prepare_checkpoint_dir(ckdir, self.args, self.header)
+            for i, ck in enumerate(ck_of):
+                status, got = _C.load_spill(ck, ckey)
+                if status == "loaded":
+                    resumed[i] = got
+                elif status != "missing":
+                    warnings.warn(f"checkpoint spill {ck} is {status}; recomputing DMs {blocks[i]}")
+        todo = [i for i in range(len(blocks)) if i not in resumed]
         dev = self.ctx.device
         side = _C.GpuStream()
         nbuf = min(2, len(todo))
@@ -207,9 +221,8 @@ class RankSearcher:
             d0, d1 = blocks[i]
             ck = ck_of[i]
             if i not in issued:
-                # resume: same spill format as the native pipeline (CandidatePOD trees)
-                with open(ck, "rb") as f:
-                    cands.extend(_C.deserialize_candidates(f.read()))
+                # resume: same spill format as the native pipeline (keyed CandidatePOD trees)
+                cands.extend(resumed.pop(i))
                 ntrials += sum(len(self.accel_list(self.dm_list[d])) for d in range(d0, d1))
                 if progress is not None:
                     progress(d1 - d0)
@@ -265,11 +278,7 @@ class RankSearcher:
                 evs.append(ev)
             freed[k] = evs
             if ck:
-                os.makedirs(ckdir, exist_ok=True)
-                tmp = ck + f".tmp{self.ctx.rank}"
-                with open(tmp, "wb") as f:
-                    f.write(_C.serialize_candidates(chunk_cands))
-                os.replace(tmp, ck)
+                _C.save_spill(ck, ckey, chunk_cands)  # atomic; raises on a failed write
             cands.extend(chunk_cands)
         side.synchronize()
         for e in self.engines:

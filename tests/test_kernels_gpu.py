@@ -474,6 +474,37 @@ def test_results_independent_of_accel_batching(C, batch, sub):
     assert abs(best[0] - a_true) <= 30.0, best
 
 
+def test_auto_short_list_balancing_matches_fixed_batch(C):
+    """the auto path that cuts a short trial list into min_batches
+    even batches (kc < K) gives the same candidates as fixed batches, and its
+    buffers only hold the batch actually used."""
+    rng = np.random.default_rng(34)
+    nsamps, n, tsamp = 1100000, 1 << 20, 64e-6
+    t = np.arange(nsamps) * tsamp
+    ph = ((t - 250.0 * t * t / (2 * 299792458.0)) / 0.003) % 1.0
+    trial = np.clip(rng.normal(128, 6, nsamps) + 2.0 * (np.minimum(ph, 1 - ph) < 0.04), 0, 255).astype(np.uint8)
+    tt = torch.from_numpy(trial).to(dev)
+    accs = [float(a) for a in np.linspace(-500, 500, 101)]
+    s = torch.cuda.current_stream().cuda_stream
+    runs = []
+    for auto in (False, True):
+        p = C.SearchParams()
+        p.fft_size, p.tsamp, p.nharmonics, p.min_snr = n, tsamp, 3, 6.0
+        if auto:
+            # budget of exactly 64 trials (Y + X + P bytes per trial; the search range covers all bins)
+            p.accel_batch, p.batch_bytes = 0, 64 * (n * 4 + (n // 2 + 1) * 8 + (n // 2 + 1) * 4)
+        else:
+            p.accel_batch, p.sub_batch = 24, 0
+        eng = C.SearchEngine(p, s)
+        cands = eng.search_trial(tt.data_ptr(), nsamps, 1.0, 0, accs)
+        torch.cuda.synchronize()
+        if auto:
+            assert eng.batch_size == 64
+            assert eng.last_batch == 16  # 101 trials < 8 x 64: 8 even batches, floored at k_small = 16
+        runs.append(sorted((c.acc, c.nh, c.snr, c.freq) for c in cands))
+    assert runs[0] == runs[1] and len(runs[0]) > 0
+
+
 @pytest.mark.parametrize("log2n", [17, 20, 23])
 def test_whitener_real_ffts_on_fft4_match_numpy(C, log2n):
     """Whitener R2C/C2R on the four-step passes (K = 1) vs NumPy fp64 and the

@@ -179,6 +179,30 @@ def test_python_entry_fault_then_resume(tmp_path):
     assert (tmp_path / "b" / "candidates.peasoup").read_bytes() == (tmp_path / "c" / "candidates.peasoup").read_bytes()
 
 
+def test_python_resume_with_changed_options_recomputes(C, tmp_path):
+    """The Python driver ignores spills of a different run (here: another
+    --min_snr) and recomputes, matching a clean run."""
+    from conftest import TUTORIAL
+    from peasoup_amd.models.search import run_search
+
+    ck = str(tmp_path / "ck")
+
+    def search(out, *extra):
+        ok, _, args = C.parse_cmdline(["peasoup", "-i", TUTORIAL, "--dm_end", "80", "-n", "3", "-o",
+                                       str(tmp_path / out), *extra])
+        assert ok
+        return C.serialize_candidates(run_search(args).candidates)
+
+    a = search("a", "--checkpoint_dir", ck)
+    assert search("a2", "--checkpoint_dir", ck) == a  # same run: resumed
+    import warnings
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        b = search("b", "-m", "7", "--checkpoint_dir", ck)
+    assert any("mismatch" in str(x.message) for x in w)
+    assert b == search("c", "-m", "7") and b != a
+
+
 def test_accmap_tool_finds_injected_delay(tmp_path):
     """tools/peasoup_accmap.py on a synthetic DADA file with a known lag."""
     import json

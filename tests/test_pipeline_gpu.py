@@ -89,6 +89,33 @@ def test_checkpoint_resume_and_fault_injection(tmp_path):
                                                                             "rb").read()
 
 
+def test_checkpoint_resume_with_changed_options_recomputes(tmp_path):
+    """a rerun that reuses --checkpoint_dir with different search
+    options must not mix the old spills in; a corrupt spill is recomputed."""
+    exe = os.path.join(REPO, "bin", "peasoup")
+    ck = tmp_path / "ck"
+    run = lambda out, *extra: subprocess.run([exe, "-i", TUTORIAL, "--dm_end", "120", "-o", str(tmp_path / out),
+                                              *extra], capture_output=True, text=True, timeout=600)
+    r = run("a", "-n", "4", "--checkpoint_dir", str(ck))
+    assert r.returncode == 0, r.stderr
+    spills = sorted(ck.glob("dm_*.psoc"))
+    assert spills
+    r = run("b", "-n", "2", "-m", "7", "--checkpoint_dir", str(ck))  # different options, same directory
+    assert r.returncode == 0, r.stderr
+    assert "mismatch" in r.stdout + r.stderr
+    r = run("c", "-n", "2", "-m", "7")  # clean run
+    assert r.returncode == 0, r.stderr
+    cb = (tmp_path / "b" / "candidates.peasoup").read_bytes()
+    assert cb == (tmp_path / "c" / "candidates.peasoup").read_bytes()
+    assert cb != (tmp_path / "a" / "candidates.peasoup").read_bytes()
+    raw = spills[0].read_bytes()
+    spills[0].write_bytes(raw[: len(raw) // 2])  # truncated spill of the -n 2 run
+    r = run("d", "-n", "2", "-m", "7", "--checkpoint_dir", str(ck))
+    assert r.returncode == 0, r.stderr
+    assert "corrupt" in r.stdout + r.stderr
+    assert (tmp_path / "d" / "candidates.peasoup").read_bytes() == cb
+
+
 def test_injected_accelerated_pulsar_is_found(C, tmp_path):
     """A binary pulsar (a = 60 m/s^2) in synthetic noise is recovered at the
     right DM/acceleration and beats its zero-acceleration detection."""
