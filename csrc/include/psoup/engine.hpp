@@ -128,6 +128,9 @@ struct SearchParams {
   // batches are cut into min_batches even batches (multiples of 8), but never
   // below the batch a quarter of the budget gives.
   int min_batches = 8;
+  // Compute streams the sub-batches of a batch rotate over (>= 2; env
+  // PSOUP_SUB_STREAMS overrides for A/B runs).
+  int sub_streams = 2;
   int min_gap = 30;
   // Acceleration-trial FFT path: 0 = rocFFT R2C of N points; 1 = rocFFT C2C
   // of N/2 points with the real-FFT post-processing fused into the interbin
@@ -264,8 +267,9 @@ class SearchEngine {
   SearchParams p_;
   hipStream_t stream_;
   Stream copy_stream_;
-  Stream aux_stream_;              // second compute stream of the sub-batch pipeline
-  Event fork_, join_;
+  std::vector<std::unique_ptr<Stream>> aux_;  // further compute streams of the sub-batch pipeline
+  std::vector<std::unique_ptr<Event>> joins_;
+  Event fork_;
   int sub_ = 0;                    // effective sub-batch size (0 = whole batch on stream_)
   uint64_t n_, nb_;
   float bin_width_, tobs_;

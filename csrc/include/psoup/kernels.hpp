@@ -255,6 +255,8 @@ enum Fft4Flags : int {
   kFft4UniformTw = 65536,     // pass A: four-step twiddles as per-thread x workgroup-uniform (SGPR) factors
 };
 void fft4_set_flags(int flags);
+// Debug: per-workgroup phase timestamps of the fft4 passes (12 x u64 per block), nullptr = off.
+void fft4_set_trace(unsigned long long* d_events);
 int fft4_flags();
 
 struct HarmParams {

@@ -129,6 +129,14 @@ __device__ __forceinline__ uint64_t accel_index_ii(double af, double size, uint6
   return j > nmax ? nmax : j;
 }
 
+// 32-bit form of accel_index_ii for series shorter than 2^31 samples (one
+// conversion each way instead of the emulated 64-bit ones); same value.
+__device__ __forceinline__ uint32_t accel_index_ii32(double af, double size, uint32_t id, uint32_t nmax) {
+  const double r = accel_pos_ii(af, size, static_cast<double>(id));
+  const double rr = fmin(fmax(rint(r), 0.0), static_cast<double>(nmax));
+  return static_cast<uint32_t>(rr);
+}
+
 }  // namespace dev
 }  // namespace kern
 }  // namespace psoup

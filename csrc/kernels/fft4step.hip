@@ -181,40 +181,58 @@ __device__ __forceinline__ void exchange(Vec<CPT>& v, float* __restrict__ lds, i
 
 // Full forward DFT of length L on the thread's CPT channels (lds = its group's
 // region); input and output both in the pattern v[c][q] <-> element t + q*T.
+// Phase timestamps (tools/expt/fft4_trace.py): when g_fft4_trace is set,
+// thread 0 of each workgroup records the shader clock at fixed points of the
+// kernel (start, loads issued, after every FFT stage and exchange, end).
+__device__ unsigned long long* g_fft4_trace = nullptr;
+constexpr int kTraceEvents = 12;
+__device__ __forceinline__ void trace_event(int ev) {
+  unsigned long long* tr = g_fft4_trace;
+  if (tr != nullptr && threadIdx.x == 0) tr[blockIdx.x * kTraceEvents + ev] = __builtin_readcyclecounter();
+}
+
 template <int L, int CPT, int CG, int Ns>
 __device__ __forceinline__ void fft_stages(Vec<CPT>& v, float* __restrict__ lds, int t,
-                                           const float2* __restrict__ twL) {
+                                           const float2* __restrict__ twL, int ev = 2) {
   constexpr int R = (L / Ns >= 8) ? 8 : L / Ns;
   stage_compute<L, CPT, Ns, R>(v, t, twL);
+  trace_event(ev);
   if constexpr (Ns * R < L) {
     exchange<L, CPT, CG, Ns, R>(v, lds, t);
-    fft_stages<L, CPT, CG, Ns * R>(v, lds, t, twL);
+    trace_event(ev + 1);
+    fft_stages<L, CPT, CG, Ns * R>(v, lds, t, twL, ev + 2);
   }
 }
 
-// S consecutive resampled samples x[p0 .. p0+S-1].  The read index is
-// evaluated exactly (the resampleII formula, as resample_batch) at both ends
-// of the span; when the shift idx(p) - p is the same at both ends, the
-// shift function is monotone on the span (the parabola's vertex n/2 is not
-// inside) and both ends round with a margin, every sample in between has
-// that same shift and the S values are one contiguous load of
-// the padded input (S = 16: 64 bytes).  Otherwise (a shift step inside the span, series edges)
-// each sample is indexed exactly and gathered from the plain series.
+// S consecutive resampled samples x[p0 .. p0+S-1] (resampleII indices,
+// kernels.cu:338-379).  The read index is evaluated exactly, in double, at
+// both ends of the span.  The shift idx(p) - p is monotone on a span away
+// from the parabola's vertex n/2 and changes by at most one there (|af| n < 1e-3
+// for physical accelerations), so with both ends rounding by a margin:
+//   * equal end shifts: every sample has that shift and the S values are one
+//     contiguous load of the padded input (S = 16: four 16-byte loads);
+//   * end shifts one apart: a binary search over the span (log2 S exact
+//     evaluations) finds the first sample with the new shift, and the values
+//     come from one S+4-float window with a per-element select;
+// anything else (spans near the vertex or the series edges, end values within
+// 1e-7 of a rounding tie) is gathered per element.  All index math is 32-bit
+// (series < 2^31 samples; checked on the host).
+constexpr double kVertexGuard = 8192.0;  // spans this close to n/2 take the per-element path
+
 template <int S>  // S = samples per span, a multiple of 4
 __device__ __forceinline__ void load_resampled(const float* __restrict__ in, const float* __restrict__ in_pad,
-                                               uint64_t n, int log2row, uint64_t inpitch, double af, double size,
-                                               uint64_t p0, float (&x)[S]) {
-  const double d0 = static_cast<double>(p0), d1 = static_cast<double>(p0 + S - 1);
+                                               uint32_t n, int log2row, uint32_t inpitch, double af, double size,
+                                               uint32_t p0, float (&x)[S], bool expt_fast = false) {
+  const double d0 = static_cast<double>(p0), d1 = d0 + static_cast<double>(S - 1);
   const double r0 = dev::accel_pos_ii(af, size, d0), r1 = dev::accel_pos_ii(af, size, d1);
   const double q0 = rint(r0), q1 = rint(r1);
-  const double vertex = 0.5 * size;
-  const bool fast = (q1 - q0 == static_cast<double>(S - 1)) && (0.5 - fabs(r0 - q0) > 1e-7) &&
-                    (0.5 - fabs(r1 - q1) > 1e-7) && q0 >= 0.0 && q1 <= static_cast<double>(n - 1) &&
-                    !(d0 < vertex && vertex < d1);
-  if (fast) {
-    const uint64_t i0 = static_cast<uint64_t>(q0);
-    const uint64_t a = (i0 >> log2row) * inpitch + (i0 & ((uint64_t(1) << log2row) - 1));
-    const f4u* src = reinterpret_cast<const f4u*>(in_pad + a);
+  const bool ok = (0.5 - fabs(r0 - q0) > 1e-7) && (0.5 - fabs(r1 - q1) > 1e-7) && q0 >= 1.0 &&
+                  q1 <= static_cast<double>(n - 1) && fabs(0.5 * (d0 + d1) - 0.5 * size) > kVertexGuard;
+  const double ds = (q1 - q0) - static_cast<double>(S - 1);  // change of the shift over the span
+  const uint32_t rowmask = (1u << log2row) - 1u;
+  auto addr = [&](uint32_t i) { return (i >> log2row) * inpitch + (i & rowmask); };
+  if (expt_fast || (ok && ds == 0.0)) {
+    const f4u* src = reinterpret_cast<const f4u*>(in_pad + addr(static_cast<uint32_t>(q0)));
 #pragma unroll
     for (int u = 0; u < S / 4; ++u) {
       const f4u w = src[u];
@@ -223,9 +241,35 @@ __device__ __forceinline__ void load_resampled(const float* __restrict__ in, con
       x[4 * u + 2] = w.z;
       x[4 * u + 3] = w.w;
     }
+  } else if (ok && fabs(ds) == 1.0) {
+    // samples e < hi keep the first shift s0, samples e >= hi have s0 + ds
+    const double s0 = q0 - d0;
+    int lo = 0, hi = S - 1;
+#pragma unroll
+    for (int it = 0; (1 << it) < S - 1; ++it) {
+      const int mid = (lo + hi) >> 1;
+      const double dm = d0 + static_cast<double>(mid);
+      const bool same = rint(dev::accel_pos_ii(af, size, dm)) - dm == s0;
+      lo = same ? mid : lo;
+      hi = same ? hi : mid;
+    }
+    // window w[v] = x_in[q0 - 1 + v], v < S + 4 (the padded row holds the next row's head)
+    float w[S + 4];
+    const f4u* src = reinterpret_cast<const f4u*>(in_pad + addr(static_cast<uint32_t>(q0) - 1u));
+#pragma unroll
+    for (int u = 0; u < S / 4 + 1; ++u) {
+      const f4u v = src[u];
+      w[4 * u] = v.x;
+      w[4 * u + 1] = v.y;
+      w[4 * u + 2] = v.z;
+      w[4 * u + 3] = v.w;
+    }
+    const bool up = ds > 0.0;
+#pragma unroll
+    for (int e = 0; e < S; ++e) x[e] = e < hi ? w[e + 1] : (up ? w[e + 2] : w[e]);
   } else {
 #pragma unroll
-    for (int i = 0; i < S; ++i) x[i] = in[dev::accel_index_ii(af, size, p0 + i, n - 1)];
+    for (int i = 0; i < S; ++i) x[i] = in[dev::accel_index_ii32(af, size, p0 + static_cast<uint32_t>(i), n - 1)];
   }
 }
 
@@ -319,6 +363,16 @@ __device__ __forceinline__ uint32_t logical_block(uint32_t nblocks, bool remap) 
   return remap ? (b & 7u) * (nblocks >> 3) + (b >> 3) : b;
 }
 
+// Experiment (flag bit 18): the second workgroup of every CU in the first
+// dispatch round sleeps ~(flags >> 20) x 1.7 us before starting, so the two
+// workgroups sharing a CU run their load / FFT / store phases out of step.
+__device__ __forceinline__ void stagger_start(int flags) {
+  if ((flags & (1 << 18)) && blockIdx.x >= 256 && blockIdx.x < 512) {
+    const int reps = (flags >> 20) & 15;
+    for (int i = 0; i < reps; ++i) __builtin_amdgcn_s_sleep(64);
+  }
+}
+
 // Input copy with rows of 2*N1 floats at a pitch of 2*N1 + 32 (the pad holds
 // the next row's head, so a span starting in a row is contiguous).  Pass A's
 // lanes read rows 2*N1 floats apart; the odd pitch spreads them over memory
@@ -358,6 +412,8 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
   const int grp = threadIdx.x / T;
   const int t = threadIdx.x - grp * T;
   const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
+  stagger_start(flags);
+  trace_event(0);
   const int N1 = g.n1;
   const uint32_t nbt = static_cast<uint32_t>(N1 / C::CH);  // blocks per trial
   const bool tslow = flags & kFft4TrialSlow;
@@ -393,12 +449,15 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
 #pragma unroll
       for (int e = 0; e < 2 * CPT; ++e) x[e] = static_cast<float>(j + e);
     } else {
-      load_resampled<2 * CPT>(in + src * g.in_tstride, in_pad + src * g.pad_tstride, n, log2row, g.inpitch, af,
-                              size, 2 * (static_cast<uint64_t>(N1) * j + c0), x);
+      load_resampled<2 * CPT>(in + src * g.in_tstride, in_pad + src * g.pad_tstride, static_cast<uint32_t>(n),
+                              log2row, static_cast<uint32_t>(g.inpitch), af, size,
+                              2u * (static_cast<uint32_t>(N1) * static_cast<uint32_t>(j) + static_cast<uint32_t>(c0)),
+                              x, (flags & (1 << 17)) != 0);
     }
 #pragma unroll
     for (int c = 0; c < CPT; ++c) v[c][q] = make_float2(x[2 * c], x[2 * c + 1]);
   }
+  trace_event(1);
   if (!kTiming || !(flags & kFft4SkipCompute))
     fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n2);
   const uint32_t mask = static_cast<uint32_t>(N1) * L - 1;
@@ -468,6 +527,7 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
       if (!kTiming || !(flags & kFft4SkipStore) || v[0][q].x == 1234.5f) store_row<CPT>(dst, v, q, nt);
     }
   }
+  trace_event(11);
 }
 
 // Pass B.  Logical block = row block * K + trial.
@@ -482,6 +542,8 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
   const int grp = threadIdx.x / T;
   const int t = threadIdx.x - grp * T;
   const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
+  stagger_start(flags);
+  trace_event(0);
   const uint32_t nbt = static_cast<uint32_t>(g.n2 / C::CH);  // blocks per trial
   const bool tslow = flags & kFft4TrialSlow;
   const int k = static_cast<int>(tslow ? lb / nbt : lb % static_cast<uint32_t>(K));
@@ -515,6 +577,7 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
       else
         v[c][q] = yk[static_cast<uint64_t>(r0 + c) * g.ypitch + i];
     }
+  trace_event(1);
   if (!kTiming || !(flags & kFft4SkipCompute))
     fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n1);
   float2* xk = X + static_cast<uint64_t>(k) * g.xstride;
@@ -539,6 +602,7 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
 #pragma unroll
       for (int c = 0; c < CPT; ++c) dst[c * 8] = v[c][q];
     }
+    trace_event(11);
     return;
   }
 #pragma unroll
@@ -636,6 +700,9 @@ constexpr int kTimingFlags = kFft4SkipLoad | kFft4SkipStore | kFft4SkipCompute;
 }  // namespace
 
 void fft4_set_flags(int flags) { g_fft4_flags = flags; }
+void fft4_set_trace(unsigned long long* d_events) {
+  PSOUP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_fft4_trace), &d_events, sizeof(d_events)));
+}
 
 // The tiled spectrum needs 8 x 256 r2c tiles: n2 >= 256, n1 >= 16.
 bool tiled_x(const Fft4Geom& g, int f) {
@@ -654,6 +721,7 @@ int fft4_flags() { return g_fft4_flags; }
 void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
                            const Fft4Geom& g, const float2* tables, hipStream_t s) {
   PSOUP_CHECK(g.ok && K >= 1 && n == 2ull * g.n1 * g.n2, "fft4 colpass: bad geometry n=" << n << " K=" << K);
+  PSOUP_CHECK(n < (1ull << 31) && g.insize < (1ull << 32), "fft4 colpass: series too long for 32-bit indices");
   PSOUP_CHECK((reinterpret_cast<uintptr_t>(Y) & 63) == 0, "fft4 colpass: Y alignment");
   const int f = g_fft4_flags;
   const uint64_t nblocks = static_cast<uint64_t>(g.n1 / 8) * K;

@@ -503,6 +503,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("insize", &kern::Fft4Geom::insize);
   k.def("fft4_geometry", &kern::fft4_geometry);
   k.def("fft4_set_flags", &kern::fft4_set_flags);
+  k.def("fft4_set_trace", [](uintptr_t p) { kern::fft4_set_trace(reinterpret_cast<unsigned long long*>(p)); });
   k.def("fft4_flags", &kern::fft4_flags);
   k.def("fft4_tables", [](const kern::Fft4Geom& g) {
     auto t = kern::fft4_tables(g);
@@ -669,6 +670,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("zap_widths", &SearchParams::zap_widths)
       .def_readwrite("accel_batch", &SearchParams::accel_batch)
       .def_readwrite("sub_batch", &SearchParams::sub_batch)
+      .def_readwrite("sub_streams", &SearchParams::sub_streams)
       .def_readwrite("batch_bytes", &SearchParams::batch_bytes)
       .def_readwrite("engines_per_device", &SearchParams::engines_per_device)
       .def_readwrite("min_batches", &SearchParams::min_batches)

@@ -529,6 +529,14 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   }
   sub_ = mode_ != 2 ? 0 : p_.sub_batch >= 0 ? p_.sub_batch : sub_auto;
   if (sub_ >= K_) sub_ = 0;
+  {
+    int ns = std::max(2, p_.sub_streams);
+    if (const char* e = std::getenv("PSOUP_SUB_STREAMS")) ns = std::max(2, std::atoi(e));
+    for (int i = 1; i < ns; ++i) {
+      aux_.push_back(std::make_unique<Stream>());
+      joins_.push_back(std::make_unique<Event>());
+    }
+  }
   cap_ = static_cast<uint32_t>(std::max<uint64_t>(1u << 16, static_cast<uint64_t>(K_) * 4096));
   for (auto& s : slots_) {
     s.done = std::make_unique<Event>();
@@ -633,11 +641,14 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
     // flight and each intermediate (Y, X, P) is re-read soon after it was
     // written, while it is still resident in the 256 MB Infinity Cache.
     fork_.record(stream_);
-    PSOUP_HIP_CHECK(hipStreamWaitEvent(aux_stream_.get(), fork_.get(), 0));
+    for (auto& a : aux_) PSOUP_HIP_CHECK(hipStreamWaitEvent(a->get(), fork_.get(), 0));
+    const int ns = static_cast<int>(aux_.size()) + 1;
     for (int b = 0, j = 0; b < count; b += sub_, ++j)
-      run(b, std::min(sub_, count - b), (j & 1) ? aux_stream_.get() : stream_);
-    join_.record(aux_stream_.get());
-    PSOUP_HIP_CHECK(hipStreamWaitEvent(stream_, join_.get(), 0));
+      run(b, std::min(sub_, count - b), j % ns == 0 ? stream_ : aux_[static_cast<size_t>(j % ns - 1)]->get());
+    for (size_t i = 0; i < aux_.size(); ++i) {
+      joins_[i]->record(aux_[i]->get());
+      PSOUP_HIP_CHECK(hipStreamWaitEvent(stream_, joins_[i]->get(), 0));
+    }
   } else {
     run(0, count, stream_);
   }

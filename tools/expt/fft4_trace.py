@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Phase timeline of the fft4 passes from per-workgroup shader-clock stamps
+(fft4_set_trace): mean cycles between consecutive events, workgroup lifetime,
+and how many workgroups overlap per CU slot.  K = 32 trials at 2^23."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+from peasoup_amd import _C  # noqa: E402
+
+K_ = _C.kernels
+NAMES = ["start", "loads issued", "stage0", "exch1", "stage1", "exch2", "stage2", "exch3", "stage3", "-", "-", "end"]
+
+
+def report(name, ev):
+    ev = ev.astype(np.int64)
+    ok = (ev[:, 0] > 0) & (ev[:, 11] > 0)
+    ev = ev[ok]
+    t0 = ev[:, 0].min()
+    life = ev[:, 11] - ev[:, 0]
+    print(f"{name}: {ok.sum()} workgroups, span {(ev[:, 11].max() - t0):.3e} cycles, "
+          f"mean lifetime {life.mean():.0f} cycles (median {np.median(life):.0f})")
+    prev = 0
+    for e in range(1, 12):
+        if (ev[:, e] == 0).all() or NAMES[e] == "-":
+            continue
+        d = ev[:, e] - ev[:, prev]
+        print(f"   {NAMES[prev]:>13s} -> {NAMES[e]:<13s} {d.mean():8.0f} cycles ({100 * d.mean() / life.mean():4.1f}%)")
+        prev = e
+
+
+def main():
+    dev = torch.device("cuda")
+    n = 1 << 23
+    M = n // 2
+    K = 32
+    s = torch.cuda.current_stream().cuda_stream
+    g = K_.fft4_geometry(M)
+    x = torch.randn(n, device=dev)
+    tab = torch.from_numpy(K_.fft4_tables(g)).to(dev)
+    xp = torch.empty(g.insize, device=dev)
+    K_.fft4_pad_input(x.data_ptr(), n, xp.data_ptr(), g, s)
+    accs = np.linspace(-500, 500, K)
+    af = torch.tensor([a_ * 64e-6 / (2 * 299792458.0) for a_ in accs], dtype=torch.float64, device=dev)
+    Y = torch.empty(K * g.ystride * 2, device=dev)
+    X = torch.empty(K * g.xstride * 2, device=dev)
+    nblk = (g.n1 // 8) * K
+    tr = torch.zeros(nblk * 12, dtype=torch.int64, device=dev)
+    col = lambda: K_.fft4_resample_colpass(x.data_ptr(), xp.data_ptr(), n, af.data_ptr(), K, Y.data_ptr(), g,
+                                           tab.data_ptr(), s)
+    row = lambda: K_.fft4_rowpass(Y.data_ptr(), X.data_ptr(), K, g, tab.data_ptr(), s)
+    for name, fn in (("colpass", col), ("rowpass", row)):
+        fn()
+        fn()
+        torch.cuda.synchronize()
+        tr.zero_()
+        K_.fft4_set_trace(tr.data_ptr())
+        fn()
+        torch.cuda.synchronize()
+        K_.fft4_set_trace(0)
+        report(name, tr.view(nblk, 12).cpu().numpy())
+
+
+if __name__ == "__main__":
+    main()
