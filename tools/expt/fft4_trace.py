@@ -43,7 +43,7 @@ def main():
     tab = torch.from_numpy(K_.fft4_tables(g)).to(dev)
     xp = torch.empty(g.insize, device=dev)
     K_.fft4_pad_input(x.data_ptr(), n, xp.data_ptr(), g, s)
-    accs = np.linspace(-500, 500, K)
+    accs = 200.0 + 1.464 * np.arange(K)  # consecutive legacy-plan steps at 2^23 x 64 us (as in a real batch)
     af = torch.tensor([a_ * 64e-6 / (2 * 299792458.0) for a_ in accs], dtype=torch.float64, device=dev)
     Y = torch.empty(K * g.ystride * 2, device=dev)
     X = torch.empty(K * g.xstride * 2, device=dev)

@@ -49,7 +49,7 @@ def main():
     x = torch.randn(n, device=dev)
     tab = torch.from_numpy(K_.fft4_tables(g)).to(dev)
     tsamp = 64e-6
-    accs = np.linspace(-500, 500, K)
+    accs = 200.0 + 1.464 * np.arange(K)  # consecutive legacy-plan steps at 2^23 x 64 us (as in a real batch)
     af = torch.tensor([a_ * tsamp / (2 * 299792458.0) for a_ in accs], dtype=torch.float64, device=dev)
     xp = torch.empty(g.insize, device=dev)
     Y = torch.empty(K * g.ystride * 2, device=dev)

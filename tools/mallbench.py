@@ -40,7 +40,7 @@ def main():
     out = torch.empty(cap * 3, dtype=torch.int32, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     for K in [int(v) for v in a.Ks.split(",")]:
-        accs = np.linspace(-500, 500, K)
+        accs = 200.0 + 1.464 * np.arange(K)  # consecutive legacy-plan steps at 2^23 x 64 us (as in a real batch)
         af = torch.tensor([v * 64e-6 / (2 * 299792458.0) for v in accs], dtype=torch.float64, device=dev)
         Y = torch.empty(K * g.ystride * 2, device=dev)
         X = torch.empty(K * g.xstride * 2, device=dev)
