@@ -222,7 +222,7 @@ constexpr double kVertexGuard = 8192.0;  // spans this close to n/2 take the per
 template <int S>  // S = samples per span, a multiple of 4
 __device__ __forceinline__ void load_resampled(const float* __restrict__ in, const float* __restrict__ in_pad,
                                                uint32_t n, int log2row, uint32_t inpitch, double af, double size,
-                                               uint32_t p0, float (&x)[S], bool expt_fast = false) {
+                                               uint32_t p0, float (&x)[S]) {
   const double d0 = static_cast<double>(p0), d1 = d0 + static_cast<double>(S - 1);
   const double r0 = dev::accel_pos_ii(af, size, d0), r1 = dev::accel_pos_ii(af, size, d1);
   const double q0 = rint(r0), q1 = rint(r1);
@@ -231,7 +231,7 @@ __device__ __forceinline__ void load_resampled(const float* __restrict__ in, con
   const double ds = (q1 - q0) - static_cast<double>(S - 1);  // change of the shift over the span
   const uint32_t rowmask = (1u << log2row) - 1u;
   auto addr = [&](uint32_t i) { return (i >> log2row) * inpitch + (i & rowmask); };
-  if (expt_fast || (ok && ds == 0.0)) {
+  if (ok && ds == 0.0) {
     const f4u* src = reinterpret_cast<const f4u*>(in_pad + addr(static_cast<uint32_t>(q0)));
 #pragma unroll
     for (int u = 0; u < S / 4; ++u) {
@@ -363,16 +363,6 @@ __device__ __forceinline__ uint32_t logical_block(uint32_t nblocks, bool remap) 
   return remap ? (b & 7u) * (nblocks >> 3) + (b >> 3) : b;
 }
 
-// Experiment (flag bit 18): the second workgroup of every CU in the first
-// dispatch round sleeps ~(flags >> 20) x 1.7 us before starting, so the two
-// workgroups sharing a CU run their load / FFT / store phases out of step.
-__device__ __forceinline__ void stagger_start(int flags) {
-  if ((flags & (1 << 18)) && blockIdx.x >= 256 && blockIdx.x < 512) {
-    const int reps = (flags >> 20) & 15;
-    for (int i = 0; i < reps; ++i) __builtin_amdgcn_s_sleep(64);
-  }
-}
-
 // Input copy with rows of 2*N1 floats at a pitch of 2*N1 + 32 (the pad holds
 // the next row's head, so a span starting in a row is contiguous).  Pass A's
 // lanes read rows 2*N1 floats apart; the odd pitch spreads them over memory
@@ -412,7 +402,6 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
   const int grp = threadIdx.x / T;
   const int t = threadIdx.x - grp * T;
   const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
-  stagger_start(flags);
   trace_event(0);
   const int N1 = g.n1;
   const uint32_t nbt = static_cast<uint32_t>(N1 / C::CH);  // blocks per trial
@@ -452,7 +441,7 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
       load_resampled<2 * CPT>(in + src * g.in_tstride, in_pad + src * g.pad_tstride, static_cast<uint32_t>(n),
                               log2row, static_cast<uint32_t>(g.inpitch), af, size,
                               2u * (static_cast<uint32_t>(N1) * static_cast<uint32_t>(j) + static_cast<uint32_t>(c0)),
-                              x, (flags & (1 << 17)) != 0);
+                              x);
     }
 #pragma unroll
     for (int c = 0; c < CPT; ++c) v[c][q] = make_float2(x[2 * c], x[2 * c + 1]);
@@ -542,7 +531,6 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
   const int grp = threadIdx.x / T;
   const int t = threadIdx.x - grp * T;
   const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
-  stagger_start(flags);
   trace_event(0);
   const uint32_t nbt = static_cast<uint32_t>(g.n2 / C::CH);  // blocks per trial
   const bool tslow = flags & kFft4TrialSlow;

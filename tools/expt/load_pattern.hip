@@ -63,6 +63,37 @@ __global__ void __launch_bounds__(256) lk(const float* __restrict__ in, float* _
 #pragma unroll
       for (int e = 0; e < 17; ++e)
         acc += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, e * (N2 + 32) * 4, 0));
+    } else if (MODE == 9) {  // MODE 7's varying rows, shift from fp32 arithmetic (no double)
+      const float aff = (200.0f + 1.464f * k) * 64e-6f / (2 * 299792458.0f);
+      const float p = 4096.0f * j + 2.0f * c0;
+      const int sh = (int)rintf(aff * p * (p - 8388608.0f));
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in), 0, 0x7fffffff, 0x00020000);
+      const unsigned row = (unsigned)(2 * c0 + sh + 2048);
+      const unsigned vo = (row * (N2 + 32) + j) * 4u;
+#pragma unroll
+      for (int e = 0; e < 17; ++e)
+        acc += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, e * (N2 + 32) * 4, 0));
+    } else if (MODE == 10) {  // rows pattern (plain layout) with the realistic varying shift, fp32
+      const float aff = (200.0f + 1.464f * k) * 64e-6f / (2 * 299792458.0f);
+      const float p = 4096.0f * j + 2.0f * c0;
+      const int sh = (int)rintf(aff * p * (p - 8388608.0f));
+      const f4u* src = reinterpret_cast<const f4u*>(in + (size_t)j * PITCH + 2 * c0 + 2048 + sh);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const f4u w = src[u];
+        acc += w.x + w.y + w.z + w.w;
+      }
+    } else if (MODE == 7 || MODE == 8) {  // transposed, realistic per-row shift (varies along j), buffer loads
+      // shift of row j for trial k at acceleration 200 + 1.464 k m/s^2 (the parabola, 0..-375 samples)
+      const double af = (200.0 + 1.464 * k) * 64e-6 / (2 * 299792458.0);
+      const double p = 4096.0 * j + 2.0 * c0;
+      const int sh = (int)rint(af * p * (p - 8388608.0));
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(in), 0, 0x7fffffff, 0x00020000);
+      const unsigned row = MODE == 7 ? (unsigned)(2 * c0 + sh + 2048) : (unsigned)(2 * c0 + 2048 - 100);
+      const unsigned vo = (row * (N2 + 32) + j) * 4u;
+#pragma unroll
+      for (int e = 0; e < 17; ++e)
+        acc += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, vo, e * (N2 + 32) * 4, 0));
     } else {  // MODE 6: + the exact double-precision span classification per q
       const double af = (200.0 + 1.464 * k) * 64e-6 / (2 * 299792458.0), size = 8388608.0;
       const double d0 = (double)(4096u * (unsigned)j + 2u * (unsigned)c0), d1 = d0 + 15.0;
@@ -83,7 +114,7 @@ __global__ void __launch_bounds__(256) lk(const float* __restrict__ in, float* _
 
 int main(int argc, char** argv) {
   const int K = argc > 1 ? atoi(argv[1]) : 32;
-  const size_t nin = (size_t)N2 * PITCH * 2 + (1 << 20);
+  const size_t nin = (size_t)(2 * N1 + 4096 + 64) * (N2 + 32) + (1 << 20);
   float *in, *out;
   if (hipMalloc(&in, nin * 4) != hipSuccess || hipMalloc(&out, 1 << 22) != hipSuccess) return 1;
   (void)hipMemset(in, 0, nin * 4);
@@ -110,6 +141,10 @@ int main(int argc, char** argv) {
   time("contig", [&] { lk<3><<<grid, 256, lds>>>(in, out, K, 5); });
   time("tdword", [&] { lk<4><<<grid, 256, lds>>>(in, out, K, 5); });
   time("tbuffer", [&] { lk<5><<<grid, 256, lds>>>(in, out, K, 5); });
+  time("tshift", [&] { lk<7><<<grid, 256, lds>>>(in, out, K, 5); });
+  time("tnoshift", [&] { lk<8><<<grid, 256, lds>>>(in, out, K, 5); });
+  time("tshift32", [&] { lk<9><<<grid, 256, lds>>>(in, out, K, 5); });
+  time("rowshift32", [&] { lk<10><<<grid, 256, lds>>>(in, out, K, 5); });
   time("tbuf+f64", [&] { lk<6><<<grid, 256, lds>>>(in, out, K, 5); });
   time("rows", [&] { lk<0><<<grid, 256, lds>>>(in, out, K, 5); });
   return 0;
