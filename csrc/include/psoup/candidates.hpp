@@ -73,8 +73,11 @@ class HarmonicDistiller {
   HarmonicDistiller(float tol, float max_harm, bool keep_related, bool fractional_harms = true)
       : tol_(tol), max_harm_(max_harm), keep_related_(keep_related), fractional_(fractional_harms) {}
   CandidateList distill(CandidateList cands) const;
+  // the reference's O(n^2) scan (tests compare the indexed path against it)
+  CandidateList distill_reference(CandidateList cands) const { return run(std::move(cands), true); }
 
  private:
+  CandidateList run(CandidateList cands, bool force_scan) const;
   float tol_, max_harm_;
   bool keep_related_, fractional_;
 };
@@ -83,8 +86,10 @@ class AccelerationDistiller {
  public:
   AccelerationDistiller(float tobs, float tol, bool keep_related);
   CandidateList distill(CandidateList cands) const;
+  CandidateList distill_reference(CandidateList cands) const { return run(std::move(cands), true); }
 
  private:
+  CandidateList run(CandidateList cands, bool force_scan) const;
   float tobs_, tol_;
   double tobs_over_c_;
   bool keep_related_;
@@ -94,8 +99,10 @@ class DMDistiller {
  public:
   DMDistiller(float tol, bool keep_related) : tol_(tol), keep_related_(keep_related) {}
   CandidateList distill(CandidateList cands) const;
+  CandidateList distill_reference(CandidateList cands) const { return run(std::move(cands), true); }
 
  private:
+  CandidateList run(CandidateList cands, bool force_scan) const;
   float tol_;
   bool keep_related_;
 };

@@ -273,13 +273,16 @@ PYBIND11_MODULE(_C, m) {
   py::class_<HarmonicDistiller>(m, "HarmonicDistiller")
       .def(py::init<float, float, bool, bool>(), py::arg("tol"), py::arg("max_harm"), py::arg("keep_related"),
            py::arg("fractional_harms") = true)
-      .def("distill", &HarmonicDistiller::distill);
+      .def("distill", &HarmonicDistiller::distill)
+      .def("distill_reference", &HarmonicDistiller::distill_reference);
   py::class_<AccelerationDistiller>(m, "AccelerationDistiller")
       .def(py::init<float, float, bool>(), py::arg("tobs"), py::arg("tol"), py::arg("keep_related"))
-      .def("distill", &AccelerationDistiller::distill);
+      .def("distill", &AccelerationDistiller::distill)
+      .def("distill_reference", &AccelerationDistiller::distill_reference);
   py::class_<DMDistiller>(m, "DMDistiller")
       .def(py::init<float, bool>(), py::arg("tol"), py::arg("keep_related"))
-      .def("distill", &DMDistiller::distill);
+      .def("distill", &DMDistiller::distill)
+      .def("distill_reference", &DMDistiller::distill_reference);
   py::class_<CandidateScorer>(m, "CandidateScorer")
       .def(py::init<float, float, float, float>(), py::arg("tsamp"), py::arg("cfreq"), py::arg("foff"), py::arg("bw"))
       .def("score_all", [](const CandidateScorer& s, CandidateList c) {

@@ -4,6 +4,8 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <memory>
+#include <vector>
 
 #include "psoup/common.hpp"
 
@@ -46,14 +48,59 @@ std::string Candidate::print() const {
 
 namespace {
 
-// BaseDistiller::distill (distiller.hpp:27-59) with a pluggable condition.
-template <class Cond>
-CandidateList base_distill(CandidateList cands, Cond&& condition) {
+// BaseDistiller::distill (distiller.hpp:27-59): sort by S/N, then every
+// surviving candidate in turn (the "fundamental") marks the later candidates
+// related to it as non-unique (appending them to its assoc list when
+// keep_related).  The reference scans every later candidate for every
+// fundamental -- O(n^2) relation tests, 128-512 ratio tests each for the
+// harmonic distiller -- which becomes the host bottleneck on candidate-heavy
+// data.  Each distiller here also gives, per
+// fundamental, frequency windows that contain every candidate its relation
+// can accept; above kIndexedMin candidates those windows are looked up in a
+// frequency-sorted index and only the candidates found are tested, in
+// ascending S/N-rank order with the reference's exact relation (same
+// floating-point expressions, same append order and multiplicity), so the
+// output is identical to the O(n^2) scan (tests: distill_reference).
+constexpr size_t kIndexedMin = 64;
+
+struct FreqIndex {
+  std::vector<double> f;        // ascending
+  std::vector<uint32_t> rank;   // S/N rank of f[i]
+  explicit FreqIndex(const CandidateList& c) {
+    std::vector<uint32_t> order(c.size());
+    for (size_t i = 0; i < c.size(); ++i) order[i] = static_cast<uint32_t>(i);
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+      return static_cast<double>(c[a].freq) < static_cast<double>(c[b].freq);
+    });
+    f.resize(order.size());
+    rank.resize(order.size());
+    for (size_t i = 0; i < order.size(); ++i) {
+      f[i] = c[order[i]].freq;
+      rank[i] = order[i];
+    }
+  }
+  // ranks > idx with frequency in [lo, hi], appended to out
+  void query(double lo, double hi, size_t idx, std::vector<uint32_t>& out) const {
+    auto it = std::lower_bound(f.begin(), f.end(), lo);
+    for (size_t i = static_cast<size_t>(it - f.begin()); i < f.size() && f[i] <= hi; ++i)
+      if (rank[i] > idx) out.push_back(rank[i]);
+  }
+};
+
+// windows(c, idx, push(lo, hi)) lists the fundamental's frequency windows;
+// related(c, idx, ii) is the reference's inner-loop body for one later
+// candidate (performs the appends) and returns whether ii is related.
+template <class Windows, class Related>
+CandidateList base_distill(CandidateList cands, Windows&& windows, Related&& related, bool force_scan = false) {
   const size_t size = cands.size();
   std::vector<char> unique(size, 1);
   // std::sort (not stable_sort) on purpose: with the same input order it breaks
   // S/N ties exactly as the reference's libstdc++ introsort does.
   std::sort(cands.begin(), cands.end(), [](const Candidate& a, const Candidate& b) { return a.snr > b.snr; });
+  const bool indexed = !force_scan && size >= kIndexedMin;
+  std::unique_ptr<FreqIndex> index;
+  if (indexed) index = std::make_unique<FreqIndex>(cands);
+  std::vector<uint32_t> hits;
   size_t start = 0;
   while (true) {
     long idx = -1;
@@ -65,7 +112,23 @@ CandidateList base_distill(CandidateList cands, Cond&& condition) {
       }
     }
     if (idx < 0) break;
-    condition(cands, static_cast<size_t>(idx), unique);
+    const size_t fi = static_cast<size_t>(idx);
+    if (!indexed) {
+      for (size_t ii = fi + 1; ii < size; ++ii)
+        if (related(cands, fi, ii)) unique[ii] = 0;
+      continue;
+    }
+    hits.clear();
+    windows(cands, fi, [&](double lo, double hi) {
+      // a relative 1e-9 margin covers the rounding of the window bounds; the
+      // exact relation decides membership
+      const double m = 1e-9 * std::max(std::fabs(lo), std::fabs(hi));
+      index->query(lo - m, hi + m, fi, hits);
+    });
+    std::sort(hits.begin(), hits.end());
+    hits.erase(std::unique(hits.begin(), hits.end()), hits.end());
+    for (uint32_t ii : hits)
+      if (related(cands, fi, ii)) unique[ii] = 0;
   }
   CandidateList out;
   for (size_t ii = 0; ii < size; ++ii)
@@ -75,29 +138,41 @@ CandidateList base_distill(CandidateList cands, Cond&& condition) {
 
 }  // namespace
 
-CandidateList HarmonicDistiller::distill(CandidateList cands) const {
+CandidateList HarmonicDistiller::distill(CandidateList cands) const { return run(std::move(cands), false); }
+
+CandidateList HarmonicDistiller::run(CandidateList cands, bool force_scan) const {
   const double upper_tol = 1 + tol_;
   const double lower_tol = 1 - tol_;
   const float max_harm = max_harm_;
   const bool keep = keep_related_, frac = fractional_;
-  return base_distill(std::move(cands), [&](CandidateList& c, size_t idx, std::vector<char>& unique) {
+  int max_nh = 0;
+  for (const auto& c : cands) max_nh = std::max(max_nh, c.nh);
+  const float max_den_all = frac ? static_cast<float>(std::pow(2.0, max_nh)) : 1.f;
+  auto windows = [&](const CandidateList& c, size_t idx, auto&& push) {
+    // ratio = kk f / (jj fundi) in (lower, upper)  <=>  f in (lower, upper) * jj fundi / kk
     const double fundi_freq = c[idx].freq;
-    const size_t size = c.size();
-    for (size_t ii = idx + 1; ii < size; ++ii) {
-      const double freq = c[ii].freq;
-      const int nh = c[ii].nh;
-      const float max_denominator = frac ? static_cast<float>(std::pow(2.0, nh)) : 1.f;
-      for (int jj = 1; jj <= max_harm; ++jj) {
-        for (int kk = 1; kk <= max_denominator; ++kk) {
-          const double ratio = kk * freq / (jj * fundi_freq);
-          if (ratio > lower_tol && ratio < upper_tol) {
-            if (keep) c[idx].append(c[ii]);
-            unique[ii] = 0;
-          }
+    for (int jj = 1; jj <= max_harm; ++jj)
+      for (int kk = 1; kk <= max_den_all; ++kk)
+        push(lower_tol * jj * fundi_freq / kk, upper_tol * jj * fundi_freq / kk);
+  };
+  auto related = [&](CandidateList& c, size_t idx, size_t ii) {
+    const double fundi_freq = c[idx].freq;
+    const double freq = c[ii].freq;
+    const int nh = c[ii].nh;
+    const float max_denominator = frac ? static_cast<float>(std::pow(2.0, nh)) : 1.f;
+    bool rel = false;
+    for (int jj = 1; jj <= max_harm; ++jj) {
+      for (int kk = 1; kk <= max_denominator; ++kk) {
+        const double ratio = kk * freq / (jj * fundi_freq);
+        if (ratio > lower_tol && ratio < upper_tol) {
+          if (keep) c[idx].append(c[ii]);
+          rel = true;
         }
       }
     }
-  });
+    return rel;
+  };
+  return base_distill(std::move(cands), windows, related, force_scan);
 }
 
 AccelerationDistiller::AccelerationDistiller(float tobs, float tol, bool keep_related)
@@ -105,48 +180,62 @@ AccelerationDistiller::AccelerationDistiller(float tobs, float tol, bool keep_re
   tobs_over_c_ = tobs_ / kSpeedOfLight;
 }
 
-CandidateList AccelerationDistiller::distill(CandidateList cands) const {
+CandidateList AccelerationDistiller::distill(CandidateList cands) const { return run(std::move(cands), false); }
+
+CandidateList AccelerationDistiller::run(CandidateList cands, bool force_scan) const {
   const double toc = tobs_over_c_;
   const float tol = tol_;
   const bool keep = keep_related_;
-  return base_distill(std::move(cands), [&](CandidateList& c, size_t idx, std::vector<char>& unique) {
+  double acc_min = 0.0, acc_max = 0.0;
+  for (size_t i = 0; i < cands.size(); ++i) {
+    acc_min = i ? std::min(acc_min, static_cast<double>(cands[i].acc)) : cands[i].acc;
+    acc_max = i ? std::max(acc_max, static_cast<double>(cands[i].acc)) : cands[i].acc;
+  }
+  auto windows = [&](const CandidateList& c, size_t idx, auto&& push) {
+    // acc_freq spans fundi + (fundi_acc - acc) fundi toc over the candidates' accelerations
+    const double fundi_freq = c[idx].freq, fundi_acc = c[idx].acc, edge = fundi_freq * tol;
+    const double a1 = fundi_freq + (fundi_acc - acc_max) * fundi_freq * toc;
+    const double a2 = fundi_freq + (fundi_acc - acc_min) * fundi_freq * toc;
+    // acc_freq is rounded to float in the relation: widen by 1e-6 relative
+    const double lo = std::min({fundi_freq, a1, a2}) - edge, hi = std::max({fundi_freq, a1, a2}) + edge;
+    push(lo - 1e-6 * std::fabs(lo), hi + 1e-6 * std::fabs(hi));
+  };
+  auto related = [&](CandidateList& c, size_t idx, size_t ii) {
     const double fundi_freq = c[idx].freq;
     const double fundi_acc = c[idx].acc;
     const double edge = fundi_freq * tol;
-    const size_t size = c.size();
-    for (size_t ii = idx + 1; ii < size; ++ii) {
-      const double delta_acc = fundi_acc - c[ii].acc;
-      // correct_for_acceleration returns float (distiller.hpp:120-122).
-      const double acc_freq = static_cast<float>(fundi_freq + delta_acc * fundi_freq * toc);
-      const double f = c[ii].freq;
-      bool related;
-      if (acc_freq > fundi_freq)
-        related = (f > fundi_freq - edge && f < acc_freq + edge);
-      else
-        related = (f < fundi_freq + edge && f > acc_freq - edge);
-      if (related) {
-        if (keep) c[idx].append(c[ii]);
-        unique[ii] = 0;
-      }
-    }
-  });
+    const double delta_acc = fundi_acc - c[ii].acc;
+    // correct_for_acceleration returns float (distiller.hpp:120-122).
+    const double acc_freq = static_cast<float>(fundi_freq + delta_acc * fundi_freq * toc);
+    const double f = c[ii].freq;
+    bool rel;
+    if (acc_freq > fundi_freq)
+      rel = (f > fundi_freq - edge && f < acc_freq + edge);
+    else
+      rel = (f < fundi_freq + edge && f > acc_freq - edge);
+    if (rel && keep) c[idx].append(c[ii]);
+    return rel;
+  };
+  return base_distill(std::move(cands), windows, related, force_scan);
 }
 
-CandidateList DMDistiller::distill(CandidateList cands) const {
+CandidateList DMDistiller::distill(CandidateList cands) const { return run(std::move(cands), false); }
+
+CandidateList DMDistiller::run(CandidateList cands, bool force_scan) const {
   const double upper_tol = 1 + tol_;
   const double lower_tol = 1 - tol_;
   const bool keep = keep_related_;
-  return base_distill(std::move(cands), [&](CandidateList& c, size_t idx, std::vector<char>& unique) {
+  auto windows = [&](const CandidateList& c, size_t idx, auto&& push) {
     const double fundi_freq = c[idx].freq;
-    const size_t size = c.size();
-    for (size_t ii = idx + 1; ii < size; ++ii) {
-      const double ratio = c[ii].freq / fundi_freq;
-      if (ratio > lower_tol && ratio < upper_tol) {
-        if (keep) c[idx].append(c[ii]);
-        unique[ii] = 0;
-      }
-    }
-  });
+    push(lower_tol * fundi_freq, upper_tol * fundi_freq);
+  };
+  auto related = [&](CandidateList& c, size_t idx, size_t ii) {
+    const double ratio = c[ii].freq / static_cast<double>(c[idx].freq);
+    const bool rel = ratio > lower_tol && ratio < upper_tol;
+    if (rel && keep) c[idx].append(c[ii]);
+    return rel;
+  };
+  return base_distill(std::move(cands), windows, related, force_scan);
 }
 
 CandidateScorer::CandidateScorer(float tsamp, float cfreq, float foff, float bw)

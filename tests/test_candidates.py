@@ -123,6 +123,24 @@ def test_acceleration_and_dm_distillers_match_python(C, seed):
     assert [sig(c) for c in nat] == [sig(c) for c in py]
 
 
+@pytest.mark.parametrize("seed", [5, 6])
+def test_indexed_distillers_equal_reference_scan(C, seed):
+    # above 64 candidates the distillers look fundamentals' relation windows up
+    # in a frequency index; the output (order, assoc trees, multiplicity) must
+    # equal the reference's O(n^2) scan exactly
+    rng = random.Random(seed)
+    tup = random_cands(rng, 1500, base_freqs=(0.37, 1.9, 4.0, 7.3, 11.1, 53.2, 210.0))
+    tup += [(t[0], t[1], t[2], t[3], f32(t[4] + 0.5), f32(t[5] * (1 + 3e-4))) for t in tup[:200]]
+    dists = [C.HarmonicDistiller(1e-4, 16, k, fr) for k, fr in ((True, True), (False, True), (True, False))]
+    dists += [C.HarmonicDistiller(3e-3, 8, True, True), C.AccelerationDistiller(41.94304, 1e-4, True),
+              C.AccelerationDistiller(600.0, 2e-4, True), C.DMDistiller(1e-4, True), C.DMDistiller(5e-3, True)]
+    for d in dists:
+        fast = d.distill(to_native(C, tup))
+        slow = d.distill_reference(to_native(C, tup))
+        assert 0 < len(fast) < len(tup)
+        assert [[tuple(p) for p in c.pods()] for c in fast] == [[tuple(p) for p in c.pods()] for c in slow]
+
+
 def test_keep_related_appends_once_per_match(C):
     # candidate at 2x the fundamental matches jj=2,kk=1 and jj=4,kk=2 (nh=1 -> 2 denominators)
     c = [C.Candidate(10, 1, 0, 1, 50.0, 1.0), C.Candidate(10, 1, 0, 1, 20.0, 2.0)]
