@@ -253,6 +253,9 @@ enum Fft4Flags : int {
   kFft4Sub2 = 16384,     // tiled paths: two thread groups x 4 transforms per workgroup (fewer VGPRs, 4 waves/SIMD)
   kFft4StagedStores = 32768,  // tiled paths: LDS-staged stores, 4 KiB contiguous per store instruction
   kFft4UniformTw = 65536,     // pass A: four-step twiddles as per-thread x workgroup-uniform (SGPR) factors
+  kFft4OneX = 131072,         // pass A (tiled Y, column length 512..2048): 2 columns x L/G points per thread,
+                              // one LDS exchange, compile-time twiddles inside the two local DFTs
+  kFft4OneXWholeCu = 262144,  // with kFft4OneX at L = 2048: the exchange in one 128 KiB round (one workgroup per CU)
 };
 void fft4_set_flags(int flags);
 // Debug: per-workgroup phase timestamps of the fft4 passes (12 x u64 per block), nullptr = off.

@@ -274,9 +274,12 @@ __device__ __forceinline__ void load_resampled(const float* __restrict__ in, con
 }
 
 // Table layout (float2): [tw_N2 (N2)] [tw_N1 (N1)] [lo (2^kSplit)] [hi (M >> kSplit)]
+// [ox (N1 x GX)]: ox[col * GX + k2] = W_M^{col P k2}, the k2 part of the
+// one-exchange pass A's four-step twiddles (GX = onex_g(N2), P = N2 / GX).
 struct TableOffsets {
-  uint64_t n2, n1, lo, hi, total;
+  uint64_t n2, n1, lo, hi, ox, total;
 };
+__host__ __device__ constexpr int onex_g(int N2) { return N2 >= 2048 ? 64 : 32; }
 __host__ __device__ inline TableOffsets table_offsets(int N1, int N2) {
   const uint64_t M = static_cast<uint64_t>(N1) * N2;
   TableOffsets o;
@@ -284,7 +287,8 @@ __host__ __device__ inline TableOffsets table_offsets(int N1, int N2) {
   o.n1 = o.n2 + N2;
   o.lo = o.n1 + N1;
   o.hi = o.lo + (1u << kSplit);
-  o.total = o.hi + (M >> kSplit);
+  o.ox = o.hi + (M >> kSplit);
+  o.total = o.ox + static_cast<uint64_t>(N1) * onex_g(N2);
   return o;
 }
 
@@ -519,6 +523,320 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
   trace_event(11);
 }
 
+// ---------------------------------------------------------------------------
+// One-exchange pass A (kFft4OneX).  Column length L = G * P: thread
+// (cp = t & 3, g = t >> 2) owns columns c0 + 2cp and c0 + 2cp + 1 at rows
+// g + G m (m < P): one 16-byte load per row, four lanes covering a row's
+// 64-byte segment.  With n = G m + g and k = k1 + P k2,
+//   X[k] = sum_g W_G^{g k2} [ W_L^{g k1} sum_m x[G m + g] W_P^{m k1} ],
+// so each thread runs the P-point DFT over m of its two columns in registers
+// (twiddles are compile-time constants), multiplies by W_L^{g k1}, and one
+// LDS exchange (in g slices of at most 8192 complex) hands every thread
+// (column, k1) pairs holding all G values of g, whose G-point DFTs again run
+// in registers.  The Stockham kernel above needs log_8(L) - 1 exchanges (3 at
+// L = 2048) and table twiddles in every stage.  Reader pairs are assigned so
+// that every store instruction of a wave writes one contiguous 512-byte block
+// of the tiled Y.
+
+// compile-time twiddles: W_N^e = exp(-2 pi i e / N), octant-reduced Taylor series in double
+struct ccf {
+  float x, y;
+};
+constexpr double ct_sin(double x) {  // |x| <= pi/4
+  double term = x, sum = x;
+  for (int i = 1; i < 12; ++i) {
+    term *= -x * x / ((2.0 * i) * (2.0 * i + 1.0));
+    sum += term;
+  }
+  return sum;
+}
+constexpr double ct_cos(double x) {
+  double term = 1.0, sum = 1.0;
+  for (int i = 1; i < 12; ++i) {
+    term *= -x * x / ((2.0 * i - 1.0) * (2.0 * i));
+    sum += term;
+  }
+  return sum;
+}
+constexpr ccf wconst(int N, int e) {
+  e = ((e % N) + N) % N;
+  const int q = (4 * e) / N, rem = e - q * (N / 4);  // angle = q quarter turns + 2 pi rem / N
+  constexpr double kTwoPi = 6.28318530717958647692;
+  double c = 0.0, s = 0.0;
+  if (8 * rem <= N) {
+    const double th = kTwoPi * rem / N;
+    c = ct_cos(th);
+    s = ct_sin(th);
+  } else {
+    const double th = kTwoPi * (N / 4 - rem) / N;
+    c = ct_sin(th);
+    s = ct_cos(th);
+  }
+  double cq = c, sq = s;  // rotate by q quarter turns
+  if (q == 1) { cq = -s; sq = c; }
+  if (q == 2) { cq = -c; sq = -s; }
+  if (q == 3) { cq = s; sq = -c; }
+  return ccf{static_cast<float>(cq), static_cast<float>(-sq)};
+}
+
+template <int I>
+struct ic {
+  static constexpr int value = I;
+};
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(ic<B>{});
+    sfor<B + 1, E>(static_cast<F&&>(f));
+  }
+}
+
+// v * W_N^E (compile-time exponent; trivial factors without multiplications)
+template <int N, int E>
+__device__ __forceinline__ float2 twc(float2 v) {
+  constexpr int e = ((E % N) + N) % N;
+  if constexpr (e == 0) {
+    return v;
+  } else if constexpr (2 * e == N) {
+    return make_float2(-v.x, -v.y);
+  } else if constexpr (4 * e == N) {
+    return mul_mi(v);
+  } else if constexpr (4 * e == 3 * N) {
+    return make_float2(-v.y, v.x);
+  } else if constexpr (8 * e == N) {
+    constexpr float r2 = 0.70710678118654752440f;
+    return make_float2(r2 * (v.x + v.y), r2 * (v.y - v.x));
+  } else {
+    constexpr ccf w = wconst(N, e);
+    return make_float2(v.x * w.x - v.y * w.y, v.x * w.y + v.y * w.x);
+  }
+}
+
+// In-register forward DFT of length N (power of two <= 64), natural order in
+// and out: N = 8 B, n = B a + b, k = ka + 8 kb.
+template <int N>
+__device__ __forceinline__ void dft(float2 (&x)[N]) {
+  if constexpr (N == 2) {
+    fft2(x[0], x[1]);
+  } else if constexpr (N == 4) {
+    fft4(x[0], x[1], x[2], x[3]);
+  } else if constexpr (N == 8) {
+    fft8(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
+  } else {
+    constexpr int A = 8, B = N / 8;
+    float2 y[N];
+    sfor<0, B>([&](auto bc) {
+      constexpr int b = decltype(bc)::value;
+      float2 t[A];
+      sfor<0, A>([&](auto ac) { t[decltype(ac)::value] = x[B * decltype(ac)::value + b]; });
+      dft<A>(t);
+      sfor<0, A>([&](auto kc) {
+        constexpr int ka = decltype(kc)::value;
+        y[b * A + ka] = twc<N, b * ka>(t[ka]);
+      });
+    });
+    sfor<0, A>([&](auto kc) {
+      constexpr int ka = decltype(kc)::value;
+      float2 t[B];
+      sfor<0, B>([&](auto bc) { t[decltype(bc)::value] = y[decltype(bc)::value * A + ka]; });
+      dft<B>(t);
+      sfor<0, B>([&](auto jc) { x[ka + A * decltype(jc)::value] = t[decltype(jc)::value]; });
+    });
+  }
+}
+
+template <int L, int G, int R>
+struct OneX {
+  static constexpr int P = L / G;           // rows per thread and column: g + G m
+  static constexpr int THREADS = 4 * G;     // (cp, g)
+  static constexpr int NW = THREADS / 64;   // waves
+  static constexpr int NPAIR = 2 * P / G;   // (column, k1) pairs per thread after the exchange
+  static constexpr int ROUNDS = R;          // exchange rounds: g slices of GS values (one writer wave group each)
+  static constexpr int GS = G / ROUNDS;
+  // LDS element (c, k1, g') at c + SK k1 + SG g': ds_write_b128 of a thread's
+  // two columns hits 8 distinct 16-byte slots per 8-lane group (SG = 8 mod
+  // 16) and the pair reads 32 distinct dword pairs per 32-lane group (SK = 4
+  // mod 32); 8 + SG (GS - 1) <= SK keeps the (c, g') blocks of every k1 apart.
+  static constexpr int SG = 8;
+  static constexpr int SK = (SG * GS + 27) / 32 * 32 + 4;
+  static constexpr int BUF = SK * (P - 1) + SG * GS;   // complex elements per buffer
+  static constexpr int NBUF = ROUNDS > 1 ? 2 : 1;      // double-buffered rounds: one barrier each
+  static constexpr int TWS = 8 * (G + 1);              // W_M^{col P k2} rows of the 8 columns (padded: 4
+                                                       // columns read by a 32-lane group on distinct banks)
+  static_assert(P % 8 == 0 && G % 16 == 0 && NPAIR >= 1 && NPAIR * G == 2 * P, "one-exchange shape");
+  static_assert(GS * ROUNDS == G && GS % 16 == 0 && 8 + SG * (GS - 1) <= SK, "one-exchange LDS layout");
+  // R = 1 at L = 2048: the whole 128 KiB exchange in one round, one workgroup per CU
+  static constexpr bool kWholeCu = (NBUF * BUF + 8 * (G + 1)) * 8 > kLdsBudget;
+  static_assert((NBUF * BUF + TWS) * 8 <= (kWholeCu ? 160 * 1024 : kLdsBudget), "one-exchange LDS budget");
+};
+
+template <int L, int G, int R>
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, OneX<L, G, R>::THREADS),
+                               amdgpu_waves_per_eu(OneX<L, G, R>::kWholeCu ? 1 : 2)))
+fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__ in_pad, uint64_t n,
+                         const double* __restrict__ afs, int K, float2* __restrict__ Y, Fft4Geom g,
+                         const float2* __restrict__ tab, int flags) {
+  using C = OneX<L, G, R>;
+  constexpr int P = C::P;
+  __shared__ __attribute__((aligned(16))) float2 lds[C::NBUF * C::BUF + C::TWS];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int cp = t & 3, gg = t >> 2;
+  const int N1 = g.n1;
+  trace_event(0);
+  // block -> (trial k, first column c0): the Stockham kernel's order and XCD grouping
+  const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
+  const uint32_t nbt = static_cast<uint32_t>(N1 / 8);
+  const bool tslow = flags & kFft4TrialSlow;
+  int k = static_cast<int>(tslow ? lb / nbt : lb % static_cast<uint32_t>(K));
+  int c0 = static_cast<int>(tslow ? lb % nbt : lb / static_cast<uint32_t>(K)) * 8;
+  if ((flags & kFft4GroupXcd) && (K & 7) == 0) {
+    const uint32_t b = blockIdx.x;
+    const uint32_t Gp = ((b >> 7) << 3) | (b & 7u), wq = (b >> 3) & 15u;
+    const uint32_t kg = static_cast<uint32_t>(K) >> 3;
+    k = static_cast<int>(8 * (Gp % kg) + (wq & 7u));
+    c0 = static_cast<int>(2 * (Gp / kg) + (wq >> 3)) * 8;
+  } else if (flags & kFft4PairXcd) {
+    const uint32_t b = blockIdx.x;
+    const uint32_t s = (b >> 3) & 1u, u = ((b >> 4) << 3) | (b & 7u);
+    k = static_cast<int>(u % static_cast<uint32_t>(K));
+    c0 = static_cast<int>(2 * (u / static_cast<uint32_t>(K)) + s) * 8;
+  }
+  const int log2row = __builtin_ctz(static_cast<unsigned>(2 * N1));
+  const TableOffsets to = table_offsets(N1, L);
+  const double af = afs[k];
+  const uint64_t src = g.tsrc ? g.tsrc[k] : static_cast<uint64_t>(k);
+  const float* ink = in + src * g.in_tstride;
+  const float* padk = in_pad + src * g.pad_tstride;
+  const uint32_t nn = static_cast<uint32_t>(n);
+  float2* tws = lds + C::NBUF * C::BUF;
+  static_assert(onex_g(L) == G, "one-exchange twiddle table shape");
+  for (int e = t; e < 8 * G; e += C::THREADS)  // rows c0 .. c0 + 7 of the ox table (first barrier: the exchange)
+    tws[(e / G) * (G + 1) + (e % G)] = tab[to.ox + static_cast<uint64_t>(c0) * G + e];
+  const float afl = static_cast<float>(af), sizef = static_cast<float>(n);
+  // fp32 shift estimate: |af p (p - n)| <= |af| n^2 / 4 with < 2.4e-7 relative
+  // error; exact float positions need n <= 2^24
+  const float band = n <= (1ull << 24) ? 6e-7f * fabsf(afl) * sizef * sizef * 0.25f + 1e-5f : 1.0f;
+
+  float2 va[P], vb[P];  // columns c0 + 2cp, c0 + 2cp + 1
+  {
+    // four consecutive resampled samples x[p0 .. p0+3] per row (resampleII):
+    // the shift rint(af p (p - n)) is estimated in fp32 at both ends; when
+    // both estimates are further than `band` (the fp32 error bound) from a
+    // rounding tie and equal, the samples share that shift and are one
+    // 16-byte load of the padded input (32-bit buffer offsets); other rows
+    // (rare: a shift step inside the four samples, a near-tie, a series edge)
+    // are redone below with every index evaluated exactly in double
+    // (dev::accel_index_ii32, the reference's expression).
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(padk), 0, 0x7fffffff, 0x00020000);
+    const uint32_t rowmask = (1u << log2row) - 1u, pitch = static_cast<uint32_t>(g.inpitch);
+    uint32_t bad = 0;
+#pragma unroll
+    for (int m = 0; m < P; ++m) {
+      const uint32_t j = static_cast<uint32_t>(gg + G * m);
+      const uint32_t p0 = 2u * (static_cast<uint32_t>(N1) * j + static_cast<uint32_t>(c0 + 2 * cp));
+      const float pa = static_cast<float>(p0), pb = pa + 3.0f;
+      const float fa = afl * pa * (pa - sizef), fb = afl * pb * (pb - sizef);
+      const float sa = rintf(fa), sb = rintf(fb);
+      const int64_t first = static_cast<int64_t>(p0) + static_cast<int>(sa);
+      const bool ok = sa == sb && fabsf(fa - sa) < 0.5f - band && fabsf(fb - sb) < 0.5f - band && first >= 0 &&
+                      first + 3 < static_cast<int64_t>(nn);
+      const uint32_t i = ok ? static_cast<uint32_t>(first) : p0;
+      const f4v v = __builtin_bit_cast(
+          f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i >> log2row) * pitch + (i & rowmask)) * 4u, 0, 0));
+      bad |= ok ? 0u : (1u << m);
+      va[m] = make_float2(v.x, v.y);
+      vb[m] = make_float2(v.z, v.w);
+    }
+    trace_event(1);
+    if (bad != 0) {
+      const double size = static_cast<double>(n);
+#pragma unroll
+      for (int m = 0; m < P; ++m) {
+        if (bad & (1u << m)) {
+          const uint32_t j = static_cast<uint32_t>(gg + G * m);
+          const uint32_t p0 = 2u * (static_cast<uint32_t>(N1) * j + static_cast<uint32_t>(c0 + 2 * cp));
+          float x[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[e] = ink[dev::accel_index_ii32(af, size, p0 + static_cast<uint32_t>(e), nn - 1)];
+          va[m] = make_float2(x[0], x[1]);
+          vb[m] = make_float2(x[2], x[3]);
+        }
+      }
+    }
+  }
+  dft<P>(va);
+  dft<P>(vb);
+  {
+    // W_L^{g k1}, k1 = 8 a + b: (W_L^{8 g a}) (W_L^{g b}) from the length-L table
+    const float2* twL = tab + to.n2;
+    float2 pb[8];
+    pb[0] = make_float2(1.f, 0.f);
+#pragma unroll
+    for (int b = 1; b < 8; ++b) pb[b] = twL[(gg * b) & (L - 1)];
+#pragma unroll
+    for (int a = 0; a < P / 8; ++a) {
+      const float2 pa = a == 0 ? make_float2(1.f, 0.f) : twL[(gg * 8 * a) & (L - 1)];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        if (a == 0 && b == 0) continue;
+        const float2 wv = a == 0 ? pb[b] : cmul(pa, pb[b]);
+        va[8 * a + b] = cmul(va[8 * a + b], wv);
+        vb[8 * a + b] = cmul(vb[8 * a + b], wv);
+      }
+    }
+  }
+  trace_event(2);
+  // exchange: round r moves g in [r GS, (r + 1) GS); reader pair p of lane
+  // (w, lane) is column c = lane >> 3, k1 = 8 (w + NW p) + (lane & 7)
+  const int rc = (lane >> 3) & 7;
+  float2 u[C::NPAIR][G];
+#pragma unroll
+  for (int r = 0; r < C::ROUNDS; ++r) {
+    float2* buf = lds + (r & 1) * C::BUF;  // rounds alternate buffers: the barrier of round r also
+                                           // retires every read of round r - 1
+    if (gg / C::GS == r) {
+      const int gq = gg - r * C::GS;
+#pragma unroll
+      for (int k1 = 0; k1 < P; ++k1) {
+        float4* d = reinterpret_cast<float4*>(buf + 2 * cp + C::SK * k1 + C::SG * gq);
+        *d = make_float4(va[k1].x, va[k1].y, vb[k1].x, vb[k1].y);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < C::NPAIR; ++p) {
+      const int k1 = 8 * (w + C::NW * p) + (lane & 7);
+      const float2* s = buf + rc + C::SK * k1;
+#pragma unroll
+      for (int q = 0; q < C::GS; ++q) u[p][r * C::GS + q] = s[C::SG * q];
+    }
+  }
+  trace_event(3);
+#pragma unroll
+  for (int p = 0; p < C::NPAIR; ++p) dft<G>(u[p]);
+  trace_event(4);
+  // four-step twiddle W_M^{col k}, k = k1 + P k2: W_M^{col k1} (table pair)
+  // times W_M^{col P k2} (the staged ox rows); tiled store
+  // Y_t[c0 / 8][k / 8][c][k % 8] (one 512-byte block per wave and k2)
+  const uint32_t mask = static_cast<uint32_t>(N1) * L - 1;
+  const uint32_t col = static_cast<uint32_t>(c0 + rc);
+  float2* yk = Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(c0) * L;
+  const float2* twr = tws + rc * (G + 1);
+#pragma unroll
+  for (int p = 0; p < C::NPAIR; ++p) {
+    const uint32_t k1 = static_cast<uint32_t>(8 * (w + C::NW * p) + (lane & 7));
+    const float2 om = twiddle_M((col * k1) & mask, tab + to.lo, tab + to.hi);
+#pragma unroll
+    for (int k2 = 0; k2 < G; ++k2) {
+      const float2 wv = k2 == 0 ? om : cmul(om, twr[k2]);
+      const uint32_t kk = k1 + static_cast<uint32_t>(P * k2);
+      yk[(kk >> 3) * 64 + static_cast<uint32_t>(rc) * 8 + (kk & 7)] = cmul(u[p][k2], wv);
+    }
+  }
+  trace_event(11);
+}
+
 // Pass B.  Logical block = row block * K + trial.
 template <int L, int CPT, int SUB, int MODE>
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::THREADS), amdgpu_waves_per_eu((CPT == 4 ? 4 : 2)))) fft4_rowpass_kernel(
@@ -638,7 +956,11 @@ std::vector<float2> fft4_tables(const Fft4Geom& g) {
   for (int m = 0; m < g.n2; ++m) t[o.n2 + m] = w(m, g.n2);
   for (int m = 0; m < g.n1; ++m) t[o.n1 + m] = w(m, g.n1);
   for (uint64_t m = 0; m < (1u << kSplit); ++m) t[o.lo + m] = w(static_cast<double>(m), M);
-  for (uint64_t m = 0; m < (o.total - o.hi); ++m) t[o.hi + m] = w(static_cast<double>(m << kSplit), M);
+  for (uint64_t m = 0; m < (o.ox - o.hi); ++m) t[o.hi + m] = w(static_cast<double>(m << kSplit), M);
+  const uint64_t GX = static_cast<uint64_t>(onex_g(g.n2)), PX = static_cast<uint64_t>(g.n2) / GX;
+  const uint64_t Mi = static_cast<uint64_t>(g.n1) * static_cast<uint64_t>(g.n2);
+  for (uint64_t col = 0; col < static_cast<uint64_t>(g.n1); ++col)
+    for (uint64_t k2 = 0; k2 < GX; ++k2) t[o.ox + col * GX + k2] = w(static_cast<double>((col * PX * k2) % Mi), M);
   return t;
 }
 
@@ -652,7 +974,7 @@ void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& 
 
 namespace {
 int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4TileY | kFft4TileX | kFft4PairXcd |
-                   kFft4GroupXcd | kFft4UniformTw;  // fastest measured (tools/kbench.py)
+                   kFft4GroupXcd | kFft4UniformTw | kFft4OneX;  // fastest measured (tools/kbench.py, bench A/B)
 
 template <int CPT, int SUB, int MODE>
 void launch_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
@@ -716,7 +1038,27 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 16 == 0, "fft4 colpass: grid");
   PSOUP_CHECK(!(f & kFft4GroupXcd) || (K & 7) != 0 || nblocks % 128 == 0, "fft4 colpass: group grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
-  if ((f & kFft4Blocked) && (f & kFft4TileY) && (f & kFft4Sub2) && !(f & kTimingFlags))
+  if ((f & kFft4OneX) && (f & kFft4Blocked) && (f & kFft4TileY) && !(f & (kTimingFlags | kFft4Sub2)) &&
+      (g.n2 == 512 || g.n2 == 1024 || g.n2 == 2048)) {
+    switch (g.n2) {
+#define PS_ONEX(LL, GG, RR)                                                                                  \
+  case LL:                                                                                                   \
+    fft4_colpass_onex_kernel<LL, GG, RR><<<grid, OneX<LL, GG, RR>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g, \
+                                                                                  tables, f);              \
+    break;
+      PS_ONEX(512, 32, 1) PS_ONEX(1024, 32, 1)
+      case 2048:
+        if (f & kFft4OneXWholeCu)
+          fft4_colpass_onex_kernel<2048, 64, 1><<<grid, OneX<2048, 64, 1>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g,
+                                                                                          tables, f);
+        else
+          fft4_colpass_onex_kernel<2048, 64, 4><<<grid, OneX<2048, 64, 4>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g,
+                                                                                          tables, f);
+        break;
+#undef PS_ONEX
+      default: PSOUP_THROW("fft4: one-exchange column length " << g.n2);
+    }
+  } else if ((f & kFft4Blocked) && (f & kFft4TileY) && (f & kFft4Sub2) && !(f & kTimingFlags))
     launch_colpass<4, 2, kModeBlocked | kModeTileY>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   else if ((f & kFft4Blocked) && (f & kFft4TileY) && (f & kFft4StagedStores) && !(f & kTimingFlags))
     launch_colpass<8, 1, kModeBlocked | kModeTileY | kModeStaged>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);

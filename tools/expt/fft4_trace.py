@@ -13,9 +13,10 @@ from peasoup_amd import _C  # noqa: E402
 
 K_ = _C.kernels
 NAMES = ["start", "loads issued", "stage0", "exch1", "stage1", "exch2", "stage2", "exch3", "stage3", "-", "-", "end"]
+ONEX_NAMES = ["start", "loads issued", "dftP+tw", "exchange", "dftG", "-", "-", "-", "-", "-", "-", "end"]
 
 
-def report(name, ev):
+def report(name, ev, names=NAMES):
     ev = ev.astype(np.int64)
     ok = (ev[:, 0] > 0) & (ev[:, 11] > 0)
     ev = ev[ok]
@@ -25,14 +26,17 @@ def report(name, ev):
           f"mean lifetime {life.mean():.0f} cycles (median {np.median(life):.0f})")
     prev = 0
     for e in range(1, 12):
-        if (ev[:, e] == 0).all() or NAMES[e] == "-":
+        if (ev[:, e] == 0).all() or names[e] == "-":
             continue
         d = ev[:, e] - ev[:, prev]
-        print(f"   {NAMES[prev]:>13s} -> {NAMES[e]:<13s} {d.mean():8.0f} cycles ({100 * d.mean() / life.mean():4.1f}%)")
+        print(f"   {names[prev]:>13s} -> {names[e]:<13s} {d.mean():8.0f} cycles ({100 * d.mean() / life.mean():4.1f}%)")
         prev = e
 
 
 def main():
+    flags = int(sys.argv[1]) if len(sys.argv) > 1 else -1  # fft4 flag set (-1: the default)
+    if flags >= 0:
+        K_.fft4_set_flags(flags)
     dev = torch.device("cuda")
     n = 1 << 23
     M = n // 2
@@ -61,7 +65,8 @@ def main():
         fn()
         torch.cuda.synchronize()
         K_.fft4_set_trace(0)
-        report(name, tr.view(nblk, 12).cpu().numpy())
+        onex = name == "colpass" and (K_.fft4_flags() & 131072) != 0
+        report(name, tr.view(nblk, 12).cpu().numpy(), ONEX_NAMES if onex else NAMES)
 
 
 if __name__ == "__main__":

@@ -83,6 +83,38 @@ __global__ void __launch_bounds__(256) lk(const float* __restrict__ in, float* _
         const f4u w = src[u];
         acc += w.x + w.y + w.z + w.w;
       }
+    } else if (MODE == 11 || MODE == 12) {  // 8 lanes per row (c = t & 7), 8 bytes per lane, rows g + 32 m
+      if (q == 0) {
+        const int c = t & 7, g = t >> 3;
+        const float aff = (200.0f + 1.464f * k) * 64e-6f / (2 * 299792458.0f);
+#pragma unroll
+        for (int m = 0; m < 64; ++m) {
+          const int jj = g + 32 * m;
+          int sh = s;
+          if (MODE == 12) {
+            const float p = 4096.0f * jj + 2.0f * c0;
+            sh = 2048 + (int)rintf(aff * p * (p - 8388608.0f));
+          }
+          const f2u w = *reinterpret_cast<const f2u*>(in + (size_t)jj * PITCH + 2 * (c0 + c) + sh);
+          acc += w.x + w.y;
+        }
+      }
+    } else if (MODE == 13 || MODE == 14) {  // 4 lanes per row (2 columns each), 16 bytes per lane, rows g + 64 m
+      if (q == 0) {
+        const int cp = t & 3, g = t >> 2;
+        const float aff = (200.0f + 1.464f * k) * 64e-6f / (2 * 299792458.0f);
+#pragma unroll
+        for (int m = 0; m < 32; ++m) {
+          const int jj = g + 64 * m;
+          int sh = s;
+          if (MODE == 14) {
+            const float p = 4096.0f * jj + 2.0f * c0;
+            sh = 2048 + (int)rintf(aff * p * (p - 8388608.0f));
+          }
+          const f4u w = *reinterpret_cast<const f4u*>(in + (size_t)jj * PITCH + 2 * c0 + 4 * cp + sh);
+          acc += w.x + w.y + w.z + w.w;
+        }
+      }
     } else if (MODE == 7 || MODE == 8) {  // transposed, realistic per-row shift (varies along j), buffer loads
       // shift of row j for trial k at acceleration 200 + 1.464 k m/s^2 (the parabola, 0..-375 samples)
       const double af = (200.0 + 1.464 * k) * 64e-6 / (2 * 299792458.0);
@@ -146,6 +178,10 @@ int main(int argc, char** argv) {
   time("tshift32", [&] { lk<9><<<grid, 256, lds>>>(in, out, K, 5); });
   time("rowshift32", [&] { lk<10><<<grid, 256, lds>>>(in, out, K, 5); });
   time("tbuf+f64", [&] { lk<6><<<grid, 256, lds>>>(in, out, K, 5); });
+  time("lane8", [&] { lk<11><<<grid, 256, lds>>>(in, out, K, 5); });
+  time("lane8shift", [&] { lk<12><<<grid, 256, lds>>>(in, out, K, 5); });
+  time("lane4x16", [&] { lk<13><<<grid, 256, lds>>>(in, out, K, 5); });
+  time("lane4x16sh", [&] { lk<14><<<grid, 256, lds>>>(in, out, K, 5); });
   time("rows", [&] { lk<0><<<grid, 256, lds>>>(in, out, K, 5); });
   return 0;
 }
