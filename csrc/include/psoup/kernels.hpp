@@ -256,6 +256,7 @@ enum Fft4Flags : int {
   kFft4OneX = 131072,         // pass A (tiled Y, column length 512..2048): 2 columns x L/G points per thread,
                               // one LDS exchange, compile-time twiddles inside the two local DFTs
   kFft4OneXWholeCu = 262144,  // with kFft4OneX at L = 2048: the exchange in one 128 KiB round (one workgroup per CU)
+  kFft4OneXRow = 524288,      // pass B (tiled Y and X, row length 512..2048): the one-exchange structure
 };
 void fft4_set_flags(int flags);
 // Debug: per-workgroup phase timestamps of the fft4 passes (12 x u64 per block), nullptr = off.

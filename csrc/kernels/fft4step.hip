@@ -670,6 +670,65 @@ struct OneX {
   static_assert((NBUF * BUF + TWS) * 8 <= (kWholeCu ? 160 * 1024 : kLdsBudget), "one-exchange LDS budget");
 };
 
+// The part both one-exchange passes share: P-point DFTs of the thread's two
+// transforms, W_L^{g k1} (twL: the length-L table), the exchange, G-point
+// DFTs of the thread's pairs (u[p][k2] = X[k1 + P k2] of pair p).
+template <int L, int G, int R>
+__device__ __forceinline__ void onex_core(float2 (&va)[L / G], float2 (&vb)[L / G], float2 (&u)[2 * (L / G) / G][G],
+                                          float2* __restrict__ lds, const float2* __restrict__ twL, int t) {
+  using C = OneX<L, G, R>;
+  constexpr int P = C::P;
+  const int lane = t & 63, w = t >> 6, cp = t & 3, gg = t >> 2, rc = (lane >> 3) & 7;
+  dft<P>(va);
+  dft<P>(vb);
+  {
+    // W_L^{g k1}, k1 = 8 a + b: (W_L^{8 g a}) (W_L^{g b}) from the length-L table
+    float2 pb[8];
+    pb[0] = make_float2(1.f, 0.f);
+#pragma unroll
+    for (int b = 1; b < 8; ++b) pb[b] = twL[(gg * b) & (L - 1)];
+#pragma unroll
+    for (int a = 0; a < P / 8; ++a) {
+      const float2 pa = a == 0 ? make_float2(1.f, 0.f) : twL[(gg * 8 * a) & (L - 1)];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        if (a == 0 && b == 0) continue;
+        const float2 wv = a == 0 ? pb[b] : cmul(pa, pb[b]);
+        va[8 * a + b] = cmul(va[8 * a + b], wv);
+        vb[8 * a + b] = cmul(vb[8 * a + b], wv);
+      }
+    }
+  }
+  trace_event(2);
+  // exchange: round r moves g in [r GS, (r + 1) GS); reader pair p of lane
+  // (w, lane) is column c = lane >> 3, k1 = 8 (w + NW p) + (lane & 7)
+#pragma unroll
+  for (int r = 0; r < C::ROUNDS; ++r) {
+    float2* buf = lds + (r & 1) * C::BUF;  // rounds alternate buffers: the barrier of round r also
+                                           // retires every read of round r - 1
+    if (gg / C::GS == r) {
+      const int gq = gg - r * C::GS;
+#pragma unroll
+      for (int k1 = 0; k1 < P; ++k1) {
+        float4* d = reinterpret_cast<float4*>(buf + 2 * cp + C::SK * k1 + C::SG * gq);
+        *d = make_float4(va[k1].x, va[k1].y, vb[k1].x, vb[k1].y);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < C::NPAIR; ++p) {
+      const int k1 = 8 * (w + C::NW * p) + (lane & 7);
+      const float2* s = buf + rc + C::SK * k1;
+#pragma unroll
+      for (int q = 0; q < C::GS; ++q) u[p][r * C::GS + q] = s[C::SG * q];
+    }
+  }
+  trace_event(3);
+#pragma unroll
+  for (int p = 0; p < C::NPAIR; ++p) dft<G>(u[p]);
+  trace_event(4);
+}
+
 template <int L, int G, int R>
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, OneX<L, G, R>::THREADS),
                                amdgpu_waves_per_eu(OneX<L, G, R>::kWholeCu ? 1 : 2)))
@@ -765,57 +824,10 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
       }
     }
   }
-  dft<P>(va);
-  dft<P>(vb);
-  {
-    // W_L^{g k1}, k1 = 8 a + b: (W_L^{8 g a}) (W_L^{g b}) from the length-L table
-    const float2* twL = tab + to.n2;
-    float2 pb[8];
-    pb[0] = make_float2(1.f, 0.f);
-#pragma unroll
-    for (int b = 1; b < 8; ++b) pb[b] = twL[(gg * b) & (L - 1)];
-#pragma unroll
-    for (int a = 0; a < P / 8; ++a) {
-      const float2 pa = a == 0 ? make_float2(1.f, 0.f) : twL[(gg * 8 * a) & (L - 1)];
-#pragma unroll
-      for (int b = 0; b < 8; ++b) {
-        if (a == 0 && b == 0) continue;
-        const float2 wv = a == 0 ? pb[b] : cmul(pa, pb[b]);
-        va[8 * a + b] = cmul(va[8 * a + b], wv);
-        vb[8 * a + b] = cmul(vb[8 * a + b], wv);
-      }
-    }
-  }
-  trace_event(2);
-  // exchange: round r moves g in [r GS, (r + 1) GS); reader pair p of lane
-  // (w, lane) is column c = lane >> 3, k1 = 8 (w + NW p) + (lane & 7)
   const int rc = (lane >> 3) & 7;
   float2 u[C::NPAIR][G];
-#pragma unroll
-  for (int r = 0; r < C::ROUNDS; ++r) {
-    float2* buf = lds + (r & 1) * C::BUF;  // rounds alternate buffers: the barrier of round r also
-                                           // retires every read of round r - 1
-    if (gg / C::GS == r) {
-      const int gq = gg - r * C::GS;
-#pragma unroll
-      for (int k1 = 0; k1 < P; ++k1) {
-        float4* d = reinterpret_cast<float4*>(buf + 2 * cp + C::SK * k1 + C::SG * gq);
-        *d = make_float4(va[k1].x, va[k1].y, vb[k1].x, vb[k1].y);
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int p = 0; p < C::NPAIR; ++p) {
-      const int k1 = 8 * (w + C::NW * p) + (lane & 7);
-      const float2* s = buf + rc + C::SK * k1;
-#pragma unroll
-      for (int q = 0; q < C::GS; ++q) u[p][r * C::GS + q] = s[C::SG * q];
-    }
-  }
-  trace_event(3);
-#pragma unroll
-  for (int p = 0; p < C::NPAIR; ++p) dft<G>(u[p]);
-  trace_event(4);
+  onex_core<L, G, R>(va, vb, u, lds, tab + to.n2, t);
+
   // four-step twiddle W_M^{col k}, k = k1 + P k2: W_M^{col k1} (table pair)
   // times W_M^{col P k2} (the staged ox rows); tiled store
   // Y_t[c0 / 8][k / 8][c][k % 8] (one 512-byte block per wave and k2)
@@ -832,6 +844,61 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
       const float2 wv = k2 == 0 ? om : cmul(om, twr[k2]);
       const uint32_t kk = k1 + static_cast<uint32_t>(P * k2);
       yk[(kk >> 3) * 64 + static_cast<uint32_t>(rc) * 8 + (kk & 7)] = cmul(u[p][k2], wv);
+    }
+  }
+  trace_event(11);
+}
+
+// One-exchange pass B (kFft4OneX with tiled Y and X): rows r0 .. r0 + 7 of
+// Y_t, thread (cp, g) loads rows r0 + 2cp, r0 + 2cp + 1 at points i = g + G m
+// (16 bytes per lane; a wave reads two contiguous 512-byte blocks), the same
+// core as pass A, and stores X_t[r0 / 8][k1 / 8][r % 8][k1 % 8] one 512-byte
+// block per wave instruction.  Pruned spectra (keep_oct > 0) take the
+// Stockham kernel: the skip branches cost this one 20-30 spilled VGPRs.
+template <int L, int G, int R>
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, OneX<L, G, R>::THREADS),
+                               amdgpu_waves_per_eu(OneX<L, G, R>::kWholeCu ? 1 : 2)))
+fft4_rowpass_onex_kernel(const float2* __restrict__ Y, float2* __restrict__ X, int K, Fft4Geom g,
+                         const float2* __restrict__ tab, int flags) {
+  using C = OneX<L, G, R>;
+  constexpr int P = C::P;
+  __shared__ __attribute__((aligned(16))) float2 lds[C::NBUF * C::BUF];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int cp = t & 3, gg = t >> 2;
+  trace_event(0);
+  const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
+  const uint32_t nbt = static_cast<uint32_t>(g.n2 / 8);
+  const bool tslow = flags & kFft4TrialSlow;
+  const int k = static_cast<int>(tslow ? lb / nbt : lb % static_cast<uint32_t>(K));
+  const int r0 = static_cast<int>(tslow ? lb % nbt : lb / static_cast<uint32_t>(K)) * 8;
+  const TableOffsets to = table_offsets(L, g.n2);
+  const float2* yk = Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(r0 >> 3) * 64 + 2 * cp;
+  float2 va[P], vb[P];  // rows r0 + 2cp, r0 + 2cp + 1
+  {
+    // 32-bit buffer offsets (a trial's Y is < 2 GiB): one VGPR per address
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(yk), 0, 0x7fffffff, 0x00020000);
+    const uint32_t blk = 8u * static_cast<uint32_t>(g.n2);
+#pragma unroll
+    for (int m = 0; m < P; ++m) {
+      const uint32_t i = static_cast<uint32_t>(gg + G * m);
+      const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i >> 3) * blk + (i & 7) * 8) * 8u, 0, 0));
+      va[m] = make_float2(v.x, v.y);
+      vb[m] = make_float2(v.z, v.w);
+    }
+  }
+  trace_event(1);
+  const int rc = (lane >> 3) & 7;
+  float2 u[C::NPAIR][G];
+  onex_core<L, G, R>(va, vb, u, lds, tab + to.n1, t);
+  float2* xk = X + static_cast<uint64_t>(k) * g.xstride + static_cast<uint64_t>(r0) * L;
+#pragma unroll
+  for (int p = 0; p < C::NPAIR; ++p) {
+    const uint32_t k1 = static_cast<uint32_t>(8 * (w + C::NW * p) + (lane & 7));
+#pragma unroll
+    for (int k2 = 0; k2 < G; ++k2) {
+      const uint32_t kk = k1 + static_cast<uint32_t>(P * k2);
+      xk[(kk >> 3) * 64 + static_cast<uint32_t>(rc) * 8 + (kk & 7)] = u[p][k2];
     }
   }
   trace_event(11);
@@ -1094,7 +1161,18 @@ void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const fl
       const uint32_t ny = r2c_tiled_row_blocks(nbins_out, g.n1, g.n2);
       if (2 * (ny + 1) < static_cast<uint32_t>(g.n1 / 8)) keep = ny + 1;
     }
-    if (f & kFft4Sub2)
+    if ((f & kFft4OneXRow) && keep == 0 && !(f & (kFft4Sub2 | kFft4StagedStores)) &&
+        (g.n1 == 512 || g.n1 == 1024 || g.n1 == 2048)) {
+      switch (g.n1) {
+#define PS_ONEXR(LL, GG, RR)                                                                              \
+  case LL:                                                                                                \
+    fft4_rowpass_onex_kernel<LL, GG, RR><<<grid, OneX<LL, GG, RR>::THREADS, 0, s>>>(Y, X, K, g, tables, f);       \
+    break;
+        PS_ONEXR(512, 32, 1) PS_ONEXR(1024, 32, 1) PS_ONEXR(2048, 64, 4)
+#undef PS_ONEXR
+        default: PSOUP_THROW("fft4: one-exchange row length " << g.n1);
+      }
+    } else if (f & kFft4Sub2)
       launch_rowpass<4, 2, kModeBlocked | kModeTileY | kModeTileX>(Y, X, K, g, tables, grid, f, s, keep);
     else if (f & kFft4StagedStores)
       launch_rowpass<8, 1, kModeBlocked | kModeTileY | kModeTileX | kModeStaged>(Y, X, K, g, tables, grid, f, s,

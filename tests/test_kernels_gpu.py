@@ -250,7 +250,7 @@ def test_r2c_interbin_normalise_batch():
         assert np.allclose(P[k], exp, rtol=1e-4, atol=2e-3), np.abs(P[k] - exp).max()
 
 
-FFT4_FLAG_SETS = [None, 0, 1, 259, 274, 1299, 3331, 7427, 15619, 32003, 48387, 81155, 474371]  # None = default (212227: tiled Y and X + uniform pass-A twiddles + one-exchange pass A); 81155 = the Stockham pass A; 32003 = + Sub2; 474371 = + whole-CU exchange
+FFT4_FLAG_SETS = [None, 0, 1, 259, 274, 1299, 3331, 7427, 15619, 32003, 48387, 81155, 474371, 736515]  # None = default (212227: tiled Y and X + uniform pass-A twiddles + one-exchange pass A); 81155 = the Stockham pass A; 32003 = + Sub2; 474371 = + whole-CU exchange; 736515 = + one-exchange pass B
 
 
 @pytest.fixture(params=FFT4_FLAG_SETS)
@@ -269,7 +269,7 @@ def test_fft4_resample_spectrum_matches_numpy(log2n, fft4_flags):
     """Fused resample + four-step FFT vs (bit-exact GPU resample) + numpy fp64 FFT."""
     from peasoup_amd import ops
 
-    if log2n >= 23 and fft4_flags not in (None, 81155, 474371):
+    if log2n >= 23 and fft4_flags not in (None, 81155, 474371, 736515):
         pytest.skip("2^23 and 2^25 checked with the default kernel shape (and the one-exchange pass A) only")
 
     rng = np.random.default_rng(log2n)
