@@ -119,7 +119,9 @@ def main() -> int:
 
     shard = range(ctx.rank * a.dms_per_gpu, (ctx.rank + 1) * a.dms_per_gpu)
     trials_per_step_local = sum(len(rs.accel_list(rs.dm_list[d])) for d in shard)
-    trials_per_step = trials_per_step_local * ctx.world_size  # identical shards sizes
+    # exact job total: the plan's trial count shrinks slightly with DM (smearing term)
+    tot = torch.tensor([trials_per_step_local], dtype=torch.int64, device=dev)
+    trials_per_step = int(pdist.all_reduce_sum(tot).item())
 
     def step():
         local = rs.search(shard, chunk=a.dms_per_gpu)

@@ -276,9 +276,9 @@ __device__ __forceinline__ void emit(bool pred, uint32_t seg, int idx, float snr
 // neighbouring tiles need overlapping ranges), then every thread sums its
 // bins from LDS.  Even numerators repeat the previous level's terms and
 // are not re-read (as in the reference recurrence).
-template <int NLEV>
+template <int NLEV, int BPT_ = 0>
 struct HarmTile {
-  static constexpr int BPT = NLEV <= 3 ? 8 : (NLEV == 4 ? 4 : 2);
+  static constexpr int BPT = BPT_ > 0 ? BPT_ : (NLEV <= 3 ? 8 : (NLEV == 4 ? 4 : 2));
   static constexpr int B = 256 * BPT;
   static constexpr int NREG = 1 << NLEV;  // (fundamental) + sum_{h=1..NLEV} 2^(h-1) gather ranges
   static constexpr int maxlen(int h, int m) { return h == 0 ? B : (((B - 1) * m) >> h) + 2; }
@@ -318,18 +318,18 @@ struct HarmPre {
   float lo[6];
 };
 
-template <int NLEV>
+template <int NLEV, int BPT_ = 0>
 __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __restrict__ P, uint64_t pstride,
                                                              int lo, int hi, HarmParams hp,
                                                              PeakRecord* __restrict__ out,
                                                              uint32_t* __restrict__ count, int ntiles,
                                                              int xcd_trials, HarmPre pre) {
-  using Tl = HarmTile<NLEV>;
+  using Tl = HarmTile<NLEV, BPT_>;
   constexpr int B = Tl::B;
   __shared__ __attribute__((aligned(16))) float lds[Tl::TOTAL];
   const uint32_t bid = blockIdx.x;
   int k, tile;
-  if (xcd_trials) {
+  if (xcd_trials & 1) {
     const uint32_t slot = bid >> 3;
     k = static_cast<int>((slot / ntiles) * 8 + (bid & 7u));
     tile = static_cast<int>(slot % ntiles);
@@ -343,8 +343,13 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
   const int last = hi - 1;
   // ---- fundamental straight into registers (coalesced)
   float fund[Tl::BPT];
+  if (xcd_trials & 2) {  // tuning: streaming (nontemporal) fundamental loads
 #pragma unroll
-  for (int u = 0; u < Tl::BPT; ++u) fund[u] = p[min(b0 + t + 256 * u, last)];
+    for (int u = 0; u < Tl::BPT; ++u) fund[u] = __builtin_nontemporal_load(p + min(b0 + t + 256 * u, last));
+  } else {
+#pragma unroll
+    for (int u = 0; u < Tl::BPT; ++u) fund[u] = p[min(b0 + t + 256 * u, last)];
+  }
   // ---- stage every gather range in 16-byte chunks: all loads are issued
   // before the first LDS store (fixed trip counts).  Only values at indices
   // < hi are ever used; chunks reaching past `last` are gathered per element.
@@ -638,7 +643,12 @@ void fft4_c2r_post(const float2* Z, uint64_t M, const XLayoutArgs& L, float* x, 
 }
 
 namespace {
-int g_harm_flags = 1;  // bit 0: XCD-per-trial block order
+// bit 0: XCD-per-trial block order; bit 1: no pre-threshold (testing);
+// bit 2: nontemporal fundamental loads (tuning); bit 3: 1024-bin tiles at
+// 3 levels (tuning); bits 8-15: extra dynamic LDS
+// per workgroup in KiB (tuning: caps workgroups per CU, so fewer tiles -- a
+// smaller gather footprint -- are in flight per XCD)
+int g_harm_flags = 1;
 }  // namespace
 void harmonic_set_flags(int flags) { g_harm_flags = flags; }
 
@@ -656,7 +666,8 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
   PSOUP_CHECK(hi <= static_cast<int>(nbins), "search range beyond spectrum");
   if (hi <= lo) return;
   PSOUP_CHECK(static_cast<int64_t>(hi) * 32 < (int64_t(1) << 31), "spectrum too long for the int32 gather math");
-  const int xcd = (g_harm_flags & 1) && (K % 8 == 0);
+  const int xcd = ((g_harm_flags & 1) && (K % 8 == 0) ? 1 : 0) | ((g_harm_flags & 4) ? 2 : 0);
+  const size_t dyn_lds = static_cast<size_t>((g_harm_flags >> 8) & 0xff) * 1024;
   HarmPre pre;
   {
     static const double scale[6] = {1.0, 0.70710678118654752440, 0.5, 0.35355339059327376220, 0.25,
@@ -673,17 +684,27 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
   }
   auto ntiles_of = [&](int B) { return (hi - lo + B - 1) / B; };
   switch (hp.nlevels) {
-#define PS_CASE(NL)                                                                                           \
-  case NL: {                                                                                                  \
-    const int nt = ntiles_of(HarmTile<NL>::B);                                                                \
+#define PS_LAUNCH(NL, BP)                                                                                   \
+  {                                                                                                           \
+    const int nt = ntiles_of(HarmTile<NL, BP>::B);                                                            \
     PSOUP_CHECK(static_cast<int64_t>(nt) * K < (int64_t(1) << 31), "harmonic grid too large");               \
-    harmonic_peaks_kernel<NL><<<dim3(static_cast<unsigned>(nt * K)), 256, 0, s>>>(P, pstride, lo, hi, hp, out,  \
-                                                                                  count, nt, xcd, pre);        \
-    break;                                                                                                    \
+    harmonic_peaks_kernel<NL, BP><<<dim3(static_cast<unsigned>(nt * K)), 256, dyn_lds, s>>>(                  \
+        P, pstride, lo, hi, hp, out, count, nt, xcd, pre);                                                    \
   }
-    PS_CASE(0) PS_CASE(1) PS_CASE(2) PS_CASE(3) PS_CASE(4)
+#define PS_CASE(NL)    \
+  case NL:             \
+    PS_LAUNCH(NL, 0)   \
+    break;
+    case 3:
+      if (g_harm_flags & 8)  // tuning: 1024-bin tiles (half the LDS and registers per workgroup)
+        PS_LAUNCH(3, 4)
+      else
+        PS_LAUNCH(3, 0)
+      break;
+    PS_CASE(0) PS_CASE(1) PS_CASE(2) PS_CASE(4)
     default:
       PS_CASE(5)
+#undef PS_LAUNCH
 #undef PS_CASE
   }
   post_launch_check("harmonic_peaks_kernel", s);
