@@ -348,6 +348,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("dedisp_kernel", &CmdLineOptions::dedisp_kernel)
       .def_readwrite("accel_batch", &CmdLineOptions::accel_batch)
       .def_readwrite("engines_per_gpu", &CmdLineOptions::engines_per_gpu)
+      .def_readwrite("dm_schedule", &CmdLineOptions::dm_schedule)
       .def_readwrite("sub_batch", &CmdLineOptions::sub_batch)
       .def_readwrite("fft_mode", &CmdLineOptions::fft_mode)
       .def_readwrite("use_boundaries", &CmdLineOptions::use_boundaries)

@@ -232,6 +232,11 @@ static std::vector<Spec> peasoup_specs(CmdLineOptions& a) {
             "Search engines per GPU, each on its own stream and host thread, dealt every N-th DM of a chunk "
             "(0 = auto: Python driver 3 when DMs have < 128 acceleration trials, else 1; native pipeline 1)",
             a.engines_per_gpu),
+      val_s("", "dm_schedule",
+            "Multi-rank DM distribution (python -m peasoup_amd under torchrun): dynamic = ranks claim DM chunks "
+            "from a shared first-come queue, like the reference's DMDispenser; static = contiguous shards balanced "
+            "by acceleration-trial count; auto = dynamic",
+            a.dm_schedule),
       val_n("", "sub_batch", "Fused-FFT trials per sub-batch on two alternating streams (0 = off, -1 = auto)",
             a.sub_batch),
       val_n("", "fft_mode", "Accel-trial FFT: 2 = fused resample + four-step FFT (default), 1 = rocFFT C2C(N/2), 0 = rocFFT R2C",

@@ -6,10 +6,15 @@ Flow per rank (SURVEY.md §7.1 distribution model):
    an RCCL broadcast over xGMI replicates them (``broadcast_bytes``), and
    every rank unpacks them into a channel-major int8 filterbank resident in
    HBM (``DeviceFilterbank``).
-2. each rank owns a contiguous DM shard balanced by acceleration-trial count
-   (``shard_range``); it dedisperses chunks of that shard on the MFMA
-   dedispersion kernel straight into HBM and runs the native
-   ``SearchEngine`` (whitening + batched acceleration search) on each trial.
+2. ranks take 32-DM chunks first-come from a queue they share
+   (``--dm_schedule dynamic``, the default for several ranks: the reference's
+   DMDispenser, made cross-process with an atomic counter in the process
+   group's key-value store, ``pdist.WorkQueue``), or each owns a contiguous
+   DM shard balanced by acceleration-trial count (``static``,
+   ``shard_range``); a rank dedisperses its chunks straight into HBM and runs
+   the native ``SearchEngine`` (whitening + batched acceleration search) on
+   each trial.  Any rank can take any chunk: every rank holds the whole
+   filterbank.
 3. per-rank candidate trees are serialised and gathered to rank 0 over RCCL
    (``gather_bytes``); rank 0 runs the global DM / harmonic distillation and
    scoring.
@@ -31,7 +36,7 @@ import threading
 import time
 import warnings
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Callable, Dict, List, Optional, Sequence
 
 import torch
 
@@ -156,18 +161,33 @@ class RankSearcher:
             d0 = d1
         return out
 
-    def search(self, dm_indices: Sequence[int], chunk: int = 32, timers: Optional[Dict[str, Stopwatch]] = None,
-               progress=None) -> list:
-        """Dedisperse + search ``dm_indices`` chunk by chunk.  Chunk k+1 is
-        dedispersed on a side stream into the other half of a double buffer
-        while chunk k is searched (the reference dedisperses the whole DM
-        list up front, pipeline.cu:325-359); the search stream waits on an
-        event, never the host.  ``timers['dedispersion']`` accumulates the
-        dedispersion kernels' GPU time (overlapped), ``timers['searching']``
-        the wall time of the search loop."""
+    def search(self, dm_indices: Optional[Sequence[int]] = None, chunk: int = 32,
+               timers: Optional[Dict[str, Stopwatch]] = None, progress=None,
+               blocks: Optional[List[tuple]] = None, claim: Optional[Callable[[], Optional[int]]] = None) -> list:
+        """Dedisperse + search DM blocks.  Chunk k+1 is dedispersed on a side
+        stream into the other half of a double buffer while chunk k is
+        searched (the reference dedisperses the whole DM list up front,
+        pipeline.cu:325-359); the search stream waits on an event, never the
+        host.  ``timers['dedispersion']`` accumulates the dedispersion
+        kernels' GPU time (overlapped), ``timers['searching']`` the wall time
+        of the search loop.
+
+        The blocks are ``dm_indices`` cut into ``chunk``-aligned pieces, or
+        ``blocks`` as given; with ``claim`` (a callable returning the next
+        block index or None, e.g. ``pdist.WorkQueue.claim``) the blocks are
+        taken first-come from a queue shared with the other ranks -- one block
+        ahead, so the next block's dedispersion still overlaps this one's
+        search -- instead of in order.  Candidates come back in processing
+        order; every block's candidates are contiguous."""
         tile = int(_C.Dedisperser.tile_dms)
         chunk = max(tile, (int(chunk) + tile - 1) // tile * tile)
-        blocks = self.chunk_ranges(dm_indices, chunk)
+        if blocks is None:
+            blocks = self.chunk_ranges(dm_indices, chunk)
+        blocks = [tuple(b) for b in blocks]
+        width = max((d1 - d0 for d0, d1 in blocks), default=0)
+        if claim is None:
+            order = iter(range(len(blocks)))
+            claim = lambda: next(order, None)  # noqa: E731
         cands: list = []
         t_dd = timers.get("dedispersion") if timers else None
         t_s = timers.get("searching") if timers else None
@@ -175,30 +195,36 @@ class RankSearcher:
         ckdir = getattr(self.args, "checkpoint_dir", "") or ""
         fault_after = int(getattr(self.args, "fault_after_dms", -1))
         processed = 0
-        ck_of = [_C.spill_path(ckdir, d0, d1) if ckdir else "" for d0, d1 in blocks]
-        resumed: Dict[int, list] = {}
         ckey = 0
         if ckdir:
             # spills are bound to this run's identity (input, header, options):
             # a spill of another run, or a corrupt/truncated one, is recomputed
             ckey = _C.prepare_checkpoint_dir(ckdir, self.args, self.header)
-            for i, ck in enumerate(ck_of):
-                status, got = _C.load_spill(ck, ckey)
-                if status == "loaded":
-                    resumed[i] = got
-                elif status != "missing":
-                    warnings.warn(f"checkpoint spill {ck} is {status}; recomputing DMs {blocks[i]}")
-        todo = [i for i in range(len(blocks)) if i not in resumed]
         dev = self.ctx.device
         side = _C.GpuStream()
-        nbuf = min(2, len(todo))
-        bufs = [torch.empty(chunk * self.row_stride, dtype=torch.uint8, device=dev) for _ in range(nbuf)]
-        freed = [None] * nbuf      # event: search stream finished with the buffer
-        issued = {}                # block index -> (buffer, ready event, start event)
+        bufs: List[torch.Tensor] = []  # double buffer, allocated on first use
+        freed = [None, None]           # event: search stream finished with the buffer
+        nissued = [0]
+        self.blocks_done = []
 
-        def issue(j: int) -> None:
-            k = len(issued) % nbuf
+        def pull():
+            """Next block: (index, spill path, resumed candidates or None,
+            (buffer, ready event, start event) or None); None when the queue is dry."""
+            j = claim()
+            if j is None:
+                return None
             d0, d1 = blocks[j]
+            ck = _C.spill_path(ckdir, d0, d1) if ckdir else ""
+            if ck:
+                status, got = _C.load_spill(ck, ckey)
+                if status == "loaded":
+                    return j, ck, got, None
+                if status != "missing":
+                    warnings.warn(f"checkpoint spill {ck} is {status}; recomputing DMs {(d0, d1)}")
+            k = nissued[0] % 2
+            nissued[0] += 1
+            if k >= len(bufs):
+                bufs.append(torch.empty(width * self.row_stride, dtype=torch.uint8, device=dev))
             start, ready = _C.GpuEvent(True), _C.GpuEvent(True)
             for ev in freed[k] or ():
                 ev.wait(side.handle)
@@ -208,29 +234,27 @@ class RankSearcher:
             ready.record(side.handle)
             if _SYNC_DEDISP:
                 ready.synchronize()
-            issued[j] = (k, ready, start)
+            return j, ck, None, (k, ready, start)
 
         dd_events = []
         lock = threading.Lock()
-        if todo:
-            issue(todo[0])
         if t_s:
             t_s.start()
-        nxt = 1  # next entry of todo to dedisperse
-        for i in range(len(blocks)):
-            d0, d1 = blocks[i]
-            ck = ck_of[i]
-            if i not in issued:
+        cur = pull()
+        while cur is not None:
+            j, ck, resumed, inflight = cur
+            d0, d1 = blocks[j]
+            self.blocks_done.append(j)
+            if resumed is not None:
                 # resume: same spill format as the native pipeline (keyed CandidatePOD trees)
-                cands.extend(resumed.pop(i))
+                cands.extend(resumed)
                 ntrials += sum(len(self.accel_list(self.dm_list[d])) for d in range(d0, d1))
                 if progress is not None:
                     progress(d1 - d0)
+                cur = pull()
                 continue
-            k, ready, start = issued[i]
-            if nxt < len(todo):
-                issue(todo[nxt])  # overlaps the search below
-                nxt += 1
+            k, ready, start = inflight
+            nxt = pull()  # its dedispersion overlaps the search below
             for e in self.engines:
                 ready.wait(e.stream)
             dd_events.append((start, ready))
@@ -264,8 +288,8 @@ class RankSearcher:
             if ne == 1:
                 run_dms(self.engine, range(d0, d1))
             else:
-                futs = [self._executor().submit(run_dms, e, range(d0 + j, d1, ne))
-                        for j, e in enumerate(self.engines)]
+                futs = [self._executor().submit(run_dms, e, range(d0 + i, d1, ne))
+                        for i, e in enumerate(self.engines)]
                 for f in futs:
                     f.result()
             chunk_cands: list = []
@@ -280,6 +304,7 @@ class RankSearcher:
             if ck:
                 _C.save_spill(ck, ckey, chunk_cands)  # atomic; raises on a failed write
             cands.extend(chunk_cands)
+            cur = nxt
         side.synchronize()
         for e in self.engines:
             _C.stream_synchronize(e.stream)
@@ -374,6 +399,21 @@ def load_packed_for_rank(infilename: str, ctx: pdist.DistContext):
     return header, packed, nsamps
 
 
+DYNAMIC_CHUNK = 32  # DMs per claimed block (the dedispersion tile multiple the static path also uses)
+
+
+def dm_schedule(args, world_size: int) -> str:
+    """``--dm_schedule``: "dynamic" (first-come DM chunks from a queue shared
+    by the ranks), "static" (contiguous trial-weighted shards); auto = dynamic
+    for more than one rank."""
+    s = (getattr(args, "dm_schedule", "auto") or "auto").lower()
+    if s not in ("auto", "dynamic", "static"):
+        raise ValueError(f"--dm_schedule must be dynamic, static or auto, not {s!r}")
+    if world_size <= 1:
+        return "static"
+    return "dynamic" if s == "auto" else s
+
+
 def run_search(args, write: bool = True) -> Optional[SearchResult]:
     """Full distributed search (torchrun: one rank per GPU).  Returns the
     result on rank 0 (None elsewhere)."""
@@ -388,15 +428,25 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     del packed
     ndm = len(rs.dm_list)
     weights = [len(rs.accel_list(d)) for d in rs.dm_list]
-    shard = pdist.shard_range(ndm, ctx.world_size, ctx.rank, weights)
+    schedule = dm_schedule(args, ctx.world_size)
     pdist.barrier()
     t0 = time.perf_counter()
-    local = rs.search(shard, timers=timers)
+    if schedule == "dynamic":
+        # DMDispenser across processes: every rank claims 32-DM chunks of the
+        # whole list from one shared first-come queue (pipeline_multi.cu:33-81)
+        blocks = rs.chunk_ranges(range(ndm), DYNAMIC_CHUNK)
+        queue = pdist.WorkQueue("dm_chunks", len(blocks))
+        local = rs.search(blocks=blocks, claim=queue.claim, timers=timers)
+        local_trials = sum(weights[d] for j in rs.blocks_done for d in range(*blocks[j]))
+    else:
+        shard = pdist.shard_range(ndm, ctx.world_size, ctx.rank, weights)
+        local = rs.search(shard, timers=timers)
+        local_trials = sum(weights[i] for i in shard)
     torch.cuda.synchronize()
     search_wall = time.perf_counter() - t0
-    local_trials = sum(weights[i] for i in shard)
     rank_stats = rs.counters()
     rank_stats.update({"rank": ctx.rank, "search_s": search_wall, "accel_trials_planned": local_trials,
+                       "dm_schedule": schedule, "dm_blocks": len(rs.blocks_done),
                        "fft_mode": rs.engine.fft_mode, "accel_batch": rs.engine.batch_size,
                        "sub_batch": rs.engine.sub_batch,
                        "dedispersion_s": timers["dedispersion"].get_time(), "searching_s": timers["searching"].get_time()})

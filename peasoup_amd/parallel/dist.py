@@ -222,3 +222,49 @@ def shard_range(n: int, world: int, rank: int, weights: Optional[Sequence[float]
         cuts.append(n)
     cuts.append(n)
     return range(cuts[rank], cuts[rank + 1])
+
+
+_QUEUE_SEQ: dict = {}
+
+
+class WorkQueue:
+    """First-come work queue shared by every rank: ``claim()`` hands out the
+    indices ``0 .. n-1``, each to exactly one rank, then ``None``.
+
+    The cross-process form of the reference's ``DMDispenser``
+    (src/pipeline_multi.cu:33-81: a mutex-guarded "next DM" counter read by one
+    pthread per GPU).  Here the counter is an atomic ``add`` on the
+    process group's host-side key-value store (the c10d TCPStore torchrun set
+    up), so claiming a DM chunk costs one small TCP round trip to rank 0's
+    store and no GPU collective; fast ranks simply claim more chunks.
+
+    Every rank must create its queues in the same order (the key is
+    ``name`` plus a per-name sequence number, so a queue re-created by a later
+    step starts from zero).  Without a process group the queue is a local
+    counter.
+    """
+
+    def __init__(self, name: str, n: int):
+        self.n = int(n)
+        seq = _QUEUE_SEQ.get(name, 0)
+        _QUEUE_SEQ[name] = seq + 1
+        self.key = f"psoup/queue/{name}/{seq}"
+        self._local = 0
+        self._store = None
+        ctx = context()
+        if ctx.distributed:
+            from torch.distributed import distributed_c10d
+
+            self._store = distributed_c10d._get_default_store()
+        self.claimed: List[int] = []
+
+    def claim(self) -> Optional[int]:
+        if self._store is not None:
+            i = int(self._store.add(self.key, 1)) - 1
+        else:
+            i = self._local
+            self._local += 1
+        if i >= self.n:
+            return None
+        self.claimed.append(i)
+        return i

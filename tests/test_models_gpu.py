@@ -91,20 +91,23 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_multi_rank_search_equals_single_rank(tmp_path, world):
-    """DM sharding + RCCL-style gather + distributed folding reproduce the
-    single-process result (gloo transport, all ranks on one GPU)."""
+@pytest.mark.parametrize("world,schedule", [(2, "static"), (4, "static"), (2, "dynamic"), (3, "dynamic")])
+def test_multi_rank_search_equals_single_rank(tmp_path, world, schedule):
+    """DM distribution (static trial-weighted shards, or first-come chunks from
+    the shared pdist.WorkQueue) + RCCL-style gather + distributed folding
+    reproduce the single-process result (gloo transport, all ranks on one GPU)."""
     port = _free_port()
+    dm_end = "120" if schedule == "static" else "250"  # dynamic: 59 DMs = two 32-DM chunks, 3 ranks (one idle)
     script = (
         "import os,sys; sys.path.insert(0, %r)\n"
         "from peasoup_amd.parallel import dist as pdist\n"
         "pdist.init(backend='gloo')\n"
         "from peasoup_amd import _C\n"
         "from peasoup_amd.models.search import run_search\n"
-        "ok,_,a=_C.parse_cmdline(['peasoup','-i',%r,'-o',sys.argv[1],'--dm_end','120','-n','4','--npdmp','4'])\n"
+        "ok,_,a=_C.parse_cmdline(['peasoup','-i',%r,'-o',sys.argv[1],'--dm_end',%r,'-n','4','--npdmp','4',"
+        "'--dm_schedule',%r,'--trace_json',sys.argv[1]+'.json'])\n"
         "run_search(a)\n"
-        "pdist.shutdown()\n" % (REPO, TUTORIAL))
+        "pdist.shutdown()\n" % (REPO, TUTORIAL, dm_end, schedule))
     f = tmp_path / "run.py"
     f.write_text(script)
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world))
@@ -123,6 +126,12 @@ def test_multi_rank_search_equals_single_rank(tmp_path, world):
     a = open(tmp_path / "dist" / "candidates.peasoup", "rb").read()
     b = open(tmp_path / "single" / "candidates.peasoup", "rb").read()
     assert a == b
+    import json
+
+    devs = json.load(open(str(tmp_path / "dist") + ".json"))["devices"]
+    assert [d["dm_schedule"] for d in devs] == [schedule] * world
+    if schedule == "dynamic":  # every 32-DM chunk searched exactly once, by some rank
+        assert sum(d["dm_blocks"] for d in devs) == 2
 
 
 def test_time_shard_native_windows_match_whole(C):

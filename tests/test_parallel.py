@@ -76,6 +76,64 @@ def test_gloo_collectives(world):
         assert out[r]["max"] == float(world - 1)
 
 
+def _queue_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    try:
+        import time
+
+        pdist.init(backend="gloo")
+        res = {}
+        # two queues created in the same order on every rank: independent counters
+        for name, n in (("dm", 40), ("dm", 7), ("other", 0)):
+            wq = pdist.WorkQueue(name, n)
+            mine = []
+            while True:
+                i = wq.claim()
+                if i is None:
+                    break
+                mine.append(i)
+                if rank == 0:
+                    time.sleep(0.01)  # a slow rank: the others claim more
+            res[f"{name}/{n}"] = mine
+            pdist.barrier()
+        q.put((rank, res))
+        pdist.shutdown()
+    except Exception:  # pragma: no cover
+        import traceback
+
+        q.put((rank, {"error": traceback.format_exc()}))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_work_queue_hands_out_each_index_once(world):
+    """pdist.WorkQueue (the cross-rank DMDispenser): every index goes to
+    exactly one rank, in increasing order per rank, and a slow rank gets fewer."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_queue_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = dict(q.get(timeout=240) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        assert "error" not in out[r], out[r].get("error")
+    for key, n in (("dm/40", 40), ("dm/7", 7), ("other/0", 0)):
+        got = [i for r in range(world) for i in out[r][key]]
+        assert sorted(got) == list(range(n)), key
+        for r in range(world):
+            assert out[r][key] == sorted(out[r][key])
+    assert len(out[0]["dm/40"]) < 40 // world
+
+
+def test_work_queue_without_process_group():
+    wq = pdist.WorkQueue("local-test", 3)
+    assert [wq.claim() for _ in range(5)] == [0, 1, 2, None, None]
+    assert wq.claimed == [0, 1, 2]
+
+
 @pytest.mark.parametrize("world", [1, 2, 3, 8])
 def test_shard_range_partitions(world):
     n = 59
