@@ -56,6 +56,8 @@ def parse():
                    help="2: fused resample + four-step FFT; 1: rocFFT C2C(N/2) + fused r2c post; 0: rocFFT R2C")
     p.add_argument("--dedisp-kernel", default="auto", choices=["auto", "mfma", "valu", "direct"])
     p.add_argument("--fft4-flags", type=int, default=-1, help="fused-FFT kernel variant flags (tuning; -1 = default)")
+    p.add_argument("--harm-flags", type=int, default=-1,
+                   help="harmonic-sum / tiled-r2c kernel variant flags (tuning; -1 = default)")
     p.add_argument("--seed", type=int, default=1234)
     return p.parse_args()
 
@@ -74,6 +76,8 @@ def main() -> int:
     dev = ctx.device
     if a.fft4_flags >= 0:
         _C.kernels.fft4_set_flags(a.fft4_flags)
+    if a.harm_flags >= 0:
+        _C.kernels.harmonic_set_flags(a.harm_flags)
     assert dev.type == "cuda", "bench.py needs a GPU"
 
     n = 1 << a.log2n

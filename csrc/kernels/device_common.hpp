@@ -107,12 +107,14 @@ __device__ __forceinline__ float amplitude(float2 x) {
 }
 
 // Interbinned amplitude, bin_interbin_series_kernel semantics.
+// The fused multiply-adds are explicit so every kernel that forms it (LDS or
+// register neighbours) rounds identically whatever the compiler contracts.
 __device__ __forceinline__ float interbin(float2 x, float2 xl) {
-  float ampsq = x.x * x.x + x.y * x.y;
+  float ampsq = __builtin_fmaf(x.x, x.x, x.y * x.y);
   float dre = x.x - xl.x, dim = x.y - xl.y;
   // 0.5 * (double) then rounding to float == the float product by 0.5f:
   // scaling by a power of two is exact (denormals are kept in both)
-  float ampsq_diff = (dre * dre + dim * dim) * 0.5f;
+  float ampsq_diff = __builtin_fmaf(dre, dre, dim * dim) * 0.5f;
   return sqrtf(fmaxf(ampsq, ampsq_diff));
 }
 

@@ -56,7 +56,8 @@ __device__ __forceinline__ float2 r2c_combine(float2 za, float2 zb, float c, flo
   const float ex = 0.5f * (za.x + zb.x), ey = 0.5f * (za.y - zb.y);
   const float dx = 0.5f * (za.x - zb.x), dy = 0.5f * (za.y + zb.y);
   const float ox = dy, oy = -dx;  // -i * d
-  return make_float2(ex + c * ox - s * oy, ey + c * oy + s * ox);
+  // explicit FMAs: identical rounding in every kernel that uses it
+  return make_float2(__builtin_fmaf(-s, oy, __builtin_fmaf(c, ox, ex)), __builtin_fmaf(s, ox, __builtin_fmaf(c, oy, ey)));
 }
 
 // Address of bin k = k2 + 2^log2_row * k1 in a (possibly blocked) layout:
@@ -216,7 +217,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* _
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const float ws = rtw.s[r], wc = rtw.c[r];  // W^(r n2)
-      const float c = cs * wc - sn * ws, sv = cs * ws + sn * wc;
+      const float c = __builtin_fmaf(cs, wc, -(sn * ws)), sv = __builtin_fmaf(cs, ws, sn * wc);
       A[r][t + 1] = r2c_combine(za[r], zb[r], c, sv);
       D[r][t + 1] = r2c_combine(zb[r], za[r], -c, sv);
     }
@@ -249,6 +250,107 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* _
     xbin(half, xa, xm);
     xbin(half - 1, la, lm);
     p[half] = (dev::interbin(xa, la) - mean) / sigma;
+  }
+}
+
+// Same tile, neighbours by cross-lane shuffles instead of two 16.5 KiB LDS
+// planes: lane l's left neighbour X[k-1] is lane l-1's ascending bin and its
+// mirror neighbour X[M-(k+1)] is lane l+1's mirrored bin; only the values
+// crossing a wave edge (and the tile's two halo columns) go through 640 bytes
+// of LDS.  Occupancy is then set by registers, not LDS (4 -> 8 workgroups/CU).
+__global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
+    const float2* __restrict__ Z, int log2_n2, uint64_t n1, uint64_t zstride, float* __restrict__ P,
+    uint64_t pstride, uint64_t nbins_out, const float* __restrict__ stats, float nscale, RowTw8 rtw,
+    const uint32_t* __restrict__ tsrc) {
+  __shared__ float2 eA[5][8];  // eA[w][r]: X left of wave w's lane 0 (w = 0: the tile's halo column c0 - 1)
+  __shared__ float2 eD[5][8];  // eD[w][r]: mirror X of wave w's lane 0 (w = 4: the halo column c0 + 256)
+  const uint64_t n2 = uint64_t(1) << log2_n2;
+  const uint64_t M = n1 * n2, half = M / 2;
+  const int kk = blockIdx.z;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const float2* z = Z + static_cast<uint64_t>(kk) * zstride;
+  float* p = P + static_cast<uint64_t>(kk) * pstride;
+  if (tsrc) stats += 4 * tsrc[kk];
+  const float mean = stats[0] * nscale;
+  const float sigma = stats[2] * nscale;
+  const uint64_t g0 = static_cast<uint64_t>(blockIdx.y) * 8;
+  const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * 256;
+  auto xbin = [&](uint64_t k, float2& xa, float2& xm) {  // generic: X[k] and X[M-k]
+    const float2 za = z[taddr(k & (M - 1), log2_n2, n1)];
+    const float2 zb = z[taddr((M - k) & (M - 1), log2_n2, n1)];
+    float sn, cs;
+    sincospif(-static_cast<float>(k) / static_cast<float>(M), &sn, &cs);
+    xa = r2c_combine(za, zb, cs, sn);
+    xm = r2c_combine(zb, za, -cs, sn);
+  };
+  const uint64_t k2 = c0 + t;
+  float2 xa[8], xm[8];
+  if (k2 == 0) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) xbin((g0 + r) * n2, xa[r], xm[r]);
+  } else {
+    const float4* sa = reinterpret_cast<const float4*>(z + (k2 >> 3) * (8 * n1) + (g0 >> 3) * 64 + (k2 & 7) * 8);
+    const uint64_t m2 = n2 - k2, m1 = n1 - 8 - g0;
+    const float4* sb = reinterpret_cast<const float4*>(z + (m2 >> 3) * (8 * n1) + (m1 >> 3) * 64 + (m2 & 7) * 8);
+    float2 za[8], zb[8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 a = sa[u], b = sb[u];
+      za[2 * u] = make_float2(a.x, a.y);
+      za[2 * u + 1] = make_float2(a.z, a.w);
+      zb[7 - 2 * u] = make_float2(b.x, b.y);
+      zb[6 - 2 * u] = make_float2(b.z, b.w);
+    }
+    float sn, cs;
+    sincospif(-static_cast<float>(g0 * n2 + k2) / static_cast<float>(M), &sn, &cs);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float ws = rtw.s[r], wc = rtw.c[r];
+      const float c = __builtin_fmaf(cs, wc, -(sn * ws)), sv = __builtin_fmaf(cs, ws, sn * wc);
+      xa[r] = r2c_combine(za[r], zb[r], c, sv);
+      xm[r] = r2c_combine(zb[r], za[r], -c, sv);
+    }
+  }
+  if (lane == 63) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) eA[w + 1][r] = xa[r];
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) eD[w][r] = xm[r];
+  }
+  if (t < 8) {  // halos: column c0-1 (ascending neighbour) and c0+256 (mirror neighbour) of row t
+    const uint64_t row = (g0 + t) * n2 + c0;
+    float2 ha, hm;
+    if (row > 0) {
+      xbin(row - 1, ha, hm);
+      eA[0][t] = ha;
+    } else {
+      eA[0][t] = make_float2(0.f, 0.f);
+    }
+    xbin(row + 256, ha, hm);
+    eD[4][t] = hm;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 8; ++r) {
+    float2 xl = make_float2(__shfl_up(xa[r].x, 1, 64), __shfl_up(xa[r].y, 1, 64));
+    float2 xr = make_float2(__shfl_down(xm[r].x, 1, 64), __shfl_down(xm[r].y, 1, 64));
+    if (lane == 0) xl = eA[w][r];
+    if (lane == 63) xr = eD[w + 1][r];
+    const uint64_t k = (g0 + r) * n2 + k2;
+    if (k < nbins_out) {
+      if (k == 0) xl = make_float2(0.f, 0.f);
+      p[k] = (dev::interbin(xa[r], xl) - mean) / sigma;
+    }
+    const uint64_t j = M - k;
+    if (j < nbins_out) p[j] = (dev::interbin(xm[r], xr) - mean) / sigma;
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && half < nbins_out) {  // bin M/2 (row n1/2, column 0)
+    float2 ha, hm, la, lm;
+    xbin(half, ha, hm);
+    xbin(half - 1, la, lm);
+    p[half] = (dev::interbin(ha, la) - mean) / sigma;
   }
 }
 
@@ -566,6 +668,15 @@ __global__ void __launch_bounds__(256) c2r_post_kernel(const float2* __restrict_
 
 }  // namespace
 
+namespace {
+// bit 0: XCD-per-trial block order; bit 1: no pre-threshold (testing);
+// bit 2: nontemporal fundamental loads (tuning); bit 3: 1024-bin tiles at
+// 3 levels (tuning); bits 8-15: extra dynamic LDS per workgroup in KiB
+// (tuning: caps workgroups per CU, so fewer tiles -- a smaller gather
+// footprint -- are in flight per XCD); bits 16-23: the same for the tiled
+// r2c kernel (tuning)
+int g_harm_flags = 1;
+}  // namespace
 void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride, float* P, uint64_t pstride,
                               int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s) {
   (void)nbins;
@@ -610,8 +721,14 @@ void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstr
     rtw.c[r] = static_cast<float>(std::cos(a));
     rtw.s[r] = static_cast<float>(std::sin(a));
   }
-  r2c_interbin_tiled_kernel<<<grid, 256, 0, s>>>(X, lg, static_cast<uint64_t>(n1), xstride, P, pstride, nbins_out,
-                                                 stats, nscale, rtw, tsrc);
+  // tuning (harmonic_set_flags bits 16-23): extra dynamic LDS in KiB per workgroup caps workgroups per CU
+  const size_t dyn_lds = static_cast<size_t>((g_harm_flags >> 16) & 0xff) * 1024;
+  if (g_harm_flags & 16)  // tuning: the LDS-plane form (4 workgroups/CU)
+    r2c_interbin_tiled_kernel<<<grid, 256, dyn_lds, s>>>(X, lg, static_cast<uint64_t>(n1), xstride, P, pstride,
+                                                         nbins_out, stats, nscale, rtw, tsrc);
+  else
+    r2c_interbin_tiled_shfl_kernel<<<grid, 256, dyn_lds, s>>>(X, lg, static_cast<uint64_t>(n1), xstride, P, pstride,
+                                                              nbins_out, stats, nscale, rtw, tsrc);
   post_launch_check("r2c_interbin_tiled_kernel", s);
 }
 
@@ -642,14 +759,6 @@ void fft4_c2r_post(const float2* Z, uint64_t M, const XLayoutArgs& L, float* x, 
   post_launch_check("c2r_post_kernel", s);
 }
 
-namespace {
-// bit 0: XCD-per-trial block order; bit 1: no pre-threshold (testing);
-// bit 2: nontemporal fundamental loads (tuning); bit 3: 1024-bin tiles at
-// 3 levels (tuning); bits 8-15: extra dynamic LDS
-// per workgroup in KiB (tuning: caps workgroups per CU, so fewer tiles -- a
-// smaller gather footprint -- are in flight per XCD)
-int g_harm_flags = 1;
-}  // namespace
 void harmonic_set_flags(int flags) { g_harm_flags = flags; }
 
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
