@@ -167,7 +167,8 @@ class Whitener {
   uint64_t n() const { return n_; }
   uint64_t nbins() const { return n_ / 2 + 1; }
   float bin_width() const { return bin_width_; }
-  bool uses_fft4() const { return f4_; }
+  bool uses_fft4() const { return f4_ || mixed_; }  // no rocFFT (power-of-two or mixed-radix four-step passes)
+  bool mixed_radix() const { return mixed_; }
 
  private:
   FftPlan& r2c();
@@ -179,6 +180,17 @@ class Whitener {
   void ensure_batch(int count);
   void dered_stats(float2* spec, const uint32_t* d_zapmask, float* d_stats, float boundary5, float boundary25);
   bool f4_ = false;
+  // n = mm_ * mp_ (mp_ a power of two, mm_ odd): mm_ batched mp_-point
+  // complex FFTs on the four-step passes + a length-mm_ combination
+  // (kern::mixed_*), so no length needs rocFFT's runtime-compiled kernels
+  bool mixed_ = false;
+  uint32_t mm_ = 1;
+  uint64_t mp_ = 0;
+  kern::Fft4Geom gm_;
+  DeviceBuffer<float2> mtab_, mz_, my_, mx_;
+  DeviceBuffer<float> mpad_;
+  DeviceBuffer<double> maf0_;
+  void mixed_fft(const float* src, int gather_mode, void* out, int combine_mode);
   kern::Fft4Geom g4_;
   int bcap_ = 0;  // trials the fft4 batch buffers hold
   DeviceBuffer<float2> tab4_, y4_, x4_, tmp4_;

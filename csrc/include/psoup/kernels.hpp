@@ -235,6 +235,17 @@ void fft4_c2r_pre(const float2* X, uint64_t M, float2* out, hipStream_t s, int c
 // x[2m] + i x[2m+1] = conj(Z[m]) (Z in layout L): the N-point unnormalised C2R.
 void fft4_c2r_post(const float2* Z, uint64_t M, const XLayoutArgs& L, float* x, hipStream_t s, int count = 1,
                    uint64_t zstride = 0, uint64_t ostride = 0);
+// Mixed-radix (n = m p, p a power of two, m odd) transforms on the four-step
+// passes, for series whose length is not a power of two (the multi-beam
+// coincidencer transforms the whole DM-0 series): z[n1][n2] = s(n1 + m n2),
+// m batched p-point FFTs, then X[k] = sum_n1 W_n^(n1 k) Z_n1[k mod p].
+// gather mode 0: s = real series x (imaginary 0); mode 1: s = conj of the
+// Hermitian extension of the half spectrum X[0..n/2] (the C2R input).
+void mixed_gather(const float* src, uint64_t n, uint32_t m, uint64_t p, int mode, float2* dst, hipStream_t s);
+// Z_n1 in layout L at Z + n1*zstride; mode 0: out = float2 X[0..n/2]; mode 1:
+// out = float Re X[0..n-1] (the unnormalised C2R when the gather was mode 1).
+void mixed_combine(const float2* Z, uint64_t zstride, const XLayoutArgs& L, uint64_t n, uint32_t m, uint64_t p,
+                   int mode, void* out, hipStream_t s);
 // Tuning switches (process-wide, for measurement): kernel shape and store policy.
 enum Fft4Flags : int {
   kFft4Cpt8 = 1,         // 8 transforms per thread, one thread group (else 4 per thread, two groups)

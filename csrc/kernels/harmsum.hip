@@ -676,6 +676,52 @@ namespace {
 // footprint -- are in flight per XCD); bits 16-23: the same for the tiled
 // r2c kernel (tuning)
 int g_harm_flags = 1;
+
+// Mixed-radix n = m p (p a power of two, m odd): gather of the m strided
+// columns, and the length-m combination with the twiddles W_n^(n1 k)
+// (double-precision recurrence per output).
+__global__ void __launch_bounds__(256) mixed_gather_kernel(const float* __restrict__ src, uint64_t n, uint32_t m,
+                                                           int log2p, int mode, float2* __restrict__ dst) {
+  const uint64_t pmask = (uint64_t(1) << log2p) - 1, half = n / 2;
+  const float2* X = reinterpret_cast<const float2*>(src);
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t j = (i >> log2p) + m * (i & pmask);  // n1 + m n2
+    float2 v;
+    if (mode == 0) {
+      v = make_float2(src[j], 0.f);
+    } else {
+      const float2 a = j <= half ? X[j] : X[n - j];
+      v = j <= half ? make_float2(a.x, -a.y) : a;  // conj(Xfull[j]), Xfull[n-j] = conj X[j]
+    }
+    dst[i] = v;
+  }
+}
+
+__global__ void __launch_bounds__(256) mixed_combine_kernel(const float2* __restrict__ Z, uint64_t zstride,
+                                                            XLayoutArgs L, uint64_t n, uint32_t m, uint64_t pmask,
+                                                            int mode, uint64_t nout, void* __restrict__ out) {
+  for (uint64_t k = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; k < nout;
+       k += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
+    const uint64_t a = xaddr(k & pmask, L);
+    double sn, cs;
+    sincospi(-2.0 * static_cast<double>(k) / static_cast<double>(n), &sn, &cs);
+    double wr = 1.0, wi = 0.0, ar = 0.0, ai = 0.0;
+    for (uint32_t n1 = 0; n1 < m; ++n1) {
+      const float2 z = Z[n1 * zstride + a];
+      ar += wr * z.x - wi * z.y;
+      ai += wr * z.y + wi * z.x;
+      const double t = wr * cs - wi * sn;
+      wi = wr * sn + wi * cs;
+      wr = t;
+    }
+    if (mode == 0)
+      reinterpret_cast<float2*>(out)[k] = make_float2(static_cast<float>(ar), static_cast<float>(ai));
+    else
+      reinterpret_cast<float*>(out)[k] = static_cast<float>(ar);
+  }
+}
+
 }  // namespace
 void interbin_normalise_batch(const float2* X, uint64_t nbins, uint64_t xstride, float* P, uint64_t pstride,
                               int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s) {
@@ -730,6 +776,22 @@ void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstr
     r2c_interbin_tiled_shfl_kernel<<<grid, 256, dyn_lds, s>>>(X, lg, static_cast<uint64_t>(n1), xstride, P, pstride,
                                                               nbins_out, stats, nscale, rtw, tsrc);
   post_launch_check("r2c_interbin_tiled_kernel", s);
+}
+
+void mixed_gather(const float* src, uint64_t n, uint32_t m, uint64_t p, int mode, float2* dst, hipStream_t s) {
+  PSOUP_CHECK(p >= 2 && (p & (p - 1)) == 0 && m >= 1 && n == static_cast<uint64_t>(m) * p, "mixed_gather: bad shape");
+  int lg = 0;
+  while ((uint64_t(1) << lg) < p) ++lg;
+  mixed_gather_kernel<<<dev::grid_for(n, 256, 4096), 256, 0, s>>>(src, n, m, lg, mode, dst);
+  post_launch_check("mixed_gather_kernel", s);
+}
+
+void mixed_combine(const float2* Z, uint64_t zstride, const XLayoutArgs& L, uint64_t n, uint32_t m, uint64_t p,
+                   int mode, void* out, hipStream_t s) {
+  PSOUP_CHECK(p >= 2 && (p & (p - 1)) == 0 && m >= 1 && n == static_cast<uint64_t>(m) * p, "mixed_combine: bad shape");
+  const uint64_t nout = mode == 0 ? n / 2 + 1 : n;
+  mixed_combine_kernel<<<dev::grid_for(nout, 256, 4096), 256, 0, s>>>(Z, zstride, L, n, m, p - 1, mode, nout, out);
+  post_launch_check("mixed_combine_kernel", s);
 }
 
 void fft4_r2c_half(const float2* Z, uint64_t M, const XLayoutArgs& L, float2* X, hipStream_t s, int count,

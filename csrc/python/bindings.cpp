@@ -656,6 +656,7 @@ PYBIND11_MODULE(_C, m) {
       .def("whiten", [](Whitener& w, uintptr_t x, bool stats) { w.whiten(P<float>(x), nullptr, stats, 0.05f, 0.5f); },
            py::arg("series"), py::arg("with_stats") = true)
       .def_property_readonly("uses_fft4", &Whitener::uses_fft4)
+      .def_property_readonly("mixed_radix", &Whitener::mixed_radix)
       .def_property_readonly("nbins", &Whitener::nbins);
   py::class_<SearchParams>(m, "SearchParams")
       .def(py::init<>())

@@ -284,7 +284,44 @@ Whitener::Whitener(uint64_t n, float tsamp, hipStream_t stream, bool allow_fft4)
     tab4_.resize(tab.size());
     PSOUP_HIP_CHECK(hipMemcpy(tab4_.data(), tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice));
     ensure_batch(1);
+  } else if (allow_fft4) {
+    // lengths with an odd factor (e.g. the coincidencer's whole DM-0 series,
+    // 1114112 = 17 x 2^16): m batched power-of-two FFTs + a length-m pass
+    const uint64_t p = n & (~n + 1);  // largest power of two dividing n
+    const uint64_t m = n / p;
+    if (m >= 3 && m <= 255) {
+      gm_ = kern::fft4_geometry(p);
+      mixed_ = gm_.ok && gm_.n1 >= 128 && gm_.n2 >= 64;
+    }
+    if (mixed_) {
+      mm_ = static_cast<uint32_t>(m);
+      mp_ = p;
+      auto tab = kern::fft4_tables(gm_);
+      mtab_.resize(tab.size());
+      PSOUP_HIP_CHECK(hipMemcpy(mtab_.data(), tab.data(), tab.size() * sizeof(float2), hipMemcpyHostToDevice));
+      mz_.resize(n);
+      mpad_.resize(gm_.insize * m);
+      my_.resize(gm_.ystride * m);
+      mx_.resize(gm_.xstride * m);
+      maf0_.resize(m);
+      maf0_.zero_async(stream_);
+    }
   }
+}
+
+void Whitener::mixed_fft(const float* src, int gather_mode, void* out, int combine_mode) {
+  const uint64_t fl = 2 * mp_;  // floats per column (interleaved complex)
+  const int K = static_cast<int>(mm_);
+  kern::mixed_gather(src, n_, mm_, mp_, gather_mode, mz_.data(), stream_);
+  const float* z = reinterpret_cast<const float*>(mz_.data());
+  kern::Fft4Geom g = gm_;
+  g.in_tstride = fl;
+  g.pad_tstride = gm_.insize;
+  kern::fft4_pad_input(z, fl, mpad_.data(), gm_, stream_, K, fl);
+  kern::fft4_resample_colpass(z, mpad_.data(), fl, maf0_.data(), K, my_.data(), g, mtab_.data(), stream_);
+  kern::fft4_rowpass(my_.data(), mx_.data(), K, gm_, mtab_.data(), stream_);
+  kern::mixed_combine(mx_.data(), gm_.xstride, kern::xlayout_args(gm_, kern::fft4_x_layout(gm_)), n_, mm_, mp_,
+                      combine_mode, out, stream_);
 }
 
 FftPlan& Whitener::r2c() {
@@ -298,6 +335,10 @@ FftPlan& Whitener::c2r() {
 }
 
 void Whitener::forward(const float* d_series, float2* d_spec) {
+  if (mixed_) {
+    mixed_fft(d_series, 0, d_spec, 0);
+    return;
+  }
   if (!f4_) {
     r2c().execute(const_cast<float*>(d_series), d_spec, stream_);
     return;
@@ -310,6 +351,11 @@ void Whitener::forward(const float* d_series, float2* d_spec) {
 }
 
 void Whitener::inverse(const float2* d_spec, float* d_series) {
+  if (mixed_) {
+    // C2R = Re FFT(conj of the Hermitian extension), unnormalised like rocFFT's
+    mixed_fft(reinterpret_cast<const float*>(d_spec), 1, d_series, 1);
+    return;
+  }
   if (!f4_) {
     c2r().execute(const_cast<float2*>(d_spec), d_series, stream_);
     return;

@@ -238,9 +238,9 @@ class RankSearcher:
 
         dd_events = []
         lock = threading.Lock()
+        cur = pull()  # the first block's dedispersion is issued before the search timer starts
         if t_s:
             t_s.start()
-        cur = pull()
         while cur is not None:
             j, ck, resumed, inflight = cur
             d0, d1 = blocks[j]

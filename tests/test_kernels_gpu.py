@@ -533,6 +533,31 @@ def test_whitener_real_ffts_on_fft4_match_numpy(C, log2n):
     assert np.abs(outs[True] - outs[False]).max() < 2e-6 * scale * log2n
 
 
+@pytest.mark.parametrize("m,log2p", [(3, 14), (17, 16)])
+def test_whitener_mixed_radix_ffts_match_numpy(C, m, log2p):
+    """Lengths with an odd factor (n = m 2^k, e.g. the coincidencer's
+    1114112-sample DM-0 series) run as m batched power-of-two four-step FFTs
+    plus a length-m combination -- no rocFFT runtime compilation -- and match
+    NumPy's rfft / unnormalised irfft."""
+    n = m << log2p
+    rng = np.random.default_rng(n)
+    x = rng.standard_normal(n).astype(np.float32)
+    s = torch.cuda.current_stream().cuda_stream
+    w = C.Whitener(n, 64e-6, s, True)
+    assert w.mixed_radix and w.uses_fft4
+    xs = torch.from_numpy(x).to(dev)
+    X = torch.empty(n // 2 + 1, dtype=torch.complex64, device=dev)
+    w.forward(xs.data_ptr(), X.data_ptr())
+    torch.cuda.synchronize()
+    ref = np.fft.rfft(x.astype(np.float64))
+    scale = np.abs(ref).max()
+    assert np.abs(X.cpu().numpy() - ref).max() < 2e-6 * scale * np.log2(n)
+    y = torch.empty(n, dtype=torch.float32, device=dev)
+    w.inverse(X.data_ptr(), y.data_ptr())
+    torch.cuda.synchronize()
+    assert np.allclose(y.cpu().numpy() / n, x, atol=2e-5 * np.log2(n))
+
+
 def test_batched_whitening_matches_single_trial(C):
     """SearchEngine.prepare(count) + search_prepared(b) (one K = count
     four-step FFT pair for the whitening) gives the candidates, whitened
