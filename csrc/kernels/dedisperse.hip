@@ -309,11 +309,22 @@ __device__ __forceinline__ void lds_accumulate(const uint32_t* w, uint32_t sh, u
   }
 }
 
-template <bool XOR, int PASSES, int DPT, int CPB>
+// Byte-lane accumulation (BYTES): a lane's 16 samples of one DM are the four
+// dwords at the wave-uniform byte shift (v_alignbyte) added as packed bytes --
+// four adds per channel instead of eight v_perm + eight adds -- and spilled to
+// the 16-bit sums every `flush` channels (flush * max raw value <= 255, so no
+// byte carries).
+template <int Q>
+__device__ __forceinline__ void lds_accumulate_bytes(const uint32_t* w, uint32_t sh, uint32_t (&acc)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) acc[i] += __builtin_amdgcn_alignbyte(w[Q + i + 1], w[Q + i], sh);
+}
+
+template <bool XOR, int PASSES, int DPT, int CPB, bool BYTES = false>
 __global__ void __launch_bounds__(256) dedisperse_lds_kernel(
     const int8_t* __restrict__ x, uint64_t stride, const int32_t* __restrict__ active, int nactive,
     const int32_t* __restrict__ offT, int ldo, int d_base, int ndm, const int32_t* __restrict__ wmin,
-    uint64_t out_nsamps, uint8_t* __restrict__ out, uint64_t out_stride, float scale) {
+    uint64_t out_nsamps, uint8_t* __restrict__ out, uint64_t out_stride, float scale, int flush) {
   // CPB channels' windows per LDS buffer (one barrier per CPB channels),
   // double-buffered; each window is PASSES x 4 KiB
   __shared__ __attribute__((aligned(16))) uint32_t win[2][CPB * PASSES * 1024];
@@ -331,6 +342,21 @@ __global__ void __launch_bounds__(256) dedisperse_lds_kernel(
   for (int j = 0; j < DPT; ++j)
 #pragma unroll
     for (int q = 0; q < 8; ++q) pk[j][q] = 0;
+  uint32_t acc[DPT][4];  // BYTES: packed byte sums since the last spill
+#pragma unroll
+  for (int j = 0; j < DPT; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = 0;
+  auto spill = [&]() {
+#pragma unroll
+    for (int j = 0; j < DPT; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        pk[j][2 * i] += acc[j][i] & 0x00FF00FFu;            // samples 4i, 4i+2
+        pk[j][2 * i + 1] += (acc[j][i] >> 8) & 0x00FF00FFu;  // samples 4i+1, 4i+3
+        acc[j][i] = 0;
+      }
+  };
   u32x4 r[CPB][PASSES];
   // every thread stages 16 bytes per pass and channel (predicating the loads
   // to the launch's largest window measured slower: 2.57 vs 2.2 ms per chunk)
@@ -373,12 +399,24 @@ __global__ void __launch_bounds__(256) dedisperse_lds_kernel(
 #pragma unroll
     for (int j = 0; j < DPT; ++j) {
       const uint32_t sh = static_cast<uint32_t>(rel[j] & 3);
-      switch ((rel[j] >> 2) & 3) {  // uniform
-        case 0: lds_accumulate<0>(w[j], sh, pk[j]); break;
-        case 1: lds_accumulate<1>(w[j], sh, pk[j]); break;
-        case 2: lds_accumulate<2>(w[j], sh, pk[j]); break;
-        default: lds_accumulate<3>(w[j], sh, pk[j]); break;
+      if constexpr (BYTES) {
+        switch ((rel[j] >> 2) & 3) {  // uniform
+          case 0: lds_accumulate_bytes<0>(w[j], sh, acc[j]); break;
+          case 1: lds_accumulate_bytes<1>(w[j], sh, acc[j]); break;
+          case 2: lds_accumulate_bytes<2>(w[j], sh, acc[j]); break;
+          default: lds_accumulate_bytes<3>(w[j], sh, acc[j]); break;
+        }
+      } else {
+        switch ((rel[j] >> 2) & 3) {  // uniform
+          case 0: lds_accumulate<0>(w[j], sh, pk[j]); break;
+          case 1: lds_accumulate<1>(w[j], sh, pk[j]); break;
+          case 2: lds_accumulate<2>(w[j], sh, pk[j]); break;
+          default: lds_accumulate<3>(w[j], sh, pk[j]); break;
+        }
       }
+    }
+    if constexpr (BYTES) {
+      if ((ci + 1) % flush == 0) spill();  // wave-uniform
     }
   };
   gload(0);
@@ -393,6 +431,7 @@ __global__ void __launch_bounds__(256) dedisperse_lds_kernel(
     if (c0 + CPB < nactive) lstore(buf ^ 1);
     __syncthreads();
   }
+  if constexpr (BYTES) spill();
   if (t >= out_nsamps) return;
 #pragma unroll
   for (int j = 0; j < DPT; ++j) {
@@ -572,9 +611,25 @@ void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_
     const int v = e ? std::atoi(e) : 1;  // 1: 140 ms, 2: 153 ms, 4: 185 ms (fewer workgroups per CU)
     return v == 2 || v == 4 ? v : 1;
   }();
+  // byte-lane sums (narrow unsigned samples: flush * max raw value <= 255);
+  // A/B knob PSOUP_DEDISP_LDS_BYTES=0 keeps the 16-bit perm form
+  static const bool bytes_ok = [] {
+    const char* e = std::getenv("PSOUP_DEDISP_LDS_BYTES");
+    return !e || std::atoi(e) != 0;
+  }();
+  const int max_raw = (1 << std::min(nbits, 8)) - 1;
+  const int flush = max_raw > 0 ? 255 / max_raw : 255;
+  const bool bytes = bytes_ok && !xr && nbits <= 4 && flush >= 1 && cpb == 1 && !two && dpt == 4;
+  if (bytes) {
+    dedisperse_lds_kernel<false, 1, 4, 1, true><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive, d_offT,
+                                                                     ldo, d_base, ndm, d_wmin, out_nsamps, out,
+                                                                     out_stride, scale, flush);
+    post_launch_check("dedisperse_lds_kernel", s);
+    return;
+  }
 #define PSOUP_LDS_LAUNCH(X, P, D, C)                                                                           \
   dedisperse_lds_kernel<X, P, D, C><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive, d_offT, ldo, \
-                                                         d_base, ndm, d_wmin, out_nsamps, out, out_stride, scale)
+                                                         d_base, ndm, d_wmin, out_nsamps, out, out_stride, scale, 255)
 #define PSOUP_LDS_ONE(X)                                      \
   if (two) {                                                  \
     if (dpt == 8) PSOUP_LDS_LAUNCH(X, 2, 8, 1);               \
