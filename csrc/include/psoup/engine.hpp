@@ -282,6 +282,11 @@ class SearchEngine {
   std::vector<std::unique_ptr<Stream>> aux_;  // further compute streams of the sub-batch pipeline
   std::vector<std::unique_ptr<Event>> joins_;
   Event fork_;
+  // PSOUP_SUB_PHASE (tuning): bit s serialises kernel stage s (0 pass A,
+  // 1 pass B, 2 r2c, 3 harmonic sum) across consecutive sub-batches, so the
+  // two streams run different stages side by side
+  int phase_ = 0;
+  Event phase_ev_[4];
   int sub_ = 0;                    // effective sub-batch size (0 = whole batch on stream_)
   uint64_t n_, nb_;
   float bin_width_, tobs_;

@@ -574,6 +574,7 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     sub_auto = std::min(K_ / 2, cap);
   }
   sub_ = mode_ != 2 ? 0 : p_.sub_batch >= 0 ? p_.sub_batch : sub_auto;
+  if (const char* e = std::getenv("PSOUP_SUB_PHASE")) phase_ = std::atoi(e) & 15;
   if (sub_ >= K_) sub_ = 0;
   {
     int ns = std::max(2, p_.sub_streams);
@@ -642,7 +643,15 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
       mode_ == 2 ? kern::fft4_x_layout(f4_) : kern::Fft4XLayout{ilog2(n_ / 2), n_ / 2, 8, 3, false};
   PSOUP_HIP_CHECK(hipMemsetAsync(s.d_count.data(), 0, sizeof(uint32_t), stream_));
   // Trials [b, b + c) of the batch: spectrum, power spectrum, harmonic peaks.
-  auto run = [&](int b, int c, hipStream_t st) {
+  // stage gates of the sub-batch pipeline (PSOUP_SUB_PHASE): stage s of
+  // sub-batch j waits for stage s of sub-batch j - 1 (on the other stream)
+  auto gate_in = [&](int stage, int j, hipStream_t st) {
+    if ((phase_ >> stage & 1) && j > 0) PSOUP_HIP_CHECK(hipStreamWaitEvent(st, phase_ev_[stage].get(), 0));
+  };
+  auto gate_out = [&](int stage, hipStream_t st) {
+    if (phase_ >> stage & 1) phase_ev_[stage].record(st);
+  };
+  auto run = [&](int b, int c, hipStream_t st, int j) {
     float* P = P_.data() + static_cast<uint64_t>(b) * pst;
     if (mode_ == 2) {
       // res_ holds the four-step intermediates Y (complex, ystride per trial)
@@ -655,9 +664,14 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
       g.in_tstride = n_;
       g.pad_tstride = f4_.insize;
       g.tsrc = src;
+      gate_in(0, j, st);
       kern::fft4_resample_colpass(tim_.data(), f4_in_.data(), n_, af_.data() + first + b, c, Y, g, f4_tab_.data(),
                                   st);
+      gate_out(0, st);
+      gate_in(1, j, st);
       kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st, static_cast<uint64_t>(hi_));
+      gate_out(1, st);
+      gate_in(2, j, st);
       if (xl.tiled)
         kern::r2c_interbin_normalise_tiled(X, f4_.n1, f4_.n2, xs_, P, pst, c, static_cast<uint64_t>(hi_),
                                            wstats_.data(), static_cast<float>(n_), st, src);
@@ -676,10 +690,13 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
         kern::interbin_normalise_batch(spec_.data(), nb_, nb_, P, pst, c, static_cast<uint64_t>(hi_),
                                        cur_stats_, static_cast<float>(n_), st);
     }
+    gate_out(2, st);
     RoctxRange r("Harmonic summing");
     kern::HarmParams hp = hp_;
     hp.trial_base = static_cast<uint32_t>(b);
+    gate_in(3, j, st);
     kern::harmonic_peaks_batch(P, nb_, pst, c, hp, s.d_peaks.data(), s.d_count.data(), st);
+    gate_out(3, st);
   };
   if (sub_ > 0 && count > sub_) {
     // Sub-batch pipeline: consecutive sub-batches alternate between two
@@ -690,13 +707,13 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
     for (auto& a : aux_) PSOUP_HIP_CHECK(hipStreamWaitEvent(a->get(), fork_.get(), 0));
     const int ns = static_cast<int>(aux_.size()) + 1;
     for (int b = 0, j = 0; b < count; b += sub_, ++j)
-      run(b, std::min(sub_, count - b), j % ns == 0 ? stream_ : aux_[static_cast<size_t>(j % ns - 1)]->get());
+      run(b, std::min(sub_, count - b), j % ns == 0 ? stream_ : aux_[static_cast<size_t>(j % ns - 1)]->get(), j);
     for (size_t i = 0; i < aux_.size(); ++i) {
       joins_[i]->record(aux_[i]->get());
       PSOUP_HIP_CHECK(hipStreamWaitEvent(stream_, joins_[i]->get(), 0));
     }
   } else {
-    run(0, count, stream_);
+    run(0, count, stream_, 0);
   }
   PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_count.data(), s.d_count.data(), sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   s.done->record(stream_);
