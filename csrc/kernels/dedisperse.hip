@@ -596,11 +596,14 @@ void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_
   PSOUP_CHECK((chan_stride & 15) == 0 && (out_stride & 15) == 0, "dedisperse_lds: stride alignment");
   const uint64_t ty = (out_nsamps + 1023) / 1024;
   PSOUP_CHECK(ty <= 65535, "dedisperse_lds: series too long for the grid");
-  static const int dpt = [] {
+  static const int dpt_env = [] {
     const char* e = std::getenv("PSOUP_DEDISP_LDS_DPT");  // A/B knob: DMs per wave, 8, 4 or 2
-    const int v = e ? std::atoi(e) : 4;  // 4: 141 ms vs 173 ms (8) for the config-4 DM list
-    return v == 8 || v == 2 ? v : 4;
+    const int v = e ? std::atoi(e) : 0;  // default 4: 141 ms vs 173 ms (8) for the config-4 DM list
+    return v == 8 || v == 4 || v == 2 ? v : 0;
   }();
+  // a launch of <= 8 DMs (the headline bench's per-rank chunk) fills 8-DM
+  // workgroups instead of half-empty 16-DM ones
+  const int dpt = dpt_env ? dpt_env : (ndm <= 8 ? 2 : 4);
   dim3 grid(static_cast<unsigned>((ndm + 4 * dpt - 1) / (4 * dpt)), static_cast<unsigned>(ty));
   PSOUP_CHECK(d_base + static_cast<int>(grid.x) * 4 * dpt <= ldo, "dedisperse_lds: offset table too narrow");
   const bool two = max_window > 4096;
@@ -619,11 +622,16 @@ void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_
   }();
   const int max_raw = (1 << std::min(nbits, 8)) - 1;
   const int flush = max_raw > 0 ? 255 / max_raw : 255;
-  const bool bytes = bytes_ok && !xr && nbits <= 4 && flush >= 1 && cpb == 1 && !two && dpt == 4;
+  const bool bytes = bytes_ok && !xr && nbits <= 4 && flush >= 1 && cpb == 1 && !two && (dpt == 4 || dpt == 2);
   if (bytes) {
-    dedisperse_lds_kernel<false, 1, 4, 1, true><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive, d_offT,
-                                                                     ldo, d_base, ndm, d_wmin, out_nsamps, out,
-                                                                     out_stride, scale, flush);
+    if (dpt == 4)
+      dedisperse_lds_kernel<false, 1, 4, 1, true><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive,
+                                                                       d_offT, ldo, d_base, ndm, d_wmin, out_nsamps,
+                                                                       out, out_stride, scale, flush);
+    else
+      dedisperse_lds_kernel<false, 1, 2, 1, true><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive,
+                                                                       d_offT, ldo, d_base, ndm, d_wmin, out_nsamps,
+                                                                       out, out_stride, scale, flush);
     post_launch_check("dedisperse_lds_kernel", s);
     return;
   }

@@ -578,6 +578,7 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   if (sub_ >= K_) sub_ = 0;
   {
     int ns = std::max(2, p_.sub_streams);
+    if (const char* e = std::getenv("PSOUP_SUB_STREAMS")) ns = std::max(2, std::min(8, std::atoi(e)));  // A/B knob
     if (const char* e = std::getenv("PSOUP_SUB_STREAMS")) ns = std::max(2, std::atoi(e));
     for (int i = 1; i < ns; ++i) {
       aux_.push_back(std::make_unique<Stream>());
