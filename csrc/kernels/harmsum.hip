@@ -17,6 +17,7 @@
 #include "psoup/kernels.hpp"
 
 #include <cmath>
+#include <type_traits>
 
 namespace psoup {
 namespace kern {
@@ -590,6 +591,182 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
   }
 }
 
+// Two-phase form (harmonic_set_flags bit 5, tuning): levels 1..NLEV-1 are
+// staged, summed and thresholded first, then the top level's ranges reuse
+// the same LDS -- 16.4 instead of 28.8 KiB and about half the staging
+// registers at NLEV = 3, so more workgroups share a CU.  Same sums in the
+// same order, same records (emitted level by level; the host sorts each
+// (trial, level) segment).
+template <int NLEV>
+struct HarmTile2 {
+  using T = HarmTile<NLEV>;
+  static constexpr int SPLIT = 1 << (NLEV - 1);  // first region of the top level
+  static constexpr int P1 = T::offset(SPLIT);    // floats of levels 1..NLEV-1
+  static constexpr int P2 = T::TOTAL - P1;       // floats of level NLEV
+  static constexpr int LDS = P1 > P2 ? P1 : P2;
+  static constexpr int iters(int hlo, int hhi) {
+    int n = 0;
+    for (int h = hlo; h <= hhi; ++h)
+      for (int m = 1; m < (1 << h); m += 2) n += (T::chunks(h, m) + 255) / 256;
+    return n;
+  }
+  static constexpr int IT = iters(1, NLEV - 1) > iters(NLEV, NLEV) ? iters(1, NLEV - 1) : iters(NLEV, NLEV);
+};
+
+template <int NLEV>
+__global__ void __launch_bounds__(256) harmonic_peaks2_kernel(const float* __restrict__ P, uint64_t pstride, int lo,
+                                                              int hi, HarmParams hp, PeakRecord* __restrict__ out,
+                                                              uint32_t* __restrict__ count, int ntiles, int xcd_trials,
+                                                              HarmPre pre) {
+  static_assert(NLEV >= 2, "two phases need at least two levels");
+  using Tl = HarmTile<NLEV>;
+  using T2 = HarmTile2<NLEV>;
+  constexpr int B = Tl::B;
+  __shared__ __attribute__((aligned(16))) float lds[T2::LDS];
+  const uint32_t bid = blockIdx.x;
+  int k, tile;
+  if (xcd_trials & 1) {
+    const uint32_t slot = bid >> 3;
+    k = static_cast<int>((slot / ntiles) * 8 + (bid & 7u));
+    tile = static_cast<int>(slot % ntiles);
+  } else {
+    k = static_cast<int>(bid / ntiles);
+    tile = static_cast<int>(bid % ntiles);
+  }
+  const float* p = P + static_cast<uint64_t>(k) * pstride;
+  const int t = threadIdx.x;
+  const int b0 = lo + tile * B;
+  const int last = hi - 1;
+  const int i0 = b0 + t;
+  // stage the gather ranges of levels [HLO, HHI] at LDS offset base 0
+  auto stage = [&](auto hlo_c, auto hhi_c) {
+    constexpr int HLO = decltype(hlo_c)::value, HHI = decltype(hhi_c)::value;
+    constexpr int BASE = Tl::offset(1 << (HLO - 1));
+    f4u_h tmp[T2::IT];
+    int it = 0;
+#pragma unroll
+    for (int h = HLO; h <= HHI; ++h) {
+#pragma unroll
+      for (int m = 1; m < (1 << h); m += 2) {
+        const int r0 = (b0 * m + (1 << (h - 1))) >> h;
+#pragma unroll
+        for (int e = 0; e < (Tl::chunks(h, m) + 255) / 256; ++e, ++it) {
+          const int a = r0 + 4 * (t + 256 * e);
+          if (a + 3 <= last)
+            tmp[it] = *reinterpret_cast<const f4u_h*>(p + a);
+          else
+            tmp[it] = f4u_h{p[min(a, last)], p[min(a + 1, last)], p[min(a + 2, last)], p[min(a + 3, last)]};
+        }
+      }
+    }
+    it = 0;
+#pragma unroll
+    for (int h = HLO; h <= HHI; ++h) {
+#pragma unroll
+      for (int m = 1; m < (1 << h); m += 2) {
+        float4* dst = reinterpret_cast<float4*>(lds + Tl::offset(Tl::region(h, m)) - BASE);
+#pragma unroll
+        for (int e = 0; e < (Tl::chunks(h, m) + 255) / 256; ++e, ++it)
+          if (t + 256 * e < Tl::chunks(h, m)) dst[t + 256 * e] = make_float4(tmp[it].x, tmp[it].y, tmp[it].z, tmp[it].w);
+      }
+    }
+  };
+  // LDS index of term (h, m) for bin i0 + 256 u (affine in u, see harmonic_peaks_kernel)
+  auto term = [&](int h, int m, int base_off, int u) {
+    const int r = Tl::region(h, m);
+    const int b = Tl::offset(r) - base_off + (((i0 * m + (1 << (h - 1))) >> h) - ((b0 * m + (1 << (h - 1))) >> h));
+    return lds[b + u * (m << (8 - h))];
+  };
+  float fund[Tl::BPT];
+#pragma unroll
+  for (int u = 0; u < Tl::BPT; ++u) fund[u] = p[min(b0 + t + 256 * u, last)];
+  stage(std::integral_constant<int, 1>{}, std::integral_constant<int, NLEV - 1>{});
+  __syncthreads();
+  const float thr = hp.thresh;
+  const uint32_t seg0 = (static_cast<uint32_t>(k) + hp.trial_base) * 8u;
+  bool inner = true;
+#pragma unroll
+  for (int h = 0; h <= NLEV; ++h) inner = inner & (b0 >= hp.start[h]) & (b0 + B <= hp.end[h]);
+  // emit the exact-scaled records of levels [h0, h1] for bin i from the unscaled sums
+  auto check = [&](const float* sum, int h0, int h1, int i, bool valid) {
+    bool cand = false;
+    for (int h = h0; h <= h1; ++h) cand = cand | (sum[h] > pre.lo[h]);
+    if (__ballot(cand) == 0ull) return;
+    bool any = false;
+    bool pred[NLEV + 1];
+    float o[NLEV + 1];
+#pragma unroll
+    for (int h = 0; h <= NLEV; ++h) {
+      if (h < h0 || h > h1) {
+        pred[h] = false;
+        o[h] = 0.f;
+        continue;
+      }
+      if (h == 2)
+        o[h] = sum[h] * 0.5f;
+      else if (h == 4)
+        o[h] = sum[h] * 0.25f;
+      else
+        o[h] = h == 0 ? sum[0] : static_cast<float>(static_cast<double>(sum[h]) * c_level_scale[h]);
+      const bool in_range = inner | ((i >= hp.start[h]) & (i < hp.end[h]));
+      pred[h] = valid & in_range & (o[h] > thr);
+      any = any | pred[h];
+    }
+    if (__ballot(any) == 0ull) return;
+#pragma unroll
+    for (int h = 0; h <= NLEV; ++h)
+      if (h >= h0 && h <= h1) emit(pred[h], seg0 + h, i, o[h], out, count, hp.capacity);
+  };
+  float run[Tl::BPT];  // running sum after level NLEV - 1
+#pragma unroll
+  for (int u = 0; u < Tl::BPT; ++u) {
+    const int i = i0 + u * 256;
+    float val = fund[u];
+    float sum[NLEV + 1];
+    sum[0] = val;
+    val += term(1, 1, 0, u);
+    sum[1] = val;
+    if constexpr (NLEV >= 3) {
+      val += term(2, 3, 0, u);  // reference order: 3/4 before 1/4
+      val += term(2, 1, 0, u);
+      sum[2] = val;
+    }
+    if constexpr (NLEV >= 4) {
+#pragma unroll
+      for (int m = 1; m < 8; m += 2) val += term(3, m, 0, u);
+      sum[3] = val;
+    }
+    if constexpr (NLEV >= 5) {
+#pragma unroll
+      for (int m = 1; m < 16; m += 2) val += term(4, m, 0, u);
+      sum[4] = val;
+    }
+    run[u] = val;
+    check(sum, 0, NLEV - 1, i, i < hi);
+  }
+  __syncthreads();  // phase-1 ranges no longer read
+  stage(std::integral_constant<int, NLEV>{}, std::integral_constant<int, NLEV>{});
+  __syncthreads();
+  constexpr int BASE2 = Tl::offset(1 << (NLEV - 1));
+#pragma unroll
+  for (int u = 0; u < Tl::BPT; ++u) {
+    const int i = i0 + u * 256;
+    float val = run[u];
+    if constexpr (NLEV == 2) {
+      val += term(2, 3, BASE2, u);
+      val += term(2, 1, BASE2, u);
+    } else {
+#pragma unroll
+      for (int m = 1; m < (1 << NLEV); m += 2) val += term(NLEV, m, BASE2, u);
+    }
+    float sum[NLEV + 1];
+#pragma unroll
+    for (int h = 0; h < NLEV; ++h) sum[h] = 0.f;
+    sum[NLEV] = val;
+    check(sum, NLEV, NLEV, i, i < hi);
+  }
+}
+
 __global__ void __launch_bounds__(256) harmonic_sums_kernel(const float* __restrict__ p, uint64_t nbins,
                                                             int nlevels, float* __restrict__ out) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
@@ -671,7 +848,8 @@ __global__ void __launch_bounds__(256) c2r_post_kernel(const float2* __restrict_
 namespace {
 // bit 0: XCD-per-trial block order; bit 1: no pre-threshold (testing);
 // bit 2: nontemporal fundamental loads (tuning); bit 3: 1024-bin tiles at
-// 3 levels (tuning); bits 8-15: extra dynamic LDS per workgroup in KiB
+// 3 levels (tuning); bit 4: the LDS-plane r2c form; bit 5: two-phase
+// harmonic staging at 3 levels (tuning); bits 8-15: extra dynamic LDS per workgroup in KiB
 // (tuning: caps workgroups per CU, so fewer tiles -- a smaller gather
 // footprint -- are in flight per XCD); bits 16-23: the same for the tiled
 // r2c kernel (tuning)
@@ -867,10 +1045,16 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
     PS_LAUNCH(NL, 0)   \
     break;
     case 3:
-      if (g_harm_flags & 8)  // tuning: 1024-bin tiles (half the LDS and registers per workgroup)
+      if (g_harm_flags & 32) {  // tuning: two staging phases (levels 1-2, then 3) in 16.4 KiB of LDS
+        const int nt = ntiles_of(HarmTile<3>::B);
+        PSOUP_CHECK(static_cast<int64_t>(nt) * K < (int64_t(1) << 31), "harmonic grid too large");
+        harmonic_peaks2_kernel<3><<<dim3(static_cast<unsigned>(nt * K)), 256, dyn_lds, s>>>(
+            P, pstride, lo, hi, hp, out, count, nt, xcd, pre);
+      } else if (g_harm_flags & 8) {  // tuning: 1024-bin tiles (half the LDS and registers per workgroup)
         PS_LAUNCH(3, 4)
-      else
+      } else {
         PS_LAUNCH(3, 0)
+      }
       break;
     PS_CASE(0) PS_CASE(1) PS_CASE(2) PS_CASE(4)
     default:

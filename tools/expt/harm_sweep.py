@@ -57,10 +57,8 @@ def main():
 
     ref = None
     # static LDS is ~28.8 KiB: +50 KiB -> 2 workgroups/CU, +25 -> 3, +12 -> 4
-    for name, fl in [("xcd", 1), ("plain", 0), ("xcd+nt", 1 | 4),
-                     ("xcd 4wg/CU", 1 | (12 << 8)),
-                     ("xcd 1024-bin", 1 | 8), ("xcd+nt 1024-bin", 1 | 4 | 8), ("plain 1024-bin", 8),
-                     ("xcd", 1)]:
+    for name, fl in [("xcd", 1), ("xcd two-phase", 1 | 32), ("xcd", 1), ("xcd two-phase", 1 | 32),
+                     ("plain two-phase", 32), ("xcd two-phase 6wg/CU", 1 | 32 | (10 << 8))]:
         K_.harmonic_set_flags(fl)
         us = timeit(harm, a.reps)
         torch.cuda.synchronize()
