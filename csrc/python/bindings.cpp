@@ -760,6 +760,15 @@ PYBIND11_MODULE(_C, m) {
   });
   m.def("write_samp_mask", &write_samp_mask);
   m.def("write_birdie_list", &write_birdie_list);
+  // host float32 buffers by address (a 1M-sample mask without a Python list)
+  m.def("write_samp_mask_ptr", [](uintptr_t mask, uint64_t n, const std::string& fn) {
+    const float* f = P<const float>(mask);
+    write_samp_mask(std::vector<float>(f, f + n), fn);
+  });
+  m.def("write_birdie_list_ptr", [](uintptr_t mask, uint64_t n, float bin_width, const std::string& fn) {
+    const float* f = P<const float>(mask);
+    write_birdie_list(std::vector<float>(f, f + n), bin_width, fn);
+  });
 
   // ----------------------------------------------------------- pipeline ---
   m.def("run_pipeline_native", [](const CmdLineOptions& args) {

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <charconv>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
@@ -1078,11 +1079,19 @@ void coincidencer_beam(const uint8_t* d_trial, uint64_t n, float tsamp, BeamProd
 }
 
 void write_samp_mask(const std::vector<float>& mask, const std::string& filename) {
+  // "%d\n" per sample (coincidencer.cpp), formatted into one buffer
+  std::string buf = "#0 1\n";
+  buf.reserve(buf.size() + mask.size() * 3);
+  char tmp[16];
+  for (float v : mask) {
+    const auto r = std::to_chars(tmp, tmp + sizeof(tmp), static_cast<int>(v));
+    buf.append(tmp, r.ptr);
+    buf.push_back('\n');
+  }
   FILE* fo = std::fopen(filename.c_str(), "w");
   if (!fo) PSOUP_THROW("cannot write " << filename);
-  std::fprintf(fo, "#0 1\n");
-  for (float v : mask) std::fprintf(fo, "%d\n", static_cast<int>(v));
-  std::fclose(fo);
+  const bool ok = std::fwrite(buf.data(), 1, buf.size(), fo) == buf.size();
+  if (std::fclose(fo) != 0 || !ok) PSOUP_THROW("failed writing " << filename);
 }
 
 void write_birdie_list(const std::vector<float>& mask, float bin_width, const std::string& filename) {

@@ -77,8 +77,10 @@ def run_coincidencer(filterbanks: Sequence[str], samp_out: str = "rfi.eb_mask", 
     out = {"nsamps": size, "masked_samples": int((smask == 0).sum()), "masked_bins": int((fmask == 0).sum())}
     if ctx.is_root:
         bin_width = 1.0 / float(torch.tensor(size * tsamp, dtype=torch.float32))
-        _C.write_samp_mask(smask.cpu().tolist(), samp_out)
-        _C.write_birdie_list(fmask.cpu().tolist(), bin_width, spec_out)
+        hs = smask.to(torch.float32).cpu().contiguous()
+        hf = fmask.to(torch.float32).cpu().contiguous()
+        _C.write_samp_mask_ptr(hs.data_ptr(), hs.numel(), samp_out)
+        _C.write_birdie_list_ptr(hf.data_ptr(), hf.numel(), bin_width, spec_out)
     return out
 
 

@@ -43,8 +43,9 @@ def main():
     torch.cuda.synchronize()
     T["counts+masks"] = time.perf_counter() - t
     t = time.perf_counter()
-    _C.write_samp_mask(sm.cpu().tolist(), "/tmp/ct_mask.txt")
-    _C.write_birdie_list(fm.cpu().tolist(), 1.0 / (n * ts), "/tmp/ct_birdies.txt")
+    hs, hf = sm.to(torch.float32).cpu().contiguous(), fm.to(torch.float32).cpu().contiguous()
+    _C.write_samp_mask_ptr(hs.data_ptr(), hs.numel(), "/tmp/ct_mask.txt")
+    _C.write_birdie_list_ptr(hf.data_ptr(), hf.numel(), 1.0 / (n * ts), "/tmp/ct_birdies.txt")
     T["write mask + birdies"] = time.perf_counter() - t
     for k, v in T.items():
         print(f"{k:40s} {v * 1e3:9.1f} ms", flush=True)
