@@ -55,7 +55,12 @@ struct Cfg {
   static constexpr int T = L / kPts;                     // threads per group
   static constexpr int THREADS = T * SUB;
   static constexpr int PAD = L + L / 8 + kChanPad;       // complex elements per channel plane
-  static constexpr int BUDGET = CH == 4 ? kLdsBudget / 2 : kLdsBudget;  // CH 4: four workgroups per CU
+  // CH 4: four workgroups per CU.  Workgroups of fewer than 256 threads
+  // (L < 2048) get a proportional share: at L = 1024 the full 73 KiB let
+  // the 128-thread workgroup exchange all 8 channels in one round but held
+  // the CU to 2 workgroups (1 wave per SIMD)
+  static constexpr int BUDGET0 = CH == 4 ? kLdsBudget / 2 : kLdsBudget;
+  static constexpr int BUDGET = THREADS >= 256 ? BUDGET0 : BUDGET0 / 256 * THREADS;
   static constexpr int CG0 = BUDGET / (SUB * 2 * PAD * 4);
   static constexpr int CG = CG0 >= CPT ? CPT : (CG0 >= 4 ? 4 : (CG0 >= 2 ? 2 : 1));  // channels per exchange round
   static constexpr int GROUP_FLOATS = 2 * CG * PAD;
@@ -318,6 +323,14 @@ __device__ __forceinline__ void store_row(float2* __restrict__ dst, const Vec<CP
 // 72 KiB LDS budget; one complex of padding per 64 spreads the 8-byte LDS
 // writes over the banks.  keep_oct > 0 skips the octets outside
 // [0, keep_oct) u [L/8 - keep_oct, L/8) (see the pruned pass-B stores).
+// floats of LDS the staged store of one 8 x L block needs
+template <int L>
+constexpr int staged_lds_floats() {
+  constexpr int PARTS = L > 1024 ? L / 1024 : 1;
+  constexpr int PART = 8 * L / PARTS;
+  return (PART + PART / 64) * 2;
+}
+
 template <int L>
 __device__ __forceinline__ void store_tiled_staged(const Vec<8>& v, float* __restrict__ lds, int t,
                                                    float2* __restrict__ region, uint32_t keep_oct, bool nt) {
@@ -401,7 +414,10 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
   using C = Cfg<L, CPT, SUB>;
   constexpr bool kBlocked = MODE & kModeBlocked, kTiming = MODE & kModeTiming, kTileY = MODE & kModeTileY;
   static_assert(!kTileY || C::CH == 8, "tiled Y needs 8 transforms per workgroup");
-  __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
+  // the opt-in staged stores reuse the exchange buffer: size it for both
+  constexpr int kLdsN = (MODE & kModeStaged) && staged_lds_floats<L>() > C::LDS_FLOATS ? staged_lds_floats<L>()
+                                                                                      : C::LDS_FLOATS;
+  __shared__ __attribute__((aligned(16))) float lds[kLdsN];
   constexpr int T = C::T;
   const int grp = threadIdx.x / T;
   const int t = threadIdx.x - grp * T;
@@ -911,7 +927,10 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
     int flags, uint32_t keep_oct) {
   using C = Cfg<L, CPT, SUB>;
   constexpr bool kBlocked = MODE & kModeBlocked, kTiming = MODE & kModeTiming, kTileY = MODE & kModeTileY;
-  __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
+  // the opt-in staged stores reuse the exchange buffer: size it for both
+  constexpr int kLdsN = (MODE & kModeStaged) && staged_lds_floats<L>() > C::LDS_FLOATS ? staged_lds_floats<L>()
+                                                                                      : C::LDS_FLOATS;
+  __shared__ __attribute__((aligned(16))) float lds[kLdsN];
   constexpr int T = C::T;
   const int grp = threadIdx.x / T;
   const int t = threadIdx.x - grp * T;
