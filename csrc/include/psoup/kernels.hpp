@@ -267,6 +267,8 @@ enum Fft4Flags : int {
   kFft4OneX = 131072,         // pass A (tiled Y, column length 512..2048): 2 columns x L/G points per thread,
                               // one LDS exchange, compile-time twiddles inside the two local DFTs
   kFft4OneXWholeCu = 262144,  // with kFft4OneX at L = 2048: the exchange in one 128 KiB round (one workgroup per CU)
+  kFft4OneXSmall = 1048576,   // with kFft4OneX: also at column lengths 512 and 1024 (the Stockham pass A is
+                              // faster there: bench at 2^22 40.4k vs 37.3k, at 2^21 55.5k vs 53.4k trials/s)
   kFft4OneXRow = 524288,      // pass B (tiled Y and X, row length 512..2048): the one-exchange structure
 };
 void fft4_set_flags(int flags);

@@ -1125,7 +1125,7 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   PSOUP_CHECK(!(f & kFft4GroupXcd) || (K & 7) != 0 || nblocks % 128 == 0, "fft4 colpass: group grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
   if ((f & kFft4OneX) && (f & kFft4Blocked) && (f & kFft4TileY) && !(f & (kTimingFlags | kFft4Sub2)) &&
-      (g.n2 == 512 || g.n2 == 1024 || g.n2 == 2048)) {
+      (g.n2 == 2048 || ((f & kFft4OneXSmall) && (g.n2 == 512 || g.n2 == 1024)))) {
     switch (g.n2) {
 #define PS_ONEX(LL, GG, RR)                                                                                  \
   case LL:                                                                                                   \

@@ -250,7 +250,7 @@ def test_r2c_interbin_normalise_batch():
         assert np.allclose(P[k], exp, rtol=1e-4, atol=2e-3), np.abs(P[k] - exp).max()
 
 
-FFT4_FLAG_SETS = [None, 0, 1, 259, 274, 1299, 3331, 7427, 15619, 32003, 48387, 81155, 474371, 736515]  # None = default (212227: tiled Y and X + uniform pass-A twiddles + one-exchange pass A); 81155 = the Stockham pass A; 32003 = + Sub2; 474371 = + whole-CU exchange; 736515 = + one-exchange pass B
+FFT4_FLAG_SETS = [None, 0, 1, 259, 274, 1299, 3331, 7427, 15619, 32003, 48387, 81155, 474371, 736515, 1260803]  # None = default (212227: tiled Y and X + uniform pass-A twiddles + one-exchange pass A at column length 2048); 81155 = the Stockham pass A; 32003 = + Sub2; 474371 = + whole-CU exchange; 736515 = + one-exchange pass B; 1260803 = one-exchange pass A at column lengths 512/1024 too
 
 
 @pytest.fixture(params=FFT4_FLAG_SETS)
