@@ -21,3 +21,30 @@ def test_chunk_ranges_empty_and_noncontiguous():
     assert RankSearcher.chunk_ranges([], 32) == []
     with pytest.raises(AssertionError):
         RankSearcher.chunk_ranges([0, 1, 3], 32)
+
+
+def test_dm_schedule_option():
+    """--dm_schedule: dynamic is the multi-rank default, a single rank is
+    always static (in-order chunks), bad values are rejected."""
+    from peasoup_amd import _C
+    from peasoup_amd.models.search import dm_schedule
+
+    ok, _, a = _C.parse_cmdline(["peasoup", "-i", "x.fil"])
+    assert ok and a.dm_schedule == "auto"
+    assert dm_schedule(a, 1) == "static" and dm_schedule(a, 8) == "dynamic"
+    ok, _, a = _C.parse_cmdline(["peasoup", "-i", "x.fil", "--dm_schedule", "static"])
+    assert ok and dm_schedule(a, 8) == "static"
+    a.dm_schedule = "roundrobin"
+    with pytest.raises(ValueError):
+        dm_schedule(a, 2)
+
+
+def test_dynamic_blocks_cover_the_dm_list_once():
+    """The dynamic schedule's block grid (claimed first-come by the ranks)
+    covers every DM exactly once, in 32-DM tile-aligned chunks."""
+    from peasoup_amd.models.search import DYNAMIC_CHUNK
+
+    for ndm in (1, 31, 32, 59, 2026):
+        blocks = RankSearcher.chunk_ranges(range(ndm), DYNAMIC_CHUNK)
+        assert [d for b in blocks for d in range(*b)] == list(range(ndm))
+        assert all(b[0] % DYNAMIC_CHUNK == 0 for b in blocks)
