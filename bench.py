@@ -4,9 +4,10 @@ an 8-harmonic sum (-n 3), one process per MI355X (torchrun for N > 1).
 
 One step (per rank, weak scaling -- fixed work per GPU):
   * dedisperse this rank's DM shard (``--dms-per-gpu`` trials, default 8, one
-    chunk -- the production pipeline dedisperses 16-DM chunks) from the
-    resident 1024-channel 2-bit filterbank (Auto kernel choice: one-hot MFMA at
-    these low DMs, packed-byte VALU/LDS for wide tiles),
+    chunk -- the production pipeline dedisperses 32-DM chunks) from the
+    resident 1024-channel 2-bit filterbank (Auto kernel choice: the LDS-staged
+    byte-lane kernel with 8-DM workgroups; the one-hot MFMA kernel measures
+    the same at these low DMs, --dedisp-kernel mfma),
   * whiten each trial and search +-500 m/s^2 (legacy acceleration-plan
     convention: ~684 trials per DM at 2^23 x 64 us) with an 8-harmonic sum:
     fused resample + two-pass four-step FFT -> paired real-FFT post-processing
