@@ -120,11 +120,11 @@ struct SearchParams {
   int accel_batch = 0;          // 0 = auto
   int sub_batch = -1;           // fused-FFT trials per sub-batch on alternating streams (0 = off, -1 = auto)
   int host_threads = -1;        // host workers clustering/distilling peak-heavy batches (-1 = auto, 0/1 = serial)
-  // auto-batch HBM budget, capped at 70% of the device's free memory shared
-  // among its engines: 512 trials of 2^23 (~43 GB of 288).  Same-box bench,
-  // trials/s for 256 / 512 / 1024-trial batches: 21.98k / 22.58k / 22.75k and
-  // 21.94k / 22.72k / 22.53k on two boxes (profiles/r2_batch/)
-  size_t batch_bytes = 48ull << 30;
+  // auto-batch HBM budget (256 trials of 2^23; same-box A/B vs 64: +1.8%),
+  // capped at 70% of the device's free memory shared among its engines.
+  // 512/1024-trial batches measured box-dependent (-0.9% .. +3.5%,
+  // profiles/r2_batch/)
+  size_t batch_bytes = 24ull << 30;
   // Engines sharing the device: the auto budget is also capped at 70% of the
   // device's free memory divided by this count.
   int engines_per_device = 1;

@@ -557,15 +557,13 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
       budget = std::min(budget, free_b / 10 * 7 / static_cast<size_t>(std::max(1, p_.engines_per_device)));
     const size_t per = n_ * 4 + nb_ * 8 + static_cast<size_t>(hi_) * 4;  // Y/res + X/spec + P per trial
     auto round_batch = [](size_t k) {
-      int K = static_cast<int>(std::min<size_t>(512, std::max<size_t>(1, k)));
+      int K = static_cast<int>(std::min<size_t>(256, std::max<size_t>(1, k)));
       if (K >= 32) K = K / 16 * 16;  // halves stay multiples of 8 (XCD-grouped kernels)
       else if (K >= 16) K = K / 8 * 8;
       return K;
     };
     K_ = p_.accel_batch > 0 ? p_.accel_batch : round_batch(budget / per);
-    // short-list floor from at most a quarter of 24 GiB (64 trials at 2^23),
-    // whatever the (larger) budget of long lists
-    k_small_ = std::min(K_, std::max(16, std::min(round_batch(budget / 4 / per), round_batch((6ull << 30) / per))));
+    k_small_ = std::min(K_, std::max(16, round_batch(budget / 4 / per)));
   }
   // Auto: sub-batches on alternating streams (+4-5% at 2^23: the tail of
   // one sub-batch's kernels overlaps the head of the other's), half a batch
