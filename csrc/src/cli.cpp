@@ -235,7 +235,7 @@ static std::vector<Spec> peasoup_specs(CmdLineOptions& a) {
       val_s("", "dm_schedule",
             "Multi-rank DM distribution (python -m peasoup_amd under torchrun): dynamic = ranks claim DM chunks "
             "from a shared first-come queue, like the reference's DMDispenser; static = contiguous shards balanced "
-            "by acceleration-trial count; auto = dynamic",
+            "by acceleration-trial count; auto = dynamic when the list has >= 4 chunks per rank",
             a.dm_schedule),
       val_n("", "sub_batch", "Fused-FFT trials per sub-batch on two alternating streams (0 = off, -1 = auto)",
             a.sub_batch),

@@ -7,7 +7,8 @@ Flow per rank (SURVEY.md §7.1 distribution model):
    every rank unpacks them into a channel-major int8 filterbank resident in
    HBM (``DeviceFilterbank``).
 2. ranks take 32-DM chunks first-come from a queue they share
-   (``--dm_schedule dynamic``, the default for several ranks: the reference's
+   (``--dm_schedule dynamic``, the default for several ranks and at least 4
+   chunks per rank: the reference's
    DMDispenser, made cross-process with an atomic counter in the process
    group's key-value store, ``pdist.WorkQueue``), or each owns a contiguous
    DM shard balanced by acceleration-trial count (``static``,
@@ -402,16 +403,21 @@ def load_packed_for_rank(infilename: str, ctx: pdist.DistContext):
 DYNAMIC_CHUNK = 32  # DMs per claimed block (the dedispersion tile multiple the static path also uses)
 
 
-def dm_schedule(args, world_size: int) -> str:
+def dm_schedule(args, world_size: int, ndm: Optional[int] = None) -> str:
     """``--dm_schedule``: "dynamic" (first-come DM chunks from a queue shared
     by the ranks), "static" (contiguous trial-weighted shards); auto = dynamic
-    for more than one rank."""
+    for more than one rank when the list has at least 4 chunks per rank (with
+    fewer, 32-DM chunks leave ranks idle: 113 DMs on 8 ranks ran 4 ranks,
+    tools/expt/dyn8_rehearsal.sh), else static."""
     s = (getattr(args, "dm_schedule", "auto") or "auto").lower()
     if s not in ("auto", "dynamic", "static"):
         raise ValueError(f"--dm_schedule must be dynamic, static or auto, not {s!r}")
     if world_size <= 1:
         return "static"
-    return "dynamic" if s == "auto" else s
+    if s == "auto":
+        enough = ndm is None or (ndm + DYNAMIC_CHUNK - 1) // DYNAMIC_CHUNK >= 4 * world_size
+        return "dynamic" if enough else "static"
+    return s
 
 
 def run_search(args, write: bool = True) -> Optional[SearchResult]:
@@ -428,7 +434,7 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     del packed
     ndm = len(rs.dm_list)
     weights = [len(rs.accel_list(d)) for d in rs.dm_list]
-    schedule = dm_schedule(args, ctx.world_size)
+    schedule = dm_schedule(args, ctx.world_size, ndm)
     pdist.barrier()
     t0 = time.perf_counter()
     if schedule == "dynamic":

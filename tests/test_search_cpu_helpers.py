@@ -32,6 +32,9 @@ def test_dm_schedule_option():
     ok, _, a = _C.parse_cmdline(["peasoup", "-i", "x.fil"])
     assert ok and a.dm_schedule == "auto"
     assert dm_schedule(a, 1) == "static" and dm_schedule(a, 8) == "dynamic"
+    assert dm_schedule(a, 8, 2026) == "dynamic"  # 64 chunks >= 4 per rank
+    assert dm_schedule(a, 8, 113) == "static"    # 4 chunks for 8 ranks
+    assert dm_schedule(a, 2, 225) == "dynamic" and dm_schedule(a, 2, 224) == "static"  # 8 vs 7 chunks
     ok, _, a = _C.parse_cmdline(["peasoup", "-i", "x.fil", "--dm_schedule", "static"])
     assert ok and dm_schedule(a, 8) == "static"
     a.dm_schedule = "roundrobin"
