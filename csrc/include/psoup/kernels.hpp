@@ -291,6 +291,7 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
                           PeakRecord* out, uint32_t* count, hipStream_t s);
 // Tuning: bit 0 = XCD-per-trial block order (default on).
 void harmonic_set_flags(int flags);
+int harmonic_flags();
 // Debug/test: materialise level-h sums [nlevels][nbins] for one spectrum.
 void harmonic_sums(const float* P, uint64_t nbins, int nlevels, float* out, hipStream_t s);
 

@@ -853,7 +853,10 @@ namespace {
 // (tuning: caps workgroups per CU, so fewer tiles -- a smaller gather
 // footprint -- are in flight per XCD); bits 16-23: the same for the tiled
 // r2c kernel (tuning)
-int g_harm_flags = 1;
+// Default 1 | 32 | (10 << 8): XCD order, two-phase staging at 3 levels,
+// 6 workgroups per CU (ABBA same-box bench: 22.55k vs 22.47k trials/s for the
+// one-phase kernel, every pair; profiles/r2_recheck/ab_harm_abba.txt)
+int g_harm_flags = 1 | 32 | (10 << 8);
 
 // Mixed-radix n = m p (p a power of two, m odd): gather of the m strided
 // columns, and the length-m combination with the twiddles W_n^(n1 k)
@@ -1000,6 +1003,7 @@ void fft4_c2r_post(const float2* Z, uint64_t M, const XLayoutArgs& L, float* x, 
 }
 
 void harmonic_set_flags(int flags) { g_harm_flags = flags; }
+int harmonic_flags() { return g_harm_flags; }
 
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
                           PeakRecord* out, uint32_t* count, hipStream_t s) {

@@ -548,6 +548,7 @@ PYBIND11_MODULE(_C, m) {
     kern::harmonic_sums(P<const float>(Pin), nb, nlevels, P<float>(out), S(s));
   });
   k.def("harmonic_set_flags", &kern::harmonic_set_flags);
+  k.def("harmonic_flags", &kern::harmonic_flags);
   k.def("ffa_downsample", [](uintptr_t x, uint64_t n, double f, uintptr_t out, uint64_t nout, uintptr_t s) {
     kern::ffa_downsample(P<const float>(x), n, f, P<float>(out), nout, S(s));
   });

@@ -402,14 +402,17 @@ def test_harmonic_prethreshold_is_exact(nlev, thresh):
     ends = [n] * 6
     Pt = torch.from_numpy(P).to(dev)
     runs = []
+    old = C.kernels.harmonic_flags()
     try:
-        for flags in (1, 3):  # bit 1 disables the pre-threshold
+        # bit 1 disables the pre-threshold; bit 5 = two-phase staging (3 levels),
+        # bits 8-15 = occupancy cap; the default is 1 | 32 | (10 << 8)
+        for flags in (1, 3, 33, 35, 1 | 32 | (10 << 8), old):
             C.kernels.harmonic_set_flags(flags)
             trial, level, idx, snr = ops.harmonic_peaks(Pt, nlev, starts, ends, thresh)
             runs.append(sorted(zip(trial.tolist(), level.tolist(), idx.tolist(), snr.tolist())))
     finally:
-        C.kernels.harmonic_set_flags(1)
-    assert runs[0] == runs[1] and len(runs[0]) > 20
+        C.kernels.harmonic_set_flags(old)
+    assert all(r == runs[0] for r in runs) and len(runs[0]) > 20
     exp = set()
     for k in range(Kb):
         levels = [P[k]] + ref.harmonic_sums(P[k], nlev)
