@@ -314,6 +314,10 @@ class SearchEngine {
   bool zap_ = false;
   int mode_ = 2;        // effective fft_mode
   kern::Fft4Geom f4_;
+  bool fused_ = false;   // fft_mode 2 with the fused pass B (blocked spectrum Pb_, layout pl_)
+  kern::PLayout pl_;
+  DeviceBuffer<float> Pb_;
+  uint64_t pst_ = 1;     // floats per trial of P_
   DeviceBuffer<float2> f4_tab_;
   DeviceBuffer<float> f4_in_;  // padded whitened series read by the fused FFT [max_prep_][insize]
   uint64_t xs_ = 0;     // per-trial stride of spec_ (complex)

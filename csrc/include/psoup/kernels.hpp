@@ -36,6 +36,19 @@ struct PeakRecord {
 };
 static_assert(sizeof(PeakRecord) == 12, "PeakRecord layout");
 
+// Layout of a normalised spectrum P (bins 0..M of an N = 2M point series).
+// blk = 0: natural order.  blk = 1: what the fused pass B
+// (fft4_rowpass_r2c) writes -- with n1 x n2 = M, bins 8J+1 .. 8J+8 are one
+// contiguous 32-byte piece, octet J = r * (n2/8) + g stored at
+// P[g * 8 n1 + r * 8] (each workgroup's output is one contiguous block per
+// octet column g), and bin 0 at P[M].  lg_n1 = log2 n1, lg_g = log2(n2/8).
+struct PLayout {
+  int blk = 0;
+  int lg_n1 = 0;
+  int lg_g = 0;
+  uint32_t M = 0;
+};
+
 constexpr int kMaxHarmLevels = 5;  // 2,4,8,16,32 harmonics (kernels.cu:42-96)
 
 // --------------------------------------------------------- unpack/dedisp ----
@@ -188,6 +201,26 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
 // search needs bins below max_freq only: ~14% of the spectrum at 2^23).
 void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, hipStream_t s,
                   uint64_t nbins_out = 0);
+// Pass B fused with the real-FFT post-processing, interbin and normalise
+// (kFft4FusedR2c): reads pass A's tiled Y and writes the normalised spectrum
+// P (bins 0..M) in the blocked layout fft4_p_layout(g), trial k at
+// P + k*pstride (pstride >= M + 1 and a multiple of 8 floats), normalised with
+// (stats + 4*tsrc[k])[0, 2] * nscale (tsrc optional).  32-byte pieces whose
+// bins all lie at or beyond nbins_out are not stored.  Needs n1 in
+// {512, 1024, 2048} and n2 >= 128 (fft4_fused_r2c_ok).
+bool fft4_fused_r2c_ok(const Fft4Geom& g);
+PLayout fft4_p_layout(const Fft4Geom& g);
+void fft4_rowpass_r2c(const float2* Y, float* P, uint64_t pstride, int K, const Fft4Geom& g, const float2* tables,
+                      const float* stats, float nscale, const uint32_t* tsrc, uint64_t nbins_out, hipStream_t s);
+// Blocked (fft4_rowpass_r2c) -> natural spectra for the harmonic sum: bin b
+// of trial k at out + k*stride + 3 + b (so the 32-byte pieces stay aligned;
+// pass out + 3 as the natural spectrum).  stride >= M + 4, multiple of 4;
+// bins >= nbins_out (0 = all) are not written.
+void p_unblock(const float* in, float* out, uint64_t stride, int K, const PLayout& L, uint64_t nbins_out,
+               hipStream_t s);
+// Copy of K spectra (M + 1 bins each, stride floats apart) between natural
+// order and layout L: dir 0 natural -> L, dir 1 L -> natural (tests, tools).
+void p_relayout(const float* in, float* out, uint64_t stride, int K, const PLayout& L, int dir, hipStream_t s);
 // Row-octet blocks (8 rows k1 each) r2c_interbin_normalise_tiled runs for
 // bins < nbins_out; it reads spectrum rows k1 <= 8*ny and k1 >= n1 - 8*ny.
 inline uint32_t r2c_tiled_row_blocks(uint64_t nbins_out, int n1, int n2) {
@@ -270,6 +303,8 @@ enum Fft4Flags : int {
   kFft4OneXSmall = 1048576,   // with kFft4OneX: also at column lengths 512 and 1024 (the Stockham pass A is
                               // faster there: bench at 2^22 40.4k vs 37.3k, at 2^21 55.5k vs 53.4k trials/s)
   kFft4OneXRow = 524288,      // pass B (tiled Y and X, row length 512..2048): the one-exchange structure
+  kFft4FusedR2c = 2097152,    // search batches: pass B + r2c + interbin + normalise in one kernel
+                              // (fft4_rowpass_r2c; blocked spectrum layout read by the harmonic sum)
 };
 void fft4_set_flags(int flags);
 // Debug: per-workgroup phase timestamps of the fft4 passes (12 x u64 per block), nullptr = off.
@@ -287,8 +322,9 @@ struct HarmParams {
 // Fused incoherent harmonic sum + threshold + compaction: never writes the
 // summed spectra.  Records land unordered; count may exceed capacity (then
 // the caller re-runs with a bigger buffer).
+// P in layout L (natural by default; the fused pass B's blocked layout).
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
-                          PeakRecord* out, uint32_t* count, hipStream_t s);
+                          PeakRecord* out, uint32_t* count, hipStream_t s, const PLayout& L = PLayout{});
 // Tuning: bit 0 = XCD-per-trial block order (default on).
 void harmonic_set_flags(int flags);
 int harmonic_flags();

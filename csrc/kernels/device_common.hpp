@@ -6,6 +6,7 @@
 #include <cstdint>
 
 #include "psoup/common.hpp"
+#include "psoup/kernels.hpp"
 
 namespace psoup {
 namespace kern {
@@ -137,6 +138,28 @@ __device__ __forceinline__ uint32_t accel_index_ii32(double af, double size, uin
   const double r = accel_pos_ii(af, size, static_cast<double>(id));
   const double rr = fmin(fmax(rint(r), 0.0), static_cast<double>(nmax));
   return static_cast<uint32_t>(rr);
+}
+
+// Real-input FFT bin from the half-length complex FFT Z of the packed series:
+//   X[k] = (Z[k] + conj Z[M-k])/2 - i/2 e^{-i pi k/M} (Z[k] - conj Z[M-k]),
+// za = Z[k], zb = Z[M-k], (c, s) = (cos, sin) of -pi k / M; X[M-k] is
+// r2c_combine(zb, za, -c, s).  Explicit FMAs: identical rounding in every
+// kernel that forms it.
+__device__ __forceinline__ float2 r2c_combine(float2 za, float2 zb, float c, float s) {
+  const float ex = 0.5f * (za.x + zb.x), ey = 0.5f * (za.y - zb.y);
+  const float dx = 0.5f * (za.x - zb.x), dy = 0.5f * (za.y + zb.y);
+  const float ox = dy, oy = -dx;  // -i * d
+  return make_float2(__builtin_fmaf(-s, oy, __builtin_fmaf(c, ox, ex)), __builtin_fmaf(s, ox, __builtin_fmaf(c, oy, ey)));
+}
+
+// Index of spectrum bin i in a PLayout (kernels.hpp): natural, or the octet
+// blocks the fused pass B writes (bins 8J+1..8J+8 contiguous, octet
+// J = r n2/8 + g at P[g][r][.], bin 0 after the last block).
+__device__ __forceinline__ uint32_t paddr(uint32_t i, const PLayout& L) {
+  if (!L.blk) return i;
+  if (i == 0) return L.M;
+  const uint32_t s = i - 1, J = s >> 3;
+  return ((J & ((1u << L.lg_g) - 1u)) << (L.lg_n1 + 3)) + ((J >> L.lg_g) << 3) + (s & 7u);
 }
 
 }  // namespace dev

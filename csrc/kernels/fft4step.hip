@@ -280,9 +280,11 @@ __device__ __forceinline__ void load_resampled(const float* __restrict__ in, con
 
 // Table layout (float2): [tw_N2 (N2)] [tw_N1 (N1)] [lo (2^kSplit)] [hi (M >> kSplit)]
 // [ox (N1 x GX)]: ox[col * GX + k2] = W_M^{col P k2}, the k2 part of the
-// one-exchange pass A's four-step twiddles (GX = onex_g(N2), P = N2 / GX).
+// one-exchange pass A's four-step twiddles (GX = onex_g(N2), P = N2 / GX);
+// [rk (N1)]: e^{-i pi m / N1} and [rc (N2/2 + 16)]: e^{-i pi c / M}, the
+// real-FFT twiddle e^{-i pi (c + N2 k1) / M} = rc[c] rk[k1] of the fused pass B.
 struct TableOffsets {
-  uint64_t n2, n1, lo, hi, ox, total;
+  uint64_t n2, n1, lo, hi, ox, rk, rc, total;
 };
 __host__ __device__ constexpr int onex_g(int N2) { return N2 >= 2048 ? 64 : 32; }
 __host__ __device__ inline TableOffsets table_offsets(int N1, int N2) {
@@ -293,7 +295,9 @@ __host__ __device__ inline TableOffsets table_offsets(int N1, int N2) {
   o.lo = o.n1 + N1;
   o.hi = o.lo + (1u << kSplit);
   o.ox = o.hi + (M >> kSplit);
-  o.total = o.ox + static_cast<uint64_t>(N1) * onex_g(N2);
+  o.rk = o.ox + static_cast<uint64_t>(N1) * onex_g(N2);
+  o.rc = o.rk + N1;
+  o.total = o.rc + N2 / 2 + 16;
   return o;
 }
 
@@ -1007,6 +1011,207 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pass B fused with the real-FFT post-processing, interbin and normalise
+// (kFft4FusedR2c).  Replaces pass B's complex spectrum X (written, then read
+// back by r2c_interbin_tiled: 33.5 + 33.5 MB per 2^23 trial) with the
+// normalised amplitudes P (16.7 MB written once).
+//
+// Bin k = c + n2 k1 of Z = FFT_M(z) is pass-B row c at point k1.  The real
+// spectrum needs the pair Z[k], Z[M-k], and M - k = (n2 - c) + n2 (n1-1-k1)
+// (c > 0): rows c and n2 - c with the points reversed.  Running the mirror
+// row's DFT on y'[i] = conj(y[i]) W_n1^i gives, at point k1,
+//   sum_i conj(y[i]) W^i W^{i k1} = conj(sum_i y[i] W^{i(n1-1-k1)}) = conj(Z[M-k])
+// (row 0 pairs with itself at n1 - k1: y' = conj(y)), so the thread holding
+// Z[k] in the ascending group holds conj(Z[M-k]) at the same position of the
+// mirror group: pairing is a same-thread LDS hand-over, no permutation.
+//
+// Workgroup o (two groups of n1/8 threads, Stockham engine, 9 transforms per
+// thread) runs rows c = 8o .. 8o+8 and their mirrors n2 - c, and emits
+//   ascending bins c = 8o+1 .. 8o+8 (interbin neighbour c - 1: same thread),
+//   mirror bins M - k, c = 8o .. 8o+7 (neighbour M - (k+1): row c + 1),
+// i.e. the octets [8J+1, 8J+8] of PLayout blk (one extra row per group, +12.5%
+// loads, instead of cross-workgroup halos).  Octet column g of the layout is
+// one contiguous block P[g][k1][8] per workgroup, so every wave stores 2 KiB
+// contiguous; natural-order stores would be 32-byte pieces n2*4 bytes apart
+// (~1.5 TB/s, docs/ROADMAP.md).  The harmonic sum reads the blocked layout.
+// Reference: src/pipeline_multi.cu:216-224 (R2C -> form_interpolated ->
+// normalise), src/kernels.cu:231-252, 469-494.
+template <int L>
+struct FusedR2c {
+  static constexpr int T = L / kPts;  // threads per group
+  static constexpr int THREADS = 2 * T;
+  static constexpr int CPT = 9;  // rows 8o .. 8o+8 (or their mirrors)
+  static constexpr int CG = 3;   // channels per exchange round
+  static constexpr int PAD = L + L / 8 + kChanPad;
+  static constexpr int GROUP_FLOATS = 2 * CG * PAD;
+  static constexpr int FFT_FLOATS = 2 * GROUP_FLOATS;
+  static constexpr int PAIR_FLOATS = 2 * 2 * (CPT * 4 * T);  // both groups hand over 4 points x 9 rows
+  static constexpr int LDS_FLOATS = FFT_FLOATS > PAIR_FLOATS ? FFT_FLOATS : PAIR_FLOATS;
+  static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
+};
+
+template <int L>
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, FusedR2c<L>::THREADS), amdgpu_waves_per_eu(2)))
+fft4_rowpass_r2c_kernel(const float2* __restrict__ Y, float* __restrict__ P, uint64_t pstride, int K, Fft4Geom g,
+                        const float2* __restrict__ tab, const float* __restrict__ stats, float nscale,
+                        const uint32_t* __restrict__ tsrc, uint32_t nbins_out) {
+  using C = FusedR2c<L>;
+  constexpr int T = C::T, CPT = C::CPT;
+  __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
+  const int grp = threadIdx.x >= T ? 1 : 0;  // 0: rows 8o + j, 1: rows n2 - 8o - j
+  const int t = threadIdx.x - grp * T;
+  const int n2 = g.n2;
+  const int ng = n2 >> 3;  // octet columns
+  const int k = static_cast<int>(blockIdx.x % static_cast<uint32_t>(K));
+  const int o = static_cast<int>(blockIdx.x / static_cast<uint32_t>(K));
+  const TableOffsets to = table_offsets(L, n2);
+  const float2* twL = tab + to.n1;
+  const float2* yk = Y + static_cast<uint64_t>(k) * g.ystride;
+  trace_event(0);
+  Vec<CPT> v;
+  {
+    // tiled Y: row c, point i at (i >> 3) * 8 n2 + (c >> 3) * 64 + (i & 7) * 8 + (c & 7)
+    const int oc = grp == 0 ? o : ng - 1 - o;           // the group's full octet
+    const int ox = grp == 0 ? o + 1 : (ng - o) & (ng - 1);  // octet of the ninth row (position 0)
+#pragma unroll
+    for (int q = 0; q < kPts; ++q) {
+      const uint32_t i = static_cast<uint32_t>(t + q * T);
+      const float2* base = yk + static_cast<uint64_t>(i >> 3) * (8ull * n2) + (i & 7) * 8;
+      const float4* src = reinterpret_cast<const float4*>(base + oc * 64);
+      float2 r[8];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 w = src[u];
+        r[2 * u] = make_float2(w.x, w.y);
+        r[2 * u + 1] = make_float2(w.z, w.w);
+      }
+      const float2 r9 = base[ox * 64];
+      if (grp == 0) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[j][q] = r[j];
+        v[8][q] = r9;
+      } else {
+        // channel j = row n2 - 8o - j: j = 0 is the ninth row, j = 1..8 are positions 7..0
+        const float2 w = twL[i];
+        v[0][q] = o == 0 ? make_float2(r9.x, -r9.y)  // row 0 pairs with itself (point n1 - k1)
+                         : make_float2(r9.x * w.x + r9.y * w.y, r9.x * w.y - r9.y * w.x);
+#pragma unroll
+        for (int j = 1; j < 9; ++j) {
+          const float2 a = r[8 - j];
+          v[j][q] = make_float2(a.x * w.x + a.y * w.y, a.x * w.y - a.y * w.x);  // conj(a) W^i
+        }
+      }
+    }
+  }
+  trace_event(1);
+  fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, twL);
+
+  const uint32_t M = static_cast<uint32_t>(L) * static_cast<uint32_t>(n2);
+  const float* st = stats + (tsrc ? 4u * tsrc[k] : 0u);
+  const float mean = st[0] * nscale, rsig = 1.0f / (st[2] * nscale);
+  float* pk = P + static_cast<uint64_t>(k) * pstride;
+  const float2* rk = tab + to.rk;             // e^{-i pi k1 / n1}
+  const float2* rc = tab + to.rc + 8 * o;     // e^{-i pi c / M}, c = 8o + j
+  // hand-over: group 0 emits points q = 0..3, group 1 points 4..7 (one round,
+  // 9 rows x 4 points x T float2 per group); both groups then run one code
+  // path (wave-uniform selects), which keeps the kernel small enough for the
+  // instruction cache
+  float2* pb = reinterpret_cast<float2*>(lds);
+  auto slot = [&](int from, int j, int qq) { return pb + ((from * CPT + j) * 4 + qq) * T + t; };
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq)
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) *slot(grp, j, qq) = grp == 0 ? v[j][4 + qq] : v[j][qq];
+  __syncthreads();
+  trace_event(9);
+#pragma unroll
+  for (int qq = 0; qq < 4; ++qq) {
+    // za = Z[c + n2 k1] (rows 8o + j), zb = Z[M - (c + n2 k1)]
+    const uint32_t k1 = static_cast<uint32_t>(t + (grp * 4 + qq) * T);
+    const float2 w1 = rk[k1];
+    float2 xa[CPT], xm[CPT];
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const float2 other = *slot(1 - grp, j, qq);
+      const float2 za = grp == 0 ? v[j][qq] : other;
+      const float2 cz = grp == 0 ? other : v[j][4 + qq];
+      const float2 wc = rc[j];
+      const float wx = __builtin_fmaf(wc.x, w1.x, -(wc.y * w1.y)), wy = __builtin_fmaf(wc.x, w1.y, wc.y * w1.x);
+      const float2 zb = make_float2(cz.x, -cz.y);
+      xa[j] = dev::r2c_combine(za, zb, wx, wy);
+      xm[j] = dev::r2c_combine(zb, za, -wx, wy);
+    }
+    float pa[8], pm[8];
+#pragma unroll
+    for (int j = 1; j <= 8; ++j) pa[j - 1] = (dev::interbin(xa[j], xa[j - 1]) - mean) * rsig;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pm[7 - j] = (dev::interbin(xm[j], xm[j + 1]) - mean) * rsig;
+    const uint32_t base = static_cast<uint32_t>(8 * o) + static_cast<uint32_t>(n2) * k1;  // c = 8o
+    if (base + 1 < nbins_out) {  // ascending bins base+1 .. base+8: octet column o, row k1
+      f4v* d = reinterpret_cast<f4v*>(pk + (static_cast<uint64_t>(o) * L + k1) * 8);
+      d[0] = f4v{pa[0], pa[1], pa[2], pa[3]};
+      d[1] = f4v{pa[4], pa[5], pa[6], pa[7]};
+    }
+    if (M - base - 7 < nbins_out) {  // mirror bins M-base-7 .. M-base: column ng-1-o, row n1-1-k1
+      f4v* d = reinterpret_cast<f4v*>(pk + (static_cast<uint64_t>(ng - 1 - o) * L + (L - 1 - k1)) * 8);
+      d[0] = f4v{pm[0], pm[1], pm[2], pm[3]};
+      d[1] = f4v{pm[4], pm[5], pm[6], pm[7]};
+    }
+    if (o == 0 && k1 == 0) pk[M] = (dev::interbin(xa[0], make_float2(0.f, 0.f)) - mean) * rsig;  // bin 0
+  }
+  trace_event(11);
+}
+
+// natural <-> blocked spectrum copy (tests and tools)
+__global__ void __launch_bounds__(256) p_relayout_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                         uint64_t stride, PLayout L, int dir) {
+  in += blockIdx.y * stride;
+  out += blockIdx.y * stride;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i <= L.M; i += gridDim.x * blockDim.x) {
+    const uint32_t b = dev::paddr(i, L);
+    if (dir == 0)
+      out[b] = in[i];
+    else
+      out[i] = in[b];
+  }
+}
+
+// Blocked -> natural spectrum transpose for the harmonic sum (its gathers
+// need natural-order ranges: on the blocked layout every 16-byte load of a
+// wave touches its own 32-byte piece, 4x the cache-line requests, and the
+// harmonic kernel ran 2.1x slower).  A workgroup moves 16 octet columns x 16
+// rows of 32-byte pieces through LDS: 16 lanes read 512 contiguous bytes of
+// one octet column and write 512 contiguous bytes of one natural row.
+// Natural bin b lands at out + 3 + b (pieces 16-byte aligned when out is).
+__global__ void __launch_bounds__(256) p_unblock_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                        uint64_t stride, PLayout L, uint32_t nbins_out) {
+  __shared__ float4 tile[16][33];  // [row][2 * column + half], padded
+  const uint32_t ng = 1u << L.lg_g, n1 = 1u << L.lg_n1;
+  const uint32_t gblocks = ng >> 4;
+  const uint32_t g0 = (blockIdx.x % gblocks) * 16, r0 = (blockIdx.x / gblocks) * 16;
+  const float* pb = in + blockIdx.y * stride;
+  float* pn = out + blockIdx.y * stride + 3;
+  const uint32_t ngb = ng * 8;  // bins per row
+  if (r0 * ngb + 1 >= nbins_out) return;  // the whole tile lies at or beyond nbins_out
+  const int t = threadIdx.x;
+  {
+    const uint32_t g = g0 + (t >> 4), r = r0 + (t & 15);
+    const float4* src = reinterpret_cast<const float4*>(pb + (static_cast<uint64_t>(g) * n1 + r) * 8);
+    tile[t & 15][2 * (t >> 4)] = src[0];
+    tile[t & 15][2 * (t >> 4) + 1] = src[1];
+  }
+  __syncthreads();
+  const uint32_t r = r0 + (t >> 4), g = g0 + (t & 15);
+  const uint32_t b = r * ngb + g * 8 + 1;  // first bin of the piece
+  if (b < nbins_out) {
+    float4* dst = reinterpret_cast<float4*>(pn + b);
+    dst[0] = tile[t >> 4][2 * (t & 15)];
+    dst[1] = tile[t >> 4][2 * (t & 15) + 1];
+  }
+  if (blockIdx.x == 0 && t == 0) pn[0] = pb[L.M];  // bin 0
+}
+
 bool supported_len(int L) { return L >= 128 && L <= 4096 && (L & (L - 1)) == 0; }
 
 }  // namespace
@@ -1047,6 +1252,8 @@ std::vector<float2> fft4_tables(const Fft4Geom& g) {
   const uint64_t Mi = static_cast<uint64_t>(g.n1) * static_cast<uint64_t>(g.n2);
   for (uint64_t col = 0; col < static_cast<uint64_t>(g.n1); ++col)
     for (uint64_t k2 = 0; k2 < GX; ++k2) t[o.ox + col * GX + k2] = w(static_cast<double>((col * PX * k2) % Mi), M);
+  for (int m = 0; m < g.n1; ++m) t[o.rk + m] = w(m, 2.0 * g.n1);
+  for (uint64_t c = 0; c < o.total - o.rc; ++c) t[o.rc + c] = w(static_cast<double>(c), 2.0 * M);
   return t;
 }
 
@@ -1214,6 +1421,65 @@ void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const fl
   else
     launch_rowpass<4, 2, 0>(Y, X, K, g, tables, grid, f, s);
   post_launch_check("fft4_rowpass_kernel", s);
+}
+
+bool fft4_fused_r2c_ok(const Fft4Geom& g) {
+  const int f = g_fft4_flags;
+  return g.ok && (f & kFft4FusedR2c) && (f & kFft4Blocked) && (f & kFft4TileY) && !(f & kTimingFlags) &&
+         (g.n1 == 512 || g.n1 == 1024 || g.n1 == 2048) && g.n2 >= 128;
+}
+
+PLayout fft4_p_layout(const Fft4Geom& g) {
+  PLayout l;
+  l.blk = 1;
+  l.lg_n1 = __builtin_ctz(static_cast<unsigned>(g.n1));
+  l.lg_g = __builtin_ctz(static_cast<unsigned>(g.n2 / 8));
+  l.M = static_cast<uint32_t>(g.n1) * static_cast<uint32_t>(g.n2);
+  return l;
+}
+
+void fft4_rowpass_r2c(const float2* Y, float* P, uint64_t pstride, int K, const Fft4Geom& g, const float2* tables,
+                      const float* stats, float nscale, const uint32_t* tsrc, uint64_t nbins_out, hipStream_t s) {
+  PSOUP_CHECK(fft4_fused_r2c_ok(g) && K >= 1, "fft4 rowpass_r2c: unsupported geometry/flags");
+  const uint64_t M = static_cast<uint64_t>(g.n1) * g.n2;
+  PSOUP_CHECK(M < (1ull << 31) && pstride >= M + 1 && pstride % 8 == 0, "fft4 rowpass_r2c: P stride " << pstride);
+  PSOUP_CHECK((reinterpret_cast<uintptr_t>(P) & 31) == 0 && (reinterpret_cast<uintptr_t>(Y) & 15) == 0,
+              "fft4 rowpass_r2c: alignment");
+  const uint64_t nblocks = static_cast<uint64_t>(g.n2 / 16) * K;
+  PSOUP_CHECK(nblocks < (1ull << 31), "fft4 rowpass_r2c: grid");
+  const uint32_t nbo = static_cast<uint32_t>(std::min<uint64_t>(nbins_out == 0 ? M + 1 : nbins_out, M + 1));
+  const dim3 grid(static_cast<unsigned>(nblocks));
+  switch (g.n1) {
+#define PS_FUSED(LL)                                                                                           \
+  case LL:                                                                                                     \
+    fft4_rowpass_r2c_kernel<LL><<<grid, FusedR2c<LL>::THREADS, 0, s>>>(Y, P, pstride, K, g, tables, stats, nscale, \
+                                                                      tsrc, nbo);                             \
+    break;
+    PS_FUSED(512) PS_FUSED(1024) PS_FUSED(2048)
+#undef PS_FUSED
+    default: PSOUP_THROW("fft4 rowpass_r2c: row length " << g.n1);
+  }
+  post_launch_check("fft4_rowpass_r2c_kernel", s);
+}
+
+void p_unblock(const float* in, float* out, uint64_t stride, int K, const PLayout& L, uint64_t nbins_out,
+               hipStream_t s) {
+  PSOUP_CHECK(L.blk && L.lg_g >= 4 && L.lg_n1 >= 4, "p_unblock: needs n2 >= 128 and n1 >= 16");
+  PSOUP_CHECK(K >= 1 && K <= 65535 && stride >= static_cast<uint64_t>(L.M) + 4 && stride % 4 == 0,
+              "p_unblock: bad shape");
+  PSOUP_CHECK((reinterpret_cast<uintptr_t>(in) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0,
+              "p_unblock: alignment");
+  const uint32_t nbo = static_cast<uint32_t>(std::min<uint64_t>(nbins_out == 0 ? L.M + 1ull : nbins_out, L.M + 1ull));
+  const dim3 grid((L.M / 8) / 256, static_cast<unsigned>(K));
+  p_unblock_kernel<<<grid, 256, 0, s>>>(in, out, stride, L, nbo);
+  post_launch_check("p_unblock_kernel", s);
+}
+
+void p_relayout(const float* in, float* out, uint64_t stride, int K, const PLayout& L, int dir, hipStream_t s) {
+  PSOUP_CHECK(K >= 1 && K <= 65535 && stride >= static_cast<uint64_t>(L.M) + 1, "p_relayout: bad shape");
+  const dim3 grid(dev::grid_for(static_cast<uint64_t>(L.M) + 1, 256, 4096), static_cast<unsigned>(K));
+  p_relayout_kernel<<<grid, 256, 0, s>>>(in, out, stride, L, dir);
+  post_launch_check("p_relayout_kernel", s);
 }
 
 }  // namespace kern

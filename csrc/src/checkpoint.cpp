@@ -25,7 +25,15 @@ namespace {
 
 constexpr uint32_t kSpillMagic = 0x4B435350u;  // "PSCK"
 constexpr uint32_t kSpillVersion = 1;
-constexpr int kIdentityVersion = 1;
+// Bump kIdentityVersion whenever the per-DM candidate numerics change in a
+// way the build id below does not capture; PSOUP_NUMERICS_ID (generated at
+// build time from the kernel and engine sources, cmake/numerics_id.cmake)
+// changes with every edit of those sources, so spills written by another
+// build are never mixed into a resumed run.
+constexpr int kIdentityVersion = 2;
+#ifndef PSOUP_NUMERICS_ID
+#include "psoup_numerics_id.hpp"
+#endif
 
 struct SpillHeader {
   uint32_t magic;
@@ -43,10 +51,23 @@ std::string hex64(uint64_t v) {
 }
 
 // Size and sampled-content hash of a file; "absent" when it cannot be opened.
+// Sampled fingerprints (large inputs) also carry the inode and the
+// modification time in nanoseconds: a file regenerated in place with the
+// same size, differing outside the sampled blocks, still changes its key.
 std::string file_fingerprint(const std::string& path, bool sample_only) {
   if (path.empty()) return "none";
   std::ifstream in(path, std::ios::binary);
   if (!in) return "absent";
+  std::string stamp;
+  if (sample_only) {
+    struct stat sb {};
+    if (::stat(path.c_str(), &sb) == 0) {
+      std::ostringstream st;
+      st << ", inode " << sb.st_ino << ", mtime " << sb.st_mtim.tv_sec << "." << std::setw(9) << std::setfill('0')
+         << sb.st_mtim.tv_nsec;
+      stamp = st.str();
+    }
+  }
   in.seekg(0, std::ios::end);
   const uint64_t size = static_cast<uint64_t>(in.tellg());
   uint64_t h = fnv1a64(&size, sizeof(size));
@@ -67,7 +88,7 @@ std::string file_fingerprint(const std::string& path, bool sample_only) {
     }
   }
   std::ostringstream os;
-  os << size << " bytes, hash " << hex64(h);
+  os << size << " bytes, hash " << hex64(h) << stamp;
   return os.str();
 }
 
@@ -93,6 +114,7 @@ RunIdentity make_run_identity(const CmdLineOptions& a, const SigprocHeader& hdr)
   os << std::setprecision(9);
   const uint64_t fft = a.size == 0 ? prev_power_of_two(static_cast<uint64_t>(hdr.nsamples)) : a.size;
   os << "peasoup-amd checkpoint identity v" << kIdentityVersion << "\n";
+  os << "build: " << PSOUP_NUMERICS_ID << "\n";
   os << "input: " << canonical_path(a.infilename) << "\n";
   os << "input_file: " << file_fingerprint(a.infilename, true) << "\n";
   os << "header: tsamp=" << std::setprecision(17) << hdr.tsamp << " fch1=" << hdr.fch1 << " foff=" << hdr.foff

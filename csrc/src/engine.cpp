@@ -548,6 +548,20 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
       hp_.start[h] = hp_.end[h] = 0;
     }
   }
+  // Fused pass B (kFft4FusedR2c): writes the normalised spectrum itself, in
+  // the blocked layout, for the whole spectrum.  The unfused path prunes its
+  // stores to bins < hi_ instead, which moves fewer bytes only when under
+  // ~8% of the spectrum is searched (few harmonics, low max_freq).
+  fused_ = mode_ == 2 && kern::fft4_fused_r2c_ok(f4_) && static_cast<uint64_t>(hi_) >= nb_ / 8;
+  if (const char* e = std::getenv("PSOUP_FUSED_R2C")) fused_ = fused_ && std::atoi(e) != 0;
+  if (fused_) {
+    // blocked spectra Pb_ -> p_unblock -> natural spectra P_ (offset 3: aligned pieces)
+    pl_ = kern::fft4_p_layout(f4_);
+    pst_ = (n_ / 2 + 4 + 7) / 8 * 8;
+  } else {
+    pl_ = kern::PLayout{};
+    pst_ = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
+  }
   // batch size
   {
     // auto budget: capped by the device's free memory shared among its engines
@@ -555,7 +569,7 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
       budget = std::min(budget, free_b / 10 * 7 / static_cast<size_t>(std::max(1, p_.engines_per_device)));
-    const size_t per = n_ * 4 + nb_ * 8 + static_cast<size_t>(hi_) * 4;  // Y/res + X/spec + P per trial
+    const size_t per = n_ * 4 + (fused_ ? pst_ * 4 : nb_ * 8) + pst_ * 4;  // Y/res + X/spec or Pb + P per trial
     auto round_batch = [](size_t k) {
       int K = static_cast<int>(std::min<size_t>(256, std::max<size_t>(1, k)));
       if (K >= 32) K = K / 16 * 16;  // halves stay multiples of 8 (XCD-grouped kernels)
@@ -619,8 +633,11 @@ void SearchEngine::ensure_batch_buffers(int k) {
   buf_k_ = k;
   const uint64_t rs = mode_ == 2 ? 2 * f4_.ystride : n_;  // floats per trial
   res_.resize(static_cast<uint64_t>(k) * rs);
-  spec_.resize(static_cast<uint64_t>(k) * xs_);
-  P_.resize(static_cast<uint64_t>(k) * std::max<uint64_t>(1, static_cast<uint64_t>(hi_)));
+  if (fused_)
+    Pb_.resize(static_cast<uint64_t>(k) * pst_);
+  else
+    spec_.resize(static_cast<uint64_t>(k) * xs_);
+  P_.resize(static_cast<uint64_t>(k) * pst_);
 }
 
 FftPlan& SearchEngine::batch_plan(int count) {
@@ -639,7 +656,7 @@ FftPlan& SearchEngine::batch_plan(int count) {
 void SearchEngine::launch_batch(Slot& s, int first, int count) {
   s.first = first;
   s.count = count;
-  const uint64_t pst = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
+  const uint64_t pst = pst_;
   const kern::Fft4XLayout xl =
       mode_ == 2 ? kern::fft4_x_layout(f4_) : kern::Fft4XLayout{ilog2(n_ / 2), n_ / 2, 8, 3, false};
   PSOUP_HIP_CHECK(hipMemsetAsync(s.d_count.data(), 0, sizeof(uint32_t), stream_));
@@ -653,11 +670,10 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
     if (phase_ >> stage & 1) phase_ev_[stage].record(st);
   };
   auto run = [&](int b, int c, hipStream_t st, int j) {
-    float* P = P_.data() + static_cast<uint64_t>(b) * pst;
+    float* P = P_.data() + static_cast<uint64_t>(b) * pst + (fused_ ? 3 : 0);  // natural spectra
     if (mode_ == 2) {
       // res_ holds the four-step intermediates Y (complex, ystride per trial)
       float2* Y = reinterpret_cast<float2*>(res_.data()) + static_cast<uint64_t>(b) * f4_.ystride;
-      float2* X = spec_.data() + static_cast<uint64_t>(b) * xs_;
       // trial first+b+i resamples prepared series d_src_[first+b+i] and is
       // normalised with that series' whitening stats
       const uint32_t* src = d_src_.data() + first + b;
@@ -670,16 +686,28 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
                                   st);
       gate_out(0, st);
       gate_in(1, j, st);
-      kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st, static_cast<uint64_t>(hi_));
-      gate_out(1, st);
-      gate_in(2, j, st);
-      if (xl.tiled)
-        kern::r2c_interbin_normalise_tiled(X, f4_.n1, f4_.n2, xs_, P, pst, c, static_cast<uint64_t>(hi_),
-                                           wstats_.data(), static_cast<float>(n_), st, src);
-      else
-        kern::r2c_interbin_normalise_batch(X, n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch, xl.log2_blk,
-                                           P, pst, c, static_cast<uint64_t>(hi_), wstats_.data(),
-                                           static_cast<float>(n_), st, src);
+      if (fused_) {
+        // pass B + r2c + interbin + normalise in one kernel (blocked layout
+        // pl_), then the blocked -> natural transpose the harmonic sum reads
+        float* Pb = Pb_.data() + static_cast<uint64_t>(b) * pst;
+        kern::fft4_rowpass_r2c(Y, Pb, pst, c, f4_, f4_tab_.data(), wstats_.data(), static_cast<float>(n_), src,
+                               static_cast<uint64_t>(hi_), st);
+        gate_out(1, st);
+        gate_in(2, j, st);
+        kern::p_unblock(Pb, P - 3, pst, c, pl_, static_cast<uint64_t>(hi_), st);
+      } else {
+        float2* X = spec_.data() + static_cast<uint64_t>(b) * xs_;
+        kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st, static_cast<uint64_t>(hi_));
+        gate_out(1, st);
+        gate_in(2, j, st);
+        if (xl.tiled)
+          kern::r2c_interbin_normalise_tiled(X, f4_.n1, f4_.n2, xs_, P, pst, c, static_cast<uint64_t>(hi_),
+                                             wstats_.data(), static_cast<float>(n_), st, src);
+        else
+          kern::r2c_interbin_normalise_batch(X, n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch, xl.log2_blk,
+                                             P, pst, c, static_cast<uint64_t>(hi_), wstats_.data(),
+                                             static_cast<float>(n_), st, src);
+      }
     } else {
       kern::resample_batch(cur_tim_, n_, res_.data(), n_, af_.data() + first, c, st);
       batch_plan(c).execute(res_.data(), spec_.data(), st);

@@ -97,6 +97,9 @@ class RankSearcher:
         self.header = dict(header)
         self.header["nsamples"] = int(nsamps)
         params, dm_list, kill, fft_size, cfreq = _C.search_params_from_args(args, self.header)
+        # constructor overrides of the options: the checkpoint identity is
+        # built from args, so spills are refused under an override (search())
+        self._overrides = [n for n, v in (("killmask", killmask), ("fft_mode", fft_mode)) if v is not None]
         if killmask is not None:
             kill = list(killmask)
         if fft_mode is not None:
@@ -198,6 +201,9 @@ class RankSearcher:
         processed = 0
         ckey = 0
         if ckdir:
+            if self._overrides:
+                raise ValueError(f"checkpoint_dir with RankSearcher overrides {self._overrides}: the spill identity "
+                                 "covers the command-line options only; pass them through args instead")
             # spills are bound to this run's identity (input, header, options):
             # a spill of another run, or a corrupt/truncated one, is recomputed
             ckey = _C.prepare_checkpoint_dir(ckdir, self.args, self.header)
