@@ -162,7 +162,13 @@ def main() -> int:
             "ms_per_step": round(ms_per_step, 3),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_TRIALS_PER_S, 2),
+            # BASELINE.json publishes no number for this metric: no ratio is
+            # claimed; the N log N extrapolation of the 2^17 golden run is
+            # reported separately, labelled as such
+            "vs_baseline": None,
+            "vs_extrapolated_reference": round(value / BASELINE_TRIALS_PER_S, 2),
+            "baseline_note": "no published reference number; 6.6 trials/s = the 2^17 golden run (2x C2070, "
+                             "573 trials/s) scaled by N log N to 2^23 -- orientation only",
             "dtype": "fp32",
             "data": "synthetic (uniform 2-bit noise filterbank, random seed)",
             "config": {

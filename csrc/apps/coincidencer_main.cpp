@@ -23,6 +23,8 @@ int main(int argc, char** argv) {
   if (exit_now) return 0;
   try {
     const int nfiles = static_cast<int>(args.filterbanks.size());
+    // per-sample beam counts are uint8 (kern::count_above): more beams would wrap
+    PSOUP_CHECK(nfiles <= 255, nfiles << " beams: the coincidencer counts beams in uint8, at most 255");
     std::vector<Filterbank> fbs;
     for (const auto& f : args.filterbanks) fbs.push_back(Filterbank::from_file(f));
     std::vector<uint64_t> lens;

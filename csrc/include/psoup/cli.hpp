@@ -46,7 +46,9 @@ struct CmdLineOptions {
   std::string dedisp_kernel = "auto";       // auto | mfma | direct
   int accel_batch = 0;                      // 0 = auto (sized for HBM)
   int engines_per_gpu = 0;                  // search engines (streams + host threads) per GPU, 0 = auto
-  std::string dm_schedule = "auto";         // multi-rank DM distribution: dynamic | static | auto (= dynamic)
+  std::string dm_schedule = "auto";         // multi-rank DM distribution: dynamic | static | auto (dynamic with
+                                            // >= 2 ranks and >= 4 32-DM chunks per rank, else static; an
+                                            // explicit dynamic also runs the queue on one rank)
   int sub_batch = -1;                       // -1 = auto
   int fft_mode = 2;                         // see SearchParams::fft_mode
   bool use_boundaries = false;              // honour --boundary_* (reference ignores them)

@@ -89,10 +89,16 @@ class Dedisperser {
   DedispKernel choose(int d0, int d1);
   // resident-plan MFMA steps per (tile, active channel) over [d0, d1)'s tiles
   double mfma_steps_per_channel(int d0, int d1);
+  // Auto's split of a tile-aligned range: DMs [d0, split) run the LDS-fed
+  // MFMA kernel (leading tiles whose offset spread is narrow enough for the
+  // one-hot GEMM to beat the VALU kernels), [split, d1) the VALU kernels
+  int mfma_lds_split(int d0, int d1);
 
  private:
   void build_resident_plan();
   void build_valu_tables();
+  void build_mfma_lds_tables();
+  void run_mfma_lds(int d0, int d1, uint8_t* out, uint64_t out_stride, hipStream_t s);
   const DeviceFilterbank& fb_;
   hipStream_t stream_;
   DeviceBuffer<int32_t> d_offsets_, d_kill_, d_active_, d_steps_, d_tile_info_;
@@ -103,6 +109,12 @@ class Dedisperser {
   std::vector<int32_t> h_tile_win_;    // LDS kernel: largest channel window per 32-DM tile (bytes)
   DeviceBuffer<int32_t> r_steps_, r_tile_info_, r_offT_, r_wmin_;
   DeviceBuffer<int8_t> r_deltas_;
+  // LDS-fed MFMA plan of the whole DM list (resident, built on first use)
+  bool ml_ready_ = false;
+  int ml_ngroups_ = 0;
+  std::vector<int32_t> ml_tile_ok_, ml_tile_steps_;
+  DeviceBuffer<int32_t> ml_steps_, ml_ginfo_, ml_wmin_;
+  DeviceBuffer<int8_t> ml_deltas_;
 };
 
 struct SearchParams {
@@ -363,6 +375,17 @@ class FoldEngine {
   // Fold + optimise candidates (period, acc) of one DM trial.
   std::vector<FoldResult> fold_trial(const uint8_t* d_trial, uint64_t trial_nsamps, const std::vector<double>& periods,
                                      const std::vector<float>& accs);
+  // Fold + optimise the candidates of ntrials DM trials (trial t at
+  // d_trials + t*row_stride, its candidates periods[t], accs[t]): the trials
+  // are whitened as batches (one four-step FFT pair per batch), then one
+  // accumulate / reduce / optimise launch folds every candidate of a batch
+  // and one copy brings the results back (folder.hpp:352-406 per DM).
+  std::vector<std::vector<FoldResult>> fold_trials(const uint8_t* d_trials, uint64_t row_stride,
+                                                   uint64_t trial_nsamps, int ntrials,
+                                                   const std::vector<std::vector<double>>& periods,
+                                                   const std::vector<std::vector<float>>& accs);
+  // DM trials whitened per batch (device memory bounds it)
+  int max_batch() const { return max_batch_; }
   // Fold + optimise candidates on an already-whitened series (testing).
   std::vector<FoldResult> fold_series(const float* d_series, const std::vector<double>& periods,
                                       const std::vector<float>& accs);
@@ -373,12 +396,11 @@ class FoldEngine {
   float tsamp_;
   hipStream_t stream_;
   std::unique_ptr<Whitener> wh_;
-  DeviceBuffer<float> tim_;    // whitened series of the prepared trials [max_prep_][n_]
-  DeviceBuffer<float> wstats_; // their interbin stats [max_prep_][4]
-  int prepared_ = 0, max_prep_ = 1;
-  const float* cur_tim_ = nullptr;  // trial being searched
-  const float* cur_pad_ = nullptr;
-  const float* cur_stats_ = nullptr;
+  int max_batch_ = 1;
+  std::vector<FoldResult> fold_jobs(const float* d_series, const std::vector<kern::FoldJob>& jobs,
+                                    const std::vector<double>& periods);
+  DeviceBuffer<float> bstats_;
+  DeviceBuffer<float> tim_;  // whitened series of the current fold batch [batch][n_]
   DeviceBuffer<float2> shift_table_;
   DeviceBuffer<kern::FoldJob> jobs_;
   DeviceBuffer<float> psum_, folds_, opt_fold_, opt_prof_, opt_val_;

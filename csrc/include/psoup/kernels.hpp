@@ -83,6 +83,31 @@ void dedisperse_mfma(const int8_t* chan_major, uint64_t chan_stride, const int32
                      const int32_t* d_tile_info, int ntiles, int ndm, uint64_t out_nsamps, uint8_t* out,
                      uint64_t out_stride, float scale, int bias_total, hipStream_t s);
 
+// LDS-fed one-hot MFMA dedispersion (dedisperse_mfma_lds_kernel): per
+// 32-DM tile and group of kMfmaLdsGroup active channels, the channel windows
+// are staged in LDS and the A fragments built from there.  Tiles whose
+// per-channel offset spread does not fit the kMfmaLdsWindow-byte window are
+// marked tile_ok = 0 (no steps; the VALU kernels take them).
+constexpr int kMfmaLdsGroup = 16;
+constexpr int kMfmaLdsWindow = 1280;
+struct MfmaLdsPlan {
+  int ntiles = 0, ngroups = 0, nactive = 0;
+  std::vector<int32_t> steps;       // [total][4] = {slot0, rel0, slot1, rel1} (rel: byte offset in the window)
+  std::vector<int8_t> deltas;       // [total][64] one-hot position per lane, -1 = none
+  std::vector<int32_t> ginfo;       // [ntiles][ngroups][2] = {first step, step count}
+  std::vector<int32_t> wmin;        // [ntiles][nactive]: window start (offset, 16-byte aligned) per channel
+  std::vector<int32_t> tile_ok;     // [ntiles]
+  std::vector<int32_t> tile_steps;  // [ntiles] MFMA steps of the tile (0 if not ok)
+};
+void build_mfma_lds_plan(const int32_t* offsets, int ndm, int nchans, const int32_t* killmask, MfmaLdsPlan& plan);
+// Tiles [tile0, tile0 + ntiles) of a plan (pointers already offset to tile0
+// for ginfo and wmin; ndm DMs from the range's first): bit-identical to
+// dedisperse_direct.  Rows are read up to 1280 bytes past t + wmin.
+void dedisperse_mfma_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_active, int nactive,
+                         const int32_t* d_steps, const int8_t* d_deltas, const int32_t* d_ginfo, int ngroups,
+                         const int32_t* d_wmin, int ntiles, int ndm, uint64_t out_nsamps, uint8_t* out,
+                         uint64_t out_stride, float scale, int bias_total, hipStream_t s);
+
 // Packed-byte VALU dedispersion (wide-spread DM tiles), bit-identical to
 // dedisperse_direct.  d_offT: int32 [nactive][ldo] offsets of active channel
 // ci for DM column d_base + k (k < ndm rounded up to the workgroup's DM count,
@@ -335,9 +360,11 @@ void harmonic_sums(const float* P, uint64_t nbins, int nlevels, float* out, hipS
 struct FoldJob {
   double tsamp_by_period;  // tsamp / period
   double af;               // acc*tsamp/(2c) for the v1 resampler
+  uint64_t series = 0;     // the job folds in + series * n (a batch of whitened DM trials)
 };
 // Partial fold sums: partial[(job*nints + subint)*nchunk + chunk][nbins] (sum),
-// counts likewise.  n = samples in the (whitened) series.
+// counts likewise.  n = samples per (whitened) series; job j reads series
+// jobs[j].series of the batch at `in`.
 void fold_accumulate(const float* in, uint64_t n, const FoldJob* jobs, int njobs, int nbins, int nints,
                      int chunk, float* psum, int32_t* pcount, hipStream_t s);
 void fold_reduce(const float* psum, const int32_t* pcount, int njobs, int nbins, int nints, int nchunk,

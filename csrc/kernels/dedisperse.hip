@@ -454,6 +454,114 @@ __global__ void __launch_bounds__(256) dedisperse_lds_kernel(
   }
 }
 
+// ------------------------------------------------------- MFMA, LDS-fed ----
+// The one-hot GEMM of dedisperse_mfma_kernel with its A operand built from
+// LDS instead of global memory: per 16-channel group the workgroup (one
+// 32-DM tile x 1024 samples) stages each channel's window
+// [t0 + w0, t0 + w0 + 1280) -- w0 = the tile's smallest offset of the
+// channel, rounded down to 16 bytes -- with aligned dwordx4 loads one group
+// ahead (double buffer, one barrier per group); a lane's 16 shifted bytes
+// come from five dword LDS reads and v_alignbyte.  Only tiles whose offset
+// spread fits the window take this path (low DM, few 16-shift blocks per
+// channel: there the one-hot MFMA beats the packed-byte VALU kernel).  Plan:
+// build_mfma_lds_plan (steps {slot0, rel0, slot1, rel1} per channel group).
+constexpr int kMlWin = 1280;  // staged bytes per channel: 1024 samples + spread + the 20-byte read
+constexpr int kMlTs = 1024;   // samples per workgroup (4 waves x 8 tiles of 32)
+
+template <int CG>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) dedisperse_mfma_lds_kernel(
+    const int8_t* __restrict__ x, uint64_t stride, const int32_t* __restrict__ active, int nactive,
+    const int4* __restrict__ steps, const int8_t* __restrict__ deltas, const int2* __restrict__ ginfo, int ngroups,
+    const int32_t* __restrict__ wmin, int ndm, uint64_t out_nsamps, uint8_t* __restrict__ out, uint64_t out_stride,
+    float scale, int bias_total) {
+  __shared__ __attribute__((aligned(16))) uint32_t win[2][CG * kMlWin / 4];
+  const int tile = blockIdx.x;
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const uint64_t t0 = static_cast<uint64_t>(blockIdx.y) * kMlTs;
+  const int2* gi = ginfo + static_cast<uint64_t>(tile) * ngroups;
+  const int32_t* wm = wmin + static_cast<uint64_t>(tile) * nactive;
+  constexpr int kV = CG * kMlWin / 16 / 256;  // 16-byte staging loads per thread per group
+  static_assert(kV * 256 * 16 == CG * kMlWin, "staging shape");
+  u32x4 rg[kV];
+  auto gload = [&](int g) {
+#pragma unroll
+    for (int v = 0; v < kV; ++v) {
+      const int e = v * 256 + static_cast<int>(threadIdx.x);  // 16-byte unit in the group's windows
+      const int q = e / (kMlWin / 16), u = e - q * (kMlWin / 16);
+      const int ci = min(g * CG + q, nactive - 1);  // past the last channel: a harmless reload
+      rg[v] = *reinterpret_cast<const u32x4*>(x + static_cast<uint64_t>(active[ci]) * stride + t0 + wm[ci] + 16 * u);
+    }
+  };
+  auto lstore = [&](int b) {
+#pragma unroll
+    for (int v = 0; v < kV; ++v) *reinterpret_cast<u32x4*>(&win[b][4 * (v * 256 + threadIdx.x)]) = rg[v];
+  };
+  v16i acc[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int e = 0; e < 16; ++e) acc[m][e] = 0;
+  const int sbase = wave * 256 + r;  // this lane's first sample in the window, before the shift
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int g = 0; g < ngroups; ++g) {
+    const int b = g & 1;
+    if (g + 1 < ngroups) gload(g + 1);
+    const int2 info = gi[g];
+    const uint8_t* wb = reinterpret_cast<const uint8_t*>(win[b]);
+    for (int s = info.x; s < info.x + info.y; ++s) {
+      const int4 st = steps[s];
+      const int slot = h ? st.z : st.x;
+      const int rel = h ? st.w : st.y;
+      const int delta = deltas[static_cast<uint64_t>(s) * 64 + lane];
+      v4i bf;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bf[q] = (delta >= 0 && (delta >> 2) == q) ? (1 << ((delta & 3) * 8)) : 0;
+      const int o0 = slot * kMlWin + rel + sbase;  // byte offset of m-tile 0's 16 bytes
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        const int o = o0 + 32 * m;
+        const uint32_t* p = reinterpret_cast<const uint32_t*>(wb + (o & ~3));
+        const uint32_t sh = static_cast<uint32_t>(o & 3);
+        const uint32_t w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3], w4 = p[4];
+        v4i a;
+        a[0] = static_cast<int>(__builtin_amdgcn_alignbyte(w1, w0, sh));
+        a[1] = static_cast<int>(__builtin_amdgcn_alignbyte(w2, w1, sh));
+        a[2] = static_cast<int>(__builtin_amdgcn_alignbyte(w3, w2, sh));
+        a[3] = static_cast<int>(__builtin_amdgcn_alignbyte(w4, w3, sh));
+        acc[m] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bf, acc[m], 0, 0, 0);
+      }
+    }
+    if (g + 1 < ngroups) lstore(b ^ 1);
+    __syncthreads();
+  }
+  // C/D layout (32x32): col = lane&31 (DM), row = (reg&3) + 8*(reg>>2) + 4*(lane>>5) (sample)
+  const int d = tile * 32 + r;
+  if (d >= ndm) return;
+  uint8_t* o = out + static_cast<uint64_t>(d) * out_stride;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+#pragma unroll
+    for (int gq = 0; gq < 4; ++gq) {
+      const uint64_t t = t0 + wave * 256 + m * 32 + 8 * gq + 4 * h;
+      uint32_t packed = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        packed |= static_cast<uint32_t>(scale_out(acc[m][4 * gq + e] + bias_total, scale)) << (8 * e);
+      if (t + 4 <= out_nsamps) {
+        *reinterpret_cast<uint32_t*>(o + t) = packed;
+      } else {
+        for (int e = 0; e < 4; ++e)
+          if (t + e < out_nsamps) o[t + e] = static_cast<uint8_t>(packed >> (8 * e));
+      }
+    }
+  }
+}
+
 }  // namespace
 
 void dedisperse_direct(const int8_t* chan_major, uint64_t chan_stride, int nchans, const int32_t* offsets,
@@ -579,6 +687,102 @@ void dedisperse_valu(const int8_t* chan_major, uint64_t chan_stride, const int32
   }
 #undef PSOUP_VALU_LAUNCH
   post_launch_check("dedisperse_valu_kernel", s);
+}
+
+void build_mfma_lds_plan(const int32_t* offsets, int ndm, int nchans, const int32_t* killmask, MfmaLdsPlan& plan) {
+  constexpr int CG = kMfmaLdsGroup;
+  std::vector<int> active;
+  for (int c = 0; c < nchans; ++c)
+    if (!killmask || killmask[c]) active.push_back(c);
+  const int na = static_cast<int>(active.size());
+  const int ntiles = (ndm + 31) / 32;
+  const int ngroups = (na + CG - 1) / CG;
+  plan.ntiles = ntiles;
+  plan.ngroups = ngroups;
+  plan.nactive = na;
+  plan.steps.clear();
+  plan.deltas.clear();
+  plan.ginfo.assign(static_cast<size_t>(ntiles) * std::max(1, ngroups) * 2, 0);
+  plan.wmin.assign(static_cast<size_t>(ntiles) * std::max(1, na), 0);
+  plan.tile_ok.assign(static_cast<size_t>(ntiles), 0);
+  plan.tile_steps.assign(static_cast<size_t>(ntiles), 0);
+  for (int T = 0; T < ntiles; ++T) {
+    auto off = [&](int dd, int c) {
+      const int d = std::min(T * 32 + dd, ndm - 1);  // pad the last tile with the last DM
+      return offsets[static_cast<size_t>(d) * nchans + c];
+    };
+    bool ok = true;
+    std::vector<int> lo(static_cast<size_t>(na)), hi(static_cast<size_t>(na));
+    for (int ci = 0; ci < na; ++ci) {
+      int a = off(0, active[ci]), b = a;
+      for (int dd = 1; dd < 32; ++dd) {
+        a = std::min(a, off(dd, active[ci]));
+        b = std::max(b, off(dd, active[ci]));
+      }
+      PSOUP_CHECK(a >= 0, "negative dispersion offset (foff > 0 is not supported)");
+      lo[ci] = a;
+      hi[ci] = b;
+      const int w0 = a & ~15;
+      plan.wmin[static_cast<size_t>(T) * na + ci] = w0;
+      // the last 16-shift block read ends at most (hi - w0) + 15 + 1023 + 4 bytes into the window
+      if ((hi[ci] - w0) + 15 + 1023 + 5 > kMfmaLdsWindow) ok = false;
+    }
+    plan.tile_ok[static_cast<size_t>(T)] = ok ? 1 : 0;
+    if (!ok) continue;  // the VALU kernels take this tile
+    int tsteps = 0;
+    for (int g = 0; g < ngroups; ++g) {
+      std::vector<std::pair<int, int>> blocks;  // (slot, rel)
+      for (int ci = g * CG; ci < std::min(na, (g + 1) * CG); ++ci) {
+        const int w0 = plan.wmin[static_cast<size_t>(T) * na + ci];
+        for (int sb = lo[ci]; sb <= hi[ci]; sb += 16) blocks.emplace_back(ci - g * CG, sb - w0);
+      }
+      if (blocks.size() % 2) blocks.push_back(std::make_pair(-1, -1));  // dummy half (zero one-hot)
+      const int nst = static_cast<int>(blocks.size() / 2);
+      plan.ginfo[(static_cast<size_t>(T) * ngroups + g) * 2] = static_cast<int32_t>(plan.steps.size() / 4);
+      plan.ginfo[(static_cast<size_t>(T) * ngroups + g) * 2 + 1] = nst;
+      for (int st = 0; st < nst; ++st) {
+        for (int hh = 0; hh < 2; ++hh) {
+          const auto blk = blocks[static_cast<size_t>(2 * st + hh)];
+          const bool dummy = blk.first < 0;
+          const auto use = dummy ? blocks[static_cast<size_t>(2 * st)] : blk;
+          plan.steps.push_back(use.first);
+          plan.steps.push_back(use.second);
+        }
+        for (int hh = 0; hh < 2; ++hh) {
+          const auto blk = blocks[static_cast<size_t>(2 * st + hh)];
+          for (int rr = 0; rr < 32; ++rr) {
+            int delta = -1;
+            if (blk.first >= 0 && T * 32 + rr < ndm) {
+              const int ci = g * CG + blk.first;
+              const int w0 = plan.wmin[static_cast<size_t>(T) * na + ci];
+              const int dv = off(rr, active[ci]) - (w0 + blk.second);
+              if (dv >= 0 && dv < 16) delta = dv;
+            }
+            plan.deltas.push_back(static_cast<int8_t>(delta));
+          }
+        }
+      }
+      tsteps += nst;
+    }
+    plan.tile_steps[static_cast<size_t>(T)] = tsteps;
+    PSOUP_CHECK(plan.steps.size() / 4 < (1ull << 31), "MFMA-LDS dedispersion plan too large");
+  }
+}
+
+void dedisperse_mfma_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_active, int nactive,
+                         const int32_t* d_steps, const int8_t* d_deltas, const int32_t* d_ginfo, int ngroups,
+                         const int32_t* d_wmin, int ntiles, int ndm, uint64_t out_nsamps, uint8_t* out,
+                         uint64_t out_stride, float scale, int bias_total, hipStream_t s) {
+  if (ndm <= 0 || out_nsamps == 0 || nactive <= 0) return;
+  PSOUP_CHECK(ntiles >= 1 && ntiles <= 65535 && ndm <= 32 * ntiles, "dedisperse_mfma_lds: bad tile range");
+  PSOUP_CHECK((chan_stride & 15) == 0, "dedisperse_mfma_lds: stride alignment");
+  const uint64_t ty = (out_nsamps + kMlTs - 1) / kMlTs;
+  PSOUP_CHECK(ty <= 65535, "dedisperse_mfma_lds: series too long for the grid");
+  dim3 grid(static_cast<unsigned>(ntiles), static_cast<unsigned>(ty));
+  dedisperse_mfma_lds_kernel<kMfmaLdsGroup><<<grid, 256, 0, s>>>(
+      chan_major, chan_stride, d_active, nactive, reinterpret_cast<const int4*>(d_steps), d_deltas,
+      reinterpret_cast<const int2*>(d_ginfo), ngroups, d_wmin, ndm, out_nsamps, out, out_stride, scale, bias_total);
+  post_launch_check("dedisperse_mfma_lds_kernel", s);
 }
 
 bool dedisperse_lds_fits(int nbits, int nactive, int max_window) {

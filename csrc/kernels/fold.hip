@@ -45,6 +45,7 @@ __global__ void __launch_bounds__(256) fold_accumulate_kernel(const float* __res
   for (int b = threadIdx.x; b < nbins; b += blockDim.x) lcnt[b] = 0;
   __syncthreads();
   const FoldJob J = jobs[job];
+  in += J.series * n;
   const uint64_t nps = n / nints;
   const uint64_t beg = static_cast<uint64_t>(subint) * nps + static_cast<uint64_t>(ch) * chunk;
   const uint64_t end = min(beg + static_cast<uint64_t>(chunk), static_cast<uint64_t>(subint + 1) * nps);

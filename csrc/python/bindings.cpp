@@ -671,6 +671,7 @@ PYBIND11_MODULE(_C, m) {
       .def_static("row_stride", &Dedisperser::row_stride)
       .def("choose", &Dedisperser::choose, py::arg("d0"), py::arg("d1"))
       .def("mfma_steps_per_channel", &Dedisperser::mfma_steps_per_channel, py::arg("d0"), py::arg("d1"))
+      .def("mfma_lds_split", &Dedisperser::mfma_lds_split, py::arg("d0"), py::arg("d1"))
       .def_property_readonly_static("tile_dms", [](py::object) { return Dedisperser::kTileDms; });
 
   py::class_<Whitener>(m, "Whitener")
@@ -771,6 +772,13 @@ PYBIND11_MODULE(_C, m) {
       .def("fold_trial", [](FoldEngine& f, uintptr_t trial, uint64_t nsamps, const std::vector<double>& periods,
                             const std::vector<float>& accs) { return f.fold_trial(P<const uint8_t>(trial), nsamps, periods, accs); },
            py::call_guard<py::gil_scoped_release>())
+      .def("fold_trials", [](FoldEngine& f, uintptr_t trials, uint64_t row_stride, uint64_t nsamps,
+                             const std::vector<std::vector<double>>& periods,
+                             const std::vector<std::vector<float>>& accs) {
+        return f.fold_trials(P<const uint8_t>(trials), row_stride, nsamps, static_cast<int>(periods.size()), periods,
+                             accs);
+      })
+      .def_property_readonly("max_batch", &FoldEngine::max_batch)
       .def("fold_series", [](FoldEngine& f, uintptr_t series, const std::vector<double>& periods,
                              const std::vector<float>& accs) { return f.fold_series(P<const float>(series), periods, accs); },
            py::call_guard<py::gil_scoped_release>())

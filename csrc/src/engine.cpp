@@ -202,12 +202,89 @@ DedispKernel Dedisperser::choose(int d0, int d1) {
   return mfma_steps_per_channel(d0, d1) > ratio ? DedispKernel::Valu : DedispKernel::Mfma;
 }
 
+void Dedisperser::build_mfma_lds_tables() {
+  const auto& g = fb_.geometry();
+  const int ndm = static_cast<int>(g.dm_list.size());
+  std::vector<int32_t> offs = g.offsets(0, ndm);
+  std::vector<int32_t> kill(g.killmask.begin(), g.killmask.end());
+  kern::MfmaLdsPlan plan;
+  kern::build_mfma_lds_plan(offs.data(), ndm, g.nchans, kill.data(), plan);
+  ml_ngroups_ = plan.ngroups;
+  ml_tile_ok_ = plan.tile_ok;
+  ml_tile_steps_ = plan.tile_steps;
+  auto up = [](auto& dev, const auto& host) {
+    using T = typename std::decay_t<decltype(host)>::value_type;
+    dev.resize(std::max<size_t>(1, host.size()));
+    if (!host.empty()) PSOUP_HIP_CHECK(hipMemcpy(dev.data(), host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice));
+  };
+  up(ml_steps_, plan.steps);
+  up(ml_deltas_, plan.deltas);
+  up(ml_ginfo_, plan.ginfo);
+  up(ml_wmin_, plan.wmin);
+  ml_ready_ = true;
+}
+
+static double mfma_lds_ratio() {
+  // LDS-fed MFMA steps per (tile, active channel) up to which a tile takes the
+  // MFMA kernel in Auto (each step is 2 x 16-shift blocks of one-hot GEMM;
+  // the VALU kernels cost the same per channel whatever the spread)
+  static const double r = [] {
+    const char* e = std::getenv("PSOUP_DEDISP_MFMA_RATIO");
+    return e ? std::atof(e) : 2.5;
+  }();
+  return r;
+}
+
+int Dedisperser::mfma_lds_split(int d0, int d1) {
+  const auto& g = fb_.geometry();
+  if (d0 % kTileDms != 0 || g.nactive == 0 || mfma_lds_ratio() <= 0) return d0;
+  if (!ml_ready_) build_mfma_lds_tables();
+  int T = d0 / kTileDms;
+  const int T1 = (d1 - 1) / kTileDms + 1;
+  while (T < T1 && ml_tile_ok_[static_cast<size_t>(T)] &&
+         ml_tile_steps_[static_cast<size_t>(T)] <= mfma_lds_ratio() * g.nactive)
+    ++T;
+  return std::min(d1, T * kTileDms);
+}
+
+void Dedisperser::run_mfma_lds(int d0, int d1, uint8_t* out, uint64_t out_stride, hipStream_t s) {
+  const auto& g = fb_.geometry();
+  if (!ml_ready_) build_mfma_lds_tables();
+  const int T0 = d0 / kTileDms, nt = (d1 - d0 + kTileDms - 1) / kTileDms;
+  kern::dedisperse_mfma_lds(fb_.data(), fb_.stride(), d_active_.data(), g.nactive, ml_steps_.data(),
+                            ml_deltas_.data(), ml_ginfo_.data() + static_cast<size_t>(T0) * ml_ngroups_ * 2,
+                            ml_ngroups_, ml_wmin_.data() + static_cast<size_t>(T0) * g.nactive, nt, d1 - d0,
+                            g.out_nsamps, out, out_stride, g.out_scale, g.bias * g.nactive, s);
+}
+
 void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispKernel kind, hipStream_t s) {
   const auto& g = fb_.geometry();
   PSOUP_CHECK(d0 >= 0 && d1 <= static_cast<int>(g.dm_list.size()) && d0 <= d1, "bad DM range");
   if (d0 == d1) return;
   if (!s) s = stream_;
   RoctxRange r("Dedisperse");
+  const int ndm_list = static_cast<int>(g.dm_list.size());
+  const bool aligned = d0 % kTileDms == 0 && (d1 % kTileDms == 0 || d1 == ndm_list);
+  if (kind == DedispKernel::Auto && g.nactive > 0 && d0 % kTileDms == 0) {
+    // hybrid: the leading narrow-spread tiles on the LDS-fed MFMA kernel, the
+    // rest (tile-aligned from the split) on the VALU kernels
+    const int split = mfma_lds_split(d0, d1);
+    if (split > d0) {
+      run_mfma_lds(d0, split, out, out_stride, s);
+      if (split < d1) run(split, d1, out + static_cast<uint64_t>(split - d0) * out_stride, out_stride, DedispKernel::Valu, s);
+      return;
+    }
+  }
+  if (kind == DedispKernel::Mfma && aligned && g.nactive > 0) {
+    // explicit MFMA on whole tiles: the LDS-fed kernel where every tile fits its window
+    if (!ml_ready_) build_mfma_lds_tables();
+    bool fit = true;
+    for (int T = d0 / kTileDms; T <= (d1 - 1) / kTileDms; ++T) fit = fit && ml_tile_ok_[static_cast<size_t>(T)];
+    if (fit) {
+      run_mfma_lds(d0, d1, out, out_stride, s);
+      return;
+    }
+  }
   if (kind == DedispKernel::Auto) kind = choose(d0, d1);
   if (kind == DedispKernel::Valu && g.nactive == 0) kind = DedispKernel::Direct;
   const int ndm = d1 - d0;
@@ -1010,6 +1087,9 @@ void fold_calculate_sn(const float* prof, int bin, int width, int nbins, float* 
 FoldEngine::FoldEngine(uint64_t nsamps, float tsamp, hipStream_t stream) : n_(nsamps), tsamp_(tsamp), stream_(stream) {
   PSOUP_CHECK(n_ >= 1024, "fold series too short");
   wh_ = std::make_unique<Whitener>(n_, tsamp_, stream_);
+  // whitening batch: up to ~2 GB of per-trial state, at most 64 trials
+  const uint64_t per = wh_->batch_bytes_per_trial() + n_ * 4;
+  max_batch_ = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(64, (2ull << 30) / std::max<uint64_t>(1, per))));
   tim_.resize(n_);
   shift_table_.resize(static_cast<uint64_t>(kNbins) * kNbins * kNints);
   kern::fold_shift_table(shift_table_.data(), kNbins, kNints, stream_);
@@ -1023,16 +1103,61 @@ std::vector<FoldResult> FoldEngine::fold_trial(const uint8_t* d_trial, uint64_t 
   return fold_series(tim_.data(), periods, accs);
 }
 
+std::vector<std::vector<FoldResult>> FoldEngine::fold_trials(const uint8_t* d_trials, uint64_t row_stride,
+                                                             uint64_t trial_nsamps, int ntrials,
+                                                             const std::vector<std::vector<double>>& periods,
+                                                             const std::vector<std::vector<float>>& accs) {
+  PSOUP_CHECK(ntrials >= 0 && static_cast<int>(periods.size()) == ntrials && static_cast<int>(accs.size()) == ntrials,
+              "fold_trials: one candidate list per trial");
+  std::vector<std::vector<FoldResult>> out(static_cast<size_t>(ntrials));
+  for (int t0 = 0; t0 < ntrials; t0 += max_batch_) {
+    const int cnt = std::min(max_batch_, ntrials - t0);
+    tim_.resize(static_cast<uint64_t>(cnt) * n_);
+    bstats_.resize(4 * static_cast<uint64_t>(cnt));
+    // the fold's whitening: no zap mask, default boundaries (pipeline_multi.cu
+    // ignores --boundary_*), stats unused
+    wh_->whiten_batch(d_trials + static_cast<uint64_t>(t0) * row_stride, row_stride, trial_nsamps, cnt, tim_.data(),
+                      n_, nullptr, bstats_.data(), 0.05f, 0.5f);
+    std::vector<kern::FoldJob> jobs;
+    std::vector<double> ps;
+    for (int t = 0; t < cnt; ++t) {
+      const auto& P = periods[static_cast<size_t>(t0 + t)];
+      const auto& A = accs[static_cast<size_t>(t0 + t)];
+      PSOUP_CHECK(P.size() == A.size(), "fold_trials: periods/accs size mismatch");
+      for (size_t i = 0; i < P.size(); ++i) {
+        kern::FoldJob j;
+        j.tsamp_by_period = static_cast<double>(tsamp_) / P[i];
+        j.af = (static_cast<double>(A[i]) * tsamp_) / (2 * kC);
+        j.series = static_cast<uint64_t>(t);
+        jobs.push_back(j);
+        ps.push_back(P[i]);
+      }
+    }
+    std::vector<FoldResult> r = fold_jobs(tim_.data(), jobs, ps);
+    size_t k = 0;
+    for (int t = 0; t < cnt; ++t)
+      for (size_t i = 0; i < periods[static_cast<size_t>(t0 + t)].size(); ++i)
+        out[static_cast<size_t>(t0 + t)].push_back(std::move(r[k++]));
+  }
+  return out;
+}
+
 std::vector<FoldResult> FoldEngine::fold_series(const float* d_series, const std::vector<double>& periods,
                                                 const std::vector<float>& accs) {
-  const int nj = static_cast<int>(periods.size());
-  std::vector<FoldResult> res(static_cast<size_t>(nj));
-  if (nj == 0) return res;
-  std::vector<kern::FoldJob> jobs(static_cast<size_t>(nj));
-  for (int i = 0; i < nj; ++i) {
+  std::vector<kern::FoldJob> jobs(periods.size());
+  for (size_t i = 0; i < periods.size(); ++i) {
     jobs[i].tsamp_by_period = static_cast<double>(tsamp_) / periods[i];
     jobs[i].af = (static_cast<double>(accs[i]) * tsamp_) / (2 * kC);
+    jobs[i].series = 0;
   }
+  return fold_jobs(d_series, jobs, periods);
+}
+
+std::vector<FoldResult> FoldEngine::fold_jobs(const float* d_series, const std::vector<kern::FoldJob>& jobs,
+                                              const std::vector<double>& periods) {
+  const int nj = static_cast<int>(jobs.size());
+  std::vector<FoldResult> res(static_cast<size_t>(nj));
+  if (nj == 0) return res;
   const uint64_t nps = n_ / kNints;
   const int nchunk = static_cast<int>((nps + chunk_ - 1) / chunk_);
   jobs_.resize(jobs.size());
@@ -1140,8 +1265,9 @@ void write_birdie_list(const std::vector<float>& mask, float bin_width, const st
   }
   FILE* fo = std::fopen(filename.c_str(), "w");
   if (!fo) PSOUP_THROW("cannot write " << filename);
-  for (const auto& b : birdies) std::fprintf(fo, "%.9f\t%.6f\n", b.first, b.second);
-  std::fclose(fo);
+  bool ok = true;
+  for (const auto& b : birdies) ok = ok && std::fprintf(fo, "%.9f\t%.6f\n", b.first, b.second) > 0;
+  if (std::fclose(fo) != 0 || !ok) PSOUP_THROW("failed writing " << filename);
 }
 
 }  // namespace psoup

@@ -153,8 +153,16 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   res.setup = setup;
   const int ndev_avail = device_count();
   PSOUP_CHECK(ndev_avail > 0, "no HIP devices visible");
-  const int ngpu = std::max(1, std::min(ndev_avail, args.max_num_threads));
-  for (int i = 0; i < ngpu; ++i) res.devices.push_back(i);
+  // Device workers: one per GPU (the reference's Worker pool,
+  // pipeline_multi.cu:276-277, 342-351).  PSOUP_OVERSUBSCRIBE=1 keeps -t
+  // workers even beyond the visible devices, worker d on device d % ndev:
+  // the multi-device feeder / queue / fold-distribution paths then run (and
+  // are tested) on a one-GPU box.
+  const char* ovs = std::getenv("PSOUP_OVERSUBSCRIBE");
+  const bool oversub = ovs && std::atoi(ovs) != 0;
+  const int ngpu = std::max(1, oversub ? args.max_num_threads : std::min(ndev_avail, args.max_num_threads));
+  auto hip_dev = [ndev_avail](int d) { return d % ndev_avail; };
+  for (int i = 0; i < ngpu; ++i) res.devices.push_back(hip_dev(i));
   log_verbose("Using " + std::to_string(ngpu) + " GPU(s); " + std::to_string(setup.dm_list.size()) + " DM trials; fft " +
               std::to_string(setup.fft_size));
 
@@ -211,7 +219,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     for (int dev = 0; dev < ngpu; ++dev)
       lth.emplace_back([&, dev] {
         try {
-          PSOUP_HIP_CHECK(hipSetDevice(dev));
+          PSOUP_HIP_CHECK(hipSetDevice(hip_dev(dev)));
           DevState& ds = devs[static_cast<size_t>(dev)];
           Stopwatch wl;
           wl.start();
@@ -266,7 +274,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   std::vector<std::unique_ptr<DevSched>> scheds;
   const uint64_t rstride = Dedisperser::row_stride(geom.out_nsamps);
   for (int d = 0; d < ngpu; ++d) {
-    PSOUP_HIP_CHECK(hipSetDevice(d));
+    PSOUP_HIP_CHECK(hipSetDevice(hip_dev(d)));
     auto sc = std::make_unique<DevSched>();
     sc->dstream = std::make_unique<Stream>();
     for (int k = 0; k < 2; ++k) {
@@ -291,7 +299,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   auto feeder = [&](int dev) {
     DevSched& sc = *scheds[static_cast<size_t>(dev)];
     try {
-      PSOUP_HIP_CHECK(hipSetDevice(dev));
+      PSOUP_HIP_CHECK(hipSetDevice(hip_dev(dev)));
       DevState& ds = devs[static_cast<size_t>(dev)];
       hipStream_t dst = sc.dstream->get();
       int k = 0;
@@ -343,7 +351,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   auto worker = [&](int dev, int slot) {
     DevSched& sc = *scheds[static_cast<size_t>(dev)];
     try {
-      PSOUP_HIP_CHECK(hipSetDevice(dev));
+      PSOUP_HIP_CHECK(hipSetDevice(hip_dev(dev)));
       DevState& ds = devs[static_cast<size_t>(dev)];
       SearchEngine& engine = *ds.engines[static_cast<size_t>(slot)];
       hipStream_t st = engine.stream();
@@ -443,7 +451,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   }
   for (auto& t : threads) t.join();
   for (int d = 0; d < ngpu; ++d) {
-    PSOUP_HIP_CHECK(hipSetDevice(d));
+    PSOUP_HIP_CHECK(hipSetDevice(hip_dev(d)));
     scheds[static_cast<size_t>(d)]->dstream->sync();
     const double dd = scheds[static_cast<size_t>(d)]->dd_ms * 1e-3;  // GPU time of the (overlapped) kernels
     sh.dedisp_s[static_cast<size_t>(d)] = dd;
@@ -471,27 +479,38 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     for (int dev = 0; dev < ngpu; ++dev) {
       fth.emplace_back([&, dev] {
         try {
-          PSOUP_HIP_CHECK(hipSetDevice(dev));
+          PSOUP_HIP_CHECK(hipSetDevice(hip_dev(dev)));
           DevState& ds = devs[static_cast<size_t>(dev)];
           hipStream_t st = ds.stream->get();
           FoldEngine fe(fold_n, static_cast<float>(geom.tsamp), st);
           const uint64_t rstride = Dedisperser::row_stride(geom.out_nsamps);
-          DeviceBuffer<uint8_t> trial(rstride);
-          for (size_t g = static_cast<size_t>(dev); g < glist.size(); g += static_cast<size_t>(ngpu)) {
-            const int dm_idx = glist[g].first;
-            ds.dd->run(dm_idx, dm_idx + 1, trial.data(), rstride, setup.dedisp_kernel);
-            std::vector<double> periods;
-            std::vector<float> accs;
-            for (int ci : glist[g].second) {
-              periods.push_back(static_cast<double>(static_cast<float>(1.0 / cands[ci].freq)));
-              accs.push_back(cands[ci].acc);
+          // this worker's DM groups, batched: every DM of a batch dedispersed
+          // into one buffer (no host waits), then whitened and folded together
+          std::vector<size_t> mine;
+          for (size_t g = static_cast<size_t>(dev); g < glist.size(); g += static_cast<size_t>(ngpu)) mine.push_back(g);
+          const int B = fe.max_batch();
+          DeviceBuffer<uint8_t> trials(rstride * static_cast<uint64_t>(std::max<size_t>(1, std::min<size_t>(mine.size(), B))));
+          for (size_t b0 = 0; b0 < mine.size(); b0 += static_cast<size_t>(B)) {
+            const size_t cnt = std::min<size_t>(static_cast<size_t>(B), mine.size() - b0);
+            std::vector<std::vector<double>> periods(cnt);
+            std::vector<std::vector<float>> accs(cnt);
+            for (size_t t = 0; t < cnt; ++t) {
+              const auto& grp = glist[mine[b0 + t]];
+              ds.dd->run(grp.first, grp.first + 1, trials.data() + t * rstride, rstride, setup.dedisp_kernel, st);
+              for (int ci : grp.second) {
+                periods[t].push_back(static_cast<double>(static_cast<float>(1.0 / cands[ci].freq)));
+                accs[t].push_back(cands[ci].acc);
+              }
             }
-            auto fr = fe.fold_trial(trial.data(), geom.out_nsamps, periods, accs);
-            for (size_t k = 0; k < fr.size(); ++k) {
-              Candidate& c = cands[static_cast<size_t>(glist[g].second[k])];
-              c.folded_snr = fr[k].folded_snr;
-              c.set_fold(fr[k].fold.data(), FoldEngine::kNbins, FoldEngine::kNints);
-              c.opt_period = fr[k].opt_period;
+            auto fr = fe.fold_trials(trials.data(), rstride, geom.out_nsamps, static_cast<int>(cnt), periods, accs);
+            for (size_t t = 0; t < cnt; ++t) {
+              const auto& grp = glist[mine[b0 + t]];
+              for (size_t k = 0; k < fr[t].size(); ++k) {
+                Candidate& c = cands[static_cast<size_t>(grp.second[k])];
+                c.folded_snr = fr[t][k].folded_snr;
+                c.set_fold(fr[t][k].fold.data(), FoldEngine::kNbins, FoldEngine::kNints);
+                c.opt_period = fr[t][k].opt_period;
+              }
             }
           }
         } catch (...) {

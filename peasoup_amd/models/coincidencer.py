@@ -41,6 +41,9 @@ def _beam_trial(path: str, device: torch.device):
 
 def run_coincidencer(filterbanks: Sequence[str], samp_out: str = "rfi.eb_mask", spec_out: str = "birdies.txt",
                      thresh: float = 4.0, beam_thresh: int = 4) -> dict:
+    if len(filterbanks) > 255:
+        # the per-sample beam counts are uint8 (count_above / the RCCL sum)
+        raise ValueError(f"{len(filterbanks)} beams: the coincidencer counts beams in uint8, at most 255")
     ctx = pdist.init()
     dev = ctx.device
     mine = [f for i, f in enumerate(filterbanks) if i % ctx.world_size == ctx.rank]

@@ -129,6 +129,7 @@ class RankSearcher:
                                         for i in range(1, neng)]
         self._pool = None
         self._trials: Optional[torch.Tensor] = None
+        self._fold_engine = None
 
     def load_packed(self, packed: torch.Tensor) -> None:
         if packed.is_cuda:
@@ -340,15 +341,28 @@ class RankSearcher:
         out: Dict[int, tuple] = {}
         if not groups:
             return out
-        n = _C.prev_power_of_two(self.geom.out_nsamps)
-        fe = _C.FoldEngine(n, float(self.header["tsamp"]), self.stream)
-        for dm_idx, members in sorted(groups.items()):
-            trials = self.dedisperse(dm_idx, dm_idx + 1)
-            periods = [float(struct.unpack("f", struct.pack("f", 1.0 / cands[i].freq))[0]) for i in members]
-            accs = [cands[i].acc for i in members]
-            res = fe.fold_trial(trials.data_ptr(), self.geom.out_nsamps, periods, accs)
-            for i, r in zip(members, res):
-                out[i] = (r.folded_snr, r.opt_period, list(r.fold))
+        if self._fold_engine is None:  # one engine (whitener, shift table, buffers) per searcher
+            n = _C.prev_power_of_two(self.geom.out_nsamps)
+            self._fold_engine = _C.FoldEngine(n, float(self.header["tsamp"]), self.stream)
+        fe = self._fold_engine
+        items = sorted(groups.items())
+        B = int(fe.max_batch)
+        for b0 in range(0, len(items), B):
+            batch = items[b0:b0 + B]
+            # every DM of the batch dedispersed into one buffer, then whitened
+            # and folded together (one accumulate / optimise launch)
+            buf = torch.empty(len(batch) * self.row_stride, dtype=torch.uint8, device=self.ctx.device)
+            torch.cuda.current_stream(self.ctx.device).synchronize()  # the allocation is ours on self.stream
+            for t, (dm_idx, _) in enumerate(batch):
+                self.dedisperser.run(dm_idx, dm_idx + 1, buf.data_ptr() + t * self.row_stride, self.row_stride,
+                                     self.kernel, self.stream)
+            periods = [[float(struct.unpack("f", struct.pack("f", 1.0 / cands[i].freq))[0]) for i in members]
+                       for _, members in batch]
+            accs = [[cands[i].acc for i in members] for _, members in batch]
+            res = fe.fold_trials(buf.data_ptr(), self.row_stride, self.geom.out_nsamps, periods, accs)
+            for (_, members), rr in zip(batch, res):
+                for i, r in zip(members, rr):
+                    out[i] = (r.folded_snr, r.opt_period, list(r.fold))
         return out
 
 
@@ -414,12 +428,13 @@ def dm_schedule(args, world_size: int, ndm: Optional[int] = None) -> str:
     by the ranks), "static" (contiguous trial-weighted shards); auto = dynamic
     for more than one rank when the list has at least 4 chunks per rank (with
     fewer, 32-DM chunks leave ranks idle: 113 DMs on 8 ranks ran 4 ranks,
-    tools/expt/dyn8_rehearsal.sh), else static."""
+    tools/expt/dyn8_rehearsal.sh), else static.  An explicit "dynamic" is
+    honoured on one rank too (the rank claims every chunk from the queue)."""
     s = (getattr(args, "dm_schedule", "auto") or "auto").lower()
     if s not in ("auto", "dynamic", "static"):
         raise ValueError(f"--dm_schedule must be dynamic, static or auto, not {s!r}")
     if world_size <= 1:
-        return "static"
+        return "dynamic" if s == "dynamic" else "static"
     if s == "auto":
         enough = ndm is None or (ndm + DYNAMIC_CHUNK - 1) // DYNAMIC_CHUNK >= 4 * world_size
         return "dynamic" if enough else "static"

@@ -31,6 +31,7 @@ class DistContext:
     local_rank: int = 0
     backend: str = "none"
     device: torch.device = torch.device("cpu")
+    forced: bool = False  # PSOUP_FORCE_PG: a process group (and every collective) at world size 1
 
     @property
     def is_root(self) -> bool:
@@ -38,7 +39,7 @@ class DistContext:
 
     @property
     def distributed(self) -> bool:
-        return self.world_size > 1 and dist.is_available() and dist.is_initialized()
+        return (self.world_size > 1 or self.forced) and dist.is_available() and dist.is_initialized()
 
 
 _CTX: Optional[DistContext] = None
@@ -48,7 +49,10 @@ def init(backend: Optional[str] = None, timeout_s: float = 1800.0) -> DistContex
     """Initialise (or return) the process group from torchrun-style env vars.
 
     ``backend`` defaults to ``nccl`` (RCCL) when a GPU is visible, else
-    ``gloo``.  A single process (WORLD_SIZE unset or 1) needs no rendezvous.
+    ``gloo``.  A single process (WORLD_SIZE unset or 1) needs no rendezvous,
+    unless ``PSOUP_FORCE_PG=1``: then a world-1 process group is created and
+    every collective of the pipeline (filterbank broadcast, candidate gather,
+    reductions, barriers) really runs through RCCL on the one GPU.
     """
     global _CTX
     if _CTX is not None:
@@ -68,7 +72,8 @@ def init(backend: Optional[str] = None, timeout_s: float = 1800.0) -> DistContex
     elif has_gpu:
         device = torch.device("cuda", local % torch.cuda.device_count())
         torch.cuda.set_device(device)
-    if world > 1 and not dist.is_initialized():
+    forced = world == 1 and os.environ.get("PSOUP_FORCE_PG", "0") not in ("", "0")
+    if (world > 1 or forced) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")
         kwargs = dict(backend=backend, rank=rank, world_size=world,
@@ -77,7 +82,7 @@ def init(backend: Optional[str] = None, timeout_s: float = 1800.0) -> DistContex
             kwargs["device_id"] = device
         dist.init_process_group(**kwargs)
     _CTX = DistContext(rank=rank, world_size=world, local_rank=local,
-                       backend=backend if world > 1 else "none", device=device)
+                       backend=backend if (world > 1 or forced) else "none", device=device, forced=forced)
     try:
         from .. import _C
 

@@ -73,6 +73,45 @@ def test_dedisperse_direct_mfma_valu_bit_exact(C, nbits, nchans, kill):
         assert np.array_equal(o.view(5, stride)[:, : g.out_nsamps].cpu().numpy(), exp[3:8]), k
 
 
+def test_dedisperse_1024ch_hybrid_mfma_bit_exact(C):
+    """Config-4 geometry (1024 channels, 64 us, 1550 MHz - 400 MHz), 2^18
+    output samples, 7 DM tiles from DM 0 to high DM: the LDS-fed one-hot MFMA
+    kernel (low-spread tiles), the VALU kernels and Auto's hybrid split all
+    equal the direct kernel byte for byte."""
+    rng = np.random.default_rng(21)
+    nchans, tsamp, fch1, foff = 1024, 64e-6, 1550.0, -400.0 / 1024
+    dms = C.generate_dm_list(0.0, 300.0, tsamp, 64.0, fch1, foff, nchans, 1.25)
+    ndm = 320  # the first 10 tiles: ~2.1 -> 2.9 MFMA steps per channel (window-fitting to tile 10)
+    delays = C.generate_delay_table(nchans, tsamp, fch1, foff)
+    nsamps = (1 << 18) + C.compute_max_delay(dms, delays)
+    hdr = synthetic.make_header(nchans=nchans, nbits=2, tsamp=tsamp, fch1=fch1, foff=foff, nsamples=nsamps)
+    killmask = [int(rng.random() > 0.05) for _ in range(nchans)]
+    g = C.DedispGeometry.make(hdr, nsamps, dms, killmask)
+    s = torch.cuda.current_stream().cuda_stream
+    dfb = C.DeviceFilterbank(g, s)
+    packed = torch.randint(0, 256, (nsamps * nchans * 2 // 8,), dtype=torch.uint8, device=dev)
+    dfb.load_packed_device(packed.data_ptr())
+    dd = C.Dedisperser(dfb, s)
+    split = dd.mfma_lds_split(0, ndm)
+    assert 0 < split < ndm and split % 32 == 0, split  # both kernels run in Auto
+    stride = C.Dedisperser.row_stride(g.out_nsamps)
+    outs = {}
+    for k in (C.DedispKernel.Direct, C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto):
+        o = torch.zeros(ndm * stride, dtype=torch.uint8, device=dev)
+        dd.run(0, ndm, o.data_ptr(), stride, k)
+        outs[k] = o.view(ndm, stride)[:, : g.out_nsamps]
+    ref_ = outs[C.DedispKernel.Direct]
+    for k in (C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto):
+        assert torch.equal(outs[k], ref_), k
+    # MFMA-LDS on the low-DM tiles alone, and a range starting inside the split
+    o = torch.zeros(split * stride, dtype=torch.uint8, device=dev)
+    dd.run(0, split, o.data_ptr(), stride, C.DedispKernel.Mfma)
+    assert torch.equal(o.view(split, stride)[:, : g.out_nsamps], ref_[:split])
+    o = torch.zeros((ndm - 32) * stride, dtype=torch.uint8, device=dev)
+    dd.run(32, ndm, o.data_ptr(), stride, C.DedispKernel.Auto)
+    assert torch.equal(o.view(ndm - 32, stride)[:, : g.out_nsamps], ref_[32:])
+
+
 def test_mfma_resident_plan_ranges_and_side_stream(C):
     """Whole-tile ranges use the resident plan (ragged per-tile step lists),
     other ranges a per-call plan; both bit-exact, also on a side stream."""

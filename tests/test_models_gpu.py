@@ -134,6 +134,91 @@ def test_multi_rank_search_equals_single_rank(tmp_path, world, schedule):
         assert sum(d["dm_blocks"] for d in devs) == 2
 
 
+def test_dynamic_schedule_four_ranks_many_chunks(tmp_path):
+    """The mode 8-GPU config 4 uses: four ranks claim first-come 32-DM chunks
+    from the shared queue, with 18 chunks (>= 4 per rank) on a 572-DM list;
+    the merged output is byte-identical to one rank's."""
+    port = _free_port()
+    script = (
+        "import os,sys; sys.path.insert(0, %r)\n"
+        "from peasoup_amd.parallel import dist as pdist\n"
+        "pdist.init(backend='gloo')\n"
+        "from peasoup_amd import _C\n"
+        "from peasoup_amd.models.search import run_search\n"
+        "ok,_,a=_C.parse_cmdline(['peasoup','-i',%r,'-o',sys.argv[1],'--dm_end','2000','--dm_tol','1.01',"
+        "'-n','3','--npdmp','4','--dm_schedule','dynamic','--trace_json',sys.argv[1]+'.json'])\n"
+        "run_search(a)\n"
+        "pdist.shutdown()\n" % (REPO, TUTORIAL))
+    f = tmp_path / "run.py"
+    f.write_text(script)
+    world = 4
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world))
+    procs = [subprocess.Popen([sys.executable, str(f), str(tmp_path / "dist")], env=dict(env, RANK=str(r), LOCAL_RANK="0"),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for r in range(world)]
+    for p in procs:
+        out, err = p.communicate(timeout=600)
+        assert p.returncode == 0, err[-3000:]
+    r = subprocess.run([sys.executable, str(f), str(tmp_path / "single")],
+                       env=dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert open(tmp_path / "dist" / "candidates.peasoup", "rb").read() == \
+        open(tmp_path / "single" / "candidates.peasoup", "rb").read()
+    import json
+
+    devs = json.load(open(str(tmp_path / "dist") + ".json"))["devices"]
+    blocks = [d["dm_blocks"] for d in devs]
+    assert sum(blocks) == 18 and [d["dm_schedule"] for d in devs] == ["dynamic"] * world
+    assert min(blocks) >= 1, blocks
+
+
+def test_forced_rccl_process_group_world1(tmp_path):
+    """PSOUP_FORCE_PG=1: a world-1 RCCL process group, so every collective the
+    pipeline uses (broadcast_bytes, broadcast_object_bytes, gather_bytes,
+    all_reduce_sum, all_reduce_max_float, barrier, the store-backed work
+    queue) executes on the GPU through RCCL; a search through it equals the
+    plain single-process search byte for byte."""
+    port = _free_port()
+    script = (
+        "import os,sys; sys.path.insert(0, %r)\n"
+        "import torch\n"
+        "from peasoup_amd.parallel import dist as pdist\n"
+        "ctx = pdist.init()\n"
+        "forced = os.environ.get('PSOUP_FORCE_PG') == '1'\n"
+        "if forced:\n"
+        "    import torch.distributed as dist\n"
+        "    assert ctx.backend == 'nccl' and ctx.distributed and dist.get_backend() == 'nccl', ctx\n"
+        "    b = torch.arange(1 << 20, dtype=torch.int64, device=ctx.device).to(torch.uint8)\n"
+        "    out = pdist.broadcast_bytes(b, b.numel())\n"
+        "    assert out.is_cuda and torch.equal(out, b)\n"
+        "    assert pdist.broadcast_object_bytes(b'header') == b'header'\n"
+        "    assert pdist.gather_bytes(b'abc', dst=None) == [b'abc']\n"
+        "    t = torch.tensor([7, 9], dtype=torch.int64, device=ctx.device)\n"
+        "    assert pdist.all_reduce_sum(t).tolist() == [7, 9]\n"
+        "    assert pdist.all_reduce_max_float(2.5) == 2.5\n"
+        "    pdist.barrier()\n"
+        "    q = pdist.WorkQueue('forced', 3)\n"
+        "    assert [q.claim() for _ in range(4)] == [0, 1, 2, None]\n"
+        "from peasoup_amd import _C\n"
+        "from peasoup_amd.models.search import run_search\n"
+        "ok,_,a=_C.parse_cmdline(['peasoup','-i',%r,'-o',sys.argv[1],'--dm_end','250','--acc_start','-5',"
+        "'--acc_end','5','-n','4','--npdmp','10','--dm_schedule','dynamic'])\n"
+        "run_search(a)\n"
+        "pdist.shutdown()\n"
+        "print('OK forced' if forced else 'OK plain')\n" % (REPO, TUTORIAL))
+    f = tmp_path / "run.py"
+    f.write_text(script)
+    base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    outs = {}
+    for forced in ("1", "0"):
+        r = subprocess.run([sys.executable, str(f), str(tmp_path / forced)], env=dict(base, PSOUP_FORCE_PG=forced),
+                           capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        assert ("OK forced" if forced == "1" else "OK plain") in r.stdout
+        outs[forced] = open(tmp_path / forced / "candidates.peasoup", "rb").read()
+    assert outs["1"] == outs["0"] and len(outs["1"]) > 1000
+
+
 def test_time_shard_native_windows_match_whole(C):
     """Each rank's haloed window dedispersed by the MFMA kernel equals the
     corresponding columns of the whole-observation dedispersion."""

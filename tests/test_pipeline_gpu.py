@@ -227,3 +227,29 @@ def test_engines_per_gpu_do_not_change_results(tmp_path):
         outs.append((d / "candidates.peasoup").read_bytes())
     assert outs[0] == outs[1]
     assert outs[2] == outs[3]
+
+
+def test_native_oversubscribed_device_workers_match_one(tmp_path):
+    """PSOUP_OVERSUBSCRIBE=1: `peasoup -t 4` runs four device workers (feeder +
+    engine threads, per-device filterbank upload, DM queue, fold
+    distribution) on the one GPU; the candidates file and every candidate
+    field of the overview equal the -t 1 run's."""
+    exe = os.path.join(REPO, "bin", "peasoup")
+    env = dict(os.environ, PSOUP_OVERSUBSCRIBE="1")
+    for t in ("1", "4"):
+        r = subprocess.run([exe, "-i", TUTORIAL, "-o", str(tmp_path / t), "-t", t, "--trace_json",
+                            str(tmp_path / (t + ".json"))] + GOLDEN_ARGS, capture_output=True, text=True, timeout=600,
+                           env=env)
+        assert r.returncode == 0, r.stderr
+    a = open(tmp_path / "1" / "candidates.peasoup", "rb").read()
+    b = open(tmp_path / "4" / "candidates.peasoup", "rb").read()
+    assert a == b
+    o1, o4 = OverviewFile(str(tmp_path / "1" / "overview.xml")), OverviewFile(str(tmp_path / "4" / "overview.xml"))
+    assert len(o1) == len(o4) > 5
+    for i in range(len(o1)):
+        assert o1.get_candidate(i) == o4.get_candidate(i), i
+    import json
+
+    devs = json.load(open(tmp_path / "4.json"))["devices"]
+    assert len(devs) == 4 and sum(d["dm_trials"] for d in devs) == 59
+    assert sum(1 for d in devs if d["dm_trials"] > 0) >= 2  # the DM queue was shared

@@ -24,8 +24,9 @@ def test_chunk_ranges_empty_and_noncontiguous():
 
 
 def test_dm_schedule_option():
-    """--dm_schedule: dynamic is the multi-rank default, a single rank is
-    always static (in-order chunks), bad values are rejected."""
+    """--dm_schedule: dynamic is the multi-rank default, auto on a single rank
+    is static (in-order chunks), an explicit dynamic runs the queue even on
+    one rank, bad values are rejected."""
     from peasoup_amd import _C
     from peasoup_amd.models.search import dm_schedule
 
@@ -37,6 +38,8 @@ def test_dm_schedule_option():
     assert dm_schedule(a, 2, 225) == "dynamic" and dm_schedule(a, 2, 224) == "static"  # 8 vs 7 chunks
     ok, _, a = _C.parse_cmdline(["peasoup", "-i", "x.fil", "--dm_schedule", "static"])
     assert ok and dm_schedule(a, 8) == "static"
+    ok, _, a = _C.parse_cmdline(["peasoup", "-i", "x.fil", "--dm_schedule", "dynamic"])
+    assert ok and dm_schedule(a, 1) == "dynamic" and dm_schedule(a, 8, 64) == "dynamic"
     a.dm_schedule = "roundrobin"
     with pytest.raises(ValueError):
         dm_schedule(a, 2)

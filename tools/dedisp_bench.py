@@ -76,7 +76,8 @@ def main():
         same = bool(torch.equal(bufs["m"][: (d1 - d0) * rs].view(d1 - d0, rs)[:, :n],
                                 bufs["v"][: (d1 - d0) * rs].view(d1 - d0, rs)[:, :n]))
         print(json.dumps({"d0": d0, "dm": round(dms[d0], 2), "mfma_ms": round(tm, 4), "valu_ms": round(tv, 4),
-                          "auto": str(dd.choose(d0, d1)).split(".")[-1], "bit_exact": same,
+                          "auto": "MfmaLds" if dd.mfma_lds_split(d0, d1) > d0 else str(dd.choose(d0, d1)).split(".")[-1],
+                          "bit_exact": same,
                           "mfma_steps_per_chan": round(dd.mfma_steps_per_channel(d0, d1), 3)}), flush=True)
     tot = {}
     for k in ("m", "v", "auto"):
@@ -88,9 +89,21 @@ def main():
         e1.record(s.handle)
         e1.synchronize()
         tot[k] = round(e0.elapsed_ms(e1), 2)
+    # the whole list in one Auto call (the hybrid split: MFMA tiles, then VALU)
+    whole = torch.empty(ndm * rs, dtype=torch.uint8, device="cuda")
+    dd.run(0, ndm, whole.data_ptr(), rs, _C.DedispKernel.Auto, s.handle)
+    e0, e1 = _C.GpuEvent(True), _C.GpuEvent(True)
+    e0.record(s.handle)
+    dd.run(0, ndm, whole.data_ptr(), rs, _C.DedispKernel.Auto, s.handle)
+    e1.record(s.handle)
+    e1.synchronize()
+    tot["auto_whole"] = round(e0.elapsed_ms(e1), 2)
+    tot["split_dm"] = dd.mfma_lds_split(0, ndm)
     gsamp = ndm * g.out_nsamps * g.nactive / 1e9
     print(json.dumps({"ndm": ndm, "nchans": a.nchans, "nbits": a.nbits, "out_nsamps": g.out_nsamps,
-                      "total_ms": {"mfma": tot["m"], "valu": tot["v"], "auto": tot["auto"]},
+                      "total_ms": {"mfma": tot["m"], "valu": tot["v"], "auto": tot["auto"],
+                                   "auto_whole_list": tot["auto_whole"]},
+                      "mfma_lds_split_dm_index": tot["split_dm"],
                       "G_chan_samples_per_s": {k: round(gsamp / (v * 1e-3), 1) for k, v in
                                                (("mfma", tot["m"]), ("valu", tot["v"]), ("auto", tot["auto"]))}}))
 
