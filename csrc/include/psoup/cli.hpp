@@ -55,6 +55,7 @@ struct CmdLineOptions {
   std::string checkpoint_dir;               // per-DM candidate spill + resume
   std::string trace_json;                   // optional per-stage JSON trace
   int fault_after_dms = -1;                 // fault injection (testing)
+  bool time_shards = false;                 // Python driver: time-sharded dedispersion (halo + all-to-all)
 };
 
 // Returns false on a parse error (message printed to stderr).  Sets

@@ -114,7 +114,7 @@ class Dedisperser {
   int ml_ngroups_ = 0;
   std::vector<int32_t> ml_tile_ok_, ml_tile_steps_;
   DeviceBuffer<int32_t> ml_steps_, ml_ginfo_, ml_wmin_;
-  DeviceBuffer<int8_t> ml_deltas_;
+  DeviceBuffer<uint8_t> ml_relo_;
 };
 
 struct SearchParams {

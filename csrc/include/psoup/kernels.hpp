@@ -87,13 +87,19 @@ void dedisperse_mfma(const int8_t* chan_major, uint64_t chan_stride, const int32
 // 32-DM tile and group of kMfmaLdsGroup active channels, the channel windows
 // are staged in LDS and the A fragments built from there.  Tiles whose
 // per-channel offset spread does not fit the kMfmaLdsWindow-byte window are
-// marked tile_ok = 0 (no steps; the VALU kernels take them).
+// marked tile_ok = 0 (no steps; the VALU kernels take them).  Everything a
+// step needs is staged in LDS with the windows, so the MFMA loop issues no
+// global or scalar loads: a 32-bit step word (two 16-bit halves, one per
+// K-half of the MFMA: bits 0-3 channel slot, 4-11 window byte offset rel,
+// 12 = empty half) and per channel slot the 32 DMs' window-relative offsets
+// (bytes); a lane's one-hot position is relo[slot][dm] - rel.
 constexpr int kMfmaLdsGroup = 16;
 constexpr int kMfmaLdsWindow = 1280;
+constexpr int kMfmaLdsMaxSteps = 128;  // step words staged per channel group
 struct MfmaLdsPlan {
   int ntiles = 0, ngroups = 0, nactive = 0;
-  std::vector<int32_t> steps;       // [total][4] = {slot0, rel0, slot1, rel1} (rel: byte offset in the window)
-  std::vector<int8_t> deltas;       // [total][64] one-hot position per lane, -1 = none
+  std::vector<int32_t> steps;       // [total + kMfmaLdsMaxSteps] packed step words (zero padded)
+  std::vector<uint8_t> relo;        // [ntiles][ngroups][kMfmaLdsGroup][32] offset - window start per DM
   std::vector<int32_t> ginfo;       // [ntiles][ngroups][2] = {first step, step count}
   std::vector<int32_t> wmin;        // [ntiles][nactive]: window start (offset, 16-byte aligned) per channel
   std::vector<int32_t> tile_ok;     // [ntiles]
@@ -101,10 +107,10 @@ struct MfmaLdsPlan {
 };
 void build_mfma_lds_plan(const int32_t* offsets, int ndm, int nchans, const int32_t* killmask, MfmaLdsPlan& plan);
 // Tiles [tile0, tile0 + ntiles) of a plan (pointers already offset to tile0
-// for ginfo and wmin; ndm DMs from the range's first): bit-identical to
+// for ginfo, relo and wmin; ndm DMs from the range's first): bit-identical to
 // dedisperse_direct.  Rows are read up to 1280 bytes past t + wmin.
 void dedisperse_mfma_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_active, int nactive,
-                         const int32_t* d_steps, const int8_t* d_deltas, const int32_t* d_ginfo, int ngroups,
+                         const int32_t* d_steps, const uint8_t* d_relo, const int32_t* d_ginfo, int ngroups,
                          const int32_t* d_wmin, int ntiles, int ndm, uint64_t out_nsamps, uint8_t* out,
                          uint64_t out_stride, float scale, int bias_total, hipStream_t s);
 

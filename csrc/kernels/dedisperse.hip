@@ -464,17 +464,25 @@ __global__ void __launch_bounds__(256) dedisperse_lds_kernel(
 // come from five dword LDS reads and v_alignbyte.  Only tiles whose offset
 // spread fits the window take this path (low DM, few 16-shift blocks per
 // channel: there the one-hot MFMA beats the packed-byte VALU kernel).  Plan:
-// build_mfma_lds_plan (steps {slot0, rel0, slot1, rel1} per channel group).
+// build_mfma_lds_plan (packed step words + window-relative DM offsets per
+// channel group, staged in LDS with the windows: the step loop is LDS + MFMA
+// only -- a per-step global one-hot load measured 3.7x the MFMA time).
 constexpr int kMlWin = 1280;  // staged bytes per channel: 1024 samples + spread + the 20-byte read
 constexpr int kMlTs = 1024;   // samples per workgroup (4 waves x 8 tiles of 32)
 
 template <int CG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) dedisperse_mfma_lds_kernel(
     const int8_t* __restrict__ x, uint64_t stride, const int32_t* __restrict__ active, int nactive,
-    const int4* __restrict__ steps, const int8_t* __restrict__ deltas, const int2* __restrict__ ginfo, int ngroups,
-    const int32_t* __restrict__ wmin, int ndm, uint64_t out_nsamps, uint8_t* __restrict__ out, uint64_t out_stride,
-    float scale, int bias_total) {
-  __shared__ __attribute__((aligned(16))) uint32_t win[2][CG * kMlWin / 4];
+    const uint32_t* __restrict__ steps, const uint8_t* __restrict__ relo, const int2* __restrict__ ginfo,
+    int ngroups, const int32_t* __restrict__ wmin, int ndm, uint64_t out_nsamps, uint8_t* __restrict__ out,
+    uint64_t out_stride, float scale, int bias_total) {
+  // per buffer: CG windows, then kMfmaLdsMaxSteps step words, then the
+  // CG x 32 relo bytes (all 16-byte units)
+  constexpr int kWinU = CG * kMlWin / 16;            // window units
+  constexpr int kStepU = kMfmaLdsMaxSteps * 4 / 16;  // step-word units
+  constexpr int kReloU = CG * 32 / 16;               // relo units
+  constexpr int kBufW = (kWinU + kStepU + kReloU) * 4;
+  __shared__ __attribute__((aligned(16))) uint32_t win[2][kBufW];
   const int tile = blockIdx.x;
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
@@ -483,9 +491,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) d
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.y) * kMlTs;
   const int2* gi = ginfo + static_cast<uint64_t>(tile) * ngroups;
   const int32_t* wm = wmin + static_cast<uint64_t>(tile) * nactive;
-  constexpr int kV = CG * kMlWin / 16 / 256;  // 16-byte staging loads per thread per group
-  static_assert(kV * 256 * 16 == CG * kMlWin, "staging shape");
-  u32x4 rg[kV];
+  const uint8_t* rl = relo + static_cast<uint64_t>(tile) * ngroups * CG * 32;
+  constexpr int kV = kWinU / 256;  // 16-byte window loads per thread per group
+  static_assert(kV * 256 == kWinU && kStepU + kReloU <= 256, "staging shape");
+  u32x4 rg[kV + 1];
+  const bool extra = threadIdx.x < kStepU + kReloU;
   auto gload = [&](int g) {
 #pragma unroll
     for (int v = 0; v < kV; ++v) {
@@ -494,70 +504,118 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) d
       const int ci = min(g * CG + q, nactive - 1);  // past the last channel: a harmless reload
       rg[v] = *reinterpret_cast<const u32x4*>(x + static_cast<uint64_t>(active[ci]) * stride + t0 + wm[ci] + 16 * u);
     }
+    if (extra) {
+      const int e = static_cast<int>(threadIdx.x);
+      rg[kV] = e < kStepU ? *reinterpret_cast<const u32x4*>(steps + gi[g].x + 4 * e)  // padded past the end
+                          : *reinterpret_cast<const u32x4*>(rl + static_cast<uint64_t>(g) * CG * 32 + 16 * (e - kStepU));
+    }
   };
   auto lstore = [&](int b) {
 #pragma unroll
     for (int v = 0; v < kV; ++v) *reinterpret_cast<u32x4*>(&win[b][4 * (v * 256 + threadIdx.x)]) = rg[v];
+    if (extra) *reinterpret_cast<u32x4*>(&win[b][4 * (kWinU + threadIdx.x)]) = rg[kV];
   };
+  // MFMA row r of sub-tile m is sample w*256 + 8r + m: the eight sub-tiles of
+  // a lane read the 23 consecutive window bytes from 8r, so one 7-dword LDS
+  // read per lane and step feeds all eight MFMAs (rel is a multiple of 4, so
+  // each sub-tile's byte shift m & 3 is a compile-time constant)
   v16i acc[8];
 #pragma unroll
   for (int m = 0; m < 8; ++m)
 #pragma unroll
     for (int e = 0; e < 16; ++e) acc[m][e] = 0;
-  const int sbase = wave * 256 + r;  // this lane's first sample in the window, before the shift
+  const int sbase = wave * 256 + 8 * r;  // this lane's first sample in the window, before the block shift
   gload(0);
   lstore(0);
   __syncthreads();
   for (int g = 0; g < ngroups; ++g) {
     const int b = g & 1;
     if (g + 1 < ngroups) gload(g + 1);
-    const int2 info = gi[g];
-    const uint8_t* wb = reinterpret_cast<const uint8_t*>(win[b]);
-    for (int s = info.x; s < info.x + info.y; ++s) {
-      const int4 st = steps[s];
-      const int slot = h ? st.z : st.x;
-      const int rel = h ? st.w : st.y;
-      const int delta = deltas[static_cast<uint64_t>(s) * 64 + lane];
+    const int nst = gi[g].y;
+    const uint32_t* wb = win[b];
+    const uint32_t* sw = wb + kWinU * 4;
+    const uint8_t* rb = reinterpret_cast<const uint8_t*>(sw + kMfmaLdsMaxSteps);
+    // Pipelined over the group's steps, unrolled by two so the register
+    // halves swap roles instead of being copied: while step s's eight MFMAs
+    // issue, the lane's window words and one-hot position for step s+1 and
+    // the (uniform, broadcast) step word for s+2 are in flight.  All from
+    // LDS: the step loop issues no global or scalar load.
+    struct Frag {
+      uint32_t w[7];  // the lane's 28 window bytes
+      int rv;         // relo byte of (slot, DM)
+      uint32_t hw;    // the lane's step half-word
+    };
+    auto lread = [&](uint32_t word, Frag& f) {  // issue only: nothing here waits on LDS
+      f.hw = h ? (word >> 16) : (word & 0xFFFF);
+      const int slot = static_cast<int>(f.hw & 15), rel = static_cast<int>((f.hw >> 4) & 255);
+      const uint32_t* p = wb + ((slot * kMlWin + rel + sbase) >> 2);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) f.w[k] = p[k];
+      f.rv = rb[slot * 32 + r];  // unconditional: no divergent branch
+    };
+    auto mfma8 = [&](const Frag& f) {
+      // one-hot column: byte dl of the 16-byte K-half (dl outside [0, 16)
+      // -- negative or >= 16 -- gives (dl >> 2) outside 0..3: all zero)
+      const int dl = (f.hw & 4096) ? -1 : f.rv - static_cast<int>((f.hw >> 4) & 255);
+      const uint32_t* w = f.w;
       v4i bf;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) bf[q] = (delta >= 0 && (delta >> 2) == q) ? (1 << ((delta & 3) * 8)) : 0;
-      const int o0 = slot * kMlWin + rel + sbase;  // byte offset of m-tile 0's 16 bytes
+      for (int q = 0; q < 4; ++q) bf[q] = ((dl >> 2) == q) ? (1 << ((dl & 3) * 8)) : 0;
 #pragma unroll
       for (int m = 0; m < 8; ++m) {
-        const int o = o0 + 32 * m;
-        const uint32_t* p = reinterpret_cast<const uint32_t*>(wb + (o & ~3));
-        const uint32_t sh = static_cast<uint32_t>(o & 3);
-        const uint32_t w0 = p[0], w1 = p[1], w2 = p[2], w3 = p[3], w4 = p[4];
+        const int q = m >> 2;
+        const uint32_t sh = static_cast<uint32_t>(m & 3);
         v4i a;
-        a[0] = static_cast<int>(__builtin_amdgcn_alignbyte(w1, w0, sh));
-        a[1] = static_cast<int>(__builtin_amdgcn_alignbyte(w2, w1, sh));
-        a[2] = static_cast<int>(__builtin_amdgcn_alignbyte(w3, w2, sh));
-        a[3] = static_cast<int>(__builtin_amdgcn_alignbyte(w4, w3, sh));
+        a[0] = static_cast<int>(__builtin_amdgcn_alignbyte(w[q + 1], w[q], sh));
+        a[1] = static_cast<int>(__builtin_amdgcn_alignbyte(w[q + 2], w[q + 1], sh));
+        a[2] = static_cast<int>(__builtin_amdgcn_alignbyte(w[q + 3], w[q + 2], sh));
+        a[3] = static_cast<int>(__builtin_amdgcn_alignbyte(w[q + 4], w[q + 3], sh));
         acc[m] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, bf, acc[m], 0, 0, 0);
+      }
+    };
+    if (nst > 0) {
+      const int last = nst - 1;
+      Frag fA, fB;
+      lread(sw[0], fA);
+      uint32_t wordN = sw[min(1, last)];  // step s+1's word
+      for (int s = 0; s < nst; s += 2) {
+        // (sched_barrier: keep the prefetch reads in front of the MFMAs;
+        // left alone the scheduler sinks them and waits on them at once)
+        const uint32_t wordN2 = sw[min(s + 2, last)];
+        lread(wordN, fB);  // step s+1 (a harmless re-read past the end)
+        __builtin_amdgcn_sched_barrier(0);
+        mfma8(fA);  // step s
+        __builtin_amdgcn_sched_barrier(0);
+        if (s + 1 > last) break;
+        wordN = sw[min(s + 3, last)];
+        lread(wordN2, fA);  // step s+2
+        __builtin_amdgcn_sched_barrier(0);
+        mfma8(fB);  // step s+1
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     if (g + 1 < ngroups) lstore(b ^ 1);
     __syncthreads();
   }
-  // C/D layout (32x32): col = lane&31 (DM), row = (reg&3) + 8*(reg>>2) + 4*(lane>>5) (sample)
+  // C/D layout (32x32): col = lane&31 (DM), row = (reg&3) + 8*(reg>>2) + 4*(lane>>5);
+  // sub-tiles m = 0..7 of a (lane, reg) are the 8 consecutive samples 8*row + m
   const int d = tile * 32 + r;
   if (d >= ndm) return;
   uint8_t* o = out + static_cast<uint64_t>(d) * out_stride;
 #pragma unroll
-  for (int m = 0; m < 8; ++m) {
+  for (int e = 0; e < 16; ++e) {
+    const int row = (e & 3) + 8 * (e >> 2) + 4 * h;
+    const uint64_t t = t0 + wave * 256 + 8 * row;
+    uint32_t lo = 0, hi = 0;
 #pragma unroll
-    for (int gq = 0; gq < 4; ++gq) {
-      const uint64_t t = t0 + wave * 256 + m * 32 + 8 * gq + 4 * h;
-      uint32_t packed = 0;
+    for (int m = 0; m < 4; ++m) lo |= static_cast<uint32_t>(scale_out(acc[m][e] + bias_total, scale)) << (8 * m);
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        packed |= static_cast<uint32_t>(scale_out(acc[m][4 * gq + e] + bias_total, scale)) << (8 * e);
-      if (t + 4 <= out_nsamps) {
-        *reinterpret_cast<uint32_t*>(o + t) = packed;
-      } else {
-        for (int e = 0; e < 4; ++e)
-          if (t + e < out_nsamps) o[t + e] = static_cast<uint8_t>(packed >> (8 * e));
-      }
+    for (int m = 0; m < 4; ++m) hi |= static_cast<uint32_t>(scale_out(acc[m + 4][e] + bias_total, scale)) << (8 * m);
+    if (t + 8 <= out_nsamps) {
+      *reinterpret_cast<uint2*>(o + t) = make_uint2(lo, hi);
+    } else {
+      for (int m = 0; m < 8; ++m)
+        if (t + m < out_nsamps) o[t + m] = static_cast<uint8_t>((m < 4 ? lo : hi) >> (8 * (m & 3)));
     }
   }
 }
@@ -701,7 +759,7 @@ void build_mfma_lds_plan(const int32_t* offsets, int ndm, int nchans, const int3
   plan.ngroups = ngroups;
   plan.nactive = na;
   plan.steps.clear();
-  plan.deltas.clear();
+  plan.relo.assign(static_cast<size_t>(ntiles) * std::max(1, ngroups) * CG * 32, 0);
   plan.ginfo.assign(static_cast<size_t>(ntiles) * std::max(1, ngroups) * 2, 0);
   plan.wmin.assign(static_cast<size_t>(ntiles) * std::max(1, na), 0);
   plan.tile_ok.assign(static_cast<size_t>(ntiles), 0);
@@ -724,8 +782,9 @@ void build_mfma_lds_plan(const int32_t* offsets, int ndm, int nchans, const int3
       hi[ci] = b;
       const int w0 = a & ~15;
       plan.wmin[static_cast<size_t>(T) * na + ci] = w0;
-      // the last 16-shift block read ends at most (hi - w0) + 15 + 1023 + 4 bytes into the window
-      if ((hi[ci] - w0) + 15 + 1023 + 5 > kMfmaLdsWindow) ok = false;
+      // the last block starts at most (hi - w0) bytes in; a lane reads 7
+      // dwords from there + 256 * wave + 8 * row (<= 1016): 1044 bytes past it
+      if ((hi[ci] - w0) + 1044 > kMfmaLdsWindow) ok = false;
     }
     plan.tile_ok[static_cast<size_t>(T)] = ok ? 1 : 0;
     if (!ok) continue;  // the VALU kernels take this tile
@@ -734,43 +793,48 @@ void build_mfma_lds_plan(const int32_t* offsets, int ndm, int nchans, const int3
       std::vector<std::pair<int, int>> blocks;  // (slot, rel)
       for (int ci = g * CG; ci < std::min(na, (g + 1) * CG); ++ci) {
         const int w0 = plan.wmin[static_cast<size_t>(T) * na + ci];
-        for (int sb = lo[ci]; sb <= hi[ci]; sb += 16) blocks.emplace_back(ci - g * CG, sb - w0);
+        // blocks start on a multiple of 4 (w0 is one of 16): every window
+        // offset rel is 4-aligned, so the kernel's byte shifts are static
+        for (int sb = lo[ci] & ~3; sb <= hi[ci]; sb += 16) blocks.emplace_back(ci - g * CG, sb - w0);
       }
-      if (blocks.size() % 2) blocks.push_back(std::make_pair(-1, -1));  // dummy half (zero one-hot)
+      if (blocks.size() % 2) blocks.push_back(std::make_pair(-1, -1));  // empty half (zero one-hot)
       const int nst = static_cast<int>(blocks.size() / 2);
-      plan.ginfo[(static_cast<size_t>(T) * ngroups + g) * 2] = static_cast<int32_t>(plan.steps.size() / 4);
+      PSOUP_CHECK(nst <= kMfmaLdsMaxSteps, "MFMA-LDS plan: too many steps in a channel group");
+      while (plan.steps.size() % 4) plan.steps.push_back(0);  // 16-byte aligned group start
+      plan.ginfo[(static_cast<size_t>(T) * ngroups + g) * 2] = static_cast<int32_t>(plan.steps.size());
       plan.ginfo[(static_cast<size_t>(T) * ngroups + g) * 2 + 1] = nst;
       for (int st = 0; st < nst; ++st) {
+        uint32_t word = 0;
         for (int hh = 0; hh < 2; ++hh) {
           const auto blk = blocks[static_cast<size_t>(2 * st + hh)];
-          const bool dummy = blk.first < 0;
-          const auto use = dummy ? blocks[static_cast<size_t>(2 * st)] : blk;
-          plan.steps.push_back(use.first);
-          plan.steps.push_back(use.second);
+          const bool empty = blk.first < 0;
+          const auto use = empty ? blocks[static_cast<size_t>(2 * st)] : blk;  // a valid address
+          PSOUP_CHECK(use.second >= 0 && use.second < 256, "MFMA-LDS plan: window offset");
+          const uint32_t half = static_cast<uint32_t>(use.first) | (static_cast<uint32_t>(use.second) << 4) |
+                                (empty ? 4096u : 0u);
+          word |= half << (16 * hh);
         }
-        for (int hh = 0; hh < 2; ++hh) {
-          const auto blk = blocks[static_cast<size_t>(2 * st + hh)];
-          for (int rr = 0; rr < 32; ++rr) {
-            int delta = -1;
-            if (blk.first >= 0 && T * 32 + rr < ndm) {
-              const int ci = g * CG + blk.first;
-              const int w0 = plan.wmin[static_cast<size_t>(T) * na + ci];
-              const int dv = off(rr, active[ci]) - (w0 + blk.second);
-              if (dv >= 0 && dv < 16) delta = dv;
-            }
-            plan.deltas.push_back(static_cast<int8_t>(delta));
-          }
+        plan.steps.push_back(static_cast<int32_t>(word));
+      }
+      for (int ci = g * CG; ci < std::min(na, (g + 1) * CG); ++ci) {
+        const int w0 = plan.wmin[static_cast<size_t>(T) * na + ci];
+        uint8_t* dst = &plan.relo[((static_cast<size_t>(T) * ngroups + g) * CG + (ci - g * CG)) * 32];
+        for (int rr = 0; rr < 32; ++rr) {
+          const int v = off(rr, active[ci]) - w0;  // padded DMs repeat the last one (never stored)
+          PSOUP_CHECK(v >= 0 && v < 256, "MFMA-LDS plan: relative offset");
+          dst[rr] = static_cast<uint8_t>(v);
         }
       }
       tsteps += nst;
     }
     plan.tile_steps[static_cast<size_t>(T)] = tsteps;
-    PSOUP_CHECK(plan.steps.size() / 4 < (1ull << 31), "MFMA-LDS dedispersion plan too large");
+    PSOUP_CHECK(plan.steps.size() < (1ull << 31), "MFMA-LDS dedispersion plan too large");
   }
+  plan.steps.resize(plan.steps.size() + kMfmaLdsMaxSteps, 0);  // the staging reads a full step block
 }
 
 void dedisperse_mfma_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_active, int nactive,
-                         const int32_t* d_steps, const int8_t* d_deltas, const int32_t* d_ginfo, int ngroups,
+                         const int32_t* d_steps, const uint8_t* d_relo, const int32_t* d_ginfo, int ngroups,
                          const int32_t* d_wmin, int ntiles, int ndm, uint64_t out_nsamps, uint8_t* out,
                          uint64_t out_stride, float scale, int bias_total, hipStream_t s) {
   if (ndm <= 0 || out_nsamps == 0 || nactive <= 0) return;
@@ -780,7 +844,7 @@ void dedisperse_mfma_lds(const int8_t* chan_major, uint64_t chan_stride, const i
   PSOUP_CHECK(ty <= 65535, "dedisperse_mfma_lds: series too long for the grid");
   dim3 grid(static_cast<unsigned>(ntiles), static_cast<unsigned>(ty));
   dedisperse_mfma_lds_kernel<kMfmaLdsGroup><<<grid, 256, 0, s>>>(
-      chan_major, chan_stride, d_active, nactive, reinterpret_cast<const int4*>(d_steps), d_deltas,
+      chan_major, chan_stride, d_active, nactive, reinterpret_cast<const uint32_t*>(d_steps), d_relo,
       reinterpret_cast<const int2*>(d_ginfo), ngroups, d_wmin, ndm, out_nsamps, out, out_stride, scale, bias_total);
   post_launch_check("dedisperse_mfma_lds_kernel", s);
 }

@@ -354,7 +354,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("use_boundaries", &CmdLineOptions::use_boundaries)
       .def_readwrite("checkpoint_dir", &CmdLineOptions::checkpoint_dir)
       .def_readwrite("trace_json", &CmdLineOptions::trace_json)
-      .def_readwrite("fault_after_dms", &CmdLineOptions::fault_after_dms);
+      .def_readwrite("fault_after_dms", &CmdLineOptions::fault_after_dms)
+      .def_readwrite("time_shards", &CmdLineOptions::time_shards);
   m.def("parse_cmdline", [](const std::vector<std::string>& argv) {
     CmdLineOptions a;
     bool exit_now = false;

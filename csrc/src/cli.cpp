@@ -246,6 +246,10 @@ static std::vector<Spec> peasoup_specs(CmdLineOptions& a) {
       val_s("", "checkpoint_dir", "Spill per-DM candidates here and resume from it", a.checkpoint_dir),
       val_s("", "trace_json", "Write per-stage timings as JSON to this file", a.trace_json),
       val_n("", "fault_after_dms", "Testing: abort after this many DM trials", a.fault_after_dms),
+      sw("", "time_shards",
+         "Python driver under torchrun: each rank holds only its time slice of the filterbank; ring halo exchange "
+         "+ all-to-all corner turn to DM shards (series too long to replicate on every GPU)",
+         a.time_shards),
   };
 }
 

@@ -218,7 +218,7 @@ void Dedisperser::build_mfma_lds_tables() {
     if (!host.empty()) PSOUP_HIP_CHECK(hipMemcpy(dev.data(), host.data(), host.size() * sizeof(T), hipMemcpyHostToDevice));
   };
   up(ml_steps_, plan.steps);
-  up(ml_deltas_, plan.deltas);
+  up(ml_relo_, plan.relo);
   up(ml_ginfo_, plan.ginfo);
   up(ml_wmin_, plan.wmin);
   ml_ready_ = true;
@@ -227,10 +227,11 @@ void Dedisperser::build_mfma_lds_tables() {
 static double mfma_lds_ratio() {
   // LDS-fed MFMA steps per (tile, active channel) up to which a tile takes the
   // MFMA kernel in Auto (each step is 2 x 16-shift blocks of one-hot GEMM;
-  // the VALU kernels cost the same per channel whatever the spread)
+  // the VALU kernels cost the same per channel whatever the spread).
+  // Measured crossover on MI355X (profiles/r3_dedisp): ~2.35 steps/channel
   static const double r = [] {
     const char* e = std::getenv("PSOUP_DEDISP_MFMA_RATIO");
-    return e ? std::atof(e) : 2.5;
+    return e ? std::atof(e) : 2.3;
   }();
   return r;
 }
@@ -252,7 +253,8 @@ void Dedisperser::run_mfma_lds(int d0, int d1, uint8_t* out, uint64_t out_stride
   if (!ml_ready_) build_mfma_lds_tables();
   const int T0 = d0 / kTileDms, nt = (d1 - d0 + kTileDms - 1) / kTileDms;
   kern::dedisperse_mfma_lds(fb_.data(), fb_.stride(), d_active_.data(), g.nactive, ml_steps_.data(),
-                            ml_deltas_.data(), ml_ginfo_.data() + static_cast<size_t>(T0) * ml_ngroups_ * 2,
+                            ml_relo_.data() + static_cast<size_t>(T0) * ml_ngroups_ * kern::kMfmaLdsGroup * 32,
+                            ml_ginfo_.data() + static_cast<size_t>(T0) * ml_ngroups_ * 2,
                             ml_ngroups_, ml_wmin_.data() + static_cast<size_t>(T0) * g.nactive, nt, d1 - d0,
                             g.out_nsamps, out, out_stride, g.out_scale, g.bias * g.nactive, s);
 }

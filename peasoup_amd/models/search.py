@@ -91,7 +91,10 @@ class RankSearcher:
     """Per-rank search state: resident filterbank, dedisperser, engine."""
 
     def __init__(self, args, header: dict, packed: Optional[torch.Tensor], nsamps: int,
-                 killmask: Optional[Sequence[int]] = None, fft_mode: Optional[int] = None):
+                 killmask: Optional[Sequence[int]] = None, fft_mode: Optional[int] = None, resident: bool = True):
+        """``resident=False``: no device filterbank / dedisperser (the
+        time-sharded path hands DM trials over already dedispersed:
+        :meth:`search_rows`, ``fold(..., rows=...)``)."""
         self.ctx = pdist.context()
         self.args = args
         self.header = dict(header)
@@ -113,10 +116,12 @@ class RankSearcher:
         # stream; torch work that produced `packed` is drained first
         self.stream = _engine_stream(self.ctx.device)
         torch.cuda.synchronize(self.ctx.device)
-        self.dfb = _C.DeviceFilterbank(self.geom, self.stream)
-        if packed is not None:
-            self.load_packed(packed)
-        self.dedisperser = _C.Dedisperser(self.dfb, self.stream)
+        self.dfb = self.dedisperser = None
+        if resident:
+            self.dfb = _C.DeviceFilterbank(self.geom, self.stream)
+            if packed is not None:
+                self.load_packed(packed)
+            self.dedisperser = _C.Dedisperser(self.dfb, self.stream)
         self.kernel = {"auto": _C.DedispKernel.Auto, "mfma": _C.DedispKernel.Mfma, "valu": _C.DedispKernel.Valu,
                        "direct": _C.DedispKernel.Direct}[args.dedisp_kernel]
         self.row_stride = _C.Dedisperser.row_stride(self.geom.out_nsamps)
@@ -323,6 +328,36 @@ class RankSearcher:
         self.accel_trials = ntrials
         return cands
 
+    def search_rows(self, rows: torch.Tensor, dm_first: int, timers: Optional[Dict[str, Stopwatch]] = None) -> list:
+        """Search DM trials already resident on the GPU: ``rows`` is uint8
+        ``[n, row_stride]``, row i = DM trial ``dm_first + i`` (the time-sharded
+        path's DM shard after the corner turn).  Whitened in batches of
+        ``max_prepare`` and searched as flat trial lists, like :meth:`search`."""
+        assert rows.dtype == torch.uint8 and rows.is_cuda and rows.shape[1] == self.row_stride
+        rows = rows.contiguous()
+        t_s = timers.get("searching") if timers else None
+        if t_s:
+            t_s.start()
+        torch.cuda.current_stream(self.ctx.device).synchronize()  # rows were produced on torch's stream
+        e = self.engine
+        cands: list = []
+        ntrials = 0
+        base = rows.data_ptr()
+        for p0 in range(0, rows.shape[0], e.max_prepare):
+            cnt = min(e.max_prepare, rows.shape[0] - p0)
+            e.prepare(base + p0 * self.row_stride, self.row_stride, self.geom.out_nsamps, cnt)
+            jobs = [(b, self.dm_list[d], d, self.accel_list(self.dm_list[d]))
+                    for b, d in enumerate(range(dm_first + p0, dm_first + p0 + cnt))]
+            for (_, _, _, accs), c in zip(jobs, e.search_prepared_many(jobs)):
+                cands.extend(c)
+                ntrials += len(accs)
+        _C.stream_synchronize(e.stream)
+        if t_s:
+            t_s.stop()
+        self.accel_trials = ntrials
+        self.blocks_done = []
+        return cands
+
     def _executor(self):
         if self._pool is None:
             self._pool = concurrent.futures.ThreadPoolExecutor(len(self.engines), thread_name_prefix="psoup-eng")
@@ -336,8 +371,11 @@ class RankSearcher:
                 out[key] = out.get(key, 0) + v
         return out
 
-    def fold(self, groups: Dict[int, List[int]], cands: list) -> Dict[int, tuple]:
-        """Fold candidates (index -> (folded_snr, opt_period, fold)) for the DM groups given."""
+    def fold(self, groups: Dict[int, List[int]], cands: list, rows: Optional[torch.Tensor] = None,
+             dm_first: int = 0) -> Dict[int, tuple]:
+        """Fold candidates (index -> (folded_snr, opt_period, fold)) for the DM
+        groups given; the DM trials are dedispersed again, or taken from
+        resident ``rows`` (row i = DM ``dm_first + i``, see :meth:`search_rows`)."""
         out: Dict[int, tuple] = {}
         if not groups:
             return out
@@ -353,9 +391,14 @@ class RankSearcher:
             # and folded together (one accumulate / optimise launch)
             buf = torch.empty(len(batch) * self.row_stride, dtype=torch.uint8, device=self.ctx.device)
             torch.cuda.current_stream(self.ctx.device).synchronize()  # the allocation is ours on self.stream
-            for t, (dm_idx, _) in enumerate(batch):
-                self.dedisperser.run(dm_idx, dm_idx + 1, buf.data_ptr() + t * self.row_stride, self.row_stride,
-                                     self.kernel, self.stream)
+            if rows is not None:
+                idx = torch.tensor([d - dm_first for d, _ in batch], dtype=torch.int64, device=rows.device)
+                buf.view(len(batch), self.row_stride).copy_(rows.index_select(0, idx))
+                torch.cuda.current_stream(self.ctx.device).synchronize()
+            else:
+                for t, (dm_idx, _) in enumerate(batch):
+                    self.dedisperser.run(dm_idx, dm_idx + 1, buf.data_ptr() + t * self.row_stride, self.row_stride,
+                                         self.kernel, self.stream)
             periods = [[float(struct.unpack("f", struct.pack("f", 1.0 / cands[i].freq))[0]) for i in members]
                        for _, members in batch]
             accs = [[cands[i].acc for i in members] for _, members in batch]
@@ -385,6 +428,17 @@ def _decode_fold_results(b: bytes) -> Dict[int, tuple]:
         off += 4 * nf
         out[i] = (snr, per, fold)
     return out
+
+
+def broadcast_header(infilename: str, ctx: pdist.DistContext) -> dict:
+    """Rank 0 reads the SIGPROC header; every rank gets it (RCCL broadcast)."""
+    hdr_bytes = None
+    if ctx.is_root:
+        hdr_bytes = repr(_C.read_header(infilename)).encode()
+    hdr_bytes = pdist.broadcast_object_bytes(hdr_bytes)
+    import ast
+
+    return ast.literal_eval(hdr_bytes.decode())
 
 
 def load_packed_for_rank(infilename: str, ctx: pdist.DistContext):
@@ -448,17 +502,53 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     timers = {k: Stopwatch() for k in ("reading", "dedispersion", "searching", "folding", "total")}
     timers["total"].start()
     timers["reading"].start()
-    header, packed, nsamps = load_packed_for_rank(args.infilename, ctx)
+    sharded = bool(getattr(args, "time_shards", False))
+    if sharded:
+        header, packed, nsamps = broadcast_header(args.infilename, ctx), None, 0
+        nsamps = int(header["nsamples"])
+    else:
+        header, packed, nsamps = load_packed_for_rank(args.infilename, ctx)
     timers["reading"].stop()
 
-    rs = RankSearcher(args, header, packed, nsamps)
+    rs = RankSearcher(args, header, packed, nsamps, resident=not sharded)
     del packed
     ndm = len(rs.dm_list)
     weights = [len(rs.accel_list(d)) for d in rs.dm_list]
-    schedule = dm_schedule(args, ctx.world_size, ndm)
+    schedule = "time_sharded" if sharded else dm_schedule(args, ctx.world_size, ndm)
+    rows = None
+    row_first = 0
     pdist.barrier()
     t0 = time.perf_counter()
-    if schedule == "dynamic":
+    if sharded:
+        # every rank holds only its time slice of the filterbank;
+        # ring halo exchange + all-to-all corner turn hand each rank whole DM
+        # series for its trial-weighted DM shard, searched in place
+        from ..parallel import timeshard
+
+        plan = timeshard.make_plan(rs.header, nsamps, rs.dm_list, ctx.world_size, weights)
+        timers["reading"].start()
+        fb = _C.Filterbank.from_file(args.infilename)
+        rr = plan.input_range(ctx.rank)
+        with warnings.catch_warnings():  # read-only mmap view, only copied to the device
+            warnings.simplefilter("ignore", UserWarning)
+            own = torch.from_numpy(fb.data()[rr.start * plan.bytes_per_sample:rr.stop * plan.bytes_per_sample])
+            own = own.to(ctx.device)
+        del fb
+        timers["reading"].stop()
+        timers["dedispersion"].start()
+        dd = timeshard.native_dedisperser(rs.header, rs.dm_list, list(rs.geom.killmask), kernel=args.dedisp_kernel)
+        trials = timeshard.time_sharded_dedisperse(own, plan, dd)
+        del own
+        shard = plan.dm_shards[ctx.rank]
+        rows = torch.zeros((len(shard), rs.row_stride), dtype=torch.uint8, device=ctx.device)
+        rows[:, :rs.geom.out_nsamps] = trials
+        del trials
+        torch.cuda.synchronize()
+        timers["dedispersion"].stop()
+        row_first = shard.start
+        local = rs.search_rows(rows, shard.start, timers)
+        local_trials = sum(weights[i] for i in shard)
+    elif schedule == "dynamic":
         # DMDispenser across processes: every rank claims 32-DM chunks of the
         # whole list from one shared first-come queue (pipeline_multi.cu:33-81)
         blocks = rs.chunk_ranges(range(ndm), DYNAMIC_CHUNK)
@@ -499,8 +589,11 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
             if 0.001 < p < 10.0:
                 groups.setdefault(cands[i].dm_idx, []).append(i)
         keys = sorted(groups)
-        mine = {k: groups[k] for j, k in enumerate(keys) if j % ctx.world_size == ctx.rank}
-        res = rs.fold(mine, cands)
+        if rows is not None:  # time-sharded: the owner of the DM row folds it
+            mine = {k: groups[k] for k in keys if row_first <= k < row_first + rows.shape[0]}
+        else:
+            mine = {k: groups[k] for j, k in enumerate(keys) if j % ctx.world_size == ctx.rank}
+        res = rs.fold(mine, cands, rows=rows, dm_first=row_first)
         parts = pdist.gather_bytes(_encode_fold_results(res), dst=0)
         if ctx.is_root:
             for p in parts:

@@ -151,8 +151,9 @@ def reference_dedisperser(header: dict, dm_list: Sequence[float], killmask=None)
     return fn
 
 
-def native_dedisperser(header: dict, dm_list: Sequence[float], killmask=None, kernel: str = "mfma") -> DedispFn:
-    """MFMA dedispersion of the rank's (haloed) window on its GPU."""
+def native_dedisperser(header: dict, dm_list: Sequence[float], killmask=None, kernel: str = "auto") -> DedispFn:
+    """Dedispersion of the rank's (haloed) window on its GPU (kernel: auto |
+    mfma | valu | direct; bit-identical outputs)."""
     from .. import _C
 
     def fn(packed: torch.Tensor, nin: int, nout: int) -> torch.Tensor:
@@ -166,7 +167,8 @@ def native_dedisperser(header: dict, dm_list: Sequence[float], killmask=None, ke
         dd = _C.Dedisperser(dfb, stream)
         stride = _C.Dedisperser.row_stride(nout)
         out = torch.empty((len(dm_list), stride), dtype=torch.uint8, device=packed.device)
-        k = _C.DedispKernel.Mfma if kernel == "mfma" else _C.DedispKernel.Direct
+        k = {"auto": _C.DedispKernel.Auto, "mfma": _C.DedispKernel.Mfma, "valu": _C.DedispKernel.Valu,
+             "direct": _C.DedispKernel.Direct}[kernel]
         dd.run(0, len(dm_list), out.data_ptr(), stride, k)
         torch.cuda.current_stream().synchronize()
         return out[:, :nout]

@@ -77,3 +77,56 @@ def write(path: str, nsamps: int, header: Optional[Dict] = None, pulsars=(), see
 
 def packed(nsamps: int, header: Dict, pulsars=(), seed: int = 0) -> np.ndarray:
     return pack_samples(generate(nsamps, header, pulsars, seed), int(header["nbits"]))
+
+
+def generate_packed_torch(nsamps: int, header: Dict, pulsars=(), seed: int = 0, device=None,
+                          chunk: int = 1 << 15, birdies=()):
+    """GPU form of :func:`packed` (same noise model, quantiser, dispersion and
+    acceleration law; torch's generator instead of NumPy's, so not the same
+    noise samples): packed SIGPROC bytes as a uint8 tensor on ``device``.
+    ``birdies``: (frequency Hz, amplitude) sinusoids added to every channel
+    (periodic RFI: strong, undispersed, many harmonics of threshold crossings).
+    Minutes-long 2^23-sample, 1024-channel filterbanks take seconds."""
+    import torch
+
+    dev = torch.device(device) if device is not None else torch.device("cuda")
+    g = torch.Generator(device=dev)
+    g.manual_seed(int(seed))
+    nchans = int(header["nchans"])
+    nbits = int(header["nbits"])
+    tsamp = float(header["tsamp"])
+    fch1 = float(header["fch1"])
+    foff = float(header["foff"])
+    levels = (1 << nbits) - 1
+    mean = levels / 2.0
+    sigma = max(levels / 4.0, 0.5)
+    per = 8 // nbits if nbits < 8 else 1
+    assert nbits in (1, 2, 4, 8) and nchans % per == 0
+    freqs = fch1 + foff * torch.arange(nchans, device=dev, dtype=torch.float64)
+    out = torch.empty(nsamps * nchans * nbits // 8, dtype=torch.uint8, device=dev)
+    row = nchans * nbits // 8
+    for t0 in range(0, nsamps, chunk):
+        n = min(chunk, nsamps - t0)
+        x = torch.randn((n, nchans), device=dev, generator=g)
+        t = (torch.arange(t0, t0 + n, device=dev, dtype=torch.float64) * tsamp)[:, None]
+        for p in pulsars:
+            delay = 4.15e3 * p.dm * (1.0 / freqs ** 2 - 1.0 / fch1 ** 2)
+            te = t - delay[None, :]
+            ph = (te - p.accel * te * te / (2 * C_LIGHT)) / p.period + p.phase
+            ph = ph - torch.floor(ph)
+            d = torch.minimum(ph, 1.0 - ph)
+            w = p.duty / 2.3548
+            x += (p.amplitude * torch.exp(-0.5 * (d / w) ** 2)).float()
+        for f, amp in birdies:
+            x += (amp * torch.sin(2 * np.pi * f * t)).float()
+        q = torch.clamp(torch.round(mean + sigma * x), 0, levels).to(torch.uint8)
+        if nbits == 8:
+            packed = q.reshape(-1)
+        else:
+            q = q.view(n, nchans // per, per).to(torch.int32)
+            acc = torch.zeros((n, nchans // per), dtype=torch.int32, device=dev)
+            for k in range(per):
+                acc |= q[..., k] << (k * nbits)
+            packed = acc.to(torch.uint8).reshape(-1)
+        out[t0 * row:(t0 + n) * row] = packed
+    return out

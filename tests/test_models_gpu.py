@@ -172,6 +172,47 @@ def test_dynamic_schedule_four_ranks_many_chunks(tmp_path):
     assert min(blocks) >= 1, blocks
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_time_sharded_run_search_equals_replicated(tmp_path, world):
+    """--time_shards: every rank holds only its time slice of tutorial.fil,
+    ring halo exchange + all-to-all corner turn to DM shards, search and fold
+    of the rank's resident DM rows; the output files equal the
+    replicated single-rank run's byte for byte."""
+    port = _free_port()
+    script = (
+        "import os,sys; sys.path.insert(0, %r)\n"
+        "from peasoup_amd.parallel import dist as pdist\n"
+        "pdist.init(backend='gloo')\n"
+        "from peasoup_amd import _C\n"
+        "from peasoup_amd.models.search import run_search\n"
+        "extra = ['--time_shards'] if sys.argv[2] == '1' else []\n"
+        "ok,_,a=_C.parse_cmdline(['peasoup','-i',%r,'-o',sys.argv[1],'--dm_end','120','-n','4','--npdmp','6',"
+        "'--acc_start','-5','--acc_end','5','--trace_json',sys.argv[1]+'.json'] + extra)\n"
+        "assert a.time_shards == bool(extra)\n"
+        "run_search(a)\n"
+        "pdist.shutdown()\n" % (REPO, TUTORIAL))
+    f = tmp_path / "run.py"
+    f.write_text(script)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world))
+    procs = [subprocess.Popen([sys.executable, str(f), str(tmp_path / "ts"), "1"],
+                              env=dict(env, RANK=str(r), LOCAL_RANK="0"), stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE, text=True) for r in range(world)]
+    for p in procs:
+        out, err = p.communicate(timeout=600)
+        assert p.returncode == 0, err[-3000:]
+    r = subprocess.run([sys.executable, str(f), str(tmp_path / "rep"), "0"],
+                       env=dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), capture_output=True,
+                       text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    a = open(tmp_path / "ts" / "candidates.peasoup", "rb").read()
+    b = open(tmp_path / "rep" / "candidates.peasoup", "rb").read()
+    assert a == b and len(a) > 1000
+    import json
+
+    devs = json.load(open(str(tmp_path / "ts") + ".json"))["devices"]
+    assert [d["dm_schedule"] for d in devs] == ["time_sharded"] * world
+
+
 def test_forced_rccl_process_group_world1(tmp_path):
     """PSOUP_FORCE_PG=1: a world-1 RCCL process group, so every collective the
     pipeline uses (broadcast_bytes, broadcast_object_bytes, gather_bytes,

@@ -253,3 +253,47 @@ def test_native_oversubscribed_device_workers_match_one(tmp_path):
     devs = json.load(open(tmp_path / "4.json"))["devices"]
     assert len(devs) == 4 and sum(d["dm_trials"] for d in devs) == 59
     assert sum(1 for d in devs if d["dm_trials"] > 0) >= 2  # the DM queue was shared
+
+
+def test_headline_shape_binary_pulsar_and_fft_modes(C):
+    """The bench's search at its shape -- 2^23 x 64 us, +-500 m/s^2 (legacy
+    plan, 685 trials per DM), -n 3 -- on a 256-channel filterbank with an
+    injected binary pulsar, through RankSearcher.search +
+    global_distill_and_score (pipeline_multi.cu:209-243, 364-369): recovered
+    at its DM, acceleration and fundamental frequency, and the fused
+    four-step FFT (fft_mode 2) gives the candidate list of rocFFT R2C
+    (fft_mode 0)."""
+    from peasoup_amd.models.search import RankSearcher
+    from peasoup_amd.utils import synthetic
+
+    nchans, tsamp, fch1, foff = 256, 64e-6, 1550.0, -400.0 / 256
+    psr = synthetic.PulsarSpec(period=0.0073, dm=50.0, duty=0.06, amplitude=0.03, accel=210.0)
+    n = 1 << 23
+    dms = C.generate_dm_list(44.0, 56.0, tsamp, 64.0, fch1, foff, nchans, 1.1)
+    nsamps = n + C.compute_max_delay(dms, C.generate_delay_table(nchans, tsamp, fch1, foff)) + 4096
+    hdr = synthetic.make_header(nchans=nchans, nbits=2, tsamp=tsamp, fch1=fch1, foff=foff, nsamples=nsamps)
+    packed = synthetic.generate_packed_torch(nsamps, hdr, [psr], seed=23, device="cuda")
+    ok, _, args = C.parse_cmdline(["peasoup", "-i", "synthetic", "--dm_start", "44", "--dm_end", "56",
+                                   "--acc_start", "-500", "--acc_end", "500", "-n", "3", "--fft_size", str(n)])
+    assert ok
+    lists = {}
+    for mode in (2, 0):
+        rs = RankSearcher(args, hdr, packed, nsamps, fft_mode=mode)
+        assert rs.engine.fft_mode == mode
+        assert len(rs.accel_list(rs.dm_list[0])) > 680
+        cands = rs.search(range(len(rs.dm_list)))
+        lists[mode] = C.global_distill_and_score(cands, args, rs.header)
+        del rs
+        torch.cuda.empty_cache()
+    best = lists[2][0]
+    f0 = 1.0 / psr.period
+    assert abs(best.freq / f0 - 1.0) < 2e-4, (best.freq, f0)
+    assert abs(best.dm - psr.dm) < 3.0, best.dm
+    assert abs(best.acc - psr.accel) < 6.0, best.acc
+    assert best.snr > 30, (best.nh, best.snr)
+    strong = {m: [c for c in lists[m] if c.snr >= 9.05] for m in lists}
+    assert len(strong[0]) == len(strong[2]) > 3
+    for a, b in zip(strong[0], strong[2]):
+        assert b.freq == pytest.approx(a.freq, rel=1e-7)
+        assert (b.dm, b.nh, b.acc) == (a.dm, a.nh, a.acc)
+        assert b.snr == pytest.approx(a.snr, rel=1e-4)

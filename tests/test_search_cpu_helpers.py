@@ -54,3 +54,13 @@ def test_dynamic_blocks_cover_the_dm_list_once():
         blocks = RankSearcher.chunk_ranges(range(ndm), DYNAMIC_CHUNK)
         assert [d for b in blocks for d in range(*b)] == list(range(ndm))
         assert all(b[0] % DYNAMIC_CHUNK == 0 for b in blocks)
+
+
+def test_time_shards_option():
+    """--time_shards (Python driver: halo exchange + all-to-all corner turn)."""
+    from peasoup_amd import _C
+
+    ok, _, a = _C.parse_cmdline(["peasoup", "-i", "x.fil"])
+    assert ok and a.time_shards is False
+    ok, _, a = _C.parse_cmdline(["peasoup", "-i", "x.fil", "--time_shards"])
+    assert ok and a.time_shards is True

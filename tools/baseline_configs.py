@@ -132,10 +132,37 @@ def config3(a):
             "best_period_s": (1.0 / best.freq) if best else None, "best_snr": best.snr if best else None}
 
 
+def config5_pulsars(n: int = 64, seed: int = 5):
+    """The config-5 sky: n pulsars with incommensurate periods (2 ms - 1 s,
+    log-uniform), DMs over the searched range, accelerations within +-100
+    m/s^2 and 3-12% duty cycles, bright enough that each survives the
+    harmonic / acceleration / DM distillation as its own candidate family:
+    >= 128 candidates to fold (verdict r2: the single-pulsar file gave 22)."""
+    from peasoup_amd.utils import synthetic
+
+    rng = np.random.default_rng(seed)
+    periods = np.exp(rng.uniform(np.log(0.002), np.log(1.0), n))
+    return [synthetic.PulsarSpec(period=float(p), dm=float(rng.uniform(20.0, 1100.0)),
+                                 duty=float(rng.uniform(0.03, 0.12)), amplitude=float(rng.uniform(0.06, 0.12)),
+                                 accel=float(rng.uniform(-100.0, 100.0)), phase=float(rng.random()))
+            for p in periods]
+
+
 def _make_fb(a, ctx):
-    path = os.path.join(a.workdir, f"cfg45_{a.log2n}.fil")
+    path = os.path.join(a.workdir, f"cfg45_{a.log2n}_multi.fil")
     if ctx.is_root and not os.path.exists(path):
-        gpu_filterbank(path, (1 << a.log2n) + 65536, 1024, TSAMP, FCH1, FOFF, 0.0371, 110.0, 0.05, 0.08, 7)
+        from peasoup_amd.utils import synthetic
+        from peasoup_amd.utils.sigproc import header_bytes as _hb
+
+        nsamps = (1 << a.log2n) + 65536
+        hdr = {"source_name": "synthetic: 64 pulsars (tools/baseline_configs.config5_pulsars)", "tsamp": TSAMP,
+               "fch1": FCH1, "foff": FOFF, "nchans": 1024, "nbits": 2, "nifs": 1, "data_type": 1,
+               "tstart": 60000.0, "nsamples": nsamps}
+        packed = synthetic.generate_packed_torch(nsamps, hdr, config5_pulsars(), seed=7)
+        with open(path, "wb") as f:
+            f.write(_hb(hdr))
+            f.write(packed.cpu().numpy().tobytes())
+        del packed
     pdist.barrier()
     return path
 

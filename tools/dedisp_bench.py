@@ -98,11 +98,16 @@ def main():
     e1.record(s.handle)
     e1.synchronize()
     tot["auto_whole"] = round(e0.elapsed_ms(e1), 2)
+    e0.record(s.handle)
+    dd.run(0, ndm, whole.data_ptr(), rs, _C.DedispKernel.Valu, s.handle)
+    e1.record(s.handle)
+    e1.synchronize()
+    tot["valu_whole"] = round(e0.elapsed_ms(e1), 2)
     tot["split_dm"] = dd.mfma_lds_split(0, ndm)
     gsamp = ndm * g.out_nsamps * g.nactive / 1e9
     print(json.dumps({"ndm": ndm, "nchans": a.nchans, "nbits": a.nbits, "out_nsamps": g.out_nsamps,
                       "total_ms": {"mfma": tot["m"], "valu": tot["v"], "auto": tot["auto"],
-                                   "auto_whole_list": tot["auto_whole"]},
+                                   "auto_whole_list": tot["auto_whole"], "valu_whole_list": tot["valu_whole"]},
                       "mfma_lds_split_dm_index": tot["split_dm"],
                       "G_chan_samples_per_s": {k: round(gsamp / (v * 1e-3), 1) for k, v in
                                                (("mfma", tot["m"]), ("valu", tot["v"]), ("auto", tot["auto"]))}}))
