@@ -63,6 +63,8 @@ def parse():
     p.add_argument("--signal", action="store_true",
                    help="peak-heavy data instead of pure noise: injected pulsars plus strong undispersed periodic "
                         "RFI (>= 1e4 threshold crossings per DM), to time the host clustering / distillation")
+    p.add_argument("--rfi-amp", type=float, default=0.05,
+                   help="--signal: amplitude of the two undispersed RFI pulse trains (the pulsars: 0.05-0.08)")
     return p.parse_args()
 
 
@@ -124,8 +126,8 @@ def main() -> int:
         # threshold in every acceleration trial of every DM)
         sky = [synthetic.PulsarSpec(period=0.00731, dm=2.0, duty=0.05, amplitude=0.05, accel=120.0),
                synthetic.PulsarSpec(period=0.1532, dm=1.0, duty=0.04, amplitude=0.08, accel=-40.0),
-               synthetic.PulsarSpec(period=0.02, dm=0.0, duty=0.02, amplitude=0.6),
-               synthetic.PulsarSpec(period=0.06, dm=0.0, duty=0.03, amplitude=0.4)]
+               synthetic.PulsarSpec(period=0.02, dm=0.0, duty=0.02, amplitude=a.rfi_amp),
+               synthetic.PulsarSpec(period=0.06, dm=0.0, duty=0.03, amplitude=0.67 * a.rfi_amp)]
         packed.copy_(synthetic.generate_packed_torch(nsamps, header, sky, seed=a.seed, device=dev))
     elif ctx.is_root:
         g = torch.Generator(device=dev)

@@ -15,6 +15,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -82,6 +83,12 @@ class Dedisperser {
   // upload.
   void run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispKernel kind = DedispKernel::Auto,
            hipStream_t s = nullptr);
+  // An arbitrary list of DM indices (row i = DM dms[i]) in ONE packed-byte
+  // VALU launch over ceil(n / 32) DM tiles (the fold stage: scattered DMs,
+  // where per-DM runs would each pay a whole tile).  Bit-identical to run().
+  // Waits for its offset-table upload (the host table goes out of scope);
+  // successive calls must share one stream (the device table is reused).
+  void run_list(const std::vector<int>& dms, uint8_t* out, uint64_t out_stride, hipStream_t s = nullptr);
   static uint64_t row_stride(uint64_t out_nsamps) { return (out_nsamps + 255) / 256 * 256; }
   static constexpr int kTileDms = 32;  // DMs per MFMA tile
   // Auto's choice for [d0, d1): one-hot MFMA while the tiles' offset spread is
@@ -101,7 +108,7 @@ class Dedisperser {
   void run_mfma_lds(int d0, int d1, uint8_t* out, uint64_t out_stride, hipStream_t s);
   const DeviceFilterbank& fb_;
   hipStream_t stream_;
-  DeviceBuffer<int32_t> d_offsets_, d_kill_, d_active_, d_steps_, d_tile_info_;
+  DeviceBuffer<int32_t> d_offsets_, d_kill_, d_active_, d_steps_, d_tile_info_, d_list_offT_;
   DeviceBuffer<int8_t> d_deltas_;
   bool resident_ = false, valu_ready_ = false;
   std::vector<int32_t> h_tile_steps_;  // resident plan: MFMA steps per tile
@@ -272,9 +279,14 @@ class SearchEngine {
  private:
   struct Slot {
     DeviceBuffer<kern::PeakRecord> d_peaks;
-    DeviceBuffer<uint32_t> d_count;
+    DeviceBuffer<uint32_t> d_count;  // [0] threshold crossings, [1] cluster peaks (GPU clustering)
     PinnedBuffer<kern::PeakRecord> h_peaks;
     PinnedBuffer<uint32_t> h_count;
+    // GPU clustering (kern::peak_cluster_batch): segment work/table, the
+    // crossings grouped by segment, the cluster peaks; host copies
+    DeviceBuffer<uint32_t> d_work;
+    DeviceBuffer<uint2> d_sorted, d_clust, d_segtab;
+    PinnedBuffer<uint2> h_clust, h_raw, h_segtab;
     std::unique_ptr<Event> done, copied;
     int first = 0, count = 0;
   };
@@ -285,6 +297,17 @@ class SearchEngine {
   // first/count/npeaks are the batch's values captured before the slot was
   // re-issued (launch_batch overwrites Slot::first/count/h_count)
   void process_slot(Slot& s, int first, int count, uint32_t npeaks, std::vector<CandidateList>& out_by_job);
+  // GPU-clustered batch: segtab is the batch's segment table (snapshot taken
+  // before the slot was re-issued), cluster peaks in s.h_clust, raw segments
+  // in s.h_raw
+  void process_clustered(Slot& s, int first, int count, const std::vector<uint2>& segtab,
+                         std::vector<CandidateList>& out_by_job);
+  // per-trial candidates from (idx, snr) cluster peaks of each level, then the
+  // harmonic distiller; trials [0, count) over the host pool when heavy
+  void build_trials(int first, int count, size_t work, const std::function<void(int, int, std::vector<int>&,
+                    std::vector<float>&)>& peaks_of, std::vector<CandidateList>& out_by_job);
+  std::vector<uint2> segtab_;  // segment table snapshot of the batch being processed
+  bool gpu_cluster_ = true;  // env PSOUP_GPU_CLUSTER=0: cluster on the host (reference path)
   // flat trial list of the current search_prepared_many call
   const std::vector<Job>* jobs_ = nullptr;
   std::vector<int> flat_job_;

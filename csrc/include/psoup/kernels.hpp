@@ -356,6 +356,20 @@ struct HarmParams {
 // P in layout L (natural by default; the fused pass B's blocked layout).
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
                           PeakRecord* out, uint32_t* count, hipStream_t s, const PLayout& L = PLayout{});
+// Peak clustering on the device (peakcluster.hip; peakfinder.hpp:24-55):
+// the records of harmonic_peaks_batch (first min(*d_count, cap)) grouped by
+// segment (seg < nseg), each segment's crossings clustered with the
+// reference's gap rule.  d_segtab[seg] = {first, count} of its cluster peaks
+// in d_out (ascending idx; uint2 = {idx, snr bits}; segments packed in any
+// order, *d_total in all), or {first, count | kClusterRaw} when the segment
+// has more than kClusterCap crossings: then its raw, unsorted crossings are
+// d_sorted[first .. first + count) for the host to cluster.
+// d_work: 3 * nseg uint32; d_sorted, d_out: cap entries each.
+constexpr uint32_t kClusterCap = 16384;
+constexpr uint32_t kClusterRaw = 0x80000000u;
+void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint32_t cap, uint32_t nseg, int gap,
+                        uint32_t* d_work, uint2* d_sorted, uint2* d_out, uint2* d_segtab, uint32_t* d_total,
+                        hipStream_t s);
 // Tuning: bit 0 = XCD-per-trial block order (default on).
 void harmonic_set_flags(int flags);
 int harmonic_flags();

@@ -569,6 +569,14 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("P"), py::arg("nb"), py::arg("pstride"), py::arg("K"), py::arg("nlevels"), py::arg("start"),
      py::arg("end"), py::arg("thresh"), py::arg("capacity"), py::arg("out"), py::arg("count"), py::arg("s"),
      py::arg("layout") = kern::PLayout{});
+  k.def("peak_cluster_batch", [](uintptr_t peaks, uintptr_t count, uint32_t cap, uint32_t nseg, int gap,
+                                 uintptr_t work, uintptr_t sorted, uintptr_t out, uintptr_t segtab, uintptr_t total,
+                                 uintptr_t s) {
+    kern::peak_cluster_batch(P<const kern::PeakRecord>(peaks), P<const uint32_t>(count), cap, nseg, gap,
+                             P<uint32_t>(work), P<uint2>(sorted), P<uint2>(out), P<uint2>(segtab), P<uint32_t>(total),
+                             S(s));
+  });
+  k.attr("cluster_cap") = kern::kClusterCap;
   k.def("harmonic_sums", [](uintptr_t Pin, uint64_t nb, int nlevels, uintptr_t out, uintptr_t s) {
     kern::harmonic_sums(P<const float>(Pin), nb, nlevels, P<float>(out), S(s));
   });
@@ -669,6 +677,10 @@ PYBIND11_MODULE(_C, m) {
         d.run(d0, d1, P<uint8_t>(out), ostride, k, S(s));
       }, py::arg("d0"), py::arg("d1"), py::arg("out"), py::arg("out_stride"), py::arg("kind") = DedispKernel::Auto,
            py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("run_list", [](Dedisperser& d, const std::vector<int>& dms, uintptr_t out, uint64_t ostride, uintptr_t s) {
+        d.run_list(dms, P<uint8_t>(out), ostride, S(s));
+      }, py::arg("dms"), py::arg("out"), py::arg("out_stride"), py::arg("stream") = 0,
+           py::call_guard<py::gil_scoped_release>())
       .def_static("row_stride", &Dedisperser::row_stride)
       .def("choose", &Dedisperser::choose, py::arg("d0"), py::arg("d1"))
       .def("mfma_steps_per_channel", &Dedisperser::mfma_steps_per_channel, py::arg("d0"), py::arg("d1"))

@@ -259,6 +259,36 @@ void Dedisperser::run_mfma_lds(int d0, int d1, uint8_t* out, uint64_t out_stride
                             g.out_nsamps, out, out_stride, g.out_scale, g.bias * g.nactive, s);
 }
 
+void Dedisperser::run_list(const std::vector<int>& dms, uint8_t* out, uint64_t out_stride, hipStream_t s) {
+  const auto& g = fb_.geometry();
+  if (dms.empty()) return;
+  if (!s) s = stream_;
+  const int ndm_list = static_cast<int>(g.dm_list.size());
+  for (int d : dms) PSOUP_CHECK(d >= 0 && d < ndm_list, "run_list: DM index " << d << " outside the list");
+  if (g.nactive == 0) {  // every channel killed: the direct kernel writes the bias rows
+    for (size_t i = 0; i < dms.size(); ++i)
+      run(dms[i], dms[i] + 1, out + i * out_stride, out_stride, DedispKernel::Direct, s);
+    return;
+  }
+  RoctxRange r("Dedisperse");
+  const int n = static_cast<int>(dms.size());
+  const int ldo = (n + kTileDms - 1) / kTileDms * kTileDms + kTileDms;  // padded like build_valu_tables
+  std::vector<int> active;
+  for (int c = 0; c < g.nchans; ++c)
+    if (g.killmask[c]) active.push_back(c);
+  std::vector<int32_t> t(active.size() * static_cast<size_t>(ldo));
+  for (int j = 0; j < ldo; ++j) {
+    const int d = dms[static_cast<size_t>(std::min(j, n - 1))];  // padded columns repeat the last DM
+    const std::vector<int32_t> offs = g.offsets(d, d + 1);
+    for (size_t ci = 0; ci < active.size(); ++ci) t[ci * ldo + j] = offs[static_cast<size_t>(active[ci])];
+  }
+  d_list_offT_.resize(t.size());
+  PSOUP_HIP_CHECK(hipMemcpyAsync(d_list_offT_.data(), t.data(), t.size() * 4, hipMemcpyHostToDevice, s));
+  PSOUP_HIP_CHECK(hipStreamSynchronize(s));
+  kern::dedisperse_valu(fb_.data(), fb_.stride(), d_active_.data(), g.nactive, d_list_offT_.data(), ldo, 0, n,
+                        g.out_nsamps, out, out_stride, g.out_scale, g.nbits, g.bias, s);
+}
+
 void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispKernel kind, hipStream_t s) {
   const auto& g = fb_.geometry();
   PSOUP_CHECK(d0 >= 0 && d1 <= static_cast<int>(g.dm_list.size()) && d0 <= d1, "bad DM range");
@@ -682,9 +712,10 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   for (auto& s : slots_) {
     s.done = std::make_unique<Event>();
     s.copied = std::make_unique<Event>();
-    s.d_count.resize(1);
-    s.h_count.resize(1);
+    s.d_count.resize(2);
+    s.h_count.resize(2);
   }
+  if (const char* e = std::getenv("PSOUP_GPU_CLUSTER")) gpu_cluster_ = std::atoi(e) != 0;
   grow_capacity(cap_);
   int ht = p_.host_threads;
   if (ht < 0) ht = static_cast<int>(std::min(4u, std::max(1u, std::thread::hardware_concurrency() / 4)));
@@ -700,7 +731,14 @@ void SearchEngine::grow_capacity(uint32_t need) {
   cap_ = std::max(cap_, need);
   for (auto& s : slots_) {
     s.d_peaks.resize(cap_);
-    s.h_peaks.resize(cap_);
+    if (gpu_cluster_) {
+      s.d_sorted.resize(cap_);
+      s.d_clust.resize(cap_);
+      s.h_clust.resize(cap_);
+      s.h_raw.resize(cap_);
+    } else {
+      s.h_peaks.resize(cap_);
+    }
   }
   hp_.capacity = cap_;
 }
@@ -710,6 +748,12 @@ void SearchEngine::ensure_batch_buffers(int k) {
   // allocates a whole K_-trial batch)
   if (k <= buf_k_) return;
   buf_k_ = k;
+  if (gpu_cluster_)
+    for (auto& s : slots_) {
+      s.d_work.resize(3 * 8 * static_cast<size_t>(k));
+      s.d_segtab.resize(8 * static_cast<size_t>(k));
+      s.h_segtab.resize(8 * static_cast<size_t>(k));
+    }
   const uint64_t rs = mode_ == 2 ? 2 * f4_.ystride : n_;  // floats per trial
   res_.resize(static_cast<uint64_t>(k) * rs);
   if (fused_)
@@ -823,7 +867,16 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
   } else {
     run(0, count, stream_, 0);
   }
-  PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_count.data(), s.d_count.data(), sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  if (gpu_cluster_) {
+    // cluster on the device: only cluster peaks (and the rare over-capacity
+    // segment's raw crossings) are copied out
+    kern::peak_cluster_batch(s.d_peaks.data(), s.d_count.data(), cap_, static_cast<uint32_t>(count) * 8, p_.min_gap,
+                             s.d_work.data(), s.d_sorted.data(), s.d_clust.data(), s.d_segtab.data(),
+                             s.d_count.data() + 1, stream_);
+    PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_segtab.data(), s.d_segtab.data(), 8ull * count * sizeof(uint2),
+                                   hipMemcpyDeviceToHost, stream_));
+  }
+  PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_count.data(), s.d_count.data(), 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   s.done->record(stream_);
 }
 
@@ -849,11 +902,73 @@ void SearchEngine::process_slot(Slot& s, int first, int count, uint32_t npeaks,
   // Per-trial clustering + harmonic distillation.  Trials own disjoint
   // segments of sorted_, so peak-heavy batches (RFI) are spread over the
   // host pool; results are concatenated in trial order (deterministic).
+  build_trials(first, count, cnt, [&](int k, int h, std::vector<int>& pidx, std::vector<float>& psnr) {
+    thread_local std::vector<int> idxs;
+    thread_local std::vector<float> snrs;
+    const int seg = k * 8 + h;
+    const uint32_t a = seg_off_[seg], b = seg_off_[seg + 1];
+    if (a == b) return;
+    std::sort(sorted_.begin() + a, sorted_.begin() + b,
+              [](const kern::PeakRecord& x, const kern::PeakRecord& y) { return x.idx < y.idx; });
+    idxs.resize(b - a);
+    snrs.resize(b - a);
+    for (uint32_t i = a; i < b; ++i) {
+      idxs[i - a] = sorted_[i].idx;
+      snrs[i - a] = sorted_[i].snr;
+    }
+    identify_unique_peaks(idxs.data(), snrs.data(), idxs.size(), p_.min_gap, pidx, psnr);
+  }, out_by_job);
+}
+
+void SearchEngine::process_clustered(Slot& s, int first, int count, const std::vector<uint2>& segtab,
+                                     std::vector<CandidateList>& out_by_job) {
+  size_t work = 0;
+  for (int i = 0; i < count * 8; ++i) work += segtab[static_cast<size_t>(i)].y & ~kern::kClusterRaw;
+  build_trials(first, count, work, [&](int k, int h, std::vector<int>& pidx, std::vector<float>& psnr) {
+    const uint2 e = segtab[static_cast<size_t>(k * 8 + h)];
+    if (e.y == 0) return;
+    if (e.y & kern::kClusterRaw) {
+      // a segment over the device's LDS capacity: the reference scan here
+      thread_local std::vector<std::pair<int, float>> raw;
+      thread_local std::vector<int> idxs;
+      thread_local std::vector<float> snrs;
+      const uint32_t n = e.y & ~kern::kClusterRaw;
+      raw.resize(n);
+      for (uint32_t i = 0; i < n; ++i) {
+        const uint2 v = s.h_raw[e.x + i];
+        float f;
+        std::memcpy(&f, &v.y, 4);
+        raw[i] = {static_cast<int>(v.x), f};
+      }
+      std::sort(raw.begin(), raw.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+      idxs.resize(n);
+      snrs.resize(n);
+      for (uint32_t i = 0; i < n; ++i) {
+        idxs[i] = raw[i].first;
+        snrs[i] = raw[i].second;
+      }
+      identify_unique_peaks(idxs.data(), snrs.data(), n, p_.min_gap, pidx, psnr);
+      return;
+    }
+    pidx.resize(e.y);
+    psnr.resize(e.y);
+    for (uint32_t i = 0; i < e.y; ++i) {
+      const uint2 v = s.h_clust[e.x + i];
+      pidx[i] = static_cast<int>(v.x);
+      std::memcpy(&psnr[i], &v.y, 4);
+    }
+  }, out_by_job);
+}
+
+void SearchEngine::build_trials(int first, int count, size_t work,
+                                const std::function<void(int, int, std::vector<int>&, std::vector<float>&)>& peaks_of,
+                                std::vector<CandidateList>& out_by_job) {
+  const int L = nlev_ + 1;
   // per-trial results, appended to their jobs' lists in trial order below
   std::vector<CandidateList> per_trial(static_cast<size_t>(count));
   auto trial_range = [&](int k0, int k1) {
-    std::vector<int> idxs, pidx;
-    std::vector<float> snrs, psnr;
+    std::vector<int> pidx;
+    std::vector<float> psnr;
     for (int k = k0; k < k1; ++k) {
       const size_t ft = static_cast<size_t>(first + k);
       const float acc = flat_acc_[ft];
@@ -862,20 +977,9 @@ void SearchEngine::process_slot(Slot& s, int first, int count, uint32_t npeaks,
       const int dm_idx = job.dm_idx;
       CandidateList trial;
       for (int h = 0; h < L; ++h) {
-        const int seg = k * 8 + h;
-        const uint32_t a = seg_off_[seg], b = seg_off_[seg + 1];
-        if (a == b) continue;
-        std::sort(sorted_.begin() + a, sorted_.begin() + b,
-                  [](const kern::PeakRecord& x, const kern::PeakRecord& y) { return x.idx < y.idx; });
-        idxs.resize(b - a);
-        snrs.resize(b - a);
-        for (uint32_t i = a; i < b; ++i) {
-          idxs[i - a] = sorted_[i].idx;
-          snrs[i - a] = sorted_[i].snr;
-        }
         pidx.clear();
         psnr.clear();
-        identify_unique_peaks(idxs.data(), snrs.data(), idxs.size(), p_.min_gap, pidx, psnr);
+        peaks_of(k, h, pidx, psnr);
         const double factor = bounds_[static_cast<size_t>(h)].factor;
         for (size_t i = 0; i < pidx.size(); ++i)
           trial.emplace_back(dm, dm_idx, acc, h, psnr[i], static_cast<float>(pidx[i] * factor));
@@ -883,8 +987,8 @@ void SearchEngine::process_slot(Slot& s, int first, int count, uint32_t npeaks,
       if (!trial.empty()) per_trial[static_cast<size_t>(k)] = harm_.distill(std::move(trial));
     }
   };
-  constexpr uint32_t kParallelPeaks = 8192;  // below this the serial loop is cheaper
-  if (pool_ && cnt >= kParallelPeaks && count > 1) {
+  constexpr size_t kParallelPeaks = 8192;  // below this the serial loop is cheaper
+  if (pool_ && work >= kParallelPeaks && count > 1) {
     const int nparts = std::min(count, 4 * pool_->size());
     pool_->parallel_for(nparts, [&](int j) {
       const int k0 = static_cast<int>(static_cast<int64_t>(count) * j / nparts);
@@ -1025,16 +1129,35 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
     // The batch's identity: the slot is re-issued below (launch_batch
     // overwrites first/count/h_count) before its records are processed.
     const int b_first = s.first, b_count = s.count;
-    if (cnt > 0)
+    if (gpu_cluster_) {
+      // snapshot the segment table (the re-issued launch rewrites it) and
+      // copy the cluster peaks plus any raw over-capacity segments
+      segtab_.assign(s.h_segtab.data(), s.h_segtab.data() + 8 * static_cast<size_t>(b_count));
+      const uint32_t tot = s.h_count[1];
+      if (tot > 0)
+        PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_clust.data(), s.d_clust.data(), tot * sizeof(uint2), hipMemcpyDeviceToHost,
+                                       copy_stream_.get()));
+      for (const uint2& e : segtab_)
+        if (e.y & kern::kClusterRaw)
+          PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_raw.data() + e.x, s.d_sorted.data() + e.x,
+                                         (e.y & ~kern::kClusterRaw) * sizeof(uint2), hipMemcpyDeviceToHost,
+                                         copy_stream_.get()));
+    } else if (cnt > 0) {
       PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_peaks.data(), s.d_peaks.data(), cnt * sizeof(kern::PeakRecord),
                                      hipMemcpyDeviceToHost, copy_stream_.get()));
+    }
     s.copied->record(copy_stream_.get());
     // the next batch that reuses this slot must wait for the copy-out
     PSOUP_HIP_CHECK(hipStreamWaitEvent(stream_, s.copied->get(), 0));
     if (next < ntr) issue(sl);
     s.copied->sync();
     host.start();
-    process_slot(s, b_first, b_count, cnt, by_job);
+    if (gpu_cluster_) {
+      ctr_.peaks += std::min(cnt, cap_);
+      process_clustered(s, b_first, b_count, segtab_, by_job);
+    } else {
+      process_slot(s, b_first, b_count, cnt, by_job);
+    }
     host.stop();
     ctr_.accel_trials += static_cast<uint64_t>(b_count);
   }

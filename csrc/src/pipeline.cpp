@@ -494,9 +494,11 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
             const size_t cnt = std::min<size_t>(static_cast<size_t>(B), mine.size() - b0);
             std::vector<std::vector<double>> periods(cnt);
             std::vector<std::vector<float>> accs(cnt);
+            std::vector<int> dms(cnt);
+            for (size_t t = 0; t < cnt; ++t) dms[t] = glist[mine[b0 + t]].first;
+            ds.dd->run_list(dms, trials.data(), rstride, st);  // one launch for the batch's DMs
             for (size_t t = 0; t < cnt; ++t) {
               const auto& grp = glist[mine[b0 + t]];
-              ds.dd->run(grp.first, grp.first + 1, trials.data() + t * rstride, rstride, setup.dedisp_kernel, st);
               for (int ci : grp.second) {
                 periods[t].push_back(static_cast<double>(static_cast<float>(1.0 / cands[ci].freq)));
                 accs[t].push_back(cands[ci].acc);

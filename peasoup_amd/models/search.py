@@ -395,10 +395,8 @@ class RankSearcher:
                 idx = torch.tensor([d - dm_first for d, _ in batch], dtype=torch.int64, device=rows.device)
                 buf.view(len(batch), self.row_stride).copy_(rows.index_select(0, idx))
                 torch.cuda.current_stream(self.ctx.device).synchronize()
-            else:
-                for t, (dm_idx, _) in enumerate(batch):
-                    self.dedisperser.run(dm_idx, dm_idx + 1, buf.data_ptr() + t * self.row_stride, self.row_stride,
-                                         self.kernel, self.stream)
+            else:  # one launch for the batch's (scattered) DMs
+                self.dedisperser.run_list([d for d, _ in batch], buf.data_ptr(), self.row_stride, self.stream)
             periods = [[float(struct.unpack("f", struct.pack("f", 1.0 / cands[i].freq))[0]) for i in members]
                        for _, members in batch]
             accs = [[cands[i].acc for i in members] for _, members in batch]

@@ -110,6 +110,11 @@ def test_dedisperse_1024ch_hybrid_mfma_bit_exact(C):
     o = torch.zeros((ndm - 32) * stride, dtype=torch.uint8, device=dev)
     dd.run(32, ndm, o.data_ptr(), stride, C.DedispKernel.Auto)
     assert torch.equal(o.view(ndm - 32, stride)[:, : g.out_nsamps], ref_[32:])
+    # the fold stage's scattered DM list (unsorted, a repeat, > one 32-DM tile)
+    lst = [int(v) for v in rng.choice(ndm, 40, replace=False)] + [7, 7]
+    o = torch.zeros(len(lst) * stride, dtype=torch.uint8, device=dev)
+    dd.run_list(lst, o.data_ptr(), stride)
+    assert torch.equal(o.view(len(lst), stride)[:, : g.out_nsamps], ref_[lst])
 
 
 def test_mfma_resident_plan_ranges_and_side_stream(C):

@@ -1,0 +1,109 @@
+"""GPU peak clustering (kern::peak_cluster_batch) against the reference's
+host scan (identify_unique_peaks, include/transforms/peakfinder.hpp:24-55),
+and the search engine with device clustering against host clustering."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _segment(rng, n, span, ties):
+    idx = np.sort(rng.choice(span, n, replace=False)).astype(np.int32)
+    # bumps (runs of crossings rising to a peak and falling) plus noise
+    snr = 9.0 + 40.0 * rng.random(n)
+    for c in rng.choice(span, max(1, n // 200), replace=False):
+        snr += 200.0 * np.exp(-0.5 * ((idx - c) / (5 + 40 * rng.random())) ** 2)
+    if ties:
+        snr = np.round(snr * 2) / 2  # equal S/N neighbours: the strict '>' rule
+    return idx, snr.astype(np.float32)
+
+
+def test_peak_cluster_matches_host_scan(C):
+    K = C.kernels
+    rng = np.random.default_rng(3)
+    gap = 30
+    cap_seg = int(K.cluster_cap)
+    sizes = [0, 1, 2, 31, 64, 65, 500, 4096, 5000, cap_seg, cap_seg + 1, 20000, 7, 0, 900, 12000]
+    segs = {}
+    recs = []
+    for s, n in enumerate(sizes):
+        if n == 0:
+            continue
+        span = n * (1 + s % 4) + 10  # dense (most within the gap) to sparse
+        idx, snr = _segment(rng, n, span, ties=s % 2 == 0)
+        segs[s] = (idx, snr)
+        recs.append(np.stack([np.full(n, s, np.uint32), idx.view(np.uint32), snr.view(np.uint32)], axis=1))
+    allr = np.concatenate(recs)
+    allr = allr[rng.permutation(len(allr))]  # the harmonic kernel's records land unordered
+    n = len(allr)
+    nseg = len(sizes)
+    cap = n + 100
+    peaks = torch.from_numpy(allr.reshape(-1).view(np.int32).copy()).to(dev)
+    count = torch.tensor([n], dtype=torch.int32, device=dev)
+    work = torch.empty(3 * nseg, dtype=torch.int32, device=dev)
+    srt = torch.empty(2 * cap, dtype=torch.int32, device=dev)
+    out = torch.empty(2 * cap, dtype=torch.int32, device=dev)
+    tab = torch.empty(2 * nseg, dtype=torch.int32, device=dev)
+    tot = torch.zeros(1, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    K.peak_cluster_batch(peaks.data_ptr(), count.data_ptr(), cap, nseg, gap, work.data_ptr(), srt.data_ptr(),
+                         out.data_ptr(), tab.data_ptr(), tot.data_ptr(), s)
+    torch.cuda.synchronize()
+    tab_h = tab.cpu().numpy().view(np.uint32).reshape(nseg, 2)
+    out_h = out.cpu().numpy().view(np.uint32).reshape(cap, 2)
+    srt_h = srt.cpu().numpy().view(np.uint32).reshape(cap, 2)
+    assert int(tot.item()) == sum(int(tab_h[s_, 1]) for s_ in range(nseg) if not tab_h[s_, 1] & 0x80000000)
+    for s_, sz in enumerate(sizes):
+        first, cnt = int(tab_h[s_, 0]), int(tab_h[s_, 1])
+        if sz == 0:
+            assert cnt == 0
+            continue
+        idx, snr = segs[s_]
+        if sz > cap_seg:  # left to the host: the raw crossings of exactly this segment
+            assert cnt == (sz | 0x80000000), (s_, hex(cnt))
+            raw = srt_h[first:first + sz]
+            assert np.array_equal(np.sort(raw[:, 0].astype(np.int32)), idx)
+            continue
+        exp_i, exp_s = C.identify_unique_peaks(idx.tolist(), snr.tolist(), gap)
+        got = out_h[first:first + cnt]
+        assert cnt == len(exp_i), (s_, sz, cnt, len(exp_i))
+        assert np.array_equal(got[:, 0].astype(np.int32), np.array(exp_i, np.int32)), s_
+        assert np.array_equal(got[:, 1].view(np.float32), np.array(exp_s, np.float32)), s_
+
+
+def _search(C, trial, nsamps, accs, gpu_cluster):
+    os.environ["PSOUP_GPU_CLUSTER"] = "1" if gpu_cluster else "0"
+    try:
+        p = C.SearchParams()
+        p.fft_size, p.tsamp, p.nharmonics = 1 << 20, 64e-6, 4
+        eng = C.SearchEngine(p, torch.cuda.current_stream().cuda_stream)
+        c = eng.search_trial(trial.data_ptr(), nsamps, 10.0, 3, accs)
+        ctr = eng.counters()
+    finally:
+        os.environ.pop("PSOUP_GPU_CLUSTER", None)
+    return [(x.dm_idx, x.acc, x.nh, x.snr, x.freq) for x in c], ctr
+
+
+def test_engine_gpu_clustering_equals_host(C):
+    """A peak-heavy trial (bright narrow pulse train + strong undispersed
+    periodic RFI): device clustering gives the candidate list of the host
+    scan, field for field."""
+    rng = np.random.default_rng(5)
+    n = (1 << 20) + 512
+    t = np.arange(n) * 64e-6
+    x = rng.normal(128, 6, n)
+    for per, amp in ((0.00731, 30.0), (0.02, 60.0), (0.0613, 25.0)):
+        ph = (t / per) % 1.0
+        x += amp * (np.minimum(ph, 1 - ph) < 0.015)
+    trial = torch.from_numpy(np.clip(np.rint(x), 0, 255).astype(np.uint8)).to(dev)
+    accs = [float(a) for a in np.linspace(-60, 60, 41)]
+    host, ch = _search(C, trial, n, accs, False)
+    gpu, cg = _search(C, trial, n, accs, True)
+    assert ch["peaks"] > 100000, ch  # peak-heavy: the clustering matters
+    assert cg["peaks"] == ch["peaks"]
+    assert len(gpu) == len(host) and len(gpu) > 0
+    assert gpu == host

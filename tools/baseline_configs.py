@@ -212,6 +212,8 @@ def config45(a, npdmp, cfg):
                "timers_s": {k: round(v, 3) for k, v in res.timers.items()},
                "dm_accel_trials_per_s": round(res.performance["dm_accel_trials_per_sec"], 1),
                "candidates": len(res.candidates),
+               "folded": sum(1 for c in res.candidates if c.folded_snr != 0.0),
+               "rank_stats": res.rank_stats,
                "best": {"period_s": 1.0 / best.freq, "dm": best.dm, "acc": best.acc, "snr": best.snr,
                         "folded_snr": best.folded_snr} if best else None}
     if cfg == 5:
