@@ -233,6 +233,7 @@ struct SearchCounters {
   uint64_t accel_trials = 0;
   uint64_t peaks = 0;
   uint64_t overflows = 0;
+  uint64_t harm_in = 0, harm_out = 0;  // candidates into / out of the per-trial harmonic distiller
   double whiten_s = 0, accel_s = 0, host_s = 0;
 };
 

@@ -365,7 +365,7 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
 // has more than kClusterCap crossings: then its raw, unsorted crossings are
 // d_sorted[first .. first + count) for the host to cluster.
 // d_work: 3 * nseg uint32; d_sorted, d_out: cap entries each.
-constexpr uint32_t kClusterCap = 16384;
+constexpr uint32_t kClusterCap = 14000;
 constexpr uint32_t kClusterRaw = 0x80000000u;
 void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint32_t cap, uint32_t nseg, int gap,
                         uint32_t* d_work, uint2* d_sorted, uint2* d_out, uint2* d_segtab, uint32_t* d_total,

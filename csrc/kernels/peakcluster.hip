@@ -16,11 +16,16 @@
 //       gap-windows: within a "run" of survivors spaced < gap apart the peaks
 //       are the run's first survivor, then the first survivor >= anchor + gap,
 //       and so on; a survivor >= gap after the previous survivor starts a run.
+// So the peaks of a whole segment are one chain: the first survivor, then
+// next(i) = the first survivor with idx >= idx_i + gap, and so on (a run's
+// last anchor has every later survivor of its run within the gap, so its
+// next is the following run's start).
 // peak_cluster_kernel: one workgroup per segment (trial x level): bitonic
-// sort by idx in LDS, the window test (1) in parallel, runs marked with a
-// max-scan, one thread walks each run (2), a scan compacts the peaks in idx
-// order.  Segments over kClusterCap crossings are left to the host (flagged
-// in the segment table with their raw, unsorted range).
+// sort by idx in LDS, the window test (1) and next() in parallel (a suffix
+// scan gives the next survivor at or after any position), one thread follows
+// the chain (one LDS read per peak), a scan compacts the peaks in idx order.
+// Segments over kClusterCap crossings are left to the host (flagged in the
+// segment table with their raw, unsorted range).
 #include "device_common.hpp"
 
 namespace psoup {
@@ -28,9 +33,11 @@ namespace kern {
 namespace {
 
 constexpr int kClThreads = 512;
+constexpr uint32_t kClSmall = 4096;  // segments up to this size: the small-LDS kernel (3 workgroups per CU)
+constexpr int kSegLds = 8192;        // segments a batch may have for the LDS-aggregated hist/scatter
+constexpr int kRecPerThread = 16;    // records per thread in hist/scatter blocks (256 threads)
 
-// Hillis-Steele scans over one value per thread (kClThreads); returns the
-// exclusive sum / the inclusive max of the preceding threads' values.
+// Hillis-Steele scans over one value per thread (kClThreads).
 __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* sc, uint32_t* total) {
   const int t = threadIdx.x;
   sc[t] = v;
@@ -47,29 +54,45 @@ __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* sc, uin
   return incl - v;
 }
 
-__device__ __forceinline__ int block_excl_max(int v, int* sc) {
+// min over the threads after this one (exclusive suffix min)
+__device__ __forceinline__ uint32_t block_excl_suffix_min(uint32_t v, uint32_t* sc) {
   const int t = threadIdx.x;
   sc[t] = v;
   __syncthreads();
   for (int off = 1; off < kClThreads; off <<= 1) {
-    const int a = t >= off ? sc[t - off] : -1;
+    const uint32_t a = t + off < kClThreads ? sc[t + off] : 0xffffffffu;
     __syncthreads();
-    sc[t] = max(sc[t], a);
+    sc[t] = min(sc[t], a);
     __syncthreads();
   }
-  const int prev = t > 0 ? sc[t - 1] : -1;
+  const uint32_t r = t + 1 < kClThreads ? sc[t + 1] : 0xffffffffu;
   __syncthreads();
-  return prev;
+  return r;
 }
 
+// Per-segment counts: each block counts its records in LDS and adds the
+// non-zero counts to the global ones (one atomic per block and segment, not
+// per record: heavy segments get tens of thousands of records).
 __global__ void __launch_bounds__(256) seg_hist_kernel(const PeakRecord* __restrict__ in,
                                                        const uint32_t* __restrict__ count, uint32_t cap,
                                                        uint32_t nseg, uint32_t* __restrict__ segcnt) {
+  __shared__ uint32_t lc[kSegLds];
   const uint32_t n = min(*count, cap);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t s = in[i].seg;
-    if (s < nseg) atomicAdd(&segcnt[s], 1u);
+  const uint32_t base = blockIdx.x * 256u * kRecPerThread;
+  if (base >= n) return;
+  for (uint32_t i = threadIdx.x; i < nseg; i += 256) lc[i] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRecPerThread; ++r) {
+    const uint32_t i = base + r * 256u + threadIdx.x;
+    if (i < n) {
+      const uint32_t sg = in[i].seg;
+      if (sg < nseg) atomicAdd(&lc[sg], 1u);
+    }
   }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nseg; i += 256)
+    if (lc[i]) atomicAdd(&segcnt[i], lc[i]);
 }
 
 __global__ void __launch_bounds__(kClThreads) seg_scan_kernel(const uint32_t* __restrict__ segcnt, uint32_t nseg,
@@ -90,58 +113,98 @@ __global__ void __launch_bounds__(kClThreads) seg_scan_kernel(const uint32_t* __
   }
 }
 
+// Records grouped by segment: LDS ranks within the block, one global atomic
+// per (block, segment) reserves the block's range of the segment.
 __global__ void __launch_bounds__(256) seg_scatter_kernel(const PeakRecord* __restrict__ in,
                                                           const uint32_t* __restrict__ count, uint32_t cap,
                                                           uint32_t nseg, const uint32_t* __restrict__ segoff,
                                                           uint32_t* __restrict__ cursor, uint2* __restrict__ out) {
+  __shared__ uint32_t lc[kSegLds];
+  __shared__ uint32_t lb[kSegLds];
   const uint32_t n = min(*count, cap);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const PeakRecord r = in[i];
-    if (r.seg >= nseg) continue;
-    const uint32_t pos = segoff[r.seg] + atomicAdd(&cursor[r.seg], 1u);
-    out[pos] = make_uint2(static_cast<uint32_t>(r.idx), __float_as_uint(r.snr));
+  const uint32_t base = blockIdx.x * 256u * kRecPerThread;
+  if (base >= n) return;
+  for (uint32_t i = threadIdx.x; i < nseg; i += 256) lc[i] = 0;
+  __syncthreads();
+  PeakRecord rec[kRecPerThread];
+  uint32_t rank[kRecPerThread];
+#pragma unroll
+  for (int r = 0; r < kRecPerThread; ++r) {
+    const uint32_t i = base + r * 256u + threadIdx.x;
+    rec[r].seg = 0xffffffffu;
+    if (i < n) {
+      rec[r] = in[i];
+      if (rec[r].seg < nseg) rank[r] = atomicAdd(&lc[rec[r].seg], 1u);
+    }
   }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < nseg; i += 256)
+    if (lc[i]) lb[i] = segoff[i] + atomicAdd(&cursor[i], lc[i]);
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < kRecPerThread; ++r)
+    if (rec[r].seg < nseg)
+      out[lb[rec[r].seg] + rank[r]] = make_uint2(static_cast<uint32_t>(rec[r].idx), __float_as_uint(rec[r].snr));
 }
 
+// One workgroup per segment with lo_n < n <= CAP crossings (the small
+// kernel also writes the empty segments' entries, the large one the raw
+// entries of segments over its capacity).
+template <uint32_t CAP>
 __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* __restrict__ sorted,
                                                                   const uint32_t* __restrict__ segoff,
                                                                   const uint32_t* __restrict__ segcnt, int gap,
-                                                                  uint2* __restrict__ out, uint2* __restrict__ segtab,
+                                                                  uint32_t lo_n, uint2* __restrict__ out,
+                                                                  uint2* __restrict__ segtab,
                                                                   uint32_t* __restrict__ total) {
-  __shared__ uint2 key[kClusterCap];    // (idx, snr bits)
-  __shared__ uint8_t flag[kClusterCap];  // bit 0: survives the window test, bit 1: cluster peak
+  constexpr uint32_t C = (CAP + kClThreads - 1) / kClThreads;  // positions per thread (contiguous chunk)
+  __shared__ uint2 key[CAP];      // (idx, snr bits)
+  __shared__ uint16_t jmp[CAP];   // next survivor at/after a position, then chain jumps
+  __shared__ uint8_t flag[CAP];   // bit 0: survives the window test, bit 1: cluster peak
   __shared__ uint32_t sc[kClThreads];
-  __shared__ uint32_t base_s;
+  __shared__ uint32_t base_s, first_s;
   const int t = threadIdx.x;
   const uint32_t seg = blockIdx.x;
   const uint32_t n = segcnt[seg], off = segoff[seg];
-  if (n == 0 || n > kClusterCap) {
-    if (t == 0) segtab[seg] = n == 0 ? make_uint2(0u, 0u) : make_uint2(off, n | kClusterRaw);
+  if (n <= lo_n || n > CAP) {
+    if (t == 0) {
+      if (n == 0 && lo_n == 0) segtab[seg] = make_uint2(0u, 0u);
+      if (n > CAP && CAP > kClSmall) segtab[seg] = make_uint2(off, n | kClusterRaw);
+    }
     return;
   }
-  uint32_t P = 64;
+  for (uint32_t i = t; i < n; i += kClThreads) key[i] = sorted[off + i];
+  uint32_t P = 2;
   while (P < n) P <<= 1;
-  for (uint32_t i = t; i < P; i += kClThreads)
-    key[i] = i < n ? sorted[off + i] : make_uint2(0x7fffffffu, 0u);  // pads sort last
   __syncthreads();
-  // bitonic sort, ascending idx (distinct within a segment; idx >= 0)
+  // bitonic sort with ascending comparators only (a "flip" stage then half
+  // cleaners per merge size): positions >= n act as +inf and never move, so
+  // comparators reaching them are skipped -- no padding
+  auto cswap = [&](uint32_t lo, uint32_t hi) {
+    const uint2 a = key[lo], b = key[hi];
+    if (static_cast<int>(a.x) > static_cast<int>(b.x)) {
+      key[lo] = b;
+      key[hi] = a;
+    }
+  };
   for (uint32_t k = 2; k <= P; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = t; i < P / 2; i += kClThreads) {
-        const uint32_t lo = 2 * j * (i / j) + (i & (j - 1)), hi = lo + j;
-        const uint2 a = key[lo], b = key[hi];
-        if ((static_cast<int>(a.x) > static_cast<int>(b.x)) == ((lo & k) == 0)) {
-          key[lo] = b;
-          key[hi] = a;
-        }
+    const uint32_t h = k >> 1;
+    for (uint32_t q = t; q < P / 2; q += kClThreads) {
+      const uint32_t lo = (q / h) * k + (q & (h - 1)), hi = lo ^ (k - 1);
+      if (hi < n) cswap(lo, hi);
+    }
+    __syncthreads();
+    for (uint32_t j = k >> 2; j > 0; j >>= 1) {
+      for (uint32_t q = t; q < P / 2; q += kClThreads) {
+        const uint32_t lo = 2 * j * (q / j) + (q & (j - 1)), hi = lo + j;
+        if (hi < n) cswap(lo, hi);
       }
       __syncthreads();
     }
   }
-  // (1) window test over a contiguous chunk per thread
-  const uint32_t C = (P + kClThreads - 1) / kClThreads;
+  // (1) window test, contiguous chunk per thread
   const uint32_t b0 = min(static_cast<uint32_t>(t) * C, n), b1 = min(b0 + C, n);
-  int last = -1;  // this chunk's last survivor
+  uint32_t firstv = n, nsurv = 0;
   for (uint32_t i = b0; i < b1; ++i) {
     const int xi = static_cast<int>(key[i].x);
     const float si = __uint_as_float(key[i].y);
@@ -152,31 +215,66 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
         break;
       }
     flag[i] = keep ? 1 : 0;
-    if (keep) last = static_cast<int>(i);
+    if (keep) {
+      firstv = min(firstv, i);
+      ++nsurv;
+    }
   }
-  // the survivor before this chunk (max-scan of chunk-last positions)
-  int prev = block_excl_max(last, reinterpret_cast<int*>(sc));
-  // (2) one thread per run: from each run start, greedy gap windows
-  for (uint32_t i = b0; i < b1; ++i) {
-    if (!(flag[i] & 1)) continue;
-    const int xi = static_cast<int>(key[i].x);
-    const bool start = prev < 0 || xi - static_cast<int>(key[prev].x) >= gap;
-    prev = static_cast<int>(i);
-    if (!start) continue;
-    int anchor = xi, lastx = xi;
-    flag[i] = 3;
-    for (uint32_t j = i + 1; j < n; ++j) {
-      if (!(flag[j] & 1)) continue;
-      const int xj = static_cast<int>(key[j].x);
-      if (xj - lastx >= gap) break;  // the next run (its own walker)
-      lastx = xj;
-      if (xj - anchor >= gap) {
-        anchor = xj;
-        flag[j] = 3;
-      }
+  // next survivor at or after every position (suffix min over the chunks)
+  uint32_t cur = min(block_excl_suffix_min(firstv, sc), n);
+  for (uint32_t i = b1; i-- > b0;) {
+    if (flag[i] & 1) cur = i;
+    jmp[i] = static_cast<uint16_t>(cur);
+  }
+  uint32_t totsurv;
+  block_excl_sum(nsurv, sc, &totsurv);  // (its barriers also publish jmp)
+  if (t == 0) first_s = jmp[0];
+  // next(i): the first survivor with idx >= idx_i + gap (at most gap - 1
+  // positions ahead have smaller idx: distinct bins)
+  uint32_t nx[C];
+#pragma unroll
+  for (uint32_t c = 0; c < C; ++c) {
+    const uint32_t i = b0 + c;
+    nx[c] = n;
+    if (i < b1 && (flag[i] & 1)) {
+      const int target = static_cast<int>(key[i].x) + gap;
+      uint32_t p = i + 1;
+      while (p < n && static_cast<int>(key[p].x) < target) ++p;
+      nx[c] = p < n ? jmp[p] : n;
     }
   }
   __syncthreads();
+#pragma unroll
+  for (uint32_t c = 0; c < C; ++c)
+    if (b0 + c < b1 && (flag[b0 + c] & 1)) jmp[b0 + c] = static_cast<uint16_t>(nx[c]);
+  if (t == 0 && first_s < n) flag[first_s] = 3;
+  __syncthreads();
+  // (2) the chain from the first survivor, by pointer doubling: after round
+  // r every survivor within 2^(r+1) - 1 jumps of the start is marked
+  for (uint32_t span = 1; span < totsurv; span <<= 1) {
+    uint32_t tgt[C], nj[C];
+#pragma unroll
+    for (uint32_t c = 0; c < C; ++c) {
+      const uint32_t i = b0 + c;
+      tgt[c] = n;
+      nj[c] = n;
+      if (i < b1 && (flag[i] & 1)) {
+        const uint32_t j = jmp[i];
+        if (j < n) {
+          if (flag[i] & 2) tgt[c] = j;
+          nj[c] = jmp[j];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t c = 0; c < C; ++c) {
+      const uint32_t i = b0 + c;
+      if (tgt[c] < n) flag[tgt[c]] = 3;
+      if (i < b1 && (flag[i] & 1)) jmp[i] = static_cast<uint16_t>(nj[c]);
+    }
+    __syncthreads();
+  }
   // compaction of the peaks, idx order
   uint32_t cnt = 0;
   for (uint32_t i = b0; i < b1; ++i) cnt += flag[i] >> 1;
@@ -192,6 +290,31 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
     if (flag[i] >> 1) out[o++] = key[i];
 }
 
+// Fallbacks for batches with more than kSegLds segments: one global atomic per record.
+__global__ void __launch_bounds__(256) seg_hist_global_kernel(const PeakRecord* __restrict__ in,
+                                                              const uint32_t* __restrict__ count, uint32_t cap,
+                                                              uint32_t nseg, uint32_t* __restrict__ segcnt) {
+  const uint32_t n = min(*count, cap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t sg = in[i].seg;
+    if (sg < nseg) atomicAdd(&segcnt[sg], 1u);
+  }
+}
+
+__global__ void __launch_bounds__(256) seg_scatter_global_kernel(const PeakRecord* __restrict__ in,
+                                                                 const uint32_t* __restrict__ count, uint32_t cap,
+                                                                 uint32_t nseg, const uint32_t* __restrict__ segoff,
+                                                                 uint32_t* __restrict__ cursor,
+                                                                 uint2* __restrict__ out) {
+  const uint32_t n = min(*count, cap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const PeakRecord r = in[i];
+    if (r.seg >= nseg) continue;
+    const uint32_t pos = segoff[r.seg] + atomicAdd(&cursor[r.seg], 1u);
+    out[pos] = make_uint2(static_cast<uint32_t>(r.idx), __float_as_uint(r.snr));
+  }
+}
+
 }  // namespace
 
 void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint32_t cap, uint32_t nseg, int gap,
@@ -204,15 +327,30 @@ void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint
   uint32_t* cursor = d_work + 2 * nseg;
   PSOUP_HIP_CHECK(hipMemsetAsync(d_work, 0, 3ull * nseg * sizeof(uint32_t), s));
   PSOUP_HIP_CHECK(hipMemsetAsync(d_total, 0, sizeof(uint32_t), s));
-  const unsigned g = dev::grid_for(cap, 256, 4096);
-  seg_hist_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segcnt);
-  post_launch_check("seg_hist_kernel", s);
-  seg_scan_kernel<<<1, kClThreads, 0, s>>>(segcnt, nseg, segoff);
-  post_launch_check("seg_scan_kernel", s);
-  seg_scatter_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segoff, cursor, d_sorted);
-  post_launch_check("seg_scatter_kernel", s);
-  peak_cluster_kernel<<<nseg, kClThreads, 0, s>>>(d_sorted, segoff, segcnt, gap, d_out, d_segtab, d_total);
-  post_launch_check("peak_cluster_kernel", s);
+  if (nseg <= static_cast<uint32_t>(kSegLds)) {
+    const uint64_t per = 256ull * kRecPerThread;
+    const unsigned g = static_cast<unsigned>(std::max<uint64_t>(1, (static_cast<uint64_t>(cap) + per - 1) / per));
+    seg_hist_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segcnt);
+    post_launch_check("seg_hist_kernel", s);
+    seg_scan_kernel<<<1, kClThreads, 0, s>>>(segcnt, nseg, segoff);
+    post_launch_check("seg_scan_kernel", s);
+    seg_scatter_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segoff, cursor, d_sorted);
+    post_launch_check("seg_scatter_kernel", s);
+  } else {
+    const unsigned g = dev::grid_for(cap, 256, 4096);
+    seg_hist_global_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segcnt);
+    post_launch_check("seg_hist_global_kernel", s);
+    seg_scan_kernel<<<1, kClThreads, 0, s>>>(segcnt, nseg, segoff);
+    post_launch_check("seg_scan_kernel", s);
+    seg_scatter_global_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segoff, cursor, d_sorted);
+    post_launch_check("seg_scatter_global_kernel", s);
+  }
+  peak_cluster_kernel<kClSmall><<<nseg, kClThreads, 0, s>>>(d_sorted, segoff, segcnt, gap, 0u, d_out, d_segtab,
+                                                             d_total);
+  post_launch_check("peak_cluster_kernel<small>", s);
+  peak_cluster_kernel<kClusterCap><<<nseg, kClThreads, 0, s>>>(d_sorted, segoff, segcnt, gap, kClSmall, d_out,
+                                                                d_segtab, d_total);
+  post_launch_check("peak_cluster_kernel<large>", s);
 }
 
 }  // namespace kern

@@ -762,6 +762,8 @@ PYBIND11_MODULE(_C, m) {
         d["accel_trials"] = c.accel_trials;
         d["peaks"] = c.peaks;
         d["overflows"] = c.overflows;
+        d["harm_in"] = c.harm_in;
+        d["harm_out"] = c.harm_out;
         d["accel_s"] = c.accel_s;
         d["host_s"] = c.host_s;
         return d;

@@ -85,13 +85,34 @@ struct FreqIndex {
     for (size_t i = static_cast<size_t>(it - f.begin()); i < f.size() && f[i] <= hi; ++i)
       if (rank[i] > idx) out.push_back(rank[i]);
   }
+  // the same for windows sorted by lo (and hi): one forward pointer,
+  // galloping to each window's start instead of a full binary search
+  void query_sorted(const std::vector<std::pair<double, double>>& w, size_t idx, std::vector<uint32_t>& out) const {
+    const size_t n = f.size();
+    size_t p = 0;
+    for (const auto& [lo, hi] : w) {
+      if (p < n && f[p] < lo) {
+        size_t q = p, step = 1;
+        while (q + step < n && f[q + step] < lo) {
+          q += step;
+          step <<= 1;
+        }
+        const size_t e = std::min(q + step, n);
+        p = static_cast<size_t>(std::lower_bound(f.begin() + static_cast<long>(q) + 1, f.begin() + static_cast<long>(e), lo) -
+                                f.begin());
+      }
+      for (size_t i = p; i < n && f[i] <= hi; ++i)
+        if (rank[i] > idx) out.push_back(rank[i]);
+    }
+  }
 };
 
 // windows(c, idx, push(lo, hi)) lists the fundamental's frequency windows;
 // related(c, idx, ii) is the reference's inner-loop body for one later
 // candidate (performs the appends) and returns whether ii is related.
 template <class Windows, class Related>
-CandidateList base_distill(CandidateList cands, Windows&& windows, Related&& related, bool force_scan = false) {
+CandidateList base_distill(CandidateList cands, Windows&& windows, Related&& related, bool force_scan = false,
+                           bool sorted_windows = false) {
   const size_t size = cands.size();
   std::vector<char> unique(size, 1);
   // std::sort (not stable_sort) on purpose: with the same input order it breaks
@@ -101,6 +122,7 @@ CandidateList base_distill(CandidateList cands, Windows&& windows, Related&& rel
   std::unique_ptr<FreqIndex> index;
   if (indexed) index = std::make_unique<FreqIndex>(cands);
   std::vector<uint32_t> hits;
+  std::vector<std::pair<double, double>> wins;
   size_t start = 0;
   while (true) {
     long idx = -1;
@@ -119,12 +141,21 @@ CandidateList base_distill(CandidateList cands, Windows&& windows, Related&& rel
       continue;
     }
     hits.clear();
-    windows(cands, fi, [&](double lo, double hi) {
-      // a relative 1e-9 margin covers the rounding of the window bounds; the
-      // exact relation decides membership
-      const double m = 1e-9 * std::max(std::fabs(lo), std::fabs(hi));
-      index->query(lo - m, hi + m, fi, hits);
-    });
+    if (sorted_windows) {
+      wins.clear();
+      windows(cands, fi, [&](double lo, double hi) {
+        const double m = 1e-9 * std::max(std::fabs(lo), std::fabs(hi));
+        wins.emplace_back(lo - m, hi + m);
+      });
+      index->query_sorted(wins, fi, hits);
+    } else {
+      windows(cands, fi, [&](double lo, double hi) {
+        // a relative 1e-9 margin covers the rounding of the window bounds; the
+        // exact relation decides membership
+        const double m = 1e-9 * std::max(std::fabs(lo), std::fabs(hi));
+        index->query(lo - m, hi + m, fi, hits);
+      });
+    }
     std::sort(hits.begin(), hits.end());
     hits.erase(std::unique(hits.begin(), hits.end()), hits.end());
     for (uint32_t ii : hits)
@@ -148,18 +179,44 @@ CandidateList HarmonicDistiller::run(CandidateList cands, bool force_scan) const
   int max_nh = 0;
   for (const auto& c : cands) max_nh = std::max(max_nh, c.nh);
   const float max_den_all = frac ? static_cast<float>(std::pow(2.0, max_nh)) : 1.f;
+  // ratio = kk f / (jj fundi) in (lower, upper)  <=>  f in (lower, upper) * jj fundi / kk:
+  // the distinct jj / kk ascending, so each fundamental's windows come sorted
+  std::vector<double> ratios;
+  for (int jj = 1; jj <= max_harm; ++jj)
+    for (int kk = 1; kk <= max_den_all; ++kk) ratios.push_back(static_cast<double>(jj) / kk);
+  std::sort(ratios.begin(), ratios.end());
+  ratios.erase(std::unique(ratios.begin(), ratios.end(),
+                           [](double a, double b) { return std::fabs(a - b) <= 1e-12 * b; }),
+               ratios.end());
   auto windows = [&](const CandidateList& c, size_t idx, auto&& push) {
-    // ratio = kk f / (jj fundi) in (lower, upper)  <=>  f in (lower, upper) * jj fundi / kk
     const double fundi_freq = c[idx].freq;
-    for (int jj = 1; jj <= max_harm; ++jj)
-      for (int kk = 1; kk <= max_den_all; ++kk)
-        push(lower_tol * jj * fundi_freq / kk, upper_tol * jj * fundi_freq / kk);
+    for (double r : ratios) push(lower_tol * r * fundi_freq, upper_tol * r * fundi_freq);
   };
+  // the reference scan (force_scan) keeps the reference's full jj x kk loop
+  const bool fast = !keep && tol_ <= 1e-3f && !force_scan;
   auto related = [&](CandidateList& c, size_t idx, size_t ii) {
     const double fundi_freq = c[idx].freq;
     const double freq = c[ii].freq;
     const int nh = c[ii].nh;
-    const float max_denominator = frac ? static_cast<float>(std::pow(2.0, nh)) : 1.f;
+    const float max_denominator =
+        frac ? (nh >= 0 && nh < 24 ? static_cast<float>(1u << nh) : static_cast<float>(std::pow(2.0, nh))) : 1.f;
+    if (fast) {
+      // Only the whole result matters: for each kk just the jj nearest
+      // kk freq / fundi (|jj - that| <= 16 tol < 0.02 for any passing jj)
+      // and its neighbours, tested with the exact expression.
+      // (a multiply-and-round prefilter skips every kk whose kk freq / fundi
+      // is not within 1.5 jj tol of an integer jj: only then the exact test)
+      const double x1 = freq / fundi_freq;
+      for (int kk = 1; kk <= max_denominator; ++kk) {
+        const double x = kk * x1;
+        if (!(x < max_harm + 2.0)) break;
+        const int j0 = static_cast<int>(std::lround(x));
+        if (j0 < 1 || j0 > max_harm || std::fabs(x - j0) > 1.5 * tol_ * j0 + 1e-9) continue;
+        const double ratio = kk * freq / (j0 * fundi_freq);
+        if (ratio > lower_tol && ratio < upper_tol) return true;
+      }
+      return false;
+    }
     bool rel = false;
     for (int jj = 1; jj <= max_harm; ++jj) {
       for (int kk = 1; kk <= max_denominator; ++kk) {
@@ -172,7 +229,7 @@ CandidateList HarmonicDistiller::run(CandidateList cands, bool force_scan) const
     }
     return rel;
   };
-  return base_distill(std::move(cands), windows, related, force_scan);
+  return base_distill(std::move(cands), windows, related, force_scan, true);
 }
 
 AccelerationDistiller::AccelerationDistiller(float tobs, float tol, bool keep_related)

@@ -3,6 +3,7 @@
 #include <thread>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <charconv>
@@ -966,6 +967,7 @@ void SearchEngine::build_trials(int first, int count, size_t work,
   const int L = nlev_ + 1;
   // per-trial results, appended to their jobs' lists in trial order below
   std::vector<CandidateList> per_trial(static_cast<size_t>(count));
+  std::atomic<uint64_t> harm_in{0};
   auto trial_range = [&](int k0, int k1) {
     std::vector<int> pidx;
     std::vector<float> psnr;
@@ -984,6 +986,7 @@ void SearchEngine::build_trials(int first, int count, size_t work,
         for (size_t i = 0; i < pidx.size(); ++i)
           trial.emplace_back(dm, dm_idx, acc, h, psnr[i], static_cast<float>(pidx[i] * factor));
       }
+      harm_in += trial.size();
       if (!trial.empty()) per_trial[static_cast<size_t>(k)] = harm_.distill(std::move(trial));
     }
   };
@@ -1000,8 +1003,10 @@ void SearchEngine::build_trials(int first, int count, size_t work,
   }
   for (int k = 0; k < count; ++k) {
     CandidateList& dst = out_by_job[static_cast<size_t>(flat_job_[static_cast<size_t>(first + k)])];
+    ctr_.harm_out += per_trial[static_cast<size_t>(k)].size();
     for (auto& c : per_trial[static_cast<size_t>(k)]) dst.push_back(std::move(c));
   }
+  ctr_.harm_in += harm_in.load();
 }
 
 void SearchEngine::prepare(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count) {
@@ -1163,7 +1168,21 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
   }
   ctr_.host_s += host.get_time();
   std::vector<CandidateList> out(static_cast<size_t>(njobs));
-  for (int j = 0; j < njobs; ++j) out[static_cast<size_t>(j)] = accd_.distill(std::move(by_job[static_cast<size_t>(j)]));
+  // acceleration distillation per DM; the DMs of a candidate-heavy call over the host pool
+  size_t ncand = 0;
+  for (const auto& b : by_job) ncand += b.size();
+  auto accd_range = [&](int j0, int j1) {
+    for (int j = j0; j < j1; ++j) out[static_cast<size_t>(j)] = accd_.distill(std::move(by_job[static_cast<size_t>(j)]));
+  };
+  if (pool_ && njobs > 1 && ncand >= 4096) {
+    const int nparts = std::min(njobs, 4 * pool_->size());
+    pool_->parallel_for(nparts, [&](int q) {
+      accd_range(static_cast<int>(static_cast<int64_t>(njobs) * q / nparts),
+                 static_cast<int>(static_cast<int64_t>(njobs) * (q + 1) / nparts));
+    });
+  } else {
+    accd_range(0, njobs);
+  }
   jobs_ = nullptr;
   sw.stop();
   ctr_.accel_s += sw.get_time();

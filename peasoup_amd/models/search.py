@@ -58,6 +58,7 @@ class SearchResult:
     args: object = None
     accel_trials: int = 0
     rank_stats: list = field(default_factory=list)
+    fold_stats: dict = field(default_factory=dict)
 
 
 _SYNC_DEDISP = os.environ.get("PSOUP_SYNC_DEDISP", "0") == "1"  # debug: no dedispersion/search overlap
@@ -385,6 +386,7 @@ class RankSearcher:
         fe = self._fold_engine
         items = sorted(groups.items())
         B = int(fe.max_batch)
+        t_dd = t_fe = 0.0
         for b0 in range(0, len(items), B):
             batch = items[b0:b0 + B]
             # every DM of the batch dedispersed into one buffer, then whitened
@@ -396,14 +398,21 @@ class RankSearcher:
                 buf.view(len(batch), self.row_stride).copy_(rows.index_select(0, idx))
                 torch.cuda.current_stream(self.ctx.device).synchronize()
             else:  # one launch for the batch's (scattered) DMs
+                t0 = time.perf_counter()
                 self.dedisperser.run_list([d for d, _ in batch], buf.data_ptr(), self.row_stride, self.stream)
+                torch.cuda.current_stream(self.ctx.device).synchronize()
+                t_dd += time.perf_counter() - t0
             periods = [[float(struct.unpack("f", struct.pack("f", 1.0 / cands[i].freq))[0]) for i in members]
                        for _, members in batch]
             accs = [[cands[i].acc for i in members] for _, members in batch]
+            t0 = time.perf_counter()
             res = fe.fold_trials(buf.data_ptr(), self.row_stride, self.geom.out_nsamps, periods, accs)
+            t_fe += time.perf_counter() - t0
             for (_, members), rr in zip(batch, res):
                 for i, r in zip(members, rr):
                     out[i] = (r.folded_snr, r.opt_period, list(r.fold))
+        self.fold_stats = {"fold_dedisp_s": t_dd, "fold_engine_s": t_fe, "fold_dms": len(items),
+                           "fold_batches": (len(items) + B - 1) // B}
         return out
 
 
@@ -579,6 +588,7 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
 
     # ---- distributed folding (all ranks hold identical `cands`)
     timers["folding"].start()
+    fold_stats: Dict[str, float] = {}
     if args.npdmp > 0 and cands:
         groups = {}
         count = min(args.npdmp, len(cands))
@@ -591,7 +601,9 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
             mine = {k: groups[k] for k in keys if row_first <= k < row_first + rows.shape[0]}
         else:
             mine = {k: groups[k] for j, k in enumerate(keys) if j % ctx.world_size == ctx.rank}
+        t_f0 = time.perf_counter()
         res = rs.fold(mine, cands, rows=rows, dm_first=row_first)
+        t_f1 = time.perf_counter()
         parts = pdist.gather_bytes(_encode_fold_results(res), dst=0)
         if ctx.is_root:
             for p in parts:
@@ -603,6 +615,8 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
                     c.nbins, c.nints = 64, 16
                     cands[i] = c
             cands = _C.sort_by_folded_snr(cands)
+        fold_stats = dict(getattr(rs, "fold_stats", {}))
+        fold_stats.update({"fold_call_s": t_f1 - t_f0, "fold_merge_s": time.perf_counter() - t_f1})
     timers["folding"].stop()
     if not ctx.is_root:
         timers["total"].stop()
@@ -619,6 +633,7 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     res = SearchResult(cands, tdict, perf, rs.dm_list, acc0, list(range(ctx.world_size)) if ctx.device.type == "cuda" else [],
                        rs.header, args, total_trials)
     res.rank_stats = [json.loads(b.decode()) for b in all_stats] if all_stats else []
+    res.fold_stats = fold_stats  # rank 0's fold-stage breakdown (seconds)
     if write:
         write_outputs(args, res)
     return res

@@ -27,7 +27,7 @@ def test_peak_cluster_matches_host_scan(C):
     rng = np.random.default_rng(3)
     gap = 30
     cap_seg = int(K.cluster_cap)
-    sizes = [0, 1, 2, 31, 64, 65, 500, 4096, 5000, cap_seg, cap_seg + 1, 20000, 7, 0, 900, 12000]
+    sizes = [0, 1, 2, 31, 64, 65, 500, 4096, 4097, 5000, cap_seg, cap_seg + 1, 20000, 7, 0, 900, 12000, 3]
     segs = {}
     recs = []
     for s, n in enumerate(sizes):

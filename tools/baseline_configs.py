@@ -214,6 +214,7 @@ def config45(a, npdmp, cfg):
                "candidates": len(res.candidates),
                "folded": sum(1 for c in res.candidates if c.folded_snr != 0.0),
                "rank_stats": res.rank_stats,
+               "fold_stats": res.fold_stats,
                "best": {"period_s": 1.0 / best.freq, "dm": best.dm, "acc": best.acc, "snr": best.snr,
                         "folded_snr": best.folded_snr} if best else None}
     if cfg == 5:

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU peak clustering: kernel + engine equality tests, signal sweep, configs 4/5
 set -o pipefail
-O=gpurun_out/r3d
+O=${O:-gpurun_out/r3d}
 W=/tmp/psoup_cfg
 mkdir -p $O $W
 export TMPDIR=/tmp
@@ -14,6 +14,6 @@ timeout -k 10 400 python -u tools/baseline_configs.py --configs 4,5 --workdir $W
 python -c "
 import json
 for l in open('$O/configs.jsonl'):
-    d=json.loads(l); print(d['config'], d['wall_s'], d['timers_s'], d['candidates'], d.get('folded'), d['rank_stats'][0]['peaks'], d['rank_stats'][0]['host_s'], d['best'])
+    d=json.loads(l); print(d['config'], d['wall_s'], d['timers_s'], d['candidates'], d.get('folded'), d['rank_stats'][0]['peaks'], d['rank_stats'][0]['host_s'], d['rank_stats'][0].get('harm_in'), d['rank_stats'][0].get('harm_out'), d.get('fold_stats'), d['best'])
 "
 echo DONE
