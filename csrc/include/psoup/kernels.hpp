@@ -336,6 +336,10 @@ enum Fft4Flags : int {
   kFft4OneXRow = 524288,      // pass B (tiled Y and X, row length 512..2048): the one-exchange structure
   kFft4FusedR2c = 2097152,    // search batches: pass B + r2c + interbin + normalise in one kernel
                               // (fft4_rowpass_r2c; blocked spectrum layout read by the harmonic sum)
+  kFft4WideProbe = 8388608,   // timing experiment (one-exchange pass A, with kFft4SkipCompute|kFft4SkipStore):
+                              // the same load bytes as 128-byte row pieces
+  kFft4Stagger = 4194304,     // experiment (one-exchange pass A): blocks 256..511 sleep ((flags >> 24) & 63)
+                              // x 8k cycles first, putting each CU's two workgroups out of phase
 };
 void fft4_set_flags(int flags);
 // Debug: per-workgroup phase timestamps of the fft4 passes (12 x u64 per block), nullptr = off.

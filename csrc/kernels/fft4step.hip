@@ -749,6 +749,8 @@ __device__ __forceinline__ void onex_core(float2 (&va)[L / G], float2 (&vb)[L / 
   trace_event(4);
 }
 
+constexpr bool kWideProbe = true;  // compile the kFft4WideProbe addressing (timing experiment)
+
 template <int L, int G, int R>
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, OneX<L, G, R>::THREADS),
                                amdgpu_waves_per_eu(OneX<L, G, R>::kWholeCu ? 1 : 2)))
@@ -761,6 +763,12 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int cp = t & 3, gg = t >> 2;
   const int N1 = g.n1;
+  if ((flags & kFft4Stagger) && blockIdx.x >= 256 && blockIdx.x < 512) {
+    // experiment: start the second workgroup of each CU late, so the two
+    // workgroups' load / compute / store phases are out of step
+    const int reps = (flags >> 24) & 63;
+    for (int i = 0; i < reps; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   trace_event(0);
   // block -> (trial k, first column c0): the Stockham kernel's order and XCD grouping
   const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
@@ -812,8 +820,13 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
     uint32_t bad = 0;
 #pragma unroll
     for (int m = 0; m < P; ++m) {
-      const uint32_t j = static_cast<uint32_t>(gg + G * m);
-      const uint32_t p0 = 2u * (static_cast<uint32_t>(N1) * j + static_cast<uint32_t>(c0 + 2 * cp));
+      // (kFft4WideProbe, timing only: the same bytes as 128-byte row pieces --
+      // 16 columns x half the rows per workgroup, 8 lanes per row)
+      const bool wide = kWideProbe && (flags & kFft4WideProbe);
+      const uint32_t j = wide ? static_cast<uint32_t>((t >> 3) + 32 * m + ((c0 & 8) ? L / 2 : 0))
+                              : static_cast<uint32_t>(gg + G * m);
+      const uint32_t col = wide ? static_cast<uint32_t>((c0 & ~15) + 2 * (t & 7)) : static_cast<uint32_t>(c0 + 2 * cp);
+      const uint32_t p0 = 2u * (static_cast<uint32_t>(N1) * j + col);
       const float pa = static_cast<float>(p0), pb = pa + 3.0f;
       const float fa = afl * pa * (pa - sizef), fb = afl * pb * (pb - sizef);
       const float sa = rintf(fa), sb = rintf(fb);
@@ -821,9 +834,14 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
       const bool ok = sa == sb && fabsf(fa - sa) < 0.5f - band && fabsf(fb - sb) < 0.5f - band && first >= 0 &&
                       first + 3 < static_cast<int64_t>(nn);
       const uint32_t i = ok ? static_cast<uint32_t>(first) : p0;
-      const f4v v = __builtin_bit_cast(
-          f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i >> log2row) * pitch + (i & rowmask)) * 4u, 0, 0));
-      bad |= ok ? 0u : (1u << m);
+      f4v v;
+      if (flags & kFft4SkipLoad) {  // timing only: no global loads
+        v = f4v{pa, fa, sa, sb};
+      } else {
+        v = __builtin_bit_cast(
+            f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i >> log2row) * pitch + (i & rowmask)) * 4u, 0, 0));
+        bad |= ok ? 0u : (1u << m);
+      }
       va[m] = make_float2(v.x, v.y);
       vb[m] = make_float2(v.z, v.w);
     }
@@ -846,7 +864,15 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
   }
   const int rc = (lane >> 3) & 7;
   float2 u[C::NPAIR][G];
-  onex_core<L, G, R>(va, vb, u, lds, tab + to.n2, t);
+  if (flags & kFft4SkipCompute) {  // timing only: the loaded values go straight to the stores
+#pragma unroll
+    for (int p = 0; p < C::NPAIR; ++p)
+#pragma unroll
+      for (int q = 0; q < G; ++q) u[p][q] = (q & 1) ? vb[(p * G + q) % P] : va[(p * G + q) % P];
+  } else {
+    onex_core<L, G, R>(va, vb, u, lds, tab + to.n2, t);
+  }
+  const bool skip_store = flags & kFft4SkipStore;
 
   // four-step twiddle W_M^{col k}, k = k1 + P k2: W_M^{col k1} (table pair)
   // times W_M^{col P k2} (the staged ox rows); tiled store
@@ -863,7 +889,8 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
     for (int k2 = 0; k2 < G; ++k2) {
       const float2 wv = k2 == 0 ? om : cmul(om, twr[k2]);
       const uint32_t kk = k1 + static_cast<uint32_t>(P * k2);
-      yk[(kk >> 3) * 64 + static_cast<uint32_t>(rc) * 8 + (kk & 7)] = cmul(u[p][k2], wv);
+      const float2 yv = cmul(u[p][k2], wv);
+      if (!skip_store || yv.x == 1234.5f) yk[(kk >> 3) * 64 + static_cast<uint32_t>(rc) * 8 + (kk & 7)] = yv;
     }
   }
   trace_event(11);
@@ -1331,7 +1358,8 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 16 == 0, "fft4 colpass: grid");
   PSOUP_CHECK(!(f & kFft4GroupXcd) || (K & 7) != 0 || nblocks % 128 == 0, "fft4 colpass: group grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
-  if ((f & kFft4OneX) && (f & kFft4Blocked) && (f & kFft4TileY) && !(f & (kTimingFlags | kFft4Sub2)) &&
+  // (the one-exchange pass A honours the timing flags itself)
+  if ((f & kFft4OneX) && (f & kFft4Blocked) && (f & kFft4TileY) && !(f & kFft4Sub2) &&
       (g.n2 == 2048 || ((f & kFft4OneXSmall) && (g.n2 == 512 || g.n2 == 1024)))) {
     switch (g.n2) {
 #define PS_ONEX(LL, GG, RR)                                                                                  \

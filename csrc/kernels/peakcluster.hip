@@ -54,22 +54,6 @@ __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* sc, uin
   return incl - v;
 }
 
-// min over the threads after this one (exclusive suffix min)
-__device__ __forceinline__ uint32_t block_excl_suffix_min(uint32_t v, uint32_t* sc) {
-  const int t = threadIdx.x;
-  sc[t] = v;
-  __syncthreads();
-  for (int off = 1; off < kClThreads; off <<= 1) {
-    const uint32_t a = t + off < kClThreads ? sc[t + off] : 0xffffffffu;
-    __syncthreads();
-    sc[t] = min(sc[t], a);
-    __syncthreads();
-  }
-  const uint32_t r = t + 1 < kClThreads ? sc[t + 1] : 0xffffffffu;
-  __syncthreads();
-  return r;
-}
-
 // Per-segment counts: each block counts its records in LDS and adds the
 // non-zero counts to the global ones (one atomic per block and segment, not
 // per record: heavy segments get tens of thousands of records).
@@ -157,11 +141,13 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
                                                                   uint32_t lo_n, uint2* __restrict__ out,
                                                                   uint2* __restrict__ segtab,
                                                                   uint32_t* __restrict__ total) {
-  constexpr uint32_t C = (CAP + kClThreads - 1) / kClThreads;  // positions per thread (contiguous chunk)
+  constexpr uint32_t R = (CAP + kClThreads - 1) / kClThreads;  // rows of kClThreads positions
   __shared__ uint2 key[CAP];      // (idx, snr bits)
   __shared__ uint16_t jmp[CAP];   // next survivor at/after a position, then chain jumps
   __shared__ uint8_t flag[CAP];   // bit 0: survives the window test, bit 1: cluster peak
   __shared__ uint32_t sc[kClThreads];
+  __shared__ uint32_t wcnt[kClThreads / 64];   // per wave: first survivor of the row
+  __shared__ uint32_t rw[R * (kClThreads / 64)];  // per (row, wave): peak count, then its output offset
   __shared__ uint32_t base_s, first_s;
   const int t = threadIdx.x;
   const uint32_t seg = blockIdx.x;
@@ -202,10 +188,17 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
       __syncthreads();
     }
   }
-  // (1) window test, contiguous chunk per thread
-  const uint32_t b0 = min(static_cast<uint32_t>(t) * C, n), b1 = min(b0 + C, n);
-  uint32_t firstv = n, nsurv = 0;
-  for (uint32_t i = b0; i < b1; ++i) {
+  // Every phase below gives position i = r * kClThreads + t to thread t
+  // (row r): consecutive lanes touch consecutive LDS words, and wave ballots
+  // order the survivors / peaks inside a row.
+  constexpr uint32_t kW = kClThreads / 64;
+  const uint32_t nrow = (n + kClThreads - 1) / kClThreads;
+  const int lane = t & 63, w = t >> 6;
+  // (1) window test
+  uint32_t mysurv = 0;
+  for (uint32_t r = 0; r < nrow; ++r) {
+    const uint32_t i = r * kClThreads + t;
+    if (i >= n) break;
     const int xi = static_cast<int>(key[i].x);
     const float si = __uint_as_float(key[i].y);
     bool keep = true;
@@ -215,79 +208,104 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
         break;
       }
     flag[i] = keep ? 1 : 0;
-    if (keep) {
-      firstv = min(firstv, i);
-      ++nsurv;
-    }
-  }
-  // next survivor at or after every position (suffix min over the chunks)
-  uint32_t cur = min(block_excl_suffix_min(firstv, sc), n);
-  for (uint32_t i = b1; i-- > b0;) {
-    if (flag[i] & 1) cur = i;
-    jmp[i] = static_cast<uint16_t>(cur);
+    mysurv += keep ? 1u : 0u;
   }
   uint32_t totsurv;
-  block_excl_sum(nsurv, sc, &totsurv);  // (its barriers also publish jmp)
-  if (t == 0) first_s = jmp[0];
+  block_excl_sum(mysurv, sc, &totsurv);  // (its barriers also publish flag)
+  // (3) next survivor at or after every position: rows from the last, a
+  // row's waves from their ballots, the carry from the rows after it
+  uint32_t carry = n;
+  for (uint32_t r = nrow; r-- > 0;) {
+    const uint32_t i = r * kClThreads + t;
+    const bool sv = i < n && (flag[i] & 1);
+    const uint64_t mask = __ballot(sv);
+    if (lane == 0) wcnt[w] = mask ? r * kClThreads + w * 64 + static_cast<uint32_t>(__builtin_ctzll(mask)) : n;
+    __syncthreads();
+    uint32_t c = carry;
+    for (int v = static_cast<int>(kW) - 1; v > w; --v) c = wcnt[v] < n ? wcnt[v] : c;
+    const uint64_t ge = mask >> lane;
+    if (i < n) jmp[i] = static_cast<uint16_t>(ge ? i + static_cast<uint32_t>(__builtin_ctzll(ge)) : c);
+    uint32_t rowfirst = n;
+    for (uint32_t v = 0; v < kW; ++v) rowfirst = min(rowfirst, wcnt[v]);
+    carry = rowfirst < n ? rowfirst : carry;
+    __syncthreads();
+  }
   // next(i): the first survivor with idx >= idx_i + gap (at most gap - 1
   // positions ahead have smaller idx: distinct bins)
-  uint32_t nx[C];
+  uint32_t nx[R];
+  if (t == 0) first_s = jmp[0];
 #pragma unroll
-  for (uint32_t c = 0; c < C; ++c) {
-    const uint32_t i = b0 + c;
-    nx[c] = n;
-    if (i < b1 && (flag[i] & 1)) {
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t i = r * kClThreads + t;
+    nx[r] = n;
+    if (i < n && (flag[i] & 1)) {
       const int target = static_cast<int>(key[i].x) + gap;
       uint32_t p = i + 1;
       while (p < n && static_cast<int>(key[p].x) < target) ++p;
-      nx[c] = p < n ? jmp[p] : n;
+      nx[r] = p < n ? jmp[p] : n;
     }
   }
   __syncthreads();
 #pragma unroll
-  for (uint32_t c = 0; c < C; ++c)
-    if (b0 + c < b1 && (flag[b0 + c] & 1)) jmp[b0 + c] = static_cast<uint16_t>(nx[c]);
+  for (uint32_t r = 0; r < R; ++r) {
+    const uint32_t i = r * kClThreads + t;
+    if (i < n && (flag[i] & 1)) jmp[i] = static_cast<uint16_t>(nx[r]);
+  }
+  __syncthreads();
   if (t == 0 && first_s < n) flag[first_s] = 3;
   __syncthreads();
   // (2) the chain from the first survivor, by pointer doubling: after round
-  // r every survivor within 2^(r+1) - 1 jumps of the start is marked
+  // m every survivor within 2^(m+1) - 1 jumps of the start is marked
   for (uint32_t span = 1; span < totsurv; span <<= 1) {
-    uint32_t tgt[C], nj[C];
+    uint32_t tgt[R], nj[R];
 #pragma unroll
-    for (uint32_t c = 0; c < C; ++c) {
-      const uint32_t i = b0 + c;
-      tgt[c] = n;
-      nj[c] = n;
-      if (i < b1 && (flag[i] & 1)) {
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t i = r * kClThreads + t;
+      tgt[r] = n;
+      nj[r] = n;
+      if (i < n && (flag[i] & 1)) {
         const uint32_t j = jmp[i];
         if (j < n) {
-          if (flag[i] & 2) tgt[c] = j;
-          nj[c] = jmp[j];
+          if (flag[i] & 2) tgt[r] = j;
+          nj[r] = jmp[j];
         }
       }
     }
     __syncthreads();
 #pragma unroll
-    for (uint32_t c = 0; c < C; ++c) {
-      const uint32_t i = b0 + c;
-      if (tgt[c] < n) flag[tgt[c]] = 3;
-      if (i < b1 && (flag[i] & 1)) jmp[i] = static_cast<uint16_t>(nj[c]);
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t i = r * kClThreads + t;
+      if (tgt[r] < n) flag[tgt[r]] = 3;
+      if (i < n && (flag[i] & 1)) jmp[i] = static_cast<uint16_t>(nj[r]);
     }
     __syncthreads();
   }
-  // compaction of the peaks, idx order
-  uint32_t cnt = 0;
-  for (uint32_t i = b0; i < b1; ++i) cnt += flag[i] >> 1;
-  uint32_t npk;
-  const uint32_t ex = block_excl_sum(cnt, sc, &npk);
-  if (t == 0) {
-    base_s = atomicAdd(total, npk);
-    segtab[seg] = make_uint2(base_s, npk);
+  // compaction of the peaks in idx order: per (row, wave) counts, their
+  // exclusive scan (one thread), then ballot ranks inside each wave
+  for (uint32_t r = 0; r < nrow; ++r) {
+    const uint32_t i = r * kClThreads + t;
+    const uint64_t mask = __ballot(i < n && (flag[i] >> 1));
+    if (lane == 0) rw[r * kW + w] = static_cast<uint32_t>(__builtin_popcountll(mask));
   }
   __syncthreads();
-  uint32_t o = base_s + ex;
-  for (uint32_t i = b0; i < b1; ++i)
-    if (flag[i] >> 1) out[o++] = key[i];
+  if (t == 0) {
+    uint32_t acc = 0;
+    for (uint32_t q = 0; q < nrow * kW; ++q) {
+      const uint32_t c = rw[q];
+      rw[q] = acc;
+      acc += c;
+    }
+    base_s = atomicAdd(total, acc);
+    segtab[seg] = make_uint2(base_s, acc);
+  }
+  __syncthreads();
+  for (uint32_t r = 0; r < nrow; ++r) {
+    const uint32_t i = r * kClThreads + t;
+    const bool pk = i < n && (flag[i] >> 1);
+    const uint64_t mask = __ballot(pk);
+    if (pk)
+      out[base_s + rw[r * kW + w] + static_cast<uint32_t>(__builtin_popcountll(mask & ((1ull << lane) - 1)))] = key[i];
+  }
 }
 
 // Fallbacks for batches with more than kSegLds segments: one global atomic per record.

@@ -303,6 +303,23 @@ PYBIND11_MODULE(_C, m) {
     sort_by_folded_snr(c);
     return c;
   });
+  // The permutation sort_by_folded_snr applies, from the keys max(snr,
+  // folded_snr) alone: std::sort's result depends only on the comparison
+  // outcomes, so reordering a Python list by it equals sorting the list
+  // (without converting candidates and their association trees).
+  m.def("sort_order_by_folded_snr", [](const std::vector<float>& snr, const std::vector<float>& folded) {
+    PSOUP_CHECK(snr.size() == folded.size(), "sort_order_by_folded_snr: size mismatch");
+    struct K {
+      float v;
+      int i;
+    };
+    std::vector<K> k(snr.size());
+    for (size_t i = 0; i < k.size(); ++i) k[i] = K{std::max(snr[i], folded[i]), static_cast<int>(i)};
+    std::sort(k.begin(), k.end(), [](const K& x, const K& y) { return x.v > y.v; });
+    std::vector<int> order(k.size());
+    for (size_t i = 0; i < k.size(); ++i) order[i] = k[i].i;
+    return order;
+  });
   m.def("serialize_candidates", [](const CandidateList& c) {
     auto v = serialize_candidates(c);
     return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
@@ -781,6 +798,11 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("opt_width", &FoldResult::opt_width)
       .def_readonly("opt_bin", &FoldResult::opt_bin)
       .def_readonly("fold", &FoldResult::fold)
+      .def_property_readonly("fold_array", [](const FoldResult& r) {  // float32 copy, no per-element conversion
+        py::array_t<float> a(static_cast<py::ssize_t>(r.fold.size()));
+        std::copy(r.fold.begin(), r.fold.end(), a.mutable_data());
+        return a;
+      })
       .def_readonly("prof", &FoldResult::prof);
   py::class_<FoldEngine>(m, "FoldEngine")
       .def(py::init([](uint64_t n, float tsamp, uintptr_t s) { return new FoldEngine(n, tsamp, S(s)); }))

@@ -39,6 +39,7 @@ import warnings
 from dataclasses import dataclass, field
 from typing import Callable, Dict, List, Optional, Sequence
 
+import numpy as np
 import torch
 
 from .. import _C
@@ -410,7 +411,7 @@ class RankSearcher:
             t_fe += time.perf_counter() - t0
             for (_, members), rr in zip(batch, res):
                 for i, r in zip(members, rr):
-                    out[i] = (r.folded_snr, r.opt_period, list(r.fold))
+                    out[i] = (r.folded_snr, r.opt_period, r.fold_array)
         self.fold_stats = {"fold_dedisp_s": t_dd, "fold_engine_s": t_fe, "fold_dms": len(items),
                            "fold_batches": (len(items) + B - 1) // B}
         return out
@@ -419,8 +420,9 @@ class RankSearcher:
 def _encode_fold_results(res: Dict[int, tuple]) -> bytes:
     parts = [struct.pack("<i", len(res))]
     for i, (snr, per, fold) in res.items():
-        parts.append(struct.pack("<ifdi", i, snr, per, len(fold)))
-        parts.append(struct.pack(f"<{len(fold)}f", *fold))
+        fold = np.ascontiguousarray(fold, dtype="<f4")
+        parts.append(struct.pack("<ifdi", i, snr, per, fold.size))
+        parts.append(fold.tobytes())
     return b"".join(parts)
 
 
@@ -431,7 +433,7 @@ def _decode_fold_results(b: bytes) -> Dict[int, tuple]:
     for _ in range(n):
         i, snr, per, nf = struct.unpack_from("<ifdi", b, off)
         off += struct.calcsize("<ifdi")
-        fold = list(struct.unpack_from(f"<{nf}f", b, off))
+        fold = np.frombuffer(b, dtype="<f4", count=nf, offset=off).tolist()
         off += 4 * nf
         out[i] = (snr, per, fold)
     return out
@@ -614,7 +616,9 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
                     c.fold = fold
                     c.nbins, c.nints = 64, 16
                     cands[i] = c
-            cands = _C.sort_by_folded_snr(cands)
+            # sort_by_folded_snr's permutation, applied to the Python list
+            order = _C.sort_order_by_folded_snr([c.snr for c in cands], [c.folded_snr for c in cands])
+            cands = [cands[i] for i in order]
         fold_stats = dict(getattr(rs, "fold_stats", {}))
         fold_stats.update({"fold_call_s": t_f1 - t_f0, "fold_merge_s": time.perf_counter() - t_f1})
     timers["folding"].stop()

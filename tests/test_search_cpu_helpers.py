@@ -64,3 +64,22 @@ def test_time_shards_option():
     assert ok and a.time_shards is False
     ok, _, a = _C.parse_cmdline(["peasoup", "-i", "x.fil", "--time_shards"])
     assert ok and a.time_shards is True
+
+
+def test_sort_order_by_folded_snr_is_the_sort_permutation():
+    """The fold merge reorders the Python candidate list by the permutation
+    sort_by_folded_snr (std::sort, unstable) applies: equal keys included."""
+    import numpy as np
+
+    from peasoup_amd import _C
+
+    rng = np.random.default_rng(4)
+    for n in (1, 5, 17, 300, 2000):
+        cands = []
+        for i in range(n):
+            c = _C.Candidate(1.0, i, 0.0, 0, float(rng.integers(9, 14)), float(i + 1))
+            c.folded_snr = float(rng.integers(0, 16)) if rng.random() < 0.5 else 0.0
+            cands.append(c)
+        ref = [c.freq for c in _C.sort_by_folded_snr(cands)]
+        order = _C.sort_order_by_folded_snr([c.snr for c in cands], [c.folded_snr for c in cands])
+        assert [cands[i].freq for i in order] == ref
