@@ -26,10 +26,15 @@
 // Block ids are remapped so that each XCD (blockIdx % 8 under round-robin
 // dispatch) works on a contiguous range of (column block, trial) pairs: the
 // trials of one column block, whose resampled reads overlap, share one L2.
+#include "cplx_pk.hpp"
 #include "device_common.hpp"
 #include "psoup/kernels.hpp"
 
 #include <cmath>
+
+#ifndef PSOUP_FFT_SCALAR
+#define PSOUP_FFT_SCALAR 0
+#endif
 
 namespace psoup {
 namespace kern {
@@ -73,12 +78,36 @@ typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // dword-ali
 typedef float f4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int lds_pad(int x) { return x + (x >> 3); }
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // * -i
+
+// The butterflies and twiddle products run on the packed-f32 VALU
+// (cplx_pk.hpp: half the VALU issue slots of the scalar forms, which
+// PSOUP_FFT_SCALAR=1 at compile time restores for A/B runs).
+#if PSOUP_FFT_SCALAR
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
-__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // * -i
+__device__ __forceinline__ float2 cadd_mi(float2 a, float2 b) { return cadd(a, mul_mi(b)); }
+__device__ __forceinline__ float2 csub_mi(float2 a, float2 b) { return csub(a, mul_mi(b)); }
+__device__ __forceinline__ float2 mul_w8(float2 c) {
+  constexpr float r2 = 0.70710678118654752440f;
+  return make_float2(r2 * (c.x + c.y), r2 * (c.y - c.x));
+}
+__device__ __forceinline__ float2 mul_w83(float2 c) {
+  constexpr float r2 = 0.70710678118654752440f;
+  return make_float2(r2 * (c.y - c.x), -r2 * (c.x + c.y));
+}
+#else
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return pk::add(a, b); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return pk::sub(a, b); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) { return pk::mul(a, b); }
+__device__ __forceinline__ float2 cadd_mi(float2 a, float2 b) { return pk::add_mi(a, b); }
+__device__ __forceinline__ float2 csub_mi(float2 a, float2 b) { return pk::sub_mi(a, b); }
+__device__ __forceinline__ float2 mul_w8(float2 c) { return pk::mul_w8(c); }
+__device__ __forceinline__ float2 mul_w83(float2 c) { return pk::mul_w83(c); }
+#endif
 
 __device__ __forceinline__ void fft2(float2& a, float2& b) {
   const float2 t = a;
@@ -89,22 +118,21 @@ __device__ __forceinline__ void fft2(float2& a, float2& b) {
 // Forward 4-point DFT, natural order in and out.
 __device__ __forceinline__ void fft4(float2& x0, float2& x1, float2& x2, float2& x3) {
   const float2 s0 = cadd(x0, x2), d0 = csub(x0, x2);
-  const float2 s1 = cadd(x1, x3), d1 = mul_mi(csub(x1, x3));
+  const float2 s1 = cadd(x1, x3), e1 = csub(x1, x3);
   x0 = cadd(s0, s1);
   x2 = csub(s0, s1);
-  x1 = cadd(d0, d1);
-  x3 = csub(d0, d1);
+  x1 = cadd_mi(d0, e1);  // d0 + (-i) e1
+  x3 = csub_mi(d0, e1);
 }
 
 // Forward 8-point DFT (decimation in frequency), natural order in and out.
 __device__ __forceinline__ void fft8(float2& a0, float2& a1, float2& a2, float2& a3, float2& a4, float2& a5,
                                      float2& a6, float2& a7) {
-  constexpr float r2 = 0.70710678118654752440f;
   float2 b0 = cadd(a0, a4), b1 = cadd(a1, a5), b2 = cadd(a2, a6), b3 = cadd(a3, a7);
   float2 c0 = csub(a0, a4), c1 = csub(a1, a5), c2 = csub(a2, a6), c3 = csub(a3, a7);
-  c1 = make_float2(r2 * (c1.x + c1.y), r2 * (c1.y - c1.x));     // * W8
-  c2 = mul_mi(c2);                                             // * W8^2
-  c3 = make_float2(r2 * (c3.y - c3.x), -r2 * (c3.x + c3.y));    // * W8^3
+  c1 = mul_w8(c1);    // * W8
+  c2 = mul_mi(c2);    // * W8^2
+  c3 = mul_w83(c3);   // * W8^3
   fft4(b0, b1, b2, b3);
   fft4(c0, c1, c2, c3);
   a0 = b0; a1 = c0; a2 = b1; a3 = c1; a4 = b2; a5 = c2; a6 = b3; a7 = c3;
@@ -624,11 +652,12 @@ __device__ __forceinline__ float2 twc(float2 v) {
   } else if constexpr (4 * e == 3 * N) {
     return make_float2(-v.y, v.x);
   } else if constexpr (8 * e == N) {
-    constexpr float r2 = 0.70710678118654752440f;
-    return make_float2(r2 * (v.x + v.y), r2 * (v.y - v.x));
+    return mul_w8(v);
+  } else if constexpr (8 * e == 3 * N) {
+    return mul_w83(v);
   } else {
     constexpr ccf w = wconst(N, e);
-    return make_float2(v.x * w.x - v.y * w.y, v.x * w.y + v.y * w.x);
+    return cmul(v, make_float2(w.x, w.y));
   }
 }
 
