@@ -192,6 +192,8 @@ class Whitener {
   float bin_width() const { return bin_width_; }
   bool uses_fft4() const { return f4_ || mixed_; }  // no rocFFT (power-of-two or mixed-radix four-step passes)
   bool mixed_radix() const { return mixed_; }
+  // Allocate whiten_batch's buffers for `count` trials now.
+  void reserve_batch(int count);
 
  private:
   FftPlan& r2c();
@@ -408,6 +410,14 @@ class FoldEngine {
                                                    uint64_t trial_nsamps, int ntrials,
                                                    const std::vector<std::vector<double>>& periods,
                                                    const std::vector<std::vector<float>>& accs);
+  // The same for DM trials resident at scattered device rows (the search's
+  // kept dedispersed rows): gathered per batch by one copy kernel.
+  std::vector<std::vector<FoldResult>> fold_rows(const std::vector<const uint8_t*>& rows, uint64_t trial_nsamps,
+                                                 const std::vector<std::vector<double>>& periods,
+                                                 const std::vector<std::vector<float>>& accs);
+  // Allocate every batch buffer up front (a full batch of trials and
+  // njobs_hint candidates), so the fold stage's first batch does not pay it.
+  void reserve(int njobs_hint);
   // DM trials whitened per batch (device memory bounds it)
   int max_batch() const { return max_batch_; }
   // Fold + optimise candidates on an already-whitened series (testing).
@@ -421,6 +431,7 @@ class FoldEngine {
   hipStream_t stream_;
   std::unique_ptr<Whitener> wh_;
   int max_batch_ = 1;
+  DeviceBuffer<uint8_t> gathered_;  // fold_rows: one batch of gathered rows
   std::vector<FoldResult> fold_jobs(const float* d_series, const std::vector<kern::FoldJob>& jobs,
                                     const std::vector<double>& periods);
   DeviceBuffer<float> bstats_;

@@ -207,7 +207,7 @@ struct Fft4Geom {
   uint64_t ypitch = 0, ystride = 0;  // complex
   uint64_t xpitch = 0, xstride = 0;  // complex
   int log2_xrow = 0;                 // log2(n2): X index of bin k = (k >> log2_xrow)*xpitch + (k & (n2-1))
-  uint64_t inpitch = 0, insize = 0;  // floats: padded input copy
+  uint64_t inpitch = 0, insize = 0;  // floats: padded input copy (room for either layout: row pitch or strips)
   bool ok = false;
   // Pass A input per trial k: in + k*in_tstride, in_pad + k*pad_tstride
   // (0 = every trial resamples the same series; the batched whitener sets n, insize).
@@ -340,6 +340,9 @@ enum Fft4Flags : int {
                               // the same load bytes as 128-byte row pieces
   kFft4Stagger = 4194304,     // experiment (one-exchange pass A): blocks 256..511 sleep ((flags >> 24) & 63)
                               // x 8k cycles first, putting each CU's two workgroups out of phase
+  kFft4StripInput = 1073741824,  // one-exchange pass A: the padded input in column strips (16 + 4 floats of
+                                 // every row per strip, strips row-contiguous), so a wave's 16 rows are
+                                 // one ~1.3 KiB contiguous range instead of 16 pieces 16 KiB apart
 };
 void fft4_set_flags(int flags);
 // Debug: per-workgroup phase timestamps of the fft4 passes (12 x u64 per block), nullptr = off.
@@ -408,6 +411,14 @@ void coincidence_mask(const uint8_t* counts, uint64_t n, int beam_thresh, float*
 // ------------------------------------------------------------- correlation --
 void conjugate(float2* x, uint64_t n, hipStream_t s);
 void cmul_inplace(const float2* x, float2* y, uint64_t n, hipStream_t s);
+// Copy nrows scattered device rows of nbytes (16-byte aligned multiples) to
+// dst + i * dst_stride, one launch per kGatherRows rows.
+constexpr int kGatherRows = 64;
+struct RowPtrs {
+  const uint8_t* p[kGatherRows];
+};
+void gather_rows(const uint8_t* const* rows, int nrows, uint64_t nbytes, uint8_t* dst, uint64_t dst_stride,
+                 hipStream_t s);
 
 }  // namespace kern
 }  // namespace psoup

@@ -26,15 +26,11 @@
 // Block ids are remapped so that each XCD (blockIdx % 8 under round-robin
 // dispatch) works on a contiguous range of (column block, trial) pairs: the
 // trials of one column block, whose resampled reads overlap, share one L2.
-#include "cplx_pk.hpp"
 #include "device_common.hpp"
+#include "dft_reg.hpp"
 #include "psoup/kernels.hpp"
 
 #include <cmath>
-
-#ifndef PSOUP_FFT_SCALAR
-#define PSOUP_FFT_SCALAR 0
-#endif
 
 namespace psoup {
 namespace kern {
@@ -78,65 +74,7 @@ typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // dword-ali
 typedef float f4v __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ int lds_pad(int x) { return x + (x >> 3); }
-__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // * -i
-
-// The butterflies and twiddle products run on the packed-f32 VALU
-// (cplx_pk.hpp: half the VALU issue slots of the scalar forms, which
-// PSOUP_FFT_SCALAR=1 at compile time restores for A/B runs).
-#if PSOUP_FFT_SCALAR
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ float2 cadd_mi(float2 a, float2 b) { return cadd(a, mul_mi(b)); }
-__device__ __forceinline__ float2 csub_mi(float2 a, float2 b) { return csub(a, mul_mi(b)); }
-__device__ __forceinline__ float2 mul_w8(float2 c) {
-  constexpr float r2 = 0.70710678118654752440f;
-  return make_float2(r2 * (c.x + c.y), r2 * (c.y - c.x));
-}
-__device__ __forceinline__ float2 mul_w83(float2 c) {
-  constexpr float r2 = 0.70710678118654752440f;
-  return make_float2(r2 * (c.y - c.x), -r2 * (c.x + c.y));
-}
-#else
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return pk::add(a, b); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return pk::sub(a, b); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) { return pk::mul(a, b); }
-__device__ __forceinline__ float2 cadd_mi(float2 a, float2 b) { return pk::add_mi(a, b); }
-__device__ __forceinline__ float2 csub_mi(float2 a, float2 b) { return pk::sub_mi(a, b); }
-__device__ __forceinline__ float2 mul_w8(float2 c) { return pk::mul_w8(c); }
-__device__ __forceinline__ float2 mul_w83(float2 c) { return pk::mul_w83(c); }
-#endif
-
-__device__ __forceinline__ void fft2(float2& a, float2& b) {
-  const float2 t = a;
-  a = cadd(t, b);
-  b = csub(t, b);
-}
-
-// Forward 4-point DFT, natural order in and out.
-__device__ __forceinline__ void fft4(float2& x0, float2& x1, float2& x2, float2& x3) {
-  const float2 s0 = cadd(x0, x2), d0 = csub(x0, x2);
-  const float2 s1 = cadd(x1, x3), e1 = csub(x1, x3);
-  x0 = cadd(s0, s1);
-  x2 = csub(s0, s1);
-  x1 = cadd_mi(d0, e1);  // d0 + (-i) e1
-  x3 = csub_mi(d0, e1);
-}
-
-// Forward 8-point DFT (decimation in frequency), natural order in and out.
-__device__ __forceinline__ void fft8(float2& a0, float2& a1, float2& a2, float2& a3, float2& a4, float2& a5,
-                                     float2& a6, float2& a7) {
-  float2 b0 = cadd(a0, a4), b1 = cadd(a1, a5), b2 = cadd(a2, a6), b3 = cadd(a3, a7);
-  float2 c0 = csub(a0, a4), c1 = csub(a1, a5), c2 = csub(a2, a6), c3 = csub(a3, a7);
-  c1 = mul_w8(c1);    // * W8
-  c2 = mul_mi(c2);    // * W8^2
-  c3 = mul_w83(c3);   // * W8^3
-  fft4(b0, b1, b2, b3);
-  fft4(c0, c1, c2, c3);
-  a0 = b0; a1 = c0; a2 = b1; a3 = c1; a4 = b2; a5 = c2; a6 = b3; a7 = c3;
-}
+using namespace dreg;  // butterflies, packed complex arithmetic, dft<N> (dft_reg.hpp)
 
 // One Stockham iteration's arithmetic (Govindaraju et al. formulation): for
 // virtual thread j' = t + b*T, points v[b + r*B] = data[j' + r*L/R] are
@@ -418,13 +356,47 @@ __device__ __forceinline__ uint32_t logical_block(uint32_t nblocks, bool remap) 
 // channels instead of one.
 __global__ void __launch_bounds__(256) fft4_pad_input_kernel(const float* __restrict__ in, uint64_t n,
                                                              float* __restrict__ out, uint64_t rowlen,
-                                                             uint64_t pitch, uint64_t total, uint64_t in_stride) {
+                                                             uint64_t pitch, uint64_t total, uint64_t in_stride,
+                                                             uint64_t out_stride) {
   in += blockIdx.y * in_stride;
-  out += blockIdx.y * total;
+  out += blockIdx.y * out_stride;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t u = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; u < total; u += stride) {
     const uint64_t row = u / pitch, r = u - row * pitch;
     const uint64_t src = row * rowlen + r;
+    out[u] = src < n ? in[src] : 0.f;
+  }
+}
+
+// Strip layout of the padded input (kFft4StripInput, one-exchange pass A):
+// strip b holds floats [16 b, 16 b + kStripW) of every row (rows of 2*N1
+// floats; the last strip's tail is the next row's head), rows of a strip
+// contiguous: element (row j, strip b, e) at (b * N2 + j) * kStripW + e.  A
+// lane's four resampled samples start at offset (col & 15) <= 15 of the
+// strip its first sample falls in, so kStripW = 20 always covers them, and a
+// wave's 16 consecutive rows (at most two strips) are one or two contiguous
+// ~1.3 KiB ranges.  1.25 x the series in floats.
+constexpr int kStripW = 20;
+__host__ __device__ constexpr uint64_t strip_floats(int n1, int n2) {
+  return static_cast<uint64_t>(n1 / 8) * static_cast<uint64_t>(n2) * kStripW;
+}
+__host__ __device__ inline bool onex_colpass(int n2, int f) {
+  return (f & kFft4OneX) && (f & kFft4Blocked) && (f & kFft4TileY) && !(f & kFft4Sub2) &&
+         (n2 == 2048 || ((f & kFft4OneXSmall) && (n2 == 512 || n2 == 1024)));
+}
+__host__ __device__ inline bool strip_input(int n2, int f) { return (f & kFft4StripInput) && onex_colpass(n2, f); }
+
+__global__ void __launch_bounds__(256) fft4_pad_strips_kernel(const float* __restrict__ in, uint64_t n,
+                                                              float* __restrict__ out, uint32_t rowlen,
+                                                              uint32_t nrows, uint32_t total, uint64_t in_stride,
+                                                              uint64_t out_stride) {
+  in += blockIdx.y * in_stride;
+  out += blockIdx.y * out_stride;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < total; u += stride) {
+    const uint32_t rest = u / kStripW, e = u - rest * kStripW;
+    const uint32_t b = rest / nrows, j = rest - b * nrows;
+    const uint64_t src = static_cast<uint64_t>(j) * rowlen + 16u * b + e;
     out[u] = src < n ? in[src] : 0.f;
   }
 }
@@ -586,113 +558,6 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
 // that every store instruction of a wave writes one contiguous 512-byte block
 // of the tiled Y.
 
-// compile-time twiddles: W_N^e = exp(-2 pi i e / N), octant-reduced Taylor series in double
-struct ccf {
-  float x, y;
-};
-constexpr double ct_sin(double x) {  // |x| <= pi/4
-  double term = x, sum = x;
-  for (int i = 1; i < 12; ++i) {
-    term *= -x * x / ((2.0 * i) * (2.0 * i + 1.0));
-    sum += term;
-  }
-  return sum;
-}
-constexpr double ct_cos(double x) {
-  double term = 1.0, sum = 1.0;
-  for (int i = 1; i < 12; ++i) {
-    term *= -x * x / ((2.0 * i - 1.0) * (2.0 * i));
-    sum += term;
-  }
-  return sum;
-}
-constexpr ccf wconst(int N, int e) {
-  e = ((e % N) + N) % N;
-  const int q = (4 * e) / N, rem = e - q * (N / 4);  // angle = q quarter turns + 2 pi rem / N
-  constexpr double kTwoPi = 6.28318530717958647692;
-  double c = 0.0, s = 0.0;
-  if (8 * rem <= N) {
-    const double th = kTwoPi * rem / N;
-    c = ct_cos(th);
-    s = ct_sin(th);
-  } else {
-    const double th = kTwoPi * (N / 4 - rem) / N;
-    c = ct_sin(th);
-    s = ct_cos(th);
-  }
-  double cq = c, sq = s;  // rotate by q quarter turns
-  if (q == 1) { cq = -s; sq = c; }
-  if (q == 2) { cq = -c; sq = -s; }
-  if (q == 3) { cq = s; sq = -c; }
-  return ccf{static_cast<float>(cq), static_cast<float>(-sq)};
-}
-
-template <int I>
-struct ic {
-  static constexpr int value = I;
-};
-template <int B, int E, class F>
-__device__ __forceinline__ void sfor(F&& f) {
-  if constexpr (B < E) {
-    f(ic<B>{});
-    sfor<B + 1, E>(static_cast<F&&>(f));
-  }
-}
-
-// v * W_N^E (compile-time exponent; trivial factors without multiplications)
-template <int N, int E>
-__device__ __forceinline__ float2 twc(float2 v) {
-  constexpr int e = ((E % N) + N) % N;
-  if constexpr (e == 0) {
-    return v;
-  } else if constexpr (2 * e == N) {
-    return make_float2(-v.x, -v.y);
-  } else if constexpr (4 * e == N) {
-    return mul_mi(v);
-  } else if constexpr (4 * e == 3 * N) {
-    return make_float2(-v.y, v.x);
-  } else if constexpr (8 * e == N) {
-    return mul_w8(v);
-  } else if constexpr (8 * e == 3 * N) {
-    return mul_w83(v);
-  } else {
-    constexpr ccf w = wconst(N, e);
-    return cmul(v, make_float2(w.x, w.y));
-  }
-}
-
-// In-register forward DFT of length N (power of two <= 64), natural order in
-// and out: N = 8 B, n = B a + b, k = ka + 8 kb.
-template <int N>
-__device__ __forceinline__ void dft(float2 (&x)[N]) {
-  if constexpr (N == 2) {
-    fft2(x[0], x[1]);
-  } else if constexpr (N == 4) {
-    fft4(x[0], x[1], x[2], x[3]);
-  } else if constexpr (N == 8) {
-    fft8(x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]);
-  } else {
-    constexpr int A = 8, B = N / 8;
-    float2 y[N];
-    sfor<0, B>([&](auto bc) {
-      constexpr int b = decltype(bc)::value;
-      float2 t[A];
-      sfor<0, A>([&](auto ac) { t[decltype(ac)::value] = x[B * decltype(ac)::value + b]; });
-      dft<A>(t);
-      sfor<0, A>([&](auto kc) {
-        constexpr int ka = decltype(kc)::value;
-        y[b * A + ka] = twc<N, b * ka>(t[ka]);
-      });
-    });
-    sfor<0, A>([&](auto kc) {
-      constexpr int ka = decltype(kc)::value;
-      float2 t[B];
-      sfor<0, B>([&](auto bc) { t[decltype(bc)::value] = y[decltype(bc)::value * A + ka]; });
-      dft<B>(t);
-      sfor<0, B>([&](auto jc) { x[ka + A * decltype(jc)::value] = t[decltype(jc)::value]; });
-    });
-  }
-}
 
 template <int L, int G, int R>
 struct OneX {
@@ -846,6 +711,8 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(padk), 0, 0x7fffffff, 0x00020000);
     const uint32_t rowmask = (1u << log2row) - 1u, pitch = static_cast<uint32_t>(g.inpitch);
+    const bool strips = flags & kFft4StripInput;  // (the host pads in strips exactly when this kernel runs)
+    const uint32_t nrows = static_cast<uint32_t>(L);
     uint32_t bad = 0;
 #pragma unroll
     for (int m = 0; m < P; ++m) {
@@ -867,8 +734,9 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
       if (flags & kFft4SkipLoad) {  // timing only: no global loads
         v = f4v{pa, fa, sa, sb};
       } else {
-        v = __builtin_bit_cast(
-            f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i >> log2row) * pitch + (i & rowmask)) * 4u, 0, 0));
+        const uint32_t row = i >> log2row, col = i & rowmask;
+        const uint32_t off = strips ? ((col >> 4) * nrows + row) * kStripW + (col & 15u) : row * pitch + col;
+        v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, off * 4u, 0, 0));
         bad |= ok ? 0u : (1u << m);
       }
       va[m] = make_float2(v.x, v.y);
@@ -1287,7 +1155,7 @@ Fft4Geom fft4_geometry(uint64_t M) {
   g.xstride = g.xpitch * g.n1;
   g.log2_xrow = a;
   g.inpitch = 2 * static_cast<uint64_t>(g.n1) + 32;
-  g.insize = g.inpitch * g.n2;
+  g.insize = std::max(g.inpitch * g.n2, strip_floats(g.n1, g.n2));
   g.ok = true;
   return g;
 }
@@ -1313,17 +1181,33 @@ std::vector<float2> fft4_tables(const Fft4Geom& g) {
   return t;
 }
 
+namespace {
+// fastest measured (tools/kbench.py, bench A/B); the strip input: pass A 15.9 -> 13.9 us/trial alone,
+// bench within noise (profiles/r3_strip)
+int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4TileY | kFft4TileX | kFft4PairXcd |
+                   kFft4GroupXcd | kFft4UniformTw | kFft4OneX | kFft4StripInput;
+}  // namespace
+
 void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& g, hipStream_t s, int count,
                     uint64_t in_stride) {
   PSOUP_CHECK(count >= 1 && count <= 65535, "fft4_pad_input: bad count");
-  const dim3 grid(dev::grid_for(g.insize, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
-  fft4_pad_input_kernel<<<grid, 256, 0, s>>>(in, n, in_pad, 2ull * g.n1, g.inpitch, g.insize, in_stride);
+  if (strip_input(g.n2, g_fft4_flags)) {
+    const uint64_t total = strip_floats(g.n1, g.n2);
+    PSOUP_CHECK(total < (1ull << 32) && total <= g.insize, "fft4_pad_input: strip layout size");
+    const dim3 grid(dev::grid_for(total, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
+    fft4_pad_strips_kernel<<<grid, 256, 0, s>>>(in, n, in_pad, 2u * static_cast<uint32_t>(g.n1),
+                                                static_cast<uint32_t>(g.n2), static_cast<uint32_t>(total), in_stride,
+                                                g.insize);
+    post_launch_check("fft4_pad_strips_kernel", s);
+    return;
+  }
+  const uint64_t total = g.inpitch * g.n2;
+  const dim3 grid(dev::grid_for(total, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
+  fft4_pad_input_kernel<<<grid, 256, 0, s>>>(in, n, in_pad, 2ull * g.n1, g.inpitch, total, in_stride, g.insize);
   post_launch_check("fft4_pad_input_kernel", s);
 }
 
 namespace {
-int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4TileY | kFft4TileX | kFft4PairXcd |
-                   kFft4GroupXcd | kFft4UniformTw | kFft4OneX;  // fastest measured (tools/kbench.py, bench A/B)
 
 template <int CPT, int SUB, int MODE>
 void launch_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,

@@ -9,7 +9,8 @@
 // Here: (1) fold_accumulate fuses the v1 acceleration resampler (K5) into
 // the fold and runs many blocks per subint with register run-length
 // accumulation before LDS atomics, writing deterministic partial sums;
-// (2) fold_optimise is ONE workgroup per candidate doing every step in LDS.
+// (2) fold_optimise is ONE workgroup per candidate doing every step in LDS
+// and registers, its 64-point DFTs as register FFTs.
 // The template search uses the identity
 //     IFFT(P . FFT(boxcar_w))[j] = sum_{m<w} IFFT(P)[j-m]
 // so the 63 widths are sliding-window sums of one 64-pt inverse DFT per drift
@@ -18,12 +19,15 @@
 #include <cmath>
 
 #include "device_common.hpp"
+#include "dft_reg.hpp"
 #include "psoup/kernels.hpp"
 
 namespace psoup {
 namespace kern {
 
 namespace {
+
+using namespace dreg;  // cadd / cmul / dft<64> / idft<64> (dft_reg.hpp)
 
 constexpr int kNb = 64;  // bins (the reference hard-codes 64 bins x 16 subints)
 constexpr int kNi = 16;
@@ -133,102 +137,121 @@ __global__ void fold_shift_table_kernel(float2* __restrict__ table, int nbins, i
   table[idx] = make_float2(cs * e, sn * e);
 }
 
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+// |S|^2 / (t + 1) of a template response (the reference ranks |S| / sqrt(t + 1),
+// the same order); one explicit fma so both passes below compute it bitwise
+// alike under any contraction setting.
+__device__ __forceinline__ float template_power(float2 S, float inv_w) {
+  return __builtin_fmaf(S.y, S.y, S.x * S.x) * inv_w;
 }
 
-// One block (256 threads) per candidate fold [kNi][kNb].
+// One block (256 threads) per candidate fold [kNi][kNb].  The DFTs of steps
+// 1, 3 and 5 are 64-point radix-8 FFTs in registers (dft_reg.hpp: packed-f32
+// butterflies, literal twiddles) -- ~550 packed VALU instructions per
+// transform where a 64 x 64 DFT-matrix product costs 64x more multiply-adds
+// (as four real 64^3 GEMMs on the f32 MFMA: 512 v_mfma_f32_32x32x2f32 of
+// 64 cycles per candidate vs ~2.2k cycles for the 64 row FFTs of step 3).
+// Step 4 (every boxcar width at every drift and phase: 258k template
+// responses per candidate, the bulk of the work) runs on each thread's
+// rotated copy of its drift row in registers with compile-time indices.
 __global__ void __launch_bounds__(256) fold_optimise_kernel(const float* __restrict__ folds,
                                                             const float2* __restrict__ shift_table,
                                                             float* __restrict__ opt_fold,
                                                             float* __restrict__ opt_prof,
                                                             int32_t* __restrict__ opt_int,
                                                             float* __restrict__ opt_val) {
-  __shared__ float2 tw[kNb];                 // e^{+2 pi i m/64}
-  __shared__ float fin[kNi * kNb];           // input fold
-  __shared__ float2 F[kNi * kNb];            // per-subint forward DFT
-  __shared__ float2 prof[kNb * kNb];         // [shift][bin] collapsed profiles
-  __shared__ float2 Q[kNb * kNb];            // [shift][j] inverse DFT (DC removed)
+  constexpr int P = kNb + 1;                 // padded LDS rows (complex)
+  __shared__ float2 F[kNi * P];              // per-subint forward DFT [i][b]
+  __shared__ float2 prof[kNb * P];           // [shift][bin] collapsed profiles
+  __shared__ float2 Q[kNb * P];              // [shift][j] inverse DFT (DC removed)
   __shared__ float red_v[256];
   __shared__ int red_i[256];
   const int tid = threadIdx.x;
   const int cand = blockIdx.x;
   const float* f = folds + static_cast<uint64_t>(cand) * kNi * kNb;
+  // 1. F[i][b] = sum_t f[i][t] e^{-2 pi i b t / 64}
+  if (tid < kNi) {
+    float2 x[kNb];
+    const float4* src = reinterpret_cast<const float4*>(f + tid * kNb);
+#pragma unroll
+    for (int q = 0; q < kNb / 4; ++q) {
+      const float4 v = src[q];
+      x[4 * q] = make_float2(v.x, 0.f);
+      x[4 * q + 1] = make_float2(v.y, 0.f);
+      x[4 * q + 2] = make_float2(v.z, 0.f);
+      x[4 * q + 3] = make_float2(v.w, 0.f);
+    }
+    dft<kNb>(x);
+#pragma unroll
+    for (int b = 0; b < kNb; ++b) F[tid * P + b] = x[b];
+  }
+  __syncthreads();
+  // 2. drifts and subint collapse: prof[s][b] = sum_i F[i][b] * shift[s][i][b]
+  {
+    const int b = tid & (kNb - 1), sg = tid >> 6;
+    float2 Fi[kNi];
+#pragma unroll
+    for (int i = 0; i < kNi; ++i) Fi[i] = F[i * P + b];
+    for (int s = sg; s < kNb; s += 4) {
+      float2 acc = make_float2(0.f, 0.f);
+#pragma unroll
+      for (int i = 0; i < kNi; ++i) acc = cadd(acc, cmul(Fi[i], shift_table[(s * kNi + i) * kNb + b]));
+      prof[s * P + b] = acc;
+    }
+  }
+  __syncthreads();
+  // 3. Q[s][j] = sum_{b>=1} prof[s][b] e^{+2 pi i b j / 64}   (template bin 0 is zeroed)
   if (tid < kNb) {
-    double sn, cs;
-    sincospi(2.0 * tid / kNb, &sn, &cs);
-    tw[tid] = make_float2(static_cast<float>(cs), static_cast<float>(sn));
-  }
-  for (int i = tid; i < kNi * kNb; i += 256) fin[i] = f[i];
-  __syncthreads();
-  // 1. forward DFT of each subint: F[i][b] = sum_t f[i][t] e^{-2 pi i b t/64}
-  for (int o = tid; o < kNi * kNb; o += 256) {
-    const int i = o / kNb, b = o % kNb;
-    float re = 0.f, im = 0.f;
-    for (int t = 0; t < kNb; ++t) {
-      const float2 w = tw[(b * t) & (kNb - 1)];
-      const float v = fin[i * kNb + t];
-      re += v * w.x;
-      im -= v * w.y;
-    }
-    F[o] = make_float2(re, im);
+    float2 x[kNb];
+    x[0] = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int b = 1; b < kNb; ++b) x[b] = prof[tid * P + b];
+    idft<kNb>(x);
+#pragma unroll
+    for (int j = 0; j < kNb; ++j) Q[tid * P + j] = x[j];
   }
   __syncthreads();
-  // 2. apply drifts and collapse subints: prof[s][b] = sum_i F[i][b] * shift[s][i][b]
-  for (int o = tid; o < kNb * kNb; o += 256) {
-    const int s = o / kNb, b = o % kNb;
-    float2 acc = make_float2(0.f, 0.f);
-    for (int i = 0; i < kNi; ++i) {
-      const float2 v = cmul(F[i * kNb + b], shift_table[(s * kNi + i) * kNb + b]);
-      acc.x += v.x;
-      acc.y += v.y;
-    }
-    prof[o] = acc;
-  }
-  __syncthreads();
-  // 3. Q[s][j] = sum_{b>=1} prof[s][b] e^{+2 pi i b j/64}   (template bin 0 is zeroed)
-  for (int o = tid; o < kNb * kNb; o += 256) {
-    const int s = o / kNb, j = o % kNb;
-    float re = 0.f, im = 0.f;
-    for (int b = 1; b < kNb; ++b) {
-      const float2 p = prof[s * kNb + b];
-      const float2 w = tw[(b * j) & (kNb - 1)];
-      re += p.x * w.x - p.y * w.y;
-      im += p.x * w.y + p.y * w.x;
-    }
-    Q[o] = make_float2(re, im);
-  }
-  __syncthreads();
-  // 4. boxcar widths 1..63 as sliding sums; argmax over (template, shift, bin)
+  // 4. boxcar widths 1..63 as sliding sums of Q; argmax over (template, shift,
+  // bin) with the first-maximum rule of thrust::max_element (index
+  // t * 4096 + s * 64 + j): the maximum first, then the first index holding it
+  const int s = tid >> 2, q = tid & 3;       // drift row s, bins j = 16 q + jj
   float best = -1.f;
-  int besti = 0x7fffffff;
-  for (int o = tid; o < kNb * kNb; o += 256) {
-    const int s = o / kNb, j = o % kNb;
-    float sr = 0.f, si = 0.f;
-    for (int t = 0; t < kNb - 1; ++t) {
-      const float2 q = Q[s * kNb + ((j - t) & (kNb - 1))];
-      sr += q.x;
-      si += q.y;
-      const float v = sqrtf(sr * sr + si * si) / sqrtf(static_cast<float>(t + 1));
-      const int idx = t * (kNb * kNb) + s * kNb + j;
-      if (v > best || (v == best && idx < besti)) {
-        best = v;
-        besti = idx;
+  {
+    float2 rot[kNb];                          // rot[x] = Q[s][(16 q + x) mod 64]
+#pragma unroll
+    for (int x = 0; x < kNb; ++x) rot[x] = Q[s * P + ((16 * q + x) & (kNb - 1))];
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      float2 S = make_float2(0.f, 0.f);
+#pragma unroll
+      for (int t = 0; t < kNb - 1; ++t) {
+        S = cadd(S, rot[(jj - t) & (kNb - 1)]);
+        best = fmaxf(best, template_power(S, 1.0f / static_cast<float>(t + 1)));
       }
     }
   }
   red_v[tid] = best;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w) red_v[tid] = fmaxf(red_v[tid], red_v[tid + w]);
+    __syncthreads();
+  }
+  const float gbest = red_v[0];
+  int besti = 0x7fffffff;
+  if (best == gbest) {  // the (few) threads holding the maximum locate its first index
+    for (int jj = 0; jj < 16; ++jj) {
+      float2 S = make_float2(0.f, 0.f);
+      const int j = 16 * q + jj;
+      for (int t = 0; t < kNb - 1; ++t) {
+        S = cadd(S, Q[s * P + ((j - t) & (kNb - 1))]);
+        const int idx = t * (kNb * kNb) + s * kNb + j;
+        if (template_power(S, 1.0f / static_cast<float>(t + 1)) == gbest && idx < besti) besti = idx;
+      }
+    }
+  }
   red_i[tid] = besti;
   __syncthreads();
   for (int w = 128; w > 0; w >>= 1) {
-    if (tid < w) {
-      const float v2 = red_v[tid + w];
-      const int i2 = red_i[tid + w];
-      if (v2 > red_v[tid] || (v2 == red_v[tid] && i2 < red_i[tid])) {
-        red_v[tid] = v2;
-        red_i[tid] = i2;
-      }
-    }
+    if (tid < w) red_i[tid] = min(red_i[tid], red_i[tid + w]);
     __syncthreads();
   }
   const int am = red_i[0];
@@ -237,26 +260,25 @@ __global__ void __launch_bounds__(256) fold_optimise_kernel(const float* __restr
   const int opt_bin = am % kNb;
   // 5. optimal subints: Re(IDFT_b(F[i][b] * shift[s*][i][b]))[t]
   float* of = opt_fold + static_cast<uint64_t>(cand) * kNi * kNb;
-  for (int o = tid; o < kNi * kNb; o += 256) {
-    const int i = o / kNb, t = o % kNb;
-    float re = 0.f;
-    for (int b = 0; b < kNb; ++b) {
-      const float2 v = cmul(F[i * kNb + b], shift_table[(opt_shift * kNi + i) * kNb + b]);
-      const float2 w = tw[(b * t) & (kNb - 1)];
-      re += v.x * w.x - v.y * w.y;
-    }
-    of[o] = re;
+  if (tid < kNi) {
+    float2 x[kNb];
+#pragma unroll
+    for (int b = 0; b < kNb; ++b) x[b] = cmul(F[tid * P + b], shift_table[(opt_shift * kNi + tid) * kNb + b]);
+    idft<kNb>(x);
+    float4* dst = reinterpret_cast<float4*>(of + tid * kNb);
+#pragma unroll
+    for (int u = 0; u < kNb / 4; ++u) dst[u] = make_float4(x[4 * u].x, x[4 * u + 1].x, x[4 * u + 2].x, x[4 * u + 3].x);
   }
   // 6. optimal profile: Re(IDFT(prof[s*]))[j] (DC included)
   if (tid < kNb) {
-    const float2 q = Q[opt_shift * kNb + tid];
-    opt_prof[static_cast<uint64_t>(cand) * kNb + tid] = q.x + prof[opt_shift * kNb].x;
+    const float2 qv = Q[opt_shift * P + tid];
+    opt_prof[static_cast<uint64_t>(cand) * kNb + tid] = qv.x + prof[opt_shift * P].x;
   }
   if (tid == 0) {
     opt_int[3 * cand + 0] = opt_template;
     opt_int[3 * cand + 1] = opt_shift;
     opt_int[3 * cand + 2] = opt_bin;
-    opt_val[cand] = red_v[0];
+    opt_val[cand] = sqrtf(gbest);
   }
 }
 

@@ -4,6 +4,8 @@
 // multiply).  The coincidencer is split into a per-beam indicator (so beams
 // on different GPUs can be summed by an RCCL all-reduce over xGMI) and a
 // final threshold.
+#include <algorithm>
+
 #include "device_common.hpp"
 #include "psoup/kernels.hpp"
 
@@ -32,6 +34,16 @@ __global__ void __launch_bounds__(256) conjugate_kernel(float2* __restrict__ x, 
     x[i].y *= -1.0f;
 }
 
+// One launch copying up to kGatherRows scattered rows (16-byte multiples)
+// into consecutive rows of dst: blockIdx.y = row.
+__global__ void __launch_bounds__(256) gather_rows_kernel(RowPtrs src, uint64_t nvec, uint4* __restrict__ dst,
+                                                          uint64_t dst_stride_vec) {
+  const uint4* __restrict__ s = reinterpret_cast<const uint4*>(src.p[blockIdx.y]);
+  uint4* __restrict__ d = dst + blockIdx.y * dst_stride_vec;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < nvec; i += stride) d[i] = s[i];
+}
+
 __global__ void __launch_bounds__(256) cmul_kernel(const float2* __restrict__ x, float2* __restrict__ y, uint64_t n) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n; i += stride) {
@@ -55,6 +67,24 @@ void coincidence_mask(const uint8_t* counts, uint64_t n, int beam_thresh, float*
 void conjugate(float2* x, uint64_t n, hipStream_t s) {
   conjugate_kernel<<<dev::grid_for(n, 256), 256, 0, s>>>(x, n);
   post_launch_check("conjugate_kernel", s);
+}
+
+void gather_rows(const uint8_t* const* rows, int nrows, uint64_t nbytes, uint8_t* dst, uint64_t dst_stride,
+                 hipStream_t s) {
+  PSOUP_CHECK(nbytes % 16 == 0 && dst_stride % 16 == 0 && (reinterpret_cast<uintptr_t>(dst) & 15) == 0,
+              "gather_rows: 16-byte rows");
+  for (int r0 = 0; r0 < nrows; r0 += kGatherRows) {
+    RowPtrs rp{};
+    const int n = nrows - r0 < kGatherRows ? nrows - r0 : kGatherRows;
+    for (int i = 0; i < n; ++i) {
+      PSOUP_CHECK((reinterpret_cast<uintptr_t>(rows[r0 + i]) & 15) == 0, "gather_rows: row alignment");
+      rp.p[i] = rows[r0 + i];
+    }
+    const uint64_t nvec = nbytes / 16;
+    const dim3 grid(static_cast<unsigned>(std::min<uint64_t>((nvec + 255) / 256, 256)), static_cast<unsigned>(n));
+    gather_rows_kernel<<<grid, 256, 0, s>>>(rp, nvec, reinterpret_cast<uint4*>(dst + r0 * dst_stride), dst_stride / 16);
+    post_launch_check("gather_rows_kernel", s);
+  }
 }
 
 void cmul_inplace(const float2* x, float2* y, uint64_t n, hipStream_t s) {

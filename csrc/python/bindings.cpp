@@ -255,6 +255,13 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("fold", &Candidate::fold)
       .def_readwrite("nbins", &Candidate::nbins)
       .def_readwrite("nints", &Candidate::nints)
+      .def("set_fold_array",
+           [](Candidate& c, py::array_t<float, py::array::c_style | py::array::forcecast> a, int nbins, int nints) {
+             c.fold.assign(a.data(), a.data() + a.size());  // one copy, no per-element conversion
+             c.nbins = nbins;
+             c.nints = nints;
+           },
+           py::arg("fold"), py::arg("nbins") = 64, py::arg("nints") = 16)
       .def("count_assoc", &Candidate::count_assoc)
       .def("print", &Candidate::print)
       .def("pods", [](const Candidate& c) {
@@ -815,6 +822,14 @@ PYBIND11_MODULE(_C, m) {
         return f.fold_trials(P<const uint8_t>(trials), row_stride, nsamps, static_cast<int>(periods.size()), periods,
                              accs);
       })
+      .def("fold_rows", [](FoldEngine& f, const std::vector<uintptr_t>& rows, uint64_t nsamps,
+                           const std::vector<std::vector<double>>& periods,
+                           const std::vector<std::vector<float>>& accs) {
+        std::vector<const uint8_t*> r;
+        for (uintptr_t v : rows) r.push_back(P<const uint8_t>(v));
+        return f.fold_rows(r, nsamps, periods, accs);
+      })
+      .def("reserve", &FoldEngine::reserve, py::arg("njobs_hint"))
       .def_property_readonly("max_batch", &FoldEngine::max_batch)
       .def("fold_series", [](FoldEngine& f, uintptr_t series, const std::vector<double>& periods,
                              const std::vector<float>& accs) { return f.fold_series(P<const float>(series), periods, accs); },

@@ -512,6 +512,10 @@ uint64_t Whitener::batch_bytes_per_trial() const {
          3 * (nbins() / 5 + 1) * 4 + 2 * 1024 * 8;
 }
 
+void Whitener::reserve_batch(int count) {
+  if (f4_) ensure_batch(count);
+}
+
 void Whitener::ensure_batch(int count) {
   if (count <= bcap_) return;
   y4_.resize(g4_.ystride * count);
@@ -719,6 +723,7 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   if (const char* e = std::getenv("PSOUP_GPU_CLUSTER")) gpu_cluster_ = std::atoi(e) != 0;
   grow_capacity(cap_);
   int ht = p_.host_threads;
+  if (const char* e = std::getenv("PSOUP_HOST_THREADS")) ht = std::atoi(e);
   if (ht < 0) ht = static_cast<int>(std::min(4u, std::max(1u, std::thread::hardware_concurrency() / 4)));
   if (ht > 1) pool_ = std::make_unique<HostPool>(ht - 1);
 }
@@ -1284,6 +1289,48 @@ std::vector<std::vector<FoldResult>> FoldEngine::fold_trials(const uint8_t* d_tr
         out[static_cast<size_t>(t0 + t)].push_back(std::move(r[k++]));
   }
   return out;
+}
+
+std::vector<std::vector<FoldResult>> FoldEngine::fold_rows(const std::vector<const uint8_t*>& rows,
+                                                           uint64_t trial_nsamps,
+                                                           const std::vector<std::vector<double>>& periods,
+                                                           const std::vector<std::vector<float>>& accs) {
+  const int ntrials = static_cast<int>(rows.size());
+  PSOUP_CHECK(static_cast<int>(periods.size()) == ntrials && static_cast<int>(accs.size()) == ntrials,
+              "fold_rows: one candidate list per row");
+  const uint64_t rstride = (trial_nsamps + 255) / 256 * 256;
+  std::vector<std::vector<FoldResult>> out;
+  out.reserve(static_cast<size_t>(ntrials));
+  for (int t0 = 0; t0 < ntrials; t0 += max_batch_) {
+    const int cnt = std::min(max_batch_, ntrials - t0);
+    gathered_.resize(rstride * static_cast<uint64_t>(max_batch_));
+    kern::gather_rows(rows.data() + t0, cnt, rstride, gathered_.data(), rstride, stream_);
+    std::vector<std::vector<double>> p(periods.begin() + t0, periods.begin() + t0 + cnt);
+    std::vector<std::vector<float>> a(accs.begin() + t0, accs.begin() + t0 + cnt);
+    auto r = fold_trials(gathered_.data(), rstride, trial_nsamps, cnt, p, a);
+    for (auto& x : r) out.push_back(std::move(x));
+  }
+  return out;
+}
+
+void FoldEngine::reserve(int njobs_hint) {
+  const int b = max_batch_;
+  wh_->reserve_batch(b);
+  tim_.resize(static_cast<uint64_t>(b) * n_);
+  bstats_.resize(4 * static_cast<uint64_t>(b));
+  const uint64_t nj = static_cast<uint64_t>(std::max(1, njobs_hint));
+  const uint64_t nps = n_ / kNints;
+  const uint64_t nchunk = (nps + chunk_ - 1) / chunk_;
+  const uint64_t nfold = nj * kNints * kNbins;
+  jobs_.resize(nj);
+  psum_.resize(nfold * nchunk);
+  pcount_.resize(nfold * nchunk);
+  folds_.resize(nfold);
+  opt_fold_.resize(nfold);
+  opt_prof_.resize(nj * kNbins);
+  opt_int_.resize(nj * 3);
+  opt_val_.resize(nj);
+  PSOUP_HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
 std::vector<FoldResult> FoldEngine::fold_series(const float* d_series, const std::vector<double>& periods,

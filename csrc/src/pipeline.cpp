@@ -195,6 +195,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     std::unique_ptr<Dedisperser> dd;
     std::vector<std::unique_ptr<Stream>> estreams;       // engines 1.. (engine 0 uses `stream`)
     std::vector<std::unique_ptr<SearchEngine>> engines;  // built with the resident data, outside the search timer
+    std::unique_ptr<FoldEngine> fe;                       // --npdmp > 0: buffers allocated up front
   };
   std::vector<DevState> devs(static_cast<size_t>(ngpu));
 
@@ -232,6 +233,11 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
             ds.engines.push_back(std::make_unique<SearchEngine>(
                 setup.search, e > 0 ? ds.estreams.back()->get() : ds.stream->get()));
           }
+          if (args.npdmp > 0 && prev_power_of_two(geom.out_nsamps) >= 1024) {
+            ds.fe = std::make_unique<FoldEngine>(prev_power_of_two(geom.out_nsamps), static_cast<float>(geom.tsamp),
+                                                 ds.stream->get());
+            ds.fe->reserve(args.npdmp);
+          }
           PSOUP_HIP_CHECK(hipStreamSynchronize(ds.stream->get()));
           wl.stop();
           std::lock_guard<std::mutex> lk(sh.mu);
@@ -255,6 +261,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     int d0 = 0, d1 = 0;
     bool resumed = false;
     int pending = 0;
+    const uint8_t* rows = nullptr;  // the chunk's dedispersed rows (row d at rows + (d - d0) * rstride)
     CandidateList cands;
   };
   struct DevSched {
@@ -273,14 +280,35 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   };
   std::vector<std::unique_ptr<DevSched>> scheds;
   const uint64_t rstride = Dedisperser::row_stride(geom.out_nsamps);
+  // Kept trials: each device dedisperses its chunks straight into a
+  // DM-indexed store (row d at d * rstride) that outlives the search, so the
+  // fold stage reads the rows instead of dedispersing them again (the
+  // reference keeps its DispersionTrials in host memory for the folder).
+  // On when folding is requested and the whole DM list fits in a quarter of
+  // the free HBM of every device (PSOUP_KEEP_TRIALS=0/1 forces it).
+  bool keep = args.npdmp > 0;
+  {
+    const uint64_t need = rstride * static_cast<uint64_t>(sh.ndm);
+    for (int d = 0; d < ngpu && keep; ++d) {
+      PSOUP_HIP_CHECK(hipSetDevice(hip_dev(d)));
+      size_t free_b = 0, total_b = 0;
+      PSOUP_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
+      keep = need <= free_b / 4;
+    }
+    if (const char* e = std::getenv("PSOUP_KEEP_TRIALS")) keep = std::atoi(e) != 0;
+  }
+  std::vector<std::unique_ptr<DeviceBuffer<uint8_t>>> kept(static_cast<size_t>(ngpu));
+  std::vector<int> row_owner(static_cast<size_t>(sh.ndm), -1);  // written by the feeders, disjoint chunks
   for (int d = 0; d < ngpu; ++d) {
     PSOUP_HIP_CHECK(hipSetDevice(hip_dev(d)));
     auto sc = std::make_unique<DevSched>();
     sc->dstream = std::make_unique<Stream>();
     for (int k = 0; k < 2; ++k) {
-      sc->trials[k] = std::make_unique<DeviceBuffer<uint8_t>>(rstride * static_cast<uint64_t>(sh.chunk));
+      if (!keep) sc->trials[k] = std::make_unique<DeviceBuffer<uint8_t>>(rstride * static_cast<uint64_t>(sh.chunk));
       for (int e = 0; e < neng; ++e) sc->freed[k].push_back(std::make_unique<Event>());
     }
+    if (keep) kept[static_cast<size_t>(d)] = std::make_unique<DeviceBuffer<uint8_t>>(rstride * static_cast<uint64_t>(sh.ndm));
+    sh.dev_stats[static_cast<size_t>(d)]["kept_trials"] = keep ? 1.0 : 0.0;
     scheds.push_back(std::move(sc));
   }
   auto fail = [&](int dev) {
@@ -326,12 +354,17 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
             log_info("checkpoint spill " + ck + " is " + spill_status_name(st) + "; recomputing DMs [" +
                      std::to_string(d0) + "," + std::to_string(d1) + ")");
           p.cands.clear();
-          if (sc.used[k])
+          uint8_t* rows = keep ? kept[static_cast<size_t>(dev)]->data() + static_cast<uint64_t>(d0) * rstride
+                               : sc.trials[k]->data();
+          if (sc.used[k] && !keep)
             for (auto& ev : sc.freed[k]) PSOUP_HIP_CHECK(hipStreamWaitEvent(dst, ev->get(), 0));
           sc.began[k].record(dst);
-          ds.dd->run(d0, d1, sc.trials[k]->data(), rstride, setup.dedisp_kernel, dst);
+          ds.dd->run(d0, d1, rows, rstride, setup.dedisp_kernel, dst);
           sc.ready[k].record(dst);
           sc.used[k] = true;
+          p.rows = rows;
+          if (keep)
+            for (int d = d0; d < d1; ++d) row_owner[static_cast<size_t>(d)] = dev;
         }
         {
           std::lock_guard<std::mutex> lk(sc.mu);
@@ -375,7 +408,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
             const int before = sc.processed.fetch_add(cnt);
             if (args.fault_after_dms >= 0 && before + cnt > args.fault_after_dms)
               PSOUP_THROW("fault injection: device " << dev << " aborting after " << before << " DM trials");
-            engine.prepare(sc.trials[k]->data() + static_cast<uint64_t>(rows[r0] - p.d0) * rstride,
+            engine.prepare(p.rows + static_cast<uint64_t>(rows[r0] - p.d0) * rstride,
                            static_cast<uint64_t>(neng) * rstride, geom.out_nsamps, cnt);
             std::vector<SearchEngine::Job> jobs;
             for (int i = 0; i < cnt; ++i) {
@@ -482,21 +515,41 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
           PSOUP_HIP_CHECK(hipSetDevice(hip_dev(dev)));
           DevState& ds = devs[static_cast<size_t>(dev)];
           hipStream_t st = ds.stream->get();
-          FoldEngine fe(fold_n, static_cast<float>(geom.tsamp), st);
+          if (!ds.fe) ds.fe = std::make_unique<FoldEngine>(fold_n, static_cast<float>(geom.tsamp), st);
+          FoldEngine& fe = *ds.fe;
           const uint64_t rstride = Dedisperser::row_stride(geom.out_nsamps);
           // this worker's DM groups, batched: every DM of a batch dedispersed
           // into one buffer (no host waits), then whitened and folded together
+          // the device holding a DM's kept row folds it; DMs nobody kept
+          // (resumed from a checkpoint, or keep off) go round-robin
           std::vector<size_t> mine;
-          for (size_t g = static_cast<size_t>(dev); g < glist.size(); g += static_cast<size_t>(ngpu)) mine.push_back(g);
+          size_t nrest = 0;
+          for (size_t g = 0; g < glist.size(); ++g) {
+            const int own = row_owner[static_cast<size_t>(glist[g].first)];
+            if (own >= 0) {
+              if (own == dev) mine.push_back(g);
+            } else if (nrest++ % static_cast<size_t>(ngpu) == static_cast<size_t>(dev)) {
+              mine.push_back(g);
+            }
+          }
           const int B = fe.max_batch();
-          DeviceBuffer<uint8_t> trials(rstride * static_cast<uint64_t>(std::max<size_t>(1, std::min<size_t>(mine.size(), B))));
+          DeviceBuffer<uint8_t> trials;  // dedispersion target of batches with rows nobody kept
           for (size_t b0 = 0; b0 < mine.size(); b0 += static_cast<size_t>(B)) {
             const size_t cnt = std::min<size_t>(static_cast<size_t>(B), mine.size() - b0);
             std::vector<std::vector<double>> periods(cnt);
             std::vector<std::vector<float>> accs(cnt);
             std::vector<int> dms(cnt);
             for (size_t t = 0; t < cnt; ++t) dms[t] = glist[mine[b0 + t]].first;
-            ds.dd->run_list(dms, trials.data(), rstride, st);  // one launch for the batch's DMs
+            bool all_kept = true;
+            for (size_t t = 0; t < cnt; ++t) all_kept = all_kept && row_owner[static_cast<size_t>(dms[t])] == dev;
+            std::vector<const uint8_t*> kept_rows;
+            if (all_kept)  // rows kept from the search: gathered by the folder, no dedispersion
+              for (size_t t = 0; t < cnt; ++t)
+                kept_rows.push_back(kept[static_cast<size_t>(dev)]->data() + static_cast<uint64_t>(dms[t]) * rstride);
+            else {
+              trials.resize(rstride * static_cast<uint64_t>(B));
+              ds.dd->run_list(dms, trials.data(), rstride, st);  // one launch for the batch's DMs
+            }
             for (size_t t = 0; t < cnt; ++t) {
               const auto& grp = glist[mine[b0 + t]];
               for (int ci : grp.second) {
@@ -504,7 +557,9 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
                 accs[t].push_back(cands[ci].acc);
               }
             }
-            auto fr = fe.fold_trials(trials.data(), rstride, geom.out_nsamps, static_cast<int>(cnt), periods, accs);
+            auto fr = all_kept ? fe.fold_rows(kept_rows, geom.out_nsamps, periods, accs)
+                               : fe.fold_trials(trials.data(), rstride, geom.out_nsamps, static_cast<int>(cnt), periods,
+                                                accs);
             for (size_t t = 0; t < cnt; ++t) {
               const auto& grp = glist[mine[b0 + t]];
               for (size_t k = 0; k < fr[t].size(); ++k) {

@@ -137,6 +137,13 @@ class RankSearcher:
         self._pool = None
         self._trials: Optional[torch.Tensor] = None
         self._fold_engine = None
+        # keep_trials: every searched block's dedispersed rows stay in HBM
+        # ({d0: (d1, rows)}) so the fold stage reads them instead of running the
+        # dedispersion again (the reference keeps its DispersionTrials in host
+        # memory for the folder, pipeline_multi.cu:372-386); run_search turns
+        # it on when the rank's DMs fit in a quarter of the free HBM
+        self.keep_trials = False
+        self.resident_rows: Dict[int, tuple] = {}
 
     def load_packed(self, packed: torch.Tensor) -> None:
         if packed.is_cuda:
@@ -238,18 +245,25 @@ class RankSearcher:
                     warnings.warn(f"checkpoint spill {ck} is {status}; recomputing DMs {(d0, d1)}")
             k = nissued[0] % 2
             nissued[0] += 1
-            if k >= len(bufs):
-                bufs.append(torch.empty(width * self.row_stride, dtype=torch.uint8, device=dev))
             start, ready = _C.GpuEvent(True), _C.GpuEvent(True)
-            for ev in freed[k] or ():
-                ev.wait(side.handle)
+            if self.keep_trials:
+                # a fresh buffer per block, kept for the fold stage (never reused
+                # during the search, so no wait on the previous user)
+                buf = torch.empty((d1 - d0) * self.row_stride, dtype=torch.uint8, device=dev)
+                self.resident_rows[d0] = (d1, buf)
+            else:
+                if k >= len(bufs):
+                    bufs.append(torch.empty(width * self.row_stride, dtype=torch.uint8, device=dev))
+                buf = bufs[k]
+                for ev in freed[k] or ():
+                    ev.wait(side.handle)
             start.record(side.handle)
             with roctx_range("Dedisperse"):
-                self.dedisperser.run(d0, d1, bufs[k].data_ptr(), self.row_stride, self.kernel, side.handle)
+                self.dedisperser.run(d0, d1, buf.data_ptr(), self.row_stride, self.kernel, side.handle)
             ready.record(side.handle)
             if _SYNC_DEDISP:
                 ready.synchronize()
-            return j, ck, None, (k, ready, start)
+            return j, ck, None, (k, buf, ready, start)
 
         dd_events = []
         lock = threading.Lock()
@@ -268,7 +282,7 @@ class RankSearcher:
                     progress(d1 - d0)
                 cur = pull()
                 continue
-            k, ready, start = inflight
+            k, buf, ready, start = inflight
             nxt = pull()  # its dedispersion overlaps the search below
             for e in self.engines:
                 ready.wait(e.stream)
@@ -288,7 +302,7 @@ class RankSearcher:
                             raise RuntimeError(f"fault injection: rank {self.ctx.rank} aborting after "
                                                f"{processed} DM trials")
                         processed += len(part)
-                    e.prepare(bufs[k].data_ptr() + (part[0] - d0) * self.row_stride, step * self.row_stride,
+                    e.prepare(buf.data_ptr() + (part[0] - d0) * self.row_stride, step * self.row_stride,
                               self.geom.out_nsamps, len(part))
                     jobs = [(b, self.dm_list[d], d, self.accel_list(self.dm_list[d])) for b, d in enumerate(part)]
                     # one flat trial list over the part's DMs (batches span DM boundaries)
@@ -315,7 +329,8 @@ class RankSearcher:
                 ev = _C.GpuEvent()
                 ev.record(e.stream)
                 evs.append(ev)
-            freed[k] = evs
+            if not self.keep_trials:
+                freed[k] = evs
             if ck:
                 _C.save_spill(ck, ckey, chunk_cands)  # atomic; raises on a failed write
             cands.extend(chunk_cands)
@@ -360,6 +375,27 @@ class RankSearcher:
         self.blocks_done = []
         return cands
 
+    def fold_engine(self, njobs_hint: int = 0):
+        """The searcher's FoldEngine (whitener, shift table, buffers), built on
+        first use; ``njobs_hint`` > 0 also allocates a full batch's buffers
+        (run_search does this before the search, outside the fold stage)."""
+        if self._fold_engine is None:
+            n = _C.prev_power_of_two(self.geom.out_nsamps)
+            self._fold_engine = _C.FoldEngine(n, float(self.header["tsamp"]), self.stream)
+        if njobs_hint > 0:
+            self._fold_engine.reserve(njobs_hint)
+        return self._fold_engine
+
+    def resident_row(self, d: int) -> Optional[torch.Tensor]:
+        """DM ``d``'s dedispersed row kept from the search (keep_trials), or None."""
+        for d0, (d1, buf) in self.resident_rows.items():
+            if d0 <= d < d1:
+                return buf[(d - d0) * self.row_stride:(d - d0 + 1) * self.row_stride]
+        return None
+
+    def resident_dms(self) -> List[int]:
+        return sorted(d for d0, (d1, _) in self.resident_rows.items() for d in range(d0, d1))
+
     def _executor(self):
         if self._pool is None:
             self._pool = concurrent.futures.ThreadPoolExecutor(len(self.engines), thread_name_prefix="psoup-eng")
@@ -381,15 +417,28 @@ class RankSearcher:
         out: Dict[int, tuple] = {}
         if not groups:
             return out
-        if self._fold_engine is None:  # one engine (whitener, shift table, buffers) per searcher
-            n = _C.prev_power_of_two(self.geom.out_nsamps)
-            self._fold_engine = _C.FoldEngine(n, float(self.header["tsamp"]), self.stream)
-        fe = self._fold_engine
+        fe = self.fold_engine()
         items = sorted(groups.items())
         B = int(fe.max_batch)
         t_dd = t_fe = 0.0
+        n_kept = 0
         for b0 in range(0, len(items), B):
             batch = items[b0:b0 + B]
+            periods = [[float(struct.unpack("f", struct.pack("f", 1.0 / cands[i].freq))[0]) for i in members]
+                       for _, members in batch]
+            accs = [[cands[i].acc for i in members] for _, members in batch]
+            kept = [self.resident_row(d) for d, _ in batch] if rows is None and self.resident_rows else []
+            if kept and all(r is not None for r in kept):
+                # rows kept from the search: gathered on the device by one
+                # kernel, whitened and folded (no dedispersion, no host wait)
+                t0 = time.perf_counter()
+                res = fe.fold_rows([r.data_ptr() for r in kept], self.geom.out_nsamps, periods, accs)
+                t_fe += time.perf_counter() - t0
+                n_kept += len(batch)
+                for (_, members), rr in zip(batch, res):
+                    for i, r in zip(members, rr):
+                        out[i] = (r.folded_snr, r.opt_period, r.fold_array)
+                continue
             # every DM of the batch dedispersed into one buffer, then whitened
             # and folded together (one accumulate / optimise launch)
             buf = torch.empty(len(batch) * self.row_stride, dtype=torch.uint8, device=self.ctx.device)
@@ -401,11 +450,8 @@ class RankSearcher:
             else:  # one launch for the batch's (scattered) DMs
                 t0 = time.perf_counter()
                 self.dedisperser.run_list([d for d, _ in batch], buf.data_ptr(), self.row_stride, self.stream)
-                torch.cuda.current_stream(self.ctx.device).synchronize()
+                _C.stream_synchronize(self.stream)  # (GPU time of the dedispersion included)
                 t_dd += time.perf_counter() - t0
-            periods = [[float(struct.unpack("f", struct.pack("f", 1.0 / cands[i].freq))[0]) for i in members]
-                       for _, members in batch]
-            accs = [[cands[i].acc for i in members] for _, members in batch]
             t0 = time.perf_counter()
             res = fe.fold_trials(buf.data_ptr(), self.row_stride, self.geom.out_nsamps, periods, accs)
             t_fe += time.perf_counter() - t0
@@ -413,7 +459,7 @@ class RankSearcher:
                 for i, r in zip(members, rr):
                     out[i] = (r.folded_snr, r.opt_period, r.fold_array)
         self.fold_stats = {"fold_dedisp_s": t_dd, "fold_engine_s": t_fe, "fold_dms": len(items),
-                           "fold_batches": (len(items) + B - 1) // B}
+                           "fold_batches": (len(items) + B - 1) // B, "fold_rows_kept": n_kept}
         return out
 
 
@@ -433,7 +479,7 @@ def _decode_fold_results(b: bytes) -> Dict[int, tuple]:
     for _ in range(n):
         i, snr, per, nf = struct.unpack_from("<ifdi", b, off)
         off += struct.calcsize("<ifdi")
-        fold = np.frombuffer(b, dtype="<f4", count=nf, offset=off).tolist()
+        fold = np.frombuffer(b, dtype="<f4", count=nf, offset=off)
         off += 4 * nf
         out[i] = (snr, per, fold)
     return out
@@ -504,6 +550,35 @@ def dm_schedule(args, world_size: int, ndm: Optional[int] = None) -> str:
     return s
 
 
+def keep_trials_fits(rs: RankSearcher, ndm: int, world: int) -> bool:
+    """Keep every searched DM row in HBM for the fold stage when this rank's
+    share (with 2x slack for dynamic-schedule imbalance) fits in a quarter of
+    the free device memory.  PSOUP_KEEP_TRIALS=0/1 forces it."""
+    env = os.environ.get("PSOUP_KEEP_TRIALS")
+    if env is not None:
+        return env not in ("0", "")
+    if rs.ctx.device.type != "cuda":
+        return False
+    free, _ = torch.cuda.mem_get_info(rs.ctx.device)
+    share = (ndm + world - 1) // world * (2 if world > 1 else 1)
+    return share * rs.row_stride <= free // 4
+
+
+def fold_owners(rs: RankSearcher, ctx) -> Dict[int, int]:
+    """DM index -> the rank that kept its dedispersed row (all ranks agree:
+    every rank's kept ranges are all-gathered)."""
+    mine = [(d0, d1) for d0, (d1, _) in sorted(rs.resident_rows.items())]
+    if ctx.world_size == 1:
+        return {d: 0 for d0, d1 in mine for d in range(d0, d1)}
+    blobs = pdist.gather_bytes(json.dumps(mine).encode(), dst=None)
+    owner: Dict[int, int] = {}
+    for r, b in enumerate(blobs):
+        for d0, d1 in json.loads(b.decode()):
+            for d in range(d0, d1):
+                owner.setdefault(d, r)
+    return owner
+
+
 def run_search(args, write: bool = True) -> Optional[SearchResult]:
     """Full distributed search (torchrun: one rank per GPU).  Returns the
     result on rank 0 (None elsewhere)."""
@@ -526,6 +601,10 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     schedule = "time_sharded" if sharded else dm_schedule(args, ctx.world_size, ndm)
     rows = None
     row_first = 0
+    if not sharded and args.npdmp > 0:
+        rs.keep_trials = keep_trials_fits(rs, ndm, ctx.world_size)
+    if args.npdmp > 0 and _C.prev_power_of_two(rs.geom.out_nsamps) >= 1024:
+        rs.fold_engine(njobs_hint=args.npdmp)  # folder buffers allocated with the rest of the setup
     pdist.barrier()
     t0 = time.perf_counter()
     if sharded:
@@ -602,20 +681,25 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
         if rows is not None:  # time-sharded: the owner of the DM row folds it
             mine = {k: groups[k] for k in keys if row_first <= k < row_first + rows.shape[0]}
         else:
-            mine = {k: groups[k] for j, k in enumerate(keys) if j % ctx.world_size == ctx.rank}
+            # the rank holding a DM's dedispersed row (keep_trials) folds it;
+            # DMs nobody kept (resumed blocks) go round-robin
+            owner = fold_owners(rs, ctx)
+            rest = [k for k in keys if k not in owner]
+            mine = {k: groups[k] for k in keys if owner.get(k) == ctx.rank}
+            mine.update({k: groups[k] for j, k in enumerate(rest) if j % ctx.world_size == ctx.rank})
         t_f0 = time.perf_counter()
         res = rs.fold(mine, cands, rows=rows, dm_first=row_first)
         t_f1 = time.perf_counter()
-        parts = pdist.gather_bytes(_encode_fold_results(res), dst=0)
+        # one rank: the results as they are; more: encoded and gathered to rank 0
+        parts = [res] if ctx.world_size == 1 else [
+            _decode_fold_results(p) for p in pdist.gather_bytes(_encode_fold_results(res), dst=0) or []]
         if ctx.is_root:
-            for p in parts:
-                for i, (snr, per, fold) in _decode_fold_results(p).items():
+            for part in parts:
+                for i, (snr, per, fold) in part.items():
                     c = cands[i]
                     c.folded_snr = snr
                     c.opt_period = per
-                    c.fold = fold
-                    c.nbins, c.nints = 64, 16
-                    cands[i] = c
+                    c.set_fold_array(fold, 64, 16)
             # sort_by_folded_snr's permutation, applied to the Python list
             order = _C.sort_order_by_folded_snr([c.snr for c in cands], [c.folded_snr for c in cands])
             cands = [cands[i] for i in order]

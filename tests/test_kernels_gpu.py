@@ -294,7 +294,8 @@ def test_r2c_interbin_normalise_batch():
         assert np.allclose(P[k], exp, rtol=1e-4, atol=2e-3), np.abs(P[k] - exp).max()
 
 
-FFT4_FLAG_SETS = [None, 0, 1, 259, 274, 1299, 3331, 7427, 15619, 32003, 48387, 81155, 474371, 736515, 1260803]  # None = default (212227: tiled Y and X + uniform pass-A twiddles + one-exchange pass A at column length 2048); 81155 = the Stockham pass A; 32003 = + Sub2; 474371 = + whole-CU exchange; 736515 = + one-exchange pass B; 1260803 = one-exchange pass A at column lengths 512/1024 too
+FFT4_FLAG_SETS = [None, 0, 1, 259, 274, 1299, 3331, 7427, 15619, 32003, 48387, 81155, 474371, 736515, 1260803,
+                  212227, 1074216195, 1075002627]  # 1074216195 / 1075002627 = whole-CU / small-length one-exchange sets with the strip-layout input (kFft4StripInput); None = default (1073954051: tiled Y and X + uniform pass-A twiddles + one-exchange pass A at column length 2048 + strip input); 212227 = the same with the row-pitch input; 81155 = the Stockham pass A; 32003 = + Sub2; 474371 = + whole-CU exchange; 736515 = + one-exchange pass B; 1260803 = one-exchange pass A at column lengths 512/1024 too
 
 
 @pytest.fixture(params=FFT4_FLAG_SETS)
@@ -313,7 +314,7 @@ def test_fft4_resample_spectrum_matches_numpy(log2n, fft4_flags):
     """Fused resample + four-step FFT vs (bit-exact GPU resample) + numpy fp64 FFT."""
     from peasoup_amd import ops
 
-    if log2n >= 23 and fft4_flags not in (None, 81155, 474371, 736515):
+    if log2n >= 23 and fft4_flags not in (None, 212227, 81155, 474371, 736515, 1074216195):
         pytest.skip("2^23 and 2^25 checked with the default kernel shape (and the one-exchange pass A) only")
 
     rng = np.random.default_rng(log2n)

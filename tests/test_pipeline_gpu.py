@@ -60,6 +60,39 @@ def test_python_run_search_golden(C, tmp_path):
     _compare_with_golden(str(tmp_path))
 
 
+def test_fold_from_kept_rows_equals_redispersed(C, tmp_path, monkeypatch):
+    """keep_trials: folding the search's resident dedispersed rows gives the
+    candidate file byte for byte of re-running the dedispersion for the fold."""
+    from peasoup_amd.models.search import run_search
+
+    outs, stats = [], []
+    for keep in ("0", "1"):
+        monkeypatch.setenv("PSOUP_KEEP_TRIALS", keep)
+        d = tmp_path / f"keep{keep}"
+        ok, _, args = C.parse_cmdline(["peasoup", "-i", TUTORIAL, "-o", str(d)] + GOLDEN_ARGS)
+        res = run_search(args)
+        outs.append(open(d / "candidates.peasoup", "rb").read())
+        stats.append(res.fold_stats)
+    assert outs[0] == outs[1]
+    assert stats[0]["fold_rows_kept"] == 0 and stats[1]["fold_rows_kept"] == stats[1]["fold_dms"] > 0
+
+
+def test_native_fold_from_kept_rows_equals_redispersed(tmp_path):
+    """bin/peasoup: the kept-trials fold (rows read from the search's DM store)
+    writes the same candidate file as dedispersing the fold DMs again, on one
+    device worker and on three oversubscribed ones (fold owners differ)."""
+    exe = os.path.join(REPO, "bin", "peasoup")
+    outs = []
+    for keep, extra, env_extra in (("0", [], {}), ("1", [], {}), ("1", ["-t", "3"], {"PSOUP_OVERSUBSCRIBE": "1"})):
+        d = tmp_path / f"k{keep}{len(extra)}"
+        env = dict(os.environ, PSOUP_KEEP_TRIALS=keep, **env_extra)
+        r = subprocess.run([exe, "-i", TUTORIAL, "-o", str(d)] + GOLDEN_ARGS + extra, capture_output=True, text=True,
+                           timeout=600, env=env)
+        assert r.returncode == 0, r.stderr
+        outs.append(open(d / "candidates.peasoup", "rb").read())
+    assert outs[0] == outs[1] == outs[2]
+
+
 def test_direct_and_mfma_dedispersion_give_identical_search(C, tmp_path):
     outs = []
     for k in ("direct", "mfma"):

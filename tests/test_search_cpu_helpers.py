@@ -83,3 +83,29 @@ def test_sort_order_by_folded_snr_is_the_sort_permutation():
         ref = [c.freq for c in _C.sort_by_folded_snr(cands)]
         order = _C.sort_order_by_folded_snr([c.snr for c in cands], [c.folded_snr for c in cands])
         assert [cands[i].freq for i in order] == ref
+
+
+def test_resident_rows_lookup_and_fold_owners(monkeypatch):
+    """keep_trials bookkeeping: row lookup inside kept blocks, the owner map of
+    a single rank, and the PSOUP_KEEP_TRIALS override of the memory rule."""
+    import types
+
+    import torch
+
+    from peasoup_amd.models import search as S
+
+    rs = types.SimpleNamespace(row_stride=4, resident_rows={}, ctx=types.SimpleNamespace(device=torch.device("cpu")))
+    rs.resident_rows[0] = (3, torch.arange(12, dtype=torch.uint8))
+    rs.resident_rows[32] = (34, torch.arange(100, 108, dtype=torch.uint8))
+    row = S.RankSearcher.resident_row(rs, 2)
+    assert row.tolist() == [8, 9, 10, 11]
+    assert S.RankSearcher.resident_row(rs, 33).tolist() == [104, 105, 106, 107]
+    assert S.RankSearcher.resident_row(rs, 3) is None and S.RankSearcher.resident_row(rs, 31) is None
+    assert S.RankSearcher.resident_dms(rs) == [0, 1, 2, 32, 33]
+    ctx = types.SimpleNamespace(world_size=1, rank=0)
+    assert S.fold_owners(rs, ctx) == {0: 0, 1: 0, 2: 0, 32: 0, 33: 0}
+    assert S.keep_trials_fits(rs, 100, 1) is False  # no GPU: never kept
+    monkeypatch.setenv("PSOUP_KEEP_TRIALS", "1")
+    assert S.keep_trials_fits(rs, 100, 1) is True
+    monkeypatch.setenv("PSOUP_KEEP_TRIALS", "0")
+    assert S.keep_trials_fits(rs, 100, 1) is False

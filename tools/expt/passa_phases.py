@@ -55,6 +55,7 @@ def main():
                         ("loads only", SKIP_COMPUTE | SKIP_STORE), ("stores only", SKIP_COMPUTE | SKIP_LOAD),
                         ("compute only", SKIP_LOAD | SKIP_STORE))[: 1 if a.only_full else 7]:
             K_.fft4_set_flags(base | extra | f)
+            K_.fft4_pad_input(x.data_ptr(), n, xp.data_ptr(), g, s)  # the input layout follows the flags
             t = timeit(lambda: K_.fft4_resample_colpass(x.data_ptr(), xp.data_ptr(), n, af.data_ptr(), K, Y.data_ptr(),
                                                         g, tab.data_ptr(), s), a.reps)
             print(f"extra={extra:<8d} {name:14s} {t:9.1f} us/launch {t / K:7.2f} us/trial", flush=True)
