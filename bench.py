@@ -50,9 +50,9 @@ def parse():
     p.add_argument("--acc", type=float, default=500.0, help="search +-acc m/s^2")
     p.add_argument("--nharmonics", type=int, default=3)
     p.add_argument("--accel-batch", type=int, default=0,
-                   help="acceleration trials per batch (0 = auto: 256 at 2^23 within a 24 GiB budget, capped by free memory)")
+                   help="acceleration trials per batch (0 = auto: 512 at 2^23 within a 48 GiB budget, capped by free memory)")
     p.add_argument("--sub-batch", type=int, default=-1,
-                   help="trials per sub-batch on two alternating streams (0 = off, -1 = auto: half a batch, at most 2^28 samples)")
+                   help="trials per sub-batch on two alternating streams (0 = off, -1 = auto: off from 2^22 samples, else half a batch, at most 2^28 samples)")
     p.add_argument("--fft-mode", type=int, default=2,
                    help="2: fused resample + four-step FFT; 1: rocFFT C2C(N/2) + fused r2c post; 0: rocFFT R2C")
     p.add_argument("--dedisp-kernel", default="auto", choices=["auto", "mfma", "valu", "direct"])

@@ -139,17 +139,17 @@ struct SearchParams {
   int accel_batch = 0;          // 0 = auto
   int sub_batch = -1;           // fused-FFT trials per sub-batch on alternating streams (0 = off, -1 = auto)
   int host_threads = -1;        // host workers clustering/distilling peak-heavy batches (-1 = auto, 0/1 = serial)
-  // auto-batch HBM budget (256 trials of 2^23; same-box A/B vs 64: +1.8%),
-  // capped at 70% of the device's free memory shared among its engines.
-  // 512/1024-trial batches measured box-dependent (-0.9% .. +3.5%,
-  // profiles/r2_batch/)
-  size_t batch_bytes = 24ull << 30;
+  // auto-batch HBM budget (512 trials of 2^23: 43 GB of intermediates on a
+  // 288 GB device; same-box sweep without sub-batches: K = 512 22.25k/22.17k,
+  // 256 21.98k/21.97k, 128 21.65k trials/s, profiles/r3_sub/), capped at 70%
+  // of the device's free memory shared among its engines
+  size_t batch_bytes = 48ull << 30;
   // Engines sharing the device: the auto budget is also capped at 70% of the
   // device's free memory divided by this count.
   int engines_per_device = 1;
   // Auto batching of short trial lists: lists shorter than min_batches full
   // batches are cut into min_batches even batches (multiples of 8), but never
-  // below the batch a quarter of the budget gives.
+  // below the batch an eighth of the budget gives.
   int min_batches = 8;
   // Compute streams the sub-batches of a batch rotate over (>= 2; env
   // PSOUP_SUB_STREAMS overrides for A/B runs).

@@ -368,6 +368,23 @@ __global__ void __launch_bounds__(256) fft4_pad_input_kernel(const float* __rest
   }
 }
 
+// The same copy in 16-byte vectors with 32-bit indices (rowlen, pitch, n and
+// the strides multiples of 4 floats, 16-byte aligned pointers): a vector never
+// straddles a row or the series end.
+__global__ void __launch_bounds__(256) fft4_pad_input_vec_kernel(const float4* __restrict__ in, uint32_t n4,
+                                                                 float4* __restrict__ out, uint32_t rowlen4,
+                                                                 uint32_t pitch4, uint32_t total4, uint64_t in_stride4,
+                                                                 uint64_t out_stride4) {
+  in += blockIdx.y * in_stride4;
+  out += blockIdx.y * out_stride4;
+  const uint32_t stride = gridDim.x * blockDim.x;
+  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < total4; u += stride) {
+    const uint32_t row = u / pitch4, r = u - row * pitch4;
+    const uint32_t src = row * rowlen4 + r;
+    out[u] = src < n4 ? in[src] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
 // Strip layout of the padded input (kFft4StripInput, one-exchange pass A):
 // strip b holds floats [16 b, 16 b + kStripW) of every row (rows of 2*N1
 // floats; the last strip's tail is the next row's head), rows of a strip
@@ -1202,6 +1219,18 @@ void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& 
     return;
   }
   const uint64_t total = g.inpitch * g.n2;
+  const bool vec = n % 4 == 0 && g.inpitch % 4 == 0 && g.n1 % 2 == 0 && in_stride % 4 == 0 && g.insize % 4 == 0 &&
+                   (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (reinterpret_cast<uintptr_t>(in_pad) & 15) == 0 &&
+                   total / 4 < (1ull << 32) && n / 4 < (1ull << 32);
+  if (vec) {
+    const dim3 grid(dev::grid_for(total / 4, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
+    fft4_pad_input_vec_kernel<<<grid, 256, 0, s>>>(
+        reinterpret_cast<const float4*>(in), static_cast<uint32_t>(n / 4), reinterpret_cast<float4*>(in_pad),
+        static_cast<uint32_t>(g.n1 / 2), static_cast<uint32_t>(g.inpitch / 4), static_cast<uint32_t>(total / 4),
+        in_stride / 4, g.insize / 4);
+    post_launch_check("fft4_pad_input_vec_kernel", s);
+    return;
+  }
   const dim3 grid(dev::grid_for(total, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
   fft4_pad_input_kernel<<<grid, 256, 0, s>>>(in, n, in_pad, 2ull * g.n1, g.inpitch, total, in_stride, g.insize);
   post_launch_check("fft4_pad_input_kernel", s);

@@ -26,6 +26,8 @@
 // the chain (one LDS read per peak), a scan compacts the peaks in idx order.
 // Segments over kClusterCap crossings are left to the host (flagged in the
 // segment table with their raw, unsorted range).
+#include <cstdlib>
+
 #include "device_common.hpp"
 
 namespace psoup {
@@ -37,19 +39,20 @@ constexpr uint32_t kClSmall = 4096;  // segments up to this size: the small-LDS 
 constexpr int kSegLds = 8192;        // segments a batch may have for the LDS-aggregated hist/scatter
 constexpr int kRecPerThread = 16;    // records per thread in hist/scatter blocks (256 threads)
 
-// Hillis-Steele scans over one value per thread (kClThreads).
+// Hillis-Steele scans over one value per thread (TH threads).
+template <int TH = kClThreads>
 __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* sc, uint32_t* total) {
   const int t = threadIdx.x;
   sc[t] = v;
   __syncthreads();
-  for (int off = 1; off < kClThreads; off <<= 1) {
+  for (int off = 1; off < TH; off <<= 1) {
     const uint32_t a = t >= off ? sc[t - off] : 0u;
     __syncthreads();
     sc[t] += a;
     __syncthreads();
   }
   const uint32_t incl = sc[t];
-  if (total) *total = sc[kClThreads - 1];
+  if (total) *total = sc[TH - 1];
   __syncthreads();
   return incl - v;
 }
@@ -134,7 +137,7 @@ __global__ void __launch_bounds__(256) seg_scatter_kernel(const PeakRecord* __re
 // One workgroup per segment with lo_n < n <= CAP crossings (the small
 // kernel also writes the empty segments' entries, the large one the raw
 // entries of segments over its capacity).
-template <uint32_t CAP>
+template <uint32_t CAP, int kClThreads>
 __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* __restrict__ sorted,
                                                                   const uint32_t* __restrict__ segoff,
                                                                   const uint32_t* __restrict__ segcnt, int gap,
@@ -211,7 +214,7 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
     mysurv += keep ? 1u : 0u;
   }
   uint32_t totsurv;
-  block_excl_sum(mysurv, sc, &totsurv);  // (its barriers also publish flag)
+  block_excl_sum<kClThreads>(mysurv, sc, &totsurv);  // (its barriers also publish flag)
   // (3) next survivor at or after every position: rows from the last, a
   // row's waves from their ballots, the carry from the rows after it
   uint32_t carry = n;
@@ -363,11 +366,22 @@ void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint
     seg_scatter_global_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segoff, cursor, d_sorted);
     post_launch_check("seg_scatter_global_kernel", s);
   }
-  peak_cluster_kernel<kClSmall><<<nseg, kClThreads, 0, s>>>(d_sorted, segoff, segcnt, gap, 0u, d_out, d_segtab,
-                                                             d_total);
+  peak_cluster_kernel<kClSmall, kClThreads><<<nseg, kClThreads, 0, s>>>(d_sorted, segoff, segcnt, gap, 0u, d_out,
+                                                                         d_segtab, d_total);
   post_launch_check("peak_cluster_kernel<small>", s);
-  peak_cluster_kernel<kClusterCap><<<nseg, kClThreads, 0, s>>>(d_sorted, segoff, segcnt, gap, kClSmall, d_out,
+  // the large kernel holds a CU's LDS alone: 1024 threads (16 waves) hide the
+  // LDS latency of its dependent sort / scan steps (PSOUP_CLUSTER_TH=512: the
+  // previous shape)
+  static const bool th512 = [] {
+    const char* e = std::getenv("PSOUP_CLUSTER_TH");
+    return e && std::atoi(e) == 512;
+  }();
+  if (th512)
+    peak_cluster_kernel<kClusterCap, 512><<<nseg, 512, 0, s>>>(d_sorted, segoff, segcnt, gap, kClSmall, d_out,
                                                                 d_segtab, d_total);
+  else
+    peak_cluster_kernel<kClusterCap, 1024><<<nseg, 1024, 0, s>>>(d_sorted, segoff, segcnt, gap, kClSmall, d_out,
+                                                                  d_segtab, d_total);
   post_launch_check("peak_cluster_kernel<large>", s);
 }
 

@@ -684,21 +684,27 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
       budget = std::min(budget, free_b / 10 * 7 / static_cast<size_t>(std::max(1, p_.engines_per_device)));
     const size_t per = n_ * 4 + (fused_ ? pst_ * 4 : nb_ * 8) + pst_ * 4;  // Y/res + X/spec or Pb + P per trial
-    auto round_batch = [](size_t k) {
-      int K = static_cast<int>(std::min<size_t>(256, std::max<size_t>(1, k)));
+    // at most 512 trials per batch from 2^23 samples up, 256 below (the
+    // shorter series were only measured up to 256)
+    const size_t kmax = n_ >= (uint64_t(1) << 23) ? 512 : 256;
+    auto round_batch = [kmax](size_t k) {
+      int K = static_cast<int>(std::min<size_t>(kmax, std::max<size_t>(1, k)));
       if (K >= 32) K = K / 16 * 16;  // halves stay multiples of 8 (XCD-grouped kernels)
       else if (K >= 16) K = K / 8 * 8;
       return K;
     };
     K_ = p_.accel_batch > 0 ? p_.accel_batch : round_batch(budget / per);
-    k_small_ = std::min(K_, std::max(16, round_batch(budget / 4 / per)));
+    k_small_ = std::min(K_, std::max(16, round_batch(budget / 8 / per)));  // 64 at 2^23
   }
-  // Auto: sub-batches on alternating streams (+4-5% at 2^23: the tail of
-  // one sub-batch's kernels overlaps the head of the other's), half a batch
-  // but at most 2^28 samples (32 trials of 2^23: at K = 256, sub-batches of
-  // 16/32/64/128 measured 20.81k/20.84k/20.71k/20.47k trials/s same-box).
+  // Auto: sub-batches on alternating streams, half a batch but at most 2^28
+  // samples -- below 2^22 samples only.  At 2^23 they were +4-5% in round 1
+  // (20.81k at 16, 20.84k at 32 trials per sub-batch), but with the current
+  // passes one stream wins on the same box: K = 256 without sub-batches
+  // 21.98k/21.97k vs 21.0k/21.5k/21.5k/21.6k with 16/32/64/128; at 2^22
+  // 44.0k vs 42.9k; at 2^20 they still win, 81.0k vs 78.2k
+  // (profiles/r3_sub/, profiles/r3_k512/).
   int sub_auto = 0;
-  if (K_ >= 16) {
+  if (K_ >= 16 && n_ < (uint64_t(1) << 22)) {
     const int cap = static_cast<int>(std::max<uint64_t>(8, (uint64_t(1) << 28) / n_)) / 8 * 8;
     sub_auto = std::min(K_ / 2, cap);
   }
@@ -1093,8 +1099,8 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
   // Short trial lists (one DM at 2^23: 685 trials) keep at least min_batches
   // (default 8, env PSOUP_MIN_BATCHES) batches in the two-slot pipeline so
   // host clustering still overlaps the GPU, but never fall below k_small_
-  // (the batch a quarter of the budget gives: 64 at 2^23 with the default
-  // 24 GiB, rounded like K_).
+  // (the batch an eighth of the budget gives: 64 at 2^23 with the default
+  // 48 GiB, rounded like K_).
   int kc = K_;
   {
     static const int env_min_batches = [] {

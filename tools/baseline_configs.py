@@ -149,8 +149,12 @@ def config5_pulsars(n: int = 64, seed: int = 5):
 
 
 def _make_fb(a, ctx):
-    path = os.path.join(a.workdir, f"cfg45_{a.log2n}_multi.fil")
-    if ctx.is_root and not os.path.exists(path):
+    path = os.path.join(a.workdir, f"cfg45_{a.log2n}_{a.sky}.fil")
+    if ctx.is_root and not os.path.exists(path) and a.sky == "single":
+        # round-2 config-4 data: one dispersed 37.1 ms pulsar at DM 110 in noise
+        gpu_filterbank(path, (1 << a.log2n) + 65536, 1024, TSAMP, FCH1, FOFF, period=0.0371, dm=110.0, duty=0.05,
+                       amp=0.25, seed=11)
+    elif ctx.is_root and not os.path.exists(path):
         from peasoup_amd.utils import synthetic
         from peasoup_amd.utils.sigproc import header_bytes as _hb
 
@@ -236,6 +240,8 @@ def main():
     ap.add_argument("--ndm", type=int, default=2000)
     ap.add_argument("--log2n", type=int, default=20)
     ap.add_argument("--workdir", default=os.path.join(REPO, "gpurun_out", "configs"))
+    ap.add_argument("--sky", default="multi", choices=["multi", "single"],
+                    help="configs 4/5 data: the 64-pulsar sky (default) or one pulsar in noise (the round-2 data)")
     ap.add_argument("--out", default="")
     ap.add_argument("--native", action="store_true", help="configs 4/5 through bin/peasoup instead of Python")
     a = ap.parse_args()
