@@ -6,13 +6,15 @@ One step (per rank, weak scaling -- fixed work per GPU):
   * dedisperse this rank's DM shard (``--dms-per-gpu`` trials, default 8, one
     chunk -- the production pipeline dedisperses 32-DM chunks) from the
     resident 1024-channel 2-bit filterbank (Auto kernel choice: the LDS-staged
-    byte-lane kernel with 8-DM workgroups; the one-hot MFMA kernel measures
-    the same at these low DMs, --dedisp-kernel mfma),
+    byte-lane kernel with 8-DM workgroups -- the one-hot MFMA kernel computes
+    whole 32-DM tiles, so an 8-DM chunk costs it twice as much; full tiles of
+    low DMs go to MFMA),
   * whiten each trial and search +-500 m/s^2 (legacy acceleration-plan
-    convention: ~684 trials per DM at 2^23 x 64 us) with an 8-harmonic sum:
-    fused resample + two-pass four-step FFT -> paired real-FFT post-processing
-    + interbin/normalise -> LDS-staged harmonic sum + peak compaction -> host
-    clustering + distillation (overlapped with the next batch),
+    convention: ~684 trials per DM at 2^23 x 64 us) with an 8-harmonic sum,
+    in 512-trial batches on one stream: fused resample + two-pass four-step
+    FFT -> paired real-FFT post-processing + interbin/normalise -> LDS-staged
+    harmonic sum + peak compaction -> peak clustering on the GPU -> host
+    distillation (overlapped with the next batch),
   * gather every rank's candidates to all ranks over RCCL and run the global
     DM/harmonic distillation + scoring.
 The synthetic filterbank (uniform 2-bit noise, random seed) is generated on

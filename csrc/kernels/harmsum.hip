@@ -249,6 +249,90 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* _
   }
 }
 
+// The whitener's half spectrum X[0..M] from the tiled four-step output: the
+// tile of r2c_interbin_tiled_kernel (8 rows x 256 columns, 64 contiguous
+// bytes per lane and mirror) without the interbin step, so every load is a
+// 16-byte vector and every row of the output a contiguous 2 KiB store (the
+// generic r2c_half_kernel reads one 8-byte element per 64-byte segment).
+__global__ void __launch_bounds__(256) r2c_half_tiled_kernel(const float2* __restrict__ Z, int log2_n2, uint64_t n1,
+                                                             uint64_t zstride, float2* __restrict__ X,
+                                                             uint64_t xstride, RowTw8 rtw) {
+  const uint64_t n2 = uint64_t(1) << log2_n2;
+  const uint64_t M = n1 * n2, half = M / 2;
+  const int t = threadIdx.x;
+  const float2* z = Z + static_cast<uint64_t>(blockIdx.z) * zstride;
+  float2* x = X + static_cast<uint64_t>(blockIdx.z) * xstride;
+  const uint64_t g0 = static_cast<uint64_t>(blockIdx.y) * 8;
+  const uint64_t k2 = static_cast<uint64_t>(blockIdx.x) * 256 + t;
+  auto xbin = [&](uint64_t k, float2& xa, float2& xm) {  // generic: X[k] and X[M-k]
+    const float2 za = z[taddr(k & (M - 1), log2_n2, n1)];
+    const float2 zb = z[taddr((M - k) & (M - 1), log2_n2, n1)];
+    float sn, cs;
+    sincospif(-static_cast<float>(k) / static_cast<float>(M), &sn, &cs);
+    xa = r2c_combine(za, zb, cs, sn);
+    xm = r2c_combine(zb, za, -cs, sn);
+  };
+  if (k2 == 0) {
+    // column 0 pairs row k1 with row n1 - k1 (not n1 - 1 - k1)
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const uint64_t k = (g0 + r) * n2;
+      float2 xa, xm;
+      xbin(k, xa, xm);
+      x[k] = xa;
+      x[M - k] = xm;  // k = 0: bin M
+    }
+  } else {
+    const float4* sa = reinterpret_cast<const float4*>(z + (k2 >> 3) * (8 * n1) + (g0 >> 3) * 64 + (k2 & 7) * 8);
+    const uint64_t m2 = n2 - k2, m1 = n1 - 8 - g0;  // mirror column, first mirror row (rows reversed)
+    const float4* sb = reinterpret_cast<const float4*>(z + (m2 >> 3) * (8 * n1) + (m1 >> 3) * 64 + (m2 & 7) * 8);
+    float2 za[8], zb[8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 a = sa[u], b = sb[u];
+      za[2 * u] = make_float2(a.x, a.y);
+      za[2 * u + 1] = make_float2(a.z, a.w);
+      zb[7 - 2 * u] = make_float2(b.x, b.y);
+      zb[6 - 2 * u] = make_float2(b.z, b.w);
+    }
+    float sn, cs;
+    sincospif(-static_cast<float>(g0 * n2 + k2) / static_cast<float>(M), &sn, &cs);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const float ws = rtw.s[r], wc = rtw.c[r];  // W^(r n2)
+      const float c = __builtin_fmaf(cs, wc, -(sn * ws)), sv = __builtin_fmaf(cs, ws, sn * wc);
+      const uint64_t k = (g0 + r) * n2 + k2;
+      x[k] = r2c_combine(za[r], zb[r], c, sv);
+      x[M - k] = r2c_combine(zb[r], za[r], -c, sv);
+    }
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0) {  // bin M/2 (row n1/2, column 0)
+    float2 xa, xm;
+    xbin(half, xa, xm);
+    x[half] = xa;
+  }
+}
+
+// The whitener's inverse: x[m] = conj(Z[m]) in natural order from the tiled
+// four-step output, 8 rows x 256 columns per workgroup: each lane reads its
+// column's 8 rows as 64 contiguous bytes, each row is stored as 2 KiB.
+__global__ void __launch_bounds__(256) c2r_post_tiled_kernel(const float2* __restrict__ Z, int log2_n2, uint64_t n1,
+                                                             uint64_t zstride, float2* __restrict__ x,
+                                                             uint64_t ostride) {
+  const uint64_t n2 = uint64_t(1) << log2_n2;
+  const float2* z = Z + static_cast<uint64_t>(blockIdx.z) * zstride;
+  float2* o = x + static_cast<uint64_t>(blockIdx.z) * ostride;
+  const uint64_t g0 = static_cast<uint64_t>(blockIdx.y) * 8;
+  const uint64_t k2 = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const float4* sa = reinterpret_cast<const float4*>(z + (k2 >> 3) * (8 * n1) + (g0 >> 3) * 64 + (k2 & 7) * 8);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float4 a = sa[u];
+    o[(g0 + 2 * u) * n2 + k2] = make_float2(a.x, -a.y);
+    o[(g0 + 2 * u + 1) * n2 + k2] = make_float2(a.z, -a.w);
+  }
+}
+
 // Same tile, neighbours by cross-lane shuffles instead of two 16.5 KiB LDS
 // planes: lane l's left neighbour X[k-1] is lane l-1's ascending bin and its
 // mirror neighbour X[M-(k+1)] is lane l+1's mirrored bin; only the values
@@ -994,6 +1078,20 @@ void fft4_r2c_half(const float2* Z, uint64_t M, const XLayoutArgs& L, float2* X,
                    uint64_t zstride, uint64_t xstride) {
   PSOUP_CHECK(M >= 2 && (M & (M - 1)) == 0, "r2c_half: M must be a power of two");
   PSOUP_CHECK(count >= 1 && count <= 65535, "r2c_half: bad count");
+  const uint64_t n1 = L.n1, n2 = L.tiled ? (uint64_t(1) << L.log2_row) : 0;
+  if (L.tiled && n1 >= 16 && n2 >= 256 && n1 * n2 == M && (reinterpret_cast<uintptr_t>(Z) & 15) == 0 &&
+      zstride % 2 == 0) {
+    RowTw8 rtw;
+    for (int r = 0; r < 8; ++r) {
+      const double a = -M_PI * r / static_cast<double>(n1);
+      rtw.c[r] = static_cast<float>(std::cos(a));
+      rtw.s[r] = static_cast<float>(std::sin(a));
+    }
+    const dim3 grid(static_cast<unsigned>(n2 / 256), static_cast<unsigned>(n1 / 16), static_cast<unsigned>(count));
+    r2c_half_tiled_kernel<<<grid, 256, 0, s>>>(Z, L.log2_row, n1, zstride, X, xstride, rtw);
+    post_launch_check("r2c_half_tiled_kernel", s);
+    return;
+  }
   const dim3 grid(dev::grid_for(M + 1, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
   r2c_half_kernel<<<grid, 256, 0, s>>>(Z, M, L, X, zstride, xstride);
   post_launch_check("r2c_half_kernel", s);
@@ -1012,6 +1110,14 @@ void fft4_c2r_post(const float2* Z, uint64_t M, const XLayoutArgs& L, float* x, 
                    uint64_t zstride, uint64_t ostride) {
   PSOUP_CHECK((reinterpret_cast<uintptr_t>(x) & 7) == 0 && ostride % 2 == 0, "c2r_post: output alignment");
   PSOUP_CHECK(count >= 1 && count <= 65535, "c2r_post: bad count");
+  const uint64_t n1 = L.n1, n2 = L.tiled ? (uint64_t(1) << L.log2_row) : 0;
+  if (L.tiled && n1 >= 8 && n2 >= 256 && n1 * n2 == M && (reinterpret_cast<uintptr_t>(Z) & 15) == 0 &&
+      zstride % 2 == 0) {
+    const dim3 grid(static_cast<unsigned>(n2 / 256), static_cast<unsigned>(n1 / 8), static_cast<unsigned>(count));
+    c2r_post_tiled_kernel<<<grid, 256, 0, s>>>(Z, L.log2_row, n1, zstride, reinterpret_cast<float2*>(x), ostride / 2);
+    post_launch_check("c2r_post_tiled_kernel", s);
+    return;
+  }
   const dim3 grid(dev::grid_for(M, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
   c2r_post_kernel<<<grid, 256, 0, s>>>(Z, M, L, reinterpret_cast<float2*>(x), zstride, ostride / 2);
   post_launch_check("c2r_post_kernel", s);

@@ -243,8 +243,13 @@ int Dedisperser::mfma_lds_split(int d0, int d1) {
   if (!ml_ready_) build_mfma_lds_tables();
   int T = d0 / kTileDms;
   const int T1 = (d1 - 1) / kTileDms + 1;
+  // the MFMA kernel computes whole 32-DM tiles, the VALU kernels only the
+  // DMs asked for (8-DM workgroups for short ranges): a partial tile's MFMA
+  // budget shrinks with its DM count (the bench's 8-DM chunk at DM 0:
+  // MFMA 9.7 ms vs VALU 4.9 ms per step at 2^23)
+  auto tile_dms = [&](int t) { return std::min(d1, (t + 1) * kTileDms) - std::max(d0, t * kTileDms); };
   while (T < T1 && ml_tile_ok_[static_cast<size_t>(T)] &&
-         ml_tile_steps_[static_cast<size_t>(T)] <= mfma_lds_ratio() * g.nactive)
+         ml_tile_steps_[static_cast<size_t>(T)] <= mfma_lds_ratio() * g.nactive * tile_dms(T) / kTileDms)
     ++T;
   return std::min(d1, T * kTileDms);
 }

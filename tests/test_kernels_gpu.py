@@ -94,6 +94,7 @@ def test_dedisperse_1024ch_hybrid_mfma_bit_exact(C):
     dd = C.Dedisperser(dfb, s)
     split = dd.mfma_lds_split(0, ndm)
     assert 0 < split < ndm and split % 32 == 0, split  # both kernels run in Auto
+    assert dd.mfma_lds_split(0, 8) == 0  # an 8-DM partial tile: the VALU kernel (MFMA computes all 32 DMs)
     stride = C.Dedisperser.row_stride(g.out_nsamps)
     outs = {}
     for k in (C.DedispKernel.Direct, C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto):
