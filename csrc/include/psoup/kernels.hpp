@@ -340,6 +340,7 @@ enum Fft4Flags : int {
                               // the same load bytes as 128-byte row pieces
   kFft4Stagger = 4194304,     // experiment (one-exchange pass A): blocks 256..511 sleep ((flags >> 24) & 63)
                               // x 8k cycles first, putting each CU's two workgroups out of phase
+  kFft4LoadPrio = 512,        // experiment (one-exchange pass A): s_setprio 3 while issuing the column loads
   kFft4StripInput = 1073741824,  // one-exchange pass A: the padded input in column strips (16 + 4 floats of
                                  // every row per strip, strips row-contiguous), so a wave's 16 rows are
                                  // one ~1.3 KiB contiguous range instead of 16 pieces 16 KiB apart

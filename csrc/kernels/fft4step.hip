@@ -155,7 +155,9 @@ __device__ __forceinline__ void exchange(Vec<CPT>& v, float* __restrict__ lds, i
 // Phase timestamps (tools/expt/fft4_trace.py): when g_fft4_trace is set,
 // thread 0 of each workgroup records the shader clock at fixed points of the
 // kernel (start, loads issued, after every FFT stage and exchange, end).
-__device__ unsigned long long* g_fft4_trace = nullptr;
+// (__constant__: read with a scalar load, so a trace point costs an lgkmcnt
+// wait, not a vmcnt(0) that would drain every global load in flight)
+__constant__ unsigned long long* g_fft4_trace = nullptr;
 constexpr int kTraceEvents = 12;
 __device__ __forceinline__ void trace_event(int ev) {
   unsigned long long* tr = g_fft4_trace;
@@ -468,7 +470,8 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
   const int log2row = __builtin_ctz(static_cast<unsigned>(2 * N1));
   const TableOffsets to = table_offsets(N1, L);
   const double af = afs[k];
-  const uint64_t src = g.tsrc ? g.tsrc[k] : static_cast<uint64_t>(k);  // series this trial resamples
+  const uint64_t src = __builtin_amdgcn_readfirstlane(  // series this trial resamples (workgroup-uniform)
+      static_cast<uint32_t>(g.tsrc ? g.tsrc[k] : static_cast<uint64_t>(k)));
   const double size = static_cast<double>(n);
   Vec<CPT> v;
 #pragma unroll
@@ -702,7 +705,11 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
   const int log2row = __builtin_ctz(static_cast<unsigned>(2 * N1));
   const TableOffsets to = table_offsets(N1, L);
   const double af = afs[k];
-  const uint64_t src = g.tsrc ? g.tsrc[k] : static_cast<uint64_t>(k);
+  // workgroup-uniform: readfirstlane keeps pointers built from it (and the
+  // buffer resource of the one-exchange loads) in SGPRs -- a VGPR resource
+  // wraps every buffer load in a waterfall loop
+  const uint64_t src =
+      __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(g.tsrc ? g.tsrc[k] : static_cast<uint64_t>(k)));
   const float* ink = in + src * g.in_tstride;
   const float* padk = in_pad + src * g.pad_tstride;
   const uint32_t nn = static_cast<uint32_t>(n);
@@ -731,8 +738,15 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
     const bool strips = flags & kFft4StripInput;  // (the host pads in strips exactly when this kernel runs)
     const uint32_t nrows = static_cast<uint32_t>(L);
     uint32_t bad = 0;
+    const bool prio = flags & kFft4LoadPrio;
+    if (prio) __builtin_amdgcn_s_setprio(3);  // experiment: issue this workgroup's loads ahead of the other's math
+    // Rows are loaded in the order dft<P> consumes them: its first radix-8
+    // pass takes rows b, b + P/8, ..., b + 7 P/8 for b = 0, 1, ..., so the
+    // compiler's vmcnt waits let the first groups' butterflies run while the
+    // later groups' loads are still in flight.
 #pragma unroll
-    for (int m = 0; m < P; ++m) {
+    for (int ii = 0; ii < P; ++ii) {
+      const int m = P >= 16 ? (P / 8) * (ii % 8) + ii / 8 : ii;
       // (kFft4WideProbe, timing only: the same bytes as 128-byte row pieces --
       // 16 columns x half the rows per workgroup, 8 lanes per row)
       const bool wide = kWideProbe && (flags & kFft4WideProbe);
@@ -759,6 +773,7 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
       va[m] = make_float2(v.x, v.y);
       vb[m] = make_float2(v.z, v.w);
     }
+    if (prio) __builtin_amdgcn_s_setprio(0);
     trace_event(1);
     if (bad != 0) {
       const double size = static_cast<double>(n);
