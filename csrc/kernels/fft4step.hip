@@ -848,7 +848,9 @@ fft4_rowpass_onex_kernel(const float2* __restrict__ Y, float2* __restrict__ X, i
   const int k = static_cast<int>(tslow ? lb / nbt : lb % static_cast<uint32_t>(K));
   const int r0 = static_cast<int>(tslow ? lb % nbt : lb / static_cast<uint32_t>(K)) * 8;
   const TableOffsets to = table_offsets(L, g.n2);
-  const float2* yk = Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(r0 >> 3) * 64 + 2 * cp;
+  // workgroup-uniform base (the lane's 2 cp goes into the offset): the buffer
+  // resource stays in SGPRs, no waterfall loop around the loads
+  const float2* yk = Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(r0 >> 3) * 64;
   float2 va[P], vb[P];  // rows r0 + 2cp, r0 + 2cp + 1
   {
     // 32-bit buffer offsets (a trial's Y is < 2 GiB): one VGPR per address
@@ -858,7 +860,8 @@ fft4_rowpass_onex_kernel(const float2* __restrict__ Y, float2* __restrict__ X, i
 #pragma unroll
     for (int m = 0; m < P; ++m) {
       const uint32_t i = static_cast<uint32_t>(gg + G * m);
-      const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i >> 3) * blk + (i & 7) * 8) * 8u, 0, 0));
+      const f4v v = __builtin_bit_cast(
+          f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i >> 3) * blk + (i & 7) * 8 + 2u * cp) * 8u, 0, 0));
       va[m] = make_float2(v.x, v.y);
       vb[m] = make_float2(v.z, v.w);
     }
