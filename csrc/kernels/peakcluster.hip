@@ -143,7 +143,7 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
                                                                   const uint32_t* __restrict__ segcnt, int gap,
                                                                   uint32_t lo_n, uint2* __restrict__ out,
                                                                   uint2* __restrict__ segtab,
-                                                                  uint32_t* __restrict__ total) {
+                                                                  uint32_t* __restrict__ total, int stop_after) {
   constexpr uint32_t R = (CAP + kClThreads - 1) / kClThreads;  // rows of kClThreads positions
   __shared__ uint2 key[CAP];      // (idx, snr bits)
   __shared__ uint16_t jmp[CAP];   // next survivor at/after a position, then chain jumps
@@ -191,6 +191,7 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
       __syncthreads();
     }
   }
+  if (stop_after == 1) return;  // timing only (PSOUP_CLUSTER_STOP): load + sort
   // Every phase below gives position i = r * kClThreads + t to thread t
   // (row r): consecutive lanes touch consecutive LDS words, and wave ballots
   // order the survivors / peaks inside a row.
@@ -215,6 +216,7 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
   }
   uint32_t totsurv;
   block_excl_sum<kClThreads>(mysurv, sc, &totsurv);  // (its barriers also publish flag)
+  if (stop_after == 2) return;  // timing only: + window test
   // (3) next survivor at or after every position: rows from the last, a
   // row's waves from their ballots, the carry from the rows after it
   uint32_t carry = n;
@@ -257,6 +259,7 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
   __syncthreads();
   if (t == 0 && first_s < n) flag[first_s] = 3;
   __syncthreads();
+  if (stop_after == 3) return;  // timing only: + next survivor / next()
   // (2) the chain from the first survivor, by pointer doubling: after round
   // m every survivor within 2^(m+1) - 1 jumps of the start is marked
   for (uint32_t span = 1; span < totsurv; span <<= 1) {
@@ -283,6 +286,7 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
     }
     __syncthreads();
   }
+  if (stop_after == 4) return;  // timing only: + chain marking
   // compaction of the peaks in idx order: per (row, wave) counts, their
   // exclusive scan (one thread), then ballot ranks inside each wave
   for (uint32_t r = 0; r < nrow; ++r) {
@@ -366,8 +370,12 @@ void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint
     seg_scatter_global_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segoff, cursor, d_sorted);
     post_launch_check("seg_scatter_global_kernel", s);
   }
+  static const int stop = [] {  // timing experiments only: end the kernels after a phase
+    const char* e = std::getenv("PSOUP_CLUSTER_STOP");
+    return e ? std::atoi(e) : 99;
+  }();
   peak_cluster_kernel<kClSmall, kClThreads><<<nseg, kClThreads, 0, s>>>(d_sorted, segoff, segcnt, gap, 0u, d_out,
-                                                                         d_segtab, d_total);
+                                                                         d_segtab, d_total, stop);
   post_launch_check("peak_cluster_kernel<small>", s);
   // the large kernel holds a CU's LDS alone: 1024 threads (16 waves) hide the
   // LDS latency of its dependent sort / scan steps (PSOUP_CLUSTER_TH=512: the
@@ -378,10 +386,10 @@ void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint
   }();
   if (th512)
     peak_cluster_kernel<kClusterCap, 512><<<nseg, 512, 0, s>>>(d_sorted, segoff, segcnt, gap, kClSmall, d_out,
-                                                                d_segtab, d_total);
+                                                                d_segtab, d_total, stop);
   else
     peak_cluster_kernel<kClusterCap, 1024><<<nseg, 1024, 0, s>>>(d_sorted, segoff, segcnt, gap, kClSmall, d_out,
-                                                                  d_segtab, d_total);
+                                                                  d_segtab, d_total, stop);
   post_launch_check("peak_cluster_kernel<large>", s);
 }
 

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Peak-clustering kernels on RFI-like segments: nseg segments of ~n
+threshold crossings each (dense runs around periodic spikes plus scattered
+noise crossings), records shuffled like the harmonic kernel's atomics emit
+them.  Prints the time of kern::peak_cluster_batch (the phase cut
+PSOUP_CLUSTER_STOP selects, for timing experiments)."""
+import argparse
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+from peasoup_amd import _C  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nseg", type=int, default=2048)
+    ap.add_argument("--n", type=int, default=4200)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    K = _C.kernels
+    rng = np.random.default_rng(1)
+    recs = []
+    for sgi in range(a.nseg):
+        n = int(rng.integers(a.n // 2, a.n * 3 // 2))
+        spikes = rng.choice(1 << 22, max(1, n // 40), replace=False)
+        idx = np.unique((spikes[:, None] + np.arange(-20, 20)[None, :]).reshape(-1))[:n].astype(np.int32)
+        snr = (9.0 + 30.0 * rng.random(idx.size)).astype(np.float32)
+        recs.append(np.stack([np.full(idx.size, sgi, np.uint32), idx.view(np.uint32), snr.view(np.uint32)], axis=1))
+    allr = np.concatenate(recs)
+    allr = allr[rng.permutation(len(allr))]
+    n = len(allr)
+    dev = "cuda"
+    cap = n + 100
+    peaks = torch.from_numpy(allr.reshape(-1).view(np.int32).copy()).to(dev)
+    count = torch.tensor([n], dtype=torch.int32, device=dev)
+    work = torch.empty(3 * a.nseg, dtype=torch.int32, device=dev)
+    srt = torch.empty(2 * cap, dtype=torch.int32, device=dev)
+    out = torch.empty(2 * cap, dtype=torch.int32, device=dev)
+    tab = torch.empty(2 * a.nseg, dtype=torch.int32, device=dev)
+    tot = torch.zeros(1, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    run = lambda: K.peak_cluster_batch(peaks.data_ptr(), count.data_ptr(), cap, a.nseg, 30, work.data_ptr(),
+                                       srt.data_ptr(), out.data_ptr(), tab.data_ptr(), tot.data_ptr(), s)
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    print(f"stop={os.environ.get('PSOUP_CLUSTER_TH', '1024')}/{os.environ.get('PSOUP_CLUSTER_STOP', 'full')} "
+          f"records={n} segments={a.nseg}: {e0.elapsed_time(e1) / a.reps:.3f} ms per batch", flush=True)
+
+
+if __name__ == "__main__":
+    main()
