@@ -37,13 +37,12 @@ __global__ void __launch_bounds__(256) interbin_normalise_batch_kernel(const flo
   float* p = P + static_cast<uint64_t>(k) * pstride;
   const float mean = stats[0] * nscale;
   const float sigma = stats[2] * nscale;
+  const float rsig = 1.0f / sigma;  // one division per thread, not one per bin
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < nbins_out; i += stride) {
     float2 xl = i > 0 ? x[i - 1] : make_float2(0.f, 0.f);
     float v = dev::interbin(x[i], xl);
-    v -= mean;
-    v /= sigma;
-    p[i] = v;
+    p[i] = (v - mean) * rsig;
   }
 }
 
@@ -86,6 +85,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
   if (tsrc) stats += 4 * tsrc[kk];  // multi-series batch: this trial's whitening stats
   const float mean = stats[0] * nscale;
   const float sigma = stats[2] * nscale;
+  const float rsig = 1.0f / sigma;  // one division per thread, not one per bin
   const uint64_t half = M / 2;
   float2 wu[kR2cBpt];  // W^(256 u), W = e^{-i pi / M}
 #pragma unroll
@@ -134,10 +134,10 @@ __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
       if (k <= half) {
         if (k < nbins_out) {
           const float2 xl = k > 0 ? A[slot - 1] : make_float2(0.f, 0.f);
-          p[k] = (dev::interbin(A[slot], xl) - mean) / sigma;
+          p[k] = (dev::interbin(A[slot], xl) - mean) * rsig;
         }
         const uint64_t j = M - k;  // mirrored bin (> M/2), neighbour X[j-1] = D[slot+1]
-        if (j > half && j < nbins_out) p[j] = (dev::interbin(D[slot], D[slot + 1]) - mean) / sigma;
+        if (j > half && j < nbins_out) p[j] = (dev::interbin(D[slot], D[slot + 1]) - mean) * rsig;
       }
     }
     __syncthreads();
@@ -180,6 +180,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* _
   if (tsrc) stats += 4 * tsrc[kk];  // multi-series batch: this trial's whitening stats
   const float mean = stats[0] * nscale;
   const float sigma = stats[2] * nscale;
+  const float rsig = 1.0f / sigma;  // one division per thread, not one per bin
   const uint64_t g0 = static_cast<uint64_t>(blockIdx.y) * 8;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * 256;
   auto xbin = [&](uint64_t k, float2& xa, float2& xm) {  // generic: X[k] and X[M-k]
@@ -236,16 +237,16 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* _
     const uint64_t k = (g0 + r) * n2 + k2;
     if (k < nbins_out) {
       const float2 xl = k > 0 ? A[r][t] : make_float2(0.f, 0.f);
-      p[k] = (dev::interbin(A[r][t + 1], xl) - mean) / sigma;
+      p[k] = (dev::interbin(A[r][t + 1], xl) - mean) * rsig;
     }
     const uint64_t j = M - k;  // > M/2 for every k in the ascending rows
-    if (j < nbins_out) p[j] = (dev::interbin(D[r][t + 1], D[r][t + 2]) - mean) / sigma;
+    if (j < nbins_out) p[j] = (dev::interbin(D[r][t + 1], D[r][t + 2]) - mean) * rsig;
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && half < nbins_out) {  // bin M/2 (row n1/2, column 0)
     float2 xa, xm, la, lm;
     xbin(half, xa, xm);
     xbin(half - 1, la, lm);
-    p[half] = (dev::interbin(xa, la) - mean) / sigma;
+    p[half] = (dev::interbin(xa, la) - mean) * rsig;
   }
 }
 
@@ -353,6 +354,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
   if (tsrc) stats += 4 * tsrc[kk];
   const float mean = stats[0] * nscale;
   const float sigma = stats[2] * nscale;
+  const float rsig = 1.0f / sigma;  // one division per thread, not one per bin
   const uint64_t g0 = static_cast<uint64_t>(blockIdx.y) * 8;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * 256;
   auto xbin = [&](uint64_t k, float2& xa, float2& xm) {  // generic: X[k] and X[M-k]
@@ -421,16 +423,16 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
     const uint64_t k = (g0 + r) * n2 + k2;
     if (k < nbins_out) {
       if (k == 0) xl = make_float2(0.f, 0.f);
-      p[k] = (dev::interbin(xa[r], xl) - mean) / sigma;
+      p[k] = (dev::interbin(xa[r], xl) - mean) * rsig;
     }
     const uint64_t j = M - k;
-    if (j < nbins_out) p[j] = (dev::interbin(xm[r], xr) - mean) / sigma;
+    if (j < nbins_out) p[j] = (dev::interbin(xm[r], xr) - mean) * rsig;
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && half < nbins_out) {  // bin M/2 (row n1/2, column 0)
     float2 ha, hm, la, lm;
     xbin(half, ha, hm);
     xbin(half - 1, la, lm);
-    p[half] = (dev::interbin(ha, la) - mean) / sigma;
+    p[half] = (dev::interbin(ha, la) - mean) * rsig;
   }
 }
 

@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <fstream>
 #include <iostream>
+#include <map>
 #include <mutex>
 #include <sstream>
 #include <thread>
@@ -288,12 +289,16 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   // the free HBM of every device (PSOUP_KEEP_TRIALS=0/1 forces it).
   bool keep = args.npdmp > 0;
   {
+    // every worker mapped to a physical device holds its own store
     const uint64_t need = rstride * static_cast<uint64_t>(sh.ndm);
-    for (int d = 0; d < ngpu && keep; ++d) {
-      PSOUP_HIP_CHECK(hipSetDevice(hip_dev(d)));
+    std::map<int, uint64_t> per_dev;
+    for (int d = 0; d < ngpu; ++d) per_dev[hip_dev(d)] += need;
+    for (const auto& [phys, bytes] : per_dev) {
+      if (!keep) break;
+      PSOUP_HIP_CHECK(hipSetDevice(phys));
       size_t free_b = 0, total_b = 0;
       PSOUP_HIP_CHECK(hipMemGetInfo(&free_b, &total_b));
-      keep = need <= free_b / 4;
+      keep = bytes <= free_b / 4;
     }
     if (const char* e = std::getenv("PSOUP_KEEP_TRIALS")) keep = std::atoi(e) != 0;
   }

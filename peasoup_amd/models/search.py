@@ -223,6 +223,8 @@ class RankSearcher:
             # a spill of another run, or a corrupt/truncated one, is recomputed
             ckey = _C.prepare_checkpoint_dir(ckdir, self.args, self.header)
         dev = self.ctx.device
+        if self.keep_trials:
+            self.resident_rows = {}  # rows of this call only (a searcher reused across calls must not grow)
         side = _C.GpuStream()
         bufs: List[torch.Tensor] = []  # double buffer, allocated on first use
         freed = [None, None]           # event: search stream finished with the buffer
