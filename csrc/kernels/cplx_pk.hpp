@@ -26,16 +26,13 @@ typedef float v2f __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ v2f tv(float2 a) { return __builtin_bit_cast(v2f, a); }
 __device__ __forceinline__ float2 tf(v2f a) { return __builtin_bit_cast(float2, a); }
 
-__device__ __forceinline__ float2 add(float2 a, float2 b) {
-  v2f d;
-  asm("v_pk_add_f32 %0, %1, %2" : "=v"(d) : "v"(tv(a)), "v"(tv(b)));
-  return tf(d);
-}
-__device__ __forceinline__ float2 sub(float2 a, float2 b) {
-  v2f d;
-  asm("v_pk_add_f32 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]" : "=v"(d) : "v"(tv(a)), "v"(tv(b)));
-  return tf(d);
-}
+// Plain adds / subtracts as vector arithmetic: the compiler emits the same
+// v_pk_add_f32 (neg modifiers for the subtract) and, seeing them, can
+// schedule independent work between dependent packed ops (gfx950 needs one
+// wait state there, an s_nop when nothing else is ready); the swizzled forms
+// below stay inline asm.
+__device__ __forceinline__ float2 add(float2 a, float2 b) { return tf(tv(a) + tv(b)); }
+__device__ __forceinline__ float2 sub(float2 a, float2 b) { return tf(tv(a) - tv(b)); }
 // a + (-i) b = (a.x + b.y, a.y - b.x)
 __device__ __forceinline__ float2 add_mi(float2 a, float2 b) {
   v2f d;

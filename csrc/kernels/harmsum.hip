@@ -87,10 +87,11 @@ __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
   const float sigma = stats[2] * nscale;
   const float rsig = 1.0f / sigma;  // one division per thread, not one per bin
   const uint64_t half = M / 2;
+  const float invM = 1.0f / static_cast<float>(M);  // M a power of two: x * invM == x / M exactly
   float2 wu[kR2cBpt];  // W^(256 u), W = e^{-i pi / M}
 #pragma unroll
   for (int u = 0; u < kR2cBpt; ++u)
-    sincospif(-static_cast<float>(256 * u) / static_cast<float>(M), &wu[u].y, &wu[u].x);
+    sincospif(-static_cast<float>(256 * u) * invM, &wu[u].y, &wu[u].x);
   auto halo = [&](int64_t k, int u) {
     if (k < 0 || static_cast<uint64_t>(k) > half + 1) {
       A[u] = D[u] = make_float2(0.f, 0.f);
@@ -100,7 +101,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
     const float2 za = z[zaddr(uk & (M - 1), log2_row, pitch, blk, lw)];
     const float2 zb = z[zaddr((M - uk) & (M - 1), log2_row, pitch, blk, lw)];
     float sn, cs;
-    sincospif(-static_cast<float>(uk) / static_cast<float>(M), &sn, &cs);
+    sincospif(-static_cast<float>(uk) * invM, &sn, &cs);
     A[u] = r2c_combine(za, zb, cs, sn);
     D[u] = r2c_combine(zb, za, -cs, sn);  // angle -pi (M-k)/M = -pi + pi k/M
   };
@@ -118,7 +119,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
     if (t == 0) halo(static_cast<int64_t>(k0) - 1, 0);
     if (t == 1) halo(static_cast<int64_t>(k0 + kR2cTile), kR2cTile + 1);
     float sn, cs;
-    sincospif(-static_cast<float>(kb) / static_cast<float>(M), &sn, &cs);
+    sincospif(-static_cast<float>(kb) * invM, &sn, &cs);
 #pragma unroll
     for (int u = 0; u < kR2cBpt; ++u) {
       const float c = cs * wu[u].x - sn * wu[u].y, s = cs * wu[u].y + sn * wu[u].x;  // W^(kb+256u)
@@ -173,6 +174,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* _
   __shared__ float2 D[8][258];  // D[r][u] = X[M - ((g0+r)*n2 + c0 - 1 + u)]
   const uint64_t n2 = uint64_t(1) << log2_n2;
   const uint64_t M = n1 * n2, half = M / 2;
+  const float invM = 1.0f / static_cast<float>(M);  // M a power of two: x * invM == x / M exactly
   const int kk = blockIdx.z;
   const int t = threadIdx.x;
   const float2* z = Z + static_cast<uint64_t>(kk) * zstride;
@@ -187,7 +189,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* _
     const float2 za = z[taddr(k & (M - 1), log2_n2, n1)];
     const float2 zb = z[taddr((M - k) & (M - 1), log2_n2, n1)];
     float sn, cs;
-    sincospif(-static_cast<float>(k) / static_cast<float>(M), &sn, &cs);
+    sincospif(-static_cast<float>(k) * invM, &sn, &cs);
     xa = r2c_combine(za, zb, cs, sn);
     xm = r2c_combine(zb, za, -cs, sn);
   };
@@ -210,7 +212,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* _
       zb[6 - 2 * u] = make_float2(b.z, b.w);
     }
     float sn, cs;
-    sincospif(-static_cast<float>(g0 * n2 + k2) / static_cast<float>(M), &sn, &cs);
+    sincospif(-static_cast<float>(g0 * n2 + k2) * invM, &sn, &cs);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const float ws = rtw.s[r], wc = rtw.c[r];  // W^(r n2)
@@ -260,6 +262,7 @@ __global__ void __launch_bounds__(256) r2c_half_tiled_kernel(const float2* __res
                                                              uint64_t xstride, RowTw8 rtw) {
   const uint64_t n2 = uint64_t(1) << log2_n2;
   const uint64_t M = n1 * n2, half = M / 2;
+  const float invM = 1.0f / static_cast<float>(M);  // M a power of two: x * invM == x / M exactly
   const int t = threadIdx.x;
   const float2* z = Z + static_cast<uint64_t>(blockIdx.z) * zstride;
   float2* x = X + static_cast<uint64_t>(blockIdx.z) * xstride;
@@ -269,7 +272,7 @@ __global__ void __launch_bounds__(256) r2c_half_tiled_kernel(const float2* __res
     const float2 za = z[taddr(k & (M - 1), log2_n2, n1)];
     const float2 zb = z[taddr((M - k) & (M - 1), log2_n2, n1)];
     float sn, cs;
-    sincospif(-static_cast<float>(k) / static_cast<float>(M), &sn, &cs);
+    sincospif(-static_cast<float>(k) * invM, &sn, &cs);
     xa = r2c_combine(za, zb, cs, sn);
     xm = r2c_combine(zb, za, -cs, sn);
   };
@@ -297,7 +300,7 @@ __global__ void __launch_bounds__(256) r2c_half_tiled_kernel(const float2* __res
       zb[6 - 2 * u] = make_float2(b.z, b.w);
     }
     float sn, cs;
-    sincospif(-static_cast<float>(g0 * n2 + k2) / static_cast<float>(M), &sn, &cs);
+    sincospif(-static_cast<float>(g0 * n2 + k2) * invM, &sn, &cs);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const float ws = rtw.s[r], wc = rtw.c[r];  // W^(r n2)
@@ -347,6 +350,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
   __shared__ float2 eD[5][8];  // eD[w][r]: mirror X of wave w's lane 0 (w = 4: the halo column c0 + 256)
   const uint64_t n2 = uint64_t(1) << log2_n2;
   const uint64_t M = n1 * n2, half = M / 2;
+  const float invM = 1.0f / static_cast<float>(M);  // M a power of two: x * invM == x / M exactly
   const int kk = blockIdx.z;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const float2* z = Z + static_cast<uint64_t>(kk) * zstride;
@@ -361,7 +365,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
     const float2 za = z[taddr(k & (M - 1), log2_n2, n1)];
     const float2 zb = z[taddr((M - k) & (M - 1), log2_n2, n1)];
     float sn, cs;
-    sincospif(-static_cast<float>(k) / static_cast<float>(M), &sn, &cs);
+    sincospif(-static_cast<float>(k) * invM, &sn, &cs);
     xa = r2c_combine(za, zb, cs, sn);
     xm = r2c_combine(zb, za, -cs, sn);
   };
@@ -384,7 +388,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
       zb[6 - 2 * u] = make_float2(b.z, b.w);
     }
     float sn, cs;
-    sincospif(-static_cast<float>(g0 * n2 + k2) / static_cast<float>(M), &sn, &cs);
+    sincospif(-static_cast<float>(g0 * n2 + k2) * invM, &sn, &cs);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const float ws = rtw.s[r], wc = rtw.c[r];
@@ -905,12 +909,13 @@ __global__ void __launch_bounds__(256) r2c_half_kernel(const float2* __restrict_
                                                        float2* __restrict__ X, uint64_t zstride, uint64_t xstride) {
   Z += blockIdx.y * zstride;
   X += blockIdx.y * xstride;
+  const float invM = 1.0f / static_cast<float>(M);  // M a power of two: x * invM == x / M exactly
   for (uint64_t k = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; k <= M;
        k += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
     const float2 za = Z[xaddr(k & (M - 1), L)];
     const float2 zb = Z[xaddr((M - k) & (M - 1), L)];
     float sn, cs;
-    sincospif(-static_cast<float>(k) / static_cast<float>(M), &sn, &cs);
+    sincospif(-static_cast<float>(k) * invM, &sn, &cs);
     X[k] = r2c_combine(za, zb, cs, sn);
   }
 }
@@ -919,13 +924,14 @@ __global__ void __launch_bounds__(256) c2r_pre_kernel(const float2* __restrict__
                                                       float2* __restrict__ out, uint64_t xstride, uint64_t ostride) {
   X += blockIdx.y * xstride;
   out += blockIdx.y * ostride;
+  const float invM = 1.0f / static_cast<float>(M);  // M a power of two: x * invM == x / M exactly
   for (uint64_t k = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; k < M;
        k += static_cast<uint64_t>(gridDim.x) * blockDim.x) {
     const float2 a = X[k], b = X[M - k];
     const float ex = a.x + b.x, ey = a.y - b.y;  // X[k] + conj X[M-k]
     const float dx = a.x - b.x, dy = a.y + b.y;  // X[k] - conj X[M-k]
     float sn, cs;
-    sincospif(static_cast<float>(k) / static_cast<float>(M), &sn, &cs);
+    sincospif(static_cast<float>(k) * invM, &sn, &cs);
     const float wx = cs * dx - sn * dy, wy = cs * dy + sn * dx;  // W^k d
     // e + i (W^k d), conjugated
     out[k] = make_float2(ex - wy, -(ey + wx));
@@ -1101,7 +1107,7 @@ void fft4_r2c_half(const float2* Z, uint64_t M, const XLayoutArgs& L, float2* X,
 
 void fft4_c2r_pre(const float2* X, uint64_t M, float2* out, hipStream_t s, int count, uint64_t xstride,
                   uint64_t ostride) {
-  PSOUP_CHECK(M >= 2, "c2r_pre: bad size");
+  PSOUP_CHECK(M >= 2 && (M & (M - 1)) == 0, "c2r_pre: M must be a power of two");
   PSOUP_CHECK(count >= 1 && count <= 65535, "c2r_pre: bad count");
   const dim3 grid(dev::grid_for(M, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
   c2r_pre_kernel<<<grid, 256, 0, s>>>(X, M, out, xstride, ostride);
