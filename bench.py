@@ -146,19 +146,27 @@ def main() -> int:
     tot = torch.tensor([trials_per_step_local], dtype=torch.int64, device=dev)
     trials_per_step = int(pdist.all_reduce_sum(tot).item())
 
+    phase = {"search": 0.0, "merge": 0.0}
+
     def step():
+        t = time.perf_counter()
         local = rs.search(shard, chunk=a.dms_per_gpu)
+        t1 = time.perf_counter()
+        phase["search"] += t1 - t
         blobs = pdist.gather_bytes(_C.serialize_candidates(local), dst=None)
         cands = []
         for b in blobs:
             cands.extend(_C.deserialize_candidates(b))
         cands.sort(key=lambda c: c.dm_idx)
-        return _C.global_distill_and_score(cands, args, rs.header)
+        out = _C.global_distill_and_score(cands, args, rs.header)
+        phase["merge"] += time.perf_counter() - t1
+        return out
 
     for _ in range(a.warmup):
         step()
     for e in rs.engines:
         e.reset_counters()
+    phase.update(search=0.0, merge=0.0)
     pdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -209,6 +217,11 @@ def main() -> int:
                 "signal": bool(a.signal),
                 "peaks_per_dm": round(ctr.get("peaks", 0) / max(1, a.steps * a.dms_per_gpu), 1),
                 "host_distill_s_per_step": round(ctr.get("host_s", 0) / a.steps, 4),
+                # rank 0's wall split of a step: dedispersion + whitening + the
+                # acceleration loop, then the candidate gather + global distillation
+                "search_s_per_step": round(phase["search"] / a.steps, 4),
+                "merge_s_per_step": round(phase["merge"] / a.steps, 4),
+                "accel_s_per_step": round(ctr.get("accel_s", 0) / a.steps, 4),
             },
         }
         print(json.dumps(out), flush=True)

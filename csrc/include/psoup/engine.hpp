@@ -100,6 +100,10 @@ class Dedisperser {
   // MFMA kernel (leading tiles whose offset spread is narrow enough for the
   // one-hot GEMM to beat the VALU kernels), [split, d1) the VALU kernels
   int mfma_lds_split(int d0, int d1);
+  // Build every table Auto / MFMA / VALU runs use (otherwise built on the
+  // first run that needs them, with blocking uploads, mid-search: the
+  // 2026-DM config-4 list's first VALU tile stalled the host 64 ms)
+  void warm();
 
  private:
   void build_resident_plan();
@@ -265,6 +269,12 @@ class SearchEngine {
   };
   std::vector<CandidateList> search_prepared_many(const std::vector<Job>& jobs);
   int max_prepare() const { return max_prep_; }
+  // Allocate up front what prepare(count) and search_prepared_many over
+  // `trials` trials would grow on first use (a growth mid-search frees the
+  // old buffer: hipFree waits for the whole device, every engine's stream)
+  void reserve(int count, int trials);
+  // the acceleration batch search_prepared_many uses for a flat list of ntr trials
+  int batch_for(int ntr) const;
   const SearchParams& params() const { return p_; }
   const SearchCounters& counters() const { return ctr_; }
   void reset_counters() { ctr_ = SearchCounters(); }

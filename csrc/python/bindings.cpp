@@ -709,6 +709,7 @@ PYBIND11_MODULE(_C, m) {
       .def("choose", &Dedisperser::choose, py::arg("d0"), py::arg("d1"))
       .def("mfma_steps_per_channel", &Dedisperser::mfma_steps_per_channel, py::arg("d0"), py::arg("d1"))
       .def("mfma_lds_split", &Dedisperser::mfma_lds_split, py::arg("d0"), py::arg("d1"))
+      .def("warm", &Dedisperser::warm, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly_static("tile_dms", [](py::object) { return Dedisperser::kTileDms; });
 
   py::class_<Whitener>(m, "Whitener")
@@ -754,6 +755,9 @@ PYBIND11_MODULE(_C, m) {
         e.prepare(P<const uint8_t>(trials), row_stride, nsamps, count);
       }, py::arg("trials"), py::arg("row_stride"), py::arg("nsamps"), py::arg("count"),
          py::call_guard<py::gil_scoped_release>())
+      .def("reserve", &SearchEngine::reserve, py::arg("count"), py::arg("trials"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("batch_for", &SearchEngine::batch_for, py::arg("ntr"))
       .def("search_prepared", [](SearchEngine& e, int b, float dm, int dm_idx, const std::vector<float>& accs) {
         return e.search_prepared(b, dm, dm_idx, accs);
       }, py::call_guard<py::gil_scoped_release>())

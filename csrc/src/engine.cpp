@@ -113,6 +113,14 @@ Dedisperser::Dedisperser(const DeviceFilterbank& fb, hipStream_t stream) : fb_(f
     PSOUP_HIP_CHECK(hipMemcpy(d_active_.data(), active.data(), active.size() * 4, hipMemcpyHostToDevice));
 }
 
+void Dedisperser::warm() {
+  const auto& g = fb_.geometry();
+  if (g.dm_list.empty() || g.nactive == 0) return;
+  if (!resident_) build_resident_plan();
+  if (!valu_ready_) build_valu_tables();
+  if (!ml_ready_) build_mfma_lds_tables();
+}
+
 void Dedisperser::build_resident_plan() {
   const auto& g = fb_.geometry();
   const int ndm = static_cast<int>(g.dm_list.size());
@@ -1052,6 +1060,32 @@ CandidateList SearchEngine::search_prepared(int b, float dm, int dm_idx, const s
   return std::move(search_prepared_many(jobs)[0]);
 }
 
+int SearchEngine::batch_for(int ntr) const {
+  // Short trial lists (one DM at 2^23: 685 trials) keep at least min_batches
+  // (default 8, env PSOUP_MIN_BATCHES) batches in the two-slot pipeline so
+  // host clustering still overlaps the GPU, but never fall below k_small_
+  // (the batch an eighth of the budget gives: 64 at 2^23 with the default
+  // 48 GiB, rounded like K_).
+  static const int env_min_batches = [] {
+    const char* e = std::getenv("PSOUP_MIN_BATCHES");
+    return e ? std::max(1, std::atoi(e)) : 0;
+  }();
+  const int min_batches = env_min_batches > 0 ? env_min_batches : std::max(1, p_.min_batches);
+  if (p_.accel_batch <= 0 && ntr < min_batches * K_) {
+    const int even = (ntr + min_batches - 1) / min_batches;
+    return std::min(K_, std::max(k_small_, (even + 7) / 8 * 8));
+  }
+  return K_;
+}
+
+void SearchEngine::reserve(int count, int trials) {
+  count = std::max(1, std::min(count, max_prep_));
+  tim_.resize(n_ * static_cast<uint64_t>(count));
+  wh_->reserve_batch(count);
+  if (mode_ == 2) f4_in_.resize(f4_.insize * static_cast<uint64_t>(count));
+  if (trials > 0) ensure_batch_buffers(std::min(batch_for(trials), trials));
+}
+
 std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<Job>& jobs) {
   RoctxRange dm_range("DM-Loop");
   Stopwatch sw;
@@ -1106,18 +1140,7 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
   // host clustering still overlaps the GPU, but never fall below k_small_
   // (the batch an eighth of the budget gives: 64 at 2^23 with the default
   // 48 GiB, rounded like K_).
-  int kc = K_;
-  {
-    static const int env_min_batches = [] {
-      const char* e = std::getenv("PSOUP_MIN_BATCHES");
-      return e ? std::max(1, std::atoi(e)) : 0;
-    }();
-    const int min_batches = env_min_batches > 0 ? env_min_batches : std::max(1, p_.min_batches);
-    if (p_.accel_batch <= 0 && ntr < min_batches * K_) {
-      const int even = (ntr + min_batches - 1) / min_batches;
-      kc = std::min(K_, std::max(k_small_, (even + 7) / 8 * 8));
-    }
-  }
+  const int kc = batch_for(ntr);
   last_kc_ = kc;
   ensure_batch_buffers(std::min(kc, ntr));
   auto issue = [&](int sl) {

@@ -229,10 +229,12 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
           ds.dfb = std::make_unique<DeviceFilterbank>(geom, ds.stream->get());
           ds.dfb->load_packed_host(fb.data());
           ds.dd = std::make_unique<Dedisperser>(*ds.dfb, ds.stream->get());
+          ds.dd->warm();  // plan tables now, not at the first tile that needs them
           for (int e = 0; e < neng; ++e) {
             if (e > 0) ds.estreams.push_back(std::make_unique<Stream>());
             ds.engines.push_back(std::make_unique<SearchEngine>(
                 setup.search, e > 0 ? ds.estreams.back()->get() : ds.stream->get()));
+            ds.engines.back()->reserve(ds.engines.back()->max_prepare(), 0);
           }
           if (args.npdmp > 0 && prev_power_of_two(geom.out_nsamps) >= 1024) {
             ds.fe = std::make_unique<FoldEngine>(prev_power_of_two(geom.out_nsamps), static_cast<float>(geom.tsamp),

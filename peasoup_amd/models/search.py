@@ -63,6 +63,7 @@ class SearchResult:
 
 
 _SYNC_DEDISP = os.environ.get("PSOUP_SYNC_DEDISP", "0") == "1"  # debug: no dedispersion/search overlap
+_BLOCK_TRACE = os.environ.get("PSOUP_BLOCK_TRACE", "")  # diagnostics: per-block host timeline (JSON lines)
 
 
 _ENGINE_STREAMS: Dict[tuple, object] = {}  # (device index, slot) -> _C.GpuStream, alive for the process
@@ -124,11 +125,13 @@ class RankSearcher:
             if packed is not None:
                 self.load_packed(packed)
             self.dedisperser = _C.Dedisperser(self.dfb, self.stream)
+            self.dedisperser.warm()  # plan tables at setup, not at the first tile that needs them
         self.kernel = {"auto": _C.DedispKernel.Auto, "mfma": _C.DedispKernel.Mfma, "valu": _C.DedispKernel.Valu,
                        "direct": _C.DedispKernel.Direct}[args.dedisp_kernel]
         self.row_stride = _C.Dedisperser.row_stride(self.geom.out_nsamps)
         self.accel_plan = _C.accel_plan_from_args(args, self.header)
         max_trials = max((len(self.accel_list(d)) for d in self.dm_list), default=0)
+        self.max_trials = max_trials
         neng = engines_per_gpu(args, max_trials)
         self.params.engines_per_device = neng  # the auto batch budget is shared among them
         self.engine = _C.SearchEngine(self.params, self.stream)
@@ -269,6 +272,14 @@ class RankSearcher:
 
         dd_events = []
         lock = threading.Lock()
+        if self.engines and width > getattr(self, "_reserved_width", 0):
+            # whitening / batch buffers sized before the timer (growing one
+            # mid-search frees the old buffer, which waits for the whole device)
+            ne = len(self.engines)
+            per_e = max(1, min(self.engine.max_prepare, -(-width // ne)))
+            for e in self.engines:
+                e.reserve(per_e, per_e * self.max_trials)
+            self._reserved_width = width
         cur = pull()  # the first block's dedispersion is issued before the search timer starts
         if t_s:
             t_s.start()
@@ -285,11 +296,16 @@ class RankSearcher:
                 cur = pull()
                 continue
             k, buf, ready, start = inflight
-            nxt = pull()  # its dedispersion overlaps the search below
+            ne = len(self.engines)
+            tb0 = tb1 = time.perf_counter()
+            if ne == 1:
+                nxt = pull()  # its dedispersion overlaps the search below
+                tb1 = time.perf_counter()
             for e in self.engines:
                 ready.wait(e.stream)
             dd_events.append((start, ready))
             per_dm: Dict[int, list] = {}
+            eng_t: Dict[int, list] = {}
 
             def run_dms(e, dms):
                 # this engine's DMs are every ne-th row of the chunk: whitened
@@ -304,25 +320,35 @@ class RankSearcher:
                             raise RuntimeError(f"fault injection: rank {self.ctx.rank} aborting after "
                                                f"{processed} DM trials")
                         processed += len(part)
+                    te0 = time.perf_counter()
                     e.prepare(buf.data_ptr() + (part[0] - d0) * self.row_stride, step * self.row_stride,
                               self.geom.out_nsamps, len(part))
+                    te1 = time.perf_counter()
                     jobs = [(b, self.dm_list[d], d, self.accel_list(self.dm_list[d])) for b, d in enumerate(part)]
                     # one flat trial list over the part's DMs (batches span DM boundaries)
-                    for (b, dm, d, accs), c in zip(jobs, e.search_prepared_many(jobs)):
+                    got = e.search_prepared_many(jobs)
+                    if _BLOCK_TRACE:
+                        eng_t.setdefault(dms[0] - d0, []).append((te0 - tb1, te1 - te0, time.perf_counter() - te1))
+                    for (b, dm, d, accs), c in zip(jobs, got):
                         per_dm[d] = c
                         with lock:
                             ntrials += len(accs)
                             if progress is not None:
                                 progress(1)
 
-            ne = len(self.engines)
             if ne == 1:
                 run_dms(self.engine, range(d0, d1))
             else:
                 futs = [self._executor().submit(run_dms, e, range(d0 + i, d1, ne))
                         for i, e in enumerate(self.engines)]
+                # the next block is issued while the engines run: whatever it
+                # costs on the host (a plan table, a spill read) no longer
+                # leaves the GPU idle
+                nxt = pull()
+                tb1 = time.perf_counter()
                 for f in futs:
                     f.result()
+            tb2 = time.perf_counter()
             chunk_cands: list = []
             for d in range(d0, d1):
                 chunk_cands.extend(per_dm[d])
@@ -336,6 +362,10 @@ class RankSearcher:
             if ck:
                 _C.save_spill(ck, ckey, chunk_cands)  # atomic; raises on a failed write
             cands.extend(chunk_cands)
+            if _BLOCK_TRACE:
+                with open(_BLOCK_TRACE, "a") as f:
+                    f.write(json.dumps({"block": j, "t0": tb0, "pull_s": tb1 - tb0, "search_s": tb2 - tb1,
+                                        "engines": eng_t, "tail_s": time.perf_counter() - tb2}) + "\n")
             cur = nxt
         side.synchronize()
         for e in self.engines:

@@ -1,9 +1,11 @@
 #!/bin/bash
-# --signal bench sweep over the RFI amplitude (peaks per DM vs throughput)
+# Dedisperser plan-table host cost; peak-heavy bench kernel trace.
 set -o pipefail
-O=${O:-gpurun_out/r3c}
+O=gpurun_out/r3sig
 mkdir -p $O
-for amp in 0 0.02 0.05 0.1 0.3; do
-  timeout -k 10 200 python -u bench.py --steps 3 --warmup 1 --signal --rfi-amp $amp > $O/sig_$amp.log 2>&1 || { echo SIG_FAIL $amp; tail -20 $O/sig_$amp.log; exit 1; }
-  echo "amp $amp"; grep '^{"metric"' $O/sig_$amp.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['config']; print(d['value'], c['peaks_per_dm'], c['host_distill_s_per_step'], c['candidates_after_distill'])"
-done
+export TMPDIR=/tmp
+timeout -k 10 200 python3 tools/expt/dedisp_setup_timing.py > $O/dd_setup.log 2>&1 || { echo DD_FAIL; tail -20 $O/dd_setup.log; exit 1; }
+tail -1 $O/dd_setup.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o sig -- python3 bench.py --signal --steps 3 --warmup 1 > $O/sig.log 2>&1 || { echo PROF_FAIL; tail -20 $O/sig.log; exit 1; }
+grep '^{"metric"' $O/sig.log | cut -c1-200
+echo DONE
