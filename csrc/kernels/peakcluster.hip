@@ -143,7 +143,11 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
                                                                   const uint32_t* __restrict__ segcnt, int gap,
                                                                   uint32_t lo_n, uint2* __restrict__ out,
                                                                   uint2* __restrict__ segtab,
-                                                                  uint32_t* __restrict__ total, int stop_after) {
+                                                                  uint32_t* __restrict__ total, int mode) {
+  // mode bits 0-7: timing phase cut (PSOUP_CLUSTER_STOP); bit 8: register
+  // stages in the sort (PSOUP_CLUSTER_RSORT=1, opt-in until measured on the GPU)
+  const int stop_after = mode & 255;
+  const bool rsort = (mode & 256) != 0;
   constexpr uint32_t R = (CAP + kClThreads - 1) / kClThreads;  // rows of kClThreads positions
   __shared__ uint2 key[CAP];      // (idx, snr bits)
   __shared__ uint16_t jmp[CAP];   // next survivor at/after a position, then chain jumps
@@ -168,7 +172,12 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
   __syncthreads();
   // bitonic sort with ascending comparators only (a "flip" stage then half
   // cleaners per merge size): positions >= n act as +inf and never move, so
-  // comparators reaching them are skipped -- no padding
+  // comparators reaching them are skipped -- no padding.  Every stage whose
+  // pairs lie inside one aligned 16-position chunk runs in registers: each
+  // chunk is sorted there first (merge sizes 2..16), and after the LDS stages
+  // of each larger merge size its last four half cleaners (j = 8, 4, 2, 1) are
+  // one register pass -- 66 barriers and LDS round trips instead of 105 at
+  // P = 16384 (opt-in, `rsort`; the all-LDS form is the default).
   auto cswap = [&](uint32_t lo, uint32_t hi) {
     const uint2 a = key[lo], b = key[hi];
     if (static_cast<int>(a.x) > static_cast<int>(b.x)) {
@@ -176,19 +185,77 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
       key[hi] = a;
     }
   };
-  for (uint32_t k = 2; k <= P; k <<= 1) {
-    const uint32_t h = k >> 1;
-    for (uint32_t q = t; q < P / 2; q += kClThreads) {
-      const uint32_t lo = (q / h) * k + (q & (h - 1)), hi = lo ^ (k - 1);
-      if (hi < n) cswap(lo, hi);
+  constexpr int B = 16;
+  auto rswap = [](uint2& a, uint2& b) {
+    const bool sw = static_cast<int>(a.x) > static_cast<int>(b.x);
+    const uint2 lo = sw ? b : a, hi = sw ? a : b;
+    a = lo;
+    b = hi;
+  };
+  auto chunk_pass = [&](bool full) {
+    for (uint32_t c = t; c * B < P; c += kClThreads) {
+      const uint32_t b0 = c * B;
+      uint2 r[B];
+#pragma unroll
+      for (int i = 0; i < B; ++i) r[i] = b0 + i < n ? key[b0 + i] : make_uint2(0x7fffffffu, 0u);
+      if (full) {
+#pragma unroll
+        for (int k = 2; k <= B; k <<= 1) {
+#pragma unroll
+          for (int i = 0; i < B; ++i)
+            if ((i & (k >> 1)) == 0) rswap(r[i], r[i ^ (k - 1)]);
+#pragma unroll
+          for (int j = k >> 2; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < B; ++i)
+              if ((i & j) == 0) rswap(r[i], r[i + j]);
+        }
+      } else {
+#pragma unroll
+        for (int j = B >> 1; j > 0; j >>= 1)
+#pragma unroll
+          for (int i = 0; i < B; ++i)
+            if ((i & j) == 0) rswap(r[i], r[i + j]);
+      }
+#pragma unroll
+      for (int i = 0; i < B; ++i)
+        if (b0 + i < n) key[b0 + i] = r[i];
     }
     __syncthreads();
-    for (uint32_t j = k >> 2; j > 0; j >>= 1) {
+  };
+  if (rsort) {
+    chunk_pass(true);
+    for (uint32_t k = 2 * B; k <= P; k <<= 1) {
+      const uint32_t h = k >> 1;
       for (uint32_t q = t; q < P / 2; q += kClThreads) {
-        const uint32_t lo = 2 * j * (q / j) + (q & (j - 1)), hi = lo + j;
+        const uint32_t lo = (q / h) * k + (q & (h - 1)), hi = lo ^ (k - 1);
         if (hi < n) cswap(lo, hi);
       }
       __syncthreads();
+      for (uint32_t j = k >> 2; j >= static_cast<uint32_t>(B); j >>= 1) {
+        for (uint32_t q = t; q < P / 2; q += kClThreads) {
+          const uint32_t lo = 2 * j * (q / j) + (q & (j - 1)), hi = lo + j;
+          if (hi < n) cswap(lo, hi);
+        }
+        __syncthreads();
+      }
+      chunk_pass(false);
+    }
+  } else {
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+      const uint32_t h = k >> 1;
+      for (uint32_t q = t; q < P / 2; q += kClThreads) {
+        const uint32_t lo = (q / h) * k + (q & (h - 1)), hi = lo ^ (k - 1);
+        if (hi < n) cswap(lo, hi);
+      }
+      __syncthreads();
+      for (uint32_t j = k >> 2; j > 0; j >>= 1) {
+        for (uint32_t q = t; q < P / 2; q += kClThreads) {
+          const uint32_t lo = 2 * j * (q / j) + (q & (j - 1)), hi = lo + j;
+          if (hi < n) cswap(lo, hi);
+        }
+        __syncthreads();
+      }
     }
   }
   if (stop_after == 1) return;  // timing only (PSOUP_CLUSTER_STOP): load + sort
@@ -372,7 +439,8 @@ void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint
   }
   static const int stop = [] {  // timing experiments only: end the kernels after a phase
     const char* e = std::getenv("PSOUP_CLUSTER_STOP");
-    return e ? std::atoi(e) : 99;
+    const char* r = std::getenv("PSOUP_CLUSTER_RSORT");
+    return (e ? std::atoi(e) : 99) | (r && std::atoi(r) == 1 ? 256 : 0);
   }();
   peak_cluster_kernel<kClSmall, kClThreads><<<nseg, kClThreads, 0, s>>>(d_sorted, segoff, segcnt, gap, 0u, d_out,
                                                                          d_segtab, d_total, stop);
