@@ -222,6 +222,10 @@ def main() -> int:
                 "search_s_per_step": round(phase["search"] / a.steps, 4),
                 "merge_s_per_step": round(phase["merge"] / a.steps, 4),
                 "accel_s_per_step": round(ctr.get("accel_s", 0) / a.steps, 4),
+                "accel_distill_s_per_step": round(ctr.get("accd_s", 0) / a.steps, 4),
+                "tail_s_per_step": round(ctr.get("tail_s", 0) / a.steps, 4),
+                "trials_distilled_on_gpu": int(ctr.get("gpu_distilled", 0)),
+                "trials_distilled_on_host": int(ctr.get("host_distilled", 0)),
             },
         }
         print(json.dumps(out), flush=True)

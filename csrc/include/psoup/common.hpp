@@ -17,6 +17,7 @@
 
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <exception>
 #include <functional>
 #include <mutex>
@@ -41,6 +42,13 @@ class Error : public std::runtime_error {
 int log_rank();                 // rank used as log prefix (-1 = none)
 void set_log_rank(int rank);
 bool debug_sync_enabled();      // PSOUP_DEBUG_SYNC env var
+
+// Runtime switches that change candidate numerics (kernel variant flag words,
+// numerics-affecting env knobs), recorded by name for the checkpoint identity
+// (checkpoint.cpp make_run_identity): spills from a run with other switches
+// are never resumed.
+void set_numerics_flag(const std::string& name, long value);
+std::string numerics_flags();   // "name=value ..." sorted by name
 
 [[noreturn]] void throw_error(const std::string& what, const char* file, int line);
 
@@ -315,6 +323,30 @@ class HostPool {
   const std::function<void(int)>* job_ = nullptr;
   int n_ = 0, next_ = 0, active_ = 0;
   uint64_t generation_ = 0;
+  bool stop_ = false;
+  std::exception_ptr err_;
+};
+
+// FIFO of host tasks run asynchronously by `workers` threads (the engine's
+// per-DM acceleration distillation, overlapped with the GPU's next batches).
+// wait() blocks until every submitted task has finished and rethrows the
+// first exception a task raised; the destructor waits without rethrowing.
+class TaskQueue {
+ public:
+  explicit TaskQueue(int workers);
+  ~TaskQueue();
+  TaskQueue(const TaskQueue&) = delete;
+  TaskQueue& operator=(const TaskQueue&) = delete;
+  void submit(std::function<void()> fn);
+  void wait();
+
+ private:
+  void loop();
+  std::vector<std::thread> threads_;
+  std::mutex mu_;
+  std::condition_variable cv_, idle_cv_;
+  std::deque<std::function<void()>> q_;
+  int busy_ = 0;
   bool stop_ = false;
   std::exception_ptr err_;
 };

@@ -240,7 +240,10 @@ struct SearchCounters {
   uint64_t peaks = 0;
   uint64_t overflows = 0;
   uint64_t harm_in = 0, harm_out = 0;  // candidates into / out of the per-trial harmonic distiller
+  uint64_t gpu_distilled = 0, host_distilled = 0;  // trials distilled on the device / on the host
   double whiten_s = 0, accel_s = 0, host_s = 0;
+  double accd_s = 0;    // acceleration distillation (host worker time, mostly overlapped)
+  double tail_s = 0;    // wall time from the last batch's retirement to the call's return
 };
 
 class SearchEngine {
@@ -292,7 +295,7 @@ class SearchEngine {
  private:
   struct Slot {
     DeviceBuffer<kern::PeakRecord> d_peaks;
-    DeviceBuffer<uint32_t> d_count;  // [0] threshold crossings, [1] cluster peaks (GPU clustering)
+    DeviceBuffer<uint32_t> d_count;  // [0] threshold crossings, [1] cluster peaks, [2] distilled candidates
     PinnedBuffer<kern::PeakRecord> h_peaks;
     PinnedBuffer<uint32_t> h_count;
     // GPU clustering (kern::peak_cluster_batch): segment work/table, the
@@ -300,6 +303,10 @@ class SearchEngine {
     DeviceBuffer<uint32_t> d_work;
     DeviceBuffer<uint2> d_sorted, d_clust, d_segtab;
     PinnedBuffer<uint2> h_clust, h_raw, h_segtab;
+    // GPU harmonic distillation (kern::harm_distill_batch): distilled
+    // candidates and the per-trial table; host copies
+    DeviceBuffer<uint2> d_hout, d_ttab;
+    PinnedBuffer<uint2> h_hout, h_ttab;
     std::unique_ptr<Event> done, copied;
     int first = 0, count = 0;
   };
@@ -313,14 +320,24 @@ class SearchEngine {
   // GPU-clustered batch: segtab is the batch's segment table (snapshot taken
   // before the slot was re-issued), cluster peaks in s.h_clust, raw segments
   // in s.h_raw
+  // ttab (GPU harmonic distillation, else null): the batch's per-trial table;
+  // distilled trials' candidates in s.h_hout, the host-flagged trials'
+  // cluster peaks copied into s.h_clust / s.h_raw at their device offsets
   void process_clustered(Slot& s, int first, int count, const std::vector<uint2>& segtab,
-                         std::vector<CandidateList>& out_by_job);
+                         const std::vector<uint2>* ttab, std::vector<CandidateList>& out_by_job);
   // per-trial candidates from (idx, snr) cluster peaks of each level, then the
-  // harmonic distiller; trials [0, count) over the host pool when heavy
+  // harmonic distiller; trials [0, count) over the host pool when heavy.
+  // distilled(k, list), when given, fills trial k's already distilled list and
+  // returns true, or returns false to send the trial through peaks_of.
   void build_trials(int first, int count, size_t work, const std::function<void(int, int, std::vector<int>&,
-                    std::vector<float>&)>& peaks_of, std::vector<CandidateList>& out_by_job);
+                    std::vector<float>&)>& peaks_of, std::vector<CandidateList>& out_by_job,
+                    const std::function<bool(int, CandidateList&)>* distilled = nullptr);
   std::vector<uint2> segtab_;  // segment table snapshot of the batch being processed
+  std::vector<uint2> ttab_;    // its per-trial distillation table
   bool gpu_cluster_ = true;  // env PSOUP_GPU_CLUSTER=0: cluster on the host (reference path)
+  bool gpu_distill_ = true;  // env PSOUP_GPU_DISTILL=0: per-trial harmonic distillation on the host
+  kern::HarmDistillParams hdp_{};
+  std::unique_ptr<TaskQueue> accq_;  // per-DM acceleration distillation as each DM's last batch retires
   // flat trial list of the current search_prepared_many call
   const std::vector<Job>* jobs_ = nullptr;
   std::vector<int> flat_job_;

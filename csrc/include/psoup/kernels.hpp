@@ -378,6 +378,30 @@ constexpr uint32_t kClusterRaw = 0x80000000u;
 void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint32_t cap, uint32_t nseg, int gap,
                         uint32_t* d_work, uint2* d_sorted, uint2* d_out, uint2* d_segtab, uint32_t* d_total,
                         hipStream_t s);
+// Per-trial harmonic distillation on the device (harmdistill.hip;
+// distiller.hpp:63-108, HarmonicDistiller(tol, max_harm, keep_related=false,
+// fractional_harms=true) on the cluster peaks of every level of one trial).
+// For trial k (segments 8k .. 8k + nlevels of peak_cluster_batch's table):
+// d_ttab[k] = {first, count} of its unique candidates in d_out, in
+// descending S/N order -- uint2 = {idx | level << 29, snr bits}; trials packed
+// in any order, *d_total in all -- or {0, kHarmHost} when the host must
+// distill the trial from its cluster peaks: a raw (over-capacity) segment,
+// more than kHarmCap peaks, or two peaks with equal S/N (the reference's
+// introsort order of ties is not reproduced on the device).
+// Equal to the host distiller's output (candidates.cpp, fast relation path:
+// tol <= 1e-3): same double-precision expressions, no contraction.
+struct HarmDistillParams {
+  int nlevels;          // levels 0..nlevels
+  double factor[6];     // freq of bin idx at level h: float(idx * factor[h])
+  float tol;            // freq_tol (float, as HarmonicDistiller::tol_)
+  float max_harm;       // max_harm_match
+  double lower_tol;     // 1 - tol
+  double upper_tol;     // 1 + tol
+};
+constexpr uint32_t kHarmCap = 4096;
+constexpr uint32_t kHarmHost = 0x80000000u;
+void harm_distill_batch(const uint2* d_clust, const uint2* d_segtab, int ntrials, const HarmDistillParams& p,
+                        uint2* d_out, uint2* d_ttab, uint32_t* d_total, hipStream_t s);
 // Tuning: bit 0 = XCD-per-trial block order (default on).
 void harmonic_set_flags(int flags);
 int harmonic_flags();

@@ -1289,7 +1289,10 @@ void launch_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const 
 constexpr int kTimingFlags = kFft4SkipLoad | kFft4SkipStore | kFft4SkipCompute;
 }  // namespace
 
-void fft4_set_flags(int flags) { g_fft4_flags = flags; }
+void fft4_set_flags(int flags) {
+  g_fft4_flags = flags;
+  set_numerics_flag("fft4_flags", flags);
+}
 void fft4_set_trace(unsigned long long* d_events) {
   PSOUP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_fft4_trace), &d_events, sizeof(d_events)));
 }

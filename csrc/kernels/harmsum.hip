@@ -1131,7 +1131,10 @@ void fft4_c2r_post(const float2* Z, uint64_t M, const XLayoutArgs& L, float* x, 
   post_launch_check("c2r_post_kernel", s);
 }
 
-void harmonic_set_flags(int flags) { g_harm_flags = flags; }
+void harmonic_set_flags(int flags) {
+  g_harm_flags = flags;
+  set_numerics_flag("harm_flags", flags);
+}
 int harmonic_flags() { return g_harm_flags; }
 
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,

@@ -601,6 +601,21 @@ PYBIND11_MODULE(_C, m) {
                              S(s));
   });
   k.attr("cluster_cap") = kern::kClusterCap;
+  k.def("harm_distill_batch", [](uintptr_t clust, uintptr_t segtab, int ntrials, int nlevels,
+                                 const std::vector<double>& factor, float tol, float max_harm, uintptr_t out,
+                                 uintptr_t ttab, uintptr_t total, uintptr_t s) {
+    kern::HarmDistillParams p{};
+    p.nlevels = nlevels;
+    PSOUP_CHECK(static_cast<int>(factor.size()) >= nlevels + 1, "harm_distill_batch: one factor per level");
+    for (int h = 0; h <= nlevels; ++h) p.factor[h] = factor[static_cast<size_t>(h)];
+    p.tol = tol;
+    p.max_harm = max_harm;
+    p.lower_tol = 1 - tol;
+    p.upper_tol = 1 + tol;
+    kern::harm_distill_batch(P<const uint2>(clust), P<const uint2>(segtab), ntrials, p, P<uint2>(out), P<uint2>(ttab),
+                             P<uint32_t>(total), S(s));
+  });
+  k.attr("harm_cap") = kern::kHarmCap;
   k.def("harmonic_sums", [](uintptr_t Pin, uint64_t nb, int nlevels, uintptr_t out, uintptr_t s) {
     kern::harmonic_sums(P<const float>(Pin), nb, nlevels, P<float>(out), S(s));
   });
@@ -794,6 +809,10 @@ PYBIND11_MODULE(_C, m) {
         d["harm_out"] = c.harm_out;
         d["accel_s"] = c.accel_s;
         d["host_s"] = c.host_s;
+        d["accd_s"] = c.accd_s;
+        d["tail_s"] = c.tail_s;
+        d["gpu_distilled"] = c.gpu_distilled;
+        d["host_distilled"] = c.host_distilled;
         return d;
       })
       .def("reset_counters", &SearchEngine::reset_counters);

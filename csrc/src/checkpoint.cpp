@@ -131,6 +131,12 @@ RunIdentity make_run_identity(const CmdLineOptions& a, const SigprocHeader& hdr)
      << " boundary_25=" << (a.use_boundaries ? a.boundary_25_freq : 0.5f) << "\n";
   os << "killfile: " << canonical_path(a.killfilename) << " " << file_fingerprint(a.killfilename, false) << "\n";
   os << "zapfile: " << canonical_path(a.zapfilename) << " " << file_fingerprint(a.zapfilename, false) << "\n";
+  // numerics-affecting runtime switches: kernel flag words set through the
+  // API, and the env knobs that select another arithmetic path
+  os << "switches: " << numerics_flags();
+  for (const char* k : {"PSOUP_FUSED_R2C", "PSOUP_WHITEN_ROCFFT"})
+    if (const char* v = std::getenv(k)) os << " " << k << "=" << v;
+  os << "\n";
   RunIdentity id;
   id.text = os.str();
   id.key = fnv1a64(id.text.data(), id.text.size());

@@ -1,5 +1,7 @@
 #include "psoup/common.hpp"
 
+#include <map>
+
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <atomic>
@@ -20,6 +22,26 @@ std::string prefix() {
   return "[rank " + std::to_string(r) + "] ";
 }
 }  // namespace
+
+namespace {
+std::mutex g_numerics_mu;
+std::map<std::string, long>& numerics_map() {
+  static std::map<std::string, long> m;
+  return m;
+}
+}  // namespace
+
+void set_numerics_flag(const std::string& name, long value) {
+  std::lock_guard<std::mutex> lk(g_numerics_mu);
+  numerics_map()[name] = value;
+}
+
+std::string numerics_flags() {
+  std::lock_guard<std::mutex> lk(g_numerics_mu);
+  std::string s;
+  for (const auto& [k, v] : numerics_map()) s += (s.empty() ? "" : " ") + k + "=" + std::to_string(v);
+  return s;
+}
 
 int log_rank() { return g_rank.load(); }
 void set_log_rank(int rank) { g_rank.store(rank); }
@@ -174,6 +196,64 @@ void HostPool::parallel_for(int n, const std::function<void(int)>& fn) {
   job_ = nullptr;
   n_ = 0;
   if (err_) std::rethrow_exception(err_);
+}
+
+TaskQueue::TaskQueue(int workers) {
+  for (int i = 0; i < workers; ++i) threads_.emplace_back([this] { loop(); });
+}
+
+TaskQueue::~TaskQueue() {
+  {
+    std::unique_lock<std::mutex> lk(mu_);
+    idle_cv_.wait(lk, [&] { return q_.empty() && busy_ == 0; });
+    stop_ = true;
+  }
+  cv_.notify_all();
+  for (auto& t : threads_) t.join();
+}
+
+void TaskQueue::submit(std::function<void()> fn) {
+  if (threads_.empty()) {
+    fn();
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    q_.push_back(std::move(fn));
+  }
+  cv_.notify_one();
+}
+
+void TaskQueue::loop() {
+  std::unique_lock<std::mutex> lk(mu_);
+  while (true) {
+    cv_.wait(lk, [&] { return stop_ || !q_.empty(); });
+    if (q_.empty()) return;  // stop_ with nothing left
+    std::function<void()> fn = std::move(q_.front());
+    q_.pop_front();
+    ++busy_;
+    lk.unlock();
+    try {
+      fn();
+    } catch (...) {
+      lk.lock();
+      if (!err_) err_ = std::current_exception();
+      lk.unlock();
+    }
+    lk.lock();
+    --busy_;
+    if (q_.empty() && busy_ == 0) idle_cv_.notify_all();
+  }
+}
+
+void TaskQueue::wait() {
+  std::unique_lock<std::mutex> lk(mu_);
+  idle_cv_.wait(lk, [&] { return q_.empty() && busy_ == 0; });
+  if (err_) {
+    std::exception_ptr e = err_;
+    err_ = nullptr;
+    std::rethrow_exception(e);
+  }
 }
 
 }  // namespace psoup

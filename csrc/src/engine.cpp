@@ -736,15 +736,28 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   for (auto& s : slots_) {
     s.done = std::make_unique<Event>();
     s.copied = std::make_unique<Event>();
-    s.d_count.resize(2);
-    s.h_count.resize(2);
+    s.d_count.resize(3);
+    s.h_count.resize(3);
   }
   if (const char* e = std::getenv("PSOUP_GPU_CLUSTER")) gpu_cluster_ = std::atoi(e) != 0;
+  // per-trial harmonic distillation on the device: needs the device clusters,
+  // the fast relation's tolerance range, and bins that fit the record's 29 bits
+  if (const char* e = std::getenv("PSOUP_GPU_DISTILL")) gpu_distill_ = std::atoi(e) != 0;
+  gpu_distill_ = gpu_distill_ && gpu_cluster_ && p_.freq_tol <= 1e-3f && nb_ < (uint64_t(1) << 29);
+  hdp_.nlevels = nlev_;
+  for (int h = 0; h <= nlev_; ++h) hdp_.factor[h] = bounds_[static_cast<size_t>(h)].factor;
+  hdp_.tol = p_.freq_tol;
+  hdp_.max_harm = static_cast<float>(p_.max_harm);
+  hdp_.lower_tol = 1 - hdp_.tol;  // HarmonicDistiller::run: double(1 -/+ float tol)
+  hdp_.upper_tol = 1 + hdp_.tol;
   grow_capacity(cap_);
   int ht = p_.host_threads;
   if (const char* e = std::getenv("PSOUP_HOST_THREADS")) ht = std::atoi(e);
   if (ht < 0) ht = static_cast<int>(std::min(4u, std::max(1u, std::thread::hardware_concurrency() / 4)));
   if (ht > 1) pool_ = std::make_unique<HostPool>(ht - 1);
+  // acceleration distillation of each DM as its last batch retires, on two
+  // workers of their own (none: synchronous, in the calling thread)
+  accq_ = std::make_unique<TaskQueue>(ht > 1 ? 2 : 0);
 }
 
 SearchEngine::~SearchEngine() {
@@ -761,6 +774,10 @@ void SearchEngine::grow_capacity(uint32_t need) {
       s.d_clust.resize(cap_);
       s.h_clust.resize(cap_);
       s.h_raw.resize(cap_);
+      if (gpu_distill_) {
+        s.d_hout.resize(cap_);
+        s.h_hout.resize(cap_);
+      }
     } else {
       s.h_peaks.resize(cap_);
     }
@@ -778,6 +795,10 @@ void SearchEngine::ensure_batch_buffers(int k) {
       s.d_work.resize(3 * 8 * static_cast<size_t>(k));
       s.d_segtab.resize(8 * static_cast<size_t>(k));
       s.h_segtab.resize(8 * static_cast<size_t>(k));
+      if (gpu_distill_) {
+        s.d_ttab.resize(static_cast<size_t>(k));
+        s.h_ttab.resize(static_cast<size_t>(k));
+      }
     }
   const uint64_t rs = mode_ == 2 ? 2 * f4_.ystride : n_;  // floats per trial
   res_.resize(static_cast<uint64_t>(k) * rs);
@@ -900,8 +921,16 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
                              s.d_count.data() + 1, stream_);
     PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_segtab.data(), s.d_segtab.data(), 8ull * count * sizeof(uint2),
                                    hipMemcpyDeviceToHost, stream_));
+    if (gpu_distill_) {
+      // per-trial harmonic distillation of the cluster peaks: only the
+      // distilled candidates (and the rare host-flagged trials' peaks) go out
+      kern::harm_distill_batch(s.d_clust.data(), s.d_segtab.data(), count, hdp_, s.d_hout.data(), s.d_ttab.data(),
+                               s.d_count.data() + 2, stream_);
+      PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_ttab.data(), s.d_ttab.data(), static_cast<size_t>(count) * sizeof(uint2),
+                                     hipMemcpyDeviceToHost, stream_));
+    }
   }
-  PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_count.data(), s.d_count.data(), 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
+  PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_count.data(), s.d_count.data(), 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, stream_));
   s.done->record(stream_);
 }
 
@@ -946,9 +975,34 @@ void SearchEngine::process_slot(Slot& s, int first, int count, uint32_t npeaks,
 }
 
 void SearchEngine::process_clustered(Slot& s, int first, int count, const std::vector<uint2>& segtab,
-                                     std::vector<CandidateList>& out_by_job) {
+                                     const std::vector<uint2>* ttab, std::vector<CandidateList>& out_by_job) {
   size_t work = 0;
-  for (int i = 0; i < count * 8; ++i) work += segtab[static_cast<size_t>(i)].y & ~kern::kClusterRaw;
+  for (int k = 0; k < count; ++k) {
+    if (ttab && !((*ttab)[static_cast<size_t>(k)].y & kern::kHarmHost)) {
+      work += (*ttab)[static_cast<size_t>(k)].y / 8;  // building the distilled list only
+      continue;
+    }
+    for (int h = 0; h < 8; ++h) work += segtab[static_cast<size_t>(k) * 8 + h].y & ~kern::kClusterRaw;
+  }
+  // a device-distilled trial's list: {idx | level << 29, snr} in S/N order
+  const std::function<bool(int, CandidateList&)> distilled = [&](int k, CandidateList& trial) {
+    const uint2 e = (*ttab)[static_cast<size_t>(k)];
+    if (e.y & kern::kHarmHost) return false;
+    const size_t ft = static_cast<size_t>(first + k);
+    const float acc = flat_acc_[ft];
+    const Job& job = (*jobs_)[static_cast<size_t>(flat_job_[ft])];
+    trial.reserve(e.y);
+    for (uint32_t i = 0; i < e.y; ++i) {
+      const uint2 v = s.h_hout[e.x + i];
+      const int h = static_cast<int>(v.x >> 29);
+      const int idx = static_cast<int>(v.x & ((1u << 29) - 1));
+      float snr;
+      std::memcpy(&snr, &v.y, 4);
+      trial.emplace_back(job.dm, job.dm_idx, acc, h, snr,
+                         static_cast<float>(idx * bounds_[static_cast<size_t>(h)].factor));
+    }
+    return true;
+  };
   build_trials(first, count, work, [&](int k, int h, std::vector<int>& pidx, std::vector<float>& psnr) {
     const uint2 e = segtab[static_cast<size_t>(k * 8 + h)];
     if (e.y == 0) return;
@@ -982,20 +1036,25 @@ void SearchEngine::process_clustered(Slot& s, int first, int count, const std::v
       pidx[i] = static_cast<int>(v.x);
       std::memcpy(&psnr[i], &v.y, 4);
     }
-  }, out_by_job);
+  }, out_by_job, ttab ? &distilled : nullptr);
 }
 
 void SearchEngine::build_trials(int first, int count, size_t work,
                                 const std::function<void(int, int, std::vector<int>&, std::vector<float>&)>& peaks_of,
-                                std::vector<CandidateList>& out_by_job) {
+                                std::vector<CandidateList>& out_by_job,
+                                const std::function<bool(int, CandidateList&)>* distilled) {
   const int L = nlev_ + 1;
   // per-trial results, appended to their jobs' lists in trial order below
   std::vector<CandidateList> per_trial(static_cast<size_t>(count));
-  std::atomic<uint64_t> harm_in{0};
+  std::atomic<uint64_t> harm_in{0}, on_gpu{0};
   auto trial_range = [&](int k0, int k1) {
     std::vector<int> pidx;
     std::vector<float> psnr;
     for (int k = k0; k < k1; ++k) {
+      if (distilled && (*distilled)(k, per_trial[static_cast<size_t>(k)])) {
+        on_gpu++;
+        continue;
+      }
       const size_t ft = static_cast<size_t>(first + k);
       const float acc = flat_acc_[ft];
       const Job& job = (*jobs_)[static_cast<size_t>(flat_job_[ft])];
@@ -1031,6 +1090,8 @@ void SearchEngine::build_trials(int first, int count, size_t work,
     for (auto& c : per_trial[static_cast<size_t>(k)]) dst.push_back(std::move(c));
   }
   ctr_.harm_in += harm_in.load();
+  ctr_.gpu_distilled += on_gpu.load();
+  ctr_.host_distilled += static_cast<uint64_t>(count) - on_gpu.load();
 }
 
 void SearchEngine::prepare(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count) {
@@ -1133,6 +1194,38 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
   PSOUP_HIP_CHECK(hipMemcpyAsync(d_src_.data(), flat_src_.data(), flat_src_.size() * sizeof(uint32_t),
                                  hipMemcpyHostToDevice, stream_));
   RoctxRange acc_range("Acceleration-Loop");
+  // Acceleration distillation (pipeline_multi.cu:243) of each DM as soon as
+  // the batch holding its last trial has been processed, on accq_'s workers
+  // while the GPU runs the next batches: only the last DMs' distillation
+  // remains after the last batch retires.
+  std::vector<CandidateList> out(static_cast<size_t>(njobs));
+  std::vector<int> job_end(static_cast<size_t>(njobs));
+  for (int j = 0, e = 0; j < njobs; ++j) job_end[static_cast<size_t>(j)] = e += static_cast<int>(jobs[static_cast<size_t>(j)].accs.size());
+  std::vector<double> accd_t(static_cast<size_t>(njobs), 0.0);
+  int jobs_sent = 0;
+  struct Drain {  // tasks reference this frame: never leave it with one running
+    TaskQueue* q;
+    ~Drain() {
+      try {
+        q->wait();
+      } catch (...) {
+      }
+    }
+  } drain{accq_.get()};
+  auto send_done = [&](int processed) {
+    while (jobs_sent < njobs && job_end[static_cast<size_t>(jobs_sent)] <= processed) {
+      const int j = jobs_sent++;
+      accq_->submit([this, j, &out, &by_job, &accd_t] {
+        Stopwatch w;
+        w.start();
+        out[static_cast<size_t>(j)] = accd_.distill(std::move(by_job[static_cast<size_t>(j)]));
+        w.stop();
+        accd_t[static_cast<size_t>(j)] = w.get_time();
+      });
+    }
+  };
+  send_done(0);
+  auto last_done = std::chrono::steady_clock::now();
   std::deque<int> inflight;  // slot indices
   int next = 0, slot = 0;
   // Short trial lists (one DM at 2^23: 685 trials) keep at least min_batches
@@ -1158,6 +1251,7 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
     const int sl = inflight.front();
     Slot& s = slots_[sl];
     s.done->sync();
+    last_done = std::chrono::steady_clock::now();
     uint32_t cnt = s.h_count[0];
     if (cnt > cap_) {
       // Peak buffer overflow: drain, grow, recompute every in-flight batch.
@@ -1177,15 +1271,34 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
       // snapshot the segment table (the re-issued launch rewrites it) and
       // copy the cluster peaks plus any raw over-capacity segments
       segtab_.assign(s.h_segtab.data(), s.h_segtab.data() + 8 * static_cast<size_t>(b_count));
-      const uint32_t tot = s.h_count[1];
-      if (tot > 0)
-        PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_clust.data(), s.d_clust.data(), tot * sizeof(uint2), hipMemcpyDeviceToHost,
-                                       copy_stream_.get()));
-      for (const uint2& e : segtab_)
+      auto copy_seg = [&](const uint2& e) {
         if (e.y & kern::kClusterRaw)
           PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_raw.data() + e.x, s.d_sorted.data() + e.x,
                                          (e.y & ~kern::kClusterRaw) * sizeof(uint2), hipMemcpyDeviceToHost,
                                          copy_stream_.get()));
+        else if (e.y > 0)
+          PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_clust.data() + e.x, s.d_clust.data() + e.x, e.y * sizeof(uint2),
+                                         hipMemcpyDeviceToHost, copy_stream_.get()));
+      };
+      if (gpu_distill_) {
+        // the distilled candidates, plus the cluster peaks of the trials the
+        // device left to the host
+        ttab_.assign(s.h_ttab.data(), s.h_ttab.data() + b_count);
+        const uint32_t tot2 = s.h_count[2];
+        if (tot2 > 0)
+          PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_hout.data(), s.d_hout.data(), tot2 * sizeof(uint2),
+                                         hipMemcpyDeviceToHost, copy_stream_.get()));
+        for (int k = 0; k < b_count; ++k)
+          if (ttab_[static_cast<size_t>(k)].y & kern::kHarmHost)
+            for (int h = 0; h <= nlev_; ++h) copy_seg(segtab_[static_cast<size_t>(k) * 8 + h]);
+      } else {
+        const uint32_t tot = s.h_count[1];
+        if (tot > 0)
+          PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_clust.data(), s.d_clust.data(), tot * sizeof(uint2),
+                                         hipMemcpyDeviceToHost, copy_stream_.get()));
+        for (const uint2& e : segtab_)
+          if (e.y & kern::kClusterRaw) copy_seg(e);
+      }
     } else if (cnt > 0) {
       PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_peaks.data(), s.d_peaks.data(), cnt * sizeof(kern::PeakRecord),
                                      hipMemcpyDeviceToHost, copy_stream_.get()));
@@ -1198,30 +1311,19 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
     host.start();
     if (gpu_cluster_) {
       ctr_.peaks += std::min(cnt, cap_);
-      process_clustered(s, b_first, b_count, segtab_, by_job);
+      process_clustered(s, b_first, b_count, segtab_, gpu_distill_ ? &ttab_ : nullptr, by_job);
     } else {
       process_slot(s, b_first, b_count, cnt, by_job);
     }
     host.stop();
     ctr_.accel_trials += static_cast<uint64_t>(b_count);
+    send_done(b_first + b_count);
   }
   ctr_.host_s += host.get_time();
-  std::vector<CandidateList> out(static_cast<size_t>(njobs));
-  // acceleration distillation per DM; the DMs of a candidate-heavy call over the host pool
-  size_t ncand = 0;
-  for (const auto& b : by_job) ncand += b.size();
-  auto accd_range = [&](int j0, int j1) {
-    for (int j = j0; j < j1; ++j) out[static_cast<size_t>(j)] = accd_.distill(std::move(by_job[static_cast<size_t>(j)]));
-  };
-  if (pool_ && njobs > 1 && ncand >= 4096) {
-    const int nparts = std::min(njobs, 4 * pool_->size());
-    pool_->parallel_for(nparts, [&](int q) {
-      accd_range(static_cast<int>(static_cast<int64_t>(njobs) * q / nparts),
-                 static_cast<int>(static_cast<int64_t>(njobs) * (q + 1) / nparts));
-    });
-  } else {
-    accd_range(0, njobs);
-  }
+  send_done(ntr);
+  accq_->wait();
+  for (double t : accd_t) ctr_.accd_s += t;
+  ctr_.tail_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - last_done).count();
   jobs_ = nullptr;
   sw.stop();
   ctr_.accel_s += sw.get_time();
