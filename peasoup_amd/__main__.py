@@ -54,6 +54,7 @@ def main(argv=None) -> int:
 
         rank = os.environ.get("RANK", "0")
         print(f"[rank {rank}] peasoup failed: {e}", file=sys.stderr)
+        pdist.report_failure(f"{type(e).__name__}: {e}")
         traceback.print_exc()
         sys.stderr.flush()
         sys.stdout.flush()

@@ -216,6 +216,9 @@ class RankSearcher:
         ntrials = 0
         ckdir = getattr(self.args, "checkpoint_dir", "") or ""
         fault_after = int(getattr(self.args, "fault_after_dms", -1))
+        fault_rank = int(os.environ.get("PSOUP_FAULT_RANK", "-1"))  # testing: inject on this rank only
+        if fault_rank >= 0 and fault_rank != self.ctx.rank:
+            fault_after = -1
         processed = 0
         ckey = 0
         if ckdir:

@@ -12,11 +12,33 @@ over xGMI on ROCm.  Collectives used by the pipeline:
 * fold-job results (per-candidate fold records)               ``gather_bytes``
 
 On a CPU box (tests) the same code runs on the ``gloo`` backend.
+
+Peer-failure handling (the reference throws and terminates,
+include/utils/exceptions.hpp:13-153).  A multi-rank group must not leave its
+surviving ranks blocked in a collective when one rank fails:
+
+* ``report_failure(msg)``: a failing rank publishes "rank r: msg" under one
+  key of the rendezvous store before it exits non-zero;
+* a watchdog thread on every rank polls that key and the peers' heartbeat
+  counters (``PSOUP_HEARTBEAT_S``, default 1 s); on a published failure, on a
+  peer whose counter has not moved for ``PSOUP_PEER_TIMEOUT`` seconds
+  (default 60: a peer killed without reporting), or when the store itself is
+  gone (rank 0 died), it prints the cause with this rank's context and ends
+  the process with exit code 3 -- which tears down its RCCL communicator (the
+  ``ncclCommAbort`` equivalent) instead of waiting in a collective;
+* every collective is also bounded by the process-group timeout
+  (``PSOUP_COLLECTIVE_TIMEOUT``, default 300 s) as the last backstop.
+No re-exec and no in-process restart: recovery is a re-run (or torchrun's
+``--max-restarts``) with ``--checkpoint_dir``, which resumes from the per-DM
+spill files.
 """
 from __future__ import annotations
 
 import datetime
 import os
+import sys
+import threading
+import time
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -45,7 +67,91 @@ class DistContext:
 _CTX: Optional[DistContext] = None
 
 
-def init(backend: Optional[str] = None, timeout_s: float = 1800.0) -> DistContext:
+_ABORT_KEY = "psoup/abort"
+_WATCHDOG: Optional["_Watchdog"] = None
+
+
+class _Watchdog(threading.Thread):
+    """Heartbeat + failure watch over the rendezvous store (see module doc)."""
+
+    def __init__(self, store, rank: int, world: int, period: float, peer_timeout: float):
+        super().__init__(name="psoup-watchdog", daemon=True)
+        self.store, self.rank, self.world = store, rank, world
+        self.period, self.peer_timeout = period, peer_timeout
+        self.stop = threading.Event()
+        self.beats = 0
+
+    def _abort(self, why: str) -> None:
+        sys.stderr.write(f"[rank {self.rank}] aborting: {why}\n")
+        sys.stderr.flush()
+        sys.stdout.flush()
+        if self.rank == 0:
+            # rank 0 hosts the store: keep it up a few polls so every peer
+            # reads the failure record instead of a vanished store
+            time.sleep(max(1.0, 5 * self.period))
+        os._exit(3)
+
+    def run(self) -> None:
+        seen = {r: (-1, time.monotonic()) for r in range(self.world) if r != self.rank}
+        while not self.stop.wait(self.period):
+            try:
+                self.beats += 1
+                self.store.set(f"psoup/hb/{self.rank}", str(self.beats))
+                if self.store.check([_ABORT_KEY]):
+                    msg = self.store.get(_ABORT_KEY).decode(errors="replace")
+                    if not self.stop.is_set():
+                        self._abort(f"peer failure: {msg}")
+                    return
+                now = time.monotonic()
+                for r, (last, since) in seen.items():
+                    key = f"psoup/hb/{r}"
+                    cur = int(self.store.get(key)) if self.store.check([key]) else -1
+                    if cur != last:
+                        seen[r] = (cur, now)
+                    elif now - since > self.peer_timeout and not self.stop.is_set():
+                        try:
+                            self.store.set(_ABORT_KEY, f"rank {r}: no heartbeat for {now - since:.0f} s")
+                        except Exception:  # noqa: BLE001
+                            pass
+                        self._abort(f"peer failure: rank {r} stopped responding ({now - since:.0f} s without a "
+                                    f"heartbeat)")
+            except Exception as e:  # noqa: BLE001 - the store (rank 0's TCPStore) is gone
+                if self.stop.is_set():
+                    return
+                self._abort(f"lost the rendezvous store ({type(e).__name__}: {e}); rank 0 has failed or exited")
+
+
+def _start_watchdog(ctx: "DistContext") -> None:
+    global _WATCHDOG
+    if ctx.world_size <= 1 or os.environ.get("PSOUP_WATCHDOG", "1") == "0":
+        return
+    from torch.distributed import distributed_c10d
+
+    store = distributed_c10d._get_default_store()
+    period = float(os.environ.get("PSOUP_HEARTBEAT_S", "1.0"))
+    peer_timeout = float(os.environ.get("PSOUP_PEER_TIMEOUT", "60"))
+    store.set(f"psoup/hb/{ctx.rank}", "0")
+    _WATCHDOG = _Watchdog(store, ctx.rank, ctx.world_size, period, peer_timeout)
+    _WATCHDOG.start()
+
+
+def report_failure(msg: str) -> None:
+    """Publish this rank's failure so every peer aborts promptly (call before
+    exiting non-zero).  Best effort: a dead store is not an error here."""
+    ctx = _CTX
+    if ctx is None or not ctx.distributed:
+        return
+    if _WATCHDOG is not None:
+        _WATCHDOG.stop.set()  # this rank exits on its own
+    try:
+        from torch.distributed import distributed_c10d
+
+        distributed_c10d._get_default_store().set(_ABORT_KEY, f"rank {ctx.rank}: {msg}")
+    except Exception:  # noqa: BLE001
+        pass
+
+
+def init(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> DistContext:
     """Initialise (or return) the process group from torchrun-style env vars.
 
     ``backend`` defaults to ``nccl`` (RCCL) when a GPU is visible, else
@@ -57,6 +163,8 @@ def init(backend: Optional[str] = None, timeout_s: float = 1800.0) -> DistContex
     global _CTX
     if _CTX is not None:
         return _CTX
+    if timeout_s is None:
+        timeout_s = float(os.environ.get("PSOUP_COLLECTIVE_TIMEOUT", "300"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -89,6 +197,8 @@ def init(backend: Optional[str] = None, timeout_s: float = 1800.0) -> DistContex
         _C.set_log_rank(rank if world > 1 else -1)
     except Exception:  # pragma: no cover
         pass
+    if _CTX.distributed:
+        _start_watchdog(_CTX)
     return _CTX
 
 
@@ -97,7 +207,15 @@ def context() -> DistContext:
 
 
 def shutdown() -> None:
-    global _CTX
+    global _CTX, _WATCHDOG
+    if _WATCHDOG is not None:
+        # peers may finish (and stop beating) before this rank: a clean
+        # shutdown ends the watch first
+        _WATCHDOG.stop.set()
+        _WATCHDOG.join(timeout=5)
+        _WATCHDOG = None
+        # every rank's watch has ended before rank 0 takes the store down
+        barrier()
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
     _CTX = None

@@ -362,3 +362,42 @@ def test_accmap_tool_finds_injected_delay(tmp_path):
     assert r.returncode == 0, r.stderr
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert abs(d["delays"]["0-1"]) == lag
+
+
+def test_rank_fault_aborts_group_then_resume(tmp_path):
+    """Peer failure, gloo world 3 on the one GPU: rank 1 alone
+    faults after its first DM chunk; every rank exits non-zero within 60 s,
+    the survivors naming rank 1; a re-run with the same --checkpoint_dir
+    resumes from the spills and writes the clean run's candidates byte for byte."""
+    ck = tmp_path / "ck"
+    base = [sys.executable, "-m", "peasoup_amd", "-i", TUTORIAL, "--dm_end", "250", "-n", "3", "--npdmp", "4"]
+    env = dict(os.environ, PYTHONPATH=REPO, MASTER_ADDR="127.0.0.1", WORLD_SIZE="3", PSOUP_DIST_BACKEND="gloo",
+               PSOUP_HEARTBEAT_S="0.5")
+
+    def group(out, extra, extra_env=None):
+        e = dict(env, MASTER_PORT=str(_free_port()), **(extra_env or {}))
+        ps = [subprocess.Popen(base + ["-o", str(out)] + extra, env=dict(e, RANK=str(r), LOCAL_RANK="0"),
+                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, cwd=REPO)
+              for r in range(3)]
+        out_ = []
+        for p in ps:
+            _, err = p.communicate(timeout=600)
+            out_.append((p.returncode, err))
+        return out_
+
+    import time as _time
+
+    t0 = _time.monotonic()
+    res = group(tmp_path / "a", ["--checkpoint_dir", str(ck), "--fault_after_dms", "1", "--dm_schedule", "static"],
+                {"PSOUP_FAULT_RANK": "1"})
+    dt = _time.monotonic() - t0
+    assert dt < 120, dt  # includes three interpreter + GPU start-ups
+    for r, (rc, err) in enumerate(res):
+        assert rc != 0, (r, err[-2000:])
+        assert "rank 1" in err, (r, err[-2000:])
+    assert "[rank 1] peasoup failed: fault injection" in res[1][1]
+    res = group(tmp_path / "b", ["--checkpoint_dir", str(ck), "--dm_schedule", "static"])
+    assert all(rc == 0 for rc, _ in res), [e[-2000:] for _, e in res]
+    res = group(tmp_path / "c", ["--dm_schedule", "static"])
+    assert all(rc == 0 for rc, _ in res), [e[-2000:] for _, e in res]
+    assert (tmp_path / "b" / "candidates.peasoup").read_bytes() == (tmp_path / "c" / "candidates.peasoup").read_bytes()
