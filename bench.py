@@ -65,6 +65,9 @@ def parse():
     p.add_argument("--signal", action="store_true",
                    help="peak-heavy data instead of pure noise: injected pulsars plus strong undispersed periodic "
                         "RFI (>= 1e4 threshold crossings per DM), to time the host clustering / distillation")
+    p.add_argument("--as-rank", default="",
+                   help="N:r[,r...] -- on one GPU, time rank r's shard of a world-N run (the DM list of N ranks, "
+                        "shard [r*dms, (r+1)*dms)), one JSON line per r: checks that every rank's step costs the same")
     p.add_argument("--rfi-amp", type=float, default=0.05,
                    help="--signal: amplitude of the two undispersed RFI pulse trains (the pulsars: 0.05-0.08)")
     return p.parse_args()
@@ -82,6 +85,11 @@ def main() -> int:
         return 2
     ctx = pdist.init()
     dev = ctx.device
+    as_world, as_ranks = 0, []
+    if a.as_rank:
+        w, _, rs_ = a.as_rank.partition(":")
+        as_world, as_ranks = int(w), [int(x) for x in rs_.split(",") if x != ""]
+        assert ctx.world_size == 1 and as_ranks and all(0 <= r < as_world for r in as_ranks), a.as_rank
     if a.fft4_flags >= 0:
         _C.kernels.fft4_set_flags(a.fft4_flags)
     if a.harm_flags >= 0:
@@ -95,7 +103,7 @@ def main() -> int:
     args.infilename = "synthetic"
     args.outdir = "/tmp/peasoup_bench"
     args.dm_start = 0.0
-    need = a.dms_per_gpu * ctx.world_size
+    need = a.dms_per_gpu * (as_world or ctx.world_size)
     dm_end = 5.0
     while True:
         dms = _C.generate_dm_list(0.0, dm_end, a.tsamp, 64.0, fch1, foff, a.nchans, 1.1)
@@ -140,6 +148,8 @@ def main() -> int:
     del packed
     torch.cuda.empty_cache()
 
+    if as_world:
+        return _as_rank(a, rs, args, as_world, as_ranks)
     shard = range(ctx.rank * a.dms_per_gpu, (ctx.rank + 1) * a.dms_per_gpu)
     trials_per_step_local = sum(len(rs.accel_list(rs.dm_list[d])) for d in shard)
     # exact job total: the plan's trial count shrinks slightly with DM (smearing term)
@@ -229,6 +239,38 @@ def main() -> int:
             },
         }
         print(json.dumps(out), flush=True)
+    pdist.shutdown()
+    return 0
+
+
+def _as_rank(a, rs, args, world, ranks) -> int:
+    """Time, on this one GPU, the step of each given rank of a world-N run:
+    its shard's dedispersion + search + the candidate merge (a world of one)."""
+    from peasoup_amd import _C
+    from peasoup_amd.parallel import dist as pdist
+
+    for r in ranks:
+        shard = range(r * a.dms_per_gpu, (r + 1) * a.dms_per_gpu)
+        trials = sum(len(rs.accel_list(rs.dm_list[d])) for d in shard)
+
+        def step():
+            local = rs.search(shard, chunk=a.dms_per_gpu)
+            local.sort(key=lambda c: c.dm_idx)
+            return _C.global_distill_and_score(local, args, rs.header)
+
+        for _ in range(a.warmup):
+            step()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            step()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        print(json.dumps({"as_rank": r, "world": world, "dms": [shard.start, shard.stop],
+                          "dm_range": [round(rs.dm_list[shard.start], 3), round(rs.dm_list[shard.stop - 1], 3)],
+                          "trials_per_step": trials, "ms_per_step": round(1e3 * el / a.steps, 3),
+                          "trials_per_s": round(trials * a.steps / el, 2),
+                          "dedisp_kernel": a.dedisp_kernel, "signal": bool(a.signal)}), flush=True)
     pdist.shutdown()
     return 0
 

@@ -112,8 +112,7 @@ class Dedisperser {
   void run_mfma_lds(int d0, int d1, uint8_t* out, uint64_t out_stride, hipStream_t s);
   const DeviceFilterbank& fb_;
   hipStream_t stream_;
-  DeviceBuffer<int32_t> d_offsets_, d_kill_, d_active_, d_steps_, d_tile_info_, d_list_offT_;
-  DeviceBuffer<int8_t> d_deltas_;
+  DeviceBuffer<int32_t> d_offsets_, d_kill_, d_active_, d_list_offT_;
   bool resident_ = false, valu_ready_ = false;
   std::vector<int32_t> h_tile_steps_;  // resident plan: MFMA steps per tile
   int ldo_ = 0;                        // columns of r_offT_

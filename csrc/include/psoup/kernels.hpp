@@ -79,9 +79,11 @@ struct MfmaDedispPlan {
 void build_mfma_dedisp_plan(const int32_t* offsets, int ndm, int nchans, const int32_t* killmask,
                             MfmaDedispPlan& plan);
 // Reads up to 560 bytes past out_nsamps + max offset in each channel row.
+// d_skip: the first tile's leading DMs before the range (not stored); out is
+// the range's first DM.
 void dedisperse_mfma(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_steps, const int8_t* d_deltas,
                      const int32_t* d_tile_info, int ntiles, int ndm, uint64_t out_nsamps, uint8_t* out,
-                     uint64_t out_stride, float scale, int bias_total, hipStream_t s);
+                     uint64_t out_stride, float scale, int bias_total, hipStream_t s, int d_skip = 0);
 
 // LDS-fed one-hot MFMA dedispersion (dedisperse_mfma_lds_kernel): per
 // 32-DM tile and group of kMfmaLdsGroup active channels, the channel windows
@@ -112,7 +114,7 @@ void build_mfma_lds_plan(const int32_t* offsets, int ndm, int nchans, const int3
 void dedisperse_mfma_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_active, int nactive,
                          const int32_t* d_steps, const uint8_t* d_relo, const int32_t* d_ginfo, int ngroups,
                          const int32_t* d_wmin, int ntiles, int ndm, uint64_t out_nsamps, uint8_t* out,
-                         uint64_t out_stride, float scale, int bias_total, hipStream_t s);
+                         uint64_t out_stride, float scale, int bias_total, hipStream_t s, int d_skip = 0);
 
 // Packed-byte VALU dedispersion (wide-spread DM tiles), bit-identical to
 // dedisperse_direct.  d_offT: int32 [nactive][ldo] offsets of active channel
@@ -122,10 +124,12 @@ void dedisperse_valu(const int8_t* chan_major, uint64_t chan_stride, const int32
                      const int32_t* d_offT, int ldo, int d_base, int ndm, uint64_t out_nsamps, uint8_t* out,
                      uint64_t out_stride, float scale, int nbits, int bias, hipStream_t s);
 
-// LDS-staged packed-byte kernel: same contract as dedisperse_valu for ranges
-// starting on a 32-DM tile, plus d_wmin [tile][nactive] = each tile's
-// smallest offset per channel rounded down to 16 and max_window = the largest
-// (tile, channel) window 1024 + (max offset - wmin) + 32 bytes.
+// LDS-staged packed-byte kernel: same contract as dedisperse_valu for the
+// DMs [d0, d0 + ndm) of the offset table (any d0: workgroups start on their
+// DM-count boundary below d0 and skip the DMs before it), plus d_wmin
+// [absolute 32-DM tile][nactive] = each tile's smallest offset per channel
+// rounded down to 16 and max_window = the largest (tile, channel) window
+// 1024 + (max offset - wmin) + 32 bytes.
 bool dedisperse_lds_fits(int nbits, int nactive, int max_window);
 void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_active, int nactive,
                     const int32_t* d_offT, int ldo, int d_base, int ndm, const int32_t* d_wmin, int max_window,

@@ -83,7 +83,7 @@ constexpr int kMfmaWgSamples = 4 * 32 * kMfmaWaveTiles;  // 512
 
 __global__ void __launch_bounds__(256) dedisperse_mfma_kernel(
     const int8_t* __restrict__ x, uint64_t stride, const int4* __restrict__ steps, const int8_t* __restrict__ deltas,
-    const int2* __restrict__ tile_info, int ndm, uint64_t out_nsamps, uint8_t* __restrict__ out,
+    const int2* __restrict__ tile_info, int ndm, int d_skip, uint64_t out_nsamps, uint8_t* __restrict__ out,
     uint64_t out_stride, float scale, int bias_total, uint64_t ntime_tiles) {
   const int tile = blockIdx.x;  // DM tile (fastest: concurrent WGs share the x window in L2)
   const int wave = threadIdx.x >> 6;
@@ -128,8 +128,9 @@ __global__ void __launch_bounds__(256) dedisperse_mfma_kernel(
       }
     }
     // C/D layout (32x32): col = lane&31 (DM), row = (reg&3) + 8*(reg>>2) + 4*(lane>>5) (sample)
-    const int d = tile * 32 + r;
-    if (d < ndm) {
+    // DMs before the range's first (its first tile's leading d_skip) are not stored
+    const int d = tile * 32 + r - d_skip;
+    if (d >= 0 && d < ndm) {
       uint8_t* o = out + static_cast<uint64_t>(d) * out_stride;
 #pragma unroll
       for (int m = 0; m < kMfmaWaveTiles; ++m) {
@@ -323,7 +324,7 @@ __device__ __forceinline__ void lds_accumulate_bytes(const uint32_t* w, uint32_t
 template <bool XOR, int PASSES, int DPT, int CPB, bool BYTES = false>
 __global__ void __launch_bounds__(256) dedisperse_lds_kernel(
     const int8_t* __restrict__ x, uint64_t stride, const int32_t* __restrict__ active, int nactive,
-    const int32_t* __restrict__ offT, int ldo, int d_base, int ndm, const int32_t* __restrict__ wmin,
+    const int32_t* __restrict__ offT, int ldo, int d_base, int d_skip, int ndm, const int32_t* __restrict__ wmin,
     uint64_t out_nsamps, uint8_t* __restrict__ out, uint64_t out_stride, float scale, int flush) {
   // CPB channels' windows per LDS buffer (one barrier per CPB channels),
   // double-buffered; each window is PASSES x 4 KiB
@@ -332,11 +333,14 @@ __global__ void __launch_bounds__(256) dedisperse_lds_kernel(
   // workgroups per CU to hide the channel-window loads)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
+  // d_base is a multiple of the workgroup's 4*DPT DMs, so every workgroup
+  // lies in one absolute 32-DM tile of the window table; its first d_skip
+  // DMs (before the range) are computed but not stored
   const int dm0 = blockIdx.x * (4 * DPT) + wave * DPT;  // relative to d_base
-  const int tile = (blockIdx.x * 4 * DPT) / 32;
+  const int tile = (d_base + static_cast<int>(blockIdx.x) * 4 * DPT) / 32;
   const uint64_t tb = static_cast<uint64_t>(blockIdx.y) * 1024;
   const uint64_t t = tb + static_cast<uint64_t>(lane) * 16;
-  const int32_t* wm = wmin + static_cast<uint64_t>(d_base / 32 + tile) * nactive;
+  const int32_t* wm = wmin + static_cast<uint64_t>(tile) * nactive;
   uint32_t pk[DPT][8];
 #pragma unroll
   for (int j = 0; j < DPT; ++j)
@@ -435,8 +439,9 @@ __global__ void __launch_bounds__(256) dedisperse_lds_kernel(
   if (t >= out_nsamps) return;
 #pragma unroll
   for (int j = 0; j < DPT; ++j) {
-    const int d = dm0 + j;
+    const int d = dm0 + j - d_skip;
     if (d >= ndm) break;
+    if (d < 0) continue;
     uint32_t ob[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -474,8 +479,8 @@ template <int CG>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) dedisperse_mfma_lds_kernel(
     const int8_t* __restrict__ x, uint64_t stride, const int32_t* __restrict__ active, int nactive,
     const uint32_t* __restrict__ steps, const uint8_t* __restrict__ relo, const int2* __restrict__ ginfo,
-    int ngroups, const int32_t* __restrict__ wmin, int ndm, uint64_t out_nsamps, uint8_t* __restrict__ out,
-    uint64_t out_stride, float scale, int bias_total) {
+    int ngroups, const int32_t* __restrict__ wmin, int ndm, int d_skip, uint64_t out_nsamps,
+    uint8_t* __restrict__ out, uint64_t out_stride, float scale, int bias_total) {
   // per buffer: CG windows, then kMfmaLdsMaxSteps step words, then the
   // CG x 32 relo bytes (all 16-byte units)
   constexpr int kWinU = CG * kMlWin / 16;            // window units
@@ -599,8 +604,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) d
   }
   // C/D layout (32x32): col = lane&31 (DM), row = (reg&3) + 8*(reg>>2) + 4*(lane>>5);
   // sub-tiles m = 0..7 of a (lane, reg) are the 8 consecutive samples 8*row + m
-  const int d = tile * 32 + r;
-  if (d >= ndm) return;
+  const int d = tile * 32 + r - d_skip;  // the first tile's leading d_skip DMs are not stored
+  if (d < 0 || d >= ndm) return;
   uint8_t* o = out + static_cast<uint64_t>(d) * out_stride;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
@@ -704,13 +709,15 @@ void build_mfma_dedisp_plan(const int32_t* offsets, int ndm, int nchans, const i
 
 void dedisperse_mfma(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_steps, const int8_t* d_deltas,
                      const int32_t* d_tile_info, int ntiles, int ndm, uint64_t out_nsamps, uint8_t* out,
-                     uint64_t out_stride, float scale, int bias_total, hipStream_t s) {
+                     uint64_t out_stride, float scale, int bias_total, hipStream_t s, int d_skip) {
   if (ndm <= 0 || out_nsamps == 0) return;
   PSOUP_CHECK(ntiles <= 65535, "too many DM tiles");
+  PSOUP_CHECK(d_skip >= 0 && d_skip < 32 && d_skip + ndm <= 32 * ntiles, "dedisperse_mfma: bad tile range");
   const uint64_t ntt = (out_nsamps + kMfmaWgSamples - 1) / kMfmaWgSamples;
   dim3 grid(static_cast<unsigned>(ntiles), static_cast<unsigned>(std::min<uint64_t>(ntt, 65535)));
   dedisperse_mfma_kernel<<<grid, 256, 0, s>>>(chan_major, chan_stride, reinterpret_cast<const int4*>(d_steps),
-                                               d_deltas, reinterpret_cast<const int2*>(d_tile_info), ndm, out_nsamps,
+                                               d_deltas, reinterpret_cast<const int2*>(d_tile_info), ndm, d_skip,
+                                               out_nsamps,
                                                out, out_stride, scale,
                                                bias_total, ntt);
   post_launch_check("dedisperse_mfma_kernel", s);
@@ -836,16 +843,18 @@ void build_mfma_lds_plan(const int32_t* offsets, int ndm, int nchans, const int3
 void dedisperse_mfma_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_active, int nactive,
                          const int32_t* d_steps, const uint8_t* d_relo, const int32_t* d_ginfo, int ngroups,
                          const int32_t* d_wmin, int ntiles, int ndm, uint64_t out_nsamps, uint8_t* out,
-                         uint64_t out_stride, float scale, int bias_total, hipStream_t s) {
+                         uint64_t out_stride, float scale, int bias_total, hipStream_t s, int d_skip) {
   if (ndm <= 0 || out_nsamps == 0 || nactive <= 0) return;
-  PSOUP_CHECK(ntiles >= 1 && ntiles <= 65535 && ndm <= 32 * ntiles, "dedisperse_mfma_lds: bad tile range");
+  PSOUP_CHECK(ntiles >= 1 && ntiles <= 65535 && d_skip >= 0 && d_skip < 32 && d_skip + ndm <= 32 * ntiles,
+              "dedisperse_mfma_lds: bad tile range");
   PSOUP_CHECK((chan_stride & 15) == 0, "dedisperse_mfma_lds: stride alignment");
   const uint64_t ty = (out_nsamps + kMlTs - 1) / kMlTs;
   PSOUP_CHECK(ty <= 65535, "dedisperse_mfma_lds: series too long for the grid");
   dim3 grid(static_cast<unsigned>(ntiles), static_cast<unsigned>(ty));
   dedisperse_mfma_lds_kernel<kMfmaLdsGroup><<<grid, 256, 0, s>>>(
       chan_major, chan_stride, d_active, nactive, reinterpret_cast<const uint32_t*>(d_steps), d_relo,
-      reinterpret_cast<const int2*>(d_ginfo), ngroups, d_wmin, ndm, out_nsamps, out, out_stride, scale, bias_total);
+      reinterpret_cast<const int2*>(d_ginfo), ngroups, d_wmin, ndm, d_skip, out_nsamps, out, out_stride, scale,
+      bias_total);
   post_launch_check("dedisperse_mfma_lds_kernel", s);
 }
 
@@ -855,11 +864,11 @@ bool dedisperse_lds_fits(int nbits, int nactive, int max_window) {
 }
 
 void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_active, int nactive,
-                    const int32_t* d_offT, int ldo, int d_base, int ndm, const int32_t* d_wmin, int max_window,
+                    const int32_t* d_offT, int ldo, int d0, int ndm, const int32_t* d_wmin, int max_window,
                     uint64_t out_nsamps, uint8_t* out, uint64_t out_stride, float scale, int nbits, int bias,
                     hipStream_t s) {
   if (ndm <= 0 || out_nsamps == 0 || nactive <= 0) return;
-  PSOUP_CHECK(d_base % 32 == 0, "dedisperse_lds: range must start on a 32-DM tile");
+  PSOUP_CHECK(d0 >= 0, "dedisperse_lds: negative first DM");
   PSOUP_CHECK(dedisperse_lds_fits(nbits, nactive, max_window), "dedisperse_lds: window or sums too large");
   PSOUP_CHECK((chan_stride & 15) == 0 && (out_stride & 15) == 0, "dedisperse_lds: stride alignment");
   const uint64_t ty = (out_nsamps + 1023) / 1024;
@@ -872,7 +881,11 @@ void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_
   // a launch of <= 8 DMs (the headline bench's per-rank chunk) fills 8-DM
   // workgroups instead of half-empty 16-DM ones
   const int dpt = dpt_env ? dpt_env : (ndm <= 8 ? 2 : 4);
-  dim3 grid(static_cast<unsigned>((ndm + 4 * dpt - 1) / (4 * dpt)), static_cast<unsigned>(ty));
+  // workgroups start on multiples of their 4*dpt DMs (one absolute tile's
+  // window each): a range from any DM starts at the workgroup boundary below
+  // it and skips the DMs before d0
+  const int d_base = d0 / (4 * dpt) * (4 * dpt), d_skip = d0 - d_base;
+  dim3 grid(static_cast<unsigned>((ndm + d_skip + 4 * dpt - 1) / (4 * dpt)), static_cast<unsigned>(ty));
   PSOUP_CHECK(d_base + static_cast<int>(grid.x) * 4 * dpt <= ldo, "dedisperse_lds: offset table too narrow");
   const bool two = max_window > 4096;
   const bool xr = bias == 128;
@@ -894,18 +907,21 @@ void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_
   if (bytes) {
     if (dpt == 4)
       dedisperse_lds_kernel<false, 1, 4, 1, true><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive,
-                                                                       d_offT, ldo, d_base, ndm, d_wmin, out_nsamps,
-                                                                       out, out_stride, scale, flush);
+                                                                       d_offT, ldo, d_base, d_skip, ndm + d_skip,
+                                                                       d_wmin, out_nsamps, out, out_stride, scale,
+                                                                       flush);
     else
       dedisperse_lds_kernel<false, 1, 2, 1, true><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive,
-                                                                       d_offT, ldo, d_base, ndm, d_wmin, out_nsamps,
-                                                                       out, out_stride, scale, flush);
+                                                                       d_offT, ldo, d_base, d_skip, ndm + d_skip,
+                                                                       d_wmin, out_nsamps, out, out_stride, scale,
+                                                                       flush);
     post_launch_check("dedisperse_lds_kernel", s);
     return;
   }
 #define PSOUP_LDS_LAUNCH(X, P, D, C)                                                                           \
   dedisperse_lds_kernel<X, P, D, C><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive, d_offT, ldo, \
-                                                         d_base, ndm, d_wmin, out_nsamps, out, out_stride, scale, 255)
+                                                         d_base, d_skip, ndm + d_skip, d_wmin, out_nsamps, out,      \
+                                                         out_stride, scale, 255)
 #define PSOUP_LDS_ONE(X)                                      \
   if (two) {                                                  \
     if (dpt == 8) PSOUP_LDS_LAUNCH(X, 2, 8, 1);               \

@@ -206,7 +206,7 @@ DedispKernel Dedisperser::choose(int d0, int d1) {
   if (!valu_ready_) build_valu_tables();
   int win = 0;
   for (int T = d0 / kTileDms; T <= (d1 - 1) / kTileDms; ++T) win = std::max(win, h_tile_win_[static_cast<size_t>(T)]);
-  const bool lds = d0 % kTileDms == 0 && kern::dedisperse_lds_fits(g.nbits, g.nactive, win);
+  const bool lds = kern::dedisperse_lds_fits(g.nbits, g.nactive, win);
   const double ratio = lds ? valu_ratio() * (1.0 / 1.85) : valu_ratio();
   return mfma_steps_per_channel(d0, d1) > ratio ? DedispKernel::Valu : DedispKernel::Mfma;
 }
@@ -247,7 +247,7 @@ static double mfma_lds_ratio() {
 
 int Dedisperser::mfma_lds_split(int d0, int d1) {
   const auto& g = fb_.geometry();
-  if (d0 % kTileDms != 0 || g.nactive == 0 || mfma_lds_ratio() <= 0) return d0;
+  if (g.nactive == 0 || mfma_lds_ratio() <= 0) return d0;
   if (!ml_ready_) build_mfma_lds_tables();
   int T = d0 / kTileDms;
   const int T1 = (d1 - 1) / kTileDms + 1;
@@ -265,12 +265,13 @@ int Dedisperser::mfma_lds_split(int d0, int d1) {
 void Dedisperser::run_mfma_lds(int d0, int d1, uint8_t* out, uint64_t out_stride, hipStream_t s) {
   const auto& g = fb_.geometry();
   if (!ml_ready_) build_mfma_lds_tables();
-  const int T0 = d0 / kTileDms, nt = (d1 - d0 + kTileDms - 1) / kTileDms;
+  // whole tiles from the one holding d0; its DMs before d0 are not stored
+  const int T0 = d0 / kTileDms, skip = d0 - T0 * kTileDms, nt = (d1 - T0 * kTileDms + kTileDms - 1) / kTileDms;
   kern::dedisperse_mfma_lds(fb_.data(), fb_.stride(), d_active_.data(), g.nactive, ml_steps_.data(),
                             ml_relo_.data() + static_cast<size_t>(T0) * ml_ngroups_ * kern::kMfmaLdsGroup * 32,
                             ml_ginfo_.data() + static_cast<size_t>(T0) * ml_ngroups_ * 2,
                             ml_ngroups_, ml_wmin_.data() + static_cast<size_t>(T0) * g.nactive, nt, d1 - d0,
-                            g.out_nsamps, out, out_stride, g.out_scale, g.bias * g.nactive, s);
+                            g.out_nsamps, out, out_stride, g.out_scale, g.bias * g.nactive, s, skip);
 }
 
 void Dedisperser::run_list(const std::vector<int>& dms, uint8_t* out, uint64_t out_stride, hipStream_t s) {
@@ -310,8 +311,12 @@ void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispK
   if (!s) s = stream_;
   RoctxRange r("Dedisperse");
   const int ndm_list = static_cast<int>(g.dm_list.size());
-  const bool aligned = d0 % kTileDms == 0 && (d1 % kTileDms == 0 || d1 == ndm_list);
-  if (kind == DedispKernel::Auto && g.nactive > 0 && d0 % kTileDms == 0) {
+  (void)ndm_list;
+  // Every kernel below takes any DM range: a range not starting on a 32-DM
+  // tile computes its first tile (or workgroup) whole and stores from d0, so
+  // every rank of a DM-sharded run dedisperses with the same kernels and no
+  // per-call host tables.
+  if (kind == DedispKernel::Auto && g.nactive > 0) {
     // hybrid: the leading narrow-spread tiles on the LDS-fed MFMA kernel, the
     // rest (tile-aligned from the split) on the VALU kernels
     const int split = mfma_lds_split(d0, d1);
@@ -321,8 +326,8 @@ void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispK
       return;
     }
   }
-  if (kind == DedispKernel::Mfma && aligned && g.nactive > 0) {
-    // explicit MFMA on whole tiles: the LDS-fed kernel where every tile fits its window
+  if (kind == DedispKernel::Mfma && g.nactive > 0) {
+    // explicit MFMA: the LDS-fed kernel where every tile fits its window
     if (!ml_ready_) build_mfma_lds_tables();
     bool fit = true;
     for (int T = d0 / kTileDms; T <= (d1 - 1) / kTileDms; ++T) fit = fit && ml_tile_ok_[static_cast<size_t>(T)];
@@ -342,7 +347,7 @@ void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispK
     }();
     int win = 0;
     for (int T = d0 / kTileDms; T <= (d1 - 1) / kTileDms; ++T) win = std::max(win, h_tile_win_[static_cast<size_t>(T)]);
-    if (lds_on && d0 % kTileDms == 0 && kern::dedisperse_lds_fits(g.nbits, g.nactive, win))
+    if (lds_on && kern::dedisperse_lds_fits(g.nbits, g.nactive, win))
       kern::dedisperse_lds(fb_.data(), fb_.stride(), d_active_.data(), g.nactive, r_offT_.data(), ldo_, d0, ndm,
                            r_wmin_.data(), win, g.out_nsamps, out, out_stride, g.out_scale, g.nbits, g.bias, s);
     else
@@ -350,30 +355,13 @@ void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispK
                             g.out_nsamps, out, out_stride, g.out_scale, g.nbits, g.bias, s);
     return;
   }
-  const int ntiles = (ndm + kTileDms - 1) / kTileDms;
-  const int ndm_all = static_cast<int>(g.dm_list.size());
-  if (kind == DedispKernel::Mfma && d0 % kTileDms == 0 && (d1 % kTileDms == 0 || d1 == ndm_all)) {
-    // whole tiles of the resident plan cover exactly these DMs
+  if (kind == DedispKernel::Mfma) {
+    // whole tiles of the resident plan from the one holding d0
     if (!resident_) build_resident_plan();
-    kern::dedisperse_mfma(fb_.data(), fb_.stride(), r_steps_.data(), r_deltas_.data(),
-                          r_tile_info_.data() + 2 * (d0 / kTileDms), ntiles, ndm, g.out_nsamps, out, out_stride,
-                          g.out_scale, g.bias * g.nactive, s);
-  } else if (kind == DedispKernel::Mfma) {
-    std::vector<int32_t> offs = g.offsets(d0, d1);
-    std::vector<int32_t> kill(g.killmask.begin(), g.killmask.end());
-    kern::MfmaDedispPlan plan;
-    kern::build_mfma_dedisp_plan(offs.data(), ndm, g.nchans, kill.data(), plan);
-    PSOUP_CHECK(plan.ntiles == ntiles, "MFMA plan tile count");
-    d_steps_.resize(plan.steps.size());
-    d_deltas_.resize(plan.deltas.size());
-    d_tile_info_.resize(plan.tile_info.size());
-    PSOUP_HIP_CHECK(hipMemcpyAsync(d_steps_.data(), plan.steps.data(), plan.steps.size() * 4, hipMemcpyHostToDevice, s));
-    PSOUP_HIP_CHECK(hipMemcpyAsync(d_deltas_.data(), plan.deltas.data(), plan.deltas.size(), hipMemcpyHostToDevice, s));
-    PSOUP_HIP_CHECK(hipMemcpyAsync(d_tile_info_.data(), plan.tile_info.data(), plan.tile_info.size() * 4,
-                                   hipMemcpyHostToDevice, s));
-    PSOUP_HIP_CHECK(hipStreamSynchronize(s));  // host tables go out of scope
-    kern::dedisperse_mfma(fb_.data(), fb_.stride(), d_steps_.data(), d_deltas_.data(), d_tile_info_.data(), ntiles,
-                          ndm, g.out_nsamps, out, out_stride, g.out_scale, g.bias * g.nactive, s);
+    const int T0 = d0 / kTileDms, skip = d0 - T0 * kTileDms;
+    const int ntiles = (d1 - T0 * kTileDms + kTileDms - 1) / kTileDms;
+    kern::dedisperse_mfma(fb_.data(), fb_.stride(), r_steps_.data(), r_deltas_.data(), r_tile_info_.data() + 2 * T0,
+                          ntiles, ndm, g.out_nsamps, out, out_stride, g.out_scale, g.bias * g.nactive, s, skip);
   } else {
     std::vector<int32_t> offs = g.offsets(d0, d1);
     d_offsets_.resize(offs.size());

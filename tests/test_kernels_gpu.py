@@ -111,6 +111,16 @@ def test_dedisperse_1024ch_hybrid_mfma_bit_exact(C):
     o = torch.zeros((ndm - 32) * stride, dtype=torch.uint8, device=dev)
     dd.run(32, ndm, o.data_ptr(), stride, C.DedispKernel.Auto)
     assert torch.equal(o.view(ndm - 32, stride)[:, : g.out_nsamps], ref_[32:])
+    # ranges that do not start on a 32-DM tile (DM-sharded ranks: the bench's
+    # [8r, 8r + 8), static shards cut anywhere): every kernel, no per-call plan
+    for d0, d1 in ((8, 16), (24, 32), (40, 48), (1, 9), (5, 70), (13, 40), (33, 97), (100, 101),
+                   (split - 3, split + 37), (250, ndm)):
+        for k in (C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto):
+            o = torch.zeros((d1 - d0 + 2) * stride, dtype=torch.uint8, device=dev)  # a guard row each side
+            dd.run(d0, d1, o.data_ptr() + stride, stride, k)
+            got = o.view(d1 - d0 + 2, stride)
+            assert torch.equal(got[1: d1 - d0 + 1, : g.out_nsamps], ref_[d0:d1]), (d0, d1, k)
+            assert not got[0].any() and not got[d1 - d0 + 1].any(), (d0, d1, k)  # nothing stored outside
     # the fold stage's scattered DM list (unsorted, a repeat, > one 32-DM tile)
     lst = [int(v) for v in rng.choice(ndm, 40, replace=False)] + [7, 7]
     o = torch.zeros(len(lst) * stride, dtype=torch.uint8, device=dev)
@@ -119,8 +129,9 @@ def test_dedisperse_1024ch_hybrid_mfma_bit_exact(C):
 
 
 def test_mfma_resident_plan_ranges_and_side_stream(C):
-    """Whole-tile ranges use the resident plan (ragged per-tile step lists),
-    other ranges a per-call plan; both bit-exact, also on a side stream."""
+    """Every range uses the resident plan (ragged per-tile step lists; a
+    range inside a tile skips the tile's leading DMs): bit-exact, also on a
+    side stream."""
     rng = np.random.default_rng(11)
     nchans, nsamps = 64, 6000
     hdr, dms = _geometry(C, nchans=nchans, nbits=2, nsamps=nsamps, dm_end=900.0)
