@@ -61,6 +61,10 @@ class DeviceFilterbank {
   void load_packed_device(const uint8_t* d_packed);
   // Packed bytes in host memory (H2D in chunks through pinned staging).
   void load_packed_host(const uint8_t* h_packed);
+  // Samples [t0, t0 + ns) from their packed bytes on this device (stream s;
+  // nullptr = the constructor's stream).
+  void unpack_chunk(const uint8_t* d_packed, uint64_t t0, uint64_t ns, hipStream_t s = nullptr);
+  hipStream_t stream() const { return stream_; }
   const int8_t* data() const { return chan_.data(); }
   uint64_t stride() const { return stride_; }
   const DedispGeometry& geometry() const { return g_; }
@@ -72,15 +76,25 @@ class DeviceFilterbank {
   DeviceBuffer<int8_t> chan_;
 };
 
+// One host upload, then a device-to-device fan-out (SURVEY.md §2.7, §5.8
+// item 1): the packed filterbank goes host -> devs[0] in chunks through pinned
+// staging; every other device copies each chunk from devs[0] as it lands
+// (hipMemcpyPeerAsync: SDMA over xGMI, all peers in parallel on their own
+// links) and unpacks it while the next chunk is in flight.  fbs[i] lives on
+// HIP device devices[i] (the same device may repeat: a device-local copy).
+// Returns when every device holds its unpacked filterbank.
+void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std::vector<int>& devices,
+                            const uint8_t* h_packed);
+
 class Dedisperser {
  public:
   Dedisperser(const DeviceFilterbank& fb, hipStream_t stream);
   // DM trials [d0, d1) -> out[(d-d0)*out_stride + t], t < out_nsamps, on
   // stream s (nullptr = the constructor's stream).  MFMA runs made of whole
-  // kTileDms-DM tiles (d0 and d1 multiples of it, or d1 = the list's end) use
-  // the resident whole-DM-list plan (built on first use, one upload) and never
-  // block the host; other ranges build a plan for [d0, d1) and wait for its
-  // upload.
+  // Every range (tile-aligned or not) runs on the resident tables (built on
+  // first use or by warm(), one upload each) and never blocks the host; a
+  // range not starting on a tile computes its first tile (or workgroup) whole
+  // and stores from d0.
   void run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispKernel kind = DedispKernel::Auto,
            hipStream_t s = nullptr);
   // An arbitrary list of DM indices (row i = DM dms[i]) in ONE packed-byte

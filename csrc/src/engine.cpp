@@ -100,6 +100,66 @@ void DeviceFilterbank::load_packed_host(const uint8_t* h_packed) {
   PSOUP_HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
+void DeviceFilterbank::unpack_chunk(const uint8_t* d_packed, uint64_t t0, uint64_t ns, hipStream_t s) {
+  PSOUP_CHECK(t0 + ns <= g_.nsamps, "unpack_chunk: samples past the filterbank");
+  kern::unpack_transpose(d_packed, ns, g_.nchans, g_.nbits, chan_.data() + t0, stride_, g_.bias, s ? s : stream_);
+}
+
+void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std::vector<int>& devices,
+                            const uint8_t* h_packed) {
+  PSOUP_CHECK(!fbs.empty() && fbs.size() == devices.size(), "load_filterbank_fanout: one device per filterbank");
+  const DedispGeometry& g = fbs[0]->geometry();
+  const uint64_t bps = static_cast<uint64_t>(g.nchans) * g.nbits / 8;  // bytes per sample
+  const uint64_t bytes = g.nsamps * bps;
+  const uint64_t chunk = std::max<uint64_t>(256, ((64ull << 20) / bps) / 256 * 256);  // samples per chunk
+  int prev = 0;
+  PSOUP_HIP_CHECK(hipGetDevice(&prev));
+  const size_t n = fbs.size();
+  // the packed bytes on every device (transient: freed on return)
+  std::vector<DeviceBuffer<uint8_t>> packed(n);
+  for (size_t i = 0; i < n; ++i) {
+    PSOUP_HIP_CHECK(hipSetDevice(devices[i]));
+    packed[i].resize(bytes);
+  }
+  PSOUP_HIP_CHECK(hipSetDevice(devices[0]));
+  PinnedBuffer<uint8_t> stage[2];
+  Event staged[2], landed;
+  for (int i = 0; i < 2; ++i) stage[i].resize(chunk * bps);
+  bool used[2] = {false, false};
+  hipStream_t s0 = fbs[0]->stream();
+  int slot = 0;
+  for (uint64_t t0 = 0; t0 < g.nsamps; t0 += chunk, slot ^= 1) {
+    const uint64_t ns = std::min(chunk, g.nsamps - t0);
+    const uint64_t off = t0 * bps, nb = ns * bps;
+    PSOUP_HIP_CHECK(hipSetDevice(devices[0]));
+    if (used[slot]) staged[slot].sync();
+    std::memcpy(stage[slot].data(), h_packed + off, nb);
+    PSOUP_HIP_CHECK(hipMemcpyAsync(packed[0].data() + off, stage[slot].data(), nb, hipMemcpyHostToDevice, s0));
+    staged[slot].record(s0);
+    used[slot] = true;
+    landed.record(s0);
+    fbs[0]->unpack_chunk(packed[0].data() + off, t0, ns);
+    for (size_t i = 1; i < n; ++i) {
+      PSOUP_HIP_CHECK(hipSetDevice(devices[i]));
+      hipStream_t si = fbs[i]->stream();
+      PSOUP_HIP_CHECK(hipStreamWaitEvent(si, landed.get(), 0));
+      PSOUP_HIP_CHECK(hipMemcpyPeerAsync(packed[i].data() + off, devices[i], packed[0].data() + off, devices[0], nb, si));
+      fbs[i]->unpack_chunk(packed[i].data() + off, t0, ns);
+    }
+  }
+  for (size_t i = 0; i < n; ++i) {
+    PSOUP_HIP_CHECK(hipSetDevice(devices[i]));
+    PSOUP_HIP_CHECK(hipStreamSynchronize(fbs[i]->stream()));
+  }
+  PSOUP_HIP_CHECK(hipSetDevice(prev));
+  // the transient copies are freed on their own devices
+  for (size_t i = 0; i < n; ++i) {
+    PSOUP_HIP_CHECK(hipSetDevice(devices[i]));
+    packed[i] = DeviceBuffer<uint8_t>();
+  }
+  PSOUP_HIP_CHECK(hipSetDevice(prev));
+}
+
 Dedisperser::Dedisperser(const DeviceFilterbank& fb, hipStream_t stream) : fb_(fb), stream_(stream) {
   const auto& g = fb_.geometry();
   std::vector<int32_t> kill(g.killmask.begin(), g.killmask.end());

@@ -213,10 +213,28 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   res.performance["engines_per_gpu"] = neng;
   setup.search.engines_per_device = neng;  // the auto batch budget is shared among them
 
-  // phase 1: resident filterbank per device (host-to-device upload + unpack,
-  // timed as part of "reading")
+  // phase 1: resident filterbank per device, timed as part of "reading": one
+  // host upload to the first device and a chunk-pipelined device-to-device
+  // fan-out to the others (load_filterbank_fanout) -- not one host upload
+  // per device -- then each device's tables and engines in parallel
   t_read.start();
   {
+    Stopwatch wf;
+    wf.start();
+    std::vector<DeviceFilterbank*> fbs;
+    std::vector<int> phys;
+    for (int dev = 0; dev < ngpu; ++dev) {
+      PSOUP_HIP_CHECK(hipSetDevice(hip_dev(dev)));
+      DevState& ds = devs[static_cast<size_t>(dev)];
+      ds.stream = std::make_unique<Stream>();
+      ds.dfb = std::make_unique<DeviceFilterbank>(geom, ds.stream->get());
+      fbs.push_back(ds.dfb.get());
+      phys.push_back(hip_dev(dev));
+    }
+    load_filterbank_fanout(fbs, phys, fb.data());
+    wf.stop();
+    res.performance["filterbank_load_s"] = wf.get_time();
+    res.performance["filterbank_devices"] = ngpu;
     std::vector<std::thread> lth;
     for (int dev = 0; dev < ngpu; ++dev)
       lth.emplace_back([&, dev] {
@@ -225,9 +243,6 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
           DevState& ds = devs[static_cast<size_t>(dev)];
           Stopwatch wl;
           wl.start();
-          ds.stream = std::make_unique<Stream>();
-          ds.dfb = std::make_unique<DeviceFilterbank>(geom, ds.stream->get());
-          ds.dfb->load_packed_host(fb.data());
           ds.dd = std::make_unique<Dedisperser>(*ds.dfb, ds.stream->get());
           ds.dd->warm();  // plan tables now, not at the first tile that needs them
           for (int e = 0; e < neng; ++e) {

@@ -264,7 +264,7 @@ def test_engines_per_gpu_do_not_change_results(tmp_path):
 
 def test_native_oversubscribed_device_workers_match_one(tmp_path):
     """PSOUP_OVERSUBSCRIBE=1: `peasoup -t 4` runs four device workers (feeder +
-    engine threads, per-device filterbank upload, DM queue, fold
+    engine threads, one filterbank upload fanned out device to device, DM queue, fold
     distribution) on the one GPU; the candidates file and every candidate
     field of the overview equal the -t 1 run's."""
     exe = os.path.join(REPO, "bin", "peasoup")
@@ -283,8 +283,11 @@ def test_native_oversubscribed_device_workers_match_one(tmp_path):
         assert o1.get_candidate(i) == o4.get_candidate(i), i
     import json
 
-    devs = json.load(open(tmp_path / "4.json"))["devices"]
+    tr = json.load(open(tmp_path / "4.json"))
+    devs = tr["devices"]
     assert len(devs) == 4 and sum(d["dm_trials"] for d in devs) == 59
+    # one host upload fanned out device to device (all four workers)
+    assert tr["performance"]["filterbank_devices"] == 4 and tr["performance"]["filterbank_load_s"] > 0
     assert sum(1 for d in devs if d["dm_trials"] > 0) >= 2  # the DM queue was shared
 
 
