@@ -1068,7 +1068,7 @@ fft4_rowpass_r2c_kernel(const float2* __restrict__ Y, float* __restrict__ P, uin
 
   const uint32_t M = static_cast<uint32_t>(L) * static_cast<uint32_t>(n2);
   const float* st = stats + (tsrc ? 4u * tsrc[k] : 0u);
-  const float mean = st[0] * nscale, rsig = 1.0f / (st[2] * nscale);
+  const float mean = st[0] * nscale, sigma = st[2] * nscale, rsig = 1.0f / sigma;
   float* pk = P + static_cast<uint64_t>(k) * pstride;
   const float2* rk = tab + to.rk;             // e^{-i pi k1 / n1}
   const float2* rc = tab + to.rc + 8 * o;     // e^{-i pi c / M}, c = 8o + j
@@ -1103,9 +1103,9 @@ fft4_rowpass_r2c_kernel(const float2* __restrict__ Y, float* __restrict__ P, uin
     }
     float pa[8], pm[8];
 #pragma unroll
-    for (int j = 1; j <= 8; ++j) pa[j - 1] = (dev::interbin(xa[j], xa[j - 1]) - mean) * rsig;
+    for (int j = 1; j <= 8; ++j) pa[j - 1] = dev::div_rn(dev::interbin(xa[j], xa[j - 1]) - mean, sigma, rsig);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) pm[7 - j] = (dev::interbin(xm[j], xm[j + 1]) - mean) * rsig;
+    for (int j = 0; j < 8; ++j) pm[7 - j] = dev::div_rn(dev::interbin(xm[j], xm[j + 1]) - mean, sigma, rsig);
     const uint32_t base = static_cast<uint32_t>(8 * o) + static_cast<uint32_t>(n2) * k1;  // c = 8o
     if (base + 1 < nbins_out) {  // ascending bins base+1 .. base+8: octet column o, row k1
       f4v* d = reinterpret_cast<f4v*>(pk + (static_cast<uint64_t>(o) * L + k1) * 8);
@@ -1117,7 +1117,7 @@ fft4_rowpass_r2c_kernel(const float2* __restrict__ Y, float* __restrict__ P, uin
       d[0] = f4v{pm[0], pm[1], pm[2], pm[3]};
       d[1] = f4v{pm[4], pm[5], pm[6], pm[7]};
     }
-    if (o == 0 && k1 == 0) pk[M] = (dev::interbin(xa[0], make_float2(0.f, 0.f)) - mean) * rsig;  // bin 0
+    if (o == 0 && k1 == 0) pk[M] = dev::div_rn(dev::interbin(xa[0], make_float2(0.f, 0.f)) - mean, sigma, rsig);  // bin 0
   }
   trace_event(11);
 }

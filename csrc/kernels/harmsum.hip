@@ -37,12 +37,12 @@ __global__ void __launch_bounds__(256) interbin_normalise_batch_kernel(const flo
   float* p = P + static_cast<uint64_t>(k) * pstride;
   const float mean = stats[0] * nscale;
   const float sigma = stats[2] * nscale;
-  const float rsig = 1.0f / sigma;  // one division per thread, not one per bin
+  const float rsig = 1.0f / sigma;  // one division per thread; per bin dev::div_rn
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < nbins_out; i += stride) {
     float2 xl = i > 0 ? x[i - 1] : make_float2(0.f, 0.f);
     float v = dev::interbin(x[i], xl);
-    p[i] = (v - mean) * rsig;
+    p[i] = dev::div_rn(v - mean, sigma, rsig);
   }
 }
 
@@ -85,7 +85,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
   if (tsrc) stats += 4 * tsrc[kk];  // multi-series batch: this trial's whitening stats
   const float mean = stats[0] * nscale;
   const float sigma = stats[2] * nscale;
-  const float rsig = 1.0f / sigma;  // one division per thread, not one per bin
+  const float rsig = 1.0f / sigma;  // one division per thread; per bin dev::div_rn
   const uint64_t half = M / 2;
   const float invM = 1.0f / static_cast<float>(M);  // M a power of two: x * invM == x / M exactly
   float2 wu[kR2cBpt];  // W^(256 u), W = e^{-i pi / M}
@@ -135,10 +135,10 @@ __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
       if (k <= half) {
         if (k < nbins_out) {
           const float2 xl = k > 0 ? A[slot - 1] : make_float2(0.f, 0.f);
-          p[k] = (dev::interbin(A[slot], xl) - mean) * rsig;
+          p[k] = dev::div_rn(dev::interbin(A[slot], xl) - mean, sigma, rsig);
         }
         const uint64_t j = M - k;  // mirrored bin (> M/2), neighbour X[j-1] = D[slot+1]
-        if (j > half && j < nbins_out) p[j] = (dev::interbin(D[slot], D[slot + 1]) - mean) * rsig;
+        if (j > half && j < nbins_out) p[j] = dev::div_rn(dev::interbin(D[slot], D[slot + 1]) - mean, sigma, rsig);
       }
     }
     __syncthreads();
@@ -182,7 +182,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* _
   if (tsrc) stats += 4 * tsrc[kk];  // multi-series batch: this trial's whitening stats
   const float mean = stats[0] * nscale;
   const float sigma = stats[2] * nscale;
-  const float rsig = 1.0f / sigma;  // one division per thread, not one per bin
+  const float rsig = 1.0f / sigma;  // one division per thread; per bin dev::div_rn
   const uint64_t g0 = static_cast<uint64_t>(blockIdx.y) * 8;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * 256;
   auto xbin = [&](uint64_t k, float2& xa, float2& xm) {  // generic: X[k] and X[M-k]
@@ -239,16 +239,16 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* _
     const uint64_t k = (g0 + r) * n2 + k2;
     if (k < nbins_out) {
       const float2 xl = k > 0 ? A[r][t] : make_float2(0.f, 0.f);
-      p[k] = (dev::interbin(A[r][t + 1], xl) - mean) * rsig;
+      p[k] = dev::div_rn(dev::interbin(A[r][t + 1], xl) - mean, sigma, rsig);
     }
     const uint64_t j = M - k;  // > M/2 for every k in the ascending rows
-    if (j < nbins_out) p[j] = (dev::interbin(D[r][t + 1], D[r][t + 2]) - mean) * rsig;
+    if (j < nbins_out) p[j] = dev::div_rn(dev::interbin(D[r][t + 1], D[r][t + 2]) - mean, sigma, rsig);
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && half < nbins_out) {  // bin M/2 (row n1/2, column 0)
     float2 xa, xm, la, lm;
     xbin(half, xa, xm);
     xbin(half - 1, la, lm);
-    p[half] = (dev::interbin(xa, la) - mean) * rsig;
+    p[half] = dev::div_rn(dev::interbin(xa, la) - mean, sigma, rsig);
   }
 }
 
@@ -358,7 +358,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
   if (tsrc) stats += 4 * tsrc[kk];
   const float mean = stats[0] * nscale;
   const float sigma = stats[2] * nscale;
-  const float rsig = 1.0f / sigma;  // one division per thread, not one per bin
+  const float rsig = 1.0f / sigma;  // one division per thread; per bin dev::div_rn
   const uint64_t g0 = static_cast<uint64_t>(blockIdx.y) * 8;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * 256;
   auto xbin = [&](uint64_t k, float2& xa, float2& xm) {  // generic: X[k] and X[M-k]
@@ -427,16 +427,16 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
     const uint64_t k = (g0 + r) * n2 + k2;
     if (k < nbins_out) {
       if (k == 0) xl = make_float2(0.f, 0.f);
-      p[k] = (dev::interbin(xa[r], xl) - mean) * rsig;
+      p[k] = dev::div_rn(dev::interbin(xa[r], xl) - mean, sigma, rsig);
     }
     const uint64_t j = M - k;
-    if (j < nbins_out) p[j] = (dev::interbin(xm[r], xr) - mean) * rsig;
+    if (j < nbins_out) p[j] = dev::div_rn(dev::interbin(xm[r], xr) - mean, sigma, rsig);
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && half < nbins_out) {  // bin M/2 (row n1/2, column 0)
     float2 ha, hm, la, lm;
     xbin(half, ha, hm);
     xbin(half - 1, la, lm);
-    p[half] = (dev::interbin(ha, la) - mean) * rsig;
+    p[half] = dev::div_rn(dev::interbin(ha, la) - mean, sigma, rsig);
   }
 }
 

@@ -254,12 +254,22 @@ class RankSearcher:
             k = nissued[0] % 2
             nissued[0] += 1
             start, ready = _C.GpuEvent(True), _C.GpuEvent(True)
+            buf = None
             if self.keep_trials:
                 # a fresh buffer per block, kept for the fold stage (never reused
-                # during the search, so no wait on the previous user)
-                buf = torch.empty((d1 - d0) * self.row_stride, dtype=torch.uint8, device=dev)
-                self.resident_rows[d0] = (d1, buf)
-            else:
+                # during the search, so no wait on the previous user).  The store
+                # is sized by keep_trials_fits for this rank's even share; a
+                # dynamic-schedule rank that claims far more and runs out of HBM
+                # keeps the rows it has and searches on from the double buffer
+                # (the fold stage re-dedisperses the rows nobody kept).
+                try:
+                    buf = torch.empty((d1 - d0) * self.row_stride, dtype=torch.uint8, device=dev)
+                    self.resident_rows[d0] = (d1, buf)
+                except torch.cuda.OutOfMemoryError:
+                    warnings.warn(f"rank {self.ctx.rank}: no HBM left to keep DM rows {d0}..{d1 - 1}; keeping no "
+                                  "further rows (the fold stage re-dedisperses them)")
+                    self.keep_trials = False
+            if buf is None:
                 if k >= len(bufs):
                     bufs.append(torch.empty(width * self.row_stride, dtype=torch.uint8, device=dev))
                 buf = bufs[k]
@@ -360,8 +370,7 @@ class RankSearcher:
                 ev = _C.GpuEvent()
                 ev.record(e.stream)
                 evs.append(ev)
-            if not self.keep_trials:
-                freed[k] = evs
+            freed[k] = evs  # the double buffer's slot k is free once these retire
             if ck:
                 _C.save_spill(ck, ckey, chunk_cands)  # atomic; raises on a failed write
             cands.extend(chunk_cands)
