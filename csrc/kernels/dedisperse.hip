@@ -439,8 +439,8 @@ __global__ void __launch_bounds__(256) dedisperse_lds_kernel(
   if (t >= out_nsamps) return;
 #pragma unroll
   for (int j = 0; j < DPT; ++j) {
+    if (dm0 + j >= ndm) break;  // ndm counts from d_base
     const int d = dm0 + j - d_skip;
-    if (d >= ndm) break;
     if (d < 0) continue;
     uint32_t ob[4];
 #pragma unroll

@@ -53,6 +53,16 @@ def main(argv=None) -> int:
         import traceback
 
         rank = os.environ.get("RANK", "0")
+        peer = pdist.peer_failure()
+        if peer is not None:
+            # a peer failed first and this rank's collective broke with it
+            print(f"[rank {rank}] aborting: peer failure: {peer}", file=sys.stderr)
+            sys.stderr.flush()
+            if rank == "0":
+                import time
+
+                time.sleep(2.0)  # rank 0 hosts the store: let the other peers read the record
+            os._exit(3)
         print(f"[rank {rank}] peasoup failed: {e}", file=sys.stderr)
         pdist.report_failure(f"{type(e).__name__}: {e}")
         traceback.print_exc()

@@ -151,6 +151,24 @@ def report_failure(msg: str) -> None:
         pass
 
 
+def peer_failure() -> Optional[str]:
+    """The failure record a peer published ("rank r: msg"), or None.  A rank
+    whose collective broke because a peer exited checks this first, so it
+    reports the peer's failure, not the broken connection."""
+    ctx = _CTX
+    if ctx is None or not ctx.distributed:
+        return None
+    try:
+        from torch.distributed import distributed_c10d
+
+        store = distributed_c10d._get_default_store()
+        if store.check([_ABORT_KEY]):
+            return store.get(_ABORT_KEY).decode(errors="replace")
+    except Exception:  # noqa: BLE001
+        pass
+    return None
+
+
 def init(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> DistContext:
     """Initialise (or return) the process group from torchrun-style env vars.
 

@@ -36,7 +36,7 @@ def _trial(rng, n, nlev, df, ties=False):
             if 0 < b < (1 << 28):
                 idx.add(b)
         idx = np.array(sorted(idx), np.int32)
-        snr = (9.0 + 80.0 * rng.random(m) ** 3).astype(np.float32)
+        snr = (9.0 + 80.0 * rng.random(m)).astype(np.float32)
         if ties and m > 3:
             snr[2] = snr[0]
         levels.append((idx, snr))
@@ -78,13 +78,16 @@ def test_harm_distill_matches_host(C):
     ttab = d_ttab.cpu().numpy().view(np.uint32).reshape(nt, 2)
     out = d_out.cpu().numpy().view(np.uint32).reshape(-1, 2)
     hd = C.HarmonicDistiller(tol, max_harm, False, True)
-    total = 0
+    total = ndev = 0
     for k, n in enumerate(sizes):
         first, cnt = int(ttab[k, 0]), int(ttab[k, 1])
-        if k in (raw_trial, tie_trial) or n > cap:
+        allsnr = np.concatenate([snr for _, snr in trials[k]]) if n else np.zeros(0, np.float32)
+        tie = len(np.unique(allsnr)) < len(allsnr)
+        if k in (raw_trial, tie_trial) or n > cap or tie:
             assert cnt == HOST, (k, hex(cnt))
             continue
         assert not cnt & HOST, (k, n)
+        ndev += 1
         cands = []
         for h, (idx, snr) in enumerate(trials[k]):
             for i, v in zip(idx, snr):
@@ -101,6 +104,7 @@ def test_harm_distill_matches_host(C):
             assert len(exp) < n  # the relation removed candidates
         total += cnt
     assert int(d_tot.item()) == total
+    assert ndev >= 10, ndev  # most trials distilled on the device
 
 
 def _search(C, trial, nsamps, accs, cluster, distill):
