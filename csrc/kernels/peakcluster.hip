@@ -20,14 +20,12 @@
 // next(i) = the first survivor with idx >= idx_i + gap, and so on (a run's
 // last anchor has every later survivor of its run within the gap, so its
 // next is the following run's start).
-// peak_cluster_kernel: one workgroup per segment (trial x level): bitonic
+// peak_cluster_kernel: one workgroup per segment (trial x level): radix
 // sort by idx in LDS, the window test (1) and next() in parallel (a suffix
 // scan gives the next survivor at or after any position), one thread follows
 // the chain (one LDS read per peak), a scan compacts the peaks in idx order.
 // Segments over kClusterCap crossings are left to the host (flagged in the
 // segment table with their raw, unsorted range).
-#include <cstdlib>
-
 #include "device_common.hpp"
 
 namespace psoup {
@@ -134,28 +132,64 @@ __global__ void __launch_bounds__(256) seg_scatter_kernel(const PeakRecord* __re
       out[lb[rec[r].seg] + rank[r]] = make_uint2(static_cast<uint32_t>(rec[r].idx), __float_as_uint(rec[r].snr));
 }
 
+// Exclusive scan of one value per thread over the block (TH threads): wave
+// scans by shuffles, one wave scans the wave totals; two barriers.
+template <int TH>
+__device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t* wtot, uint32_t* total) {
+  constexpr int W = TH / 64;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t incl = v;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const uint32_t u = __shfl_up(incl, off, 64);
+    if (lane >= off) incl += u;
+  }
+  if (lane == 63) wtot[w] = incl;
+  __syncthreads();
+  if (w == 0) {
+    uint32_t x = lane < W ? wtot[lane] : 0u, xi = x;
+#pragma unroll
+    for (int off = 1; off < W; off <<= 1) {
+      const uint32_t u = __shfl_up(xi, off, 64);
+      if (lane >= off) xi += u;
+    }
+    if (lane < W) wtot[lane] = xi - x;  // exclusive wave offsets
+    if (lane == W - 1 && total) *total = xi;
+  }
+  __syncthreads();
+  return wtot[w] + incl - v;
+}
+
 // One workgroup per segment with lo_n < n <= CAP crossings (the small
 // kernel also writes the empty segments' entries, the large one the raw
 // entries of segments over its capacity).
+//
+// Sort by idx: an LSD radix sort with 4-bit digits of idx - min(idx) (as many
+// passes as the segment's idx span needs: 5-6 for a whole-spectrum RFI
+// segment).  Between passes the keys live in registers (R per thread,
+// position r * TH + t); a pass ranks each key stably among its digit by wave
+// ballots (16 per row of TH keys), scans the (digit, row, wave) counts and
+// scatters into LDS, then reads the keys back in the new order -- 4 barriers
+// per pass, where the bitonic network it replaces needed ~O(log^2 n) (105 at
+// 14000 crossings), each a full LDS round trip.  The counts alias the jump
+// table, which is only used after the sort.
 template <uint32_t CAP, int kClThreads>
 __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* __restrict__ sorted,
                                                                   const uint32_t* __restrict__ segoff,
                                                                   const uint32_t* __restrict__ segcnt, int gap,
                                                                   uint32_t lo_n, uint2* __restrict__ out,
                                                                   uint2* __restrict__ segtab,
-                                                                  uint32_t* __restrict__ total, int mode) {
-  // mode bits 0-7: timing phase cut (PSOUP_CLUSTER_STOP); bit 8: register
-  // stages in the sort (PSOUP_CLUSTER_RSORT=1, opt-in until measured on the GPU)
-  const int stop_after = mode & 255;
-  const bool rsort = (mode & 256) != 0;
+                                                                  uint32_t* __restrict__ total) {
   constexpr uint32_t R = (CAP + kClThreads - 1) / kClThreads;  // rows of kClThreads positions
+  constexpr uint32_t kW = kClThreads / 64;
+  constexpr uint32_t kCnt = 16 * R * kW;  // radix counts (digit, row, wave)
   __shared__ uint2 key[CAP];      // (idx, snr bits)
-  __shared__ uint16_t jmp[CAP];   // next survivor at/after a position, then chain jumps
+  __shared__ uint16_t jmp[CAP > 2 * kCnt ? CAP : 2 * kCnt];  // next survivor / chain jumps; radix counts before
   __shared__ uint8_t flag[CAP];   // bit 0: survives the window test, bit 1: cluster peak
   __shared__ uint32_t sc[kClThreads];
   __shared__ uint32_t wcnt[kClThreads / 64];   // per wave: first survivor of the row
   __shared__ uint32_t rw[R * (kClThreads / 64)];  // per (row, wave): peak count, then its output offset
-  __shared__ uint32_t base_s, first_s;
+  __shared__ uint32_t base_s, first_s, lo_s, hi_s;
   const int t = threadIdx.x;
   const uint32_t seg = blockIdx.x;
   const uint32_t n = segcnt[seg], off = segoff[seg];
@@ -166,105 +200,106 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
     }
     return;
   }
-  for (uint32_t i = t; i < n; i += kClThreads) key[i] = sorted[off + i];
-  uint32_t P = 2;
-  while (P < n) P <<= 1;
-  __syncthreads();
-  // bitonic sort with ascending comparators only (a "flip" stage then half
-  // cleaners per merge size): positions >= n act as +inf and never move, so
-  // comparators reaching them are skipped -- no padding.  Every stage whose
-  // pairs lie inside one aligned 16-position chunk runs in registers: each
-  // chunk is sorted there first (merge sizes 2..16), and after the LDS stages
-  // of each larger merge size its last four half cleaners (j = 8, 4, 2, 1) are
-  // one register pass -- 66 barriers and LDS round trips instead of 105 at
-  // P = 16384 (opt-in, `rsort`; the all-LDS form is the default).
-  auto cswap = [&](uint32_t lo, uint32_t hi) {
-    const uint2 a = key[lo], b = key[hi];
-    if (static_cast<int>(a.x) > static_cast<int>(b.x)) {
-      key[lo] = b;
-      key[hi] = a;
-    }
-  };
-  constexpr int B = 16;
-  auto rswap = [](uint2& a, uint2& b) {
-    const bool sw = static_cast<int>(a.x) > static_cast<int>(b.x);
-    const uint2 lo = sw ? b : a, hi = sw ? a : b;
-    a = lo;
-    b = hi;
-  };
-  auto chunk_pass = [&](bool full) {
-    for (uint32_t c = t; c * B < P; c += kClThreads) {
-      const uint32_t b0 = c * B;
-      uint2 r[B];
+  const int lane = t & 63, w = t >> 6;
+  // ---- radix sort by idx (see above)
+  {
+    uint2 kv[R];
+    int lo = 0x7fffffff, hi = -0x7fffffff;
 #pragma unroll
-      for (int i = 0; i < B; ++i) r[i] = b0 + i < n ? key[b0 + i] : make_uint2(0x7fffffffu, 0u);
-      if (full) {
-#pragma unroll
-        for (int k = 2; k <= B; k <<= 1) {
-#pragma unroll
-          for (int i = 0; i < B; ++i)
-            if ((i & (k >> 1)) == 0) rswap(r[i], r[i ^ (k - 1)]);
-#pragma unroll
-          for (int j = k >> 2; j > 0; j >>= 1)
-#pragma unroll
-            for (int i = 0; i < B; ++i)
-              if ((i & j) == 0) rswap(r[i], r[i + j]);
-        }
-      } else {
-#pragma unroll
-        for (int j = B >> 1; j > 0; j >>= 1)
-#pragma unroll
-          for (int i = 0; i < B; ++i)
-            if ((i & j) == 0) rswap(r[i], r[i + j]);
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t i = r * kClThreads + t;
+      kv[r] = i < n ? sorted[off + i] : make_uint2(0u, 0u);
+      if (i < n) {
+        lo = min(lo, static_cast<int>(kv[r].x));
+        hi = max(hi, static_cast<int>(kv[r].x));
       }
+    }
+    if (t == 0) {
+      lo_s = 0x7fffffffu;
+      hi_s = 0u;
+    }
 #pragma unroll
-      for (int i = 0; i < B; ++i)
-        if (b0 + i < n) key[b0 + i] = r[i];
+    for (int o = 32; o > 0; o >>= 1) {
+      lo = min(lo, __shfl_xor(lo, o, 64));
+      hi = max(hi, __shfl_xor(hi, o, 64));
     }
     __syncthreads();
-  };
-  if (rsort) {
-    chunk_pass(true);
-    for (uint32_t k = 2 * B; k <= P; k <<= 1) {
-      const uint32_t h = k >> 1;
-      for (uint32_t q = t; q < P / 2; q += kClThreads) {
-        const uint32_t lo = (q / h) * k + (q & (h - 1)), hi = lo ^ (k - 1);
-        if (hi < n) cswap(lo, hi);
-      }
-      __syncthreads();
-      for (uint32_t j = k >> 2; j >= static_cast<uint32_t>(B); j >>= 1) {
-        for (uint32_t q = t; q < P / 2; q += kClThreads) {
-          const uint32_t lo = 2 * j * (q / j) + (q & (j - 1)), hi = lo + j;
-          if (hi < n) cswap(lo, hi);
-        }
-        __syncthreads();
-      }
-      chunk_pass(false);
+    if (lane == 0) {
+      atomicMin(&lo_s, static_cast<uint32_t>(lo));
+      atomicMax(&hi_s, static_cast<uint32_t>(hi));
     }
-  } else {
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-      const uint32_t h = k >> 1;
-      for (uint32_t q = t; q < P / 2; q += kClThreads) {
-        const uint32_t lo = (q / h) * k + (q & (h - 1)), hi = lo ^ (k - 1);
-        if (hi < n) cswap(lo, hi);
+    __syncthreads();
+    const uint32_t base = lo_s, span = hi_s - lo_s;
+    const int passes = span == 0 ? 0 : (32 - __builtin_clz(span) + 3) / 4;
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(jmp);  // [digit][row][wave]
+    constexpr uint32_t kPer = (kCnt + kClThreads - 1) / kClThreads;  // counts scanned per thread
+    for (int ps = 0; ps < passes; ++ps) {
+      const int shift = 4 * ps;
+      uint32_t dig[R], rank[R];
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t i = r * kClThreads + t;
+        const bool valid = i < n;
+        dig[r] = valid ? ((kv[r].x - base) >> shift) & 15u : 16u;
+        rank[r] = 0;
+        if (r * kClThreads + w * 64 < n) {  // wave-uniform: the row's wave holds keys
+#pragma unroll
+          for (uint32_t d = 0; d < 16; ++d) {
+            const uint64_t m = __ballot(dig[r] == d);
+            if (dig[r] == d) rank[r] = static_cast<uint32_t>(__builtin_popcountll(m & ((1ull << lane) - 1)));
+            if (lane == 0) cnt[(d * R + r) * kW + w] = static_cast<uint32_t>(__builtin_popcountll(m));
+          }
+        } else if (lane == 0) {
+#pragma unroll
+          for (uint32_t d = 0; d < 16; ++d) cnt[(d * R + r) * kW + w] = 0u;
+        }
       }
       __syncthreads();
-      for (uint32_t j = k >> 2; j > 0; j >>= 1) {
-        for (uint32_t q = t; q < P / 2; q += kClThreads) {
-          const uint32_t lo = 2 * j * (q / j) + (q & (j - 1)), hi = lo + j;
-          if (hi < n) cswap(lo, hi);
+      // exclusive scan of the counts in (digit, row, wave) order: each thread
+      // takes kPer consecutive entries
+      {
+        uint32_t loc[kPer], sum = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; ++q) {
+          const uint32_t e = t * kPer + q;
+          loc[q] = e < kCnt ? cnt[e] : 0u;
+          sum += loc[q];
         }
-        __syncthreads();
+        uint32_t run = block_scan_excl<kClThreads>(sum, sc, nullptr);
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; ++q) {
+          const uint32_t e = t * kPer + q;
+          if (e < kCnt) cnt[e] = run;
+          run += loc[q];
+        }
       }
+      __syncthreads();
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r)
+        if (dig[r] < 16) key[cnt[(dig[r] * R + r) * kW + w] + rank[r]] = kv[r];
+      __syncthreads();
+      if (ps + 1 < passes) {
+#pragma unroll
+        for (uint32_t r = 0; r < R; ++r) {
+          const uint32_t i = r * kClThreads + t;
+          if (i < n) kv[r] = key[i];
+        }
+        __syncthreads();  // the next pass's counts and scatter overwrite cnt / key
+      }
+    }
+    if (passes == 0) {  // a single crossing (or all at one bin): already in order
+#pragma unroll
+      for (uint32_t r = 0; r < R; ++r) {
+        const uint32_t i = r * kClThreads + t;
+        if (i < n) key[i] = kv[r];
+      }
+      __syncthreads();
     }
   }
-  if (stop_after == 1) return;  // timing only (PSOUP_CLUSTER_STOP): load + sort
   // Every phase below gives position i = r * kClThreads + t to thread t
   // (row r): consecutive lanes touch consecutive LDS words, and wave ballots
   // order the survivors / peaks inside a row.
-  constexpr uint32_t kW = kClThreads / 64;
   const uint32_t nrow = (n + kClThreads - 1) / kClThreads;
-  const int lane = t & 63, w = t >> 6;
   // (1) window test
   uint32_t mysurv = 0;
   for (uint32_t r = 0; r < nrow; ++r) {
@@ -283,7 +318,6 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
   }
   uint32_t totsurv;
   block_excl_sum<kClThreads>(mysurv, sc, &totsurv);  // (its barriers also publish flag)
-  if (stop_after == 2) return;  // timing only: + window test
   // (3) next survivor at or after every position: rows from the last, a
   // row's waves from their ballots, the carry from the rows after it
   uint32_t carry = n;
@@ -326,7 +360,6 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
   __syncthreads();
   if (t == 0 && first_s < n) flag[first_s] = 3;
   __syncthreads();
-  if (stop_after == 3) return;  // timing only: + next survivor / next()
   // (2) the chain from the first survivor, by pointer doubling: after round
   // m every survivor within 2^(m+1) - 1 jumps of the start is marked
   for (uint32_t span = 1; span < totsurv; span <<= 1) {
@@ -353,7 +386,6 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
     }
     __syncthreads();
   }
-  if (stop_after == 4) return;  // timing only: + chain marking
   // compaction of the peaks in idx order: per (row, wave) counts, their
   // exclusive scan (one thread), then ballot ranks inside each wave
   for (uint32_t r = 0; r < nrow; ++r) {
@@ -437,27 +469,12 @@ void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint
     seg_scatter_global_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segoff, cursor, d_sorted);
     post_launch_check("seg_scatter_global_kernel", s);
   }
-  static const int stop = [] {  // timing experiments only: end the kernels after a phase
-    const char* e = std::getenv("PSOUP_CLUSTER_STOP");
-    const char* r = std::getenv("PSOUP_CLUSTER_RSORT");
-    return (e ? std::atoi(e) : 99) | (r && std::atoi(r) == 1 ? 256 : 0);
-  }();
   peak_cluster_kernel<kClSmall, kClThreads><<<nseg, kClThreads, 0, s>>>(d_sorted, segoff, segcnt, gap, 0u, d_out,
-                                                                         d_segtab, d_total, stop);
+                                                                         d_segtab, d_total);
   post_launch_check("peak_cluster_kernel<small>", s);
-  // the large kernel holds a CU's LDS alone: 1024 threads (16 waves) hide the
-  // LDS latency of its dependent sort / scan steps (PSOUP_CLUSTER_TH=512: the
-  // previous shape)
-  static const bool th512 = [] {
-    const char* e = std::getenv("PSOUP_CLUSTER_TH");
-    return e && std::atoi(e) == 512;
-  }();
-  if (th512)
-    peak_cluster_kernel<kClusterCap, 512><<<nseg, 512, 0, s>>>(d_sorted, segoff, segcnt, gap, kClSmall, d_out,
-                                                                d_segtab, d_total, stop);
-  else
-    peak_cluster_kernel<kClusterCap, 1024><<<nseg, 1024, 0, s>>>(d_sorted, segoff, segcnt, gap, kClSmall, d_out,
-                                                                  d_segtab, d_total, stop);
+  // the large kernel holds a CU's LDS alone: 1024 threads (16 waves)
+  peak_cluster_kernel<kClusterCap, 1024><<<nseg, 1024, 0, s>>>(d_sorted, segoff, segcnt, gap, kClSmall, d_out,
+                                                                d_segtab, d_total);
   post_launch_check("peak_cluster_kernel<large>", s);
 }
 
