@@ -156,7 +156,7 @@ def main() -> int:
     tot = torch.tensor([trials_per_step_local], dtype=torch.int64, device=dev)
     trials_per_step = int(pdist.all_reduce_sum(tot).item())
 
-    phase = {"search": 0.0, "merge": 0.0, "ser": 0.0, "deser": 0.0, "gds": 0.0}
+    phase = {"search": 0.0, "merge": 0.0, "ser": 0.0, "gather": 0.0, "gds": 0.0}
 
     def step():
         t = time.perf_counter()
@@ -166,16 +166,12 @@ def main() -> int:
         blob = _C.serialize_candidates(local)
         t2 = time.perf_counter()
         blobs = pdist.gather_bytes(blob, dst=None)
-        cands = []
-        for b in blobs:
-            cands.extend(_C.deserialize_candidates(b))
-        cands.sort(key=lambda c: c.dm_idx)
         t3 = time.perf_counter()
-        out = _C.global_distill_and_score(cands, args, rs.header)
+        out = _C.merge_candidate_blobs(blobs, args, rs.header)  # rank order, stable by DM, global distill
         t4 = time.perf_counter()
         phase["merge"] += t4 - t1
         phase["ser"] += t2 - t1
-        phase["deser"] += t3 - t2
+        phase["gather"] += t3 - t2
         phase["gds"] += t4 - t3
         phase["blob_bytes"] = len(blob)
         return out
@@ -184,7 +180,7 @@ def main() -> int:
         step()
     for e in rs.engines:
         e.reset_counters()
-    phase.update(search=0.0, merge=0.0, ser=0.0, deser=0.0, gds=0.0)
+    phase.update(search=0.0, merge=0.0, ser=0.0, gather=0.0, gds=0.0)
     pdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -239,7 +235,7 @@ def main() -> int:
                 # acceleration loop, then the candidate gather + global distillation
                 "search_s_per_step": round(phase["search"] / a.steps, 4),
                 "merge_s_per_step": round(phase["merge"] / a.steps, 4),
-                "merge_split_s": {k: round(phase[k] / a.steps, 4) for k in ("ser", "deser", "gds")},
+                "merge_split_s": {k: round(phase[k] / a.steps, 4) for k in ("ser", "gather", "gds")},
                 "candidate_blob_bytes": phase.get("blob_bytes", 0),
                 "accel_s_per_step": round(ctr.get("accel_s", 0) / a.steps, 4),
                 "accel_distill_s_per_step": round(ctr.get("accd_s", 0) / a.steps, 4),

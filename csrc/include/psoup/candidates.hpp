@@ -141,6 +141,10 @@ void sort_by_folded_snr(CandidateList& cands);
 // Compact binary encoding of candidate trees (used for the RCCL gather of
 // per-rank candidates and for checkpoint spill files).
 std::vector<uint8_t> serialize_candidates(const CandidateList& cands);
+// the same encoding of candidates held elsewhere (no copy of their trees)
+std::vector<uint8_t> serialize_candidates(const std::vector<const Candidate*>& cands);
 CandidateList deserialize_candidates(const uint8_t* data, size_t nbytes);
+// deserialised candidates appended to `out` (moved, no intermediate list)
+void deserialize_candidates_into(const uint8_t* data, size_t nbytes, CandidateList& out);
 
 }  // namespace psoup

@@ -189,7 +189,7 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
   __shared__ uint32_t sc[kClThreads];
   __shared__ uint32_t wcnt[kClThreads / 64];   // per wave: first survivor of the row
   __shared__ uint32_t rw[R * (kClThreads / 64)];  // per (row, wave): peak count, then its output offset
-  __shared__ uint32_t base_s, first_s, lo_s, hi_s;
+  __shared__ uint32_t base_s, lo_s, hi_s;
   const int t = threadIdx.x;
   const uint32_t seg = blockIdx.x;
   const uint32_t n = segcnt[seg], off = segoff[seg];
@@ -300,24 +300,28 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
   // (row r): consecutive lanes touch consecutive LDS words, and wave ballots
   // order the survivors / peaks inside a row.
   const uint32_t nrow = (n + kClThreads - 1) / kClThreads;
-  // (1) window test
-  uint32_t mysurv = 0;
+  // (1) window test: the following crossings within the gap, four
+  // independent LDS reads at a time (dense runs test ~gap neighbours)
   for (uint32_t r = 0; r < nrow; ++r) {
     const uint32_t i = r * kClThreads + t;
     if (i >= n) break;
     const int xi = static_cast<int>(key[i].x);
     const float si = __uint_as_float(key[i].y);
-    bool keep = true;
-    for (uint32_t j = i + 1; j < n && static_cast<int>(key[j].x) - xi < gap; ++j)
-      if (__uint_as_float(key[j].y) > si) {
-        keep = false;
-        break;
+    bool keep = true, more = true;
+    for (uint32_t j = i + 1; more && keep && j < n; j += 4) {
+      uint2 q[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) q[e] = key[min(j + e, n - 1)];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const bool in = more && j + e < n && static_cast<int>(q[e].x) - xi < gap;
+        more = in;
+        keep = keep && !(in && __uint_as_float(q[e].y) > si);
       }
+    }
     flag[i] = keep ? 1 : 0;
-    mysurv += keep ? 1u : 0u;
   }
-  uint32_t totsurv;
-  block_excl_sum<kClThreads>(mysurv, sc, &totsurv);  // (its barriers also publish flag)
+  __syncthreads();
   // (3) next survivor at or after every position: rows from the last, a
   // row's waves from their ballots, the carry from the rows after it
   uint32_t carry = n;
@@ -337,77 +341,89 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
     __syncthreads();
   }
   // next(i): the first survivor with idx >= idx_i + gap (at most gap - 1
-  // positions ahead have smaller idx: distinct bins)
+  // positions ahead have smaller idx: distinct bins); a survivor starts a
+  // run when no survivor lies within the gap before it (bit 2)
   uint32_t nx[R];
-  if (t == 0) first_s = jmp[0];
+  bool rs[R];
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
     const uint32_t i = r * kClThreads + t;
     nx[r] = n;
+    rs[r] = false;
     if (i < n && (flag[i] & 1)) {
-      const int target = static_cast<int>(key[i].x) + gap;
+      const int xi = static_cast<int>(key[i].x);
+      const int target = xi + gap;
       uint32_t p = i + 1;
-      while (p < n && static_cast<int>(key[p].x) < target) ++p;
+      bool go = true;
+      while (go && p < n) {  // four reads at a time
+        uint32_t a[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) a[e] = key[min(p + e, n - 1)].x;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool step = go && p < n && static_cast<int>(a[e]) < target;
+          p += step ? 1u : 0u;
+          go = step;
+        }
+      }
       nx[r] = p < n ? jmp[p] : n;
+      bool start = true;
+      for (uint32_t q = i; start && q-- > 0;) {
+        if (xi - static_cast<int>(key[q].x) >= gap) break;
+        if (flag[q] & 1) start = false;
+      }
+      rs[r] = start;
     }
   }
   __syncthreads();
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
     const uint32_t i = r * kClThreads + t;
-    if (i < n && (flag[i] & 1)) jmp[i] = static_cast<uint16_t>(nx[r]);
+    if (i < n && (flag[i] & 1)) {
+      jmp[i] = static_cast<uint16_t>(nx[r]);
+      if (rs[r]) flag[i] = 5;
+    }
   }
   __syncthreads();
-  if (t == 0 && first_s < n) flag[first_s] = 3;
-  __syncthreads();
-  // (2) the chain from the first survivor, by pointer doubling: after round
-  // m every survivor within 2^(m+1) - 1 jumps of the start is marked
-  for (uint32_t span = 1; span < totsurv; span <<= 1) {
-    uint32_t tgt[R], nj[R];
+  // (2) the chains: within a run an anchor never moves, so the run's peaks
+  // are its start, then next(), next(next()), ... until the chain reaches the
+  // following run's start; each run start's thread follows its own run
 #pragma unroll
-    for (uint32_t r = 0; r < R; ++r) {
-      const uint32_t i = r * kClThreads + t;
-      tgt[r] = n;
-      nj[r] = n;
-      if (i < n && (flag[i] & 1)) {
-        const uint32_t j = jmp[i];
-        if (j < n) {
-          if (flag[i] & 2) tgt[r] = j;
-          nj[r] = jmp[j];
-        }
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (uint32_t r = 0; r < R; ++r) {
-      const uint32_t i = r * kClThreads + t;
-      if (tgt[r] < n) flag[tgt[r]] = 3;
-      if (i < n && (flag[i] & 1)) jmp[i] = static_cast<uint16_t>(nj[r]);
-    }
-    __syncthreads();
+  for (uint32_t r = 0; r < R; ++r) {
+    if (!rs[r]) continue;
+    uint32_t p = r * kClThreads + t;
+    do {
+      flag[p] = static_cast<uint8_t>(flag[p] | 2);
+      p = jmp[p];
+    } while (p < n && !(flag[p] & 4));
   }
+  __syncthreads();
   // compaction of the peaks in idx order: per (row, wave) counts, their
-  // exclusive scan (one thread), then ballot ranks inside each wave
+  // exclusive scan, then ballot ranks inside each wave
   for (uint32_t r = 0; r < nrow; ++r) {
     const uint32_t i = r * kClThreads + t;
-    const uint64_t mask = __ballot(i < n && (flag[i] >> 1));
+    const uint64_t mask = __ballot(i < n && (flag[i] & 2));
     if (lane == 0) rw[r * kW + w] = static_cast<uint32_t>(__builtin_popcountll(mask));
   }
   __syncthreads();
-  if (t == 0) {
-    uint32_t acc = 0;
-    for (uint32_t q = 0; q < nrow * kW; ++q) {
-      const uint32_t c = rw[q];
-      rw[q] = acc;
-      acc += c;
+  {
+    static_assert(R * kW <= kClThreads, "one (row, wave) count per thread");
+    const uint32_t v = static_cast<uint32_t>(t) < nrow * kW ? rw[t] : 0u;
+    uint32_t acc;
+    const uint32_t ex = block_scan_excl<kClThreads>(v, sc, &base_s);
+    if (static_cast<uint32_t>(t) < nrow * kW) rw[t] = ex;
+    __syncthreads();
+    acc = base_s;  // the segment's peak count
+    __syncthreads();
+    if (t == 0) {
+      base_s = atomicAdd(total, acc);
+      segtab[seg] = make_uint2(base_s, acc);
     }
-    base_s = atomicAdd(total, acc);
-    segtab[seg] = make_uint2(base_s, acc);
   }
   __syncthreads();
   for (uint32_t r = 0; r < nrow; ++r) {
     const uint32_t i = r * kClThreads + t;
-    const bool pk = i < n && (flag[i] >> 1);
+    const bool pk = i < n && (flag[i] & 2);
     const uint64_t mask = __ballot(pk);
     if (pk)
       out[base_s + rw[r * kW + w] + static_cast<uint32_t>(__builtin_popcountll(mask & ((1ull << lane) - 1)))] = key[i];

@@ -327,9 +327,39 @@ PYBIND11_MODULE(_C, m) {
     for (size_t i = 0; i < k.size(); ++i) order[i] = k[i].i;
     return order;
   });
-  m.def("serialize_candidates", [](const CandidateList& c) {
-    auto v = serialize_candidates(c);
+  // a sequence of Candidate objects, serialised in place: no copy of the
+  // trees into a temporary C++ list (candidate-heavy searches carry large
+  // keep_related trees)
+  m.def("serialize_candidates", [](const py::sequence& seq) {
+    std::vector<const Candidate*> p;
+    p.reserve(seq.size());
+    for (auto h : seq) p.push_back(&h.cast<const Candidate&>());
+    std::vector<uint8_t> v;
+    {
+      py::gil_scoped_release nogil;
+      v = serialize_candidates(p);
+    }
     return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+  });
+  // The multi-rank merge (pipeline_multi.cu:353-369) in one native call:
+  // every rank's serialised candidates (rank order), a stable sort by DM
+  // index, then the global DM + harmonic distillation and scoring -- no
+  // intermediate Python lists.
+  m.def("merge_candidate_blobs", [](const std::vector<py::bytes>& blobs, const CmdLineOptions& args,
+                                    const py::dict& hdr) {
+    std::vector<std::string> raw;
+    raw.reserve(blobs.size());
+    for (const auto& b : blobs) raw.push_back(static_cast<std::string>(b));
+    SearchSetup s = make_search_setup(args, dict_to_header(hdr));
+    CandidateList out;
+    {
+      py::gil_scoped_release nogil;
+      CandidateList all;
+      for (const auto& r : raw) deserialize_candidates_into(reinterpret_cast<const uint8_t*>(r.data()), r.size(), all);
+      std::stable_sort(all.begin(), all.end(), [](const Candidate& a, const Candidate& b) { return a.dm_idx < b.dm_idx; });
+      out = global_distill_and_score(std::move(all), args, s);
+    }
+    return out;
   });
   m.def("deserialize_candidates", [](py::buffer b) {
     py::buffer_info info = b.request();

@@ -451,18 +451,24 @@ Candidate de_node(Reader& r, int depth) {
 }  // namespace
 
 std::vector<uint8_t> serialize_candidates(const CandidateList& cands) {
+  std::vector<const Candidate*> p;
+  p.reserve(cands.size());
+  for (const auto& c : cands) p.push_back(&c);
+  return serialize_candidates(p);
+}
+
+std::vector<uint8_t> serialize_candidates(const std::vector<const Candidate*>& cands) {
   std::vector<uint8_t> out;
   uint32_t magic = 0x50534F43u;  // "PSOC"
   int64_t n = static_cast<int64_t>(cands.size());
   put(out, &magic, 4);
   put(out, &n, 8);
-  for (const auto& c : cands) ser_node(c, out);
+  for (const Candidate* c : cands) ser_node(*c, out);
   return out;
 }
 
-CandidateList deserialize_candidates(const uint8_t* data, size_t nbytes) {
-  CandidateList out;
-  if (nbytes == 0) return out;
+void deserialize_candidates_into(const uint8_t* data, size_t nbytes, CandidateList& out) {
+  if (nbytes == 0) return;
   Reader r{data, nbytes};
   uint32_t magic = 0;
   int64_t n = 0;
@@ -470,8 +476,13 @@ CandidateList deserialize_candidates(const uint8_t* data, size_t nbytes) {
   PSOUP_CHECK(magic == 0x50534F43u, "bad candidate stream magic");
   r.get(&n, 8);
   PSOUP_CHECK(n >= 0, "bad candidate count");
-  out.reserve(static_cast<size_t>(n));
+  out.reserve(out.size() + static_cast<size_t>(n));
   for (int64_t i = 0; i < n; ++i) out.push_back(de_node(r, 0));
+}
+
+CandidateList deserialize_candidates(const uint8_t* data, size_t nbytes) {
+  CandidateList out;
+  deserialize_candidates_into(data, nbytes, out);
   return out;
 }
 

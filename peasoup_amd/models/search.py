@@ -704,11 +704,8 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     # ---- candidate gather (RCCL) + global distillation on rank 0
     blobs = pdist.gather_bytes(_C.serialize_candidates(local), dst=None)
     total_trials = sum(weights)
-    cands = []
-    for b in blobs:
-        cands.extend(_C.deserialize_candidates(b))
-    cands.sort(key=lambda c: c.dm_idx)
-    cands = _C.global_distill_and_score(cands, args, rs.header)
+    # rank order, stable by DM index, then the global distillation: one native call
+    cands = _C.merge_candidate_blobs(blobs, args, rs.header)
     search_wall = pdist.all_reduce_max_float(search_wall)
 
     # ---- distributed folding (all ranks hold identical `cands`)

@@ -198,3 +198,34 @@ def test_serialisation_roundtrip(C):
     assert back[0].opt_period == a.opt_period and back[0].assoc[0].assoc[0].freq == 13.0
     assert [p[5] for p in back[0].pods()] == [3.25, 6.5, 13.0]
     assert C.deserialize_candidates(C.serialize_candidates([])) == []
+
+
+def test_merge_candidate_blobs_equals_python_merge(C):
+    """The native multi-rank merge (deserialise every rank's blob, stable sort
+    by DM index, global DM + harmonic distillation and scoring) equals the
+    step-by-step Python path, tree for tree; serialize_candidates reads the
+    Python objects in place."""
+    from conftest import TUTORIAL
+
+    rng = random.Random(5)
+    ok, _, args = C.parse_cmdline(["peasoup", "-i", TUTORIAL, "--dm_end", "250", "-n", "4"])
+    hdr = dict(C.Filterbank.from_file(TUTORIAL).header)
+    ranks = []
+    for r in range(3):
+        lst = []
+        for _ in range(60):
+            f = rng.choice([rng.uniform(1, 300), 4.0, 8.0, 33.3]) * (1 + rng.uniform(-2e-5, 2e-5))
+            c = C.Candidate(rng.uniform(0, 250), rng.randrange(0, 59), rng.uniform(-5, 5), rng.randrange(0, 5),
+                            rng.uniform(9, 90), f)
+            c.assoc = [C.Candidate(1.0, c.dm_idx, 0.0, 1, rng.uniform(9, 20), f * 1.00001)] * rng.randrange(0, 3)
+            lst.append(c)
+        ranks.append(lst)
+    blobs = [C.serialize_candidates(lst) for lst in ranks]
+    got = C.merge_candidate_blobs(blobs, args, hdr)
+    cands = []
+    for b in blobs:
+        cands.extend(C.deserialize_candidates(b))
+    cands.sort(key=lambda c: c.dm_idx)
+    exp = C.global_distill_and_score(cands, args, hdr)
+    assert len(got) > 5
+    assert C.serialize_candidates(got) == C.serialize_candidates(exp)

@@ -20,15 +20,31 @@ def main():
     ap.add_argument("--nseg", type=int, default=2048)
     ap.add_argument("--n", type=int, default=4200)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--dense", action="store_true",
+                    help="RFI-like segments: runs of 100-500 consecutive bins (acceleration-smeared harmonics), "
+                         "S/N a smooth bump plus noise")
     a = ap.parse_args()
     K = _C.kernels
     rng = np.random.default_rng(1)
     recs = []
     for sgi in range(a.nseg):
         n = int(rng.integers(a.n // 2, a.n * 3 // 2))
-        spikes = rng.choice(1 << 22, max(1, n // 40), replace=False)
-        idx = np.unique((spikes[:, None] + np.arange(-20, 20)[None, :]).reshape(-1))[:n].astype(np.int32)
-        snr = (9.0 + 30.0 * rng.random(idx.size)).astype(np.float32)
+        if a.dense:
+            parts, snrs, tot_ = [], [], 0
+            while tot_ < n:
+                L = int(rng.integers(100, 500))
+                c = int(rng.integers(0, (1 << 22) - L))
+                parts.append(np.arange(c, c + L))
+                x = np.linspace(-1, 1, L)
+                snrs.append(9.5 + 30.0 * np.exp(-3 * x * x) * rng.uniform(0.5, 1.5) + rng.normal(0, 1.5, L))
+                tot_ += L
+            idx, first = np.unique(np.concatenate(parts), return_index=True)
+            snr = np.maximum(np.concatenate(snrs)[first], 9.01)
+            idx, snr = idx[:n].astype(np.int32), snr[:n].astype(np.float32)
+        else:
+            spikes = rng.choice(1 << 22, max(1, n // 40), replace=False)
+            idx = np.unique((spikes[:, None] + np.arange(-20, 20)[None, :]).reshape(-1))[:n].astype(np.int32)
+            snr = (9.0 + 30.0 * rng.random(idx.size)).astype(np.float32)
         recs.append(np.stack([np.full(idx.size, sgi, np.uint32), idx.view(np.uint32), snr.view(np.uint32)], axis=1))
     allr = np.concatenate(recs)
     allr = allr[rng.permutation(len(allr))]
@@ -53,8 +69,8 @@ def main():
         run()
     e1.record()
     torch.cuda.synchronize()
-    print(f"stop={os.environ.get('PSOUP_CLUSTER_TH', '1024')}/{os.environ.get('PSOUP_CLUSTER_STOP', 'full')} "
-          f"records={n} segments={a.nseg}: {e0.elapsed_time(e1) / a.reps:.3f} ms per batch", flush=True)
+    print(f"{'dense' if a.dense else 'spiky'} records={n} segments={a.nseg}: "
+          f"{e0.elapsed_time(e1) / a.reps:.3f} ms per batch", flush=True)
 
 
 if __name__ == "__main__":
