@@ -29,8 +29,13 @@ namespace psoup {
 namespace kern {
 
 // ---------------------------------------------------------------- records ---
+// harmonic_peaks_batch output: crossings {segment, idx, snr} (segment =
+// batch_item * 8 + level), each run of one (wave, 64-bin group, level)
+// preceded by a chunk descriptor {kPeakChunk | count << 16 | segment, first
+// idx, position of its first crossing (as the snr bits)}.
+constexpr uint32_t kPeakChunk = 0x80000000u;
 struct PeakRecord {
-  uint32_t seg;  // batch_item * 8 + level
+  uint32_t seg;  // batch_item * 8 + level, or a chunk descriptor (kPeakChunk)
   int32_t idx;
   float snr;
 };
@@ -369,14 +374,16 @@ struct HarmParams {
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
                           PeakRecord* out, uint32_t* count, hipStream_t s, const PLayout& L = PLayout{});
 // Peak clustering on the device (peakcluster.hip; peakfinder.hpp:24-55):
-// the records of harmonic_peaks_batch (first min(*d_count, cap)) grouped by
-// segment (seg < nseg), each segment's crossings clustered with the
-// reference's gap rule.  d_segtab[seg] = {first, count} of its cluster peaks
-// in d_out (ascending idx; uint2 = {idx, snr bits}; segments packed in any
-// order, *d_total in all), or {first, count | kClusterRaw} when the segment
-// has more than kClusterCap crossings: then its raw, unsorted crossings are
-// d_sorted[first .. first + count) for the host to cluster.
-// d_work: 3 * nseg uint32; d_sorted, d_out: cap entries each.
+// the records of harmonic_peaks_batch (first min(*d_count, cap)) -- chunks
+// of idx-ascending crossings, each behind its descriptor record (seg field
+// kPeakChunk | count << 16 | segment, idx = first idx, snr bits = position
+// of the first crossing) -- per segment (seg < nseg <= 65536) clustered with
+// the reference's gap rule.  d_segtab[seg] = {first, count} of its cluster
+// peaks in d_out (ascending idx; uint2 = {idx, snr bits}; segments packed in
+// any order, *d_total in all), or {first, count | kClusterRaw} when the
+// segment has more than kClusterCap crossings: then its raw, unsorted
+// crossings are d_sorted[cap + first .. cap + first + count) for the host.
+// d_work: 5 * nseg uint32; d_sorted: 2 * cap entries; d_out: cap entries.
 constexpr uint32_t kClusterCap = 14000;
 constexpr uint32_t kClusterRaw = 0x80000000u;
 void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint32_t cap, uint32_t nseg, int gap,

@@ -440,19 +440,44 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
   }
 }
 
-__device__ __forceinline__ void emit(bool pred, uint32_t seg, int idx, float snr, PeakRecord* __restrict__ out,
-                                     uint32_t* __restrict__ count, uint32_t capacity) {
-  const unsigned long long mask = __ballot(pred);
-  if (mask == 0ull) return;
+// The records of levels [h0, h1] of one bin group with one atomic per wave
+// (not one per level): on peak-heavy (RFI) spectra every bin group of a tile
+// crosses on several levels, and the single global counter's atomics were
+// the emission cost.  Each level's crossings are one chunk in lane (= idx)
+// order behind its descriptor {kPeakChunk | count << 16 | segment, first
+// idx, position}: the clustering (peakcluster.hip) then sorts chunks, not
+// crossings.  Segments are < 2^16 (checked on the host).
+template <int NL>
+__device__ __forceinline__ void emit_levels(const bool (&pred)[NL], int h0, int h1, uint32_t seg0, int idx,
+                                            const float (&snr)[NL], PeakRecord* __restrict__ out,
+                                            uint32_t* __restrict__ count, uint32_t capacity) {
   const int lane = threadIdx.x & 63;
-  const int leader = __ffsll(static_cast<long long>(mask)) - 1;
+  unsigned long long mask[NL];
+  uint32_t tot = 0;
+#pragma unroll
+  for (int h = 0; h < NL; ++h) {
+    mask[h] = (h >= h0 && h <= h1) ? __ballot(pred[h]) : 0ull;
+    tot += mask[h] ? static_cast<uint32_t>(__popcll(mask[h])) + 1u : 0u;  // + its descriptor
+  }
+  if (tot == 0) return;
   uint32_t base = 0;
-  if (lane == leader) base = atomicAdd(count, static_cast<uint32_t>(__popcll(mask)));
-  base = __shfl(base, leader, 64);
-  if (pred) {
-    const unsigned long long lt = (lane == 0) ? 0ull : (mask & ((1ull << lane) - 1ull));
-    const uint32_t pos = base + static_cast<uint32_t>(__popcll(lt));
-    if (pos < capacity) out[pos] = PeakRecord{seg, idx, snr};
+  if (lane == 0) base = atomicAdd(count, tot);
+  base = __shfl(base, 0, 64);
+  const unsigned long long lt = (lane == 0) ? 0ull : ((1ull << lane) - 1ull);
+#pragma unroll
+  for (int h = 0; h < NL; ++h) {
+    if (mask[h] == 0ull) continue;  // wave-uniform
+    const uint32_t cnt = static_cast<uint32_t>(__popcll(mask[h]));
+    const uint32_t first = base + 1u;  // the chunk's first crossing
+    if (pred[h]) {
+      const uint32_t below = static_cast<uint32_t>(__popcll(mask[h] & lt));
+      if (below == 0 && base < capacity)  // the chunk's lowest lane: the descriptor
+        out[base] = PeakRecord{kPeakChunk | (cnt << 16) | (seg0 + static_cast<uint32_t>(h)), idx,
+                               __uint_as_float(first)};
+      const uint32_t pos = first + below;
+      if (pos < capacity) out[pos] = PeakRecord{seg0 + static_cast<uint32_t>(h), idx, snr[h]};
+    }
+    base = first + cnt;
   }
 }
 
@@ -695,8 +720,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
       any = any | pred[h];
     }
     if (__ballot(any) == 0ull) continue;  // one ballot per bin group in the (usual) no-peak case
-#pragma unroll
-    for (int h = 0; h <= NLEV; ++h) emit(pred[h], seg0 + h, i, o[h], out, count, hp.capacity);
+    emit_levels<NLEV + 1>(pred, 0, NLEV, seg0, i, o, out, count, hp.capacity);
   }
 }
 
@@ -817,9 +841,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks2_kernel(const float* __res
       any = any | pred[h];
     }
     if (__ballot(any) == 0ull) return;
-#pragma unroll
-    for (int h = 0; h <= NLEV; ++h)
-      if (h >= h0 && h <= h1) emit(pred[h], seg0 + h, i, o[h], out, count, hp.capacity);
+    emit_levels<NLEV + 1>(pred, h0, h1, seg0, i, o, out, count, hp.capacity);
   };
   float run[Tl::BPT];  // running sum after level NLEV - 1
 #pragma unroll
@@ -1149,6 +1171,7 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
     }
   }
   PSOUP_CHECK(hi <= static_cast<int>(nbins), "search range beyond spectrum");
+  PSOUP_CHECK((static_cast<uint64_t>(K) + hp.trial_base) * 8 <= 65536, "chunk descriptors hold 16-bit segments");
   if (hi <= lo) return;
   PSOUP_CHECK(static_cast<int64_t>(hi) * 32 < (int64_t(1) << 31), "spectrum too long for the int32 gather math");
   if (pl.blk) {

@@ -20,12 +20,20 @@
 // next(i) = the first survivor with idx >= idx_i + gap, and so on (a run's
 // last anchor has every later survivor of its run within the gap, so its
 // next is the following run's start).
+// Input: the harmonic kernel's records (harmsum.hip emit_levels): every
+// (wave, bin group, level) with crossings wrote one chunk -- a descriptor
+// {kPeakChunk | count << 16 | segment, first idx, position} and its `count`
+// crossings, idx-ascending, at that position.  Chunks of one segment cover
+// disjoint 64-bin groups, so the segment in idx order is its chunks in
+// first-idx order: only the descriptors (~1/20 of the records on dense RFI
+// spectra) are grouped by segment and sorted.
 // peak_cluster_kernel: one workgroup per segment (trial x level): radix
-// sort by idx in LDS, the window test (1) and next() in parallel (a suffix
-// scan gives the next survivor at or after any position), one thread follows
-// the chain (one LDS read per peak), a scan compacts the peaks in idx order.
-// Segments over kClusterCap crossings are left to the host (flagged in the
-// segment table with their raw, unsorted range).
+// sort of its chunk descriptors in LDS, the crossings gathered in idx order,
+// the window test (1) and next() in parallel (a suffix scan gives the next
+// survivor at or after any position), each run's chain followed by the thread
+// of its start, a scan compacts the peaks in idx order.  Segments over
+// kClusterCap crossings are left to the host (flagged in the segment table
+// with their raw, unsorted range).
 #include "device_common.hpp"
 
 namespace psoup {
@@ -55,29 +63,40 @@ __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* sc, uin
   return incl - v;
 }
 
-// Per-segment counts: each block counts its records in LDS and adds the
-// non-zero counts to the global ones (one atomic per block and segment, not
-// per record: heavy segments get tens of thousands of records).
+// A chunk descriptor's segment and crossing count (kPeakChunk records only).
+__device__ __forceinline__ uint32_t chunk_seg(uint32_t f) { return f & 0xffffu; }
+__device__ __forceinline__ uint32_t chunk_count(uint32_t f) { return (f >> 16) & 0x7fu; }
+
+// Per-segment chunk and crossing counts: each block counts its descriptors
+// in LDS and adds the non-zero counts to the global ones (one atomic per
+// block and segment).
 __global__ void __launch_bounds__(256) seg_hist_kernel(const PeakRecord* __restrict__ in,
                                                        const uint32_t* __restrict__ count, uint32_t cap,
-                                                       uint32_t nseg, uint32_t* __restrict__ segcnt) {
-  __shared__ uint32_t lc[kSegLds];
+                                                       uint32_t nseg, uint32_t* __restrict__ segcnt,
+                                                       uint32_t* __restrict__ segdcnt) {
+  __shared__ uint32_t lr[kSegLds], lc[kSegLds];
   const uint32_t n = min(*count, cap);
   const uint32_t base = blockIdx.x * 256u * kRecPerThread;
   if (base >= n) return;
-  for (uint32_t i = threadIdx.x; i < nseg; i += 256) lc[i] = 0;
+  for (uint32_t i = threadIdx.x; i < nseg; i += 256) lr[i] = lc[i] = 0;
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kRecPerThread; ++r) {
     const uint32_t i = base + r * 256u + threadIdx.x;
     if (i < n) {
-      const uint32_t sg = in[i].seg;
-      if (sg < nseg) atomicAdd(&lc[sg], 1u);
+      const uint32_t f = in[i].seg;
+      if ((f & kPeakChunk) && chunk_seg(f) < nseg) {
+        atomicAdd(&lc[chunk_seg(f)], 1u);
+        atomicAdd(&lr[chunk_seg(f)], chunk_count(f));
+      }
     }
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nseg; i += 256)
-    if (lc[i]) atomicAdd(&segcnt[i], lc[i]);
+    if (lc[i]) {
+      atomicAdd(&segdcnt[i], lc[i]);
+      atomicAdd(&segcnt[i], lr[i]);
+    }
 }
 
 __global__ void __launch_bounds__(kClThreads) seg_scan_kernel(const uint32_t* __restrict__ segcnt, uint32_t nseg,
@@ -98,12 +117,13 @@ __global__ void __launch_bounds__(kClThreads) seg_scan_kernel(const uint32_t* __
   }
 }
 
-// Records grouped by segment: LDS ranks within the block, one global atomic
-// per (block, segment) reserves the block's range of the segment.
+// Chunk descriptors grouped by segment as {first idx, position, count}: LDS
+// ranks within the block, one global atomic per (block, segment) reserves
+// the block's range of the segment.
 __global__ void __launch_bounds__(256) seg_scatter_kernel(const PeakRecord* __restrict__ in,
                                                           const uint32_t* __restrict__ count, uint32_t cap,
-                                                          uint32_t nseg, const uint32_t* __restrict__ segoff,
-                                                          uint32_t* __restrict__ cursor, uint2* __restrict__ out) {
+                                                          uint32_t nseg, const uint32_t* __restrict__ segdoff,
+                                                          uint32_t* __restrict__ cursor, uint4* __restrict__ out) {
   __shared__ uint32_t lc[kSegLds];
   __shared__ uint32_t lb[kSegLds];
   const uint32_t n = min(*count, cap);
@@ -116,20 +136,22 @@ __global__ void __launch_bounds__(256) seg_scatter_kernel(const PeakRecord* __re
 #pragma unroll
   for (int r = 0; r < kRecPerThread; ++r) {
     const uint32_t i = base + r * 256u + threadIdx.x;
-    rec[r].seg = 0xffffffffu;
+    rec[r].seg = 0u;
     if (i < n) {
       rec[r] = in[i];
-      if (rec[r].seg < nseg) rank[r] = atomicAdd(&lc[rec[r].seg], 1u);
+      if (!(rec[r].seg & kPeakChunk) || chunk_seg(rec[r].seg) >= nseg) rec[r].seg = 0u;
+      else rank[r] = atomicAdd(&lc[chunk_seg(rec[r].seg)], 1u);
     }
   }
   __syncthreads();
   for (uint32_t i = threadIdx.x; i < nseg; i += 256)
-    if (lc[i]) lb[i] = segoff[i] + atomicAdd(&cursor[i], lc[i]);
+    if (lc[i]) lb[i] = segdoff[i] + atomicAdd(&cursor[i], lc[i]);
   __syncthreads();
 #pragma unroll
   for (int r = 0; r < kRecPerThread; ++r)
-    if (rec[r].seg < nseg)
-      out[lb[rec[r].seg] + rank[r]] = make_uint2(static_cast<uint32_t>(rec[r].idx), __float_as_uint(rec[r].snr));
+    if (rec[r].seg & kPeakChunk)
+      out[lb[chunk_seg(rec[r].seg)] + rank[r]] = make_uint4(static_cast<uint32_t>(rec[r].idx),
+                                                             __float_as_uint(rec[r].snr), chunk_count(rec[r].seg), 0u);
 }
 
 // Exclusive scan of one value per thread over the block (TH threads): wave
@@ -174,42 +196,64 @@ __device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t* wtot, 
 // 14000 crossings), each a full LDS round trip.  The counts alias the jump
 // table, which is only used after the sort.
 template <uint32_t CAP, int kClThreads>
-__global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* __restrict__ sorted,
+__global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakRecord* __restrict__ recs,
+                                                                  const uint4* __restrict__ desc,
                                                                   const uint32_t* __restrict__ segoff,
-                                                                  const uint32_t* __restrict__ segcnt, int gap,
+                                                                  const uint32_t* __restrict__ segcnt,
+                                                                  const uint32_t* __restrict__ segdoff,
+                                                                  const uint32_t* __restrict__ segdcnt, int gap,
                                                                   uint32_t lo_n, uint2* __restrict__ out,
                                                                   uint2* __restrict__ segtab,
-                                                                  uint32_t* __restrict__ total) {
+                                                                  uint32_t* __restrict__ total,
+                                                                  uint2* __restrict__ raw) {
   constexpr uint32_t R = (CAP + kClThreads - 1) / kClThreads;  // rows of kClThreads positions
   constexpr uint32_t kW = kClThreads / 64;
   constexpr uint32_t kCnt = 16 * R * kW;  // radix counts (digit, row, wave)
-  __shared__ uint2 key[CAP];      // (idx, snr bits)
+  __shared__ uint2 key[CAP];      // sorted chunk descriptors (first idx, index), then the crossings (idx, snr bits)
   __shared__ uint16_t jmp[CAP > 2 * kCnt ? CAP : 2 * kCnt];  // next survivor / chain jumps; radix counts before
-  __shared__ uint8_t flag[CAP];   // bit 0: survives the window test, bit 1: cluster peak
+  __shared__ uint8_t flag[CAP];   // bit 0: survives the window test, bit 1: cluster peak, bit 2: run start
   __shared__ uint32_t sc[kClThreads];
   __shared__ uint32_t wcnt[kClThreads / 64];   // per wave: first survivor of the row
   __shared__ uint32_t rw[R * (kClThreads / 64)];  // per (row, wave): peak count, then its output offset
   __shared__ uint32_t base_s, lo_s, hi_s;
   const int t = threadIdx.x;
   const uint32_t seg = blockIdx.x;
-  const uint32_t n = segcnt[seg], off = segoff[seg];
+  const uint32_t n = segcnt[seg];                        // crossings
+  const uint32_t m = segdcnt[seg], doff = segdoff[seg];  // chunks
+  const uint4* dsc = desc + doff;
   if (n <= lo_n || n > CAP) {
-    if (t == 0) {
-      if (n == 0 && lo_n == 0) segtab[seg] = make_uint2(0u, 0u);
-      if (n > CAP && CAP > kClSmall) segtab[seg] = make_uint2(off, n | kClusterRaw);
+    if (n == 0 && lo_n == 0 && t == 0) segtab[seg] = make_uint2(0u, 0u);
+    if (n > CAP && CAP > kClSmall) {
+      // over capacity: the raw crossings (any order) at raw[segoff ..] for the
+      // host; chunk j's crossings after chunks 0 .. j-1's
+      uint32_t carry = 0;
+      for (uint32_t j0 = 0; j0 < m; j0 += kClThreads) {
+        const uint32_t j = j0 + t;
+        const uint4 d = j < m ? dsc[j] : make_uint4(0u, 0u, 0u, 0u);
+        uint32_t tot;
+        const uint32_t ex = block_scan_excl<kClThreads>(d.z, sc, &base_s);
+        tot = base_s;
+        for (uint32_t q = 0; q < d.z; ++q) {
+          const PeakRecord r = recs[d.y + q];
+          raw[segoff[seg] + carry + ex + q] = make_uint2(static_cast<uint32_t>(r.idx), __float_as_uint(r.snr));
+        }
+        carry += tot;
+        __syncthreads();
+      }
+      if (t == 0) segtab[seg] = make_uint2(segoff[seg], n | kClusterRaw);
     }
     return;
   }
   const int lane = t & 63, w = t >> 6;
-  // ---- radix sort by idx (see above)
+  // ---- radix sort of the m chunk descriptors by first idx (see above)
   {
     uint2 kv[R];
     int lo = 0x7fffffff, hi = -0x7fffffff;
 #pragma unroll
     for (uint32_t r = 0; r < R; ++r) {
       const uint32_t i = r * kClThreads + t;
-      kv[r] = i < n ? sorted[off + i] : make_uint2(0u, 0u);
-      if (i < n) {
+      kv[r] = i < m ? make_uint2(dsc[i].x, i) : make_uint2(0u, 0u);
+      if (i < m) {
         lo = min(lo, static_cast<int>(kv[r].x));
         hi = max(hi, static_cast<int>(kv[r].x));
       }
@@ -239,10 +283,10 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
 #pragma unroll
       for (uint32_t r = 0; r < R; ++r) {
         const uint32_t i = r * kClThreads + t;
-        const bool valid = i < n;
+        const bool valid = i < m;
         dig[r] = valid ? ((kv[r].x - base) >> shift) & 15u : 16u;
         rank[r] = 0;
-        if (r * kClThreads + w * 64 < n) {  // wave-uniform: the row's wave holds keys
+        if (r * kClThreads + w * 64 < m) {  // wave-uniform: the row's wave holds keys
 #pragma unroll
           for (uint32_t d = 0; d < 16; ++d) {
             const uint64_t m = __ballot(dig[r] == d);
@@ -282,19 +326,43 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
 #pragma unroll
         for (uint32_t r = 0; r < R; ++r) {
           const uint32_t i = r * kClThreads + t;
-          if (i < n) kv[r] = key[i];
+          if (i < m) kv[r] = key[i];
         }
         __syncthreads();  // the next pass's counts and scatter overwrite cnt / key
       }
     }
-    if (passes == 0) {  // a single crossing (or all at one bin): already in order
+    if (passes == 0) {  // a single chunk: already in order
 #pragma unroll
       for (uint32_t r = 0; r < R; ++r) {
         const uint32_t i = r * kClThreads + t;
-        if (i < n) key[i] = kv[r];
+        if (i < m) key[i] = kv[r];
       }
       __syncthreads();
     }
+  }
+  // ---- the crossings in idx order: sorted chunk p starts at the sum of the
+  // counts of chunks 0 .. p-1 (thread t owns the consecutive sorted chunks
+  // [t q, t q + q)); the sorted chunk indices move to the jump table (< 2^16)
+  // so each thread can copy its chunks' crossings over the keys
+  {
+    const uint32_t q = (m + kClThreads - 1) / kClThreads;
+    const uint32_t p0 = t * q, p1 = min(m, p0 + q);
+    uint32_t sum = 0;
+    for (uint32_t p = p0; p < p1; ++p) {
+      const uint32_t j = key[p].y;
+      jmp[p] = static_cast<uint16_t>(j);
+      sum += dsc[j].z;
+    }
+    uint32_t dst = block_scan_excl<kClThreads>(sum, sc, nullptr);  // (its barriers retire the key reads)
+    for (uint32_t p = p0; p < p1; ++p) {
+      const uint4 d = dsc[jmp[p]];
+      for (uint32_t c = 0; c < d.z; ++c) {
+        const PeakRecord r = recs[d.y + c];
+        key[dst + c] = make_uint2(static_cast<uint32_t>(r.idx), __float_as_uint(r.snr));
+      }
+      dst += d.z;
+    }
+    __syncthreads();
   }
   // Every phase below gives position i = r * kClThreads + t to thread t
   // (row r): consecutive lanes touch consecutive LDS words, and wave ballots
@@ -430,28 +498,33 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const uint2* _
   }
 }
 
-// Fallbacks for batches with more than kSegLds segments: one global atomic per record.
+// Fallbacks for batches with more than kSegLds segments: one global atomic per descriptor.
 __global__ void __launch_bounds__(256) seg_hist_global_kernel(const PeakRecord* __restrict__ in,
                                                               const uint32_t* __restrict__ count, uint32_t cap,
-                                                              uint32_t nseg, uint32_t* __restrict__ segcnt) {
+                                                              uint32_t nseg, uint32_t* __restrict__ segcnt,
+                                                              uint32_t* __restrict__ segdcnt) {
   const uint32_t n = min(*count, cap);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t sg = in[i].seg;
-    if (sg < nseg) atomicAdd(&segcnt[sg], 1u);
+    const uint32_t f = in[i].seg;
+    if ((f & kPeakChunk) && chunk_seg(f) < nseg) {
+      atomicAdd(&segdcnt[chunk_seg(f)], 1u);
+      atomicAdd(&segcnt[chunk_seg(f)], chunk_count(f));
+    }
   }
 }
 
 __global__ void __launch_bounds__(256) seg_scatter_global_kernel(const PeakRecord* __restrict__ in,
                                                                  const uint32_t* __restrict__ count, uint32_t cap,
-                                                                 uint32_t nseg, const uint32_t* __restrict__ segoff,
+                                                                 uint32_t nseg, const uint32_t* __restrict__ segdoff,
                                                                  uint32_t* __restrict__ cursor,
-                                                                 uint2* __restrict__ out) {
+                                                                 uint4* __restrict__ out) {
   const uint32_t n = min(*count, cap);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const PeakRecord r = in[i];
-    if (r.seg >= nseg) continue;
-    const uint32_t pos = segoff[r.seg] + atomicAdd(&cursor[r.seg], 1u);
-    out[pos] = make_uint2(static_cast<uint32_t>(r.idx), __float_as_uint(r.snr));
+    if (!(r.seg & kPeakChunk) || chunk_seg(r.seg) >= nseg) continue;
+    const uint32_t sg = chunk_seg(r.seg);
+    out[segdoff[sg] + atomicAdd(&cursor[sg], 1u)] =
+        make_uint4(static_cast<uint32_t>(r.idx), __float_as_uint(r.snr), chunk_count(r.seg), 0u);
   }
 }
 
@@ -462,35 +535,44 @@ void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint
                         hipStream_t s) {
   if (nseg == 0) return;
   PSOUP_CHECK(gap >= 1, "peak_cluster_batch: gap must be positive");
-  uint32_t* segcnt = d_work;
-  uint32_t* segoff = d_work + nseg;
-  uint32_t* cursor = d_work + 2 * nseg;
-  PSOUP_HIP_CHECK(hipMemsetAsync(d_work, 0, 3ull * nseg * sizeof(uint32_t), s));
+  PSOUP_CHECK(nseg <= 65536, "peak_cluster_batch: segment ids are 16-bit in the chunk descriptors");
+  uint32_t* segcnt = d_work;              // crossings per segment
+  uint32_t* segoff = d_work + nseg;       // their exclusive scan (raw segments' offsets)
+  uint32_t* segdcnt = d_work + 2 * nseg;  // chunks per segment
+  uint32_t* segdoff = d_work + 3 * nseg;
+  uint32_t* cursor = d_work + 4 * nseg;
+  uint4* desc = reinterpret_cast<uint4*>(d_sorted);  // chunks <= cap / 2: the first cap entries
+  uint2* raw = d_sorted + cap;
+  PSOUP_HIP_CHECK(hipMemsetAsync(d_work, 0, 5ull * nseg * sizeof(uint32_t), s));
   PSOUP_HIP_CHECK(hipMemsetAsync(d_total, 0, sizeof(uint32_t), s));
   if (nseg <= static_cast<uint32_t>(kSegLds)) {
     const uint64_t per = 256ull * kRecPerThread;
     const unsigned g = static_cast<unsigned>(std::max<uint64_t>(1, (static_cast<uint64_t>(cap) + per - 1) / per));
-    seg_hist_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segcnt);
+    seg_hist_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segcnt, segdcnt);
     post_launch_check("seg_hist_kernel", s);
     seg_scan_kernel<<<1, kClThreads, 0, s>>>(segcnt, nseg, segoff);
     post_launch_check("seg_scan_kernel", s);
-    seg_scatter_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segoff, cursor, d_sorted);
+    seg_scan_kernel<<<1, kClThreads, 0, s>>>(segdcnt, nseg, segdoff);
+    post_launch_check("seg_scan_kernel", s);
+    seg_scatter_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segdoff, cursor, desc);
     post_launch_check("seg_scatter_kernel", s);
   } else {
     const unsigned g = dev::grid_for(cap, 256, 4096);
-    seg_hist_global_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segcnt);
+    seg_hist_global_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segcnt, segdcnt);
     post_launch_check("seg_hist_global_kernel", s);
     seg_scan_kernel<<<1, kClThreads, 0, s>>>(segcnt, nseg, segoff);
     post_launch_check("seg_scan_kernel", s);
-    seg_scatter_global_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segoff, cursor, d_sorted);
+    seg_scan_kernel<<<1, kClThreads, 0, s>>>(segdcnt, nseg, segdoff);
+    post_launch_check("seg_scan_kernel", s);
+    seg_scatter_global_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segdoff, cursor, desc);
     post_launch_check("seg_scatter_global_kernel", s);
   }
-  peak_cluster_kernel<kClSmall, kClThreads><<<nseg, kClThreads, 0, s>>>(d_sorted, segoff, segcnt, gap, 0u, d_out,
-                                                                         d_segtab, d_total);
+  peak_cluster_kernel<kClSmall, kClThreads><<<nseg, kClThreads, 0, s>>>(
+      d_peaks, desc, segoff, segcnt, segdoff, segdcnt, gap, 0u, d_out, d_segtab, d_total, raw);
   post_launch_check("peak_cluster_kernel<small>", s);
   // the large kernel holds a CU's LDS alone: 1024 threads (16 waves)
-  peak_cluster_kernel<kClusterCap, 1024><<<nseg, 1024, 0, s>>>(d_sorted, segoff, segcnt, gap, kClSmall, d_out,
-                                                                d_segtab, d_total);
+  peak_cluster_kernel<kClusterCap, 1024><<<nseg, 1024, 0, s>>>(
+      d_peaks, desc, segoff, segcnt, segdoff, segdcnt, gap, kClSmall, d_out, d_segtab, d_total, raw);
   post_launch_check("peak_cluster_kernel<large>", s);
 }
 

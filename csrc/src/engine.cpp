@@ -818,7 +818,7 @@ void SearchEngine::grow_capacity(uint32_t need) {
   for (auto& s : slots_) {
     s.d_peaks.resize(cap_);
     if (gpu_cluster_) {
-      s.d_sorted.resize(cap_);
+      s.d_sorted.resize(2 * static_cast<size_t>(cap_));  // chunk descriptors, then raw segments' crossings
       s.d_clust.resize(cap_);
       s.h_clust.resize(cap_);
       s.h_raw.resize(cap_);
@@ -840,7 +840,7 @@ void SearchEngine::ensure_batch_buffers(int k) {
   buf_k_ = k;
   if (gpu_cluster_)
     for (auto& s : slots_) {
-      s.d_work.resize(3 * 8 * static_cast<size_t>(k));
+      s.d_work.resize(5 * 8 * static_cast<size_t>(k));
       s.d_segtab.resize(8 * static_cast<size_t>(k));
       s.h_segtab.resize(8 * static_cast<size_t>(k));
       if (gpu_distill_) {
@@ -991,6 +991,7 @@ void SearchEngine::process_slot(Slot& s, int first, int count, uint32_t npeaks,
   seg_count_.assign(static_cast<size_t>(nseg) + 1, 0);
   for (uint32_t i = 0; i < cnt; ++i) {
     const uint32_t seg = s.h_peaks[i].seg;
+    if (seg & kern::kPeakChunk) continue;  // chunk descriptor (device clustering only)
     PSOUP_CHECK(seg < static_cast<uint32_t>(nseg), "peak record outside its batch (segment " << seg << ")");
     seg_count_[seg]++;
   }
@@ -999,7 +1000,8 @@ void SearchEngine::process_slot(Slot& s, int first, int count, uint32_t npeaks,
   sorted_.resize(cnt);
   {
     std::vector<uint32_t> fill(seg_off_.begin(), seg_off_.end() - 1);
-    for (uint32_t i = 0; i < cnt; ++i) sorted_[fill[s.h_peaks[i].seg]++] = s.h_peaks[i];
+    for (uint32_t i = 0; i < cnt; ++i)
+      if (!(s.h_peaks[i].seg & kern::kPeakChunk)) sorted_[fill[s.h_peaks[i].seg]++] = s.h_peaks[i];
   }
   // Per-trial clustering + harmonic distillation.  Trials own disjoint
   // segments of sorted_, so peak-heavy batches (RFI) are spread over the
@@ -1321,7 +1323,7 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
       segtab_.assign(s.h_segtab.data(), s.h_segtab.data() + 8 * static_cast<size_t>(b_count));
       auto copy_seg = [&](const uint2& e) {
         if (e.y & kern::kClusterRaw)
-          PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_raw.data() + e.x, s.d_sorted.data() + e.x,
+          PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_raw.data() + e.x, s.d_sorted.data() + cap_ + e.x,
                                          (e.y & ~kern::kClusterRaw) * sizeof(uint2), hipMemcpyDeviceToHost,
                                          copy_stream_.get()));
         else if (e.y > 0)

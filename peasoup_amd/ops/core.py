@@ -361,7 +361,8 @@ def harmonic_sums(P: torch.Tensor, nlevels: int) -> torch.Tensor:
 def harmonic_peaks(P: torch.Tensor, nlevels: int, starts: Sequence[int], ends: Sequence[int], thresh: float,
                    capacity: int = 1 << 20, layout=None, nbins: int | None = None):
     """Fused harmonic sum + threshold: P [K, n] -> records (trial, level, idx, snr)
-    as int64/float32 tensors sorted by (trial, level, idx).  ``layout``: P's
+    as int64/float32 tensors sorted by (trial, level, idx) (the kernel's chunk
+    descriptors, kernels.hpp kPeakChunk, are dropped).  ``layout``: P's
     rows are spectra of ``nbins`` bins in that PLayout (the fused pass B's
     blocked layout) instead of natural order."""
     _check(P, torch.float32, "P")
@@ -376,6 +377,7 @@ def harmonic_peaks(P: torch.Tensor, nlevels: int, starts: Sequence[int], ends: S
     if c > capacity:
         return harmonic_peaks(P, nlevels, starts, ends, thresh, capacity=c + 1024, layout=layout, nbins=nbins)
     r = rec[:c]
+    r = r[r[:, 0] >= 0]  # drop the chunk descriptors (seg field with kPeakChunk, bit 31, set)
     seg = r[:, 0].to(torch.int64)
     idx = r[:, 1].to(torch.int64)
     snr = r[:, 2].view(torch.float32)

@@ -22,6 +22,28 @@ def _segment(rng, n, span, ties):
     return idx, snr.astype(np.float32)
 
 
+def chunked_records(segs, rng):
+    """Records as harmonic_peaks_batch emits them: per segment, runs of
+    idx-ascending crossings of one 64-bin group, each behind its descriptor
+    {0x80000000 | count << 16 | segment, first idx, position}; chunks in any
+    order (kernels.hpp kPeakChunk)."""
+    chunks = []
+    for s, (idx, snr) in segs.items():
+        grp = idx >> 6
+        cuts = np.flatnonzero(np.diff(grp)) + 1
+        for a, b in zip(np.r_[0, cuts], np.r_[cuts, len(idx)]):
+            chunks.append((s, idx[a:b], snr[a:b]))
+    order = rng.permutation(len(chunks))
+    rows, pos = [], 0
+    for k in order:
+        s, ci, cs = chunks[k]
+        c = len(ci)
+        rows.append(np.array([[0x80000000 | (c << 16) | s, int(ci[0]), pos + 1]], np.uint32))
+        rows.append(np.stack([np.full(c, s, np.uint32), ci.view(np.uint32), cs.view(np.uint32)], axis=1))
+        pos += 1 + c
+    return np.concatenate(rows)
+
+
 def test_peak_cluster_matches_host_scan(C):
     K = C.kernels
     rng = np.random.default_rng(3)
@@ -36,16 +58,14 @@ def test_peak_cluster_matches_host_scan(C):
         span = n * (1 + s % 4) + 10  # dense (most within the gap) to sparse
         idx, snr = _segment(rng, n, span, ties=s % 2 == 0)
         segs[s] = (idx, snr)
-        recs.append(np.stack([np.full(n, s, np.uint32), idx.view(np.uint32), snr.view(np.uint32)], axis=1))
-    allr = np.concatenate(recs)
-    allr = allr[rng.permutation(len(allr))]  # the harmonic kernel's records land unordered
+    allr = chunked_records(segs, rng)  # chunks land in any order
     n = len(allr)
     nseg = len(sizes)
     cap = n + 100
     peaks = torch.from_numpy(allr.reshape(-1).view(np.int32).copy()).to(dev)
     count = torch.tensor([n], dtype=torch.int32, device=dev)
-    work = torch.empty(3 * nseg, dtype=torch.int32, device=dev)
-    srt = torch.empty(2 * cap, dtype=torch.int32, device=dev)
+    work = torch.empty(5 * nseg, dtype=torch.int32, device=dev)
+    srt = torch.empty(4 * cap, dtype=torch.int32, device=dev)
     out = torch.empty(2 * cap, dtype=torch.int32, device=dev)
     tab = torch.empty(2 * nseg, dtype=torch.int32, device=dev)
     tot = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -55,7 +75,7 @@ def test_peak_cluster_matches_host_scan(C):
     torch.cuda.synchronize()
     tab_h = tab.cpu().numpy().view(np.uint32).reshape(nseg, 2)
     out_h = out.cpu().numpy().view(np.uint32).reshape(cap, 2)
-    srt_h = srt.cpu().numpy().view(np.uint32).reshape(cap, 2)
+    srt_h = srt.cpu().numpy().view(np.uint32).reshape(2 * cap, 2)[cap:]  # raw segments: the second half
     assert int(tot.item()) == sum(int(tab_h[s_, 1]) for s_ in range(nseg) if not tab_h[s_, 1] & 0x80000000)
     for s_, sz in enumerate(sizes):
         first, cnt = int(tab_h[s_, 0]), int(tab_h[s_, 1])

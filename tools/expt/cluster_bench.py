@@ -13,6 +13,8 @@ import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
 from peasoup_amd import _C  # noqa: E402
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "tests"))
+from test_peakcluster_gpu import chunked_records  # noqa: E402
 
 
 def main():
@@ -26,7 +28,7 @@ def main():
     a = ap.parse_args()
     K = _C.kernels
     rng = np.random.default_rng(1)
-    recs = []
+    segs = {}
     for sgi in range(a.nseg):
         n = int(rng.integers(a.n // 2, a.n * 3 // 2))
         if a.dense:
@@ -45,16 +47,15 @@ def main():
             spikes = rng.choice(1 << 22, max(1, n // 40), replace=False)
             idx = np.unique((spikes[:, None] + np.arange(-20, 20)[None, :]).reshape(-1))[:n].astype(np.int32)
             snr = (9.0 + 30.0 * rng.random(idx.size)).astype(np.float32)
-        recs.append(np.stack([np.full(idx.size, sgi, np.uint32), idx.view(np.uint32), snr.view(np.uint32)], axis=1))
-    allr = np.concatenate(recs)
-    allr = allr[rng.permutation(len(allr))]
+        segs[sgi] = (idx, snr)
+    allr = chunked_records(segs, rng)  # chunk descriptors + crossings, as the harmonic kernel emits them
     n = len(allr)
     dev = "cuda"
     cap = n + 100
     peaks = torch.from_numpy(allr.reshape(-1).view(np.int32).copy()).to(dev)
     count = torch.tensor([n], dtype=torch.int32, device=dev)
-    work = torch.empty(3 * a.nseg, dtype=torch.int32, device=dev)
-    srt = torch.empty(2 * cap, dtype=torch.int32, device=dev)
+    work = torch.empty(5 * a.nseg, dtype=torch.int32, device=dev)
+    srt = torch.empty(4 * cap, dtype=torch.int32, device=dev)
     out = torch.empty(2 * cap, dtype=torch.int32, device=dev)
     tab = torch.empty(2 * a.nseg, dtype=torch.int32, device=dev)
     tot = torch.zeros(1, dtype=torch.int32, device=dev)
