@@ -66,6 +66,14 @@ __device__ __forceinline__ uint32_t block_excl_sum(uint32_t v, uint32_t* sc, uin
 // A chunk descriptor's segment and crossing count (kPeakChunk records only).
 __device__ __forceinline__ uint32_t chunk_seg(uint32_t f) { return f & 0xffffu; }
 __device__ __forceinline__ uint32_t chunk_count(uint32_t f) { return (f >> 16) & 0x7fu; }
+// A descriptor the clustering may use: its segment in the batch and all its
+// crossings written (a batch over the record capacity -- recomputed by the
+// engine with a larger buffer -- has chunks cut at the capacity: those are
+// skipped, so no kernel reads past the n records held).
+__device__ __forceinline__ bool chunk_ok(const PeakRecord& r, uint32_t nseg, uint32_t n) {
+  return (r.seg & kPeakChunk) && chunk_seg(r.seg) < nseg &&
+         static_cast<uint64_t>(__float_as_uint(r.snr)) + chunk_count(r.seg) <= n;
+}
 
 // Per-segment chunk and crossing counts: each block counts its descriptors
 // in LDS and adds the non-zero counts to the global ones (one atomic per
@@ -84,10 +92,10 @@ __global__ void __launch_bounds__(256) seg_hist_kernel(const PeakRecord* __restr
   for (int r = 0; r < kRecPerThread; ++r) {
     const uint32_t i = base + r * 256u + threadIdx.x;
     if (i < n) {
-      const uint32_t f = in[i].seg;
-      if ((f & kPeakChunk) && chunk_seg(f) < nseg) {
-        atomicAdd(&lc[chunk_seg(f)], 1u);
-        atomicAdd(&lr[chunk_seg(f)], chunk_count(f));
+      const PeakRecord r = in[i];
+      if (chunk_ok(r, nseg, n)) {
+        atomicAdd(&lc[chunk_seg(r.seg)], 1u);
+        atomicAdd(&lr[chunk_seg(r.seg)], chunk_count(r.seg));
       }
     }
   }
@@ -139,7 +147,7 @@ __global__ void __launch_bounds__(256) seg_scatter_kernel(const PeakRecord* __re
     rec[r].seg = 0u;
     if (i < n) {
       rec[r] = in[i];
-      if (!(rec[r].seg & kPeakChunk) || chunk_seg(rec[r].seg) >= nseg) rec[r].seg = 0u;
+      if (!chunk_ok(rec[r], nseg, n)) rec[r].seg = 0u;
       else rank[r] = atomicAdd(&lc[chunk_seg(rec[r].seg)], 1u);
     }
   }
@@ -505,10 +513,10 @@ __global__ void __launch_bounds__(256) seg_hist_global_kernel(const PeakRecord* 
                                                               uint32_t* __restrict__ segdcnt) {
   const uint32_t n = min(*count, cap);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t f = in[i].seg;
-    if ((f & kPeakChunk) && chunk_seg(f) < nseg) {
-      atomicAdd(&segdcnt[chunk_seg(f)], 1u);
-      atomicAdd(&segcnt[chunk_seg(f)], chunk_count(f));
+    const PeakRecord r = in[i];
+    if (chunk_ok(r, nseg, n)) {
+      atomicAdd(&segdcnt[chunk_seg(r.seg)], 1u);
+      atomicAdd(&segcnt[chunk_seg(r.seg)], chunk_count(r.seg));
     }
   }
 }
@@ -521,7 +529,7 @@ __global__ void __launch_bounds__(256) seg_scatter_global_kernel(const PeakRecor
   const uint32_t n = min(*count, cap);
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
     const PeakRecord r = in[i];
-    if (!(r.seg & kPeakChunk) || chunk_seg(r.seg) >= nseg) continue;
+    if (!chunk_ok(r, nseg, n)) continue;
     const uint32_t sg = chunk_seg(r.seg);
     out[segdoff[sg] + atomicAdd(&cursor[sg], 1u)] =
         make_uint4(static_cast<uint32_t>(r.idx), __float_as_uint(r.snr), chunk_count(r.seg), 0u);
