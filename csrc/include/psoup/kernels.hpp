@@ -384,6 +384,9 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
 // segment has more than kClusterCap crossings: then its raw, unsorted
 // crossings are d_sorted[cap + first .. cap + first + count) for the host.
 // d_work: 5 * nseg uint32; d_sorted: 2 * cap entries; d_out: cap entries.
+// Timing (tools/expt/cluster_bench.py --trace): the large kernel's phase
+// timestamps, 8 per workgroup (nullptr: off).
+void peak_cluster_set_trace(unsigned long long* d_events);
 constexpr uint32_t kClusterCap = 14000;
 constexpr uint32_t kClusterRaw = 0x80000000u;
 void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint32_t cap, uint32_t nseg, int gap,

@@ -162,6 +162,16 @@ __global__ void __launch_bounds__(256) seg_scatter_kernel(const PeakRecord* __re
                                                              __float_as_uint(rec[r].snr), chunk_count(rec[r].seg), 0u);
 }
 
+// Phase timestamps (tools/expt/cluster_bench.py --trace): when set, thread 0
+// of each workgroup of the large kernel records the wall clock (100 MHz) at
+// fixed points; a scalar load of a __constant__ pointer, nothing else.
+__constant__ unsigned long long* g_cl_trace = nullptr;
+constexpr int kClTraceEvents = 8;
+__device__ __forceinline__ void cl_trace(int ev) {
+  unsigned long long* tr = g_cl_trace;
+  if (tr != nullptr && threadIdx.x == 0) tr[blockIdx.x * kClTraceEvents + ev] = wall_clock64();
+}
+
 // Exclusive scan of one value per thread over the block (TH threads): wave
 // scans by shuffles, one wave scans the wave totals; two barriers.
 template <int TH>
@@ -194,15 +204,22 @@ __device__ __forceinline__ uint32_t block_scan_excl(uint32_t v, uint32_t* wtot, 
 // kernel also writes the empty segments' entries, the large one the raw
 // entries of segments over its capacity).
 //
-// Sort by idx: an LSD radix sort with 4-bit digits of idx - min(idx) (as many
-// passes as the segment's idx span needs: 5-6 for a whole-spectrum RFI
-// segment).  Between passes the keys live in registers (R per thread,
-// position r * TH + t); a pass ranks each key stably among its digit by wave
-// ballots (16 per row of TH keys), scans the (digit, row, wave) counts and
-// scatters into LDS, then reads the keys back in the new order -- 4 barriers
-// per pass, where the bitonic network it replaces needed ~O(log^2 n) (105 at
-// 14000 crossings), each a full LDS round trip.  The counts alias the jump
-// table, which is only used after the sort.
+// 1. Order the segment's m chunk descriptors by first idx: a rank sort (each
+//    thread counts the smaller first idx among all m, broadcast LDS reads)
+//    when m <= kClThreads -- the usual case: dense RFI runs give ~40
+//    crossings per chunk -- else an LSD radix sort with 4-bit digits of
+//    first idx - min (keys in registers between passes, stable ranks by wave
+//    ballots, counts scanned per (digit, row, wave)).  The sorted chunk
+//    indices end in the jump table.
+// 2. Gather the crossings in idx order into LDS as two arrays (idx, snr):
+//    sorted chunk p starts at the counts of chunks 0 .. p-1.
+// 3. Window test, next() and run starts from the 32 positions after (or
+//    before) a crossing, fetched as independent 16-byte LDS reads of the idx
+//    / snr / flag arrays -- not a dependent walk (gap - 1 <= 29 positions
+//    can lie within the gap: distinct bins).
+// 4. The next survivor at or after every position (per-row ballots, rows
+//    from the last), each run's chain followed by its start's thread, and a
+//    compaction of the peaks in idx order.
 template <uint32_t CAP, int kClThreads>
 __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakRecord* __restrict__ recs,
                                                                   const uint4* __restrict__ desc,
@@ -217,13 +234,19 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
   constexpr uint32_t R = (CAP + kClThreads - 1) / kClThreads;  // rows of kClThreads positions
   constexpr uint32_t kW = kClThreads / 64;
   constexpr uint32_t kCnt = 16 * R * kW;  // radix counts (digit, row, wave)
-  __shared__ uint2 key[CAP];      // sorted chunk descriptors (first idx, index), then the crossings (idx, snr bits)
-  __shared__ uint16_t jmp[CAP > 2 * kCnt ? CAP : 2 * kCnt];  // next survivor / chain jumps; radix counts before
-  __shared__ uint8_t flag[CAP];   // bit 0: survives the window test, bit 1: cluster peak, bit 2: run start
+  constexpr uint32_t kPad = 36;           // window reads run up to 35 positions past / before the data
+  // crossings: idx at kidx[kPad + i], snr at ksnr[kPad + i]; before the gather
+  // the same memory holds the radix sort's (first idx, chunk) keys
+  __shared__ __attribute__((aligned(16))) uint32_t kmem[2 * (CAP + 2 * kPad)];
+  __shared__ uint16_t jmp[CAP > 2 * kCnt ? CAP : 2 * kCnt];  // sorted chunks, then next survivor / chain jumps
+  __shared__ __attribute__((aligned(16))) uint8_t flag[CAP + 2 * kPad];  // at kPad + i: bit 0 survivor, 1 peak, 2 run start
   __shared__ uint32_t sc[kClThreads];
   __shared__ uint32_t wcnt[kClThreads / 64];   // per wave: first survivor of the row
   __shared__ uint32_t rw[R * (kClThreads / 64)];  // per (row, wave): peak count, then its output offset
   __shared__ uint32_t base_s, lo_s, hi_s;
+  uint32_t* const kidx = kmem;
+  float* const ksnr = reinterpret_cast<float*>(kmem + CAP + 2 * kPad);
+  uint2* const key = reinterpret_cast<uint2*>(kmem);  // radix keys (first idx, chunk)
   const int t = threadIdx.x;
   const uint32_t seg = blockIdx.x;
   const uint32_t n = segcnt[seg];                        // crossings
@@ -238,9 +261,8 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
       for (uint32_t j0 = 0; j0 < m; j0 += kClThreads) {
         const uint32_t j = j0 + t;
         const uint4 d = j < m ? dsc[j] : make_uint4(0u, 0u, 0u, 0u);
-        uint32_t tot;
         const uint32_t ex = block_scan_excl<kClThreads>(d.z, sc, &base_s);
-        tot = base_s;
+        const uint32_t tot = base_s;
         for (uint32_t q = 0; q < d.z; ++q) {
           const PeakRecord r = recs[d.y + q];
           raw[segoff[seg] + carry + ex + q] = make_uint2(static_cast<uint32_t>(r.idx), __float_as_uint(r.snr));
@@ -253,8 +275,25 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
     return;
   }
   const int lane = t & 63, w = t >> 6;
-  // ---- radix sort of the m chunk descriptors by first idx (see above)
-  {
+  if (CAP > kClSmall) cl_trace(0);
+  // ---- 1. chunk order -> jmp[p] = chunk at sorted position p
+  if (m <= static_cast<uint32_t>(kClThreads)) {
+    uint32_t* fi = kmem;  // first idx of every chunk (distinct: disjoint 64-bin groups)
+    const uint32_t mine = t < static_cast<int>(m) ? dsc[t].x : 0u;
+    if (t < static_cast<int>(m)) fi[t] = mine;
+    if (t < 4) fi[m + t] = 0xffffffffu;  // pad to a multiple of four
+    __syncthreads();
+    if (t < static_cast<int>(m)) {
+      uint32_t rank = 0;
+      const uint4* f4 = reinterpret_cast<const uint4*>(fi);
+      for (uint32_t j = 0; j < (m + 3) / 4; ++j) {
+        const uint4 v = f4[j];  // every lane reads the same 16 bytes: a broadcast
+        rank += (v.x < mine) + (v.y < mine) + (v.z < mine) + (v.w < mine);
+      }
+      jmp[rank] = static_cast<uint16_t>(t);
+    }
+    __syncthreads();
+  } else {
     uint2 kv[R];
     int lo = 0x7fffffff, hi = -0x7fffffff;
 #pragma unroll
@@ -282,7 +321,7 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
     }
     __syncthreads();
     const uint32_t base = lo_s, span = hi_s - lo_s;
-    const int passes = span == 0 ? 0 : (32 - __builtin_clz(span) + 3) / 4;
+    const int passes = span == 0 ? 1 : (32 - __builtin_clz(span) + 3) / 4;
     uint32_t* cnt = reinterpret_cast<uint32_t*>(jmp);  // [digit][row][wave]
     constexpr uint32_t kPer = (kCnt + kClThreads - 1) / kClThreads;  // counts scanned per thread
     for (int ps = 0; ps < passes; ++ps) {
@@ -291,15 +330,14 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
 #pragma unroll
       for (uint32_t r = 0; r < R; ++r) {
         const uint32_t i = r * kClThreads + t;
-        const bool valid = i < m;
-        dig[r] = valid ? ((kv[r].x - base) >> shift) & 15u : 16u;
+        dig[r] = i < m ? ((kv[r].x - base) >> shift) & 15u : 16u;
         rank[r] = 0;
         if (r * kClThreads + w * 64 < m) {  // wave-uniform: the row's wave holds keys
 #pragma unroll
           for (uint32_t d = 0; d < 16; ++d) {
-            const uint64_t m = __ballot(dig[r] == d);
-            if (dig[r] == d) rank[r] = static_cast<uint32_t>(__builtin_popcountll(m & ((1ull << lane) - 1)));
-            if (lane == 0) cnt[(d * R + r) * kW + w] = static_cast<uint32_t>(__builtin_popcountll(m));
+            const uint64_t mk = __ballot(dig[r] == d);
+            if (dig[r] == d) rank[r] = static_cast<uint32_t>(__builtin_popcountll(mk & ((1ull << lane) - 1)));
+            if (lane == 0) cnt[(d * R + r) * kW + w] = static_cast<uint32_t>(__builtin_popcountll(mk));
           }
         } else if (lane == 0) {
 #pragma unroll
@@ -307,8 +345,6 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
         }
       }
       __syncthreads();
-      // exclusive scan of the counts in (digit, row, wave) order: each thread
-      // takes kPer consecutive entries
       {
         uint32_t loc[kPer], sum = 0;
 #pragma unroll
@@ -330,80 +366,95 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
       for (uint32_t r = 0; r < R; ++r)
         if (dig[r] < 16) key[cnt[(dig[r] * R + r) * kW + w] + rank[r]] = kv[r];
       __syncthreads();
-      if (ps + 1 < passes) {
-#pragma unroll
-        for (uint32_t r = 0; r < R; ++r) {
-          const uint32_t i = r * kClThreads + t;
-          if (i < m) kv[r] = key[i];
-        }
-        __syncthreads();  // the next pass's counts and scatter overwrite cnt / key
-      }
-    }
-    if (passes == 0) {  // a single chunk: already in order
 #pragma unroll
       for (uint32_t r = 0; r < R; ++r) {
         const uint32_t i = r * kClThreads + t;
-        if (i < m) key[i] = kv[r];
+        if (i < m) kv[r] = key[i];
       }
-      __syncthreads();
+      __syncthreads();  // the next pass's counts and scatter overwrite cnt / key
     }
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t i = r * kClThreads + t;
+      if (i < m) jmp[i] = static_cast<uint16_t>(kv[r].y);
+    }
+    __syncthreads();
   }
-  // ---- the crossings in idx order: sorted chunk p starts at the sum of the
-  // counts of chunks 0 .. p-1 (thread t owns the consecutive sorted chunks
-  // [t q, t q + q)); the sorted chunk indices move to the jump table (< 2^16)
-  // so each thread can copy its chunks' crossings over the keys
+  if (CAP > kClSmall) cl_trace(1);
+  // ---- 2. the crossings in idx order (thread t owns the consecutive sorted
+  // chunks [t q, t q + q))
   {
     const uint32_t q = (m + kClThreads - 1) / kClThreads;
     const uint32_t p0 = t * q, p1 = min(m, p0 + q);
     uint32_t sum = 0;
-    for (uint32_t p = p0; p < p1; ++p) {
-      const uint32_t j = key[p].y;
-      jmp[p] = static_cast<uint16_t>(j);
-      sum += dsc[j].z;
-    }
-    uint32_t dst = block_scan_excl<kClThreads>(sum, sc, nullptr);  // (its barriers retire the key reads)
+    for (uint32_t p = p0; p < p1; ++p) sum += dsc[jmp[p]].z;
+    uint32_t dst = kPad + block_scan_excl<kClThreads>(sum, sc, nullptr);
     for (uint32_t p = p0; p < p1; ++p) {
       const uint4 d = dsc[jmp[p]];
       for (uint32_t c = 0; c < d.z; ++c) {
         const PeakRecord r = recs[d.y + c];
-        key[dst + c] = make_uint2(static_cast<uint32_t>(r.idx), __float_as_uint(r.snr));
+        kidx[dst + c] = static_cast<uint32_t>(r.idx);
+        ksnr[dst + c] = r.snr;
       }
       dst += d.z;
     }
+    // pads: idx far outside every window (before: never within the gap,
+    // after: never below a target); flags clear
+    if (t < static_cast<int>(kPad)) {
+      kidx[t] = 0x80000000u;  // as int: below everything
+      ksnr[t] = 0.f;
+      kidx[kPad + n + t] = 0x7fffffffu;
+      ksnr[kPad + n + t] = 0.f;
+      flag[t] = 0;
+      flag[kPad + n + t] = 0;
+    }
     __syncthreads();
   }
+  if (CAP > kClSmall) cl_trace(2);
   // Every phase below gives position i = r * kClThreads + t to thread t
   // (row r): consecutive lanes touch consecutive LDS words, and wave ballots
   // order the survivors / peaks inside a row.
   const uint32_t nrow = (n + kClThreads - 1) / kClThreads;
-  // (1) window test: the following crossings within the gap, four
-  // independent LDS reads at a time (dense runs test ~gap neighbours)
+  // ---- 3a. window test: survives iff no strictly larger crossing among the
+  // following positions within the gap (at most 29 of them)
   for (uint32_t r = 0; r < nrow; ++r) {
     const uint32_t i = r * kClThreads + t;
     if (i >= n) break;
-    const int xi = static_cast<int>(key[i].x);
-    const float si = __uint_as_float(key[i].y);
-    bool keep = true, more = true;
-    for (uint32_t j = i + 1; more && keep && j < n; j += 4) {
-      uint2 q[4];
+    const uint32_t a = (kPad + i + 1) & ~3u, sh = (kPad + i + 1) - a;  // aligned base, offset of i + 1 (0..3)
+    const int xi = static_cast<int>(kidx[kPad + i]);
+    const float si = ksnr[kPad + i];
+    bool keep = true;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) q[e] = key[min(j + e, n - 1)];
+    for (int hlf = 0; hlf < 2; ++hlf) {  // two halves of 16 positions: fewer live registers
+      uint4 xv[4];
+      float4 sv[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const bool in = more && j + e < n && static_cast<int>(q[e].x) - xi < gap;
-        more = in;
-        keep = keep && !(in && __uint_as_float(q[e].y) > si);
+      for (int v = 0; v < 4; ++v) {
+        xv[v] = *reinterpret_cast<const uint4*>(kidx + a + 16 * hlf + 4 * v);
+        sv[v] = *reinterpret_cast<const float4*>(ksnr + a + 16 * hlf + 4 * v);
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const uint32_t xs[4] = {xv[v].x, xv[v].y, xv[v].z, xv[v].w};
+        const float ss[4] = {sv[v].x, sv[v].y, sv[v].z, sv[v].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t off = static_cast<uint32_t>(16 * hlf + 4 * v + e);  // position a + off
+          const bool in = off >= sh && static_cast<int>(xs[e]) - xi < gap;
+          keep = keep && !(in && ss[e] > si);
+        }
       }
     }
-    flag[i] = keep ? 1 : 0;
+    flag[kPad + i] = keep ? 1 : 0;
   }
   __syncthreads();
-  // (3) next survivor at or after every position: rows from the last, a
+  if (CAP > kClSmall) cl_trace(3);
+  // ---- 3b. next survivor at or after every position: rows from the last, a
   // row's waves from their ballots, the carry from the rows after it
   uint32_t carry = n;
   for (uint32_t r = nrow; r-- > 0;) {
     const uint32_t i = r * kClThreads + t;
-    const bool sv = i < n && (flag[i] & 1);
+    const bool sv = i < n && (flag[kPad + i] & 1);
     const uint64_t mask = __ballot(sv);
     if (lane == 0) wcnt[w] = mask ? r * kClThreads + w * 64 + static_cast<uint32_t>(__builtin_ctzll(mask)) : n;
     __syncthreads();
@@ -416,9 +467,10 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
     carry = rowfirst < n ? rowfirst : carry;
     __syncthreads();
   }
-  // next(i): the first survivor with idx >= idx_i + gap (at most gap - 1
-  // positions ahead have smaller idx: distinct bins); a survivor starts a
-  // run when no survivor lies within the gap before it (bit 2)
+  if (CAP > kClSmall) cl_trace(4);
+  // ---- 3c. next(i): the first survivor with idx >= idx_i + gap = the next
+  // survivor from the first position not below that target; a survivor
+  // starts a run when no survivor lies within the gap before it (bit 2)
   uint32_t nx[R];
   bool rs[R];
 #pragma unroll
@@ -426,27 +478,38 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
     const uint32_t i = r * kClThreads + t;
     nx[r] = n;
     rs[r] = false;
-    if (i < n && (flag[i] & 1)) {
-      const int xi = static_cast<int>(key[i].x);
-      const int target = xi + gap;
-      uint32_t p = i + 1;
-      bool go = true;
-      while (go && p < n) {  // four reads at a time
-        uint32_t a[4];
+    if (i < n && (flag[kPad + i] & 1)) {
+      const int xi = static_cast<int>(kidx[kPad + i]);
+      // positions after i below the target (sorted: a prefix of the window)
+      const uint32_t a = (kPad + i + 1) & ~3u, sh = (kPad + i + 1) - a;
+      uint32_t below = 0;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) a[e] = key[min(p + e, n - 1)].x;
+      for (int v = 0; v < 8; ++v) {
+        const uint4 xv = *reinterpret_cast<const uint4*>(kidx + a + 4 * v);
+        const uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const bool step = go && p < n && static_cast<int>(a[e]) < target;
-          p += step ? 1u : 0u;
-          go = step;
+          const uint32_t off = static_cast<uint32_t>(4 * v + e);
+          below += (off >= sh && static_cast<int>(xs[e]) < xi + gap) ? 1u : 0u;
         }
       }
+      const uint32_t p = i + 1 + below;
       nx[r] = p < n ? jmp[p] : n;
+      // survivors among the 32 positions before i within the gap
+      const uint32_t b = (kPad + i - 32) & ~3u;  // >= 0: kPad >= 36
       bool start = true;
-      for (uint32_t q = i; start && q-- > 0;) {
-        if (xi - static_cast<int>(key[q].x) >= gap) break;
-        if (flag[q] & 1) start = false;
+#pragma unroll
+      for (int v = 0; v < 9; ++v) {
+        const uint4 xv = *reinterpret_cast<const uint4*>(kidx + b + 4 * v);
+        const uint32_t fw = *reinterpret_cast<const uint32_t*>(flag + b + 4 * v);
+        const uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t pos = b + static_cast<uint32_t>(4 * v + e);  // padded position
+          const bool before = pos < kPad + i;
+          const bool s1 = (fw >> (8 * e)) & 1u;
+          start = start && !(before && s1 && xi - static_cast<int>(xs[e]) < gap);
+        }
       }
       rs[r] = start;
     }
@@ -455,41 +518,42 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
     const uint32_t i = r * kClThreads + t;
-    if (i < n && (flag[i] & 1)) {
+    if (i < n && (flag[kPad + i] & 1)) {
       jmp[i] = static_cast<uint16_t>(nx[r]);
-      if (rs[r]) flag[i] = 5;
+      if (rs[r]) flag[kPad + i] = 5;
     }
   }
   __syncthreads();
-  // (2) the chains: within a run an anchor never moves, so the run's peaks
-  // are its start, then next(), next(next()), ... until the chain reaches the
-  // following run's start; each run start's thread follows its own run
+  if (CAP > kClSmall) cl_trace(5);
+  // ---- 4. the chains: within a run an anchor never moves, so the run's
+  // peaks are its start, then next(), next(next()), ... until the chain
+  // reaches the following run's start; each run start's thread follows its run
 #pragma unroll
   for (uint32_t r = 0; r < R; ++r) {
     if (!rs[r]) continue;
     uint32_t p = r * kClThreads + t;
     do {
-      flag[p] = static_cast<uint8_t>(flag[p] | 2);
+      flag[kPad + p] = static_cast<uint8_t>(flag[kPad + p] | 2);
       p = jmp[p];
-    } while (p < n && !(flag[p] & 4));
+    } while (p < n && !(flag[kPad + p] & 4));
   }
   __syncthreads();
+  if (CAP > kClSmall) cl_trace(6);
   // compaction of the peaks in idx order: per (row, wave) counts, their
   // exclusive scan, then ballot ranks inside each wave
   for (uint32_t r = 0; r < nrow; ++r) {
     const uint32_t i = r * kClThreads + t;
-    const uint64_t mask = __ballot(i < n && (flag[i] & 2));
+    const uint64_t mask = __ballot(i < n && (flag[kPad + i] & 2));
     if (lane == 0) rw[r * kW + w] = static_cast<uint32_t>(__builtin_popcountll(mask));
   }
   __syncthreads();
   {
     static_assert(R * kW <= kClThreads, "one (row, wave) count per thread");
     const uint32_t v = static_cast<uint32_t>(t) < nrow * kW ? rw[t] : 0u;
-    uint32_t acc;
     const uint32_t ex = block_scan_excl<kClThreads>(v, sc, &base_s);
     if (static_cast<uint32_t>(t) < nrow * kW) rw[t] = ex;
     __syncthreads();
-    acc = base_s;  // the segment's peak count
+    const uint32_t acc = base_s;  // the segment's peak count
     __syncthreads();
     if (t == 0) {
       base_s = atomicAdd(total, acc);
@@ -499,11 +563,13 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
   __syncthreads();
   for (uint32_t r = 0; r < nrow; ++r) {
     const uint32_t i = r * kClThreads + t;
-    const bool pk = i < n && (flag[i] & 2);
+    const bool pk = i < n && (flag[kPad + i] & 2);
     const uint64_t mask = __ballot(pk);
     if (pk)
-      out[base_s + rw[r * kW + w] + static_cast<uint32_t>(__builtin_popcountll(mask & ((1ull << lane) - 1)))] = key[i];
+      out[base_s + rw[r * kW + w] + static_cast<uint32_t>(__builtin_popcountll(mask & ((1ull << lane) - 1)))] =
+          make_uint2(kidx[kPad + i], __float_as_uint(ksnr[kPad + i]));
   }
+  if (CAP > kClSmall) cl_trace(7);
 }
 
 // Fallbacks for batches with more than kSegLds segments: one global atomic per descriptor.
@@ -538,11 +604,17 @@ __global__ void __launch_bounds__(256) seg_scatter_global_kernel(const PeakRecor
 
 }  // namespace
 
+void peak_cluster_set_trace(unsigned long long* d_events) {
+  PSOUP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_cl_trace), &d_events, sizeof(d_events)));
+}
+
 void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint32_t cap, uint32_t nseg, int gap,
                         uint32_t* d_work, uint2* d_sorted, uint2* d_out, uint2* d_segtab, uint32_t* d_total,
                         hipStream_t s) {
   if (nseg == 0) return;
-  PSOUP_CHECK(gap >= 1, "peak_cluster_batch: gap must be positive");
+  // the window phases read the 32 positions next to a crossing: gap - 1 <= 29
+  // of them can lie within the gap (the reference's min_gap is 30)
+  PSOUP_CHECK(gap >= 1 && gap <= 30, "peak_cluster_batch: gap must be in [1, 30]");
   PSOUP_CHECK(nseg <= 65536, "peak_cluster_batch: segment ids are 16-bit in the chunk descriptors");
   uint32_t* segcnt = d_work;              // crossings per segment
   uint32_t* segoff = d_work + nseg;       // their exclusive scan (raw segments' offsets)

@@ -562,6 +562,8 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("insize", &kern::Fft4Geom::insize);
   k.def("fft4_geometry", &kern::fft4_geometry);
   k.def("fft4_set_flags", &kern::fft4_set_flags);
+  k.def("peak_cluster_set_trace",
+        [](uintptr_t p) { kern::peak_cluster_set_trace(reinterpret_cast<unsigned long long*>(p)); });
   k.def("fft4_set_trace", [](uintptr_t p) { kern::fft4_set_trace(reinterpret_cast<unsigned long long*>(p)); });
   k.def("fft4_flags", &kern::fft4_flags);
   k.def("fft4_tables", [](const kern::Fft4Geom& g) {

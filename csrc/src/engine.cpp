@@ -788,6 +788,7 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     s.h_count.resize(3);
   }
   if (const char* e = std::getenv("PSOUP_GPU_CLUSTER")) gpu_cluster_ = std::atoi(e) != 0;
+  gpu_cluster_ = gpu_cluster_ && p_.min_gap >= 1 && p_.min_gap <= 30;  // the device windows span 32 positions
   // per-trial harmonic distillation on the device: needs the device clusters,
   // the fast relation's tolerance range, and bins that fit the record's 29 bits
   if (const char* e = std::getenv("PSOUP_GPU_DISTILL")) gpu_distill_ = std::atoi(e) != 0;

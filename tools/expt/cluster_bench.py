@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--nseg", type=int, default=2048)
     ap.add_argument("--n", type=int, default=4200)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--trace", action="store_true", help="per-phase wall time of the large cluster kernel")
     ap.add_argument("--dense", action="store_true",
                     help="RFI-like segments: runs of 100-500 consecutive bins (acceleration-smeared harmonics), "
                          "S/N a smooth bump plus noise")
@@ -72,6 +73,19 @@ def main():
     torch.cuda.synchronize()
     print(f"{'dense' if a.dense else 'spiky'} records={n} segments={a.nseg}: "
           f"{e0.elapsed_time(e1) / a.reps:.3f} ms per batch", flush=True)
+    if a.trace:
+        tr = torch.zeros(a.nseg * 8, dtype=torch.int64, device=dev)
+        K.peak_cluster_set_trace(tr.data_ptr())
+        run()
+        torch.cuda.synchronize()
+        K.peak_cluster_set_trace(0)
+        t = tr.view(a.nseg, 8).cpu().numpy()
+        ok = t[:, 7] > 0  # segments the large kernel clustered
+        d = np.diff(t[ok], axis=1) * 10.0  # 100 MHz ticks -> ns
+        names = ["sort", "gather", "window", "nextsurv", "next+runs", "chains", "compact"]
+        print(f"large-kernel segments: {ok.sum()}, per-segment wall (us): " +
+              ", ".join(f"{nm} {v / 1e3:.1f}" for nm, v in zip(names, d.mean(axis=0))) +
+              f"; total {d.sum(axis=1).mean() / 1e3:.1f}", flush=True)
 
 
 if __name__ == "__main__":
