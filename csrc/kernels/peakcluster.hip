@@ -470,17 +470,22 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
   if (CAP > kClSmall) cl_trace(4);
   // ---- 3c. next(i): the first survivor with idx >= idx_i + gap = the next
   // survivor from the first position not below that target; a survivor
-  // starts a run when no survivor lies within the gap before it (bit 2)
-  uint32_t nx[R];
-  bool rs[R];
-#pragma unroll
-  for (uint32_t r = 0; r < R; ++r) {
+  // starts a run when no survivor lies within the gap before it (bit 2).
+  // Both are written in place: a survivor's own jump entry is never read
+  // here (the next survivor at or after a survivor is itself), and bit 2
+  // leaves the survivor bit readers test unchanged -- so the row loop keeps
+  // no per-row registers and stays a loop.
+  for (uint32_t r = 0; r < nrow; ++r) {
     const uint32_t i = r * kClThreads + t;
-    nx[r] = n;
-    rs[r] = false;
-    if (i < n && (flag[kPad + i] & 1)) {
-      const int xi = static_cast<int>(kidx[kPad + i]);
-      // positions after i below the target (sorted: a prefix of the window)
+    if (i >= n || !(flag[kPad + i] & 1)) continue;
+    const int xi = static_cast<int>(kidx[kPad + i]);
+    // positions after i below the target (sorted: a prefix of the window);
+    // fast path: a run of consecutive bins reaches the target exactly gap
+    // positions ahead
+    uint32_t p;
+    if (i + gap < n && static_cast<int>(kidx[kPad + i + gap]) == xi + gap) {
+      p = i + gap;
+    } else {
       const uint32_t a = (kPad + i + 1) & ~3u, sh = (kPad + i + 1) - a;
       uint32_t below = 0;
 #pragma unroll
@@ -493,11 +498,16 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
           below += (off >= sh && static_cast<int>(xs[e]) < xi + gap) ? 1u : 0u;
         }
       }
-      const uint32_t p = i + 1 + below;
-      nx[r] = p < n ? jmp[p] : n;
-      // survivors among the 32 positions before i within the gap
+      p = i + 1 + below;
+    }
+    const uint32_t nx = p < n ? ((flag[kPad + p] & 1) ? p : jmp[p]) : n;
+    // run start: no survivor within the gap before i; fast path: the
+    // previous position is a survivor within the gap
+    bool start = true;
+    if (i > 0 && (flag[kPad + i - 1] & 1) && xi - static_cast<int>(kidx[kPad + i - 1]) < gap) {
+      start = false;
+    } else {
       const uint32_t b = (kPad + i - 32) & ~3u;  // >= 0: kPad >= 36
-      bool start = true;
 #pragma unroll
       for (int v = 0; v < 9; ++v) {
         const uint4 xv = *reinterpret_cast<const uint4*>(kidx + b + 4 * v);
@@ -511,27 +521,19 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
           start = start && !(before && s1 && xi - static_cast<int>(xs[e]) < gap);
         }
       }
-      rs[r] = start;
     }
-  }
-  __syncthreads();
-#pragma unroll
-  for (uint32_t r = 0; r < R; ++r) {
-    const uint32_t i = r * kClThreads + t;
-    if (i < n && (flag[kPad + i] & 1)) {
-      jmp[i] = static_cast<uint16_t>(nx[r]);
-      if (rs[r]) flag[kPad + i] = 5;
-    }
+    jmp[i] = static_cast<uint16_t>(nx);
+    if (start) flag[kPad + i] = 5;
   }
   __syncthreads();
   if (CAP > kClSmall) cl_trace(5);
   // ---- 4. the chains: within a run an anchor never moves, so the run's
   // peaks are its start, then next(), next(next()), ... until the chain
   // reaches the following run's start; each run start's thread follows its run
-#pragma unroll
-  for (uint32_t r = 0; r < R; ++r) {
-    if (!rs[r]) continue;
-    uint32_t p = r * kClThreads + t;
+  for (uint32_t r = 0; r < nrow; ++r) {
+    const uint32_t i = r * kClThreads + t;
+    if (i >= n || !(flag[kPad + i] & 4)) continue;
+    uint32_t p = i;
     do {
       flag[kPad + p] = static_cast<uint8_t>(flag[kPad + p] | 2);
       p = jmp[p];

@@ -46,7 +46,8 @@ def main():
             idx, snr = idx[:n].astype(np.int32), snr[:n].astype(np.float32)
         else:
             spikes = rng.choice(1 << 22, max(1, n // 40), replace=False)
-            idx = np.unique((spikes[:, None] + np.arange(-20, 20)[None, :]).reshape(-1))[:n].astype(np.int32)
+            idx = np.unique((spikes[:, None] + np.arange(-20, 20)[None, :]).reshape(-1))
+            idx = idx[idx >= 0][:n].astype(np.int32)
             snr = (9.0 + 30.0 * rng.random(idx.size)).astype(np.float32)
         segs[sgi] = (idx, snr)
     allr = chunked_records(segs, rng)  # chunk descriptors + crossings, as the harmonic kernel emits them
