@@ -13,10 +13,14 @@ One step (per rank, weak scaling -- fixed work per GPU):
     convention: ~684 trials per DM at 2^23 x 64 us) with an 8-harmonic sum,
     in 512-trial batches on one stream: fused resample + two-pass four-step
     FFT -> paired real-FFT post-processing + interbin/normalise -> LDS-staged
-    harmonic sum + peak compaction -> peak clustering on the GPU -> host
-    distillation (overlapped with the next batch),
+    harmonic sum + peak compaction -> peak clustering and per-trial
+    harmonic distillation on the GPU -> per-DM acceleration distillation on
+    host workers (overlapped with the next batches),
   * gather every rank's candidates to all ranks over RCCL and run the global
-    DM/harmonic distillation + scoring.
+    DM/harmonic distillation + scoring -- on a worker thread, overlapped with
+    the next step's dedispersion and search as the pipeline's DM blocks are
+    (the timed region ends after the last step's merge; --serial-merge runs
+    them back to back).
 The synthetic filterbank (uniform 2-bit noise, random seed) is generated on
 rank 0's GPU and RCCL-broadcast to the others outside the timed region.
 
@@ -65,6 +69,9 @@ def parse():
     p.add_argument("--signal", action="store_true",
                    help="peak-heavy data instead of pure noise: injected pulsars plus strong undispersed periodic "
                         "RFI (>= 1e4 threshold crossings per DM), to time the host clustering / distillation")
+    p.add_argument("--serial-merge", action="store_true",
+                   help="run each step's candidate gather + global distillation before the next step starts "
+                        "(default: overlapped with the next step, as the pipeline's DM blocks are)")
     p.add_argument("--as-rank", default="",
                    help="N:r[,r...] -- on one GPU, time rank r's shard of a world-N run (the DM list of N ranks, "
                         "shard [r*dms, (r+1)*dms)), one JSON line per r: checks that every rank's step costs the same")
@@ -157,12 +164,16 @@ def main() -> int:
     trials_per_step = int(pdist.all_reduce_sum(tot).item())
 
     phase = {"search": 0.0, "merge": 0.0, "ser": 0.0, "gather": 0.0, "gds": 0.0}
+    # Steps are pipelined like the production run's DM blocks: step k's
+    # candidate gather + global distillation (one worker thread, so the
+    # gather collectives stay in order) overlaps step k+1's dedispersion and
+    # search; the timed region ends after the last step's merge.
+    from concurrent.futures import ThreadPoolExecutor
 
-    def step():
-        t = time.perf_counter()
-        local = rs.search(shard, chunk=a.dms_per_gpu)
+    merger = ThreadPoolExecutor(max_workers=1) if not a.serial_merge else None
+
+    def merge(local):
         t1 = time.perf_counter()
-        phase["search"] += t1 - t
         blob = _C.serialize_candidates(local)
         t2 = time.perf_counter()
         blobs = pdist.gather_bytes(blob, dst=None)
@@ -176,17 +187,27 @@ def main() -> int:
         phase["blob_bytes"] = len(blob)
         return out
 
+    def step():
+        t = time.perf_counter()
+        local = rs.search(shard, chunk=a.dms_per_gpu)
+        phase["search"] += time.perf_counter() - t
+        return merger.submit(merge, local) if merger else merge(local)
+
+    def finish(r):
+        return r.result() if merger else r
+
     for _ in range(a.warmup):
-        step()
+        finish(step())
     for e in rs.engines:
         e.reset_counters()
     phase.update(search=0.0, merge=0.0, ser=0.0, gather=0.0, gds=0.0)
     pdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ncands = 0
-    for _ in range(a.steps):
-        ncands = len(step())
+    pending = [step() for _ in range(a.steps)]
+    ncands = len(finish(pending[-1]))
+    for r in pending:
+        finish(r)
     torch.cuda.synchronize()
     pdist.barrier()
     elapsed = time.perf_counter() - t0
@@ -235,6 +256,7 @@ def main() -> int:
                 # acceleration loop, then the candidate gather + global distillation
                 "search_s_per_step": round(phase["search"] / a.steps, 4),
                 "merge_s_per_step": round(phase["merge"] / a.steps, 4),
+                "merge_overlapped": not a.serial_merge,
                 "merge_split_s": {k: round(phase[k] / a.steps, 4) for k in ("ser", "gather", "gds")},
                 "candidate_blob_bytes": phase.get("blob_bytes", 0),
                 "accel_s_per_step": round(ctr.get("accel_s", 0) / a.steps, 4),
