@@ -492,6 +492,9 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
       st_map["peak_overflows"] += static_cast<double>(c.overflows);
       st_map["accel_loop_s"] += c.accel_s;
       st_map["host_distill_s"] += c.host_s;
+      st_map["trials_distilled_on_gpu"] += static_cast<double>(c.gpu_distilled);
+      st_map["trials_distilled_on_host"] += static_cast<double>(c.host_distilled);
+      st_map["accel_distill_s"] += c.accd_s;
       st_map["fft_mode"] = engine.fft_mode();
       st_map["accel_batch"] = engine.batch_size();
       st_map["sub_batch"] = engine.sub_batch();

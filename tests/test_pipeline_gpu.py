@@ -333,3 +333,38 @@ def test_headline_shape_binary_pulsar_and_fft_modes(C):
         assert b.freq == pytest.approx(a.freq, rel=1e-7)
         assert (b.dm, b.nh, b.acc) == (a.dm, a.nh, a.acc)
         assert b.snr == pytest.approx(a.snr, rel=1e-4)
+
+
+def test_peak_heavy_candidates_equal_across_clustering_paths(tmp_path):
+    """RFI-heavy data (undispersed 50 Hz / 16.7 Hz pulse trains, hundreds of
+    harmonics above threshold in every acceleration trial) through the native
+    pipeline: device clustering + device harmonic distillation (default),
+    device clustering + host distillation, and the all-host reference path
+    write byte-identical candidate files."""
+    from peasoup_amd.utils import synthetic
+
+    hdr = synthetic.make_header(nchans=64, nbits=2, tsamp=256e-6, fch1=1400.0, foff=-2.0)
+    nsamps = (1 << 18) + 2000
+    sky = [synthetic.PulsarSpec(period=0.02, dm=0.0, duty=0.02, amplitude=0.12),
+           synthetic.PulsarSpec(period=0.06, dm=0.0, duty=0.03, amplitude=0.08),
+           synthetic.PulsarSpec(period=0.0123, dm=30.0, duty=0.08, amplitude=0.08, accel=40.0)]
+    fil = str(tmp_path / "rfi.fil")
+    synthetic.write(fil, nsamps, hdr, sky, seed=4)
+    outs = {}
+    for name, env_extra in (("gpu", {}), ("host_distill", {"PSOUP_GPU_DISTILL": "0"}),
+                            ("host", {"PSOUP_GPU_CLUSTER": "0"})):
+        d = tmp_path / name
+        r = subprocess.run([os.path.join(REPO, "bin", "peasoup"), "-i", fil, "-o", str(d), "--dm_end", "60",
+                            "--acc_start", "-60", "--acc_end", "60", "-n", "4", "--npdmp", "0", "--limit", "5000",
+                            "--trace_json", str(d) + ".json"],
+                           capture_output=True, text=True, timeout=600, env=dict(os.environ, **env_extra))
+        assert r.returncode == 0, r.stderr
+        outs[name] = (d / "candidates.peasoup").read_bytes()
+    assert len(outs["gpu"]) > 10000  # many candidates with assoc trees
+    assert outs["gpu"] == outs["host_distill"] == outs["host"]
+    import json
+
+    dev = {k: json.load(open(str(tmp_path / k) + ".json"))["devices"][0] for k in outs}
+    assert dev["gpu"]["trials_distilled_on_gpu"] > 0.9 * (dev["gpu"]["trials_distilled_on_gpu"] +
+                                                          dev["gpu"]["trials_distilled_on_host"])
+    assert dev["host_distill"]["trials_distilled_on_gpu"] == 0
