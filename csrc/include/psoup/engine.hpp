@@ -256,7 +256,7 @@ struct SearchCounters {
   uint64_t gpu_distilled = 0, host_distilled = 0;  // trials distilled on the device / on the host
   double whiten_s = 0, accel_s = 0, host_s = 0;
   double accd_s = 0;    // acceleration distillation (host worker time, mostly overlapped)
-  double tail_s = 0;    // wall time from the last batch's retirement to the call's return
+  double tail_s = 0;    // time collect() waited for the acceleration distillation
 };
 
 class SearchEngine {
@@ -284,6 +284,23 @@ class SearchEngine {
     std::vector<float> accs;
   };
   std::vector<CandidateList> search_prepared_many(const std::vector<Job>& jobs);
+  // The same in two halves: search_prepared_many_async returns once every
+  // batch has retired and its peaks are on the host, while the per-DM
+  // acceleration distillation may still run on the engine's workers; the
+  // caller issues its next GPU work (the next DM block) and then collects.
+  // Any number of searches may be pending; collect() waits for one and
+  // returns its per-job lists (rethrowing a worker's error).
+  struct Pending {
+    std::vector<CandidateList> out, by_job;
+    std::vector<double> accd_t;
+    std::mutex mu;
+    std::condition_variable cv;
+    int remaining = 0;   // acceleration distillation tasks not yet finished
+    std::exception_ptr err;
+    double accel_s = 0;  // host wall time of the call until it returned
+  };
+  std::shared_ptr<Pending> search_prepared_many_async(const std::vector<Job>& jobs);
+  std::vector<CandidateList> collect(const std::shared_ptr<Pending>& p);
   int max_prepare() const { return max_prep_; }
   // Allocate up front what prepare(count) and search_prepared_many over
   // `trials` trials would grow on first use (a growth mid-search frees the
@@ -350,7 +367,6 @@ class SearchEngine {
   bool gpu_cluster_ = true;  // env PSOUP_GPU_CLUSTER=0: cluster on the host (reference path)
   bool gpu_distill_ = true;  // env PSOUP_GPU_DISTILL=0: per-trial harmonic distillation on the host
   kern::HarmDistillParams hdp_{};
-  std::unique_ptr<TaskQueue> accq_;  // per-DM acceleration distillation as each DM's last batch retires
   // flat trial list of the current search_prepared_many call
   const std::vector<Job>* jobs_ = nullptr;
   std::vector<int> flat_job_;
@@ -413,6 +429,9 @@ class SearchEngine {
   std::vector<uint32_t> seg_count_, seg_off_;
   std::vector<kern::PeakRecord> sorted_;
   std::unique_ptr<HostPool> pool_;  // null: serial host processing
+  // per-DM acceleration distillation as each DM's last batch retires (last
+  // member: destroyed first, its workers drain before accd_ goes away)
+  std::unique_ptr<TaskQueue> accq_;
 };
 
 // Zap mask for an FFT size (birdiezapper.hpp / kernels.cu:1036-1069 semantics).

@@ -792,6 +792,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("min_batches", &SearchParams::min_batches)
       .def_readwrite("min_gap", &SearchParams::min_gap)
       .def_readwrite("fft_mode", &SearchParams::fft_mode);
+  py::class_<SearchEngine::Pending, std::shared_ptr<SearchEngine::Pending>>(m, "PendingSearch");
   py::class_<SearchEngine>(m, "SearchEngine")
       .def(py::init([](const SearchParams& p, uintptr_t s) { return new SearchEngine(p, S(s)); }))
       .def("search_trial", [](SearchEngine& e, uintptr_t trial, uint64_t nsamps, float dm, int dm_idx,
@@ -815,6 +816,15 @@ PYBIND11_MODULE(_C, m) {
         return e.search_prepared_many(js);
       }, py::arg("jobs"), py::call_guard<py::gil_scoped_release>(),
          "jobs: [(prepared index, dm, dm_idx, accs)] -> one candidate list per job")
+      .def("search_prepared_many_async", [](SearchEngine& e, const std::vector<std::tuple<int, float, int, std::vector<float>>>& jobs) {
+        std::vector<SearchEngine::Job> js;
+        js.reserve(jobs.size());
+        for (const auto& j : jobs) js.push_back(SearchEngine::Job{std::get<0>(j), std::get<1>(j), std::get<2>(j), std::get<3>(j)});
+        return e.search_prepared_many_async(js);
+      }, py::arg("jobs"), py::call_guard<py::gil_scoped_release>(),
+         "as search_prepared_many, returning once the batches have retired; collect(handle) waits for the "
+         "per-DM acceleration distillation still running on the engine's workers")
+      .def("collect", &SearchEngine::collect, py::arg("handle"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("max_prepare", &SearchEngine::max_prepare)
       .def_property_readonly("batch_size", &SearchEngine::batch_size)
       .def_property_readonly("last_batch", &SearchEngine::last_batch)

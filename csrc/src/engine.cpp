@@ -1199,19 +1199,40 @@ void SearchEngine::reserve(int count, int trials) {
 }
 
 std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<Job>& jobs) {
+  return collect(search_prepared_many_async(jobs));
+}
+
+std::vector<CandidateList> SearchEngine::collect(const std::shared_ptr<Pending>& pd) {
+  Stopwatch w;
+  w.start();
+  std::unique_lock<std::mutex> lk(pd->mu);
+  pd->cv.wait(lk, [&] { return pd->remaining == 0; });
+  w.stop();
+  ctr_.tail_s += w.get_time();
+  if (pd->err) std::rethrow_exception(pd->err);
+  for (double t : pd->accd_t) ctr_.accd_s += t;
+  ctr_.accel_s += pd->accel_s + w.get_time();
+  return std::move(pd->out);
+}
+
+std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(const std::vector<Job>& jobs) {
   RoctxRange dm_range("DM-Loop");
   Stopwatch sw;
   sw.start();
   const int njobs = static_cast<int>(jobs.size());
-  std::vector<CandidateList> by_job(static_cast<size_t>(njobs));
-  if (njobs == 0) return by_job;
+  auto pd = std::make_shared<Pending>();
+  pd->out.resize(static_cast<size_t>(njobs));
+  pd->by_job.resize(static_cast<size_t>(njobs));
+  pd->accd_t.assign(static_cast<size_t>(njobs), 0.0);
+  std::vector<CandidateList>& by_job = pd->by_job;
+  if (njobs == 0) return pd;
   if (mode_ != 2 && njobs > 1) {
     // the rocFFT paths resample one series per batch: one job at a time
     for (int j = 0; j < njobs; ++j) {
       const Job& jb = jobs[static_cast<size_t>(j)];
-      by_job[static_cast<size_t>(j)] = search_prepared(jb.b, jb.dm, jb.dm_idx, jb.accs);
+      pd->out[static_cast<size_t>(j)] = search_prepared(jb.b, jb.dm, jb.dm_idx, jb.accs);
     }
-    return by_job;
+    return pd;
   }
   // flat trial list: job j's trials in order, jobs in order
   flat_job_.clear();
@@ -1234,7 +1255,7 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
   cur_pad_ = mode_ == 2 ? f4_in_.data() + static_cast<uint64_t>(j0.b) * f4_.insize : nullptr;
   cur_stats_ = wstats_.data() + 4 * static_cast<uint64_t>(j0.b);
   const int ntr = static_cast<int>(flat_acc_.size());
-  if (ntr == 0) return by_job;
+  if (ntr == 0) return pd;
   jobs_ = &jobs;
   // previous batches have all retired (their events were waited on), so the
   // device copies of the trial tables may be rewritten
@@ -1247,36 +1268,37 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
   RoctxRange acc_range("Acceleration-Loop");
   // Acceleration distillation (pipeline_multi.cu:243) of each DM as soon as
   // the batch holding its last trial has been processed, on accq_'s workers
-  // while the GPU runs the next batches: only the last DMs' distillation
-  // remains after the last batch retires.
-  std::vector<CandidateList> out(static_cast<size_t>(njobs));
+  // while the GPU runs the next batches; the tasks own their data through
+  // the Pending record, so the last DMs' distillation may outlive this call
+  // (collect() waits for it).
   std::vector<int> job_end(static_cast<size_t>(njobs));
   for (int j = 0, e = 0; j < njobs; ++j) job_end[static_cast<size_t>(j)] = e += static_cast<int>(jobs[static_cast<size_t>(j)].accs.size());
-  std::vector<double> accd_t(static_cast<size_t>(njobs), 0.0);
   int jobs_sent = 0;
-  struct Drain {  // tasks reference this frame: never leave it with one running
-    TaskQueue* q;
-    ~Drain() {
-      try {
-        q->wait();
-      } catch (...) {
-      }
-    }
-  } drain{accq_.get()};
   auto send_done = [&](int processed) {
     while (jobs_sent < njobs && job_end[static_cast<size_t>(jobs_sent)] <= processed) {
       const int j = jobs_sent++;
-      accq_->submit([this, j, &out, &by_job, &accd_t] {
+      {
+        std::lock_guard<std::mutex> lk(pd->mu);
+        pd->remaining++;
+      }
+      accq_->submit([this, j, pd] {
         Stopwatch w;
         w.start();
-        out[static_cast<size_t>(j)] = accd_.distill(std::move(by_job[static_cast<size_t>(j)]));
+        std::exception_ptr err;
+        try {
+          pd->out[static_cast<size_t>(j)] = accd_.distill(std::move(pd->by_job[static_cast<size_t>(j)]));
+        } catch (...) {
+          err = std::current_exception();
+        }
         w.stop();
-        accd_t[static_cast<size_t>(j)] = w.get_time();
+        std::lock_guard<std::mutex> lk(pd->mu);
+        pd->accd_t[static_cast<size_t>(j)] = w.get_time();
+        if (err && !pd->err) pd->err = err;
+        if (--pd->remaining == 0) pd->cv.notify_all();
       });
     }
   };
   send_done(0);
-  auto last_done = std::chrono::steady_clock::now();
   std::deque<int> inflight;  // slot indices
   int next = 0, slot = 0;
   // Short trial lists (one DM at 2^23: 685 trials) keep at least min_batches
@@ -1302,7 +1324,6 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
     const int sl = inflight.front();
     Slot& s = slots_[sl];
     s.done->sync();
-    last_done = std::chrono::steady_clock::now();
     uint32_t cnt = s.h_count[0];
     if (cnt > cap_) {
       // Peak buffer overflow: drain, grow, recompute every in-flight batch.
@@ -1372,13 +1393,10 @@ std::vector<CandidateList> SearchEngine::search_prepared_many(const std::vector<
   }
   ctr_.host_s += host.get_time();
   send_done(ntr);
-  accq_->wait();
-  for (double t : accd_t) ctr_.accd_s += t;
-  ctr_.tail_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - last_done).count();
   jobs_ = nullptr;
   sw.stop();
-  ctr_.accel_s += sw.get_time();
-  return out;
+  pd->accel_s = sw.get_time();
+  return pd;
 }
 
 // ---------------------------------------------------------------- folding ---

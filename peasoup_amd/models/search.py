@@ -296,11 +296,33 @@ class RankSearcher:
         cur = pull()  # the first block's dedispersion is issued before the search timer starts
         if t_s:
             t_s.start()
+        # A block's per-DM acceleration distillation may still be running on
+        # the engines' host workers when its batches have retired: it is
+        # collected after the next block's searches are issued, so that host
+        # tail overlaps GPU work (SearchEngine.search_prepared_many_async).
+        prev = None  # (ck, d0, d1, [(engine, jobs, handle)])
+
+        def finalize(blk):
+            ck_, b0, b1, pend = blk
+            per_dm: Dict[int, list] = {}
+            for e_, jobs_, h_ in pend:
+                for (b, dm, d, accs), c in zip(jobs_, e_.collect(h_)):
+                    per_dm[d] = c
+            chunk_cands: list = []
+            for d in range(b0, b1):
+                chunk_cands.extend(per_dm[d])
+            if ck_:
+                _C.save_spill(ck_, ckey, chunk_cands)  # atomic; raises on a failed write
+            cands.extend(chunk_cands)
+
         while cur is not None:
             j, ck, resumed, inflight = cur
             d0, d1 = blocks[j]
             self.blocks_done.append(j)
             if resumed is not None:
+                if prev is not None:  # keep the block order of the candidate list
+                    finalize(prev)
+                    prev = None
                 # resume: same spill format as the native pipeline (keyed CandidatePOD trees)
                 cands.extend(resumed)
                 ntrials += sum(len(self.accel_list(self.dm_list[d])) for d in range(d0, d1))
@@ -317,7 +339,7 @@ class RankSearcher:
             for e in self.engines:
                 ready.wait(e.stream)
             dd_events.append((start, ready))
-            per_dm: Dict[int, list] = {}
+            pend: list = []
             eng_t: Dict[int, list] = {}
 
             def run_dms(e, dms):
@@ -339,12 +361,12 @@ class RankSearcher:
                     te1 = time.perf_counter()
                     jobs = [(b, self.dm_list[d], d, self.accel_list(self.dm_list[d])) for b, d in enumerate(part)]
                     # one flat trial list over the part's DMs (batches span DM boundaries)
-                    got = e.search_prepared_many(jobs)
+                    h = e.search_prepared_many_async(jobs)
                     if _BLOCK_TRACE:
                         eng_t.setdefault(dms[0] - d0, []).append((te0 - tb1, te1 - te0, time.perf_counter() - te1))
-                    for (b, dm, d, accs), c in zip(jobs, got):
-                        per_dm[d] = c
-                        with lock:
+                    with lock:
+                        pend.append((e, jobs, h))
+                        for (b, dm, d, accs) in jobs:
                             ntrials += len(accs)
                             if progress is not None:
                                 progress(1)
@@ -362,23 +384,22 @@ class RankSearcher:
                 for f in futs:
                     f.result()
             tb2 = time.perf_counter()
-            chunk_cands: list = []
-            for d in range(d0, d1):
-                chunk_cands.extend(per_dm[d])
             evs = []
             for e in self.engines:
                 ev = _C.GpuEvent()
                 ev.record(e.stream)
                 evs.append(ev)
             freed[k] = evs  # the double buffer's slot k is free once these retire
-            if ck:
-                _C.save_spill(ck, ckey, chunk_cands)  # atomic; raises on a failed write
-            cands.extend(chunk_cands)
+            if prev is not None:
+                finalize(prev)
+            prev = (ck, d0, d1, pend)
             if _BLOCK_TRACE:
                 with open(_BLOCK_TRACE, "a") as f:
                     f.write(json.dumps({"block": j, "t0": tb0, "pull_s": tb1 - tb0, "search_s": tb2 - tb1,
                                         "engines": eng_t, "tail_s": time.perf_counter() - tb2}) + "\n")
             cur = nxt
+        if prev is not None:
+            finalize(prev)
         side.synchronize()
         for e in self.engines:
             _C.stream_synchronize(e.stream)
