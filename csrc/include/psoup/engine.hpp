@@ -168,8 +168,7 @@ struct SearchParams {
   // batches are cut into min_batches even batches (multiples of 8), but never
   // below the batch an eighth of the budget gives.
   int min_batches = 8;
-  // Compute streams the sub-batches of a batch rotate over (>= 2; env
-  // PSOUP_SUB_STREAMS overrides for A/B runs).
+  // Compute streams the sub-batches of a batch rotate over (>= 2).
   int sub_streams = 2;
   int min_gap = 30;
   // Acceleration-trial FFT path: 0 = rocFFT R2C of N points; 1 = rocFFT C2C
@@ -380,11 +379,6 @@ class SearchEngine {
   std::vector<std::unique_ptr<Stream>> aux_;  // further compute streams of the sub-batch pipeline
   std::vector<std::unique_ptr<Event>> joins_;
   Event fork_;
-  // PSOUP_SUB_PHASE (tuning): bit s serialises kernel stage s (0 pass A,
-  // 1 pass B, 2 r2c, 3 harmonic sum) across consecutive sub-batches, so the
-  // two streams run different stages side by side
-  int phase_ = 0;
-  Event phase_ev_[4];
   int sub_ = 0;                    // effective sub-batch size (0 = whole batch on stream_)
   uint64_t n_, nb_;
   float bin_width_, tobs_;
@@ -408,9 +402,6 @@ class SearchEngine {
   bool zap_ = false;
   int mode_ = 2;        // effective fft_mode
   kern::Fft4Geom f4_;
-  bool fused_ = false;   // fft_mode 2 with the fused pass B (blocked spectrum Pb_, layout pl_)
-  kern::PLayout pl_;
-  DeviceBuffer<float> Pb_;
   uint64_t pst_ = 1;     // floats per trial of P_
   DeviceBuffer<float2> f4_tab_;
   DeviceBuffer<float> f4_in_;  // padded whitened series read by the fused FFT [max_prep_][insize]

@@ -41,19 +41,6 @@ struct PeakRecord {
 };
 static_assert(sizeof(PeakRecord) == 12, "PeakRecord layout");
 
-// Layout of a normalised spectrum P (bins 0..M of an N = 2M point series).
-// blk = 0: natural order.  blk = 1: what the fused pass B
-// (fft4_rowpass_r2c) writes -- with n1 x n2 = M, bins 8J+1 .. 8J+8 are one
-// contiguous 32-byte piece, octet J = r * (n2/8) + g stored at
-// P[g * 8 n1 + r * 8] (each workgroup's output is one contiguous block per
-// octet column g), and bin 0 at P[M].  lg_n1 = log2 n1, lg_g = log2(n2/8).
-struct PLayout {
-  int blk = 0;
-  int lg_n1 = 0;
-  int lg_g = 0;
-  uint32_t M = 0;
-};
-
 constexpr int kMaxHarmLevels = 5;  // 2,4,8,16,32 harmonics (kernels.cu:42-96)
 
 // --------------------------------------------------------- unpack/dedisp ----
@@ -241,26 +228,6 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
 // search needs bins below max_freq only: ~14% of the spectrum at 2^23).
 void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, hipStream_t s,
                   uint64_t nbins_out = 0);
-// Pass B fused with the real-FFT post-processing, interbin and normalise
-// (kFft4FusedR2c): reads pass A's tiled Y and writes the normalised spectrum
-// P (bins 0..M) in the blocked layout fft4_p_layout(g), trial k at
-// P + k*pstride (pstride >= M + 1 and a multiple of 8 floats), normalised with
-// (stats + 4*tsrc[k])[0, 2] * nscale (tsrc optional).  32-byte pieces whose
-// bins all lie at or beyond nbins_out are not stored.  Needs n1 in
-// {512, 1024, 2048} and n2 >= 128 (fft4_fused_r2c_ok).
-bool fft4_fused_r2c_ok(const Fft4Geom& g);
-PLayout fft4_p_layout(const Fft4Geom& g);
-void fft4_rowpass_r2c(const float2* Y, float* P, uint64_t pstride, int K, const Fft4Geom& g, const float2* tables,
-                      const float* stats, float nscale, const uint32_t* tsrc, uint64_t nbins_out, hipStream_t s);
-// Blocked (fft4_rowpass_r2c) -> natural spectra for the harmonic sum: bin b
-// of trial k at out + k*stride + 3 + b (so the 32-byte pieces stay aligned;
-// pass out + 3 as the natural spectrum).  stride >= M + 4, multiple of 4;
-// bins >= nbins_out (0 = all) are not written.
-void p_unblock(const float* in, float* out, uint64_t stride, int K, const PLayout& L, uint64_t nbins_out,
-               hipStream_t s);
-// Copy of K spectra (M + 1 bins each, stride floats apart) between natural
-// order and layout L: dir 0 natural -> L, dir 1 L -> natural (tests, tools).
-void p_relayout(const float* in, float* out, uint64_t stride, int K, const PLayout& L, int dir, hipStream_t s);
 // Row-octet blocks (8 rows k1 each) r2c_interbin_normalise_tiled runs for
 // bins < nbins_out; it reads spectrum rows k1 <= 8*ny and k1 >= n1 - 8*ny.
 inline uint32_t r2c_tiled_row_blocks(uint64_t nbins_out, int n1, int n2) {
@@ -319,37 +286,21 @@ void mixed_gather(const float* src, uint64_t n, uint32_t m, uint64_t p, int mode
 // out = float Re X[0..n-1] (the unnormalised C2R when the gather was mode 1).
 void mixed_combine(const float2* Z, uint64_t zstride, const XLayoutArgs& L, uint64_t n, uint32_t m, uint64_t p,
                    int mode, void* out, hipStream_t s);
-// Tuning switches (process-wide, for measurement): kernel shape and store policy.
+// Kernel-shape switches (process-wide; the default is the fastest measured
+// set, every bit of it in use; tests/test_kernels_gpu.py runs each prefix of
+// the chain below).  Bit values are stable (flag sets are recorded in
+// profiles and the run identity).
 enum Fft4Flags : int {
-  kFft4Cpt8 = 1,         // 8 transforms per thread, one thread group (else 4 per thread, two groups)
-  kFft4NoRemap = 2,      // plain block order (no XCD-contiguous remap)
-  kFft4NtStores = 4,     // nontemporal stores
-  kFft4SkipCompute = 8,  // timing only: memory traffic without the FFT
-  kFft4TrialSlow = 32,   // block order: column/row block fastest, trial slowest (write locality)
-  kFft4SkipLoad = 64,    // timing only: synthetic inputs instead of global loads (blocked CPT-8 kernel)
-  kFft4SkipStore = 128,  // timing only: no global stores
-  kFft4Blocked = 256,    // blocked Y/X layouts: every lane stores its transforms' values contiguously
-  kFft4Ch4 = 16,         // with kFft4Blocked: pass B runs 4 transforms per workgroup (4 waves/SIMD)
-  kFft4TileY = 1024,     // with kFft4Blocked: 8x8-tiled Y between the passes (16-byte pass-B loads)
-  kFft4TileX = 2048,     // with kFft4TileY: 8x8-tiled spectrum X (coalesced pass-B stores; tiled r2c)
-  kFft4PairXcd = 4096,   // pass A: adjacent column blocks of a trial on one XCD (shared input lines)
-  kFft4GroupXcd = 8192,  // pass A: 8 trials x 2 adjacent column blocks per XCD group (needs K % 8 == 0)
-  kFft4Sub2 = 16384,     // tiled paths: two thread groups x 4 transforms per workgroup (fewer VGPRs, 4 waves/SIMD)
-  kFft4StagedStores = 32768,  // tiled paths: LDS-staged stores, 4 KiB contiguous per store instruction
-  kFft4UniformTw = 65536,     // pass A: four-step twiddles as per-thread x workgroup-uniform (SGPR) factors
-  kFft4OneX = 131072,         // pass A (tiled Y, column length 512..2048): 2 columns x L/G points per thread,
-                              // one LDS exchange, compile-time twiddles inside the two local DFTs
-  kFft4OneXWholeCu = 262144,  // with kFft4OneX at L = 2048: the exchange in one 128 KiB round (one workgroup per CU)
-  kFft4OneXSmall = 1048576,   // with kFft4OneX: also at column lengths 512 and 1024 (the Stockham pass A is
-                              // faster there: bench at 2^22 40.4k vs 37.3k, at 2^21 55.5k vs 53.4k trials/s)
-  kFft4OneXRow = 524288,      // pass B (tiled Y and X, row length 512..2048): the one-exchange structure
-  kFft4FusedR2c = 2097152,    // search batches: pass B + r2c + interbin + normalise in one kernel
-                              // (fft4_rowpass_r2c; blocked spectrum layout read by the harmonic sum)
-  kFft4WideProbe = 8388608,   // timing experiment (one-exchange pass A, with kFft4SkipCompute|kFft4SkipStore):
-                              // the same load bytes as 128-byte row pieces
-  kFft4Stagger = 4194304,     // experiment (one-exchange pass A): blocks 256..511 sleep ((flags >> 24) & 63)
-                              // x 8k cycles first, putting each CU's two workgroups out of phase
-  kFft4LoadPrio = 512,        // experiment (one-exchange pass A): s_setprio 3 while issuing the column loads
+  kFft4Cpt8 = 1,           // 8 transforms per thread, one thread group (else 4 per thread, two groups)
+  kFft4NoRemap = 2,        // plain block order (no XCD-contiguous remap)
+  kFft4Blocked = 256,      // blocked Y/X layouts: every lane stores its transforms' values contiguously
+  kFft4TileY = 1024,       // with kFft4Blocked: 8x8-tiled Y between the passes (16-byte pass-B loads)
+  kFft4TileX = 2048,       // with kFft4TileY: 8x8-tiled spectrum X (coalesced pass-B stores; tiled r2c)
+  kFft4PairXcd = 4096,     // pass A: adjacent column blocks of a trial on one XCD (shared input lines)
+  kFft4GroupXcd = 8192,    // pass A: 8 trials x 2 adjacent column blocks per XCD group (needs K % 8 == 0)
+  kFft4UniformTw = 65536,  // pass A: four-step twiddles as per-thread x workgroup-uniform (SGPR) factors
+  kFft4OneX = 131072,      // pass A (tiled Y, column length 2048): 2 columns x 32 points per thread,
+                           // one LDS exchange, compile-time twiddles inside the two local DFTs
   kFft4StripInput = 1073741824,  // one-exchange pass A: the padded input in column strips (16 + 4 floats of
                                  // every row per strip, strips row-contiguous), so a wave's 16 rows are
                                  // one ~1.3 KiB contiguous range instead of 16 pieces 16 KiB apart
@@ -370,9 +321,8 @@ struct HarmParams {
 // Fused incoherent harmonic sum + threshold + compaction: never writes the
 // summed spectra.  Records land unordered; count may exceed capacity (then
 // the caller re-runs with a bigger buffer).
-// P in layout L (natural by default; the fused pass B's blocked layout).
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
-                          PeakRecord* out, uint32_t* count, hipStream_t s, const PLayout& L = PLayout{});
+                          PeakRecord* out, uint32_t* count, hipStream_t s);
 // Peak clustering on the device (peakcluster.hip; peakfinder.hpp:24-55):
 // the records of harmonic_peaks_batch (first min(*d_count, cap)) -- chunks
 // of idx-ascending crossings, each behind its descriptor record (seg field

@@ -873,37 +873,24 @@ void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_
   PSOUP_CHECK((chan_stride & 15) == 0 && (out_stride & 15) == 0, "dedisperse_lds: stride alignment");
   const uint64_t ty = (out_nsamps + 1023) / 1024;
   PSOUP_CHECK(ty <= 65535, "dedisperse_lds: series too long for the grid");
-  static const int dpt_env = [] {
-    const char* e = std::getenv("PSOUP_DEDISP_LDS_DPT");  // A/B knob: DMs per wave, 8, 4 or 2
-    const int v = e ? std::atoi(e) : 0;  // default 4: 141 ms vs 173 ms (8) for the config-4 DM list
-    return v == 8 || v == 4 || v == 2 ? v : 0;
-  }();
-  // a launch of <= 8 DMs (the headline bench's per-rank chunk) fills 8-DM
-  // workgroups instead of half-empty 16-DM ones
-  const int dpt = dpt_env ? dpt_env : (ndm <= 8 ? 2 : 4);
+  // DMs per wave: a launch of <= 8 DMs (the headline bench's per-rank chunk)
+  // fills 8-DM workgroups instead of half-empty 16-DM ones; otherwise 4
+  // (config-4 DM list: 141 ms vs 173 ms at 8).  Two-pass windows (> 4096
+  // samples) are built for 4 only.
+  const bool two = max_window > 4096;
+  const int dpt = ndm <= 8 && !two ? 2 : 4;
   // workgroups start on multiples of their 4*dpt DMs (one absolute tile's
   // window each): a range from any DM starts at the workgroup boundary below
   // it and skips the DMs before d0
   const int d_base = d0 / (4 * dpt) * (4 * dpt), d_skip = d0 - d_base;
   dim3 grid(static_cast<unsigned>((ndm + d_skip + 4 * dpt - 1) / (4 * dpt)), static_cast<unsigned>(ty));
   PSOUP_CHECK(d_base + static_cast<int>(grid.x) * 4 * dpt <= ldo, "dedisperse_lds: offset table too narrow");
-  const bool two = max_window > 4096;
   const bool xr = bias == 128;
-  // channels per barrier (A/B knob PSOUP_DEDISP_LDS_CPB = 1, 2 or 4; one-pass windows only)
-  static const int cpb = [] {
-    const char* e = std::getenv("PSOUP_DEDISP_LDS_CPB");
-    const int v = e ? std::atoi(e) : 1;  // 1: 140 ms, 2: 153 ms, 4: 185 ms (fewer workgroups per CU)
-    return v == 2 || v == 4 ? v : 1;
-  }();
-  // byte-lane sums (narrow unsigned samples: flush * max raw value <= 255);
-  // A/B knob PSOUP_DEDISP_LDS_BYTES=0 keeps the 16-bit perm form
-  static const bool bytes_ok = [] {
-    const char* e = std::getenv("PSOUP_DEDISP_LDS_BYTES");
-    return !e || std::atoi(e) != 0;
-  }();
+  // byte-lane sums (narrow unsigned samples: flush * max raw value <= 255;
+  // one channel per barrier: 140 ms vs 153 / 185 ms at 2 / 4)
   const int max_raw = (1 << std::min(nbits, 8)) - 1;
   const int flush = max_raw > 0 ? 255 / max_raw : 255;
-  const bool bytes = bytes_ok && !xr && nbits <= 4 && flush >= 1 && cpb == 1 && !two && (dpt == 4 || dpt == 2);
+  const bool bytes = !xr && nbits <= 4 && flush >= 1 && !two;
   if (bytes) {
     if (dpt == 4)
       dedisperse_lds_kernel<false, 1, 4, 1, true><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive,
@@ -922,21 +909,13 @@ void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_
   dedisperse_lds_kernel<X, P, D, C><<<grid, 256, 0, s>>>(chan_major, chan_stride, d_active, nactive, d_offT, ldo, \
                                                          d_base, d_skip, ndm + d_skip, d_wmin, out_nsamps, out,      \
                                                          out_stride, scale, 255)
-#define PSOUP_LDS_ONE(X)                                      \
-  if (two) {                                                  \
-    if (dpt == 8) PSOUP_LDS_LAUNCH(X, 2, 8, 1);               \
-    else PSOUP_LDS_LAUNCH(X, 2, 4, 1);                        \
-  } else if (dpt == 8) {                                      \
-    PSOUP_LDS_LAUNCH(X, 1, 8, 1);                             \
-  } else if (dpt == 2) {                                      \
-    PSOUP_LDS_LAUNCH(X, 1, 2, 1);                             \
-  } else if (cpb == 1) {                                      \
-    PSOUP_LDS_LAUNCH(X, 1, 4, 1);                             \
-  } else if (cpb == 2) {                                      \
-    PSOUP_LDS_LAUNCH(X, 1, 4, 2);                             \
-  } else {                                                    \
-    PSOUP_LDS_LAUNCH(X, 1, 4, 4);                             \
-  }
+#define PSOUP_LDS_ONE(X)          \
+  if (two)                         \
+    PSOUP_LDS_LAUNCH(X, 2, 4, 1);  \
+  else if (dpt == 2)               \
+    PSOUP_LDS_LAUNCH(X, 1, 2, 1);  \
+  else                             \
+    PSOUP_LDS_LAUNCH(X, 1, 4, 1);
   if (xr) {
     PSOUP_LDS_ONE(true)
   } else {

@@ -165,16 +165,6 @@ __device__ __forceinline__ float2 r2c_combine(float2 za, float2 zb, float c, flo
   return make_float2(__builtin_fmaf(-s, oy, __builtin_fmaf(c, ox, ex)), __builtin_fmaf(s, ox, __builtin_fmaf(c, oy, ey)));
 }
 
-// Index of spectrum bin i in a PLayout (kernels.hpp): natural, or the octet
-// blocks the fused pass B writes (bins 8J+1..8J+8 contiguous, octet
-// J = r n2/8 + g at P[g][r][.], bin 0 after the last block).
-__device__ __forceinline__ uint32_t paddr(uint32_t i, const PLayout& L) {
-  if (!L.blk) return i;
-  if (i == 0) return L.M;
-  const uint32_t s = i - 1, J = s >> 3;
-  return ((J & ((1u << L.lg_g) - 1u)) << (L.lg_n1 + 3)) + ((J >> L.lg_g) << 3) + (s & 7u);
-}
-
 }  // namespace dev
 }  // namespace kern
 }  // namespace psoup

@@ -1,17 +1,12 @@
 // In-register complex DFT building blocks shared by the four-step FFT passes
 // (fft4step.hip) and the fold optimiser (fold.hip): complex arithmetic on
-// the packed-f32 VALU (cplx_pk.hpp; PSOUP_FFT_SCALAR=1 restores the scalar
-// forms for A/B builds), 2/4/8-point butterflies and dft<N>, a compile-time
+// the packed-f32 VALU (cplx_pk.hpp), 2/4/8-point butterflies and dft<N>, a compile-time
 // unrolled radix-8 DFT of up to 64 points whose twiddles are literals.
 #pragma once
 
 #include <hip/hip_runtime.h>
 
 #include "cplx_pk.hpp"
-
-#ifndef PSOUP_FFT_SCALAR
-#define PSOUP_FFT_SCALAR 0
-#endif
 
 namespace psoup {
 namespace kern {
@@ -20,25 +15,7 @@ namespace dreg {
 __device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }  // * -i
 
 // The butterflies and twiddle products run on the packed-f32 VALU
-// (cplx_pk.hpp: half the VALU issue slots of the scalar forms, which
-// PSOUP_FFT_SCALAR=1 at compile time restores for A/B runs).
-#if PSOUP_FFT_SCALAR
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ float2 cadd_mi(float2 a, float2 b) { return cadd(a, mul_mi(b)); }
-__device__ __forceinline__ float2 csub_mi(float2 a, float2 b) { return csub(a, mul_mi(b)); }
-__device__ __forceinline__ float2 mul_w8(float2 c) {
-  constexpr float r2 = 0.70710678118654752440f;
-  return make_float2(r2 * (c.x + c.y), r2 * (c.y - c.x));
-}
-__device__ __forceinline__ float2 mul_w83(float2 c) {
-  constexpr float r2 = 0.70710678118654752440f;
-  return make_float2(r2 * (c.y - c.x), -r2 * (c.x + c.y));
-}
-#else
+// (cplx_pk.hpp: half the VALU issue slots of the scalar forms).
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return pk::add(a, b); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return pk::sub(a, b); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) { return pk::mul(a, b); }
@@ -46,7 +23,6 @@ __device__ __forceinline__ float2 cadd_mi(float2 a, float2 b) { return pk::add_m
 __device__ __forceinline__ float2 csub_mi(float2 a, float2 b) { return pk::sub_mi(a, b); }
 __device__ __forceinline__ float2 mul_w8(float2 c) { return pk::mul_w8(c); }
 __device__ __forceinline__ float2 mul_w83(float2 c) { return pk::mul_w83(c); }
-#endif
 
 __device__ __forceinline__ void fft2(float2& a, float2& b) {
   const float2 t = a;

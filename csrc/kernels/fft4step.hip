@@ -52,16 +52,14 @@ constexpr int kChanPad = 8;
 template <int L, int CPT, int SUB>
 struct Cfg {
   static constexpr int CH = CPT * SUB;  // transforms per workgroup (blocked layout width when SUB == 1)
-  static_assert(CH == 8 || (CH == 4 && SUB == 1), "workgroups cover 8 (or, blocked, 4) transforms");
+  static_assert(CH == 8, "workgroups cover 8 transforms");
   static constexpr int T = L / kPts;                     // threads per group
   static constexpr int THREADS = T * SUB;
   static constexpr int PAD = L + L / 8 + kChanPad;       // complex elements per channel plane
-  // CH 4: four workgroups per CU.  Workgroups of fewer than 256 threads
-  // (L < 2048) get a proportional share: at L = 1024 the full 73 KiB let
-  // the 128-thread workgroup exchange all 8 channels in one round but held
-  // the CU to 2 workgroups (1 wave per SIMD)
-  static constexpr int BUDGET0 = CH == 4 ? kLdsBudget / 2 : kLdsBudget;
-  static constexpr int BUDGET = THREADS >= 256 ? BUDGET0 : BUDGET0 / 256 * THREADS;
+  // Workgroups of fewer than 256 threads (L < 2048) get a proportional
+  // share: at L = 1024 the full 73 KiB let the 128-thread workgroup exchange
+  // all 8 channels in one round but held the CU to 2 workgroups (1 wave per SIMD)
+  static constexpr int BUDGET = THREADS >= 256 ? kLdsBudget : kLdsBudget / 256 * THREADS;
   static constexpr int CG0 = BUDGET / (SUB * 2 * PAD * 4);
   static constexpr int CG = CG0 >= CPT ? CPT : (CG0 >= 4 ? 4 : (CG0 >= 2 ? 2 : 1));  // channels per exchange round
   static constexpr int GROUP_FLOATS = 2 * CG * PAD;
@@ -248,11 +246,9 @@ __device__ __forceinline__ void load_resampled(const float* __restrict__ in, con
 
 // Table layout (float2): [tw_N2 (N2)] [tw_N1 (N1)] [lo (2^kSplit)] [hi (M >> kSplit)]
 // [ox (N1 x GX)]: ox[col * GX + k2] = W_M^{col P k2}, the k2 part of the
-// one-exchange pass A's four-step twiddles (GX = onex_g(N2), P = N2 / GX);
-// [rk (N1)]: e^{-i pi m / N1} and [rc (N2/2 + 16)]: e^{-i pi c / M}, the
-// real-FFT twiddle e^{-i pi (c + N2 k1) / M} = rc[c] rk[k1] of the fused pass B.
+// one-exchange pass A's four-step twiddles (GX = onex_g(N2), P = N2 / GX).
 struct TableOffsets {
-  uint64_t n2, n1, lo, hi, ox, rk, rc, total;
+  uint64_t n2, n1, lo, hi, ox, total;
 };
 __host__ __device__ constexpr int onex_g(int N2) { return N2 >= 2048 ? 64 : 32; }
 __host__ __device__ inline TableOffsets table_offsets(int N1, int N2) {
@@ -263,9 +259,7 @@ __host__ __device__ inline TableOffsets table_offsets(int N1, int N2) {
   o.lo = o.n1 + N1;
   o.hi = o.lo + (1u << kSplit);
   o.ox = o.hi + (M >> kSplit);
-  o.rk = o.ox + static_cast<uint64_t>(N1) * onex_g(N2);
-  o.rc = o.rk + N1;
-  o.total = o.rc + N2 / 2 + 16;
+  o.total = o.ox + static_cast<uint64_t>(N1) * onex_g(N2);
   return o;
 }
 
@@ -274,74 +268,10 @@ __device__ __forceinline__ float2 twiddle_M(uint32_t a, const float2* __restrict
 }
 
 template <int CPT>
-__device__ __forceinline__ void store_row(float2* __restrict__ dst, const Vec<CPT>& v, int q, bool nt) {
+__device__ __forceinline__ void store_row(float2* __restrict__ dst, const Vec<CPT>& v, int q) {
   f4v* d = reinterpret_cast<f4v*>(dst);
 #pragma unroll
-  for (int c = 0; c < CPT; c += 2) {
-    const f4v val = {v[c][q].x, v[c][q].y, v[c + 1][q].x, v[c + 1][q].y};
-    if (nt)
-      __builtin_nontemporal_store(val, d + c / 2);
-    else
-      d[c / 2] = val;
-  }
-}
-
-// Tiled-layout store of a workgroup's 8 transforms x L points, staged
-// through LDS so that every global store instruction writes 4 KiB of
-// contiguous memory (the workgroup's output is one contiguous 8 L complex
-// region: [L/8][8 transforms][8]).  Direct per-lane stores of that layout
-// write 64-byte pieces 512 bytes apart and run at ~60% of the contiguous
-// write bandwidth.  Two halves of 4 L complex (64 KiB at L = 2048) fit the
-// 72 KiB LDS budget; one complex of padding per 64 spreads the 8-byte LDS
-// writes over the banks.  keep_oct > 0 skips the octets outside
-// [0, keep_oct) u [L/8 - keep_oct, L/8) (see the pruned pass-B stores).
-// floats of LDS the staged store of one 8 x L block needs
-template <int L>
-constexpr int staged_lds_floats() {
-  constexpr int PARTS = L > 1024 ? L / 1024 : 1;
-  constexpr int PART = 8 * L / PARTS;
-  return (PART + PART / 64) * 2;
-}
-
-template <int L>
-__device__ __forceinline__ void store_tiled_staged(const Vec<8>& v, float* __restrict__ lds, int t,
-                                                   float2* __restrict__ region, uint32_t keep_oct, bool nt) {
-  constexpr int T = L / kPts;
-  constexpr int PARTS = L > 1024 ? L / 1024 : 1;  // 64 KiB (8192 complex) per part
-  constexpr int QP = kPts / PARTS;                 // q values per part
-  constexpr int PART = 8 * L / PARTS;              // complex per part
-  static_assert((PART + PART / 64) * 2 <= kLdsBudget / 4, "staging does not fit the LDS budget");
-  float2* buf = reinterpret_cast<float2*>(lds);
-  auto pad = [](int x) { return x + (x >> 6); };
-  const uint32_t hi_oct = L / 8 - keep_oct;
-#pragma unroll
-  for (int h = 0; h < PARTS; ++h) {
-    __syncthreads();  // LDS is free (FFT exchanges / previous part done)
-#pragma unroll
-    for (int qq = 0; qq < QP; ++qq) {
-      const int k = t + (QP * h + qq) * T;  // point index of this thread's values
-      const int pos = (k >> 3) * 64 + (k & 7) - h * PART;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) buf[pad(pos + c * 8)] = v[c][QP * h + qq];
-    }
-    __syncthreads();
-    float2* out = region + static_cast<uint64_t>(h) * PART;
-#pragma unroll
-    for (int j = 0; j < PART / (2 * T); ++j) {
-      const int idx = 2 * (j * T + t);  // two complex per lane (16 bytes)
-      if (keep_oct != 0) {
-        const uint32_t oct = static_cast<uint32_t>((h * PART + idx) >> 6);
-        if (oct >= keep_oct && oct < hi_oct) continue;
-      }
-      const float2 a = buf[pad(idx)], b = buf[pad(idx + 1)];
-      const f4v val = {a.x, a.y, b.x, b.y};
-      f4v* d = reinterpret_cast<f4v*>(out + idx);
-      if (nt)
-        __builtin_nontemporal_store(val, d);
-      else
-        *d = val;
-    }
-  }
+  for (int c = 0; c < CPT; c += 2) d[c / 2] = f4v{v[c][q].x, v[c][q].y, v[c + 1][q].x, v[c + 1][q].y};
 }
 
 // XCD-aware block order (remap = true): logical block
@@ -399,9 +329,10 @@ constexpr int kStripW = 20;
 __host__ __device__ constexpr uint64_t strip_floats(int n1, int n2) {
   return static_cast<uint64_t>(n1 / 8) * static_cast<uint64_t>(n2) * kStripW;
 }
+// (at column lengths 512 and 1024 the Stockham pass A measured faster: bench
+// at 2^22 40.4k vs 37.3k trials/s, at 2^21 55.5k vs 53.4k)
 __host__ __device__ inline bool onex_colpass(int n2, int f) {
-  return (f & kFft4OneX) && (f & kFft4Blocked) && (f & kFft4TileY) && !(f & kFft4Sub2) &&
-         (n2 == 2048 || ((f & kFft4OneXSmall) && (n2 == 512 || n2 == 1024)));
+  return (f & kFft4OneX) && (f & kFft4Blocked) && (f & kFft4TileY) && n2 == 2048;
 }
 __host__ __device__ inline bool strip_input(int n2, int f) { return (f & kFft4StripInput) && onex_colpass(n2, f); }
 
@@ -420,37 +351,30 @@ __global__ void __launch_bounds__(256) fft4_pad_strips_kernel(const float* __res
   }
 }
 
-// Kernel variants: MODE bit 0 = blocked Y/X layouts (CPT 8), bit 1 = timing
-// build honouring the kFft4Skip* flags (tools/kbench.py only).
+// Kernel variants: MODE bit 0 = blocked Y/X layouts (CPT 8);
 // bit 2 = tiled Y (pass A -> pass B): Y_t[i/8][k2/8][i%8][k2%8], so a pass-B
 // lane reads its rows' values as contiguous 16-byte vectors and eight lanes
 // cover 512 contiguous bytes.
 // bit 3 = tiled X: X_t[k2/8][k1/8][k2%8][k1%8] (read by r2c_interbin_normalise_tiled).
-constexpr int kModeBlocked = 1, kModeTiming = 2, kModeTileY = 4, kModeTileX = 8;
-constexpr int kModeStaged = 16;  // LDS-staged contiguous stores of the tiled layouts
+constexpr int kModeBlocked = 1, kModeTileY = 4, kModeTileX = 8;
 
 // Pass A.  Logical block = column block * K + trial (trial fastest).
 template <int L, int CPT, int SUB, int MODE>
-__global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::THREADS), amdgpu_waves_per_eu((CPT == 4 ? 4 : 2)))) fft4_colpass_kernel(
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::THREADS), amdgpu_waves_per_eu(2))) fft4_colpass_kernel(
     const float* __restrict__ in, const float* __restrict__ in_pad, uint64_t n, const double* __restrict__ afs, int K,
     float2* __restrict__ Y, Fft4Geom g, const float2* __restrict__ tab, int flags) {
   using C = Cfg<L, CPT, SUB>;
-  constexpr bool kBlocked = MODE & kModeBlocked, kTiming = MODE & kModeTiming, kTileY = MODE & kModeTileY;
-  static_assert(!kTileY || C::CH == 8, "tiled Y needs 8 transforms per workgroup");
-  // the opt-in staged stores reuse the exchange buffer: size it for both
-  constexpr int kLdsN = (MODE & kModeStaged) && staged_lds_floats<L>() > C::LDS_FLOATS ? staged_lds_floats<L>()
-                                                                                      : C::LDS_FLOATS;
-  __shared__ __attribute__((aligned(16))) float lds[kLdsN];
+  constexpr bool kBlocked = MODE & kModeBlocked, kTileY = MODE & kModeTileY;
+  static_assert(!kTileY || (CPT == 8 && SUB == 1), "tiled Y: 8 transforms per thread");
+  __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   constexpr int T = C::T;
   const int grp = threadIdx.x / T;
   const int t = threadIdx.x - grp * T;
   const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
   trace_event(0);
   const int N1 = g.n1;
-  const uint32_t nbt = static_cast<uint32_t>(N1 / C::CH);  // blocks per trial
-  const bool tslow = flags & kFft4TrialSlow;
-  int k = static_cast<int>(tslow ? lb / nbt : lb % static_cast<uint32_t>(K));
-  int c0 = static_cast<int>(tslow ? lb % nbt : lb / static_cast<uint32_t>(K)) * C::CH + grp * CPT;
+  int k = static_cast<int>(lb % static_cast<uint32_t>(K));
+  int c0 = static_cast<int>(lb / static_cast<uint32_t>(K)) * C::CH + grp * CPT;
   if ((flags & kFft4GroupXcd) && (K & 7) == 0) {
     // 8 consecutive trials x column blocks 2p, 2p+1 (16 workgroups reading
     // nearly the same input lines) share one XCD, in consecutive slots
@@ -478,41 +402,16 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
   for (int q = 0; q < kPts; ++q) {
     const uint64_t j = t + q * T;
     float x[2 * CPT];
-    if (kTiming && (flags & kFft4SkipLoad)) {
-#pragma unroll
-      for (int e = 0; e < 2 * CPT; ++e) x[e] = static_cast<float>(j + e);
-    } else {
-      load_resampled<2 * CPT>(in + src * g.in_tstride, in_pad + src * g.pad_tstride, static_cast<uint32_t>(n),
-                              log2row, static_cast<uint32_t>(g.inpitch), af, size,
-                              2u * (static_cast<uint32_t>(N1) * static_cast<uint32_t>(j) + static_cast<uint32_t>(c0)),
-                              x);
-    }
+    load_resampled<2 * CPT>(in + src * g.in_tstride, in_pad + src * g.pad_tstride, static_cast<uint32_t>(n), log2row,
+                            static_cast<uint32_t>(g.inpitch), af, size,
+                            2u * (static_cast<uint32_t>(N1) * static_cast<uint32_t>(j) + static_cast<uint32_t>(c0)), x);
 #pragma unroll
     for (int c = 0; c < CPT; ++c) v[c][q] = make_float2(x[2 * c], x[2 * c + 1]);
   }
   trace_event(1);
-  if (!kTiming || !(flags & kFft4SkipCompute))
-    fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n2);
+  fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n2);
   const uint32_t mask = static_cast<uint32_t>(N1) * L - 1;
   float2* yk = Y + static_cast<uint64_t>(k) * g.ystride;
-  const bool nt = flags & kFft4NtStores;
-  if constexpr (kTileY && CPT == 8 && SUB == 1 && (MODE & kModeStaged) != 0) {
-    {
-#pragma unroll
-      for (int q = 0; q < kPts; ++q) {
-        const uint32_t k2 = t + q * T;
-        float2 w = twiddle_M((static_cast<uint32_t>(c0) * k2) & mask, tab + to.lo, tab + to.hi);
-        const float2 step = twiddle_M(k2, tab + to.lo, tab + to.hi);
-#pragma unroll
-        for (int c = 0; c < CPT; ++c) {
-          v[c][q] = cmul(v[c][q], w);
-          w = cmul(w, step);
-        }
-      }
-      store_tiled_staged<L>(v, lds, t, yk + static_cast<uint64_t>(c0) * g.n2, 0, nt);
-      return;
-    }
-  }
   // Four-step twiddles W^{(c0+c) k2}, k2 = t + qT: w0 = W^{c0 k2}, step =
   // W^{k2}.  kFft4UniformTw: both split into a per-thread factor (W^{c0 t},
   // W^t: one pair of table lookups) times a workgroup-uniform factor
@@ -549,15 +448,14 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
       w = cmul(w, step);
     }
     if constexpr (kTileY) {
-      // c0 & 7 != 0 when two thread groups share one 8-column tile (SUB 2)
-      float2* dst = yk + static_cast<uint64_t>(c0 & ~7) * g.n2 + (k2 >> 3) * 64 + (c0 & 7) * 8 + (k2 & 7);
+      float2* dst = yk + static_cast<uint64_t>(c0) * g.n2 + (k2 >> 3) * 64 + (k2 & 7);
 #pragma unroll
       for (int c = 0; c < CPT; ++c) dst[c * 8] = v[c][q];
     } else {
       // blocked: Y_b[c0/8][k2][c] (each lane 64 contiguous bytes); else Y[k2][i] at pitch ypitch
       float2* dst = kBlocked ? yk + static_cast<uint64_t>(c0) * g.n2 + k2 * CPT
                              : yk + static_cast<uint64_t>(k2) * g.ypitch + c0;
-      if (!kTiming || !(flags & kFft4SkipStore) || v[0][q].x == 1234.5f) store_row<CPT>(dst, v, q, nt);
+      store_row<CPT>(dst, v, q);
     }
   }
   trace_event(11);
@@ -599,9 +497,9 @@ struct OneX {
                                                        // columns read by a 32-lane group on distinct banks)
   static_assert(P % 8 == 0 && G % 16 == 0 && NPAIR >= 1 && NPAIR * G == 2 * P, "one-exchange shape");
   static_assert(GS * ROUNDS == G && GS % 16 == 0 && 8 + SG * (GS - 1) <= SK, "one-exchange LDS layout");
-  // R = 1 at L = 2048: the whole 128 KiB exchange in one round, one workgroup per CU
-  static constexpr bool kWholeCu = (NBUF * BUF + 8 * (G + 1)) * 8 > kLdsBudget;
-  static_assert((NBUF * BUF + TWS) * 8 <= (kWholeCu ? 160 * 1024 : kLdsBudget), "one-exchange LDS budget");
+  // two workgroups per CU (the whole 128 KiB exchange in one round, one
+  // workgroup per CU, measured slower)
+  static_assert((NBUF * BUF + TWS) * 8 <= kLdsBudget, "one-exchange LDS budget");
 };
 
 // The part both one-exchange passes share: P-point DFTs of the thread's two
@@ -663,11 +561,8 @@ __device__ __forceinline__ void onex_core(float2 (&va)[L / G], float2 (&vb)[L / 
   trace_event(4);
 }
 
-constexpr bool kWideProbe = true;  // compile the kFft4WideProbe addressing (timing experiment)
-
 template <int L, int G, int R>
-__global__ void __attribute__((amdgpu_flat_work_group_size(1, OneX<L, G, R>::THREADS),
-                               amdgpu_waves_per_eu(OneX<L, G, R>::kWholeCu ? 1 : 2)))
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, OneX<L, G, R>::THREADS), amdgpu_waves_per_eu(2)))
 fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__ in_pad, uint64_t n,
                          const double* __restrict__ afs, int K, float2* __restrict__ Y, Fft4Geom g,
                          const float2* __restrict__ tab, int flags) {
@@ -677,19 +572,11 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int cp = t & 3, gg = t >> 2;
   const int N1 = g.n1;
-  if ((flags & kFft4Stagger) && blockIdx.x >= 256 && blockIdx.x < 512) {
-    // experiment: start the second workgroup of each CU late, so the two
-    // workgroups' load / compute / store phases are out of step
-    const int reps = (flags >> 24) & 63;
-    for (int i = 0; i < reps; ++i) __builtin_amdgcn_s_sleep(127);
-  }
   trace_event(0);
   // block -> (trial k, first column c0): the Stockham kernel's order and XCD grouping
   const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
-  const uint32_t nbt = static_cast<uint32_t>(N1 / 8);
-  const bool tslow = flags & kFft4TrialSlow;
-  int k = static_cast<int>(tslow ? lb / nbt : lb % static_cast<uint32_t>(K));
-  int c0 = static_cast<int>(tslow ? lb % nbt : lb / static_cast<uint32_t>(K)) * 8;
+  int k = static_cast<int>(lb % static_cast<uint32_t>(K));
+  int c0 = static_cast<int>(lb / static_cast<uint32_t>(K)) * 8;
   if ((flags & kFft4GroupXcd) && (K & 7) == 0) {
     const uint32_t b = blockIdx.x;
     const uint32_t Gp = ((b >> 7) << 3) | (b & 7u), wq = (b >> 3) & 15u;
@@ -738,8 +625,6 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
     const bool strips = flags & kFft4StripInput;  // (the host pads in strips exactly when this kernel runs)
     const uint32_t nrows = static_cast<uint32_t>(L);
     uint32_t bad = 0;
-    const bool prio = flags & kFft4LoadPrio;
-    if (prio) __builtin_amdgcn_s_setprio(3);  // experiment: issue this workgroup's loads ahead of the other's math
     // Rows are loaded in the order dft<P> consumes them: its first radix-8
     // pass takes rows b, b + P/8, ..., b + 7 P/8 for b = 0, 1, ..., so the
     // compiler's vmcnt waits let the first groups' butterflies run while the
@@ -747,12 +632,8 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
 #pragma unroll
     for (int ii = 0; ii < P; ++ii) {
       const int m = P >= 16 ? (P / 8) * (ii % 8) + ii / 8 : ii;
-      // (kFft4WideProbe, timing only: the same bytes as 128-byte row pieces --
-      // 16 columns x half the rows per workgroup, 8 lanes per row)
-      const bool wide = kWideProbe && (flags & kFft4WideProbe);
-      const uint32_t j = wide ? static_cast<uint32_t>((t >> 3) + 32 * m + ((c0 & 8) ? L / 2 : 0))
-                              : static_cast<uint32_t>(gg + G * m);
-      const uint32_t col = wide ? static_cast<uint32_t>((c0 & ~15) + 2 * (t & 7)) : static_cast<uint32_t>(c0 + 2 * cp);
+      const uint32_t j = static_cast<uint32_t>(gg + G * m);
+      const uint32_t col = static_cast<uint32_t>(c0 + 2 * cp);
       const uint32_t p0 = 2u * (static_cast<uint32_t>(N1) * j + col);
       const float pa = static_cast<float>(p0), pb = pa + 3.0f;
       const float fa = afl * pa * (pa - sizef), fb = afl * pb * (pb - sizef);
@@ -761,19 +642,13 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
       const bool ok = sa == sb && fabsf(fa - sa) < 0.5f - band && fabsf(fb - sb) < 0.5f - band && first >= 0 &&
                       first + 3 < static_cast<int64_t>(nn);
       const uint32_t i = ok ? static_cast<uint32_t>(first) : p0;
-      f4v v;
-      if (flags & kFft4SkipLoad) {  // timing only: no global loads
-        v = f4v{pa, fa, sa, sb};
-      } else {
-        const uint32_t row = i >> log2row, col = i & rowmask;
-        const uint32_t off = strips ? ((col >> 4) * nrows + row) * kStripW + (col & 15u) : row * pitch + col;
-        v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, off * 4u, 0, 0));
-        bad |= ok ? 0u : (1u << m);
-      }
+      const uint32_t row = i >> log2row, ic = i & rowmask;
+      const uint32_t off = strips ? ((ic >> 4) * nrows + row) * kStripW + (ic & 15u) : row * pitch + ic;
+      const f4v v = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, off * 4u, 0, 0));
+      bad |= ok ? 0u : (1u << m);
       va[m] = make_float2(v.x, v.y);
       vb[m] = make_float2(v.z, v.w);
     }
-    if (prio) __builtin_amdgcn_s_setprio(0);
     trace_event(1);
     if (bad != 0) {
       const double size = static_cast<double>(n);
@@ -793,15 +668,7 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
   }
   const int rc = (lane >> 3) & 7;
   float2 u[C::NPAIR][G];
-  if (flags & kFft4SkipCompute) {  // timing only: the loaded values go straight to the stores
-#pragma unroll
-    for (int p = 0; p < C::NPAIR; ++p)
-#pragma unroll
-      for (int q = 0; q < G; ++q) u[p][q] = (q & 1) ? vb[(p * G + q) % P] : va[(p * G + q) % P];
-  } else {
-    onex_core<L, G, R>(va, vb, u, lds, tab + to.n2, t);
-  }
-  const bool skip_store = flags & kFft4SkipStore;
+  onex_core<L, G, R>(va, vb, u, lds, tab + to.n2, t);
 
   // four-step twiddle W_M^{col k}, k = k1 + P k2: W_M^{col k1} (table pair)
   // times W_M^{col P k2} (the staged ox rows); tiled store
@@ -818,66 +685,7 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
     for (int k2 = 0; k2 < G; ++k2) {
       const float2 wv = k2 == 0 ? om : cmul(om, twr[k2]);
       const uint32_t kk = k1 + static_cast<uint32_t>(P * k2);
-      const float2 yv = cmul(u[p][k2], wv);
-      if (!skip_store || yv.x == 1234.5f) yk[(kk >> 3) * 64 + static_cast<uint32_t>(rc) * 8 + (kk & 7)] = yv;
-    }
-  }
-  trace_event(11);
-}
-
-// One-exchange pass B (kFft4OneX with tiled Y and X): rows r0 .. r0 + 7 of
-// Y_t, thread (cp, g) loads rows r0 + 2cp, r0 + 2cp + 1 at points i = g + G m
-// (16 bytes per lane; a wave reads two contiguous 512-byte blocks), the same
-// core as pass A, and stores X_t[r0 / 8][k1 / 8][r % 8][k1 % 8] one 512-byte
-// block per wave instruction.  Pruned spectra (keep_oct > 0) take the
-// Stockham kernel: the skip branches cost this one 20-30 spilled VGPRs.
-template <int L, int G, int R>
-__global__ void __attribute__((amdgpu_flat_work_group_size(1, OneX<L, G, R>::THREADS),
-                               amdgpu_waves_per_eu(OneX<L, G, R>::kWholeCu ? 1 : 2)))
-fft4_rowpass_onex_kernel(const float2* __restrict__ Y, float2* __restrict__ X, int K, Fft4Geom g,
-                         const float2* __restrict__ tab, int flags) {
-  using C = OneX<L, G, R>;
-  constexpr int P = C::P;
-  __shared__ __attribute__((aligned(16))) float2 lds[C::NBUF * C::BUF];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int cp = t & 3, gg = t >> 2;
-  trace_event(0);
-  const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
-  const uint32_t nbt = static_cast<uint32_t>(g.n2 / 8);
-  const bool tslow = flags & kFft4TrialSlow;
-  const int k = static_cast<int>(tslow ? lb / nbt : lb % static_cast<uint32_t>(K));
-  const int r0 = static_cast<int>(tslow ? lb % nbt : lb / static_cast<uint32_t>(K)) * 8;
-  const TableOffsets to = table_offsets(L, g.n2);
-  // workgroup-uniform base (the lane's 2 cp goes into the offset): the buffer
-  // resource stays in SGPRs, no waterfall loop around the loads
-  const float2* yk = Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(r0 >> 3) * 64;
-  float2 va[P], vb[P];  // rows r0 + 2cp, r0 + 2cp + 1
-  {
-    // 32-bit buffer offsets (a trial's Y is < 2 GiB): one VGPR per address
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<float2*>(yk), 0, 0x7fffffff, 0x00020000);
-    const uint32_t blk = 8u * static_cast<uint32_t>(g.n2);
-#pragma unroll
-    for (int m = 0; m < P; ++m) {
-      const uint32_t i = static_cast<uint32_t>(gg + G * m);
-      const f4v v = __builtin_bit_cast(
-          f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i >> 3) * blk + (i & 7) * 8 + 2u * cp) * 8u, 0, 0));
-      va[m] = make_float2(v.x, v.y);
-      vb[m] = make_float2(v.z, v.w);
-    }
-  }
-  trace_event(1);
-  const int rc = (lane >> 3) & 7;
-  float2 u[C::NPAIR][G];
-  onex_core<L, G, R>(va, vb, u, lds, tab + to.n1, t);
-  float2* xk = X + static_cast<uint64_t>(k) * g.xstride + static_cast<uint64_t>(r0) * L;
-#pragma unroll
-  for (int p = 0; p < C::NPAIR; ++p) {
-    const uint32_t k1 = static_cast<uint32_t>(8 * (w + C::NW * p) + (lane & 7));
-#pragma unroll
-    for (int k2 = 0; k2 < G; ++k2) {
-      const uint32_t kk = k1 + static_cast<uint32_t>(P * k2);
-      xk[(kk >> 3) * 64 + static_cast<uint32_t>(rc) * 8 + (kk & 7)] = u[p][k2];
+      yk[(kk >> 3) * 64 + static_cast<uint32_t>(rc) * 8 + (kk & 7)] = cmul(u[p][k2], wv);
     }
   }
   trace_event(11);
@@ -885,24 +693,20 @@ fft4_rowpass_onex_kernel(const float2* __restrict__ Y, float2* __restrict__ X, i
 
 // Pass B.  Logical block = row block * K + trial.
 template <int L, int CPT, int SUB, int MODE>
-__global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::THREADS), amdgpu_waves_per_eu((CPT == 4 ? 4 : 2)))) fft4_rowpass_kernel(
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::THREADS), amdgpu_waves_per_eu(2))) fft4_rowpass_kernel(
     const float2* __restrict__ Y, float2* __restrict__ X, int K, Fft4Geom g, const float2* __restrict__ tab,
     int flags, uint32_t keep_oct) {
   using C = Cfg<L, CPT, SUB>;
-  constexpr bool kBlocked = MODE & kModeBlocked, kTiming = MODE & kModeTiming, kTileY = MODE & kModeTileY;
-  // the opt-in staged stores reuse the exchange buffer: size it for both
-  constexpr int kLdsN = (MODE & kModeStaged) && staged_lds_floats<L>() > C::LDS_FLOATS ? staged_lds_floats<L>()
-                                                                                      : C::LDS_FLOATS;
-  __shared__ __attribute__((aligned(16))) float lds[kLdsN];
+  constexpr bool kBlocked = MODE & kModeBlocked, kTileY = MODE & kModeTileY;
+  static_assert(!kTileY || (CPT == 8 && SUB == 1), "tiled Y: 8 transforms per thread");
+  __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   constexpr int T = C::T;
   const int grp = threadIdx.x / T;
   const int t = threadIdx.x - grp * T;
   const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
   trace_event(0);
-  const uint32_t nbt = static_cast<uint32_t>(g.n2 / C::CH);  // blocks per trial
-  const bool tslow = flags & kFft4TrialSlow;
-  const int k = static_cast<int>(tslow ? lb / nbt : lb % static_cast<uint32_t>(K));
-  const int r0 = static_cast<int>(tslow ? lb % nbt : lb / static_cast<uint32_t>(K)) * C::CH + grp * CPT;
+  const int k = static_cast<int>(lb % static_cast<uint32_t>(K));
+  const int r0 = static_cast<int>(lb / static_cast<uint32_t>(K)) * C::CH + grp * CPT;
   const TableOffsets to = table_offsets(L, g.n2);
   const float2* yk = Y + static_cast<uint64_t>(k) * g.ystride;
   Vec<CPT> v;
@@ -925,24 +729,14 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
 #pragma unroll
     for (int q = 0; q < kPts; ++q) {
       const uint32_t i = t + q * T;
-      if (kTiming && (flags & kFft4SkipLoad))
-        v[c][q] = make_float2(static_cast<float>(t + q), static_cast<float>(c));
-      else if (kBlocked)  // Y_b[i/8][r0 + c][i%8] (pass A always writes 8-wide blocks)
+      if (kBlocked)  // Y_b[i/8][r0 + c][i%8] (pass A always writes 8-wide blocks)
         v[c][q] = yk[static_cast<uint64_t>(i / 8) * (8 * g.n2) + (r0 + c) * 8 + (i % 8)];
       else
         v[c][q] = yk[static_cast<uint64_t>(r0 + c) * g.ypitch + i];
     }
   trace_event(1);
-  if (!kTiming || !(flags & kFft4SkipCompute))
-    fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n1);
+  fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n1);
   float2* xk = X + static_cast<uint64_t>(k) * g.xstride;
-  const bool nt = flags & kFft4NtStores;
-  if constexpr ((MODE & kModeTileX) != 0 && CPT == 8 && SUB == 1 && (MODE & kModeStaged) != 0) {
-    {
-      store_tiled_staged<L>(v, lds, t, xk + static_cast<uint64_t>(r0 >> 3) * (8 * L), keep_oct, nt);
-      return;
-    }
-  }
   if constexpr ((MODE & kModeTileX) != 0) {
     // keep_oct > 0: only k1 octets [0, keep_oct) and [L/8 - keep_oct, L/8)
     // are ever read (bins below the search limit and their mirrors); a wave's
@@ -963,212 +757,10 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
 #pragma unroll
   for (int q = 0; q < kPts; ++q) {
     const uint64_t k1 = t + q * T;
-    // blocked: X_b[r0/8][k1][r0%8 + c] (8-wide blocks; a 4-transform workgroup
-    // writes one 32-byte half); else X[k1][k2] at pitch xpitch
-    float2* dst = kBlocked ? xk + static_cast<uint64_t>(r0 / 8) * (8 * L) + k1 * 8 + (r0 % 8) : xk + k1 * g.xpitch + r0;
-    if (!kTiming || !(flags & kFft4SkipStore) || v[0][q].x == 1234.5f) store_row<CPT>(dst, v, q, nt);
+    // blocked: X_b[r0/8][k1][c] (8-wide blocks); else X[k1][k2] at pitch xpitch
+    float2* dst = kBlocked ? xk + static_cast<uint64_t>(r0 / 8) * (8 * L) + k1 * 8 : xk + k1 * g.xpitch + r0;
+    store_row<CPT>(dst, v, q);
   }
-}
-
-// ---------------------------------------------------------------------------
-// Pass B fused with the real-FFT post-processing, interbin and normalise
-// (kFft4FusedR2c).  Replaces pass B's complex spectrum X (written, then read
-// back by r2c_interbin_tiled: 33.5 + 33.5 MB per 2^23 trial) with the
-// normalised amplitudes P (16.7 MB written once).
-//
-// Bin k = c + n2 k1 of Z = FFT_M(z) is pass-B row c at point k1.  The real
-// spectrum needs the pair Z[k], Z[M-k], and M - k = (n2 - c) + n2 (n1-1-k1)
-// (c > 0): rows c and n2 - c with the points reversed.  Running the mirror
-// row's DFT on y'[i] = conj(y[i]) W_n1^i gives, at point k1,
-//   sum_i conj(y[i]) W^i W^{i k1} = conj(sum_i y[i] W^{i(n1-1-k1)}) = conj(Z[M-k])
-// (row 0 pairs with itself at n1 - k1: y' = conj(y)), so the thread holding
-// Z[k] in the ascending group holds conj(Z[M-k]) at the same position of the
-// mirror group: pairing is a same-thread LDS hand-over, no permutation.
-//
-// Workgroup o (two groups of n1/8 threads, Stockham engine, 9 transforms per
-// thread) runs rows c = 8o .. 8o+8 and their mirrors n2 - c, and emits
-//   ascending bins c = 8o+1 .. 8o+8 (interbin neighbour c - 1: same thread),
-//   mirror bins M - k, c = 8o .. 8o+7 (neighbour M - (k+1): row c + 1),
-// i.e. the octets [8J+1, 8J+8] of PLayout blk (one extra row per group, +12.5%
-// loads, instead of cross-workgroup halos).  Octet column g of the layout is
-// one contiguous block P[g][k1][8] per workgroup, so every wave stores 2 KiB
-// contiguous; natural-order stores would be 32-byte pieces n2*4 bytes apart
-// (~1.5 TB/s, docs/ROADMAP.md).  The harmonic sum reads the blocked layout.
-// Reference: src/pipeline_multi.cu:216-224 (R2C -> form_interpolated ->
-// normalise), src/kernels.cu:231-252, 469-494.
-template <int L>
-struct FusedR2c {
-  static constexpr int T = L / kPts;  // threads per group
-  static constexpr int THREADS = 2 * T;
-  static constexpr int CPT = 9;  // rows 8o .. 8o+8 (or their mirrors)
-  static constexpr int CG = 3;   // channels per exchange round
-  static constexpr int PAD = L + L / 8 + kChanPad;
-  static constexpr int GROUP_FLOATS = 2 * CG * PAD;
-  static constexpr int FFT_FLOATS = 2 * GROUP_FLOATS;
-  static constexpr int PAIR_FLOATS = 2 * 2 * (CPT * 4 * T);  // both groups hand over 4 points x 9 rows
-  static constexpr int LDS_FLOATS = FFT_FLOATS > PAIR_FLOATS ? FFT_FLOATS : PAIR_FLOATS;
-  static_assert(LDS_FLOATS * 4 <= 160 * 1024, "LDS budget");
-};
-
-template <int L>
-__global__ void __attribute__((amdgpu_flat_work_group_size(1, FusedR2c<L>::THREADS), amdgpu_waves_per_eu(2)))
-fft4_rowpass_r2c_kernel(const float2* __restrict__ Y, float* __restrict__ P, uint64_t pstride, int K, Fft4Geom g,
-                        const float2* __restrict__ tab, const float* __restrict__ stats, float nscale,
-                        const uint32_t* __restrict__ tsrc, uint32_t nbins_out) {
-  using C = FusedR2c<L>;
-  constexpr int T = C::T, CPT = C::CPT;
-  __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
-  const int grp = threadIdx.x >= T ? 1 : 0;  // 0: rows 8o + j, 1: rows n2 - 8o - j
-  const int t = threadIdx.x - grp * T;
-  const int n2 = g.n2;
-  const int ng = n2 >> 3;  // octet columns
-  const int k = static_cast<int>(blockIdx.x % static_cast<uint32_t>(K));
-  const int o = static_cast<int>(blockIdx.x / static_cast<uint32_t>(K));
-  const TableOffsets to = table_offsets(L, n2);
-  const float2* twL = tab + to.n1;
-  const float2* yk = Y + static_cast<uint64_t>(k) * g.ystride;
-  trace_event(0);
-  Vec<CPT> v;
-  {
-    // tiled Y: row c, point i at (i >> 3) * 8 n2 + (c >> 3) * 64 + (i & 7) * 8 + (c & 7)
-    const int oc = grp == 0 ? o : ng - 1 - o;           // the group's full octet
-    const int ox = grp == 0 ? o + 1 : (ng - o) & (ng - 1);  // octet of the ninth row (position 0)
-#pragma unroll
-    for (int q = 0; q < kPts; ++q) {
-      const uint32_t i = static_cast<uint32_t>(t + q * T);
-      const float2* base = yk + static_cast<uint64_t>(i >> 3) * (8ull * n2) + (i & 7) * 8;
-      const float4* src = reinterpret_cast<const float4*>(base + oc * 64);
-      float2 r[8];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float4 w = src[u];
-        r[2 * u] = make_float2(w.x, w.y);
-        r[2 * u + 1] = make_float2(w.z, w.w);
-      }
-      const float2 r9 = base[ox * 64];
-      if (grp == 0) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) v[j][q] = r[j];
-        v[8][q] = r9;
-      } else {
-        // channel j = row n2 - 8o - j: j = 0 is the ninth row, j = 1..8 are positions 7..0
-        const float2 w = twL[i];
-        v[0][q] = o == 0 ? make_float2(r9.x, -r9.y)  // row 0 pairs with itself (point n1 - k1)
-                         : make_float2(r9.x * w.x + r9.y * w.y, r9.x * w.y - r9.y * w.x);
-#pragma unroll
-        for (int j = 1; j < 9; ++j) {
-          const float2 a = r[8 - j];
-          v[j][q] = make_float2(a.x * w.x + a.y * w.y, a.x * w.y - a.y * w.x);  // conj(a) W^i
-        }
-      }
-    }
-  }
-  trace_event(1);
-  fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, twL);
-
-  const uint32_t M = static_cast<uint32_t>(L) * static_cast<uint32_t>(n2);
-  const float* st = stats + (tsrc ? 4u * tsrc[k] : 0u);
-  const float mean = st[0] * nscale, sigma = st[2] * nscale, rsig = 1.0f / sigma;
-  float* pk = P + static_cast<uint64_t>(k) * pstride;
-  const float2* rk = tab + to.rk;             // e^{-i pi k1 / n1}
-  const float2* rc = tab + to.rc + 8 * o;     // e^{-i pi c / M}, c = 8o + j
-  // hand-over: group 0 emits points q = 0..3, group 1 points 4..7 (one round,
-  // 9 rows x 4 points x T float2 per group); both groups then run one code
-  // path (wave-uniform selects), which keeps the kernel small enough for the
-  // instruction cache
-  float2* pb = reinterpret_cast<float2*>(lds);
-  auto slot = [&](int from, int j, int qq) { return pb + ((from * CPT + j) * 4 + qq) * T + t; };
-#pragma unroll
-  for (int qq = 0; qq < 4; ++qq)
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) *slot(grp, j, qq) = grp == 0 ? v[j][4 + qq] : v[j][qq];
-  __syncthreads();
-  trace_event(9);
-#pragma unroll
-  for (int qq = 0; qq < 4; ++qq) {
-    // za = Z[c + n2 k1] (rows 8o + j), zb = Z[M - (c + n2 k1)]
-    const uint32_t k1 = static_cast<uint32_t>(t + (grp * 4 + qq) * T);
-    const float2 w1 = rk[k1];
-    float2 xa[CPT], xm[CPT];
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) {
-      const float2 other = *slot(1 - grp, j, qq);
-      const float2 za = grp == 0 ? v[j][qq] : other;
-      const float2 cz = grp == 0 ? other : v[j][4 + qq];
-      const float2 wc = rc[j];
-      const float wx = __builtin_fmaf(wc.x, w1.x, -(wc.y * w1.y)), wy = __builtin_fmaf(wc.x, w1.y, wc.y * w1.x);
-      const float2 zb = make_float2(cz.x, -cz.y);
-      xa[j] = dev::r2c_combine(za, zb, wx, wy);
-      xm[j] = dev::r2c_combine(zb, za, -wx, wy);
-    }
-    float pa[8], pm[8];
-#pragma unroll
-    for (int j = 1; j <= 8; ++j) pa[j - 1] = dev::div_rn(dev::interbin(xa[j], xa[j - 1]) - mean, sigma, rsig);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) pm[7 - j] = dev::div_rn(dev::interbin(xm[j], xm[j + 1]) - mean, sigma, rsig);
-    const uint32_t base = static_cast<uint32_t>(8 * o) + static_cast<uint32_t>(n2) * k1;  // c = 8o
-    if (base + 1 < nbins_out) {  // ascending bins base+1 .. base+8: octet column o, row k1
-      f4v* d = reinterpret_cast<f4v*>(pk + (static_cast<uint64_t>(o) * L + k1) * 8);
-      d[0] = f4v{pa[0], pa[1], pa[2], pa[3]};
-      d[1] = f4v{pa[4], pa[5], pa[6], pa[7]};
-    }
-    if (M - base - 7 < nbins_out) {  // mirror bins M-base-7 .. M-base: column ng-1-o, row n1-1-k1
-      f4v* d = reinterpret_cast<f4v*>(pk + (static_cast<uint64_t>(ng - 1 - o) * L + (L - 1 - k1)) * 8);
-      d[0] = f4v{pm[0], pm[1], pm[2], pm[3]};
-      d[1] = f4v{pm[4], pm[5], pm[6], pm[7]};
-    }
-    if (o == 0 && k1 == 0) pk[M] = dev::div_rn(dev::interbin(xa[0], make_float2(0.f, 0.f)) - mean, sigma, rsig);  // bin 0
-  }
-  trace_event(11);
-}
-
-// natural <-> blocked spectrum copy (tests and tools)
-__global__ void __launch_bounds__(256) p_relayout_kernel(const float* __restrict__ in, float* __restrict__ out,
-                                                         uint64_t stride, PLayout L, int dir) {
-  in += blockIdx.y * stride;
-  out += blockIdx.y * stride;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i <= L.M; i += gridDim.x * blockDim.x) {
-    const uint32_t b = dev::paddr(i, L);
-    if (dir == 0)
-      out[b] = in[i];
-    else
-      out[i] = in[b];
-  }
-}
-
-// Blocked -> natural spectrum transpose for the harmonic sum (its gathers
-// need natural-order ranges: on the blocked layout every 16-byte load of a
-// wave touches its own 32-byte piece, 4x the cache-line requests, and the
-// harmonic kernel ran 2.1x slower).  A workgroup moves 16 octet columns x 16
-// rows of 32-byte pieces through LDS: 16 lanes read 512 contiguous bytes of
-// one octet column and write 512 contiguous bytes of one natural row.
-// Natural bin b lands at out + 3 + b (pieces 16-byte aligned when out is).
-__global__ void __launch_bounds__(256) p_unblock_kernel(const float* __restrict__ in, float* __restrict__ out,
-                                                        uint64_t stride, PLayout L, uint32_t nbins_out) {
-  __shared__ float4 tile[16][33];  // [row][2 * column + half], padded
-  const uint32_t ng = 1u << L.lg_g, n1 = 1u << L.lg_n1;
-  const uint32_t gblocks = ng >> 4;
-  const uint32_t g0 = (blockIdx.x % gblocks) * 16, r0 = (blockIdx.x / gblocks) * 16;
-  const float* pb = in + blockIdx.y * stride;
-  float* pn = out + blockIdx.y * stride + 3;
-  const uint32_t ngb = ng * 8;  // bins per row
-  if (r0 * ngb + 1 >= nbins_out) return;  // the whole tile lies at or beyond nbins_out
-  const int t = threadIdx.x;
-  {
-    const uint32_t g = g0 + (t >> 4), r = r0 + (t & 15);
-    const float4* src = reinterpret_cast<const float4*>(pb + (static_cast<uint64_t>(g) * n1 + r) * 8);
-    tile[t & 15][2 * (t >> 4)] = src[0];
-    tile[t & 15][2 * (t >> 4) + 1] = src[1];
-  }
-  __syncthreads();
-  const uint32_t r = r0 + (t >> 4), g = g0 + (t & 15);
-  const uint32_t b = r * ngb + g * 8 + 1;  // first bin of the piece
-  if (b < nbins_out) {
-    float4* dst = reinterpret_cast<float4*>(pn + b);
-    dst[0] = tile[t >> 4][2 * (t & 15)];
-    dst[1] = tile[t >> 4][2 * (t & 15) + 1];
-  }
-  if (blockIdx.x == 0 && t == 0) pn[0] = pb[L.M];  // bin 0
 }
 
 bool supported_len(int L) { return L >= 128 && L <= 4096 && (L & (L - 1)) == 0; }
@@ -1211,8 +803,6 @@ std::vector<float2> fft4_tables(const Fft4Geom& g) {
   const uint64_t Mi = static_cast<uint64_t>(g.n1) * static_cast<uint64_t>(g.n2);
   for (uint64_t col = 0; col < static_cast<uint64_t>(g.n1); ++col)
     for (uint64_t k2 = 0; k2 < GX; ++k2) t[o.ox + col * GX + k2] = w(static_cast<double>((col * PX * k2) % Mi), M);
-  for (int m = 0; m < g.n1; ++m) t[o.rk + m] = w(m, 2.0 * g.n1);
-  for (uint64_t c = 0; c < o.total - o.rc; ++c) t[o.rc + c] = w(static_cast<double>(c), 2.0 * M);
   return t;
 }
 
@@ -1286,7 +876,6 @@ void launch_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const 
   }
 }
 
-constexpr int kTimingFlags = kFft4SkipLoad | kFft4SkipStore | kFft4SkipCompute;
 }  // namespace
 
 void fft4_set_flags(int flags) {
@@ -1299,18 +888,21 @@ void fft4_set_trace(unsigned long long* d_events) {
 
 // The tiled spectrum needs 8 x 256 r2c tiles: n2 >= 256, n1 >= 16.
 bool tiled_x(const Fft4Geom& g, int f) {
-  return (f & kFft4Blocked) && (f & kFft4TileY) && (f & kFft4TileX) && !(f & kTimingFlags) && g.n2 >= 256 &&
-         g.n1 >= 16;
+  return (f & kFft4Blocked) && (f & kFft4TileY) && (f & kFft4TileX) && g.n2 >= 256 && g.n1 >= 16;
 }
 
 Fft4XLayout fft4_x_layout(const Fft4Geom& g) {
   const int f = g_fft4_flags;
   if (tiled_x(g, f)) return {g.log2_xrow, 0, 0, 3, true};
-  if ((f & kFft4Blocked) && (f & (kFft4Cpt8 | kFft4Ch4))) return {g.log2_xrow, 8, 8ull * g.n1, 3, false};
+  if ((f & kFft4Blocked) && (f & kFft4Cpt8)) return {g.log2_xrow, 8, 8ull * g.n1, 3, false};
   return {g.log2_xrow, g.xpitch, 8, 3, false};
 }
 int fft4_flags() { return g_fft4_flags; }
 
+// Kernel shape per flag set (both passes):
+//   Blocked + TileY (+ OneX at column length 2048): the production shapes;
+//   Cpt8 + Blocked: 8 transforms per thread, blocked Y/X (small geometries);
+//   Cpt8: natural Y/X, 8 transforms per thread; none: natural, 2 x 4.
 void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
                            const Fft4Geom& g, const float2* tables, hipStream_t s) {
   PSOUP_CHECK(g.ok && K >= 1 && n == 2ull * g.n1 * g.n2, "fft4 colpass: bad geometry n=" << n << " K=" << K);
@@ -1321,37 +913,11 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 16 == 0, "fft4 colpass: grid");
   PSOUP_CHECK(!(f & kFft4GroupXcd) || (K & 7) != 0 || nblocks % 128 == 0, "fft4 colpass: group grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
-  // (the one-exchange pass A honours the timing flags itself)
-  if ((f & kFft4OneX) && (f & kFft4Blocked) && (f & kFft4TileY) && !(f & kFft4Sub2) &&
-      (g.n2 == 2048 || ((f & kFft4OneXSmall) && (g.n2 == 512 || g.n2 == 1024)))) {
-    switch (g.n2) {
-#define PS_ONEX(LL, GG, RR)                                                                                  \
-  case LL:                                                                                                   \
-    fft4_colpass_onex_kernel<LL, GG, RR><<<grid, OneX<LL, GG, RR>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g, \
-                                                                                  tables, f);              \
-    break;
-      PS_ONEX(512, 32, 1) PS_ONEX(1024, 32, 1)
-      case 2048:
-        if (f & kFft4OneXWholeCu)
-          fft4_colpass_onex_kernel<2048, 64, 1><<<grid, OneX<2048, 64, 1>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g,
-                                                                                          tables, f);
-        else
-          fft4_colpass_onex_kernel<2048, 64, 4><<<grid, OneX<2048, 64, 4>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g,
-                                                                                          tables, f);
-        break;
-#undef PS_ONEX
-      default: PSOUP_THROW("fft4: one-exchange column length " << g.n2);
-    }
-  } else if ((f & kFft4Blocked) && (f & kFft4TileY) && (f & kFft4Sub2) && !(f & kTimingFlags))
-    launch_colpass<4, 2, kModeBlocked | kModeTileY>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
-  else if ((f & kFft4Blocked) && (f & kFft4TileY) && (f & kFft4StagedStores) && !(f & kTimingFlags))
-    launch_colpass<8, 1, kModeBlocked | kModeTileY | kModeStaged>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
-  else if ((f & kFft4Blocked) && (f & kFft4TileY) && !(f & kTimingFlags))
+  if (onex_colpass(g.n2, f))
+    fft4_colpass_onex_kernel<2048, 64, 4><<<grid, OneX<2048, 64, 4>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g,
+                                                                                    tables, f);
+  else if ((f & kFft4Blocked) && (f & kFft4TileY))
     launch_colpass<8, 1, kModeBlocked | kModeTileY>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
-  else if ((f & kFft4Blocked) && (f & kFft4Ch4) && !(f & kTimingFlags))  // Y stays 8-wide; only pass B narrows
-    launch_colpass<8, 1, kModeBlocked>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
-  else if (f & kTimingFlags)
-    launch_colpass<8, 1, kModeBlocked | kModeTiming>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   else if ((f & kFft4Cpt8) && (f & kFft4Blocked))
     launch_colpass<8, 1, kModeBlocked>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   else if (f & kFft4Cpt8)
@@ -1366,11 +932,10 @@ void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const fl
   PSOUP_CHECK(g.ok && K >= 1, "fft4 rowpass: bad geometry");
   PSOUP_CHECK((reinterpret_cast<uintptr_t>(X) & 63) == 0, "fft4 rowpass: X alignment");
   const int f = g_fft4_flags;
-  const int ch = ((f & kFft4Blocked) && (f & kFft4Ch4) && !(f & kTimingFlags)) ? 4 : 8;
-  const uint64_t nblocks = static_cast<uint64_t>(g.n2 / ch) * K;
+  const uint64_t nblocks = static_cast<uint64_t>(g.n2 / 8) * K;
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 8 == 0, "fft4 rowpass: grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
-  const bool tiley = (f & kFft4Blocked) && (f & kFft4TileY) && !(f & kTimingFlags);
+  const bool tiley = (f & kFft4Blocked) && (f & kFft4TileY);
   if (tiley && tiled_x(g, f)) {
     // rows r2c_interbin_normalise_tiled reads: octets [0, ny] and [n1/8 - ny, n1/8)
     uint32_t keep = 0;
@@ -1378,33 +943,9 @@ void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const fl
       const uint32_t ny = r2c_tiled_row_blocks(nbins_out, g.n1, g.n2);
       if (2 * (ny + 1) < static_cast<uint32_t>(g.n1 / 8)) keep = ny + 1;
     }
-    if ((f & kFft4OneXRow) && keep == 0 && !(f & (kFft4Sub2 | kFft4StagedStores)) &&
-        (g.n1 == 512 || g.n1 == 1024 || g.n1 == 2048)) {
-      switch (g.n1) {
-#define PS_ONEXR(LL, GG, RR)                                                                              \
-  case LL:                                                                                                \
-    fft4_rowpass_onex_kernel<LL, GG, RR><<<grid, OneX<LL, GG, RR>::THREADS, 0, s>>>(Y, X, K, g, tables, f);       \
-    break;
-        PS_ONEXR(512, 32, 1) PS_ONEXR(1024, 32, 1) PS_ONEXR(2048, 64, 4)
-#undef PS_ONEXR
-        default: PSOUP_THROW("fft4: one-exchange row length " << g.n1);
-      }
-    } else if (f & kFft4Sub2)
-      launch_rowpass<4, 2, kModeBlocked | kModeTileY | kModeTileX>(Y, X, K, g, tables, grid, f, s, keep);
-    else if (f & kFft4StagedStores)
-      launch_rowpass<8, 1, kModeBlocked | kModeTileY | kModeTileX | kModeStaged>(Y, X, K, g, tables, grid, f, s,
-                                                                                   keep);
-    else
-      launch_rowpass<8, 1, kModeBlocked | kModeTileY | kModeTileX>(Y, X, K, g, tables, grid, f, s, keep);
-  }
-  else if (ch == 4 && tiley)
-    launch_rowpass<4, 1, kModeBlocked | kModeTileY>(Y, X, K, g, tables, grid, f, s);
-  else if (tiley)
+    launch_rowpass<8, 1, kModeBlocked | kModeTileY | kModeTileX>(Y, X, K, g, tables, grid, f, s, keep);
+  } else if (tiley)
     launch_rowpass<8, 1, kModeBlocked | kModeTileY>(Y, X, K, g, tables, grid, f, s);
-  else if (ch == 4)
-    launch_rowpass<4, 1, kModeBlocked>(Y, X, K, g, tables, grid, f, s);
-  else if (f & kTimingFlags)
-    launch_rowpass<8, 1, kModeBlocked | kModeTiming>(Y, X, K, g, tables, grid, f, s);
   else if ((f & kFft4Cpt8) && (f & kFft4Blocked))
     launch_rowpass<8, 1, kModeBlocked>(Y, X, K, g, tables, grid, f, s);
   else if (f & kFft4Cpt8)
@@ -1412,65 +953,6 @@ void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const fl
   else
     launch_rowpass<4, 2, 0>(Y, X, K, g, tables, grid, f, s);
   post_launch_check("fft4_rowpass_kernel", s);
-}
-
-bool fft4_fused_r2c_ok(const Fft4Geom& g) {
-  const int f = g_fft4_flags;
-  return g.ok && (f & kFft4FusedR2c) && (f & kFft4Blocked) && (f & kFft4TileY) && !(f & kTimingFlags) &&
-         (g.n1 == 512 || g.n1 == 1024 || g.n1 == 2048) && g.n2 >= 128;
-}
-
-PLayout fft4_p_layout(const Fft4Geom& g) {
-  PLayout l;
-  l.blk = 1;
-  l.lg_n1 = __builtin_ctz(static_cast<unsigned>(g.n1));
-  l.lg_g = __builtin_ctz(static_cast<unsigned>(g.n2 / 8));
-  l.M = static_cast<uint32_t>(g.n1) * static_cast<uint32_t>(g.n2);
-  return l;
-}
-
-void fft4_rowpass_r2c(const float2* Y, float* P, uint64_t pstride, int K, const Fft4Geom& g, const float2* tables,
-                      const float* stats, float nscale, const uint32_t* tsrc, uint64_t nbins_out, hipStream_t s) {
-  PSOUP_CHECK(fft4_fused_r2c_ok(g) && K >= 1, "fft4 rowpass_r2c: unsupported geometry/flags");
-  const uint64_t M = static_cast<uint64_t>(g.n1) * g.n2;
-  PSOUP_CHECK(M < (1ull << 31) && pstride >= M + 1 && pstride % 8 == 0, "fft4 rowpass_r2c: P stride " << pstride);
-  PSOUP_CHECK((reinterpret_cast<uintptr_t>(P) & 31) == 0 && (reinterpret_cast<uintptr_t>(Y) & 15) == 0,
-              "fft4 rowpass_r2c: alignment");
-  const uint64_t nblocks = static_cast<uint64_t>(g.n2 / 16) * K;
-  PSOUP_CHECK(nblocks < (1ull << 31), "fft4 rowpass_r2c: grid");
-  const uint32_t nbo = static_cast<uint32_t>(std::min<uint64_t>(nbins_out == 0 ? M + 1 : nbins_out, M + 1));
-  const dim3 grid(static_cast<unsigned>(nblocks));
-  switch (g.n1) {
-#define PS_FUSED(LL)                                                                                           \
-  case LL:                                                                                                     \
-    fft4_rowpass_r2c_kernel<LL><<<grid, FusedR2c<LL>::THREADS, 0, s>>>(Y, P, pstride, K, g, tables, stats, nscale, \
-                                                                      tsrc, nbo);                             \
-    break;
-    PS_FUSED(512) PS_FUSED(1024) PS_FUSED(2048)
-#undef PS_FUSED
-    default: PSOUP_THROW("fft4 rowpass_r2c: row length " << g.n1);
-  }
-  post_launch_check("fft4_rowpass_r2c_kernel", s);
-}
-
-void p_unblock(const float* in, float* out, uint64_t stride, int K, const PLayout& L, uint64_t nbins_out,
-               hipStream_t s) {
-  PSOUP_CHECK(L.blk && L.lg_g >= 4 && L.lg_n1 >= 4, "p_unblock: needs n2 >= 128 and n1 >= 16");
-  PSOUP_CHECK(K >= 1 && K <= 65535 && stride >= static_cast<uint64_t>(L.M) + 4 && stride % 4 == 0,
-              "p_unblock: bad shape");
-  PSOUP_CHECK((reinterpret_cast<uintptr_t>(in) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0,
-              "p_unblock: alignment");
-  const uint32_t nbo = static_cast<uint32_t>(std::min<uint64_t>(nbins_out == 0 ? L.M + 1ull : nbins_out, L.M + 1ull));
-  const dim3 grid((L.M / 8) / 256, static_cast<unsigned>(K));
-  p_unblock_kernel<<<grid, 256, 0, s>>>(in, out, stride, L, nbo);
-  post_launch_check("p_unblock_kernel", s);
-}
-
-void p_relayout(const float* in, float* out, uint64_t stride, int K, const PLayout& L, int dir, hipStream_t s) {
-  PSOUP_CHECK(K >= 1 && K <= 65535 && stride >= static_cast<uint64_t>(L.M) + 1, "p_relayout: bad shape");
-  const dim3 grid(dev::grid_for(static_cast<uint64_t>(L.M) + 1, 256, 4096), static_cast<unsigned>(K));
-  p_relayout_kernel<<<grid, 256, 0, s>>>(in, out, stride, L, dir);
-  post_launch_check("p_relayout_kernel", s);
 }
 
 }  // namespace kern

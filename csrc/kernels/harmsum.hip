@@ -489,15 +489,13 @@ __device__ __forceinline__ void emit_levels(const bool (&pred)[NL], int h0, int 
 // neighbouring tiles need overlapping ranges), then every thread sums its
 // bins from LDS.  Even numerators repeat the previous level's terms and
 // are not re-read (as in the reference recurrence).
-// EXTRA: floats of slack per gather range (3 for the blocked layout, whose
-// staging chunks start on a piece boundary up to 3 bins before the range).
-template <int NLEV, int BPT_ = 0, int EXTRA = 0>
+template <int NLEV, int BPT_ = 0>
 struct HarmTile {
   static constexpr int BPT = BPT_ > 0 ? BPT_ : (NLEV <= 3 ? 8 : (NLEV == 4 ? 4 : 2));
   static constexpr int B = 256 * BPT;
   static constexpr int NREG = 1 << NLEV;  // (fundamental) + sum_{h=1..NLEV} 2^(h-1) gather ranges
   static constexpr int maxlen(int h, int m) { return h == 0 ? B : (((B - 1) * m) >> h) + 2; }
-  static constexpr int chunks(int h, int m) { return (maxlen(h, m) + EXTRA + 3) / 4; }  // 16-byte chunks
+  static constexpr int chunks(int h, int m) { return (maxlen(h, m) + 3) / 4; }  // 16-byte chunks
   static constexpr int region(int h, int m) { return h == 0 ? 0 : (1 << (h - 1)) + (m - 1) / 2; }
   // LDS offset (floats, multiple of 4) of gather range r >= 1; the fundamental stays in registers
   static constexpr int offset(int r) {
@@ -521,30 +519,11 @@ struct HarmTile {
 
 typedef float f4u_h __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned 16-byte load
 
-// First bin a gather range starting at r0 is staged from: r0 itself
-// (natural layout), or the start of the 4-bin chunk of r0 in the blocked
-// layout (chunks 4q+1 .. 4q+4 are contiguous and 16-byte aligned there).
-template <bool BLK>
-__device__ __forceinline__ int stage_start(int r0) {
-  return BLK ? ((r0 + 3) & ~3) - 3 : r0;
-}
-
-// 4 consecutive bins a .. a+3 (< hi) of spectrum p in layout pl; bins past
-// `last` read bin `last` (never used), bins below 0 read bin 0.
-template <bool BLK>
-__device__ __forceinline__ f4u_h load_chunk(const float* __restrict__ p, int a, int last, const PLayout& pl) {
-  if (BLK) {
-    if (a >= 1 && a + 3 <= last) return *reinterpret_cast<const f4u_h*>(p + dev::paddr(static_cast<uint32_t>(a), pl));
-    auto at = [&](int x) { return p[dev::paddr(static_cast<uint32_t>(max(0, min(x, last))), pl)]; };
-    return f4u_h{at(a), at(a + 1), at(a + 2), at(a + 3)};
-  }
+// 4 consecutive bins a .. a+3 of spectrum p; bins past `last` read bin
+// `last` (never used).
+__device__ __forceinline__ f4u_h load_chunk(const float* __restrict__ p, int a, int last) {
   if (a + 3 <= last) return *reinterpret_cast<const f4u_h*>(p + a);
   return f4u_h{p[min(a, last)], p[min(a + 1, last)], p[min(a + 2, last)], p[min(a + 3, last)]};
-}
-
-template <bool BLK>
-__device__ __forceinline__ float load_bin(const float* __restrict__ p, int i, const PLayout& pl) {
-  return BLK ? p[dev::paddr(static_cast<uint32_t>(i), pl)] : p[i];
 }
 
 // Block order: with xcd_trials (K % 8 == 0) XCD x (blockIdx % 8 under
@@ -559,13 +538,13 @@ struct HarmPre {
   float lo[6];
 };
 
-template <int NLEV, int BPT_ = 0, bool BLK = false>
+template <int NLEV, int BPT_ = 0>
 __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __restrict__ P, uint64_t pstride,
                                                              int lo, int hi, HarmParams hp,
                                                              PeakRecord* __restrict__ out,
                                                              uint32_t* __restrict__ count, int ntiles,
-                                                             int xcd_trials, HarmPre pre, PLayout pl) {
-  using Tl = HarmTile<NLEV, BPT_, BLK ? 3 : 0>;
+                                                             int xcd_trials, HarmPre pre) {
+  using Tl = HarmTile<NLEV, BPT_>;
   constexpr int B = Tl::B;
   __shared__ __attribute__((aligned(16))) float lds[Tl::TOTAL];
   const uint32_t bid = blockIdx.x;
@@ -587,11 +566,10 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
   if (xcd_trials & 2) {  // tuning: streaming (nontemporal) fundamental loads
 #pragma unroll
     for (int u = 0; u < Tl::BPT; ++u)
-      fund[u] = __builtin_nontemporal_load(p + (BLK ? dev::paddr(min(b0 + t + 256 * u, last), pl)
-                                                    : static_cast<uint32_t>(min(b0 + t + 256 * u, last))));
+      fund[u] = __builtin_nontemporal_load(p + min(b0 + t + 256 * u, last));
   } else {
 #pragma unroll
-    for (int u = 0; u < Tl::BPT; ++u) fund[u] = load_bin<BLK>(p, min(b0 + t + 256 * u, last), pl);
+    for (int u = 0; u < Tl::BPT; ++u) fund[u] = p[min(b0 + t + 256 * u, last)];
   }
   // ---- stage every gather range in 16-byte chunks: all loads are issued
   // before the first LDS store (fixed trip counts).  Only values at indices
@@ -604,10 +582,10 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
 #pragma unroll
       for (int m = 1; m < (1 << h); m += 2) {
         const int half = 1 << (h - 1);
-        const int r0 = stage_start<BLK>((b0 * m + half) >> h);
+        const int r0 = (b0 * m + half) >> h;
 #pragma unroll
         for (int e = 0; e < (Tl::chunks(h, m) + 255) / 256; ++e, ++it)
-          tmp[it] = load_chunk<BLK>(p, r0 + 4 * (t + 256 * e), last, pl);
+          tmp[it] = load_chunk(p, r0 + 4 * (t + 256 * e), last);
       }
     }
   }
@@ -642,7 +620,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
     lo_h[h] = hp.start[h];
     hi_h[h] = hp.end[h];
   }
-#define PS_BASE(h, m) (Tl::offset(Tl::region(h, m)) + (((i0 * (m) + (1 << ((h) - 1))) >> (h)) - stage_start<BLK>((b0 * (m) + (1 << ((h) - 1))) >> (h))))
+#define PS_BASE(h, m) (Tl::offset(Tl::region(h, m)) + (((i0 * (m) + (1 << ((h) - 1))) >> (h)) - ((b0 * (m) + (1 << ((h) - 1))) >> (h))))
   int base[Tl::NREG];
   if constexpr (NLEV >= 1) base[1] = PS_BASE(1, 1);
   if constexpr (NLEV >= 2) {
@@ -730,9 +708,9 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
 // registers at NLEV = 3, so more workgroups share a CU.  Same sums in the
 // same order, same records (emitted level by level; the host sorts each
 // (trial, level) segment).
-template <int NLEV, int EXTRA = 0>
+template <int NLEV>
 struct HarmTile2 {
-  using T = HarmTile<NLEV, 0, EXTRA>;
+  using T = HarmTile<NLEV, 0>;
   static constexpr int SPLIT = 1 << (NLEV - 1);  // first region of the top level
   static constexpr int P1 = T::offset(SPLIT);    // floats of levels 1..NLEV-1
   static constexpr int P2 = T::TOTAL - P1;       // floats of level NLEV
@@ -746,14 +724,14 @@ struct HarmTile2 {
   static constexpr int IT = iters(1, NLEV - 1) > iters(NLEV, NLEV) ? iters(1, NLEV - 1) : iters(NLEV, NLEV);
 };
 
-template <int NLEV, bool BLK = false>
+template <int NLEV>
 __global__ void __launch_bounds__(256) harmonic_peaks2_kernel(const float* __restrict__ P, uint64_t pstride, int lo,
                                                               int hi, HarmParams hp, PeakRecord* __restrict__ out,
                                                               uint32_t* __restrict__ count, int ntiles, int xcd_trials,
-                                                              HarmPre pre, PLayout pl) {
+                                                              HarmPre pre) {
   static_assert(NLEV >= 2, "two phases need at least two levels");
-  using Tl = HarmTile<NLEV, 0, BLK ? 3 : 0>;
-  using T2 = HarmTile2<NLEV, BLK ? 3 : 0>;
+  using Tl = HarmTile<NLEV, 0>;
+  using T2 = HarmTile2<NLEV>;
   constexpr int B = Tl::B;
   __shared__ __attribute__((aligned(16))) float lds[T2::LDS];
   const uint32_t bid = blockIdx.x;
@@ -781,10 +759,10 @@ __global__ void __launch_bounds__(256) harmonic_peaks2_kernel(const float* __res
     for (int h = HLO; h <= HHI; ++h) {
 #pragma unroll
       for (int m = 1; m < (1 << h); m += 2) {
-        const int r0 = stage_start<BLK>((b0 * m + (1 << (h - 1))) >> h);
+        const int r0 = (b0 * m + (1 << (h - 1))) >> h;
 #pragma unroll
         for (int e = 0; e < (Tl::chunks(h, m) + 255) / 256; ++e, ++it)
-          tmp[it] = load_chunk<BLK>(p, r0 + 4 * (t + 256 * e), last, pl);
+          tmp[it] = load_chunk(p, r0 + 4 * (t + 256 * e), last);
       }
     }
     it = 0;
@@ -802,12 +780,12 @@ __global__ void __launch_bounds__(256) harmonic_peaks2_kernel(const float* __res
   // LDS index of term (h, m) for bin i0 + 256 u (affine in u, see harmonic_peaks_kernel)
   auto term = [&](int h, int m, int base_off, int u) {
     const int r = Tl::region(h, m);
-    const int b = Tl::offset(r) - base_off + (((i0 * m + (1 << (h - 1))) >> h) - stage_start<BLK>((b0 * m + (1 << (h - 1))) >> h));
+    const int b = Tl::offset(r) - base_off + (((i0 * m + (1 << (h - 1))) >> h) - ((b0 * m + (1 << (h - 1))) >> h));
     return lds[b + u * (m << (8 - h))];
   };
   float fund[Tl::BPT];
 #pragma unroll
-  for (int u = 0; u < Tl::BPT; ++u) fund[u] = load_bin<BLK>(p, min(b0 + t + 256 * u, last), pl);
+  for (int u = 0; u < Tl::BPT; ++u) fund[u] = p[min(b0 + t + 256 * u, last)];
   stage(std::integral_constant<int, 1>{}, std::integral_constant<int, NLEV - 1>{});
   __syncthreads();
   const float thr = hp.thresh;
@@ -1160,7 +1138,7 @@ void harmonic_set_flags(int flags) {
 int harmonic_flags() { return g_harm_flags; }
 
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
-                          PeakRecord* out, uint32_t* count, hipStream_t s, const PLayout& pl) {
+                          PeakRecord* out, uint32_t* count, hipStream_t s) {
   PSOUP_CHECK(hp.nlevels >= 0 && hp.nlevels <= kMaxHarmLevels, "nlevels out of range");
   PSOUP_CHECK(nbins < (1ull << 31), "spectrum too long for int32 indices");
   int lo = static_cast<int>(nbins), hi = 0;
@@ -1174,11 +1152,6 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
   PSOUP_CHECK((static_cast<uint64_t>(K) + hp.trial_base) * 8 <= 65536, "chunk descriptors hold 16-bit segments");
   if (hi <= lo) return;
   PSOUP_CHECK(static_cast<int64_t>(hi) * 32 < (int64_t(1) << 31), "spectrum too long for the int32 gather math");
-  if (pl.blk) {
-    PSOUP_CHECK(static_cast<uint64_t>(hi) <= static_cast<uint64_t>(pl.M) + 1 && pstride >= static_cast<uint64_t>(pl.M) + 1 &&
-                    pstride % 4 == 0 && (reinterpret_cast<uintptr_t>(P) & 15) == 0,
-                "harmonic_peaks_batch: blocked spectrum shape");
-  }
   const int xcd = ((g_harm_flags & 1) && (K % 8 == 0) ? 1 : 0) | ((g_harm_flags & 4) ? 2 : 0);
   // bits 8-15: dynamic LDS occupancy cap, measured for (and applied to) the
   // two-phase 3-level kernel only (the other kernels keep their full occupancy)
@@ -1198,43 +1171,33 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
     }
   }
   auto ntiles_of = [&](int B) { return (hi - lo + B - 1) / B; };
-  auto one = [&](auto nl_c, auto bp_c, auto blk_c) {
+  auto one = [&](auto nl_c, auto bp_c) {
     constexpr int NL = decltype(nl_c)::value, BP = decltype(bp_c)::value;
-    constexpr bool BLK = decltype(blk_c)::value;
-    const int nt = ntiles_of(HarmTile<NL, BP, BLK ? 3 : 0>::B);
+    const int nt = ntiles_of(HarmTile<NL, BP>::B);
     PSOUP_CHECK(static_cast<int64_t>(nt) * K < (int64_t(1) << 31), "harmonic grid too large");
-    harmonic_peaks_kernel<NL, BP, BLK><<<dim3(static_cast<unsigned>(nt * K)), 256, 0, s>>>(
-        P, pstride, lo, hi, hp, out, count, nt, xcd, pre, pl);
+    harmonic_peaks_kernel<NL, BP><<<dim3(static_cast<unsigned>(nt * K)), 256, 0, s>>>(P, pstride, lo, hi, hp, out,
+                                                                                      count, nt, xcd, pre);
   };
-  auto two = [&](auto blk_c) {
-    constexpr bool BLK = decltype(blk_c)::value;
-    const int nt = ntiles_of(HarmTile<3, 0, BLK ? 3 : 0>::B);
-    PSOUP_CHECK(static_cast<int64_t>(nt) * K < (int64_t(1) << 31), "harmonic grid too large");
-    harmonic_peaks2_kernel<3, BLK><<<dim3(static_cast<unsigned>(nt * K)), 256, dyn_lds2, s>>>(
-        P, pstride, lo, hi, hp, out, count, nt, xcd, pre, pl);
-  };
-  auto dispatch = [&](auto blk_c) {
-    using I = std::integral_constant<int, 0>;
-    switch (hp.nlevels) {
-      case 0: one(I{}, I{}, blk_c); break;
-      case 1: one(std::integral_constant<int, 1>{}, I{}, blk_c); break;
-      case 2: one(std::integral_constant<int, 2>{}, I{}, blk_c); break;
-      case 3:
-        if (g_harm_flags & 32)  // two staging phases (levels 1-2, then 3) in 16.4 KiB of LDS
-          two(blk_c);
-        else if (g_harm_flags & 8)  // tuning: 1024-bin tiles (half the LDS and registers per workgroup)
-          one(std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{}, blk_c);
-        else
-          one(std::integral_constant<int, 3>{}, I{}, blk_c);
-        break;
-      case 4: one(std::integral_constant<int, 4>{}, I{}, blk_c); break;
-      default: one(std::integral_constant<int, 5>{}, I{}, blk_c); break;
-    }
-  };
-  if (pl.blk)
-    dispatch(std::true_type{});
-  else
-    dispatch(std::false_type{});
+  using I = std::integral_constant<int, 0>;
+  switch (hp.nlevels) {
+    case 0: one(I{}, I{}); break;
+    case 1: one(std::integral_constant<int, 1>{}, I{}); break;
+    case 2: one(std::integral_constant<int, 2>{}, I{}); break;
+    case 3:
+      if (g_harm_flags & 32) {  // two staging phases (levels 1-2, then 3) in 16.4 KiB of LDS
+        const int nt = ntiles_of(HarmTile<3, 0>::B);
+        PSOUP_CHECK(static_cast<int64_t>(nt) * K < (int64_t(1) << 31), "harmonic grid too large");
+        harmonic_peaks2_kernel<3><<<dim3(static_cast<unsigned>(nt * K)), 256, dyn_lds2, s>>>(P, pstride, lo, hi, hp,
+                                                                                           out, count, nt, xcd, pre);
+      } else if (g_harm_flags & 8) {  // tuning: 1024-bin tiles (half the LDS and registers per workgroup)
+        one(std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{});
+      } else {
+        one(std::integral_constant<int, 3>{}, I{});
+      }
+      break;
+    case 4: one(std::integral_constant<int, 4>{}, I{}); break;
+    default: one(std::integral_constant<int, 5>{}, I{}); break;
+  }
   post_launch_check("harmonic_peaks_kernel", s);
 }
 

@@ -587,31 +587,9 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("Y"), py::arg("X"), py::arg("K"), py::arg("g"), py::arg("tab"), py::arg("s"), py::arg("nbins_out") = 0);
   k.def("r2c_tiled_row_blocks", &kern::r2c_tiled_row_blocks);
-  py::class_<kern::PLayout>(k, "PLayout")
-      .def(py::init<>())
-      .def_readonly("blk", &kern::PLayout::blk)
-      .def_readonly("lg_n1", &kern::PLayout::lg_n1)
-      .def_readonly("lg_g", &kern::PLayout::lg_g)
-      .def_readonly("M", &kern::PLayout::M);
-  k.def("fft4_fused_r2c_ok", &kern::fft4_fused_r2c_ok);
-  k.def("fft4_p_layout", &kern::fft4_p_layout);
-  k.def(
-      "fft4_rowpass_r2c",
-      [](uintptr_t Y, uintptr_t Pout, uint64_t pstride, int K, const kern::Fft4Geom& g, uintptr_t tab,
-         uintptr_t stats, float nscale, uint64_t nbins_out, uintptr_t s) {
-        kern::fft4_rowpass_r2c(P<const float2>(Y), P<float>(Pout), pstride, K, g, P<const float2>(tab),
-                               P<const float>(stats), nscale, nullptr, nbins_out, S(s));
-      },
-      py::arg("Y"), py::arg("P"), py::arg("pstride"), py::arg("K"), py::arg("g"), py::arg("tab"), py::arg("stats"),
-      py::arg("nscale"), py::arg("nbins_out"), py::arg("s"));
-  k.def("p_unblock", [](uintptr_t in, uintptr_t out, uint64_t stride, int K, const kern::PLayout& l, uint64_t nbo,
-                        uintptr_t s) { kern::p_unblock(P<const float>(in), P<float>(out), stride, K, l, nbo, S(s)); });
-  k.def("p_relayout", [](uintptr_t in, uintptr_t out, uint64_t stride, int K, const kern::PLayout& l, int dir,
-                         uintptr_t s) { kern::p_relayout(P<const float>(in), P<float>(out), stride, K, l, dir, S(s)); });
   k.def("harmonic_peaks_batch", [](uintptr_t Pin, uint64_t nb, uint64_t pstride, int K, int nlevels,
                                    const std::vector<int>& start, const std::vector<int>& end, float thresh,
-                                   uint32_t capacity, uintptr_t out, uintptr_t count, uintptr_t s,
-                                   const kern::PLayout& layout) {
+                                   uint32_t capacity, uintptr_t out, uintptr_t count, uintptr_t s) {
     kern::HarmParams hp{};
     hp.nlevels = nlevels;
     for (int i = 0; i < 6; ++i) {
@@ -621,10 +599,9 @@ PYBIND11_MODULE(_C, m) {
     hp.thresh = thresh;
     hp.capacity = capacity;
     kern::harmonic_peaks_batch(P<const float>(Pin), nb, pstride, K, hp, P<kern::PeakRecord>(out), P<uint32_t>(count),
-                               S(s), layout);
+                               S(s));
   }, py::arg("P"), py::arg("nb"), py::arg("pstride"), py::arg("K"), py::arg("nlevels"), py::arg("start"),
-     py::arg("end"), py::arg("thresh"), py::arg("capacity"), py::arg("out"), py::arg("count"), py::arg("s"),
-     py::arg("layout") = kern::PLayout{});
+     py::arg("end"), py::arg("thresh"), py::arg("capacity"), py::arg("out"), py::arg("count"), py::arg("s"));
   k.def("peak_cluster_batch", [](uintptr_t peaks, uintptr_t count, uint32_t cap, uint32_t nseg, int gap,
                                  uintptr_t work, uintptr_t sorted, uintptr_t out, uintptr_t segtab, uintptr_t total,
                                  uintptr_t s) {

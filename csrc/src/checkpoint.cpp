@@ -134,7 +134,7 @@ RunIdentity make_run_identity(const CmdLineOptions& a, const SigprocHeader& hdr)
   // numerics-affecting runtime switches: kernel flag words set through the
   // API, and the env knobs that select another arithmetic path
   os << "switches: " << numerics_flags();
-  for (const char* k : {"PSOUP_FUSED_R2C", "PSOUP_WHITEN_ROCFFT"})
+  for (const char* k : {"PSOUP_WHITEN_ROCFFT"})
     if (const char* v = std::getenv(k)) os << " " << k << "=" << v;
   os << "\n";
   RunIdentity id;

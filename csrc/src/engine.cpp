@@ -241,11 +241,7 @@ void Dedisperser::build_valu_tables() {
 static double valu_ratio() {
   // MFMA steps per (tile, active channel) above which the VALU kernel is
   // faster (calibrated on MI355X with tools/dedisp_bench.py)
-  static const double r = [] {
-    const char* e = std::getenv("PSOUP_DEDISP_VALU_RATIO");
-    return e ? std::atof(e) : 1.85;
-  }();
-  return r;
+  return 1.85;
 }
 
 double Dedisperser::mfma_steps_per_channel(int d0, int d1) {
@@ -298,11 +294,7 @@ static double mfma_lds_ratio() {
   // MFMA kernel in Auto (each step is 2 x 16-shift blocks of one-hot GEMM;
   // the VALU kernels cost the same per channel whatever the spread).
   // Measured crossover on MI355X (profiles/r3_dedisp): ~2.35 steps/channel
-  static const double r = [] {
-    const char* e = std::getenv("PSOUP_DEDISP_MFMA_RATIO");
-    return e ? std::atof(e) : 2.3;
-  }();
-  return r;
+  return 2.3;
 }
 
 int Dedisperser::mfma_lds_split(int d0, int d1) {
@@ -401,13 +393,9 @@ void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispK
   const int ndm = d1 - d0;
   if (kind == DedispKernel::Valu) {
     if (!valu_ready_) build_valu_tables();
-    static const bool lds_on = [] {
-      const char* e = std::getenv("PSOUP_DEDISP_LDS");  // A/B knob: 0 = global-load kernel only
-      return !(e && std::atoi(e) == 0);
-    }();
     int win = 0;
     for (int T = d0 / kTileDms; T <= (d1 - 1) / kTileDms; ++T) win = std::max(win, h_tile_win_[static_cast<size_t>(T)]);
-    if (lds_on && kern::dedisperse_lds_fits(g.nbits, g.nactive, win))
+    if (kern::dedisperse_lds_fits(g.nbits, g.nactive, win))
       kern::dedisperse_lds(fb_.data(), fb_.stride(), d_active_.data(), g.nactive, r_offT_.data(), ldo_, d0, ndm,
                            r_wmin_.data(), win, g.out_nsamps, out, out_stride, g.out_scale, g.nbits, g.bias, s);
     else
@@ -681,14 +669,13 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   nlev_ = std::min(std::max(p_.nharmonics, 0), kern::kMaxHarmLevels);
   if (p_.nharmonics > kern::kMaxHarmLevels)
     log_info("warning: nharmonics > 5 is capped at 5 (32 harmonics), as the reference kernel only writes 5 levels");
-  // A/B knobs: PSOUP_WHITEN_ROCFFT=1 whitens with rocFFT, PSOUP_PREPARE_MAX caps the whitening batch
+  // PSOUP_WHITEN_ROCFFT=1 whitens with rocFFT (the fallback FFT path)
   const char* wr = std::getenv("PSOUP_WHITEN_ROCFFT");
   wh_ = std::make_unique<Whitener>(n_, p_.tsamp, stream_, p_.fft_mode == 2 && !(wr && std::atoi(wr) == 1));
   {
     // whitening batch: up to 3 GB of per-trial whitening state (>= 1 trial)
     const uint64_t per = wh_->batch_bytes_per_trial() + n_ * 4 + (p_.fft_mode == 2 ? n_ * 4 + 4096 : 0);
     max_prep_ = per ? static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(64, (3ull << 30) / per))) : 1;
-    if (const char* pm = std::getenv("PSOUP_PREPARE_MAX")) max_prep_ = std::max(1, std::min(max_prep_, std::atoi(pm)));
   }
   tim_.resize(n_);
   wstats_.resize(4 * static_cast<uint64_t>(max_prep_));
@@ -723,20 +710,12 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
       hp_.start[h] = hp_.end[h] = 0;
     }
   }
-  // Fused pass B (kFft4FusedR2c): writes the normalised spectrum itself, in
-  // the blocked layout, for the whole spectrum.  The unfused path prunes its
-  // stores to bins < hi_ instead, which moves fewer bytes only when under
-  // ~8% of the spectrum is searched (few harmonics, low max_freq).
-  fused_ = mode_ == 2 && kern::fft4_fused_r2c_ok(f4_) && static_cast<uint64_t>(hi_) >= nb_ / 8;
-  if (const char* e = std::getenv("PSOUP_FUSED_R2C")) fused_ = fused_ && std::atoi(e) != 0;
-  if (fused_) {
-    // blocked spectra Pb_ -> p_unblock -> natural spectra P_ (offset 3: aligned pieces)
-    pl_ = kern::fft4_p_layout(f4_);
-    pst_ = (n_ / 2 + 4 + 7) / 8 * 8;
-  } else {
-    pl_ = kern::PLayout{};
-    pst_ = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
-  }
+  // normalised spectra: bins below the search limit only (pass B prunes
+  // its stores to the bins the r2c kernel reads for them).  (A pass B fused
+  // with r2c + interbin + normalise was measured in round 3 and lost: the
+  // harmonic sum reads its blocked layout at 2.1x the cost,
+  // profiles/r3_fused/SUMMARY.md.)
+  pst_ = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
   // batch size
   {
     // auto budget: capped by the device's free memory shared among its engines
@@ -744,7 +723,7 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
       budget = std::min(budget, free_b / 10 * 7 / static_cast<size_t>(std::max(1, p_.engines_per_device)));
-    const size_t per = n_ * 4 + (fused_ ? pst_ * 4 : nb_ * 8) + pst_ * 4;  // Y/res + X/spec or Pb + P per trial
+    const size_t per = n_ * 4 + nb_ * 8 + pst_ * 4;  // Y/res + X/spec + P per trial
     // at most 512 trials per batch from 2^23 samples up, 256 below (the
     // shorter series were only measured up to 256)
     const size_t kmax = n_ >= (uint64_t(1) << 23) ? 512 : 256;
@@ -770,11 +749,9 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     sub_auto = std::min(K_ / 2, cap);
   }
   sub_ = mode_ != 2 ? 0 : p_.sub_batch >= 0 ? p_.sub_batch : sub_auto;
-  if (const char* e = std::getenv("PSOUP_SUB_PHASE")) phase_ = std::atoi(e) & 15;
   if (sub_ >= K_) sub_ = 0;
   {
-    int ns = std::max(2, p_.sub_streams);
-    if (const char* e = std::getenv("PSOUP_SUB_STREAMS")) ns = std::max(2, std::atoi(e));
+    const int ns = std::max(2, p_.sub_streams);
     for (int i = 1; i < ns; ++i) {
       aux_.push_back(std::make_unique<Stream>());
       joins_.push_back(std::make_unique<Event>());
@@ -851,10 +828,7 @@ void SearchEngine::ensure_batch_buffers(int k) {
     }
   const uint64_t rs = mode_ == 2 ? 2 * f4_.ystride : n_;  // floats per trial
   res_.resize(static_cast<uint64_t>(k) * rs);
-  if (fused_)
-    Pb_.resize(static_cast<uint64_t>(k) * pst_);
-  else
-    spec_.resize(static_cast<uint64_t>(k) * xs_);
+  spec_.resize(static_cast<uint64_t>(k) * xs_);
   P_.resize(static_cast<uint64_t>(k) * pst_);
 }
 
@@ -879,16 +853,8 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
       mode_ == 2 ? kern::fft4_x_layout(f4_) : kern::Fft4XLayout{ilog2(n_ / 2), n_ / 2, 8, 3, false};
   PSOUP_HIP_CHECK(hipMemsetAsync(s.d_count.data(), 0, sizeof(uint32_t), stream_));
   // Trials [b, b + c) of the batch: spectrum, power spectrum, harmonic peaks.
-  // stage gates of the sub-batch pipeline (PSOUP_SUB_PHASE): stage s of
-  // sub-batch j waits for stage s of sub-batch j - 1 (on the other stream)
-  auto gate_in = [&](int stage, int j, hipStream_t st) {
-    if ((phase_ >> stage & 1) && j > 0) PSOUP_HIP_CHECK(hipStreamWaitEvent(st, phase_ev_[stage].get(), 0));
-  };
-  auto gate_out = [&](int stage, hipStream_t st) {
-    if (phase_ >> stage & 1) phase_ev_[stage].record(st);
-  };
-  auto run = [&](int b, int c, hipStream_t st, int j) {
-    float* P = P_.data() + static_cast<uint64_t>(b) * pst + (fused_ ? 3 : 0);  // natural spectra
+  auto run = [&](int b, int c, hipStream_t st) {
+    float* P = P_.data() + static_cast<uint64_t>(b) * pst;
     if (mode_ == 2) {
       // res_ holds the four-step intermediates Y (complex, ystride per trial)
       float2* Y = reinterpret_cast<float2*>(res_.data()) + static_cast<uint64_t>(b) * f4_.ystride;
@@ -899,33 +865,17 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
       g.in_tstride = n_;
       g.pad_tstride = f4_.insize;
       g.tsrc = src;
-      gate_in(0, j, st);
       kern::fft4_resample_colpass(tim_.data(), f4_in_.data(), n_, af_.data() + first + b, c, Y, g, f4_tab_.data(),
                                   st);
-      gate_out(0, st);
-      gate_in(1, j, st);
-      if (fused_) {
-        // pass B + r2c + interbin + normalise in one kernel (blocked layout
-        // pl_), then the blocked -> natural transpose the harmonic sum reads
-        float* Pb = Pb_.data() + static_cast<uint64_t>(b) * pst;
-        kern::fft4_rowpass_r2c(Y, Pb, pst, c, f4_, f4_tab_.data(), wstats_.data(), static_cast<float>(n_), src,
-                               static_cast<uint64_t>(hi_), st);
-        gate_out(1, st);
-        gate_in(2, j, st);
-        kern::p_unblock(Pb, P - 3, pst, c, pl_, static_cast<uint64_t>(hi_), st);
-      } else {
-        float2* X = spec_.data() + static_cast<uint64_t>(b) * xs_;
-        kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st, static_cast<uint64_t>(hi_));
-        gate_out(1, st);
-        gate_in(2, j, st);
-        if (xl.tiled)
-          kern::r2c_interbin_normalise_tiled(X, f4_.n1, f4_.n2, xs_, P, pst, c, static_cast<uint64_t>(hi_),
-                                             wstats_.data(), static_cast<float>(n_), st, src);
-        else
-          kern::r2c_interbin_normalise_batch(X, n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch, xl.log2_blk,
-                                             P, pst, c, static_cast<uint64_t>(hi_), wstats_.data(),
-                                             static_cast<float>(n_), st, src);
-      }
+      float2* X = spec_.data() + static_cast<uint64_t>(b) * xs_;
+      kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st, static_cast<uint64_t>(hi_));
+      if (xl.tiled)
+        kern::r2c_interbin_normalise_tiled(X, f4_.n1, f4_.n2, xs_, P, pst, c, static_cast<uint64_t>(hi_),
+                                           wstats_.data(), static_cast<float>(n_), st, src);
+      else
+        kern::r2c_interbin_normalise_batch(X, n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch, xl.log2_blk, P,
+                                           pst, c, static_cast<uint64_t>(hi_), wstats_.data(),
+                                           static_cast<float>(n_), st, src);
     } else {
       kern::resample_batch(cur_tim_, n_, res_.data(), n_, af_.data() + first, c, st);
       batch_plan(c).execute(res_.data(), spec_.data(), st);
@@ -937,13 +887,10 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
         kern::interbin_normalise_batch(spec_.data(), nb_, nb_, P, pst, c, static_cast<uint64_t>(hi_),
                                        cur_stats_, static_cast<float>(n_), st);
     }
-    gate_out(2, st);
     RoctxRange r("Harmonic summing");
     kern::HarmParams hp = hp_;
     hp.trial_base = static_cast<uint32_t>(b);
-    gate_in(3, j, st);
     kern::harmonic_peaks_batch(P, nb_, pst, c, hp, s.d_peaks.data(), s.d_count.data(), st);
-    gate_out(3, st);
   };
   if (sub_ > 0 && count > sub_) {
     // Sub-batch pipeline: consecutive sub-batches alternate between two
@@ -954,13 +901,13 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
     for (auto& a : aux_) PSOUP_HIP_CHECK(hipStreamWaitEvent(a->get(), fork_.get(), 0));
     const int ns = static_cast<int>(aux_.size()) + 1;
     for (int b = 0, j = 0; b < count; b += sub_, ++j)
-      run(b, std::min(sub_, count - b), j % ns == 0 ? stream_ : aux_[static_cast<size_t>(j % ns - 1)]->get(), j);
+      run(b, std::min(sub_, count - b), j % ns == 0 ? stream_ : aux_[static_cast<size_t>(j % ns - 1)]->get());
     for (size_t i = 0; i < aux_.size(); ++i) {
       joins_[i]->record(aux_[i]->get());
       PSOUP_HIP_CHECK(hipStreamWaitEvent(stream_, joins_[i]->get(), 0));
     }
   } else {
-    run(0, count, stream_, 0);
+    run(0, count, stream_);
   }
   if (gpu_cluster_) {
     // cluster on the device: only cluster peaks (and the rare over-capacity
@@ -987,7 +934,6 @@ void SearchEngine::process_slot(Slot& s, int first, int count, uint32_t npeaks,
                                 std::vector<CandidateList>& out_by_job) {
   const uint32_t cnt = std::min(npeaks, cap_);
   ctr_.peaks += cnt;
-  const int L = nlev_ + 1;
   const int nseg = count * 8;
   seg_count_.assign(static_cast<size_t>(nseg) + 1, 0);
   for (uint32_t i = 0; i < cnt; ++i) {
@@ -1174,15 +1120,11 @@ CandidateList SearchEngine::search_prepared(int b, float dm, int dm_idx, const s
 
 int SearchEngine::batch_for(int ntr) const {
   // Short trial lists (one DM at 2^23: 685 trials) keep at least min_batches
-  // (default 8, env PSOUP_MIN_BATCHES) batches in the two-slot pipeline so
+  // (SearchParams::min_batches, default 8) batches in the two-slot pipeline so
   // host clustering still overlaps the GPU, but never fall below k_small_
   // (the batch an eighth of the budget gives: 64 at 2^23 with the default
   // 48 GiB, rounded like K_).
-  static const int env_min_batches = [] {
-    const char* e = std::getenv("PSOUP_MIN_BATCHES");
-    return e ? std::max(1, std::atoi(e)) : 0;
-  }();
-  const int min_batches = env_min_batches > 0 ? env_min_batches : std::max(1, p_.min_batches);
+  const int min_batches = std::max(1, p_.min_batches);
   if (p_.accel_batch <= 0 && ntr < min_batches * K_) {
     const int even = (ntr + min_batches - 1) / min_batches;
     return std::min(K_, std::max(k_small_, (even + 7) / 8 * 8));
@@ -1302,7 +1244,7 @@ std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(
   std::deque<int> inflight;  // slot indices
   int next = 0, slot = 0;
   // Short trial lists (one DM at 2^23: 685 trials) keep at least min_batches
-  // (default 8, env PSOUP_MIN_BATCHES) batches in the two-slot pipeline so
+  // (SearchParams::min_batches, default 8) batches in the two-slot pipeline so
   // host clustering still overlaps the GPU, but never fall below k_small_
   // (the batch an eighth of the budget gives: 64 at 2^23 with the default
   // 48 GiB, rounded like K_).

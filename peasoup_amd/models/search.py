@@ -62,7 +62,6 @@ class SearchResult:
     fold_stats: dict = field(default_factory=dict)
 
 
-_SYNC_DEDISP = os.environ.get("PSOUP_SYNC_DEDISP", "0") == "1"  # debug: no dedispersion/search overlap
 _BLOCK_TRACE = os.environ.get("PSOUP_BLOCK_TRACE", "")  # diagnostics: per-block host timeline (JSON lines)
 
 
@@ -279,8 +278,6 @@ class RankSearcher:
             with roctx_range("Dedisperse"):
                 self.dedisperser.run(d0, d1, buf.data_ptr(), self.row_stride, self.kernel, side.handle)
             ready.record(side.handle)
-            if _SYNC_DEDISP:
-                ready.synchronize()
             return j, ck, None, (k, buf, ready, start)
 
         dd_events = []

@@ -14,9 +14,7 @@ from .core import (  # noqa: F401
     convert_pad,
     dedisperse,
     deredden,
-    fft4_fused_ok,
     fft4_resample_interbin,
-    fft4_resample_interbin_fused,
     fft4_resample_spectrum,
     fold_optimise,
     fold_series,
@@ -29,8 +27,6 @@ from .core import (  # noqa: F401
     irfft,
     median_scrunch5,
     normalise,
-    p_to_layout,
-    p_unblock,
     r2c_interbin_normalise,
     resample,
     resample_v1,

@@ -280,68 +280,6 @@ def fft4_resample_interbin(x: torch.Tensor, accels: Sequence[float], tsamp: floa
     return P
 
 
-def fft4_fused_ok(n: int) -> bool:
-    """True if the fused pass B (kFft4FusedR2c) runs for N = n-point series
-    under the current kernel flags."""
-    g = K.fft4_geometry(n // 2)
-    return bool(g.ok) and K.fft4_fused_r2c_ok(g)
-
-
-def fft4_resample_interbin_fused(x: torch.Tensor, accels: Sequence[float], tsamp: float, stats: torch.Tensor,
-                                 nscale: float, nbins_out: int | None = None, blocked: bool = False):
-    """The search hot path with the fused pass B: resample + pass A, then
-    pass B + real-FFT post-processing + interbin + normalise in one kernel
-    (fft4_rowpass_r2c).  Returns P [K, N/2 + 1] in natural order, or with
-    ``blocked`` the raw [K, pstride] spectra in the kernel's blocked layout
-    plus that layout (``fft4_p_layout``)."""
-    _check(x, torch.float32, "x")
-    n = x.numel()
-    M = n // 2
-    g = K.fft4_geometry(M)
-    if not (g.ok and K.fft4_fused_r2c_ok(g)):
-        raise ValueError(f"fused pass B unsupported for n={n} under flags {K.fft4_flags()}")
-    tab = torch.from_numpy(K.fft4_tables(g)).to(x.device)
-    af = _accel_factors(accels, tsamp, x.device)
-    Kb = len(accels)
-    xp = torch.empty(g.insize, dtype=torch.float32, device=x.device)
-    Y = torch.empty((Kb, g.ystride, 2), dtype=torch.float32, device=x.device)
-    K.fft4_pad_input(x.data_ptr(), n, xp.data_ptr(), g, _s())
-    K.fft4_resample_colpass(x.data_ptr(), xp.data_ptr(), n, af.data_ptr(), Kb, Y.data_ptr(), g, tab.data_ptr(), _s())
-    pst = (M + 4 + 7) // 8 * 8
-    Pb = torch.zeros((Kb, pst), dtype=torch.float32, device=x.device)
-    nbo = M + 1 if nbins_out is None else int(nbins_out)
-    K.fft4_rowpass_r2c(Y.data_ptr(), Pb.data_ptr(), pst, Kb, g, tab.data_ptr(), stats.data_ptr(), float(nscale), nbo,
-                       _s())
-    lay = K.fft4_p_layout(g)
-    if blocked:
-        return Pb, lay
-    P = torch.zeros((Kb, pst), dtype=torch.float32, device=x.device)
-    K.p_relayout(Pb.data_ptr(), P.data_ptr(), pst, Kb, lay, 1, _s())
-    return P[:, :M + 1].contiguous()
-
-
-def p_unblock(Pb: torch.Tensor, layout, nbins_out: int = 0) -> torch.Tensor:
-    """The search engine's blocked -> natural transpose (p_unblock kernel):
-    [K, pstride] blocked spectra -> [K, M + 1] natural."""
-    _check(Pb, torch.float32, "Pb")
-    Kb, pst = Pb.shape
-    out = torch.zeros((Kb, pst), dtype=torch.float32, device=Pb.device)
-    K.p_unblock(Pb.data_ptr(), out.data_ptr(), pst, Kb, layout, int(nbins_out), _s())
-    return out[:, 3:3 + layout.M + 1]
-
-
-def p_to_layout(P: torch.Tensor, layout) -> torch.Tensor:
-    """Natural-order spectra P [K, M + 1] -> [K, pstride] in ``layout``."""
-    _check(P, torch.float32, "P")
-    Kb, nb = P.shape
-    pst = (nb + 7) // 8 * 8
-    src = torch.zeros((Kb, pst), dtype=torch.float32, device=P.device)
-    src[:, :nb] = P
-    out = torch.zeros_like(src)
-    K.p_relayout(src.data_ptr(), out.data_ptr(), pst, Kb, layout, 0, _s())
-    return out
-
-
 def resample_v1(x: torch.Tensor, accel: float, tsamp: float) -> torch.Tensor:
     _check(x, torch.float32, "x")
     af = (float(torch.tensor(accel, dtype=torch.float32)) * float(torch.tensor(tsamp, dtype=torch.float32))) / (2 * 299792458.0)
@@ -359,23 +297,21 @@ def harmonic_sums(P: torch.Tensor, nlevels: int) -> torch.Tensor:
 
 
 def harmonic_peaks(P: torch.Tensor, nlevels: int, starts: Sequence[int], ends: Sequence[int], thresh: float,
-                   capacity: int = 1 << 20, layout=None, nbins: int | None = None):
+                   capacity: int = 1 << 20, nbins: int | None = None):
     """Fused harmonic sum + threshold: P [K, n] -> records (trial, level, idx, snr)
     as int64/float32 tensors sorted by (trial, level, idx) (the kernel's chunk
-    descriptors, kernels.hpp kPeakChunk, are dropped).  ``layout``: P's
-    rows are spectra of ``nbins`` bins in that PLayout (the fused pass B's
-    blocked layout) instead of natural order."""
+    descriptors, kernels.hpp kPeakChunk, are dropped).  ``nbins``: bins per
+    spectrum when the rows are padded (default n)."""
     _check(P, torch.float32, "P")
     Kb, n = P.shape
     rec = torch.empty((capacity, 3), dtype=torch.int32, device=P.device)
     cnt = torch.zeros(1, dtype=torch.int32, device=P.device)
     nb = n if nbins is None else int(nbins)
-    lay = K.PLayout() if layout is None else layout
     K.harmonic_peaks_batch(P.data_ptr(), nb, n, Kb, nlevels, list(starts), list(ends), float(thresh), capacity,
-                           rec.data_ptr(), cnt.data_ptr(), _s(), lay)
+                           rec.data_ptr(), cnt.data_ptr(), _s())
     c = int(cnt.item())
     if c > capacity:
-        return harmonic_peaks(P, nlevels, starts, ends, thresh, capacity=c + 1024, layout=layout, nbins=nbins)
+        return harmonic_peaks(P, nlevels, starts, ends, thresh, capacity=c + 1024, nbins=nbins)
     r = rec[:c]
     r = r[r[:, 0] >= 0]  # drop the chunk descriptors (seg field with kPeakChunk, bit 31, set)
     seg = r[:, 0].to(torch.int64)

@@ -19,4 +19,13 @@ import json
 for l in open('$O/c4single.jsonl'):
     d=json.loads(l); print('single', d['config'], d['timers_s'])
 "
+timeout -k 10 600 python3 tools/baseline_configs.py --configs 5 --log2n 23 --workdir /tmp/cfg23 --out $O/c5_23.jsonl > $O/c5_23.log 2>&1 || { echo C5_23_FAIL; tail -20 $O/c5_23.log; exit 1; }
+cut -c1-300 $O/c5_23.jsonl
+for i in 1 2 3 4 5; do
+  timeout -k 10 120 ./bin/peasoup -i tests/data/tutorial.fil -o $O/golden_native_$i --dm_end 250 --acc_start -5 --acc_end 5 -n 4 --npdmp 10 > $O/golden_native_$i.log 2>&1 || { echo GOLDEN_NATIVE_FAIL; tail -20 $O/golden_native_$i.log; exit 1; }
+done
+for i in 1 2 3 4 5; do
+  timeout -k 10 180 python -u -m peasoup_amd -i tests/data/tutorial.fil -o $O/golden_py_$i --dm_end 250 --acc_start -5 --acc_end 5 -n 4 --npdmp 10 > $O/golden_py_$i.log 2>&1 || { echo GOLDEN_PY_FAIL; tail -20 $O/golden_py_$i.log; exit 1; }
+done
+for f in $O/golden_native_*/overview.xml $O/golden_py_*/overview.xml; do echo $f; grep -A6 "<execution_times>" $f | grep -v execution_times | tr -s ' ' | paste -sd' '; done
 echo DONE
