@@ -409,6 +409,11 @@ class SearchEngine {
   DeviceBuffer<float> res_;
   DeviceBuffer<float2> spec_;
   DeviceBuffer<float> P_;
+  // screening bytes of P_ (dev::q8) for the screened harmonic sum: written by
+  // the tiled r2c kernel (fft_mode 2); harmonic flag 4 turns the screen off
+  bool q8_ = false;
+  uint64_t qst_ = 0;  // bytes per trial of Q_ (>= hi_, multiple of 64)
+  DeviceBuffer<uint8_t> Q_;
   DeviceBuffer<double> af_;
   std::vector<double> af_host_;
   std::map<int, std::unique_ptr<FftPlan>> plans_;

@@ -190,9 +190,11 @@ void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride,
 // bin k = k2 + n2*k1 at X[k2/8][k1/8][k2%8][k1%8]; 64-byte loads per thread.
 // tsrc (device, optional): trial k normalises with stats + 4*tsrc[k] (batches
 // mixing trials of several prepared series).
+// With Q, also the screening bytes dev::q8(P) of every stored bin (row k at
+// Q + k*qstride, qstride >= nbins_out) for harmonic_peaks_batch's screen.
 void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstride, float* P, uint64_t pstride,
                                   int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s,
-                                  const uint32_t* tsrc = nullptr);
+                                  const uint32_t* tsrc = nullptr, uint8_t* Q = nullptr, uint64_t qstride = 0);
 
 // Fused resample + four-step FFT (fft4step.hip).  M = N/2 = n1*n2 with
 // n1, n2 powers of two in [128, 4096], n2 <= n1 <= 2 n2.  Intermediates use
@@ -321,8 +323,18 @@ struct HarmParams {
 // Fused incoherent harmonic sum + threshold + compaction: never writes the
 // summed spectra.  Records land unordered; count may exceed capacity (then
 // the caller re-runs with a bigger buffer).
+// With Q (the screening bytes of P, row k at Q + k*qstride, qstride >= the
+// highest searched bin, 16-byte aligned rows) the sums are screened on Q:
+// integer sums of the staged bytes (a quarter of P's gather traffic) against
+// per-level integer bounds that no bin whose fp32 sum passes the pre-threshold
+// can miss; only the bins that pass (or touch a saturated byte) are summed
+// exactly from P.  Records are identical either way.
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
-                          PeakRecord* out, uint32_t* count, hipStream_t s);
+                          PeakRecord* out, uint32_t* count, hipStream_t s, const uint8_t* Q = nullptr,
+                          uint64_t qstride = 0);
+// Q[k*qstride + i] = dev::q8(P[k*pstride + i]), i < n (tests and tools; the
+// search writes Q from the r2c kernel).
+void quantize_q8(const float* P, uint64_t pstride, uint64_t n, int K, uint8_t* Q, uint64_t qstride, hipStream_t s);
 // Peak clustering on the device (peakcluster.hip; peakfinder.hpp:24-55):
 // the records of harmonic_peaks_batch (first min(*d_count, cap)) -- chunks
 // of idx-ascending crossings, each behind its descriptor record (seg field
@@ -366,7 +378,11 @@ constexpr uint32_t kHarmCap = 4096;
 constexpr uint32_t kHarmHost = 0x80000000u;
 void harm_distill_batch(const uint2* d_clust, const uint2* d_segtab, int ntrials, const HarmDistillParams& p,
                         uint2* d_out, uint2* d_ttab, uint32_t* d_total, hipStream_t s);
-// Tuning: bit 0 = XCD-per-trial block order (default on).
+// Harmonic-sum switches (process-wide; default 1 | 32 | 10 << 8): bit 0 =
+// XCD-per-trial block order; bit 1 = pre-threshold off (tests); bit 2 = the
+// search engine's screened sum off (engines built afterwards); bit 5 = the
+// fp32 3-level kernel in two staging phases; bits 8-15 = that kernel's
+// dynamic-LDS occupancy cap in KiB.
 void harmonic_set_flags(int flags);
 int harmonic_flags();
 // Debug/test: materialise level-h sums [nlevels][nbins] for one spectrum.

@@ -165,6 +165,17 @@ __device__ __forceinline__ float2 r2c_combine(float2 za, float2 zb, float c, flo
   return make_float2(__builtin_fmaf(-s, oy, __builtin_fmaf(c, ox, ex)), __builtin_fmaf(s, ox, __builtin_fmaf(c, oy, ey)));
 }
 
+// Screening byte of a normalised spectrum value for the harmonic sum's
+// integer pre-screen (harmsum.hip): u = clamp(rint(4 p) + 128, 0, 255), so
+// (u - 128) / 4 is within 1/8 of p for u < 255.  u = 255 (p >= 31.625, or
+// NaN) makes the screen take the exact path; u = 0 (p <= -31.875) gives a
+// screen value above p, which only makes the screen more conservative.
+__device__ __forceinline__ uint8_t q8(float p) {
+  const float v = rintf(p * 4.0f) + 128.0f;
+  if (!(v < 255.0f)) return 255;  // also NaN
+  return v <= 0.0f ? 0 : static_cast<uint8_t>(v);
+}
+
 }  // namespace dev
 }  // namespace kern
 }  // namespace psoup

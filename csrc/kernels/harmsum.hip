@@ -16,6 +16,7 @@
 #include "device_common.hpp"
 #include "psoup/kernels.hpp"
 
+#include <climits>
 #include <cmath>
 #include <type_traits>
 
@@ -164,94 +165,6 @@ struct RowTw8 {
   float c[8], s[8];
 };
 
-__global__ void __launch_bounds__(256) r2c_interbin_tiled_kernel(const float2* __restrict__ Z, int log2_n2,
-                                                                 uint64_t n1, uint64_t zstride,
-                                                                 float* __restrict__ P, uint64_t pstride,
-                                                                 uint64_t nbins_out, const float* __restrict__ stats,
-                                                                 float nscale, RowTw8 rtw,
-                                                                 const uint32_t* __restrict__ tsrc) {
-  __shared__ float2 A[8][258];  // A[r][u] = X[(g0+r)*n2 + c0 - 1 + u]
-  __shared__ float2 D[8][258];  // D[r][u] = X[M - ((g0+r)*n2 + c0 - 1 + u)]
-  const uint64_t n2 = uint64_t(1) << log2_n2;
-  const uint64_t M = n1 * n2, half = M / 2;
-  const float invM = 1.0f / static_cast<float>(M);  // M a power of two: x * invM == x / M exactly
-  const int kk = blockIdx.z;
-  const int t = threadIdx.x;
-  const float2* z = Z + static_cast<uint64_t>(kk) * zstride;
-  float* p = P + static_cast<uint64_t>(kk) * pstride;
-  if (tsrc) stats += 4 * tsrc[kk];  // multi-series batch: this trial's whitening stats
-  const float mean = stats[0] * nscale;
-  const float sigma = stats[2] * nscale;
-  const float rsig = 1.0f / sigma;  // one division per thread; per bin dev::div_rn
-  const uint64_t g0 = static_cast<uint64_t>(blockIdx.y) * 8;
-  const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * 256;
-  auto xbin = [&](uint64_t k, float2& xa, float2& xm) {  // generic: X[k] and X[M-k]
-    const float2 za = z[taddr(k & (M - 1), log2_n2, n1)];
-    const float2 zb = z[taddr((M - k) & (M - 1), log2_n2, n1)];
-    float sn, cs;
-    sincospif(-static_cast<float>(k) * invM, &sn, &cs);
-    xa = r2c_combine(za, zb, cs, sn);
-    xm = r2c_combine(zb, za, -cs, sn);
-  };
-  const uint64_t k2 = c0 + t;
-  if (k2 == 0) {
-    // column 0 pairs row k1 with row n1 - k1 (not n1 - 1 - k1)
-#pragma unroll
-    for (int r = 0; r < 8; ++r) xbin((g0 + r) * n2, A[r][t + 1], D[r][t + 1]);
-  } else {
-    const float4* sa = reinterpret_cast<const float4*>(z + (k2 >> 3) * (8 * n1) + (g0 >> 3) * 64 + (k2 & 7) * 8);
-    const uint64_t m2 = n2 - k2, m1 = n1 - 8 - g0;  // mirror column, first mirror row (rows reversed)
-    const float4* sb = reinterpret_cast<const float4*>(z + (m2 >> 3) * (8 * n1) + (m1 >> 3) * 64 + (m2 & 7) * 8);
-    float2 za[8], zb[8];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float4 a = sa[u], b = sb[u];
-      za[2 * u] = make_float2(a.x, a.y);
-      za[2 * u + 1] = make_float2(a.z, a.w);
-      zb[7 - 2 * u] = make_float2(b.x, b.y);
-      zb[6 - 2 * u] = make_float2(b.z, b.w);
-    }
-    float sn, cs;
-    sincospif(-static_cast<float>(g0 * n2 + k2) * invM, &sn, &cs);
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const float ws = rtw.s[r], wc = rtw.c[r];  // W^(r n2)
-      const float c = __builtin_fmaf(cs, wc, -(sn * ws)), sv = __builtin_fmaf(cs, ws, sn * wc);
-      A[r][t + 1] = r2c_combine(za[r], zb[r], c, sv);
-      D[r][t + 1] = r2c_combine(zb[r], za[r], -c, sv);
-    }
-  }
-  if (t < 8) {  // halos: column c0-1 (ascending neighbour) and c0+256 (mirror neighbour) of row t
-    const uint64_t row = (g0 + t) * n2 + c0;
-    float2 xa, xm;
-    if (row > 0) {
-      xbin(row - 1, xa, xm);
-      A[t][0] = xa;
-    } else {
-      A[t][0] = make_float2(0.f, 0.f);
-    }
-    xbin(row + 256, xa, xm);
-    D[t][257] = xm;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 8; ++r) {
-    const uint64_t k = (g0 + r) * n2 + k2;
-    if (k < nbins_out) {
-      const float2 xl = k > 0 ? A[r][t] : make_float2(0.f, 0.f);
-      p[k] = dev::div_rn(dev::interbin(A[r][t + 1], xl) - mean, sigma, rsig);
-    }
-    const uint64_t j = M - k;  // > M/2 for every k in the ascending rows
-    if (j < nbins_out) p[j] = dev::div_rn(dev::interbin(D[r][t + 1], D[r][t + 2]) - mean, sigma, rsig);
-  }
-  if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && half < nbins_out) {  // bin M/2 (row n1/2, column 0)
-    float2 xa, xm, la, lm;
-    xbin(half, xa, xm);
-    xbin(half - 1, la, lm);
-    p[half] = dev::div_rn(dev::interbin(xa, la) - mean, sigma, rsig);
-  }
-}
-
 // The whitener's half spectrum X[0..M] from the tiled four-step output: the
 // tile of r2c_interbin_tiled_kernel (8 rows x 256 columns, 64 contiguous
 // bytes per lane and mirror) without the interbin step, so every load is a
@@ -337,15 +250,17 @@ __global__ void __launch_bounds__(256) c2r_post_tiled_kernel(const float2* __res
   }
 }
 
-// Same tile, neighbours by cross-lane shuffles instead of two 16.5 KiB LDS
-// planes: lane l's left neighbour X[k-1] is lane l-1's ascending bin and its
-// mirror neighbour X[M-(k+1)] is lane l+1's mirrored bin; only the values
-// crossing a wave edge (and the tile's two halo columns) go through 640 bytes
-// of LDS.  Occupancy is then set by registers, not LDS (4 -> 8 workgroups/CU).
+// The search's r2c + interbin + normalise on that tile.  Interbin
+// neighbours come by cross-lane shuffles: lane l's left neighbour X[k-1] is
+// lane l-1's ascending bin and its mirror neighbour X[M-(k+1)] is lane l+1's
+// mirrored bin; only the values crossing a wave edge (and the tile's two halo
+// columns) go through 640 bytes of LDS, so occupancy is set by registers
+// (8 workgroups/CU; two 16.5 KiB LDS planes held it to 4).  With Q, the
+// harmonic sum's screening bytes dev::q8(P) are stored alongside P.
 __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
     const float2* __restrict__ Z, int log2_n2, uint64_t n1, uint64_t zstride, float* __restrict__ P,
     uint64_t pstride, uint64_t nbins_out, const float* __restrict__ stats, float nscale, RowTw8 rtw,
-    const uint32_t* __restrict__ tsrc) {
+    const uint32_t* __restrict__ tsrc, uint8_t* __restrict__ Q, uint64_t qstride) {
   __shared__ float2 eA[5][8];  // eA[w][r]: X left of wave w's lane 0 (w = 0: the tile's halo column c0 - 1)
   __shared__ float2 eD[5][8];  // eD[w][r]: mirror X of wave w's lane 0 (w = 4: the halo column c0 + 256)
   const uint64_t n2 = uint64_t(1) << log2_n2;
@@ -355,12 +270,17 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const float2* z = Z + static_cast<uint64_t>(kk) * zstride;
   float* p = P + static_cast<uint64_t>(kk) * pstride;
+  uint8_t* q = Q ? Q + static_cast<uint64_t>(kk) * qstride : nullptr;
   if (tsrc) stats += 4 * tsrc[kk];
   const float mean = stats[0] * nscale;
   const float sigma = stats[2] * nscale;
   const float rsig = 1.0f / sigma;  // one division per thread; per bin dev::div_rn
   const uint64_t g0 = static_cast<uint64_t>(blockIdx.y) * 8;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * 256;
+  auto put = [&](uint64_t k, float v) {
+    p[k] = v;
+    if (q) q[k] = dev::q8(v);
+  };
   auto xbin = [&](uint64_t k, float2& xa, float2& xm) {  // generic: X[k] and X[M-k]
     const float2 za = z[taddr(k & (M - 1), log2_n2, n1)];
     const float2 zb = z[taddr((M - k) & (M - 1), log2_n2, n1)];
@@ -427,16 +347,16 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
     const uint64_t k = (g0 + r) * n2 + k2;
     if (k < nbins_out) {
       if (k == 0) xl = make_float2(0.f, 0.f);
-      p[k] = dev::div_rn(dev::interbin(xa[r], xl) - mean, sigma, rsig);
+      put(k, dev::div_rn(dev::interbin(xa[r], xl) - mean, sigma, rsig));
     }
     const uint64_t j = M - k;
-    if (j < nbins_out) p[j] = dev::div_rn(dev::interbin(xm[r], xr) - mean, sigma, rsig);
+    if (j < nbins_out) put(j, dev::div_rn(dev::interbin(xm[r], xr) - mean, sigma, rsig));
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && t == 0 && half < nbins_out) {  // bin M/2 (row n1/2, column 0)
     float2 ha, hm, la, lm;
     xbin(half, ha, hm);
     xbin(half - 1, la, lm);
-    p[half] = dev::div_rn(dev::interbin(ha, la) - mean, sigma, rsig);
+    put(half, dev::div_rn(dev::interbin(ha, la) - mean, sigma, rsig));
   }
 }
 
@@ -563,14 +483,8 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
   const int last = hi - 1;
   // ---- fundamental straight into registers (coalesced)
   float fund[Tl::BPT];
-  if (xcd_trials & 2) {  // tuning: streaming (nontemporal) fundamental loads
 #pragma unroll
-    for (int u = 0; u < Tl::BPT; ++u)
-      fund[u] = __builtin_nontemporal_load(p + min(b0 + t + 256 * u, last));
-  } else {
-#pragma unroll
-    for (int u = 0; u < Tl::BPT; ++u) fund[u] = p[min(b0 + t + 256 * u, last)];
-  }
+  for (int u = 0; u < Tl::BPT; ++u) fund[u] = p[min(b0 + t + 256 * u, last)];
   // ---- stage every gather range in 16-byte chunks: all loads are issued
   // before the first LDS store (fixed trip counts).  Only values at indices
   // < hi are ever used; chunks reaching past `last` are gathered per element.
@@ -871,6 +785,243 @@ __global__ void __launch_bounds__(256) harmonic_peaks2_kernel(const float* __res
   }
 }
 
+// Screened harmonic sum (harmonic_peaks_batch with Q).  The tile stages
+// the gather ranges of the screening bytes (dev::q8) instead of P: 16 bins
+// per 16-byte load, a quarter of the bytes.  Each level's integer sum of
+// bytes s_h is compared with lim[h], chosen on the host so that an fp32 sum
+// above the pre-threshold lo[h] always gives s_h > lim[h]: every unsaturated
+// byte is within 1/8 of its bin, (s_h - 128 * 2^h) / 4 + 2^h / 8 + 0.25 bounds
+// the fp32 sum (0.25 covers its rounding), lim = floor(4 (lo - 2^h / 8 -
+// 0.25) + 128 * 2^h) - 1.  A bin whose sums pass, or whose terms include a
+// saturated byte (255), is summed again exactly from P in the reference order:
+// the same values and records as harmonic_peaks_kernel.
+template <int NLEV, int BPT>
+struct HarmTileQ {
+  static constexpr int B = 256 * BPT;
+  static constexpr int NREG = 1 << NLEV;
+  static constexpr int maxlen(int h, int m) { return (((B - 1) * m) >> h) + 2; }
+  // 16-byte chunks staged per range, from the 16-byte boundary at or below its first bin
+  static constexpr int chunks(int h, int m) { return (maxlen(h, m) + 30) / 16; }
+  static constexpr int region(int h, int m) { return (1 << (h - 1)) + (m - 1) / 2; }
+  static constexpr int offset(int r) {  // bytes, a multiple of 16
+    int off = 0;
+    for (int h = 1; h <= NLEV; ++h)
+      for (int m = 1; m < (1 << h); m += 2) {
+        if (region(h, m) == r) return off;
+        off += 16 * chunks(h, m);
+      }
+    return off;
+  }
+  static constexpr int TOTAL = offset(NREG) > 0 ? offset(NREG) : 16;
+  static constexpr int iters() {
+    int n = 0;
+    for (int h = 1; h <= NLEV; ++h)
+      for (int m = 1; m < (1 << h); m += 2) n += (chunks(h, m) + 255) / 256;
+    return n;
+  }
+  static constexpr int ITERS = iters() > 0 ? iters() : 1;
+};
+
+struct HarmLim {
+  int v[6];
+};
+
+// 16 screening bytes a .. a+15 of row q; bytes past `last` repeat byte `last`
+// (they only feed bins at or beyond the end of the search range)
+__device__ __forceinline__ uint4 load_q16(const uint8_t* __restrict__ q, int a, int last) {
+  if (a + 15 <= last) return *reinterpret_cast<const uint4*>(q + a);
+  uint32_t w[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v |= static_cast<uint32_t>(q[min(a + 4 * j + e, last)]) << (8 * e);
+    w[j] = v;
+  }
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <int NLEV, int BPT>
+__global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __restrict__ P, uint64_t pstride,
+                                                                const uint8_t* __restrict__ Q, uint64_t qstride,
+                                                                int lo, int hi, HarmParams hp,
+                                                                PeakRecord* __restrict__ out,
+                                                                uint32_t* __restrict__ count, int ntiles,
+                                                                int xcd_trials, HarmLim lim) {
+  using Tl = HarmTileQ<NLEV, BPT>;
+  constexpr int B = Tl::B;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[Tl::TOTAL];
+  const uint32_t bid = blockIdx.x;
+  int k, tile;
+  if (xcd_trials & 1) {
+    const uint32_t slot = bid >> 3;
+    k = static_cast<int>((slot / ntiles) * 8 + (bid & 7u));
+    tile = static_cast<int>(slot % ntiles);
+  } else {
+    k = static_cast<int>(bid / ntiles);
+    tile = static_cast<int>(bid % ntiles);
+  }
+  const float* p = P + static_cast<uint64_t>(k) * pstride;
+  const uint8_t* q = Q + static_cast<uint64_t>(k) * qstride;
+  const int t = threadIdx.x;
+  const int b0 = lo + tile * B;
+  const int last = hi - 1;
+  int fund[BPT];
+#pragma unroll
+  for (int u = 0; u < BPT; ++u) fund[u] = q[min(b0 + t + 256 * u, last)];
+  {
+    uint4 tmp[Tl::ITERS];
+    int it = 0;
+#pragma unroll
+    for (int h = 1; h <= NLEV; ++h) {
+#pragma unroll
+      for (int m = 1; m < (1 << h); m += 2) {
+        const int r0 = ((b0 * m + (1 << (h - 1))) >> h) & ~15;
+#pragma unroll
+        for (int e = 0; e < (Tl::chunks(h, m) + 255) / 256; ++e, ++it)
+          tmp[it] = load_q16(q, r0 + 16 * (t + 256 * e), last);
+      }
+    }
+    it = 0;
+#pragma unroll
+    for (int h = 1; h <= NLEV; ++h) {
+#pragma unroll
+      for (int m = 1; m < (1 << h); m += 2) {
+        uint4* dst = reinterpret_cast<uint4*>(lds + Tl::offset(Tl::region(h, m)));
+#pragma unroll
+        for (int e = 0; e < (Tl::chunks(h, m) + 255) / 256; ++e, ++it)
+          if (t + 256 * e < Tl::chunks(h, m)) dst[t + 256 * e] = tmp[it];
+      }
+    }
+  }
+  __syncthreads();
+  const float thr = hp.thresh;
+  const uint32_t seg0 = (static_cast<uint32_t>(k) + hp.trial_base) * 8u;
+  bool inner = true;  // block-uniform: the whole tile lies inside every level's search range
+#pragma unroll
+  for (int h = 0; h <= NLEV; ++h) inner = inner & (b0 >= hp.start[h]) & (b0 + B <= hp.end[h]);
+  const int i0 = b0 + t;
+  // byte offset in LDS of term (h, m) of bin i0; bin i0 + 256 u adds u * (m << (8 - h))
+#define PS_QBASE(h, m) \
+  (Tl::offset(Tl::region(h, m)) + (((i0 * (m) + (1 << ((h) - 1))) >> (h)) - (((b0 * (m) + (1 << ((h) - 1))) >> (h)) & ~15)))
+  int base[Tl::NREG];
+  if constexpr (NLEV >= 1) base[1] = PS_QBASE(1, 1);
+  if constexpr (NLEV >= 2) {
+    base[2] = PS_QBASE(2, 1);
+    base[3] = PS_QBASE(2, 3);
+  }
+  if constexpr (NLEV >= 3) {
+#pragma unroll
+    for (int m = 1; m < 8; m += 2) base[4 + m / 2] = PS_QBASE(3, m);
+  }
+  if constexpr (NLEV >= 4) {
+#pragma unroll
+    for (int m = 1; m < 16; m += 2) base[8 + m / 2] = PS_QBASE(4, m);
+  }
+  if constexpr (NLEV >= 5) {
+#pragma unroll
+    for (int m = 1; m < 32; m += 2) base[16 + m / 2] = PS_QBASE(5, m);
+  }
+#undef PS_QBASE
+#pragma unroll
+  for (int u = 0; u < BPT; ++u) {
+    const int i = i0 + u * 256;
+    int sq = fund[u], mx = sq;
+    bool cand = sq > lim.v[0];
+#define PS_QTERM(h, m)                                                                  \
+  {                                                                                     \
+    const int v = lds[base[(1 << ((h) - 1)) + (m) / 2] + u * ((m) << (8 - (h)))];       \
+    sq += v;                                                                            \
+    mx = max(mx, v);                                                                    \
+  }
+    if constexpr (NLEV >= 1) {
+      PS_QTERM(1, 1)
+      cand = cand | (sq > lim.v[1]);
+    }
+    if constexpr (NLEV >= 2) {
+      PS_QTERM(2, 3)
+      PS_QTERM(2, 1)
+      cand = cand | (sq > lim.v[2]);
+    }
+    if constexpr (NLEV >= 3) {
+#pragma unroll
+      for (int m = 1; m < 8; m += 2) PS_QTERM(3, m)
+      cand = cand | (sq > lim.v[3]);
+    }
+    if constexpr (NLEV >= 4) {
+#pragma unroll
+      for (int m = 1; m < 16; m += 2) PS_QTERM(4, m)
+      cand = cand | (sq > lim.v[4]);
+    }
+    if constexpr (NLEV >= 5) {
+#pragma unroll
+      for (int m = 1; m < 32; m += 2) PS_QTERM(5, m)
+      cand = cand | (sq > lim.v[5]);
+    }
+#undef PS_QTERM
+    cand = (cand | (mx >= 255)) & (i < hi);
+    if (__ballot(cand) == 0ull) continue;  // the usual no-peak case
+    bool pred[NLEV + 1];
+    float o[NLEV + 1];
+#pragma unroll
+    for (int h = 0; h <= NLEV; ++h) {
+      pred[h] = false;
+      o[h] = 0.f;
+    }
+    if (cand) {
+      // exact: the fp32 sums of P in the reference order (harmonic_peaks_kernel)
+      float val = p[i];
+      float sum[NLEV + 1];
+      sum[0] = val;
+      if constexpr (NLEV >= 1) {
+        val += p[(i + 1) >> 1];
+        sum[1] = val;
+      }
+      if constexpr (NLEV >= 2) {
+        val += p[(i * 3 + 2) >> 2];  // reference order: 3/4 before 1/4
+        val += p[(i + 2) >> 2];
+        sum[2] = val;
+      }
+      if constexpr (NLEV >= 3) {
+#pragma unroll
+        for (int m = 1; m < 8; m += 2) val += p[(i * m + 4) >> 3];
+        sum[3] = val;
+      }
+      if constexpr (NLEV >= 4) {
+#pragma unroll
+        for (int m = 1; m < 16; m += 2) val += p[(i * m + 8) >> 4];
+        sum[4] = val;
+      }
+      if constexpr (NLEV >= 5) {
+#pragma unroll
+        for (int m = 1; m < 32; m += 2) val += p[(i * m + 16) >> 5];
+        sum[5] = val;
+      }
+#pragma unroll
+      for (int h = 0; h <= NLEV; ++h) {
+        if (h == 2)
+          o[h] = sum[h] * 0.5f;
+        else if (h == 4)
+          o[h] = sum[h] * 0.25f;
+        else
+          o[h] = h == 0 ? sum[0] : static_cast<float>(static_cast<double>(sum[h]) * c_level_scale[h]);
+        const bool in_range = inner | ((i >= hp.start[h]) & (i < hp.end[h]));
+        pred[h] = in_range & (o[h] > thr);
+      }
+    }
+    emit_levels<NLEV + 1>(pred, 0, NLEV, seg0, i, o, out, count, hp.capacity);
+  }
+}
+
+__global__ void __launch_bounds__(256) quantize_q8_kernel(const float* __restrict__ P, uint64_t pstride, uint64_t n,
+                                                          uint8_t* __restrict__ Q, uint64_t qstride) {
+  const float* p = P + blockIdx.y * pstride;
+  uint8_t* q = Q + blockIdx.y * qstride;
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    q[i] = dev::q8(p[i]);
+}
+
 __global__ void __launch_bounds__(256) harmonic_sums_kernel(const float* __restrict__ p, uint64_t nbins,
                                                             int nlevels, float* __restrict__ out) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
@@ -1039,7 +1190,7 @@ void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride,
 
 void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstride, float* P, uint64_t pstride,
                                   int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s,
-                                  const uint32_t* tsrc) {
+                                  const uint32_t* tsrc, uint8_t* Q, uint64_t qstride) {
   PSOUP_CHECK(K >= 1 && K <= 65535, "bad batch");
   PSOUP_CHECK(n1 >= 16 && n2 >= 256 && (n1 & (n1 - 1)) == 0 && (n2 & (n2 - 1)) == 0, "r2c tiled: bad geometry");
   PSOUP_CHECK(nbins_out <= static_cast<uint64_t>(n1) * n2 + 1, "nbins_out beyond the spectrum");
@@ -1055,15 +1206,10 @@ void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstr
     rtw.c[r] = static_cast<float>(std::cos(a));
     rtw.s[r] = static_cast<float>(std::sin(a));
   }
-  // tuning (harmonic_set_flags bits 16-23): extra dynamic LDS in KiB per workgroup caps workgroups per CU
-  const size_t dyn_lds = static_cast<size_t>((g_harm_flags >> 16) & 0xff) * 1024;
-  if (g_harm_flags & 16)  // tuning: the LDS-plane form (4 workgroups/CU)
-    r2c_interbin_tiled_kernel<<<grid, 256, dyn_lds, s>>>(X, lg, static_cast<uint64_t>(n1), xstride, P, pstride,
-                                                         nbins_out, stats, nscale, rtw, tsrc);
-  else
-    r2c_interbin_tiled_shfl_kernel<<<grid, 256, dyn_lds, s>>>(X, lg, static_cast<uint64_t>(n1), xstride, P, pstride,
-                                                              nbins_out, stats, nscale, rtw, tsrc);
-  post_launch_check("r2c_interbin_tiled_kernel", s);
+  PSOUP_CHECK(!Q || qstride >= nbins_out, "r2c tiled: screening row too short");
+  r2c_interbin_tiled_shfl_kernel<<<grid, 256, 0, s>>>(X, lg, static_cast<uint64_t>(n1), xstride, P, pstride, nbins_out,
+                                                      stats, nscale, rtw, tsrc, Q, qstride);
+  post_launch_check("r2c_interbin_tiled_shfl_kernel", s);
 }
 
 void mixed_gather(const float* src, uint64_t n, uint32_t m, uint64_t p, int mode, float2* dst, hipStream_t s) {
@@ -1137,8 +1283,16 @@ void harmonic_set_flags(int flags) {
 }
 int harmonic_flags() { return g_harm_flags; }
 
+void quantize_q8(const float* P, uint64_t pstride, uint64_t n, int K, uint8_t* Q, uint64_t qstride, hipStream_t s) {
+  PSOUP_CHECK(K >= 1 && K <= 65535 && qstride >= n, "quantize_q8: bad shape");
+  if (n == 0) return;
+  quantize_q8_kernel<<<dim3(dev::grid_for(n, 256, 1024), static_cast<unsigned>(K)), 256, 0, s>>>(P, pstride, n, Q,
+                                                                                                 qstride);
+  post_launch_check("quantize_q8_kernel", s);
+}
+
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
-                          PeakRecord* out, uint32_t* count, hipStream_t s) {
+                          PeakRecord* out, uint32_t* count, hipStream_t s, const uint8_t* Q, uint64_t qstride) {
   PSOUP_CHECK(hp.nlevels >= 0 && hp.nlevels <= kMaxHarmLevels, "nlevels out of range");
   PSOUP_CHECK(nbins < (1ull << 31), "spectrum too long for int32 indices");
   int lo = static_cast<int>(nbins), hi = 0;
@@ -1152,7 +1306,7 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
   PSOUP_CHECK((static_cast<uint64_t>(K) + hp.trial_base) * 8 <= 65536, "chunk descriptors hold 16-bit segments");
   if (hi <= lo) return;
   PSOUP_CHECK(static_cast<int64_t>(hi) * 32 < (int64_t(1) << 31), "spectrum too long for the int32 gather math");
-  const int xcd = ((g_harm_flags & 1) && (K % 8 == 0) ? 1 : 0) | ((g_harm_flags & 4) ? 2 : 0);
+  const int xcd = (g_harm_flags & 1) && (K % 8 == 0) ? 1 : 0;
   // bits 8-15: dynamic LDS occupancy cap, measured for (and applied to) the
   // two-phase 3-level kernel only (the other kernels keep their full occupancy)
   const size_t dyn_lds2 = static_cast<size_t>((g_harm_flags >> 8) & 0xff) * 1024;
@@ -1171,6 +1325,33 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
     }
   }
   auto ntiles_of = [&](int B) { return (hi - lo + B - 1) / B; };
+  if (Q) {
+    PSOUP_CHECK((reinterpret_cast<uintptr_t>(Q) & 15) == 0 && qstride % 16 == 0 && qstride >= static_cast<uint64_t>(hi),
+                "harmonic_peaks_batch: screening rows must be 16-byte aligned and cover the search range");
+    HarmLim lim;
+    for (int h = 0; h < 6; ++h) {
+      const double n = std::ldexp(1.0, h);
+      const double x = 4.0 * (static_cast<double>(pre.lo[h]) - n / 8.0 - 0.25) + 128.0 * n;
+      lim.v[h] = std::isfinite(x) ? static_cast<int>(std::floor(x)) - 1 : INT_MIN;
+    }
+    auto oneq = [&](auto nl_c) {
+      constexpr int NL = decltype(nl_c)::value, BP = NL <= 3 ? 8 : 4;
+      const int nt = ntiles_of(HarmTileQ<NL, BP>::B);
+      PSOUP_CHECK(static_cast<int64_t>(nt) * K < (int64_t(1) << 31), "harmonic grid too large");
+      harmonic_peaks_q8_kernel<NL, BP><<<dim3(static_cast<unsigned>(nt * K)), 256, 0, s>>>(
+          P, pstride, Q, qstride, lo, hi, hp, out, count, nt, xcd, lim);
+    };
+    switch (hp.nlevels) {
+      case 0: oneq(std::integral_constant<int, 0>{}); break;
+      case 1: oneq(std::integral_constant<int, 1>{}); break;
+      case 2: oneq(std::integral_constant<int, 2>{}); break;
+      case 3: oneq(std::integral_constant<int, 3>{}); break;
+      case 4: oneq(std::integral_constant<int, 4>{}); break;
+      default: oneq(std::integral_constant<int, 5>{}); break;
+    }
+    post_launch_check("harmonic_peaks_q8_kernel", s);
+    return;
+  }
   auto one = [&](auto nl_c, auto bp_c) {
     constexpr int NL = decltype(nl_c)::value, BP = decltype(bp_c)::value;
     const int nt = ntiles_of(HarmTile<NL, BP>::B);
@@ -1189,8 +1370,6 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
         PSOUP_CHECK(static_cast<int64_t>(nt) * K < (int64_t(1) << 31), "harmonic grid too large");
         harmonic_peaks2_kernel<3><<<dim3(static_cast<unsigned>(nt * K)), 256, dyn_lds2, s>>>(P, pstride, lo, hi, hp,
                                                                                            out, count, nt, xcd, pre);
-      } else if (g_harm_flags & 8) {  // tuning: 1024-bin tiles (half the LDS and registers per workgroup)
-        one(std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{});
       } else {
         one(std::integral_constant<int, 3>{}, I{});
       }

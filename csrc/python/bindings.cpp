@@ -543,12 +543,17 @@ PYBIND11_MODULE(_C, m) {
     kern::Fft4XLayout l = kern::fft4_x_layout(g);
     return py::make_tuple(l.log2_row, l.row_pitch, l.blk_pitch, l.log2_blk, l.tiled);
   });
-  k.def("r2c_interbin_normalise_tiled", [](uintptr_t X, int n1, int n2, uint64_t xstride, uintptr_t Pout,
-                                           uint64_t pstride, int K, uint64_t nbo, uintptr_t stats, float nscale,
-                                           uintptr_t s) {
-    kern::r2c_interbin_normalise_tiled(P<const float2>(X), n1, n2, xstride, P<float>(Pout), pstride, K, nbo,
-                                       P<const float>(stats), nscale, S(s));
-  });
+  k.def(
+      "r2c_interbin_normalise_tiled",
+      [](uintptr_t X, int n1, int n2, uint64_t xstride, uintptr_t Pout, uint64_t pstride, int K, uint64_t nbo,
+         uintptr_t stats, float nscale, uintptr_t s, uintptr_t q, uint64_t qstride) {
+        kern::r2c_interbin_normalise_tiled(P<const float2>(X), n1, n2, xstride, P<float>(Pout), pstride, K, nbo,
+                                           P<const float>(stats), nscale, S(s), nullptr, P<uint8_t>(q), qstride);
+      },
+      py::arg("X"), py::arg("n1"), py::arg("n2"), py::arg("xstride"), py::arg("P"), py::arg("pstride"), py::arg("K"),
+      py::arg("nbo"), py::arg("stats"), py::arg("nscale"), py::arg("s"), py::arg("q") = 0, py::arg("qstride") = 0);
+  k.def("quantize_q8", [](uintptr_t Pin, uint64_t pstride, uint64_t n, int K, uintptr_t q, uint64_t qstride,
+                          uintptr_t s) { kern::quantize_q8(P<const float>(Pin), pstride, n, K, P<uint8_t>(q), qstride, S(s)); });
   py::class_<kern::Fft4Geom>(k, "Fft4Geom")
       .def_readonly("ok", &kern::Fft4Geom::ok)
       .def_readonly("n1", &kern::Fft4Geom::n1)
@@ -589,7 +594,8 @@ PYBIND11_MODULE(_C, m) {
   k.def("r2c_tiled_row_blocks", &kern::r2c_tiled_row_blocks);
   k.def("harmonic_peaks_batch", [](uintptr_t Pin, uint64_t nb, uint64_t pstride, int K, int nlevels,
                                    const std::vector<int>& start, const std::vector<int>& end, float thresh,
-                                   uint32_t capacity, uintptr_t out, uintptr_t count, uintptr_t s) {
+                                   uint32_t capacity, uintptr_t out, uintptr_t count, uintptr_t s, uintptr_t q,
+                                   uint64_t qstride) {
     kern::HarmParams hp{};
     hp.nlevels = nlevels;
     for (int i = 0; i < 6; ++i) {
@@ -599,9 +605,10 @@ PYBIND11_MODULE(_C, m) {
     hp.thresh = thresh;
     hp.capacity = capacity;
     kern::harmonic_peaks_batch(P<const float>(Pin), nb, pstride, K, hp, P<kern::PeakRecord>(out), P<uint32_t>(count),
-                               S(s));
+                               S(s), P<const uint8_t>(q), qstride);
   }, py::arg("P"), py::arg("nb"), py::arg("pstride"), py::arg("K"), py::arg("nlevels"), py::arg("start"),
-     py::arg("end"), py::arg("thresh"), py::arg("capacity"), py::arg("out"), py::arg("count"), py::arg("s"));
+     py::arg("end"), py::arg("thresh"), py::arg("capacity"), py::arg("out"), py::arg("count"), py::arg("s"),
+     py::arg("q") = 0, py::arg("qstride") = 0);
   k.def("peak_cluster_batch", [](uintptr_t peaks, uintptr_t count, uint32_t cap, uint32_t nseg, int gap,
                                  uintptr_t work, uintptr_t sorted, uintptr_t out, uintptr_t segtab, uintptr_t total,
                                  uintptr_t s) {

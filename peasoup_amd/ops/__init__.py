@@ -27,6 +27,7 @@ from .core import (  # noqa: F401
     irfft,
     median_scrunch5,
     normalise,
+    quantize_q8,
     r2c_interbin_normalise,
     resample,
     resample_v1,

@@ -259,21 +259,30 @@ def fft4_resample_spectrum(x: torch.Tensor, accels: Sequence[float], tsamp: floa
 
 
 def fft4_resample_interbin(x: torch.Tensor, accels: Sequence[float], tsamp: float, stats: torch.Tensor,
-                           nscale: float, nbins_out: int | None = None) -> torch.Tensor:
+                           nscale: float, nbins_out: int | None = None, screen: bool = False):
     """The search hot path of fft_mode 2: fused resample + four-step FFT, then
     the paired real-FFT post-processing + interbin + normalise on the fused
     FFT's spectrum layout.  Returns P [K, N/2 + 1]; with ``nbins_out`` only
     bins below it are formed (pass B then stores only the spectrum rows the
-    r2c step reads, as the search engine does) and the rest stay zero."""
+    r2c step reads, as the search engine does) and the rest stay zero.  With
+    ``screen`` (tiled layout only) returns (P, Q): Q [K, qstride] uint8 the
+    screening bytes the r2c kernel writes for the harmonic sum."""
     M = (x.numel()) // 2
     nbo = M + 1 if nbins_out is None else int(nbins_out)
     g, X = _fft4_padded(x, accels, tsamp, nbins_out=0 if nbins_out is None else nbo)
     Kb = X.shape[0]
     log2_row, row, blk, lw, tiled = fft4_x_layout(g)
     P = torch.zeros((Kb, M + 1), dtype=torch.float32, device=x.device)
+    if screen and not tiled:
+        raise ValueError("screening bytes come from the tiled r2c kernel only")
     if tiled:
+        qst = (M + 1 + 63) // 64 * 64
+        Q = torch.zeros((Kb, qst), dtype=torch.uint8, device=x.device) if screen else None
         K.r2c_interbin_normalise_tiled(X.data_ptr(), g.n1, g.n2, g.xstride, P.data_ptr(), M + 1, Kb, nbo,
-                                       stats.data_ptr(), float(nscale), _s())
+                                       stats.data_ptr(), float(nscale), _s(), Q.data_ptr() if screen else 0,
+                                       qst if screen else 0)
+        if screen:
+            return P, Q
     else:
         K.r2c_interbin_normalise_batch(X.data_ptr(), M, g.xstride, log2_row, row, blk, lw, P.data_ptr(), M + 1, Kb,
                                        nbo, stats.data_ptr(), float(nscale), _s())
@@ -296,22 +305,39 @@ def harmonic_sums(P: torch.Tensor, nlevels: int) -> torch.Tensor:
     return out[:nlevels]
 
 
+def quantize_q8(P: torch.Tensor) -> torch.Tensor:
+    """Screening bytes (device_common.hpp dev::q8) of spectra P [K, n]:
+    [K, qstride] uint8, qstride = n rounded up to 64."""
+    _check(P, torch.float32, "P")
+    Kb, n = P.shape
+    qst = (n + 63) // 64 * 64
+    Q = torch.zeros((Kb, qst), dtype=torch.uint8, device=P.device)
+    K.quantize_q8(P.data_ptr(), n, n, Kb, Q.data_ptr(), qst, _s())
+    return Q
+
+
 def harmonic_peaks(P: torch.Tensor, nlevels: int, starts: Sequence[int], ends: Sequence[int], thresh: float,
-                   capacity: int = 1 << 20, nbins: int | None = None):
+                   capacity: int = 1 << 20, nbins: int | None = None, Q: torch.Tensor | None = None):
     """Fused harmonic sum + threshold: P [K, n] -> records (trial, level, idx, snr)
     as int64/float32 tensors sorted by (trial, level, idx) (the kernel's chunk
     descriptors, kernels.hpp kPeakChunk, are dropped).  ``nbins``: bins per
-    spectrum when the rows are padded (default n)."""
+    spectrum when the rows are padded (default n).  ``Q``: screening bytes of
+    P ([K, qstride] uint8, ``quantize_q8``) -- the screened kernel, same
+    records."""
     _check(P, torch.float32, "P")
     Kb, n = P.shape
     rec = torch.empty((capacity, 3), dtype=torch.int32, device=P.device)
     cnt = torch.zeros(1, dtype=torch.int32, device=P.device)
     nb = n if nbins is None else int(nbins)
+    if Q is not None:
+        if Q.dtype != torch.uint8 or Q.shape[0] != Kb or not Q.is_contiguous():
+            raise ValueError("Q must be a contiguous [K, qstride] uint8 tensor")
     K.harmonic_peaks_batch(P.data_ptr(), nb, n, Kb, nlevels, list(starts), list(ends), float(thresh), capacity,
-                           rec.data_ptr(), cnt.data_ptr(), _s())
+                           rec.data_ptr(), cnt.data_ptr(), _s(), 0 if Q is None else Q.data_ptr(),
+                           0 if Q is None else Q.shape[1])
     c = int(cnt.item())
     if c > capacity:
-        return harmonic_peaks(P, nlevels, starts, ends, thresh, capacity=c + 1024, nbins=nbins)
+        return harmonic_peaks(P, nlevels, starts, ends, thresh, capacity=c + 1024, nbins=nbins, Q=Q)
     r = rec[:c]
     r = r[r[:, 0] >= 0]  # drop the chunk descriptors (seg field with kPeakChunk, bit 31, set)
     seg = r[:, 0].to(torch.int64)

@@ -2,8 +2,8 @@
 """Peak-clustering kernels on RFI-like segments: nseg segments of ~n
 threshold crossings each (dense runs around periodic spikes plus scattered
 noise crossings), records shuffled like the harmonic kernel's atomics emit
-them.  Prints the time of kern::peak_cluster_batch (the phase cut
-PSOUP_CLUSTER_STOP selects, for timing experiments)."""
+them.  Prints the time of kern::peak_cluster_batch and, with --trace, the
+large kernel's per-phase shader-clock times."""
 import argparse
 import os
 import sys
