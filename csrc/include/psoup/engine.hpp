@@ -412,6 +412,10 @@ class SearchEngine {
   // screening bytes of P_ (dev::q8) for the screened harmonic sum: written by
   // the tiled r2c kernel (fft_mode 2); harmonic flag 4 turns the screen off
   bool q8_ = false;
+  // harmonic flag 8: P_ is not written; the screen's exact sums recompute
+  // their bins from spec_ (kern::HarmFromX)
+  bool fromx_ = false;
+  const float2* rt_ = nullptr;  // kern::r2c_twiddle_table(n_ / 2)
   uint64_t qst_ = 0;  // bytes per trial of Q_ (>= hi_, multiple of 64)
   DeviceBuffer<uint8_t> Q_;
   DeviceBuffer<double> af_;

@@ -191,10 +191,18 @@ void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride,
 // tsrc (device, optional): trial k normalises with stats + 4*tsrc[k] (batches
 // mixing trials of several prepared series).
 // With Q, also the screening bytes dev::q8(P) of every stored bin (row k at
-// Q + k*qstride, qstride >= nbins_out) for harmonic_peaks_batch's screen.
+// Q + k*qstride, qstride >= nbins_out) for harmonic_peaks_batch's screen; P
+// may then be null (Q only).  Twiddles from rt = r2c_twiddle_table(n1 * n2)
+// (nullptr: looked up): every bin's value depends on X and its index alone,
+// so the screened harmonic sum can recompute any bin exactly (HarmFromX).
 void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstride, float* P, uint64_t pstride,
                                   int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s,
-                                  const uint32_t* tsrc = nullptr, uint8_t* Q = nullptr, uint64_t qstride = 0);
+                                  const uint32_t* tsrc = nullptr, uint8_t* Q = nullptr, uint64_t qstride = 0,
+                                  const float2* rt = nullptr);
+// Device table of e^{-i pi k / M} (k = 2048 a + b: [b < 2048] then
+// [a <= M/2 >> 11]) on the current device, built on first use (synchronous
+// copy) and cached for the process.
+const float2* r2c_twiddle_table(uint64_t M);
 
 // Fused resample + four-step FFT (fft4step.hip).  M = N/2 = n1*n2 with
 // n1, n2 powers of two in [128, 4096], n2 <= n1 <= 2 n2.  Intermediates use
@@ -329,9 +337,22 @@ struct HarmParams {
 // per-level integer bounds that no bin whose fp32 sum passes the pre-threshold
 // can miss; only the bins that pass (or touch a saturated byte) are summed
 // exactly from P.  Records are identical either way.
+// With fx (and Q) the exact sums recompute their bins from the tiled
+// spectrum X exactly as r2c_interbin_normalise_tiled forms them, so P need
+// not be written at all (P is then ignored).
+struct HarmFromX {
+  const float2* X = nullptr;  // tiled pass-B spectra, trial k at X + k*xstride
+  uint64_t xstride = 0;
+  int log2_n2 = 0;
+  uint32_t n1 = 0;
+  const float2* rt = nullptr;       // r2c_twiddle_table(n1 << log2_n2)
+  const float* stats = nullptr;     // whitening stats (mean at [0], sigma at [2]) per series
+  const uint32_t* tsrc = nullptr;   // series of trial k (stats + 4*tsrc[k]); nullptr: stats itself
+  float nscale = 1.f;
+};
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
                           PeakRecord* out, uint32_t* count, hipStream_t s, const uint8_t* Q = nullptr,
-                          uint64_t qstride = 0);
+                          uint64_t qstride = 0, const HarmFromX* fx = nullptr);
 // Q[k*qstride + i] = dev::q8(P[k*pstride + i]), i < n (tests and tools; the
 // search writes Q from the r2c kernel).
 void quantize_q8(const float* P, uint64_t pstride, uint64_t n, int K, uint8_t* Q, uint64_t qstride, hipStream_t s);
@@ -380,7 +401,8 @@ void harm_distill_batch(const uint2* d_clust, const uint2* d_segtab, int ntrials
                         uint2* d_out, uint2* d_ttab, uint32_t* d_total, hipStream_t s);
 // Harmonic-sum switches (process-wide; default 1 | 32 | 10 << 8): bit 0 =
 // XCD-per-trial block order; bit 1 = pre-threshold off (tests); bit 2 = the
-// search engine's screened sum off (engines built afterwards); bit 5 = the
+// search engine's screened sum off, bit 3 = its exact sums recomputed from
+// the spectrum with no P stored (engines built afterwards); bit 5 = the
 // fp32 3-level kernel in two staging phases; bits 8-15 = that kernel's
 // dynamic-LDS occupancy cap in KiB.
 void harmonic_set_flags(int flags);

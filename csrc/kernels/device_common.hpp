@@ -165,6 +165,16 @@ __device__ __forceinline__ float2 r2c_combine(float2 za, float2 zb, float c, flo
   return make_float2(__builtin_fmaf(-s, oy, __builtin_fmaf(c, ox, ex)), __builtin_fmaf(s, ox, __builtin_fmaf(c, oy, ey)));
 }
 
+// e^{-i pi k / M} for 0 <= k <= M/2 from the two-level table of
+// r2c_twiddle_table (harmsum.hip): rt[k & 2047] * rt[2048 + (k >> 11)], the
+// product with explicit FMAs, so every kernel that forms a spectrum bin gets
+// the same twiddle (the search's r2c and the screened harmonic sum's exact
+// path recompute bins independently and must agree to the bit).
+__device__ __forceinline__ float2 r2c_tw(const float2* __restrict__ rt, uint32_t k) {
+  const float2 l = rt[k & 2047u], h = rt[2048u + (k >> 11)];
+  return make_float2(__builtin_fmaf(h.x, l.x, -(h.y * l.y)), __builtin_fmaf(h.x, l.y, h.y * l.x));
+}
+
 // Screening byte of a normalised spectrum value for the harmonic sum's
 // integer pre-screen (harmsum.hip): u = clamp(rint(4 p) + 128, 0, 255), so
 // (u - 128) / 4 is within 1/8 of p for u < 255.  u = 255 (p >= 31.625, or

@@ -19,6 +19,9 @@
 #include <climits>
 #include <cmath>
 #include <type_traits>
+#include <vector>
+#include <mutex>
+#include <map>
 
 namespace psoup {
 namespace kern {
@@ -259,17 +262,16 @@ __global__ void __launch_bounds__(256) c2r_post_tiled_kernel(const float2* __res
 // harmonic sum's screening bytes dev::q8(P) are stored alongside P.
 __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
     const float2* __restrict__ Z, int log2_n2, uint64_t n1, uint64_t zstride, float* __restrict__ P,
-    uint64_t pstride, uint64_t nbins_out, const float* __restrict__ stats, float nscale, RowTw8 rtw,
-    const uint32_t* __restrict__ tsrc, uint8_t* __restrict__ Q, uint64_t qstride) {
+    uint64_t pstride, uint64_t nbins_out, const float* __restrict__ stats, float nscale,
+    const float2* __restrict__ rt, const uint32_t* __restrict__ tsrc, uint8_t* __restrict__ Q, uint64_t qstride) {
   __shared__ float2 eA[5][8];  // eA[w][r]: X left of wave w's lane 0 (w = 0: the tile's halo column c0 - 1)
   __shared__ float2 eD[5][8];  // eD[w][r]: mirror X of wave w's lane 0 (w = 4: the halo column c0 + 256)
   const uint64_t n2 = uint64_t(1) << log2_n2;
   const uint64_t M = n1 * n2, half = M / 2;
-  const float invM = 1.0f / static_cast<float>(M);  // M a power of two: x * invM == x / M exactly
   const int kk = blockIdx.z;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const float2* z = Z + static_cast<uint64_t>(kk) * zstride;
-  float* p = P + static_cast<uint64_t>(kk) * pstride;
+  float* p = P ? P + static_cast<uint64_t>(kk) * pstride : nullptr;
   uint8_t* q = Q ? Q + static_cast<uint64_t>(kk) * qstride : nullptr;
   if (tsrc) stats += 4 * tsrc[kk];
   const float mean = stats[0] * nscale;
@@ -278,16 +280,18 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
   const uint64_t g0 = static_cast<uint64_t>(blockIdx.y) * 8;
   const uint64_t c0 = static_cast<uint64_t>(blockIdx.x) * 256;
   auto put = [&](uint64_t k, float v) {
-    p[k] = v;
+    if (p) p[k] = v;
     if (q) q[k] = dev::q8(v);
   };
-  auto xbin = [&](uint64_t k, float2& xa, float2& xm) {  // generic: X[k] and X[M-k]
+  // every bin k <= M/2 with the table twiddle of k, its mirror M - k with
+  // (-c, s): each value is a function of Z and k alone (harmonic_peaks_q8_kernel
+  // recomputes bins the same way)
+  auto xbin = [&](uint64_t k, float2& xa, float2& xm) {  // generic: X[k] and X[M-k], k <= M/2
     const float2 za = z[taddr(k & (M - 1), log2_n2, n1)];
     const float2 zb = z[taddr((M - k) & (M - 1), log2_n2, n1)];
-    float sn, cs;
-    sincospif(-static_cast<float>(k) * invM, &sn, &cs);
-    xa = r2c_combine(za, zb, cs, sn);
-    xm = r2c_combine(zb, za, -cs, sn);
+    const float2 tw = dev::r2c_tw(rt, static_cast<uint32_t>(k));
+    xa = r2c_combine(za, zb, tw.x, tw.y);
+    xm = r2c_combine(zb, za, -tw.x, tw.y);
   };
   const uint64_t k2 = c0 + t;
   float2 xa[8], xm[8];
@@ -307,14 +311,11 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
       zb[7 - 2 * u] = make_float2(b.x, b.y);
       zb[6 - 2 * u] = make_float2(b.z, b.w);
     }
-    float sn, cs;
-    sincospif(-static_cast<float>(g0 * n2 + k2) * invM, &sn, &cs);
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      const float ws = rtw.s[r], wc = rtw.c[r];
-      const float c = __builtin_fmaf(cs, wc, -(sn * ws)), sv = __builtin_fmaf(cs, ws, sn * wc);
-      xa[r] = r2c_combine(za[r], zb[r], c, sv);
-      xm[r] = r2c_combine(zb[r], za[r], -c, sv);
+      const float2 tw = dev::r2c_tw(rt, static_cast<uint32_t>((g0 + r) * n2 + k2));
+      xa[r] = r2c_combine(za[r], zb[r], tw.x, tw.y);
+      xm[r] = r2c_combine(zb[r], za[r], -tw.x, tw.y);
     }
   }
   if (lane == 63) {
@@ -335,7 +336,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
       eA[0][t] = make_float2(0.f, 0.f);
     }
     xbin(row + 256, ha, hm);
-    eD[4][t] = hm;
+    eD[4][t] = row + 256 == half ? ha : hm;  // bin M/2 in its ascending form, as it is stored
   }
   __syncthreads();
 #pragma unroll
@@ -841,13 +842,25 @@ __device__ __forceinline__ uint4 load_q16(const uint8_t* __restrict__ q, int a, 
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-template <int NLEV, int BPT>
+// Bin b of trial spectrum z exactly as r2c_interbin_tiled_shfl_kernel stores
+// it (HarmFromX): X[b] from Z[b], Z[M-b] and the table twiddle of min(b, M-b)
+// (mirror form above M/2), interbinned with X[b-1], normalised.
+__device__ __forceinline__ float2 x_canon(const float2* __restrict__ z, uint32_t b, uint32_t M, int log2_n2,
+                                          uint32_t n1, const float2* __restrict__ rt) {
+  const float2 za = z[taddr(b & (M - 1), log2_n2, n1)];
+  const float2 zb = z[taddr((M - b) & (M - 1), log2_n2, n1)];
+  const bool up = b <= M / 2;
+  const float2 tw = dev::r2c_tw(rt, up ? b : M - b);
+  return r2c_combine(za, zb, up ? tw.x : -tw.x, tw.y);
+}
+
+template <int NLEV, int BPT, bool FROMX>
 __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __restrict__ P, uint64_t pstride,
                                                                 const uint8_t* __restrict__ Q, uint64_t qstride,
                                                                 int lo, int hi, HarmParams hp,
                                                                 PeakRecord* __restrict__ out,
                                                                 uint32_t* __restrict__ count, int ntiles,
-                                                                int xcd_trials, HarmLim lim) {
+                                                                int xcd_trials, HarmLim lim, HarmFromX fx) {
   using Tl = HarmTileQ<NLEV, BPT>;
   constexpr int B = Tl::B;
   __shared__ __attribute__((aligned(16))) uint8_t lds[Tl::TOTAL];
@@ -861,7 +874,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
     k = static_cast<int>(bid / ntiles);
     tile = static_cast<int>(bid % ntiles);
   }
-  const float* p = P + static_cast<uint64_t>(k) * pstride;
+  const float* p = FROMX ? nullptr : P + static_cast<uint64_t>(k) * pstride;
   const uint8_t* q = Q + static_cast<uint64_t>(k) * qstride;
   const int t = threadIdx.x;
   const int b0 = lo + tile * B;
@@ -923,6 +936,8 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
     for (int m = 1; m < 32; m += 2) base[16 + m / 2] = PS_QBASE(5, m);
   }
 #undef PS_QBASE
+  // screen: bit u of cm = bin i0 + 256 u must be summed exactly
+  uint32_t cm = 0;
 #pragma unroll
   for (int u = 0; u < BPT; ++u) {
     const int i = i0 + u * 256;
@@ -960,7 +975,36 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
     }
 #undef PS_QTERM
     cand = (cand | (mx >= 255)) & (i < hi);
-    if (__ballot(cand) == 0ull) continue;  // the usual no-peak case
+    cm |= cand ? (1u << u) : 0u;
+  }
+  if (__ballot(cm != 0u) == 0ull) return;  // the usual no-peak case: the whole wave is done
+  // exact sums, one bin group at a time (not unrolled: the exact path is rare)
+  const float2* z = nullptr;
+  float mean = 0.f, sigma = 1.f, rsig = 1.f;
+  uint32_t M = 0;
+  if constexpr (FROMX) {
+    z = fx.X + static_cast<uint64_t>(k) * fx.xstride;
+    const float* st = fx.tsrc ? fx.stats + 4 * fx.tsrc[k] : fx.stats;
+    mean = st[0] * fx.nscale;
+    sigma = st[2] * fx.nscale;
+    rsig = 1.0f / sigma;  // as the r2c kernel
+    M = fx.n1 << fx.log2_n2;
+  }
+  auto pv = [&](int b) -> float {
+    if constexpr (FROMX) {
+      const uint32_t ub = static_cast<uint32_t>(b);
+      const float2 x0 = x_canon(z, ub, M, fx.log2_n2, fx.n1, fx.rt);
+      const float2 xl = ub > 0 ? x_canon(z, ub - 1, M, fx.log2_n2, fx.n1, fx.rt) : make_float2(0.f, 0.f);
+      return dev::div_rn(dev::interbin(x0, xl) - mean, sigma, rsig);
+    } else {
+      return p[b];
+    }
+  };
+#pragma unroll 1
+  for (int u = 0; u < BPT; ++u) {
+    const bool cand = (cm >> u) & 1u;
+    if (__ballot(cand) == 0ull) continue;
+    const int i = i0 + u * 256;
     bool pred[NLEV + 1];
     float o[NLEV + 1];
 #pragma unroll
@@ -969,32 +1013,32 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
       o[h] = 0.f;
     }
     if (cand) {
-      // exact: the fp32 sums of P in the reference order (harmonic_peaks_kernel)
-      float val = p[i];
+      // the fp32 sums in the reference order (harmonic_peaks_kernel)
+      float val = pv(i);
       float sum[NLEV + 1];
       sum[0] = val;
       if constexpr (NLEV >= 1) {
-        val += p[(i + 1) >> 1];
+        val += pv((i + 1) >> 1);
         sum[1] = val;
       }
       if constexpr (NLEV >= 2) {
-        val += p[(i * 3 + 2) >> 2];  // reference order: 3/4 before 1/4
-        val += p[(i + 2) >> 2];
+        val += pv((i * 3 + 2) >> 2);  // reference order: 3/4 before 1/4
+        val += pv((i + 2) >> 2);
         sum[2] = val;
       }
       if constexpr (NLEV >= 3) {
 #pragma unroll
-        for (int m = 1; m < 8; m += 2) val += p[(i * m + 4) >> 3];
+        for (int m = 1; m < 8; m += 2) val += pv((i * m + 4) >> 3);
         sum[3] = val;
       }
       if constexpr (NLEV >= 4) {
 #pragma unroll
-        for (int m = 1; m < 16; m += 2) val += p[(i * m + 8) >> 4];
+        for (int m = 1; m < 16; m += 2) val += pv((i * m + 8) >> 4);
         sum[4] = val;
       }
       if constexpr (NLEV >= 5) {
 #pragma unroll
-        for (int m = 1; m < 32; m += 2) val += p[(i * m + 16) >> 5];
+        for (int m = 1; m < 32; m += 2) val += pv((i * m + 16) >> 5);
         sum[5] = val;
       }
 #pragma unroll
@@ -1188,9 +1232,34 @@ void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride,
   post_launch_check("r2c_interbin_normalise_batch_kernel", s);
 }
 
+const float2* r2c_twiddle_table(uint64_t M) {
+  PSOUP_CHECK(M >= 2 && (M & (M - 1)) == 0 && M <= (uint64_t(1) << 31), "r2c_twiddle_table: M " << M);
+  int dev = 0;
+  PSOUP_HIP_CHECK(hipGetDevice(&dev));
+  static std::mutex mu;
+  static std::map<std::pair<int, uint64_t>, float2*> cache;  // per device and length, kept for the process
+  std::lock_guard<std::mutex> lk(mu);
+  const auto key = std::make_pair(dev, M);
+  auto it = cache.find(key);
+  if (it != cache.end()) return it->second;
+  const uint64_t nh = ((M / 2) >> 11) + 1;
+  std::vector<float2> h(2048 + nh);
+  auto w = [M](double num) {
+    const double a = -M_PI * num / static_cast<double>(M);
+    return make_float2(static_cast<float>(std::cos(a)), static_cast<float>(std::sin(a)));
+  };
+  for (uint64_t j = 0; j < 2048; ++j) h[j] = w(static_cast<double>(j));
+  for (uint64_t a = 0; a < nh; ++a) h[2048 + a] = w(static_cast<double>(a << 11));
+  float2* d = nullptr;
+  PSOUP_HIP_CHECK(hipMalloc(&d, h.size() * sizeof(float2)));
+  PSOUP_HIP_CHECK(hipMemcpy(d, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice));
+  cache[key] = d;
+  return d;
+}
+
 void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstride, float* P, uint64_t pstride,
                                   int K, uint64_t nbins_out, const float* stats, float nscale, hipStream_t s,
-                                  const uint32_t* tsrc, uint8_t* Q, uint64_t qstride) {
+                                  const uint32_t* tsrc, uint8_t* Q, uint64_t qstride, const float2* rt) {
   PSOUP_CHECK(K >= 1 && K <= 65535, "bad batch");
   PSOUP_CHECK(n1 >= 16 && n2 >= 256 && (n1 & (n1 - 1)) == 0 && (n2 & (n2 - 1)) == 0, "r2c tiled: bad geometry");
   PSOUP_CHECK(nbins_out <= static_cast<uint64_t>(n1) * n2 + 1, "nbins_out beyond the spectrum");
@@ -1200,15 +1269,11 @@ void r2c_interbin_normalise_tiled(const float2* X, int n1, int n2, uint64_t xstr
   while ((1 << lg) < n2) ++lg;
   // row blocks beyond the last one holding a bin < nbins_out write nothing
   dim3 grid(static_cast<unsigned>(n2 / 256), r2c_tiled_row_blocks(nbins_out, n1, n2), static_cast<unsigned>(K));
-  RowTw8 rtw;
-  for (int r = 0; r < 8; ++r) {
-    const double a = -M_PI * r / static_cast<double>(n1);
-    rtw.c[r] = static_cast<float>(std::cos(a));
-    rtw.s[r] = static_cast<float>(std::sin(a));
-  }
+  if (!rt) rt = r2c_twiddle_table(static_cast<uint64_t>(n1) * n2);
+  PSOUP_CHECK(P || Q, "r2c tiled: no output");
   PSOUP_CHECK(!Q || qstride >= nbins_out, "r2c tiled: screening row too short");
   r2c_interbin_tiled_shfl_kernel<<<grid, 256, 0, s>>>(X, lg, static_cast<uint64_t>(n1), xstride, P, pstride, nbins_out,
-                                                      stats, nscale, rtw, tsrc, Q, qstride);
+                                                      stats, nscale, rt, tsrc, Q, qstride);
   post_launch_check("r2c_interbin_tiled_shfl_kernel", s);
 }
 
@@ -1292,7 +1357,8 @@ void quantize_q8(const float* P, uint64_t pstride, uint64_t n, int K, uint8_t* Q
 }
 
 void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int K, const HarmParams& hp,
-                          PeakRecord* out, uint32_t* count, hipStream_t s, const uint8_t* Q, uint64_t qstride) {
+                          PeakRecord* out, uint32_t* count, hipStream_t s, const uint8_t* Q, uint64_t qstride,
+                          const HarmFromX* fx) {
   PSOUP_CHECK(hp.nlevels >= 0 && hp.nlevels <= kMaxHarmLevels, "nlevels out of range");
   PSOUP_CHECK(nbins < (1ull << 31), "spectrum too long for int32 indices");
   int lo = static_cast<int>(nbins), hi = 0;
@@ -1334,12 +1400,24 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
       const double x = 4.0 * (static_cast<double>(pre.lo[h]) - n / 8.0 - 0.25) + 128.0 * n;
       lim.v[h] = std::isfinite(x) ? static_cast<int>(std::floor(x)) - 1 : INT_MIN;
     }
+    HarmFromX fxv;
+    if (fx) {
+      fxv = *fx;
+      const uint64_t M = static_cast<uint64_t>(fxv.n1) << fxv.log2_n2;
+      PSOUP_CHECK(fxv.X && fxv.rt && fxv.stats && fxv.n1 >= 16 && M < (uint64_t(1) << 31) &&
+                      static_cast<uint64_t>(hi) <= M + 1,
+                  "harmonic_peaks_batch: bad spectrum for the exact recompute");
+    }
     auto oneq = [&](auto nl_c) {
       constexpr int NL = decltype(nl_c)::value, BP = NL <= 3 ? 8 : 4;
       const int nt = ntiles_of(HarmTileQ<NL, BP>::B);
       PSOUP_CHECK(static_cast<int64_t>(nt) * K < (int64_t(1) << 31), "harmonic grid too large");
-      harmonic_peaks_q8_kernel<NL, BP><<<dim3(static_cast<unsigned>(nt * K)), 256, 0, s>>>(
-          P, pstride, Q, qstride, lo, hi, hp, out, count, nt, xcd, lim);
+      if (fx)
+        harmonic_peaks_q8_kernel<NL, BP, true><<<dim3(static_cast<unsigned>(nt * K)), 256, 0, s>>>(
+            P, pstride, Q, qstride, lo, hi, hp, out, count, nt, xcd, lim, fxv);
+      else
+        harmonic_peaks_q8_kernel<NL, BP, false><<<dim3(static_cast<unsigned>(nt * K)), 256, 0, s>>>(
+            P, pstride, Q, qstride, lo, hi, hp, out, count, nt, xcd, lim, fxv);
     };
     switch (hp.nlevels) {
       case 0: oneq(std::integral_constant<int, 0>{}); break;

@@ -717,7 +717,9 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   // profiles/r3_fused/SUMMARY.md.)
   pst_ = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
   q8_ = mode_ == 2 && kern::fft4_x_layout(f4_).tiled && !(kern::harmonic_flags() & 4);
+  fromx_ = q8_ && (kern::harmonic_flags() & 8);
   qst_ = q8_ ? (pst_ + 63) / 64 * 64 : 0;
+  if (mode_ == 2) rt_ = kern::r2c_twiddle_table(n_ / 2);
   // batch size
   {
     // auto budget: capped by the device's free memory shared among its engines
@@ -725,7 +727,7 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
       budget = std::min(budget, free_b / 10 * 7 / static_cast<size_t>(std::max(1, p_.engines_per_device)));
-    const size_t per = n_ * 4 + nb_ * 8 + pst_ * 4 + qst_;  // Y/res + X/spec + P + Q per trial
+    const size_t per = n_ * 4 + nb_ * 8 + (fromx_ ? 0 : pst_ * 4) + qst_;  // Y/res + X/spec + P + Q per trial
     // at most 512 trials per batch from 2^23 samples up, 256 below (the
     // shorter series were only measured up to 256)
     const size_t kmax = n_ >= (uint64_t(1) << 23) ? 512 : 256;
@@ -831,7 +833,7 @@ void SearchEngine::ensure_batch_buffers(int k) {
   const uint64_t rs = mode_ == 2 ? 2 * f4_.ystride : n_;  // floats per trial
   res_.resize(static_cast<uint64_t>(k) * rs);
   spec_.resize(static_cast<uint64_t>(k) * xs_);
-  P_.resize(static_cast<uint64_t>(k) * pst_);
+  if (!fromx_) P_.resize(static_cast<uint64_t>(k) * pst_);
   if (q8_) Q_.resize(static_cast<uint64_t>(k) * qst_);
 }
 
@@ -857,9 +859,11 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
   PSOUP_HIP_CHECK(hipMemsetAsync(s.d_count.data(), 0, sizeof(uint32_t), stream_));
   // Trials [b, b + c) of the batch: spectrum, power spectrum, harmonic peaks.
   auto run = [&](int b, int c, hipStream_t st) {
-    float* P = P_.data() + static_cast<uint64_t>(b) * pst;
+    float* P = fromx_ ? nullptr : P_.data() + static_cast<uint64_t>(b) * pst;
     // (the kernel flags can change after construction: Q only where the tiled r2c writes it)
     uint8_t* Q = q8_ && mode_ == 2 && xl.tiled ? Q_.data() + static_cast<uint64_t>(b) * qst_ : nullptr;
+    PSOUP_CHECK(!fromx_ || Q, "fft4 kernel flags changed under an engine that recomputes spectra from X");
+    kern::HarmFromX fx;
     if (mode_ == 2) {
       // res_ holds the four-step intermediates Y (complex, ystride per trial)
       float2* Y = reinterpret_cast<float2*>(res_.data()) + static_cast<uint64_t>(b) * f4_.ystride;
@@ -876,7 +880,17 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
       kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st, static_cast<uint64_t>(hi_));
       if (xl.tiled)
         kern::r2c_interbin_normalise_tiled(X, f4_.n1, f4_.n2, xs_, P, pst, c, static_cast<uint64_t>(hi_),
-                                           wstats_.data(), static_cast<float>(n_), st, src, Q, qst_);
+                                           wstats_.data(), static_cast<float>(n_), st, src, Q, qst_, rt_);
+      if (fromx_) {
+        fx.X = X;
+        fx.xstride = xs_;
+        fx.log2_n2 = ilog2(static_cast<uint64_t>(f4_.n2));
+        fx.n1 = static_cast<uint32_t>(f4_.n1);
+        fx.rt = rt_;
+        fx.stats = wstats_.data();
+        fx.tsrc = src;
+        fx.nscale = static_cast<float>(n_);
+      }
       else
         kern::r2c_interbin_normalise_batch(X, n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch, xl.log2_blk, P,
                                            pst, c, static_cast<uint64_t>(hi_), wstats_.data(),
@@ -895,7 +909,8 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
     RoctxRange r("Harmonic summing");
     kern::HarmParams hp = hp_;
     hp.trial_base = static_cast<uint32_t>(b);
-    kern::harmonic_peaks_batch(P, nb_, pst, c, hp, s.d_peaks.data(), s.d_count.data(), st, Q, qst_);
+    kern::harmonic_peaks_batch(P, nb_, pst, c, hp, s.d_peaks.data(), s.d_count.data(), st, Q, qst_,
+                               fromx_ ? &fx : nullptr);
   };
   if (sub_ > 0 && count > sub_) {
     // Sub-batch pipeline: consecutive sub-batches alternate between two

@@ -558,9 +558,13 @@ def broadcast_header(infilename: str, ctx: pdist.DistContext) -> dict:
     return ast.literal_eval(hdr_bytes.decode())
 
 
-def load_packed_for_rank(infilename: str, ctx: pdist.DistContext):
+def load_packed_for_rank(infilename: str, ctx: pdist.DistContext, timers=None):
     """Rank 0 reads the filterbank; the packed bytes are RCCL-broadcast to
-    every rank's GPU.  Returns (header, packed_tensor_on_device, nsamps)."""
+    every rank's GPU.  Returns (header, packed_tensor_on_device, nsamps).
+    With ``timers``, "reading" (running on entry) stops after the file read and
+    the device upload is charged to "dedispersion" (the reference's timers:
+    pipeline_multi.cu:287-289 read the file, its dedispersion copies it to
+    the GPU)."""
     header = None
     packed = None
     if ctx.is_root:
@@ -577,6 +581,9 @@ def load_packed_for_rank(infilename: str, ctx: pdist.DistContext):
         header = ast.literal_eval(hdr_bytes.decode())
     nsamps = int(header["nsamples"])
     nbytes = nsamps * int(header["nchans"]) * int(header["nbits"]) // 8
+    if timers is not None:
+        timers["reading"].stop()
+        timers["dedispersion"].start()
     if ctx.device.type == "cuda":
         packed = torch.empty(nbytes, dtype=torch.uint8, device=ctx.device)
         if ctx.is_root:
@@ -588,6 +595,10 @@ def load_packed_for_rank(infilename: str, ctx: pdist.DistContext):
             pdist.broadcast_bytes(packed, nbytes)
     else:
         packed = torch.from_numpy(fb.data()[:nbytes].copy()) if ctx.is_root else None
+    if timers is not None:
+        if ctx.device.type == "cuda":
+            torch.cuda.synchronize()
+        timers["dedispersion"].stop()
     return header, packed, nsamps
 
 
@@ -652,9 +663,9 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     if sharded:
         header, packed, nsamps = broadcast_header(args.infilename, ctx), None, 0
         nsamps = int(header["nsamples"])
+        timers["reading"].stop()
     else:
-        header, packed, nsamps = load_packed_for_rank(args.infilename, ctx)
-    timers["reading"].stop()
+        header, packed, nsamps = load_packed_for_rank(args.infilename, ctx, timers)
 
     rs = RankSearcher(args, header, packed, nsamps, resident=not sharded)
     del packed

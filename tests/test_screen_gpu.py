@@ -80,8 +80,9 @@ def test_tiled_r2c_writes_screening_bytes(log2n):
 
 
 def test_engine_screen_equals_exact():
-    """SearchEngine with the screened harmonic sum (default) and without
-    (harmonic flag 4) gives identical candidates, noise and pulsar."""
+    """SearchEngine with the screened harmonic sum (default), without it
+    (harmonic flag 4) and with the exact sums recomputed from the spectrum
+    instead of a stored P (flag 8) gives identical candidates."""
     import peasoup_amd._C as C
 
     rng = np.random.default_rng(5)
@@ -95,7 +96,7 @@ def test_engine_screen_equals_exact():
     out = []
     old = C.kernels.harmonic_flags()
     try:
-        for flags in (old, old | 4):
+        for flags in (old, old | 4, old | 8):
             C.kernels.harmonic_set_flags(flags)
             p = C.SearchParams()
             p.fft_size, p.tsamp, p.nharmonics = 1 << 21, 64e-6, 4
@@ -104,4 +105,4 @@ def test_engine_screen_equals_exact():
             out.append([(x.dm_idx, x.acc, x.nh, x.snr, x.freq, x.count_assoc()) for x in c])
     finally:
         C.kernels.harmonic_set_flags(old)
-    assert out[0] == out[1] and len(out[0]) > 0
+    assert out[0] == out[1] == out[2] and len(out[0]) > 0

@@ -2,7 +2,7 @@
 """Per-kernel microbenchmark of the acceleration-search hot path at the
 headline size (2^23-point series, K trials per batch), with HIP-event timing.
 
-    python tools/kbench.py [--log2n 23] [--K 32] [--reps 10] [--flags 0,1,2,4]
+    python tools/kbench.py [--log2n 23] [--K 32] [--reps 10] [--flags 0,1,259,3331]
 
 Prints one line per (kernel, variant): time per launch, per trial, and the
 effective HBM bandwidth of the bytes the kernel must move.
@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--log2n", type=int, default=23)
     ap.add_argument("--K", type=int, default=32)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--flags", default="0,1,2,4,5")
+    ap.add_argument("--flags", default="0,1,259,3331")
     a = ap.parse_args()
     dev = torch.device("cuda")
     n = 1 << a.log2n
@@ -71,6 +71,7 @@ def main():
     K_.fft4_pad_input(x.data_ptr(), n, xp.data_ptr(), g, s)
     report("pad_input", timeit(lambda: K_.fft4_pad_input(x.data_ptr(), n, xp.data_ptr(), g, s), a.reps) * K,
            2 * 4 * n)
+    f_default = K_.fft4_flags()
     for f in [int(v) for v in a.flags.split(",")]:
         K_.fft4_set_flags(f)
         tc = timeit(lambda: K_.fft4_resample_colpass(x.data_ptr(), xp.data_ptr(), n, af.data_ptr(), K, Y.data_ptr(), g,
@@ -87,7 +88,13 @@ def main():
     tz = timeit(lambda: K_.r2c_interbin_normalise_tiled(X.data_ptr(), g.n1, g.n2, g.xstride, P.data_ptr(), M + 1, K,
                                                         M + 1, st.data_ptr(), float(n), s), a.reps)
     report("r2c_interbin_normalise tiled", tz, K * (8 * M + 4 * M))
-    K_.fft4_set_flags(0)
+    qs = (M + 1 + 63) // 64 * 64
+    Qr = torch.empty(K * qs, dtype=torch.uint8, device=dev)
+    tz = timeit(lambda: K_.r2c_interbin_normalise_tiled(X.data_ptr(), g.n1, g.n2, g.xstride, P.data_ptr(), M + 1, K,
+                                                        M + 1, st.data_ptr(), float(n), s, Qr.data_ptr(), qs), a.reps)
+    report("r2c_interbin_normalise tiled + screening bytes", tz, K * (8 * M + 5 * M))
+    del Qr
+    K_.fft4_set_flags(f_default)
     # harmonic peaks on normal noise (threshold 9 -> few peaks)
     P.normal_()
     nb = M + 1
@@ -101,11 +108,23 @@ def main():
         cnt.zero_()
         K_.harmonic_peaks_batch(P.data_ptr(), nb, nb, K, 3, starts, ends, 9.0, cap, out.data_ptr(), cnt.data_ptr(), s)
 
-    for hf in (0, 1):
+    hdef = K_.harmonic_flags()
+    for hf in (hdef & ~1, hdef):
         K_.harmonic_set_flags(hf)
         th = timeit(harm, a.reps)
-        report(f"harmonic_peaks (3 levels) xcd={hf}", th, K * 4 * M)
-    K_.harmonic_set_flags(1)
+        report(f"harmonic_peaks (3 levels, fp32 staging) flags={hf}", th, K * 4 * M)
+    qst = (nb + 63) // 64 * 64
+    Q = torch.empty(K * qst, dtype=torch.uint8, device=dev)
+    K_.quantize_q8(P.data_ptr(), nb, nb, K, Q.data_ptr(), qst, s)
+
+    def harmq():
+        cnt.zero_()
+        K_.harmonic_peaks_batch(P.data_ptr(), nb, nb, K, 3, starts, ends, 9.0, cap, out.data_ptr(), cnt.data_ptr(), s,
+                                Q.data_ptr(), qst)
+
+    th = timeit(harmq, a.reps)
+    report("harmonic_peaks (3 levels, screened)", th, K * M)
+    K_.harmonic_set_flags(hdef)
 
 
 if __name__ == "__main__":
