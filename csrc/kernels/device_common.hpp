@@ -176,14 +176,15 @@ __device__ __forceinline__ float2 r2c_tw(const float2* __restrict__ rt, uint32_t
 }
 
 // Screening byte of a normalised spectrum value for the harmonic sum's
-// integer pre-screen (harmsum.hip): u = clamp(rint(4 p) + 128, 0, 255), so
-// (u - 128) / 4 is within 1/8 of p for u < 255.  u = 255 (p >= 31.625, or
-// NaN) makes the screen take the exact path; u = 0 (p <= -31.875) gives a
-// screen value above p, which only makes the screen more conservative.
+// integer pre-screen (harmsum.hip): with v = rint(4 p) + 128, bytes 0..253
+// hold v - 1 for v in [1, 254] (|p - (byte - 127) / 4| <= 1/8), 254 marks
+// v >= 255 (or NaN) and 255 marks v <= 0.  The screen sends any bin whose
+// terms include a byte >= 254 to the exact path, so every screened term is
+// within 1/8 of its bin and below 32 in magnitude.
 __device__ __forceinline__ uint8_t q8(float p) {
   const float v = rintf(p * 4.0f) + 128.0f;
-  if (!(v < 255.0f)) return 255;  // also NaN
-  return v <= 0.0f ? 0 : static_cast<uint8_t>(v);
+  if (!(v < 255.0f)) return 254;  // also NaN
+  return v <= 0.0f ? 255 : static_cast<uint8_t>(v - 1.0f);
 }
 
 }  // namespace dev

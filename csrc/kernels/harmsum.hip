@@ -789,13 +789,14 @@ __global__ void __launch_bounds__(256) harmonic_peaks2_kernel(const float* __res
 // Screened harmonic sum (harmonic_peaks_batch with Q).  The tile stages
 // the gather ranges of the screening bytes (dev::q8) instead of P: 16 bins
 // per 16-byte load, a quarter of the bytes.  Each level's integer sum of
-// bytes s_h is compared with lim[h], chosen on the host so that an fp32 sum
-// above the pre-threshold lo[h] always gives s_h > lim[h]: every unsaturated
-// byte is within 1/8 of its bin, (s_h - 128 * 2^h) / 4 + 2^h / 8 + 0.25 bounds
-// the fp32 sum (0.25 covers its rounding), lim = floor(4 (lo - 2^h / 8 -
-// 0.25) + 128 * 2^h) - 1.  A bin whose sums pass, or whose terms include a
-// saturated byte (255), is summed again exactly from P in the reference order:
-// the same values and records as harmonic_peaks_kernel.
+// bytes s_h (2^h terms) is compared with lim[h], chosen on the host so that
+// an fp32 sum above the pre-threshold lo[h] always gives s_h > lim[h]: every
+// byte below 254 is within 1/8 of its bin, so (s_h - 127 * 2^h) / 4 + 2^h / 8
+// + 0.25 bounds the fp32 sum (0.25 covers its rounding: the terms are below
+// 32 in magnitude), lim = floor(4 (lo - 2^h / 8 - 0.25) + 127 * 2^h) - 1.  A
+// bin whose sums pass, or whose terms include a byte >= 254 (out of the byte
+// range either way), is summed again exactly in the reference order -- the
+// same values and records as harmonic_peaks_kernel.
 template <int NLEV, int BPT>
 struct HarmTileQ {
   static constexpr int B = 256 * BPT;
@@ -974,7 +975,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
       cand = cand | (sq > lim.v[5]);
     }
 #undef PS_QTERM
-    cand = (cand | (mx >= 255)) & (i < hi);
+    cand = (cand | (mx >= 254)) & (i < hi);
     cm |= cand ? (1u << u) : 0u;
   }
   if (__ballot(cm != 0u) == 0ull) return;  // the usual no-peak case: the whole wave is done
@@ -1397,7 +1398,7 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
     HarmLim lim;
     for (int h = 0; h < 6; ++h) {
       const double n = std::ldexp(1.0, h);
-      const double x = 4.0 * (static_cast<double>(pre.lo[h]) - n / 8.0 - 0.25) + 128.0 * n;
+      const double x = 4.0 * (static_cast<double>(pre.lo[h]) - n / 8.0 - 0.25) + 127.0 * n;
       lim.v[h] = std::isfinite(x) ? static_cast<int>(std::floor(x)) - 1 : INT_MIN;
     }
     HarmFromX fxv;

@@ -12,8 +12,11 @@ dev = "cuda"
 
 
 def _q8_ref(P):
-    v = np.rint(P.astype(np.float32) * np.float32(4.0)) + np.float32(128.0)
-    q = np.where(np.isnan(v) | (v >= 255), 255, np.where(v <= 0, 0, v))
+    """device_common.hpp dev::q8: v = rint(4p) + 128; bytes 0..253 = v - 1,
+    254 = v >= 255 or NaN, 255 = v <= 0."""
+    with np.errstate(invalid="ignore"):
+        v = np.rint(P.astype(np.float32) * np.float32(4.0)) + np.float32(128.0)
+        q = np.where(np.isnan(v) | (v >= 255), 254, np.where(v <= 0, 255, v - 1))
     return q.astype(np.uint8)
 
 
@@ -74,7 +77,7 @@ def test_tiled_r2c_writes_screening_bytes(log2n):
         exp = _q8_ref(P.cpu().numpy()[:, :m])
         got = Q.cpu().numpy()[:, :m]
         assert np.array_equal(got, exp)
-        assert (got == 255).any() and (got < 255).any()
+        assert (got == 254).any() and (got < 254).any()
         P0 = ops.fft4_resample_interbin(x, accs, 64e-6, st, float(n), nbins_out=nbo)
         assert torch.equal(P, P0)
 
