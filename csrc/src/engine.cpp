@@ -878,9 +878,14 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
                                   st);
       float2* X = spec_.data() + static_cast<uint64_t>(b) * xs_;
       kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st, static_cast<uint64_t>(hi_));
-      if (xl.tiled)
+      if (xl.tiled) {
         kern::r2c_interbin_normalise_tiled(X, f4_.n1, f4_.n2, xs_, P, pst, c, static_cast<uint64_t>(hi_),
                                            wstats_.data(), static_cast<float>(n_), st, src, Q, qst_, rt_);
+      } else {
+        kern::r2c_interbin_normalise_batch(X, n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch, xl.log2_blk, P,
+                                           pst, c, static_cast<uint64_t>(hi_), wstats_.data(),
+                                           static_cast<float>(n_), st, src);
+      }
       if (fromx_) {
         fx.X = X;
         fx.xstride = xs_;
@@ -891,10 +896,6 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
         fx.tsrc = src;
         fx.nscale = static_cast<float>(n_);
       }
-      else
-        kern::r2c_interbin_normalise_batch(X, n_ / 2, xs_, xl.log2_row, xl.row_pitch, xl.blk_pitch, xl.log2_blk, P,
-                                           pst, c, static_cast<uint64_t>(hi_), wstats_.data(),
-                                           static_cast<float>(n_), st, src);
     } else {
       kern::resample_batch(cur_tim_, n_, res_.data(), n_, af_.data() + first, c, st);
       batch_plan(c).execute(res_.data(), spec_.data(), st);
