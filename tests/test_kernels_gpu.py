@@ -553,8 +553,10 @@ def test_auto_short_list_balancing_matches_fixed_batch(C):
         p = C.SearchParams()
         p.fft_size, p.tsamp, p.nharmonics, p.min_snr = n, tsamp, 3, 6.0
         if auto:
-            # budget of exactly 64 trials (Y + X + P bytes per trial; the search range covers all bins)
-            p.accel_batch, p.batch_bytes = 0, 64 * (n * 4 + (n // 2 + 1) * 8 + (n // 2 + 1) * 4)
+            # budget of exactly 64 trials (Y + X + P + screening bytes per trial; the search range covers
+            # all bins)
+            nb = n // 2 + 1
+            p.accel_batch, p.batch_bytes = 0, 64 * (n * 4 + nb * 8 + nb * 4 + (nb + 63) // 64 * 64)
         else:
             p.accel_batch, p.sub_batch = 24, 0
         eng = C.SearchEngine(p, s)
