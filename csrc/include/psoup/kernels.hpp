@@ -399,10 +399,11 @@ constexpr uint32_t kHarmCap = 4096;
 constexpr uint32_t kHarmHost = 0x80000000u;
 void harm_distill_batch(const uint2* d_clust, const uint2* d_segtab, int ntrials, const HarmDistillParams& p,
                         uint2* d_out, uint2* d_ttab, uint32_t* d_total, hipStream_t s);
-// Harmonic-sum switches (process-wide; default 1 | 32 | 10 << 8): bit 0 =
+// Harmonic-sum switches (process-wide; default 1 | 8 | 32 | 10 << 8): bit 0 =
 // XCD-per-trial block order; bit 1 = pre-threshold off (tests); bit 2 = the
 // search engine's screened sum off, bit 3 = its exact sums recomputed from
-// the spectrum with no P stored (engines built afterwards); bit 5 = the
+// the spectrum with no P stored (engines built afterwards; both on by
+// default); bit 5 = the
 // fp32 3-level kernel in two staging phases; bits 8-15 = that kernel's
 // dynamic-LDS occupancy cap in KiB.
 void harmonic_set_flags(int flags);

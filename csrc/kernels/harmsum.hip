@@ -1159,7 +1159,11 @@ namespace {
 // Default 1 | 32 | (10 << 8): XCD order, two-phase staging at 3 levels,
 // 6 workgroups per CU (ABBA same-box bench: 22.55k vs 22.47k trials/s for the
 // one-phase kernel, every pair; profiles/r2_recheck/ab_harm_abba.txt)
-int g_harm_flags = 1 | 32 | (10 << 8);
+// default: XCD trial order, screened sum recomputing its exact bins from the
+// spectrum (no P stored: bench +3.9% over storing P, +10.3% over the fp32
+// kernel on the same box, profiles/r4_screen), 3-level fp32 kernel in two
+// staging phases with a 10 KiB occupancy cap
+int g_harm_flags = 1 | 8 | 32 | (10 << 8);
 
 // Mixed-radix n = m p (p a power of two, m odd): gather of the m strided
 // columns, and the length-m combination with the twiddles W_n^(n1 k)

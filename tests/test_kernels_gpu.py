@@ -464,7 +464,7 @@ def test_harmonic_prethreshold_is_exact(nlev, thresh):
     old = C.kernels.harmonic_flags()
     try:
         # bit 1 disables the pre-threshold; bit 5 = two-phase staging (3 levels),
-        # bits 8-15 = occupancy cap; the default is 1 | 32 | (10 << 8)
+        # bits 8-15 = occupancy cap; the default is 1 | 8 | 32 | (10 << 8)
         for flags in (1, 3, 33, 35, 1 | 32 | (10 << 8), old):
             C.kernels.harmonic_set_flags(flags)
             trial, level, idx, snr = ops.harmonic_peaks(Pt, nlev, starts, ends, thresh)

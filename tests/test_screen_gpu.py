@@ -99,7 +99,7 @@ def test_engine_screen_equals_exact():
     out = []
     old = C.kernels.harmonic_flags()
     try:
-        for flags in (old, old | 4, old | 8):
+        for flags in (old & ~8, old | 4, old | 8):  # P stored / screen off / bins recomputed (default)
             C.kernels.harmonic_set_flags(flags)
             p = C.SearchParams()
             p.fft_size, p.tsamp, p.nharmonics = 1 << 21, 64e-6, 4
