@@ -368,18 +368,29 @@ class RankSearcher:
                             if progress is not None:
                                 progress(1)
 
-            if ne == 1:
-                run_dms(self.engine, range(d0, d1))
-            else:
-                futs = [self._executor().submit(run_dms, e, range(d0 + i, d1, ne))
-                        for i, e in enumerate(self.engines)]
-                # the next block is issued while the engines run: whatever it
-                # costs on the host (a plan table, a spill read) no longer
-                # leaves the GPU idle
-                nxt = pull()
-                tb1 = time.perf_counter()
-                for f in futs:
-                    f.result()
+            try:
+                if ne == 1:
+                    run_dms(self.engine, range(d0, d1))
+                else:
+                    futs = [self._executor().submit(run_dms, e, range(d0 + i, d1, ne))
+                            for i, e in enumerate(self.engines)]
+                    # the next block is issued while the engines run: whatever it
+                    # costs on the host (a plan table, a spill read) no longer
+                    # leaves the GPU idle
+                    nxt = pull()
+                    tb1 = time.perf_counter()
+                    for f in futs:
+                        f.result()
+            except BaseException:
+                # the previous block completed: collect and spill it before the
+                # failure propagates, so a resume does not redo it
+                if prev is not None:
+                    try:
+                        finalize(prev)
+                    except Exception:  # the original failure is the one to report
+                        pass
+                    prev = None
+                raise
             tb2 = time.perf_counter()
             evs = []
             for e in self.engines:

@@ -1,11 +1,9 @@
 #!/bin/bash
-# Deferred per-DM acceleration-distillation collection: Python pipeline tests, configs 4/5.
+# BASELINE configs 4/5 (Python driver), config 5 at 2^23, config 4 single sky, golden command x5 (native + Python).
 set -o pipefail
 O=gpurun_out/r4async
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 280 --timeout-method thread tests/test_models_gpu.py tests/test_pipeline_gpu.py tests/test_harmdistill_gpu.py > $O/pytest.log 2>&1 || { echo PYTEST_FAIL; grep -E "FAILED|Error" $O/pytest.log | head; tail -30 $O/pytest.log; exit 1; }
-tail -1 $O/pytest.log
 timeout -k 10 500 python3 tools/baseline_configs.py --configs 4,5 --workdir /tmp/cfg --out $O/c45.jsonl > $O/c45.log 2>&1 || { echo C45_FAIL; tail -20 $O/c45.log; exit 1; }
 python3 -c "
 import json
@@ -13,6 +11,8 @@ for l in open('$O/c45.jsonl'):
     d=json.loads(l); r=d['rank_stats'][0]
     print(d['config'], d['timers_s'], {k: r[k] for k in ('host_s','accd_s','tail_s','gpu_distilled','host_distilled')})
 "
+timeout -k 10 500 python3 tools/baseline_configs.py --configs 4,5 --native --workdir /tmp/cfg --out $O/c45_native.jsonl > $O/c45n.log 2>&1 || { echo C45N_FAIL; tail -20 $O/c45n.log; exit 1; }
+cut -c1-400 $O/c45_native.jsonl
 timeout -k 10 500 python3 tools/baseline_configs.py --configs 4 --sky single --workdir /tmp/cfg --out $O/c4single.jsonl > $O/c4s.log 2>&1 || { echo C4S_FAIL; tail -20 $O/c4s.log; exit 1; }
 python3 -c "
 import json
