@@ -50,6 +50,16 @@ bool debug_sync_enabled();      // PSOUP_DEBUG_SYNC env var
 void set_numerics_flag(const std::string& name, long value);
 std::string numerics_flags();   // "name=value ..." sorted by name
 
+// One-time device start-up, outside every stage timer: HIP loads a
+// translation unit's code object at the first launch of one of its kernels
+// (tens of ms for the set the search uses), and the first allocation sets up
+// the device's memory state.  Every kernel TU registers a no-op launch
+// (device_common.hpp); warm_device() runs them all and a small
+// allocation on the current device and waits.  Returns the seconds taken.
+using WarmFn = void (*)(hipStream_t);
+bool register_warmup(WarmFn fn);
+double warm_device();
+
 [[noreturn]] void throw_error(const std::string& what, const char* file, int line);
 
 #define PSOUP_THROW(msg)                                                   \

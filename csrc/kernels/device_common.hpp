@@ -188,5 +188,14 @@ __device__ __forceinline__ uint8_t q8(float p) {
 }
 
 }  // namespace dev
+
+// Per-TU no-op kernel registered for psoup::warm_device (common.hpp): its
+// launch makes HIP load this translation unit's code object.
+namespace {
+__global__ void tu_warm_kernel() {}
+void tu_warm(hipStream_t s) { tu_warm_kernel<<<1, 1, 0, s>>>(); }
+[[maybe_unused]] const bool tu_warm_registered = register_warmup(&tu_warm);
+}  // namespace
+
 }  // namespace kern
 }  // namespace psoup

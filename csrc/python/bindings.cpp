@@ -552,6 +552,8 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("X"), py::arg("n1"), py::arg("n2"), py::arg("xstride"), py::arg("P"), py::arg("pstride"), py::arg("K"),
       py::arg("nbo"), py::arg("stats"), py::arg("nscale"), py::arg("s"), py::arg("q") = 0, py::arg("qstride") = 0);
+  m.def("warm_device", &warm_device,
+        "load every kernel module's code object on the current device (a no-op launch each); seconds taken");
   k.def("quantize_q8", [](uintptr_t Pin, uint64_t pstride, uint64_t n, int K, uintptr_t q, uint64_t qstride,
                           uintptr_t s) { kern::quantize_q8(P<const float>(Pin), pstride, n, K, P<uint8_t>(q), qstride, S(s)); });
   py::class_<kern::Fft4Geom>(k, "Fft4Geom")

@@ -1,5 +1,9 @@
 #include "psoup/common.hpp"
 
+#include <chrono>
+
+#include <vector>
+
 #include <map>
 
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -41,6 +45,28 @@ std::string numerics_flags() {
   std::string s;
   for (const auto& [k, v] : numerics_map()) s += (s.empty() ? "" : " ") + k + "=" + std::to_string(v);
   return s;
+}
+
+namespace {
+std::vector<WarmFn>& warm_list() {
+  static std::vector<WarmFn> v;  // filled by static initialisers of the kernel TUs
+  return v;
+}
+}  // namespace
+
+bool register_warmup(WarmFn fn) {
+  warm_list().push_back(fn);
+  return true;
+}
+
+double warm_device() {
+  const auto t0 = std::chrono::steady_clock::now();
+  void* p = nullptr;
+  PSOUP_HIP_CHECK(hipMalloc(&p, 256));
+  for (WarmFn fn : warm_list()) fn(nullptr);
+  PSOUP_HIP_CHECK(hipDeviceSynchronize());
+  PSOUP_HIP_CHECK(hipFree(p));
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 
 int log_rank() { return g_rank.load(); }

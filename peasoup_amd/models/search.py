@@ -669,6 +669,14 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     ctx = pdist.init()
     timers = {k: Stopwatch() for k in ("reading", "dedispersion", "searching", "folding", "total")}
     timers["total"].start()
+    # device start-up (context, allocator, kernel code objects) in "total"
+    # only, as the reference's context creation: stage timers hold stage work
+    device_init_s = 0.0
+    if ctx.device.type == "cuda":
+        t_init = time.perf_counter()
+        torch.empty(1, device=ctx.device)
+        _C.warm_device()
+        device_init_s = time.perf_counter() - t_init
     timers["reading"].start()
     sharded = bool(getattr(args, "time_shards", False))
     if sharded:
@@ -735,6 +743,7 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     search_wall = time.perf_counter() - t0
     rank_stats = rs.counters()
     rank_stats.update({"rank": ctx.rank, "search_s": search_wall, "accel_trials_planned": local_trials,
+                       "device_init_s": device_init_s,
                        "dm_schedule": schedule, "dm_blocks": len(rs.blocks_done),
                        "fft_mode": rs.engine.fft_mode, "accel_batch": rs.engine.batch_size,
                        "sub_batch": rs.engine.sub_batch,
