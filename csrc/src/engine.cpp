@@ -124,7 +124,10 @@ void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std
   PSOUP_HIP_CHECK(hipSetDevice(devices[0]));
   PinnedBuffer<uint8_t> stage[2];
   Event staged[2], landed;
-  for (int i = 0; i < 2; ++i) stage[i].resize(chunk * bps);
+  // staging sized to the file when it is shorter than a chunk (pinning
+  // 2 x 64 MiB took ~40 ms, more than a small file's whole upload)
+  const uint64_t stage_bytes = std::min(chunk, g.nsamps) * bps;
+  for (int i = 0; i < (g.nsamps > chunk ? 2 : 1); ++i) stage[i].resize(stage_bytes);
   bool used[2] = {false, false};
   hipStream_t s0 = fbs[0]->stream();
   int slot = 0;

@@ -4,6 +4,8 @@ set -o pipefail
 O=gpurun_out/r4async
 mkdir -p $O
 export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -q --timeout 280 --timeout-method thread tests/test_pipeline_gpu.py tests/test_models_gpu.py > $O/pytest.log 2>&1 || { echo PYTEST_FAIL; grep -E "FAILED|Error" $O/pytest.log | head; tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
 timeout -k 10 500 python3 tools/baseline_configs.py --configs 4,5 --workdir /tmp/cfg --out $O/c45.jsonl > $O/c45.log 2>&1 || { echo C45_FAIL; tail -20 $O/c45.log; exit 1; }
 python3 -c "
 import json
