@@ -1027,19 +1027,37 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
         val += pv((i + 2) >> 2);
         sum[2] = val;
       }
+      // (levels 3+ in runtime loops when the bins are recomputed: unrolled,
+      // their loads in flight took 106-370 VGPRs and the occupancy of the
+      // whole kernel)
       if constexpr (NLEV >= 3) {
+        if constexpr (FROMX) {
+#pragma unroll 1
+          for (int m = 1; m < 8; m += 2) val += pv((i * m + 4) >> 3);
+        } else {
 #pragma unroll
-        for (int m = 1; m < 8; m += 2) val += pv((i * m + 4) >> 3);
+          for (int m = 1; m < 8; m += 2) val += pv((i * m + 4) >> 3);
+        }
         sum[3] = val;
       }
       if constexpr (NLEV >= 4) {
+        if constexpr (FROMX) {
+#pragma unroll 1
+          for (int m = 1; m < 16; m += 2) val += pv((i * m + 8) >> 4);
+        } else {
 #pragma unroll
-        for (int m = 1; m < 16; m += 2) val += pv((i * m + 8) >> 4);
+          for (int m = 1; m < 16; m += 2) val += pv((i * m + 8) >> 4);
+        }
         sum[4] = val;
       }
       if constexpr (NLEV >= 5) {
+        if constexpr (FROMX) {
+#pragma unroll 1
+          for (int m = 1; m < 32; m += 2) val += pv((i * m + 16) >> 5);
+        } else {
 #pragma unroll
-        for (int m = 1; m < 32; m += 2) val += pv((i * m + 16) >> 5);
+          for (int m = 1; m < 32; m += 2) val += pv((i * m + 16) >> 5);
+        }
         sum[5] = val;
       }
 #pragma unroll
