@@ -79,13 +79,14 @@ def _engine_stream(device: torch.device, slot: int = 0) -> int:
 def engines_per_gpu(args, max_trials_per_dm: int) -> int:
     """Search engines per GPU (each on its own stream, fed by its own host
     thread): DM trials of a chunk are dealt round-robin so one engine's small
-    per-DM kernels (whitening, short acceleration batches) and host
-    distillation overlap the others'.  Auto: 3 when DMs carry fewer than 128
-    acceleration trials (config 4: 1.6x the search throughput), else 1 (long
-    batches already fill the GPU; a second engine costs ~2% at 684 trials)."""
+    per-DM kernels and host work overlap the others'.  Auto: 1.  Three
+    engines paid off (1.6x on config 4) while per-trial distillation ran on
+    the host; with clustering and harmonic distillation on the device and the
+    acceleration distillation overlapped, one engine is faster (round 4,
+    `profiles/r4_configs/engines.md`: config 4 search 0.42 vs 0.47 s, config 5
+    0.41 vs 0.45 s, single pulsar equal).  ``--engines_per_gpu`` /
+    ``PSOUP_ENGINES`` still select more."""
     v = int(os.environ.get("PSOUP_ENGINES", "0") or 0) or int(getattr(args, "engines_per_gpu", 0) or 0)
-    if v <= 0:
-        v = 3 if max_trials_per_dm < 128 else 1
     return max(1, v)
 
 
