@@ -220,6 +220,9 @@ struct Fft4Geom {
   uint64_t in_tstride = 0, pad_tstride = 0;
   // optional device map trial -> series index (else trial k reads series k)
   const uint32_t* tsrc = nullptr;
+  // Y in row pairs, Y_p[k2/2][i][k2%2], instead of 8x8 tiles (only where
+  // fft4_pair_y(g) holds; read by fft4_rowpass_spectrum alone)
+  bool ypair = false;
 };
 Fft4Geom fft4_geometry(uint64_t M);
 // Twiddle tables (upload once per plan): see fft4step.hip for the layout.
@@ -238,6 +241,42 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
 // search needs bins below max_freq only: ~14% of the spectrum at 2^23).
 void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, hipStream_t s,
                   uint64_t nbins_out = 0);
+// Pass B fused with the search spectrum (fft4step.hip fft4_rowpass_spectrum_kernel):
+// from the tiled Y of fft4_resample_colpass, the normalised interbinned
+// spectrum P of every bin 0..M (as r2c_interbin_normalise_tiled forms it, to
+// FFT rounding) and its screening bytes dev::q8(P), without the complex
+// spectrum ever reaching memory.  P is stored workgroup-blocked
+// (spec_pblk_index), Q in natural order: bin b of trial k at
+// Q[k*qstride + kSpecQShift + b].  Trial k normalises with stats + 4*tsrc[k]
+// (tsrc null: stats) scaled by nscale.
+constexpr int kSpecQShift = 15;
+struct SpecOut {
+  float* P = nullptr;
+  uint64_t pstride = 0;  // floats per trial, >= M + 1 (multiple of 4)
+  uint8_t* Q = nullptr;
+  uint64_t qstride = 0;  // bytes per trial, >= M + 1 + kSpecQShift (multiple of 16)
+  const float* stats = nullptr;
+  const uint32_t* tsrc = nullptr;
+  float nscale = 1.f;
+};
+// Position of bin b (0 <= b <= M = n1 << log2_n2) in the blocked P: rows
+// r = b mod n2 in [1, n2/2] at ((2v) n1 + k1) 4 + j with v = (r-1)/4, j = (r-1)%4;
+// the other bins b = M - (r + n2 k1) (r < n2/2) at ((2v+1) n1 + k1) 4 + j with
+// v = r/4, j = r%4; bin 0 at M.
+__host__ __device__ inline uint32_t spec_pblk_index(uint32_t b, int log2_n2, uint32_t n1) {
+  const uint32_t n2 = 1u << log2_n2, M = n1 << log2_n2;
+  if (b == 0) return M;
+  const uint32_t r = b & (n2 - 1);
+  if (r >= 1 && r <= n2 / 2) return (((r - 1) >> 2) * 2 * n1 + (b >> log2_n2)) * 4 + ((r - 1) & 3);
+  const uint32_t bm = M - b, rm = bm & (n2 - 1);
+  return (((rm >> 2) * 2 + 1) * n1 + (bm >> log2_n2)) * 4 + (rm & 3);
+}
+void fft4_rowpass_spectrum(const float2* Y, int K, const Fft4Geom& g, const float2* tables, const SpecOut& o,
+                           hipStream_t s);
+// Whether pass A can write the row-pair Y layout for the spectrum pass under
+// the current flags (the one-exchange pass A, column length 2048): its lanes
+// then load two rows per 16-byte vector, 1 KiB contiguous per wave.
+bool fft4_pair_y(const Fft4Geom& g);
 // Row-octet blocks (8 rows k1 each) r2c_interbin_normalise_tiled runs for
 // bins < nbins_out; it reads spectrum rows k1 <= 8*ny and k1 >= n1 - 8*ny.
 inline uint32_t r2c_tiled_row_blocks(uint64_t nbins_out, int n1, int n2) {
@@ -340,7 +379,12 @@ struct HarmParams {
 // With fx (and Q) the exact sums recompute their bins from the tiled
 // spectrum X exactly as r2c_interbin_normalise_tiled forms them, so P need
 // not be written at all (P is then ignored).
+// With fx->pblk (and Q from fft4_rowpass_spectrum), P is the blocked spectrum
+// of that pass (spec_pblk_index with fx->log2_n2, fx->n1; X unused) and the
+// screening bytes of bin b are at Q[k*qstride + fx->qshift + b].
 struct HarmFromX {
+  int pblk = 0;
+  int qshift = 0;
   const float2* X = nullptr;  // tiled pass-B spectra, trial k at X + k*xstride
   uint64_t xstride = 0;
   int log2_n2 = 0;
@@ -399,13 +443,13 @@ constexpr uint32_t kHarmCap = 4096;
 constexpr uint32_t kHarmHost = 0x80000000u;
 void harm_distill_batch(const uint2* d_clust, const uint2* d_segtab, int ntrials, const HarmDistillParams& p,
                         uint2* d_out, uint2* d_ttab, uint32_t* d_total, hipStream_t s);
-// Harmonic-sum switches (process-wide; default 1 | 8 | 32 | 10 << 8): bit 0 =
-// XCD-per-trial block order; bit 1 = pre-threshold off (tests); bit 2 = the
-// search engine's screened sum off, bit 3 = its exact sums recomputed from
-// the spectrum with no P stored (engines built afterwards; both on by
-// default); bit 5 = the
-// fp32 3-level kernel in two staging phases; bits 8-15 = that kernel's
-// dynamic-LDS occupancy cap in KiB.
+// Harmonic-sum switches (process-wide; default 1 | 8 | 32 | 64 | 10 << 8):
+// bit 0 = XCD-per-trial block order; bit 1 = pre-threshold off (tests);
+// engines built afterwards: bit 2 = the screened sum off, bit 3 = (without
+// bit 6) its exact sums recomputed from the spectrum with no P stored, bit 6
+// = the fused spectrum pass (fft4_rowpass_spectrum; needs the screen);
+// bit 5 = the fp32 3-level kernel in two staging phases; bits 8-15 = that
+// kernel's dynamic-LDS occupancy cap in KiB.
 void harmonic_set_flags(int flags);
 int harmonic_flags();
 // Debug/test: materialise level-h sums [nlevels][nbins] for one spectrum.

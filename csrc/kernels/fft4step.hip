@@ -52,7 +52,7 @@ constexpr int kChanPad = 8;
 template <int L, int CPT, int SUB>
 struct Cfg {
   static constexpr int CH = CPT * SUB;  // transforms per workgroup (blocked layout width when SUB == 1)
-  static_assert(CH == 8, "workgroups cover 8 transforms");
+  static_assert(CH == 8 || (SUB == 1 && CPT == 10), "workgroups cover 8 transforms (10: the fused spectrum pass)");
   static constexpr int T = L / kPts;                     // threads per group
   static constexpr int THREADS = T * SUB;
   static constexpr int PAD = L + L / 8 + kChanPad;       // complex elements per channel plane
@@ -134,7 +134,8 @@ __device__ __forceinline__ void exchange(Vec<CPT>& v, float* __restrict__ lds, i
       for (int r = 0; r < R; ++r) {
         const int idx = lds_pad(base + r * Ns);
 #pragma unroll
-        for (int cc = 0; cc < CG; ++cc) buf[cc * PAD + idx] = v[g + cc][b + r * B];
+        for (int cc = 0; cc < CG; ++cc)
+          if (g + cc < CPT) buf[cc * PAD + idx] = v[g + cc][b + r * B];  // (the last round may be short)
       }
     }
     __syncthreads();
@@ -142,7 +143,8 @@ __device__ __forceinline__ void exchange(Vec<CPT>& v, float* __restrict__ lds, i
     for (int q = 0; q < kPts; ++q) {
       const int idx = lds_pad(t + q * T);
 #pragma unroll
-      for (int cc = 0; cc < CG; ++cc) v[g + cc][q] = buf[cc * PAD + idx];
+      for (int cc = 0; cc < CG; ++cc)
+        if (g + cc < CPT) v[g + cc][q] = buf[cc * PAD + idx];
     }
     __syncthreads();
   }
@@ -246,9 +248,12 @@ __device__ __forceinline__ void load_resampled(const float* __restrict__ in, con
 
 // Table layout (float2): [tw_N2 (N2)] [tw_N1 (N1)] [lo (2^kSplit)] [hi (M >> kSplit)]
 // [ox (N1 x GX)]: ox[col * GX + k2] = W_M^{col P k2}, the k2 part of the
-// one-exchange pass A's four-step twiddles (GX = onex_g(N2), P = N2 / GX).
+// one-exchange pass A's four-step twiddles (GX = onex_g(N2), P = N2 / GX);
+// [hk (N1)] [hr (N2/2 + 1)]: e^{-i pi k1 / N1} and e^{-i pi r / M}, the two
+// factors of the real-FFT post-processing twiddle e^{-i pi (r + N2 k1) / M}
+// (fused spectrum pass).
 struct TableOffsets {
-  uint64_t n2, n1, lo, hi, ox, total;
+  uint64_t n2, n1, lo, hi, ox, hk, hr, total;
 };
 __host__ __device__ constexpr int onex_g(int N2) { return N2 >= 2048 ? 64 : 32; }
 __host__ __device__ inline TableOffsets table_offsets(int N1, int N2) {
@@ -259,7 +264,9 @@ __host__ __device__ inline TableOffsets table_offsets(int N1, int N2) {
   o.lo = o.n1 + N1;
   o.hi = o.lo + (1u << kSplit);
   o.ox = o.hi + (M >> kSplit);
-  o.total = o.ox + static_cast<uint64_t>(N1) * onex_g(N2);
+  o.hk = o.ox + static_cast<uint64_t>(N1) * onex_g(N2);
+  o.hr = o.hk + N1;
+  o.total = o.hr + N2 / 2 + 1;
   return o;
 }
 
@@ -676,6 +683,7 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
   const uint32_t mask = static_cast<uint32_t>(N1) * L - 1;
   const uint32_t col = static_cast<uint32_t>(c0 + rc);
   float2* yk = Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(c0) * L;
+  float2* yp = Y + static_cast<uint64_t>(k) * g.ystride + 2 * col;
   const float2* twr = tws + rc * (G + 1);
 #pragma unroll
   for (int p = 0; p < C::NPAIR; ++p) {
@@ -685,7 +693,10 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
     for (int k2 = 0; k2 < G; ++k2) {
       const float2 wv = k2 == 0 ? om : cmul(om, twr[k2]);
       const uint32_t kk = k1 + static_cast<uint32_t>(P * k2);
-      yk[(kk >> 3) * 64 + static_cast<uint32_t>(rc) * 8 + (kk & 7)] = cmul(u[p][k2], wv);
+      if (g.ypair)  // Y_p[kk/2][col][kk%2]: per wave instruction four whole 128-byte lines
+        yp[(kk >> 1) * (2 * static_cast<uint32_t>(N1)) + (kk & 1)] = cmul(u[p][k2], wv);
+      else
+        yk[(kk >> 3) * 64 + static_cast<uint32_t>(rc) * 8 + (kk & 7)] = cmul(u[p][k2], wv);
     }
   }
   trace_event(11);
@@ -763,6 +774,206 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pass B fused with the search spectrum (fft4_rowpass_spectrum): row DFTs,
+// real-FFT post-processing, interbinning, normalisation and the screening
+// bytes in one pass.  The half-length spectrum Z never leaves the registers:
+// the unfused search wrote it (8 bytes per bin) and read it back in the r2c
+// pass; here each bin costs the 4 bytes of P and the 1 byte of Q.
+//
+// Bin k = r + n2 k1 (r = k2 < n2).  X[k] = r2c_combine(Z[k], Z[M-k], e^{-i pi k/M})
+// (harmsum.hip) needs the mirror bin Z[M-k]: row n2-r at k1' = n1-1-k1 for
+// r > 0, row 0 at -k1 for r = 0.  With W = e^{-2 pi i/n1} and Y_r the pass-A
+// rows (the four-step twiddle W_M^{i r} applied), in both cases
+//   Z[M-k] = sum_i W^{-i k1} u_r[i],  u_r[i] = W^{-i} Y_{n2-r}[i] (r > 0),  Y_0[i] (r = 0),
+// = conj(FFT_n1(conj u_r))[k1]: the SAME k1 as Z[k] = FFT_n1(Y_r)[k1].  So a
+// thread that transforms Y_r and conj(u_r) = W^{i} conj(Y_{n2-r}) holds Z[k]
+// and Z[M-k] of the same bins in the same registers, with the forward FFT
+// code for both ("pair-row" r).
+//
+// A workgroup transforms the pair-rows r = 4v .. 4v+4 (10 transforms per
+// thread, v < n2/8) and forms
+//   P[k]   for k = r + n2 k1, r = 4v+1 .. 4v+4   (interbin neighbour X[k-1]: pair-row r-1),
+//   P[M-k] for k = r + n2 k1, r = 4v   .. 4v+3   (neighbour X[M-k-1] = X[M-(k+1)]: pair-row r+1),
+// i.e. rows 1 .. n2/2 ascending and the rest as mirrors: every bin 1 .. M
+// once; bin 0 (no left neighbour) by (v = 0, k1 = 0).  Pair-row 4v+4 is
+// shared with the next workgroup (25% more row transforms; its Y is read
+// again from L2: consecutive v run on one XCD, see the block order below).
+//
+// Outputs (kernels.hpp SpecOut): P in the workgroup-blocked layout
+// spec_pblk_index (each lane stores 16 contiguous bytes per side and k1: whole
+// lines per wave), Q in natural bin order shifted by kSpecQShift so that each
+// lane's 4 bytes per side are one aligned dword; the 8 workgroups that share
+// a 128-byte Q line run together on one XCD, so L2 merges the dwords.
+// Reference: src/kernels.cu:231-252 (bin_interbin), :469-494 (normalise);
+// the r2c step replaces cuFFT's R2C post-processing (pipeline_multi.cu:216-228).
+constexpr int kSpecNp = 5;  // pair-rows per workgroup
+// cos / sin of 2 pi q / 8 and of pi q / 8 = 2 pi q / 16, q < 8
+__constant__ constexpr float kCos8[8] = {1.f, 0.70710678118654752f, 0.f, -0.70710678118654752f,
+                                         -1.f, -0.70710678118654752f, 0.f, 0.70710678118654752f};
+__constant__ constexpr float kSin8[8] = {0.f, 0.70710678118654752f, 1.f, 0.70710678118654752f,
+                                         0.f, -0.70710678118654752f, -1.f, -0.70710678118654752f};
+__constant__ constexpr float kCos16[8] = {1.f, 0.92387953251128676f, 0.70710678118654752f, 0.38268343236508977f,
+                                          0.f, -0.38268343236508977f, -0.70710678118654752f, -0.92387953251128676f};
+__constant__ constexpr float kSin16[8] = {0.f, 0.38268343236508977f, 0.70710678118654752f, 0.92387953251128676f,
+                                          1.f, 0.92387953251128676f, 0.70710678118654752f, 0.38268343236508977f};
+
+template <int L, bool PAIRY>
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, 2 * kSpecNp, 1>::THREADS),
+                               amdgpu_waves_per_eu(2)))
+fft4_rowpass_spectrum_kernel(const float2* __restrict__ Y, int K, Fft4Geom g, const float2* __restrict__ tab,
+                             SpecOut o) {
+  constexpr int NP = kSpecNp, CPT = 2 * NP;
+  using C = Cfg<L, CPT, 1>;
+  __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
+  constexpr int T = C::T;
+  const int t = threadIdx.x;
+  // block order: XCD x (blockIdx % 8) runs trials x, x+8, ..., each trial's
+  // workgroups in increasing v (the writers of one Q line are consecutive)
+  trace_event(0);
+  const uint32_t n2 = static_cast<uint32_t>(g.n2), nv = n2 / 8;
+  const uint32_t slot = blockIdx.x >> 3;
+  // (readfirstlane: workgroup-uniform in SGPRs, with every address built from them)
+  const int k = __builtin_amdgcn_readfirstlane(static_cast<int>(8 * (slot / nv) + (blockIdx.x & 7u)));
+  if (k >= K) return;  // (the grid covers K rounded up to 8; workgroup-uniform)
+  const uint32_t v = __builtin_amdgcn_readfirstlane(slot % nv);
+  const TableOffsets to = table_offsets(L, static_cast<int>(n2));
+  const float2* yk = Y + static_cast<uint64_t>(k) * g.ystride;
+  const uint32_t fr = 4 * v;                     // forward rows fr .. fr+4 (channels 0..4)
+  const uint32_t mg = n2 - 4 * v - 4;            // mirror rows mg .. mg+3 = pair-rows 4v+4 .. 4v+1 (channels 9..6)
+  const uint32_t m0 = (n2 - 4 * v) & (n2 - 1);   // mirror row of pair-row 4v (channel 5; row 0 when v = 0)
+  // W^{i} = W^{t} e^{-2 pi i q / 8} for i = t + q T (T = L / 8): one table
+  // value per thread, the rest compile-time constants
+  const float2 wt = tab[to.n1 + t];
+  Vec<CPT> x;
+#pragma unroll
+  for (int q = 0; q < kPts; ++q) {
+    const uint32_t i = t + q * T;
+    float4 a0, a1, b0, b1;
+    if constexpr (PAIRY) {
+      // row pairs: Y_p[k2/2][i][k2%2] (fr, mg, m0 even)
+      const float2* yi = yk + 2 * i;
+      a0 = *reinterpret_cast<const float4*>(yi + (fr >> 1) * (2 * L));
+      a1 = *reinterpret_cast<const float4*>(yi + ((fr >> 1) + 1) * (2 * L));
+      b0 = *reinterpret_cast<const float4*>(yi + (mg >> 1) * (2 * L));
+      b1 = *reinterpret_cast<const float4*>(yi + ((mg >> 1) + 1) * (2 * L));
+      x[4][q] = yi[((fr >> 1) + 2) * (2 * L)];
+      x[5][q] = yi[(m0 >> 1) * (2 * L)];
+    } else {
+      // tiled Y: Y_t[i/8][k2/8][i%8][k2%8]
+      const float2* yi = yk + static_cast<uint64_t>(i >> 3) * (8 * n2) + (i & 7) * 8;
+      const float4* a = reinterpret_cast<const float4*>(yi + (fr >> 3) * 64 + (fr & 7));
+      const float4* b = reinterpret_cast<const float4*>(yi + (mg >> 3) * 64 + (mg & 7));
+      a0 = a[0];
+      a1 = a[1];
+      b0 = b[0];
+      b1 = b[1];
+      x[4][q] = yi[((fr + 4) >> 3) * 64 + ((fr + 4) & 7)];
+      x[5][q] = yi[(m0 >> 3) * 64 + (m0 & 7)];
+    }
+    x[0][q] = make_float2(a0.x, a0.y);
+    x[1][q] = make_float2(a0.z, a0.w);
+    x[2][q] = make_float2(a1.x, a1.y);
+    x[3][q] = make_float2(a1.z, a1.w);
+    x[9][q] = make_float2(b0.x, b0.y);
+    x[8][q] = make_float2(b0.z, b0.w);
+    x[7][q] = make_float2(b1.x, b1.y);
+    x[6][q] = make_float2(b1.z, b1.w);
+  }
+  // (every load is issued before the first use of a loaded value)
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int q = 0; q < kPts; ++q) {
+    // mirror channels: conj(u_r) = W^{i} conj(Y_{n2-r}) (pair-row 0: conj(Y_0))
+    const float2 w = q == 0 ? wt : cmul(wt, make_float2(kCos8[q], -kSin8[q]));
+#pragma unroll
+    for (int c = NP; c < CPT; ++c) {
+      const float2 y = make_float2(x[c][q].x, -x[c][q].y);
+      x[c][q] = (c == NP && v == 0) ? y : cmul(w, y);
+    }
+  }
+  trace_event(1);
+  fft_stages<L, CPT, C::CG, 1>(x, lds, t, tab + to.n1);
+  trace_event(9);
+
+  const float* st = o.stats + (o.tsrc ? 4 * static_cast<uint64_t>(o.tsrc[k]) : 0);
+  const float mean = st[0] * o.nscale;
+  const float sigma = st[2] * o.nscale;
+  const float rsig = 1.0f / sigma;  // per bin dev::div_rn: IEEE division
+  float2 hr[NP];                    // e^{-i pi r / M}, r = 4v .. 4v+4 (workgroup-uniform)
+#pragma unroll
+  for (int c = 0; c < NP; ++c) hr[c] = tab[to.hr + fr + c];
+  const uint32_t M = static_cast<uint32_t>(L) * n2;
+  float4* pk = reinterpret_cast<float4*>(o.P + static_cast<uint64_t>(k) * o.pstride);
+  uint8_t* qk = o.Q + static_cast<uint64_t>(k) * o.qstride + kSpecQShift;  // qk[b]: bin b
+  // A fresh copy of t: without it the compiler keeps the load phase's per-q
+  // indices alive across the FFT (spilled to scratch, and every reload then
+  // waited behind the Q/P stores already in flight: one vmcnt queue).
+  // The output phase issues no vector load at all.
+  uint32_t tt = static_cast<uint32_t>(t);
+  asm volatile("" : "+v"(tt));
+  // e^{-i pi k1 / L} = e^{-i pi t / L} e^{-i pi q / 8} (k1 = t + q T), formed per q
+  float2 ht = tab[to.hk + tt];
+  asm volatile("" : "+v"(ht.x), "+v"(ht.y));
+  // Scaled forms (all factors exact powers of two): with e = z + w and
+  // d = z - w (w = conj Z[M-k], as the mirror channel holds it), 2 X[k] =
+  // e + (A, B) and 2 X[M-k] = (e.x - A, B - e.y), A = c d.y + s d.x,
+  // B = s d.y - c d.x ((c, s) = e^{-i pi k / M}); interbinning the doubled
+  // values doubles the amplitude, so P = (amp2 - 2 mean) / (2 sigma) rounds
+  // exactly as (amp - mean) / sigma.
+  const float mean2 = 2.0f * mean, sigma2 = 2.0f * sigma, rsig2 = 0.5f * rsig;
+#pragma unroll
+  for (int q = 0; q < kPts; ++q) {
+    // (one iteration at a time: interleaving them raised the register peak into scratch spills)
+    __builtin_amdgcn_sched_barrier(0);
+    const uint32_t k1 = tt + q * T;
+    const float2 hk = q == 0 ? ht : cmul(ht, make_float2(kCos16[q], -kSin16[q]));  // e^{-i pi k1 / L}
+    float2 X[NP], Xm[NP];
+#pragma unroll
+    for (int c = 0; c < NP; ++c) {
+      const float2 tw = cmul(hk, hr[c]);  // e^{-i pi (r + n2 k1) / M}
+      const float2 z = x[c][q], w = x[NP + c][q];
+      const float2 e = make_float2(z.x + w.x, z.y + w.y);
+      const float2 d = make_float2(z.x - w.x, z.y - w.y);
+      const float A = __builtin_fmaf(tw.x, d.y, tw.y * d.x);
+      const float B = __builtin_fmaf(tw.y, d.y, -(tw.x * d.x));
+      X[c] = make_float2(e.x + A, e.y + B);
+      Xm[c] = make_float2(e.x - A, B - e.y);
+    }
+    // interbinned amplitude (bin_interbin: max(|X|^2, |X - X_left|^2 / 2)), hardware sqrt
+    auto amp = [](float2 a, float2 l) {
+      const float p2 = __builtin_fmaf(a.x, a.x, a.y * a.y);
+      const float dx = a.x - l.x, dy = a.y - l.y;
+      const float q2 = __builtin_fmaf(dx, dx, dy * dy) * 0.5f;
+      return __builtin_amdgcn_sqrtf(fmaxf(p2, q2));
+    };
+    float pp[4], pm[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      pp[j] = dev::div_rn(amp(X[j + 1], X[j]) - mean2, sigma2, rsig2);
+      pm[j] = dev::div_rn(amp(Xm[j], Xm[j + 1]) - mean2, sigma2, rsig2);
+    }
+    pk[2 * v * L + k1] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    pk[(2 * v + 1) * L + k1] = make_float4(pm[0], pm[1], pm[2], pm[3]);
+    // screening bytes (dev::q8): t = rint(4 p) + 127 -> t in [0, 253] as is,
+    // >= 254 or NaN -> 254, <= -1 -> 255 (min first: NaN -> 254)
+    auto qb = [](float p) {
+      const float t = fmaxf(fminf(rintf(p * 4.0f) + 127.0f, 254.0f), -1.0f);
+      return static_cast<uint32_t>(static_cast<int>(t)) & 0xffu;
+    };
+    const uint32_t qa = qb(pp[0]) | (qb(pp[1]) << 8) | (qb(pp[2]) << 16) | (qb(pp[3]) << 24);
+    const uint32_t qm = qb(pm[3]) | (qb(pm[2]) << 8) | (qb(pm[1]) << 16) | (qb(pm[0]) << 24);
+    *reinterpret_cast<uint32_t*>(qk + fr + 1 + n2 * k1) = qa;        // bins fr+1 .. fr+4 (+ n2 k1)
+    *reinterpret_cast<uint32_t*>(qk + (M - n2 * k1 - fr - 3)) = qm;  // bins M - n2 k1 - (fr+3 .. fr)
+    if (v == 0 && k1 == 0) {  // bin 0: X[-1] = 0 (bin_interbin)
+      const float p0 = dev::div_rn(amp(X[0], make_float2(0.f, 0.f)) - mean2, sigma2, rsig2);
+      o.P[static_cast<uint64_t>(k) * o.pstride + M] = p0;
+      qk[0] = static_cast<uint8_t>(qb(p0));
+    }
+  }
+  trace_event(11);
+}
+
 bool supported_len(int L) { return L >= 128 && L <= 4096 && (L & (L - 1)) == 0; }
 
 }  // namespace
@@ -803,6 +1014,8 @@ std::vector<float2> fft4_tables(const Fft4Geom& g) {
   const uint64_t Mi = static_cast<uint64_t>(g.n1) * static_cast<uint64_t>(g.n2);
   for (uint64_t col = 0; col < static_cast<uint64_t>(g.n1); ++col)
     for (uint64_t k2 = 0; k2 < GX; ++k2) t[o.ox + col * GX + k2] = w(static_cast<double>((col * PX * k2) % Mi), M);
+  for (int k1 = 0; k1 < g.n1; ++k1) t[o.hk + k1] = w(0.5 * k1, g.n1);
+  for (int r = 0; r <= g.n2 / 2; ++r) t[o.hr + r] = w(0.5 * r, M);
   return t;
 }
 
@@ -878,6 +1091,38 @@ void launch_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const 
 
 }  // namespace
 
+void fft4_rowpass_spectrum(const float2* Y, int K, const Fft4Geom& g, const float2* tables, const SpecOut& o,
+                           hipStream_t s) {
+  PSOUP_CHECK(g.ok && K >= 1 && g.n2 >= 16 && g.n1 >= 128, "fft4 spectrum pass: bad geometry");
+  const uint64_t M = static_cast<uint64_t>(g.n1) * g.n2;
+  PSOUP_CHECK(M < (1ull << 31), "fft4 spectrum pass: spectrum too long for 32-bit bin indices");
+  const int f = g_fft4_flags;
+  PSOUP_CHECK((f & kFft4Blocked) && (f & kFft4TileY), "fft4 spectrum pass: needs the tiled Y layout");
+  PSOUP_CHECK(o.P && o.Q && o.stats && o.pstride >= M + 1 && o.pstride % 4 == 0 && o.qstride >= M + 1 + kSpecQShift &&
+                  o.qstride % 16 == 0 && (reinterpret_cast<uintptr_t>(o.P) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(o.Q) & 15) == 0 && (reinterpret_cast<uintptr_t>(Y) & 15) == 0,
+              "fft4 spectrum pass: output layout");
+  const uint64_t nblocks = static_cast<uint64_t>(g.n2 / 8) * ((static_cast<uint64_t>(K) + 7) / 8 * 8);
+  PSOUP_CHECK(nblocks < (1ull << 31), "fft4 spectrum pass: grid");
+  const dim3 grid(static_cast<unsigned>(nblocks));
+  PSOUP_CHECK(!g.ypair || fft4_pair_y(g), "fft4 spectrum pass: the row-pair Y layout needs the one-exchange pass A");
+  switch (g.n1) {
+#define PS_CASE(LL)                                                                                         \
+  case LL:                                                                                                  \
+    if (g.ypair)                                                                                            \
+      fft4_rowpass_spectrum_kernel<LL, true><<<grid, Cfg<LL, 2 * kSpecNp, 1>::THREADS, 0, s>>>(Y, K, g, tables, o); \
+    else                                                                                                    \
+      fft4_rowpass_spectrum_kernel<LL, false><<<grid, Cfg<LL, 2 * kSpecNp, 1>::THREADS, 0, s>>>(Y, K, g, tables, o); \
+    break;
+    PS_CASE(128) PS_CASE(256) PS_CASE(512) PS_CASE(1024) PS_CASE(2048) PS_CASE(4096)
+#undef PS_CASE
+    default: PSOUP_THROW("fft4 spectrum pass: unsupported row length " << g.n1);
+  }
+  post_launch_check("fft4_rowpass_spectrum_kernel", s);
+}
+
+bool fft4_pair_y(const Fft4Geom& g) { return g.ok && onex_colpass(g.n2, g_fft4_flags); }
+
 void fft4_set_flags(int flags) {
   g_fft4_flags = flags;
   set_numerics_flag("fft4_flags", flags);
@@ -913,6 +1158,7 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 16 == 0, "fft4 colpass: grid");
   PSOUP_CHECK(!(f & kFft4GroupXcd) || (K & 7) != 0 || nblocks % 128 == 0, "fft4 colpass: group grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
+  PSOUP_CHECK(!g.ypair || onex_colpass(g.n2, f), "fft4 colpass: the row-pair Y layout needs the one-exchange pass A");
   if (onex_colpass(g.n2, f))
     fft4_colpass_onex_kernel<2048, 64, 4><<<grid, OneX<2048, 64, 4>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g,
                                                                                     tables, f);

@@ -855,7 +855,11 @@ __device__ __forceinline__ float2 x_canon(const float2* __restrict__ z, uint32_t
   return r2c_combine(za, zb, up ? tw.x : -tw.x, tw.y);
 }
 
-template <int NLEV, int BPT, bool FROMX>
+// SRC: where the exact sums read a bin -- 0: P (natural order), 1:
+// recomputed from the tiled spectrum X (HarmFromX), 2: the blocked P of
+// fft4_rowpass_spectrum (spec_pblk_index).  Q rows start fx.qshift bytes
+// before bin 0 (staging chunks stay 16-byte aligned in memory).
+template <int NLEV, int BPT, int SRC>
 __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __restrict__ P, uint64_t pstride,
                                                                 const uint8_t* __restrict__ Q, uint64_t qstride,
                                                                 int lo, int hi, HarmParams hp,
@@ -875,8 +879,10 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
     k = static_cast<int>(bid / ntiles);
     tile = static_cast<int>(bid % ntiles);
   }
+  constexpr bool FROMX = SRC == 1;
   const float* p = FROMX ? nullptr : P + static_cast<uint64_t>(k) * pstride;
-  const uint8_t* q = Q + static_cast<uint64_t>(k) * qstride;
+  const int qs = fx.qshift;
+  const uint8_t* q = Q + static_cast<uint64_t>(k) * qstride + qs;  // q[b]: bin b; q + a aligned iff (a + qs) % 16 == 0
   const int t = threadIdx.x;
   const int b0 = lo + tile * B;
   const int last = hi - 1;
@@ -890,7 +896,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
     for (int h = 1; h <= NLEV; ++h) {
 #pragma unroll
       for (int m = 1; m < (1 << h); m += 2) {
-        const int r0 = ((b0 * m + (1 << (h - 1))) >> h) & ~15;
+        const int r0 = ((((b0 * m + (1 << (h - 1))) >> h) + qs) & ~15) - qs;
 #pragma unroll
         for (int e = 0; e < (Tl::chunks(h, m) + 255) / 256; ++e, ++it)
           tmp[it] = load_q16(q, r0 + 16 * (t + 256 * e), last);
@@ -917,7 +923,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
   const int i0 = b0 + t;
   // byte offset in LDS of term (h, m) of bin i0; bin i0 + 256 u adds u * (m << (8 - h))
 #define PS_QBASE(h, m) \
-  (Tl::offset(Tl::region(h, m)) + (((i0 * (m) + (1 << ((h) - 1))) >> (h)) - (((b0 * (m) + (1 << ((h) - 1))) >> (h)) & ~15)))
+  (Tl::offset(Tl::region(h, m)) + (((i0 * (m) + (1 << ((h) - 1))) >> (h)) - (((((b0 * (m) + (1 << ((h) - 1))) >> (h)) + qs) & ~15) - qs)))
   int base[Tl::NREG];
   if constexpr (NLEV >= 1) base[1] = PS_QBASE(1, 1);
   if constexpr (NLEV >= 2) {
@@ -997,6 +1003,8 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
       const float2 x0 = x_canon(z, ub, M, fx.log2_n2, fx.n1, fx.rt);
       const float2 xl = ub > 0 ? x_canon(z, ub - 1, M, fx.log2_n2, fx.n1, fx.rt) : make_float2(0.f, 0.f);
       return dev::div_rn(dev::interbin(x0, xl) - mean, sigma, rsig);
+    } else if constexpr (SRC == 2) {
+      return p[spec_pblk_index(static_cast<uint32_t>(b), fx.log2_n2, fx.n1)];
     } else {
       return p[b];
     }
@@ -1167,21 +1175,13 @@ __global__ void __launch_bounds__(256) c2r_post_kernel(const float2* __restrict_
 
 namespace {
 // bit 0: XCD-per-trial block order; bit 1: no pre-threshold (testing);
-// bit 2: nontemporal fundamental loads (tuning); bit 3: 1024-bin tiles at
-// 3 levels (tuning); bit 4: the LDS-plane r2c form; bit 5: two-phase
-// harmonic staging at 3 levels (tuning); bits 8-15: extra dynamic LDS per
-// workgroup in KiB for the two-phase 3-level kernel only (tuning: caps
-// workgroups per CU, so fewer tiles -- a smaller gather footprint -- are in
-// flight per XCD; the one-phase kernels of the other levels are not capped);
-// bits 16-23: the same for the tiled r2c kernel (tuning)
-// Default 1 | 32 | (10 << 8): XCD order, two-phase staging at 3 levels,
-// 6 workgroups per CU (ABBA same-box bench: 22.55k vs 22.47k trials/s for the
-// one-phase kernel, every pair; profiles/r2_recheck/ab_harm_abba.txt)
-// default: XCD trial order, screened sum recomputing its exact bins from the
-// spectrum (no P stored: bench +3.9% over storing P, +10.3% over the fp32
-// kernel on the same box, profiles/r4_screen), 3-level fp32 kernel in two
-// staging phases with a 10 KiB occupancy cap
-int g_harm_flags = 1 | 8 | 32 | (10 << 8);
+// bit 2: the search engine's screened sum off; bit 3: its exact sums
+// recomputed from the spectrum X (unfused engines); bit 5: the fp32 3-level
+// kernel in two staging phases; bit 6: the engine's fused spectrum pass
+// (fft4_rowpass_spectrum: pass B writes P and Q, no X and no r2c pass);
+// bits 8-15: dynamic-LDS occupancy cap in KiB of the two-phase kernel.
+// Engines read bits 2, 3 and 6 when they are built.
+int g_harm_flags = 1 | 8 | 32 | 64 | (10 << 8);
 
 // Mixed-radix n = m p (p a power of two, m odd): gather of the m strided
 // columns, and the length-m combination with the twiddles W_n^(n1 k)
@@ -1421,26 +1421,45 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
     for (int h = 0; h < 6; ++h) {
       const double n = std::ldexp(1.0, h);
       const double x = 4.0 * (static_cast<double>(pre.lo[h]) - n / 8.0 - 0.25) + 127.0 * n;
-      lim.v[h] = std::isfinite(x) ? static_cast<int>(std::floor(x)) - 1 : INT_MIN;
+      // above INT_MAX no byte sum passes; below INT_MIN + 1 every bin does (no UB in the cast)
+      const double fl = std::isfinite(x) ? std::floor(x) : x;
+      lim.v[h] = !(fl > static_cast<double>(INT_MIN) + 1.0) ? INT_MIN
+                 : fl >= static_cast<double>(INT_MAX)     ? INT_MAX
+                                                          : static_cast<int>(fl) - 1;
     }
     HarmFromX fxv;
+    int src = 0;
     if (fx) {
       fxv = *fx;
       const uint64_t M = static_cast<uint64_t>(fxv.n1) << fxv.log2_n2;
-      PSOUP_CHECK(fxv.X && fxv.rt && fxv.stats && fxv.n1 >= 16 && M < (uint64_t(1) << 31) &&
-                      static_cast<uint64_t>(hi) <= M + 1,
-                  "harmonic_peaks_batch: bad spectrum for the exact recompute");
+      PSOUP_CHECK(fxv.qshift >= 0 && fxv.qshift < 16 && qstride >= static_cast<uint64_t>(hi) + fxv.qshift,
+                  "harmonic_peaks_batch: screening row shift");
+      if (fxv.pblk) {
+        PSOUP_CHECK(P && fxv.n1 >= 16 && M < (uint64_t(1) << 31) && static_cast<uint64_t>(hi) <= M + 1 &&
+                        pstride >= M + 1,
+                    "harmonic_peaks_batch: bad blocked spectrum");
+        src = 2;
+      } else {
+        PSOUP_CHECK(fxv.X && fxv.rt && fxv.stats && fxv.n1 >= 16 && M < (uint64_t(1) << 31) &&
+                        static_cast<uint64_t>(hi) <= M + 1,
+                    "harmonic_peaks_batch: bad spectrum for the exact recompute");
+        src = 1;
+      }
     }
     auto oneq = [&](auto nl_c) {
       constexpr int NL = decltype(nl_c)::value, BP = NL <= 3 ? 8 : 4;
       const int nt = ntiles_of(HarmTileQ<NL, BP>::B);
       PSOUP_CHECK(static_cast<int64_t>(nt) * K < (int64_t(1) << 31), "harmonic grid too large");
-      if (fx)
-        harmonic_peaks_q8_kernel<NL, BP, true><<<dim3(static_cast<unsigned>(nt * K)), 256, 0, s>>>(
-            P, pstride, Q, qstride, lo, hi, hp, out, count, nt, xcd, lim, fxv);
+      const dim3 grid(static_cast<unsigned>(nt * K));
+      if (src == 1)
+        harmonic_peaks_q8_kernel<NL, BP, 1><<<grid, 256, 0, s>>>(P, pstride, Q, qstride, lo, hi, hp, out, count, nt,
+                                                                 xcd, lim, fxv);
+      else if (src == 2)
+        harmonic_peaks_q8_kernel<NL, BP, 2><<<grid, 256, 0, s>>>(P, pstride, Q, qstride, lo, hi, hp, out, count, nt,
+                                                                 xcd, lim, fxv);
       else
-        harmonic_peaks_q8_kernel<NL, BP, false><<<dim3(static_cast<unsigned>(nt * K)), 256, 0, s>>>(
-            P, pstride, Q, qstride, lo, hi, hp, out, count, nt, xcd, lim, fxv);
+        harmonic_peaks_q8_kernel<NL, BP, 0><<<grid, 256, 0, s>>>(P, pstride, Q, qstride, lo, hi, hp, out, count, nt,
+                                                                 xcd, lim, fxv);
     };
     switch (hp.nlevels) {
       case 0: oneq(std::integral_constant<int, 0>{}); break;

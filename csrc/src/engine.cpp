@@ -720,8 +720,11 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   // profiles/r3_fused/SUMMARY.md.)
   pst_ = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
   q8_ = mode_ == 2 && kern::fft4_x_layout(f4_).tiled && !(kern::harmonic_flags() & 4);
-  fromx_ = q8_ && (kern::harmonic_flags() & 8);
-  qst_ = q8_ ? (pst_ + 63) / 64 * 64 : 0;
+  // the fused spectrum pass (harmonic flag 64) writes every bin 0..M of P (blocked) and Q
+  fused_ = q8_ && (kern::harmonic_flags() & 64) && f4_.n2 >= 16 && f4_.n1 >= 128;
+  fromx_ = q8_ && !fused_ && (kern::harmonic_flags() & 8);
+  if (fused_) pst_ = (n_ / 2 + 1 + 63) / 64 * 64;
+  qst_ = q8_ ? (pst_ + (fused_ ? kern::kSpecQShift : 0) + 63) / 64 * 64 : 0;
   if (mode_ == 2) rt_ = kern::r2c_twiddle_table(n_ / 2);
   // batch size
   {
@@ -730,7 +733,7 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
       budget = std::min(budget, free_b / 10 * 7 / static_cast<size_t>(std::max(1, p_.engines_per_device)));
-    const size_t per = n_ * 4 + nb_ * 8 + (fromx_ ? 0 : pst_ * 4) + qst_;  // Y/res + X/spec + P + Q per trial
+    const size_t per = n_ * 4 + (fused_ ? 0 : nb_ * 8) + (fromx_ ? 0 : pst_ * 4) + qst_;  // Y/res + X/spec + P + Q per trial
     // at most 512 trials per batch from 2^23 samples up, 256 below (the
     // shorter series were only measured up to 256)
     const size_t kmax = n_ >= (uint64_t(1) << 23) ? 512 : 256;
@@ -835,7 +838,7 @@ void SearchEngine::ensure_batch_buffers(int k) {
     }
   const uint64_t rs = mode_ == 2 ? 2 * f4_.ystride : n_;  // floats per trial
   res_.resize(static_cast<uint64_t>(k) * rs);
-  spec_.resize(static_cast<uint64_t>(k) * xs_);
+  if (!fused_) spec_.resize(static_cast<uint64_t>(k) * xs_);
   if (!fromx_) P_.resize(static_cast<uint64_t>(k) * pst_);
   if (q8_) Q_.resize(static_cast<uint64_t>(k) * qst_);
 }
@@ -877,8 +880,30 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
       g.in_tstride = n_;
       g.pad_tstride = f4_.insize;
       g.tsrc = src;
+      g.ypair = fused_ && kern::fft4_pair_y(f4_);
       kern::fft4_resample_colpass(tim_.data(), f4_in_.data(), n_, af_.data() + first + b, c, Y, g, f4_tab_.data(),
                                   st);
+      if (fused_) {
+        PSOUP_CHECK(Q, "fft4 kernel flags changed under an engine with the fused spectrum pass");
+        kern::SpecOut so;
+        so.P = P;
+        so.pstride = pst;
+        so.Q = Q;
+        so.qstride = qst_;
+        so.stats = wstats_.data();
+        so.tsrc = src;
+        so.nscale = static_cast<float>(n_);
+        kern::fft4_rowpass_spectrum(Y, c, g, f4_tab_.data(), so, st);
+        fx.pblk = 1;
+        fx.qshift = kern::kSpecQShift;
+        fx.log2_n2 = ilog2(static_cast<uint64_t>(f4_.n2));
+        fx.n1 = static_cast<uint32_t>(f4_.n1);
+        RoctxRange r("Harmonic summing");
+        kern::HarmParams hp = hp_;
+        hp.trial_base = static_cast<uint32_t>(b);
+        kern::harmonic_peaks_batch(P, nb_, pst, c, hp, s.d_peaks.data(), s.d_count.data(), st, Q, qst_, &fx);
+        return;
+      }
       float2* X = spec_.data() + static_cast<uint64_t>(b) * xs_;
       kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st, static_cast<uint64_t>(hi_));
       if (xl.tiled) {

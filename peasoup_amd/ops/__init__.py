@@ -15,6 +15,9 @@ from .core import (  # noqa: F401
     dedisperse,
     deredden,
     fft4_resample_interbin,
+    fft4_spectrum_pass,
+    spec_unblock,
+    spec_pblk_index,
     fft4_resample_spectrum,
     fold_optimise,
     fold_series,

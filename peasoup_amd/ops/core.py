@@ -289,6 +289,61 @@ def fft4_resample_interbin(x: torch.Tensor, accels: Sequence[float], tsamp: floa
     return P
 
 
+def fft4_spectrum_pass(x: torch.Tensor, accels: Sequence[float], tsamp: float, stats: torch.Tensor,
+                       nscale: float, pair_y: bool | None = None):
+    """The search hot path with the fused spectrum pass (the default engine
+    path): fused resample + pass A, then pass B forming the normalised
+    interbinned spectrum and its screening bytes directly
+    (kernels.hpp fft4_rowpass_spectrum).  Returns (Pb, Q, g): Pb [K, pstride]
+    in the blocked layout (``spec_unblock`` gives natural order), Q [K,
+    qstride] uint8 with bin b at column ``spec_q_shift`` + b.  ``pair_y``:
+    pass A hands over Y in row pairs (default: where ``fft4_pair_y`` allows,
+    as the search engine does)."""
+    _check(x, torch.float32, "x")
+    n = x.numel()
+    g = K.fft4_geometry(n // 2)
+    if not g.ok or n % 2:
+        raise ValueError(f"fft4: unsupported length {n}")
+    M = g.n1 * g.n2
+    g.ypair = K.fft4_pair_y(g) if pair_y is None else bool(pair_y)
+    tab = torch.from_numpy(K.fft4_tables(g)).to(x.device)
+    af = _accel_factors(accels, tsamp, x.device)
+    Kb = len(accels)
+    xp = torch.empty(g.insize, dtype=torch.float32, device=x.device)
+    Y = torch.empty((Kb, g.ystride, 2), dtype=torch.float32, device=x.device)
+    K.fft4_pad_input(x.data_ptr(), n, xp.data_ptr(), g, _s())
+    K.fft4_resample_colpass(x.data_ptr(), xp.data_ptr(), n, af.data_ptr(), Kb, Y.data_ptr(), g, tab.data_ptr(), _s())
+    pst = (M + 1 + 63) // 64 * 64
+    qst = (M + 1 + K.spec_q_shift + 63) // 64 * 64
+    Pb = torch.zeros((Kb, pst), dtype=torch.float32, device=x.device)
+    Q = torch.zeros((Kb, qst), dtype=torch.uint8, device=x.device)
+    K.fft4_rowpass_spectrum(Y.data_ptr(), Kb, g, tab.data_ptr(), Pb.data_ptr(), pst, Q.data_ptr(), qst,
+                            stats.data_ptr(), float(nscale), _s())
+    return Pb, Q, g
+
+
+def spec_pblk_index(b: torch.Tensor, log2_n2: int, n1: int) -> torch.Tensor:
+    """kernels.hpp spec_pblk_index, vectorised: position of bins b (int64,
+    0..M) in the blocked spectrum of ``fft4_spectrum_pass``."""
+    n2 = 1 << log2_n2
+    M = n1 * n2
+    r = b & (n2 - 1)
+    prim = (r >= 1) & (r <= n2 // 2)
+    ip = (((r - 1) >> 2) * 2 * n1 + (b >> log2_n2)) * 4 + ((r - 1) & 3)
+    bm = M - b
+    rm = bm & (n2 - 1)
+    im = (((rm >> 2) * 2 + 1) * n1 + (bm >> log2_n2)) * 4 + (rm & 3)
+    out = torch.where(prim, ip, im)
+    return torch.where(b == 0, torch.full_like(b, M), out)
+
+
+def spec_unblock(Pb: torch.Tensor, g) -> torch.Tensor:
+    """Natural-order P [K, M + 1] from the blocked spectrum of ``fft4_spectrum_pass``."""
+    M = g.n1 * g.n2
+    b = torch.arange(M + 1, device=Pb.device, dtype=torch.int64)
+    return Pb[:, spec_pblk_index(b, g.log2_xrow, g.n1)]
+
+
 def resample_v1(x: torch.Tensor, accel: float, tsamp: float) -> torch.Tensor:
     _check(x, torch.float32, "x")
     af = (float(torch.tensor(accel, dtype=torch.float32)) * float(torch.tensor(tsamp, dtype=torch.float32))) / (2 * 299792458.0)
@@ -317,13 +372,16 @@ def quantize_q8(P: torch.Tensor) -> torch.Tensor:
 
 
 def harmonic_peaks(P: torch.Tensor, nlevels: int, starts: Sequence[int], ends: Sequence[int], thresh: float,
-                   capacity: int = 1 << 20, nbins: int | None = None, Q: torch.Tensor | None = None):
+                   capacity: int = 1 << 20, nbins: int | None = None, Q: torch.Tensor | None = None,
+                   pblk=None):
     """Fused harmonic sum + threshold: P [K, n] -> records (trial, level, idx, snr)
     as int64/float32 tensors sorted by (trial, level, idx) (the kernel's chunk
     descriptors, kernels.hpp kPeakChunk, are dropped).  ``nbins``: bins per
     spectrum when the rows are padded (default n).  ``Q``: screening bytes of
     P ([K, qstride] uint8, ``quantize_q8``) -- the screened kernel, same
-    records."""
+    records.  ``pblk`` = the geometry ``g`` of ``fft4_spectrum_pass``: P is
+    its blocked spectrum and Q its screening rows (bins shifted by
+    ``spec_q_shift``)."""
     _check(P, torch.float32, "P")
     Kb, n = P.shape
     rec = torch.empty((capacity, 3), dtype=torch.int32, device=P.device)
@@ -332,12 +390,15 @@ def harmonic_peaks(P: torch.Tensor, nlevels: int, starts: Sequence[int], ends: S
     if Q is not None:
         if Q.dtype != torch.uint8 or Q.shape[0] != Kb or not Q.is_contiguous():
             raise ValueError("Q must be a contiguous [K, qstride] uint8 tensor")
+    extra = {}
+    if pblk is not None:
+        extra = dict(pblk_log2_n2=pblk.log2_xrow, pblk_n1=pblk.n1, qshift=K.spec_q_shift)
     K.harmonic_peaks_batch(P.data_ptr(), nb, n, Kb, nlevels, list(starts), list(ends), float(thresh), capacity,
                            rec.data_ptr(), cnt.data_ptr(), _s(), 0 if Q is None else Q.data_ptr(),
-                           0 if Q is None else Q.shape[1])
+                           0 if Q is None else Q.shape[1], **extra)
     c = int(cnt.item())
     if c > capacity:
-        return harmonic_peaks(P, nlevels, starts, ends, thresh, capacity=c + 1024, nbins=nbins, Q=Q)
+        return harmonic_peaks(P, nlevels, starts, ends, thresh, capacity=c + 1024, nbins=nbins, Q=Q, pblk=pblk)
     r = rec[:c]
     r = r[r[:, 0] >= 0]  # drop the chunk descriptors (seg field with kPeakChunk, bit 31, set)
     seg = r[:, 0].to(torch.int64)

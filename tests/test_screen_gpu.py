@@ -83,9 +83,11 @@ def test_tiled_r2c_writes_screening_bytes(log2n):
 
 
 def test_engine_screen_equals_exact():
-    """SearchEngine with the screened harmonic sum (default), without it
-    (harmonic flag 4) and with the exact sums recomputed from the spectrum
-    instead of a stored P (flag 8) gives identical candidates."""
+    """SearchEngine on the unfused spectrum path with the screened harmonic
+    sum, without it (harmonic flag 4) and with the exact sums recomputed from
+    the spectrum instead of a stored P (flag 8) gives identical candidates;
+    the fused spectrum pass (flag 64, the default) the same candidates with
+    S/N equal to FFT rounding (its mirror bins come from another transform)."""
     import peasoup_amd._C as C
 
     rng = np.random.default_rng(5)
@@ -98,8 +100,10 @@ def test_engine_screen_equals_exact():
     accs = [float(a) for a in np.linspace(-40, 40, 17)]
     out = []
     old = C.kernels.harmonic_flags()
+    unf = old & ~64
     try:
-        for flags in (old & ~8, old | 4, old | 8):  # P stored / screen off / bins recomputed (default)
+        # P stored / screen off / bins recomputed / fused (default)
+        for flags in (unf & ~8, unf | 4, unf | 8, old | 64):
             C.kernels.harmonic_set_flags(flags)
             p = C.SearchParams()
             p.fft_size, p.tsamp, p.nharmonics = 1 << 21, 64e-6, 4
@@ -109,3 +113,7 @@ def test_engine_screen_equals_exact():
     finally:
         C.kernels.harmonic_set_flags(old)
     assert out[0] == out[1] == out[2] and len(out[0]) > 0
+    fused = sorted(out[3], key=lambda r: (r[0], r[1], r[2], r[4]))
+    ref = sorted(out[0], key=lambda r: (r[0], r[1], r[2], r[4]))
+    assert [(r[0], r[1], r[2], r[4], r[5]) for r in fused] == [(r[0], r[1], r[2], r[4], r[5]) for r in ref]
+    assert all(abs(a[3] - b[3]) <= 1e-4 * abs(b[3]) for a, b in zip(fused, ref))

@@ -12,7 +12,8 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from peasoup_amd import _C  # noqa: E402
 
 K_ = _C.kernels
-NAMES = ["start", "loads issued", "stage0", "exch1", "stage1", "exch2", "stage2", "exch3", "stage3", "-", "-", "end"]
+NAMES = ["start", "loads issued", "stage0", "exch1", "stage1", "exch2", "stage2", "exch3", "stage3", "fft done", "-",
+         "end"]
 ONEX_NAMES = ["start", "loads issued", "dftP+tw", "exchange", "dftG", "-", "-", "-", "-", "-", "-", "end"]
 
 
@@ -56,7 +57,14 @@ def main():
     col = lambda: K_.fft4_resample_colpass(x.data_ptr(), xp.data_ptr(), n, af.data_ptr(), K, Y.data_ptr(), g,
                                            tab.data_ptr(), s)
     row = lambda: K_.fft4_rowpass(Y.data_ptr(), X.data_ptr(), K, g, tab.data_ptr(), s)
-    for name, fn in (("colpass", col), ("rowpass", row)):
+    pst = (M + 1 + 63) // 64 * 64
+    qst = (M + 1 + K_.spec_q_shift + 63) // 64 * 64
+    Pb = torch.empty(K * pst, device=dev)
+    Qb = torch.empty(K * qst, dtype=torch.uint8, device=dev)
+    st = torch.tensor([1.0, 2.0, 0.5, 0.0], device=dev)
+    spec = lambda: K_.fft4_rowpass_spectrum(Y.data_ptr(), K, g, tab.data_ptr(), Pb.data_ptr(), pst, Qb.data_ptr(), qst,
+                                            st.data_ptr(), float(n), s)
+    for name, fn in (("colpass", col), ("rowpass", row), ("rowpass_spectrum", spec)):
         fn()
         fn()
         torch.cuda.synchronize()

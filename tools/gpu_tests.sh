@@ -1,7 +1,11 @@
 #!/bin/bash
+# GPU-box helper: pytest -m gpu on the given test files (default: all), log
+# under gpurun_out/${OUT:-tests}/pytest.log.
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1
+O=gpurun_out/${OUT:-tests}
+mkdir -p $O
+timeout -k 10 1000 python -u -m pytest ${@:-tests} -m gpu -x -v -p no:cacheprovider --timeout 240 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?
-tail -40 gpurun_out/pytest_gpu.log
+grep -E "PASSED|FAILED|ERROR" $O/pytest.log | tail -15
+tail -3 $O/pytest.log
 exit $rc

@@ -37,7 +37,7 @@ def main():
     ap.add_argument("--log2n", type=int, default=23)
     ap.add_argument("--K", type=int, default=32)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--flags", default="0,1,259,3331")
+    ap.add_argument("--flags", default="")
     a = ap.parse_args()
     dev = torch.device("cuda")
     n = 1 << a.log2n
@@ -72,7 +72,7 @@ def main():
     report("pad_input", timeit(lambda: K_.fft4_pad_input(x.data_ptr(), n, xp.data_ptr(), g, s), a.reps) * K,
            2 * 4 * n)
     f_default = K_.fft4_flags()
-    for f in [int(v) for v in a.flags.split(",")]:
+    for f in [int(v) for v in a.flags.split(",") if v] or [f_default]:
         K_.fft4_set_flags(f)
         tc = timeit(lambda: K_.fft4_resample_colpass(x.data_ptr(), xp.data_ptr(), n, af.data_ptr(), K, Y.data_ptr(), g,
                                                      tab.data_ptr(), s), a.reps)
@@ -95,6 +95,25 @@ def main():
     report("r2c_interbin_normalise tiled + screening bytes", tz, K * (8 * M + 5 * M))
     del Qr
     K_.fft4_set_flags(f_default)
+    # fused spectrum pass (the default search path): Y -> blocked P + Q
+    pst = (M + 1 + 63) // 64 * 64
+    qst2 = (M + 1 + K_.spec_q_shift + 63) // 64 * 64
+    Pb = torch.empty(K * pst, device=dev)
+    Qb = torch.empty(K * qst2, dtype=torch.uint8, device=dev)
+    tz = timeit(lambda: K_.fft4_rowpass_spectrum(Y.data_ptr(), K, g, tab.data_ptr(), Pb.data_ptr(), pst, Qb.data_ptr(),
+                                                 qst2, st.data_ptr(), float(n), s), a.reps)
+    for pair in (False, True) if K_.fft4_pair_y(g) else (False,):
+        g.ypair = pair
+        K_.fft4_resample_colpass(x.data_ptr(), xp.data_ptr(), n, af.data_ptr(), K, Y.data_ptr(), g, tab.data_ptr(), s)
+        tz = timeit(lambda: K_.fft4_rowpass_spectrum(Y.data_ptr(), K, g, tab.data_ptr(), Pb.data_ptr(), pst,
+                                                     Qb.data_ptr(), qst2, st.data_ptr(), float(n), s), a.reps)
+        report(f"rowpass_spectrum ypair={int(pair)}", tz, K * (8 * M + 5 * M))
+        if pair:
+            tc = timeit(lambda: K_.fft4_resample_colpass(x.data_ptr(), xp.data_ptr(), n, af.data_ptr(), K,
+                                                         Y.data_ptr(), g, tab.data_ptr(), s), a.reps)
+            report("colpass ypair=1", tc, K * 8 * M)
+    g.ypair = False
+    del Pb, Qb
     # harmonic peaks on normal noise (threshold 9 -> few peaks)
     P.normal_()
     nb = M + 1
