@@ -24,6 +24,37 @@ from __future__ import annotations
 import sys
 
 
+def _fail_hard(what: str, e: BaseException) -> None:
+    """A failed rank must not leave its peers blocked in a collective: report
+    with rank context and exit hard, which destroys this rank's RCCL
+    communicator (the ncclCommAbort equivalent) and makes torchrun stop -- or,
+    with --max-restarts, restart -- the worker group (a restart with
+    --checkpoint_dir resumes from the per-DM spill files).  When a peer failed
+    first (this rank's collective broke with it), the peer's record is
+    reported instead of the broken connection."""
+    import os
+    import traceback
+
+    from .parallel import dist as pdist
+
+    rank = os.environ.get("RANK", "0")
+    peer = pdist.peer_failure()
+    if peer is not None:
+        print(f"[rank {rank}] aborting: peer failure: {peer}", file=sys.stderr)
+        sys.stderr.flush()
+        if rank == "0":
+            import time
+
+            time.sleep(2.0)  # rank 0 hosts the store: let the other peers read the record
+        os._exit(3)
+    print(f"[rank {rank}] {what} failed: {e}", file=sys.stderr)
+    pdist.report_failure(f"{type(e).__name__}: {e}")
+    traceback.print_exc()
+    sys.stderr.flush()
+    sys.stdout.flush()
+    os._exit(1)
+
+
 def main(argv=None) -> int:
     from . import _C
     from .models.search import run_search
@@ -44,31 +75,7 @@ def main(argv=None) -> int:
     try:
         res = run_search(args)
     except BaseException as e:  # noqa: BLE001 - any failure must tear the job down
-        # A failed rank must not leave its peers blocked in a collective: report
-        # with rank context and exit hard, which destroys this rank's RCCL
-        # communicator (the ncclCommAbort equivalent) and makes torchrun stop
-        # -- or, with --max-restarts, restart -- the worker group.  A restart
-        # with --checkpoint_dir resumes from the per-DM spill files.
-        import os
-        import traceback
-
-        rank = os.environ.get("RANK", "0")
-        peer = pdist.peer_failure()
-        if peer is not None:
-            # a peer failed first and this rank's collective broke with it
-            print(f"[rank {rank}] aborting: peer failure: {peer}", file=sys.stderr)
-            sys.stderr.flush()
-            if rank == "0":
-                import time
-
-                time.sleep(2.0)  # rank 0 hosts the store: let the other peers read the record
-            os._exit(3)
-        print(f"[rank {rank}] peasoup failed: {e}", file=sys.stderr)
-        pdist.report_failure(f"{type(e).__name__}: {e}")
-        traceback.print_exc()
-        sys.stderr.flush()
-        sys.stdout.flush()
-        os._exit(1)
+        _fail_hard("peasoup", e)
     if res is not None and (args.verbose or args.progress_bar):
         print(f"Wrote {len(res.candidates)} candidates to {args.outdir}; "
               f"{res.performance['dm_accel_trials_per_sec']:.1f} DMxaccel trials/s over {int(res.performance['ranks'])} rank(s)")
@@ -90,13 +97,7 @@ def _main_ffa(argv) -> int:
     try:
         res = run_ffa_search(args)
     except BaseException as e:  # noqa: BLE001 - same teardown policy as the search
-        import os
-        import traceback
-
-        print(f"[rank {os.environ.get('RANK', '0')}] ffa failed: {e}", file=sys.stderr)
-        traceback.print_exc()
-        sys.stderr.flush()
-        os._exit(1)
+        _fail_hard("ffa", e)
     if res is not None and args.verbose:
         print(f"Wrote {len(res.candidates)} FFA candidates to {args.outfilename}")
     pdist.shutdown()

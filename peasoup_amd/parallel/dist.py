@@ -27,7 +27,7 @@ surviving ranks blocked in a collective when one rank fails:
   the process with exit code 3 -- which tears down its RCCL communicator (the
   ``ncclCommAbort`` equivalent) instead of waiting in a collective;
 * every collective is also bounded by the process-group timeout
-  (``PSOUP_COLLECTIVE_TIMEOUT``, default 300 s) as the last backstop.
+  (``PSOUP_COLLECTIVE_TIMEOUT``, default 1800 s) as the last backstop.
 No re-exec and no in-process restart: recovery is a re-run (or torchrun's
 ``--max-restarts``) with ``--checkpoint_dir``, which resumes from the per-DM
 spill files.
@@ -103,6 +103,8 @@ class _Watchdog(threading.Thread):
                         self._abort(f"peer failure: {msg}")
                     return
                 now = time.monotonic()
+                for r in [r for r in seen if self.store.check([f"psoup/done/{r}"])]:
+                    del seen[r]  # finished cleanly (shutdown): its heartbeat stops on purpose
                 for r, (last, since) in seen.items():
                     key = f"psoup/hb/{r}"
                     cur = int(self.store.get(key)) if self.store.check([key]) else -1
@@ -182,7 +184,10 @@ def init(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> Di
     if _CTX is not None:
         return _CTX
     if timeout_s is None:
-        timeout_s = float(os.environ.get("PSOUP_COLLECTIVE_TIMEOUT", "300"))
+        # a last backstop only: peer death is caught by the heartbeat watchdog,
+        # and collectives legitimately wait long (rank 0 reading a large
+        # filterbank before the broadcast, shard imbalance before a gather)
+        timeout_s = float(os.environ.get("PSOUP_COLLECTIVE_TIMEOUT", "1800"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
@@ -228,7 +233,13 @@ def shutdown() -> None:
     global _CTX, _WATCHDOG
     if _WATCHDOG is not None:
         # peers may finish (and stop beating) before this rank: a clean
-        # shutdown ends the watch first
+        # shutdown first marks this rank done (the peers' watches stop
+        # expecting its heartbeat -- rank 0 may still be writing outputs long
+        # after the others got here), then ends its own watch
+        try:
+            _WATCHDOG.store.set(f"psoup/done/{_WATCHDOG.rank}", "1")
+        except Exception:  # noqa: BLE001 - the store is gone: the barrier below reports it
+            pass
         _WATCHDOG.stop.set()
         _WATCHDOG.join(timeout=5)
         _WATCHDOG = None

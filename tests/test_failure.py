@@ -39,6 +39,13 @@ if mode == "clean":
     pdist.all_reduce_sum(t)
     pdist.shutdown()
     sys.exit(0)
+if mode == "slowroot":
+    # the others are done; rank 0 keeps working (writing outputs) for longer
+    # than the peer timeout with its watchdog live, then shuts down
+    if ctx.rank == 0:
+        time.sleep(float(os.environ["PSOUP_PEER_TIMEOUT"]) * 2.5)
+    pdist.shutdown()
+    sys.exit(0)
 pdist.barrier()  # rank 1 never arrives
 print("barrier passed", flush=True)
 """
@@ -103,4 +110,14 @@ def test_clean_run_exits_zero(tmp_path):
     res, _ = _run(tmp_path, "clean", {"PSOUP_PEER_TIMEOUT": "4"})
     for r, (rc, out, err) in enumerate(res):
         assert rc == 0, (r, err[-2000:])
+        assert "aborting" not in err
+
+
+def test_slow_root_after_peers_finish_exits_zero(tmp_path):
+    """Peers that reached shutdown() stop beating on purpose: rank 0, still
+    busy past PSOUP_PEER_TIMEOUT with its watchdog running, must not declare
+    them dead (a false abort before the outputs are written)."""
+    res, dt = _run(tmp_path, "slowroot", {"PSOUP_PEER_TIMEOUT": "2"})
+    for r, (rc, out, err) in enumerate(res):
+        assert rc == 0, (r, rc, err[-2000:])
         assert "aborting" not in err

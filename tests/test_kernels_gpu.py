@@ -553,10 +553,16 @@ def test_auto_short_list_balancing_matches_fixed_batch(C):
         p = C.SearchParams()
         p.fft_size, p.tsamp, p.nharmonics, p.min_snr = n, tsamp, 3, 6.0
         if auto:
-            # budget of exactly 64 trials (Y + X + P + screening bytes per trial; the search range covers
-            # all bins)
+            # budget of exactly 64 trials: Y + blocked P + screening bytes per trial with the fused
+            # spectrum pass (harmonic flag 64, the default), else Y + X + P + bytes (the search range
+            # covers all bins)
             nb = n // 2 + 1
-            p.accel_batch, p.batch_bytes = 0, 64 * (n * 4 + nb * 8 + nb * 4 + (nb + 63) // 64 * 64)
+            if C.kernels.harmonic_flags() & 64:
+                pst = (nb + 63) // 64 * 64
+                per = n * 4 + pst * 4 + (pst + C.kernels.spec_q_shift + 63) // 64 * 64
+            else:
+                per = n * 4 + nb * 8 + nb * 4 + (nb + 63) // 64 * 64
+            p.accel_batch, p.batch_bytes = 0, 64 * per
         else:
             p.accel_batch, p.sub_batch = 24, 0
         eng = C.SearchEngine(p, s)
