@@ -16,8 +16,8 @@ One step (per rank, weak scaling -- fixed work per GPU):
     harmonic sum + peak compaction -> peak clustering and per-trial
     harmonic distillation on the GPU -> per-DM acceleration distillation on
     host workers (overlapped with the next batches),
-  * gather every rank's candidates to all ranks over RCCL and run the global
-    DM/harmonic distillation + scoring -- on a worker thread, overlapped with
+  * gather every rank's candidates to rank 0 over RCCL and run the global
+    DM/harmonic distillation + scoring there -- on a worker thread, overlapped with
     the next step's dedispersion and search as the pipeline's DM blocks are
     (the timed region ends after the last step's merge; --serial-merge runs
     them back to back).
@@ -66,7 +66,7 @@ def parse():
     p.add_argument("--harm-flags", type=int, default=-1,
                    help="harmonic-sum / tiled-r2c kernel variant flags (tuning; -1 = default)")
     p.add_argument("--seed", type=int, default=1234)
-    p.add_argument("--signal", action="store_true",
+    p.add_argument("--signal", "--peak-heavy", dest="signal", action="store_true",
                    help="peak-heavy data instead of pure noise: injected pulsars plus strong undispersed periodic "
                         "RFI (>= 1e4 threshold crossings per DM), to time the host clustering / distillation")
     p.add_argument("--serial-merge", action="store_true",
@@ -170,21 +170,32 @@ def main() -> int:
     # search; the timed region ends after the last step's merge.
     from concurrent.futures import ThreadPoolExecutor
 
-    merger = ThreadPoolExecutor(max_workers=1) if not a.serial_merge else None
+    # (the worker binds the rank's GPU first: its collectives and any torch
+    # call must not create a context on device 0)
+    merger = (ThreadPoolExecutor(max_workers=1, initializer=torch.cuda.set_device, initargs=(dev,))
+              if not a.serial_merge else None)
 
     def merge(local):
+        # as run_search: one rank's list merged in place; more: every rank's
+        # serialised list gathered to rank 0 only (RCCL), merged there
         t1 = time.perf_counter()
-        blob = _C.serialize_candidates(local)
-        t2 = time.perf_counter()
-        blobs = pdist.gather_bytes(blob, dst=None)
-        t3 = time.perf_counter()
-        out = _C.merge_candidate_blobs(blobs, args, rs.header)  # rank order, stable by DM, global distill
+        if not ctx.distributed:
+            t2 = t3 = t1
+            phase["blob_bytes"] = 0
+            out = _C.merge_local(local, args, rs.header)
+        else:
+            blob = torch.from_numpy(_C.serialize_candidates_array(local))
+            t2 = time.perf_counter()
+            bufs = pdist.gather_buffers(blob, dst=0)
+            t3 = time.perf_counter()
+            phase["blob_bytes"] = blob.numel()
+            out = (_C.merge_candidate_buffers([(b.data_ptr(), b.numel()) for b in bufs], args, rs.header)
+                   if ctx.is_root else _C.CandidateBag())
         t4 = time.perf_counter()
         phase["merge"] += t4 - t1
         phase["ser"] += t2 - t1
         phase["gather"] += t3 - t2
         phase["gds"] += t4 - t3
-        phase["blob_bytes"] = len(blob)
         return out
 
     def step():
@@ -283,7 +294,7 @@ def _as_rank(a, rs, args, world, ranks) -> int:
 
         def step():
             local = rs.search(shard, chunk=a.dms_per_gpu)
-            local.sort(key=lambda c: c.dm_idx)
+            local.sort_by_dm()
             return _C.global_distill_and_score(local, args, rs.header)
 
         for _ in range(a.warmup):

@@ -67,6 +67,11 @@ struct Candidate {
 
 using CandidateList = std::vector<Candidate>;
 
+// std::stable_sort by dm_idx (the order the reference merges its workers'
+// lists in), as one permutation of the candidates instead of moving them
+// (with their trees) at every step of the sort: same result.
+void stable_sort_by_dm_idx(CandidateList& c);
+
 // ------------------------------------------------------------ distillers ---
 class HarmonicDistiller {
  public:

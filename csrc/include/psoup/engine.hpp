@@ -108,7 +108,7 @@ class Dedisperser {
   // Auto's choice for [d0, d1): one-hot MFMA while the tiles' offset spread is
   // narrow (few 16-shift blocks per channel), packed-byte VALU once it is wide.
   DedispKernel choose(int d0, int d1);
-  // resident-plan MFMA steps per (tile, active channel) over [d0, d1)'s tiles
+  // global-load MFMA steps per (tile, active channel) over [d0, d1)'s tiles
   double mfma_steps_per_channel(int d0, int d1);
   // Auto's split of a tile-aligned range: DMs [d0, split) run the LDS-fed
   // MFMA kernel (leading tiles whose offset spread is narrow enough for the
@@ -121,14 +121,17 @@ class Dedisperser {
 
  private:
   void build_resident_plan();
-  void build_valu_tables();
-  void build_mfma_lds_tables();
+  // (offs: the whole list's offset table when the caller has it)
+  void build_valu_tables(const std::vector<int32_t>* offs = nullptr);
+  void build_mfma_lds_tables(const std::vector<int32_t>* offs = nullptr, bool upload = true);
+  void upload_mfma_lds_tables();
+  std::unique_ptr<kern::MfmaLdsPlan> ml_plan_;  // host plan between build and upload
   void run_mfma_lds(int d0, int d1, uint8_t* out, uint64_t out_stride, hipStream_t s);
   const DeviceFilterbank& fb_;
   hipStream_t stream_;
   DeviceBuffer<int32_t> d_offsets_, d_kill_, d_active_, d_list_offT_;
   bool resident_ = false, valu_ready_ = false;
-  std::vector<int32_t> h_tile_steps_;  // resident plan: MFMA steps per tile
+  std::vector<int32_t> h_tile_steps_;  // global-load MFMA plan's steps per tile (from the VALU tables)
   int ldo_ = 0;                        // columns of r_offT_
   std::vector<int32_t> h_tile_win_;    // LDS kernel: largest channel window per 32-DM tile (bytes)
   DeviceBuffer<int32_t> r_steps_, r_tile_info_, r_offT_, r_wmin_;

@@ -26,6 +26,12 @@ using namespace psoup;
 
 namespace {
 
+// the Python-facing native candidate list (see the CandidateBag class below)
+struct CandidateBag {
+  CandidateList c;
+};
+
+
 template <class T>
 T* P(uintptr_t p) {
   return reinterpret_cast<T*>(p);
@@ -277,6 +283,77 @@ PYBIND11_MODULE(_C, m) {
                       1.0 / c.freq, c.dm, c.acc, c.nh, c.snr, c.folded_snr, c.count_assoc());
         return std::string(b);
       });
+  // A candidate list that stays native: the search's per-DM results, the
+  // merged list and the written outputs pass through Python as one handle
+  // instead of a Python list of Candidate objects (each conversion of a list
+  // deep-copied every candidate's association tree: 1.7M candidates in the
+  // config-4 list).  Indexing and iteration give references into the bag
+  // (writes such as folded_snr land in it); len, extend (moves the other
+  // bag's candidates), permute, truncate and sort_by_dm are native.
+  py::class_<CandidateBag, std::shared_ptr<CandidateBag>>(m, "CandidateBag")
+      .def(py::init<>())
+      .def(py::init([](const py::sequence& seq) {
+        auto b = std::make_shared<CandidateBag>();
+        b->c.reserve(seq.size());
+        for (auto h : seq) b->c.push_back(h.cast<const Candidate&>());
+        return b;
+      }))
+      .def("__len__", [](const CandidateBag& b) { return b.c.size(); })
+      .def(
+          "__getitem__",
+          [](CandidateBag& b, long i) -> Candidate& {
+            const long n = static_cast<long>(b.c.size());
+            if (i < 0) i += n;
+            if (i < 0 || i >= n) throw py::index_error("CandidateBag index out of range");
+            return b.c[static_cast<size_t>(i)];
+          },
+          py::return_value_policy::reference_internal)
+      .def(
+          "__iter__", [](CandidateBag& b) { return py::make_iterator(b.c.begin(), b.c.end()); },
+          py::keep_alive<0, 1>())
+      .def("extend",
+           [](CandidateBag& b, CandidateBag& o) {
+             if (&b == &o) throw std::invalid_argument("CandidateBag.extend: a bag into itself");
+             b.c.reserve(b.c.size() + o.c.size());
+             for (auto& x : o.c) b.c.push_back(std::move(x));
+             o.c.clear();
+           },
+           py::arg("other"), "move every candidate of `other` (left empty) to the end of this bag")
+      .def("permute",
+           [](CandidateBag& b, const std::vector<int>& order) {
+             CandidateList out;
+             out.reserve(order.size());
+             std::vector<char> seen(b.c.size(), 0);
+             for (int i : order) {
+               PSOUP_CHECK(i >= 0 && static_cast<size_t>(i) < b.c.size() && !seen[static_cast<size_t>(i)],
+                           "CandidateBag.permute: not a permutation");
+               seen[static_cast<size_t>(i)] = 1;
+               out.push_back(std::move(b.c[static_cast<size_t>(i)]));
+             }
+             PSOUP_CHECK(out.size() == b.c.size(), "CandidateBag.permute: not a permutation");
+             b.c = std::move(out);
+           },
+           py::arg("order"), "reorder: new[i] = old[order[i]]")
+      .def("truncate", [](CandidateBag& b, size_t n) { b.c.resize(std::min(n, b.c.size())); })
+      .def("sort_by_dm",
+           [](CandidateBag& b) {
+             py::gil_scoped_release nogil;
+             stable_sort_by_dm_idx(b.c);
+           },
+           "stable sort by DM index (the merge order of the reference, pipeline_multi.cu:356-365)")
+      .def("to_list", [](const CandidateBag& b) { return b.c; });
+  m.def("collect_bags", [](SearchEngine& e, const std::shared_ptr<SearchEngine::Pending>& h) {
+    std::vector<CandidateList> v;
+    {
+      py::gil_scoped_release nogil;
+      v = e.collect(h);
+    }
+    std::vector<std::shared_ptr<CandidateBag>> out;
+    out.reserve(v.size());
+    for (auto& l : v) out.push_back(std::make_shared<CandidateBag>(CandidateBag{std::move(l)}));
+    return out;
+  }, py::arg("engine"), py::arg("handle"),
+     "SearchEngine.collect, the per-job candidate lists as CandidateBags (nothing copied)");
   py::class_<HarmonicDistiller>(m, "HarmonicDistiller")
       .def(py::init<float, float, bool, bool>(), py::arg("tol"), py::arg("max_harm"), py::arg("keep_related"),
            py::arg("fractional_harms") = true)
@@ -327,6 +404,14 @@ PYBIND11_MODULE(_C, m) {
     for (size_t i = 0; i < k.size(); ++i) order[i] = k[i].i;
     return order;
   });
+  m.def("serialize_candidates", [](const CandidateBag& b) {
+    std::vector<uint8_t> v;
+    {
+      py::gil_scoped_release nogil;
+      v = serialize_candidates(b.c);
+    }
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+  });
   // a sequence of Candidate objects, serialised in place: no copy of the
   // trees into a temporary C++ list (candidate-heavy searches carry large
   // keep_related trees)
@@ -351,13 +436,54 @@ PYBIND11_MODULE(_C, m) {
     raw.reserve(blobs.size());
     for (const auto& b : blobs) raw.push_back(static_cast<std::string>(b));
     SearchSetup s = make_search_setup(args, dict_to_header(hdr));
-    CandidateList out;
+    auto out = std::make_shared<CandidateBag>();
     {
       py::gil_scoped_release nogil;
       CandidateList all;
       for (const auto& r : raw) deserialize_candidates_into(reinterpret_cast<const uint8_t*>(r.data()), r.size(), all);
-      std::stable_sort(all.begin(), all.end(), [](const Candidate& a, const Candidate& b) { return a.dm_idx < b.dm_idx; });
-      out = global_distill_and_score(std::move(all), args, s);
+      stable_sort_by_dm_idx(all);
+      out->c = global_distill_and_score(std::move(all), args, s);
+    }
+    return out;
+  });
+  // The merge from raw buffers ((address, size) of host memory, e.g. the
+  // uint8 tensors a gather delivered): no Python bytes objects in between.
+  m.def("merge_candidate_buffers", [](const std::vector<std::pair<uintptr_t, size_t>>& bufs,
+                                      const CmdLineOptions& args, const py::dict& hdr) {
+    SearchSetup s = make_search_setup(args, dict_to_header(hdr));
+    auto out = std::make_shared<CandidateBag>();
+    {
+      py::gil_scoped_release nogil;
+      CandidateList all;
+      for (const auto& [addr, n] : bufs) deserialize_candidates_into(reinterpret_cast<const uint8_t*>(addr), n, all);
+      stable_sort_by_dm_idx(all);
+      out->c = global_distill_and_score(std::move(all), args, s);
+    }
+    return out;
+  });
+  // serialised into a uint8 numpy array that owns the bytes (torch.from_numpy
+  // takes it without a copy)
+  m.def("serialize_candidates_array", [](const CandidateBag& b) {
+    auto* v = new std::vector<uint8_t>();
+    {
+      py::gil_scoped_release nogil;
+      *v = serialize_candidates(b.c);
+    }
+    py::capsule owner(v, [](void* p) { delete static_cast<std::vector<uint8_t>*>(p); });
+    return py::array_t<uint8_t>({static_cast<py::ssize_t>(v->size())}, {static_cast<py::ssize_t>(1)}, v->data(),
+                                owner);
+  });
+  // The same merge of one rank's own candidates (a world of one): no
+  // serialisation; `local` is consumed (left empty).
+  m.def("merge_local", [](CandidateBag& local, const CmdLineOptions& args, const py::dict& hdr) {
+    SearchSetup s = make_search_setup(args, dict_to_header(hdr));
+    auto out = std::make_shared<CandidateBag>();
+    {
+      py::gil_scoped_release nogil;
+      CandidateList all = std::move(local.c);
+      local.c.clear();
+      stable_sort_by_dm_idx(all);
+      out->c = global_distill_and_score(std::move(all), args, s);
     }
     return out;
   });
@@ -439,6 +565,12 @@ PYBIND11_MODULE(_C, m) {
   // -------------------------------------------------------------- output --
   m.def("xml_fmt_float", [](float v) { return xml::fmt(v); });
   m.def("xml_fmt_double", [](double v) { return xml::fmt(v); });
+  m.def("write_candidates_binary", [](const std::string& outdir, const CandidateBag& b, const std::string& fname) {
+    CandidateFileWriter w(outdir);
+    w.write_binary(b.c, fname);
+    std::map<unsigned, long> bm = w.byte_mapping;
+    return bm;
+  });
   m.def("write_candidates_binary", [](const std::string& outdir, const CandidateList& c, const std::string& fname) {
     CandidateFileWriter w(outdir);
     w.write_binary(c, fname);
@@ -456,7 +588,7 @@ PYBIND11_MODULE(_C, m) {
   m.def(
       "write_overview",
       [](const std::string& path, const CmdLineOptions& args, const py::object& header_file, const std::vector<float>& dms,
-         const std::vector<float>& accs, const std::vector<int>& devices, const CandidateList& cands,
+         const std::vector<float>& accs, const std::vector<int>& devices, const py::object& cands_obj,
          const std::map<unsigned, long>& byte_map, const std::map<std::string, double>& timers,
          const std::map<std::string, double>& perf) {
         OverviewWriter ow;
@@ -467,7 +599,10 @@ PYBIND11_MODULE(_C, m) {
         ow.add_dm_list(dms);
         ow.add_acc_list(accs);
         if (!devices.empty()) ow.add_gpu_info(devices);
-        ow.add_candidates(cands, byte_map);
+        if (py::isinstance<CandidateBag>(cands_obj))
+          ow.add_candidates(cands_obj.cast<const CandidateBag&>().c, byte_map);
+        else
+          ow.add_candidates(cands_obj.cast<CandidateList>(), byte_map);
         ow.add_timing_info(timers);
         if (!perf.empty()) ow.add_performance(perf);
         ow.to_file(path);
@@ -955,6 +1090,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("accel_plan_from_args", [](const CmdLineOptions& args, const py::dict& hdr) {
     return make_search_setup(args, dict_to_header(hdr)).accel_plan;
   });
+  m.def("global_distill_and_score", [](CandidateBag& b, const CmdLineOptions& args, const py::dict& hdr) {
+    SearchSetup s = make_search_setup(args, dict_to_header(hdr));
+    auto out = std::make_shared<CandidateBag>();
+    py::gil_scoped_release nogil;
+    CandidateList all = std::move(b.c);
+    b.c.clear();
+    out->c = global_distill_and_score(std::move(all), args, s);
+    return out;
+  });
   m.def("global_distill_and_score", [](CandidateList c, const CmdLineOptions& args, const py::dict& hdr) {
     SearchSetup s = make_search_setup(args, dict_to_header(hdr));
     return global_distill_and_score(std::move(c), args, s);
@@ -975,7 +1119,14 @@ PYBIND11_MODULE(_C, m) {
     SpillStatus st = load_spill(path, key, c);
     return py::make_tuple(std::string(spill_status_name(st)), c);
   });
+  m.def("save_spill", [](const std::string& path, uint64_t key, const CandidateBag& b) { save_spill(path, key, b.c); },
+        py::arg("path"), py::arg("key"), py::arg("cands"));
   m.def("save_spill", &save_spill, py::arg("path"), py::arg("key"), py::arg("cands"));
+  m.def("load_spill_bag", [](const std::string& path, uint64_t key) {
+    auto b = std::make_shared<CandidateBag>();
+    SpillStatus st = load_spill(path, key, b->c);
+    return py::make_tuple(std::string(spill_status_name(st)), b);
+  });
   m.def("search_params_from_args", [](const CmdLineOptions& args, const py::dict& hdr) {
     SearchSetup s = make_search_setup(args, dict_to_header(hdr));
     return py::make_tuple(s.search, s.dm_list, s.killmask, s.fft_size, s.cfreq);

@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <thread>
 #include <vector>
 
 #include "psoup/common.hpp"
@@ -47,6 +48,14 @@ std::string Candidate::print() const {
 }
 
 namespace {
+
+// c[i] = old c[order[i]], each candidate moved once
+void apply_order(CandidateList& c, const std::vector<uint32_t>& order) {
+  CandidateList out;
+  out.reserve(c.size());
+  for (uint32_t i : order) out.push_back(std::move(c[i]));
+  c = std::move(out);
+}
 
 // BaseDistiller::distill (distiller.hpp:27-59): sort by S/N, then every
 // surviving candidate in turn (the "fundamental") marks the later candidates
@@ -109,20 +118,53 @@ struct FreqIndex {
 
 // windows(c, idx, push(lo, hi)) lists the fundamental's frequency windows;
 // related(c, idx, ii) is the reference's inner-loop body for one later
-// candidate (performs the appends) and returns whether ii is related.
+// candidate: how many times the reference appends ii to idx's assoc list
+// (0: unrelated; with keep_related off, 1 for related).
+//
+// keep_related: the reference copies each related candidate (with its own
+// assoc tree) into the fundamental's list at once; here the appends are
+// recorded and materialised after the scan, the last use of each candidate
+// moved instead of copied.  The result is the same: an appended candidate is
+// non-unique from then on, so it never becomes a fundamental and its
+// contents never change after the first append (fundamentals are the only
+// candidates whose lists grow, and they are never appended).  On the config-4
+// candidate list (138k candidates carrying 1.56M associated ones) the DM
+// distillation went 363 -> ~30 ms.
 template <class Windows, class Related>
-CandidateList base_distill(CandidateList cands, Windows&& windows, Related&& related, bool force_scan = false,
+CandidateList base_distill(CandidateList cands, Windows&& windows, Related&& related, bool keep, bool force_scan = false,
                            bool sorted_windows = false) {
   const size_t size = cands.size();
   std::vector<char> unique(size, 1);
   // std::sort (not stable_sort) on purpose: with the same input order it breaks
-  // S/N ties exactly as the reference's libstdc++ introsort does.
-  std::sort(cands.begin(), cands.end(), [](const Candidate& a, const Candidate& b) { return a.snr > b.snr; });
+  // S/N ties exactly as the reference's libstdc++ introsort does.  Sorted as
+  // an index permutation (std::sort's result depends only on the comparison
+  // outcomes), each candidate then moved once.
+  {
+    std::vector<uint32_t> order(size);
+    for (size_t i = 0; i < size; ++i) order[i] = static_cast<uint32_t>(i);
+    std::vector<float> snr(size);
+    for (size_t i = 0; i < size; ++i) snr[i] = cands[i].snr;
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return snr[a] > snr[b]; });
+    apply_order(cands, order);
+  }
   const bool indexed = !force_scan && size >= kIndexedMin;
   std::unique_ptr<FreqIndex> index;
   if (indexed) index = std::make_unique<FreqIndex>(cands);
   std::vector<uint32_t> hits;
   std::vector<std::pair<double, double>> wins;
+  std::vector<std::pair<uint32_t, uint32_t>> appends;  // (fundamental, appended), in the reference's order
+  std::vector<uint32_t> uses;                           // appends of each candidate
+  if (keep) uses.assign(size, 0);
+  auto relate = [&](size_t fi, size_t ii) {
+    const int n = related(cands, fi, ii);
+    if (n <= 0) return;
+    unique[ii] = 0;
+    if (keep)
+      for (int r = 0; r < n; ++r) {
+        appends.emplace_back(static_cast<uint32_t>(fi), static_cast<uint32_t>(ii));
+        uses[ii]++;
+      }
+  };
   size_t start = 0;
   while (true) {
     long idx = -1;
@@ -136,8 +178,7 @@ CandidateList base_distill(CandidateList cands, Windows&& windows, Related&& rel
     if (idx < 0) break;
     const size_t fi = static_cast<size_t>(idx);
     if (!indexed) {
-      for (size_t ii = fi + 1; ii < size; ++ii)
-        if (related(cands, fi, ii)) unique[ii] = 0;
+      for (size_t ii = fi + 1; ii < size; ++ii) relate(fi, ii);
       continue;
     }
     hits.clear();
@@ -158,8 +199,13 @@ CandidateList base_distill(CandidateList cands, Windows&& windows, Related&& rel
     }
     std::sort(hits.begin(), hits.end());
     hits.erase(std::unique(hits.begin(), hits.end()), hits.end());
-    for (uint32_t ii : hits)
-      if (related(cands, fi, ii)) unique[ii] = 0;
+    for (uint32_t ii : hits) relate(fi, ii);
+  }
+  for (const auto& [fi, ii] : appends) {
+    if (--uses[ii] == 0)
+      cands[fi].assoc.push_back(std::move(cands[ii]));
+    else
+      cands[fi].assoc.push_back(cands[ii]);
   }
   CandidateList out;
   for (size_t ii = 0; ii < size; ++ii)
@@ -194,7 +240,7 @@ CandidateList HarmonicDistiller::run(CandidateList cands, bool force_scan) const
   };
   // the reference scan (force_scan) keeps the reference's full jj x kk loop
   const bool fast = !keep && tol_ <= 1e-3f && !force_scan;
-  auto related = [&](CandidateList& c, size_t idx, size_t ii) {
+  auto related = [&](const CandidateList& c, size_t idx, size_t ii) -> int {
     const double fundi_freq = c[idx].freq;
     const double freq = c[ii].freq;
     const int nh = c[ii].nh;
@@ -213,23 +259,21 @@ CandidateList HarmonicDistiller::run(CandidateList cands, bool force_scan) const
         const int j0 = static_cast<int>(std::lround(x));
         if (j0 < 1 || j0 > max_harm || std::fabs(x - j0) > 1.5 * tol_ * j0 + 1e-9) continue;
         const double ratio = kk * freq / (j0 * fundi_freq);
-        if (ratio > lower_tol && ratio < upper_tol) return true;
+        if (ratio > lower_tol && ratio < upper_tol) return 1;
       }
-      return false;
+      return 0;
     }
-    bool rel = false;
+    // every (jj, kk) match appends once (keep_related)
+    int n = 0;
     for (int jj = 1; jj <= max_harm; ++jj) {
       for (int kk = 1; kk <= max_denominator; ++kk) {
         const double ratio = kk * freq / (jj * fundi_freq);
-        if (ratio > lower_tol && ratio < upper_tol) {
-          if (keep) c[idx].append(c[ii]);
-          rel = true;
-        }
+        if (ratio > lower_tol && ratio < upper_tol) ++n;
       }
     }
-    return rel;
+    return keep ? n : (n > 0 ? 1 : 0);
   };
-  return base_distill(std::move(cands), windows, related, force_scan, true);
+  return base_distill(std::move(cands), windows, related, keep, force_scan, true);
 }
 
 AccelerationDistiller::AccelerationDistiller(float tobs, float tol, bool keep_related)
@@ -257,7 +301,7 @@ CandidateList AccelerationDistiller::run(CandidateList cands, bool force_scan) c
     const double lo = std::min({fundi_freq, a1, a2}) - edge, hi = std::max({fundi_freq, a1, a2}) + edge;
     push(lo - 1e-6 * std::fabs(lo), hi + 1e-6 * std::fabs(hi));
   };
-  auto related = [&](CandidateList& c, size_t idx, size_t ii) {
+  auto related = [&](const CandidateList& c, size_t idx, size_t ii) -> int {
     const double fundi_freq = c[idx].freq;
     const double fundi_acc = c[idx].acc;
     const double edge = fundi_freq * tol;
@@ -270,10 +314,9 @@ CandidateList AccelerationDistiller::run(CandidateList cands, bool force_scan) c
       rel = (f > fundi_freq - edge && f < acc_freq + edge);
     else
       rel = (f < fundi_freq + edge && f > acc_freq - edge);
-    if (rel && keep) c[idx].append(c[ii]);
-    return rel;
+    return rel ? 1 : 0;
   };
-  return base_distill(std::move(cands), windows, related, force_scan);
+  return base_distill(std::move(cands), windows, related, keep, force_scan);
 }
 
 CandidateList DMDistiller::distill(CandidateList cands) const { return run(std::move(cands), false); }
@@ -286,13 +329,11 @@ CandidateList DMDistiller::run(CandidateList cands, bool force_scan) const {
     const double fundi_freq = c[idx].freq;
     push(lower_tol * fundi_freq, upper_tol * fundi_freq);
   };
-  auto related = [&](CandidateList& c, size_t idx, size_t ii) {
+  auto related = [&](const CandidateList& c, size_t idx, size_t ii) -> int {
     const double ratio = c[ii].freq / static_cast<double>(c[idx].freq);
-    const bool rel = ratio > lower_tol && ratio < upper_tol;
-    if (rel && keep) c[idx].append(c[ii]);
-    return rel;
+    return ratio > lower_tol && ratio < upper_tol ? 1 : 0;
   };
-  return base_distill(std::move(cands), windows, related, force_scan);
+  return base_distill(std::move(cands), windows, related, keep, force_scan);
 }
 
 CandidateScorer::CandidateScorer(float tsamp, float cfreq, float foff, float bw)
@@ -370,6 +411,14 @@ PeakBounds peak_bounds(int size, float bin_width, int nh, float min_freq, float 
   b.factor = 1.0 / size * nyquist / std::pow(2.0, static_cast<float>(nh));
   if (b.start_idx < 0) b.start_idx = 0;
   return b;
+}
+
+void stable_sort_by_dm_idx(CandidateList& c) {
+  std::vector<uint32_t> order(c.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = static_cast<uint32_t>(i);
+  // std::stable_sort's permutation depends on the comparison outcomes alone
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c[a].dm_idx < c[b].dm_idx; });
+  apply_order(c, order);
 }
 
 void sort_by_folded_snr(CandidateList& cands) {
@@ -467,6 +516,20 @@ std::vector<uint8_t> serialize_candidates(const std::vector<const Candidate*>& c
   return out;
 }
 
+namespace {
+// past one record and its subtree (headers only): the byte offsets of the
+// top-level records, so their subtrees can be rebuilt in parallel
+void skip_node(Reader& r, int depth) {
+  PSOUP_CHECK(depth < 64, "candidate tree too deep");
+  NodeRec rec;
+  r.get(&rec, sizeof(rec));
+  PSOUP_CHECK(rec.nfold >= 0 && rec.nassoc >= 0, "corrupt candidate record");
+  PSOUP_CHECK(r.off + static_cast<size_t>(rec.nfold) * sizeof(float) <= r.n, "truncated candidate stream");
+  r.off += static_cast<size_t>(rec.nfold) * sizeof(float);
+  for (int i = 0; i < rec.nassoc; ++i) skip_node(r, depth + 1);
+}
+}  // namespace
+
 void deserialize_candidates_into(const uint8_t* data, size_t nbytes, CandidateList& out) {
   if (nbytes == 0) return;
   Reader r{data, nbytes};
@@ -476,8 +539,47 @@ void deserialize_candidates_into(const uint8_t* data, size_t nbytes, CandidateLi
   PSOUP_CHECK(magic == 0x50534F43u, "bad candidate stream magic");
   r.get(&n, 8);
   PSOUP_CHECK(n >= 0, "bad candidate count");
-  out.reserve(out.size() + static_cast<size_t>(n));
-  for (int64_t i = 0; i < n; ++i) out.push_back(de_node(r, 0));
+  const size_t base = out.size();
+  // Large streams (a merge of 138k candidates carrying 1.6M associated ones:
+  // ~100 MB) are rebuilt on several threads: one header-only pass finds each
+  // top-level record, then contiguous ranges of records are deserialised in
+  // parallel straight into their final positions.
+  const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  if (nbytes < (16u << 20) || hw == 1 || n < 1024) {
+    out.reserve(base + static_cast<size_t>(n));
+    for (int64_t i = 0; i < n; ++i) out.push_back(de_node(r, 0));
+    PSOUP_CHECK(r.off == nbytes, "trailing bytes after the candidate stream");
+    return;
+  }
+  std::vector<size_t> at(static_cast<size_t>(n) + 1);
+  for (int64_t i = 0; i < n; ++i) {
+    at[static_cast<size_t>(i)] = r.off;
+    skip_node(r, 0);
+  }
+  at[static_cast<size_t>(n)] = r.off;
+  PSOUP_CHECK(r.off == nbytes, "trailing bytes after the candidate stream");
+  out.resize(base + static_cast<size_t>(n));
+  std::vector<std::thread> th;
+  std::vector<std::exception_ptr> err(hw);
+  for (unsigned t = 0; t < hw; ++t)
+    th.emplace_back([&, t] {
+      try {
+        // ranges balanced by bytes
+        const size_t lo = nbytes / hw * t, hi = t + 1 == hw ? nbytes : nbytes / hw * (t + 1);
+        size_t i0 = static_cast<size_t>(std::lower_bound(at.begin(), at.end() - 1, lo) - at.begin());
+        size_t i1 = t + 1 == hw ? static_cast<size_t>(n)
+                                : static_cast<size_t>(std::lower_bound(at.begin(), at.end() - 1, hi) - at.begin());
+        for (size_t i = i0; i < i1; ++i) {
+          Reader rr{data, nbytes, at[i]};
+          out[base + i] = de_node(rr, 0);
+        }
+      } catch (...) {
+        err[t] = std::current_exception();
+      }
+    });
+  for (auto& x : th) x.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
 }
 
 CandidateList deserialize_candidates(const uint8_t* data, size_t nbytes) {

@@ -122,12 +122,16 @@ void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std
     packed[i].resize(bytes);
   }
   PSOUP_HIP_CHECK(hipSetDevice(devices[0]));
+  // a file within one chunk goes up straight from its (mapped) pages: pinning
+  // a staging buffer and freeing it cost more than the copy (~2 ms for 3 MB)
+  const bool direct = g.nsamps <= chunk;
   PinnedBuffer<uint8_t> stage[2];
   Event staged[2], landed;
   // staging sized to the file when it is shorter than a chunk (pinning
   // 2 x 64 MiB took ~40 ms, more than a small file's whole upload)
   const uint64_t stage_bytes = std::min(chunk, g.nsamps) * bps;
-  for (int i = 0; i < (g.nsamps > chunk ? 2 : 1); ++i) stage[i].resize(stage_bytes);
+  if (!direct)
+    for (int i = 0; i < 2; ++i) stage[i].resize(stage_bytes);
   bool used[2] = {false, false};
   hipStream_t s0 = fbs[0]->stream();
   int slot = 0;
@@ -135,11 +139,15 @@ void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std
     const uint64_t ns = std::min(chunk, g.nsamps - t0);
     const uint64_t off = t0 * bps, nb = ns * bps;
     PSOUP_HIP_CHECK(hipSetDevice(devices[0]));
-    if (used[slot]) staged[slot].sync();
-    std::memcpy(stage[slot].data(), h_packed + off, nb);
-    PSOUP_HIP_CHECK(hipMemcpyAsync(packed[0].data() + off, stage[slot].data(), nb, hipMemcpyHostToDevice, s0));
-    staged[slot].record(s0);
-    used[slot] = true;
+    if (direct) {
+      PSOUP_HIP_CHECK(hipMemcpy(packed[0].data() + off, h_packed + off, nb, hipMemcpyHostToDevice));
+    } else {
+      if (used[slot]) staged[slot].sync();
+      std::memcpy(stage[slot].data(), h_packed + off, nb);
+      PSOUP_HIP_CHECK(hipMemcpyAsync(packed[0].data() + off, stage[slot].data(), nb, hipMemcpyHostToDevice, s0));
+      staged[slot].record(s0);
+      used[slot] = true;
+    }
     landed.record(s0);
     fbs[0]->unpack_chunk(packed[0].data() + off, t0, ns);
     for (size_t i = 1; i < n; ++i) {
@@ -177,11 +185,28 @@ Dedisperser::Dedisperser(const DeviceFilterbank& fb, hipStream_t stream) : fb_(f
 }
 
 void Dedisperser::warm() {
+  // The tables Auto needs (VALU offsets and windows, LDS-fed MFMA plan), from
+  // one offset table, the two builds in parallel.  The whole-list global-load
+  // MFMA plan (~380k steps on the 2026-DM config-4 list, 136 ms on the host)
+  // serves only an explicit --dedisp_kernel mfma over tiles the LDS kernel
+  // cannot take: built on first such use.
   const auto& g = fb_.geometry();
   if (g.dm_list.empty() || g.nactive == 0) return;
-  if (!resident_) build_resident_plan();
-  if (!valu_ready_) build_valu_tables();
-  if (!ml_ready_) build_mfma_lds_tables();
+  const std::vector<int32_t> offs = g.offsets(0, static_cast<int>(g.dm_list.size()));
+  std::exception_ptr err;
+  std::thread th;
+  if (!ml_ready_)
+    th = std::thread([&] {
+      try {
+        build_mfma_lds_tables(&offs, /*upload=*/false);
+      } catch (...) {
+        err = std::current_exception();
+      }
+    });
+  if (!valu_ready_) build_valu_tables(&offs);
+  if (th.joinable()) th.join();
+  if (err) std::rethrow_exception(err);
+  if (!ml_ready_) upload_mfma_lds_tables();
 }
 
 void Dedisperser::build_resident_plan() {
@@ -198,17 +223,16 @@ void Dedisperser::build_resident_plan() {
   PSOUP_HIP_CHECK(hipMemcpy(r_deltas_.data(), plan.deltas.data(), plan.deltas.size(), hipMemcpyHostToDevice));
   PSOUP_HIP_CHECK(
       hipMemcpy(r_tile_info_.data(), plan.tile_info.data(), plan.tile_info.size() * 4, hipMemcpyHostToDevice));
-  h_tile_steps_.resize(static_cast<size_t>(plan.ntiles));
-  for (int T = 0; T < plan.ntiles; ++T) h_tile_steps_[T] = plan.tile_info[2 * T + 1];
   resident_ = true;
 }
 
-void Dedisperser::build_valu_tables() {
+void Dedisperser::build_valu_tables(const std::vector<int32_t>* offs_in) {
   // offsets transposed to [active channel][DM], columns padded (with the last
   // DM) past the last workgroup of any range
   const auto& g = fb_.geometry();
   const int ndm = static_cast<int>(g.dm_list.size());
-  std::vector<int32_t> offs = g.offsets(0, ndm);
+  const std::vector<int32_t> offs_own = offs_in ? std::vector<int32_t>() : g.offsets(0, ndm);
+  const std::vector<int32_t>& offs = offs_in ? *offs_in : offs_own;
   std::vector<int> active;
   for (int c = 0; c < g.nchans; ++c)
     if (g.killmask[c]) active.push_back(c);
@@ -225,7 +249,12 @@ void Dedisperser::build_valu_tables() {
   const size_t na = std::max<size_t>(1, active.size());
   std::vector<int32_t> wmin(static_cast<size_t>(ntiles) * na, 0);
   h_tile_win_.assign(static_cast<size_t>(ntiles), 0);
-  for (int T = 0; T < ntiles; ++T)
+  // and the global-load MFMA plan's step count per tile (its 16-sample blocks
+  // from each channel's smallest offset, two per step), which Auto weighs
+  // against the VALU kernels without building that plan
+  h_tile_steps_.assign(static_cast<size_t>(ntiles), 0);
+  for (int T = 0; T < ntiles; ++T) {
+    int64_t blocks = 0;
     for (size_t ci = 0; ci < active.size(); ++ci) {
       int lo = t[ci * ldo_ + T * kTileDms], hi = lo;
       for (int k = 1; k < kTileDms; ++k) {
@@ -235,7 +264,10 @@ void Dedisperser::build_valu_tables() {
       const int w0 = lo & ~15;
       wmin[static_cast<size_t>(T) * na + ci] = w0;
       h_tile_win_[static_cast<size_t>(T)] = std::max(h_tile_win_[static_cast<size_t>(T)], 1024 + (hi - w0) + 32);
+      blocks += (hi - lo) / 16 + 1;
     }
+    h_tile_steps_[static_cast<size_t>(T)] = static_cast<int32_t>((blocks + 1) / 2);
+  }
   r_wmin_.resize(wmin.size());
   PSOUP_HIP_CHECK(hipMemcpy(r_wmin_.data(), wmin.data(), wmin.size() * 4, hipMemcpyHostToDevice));
   valu_ready_ = true;
@@ -250,7 +282,7 @@ static double valu_ratio() {
 double Dedisperser::mfma_steps_per_channel(int d0, int d1) {
   const auto& g = fb_.geometry();
   PSOUP_CHECK(d0 >= 0 && d0 < d1 && d1 <= static_cast<int>(g.dm_list.size()), "bad DM range");
-  if (!resident_) build_resident_plan();
+  if (!valu_ready_) build_valu_tables();
   double steps = 0;
   const int t0 = d0 / kTileDms, t1 = (d1 - 1) / kTileDms;
   for (int T = t0; T <= t1; ++T) steps += h_tile_steps_[static_cast<size_t>(T)];
@@ -270,13 +302,20 @@ DedispKernel Dedisperser::choose(int d0, int d1) {
   return mfma_steps_per_channel(d0, d1) > ratio ? DedispKernel::Valu : DedispKernel::Mfma;
 }
 
-void Dedisperser::build_mfma_lds_tables() {
+void Dedisperser::build_mfma_lds_tables(const std::vector<int32_t>* offs_in, bool upload) {
   const auto& g = fb_.geometry();
   const int ndm = static_cast<int>(g.dm_list.size());
-  std::vector<int32_t> offs = g.offsets(0, ndm);
+  const std::vector<int32_t> offs_own = offs_in ? std::vector<int32_t>() : g.offsets(0, ndm);
+  const std::vector<int32_t>& offs = offs_in ? *offs_in : offs_own;
   std::vector<int32_t> kill(g.killmask.begin(), g.killmask.end());
-  kern::MfmaLdsPlan plan;
-  kern::build_mfma_lds_plan(offs.data(), ndm, g.nchans, kill.data(), plan);
+  ml_plan_ = std::make_unique<kern::MfmaLdsPlan>();
+  kern::build_mfma_lds_plan(offs.data(), ndm, g.nchans, kill.data(), *ml_plan_);
+  if (upload) upload_mfma_lds_tables();
+}
+
+void Dedisperser::upload_mfma_lds_tables() {
+  PSOUP_CHECK(ml_plan_, "MFMA-LDS tables not built");
+  const kern::MfmaLdsPlan& plan = *ml_plan_;
   ml_ngroups_ = plan.ngroups;
   ml_tile_ok_ = plan.tile_ok;
   ml_tile_steps_ = plan.tile_steps;
@@ -289,6 +328,7 @@ void Dedisperser::build_mfma_lds_tables() {
   up(ml_relo_, plan.relo);
   up(ml_ginfo_, plan.ginfo);
   up(ml_wmin_, plan.wmin);
+  ml_plan_.reset();
   ml_ready_ = true;
 }
 
@@ -808,18 +848,22 @@ void SearchEngine::grow_capacity(uint32_t need) {
     if (gpu_cluster_) {
       s.d_sorted.resize(2 * static_cast<size_t>(cap_));  // chunk descriptors, then raw segments' crossings
       s.d_clust.resize(cap_);
-      s.h_clust.resize(cap_);
-      s.h_raw.resize(cap_);
-      if (gpu_distill_) {
-        s.d_hout.resize(cap_);
-        s.h_hout.resize(cap_);
-      }
-    } else {
-      s.h_peaks.resize(cap_);
+      if (gpu_distill_) s.d_hout.resize(cap_);
     }
+    // (the pinned host copies grow on demand, to what a batch's counts ask
+    // for: sized to the device capacity they were ~48 MB of pinning -- and
+    // as much again to free -- per engine, most of a small run's setup)
   }
   hp_.capacity = cap_;
 }
+
+namespace {
+// pinned host buffer b holds at least n entries (contents not kept)
+template <typename T>
+void ensure_host(PinnedBuffer<T>& b, size_t n) {
+  if (b.size() < n) b.resize(std::max<size_t>(n, std::max<size_t>(2 * b.size(), 1u << 14)));
+}
+}  // namespace
 
 void SearchEngine::ensure_batch_buffers(int k) {
   // sized for the largest batch actually launched (a short trial list never
@@ -1334,6 +1378,26 @@ std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(
       // snapshot the segment table (the re-issued launch rewrites it) and
       // copy the cluster peaks plus any raw over-capacity segments
       segtab_.assign(s.h_segtab.data(), s.h_segtab.data() + 8 * static_cast<size_t>(b_count));
+      // host copies sized to this batch (the slot's previous copies retired:
+      // s.copied was waited on before its records were processed)
+      if (gpu_distill_) ttab_.assign(s.h_ttab.data(), s.h_ttab.data() + b_count);
+      {
+        size_t n_raw = 0, n_clust = gpu_distill_ ? 0 : s.h_count[1];
+        for (int k = 0; k < b_count; ++k) {
+          // with device distillation only the host-flagged trials' segments come out
+          if (gpu_distill_ && !(ttab_[static_cast<size_t>(k)].y & kern::kHarmHost)) continue;
+          for (int h = 0; h < 8; ++h) {
+            const uint2& e = segtab_[static_cast<size_t>(k) * 8 + h];
+            if (e.y & kern::kClusterRaw)
+              n_raw = std::max<size_t>(n_raw, static_cast<size_t>(e.x) + (e.y & ~kern::kClusterRaw));
+            else
+              n_clust = std::max<size_t>(n_clust, static_cast<size_t>(e.x) + e.y);
+          }
+        }
+        ensure_host(s.h_raw, n_raw);
+        ensure_host(s.h_clust, n_clust);
+        if (gpu_distill_) ensure_host(s.h_hout, s.h_count[2]);
+      }
       auto copy_seg = [&](const uint2& e) {
         if (e.y & kern::kClusterRaw)
           PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_raw.data() + e.x, s.d_sorted.data() + cap_ + e.x,
@@ -1346,7 +1410,6 @@ std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(
       if (gpu_distill_) {
         // the distilled candidates, plus the cluster peaks of the trials the
         // device left to the host
-        ttab_.assign(s.h_ttab.data(), s.h_ttab.data() + b_count);
         const uint32_t tot2 = s.h_count[2];
         if (tot2 > 0)
           PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_hout.data(), s.d_hout.data(), tot2 * sizeof(uint2),
@@ -1363,6 +1426,7 @@ std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(
           if (e.y & kern::kClusterRaw) copy_seg(e);
       }
     } else if (cnt > 0) {
+      ensure_host(s.h_peaks, cnt);
       PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_peaks.data(), s.d_peaks.data(), cnt * sizeof(kern::PeakRecord),
                                      hipMemcpyDeviceToHost, copy_stream_.get()));
     }

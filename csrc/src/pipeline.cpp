@@ -18,6 +18,7 @@
 
 #include "psoup/checkpoint.hpp"
 #include "psoup/output.hpp"
+#include "psoup/scheduler.hpp"
 
 namespace psoup {
 
@@ -124,7 +125,6 @@ struct Shared {
   const CmdLineOptions* args;
   const SearchSetup* setup;
   const Filterbank* fb;
-  std::atomic<int> next_dm{0};
   int chunk = 8;
   int ndm = 0;
   std::mutex mu;
@@ -134,7 +134,6 @@ struct Shared {
   std::vector<double> dedisp_s, search_s;
   std::vector<std::map<std::string, double>> dev_stats;
   std::exception_ptr error;
-  std::atomic<bool> abort{false};
   ProgressBar* progress = nullptr;
 };
 
@@ -145,11 +144,20 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   Stopwatch t_total, t_read, t_dedisp, t_search, t_fold;
   t_total.start();
   if (args.verbose) set_log_level(LogLevel::Verbose);
+  // wall time of each phase in order (trace_json "performance": phase_<name>_s),
+  // together the whole of "total"
+  double t_mark = 0;
+  auto mark = [&](const char* name) {
+    const double now = t_total.get_time();
+    res.performance[std::string("phase_") + name + "_s"] = now - t_mark;
+    t_mark = now;
+  };
 
   t_read.start();
   Filterbank fb = Filterbank::from_file(args.infilename);
   t_read.stop();
 
+  mark("read");
   SearchSetup setup = make_search_setup(args, fb.header());
   res.setup = setup;
   const int ndev_avail = device_count();
@@ -174,6 +182,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     }
     res.performance["device_init_s"] = init_s;
   }
+  mark("device_init");
   log_verbose("Using " + std::to_string(ngpu) + " GPU(s); " + std::to_string(setup.dm_list.size()) + " DM trials; fft " +
               std::to_string(setup.fft_size));
 
@@ -236,8 +245,6 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   Stopwatch t_setup;
   t_setup.start();
   {
-    Stopwatch wf;
-    wf.start();
     std::vector<DeviceFilterbank*> fbs;
     std::vector<int> phys;
     for (int dev = 0; dev < ngpu; ++dev) {
@@ -248,11 +255,9 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
       fbs.push_back(ds.dfb.get());
       phys.push_back(hip_dev(dev));
     }
-    load_filterbank_fanout(fbs, phys, fb.data());
-    wf.stop();
-    setup_load = wf.get_time();
-    res.performance["filterbank_load_s"] = setup_load;
-    res.performance["filterbank_devices"] = ngpu;
+    // each device's tables, engines and fold buffers are built on a thread of
+    // their own while this thread uploads the filterbank (none of them reads
+    // its samples)
     std::vector<std::thread> lth;
     for (int dev = 0; dev < ngpu; ++dev)
       lth.emplace_back([&, dev] {
@@ -263,7 +268,6 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
           wl.start();
           ds.dd = std::make_unique<Dedisperser>(*ds.dfb, ds.stream->get());
           ds.dd->warm();  // plan tables now, not at the first tile that needs them
-          PSOUP_HIP_CHECK(hipStreamSynchronize(ds.stream->get()));
           const double t_dd = wl.get_time();
           for (int e = 0; e < neng; ++e) {
             if (e > 0) ds.estreams.push_back(std::make_unique<Stream>());
@@ -271,14 +275,12 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
                 setup.search, e > 0 ? ds.estreams.back()->get() : ds.stream->get()));
             ds.engines.back()->reserve(ds.engines.back()->max_prepare(), 0);
           }
-          PSOUP_HIP_CHECK(hipStreamSynchronize(ds.stream->get()));
           const double t_eng = wl.get_time();
           if (args.npdmp > 0 && prev_power_of_two(geom.out_nsamps) >= 1024) {
             ds.fe = std::make_unique<FoldEngine>(prev_power_of_two(geom.out_nsamps), static_cast<float>(geom.tsamp),
                                                  ds.stream->get());
             ds.fe->reserve(args.npdmp);
           }
-          PSOUP_HIP_CHECK(hipStreamSynchronize(ds.stream->get()));
           wl.stop();
           std::lock_guard<std::mutex> lk(sh.mu);
           auto& st = sh.dev_stats[static_cast<size_t>(dev)];
@@ -294,10 +296,27 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
           if (!sh.error) sh.error = std::current_exception();
         }
       });
+    Stopwatch wf;
+    wf.start();
+    try {
+      load_filterbank_fanout(fbs, phys, fb.data());
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(sh.mu);
+      if (!sh.error) sh.error = std::current_exception();
+    }
+    wf.stop();
+    setup_load = wf.get_time();
+    res.performance["filterbank_load_s"] = setup_load;
+    res.performance["filterbank_devices"] = ngpu;
     for (auto& t : lth) t.join();
+    for (int dev = 0; dev < ngpu; ++dev) {
+      PSOUP_HIP_CHECK(hipSetDevice(hip_dev(dev)));
+      PSOUP_HIP_CHECK(hipStreamSynchronize(devs[static_cast<size_t>(dev)].stream->get()));
+    }
     if (sh.error) std::rethrow_exception(sh.error);
   }
   t_setup.stop();
+  mark("setup");
   res.performance["setup_s"] = t_setup.get_time();
   res.performance["setup_dedisp_s"] = setup_dd;
   res.performance["setup_engines_s"] = setup_eng;
@@ -308,26 +327,18 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   // device's neng engine threads searches every neng-th DM row of each chunk
   // (whitened and searched as one flat trial list), so all engines work on the
   // same chunk and the feeder reuses a buffer once every engine released it.
-  struct Pub {
-    int d0 = 0, d1 = 0;
-    bool resumed = false;
-    int pending = 0;
-    const uint8_t* rows = nullptr;  // the chunk's dedispersed rows (row d at rows + (d - d0) * rstride)
-    CandidateList cands;
-  };
+  // The protocol itself (slots, hand-over, abort) is ChunkScheduler
+  // (scheduler.hpp), which the host unit tests run under the thread sanitizer.
   struct DevSched {
-    std::mutex mu;
-    std::condition_variable cv;
-    Pub pub[2];
-    long published = 0;
-    bool done = false;
     std::atomic<int> processed{0};
     std::unique_ptr<Stream> dstream;
     std::unique_ptr<DeviceBuffer<uint8_t>> trials[2];
     Event ready[2] = {Event(true), Event(true)}, began[2] = {Event(true), Event(true)};
     std::vector<std::unique_ptr<Event>> freed[2];
     bool used[2] = {false, false};
+    const uint8_t* rows[2] = {nullptr, nullptr};  // the slot's dedispersed rows (row d at rows + (d - d0) * rstride)
     double dd_ms = 0.0;
+    std::vector<Stopwatch> search_w;  // per engine
   };
   std::vector<std::unique_ptr<DevSched>> scheds;
   const uint64_t rstride = Dedisperser::row_stride(geom.out_nsamps);
@@ -363,184 +374,137 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
       for (int e = 0; e < neng; ++e) sc->freed[k].push_back(std::make_unique<Event>());
     }
     if (keep) kept[static_cast<size_t>(d)] = std::make_unique<DeviceBuffer<uint8_t>>(rstride * static_cast<uint64_t>(sh.ndm));
+    sc->search_w.resize(static_cast<size_t>(neng));
     sh.dev_stats[static_cast<size_t>(d)]["kept_trials"] = keep ? 1.0 : 0.0;
     scheds.push_back(std::move(sc));
   }
-  auto fail = [&](int dev) {
+  mark("scheduler_setup");
+  using Pending = std::shared_ptr<SearchEngine::Pending>;
+  SchedFns<Candidate, std::vector<Pending>> ops;
+  using Chunk = SchedChunk<Candidate>;
+  ops.bind = [&](int dev) { PSOUP_HIP_CHECK(hipSetDevice(hip_dev(dev))); };
+  ops.prepare = [&](int dev, int k, Chunk& p) {
+    DevSched& sc = *scheds[static_cast<size_t>(dev)];
+    DevState& ds = devs[static_cast<size_t>(dev)];
+    hipStream_t dst = sc.dstream->get();
+    const std::string ck = args.checkpoint_dir.empty() ? std::string() : spill_path(args.checkpoint_dir, p.d0, p.d1);
+    const SpillStatus st = ck.empty() ? SpillStatus::Missing : load_spill(ck, ckid.key, p.items);
+    p.resumed = st == SpillStatus::Loaded;
+    if (p.resumed) {
+      log_verbose("resumed DMs [" + std::to_string(p.d0) + "," + std::to_string(p.d1) + ") from checkpoint");
+      return;
+    }
+    if (st != SpillStatus::Missing)
+      log_info("checkpoint spill " + ck + " is " + spill_status_name(st) + "; recomputing DMs [" +
+               std::to_string(p.d0) + "," + std::to_string(p.d1) + ")");
+    p.items.clear();
+    uint8_t* rows = keep ? kept[static_cast<size_t>(dev)]->data() + static_cast<uint64_t>(p.d0) * rstride
+                         : sc.trials[k]->data();
+    if (sc.used[k] && !keep)
+      for (auto& ev : sc.freed[k]) PSOUP_HIP_CHECK(hipStreamWaitEvent(dst, ev->get(), 0));
+    sc.began[k].record(dst);
+    ds.dd->run(p.d0, p.d1, rows, rstride, setup.dedisp_kernel, dst);
+    sc.ready[k].record(dst);
+    sc.used[k] = true;
+    sc.rows[k] = rows;
+    if (keep)
+      for (int d = p.d0; d < p.d1; ++d) row_owner[static_cast<size_t>(d)] = dev;
+  };
+  // A chunk's searches are issued (search_prepared_many_async) and the
+  // previous chunk is collected only after them, so its acceleration
+  // distillation on the engine's host workers overlaps this chunk's GPU work
+  // (the Python driver's RankSearcher does the same).
+  ops.issue = [&](int dev, int slot, int k, const Chunk& p) {
+    DevSched& sc = *scheds[static_cast<size_t>(dev)];
+    SearchEngine& engine = *devs[static_cast<size_t>(dev)].engines[static_cast<size_t>(slot)];
+    hipStream_t st = engine.stream();
+    Stopwatch& ws = sc.search_w[static_cast<size_t>(slot)];
+    std::vector<Pending> pend;
+    PSOUP_HIP_CHECK(hipStreamWaitEvent(st, sc.ready[k].get(), 0));
+    ws.start();
+    std::vector<int> rows;
+    for (int d = p.d0 + slot; d < p.d1; d += neng) rows.push_back(d);
+    for (size_t r0 = 0; r0 < rows.size(); r0 += static_cast<size_t>(engine.max_prepare())) {
+      const int cnt = static_cast<int>(std::min(rows.size() - r0, static_cast<size_t>(engine.max_prepare())));
+      const int before = sc.processed.fetch_add(cnt);
+      if (args.fault_after_dms >= 0 && before + cnt > args.fault_after_dms)
+        PSOUP_THROW("fault injection: device " << dev << " aborting after " << before << " DM trials");
+      engine.prepare(sc.rows[k] + static_cast<uint64_t>(rows[r0] - p.d0) * rstride,
+                     static_cast<uint64_t>(neng) * rstride, geom.out_nsamps, cnt);
+      std::vector<SearchEngine::Job> jobs;
+      for (int i = 0; i < cnt; ++i) {
+        const int d = rows[r0 + static_cast<size_t>(i)];
+        const float dm = setup.dm_list[static_cast<size_t>(d)];
+        jobs.push_back(SearchEngine::Job{i, dm, d, setup.accel_plan.generate(dm)});
+        log_verbose("Searching " + std::to_string(jobs.back().accs.size()) + " acceleration trials for DM " +
+                    std::to_string(dm));
+        sh.accel_trials += jobs.back().accs.size();
+      }
+      // one flat trial list over these DMs (batches span DM boundaries)
+      pend.push_back(engine.search_prepared_many_async(jobs));
+    }
+    ws.stop();
+    sc.freed[k][static_cast<size_t>(slot)]->record(st);
+    return pend;
+  };
+  ops.collect = [&](int dev, int slot, std::vector<Pending>& pend, std::vector<Candidate>& out) {
+    DevSched& sc = *scheds[static_cast<size_t>(dev)];
+    SearchEngine& engine = *devs[static_cast<size_t>(dev)].engines[static_cast<size_t>(slot)];
+    Stopwatch& ws = sc.search_w[static_cast<size_t>(slot)];
+    ws.start();
+    for (auto& h : pend)
+      for (auto& c : engine.collect(h))
+        for (auto& x : c) out.push_back(std::move(x));
+    ws.stop();
+  };
+  ops.handover = [&](int dev, int k, Chunk& p) {
+    // every engine is done with this chunk: checkpoint and hand over
+    DevSched& sc = *scheds[static_cast<size_t>(dev)];
+    if (!p.resumed) {
+      float ms = 0.f;
+      PSOUP_HIP_CHECK(hipEventElapsedTime(&ms, sc.began[k].get(), sc.ready[k].get()));
+      sc.dd_ms += ms;
+      stable_sort_by_dm_idx(p.items);
+      if (!args.checkpoint_dir.empty()) save_spill(spill_path(args.checkpoint_dir, p.d0, p.d1), ckid.key, p.items);
+    }
     {
       std::lock_guard<std::mutex> lk(sh.mu);
-      if (!sh.error) sh.error = std::current_exception();
-      sh.next_dm.store(sh.ndm + 1000000);  // drain the queue
+      for (auto& x : p.items) sh.cands.push_back(x);
     }
-    sh.abort.store(true);
-    for (auto& sc : scheds) {
-      std::lock_guard<std::mutex> lk(sc->mu);
-      sc->cv.notify_all();
-    }
-    (void)dev;
+    const int done = sh.done_dms.fetch_add(p.d1 - p.d0) + (p.d1 - p.d0);
+    if (sh.progress) sh.progress->set(static_cast<double>(done) / sh.ndm);
   };
-  auto feeder = [&](int dev) {
+  ops.engine_exit = [&](int dev, int slot) {
     DevSched& sc = *scheds[static_cast<size_t>(dev)];
-    try {
-      PSOUP_HIP_CHECK(hipSetDevice(hip_dev(dev)));
-      DevState& ds = devs[static_cast<size_t>(dev)];
-      hipStream_t dst = sc.dstream->get();
-      int k = 0;
-      while (!sh.abort.load()) {
-        const int d0 = sh.next_dm.fetch_add(sh.chunk);
-        if (d0 >= sh.ndm) break;
-        const int d1 = std::min(sh.ndm, d0 + sh.chunk);
-        {
-          std::unique_lock<std::mutex> lk(sc.mu);
-          sc.cv.wait(lk, [&] { return sc.pub[k].pending == 0 || sh.abort.load(); });
-        }
-        if (sh.abort.load()) break;
-        Pub& p = sc.pub[k];
-        p.d0 = d0;
-        p.d1 = d1;
-        p.cands.clear();
-        const std::string ck = args.checkpoint_dir.empty() ? std::string() : spill_path(args.checkpoint_dir, d0, d1);
-        const SpillStatus st = ck.empty() ? SpillStatus::Missing : load_spill(ck, ckid.key, p.cands);
-        p.resumed = st == SpillStatus::Loaded;
-        if (p.resumed) {
-          log_verbose("resumed DMs [" + std::to_string(d0) + "," + std::to_string(d1) + ") from checkpoint");
-        } else {
-          if (st != SpillStatus::Missing)
-            log_info("checkpoint spill " + ck + " is " + spill_status_name(st) + "; recomputing DMs [" +
-                     std::to_string(d0) + "," + std::to_string(d1) + ")");
-          p.cands.clear();
-          uint8_t* rows = keep ? kept[static_cast<size_t>(dev)]->data() + static_cast<uint64_t>(d0) * rstride
-                               : sc.trials[k]->data();
-          if (sc.used[k] && !keep)
-            for (auto& ev : sc.freed[k]) PSOUP_HIP_CHECK(hipStreamWaitEvent(dst, ev->get(), 0));
-          sc.began[k].record(dst);
-          ds.dd->run(d0, d1, rows, rstride, setup.dedisp_kernel, dst);
-          sc.ready[k].record(dst);
-          sc.used[k] = true;
-          p.rows = rows;
-          if (keep)
-            for (int d = d0; d < d1; ++d) row_owner[static_cast<size_t>(d)] = dev;
-        }
-        {
-          std::lock_guard<std::mutex> lk(sc.mu);
-          p.pending = neng;
-          sc.published++;
-        }
-        sc.cv.notify_all();
-        k ^= 1;
-      }
-    } catch (...) {
-      fail(dev);
-    }
-    std::lock_guard<std::mutex> lk(sc.mu);
-    sc.done = true;
-    sc.cv.notify_all();
+    SearchEngine& engine = *devs[static_cast<size_t>(dev)].engines[static_cast<size_t>(slot)];
+    PSOUP_HIP_CHECK(hipStreamSynchronize(engine.stream()));
+    const double wt = sc.search_w[static_cast<size_t>(slot)].get_time();
+    const SearchCounters& c = engine.counters();
+    std::lock_guard<std::mutex> lk(sh.mu);
+    sh.search_s[static_cast<size_t>(dev)] += wt;
+    auto& st_map = sh.dev_stats[static_cast<size_t>(dev)];
+    st_map["search_s"] += wt;  // summed over the device's engines
+    st_map["dm_trials"] += static_cast<double>(c.dm_trials);
+    st_map["accel_trials"] += static_cast<double>(c.accel_trials);
+    st_map["peaks"] += static_cast<double>(c.peaks);
+    st_map["peak_overflows"] += static_cast<double>(c.overflows);
+    st_map["accel_loop_s"] += c.accel_s;
+    st_map["host_distill_s"] += c.host_s;
+    st_map["trials_distilled_on_gpu"] += static_cast<double>(c.gpu_distilled);
+    st_map["trials_distilled_on_host"] += static_cast<double>(c.host_distilled);
+    st_map["accel_distill_s"] += c.accd_s;
+    st_map["fft_mode"] = engine.fft_mode();
+    st_map["accel_batch"] = engine.batch_size();
+    st_map["sub_batch"] = engine.sub_batch();
   };
-  auto worker = [&](int dev, int slot) {
-    DevSched& sc = *scheds[static_cast<size_t>(dev)];
+  {
+    ChunkScheduler<decltype(ops)> sched(ops, ngpu, neng, sh.ndm, sh.chunk);
     try {
-      PSOUP_HIP_CHECK(hipSetDevice(hip_dev(dev)));
-      DevState& ds = devs[static_cast<size_t>(dev)];
-      SearchEngine& engine = *ds.engines[static_cast<size_t>(slot)];
-      hipStream_t st = engine.stream();
-      Stopwatch ws;
-      for (long g = 0;; ++g) {
-        {
-          std::unique_lock<std::mutex> lk(sc.mu);
-          sc.cv.wait(lk, [&] { return sc.published > g || sc.done || sh.abort.load(); });
-          if (sh.abort.load() || sc.published <= g) break;
-        }
-        const int k = static_cast<int>(g & 1);
-        Pub& p = sc.pub[k];
-        CandidateList local;
-        if (!p.resumed) {
-          PSOUP_HIP_CHECK(hipStreamWaitEvent(st, sc.ready[k].get(), 0));
-          ws.start();
-          std::vector<int> rows;
-          for (int d = p.d0 + slot; d < p.d1; d += neng) rows.push_back(d);
-          for (size_t r0 = 0; r0 < rows.size(); r0 += static_cast<size_t>(engine.max_prepare())) {
-            const int cnt = static_cast<int>(std::min(rows.size() - r0, static_cast<size_t>(engine.max_prepare())));
-            const int before = sc.processed.fetch_add(cnt);
-            if (args.fault_after_dms >= 0 && before + cnt > args.fault_after_dms)
-              PSOUP_THROW("fault injection: device " << dev << " aborting after " << before << " DM trials");
-            engine.prepare(p.rows + static_cast<uint64_t>(rows[r0] - p.d0) * rstride,
-                           static_cast<uint64_t>(neng) * rstride, geom.out_nsamps, cnt);
-            std::vector<SearchEngine::Job> jobs;
-            for (int i = 0; i < cnt; ++i) {
-              const int d = rows[r0 + static_cast<size_t>(i)];
-              const float dm = setup.dm_list[static_cast<size_t>(d)];
-              jobs.push_back(SearchEngine::Job{i, dm, d, setup.accel_plan.generate(dm)});
-              log_verbose("Searching " + std::to_string(jobs.back().accs.size()) + " acceleration trials for DM " +
-                          std::to_string(dm));
-              sh.accel_trials += jobs.back().accs.size();
-            }
-            // one flat trial list over these DMs (batches span DM boundaries)
-            std::vector<CandidateList> res = engine.search_prepared_many(jobs);
-            for (auto& c : res)
-              for (auto& x : c) local.push_back(std::move(x));
-          }
-          ws.stop();
-          sc.freed[k][static_cast<size_t>(slot)]->record(st);
-        }
-        bool last = false;
-        {
-          // the last engine keeps pending at 1 until the chunk is handed over,
-          // so the feeder cannot refill this slot while p.cands is read
-          std::lock_guard<std::mutex> lk(sc.mu);
-          for (auto& x : local) p.cands.push_back(std::move(x));
-          last = p.pending == 1;
-          if (!last) --p.pending;
-        }
-        if (last) {
-          // every engine is done with this chunk: checkpoint and hand over
-          if (!p.resumed) {
-            float ms = 0.f;
-            PSOUP_HIP_CHECK(hipEventElapsedTime(&ms, sc.began[k].get(), sc.ready[k].get()));
-            sc.dd_ms += ms;
-            std::stable_sort(p.cands.begin(), p.cands.end(),
-                             [](const Candidate& a, const Candidate& b) { return a.dm_idx < b.dm_idx; });
-            if (!args.checkpoint_dir.empty()) save_spill(spill_path(args.checkpoint_dir, p.d0, p.d1), ckid.key, p.cands);
-          }
-          {
-            std::lock_guard<std::mutex> lk(sh.mu);
-            for (auto& x : p.cands) sh.cands.push_back(x);
-          }
-          const int done = sh.done_dms.fetch_add(p.d1 - p.d0) + (p.d1 - p.d0);
-          if (sh.progress) sh.progress->set(static_cast<double>(done) / sh.ndm);
-          std::lock_guard<std::mutex> lk(sc.mu);
-          p.cands.clear();
-          p.pending = 0;
-          sc.cv.notify_all();
-        }
-      }
-      PSOUP_HIP_CHECK(hipStreamSynchronize(st));
-      const SearchCounters& c = engine.counters();
-      std::lock_guard<std::mutex> lk(sh.mu);
-      sh.search_s[static_cast<size_t>(dev)] += ws.get_time();
-      auto& st_map = sh.dev_stats[static_cast<size_t>(dev)];
-      st_map["search_s"] += ws.get_time();  // summed over the device's engines
-      st_map["dm_trials"] += static_cast<double>(c.dm_trials);
-      st_map["accel_trials"] += static_cast<double>(c.accel_trials);
-      st_map["peaks"] += static_cast<double>(c.peaks);
-      st_map["peak_overflows"] += static_cast<double>(c.overflows);
-      st_map["accel_loop_s"] += c.accel_s;
-      st_map["host_distill_s"] += c.host_s;
-      st_map["trials_distilled_on_gpu"] += static_cast<double>(c.gpu_distilled);
-      st_map["trials_distilled_on_host"] += static_cast<double>(c.host_distilled);
-      st_map["accel_distill_s"] += c.accd_s;
-      st_map["fft_mode"] = engine.fft_mode();
-      st_map["accel_batch"] = engine.batch_size();
-      st_map["sub_batch"] = engine.sub_batch();
+      sched.run();
     } catch (...) {
-      fail(dev);
+      sh.error = std::current_exception();
     }
-  };
-  std::vector<std::thread> threads;
-  for (int d = 0; d < ngpu; ++d) {
-    threads.emplace_back(feeder, d);
-    for (int e = 0; e < neng; ++e) threads.emplace_back(worker, d, e);
   }
-  for (auto& t : threads) t.join();
   for (int d = 0; d < ngpu; ++d) {
     PSOUP_HIP_CHECK(hipSetDevice(hip_dev(d)));
     scheds[static_cast<size_t>(d)]->dstream->sync();
@@ -549,14 +513,19 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     sh.dev_stats[static_cast<size_t>(d)]["dedispersion_s"] = dd;
   }
   t_search.stop();
+  mark("search");
   if (args.progress_bar) progress.stop();
   if (sh.error) std::rethrow_exception(sh.error);
 
   // Concatenation order of the reference depends on thread timing; sort by
   // DM index first so the global distillation is deterministic.
-  std::stable_sort(sh.cands.begin(), sh.cands.end(),
-                   [](const Candidate& a, const Candidate& b) { return a.dm_idx < b.dm_idx; });
+  Stopwatch t_gds;
+  t_gds.start();
+  stable_sort_by_dm_idx(sh.cands);
   CandidateList cands = global_distill_and_score(std::move(sh.cands), args, setup);
+  t_gds.stop();
+  mark("global_distill");
+  res.performance["global_distill_s"] = t_gds.get_time();
 
   // ---- folding (distributed over the devices by DM)
   t_fold.start();
@@ -639,6 +608,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     sort_by_folded_snr(cands);
   }
   t_fold.stop();
+  mark("fold");
 
   const size_t new_size = std::min(static_cast<size_t>(std::max(args.limit, 0)), cands.size());
   cands.resize(new_size);
@@ -659,6 +629,8 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   res.performance["dm_accel_trials"] = trials;
   res.performance["dm_accel_trials_per_sec"] = t_search.get_time() > 0 ? trials / t_search.get_time() : 0.0;
   res.performance["search_kernel_seconds_max_device"] = smax;
+  res.performance["search_loop_s"] = t_search.get_time();
+  res.performance["fold_s"] = t_fold.get_time();
   res.device_stats = sh.dev_stats;
   return res;
 }
@@ -717,7 +689,10 @@ std::string trace_json(const CmdLineOptions& args, const PipelineResult& res) {
   return o;
 }
 
-void write_outputs(const CmdLineOptions& args, const PipelineResult& res) {
+void write_outputs(const CmdLineOptions& args, const PipelineResult& res_in) {
+  Stopwatch tw;
+  tw.start();
+  PipelineResult res = res_in;  // (the trace adds the time taken to write the other outputs)
   CandidateFileWriter cf(args.outdir);
   cf.write_binary(res.candidates, "candidates.peasoup");
   OverviewWriter ow;
@@ -731,6 +706,8 @@ void write_outputs(const CmdLineOptions& args, const PipelineResult& res) {
   ow.add_timing_info(res.timers);
   ow.add_performance(res.performance);
   ow.to_file(args.outdir + "/overview.xml");
+  tw.stop();
+  res.performance["write_outputs_s"] = tw.get_time();
   if (!args.trace_json.empty()) {
     std::ofstream f(args.trace_json);
     if (!f) PSOUP_THROW("cannot write trace file " << args.trace_json);

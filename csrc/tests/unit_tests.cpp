@@ -7,9 +7,15 @@
 // usage: psoup_unit_tests [repo_root]   (repo_root locates the tutorial .fil)
 #include <unistd.h>
 
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <map>
+#include <mutex>
+#include <random>
 #include <cstring>
+#include <array>
 #include <functional>
 #include <iostream>
 #include <sstream>
@@ -24,6 +30,7 @@
 #include "psoup/common.hpp"
 #include "psoup/output.hpp"
 #include "psoup/plan.hpp"
+#include "psoup/scheduler.hpp"
 #include "psoup/sigproc.hpp"
 
 using namespace psoup;
@@ -256,7 +263,116 @@ void t_checkpoint_spills() {
   ::rmdir(d.c_str());
 }
 
+// The native pipeline's chunk scheduler (scheduler.hpp, run_pipeline's
+// feeder / engine threads) on fake devices: the slot a feeder fills is plain
+// memory that the engines read without a lock (as the real feeder's
+// dedispersion target), so a protocol that let a feeder refill a slot an
+// engine still reads, or two engines write one chunk's results unlocked, is
+// a data race the thread-sanitizer build reports.  Random delays vary the
+// interleavings; every DM must be handed over exactly once, resumed
+// (checkpointed) chunks included, and an injected fault must end every
+// thread of every device.
+namespace {
+struct FakeRun {
+  int ndev, neng, ndm, chunk;
+  int fault_after = -1;  // issue() throws once this many DMs were issued
+  bool racy = false;
+  std::mutex mu;
+  std::map<int, int> handed;                // DM -> times handed over
+  std::vector<std::array<int, 4>> slot_of;  // [dev * 2 + slot] = {d0, d1, fill count, -}: plain, feeder-written
+  std::atomic<int> issued{0};
+  std::atomic<long> seed{1};
+  void nap(int max_us) {
+    thread_local std::mt19937 rng(static_cast<unsigned>(seed.fetch_add(7919)));
+    std::this_thread::sleep_for(std::chrono::microseconds(rng() % static_cast<unsigned>(max_us + 1)));
+  }
+  static bool resumed_chunk(int d0, int chunk) { return (d0 / chunk) % 5 == 3; }
+  void run() {
+    slot_of.assign(static_cast<size_t>(ndev) * 2, {-1, -1, 0, 0});
+    SchedFns<int, std::vector<int>> ops;
+    using Chunk = SchedChunk<int>;
+    ops.prepare = [&](int dev, int k, Chunk& c) {
+      nap(150);
+      if (resumed_chunk(c.d0, chunk)) {  // a spill: results without any search
+        c.resumed = true;
+        for (int d = c.d0; d < c.d1; ++d) c.items.push_back(d);
+        return;
+      }
+      auto& sl = slot_of[static_cast<size_t>(dev) * 2 + k];
+      sl[0] = c.d0;  // "dedisperse" into the slot
+      sl[1] = c.d1;
+      sl[2]++;
+    };
+    ops.issue = [&](int dev, int eng, int k, const Chunk& c) {
+      const auto& sl = slot_of[static_cast<size_t>(dev) * 2 + k];
+      if (sl[0] != c.d0 || sl[1] != c.d1) throw std::runtime_error("slot refilled under a reading engine");
+      std::vector<int> mine;
+      for (int d = c.d0 + eng; d < c.d1; d += neng) mine.push_back(d);
+      if (fault_after >= 0 && issued.fetch_add(static_cast<int>(mine.size())) > fault_after)
+        throw std::runtime_error("fault injection");
+      nap(200);
+      return mine;
+    };
+    ops.collect = [&](int, int, std::vector<int>& t, std::vector<int>& out) {
+      nap(200);
+      out = t;
+    };
+    ops.handover = [&](int, int, Chunk& c) {
+      nap(50);
+      std::lock_guard<std::mutex> lk(mu);
+      for (int d : c.items) handed[d]++;
+    };
+    ChunkScheduler<decltype(ops)> sched(ops, ndev, neng, ndm, chunk);
+    sched.inject_race_for_test(racy);
+    sched.run();
+  }
+};
+}  // namespace
+
+void t_scheduler_protocol() {
+  for (int rep = 0; rep < 6; ++rep) {
+    FakeRun r{1 + rep % 3, 1 + rep % 2 + (rep == 5 ? 1 : 0), 181 + 17 * rep, 3 + rep};
+    r.run();
+    CHECK(static_cast<int>(r.handed.size()) == r.ndm);
+    for (const auto& [d, n] : r.handed) CHECK(d >= 0 && d < r.ndm && n == 1);
+  }
+}
+
+void t_scheduler_fault_ends_every_thread() {
+  for (int rep = 0; rep < 4; ++rep) {
+    FakeRun r{3, 2, 400, 4};
+    r.fault_after = 40 + 30 * rep;
+    bool threw = false;
+    try {
+      r.run();  // returns (every thread joined) and rethrows the fault
+    } catch (const std::runtime_error& e) {
+      threw = std::string(e.what()) == "fault injection";
+    }
+    CHECK(threw);
+    for (const auto& kv : r.handed) CHECK(kv.second == 1);
+    // one engine per device: the chunk issued before the failing one was
+    // still handed over (its checkpoint spill exists for a resume)
+    FakeRun one{1, 1, 100, 10};
+    one.fault_after = 15;
+    try {
+      one.run();
+    } catch (const std::runtime_error&) {
+    }
+    CHECK(one.handed.count(0) == 1 && one.handed.count(19) == 1 && one.handed.count(20) == 0);
+  }
+}
+
 int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "--inject-race") {
+    // (tests/test_native_unit.py: the thread-sanitizer build must report this)
+    for (int rep = 0; rep < 20; ++rep) {
+      FakeRun r{2, 3, 300, 6};
+      r.racy = true;
+      r.run();
+    }
+    std::cout << "race injected\n";
+    return 0;
+  }
   if (argc > 1) g_root = argv[1];
   std::vector<Case> cases = {
       {"prev_power_of_two", t_prev_power_of_two},
@@ -271,6 +387,8 @@ int main(int argc, char** argv) {
       {"threads_shared_readonly", t_threads_shared_readonly},
       {"host_pool", t_host_pool},
       {"checkpoint_spills", t_checkpoint_spills},
+      {"scheduler_protocol", t_scheduler_protocol},
+      {"scheduler_fault_ends_every_thread", t_scheduler_fault_ends_every_thread},
   };
   for (auto& c : cases) {
     const int before = g_fail;

@@ -210,7 +210,10 @@ class RankSearcher:
         if claim is None:
             order = iter(range(len(blocks)))
             claim = lambda: next(order, None)  # noqa: E731
-        cands: list = []
+        # the candidates stay native (CandidateBag): no per-candidate Python
+        # objects, no deep copies of association trees between the engine,
+        # the spills and the merge
+        cands = _C.CandidateBag()
         t_dd = timers.get("dedispersion") if timers else None
         t_s = timers.get("searching") if timers else None
         ntrials = 0
@@ -246,7 +249,7 @@ class RankSearcher:
             d0, d1 = blocks[j]
             ck = _C.spill_path(ckdir, d0, d1) if ckdir else ""
             if ck:
-                status, got = _C.load_spill(ck, ckey)
+                status, got = _C.load_spill_bag(ck, ckey)
                 if status == "loaded":
                     return j, ck, got, None
                 if status != "missing":
@@ -302,11 +305,11 @@ class RankSearcher:
 
         def finalize(blk):
             ck_, b0, b1, pend = blk
-            per_dm: Dict[int, list] = {}
+            per_dm: Dict[int, object] = {}
             for e_, jobs_, h_ in pend:
-                for (b, dm, d, accs), c in zip(jobs_, e_.collect(h_)):
+                for (b, dm, d, accs), c in zip(jobs_, _C.collect_bags(e_, h_)):
                     per_dm[d] = c
-            chunk_cands: list = []
+            chunk_cands = _C.CandidateBag()
             for d in range(b0, b1):
                 chunk_cands.extend(per_dm[d])
             if ck_:
@@ -431,7 +434,7 @@ class RankSearcher:
             t_s.start()
         torch.cuda.current_stream(self.ctx.device).synchronize()  # rows were produced on torch's stream
         e = self.engine
-        cands: list = []
+        cands = _C.CandidateBag()
         ntrials = 0
         base = rows.data_ptr()
         for p0 in range(0, rows.shape[0], e.max_prepare):
@@ -439,7 +442,7 @@ class RankSearcher:
             e.prepare(base + p0 * self.row_stride, self.row_stride, self.geom.out_nsamps, cnt)
             jobs = [(b, self.dm_list[d], d, self.accel_list(self.dm_list[d]))
                     for b, d in enumerate(range(dm_first + p0, dm_first + p0 + cnt))]
-            for (_, _, _, accs), c in zip(jobs, e.search_prepared_many(jobs)):
+            for (_, _, _, accs), c in zip(jobs, _C.collect_bags(e, e.search_prepared_many_async(jobs))):
                 cands.extend(c)
                 ntrials += len(accs)
         _C.stream_synchronize(e.stream)
@@ -472,7 +475,12 @@ class RankSearcher:
 
     def _executor(self):
         if self._pool is None:
-            self._pool = concurrent.futures.ThreadPoolExecutor(len(self.engines), thread_name_prefix="psoup-eng")
+            # engine threads bind the rank's GPU before any HIP/torch call
+            # (else a multi-GPU rank's worker could create a context on GPU 0)
+            kw = {}
+            if self.ctx.device.type == "cuda":
+                kw = dict(initializer=torch.cuda.set_device, initargs=(self.ctx.device,))
+            self._pool = concurrent.futures.ThreadPoolExecutor(len(self.engines), thread_name_prefix="psoup-eng", **kw)
         return self._pool
 
     def counters(self) -> Dict[str, float]:
@@ -752,10 +760,22 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     all_stats = pdist.gather_bytes(json.dumps(rank_stats).encode(), dst=0)
 
     # ---- candidate gather (RCCL) + global distillation on rank 0
-    blobs = pdist.gather_bytes(_C.serialize_candidates(local), dst=None)
     total_trials = sum(weights)
-    # rank order, stable by DM index, then the global distillation: one native call
-    cands = _C.merge_candidate_blobs(blobs, args, rs.header)
+    if not ctx.distributed:
+        # a world of one: the merge takes the rank's own list (no serialisation)
+        cands = _C.merge_local(local, args, rs.header)
+    else:
+        # every rank's list to rank 0 only (RCCL gather of raw buffers), merged
+        # there: rank order, stable by DM index, global distillation, scoring
+        bufs = pdist.gather_buffers(torch.from_numpy(_C.serialize_candidates_array(local)), dst=0)
+        del local
+        cands = (_C.merge_candidate_buffers([(b.data_ptr(), b.numel()) for b in bufs], args, rs.header)
+                 if ctx.is_root else None)
+        del bufs
+        if args.npdmp > 0:
+            # the fold stage needs the top candidates' frequency, acceleration
+            # and DM row on every rank (not their association trees)
+            cands = _FoldView.share(cands, min(args.npdmp, len(cands)) if cands is not None else 0)
     search_wall = pdist.all_reduce_max_float(search_wall)
 
     # ---- distributed folding (all ranks hold identical `cands`)
@@ -793,14 +813,14 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
                     c.set_fold_array(fold, 64, 16)
             # sort_by_folded_snr's permutation, applied to the Python list
             order = _C.sort_order_by_folded_snr([c.snr for c in cands], [c.folded_snr for c in cands])
-            cands = [cands[i] for i in order]
+            cands.permute(order)
         fold_stats = dict(getattr(rs, "fold_stats", {}))
         fold_stats.update({"fold_call_s": t_f1 - t_f0, "fold_merge_s": time.perf_counter() - t_f1})
     timers["folding"].stop()
     if not ctx.is_root:
         timers["total"].stop()
         return None
-    cands = cands[: max(0, args.limit)]
+    cands.truncate(max(0, args.limit))
     timers["total"].stop()
     perf = {
         "dm_accel_trials": float(total_trials),
@@ -816,6 +836,46 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     if write:
         write_outputs(args, res)
     return res
+
+
+class _FoldView:
+    """Rank r != 0's view of the merged list for the fold stage: the first
+    ``n`` candidates' (freq, acc, dm_idx), broadcast from rank 0 (20 bytes per
+    candidate) -- indexable like the list, for :meth:`RankSearcher.fold`."""
+
+    class _C:
+        __slots__ = ("freq", "acc", "dm_idx")
+
+        def __init__(self, freq, acc, dm_idx):
+            self.freq, self.acc, self.dm_idx = freq, acc, dm_idx
+
+    def __init__(self, rows):
+        self._rows = rows
+
+    def __len__(self):
+        return len(self._rows)
+
+    def __getitem__(self, i):
+        return self._rows[i]
+
+    def __bool__(self):
+        return bool(self._rows)
+
+    @staticmethod
+    def share(cands, n):
+        """On rank 0 return ``cands`` (after broadcasting its head); elsewhere a _FoldView."""
+        import numpy as np
+
+        ctx = pdist.context()
+        if ctx.is_root:
+            head = np.zeros(n, dtype=[("freq", "<f4"), ("acc", "<f4"), ("dm_idx", "<i4")])
+            for i in range(n):
+                head[i] = (cands[i].freq, cands[i].acc, cands[i].dm_idx)
+            pdist.broadcast_object_bytes(head.tobytes())
+            return cands
+        raw = pdist.broadcast_object_bytes(None)
+        head = np.frombuffer(raw, dtype=[("freq", "<f4"), ("acc", "<f4"), ("dm_idx", "<i4")])
+        return _FoldView([_FoldView._C(float(r["freq"]), float(r["acc"]), int(r["dm_idx"])) for r in head])
 
 
 def trace_dict(args, res: SearchResult) -> dict:

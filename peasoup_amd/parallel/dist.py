@@ -312,6 +312,32 @@ def gather_bytes(payload: bytes, dst: Optional[int] = 0) -> Optional[List[bytes]
     return [bytes(o[:s].cpu().numpy().tobytes()) for o, s in zip(outs, sizes_i)]
 
 
+def gather_buffers(payload: torch.Tensor, dst: int = 0) -> Optional[List[torch.Tensor]]:
+    """Variable-length gather of host uint8 tensors to ``dst`` only (sizes
+    all-gathered, then one padded ``dist.gather``; RCCL on GPUs): the list of
+    every rank's buffer (host tensors, rank order) on ``dst``, None elsewhere.
+    Unlike :func:`gather_bytes` nothing reaches the other ranks and no Python
+    ``bytes`` objects are made (candidate lists are tens of MB per rank)."""
+    ctx = context()
+    assert payload.dtype == torch.uint8 and payload.dim() == 1
+    if not ctx.distributed:
+        return [payload]
+    dev = _comm_device(ctx)
+    n = torch.tensor([payload.numel()], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(ctx.world_size)]
+    dist.all_gather(sizes, n)
+    sizes_i = [int(s.item()) for s in sizes]
+    mx = max(1, max(sizes_i))
+    buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
+    if payload.numel():
+        buf[: payload.numel()].copy_(payload)
+    outs = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(ctx.world_size)] if ctx.rank == dst else None
+    dist.gather(buf, outs, dst=dst)
+    if ctx.rank != dst:
+        return None
+    return [o[:s].cpu() for o, s in zip(outs, sizes_i)]
+
+
 def broadcast_object_bytes(payload: Optional[bytes], src: int = 0) -> bytes:
     """Broadcast a byte string of unknown length from ``src``."""
     ctx = context()

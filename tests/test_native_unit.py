@@ -31,3 +31,16 @@ def test_native_unit_tests_under_host_sanitizers(san):
     r = _run(os.path.join(REPO, "bin", f"psoup_unit_tests_{san}"))
     assert "ERROR: AddressSanitizer" not in r.stderr and "WARNING: ThreadSanitizer" not in r.stderr
     assert "runtime error" not in r.stderr
+
+
+def test_thread_sanitizer_sees_an_injected_scheduler_race():
+    """The TSan build runs the native scheduler's protocol clean (above); with
+    the hand-over's lock removed (--inject-race) it must report the race, so a
+    clean run is evidence, not an unobserved path."""
+    from peasoup_amd import _build
+
+    _build.build(sanitize="thread")
+    exe = os.path.join(REPO, "bin", "psoup_unit_tests_thread")
+    r = subprocess.run([exe, "--inject-race"], capture_output=True, text=True, timeout=300)
+    assert "WARNING: ThreadSanitizer: data race" in r.stderr, r.stderr[-3000:]
+    assert "ChunkScheduler" in r.stderr and "finalize" in r.stderr
