@@ -15,6 +15,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <deque>
@@ -310,6 +312,43 @@ inline uint64_t prev_power_of_two(uint64_t val) {
   uint64_t n = 1;
   while (n * 2 < val) n *= 2;
   return n;
+}
+
+// fn(i0, i1) over contiguous ranges of [0, n) on up to max_threads threads
+// (one range per thread, the calling thread included); exceptions rethrown.
+template <class F>
+void parallel_ranges(size_t n, unsigned max_threads, F&& fn) {
+  const unsigned hw = std::max(1u, std::min(max_threads, std::thread::hardware_concurrency()));
+  const size_t nt = std::max<size_t>(1, std::min<size_t>(hw, n));
+  if (nt == 1) {
+    if (n) fn(size_t(0), n);
+    return;
+  }
+  std::vector<std::exception_ptr> err(nt);
+  std::vector<std::thread> th;
+  auto run = [&](size_t t) {
+    try {
+      fn(n * t / nt, n * (t + 1) / nt);
+    } catch (...) {
+      err[t] = std::current_exception();
+    }
+  };
+  for (size_t t = 1; t < nt; ++t) th.emplace_back(run, t);
+  run(0);
+  for (auto& x : th) x.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+}
+
+// fn(i) for every i in [0, n) on up to max_threads threads taking indices one
+// at a time (uneven items: a candidate list's association trees); exceptions
+// rethrown.
+template <class F>
+void parallel_each(size_t n, unsigned max_threads, F&& fn) {
+  std::atomic<size_t> next{0};
+  parallel_ranges(std::min<size_t>(n, max_threads), max_threads, [&](size_t, size_t) {
+    for (size_t i; (i = next.fetch_add(1)) < n;) fn(i);
+  });
 }
 
 // Small fixed-size host worker pool for data-parallel host stages (peak

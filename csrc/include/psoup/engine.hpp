@@ -83,8 +83,21 @@ class DeviceFilterbank {
 // links) and unpacks it while the next chunk is in flight.  fbs[i] lives on
 // HIP device devices[i] (the same device may repeat: a device-local copy).
 // Returns when every device holds its unpacked filterbank.
+// (read(off, n, dst): host bytes [off, off + n) of the packed data into dst)
+using HostReader = std::function<void(uint64_t, uint64_t, uint8_t*)>;
+void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std::vector<int>& devices,
+                            const HostReader& read);
 void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std::vector<int>& devices,
                             const uint8_t* h_packed);
+// straight from the file (threaded pread into the pinned stages)
+void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std::vector<int>& devices,
+                            const Filterbank& fb);
+// Host bytes [0, bytes) -> d_dst on stream s in `chunk`-byte pieces through two
+// pinned stages filled by `read` (chunk k+1 is read while chunk k copies);
+// on_chunk(off, n) runs after each piece's copy is enqueued.  Returns when the
+// stages are free (the copies done).
+void staged_upload(uint64_t bytes, uint64_t chunk, const HostReader& read, uint8_t* d_dst, hipStream_t s,
+                   const std::function<void(uint64_t, uint64_t)>& on_chunk = {});
 
 class Dedisperser {
  public:
@@ -114,30 +127,32 @@ class Dedisperser {
   // MFMA kernel (leading tiles whose offset spread is narrow enough for the
   // one-hot GEMM to beat the VALU kernels), [split, d1) the VALU kernels
   int mfma_lds_split(int d0, int d1);
-  // Build every table Auto / MFMA / VALU runs use (otherwise built on the
-  // first run that needs them, with blocking uploads, mid-search: the
-  // 2026-DM config-4 list's first VALU tile stalled the host 64 ms)
-  void warm();
+  // Build the tables Auto / MFMA / VALU runs use over DMs [d0, d1) (d1 < 0:
+  // the whole list; a static shard needs only its own).  Otherwise they are
+  // built on the first run that needs them, with blocking uploads,
+  // mid-search (the 2026-DM config-4 list's first VALU tile stalled the host
+  // 64 ms); a run outside the built tiles rebuilds the whole list's.
+  void warm(int d0 = 0, int d1 = -1);
 
  private:
   void build_resident_plan();
-  // (offs: the whole list's offset table when the caller has it)
-  void build_valu_tables(const std::vector<int32_t>* offs = nullptr);
-  void build_mfma_lds_tables(const std::vector<int32_t>* offs = nullptr, bool upload = true);
-  void upload_mfma_lds_tables();
-  std::unique_ptr<kern::MfmaLdsPlan> ml_plan_;  // host plan between build and upload
+  void ensure_tables(int d0, int d1);
+  void build_tables(int t0, int t1);  // tiles [t0, t1)
+  // offs: rows of DMs [e0, ...) covering tiles [t0, t1 + 1)
+  void build_valu_tables(const std::vector<int32_t>& offs, int e0, int t0, int t1);
+  void upload_mfma_lds_tables(const kern::MfmaLdsPlan& plan);
   void run_mfma_lds(int d0, int d1, uint8_t* out, uint64_t out_stride, hipStream_t s);
   const DeviceFilterbank& fb_;
   hipStream_t stream_;
   DeviceBuffer<int32_t> d_offsets_, d_kill_, d_active_, d_list_offT_;
-  bool resident_ = false, valu_ready_ = false;
+  bool resident_ = false;
+  int tab_t0_ = 0, tab_t1_ = 0;  // tiles the VALU and LDS-MFMA tables cover
   std::vector<int32_t> h_tile_steps_;  // global-load MFMA plan's steps per tile (from the VALU tables)
   int ldo_ = 0;                        // columns of r_offT_
   std::vector<int32_t> h_tile_win_;    // LDS kernel: largest channel window per 32-DM tile (bytes)
   DeviceBuffer<int32_t> r_steps_, r_tile_info_, r_offT_, r_wmin_;
   DeviceBuffer<int8_t> r_deltas_;
-  // LDS-fed MFMA plan of the whole DM list (resident, built on first use)
-  bool ml_ready_ = false;
+  // LDS-fed MFMA plan (tiles [tab_t0_, tab_t1_) built, the others not-ok)
   int ml_ngroups_ = 0;
   std::vector<int32_t> ml_tile_ok_, ml_tile_steps_;
   DeviceBuffer<int32_t> ml_steps_, ml_ginfo_, ml_wmin_;

@@ -99,7 +99,10 @@ struct MfmaLdsPlan {
   std::vector<int32_t> tile_ok;     // [ntiles]
   std::vector<int32_t> tile_steps;  // [ntiles] MFMA steps of the tile (0 if not ok)
 };
-void build_mfma_lds_plan(const int32_t* offsets, int ndm, int nchans, const int32_t* killmask, MfmaLdsPlan& plan);
+// Tiles [tile0, tile1) of the plan (tile1 < 0: to the end; the others are
+// left not-ok); offsets[(d - d_first) * nchans + c] for the DMs they cover.
+void build_mfma_lds_plan(const int32_t* offsets, int ndm, int nchans, const int32_t* killmask, MfmaLdsPlan& plan,
+                         int tile0 = 0, int tile1 = -1, int d_first = 0);
 // Tiles [tile0, tile0 + ntiles) of a plan (pointers already offset to tile0
 // for ginfo, relo and wmin; ndm DMs from the range's first): bit-identical to
 // dedisperse_direct.  Rows are read up to 1280 bytes past t + wmin.

@@ -56,6 +56,7 @@ class Element {
     attributes_[key] = "'" + fmt(v) + "'";
   }
   std::string to_string(bool header = false, int level = 0) const;
+  void write(std::string& out, int level) const;  // appends this element's text
   const std::string& name() const { return name_; }
   const std::vector<Element>& children() const { return children_; }
 

@@ -78,7 +78,8 @@ struct PipelineResult {
 
 // Per-stage JSON trace (--trace_json): timers, performance, per-device
 // counters and the search configuration.
-std::string trace_json(const CmdLineOptions& args, const PipelineResult& res);
+std::string trace_json(const CmdLineOptions& args, const PipelineResult& res,
+                       const std::map<std::string, double>& extra_performance = {});
 
 // Runs the whole search in this process on `ndevices` GPUs (threads).
 PipelineResult run_pipeline(const CmdLineOptions& args);

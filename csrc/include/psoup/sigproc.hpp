@@ -85,12 +85,18 @@ class Filterbank {
   // filterbank.hpp:190-196, evaluated in float like the reference.
   float cfreq() const;
   void write(const std::string& filename) const;
+  // Bytes [off, off + n) of the data block into dst: pread() from the file on
+  // up to nthreads threads when file-backed (the device upload's staging
+  // reads), else a copy.
+  void read_data(uint64_t off, uint64_t n, uint8_t* dst, int nthreads = 4) const;
 
  private:
   SigprocHeader hdr_;
   std::shared_ptr<void> owner_;  // munmap / vector owner
   const uint8_t* data_ = nullptr;
   uint64_t data_bytes_ = 0;
+  std::string path_;  // file-backed: the file and its data block's offset
+  uint64_t data_offset_ = 0;
 };
 
 // SIGPROC .tim time series (8-bit unsigned or 32-bit float samples).

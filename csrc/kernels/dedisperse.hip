@@ -754,7 +754,8 @@ void dedisperse_valu(const int8_t* chan_major, uint64_t chan_stride, const int32
   post_launch_check("dedisperse_valu_kernel", s);
 }
 
-void build_mfma_lds_plan(const int32_t* offsets, int ndm, int nchans, const int32_t* killmask, MfmaLdsPlan& plan) {
+void build_mfma_lds_plan(const int32_t* offsets, int ndm, int nchans, const int32_t* killmask, MfmaLdsPlan& plan,
+                         int tile0, int tile1, int d_first) {
   constexpr int CG = kMfmaLdsGroup;
   std::vector<int> active;
   for (int c = 0; c < nchans; ++c)
@@ -771,10 +772,15 @@ void build_mfma_lds_plan(const int32_t* offsets, int ndm, int nchans, const int3
   plan.wmin.assign(static_cast<size_t>(ntiles) * std::max(1, na), 0);
   plan.tile_ok.assign(static_cast<size_t>(ntiles), 0);
   plan.tile_steps.assign(static_cast<size_t>(ntiles), 0);
-  for (int T = 0; T < ntiles; ++T) {
+  // tiles outside [tile0, tile1) stay not-ok (no steps); offsets hold the
+  // rows of DMs [d_first, ...)
+  if (tile1 < 0 || tile1 > ntiles) tile1 = ntiles;
+  tile0 = std::max(0, tile0);
+  PSOUP_CHECK(d_first <= tile0 * 32, "MFMA-LDS plan: offsets start after the first tile");
+  for (int T = tile0; T < tile1; ++T) {
     auto off = [&](int dd, int c) {
       const int d = std::min(T * 32 + dd, ndm - 1);  // pad the last tile with the last DM
-      return offsets[static_cast<size_t>(d) * nchans + c];
+      return offsets[static_cast<size_t>(d - d_first) * nchans + c];
     };
     bool ok = true;
     std::vector<int> lo(static_cast<size_t>(na)), hi(static_cast<size_t>(na));

@@ -218,6 +218,25 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("data_bytes", &Filterbank::data_bytes)
       .def_property_readonly("data_address", [](const Filterbank& fb) { return reinterpret_cast<uintptr_t>(fb.data()); })
       .def("cfreq", &Filterbank::cfreq)
+      .def(
+          "read_into",
+          [](const Filterbank& fb, uint64_t off, uint64_t n, uintptr_t dst, int nthreads) {
+            fb.read_data(off, n, P<uint8_t>(dst), nthreads);
+          },
+          py::arg("off"), py::arg("n"), py::arg("dst"), py::arg("nthreads") = 4, py::call_guard<py::gil_scoped_release>())
+      .def(
+          "upload",
+          [](const Filterbank& fb, uintptr_t dptr, uint64_t nbytes, uintptr_t stream) {
+            // the data block -> device (threaded pread into two pinned 16 MB
+            // stages, copies overlapping the reads); returns when it landed
+            const uint64_t n = nbytes ? nbytes : fb.data_bytes();
+            PSOUP_CHECK(n <= fb.data_bytes(), "upload: more bytes than the data block");
+            auto s = reinterpret_cast<hipStream_t>(stream);
+            staged_upload(n, 16ull << 20, [&fb](uint64_t o, uint64_t k, uint8_t* d) { fb.read_data(o, k, d); },
+                          P<uint8_t>(dptr), s);
+            PSOUP_HIP_CHECK(hipStreamSynchronize(s));
+          },
+          py::arg("dptr"), py::arg("nbytes") = 0, py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>())
       .def("data", [](const Filterbank& fb) {
         // zero-copy read-only view of the mmapped data block
         py::array_t<uint8_t> a({static_cast<py::ssize_t>(fb.data_bytes())}, {1}, fb.data(), py::cast(fb));
@@ -903,7 +922,8 @@ PYBIND11_MODULE(_C, m) {
       .def("choose", &Dedisperser::choose, py::arg("d0"), py::arg("d1"))
       .def("mfma_steps_per_channel", &Dedisperser::mfma_steps_per_channel, py::arg("d0"), py::arg("d1"))
       .def("mfma_lds_split", &Dedisperser::mfma_lds_split, py::arg("d0"), py::arg("d1"))
-      .def("warm", &Dedisperser::warm, py::call_guard<py::gil_scoped_release>())
+      .def("warm", &Dedisperser::warm, py::arg("d0") = 0, py::arg("d1") = -1,
+           py::call_guard<py::gil_scoped_release>())
       .def_property_readonly_static("tile_dms", [](py::object) { return Dedisperser::kTileDms; });
 
   py::class_<Whitener>(m, "Whitener")

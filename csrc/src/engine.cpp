@@ -105,13 +105,37 @@ void DeviceFilterbank::unpack_chunk(const uint8_t* d_packed, uint64_t t0, uint64
   kern::unpack_transpose(d_packed, ns, g_.nchans, g_.nbits, chan_.data() + t0, stride_, g_.bias, s ? s : stream_);
 }
 
+void staged_upload(uint64_t bytes, uint64_t chunk, const HostReader& read, uint8_t* d_dst, hipStream_t s,
+                   const std::function<void(uint64_t, uint64_t)>& on_chunk) {
+  if (bytes == 0) return;
+  chunk = std::max<uint64_t>(1, std::min(chunk, bytes));
+  // two pinned stages: the host reads chunk k+1 while chunk k's copy runs
+  // (pinning is ~0.1 ms per MB: 16 MB stages, not the whole file)
+  PinnedBuffer<uint8_t> stage[2];
+  Event staged[2];
+  bool used[2] = {false, false};
+  int slot = 0;
+  for (uint64_t off = 0; off < bytes; off += chunk, slot ^= 1) {
+    const uint64_t nb = std::min(chunk, bytes - off);
+    if (stage[slot].size() < nb) stage[slot].resize(nb);
+    if (used[slot]) staged[slot].sync();
+    read(off, nb, stage[slot].data());
+    PSOUP_HIP_CHECK(hipMemcpyAsync(d_dst + off, stage[slot].data(), nb, hipMemcpyHostToDevice, s));
+    staged[slot].record(s);
+    used[slot] = true;
+    if (on_chunk) on_chunk(off, nb);
+  }
+  for (int i = 0; i < 2; ++i)
+    if (used[i]) staged[i].sync();
+}
+
 void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std::vector<int>& devices,
-                            const uint8_t* h_packed) {
+                            const HostReader& read) {
   PSOUP_CHECK(!fbs.empty() && fbs.size() == devices.size(), "load_filterbank_fanout: one device per filterbank");
   const DedispGeometry& g = fbs[0]->geometry();
   const uint64_t bps = static_cast<uint64_t>(g.nchans) * g.nbits / 8;  // bytes per sample
   const uint64_t bytes = g.nsamps * bps;
-  const uint64_t chunk = std::max<uint64_t>(256, ((64ull << 20) / bps) / 256 * 256);  // samples per chunk
+  const uint64_t chunk = std::max<uint64_t>(256, ((16ull << 20) / bps) / 256 * 256);  // samples per chunk
   int prev = 0;
   PSOUP_HIP_CHECK(hipGetDevice(&prev));
   const size_t n = fbs.size();
@@ -122,32 +146,10 @@ void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std
     packed[i].resize(bytes);
   }
   PSOUP_HIP_CHECK(hipSetDevice(devices[0]));
-  // a file within one chunk goes up straight from its (mapped) pages: pinning
-  // a staging buffer and freeing it cost more than the copy (~2 ms for 3 MB)
-  const bool direct = g.nsamps <= chunk;
-  PinnedBuffer<uint8_t> stage[2];
-  Event staged[2], landed;
-  // staging sized to the file when it is shorter than a chunk (pinning
-  // 2 x 64 MiB took ~40 ms, more than a small file's whole upload)
-  const uint64_t stage_bytes = std::min(chunk, g.nsamps) * bps;
-  if (!direct)
-    for (int i = 0; i < 2; ++i) stage[i].resize(stage_bytes);
-  bool used[2] = {false, false};
   hipStream_t s0 = fbs[0]->stream();
-  int slot = 0;
-  for (uint64_t t0 = 0; t0 < g.nsamps; t0 += chunk, slot ^= 1) {
-    const uint64_t ns = std::min(chunk, g.nsamps - t0);
-    const uint64_t off = t0 * bps, nb = ns * bps;
-    PSOUP_HIP_CHECK(hipSetDevice(devices[0]));
-    if (direct) {
-      PSOUP_HIP_CHECK(hipMemcpy(packed[0].data() + off, h_packed + off, nb, hipMemcpyHostToDevice));
-    } else {
-      if (used[slot]) staged[slot].sync();
-      std::memcpy(stage[slot].data(), h_packed + off, nb);
-      PSOUP_HIP_CHECK(hipMemcpyAsync(packed[0].data() + off, stage[slot].data(), nb, hipMemcpyHostToDevice, s0));
-      staged[slot].record(s0);
-      used[slot] = true;
-    }
+  Event landed;
+  staged_upload(bytes, chunk * bps, read, packed[0].data(), s0, [&](uint64_t off, uint64_t nb) {
+    const uint64_t t0 = off / bps, ns = nb / bps;
     landed.record(s0);
     fbs[0]->unpack_chunk(packed[0].data() + off, t0, ns);
     for (size_t i = 1; i < n; ++i) {
@@ -157,18 +159,30 @@ void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std
       PSOUP_HIP_CHECK(hipMemcpyPeerAsync(packed[i].data() + off, devices[i], packed[0].data() + off, devices[0], nb, si));
       fbs[i]->unpack_chunk(packed[i].data() + off, t0, ns);
     }
-  }
+    PSOUP_HIP_CHECK(hipSetDevice(devices[0]));
+  });
   for (size_t i = 0; i < n; ++i) {
     PSOUP_HIP_CHECK(hipSetDevice(devices[i]));
     PSOUP_HIP_CHECK(hipStreamSynchronize(fbs[i]->stream()));
   }
-  PSOUP_HIP_CHECK(hipSetDevice(prev));
   // the transient copies are freed on their own devices
   for (size_t i = 0; i < n; ++i) {
     PSOUP_HIP_CHECK(hipSetDevice(devices[i]));
     packed[i] = DeviceBuffer<uint8_t>();
   }
   PSOUP_HIP_CHECK(hipSetDevice(prev));
+}
+
+void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std::vector<int>& devices,
+                            const uint8_t* h_packed) {
+  load_filterbank_fanout(fbs, devices,
+                         [h_packed](uint64_t off, uint64_t n, uint8_t* dst) { std::memcpy(dst, h_packed + off, n); });
+}
+
+void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std::vector<int>& devices,
+                            const Filterbank& fb) {
+  load_filterbank_fanout(fbs, devices,
+                         [&fb](uint64_t off, uint64_t n, uint8_t* dst) { fb.read_data(off, n, dst); });
 }
 
 Dedisperser::Dedisperser(const DeviceFilterbank& fb, hipStream_t stream) : fb_(fb), stream_(stream) {
@@ -184,29 +198,62 @@ Dedisperser::Dedisperser(const DeviceFilterbank& fb, hipStream_t stream) : fb_(f
     PSOUP_HIP_CHECK(hipMemcpy(d_active_.data(), active.data(), active.size() * 4, hipMemcpyHostToDevice));
 }
 
-void Dedisperser::warm() {
-  // The tables Auto needs (VALU offsets and windows, LDS-fed MFMA plan), from
-  // one offset table, the two builds in parallel.  The whole-list global-load
-  // MFMA plan (~380k steps on the 2026-DM config-4 list, 136 ms on the host)
-  // serves only an explicit --dedisp_kernel mfma over tiles the LDS kernel
-  // cannot take: built on first such use.
+void Dedisperser::warm(int d0, int d1) {
+  // The tables Auto needs (VALU offsets and windows, LDS-fed MFMA plan) for
+  // the tiles of [d0, d1) (a rank's static shard; default the whole list),
+  // from one offset table, the two builds in parallel.  A later range outside
+  // them rebuilds the whole list's (ensure_tables).  The whole-list
+  // global-load MFMA plan (~380k steps on the 2026-DM config-4 list, 136 ms on
+  // the host) serves only an explicit --dedisp_kernel mfma over tiles the LDS
+  // kernel cannot take: built on first such use.
   const auto& g = fb_.geometry();
-  if (g.dm_list.empty() || g.nactive == 0) return;
-  const std::vector<int32_t> offs = g.offsets(0, static_cast<int>(g.dm_list.size()));
+  const int ndm = static_cast<int>(g.dm_list.size());
+  if (ndm == 0 || g.nactive == 0) return;
+  if (d1 < 0 || d1 > ndm) d1 = ndm;
+  d0 = std::max(0, std::min(d0, d1 - 1));
+  const int t0 = d0 / kTileDms, t1 = (d1 - 1) / kTileDms + 1;
+  if (tab_t0_ <= t0 && t1 <= tab_t1_) return;
+  build_tables(t0, t1);
+}
+
+void Dedisperser::ensure_tables(int d0, int d1) {
+  const int ndm = static_cast<int>(fb_.geometry().dm_list.size());
+  const int t0 = d0 / kTileDms, t1 = (std::max(d0 + 1, d1) - 1) / kTileDms + 1;
+  if (tab_t0_ <= t0 && t1 <= tab_t1_) return;
+  build_tables(0, (ndm + kTileDms - 1) / kTileDms);
+}
+
+void Dedisperser::build_tables(int t0, int t1) {
+  const auto& g = fb_.geometry();
+  const int ndm = static_cast<int>(g.dm_list.size());
+  // offsets of DMs [t0 * 32, (t1 + 1) * 32): the VALU tables' columns run one
+  // tile past the last (a range from an unaligned DM reads up to 31 beyond it)
+  const int e0 = t0 * kTileDms, e1 = std::min(ndm, (t1 + 1) * kTileDms);
+  const std::vector<int32_t> offs = g.offsets(e0, e1);
   std::exception_ptr err;
+  std::unique_ptr<kern::MfmaLdsPlan> plan;
   std::thread th;
-  if (!ml_ready_)
+  if (g.nactive > 0)
     th = std::thread([&] {
       try {
-        build_mfma_lds_tables(&offs, /*upload=*/false);
+        std::vector<int32_t> kill(g.killmask.begin(), g.killmask.end());
+        plan = std::make_unique<kern::MfmaLdsPlan>();
+        kern::build_mfma_lds_plan(offs.data(), ndm, g.nchans, kill.data(), *plan, t0, t1, e0);
       } catch (...) {
         err = std::current_exception();
       }
     });
-  if (!valu_ready_) build_valu_tables(&offs);
+  try {
+    build_valu_tables(offs, e0, t0, t1);
+  } catch (...) {
+    if (th.joinable()) th.join();
+    throw;
+  }
   if (th.joinable()) th.join();
   if (err) std::rethrow_exception(err);
-  if (!ml_ready_) upload_mfma_lds_tables();
+  if (plan) upload_mfma_lds_tables(*plan);
+  tab_t0_ = t0;
+  tab_t1_ = t1;
 }
 
 void Dedisperser::build_resident_plan() {
@@ -226,51 +273,53 @@ void Dedisperser::build_resident_plan() {
   resident_ = true;
 }
 
-void Dedisperser::build_valu_tables(const std::vector<int32_t>* offs_in) {
+void Dedisperser::build_valu_tables(const std::vector<int32_t>& offs, int e0, int t0, int t1) {
   // offsets transposed to [active channel][DM], columns padded (with the last
-  // DM) past the last workgroup of any range
+  // DM) past the last workgroup of any range; filled for the columns of tiles
+  // [t0, t1 + 1) only (offs: rows of DMs [e0, ...))
   const auto& g = fb_.geometry();
   const int ndm = static_cast<int>(g.dm_list.size());
-  const std::vector<int32_t> offs_own = offs_in ? std::vector<int32_t>() : g.offsets(0, ndm);
-  const std::vector<int32_t>& offs = offs_in ? *offs_in : offs_own;
   std::vector<int> active;
   for (int c = 0; c < g.nchans; ++c)
     if (g.killmask[c]) active.push_back(c);
   ldo_ = (ndm + kTileDms - 1) / kTileDms * kTileDms + kTileDms;
-  std::vector<int32_t> t(static_cast<size_t>(std::max<size_t>(1, active.size())) * ldo_, 0);
+  const int j0 = t0 * kTileDms, j1 = std::min(ldo_, (t1 + 1) * kTileDms), w = j1 - j0;
+  const size_t na = std::max<size_t>(1, active.size());
+  std::vector<int32_t> t(na * static_cast<size_t>(w), 0);
   for (size_t ci = 0; ci < active.size(); ++ci)
-    for (int d = 0; d < ldo_; ++d)
-      t[ci * ldo_ + d] = offs[static_cast<size_t>(std::min(d, ndm - 1)) * g.nchans + active[ci]];
-  r_offT_.resize(t.size());
-  PSOUP_HIP_CHECK(hipMemcpy(r_offT_.data(), t.data(), t.size() * 4, hipMemcpyHostToDevice));
+    for (int j = j0; j < j1; ++j)
+      t[ci * w + (j - j0)] = offs[static_cast<size_t>(std::min(j, ndm - 1) - e0) * g.nchans + active[ci]];
+  r_offT_.resize(na * static_cast<size_t>(ldo_));
+  PSOUP_HIP_CHECK(hipMemcpy2D(r_offT_.data() + j0, static_cast<size_t>(ldo_) * 4, t.data(), static_cast<size_t>(w) * 4,
+                              static_cast<size_t>(w) * 4, na, hipMemcpyHostToDevice));
   // LDS kernel windows: per 32-DM tile and channel, the smallest offset
   // (rounded down to 16 bytes) and the window length it must stage
   const int ntiles = ldo_ / kTileDms;
-  const size_t na = std::max<size_t>(1, active.size());
-  std::vector<int32_t> wmin(static_cast<size_t>(ntiles) * na, 0);
+  std::vector<int32_t> wmin(static_cast<size_t>(t1 - t0) * na, 0);
   h_tile_win_.assign(static_cast<size_t>(ntiles), 0);
   // and the global-load MFMA plan's step count per tile (its 16-sample blocks
   // from each channel's smallest offset, two per step), which Auto weighs
   // against the VALU kernels without building that plan
   h_tile_steps_.assign(static_cast<size_t>(ntiles), 0);
-  for (int T = 0; T < ntiles; ++T) {
+  for (int T = t0; T < t1; ++T) {
     int64_t blocks = 0;
     for (size_t ci = 0; ci < active.size(); ++ci) {
-      int lo = t[ci * ldo_ + T * kTileDms], hi = lo;
+      const int32_t* col = &t[ci * w + (T * kTileDms - j0)];
+      int lo = col[0], hi = lo;
       for (int k = 1; k < kTileDms; ++k) {
-        lo = std::min(lo, t[ci * ldo_ + T * kTileDms + k]);
-        hi = std::max(hi, t[ci * ldo_ + T * kTileDms + k]);
+        lo = std::min(lo, col[k]);
+        hi = std::max(hi, col[k]);
       }
       const int w0 = lo & ~15;
-      wmin[static_cast<size_t>(T) * na + ci] = w0;
+      wmin[static_cast<size_t>(T - t0) * na + ci] = w0;
       h_tile_win_[static_cast<size_t>(T)] = std::max(h_tile_win_[static_cast<size_t>(T)], 1024 + (hi - w0) + 32);
       blocks += (hi - lo) / 16 + 1;
     }
     h_tile_steps_[static_cast<size_t>(T)] = static_cast<int32_t>((blocks + 1) / 2);
   }
-  r_wmin_.resize(wmin.size());
-  PSOUP_HIP_CHECK(hipMemcpy(r_wmin_.data(), wmin.data(), wmin.size() * 4, hipMemcpyHostToDevice));
-  valu_ready_ = true;
+  r_wmin_.resize(static_cast<size_t>(ntiles) * na);
+  PSOUP_HIP_CHECK(hipMemcpy(r_wmin_.data() + static_cast<size_t>(t0) * na, wmin.data(), wmin.size() * 4,
+                            hipMemcpyHostToDevice));
 }
 
 static double valu_ratio() {
@@ -282,7 +331,7 @@ static double valu_ratio() {
 double Dedisperser::mfma_steps_per_channel(int d0, int d1) {
   const auto& g = fb_.geometry();
   PSOUP_CHECK(d0 >= 0 && d0 < d1 && d1 <= static_cast<int>(g.dm_list.size()), "bad DM range");
-  if (!valu_ready_) build_valu_tables();
+  ensure_tables(d0, d1);
   double steps = 0;
   const int t0 = d0 / kTileDms, t1 = (d1 - 1) / kTileDms;
   for (int T = t0; T <= t1; ++T) steps += h_tile_steps_[static_cast<size_t>(T)];
@@ -294,7 +343,7 @@ DedispKernel Dedisperser::choose(int d0, int d1) {
   if (g.nactive == 0 || d0 >= d1) return DedispKernel::Mfma;
   // the LDS-staged packed-byte kernel (tile-aligned ranges, narrow samples)
   // beats the MFMA plan from ~1.0 steps per channel, the global-load one from 1.85
-  if (!valu_ready_) build_valu_tables();
+  ensure_tables(d0, d1);
   int win = 0;
   for (int T = d0 / kTileDms; T <= (d1 - 1) / kTileDms; ++T) win = std::max(win, h_tile_win_[static_cast<size_t>(T)]);
   const bool lds = kern::dedisperse_lds_fits(g.nbits, g.nactive, win);
@@ -302,20 +351,7 @@ DedispKernel Dedisperser::choose(int d0, int d1) {
   return mfma_steps_per_channel(d0, d1) > ratio ? DedispKernel::Valu : DedispKernel::Mfma;
 }
 
-void Dedisperser::build_mfma_lds_tables(const std::vector<int32_t>* offs_in, bool upload) {
-  const auto& g = fb_.geometry();
-  const int ndm = static_cast<int>(g.dm_list.size());
-  const std::vector<int32_t> offs_own = offs_in ? std::vector<int32_t>() : g.offsets(0, ndm);
-  const std::vector<int32_t>& offs = offs_in ? *offs_in : offs_own;
-  std::vector<int32_t> kill(g.killmask.begin(), g.killmask.end());
-  ml_plan_ = std::make_unique<kern::MfmaLdsPlan>();
-  kern::build_mfma_lds_plan(offs.data(), ndm, g.nchans, kill.data(), *ml_plan_);
-  if (upload) upload_mfma_lds_tables();
-}
-
-void Dedisperser::upload_mfma_lds_tables() {
-  PSOUP_CHECK(ml_plan_, "MFMA-LDS tables not built");
-  const kern::MfmaLdsPlan& plan = *ml_plan_;
+void Dedisperser::upload_mfma_lds_tables(const kern::MfmaLdsPlan& plan) {
   ml_ngroups_ = plan.ngroups;
   ml_tile_ok_ = plan.tile_ok;
   ml_tile_steps_ = plan.tile_steps;
@@ -328,8 +364,6 @@ void Dedisperser::upload_mfma_lds_tables() {
   up(ml_relo_, plan.relo);
   up(ml_ginfo_, plan.ginfo);
   up(ml_wmin_, plan.wmin);
-  ml_plan_.reset();
-  ml_ready_ = true;
 }
 
 static double mfma_lds_ratio() {
@@ -343,7 +377,7 @@ static double mfma_lds_ratio() {
 int Dedisperser::mfma_lds_split(int d0, int d1) {
   const auto& g = fb_.geometry();
   if (g.nactive == 0 || mfma_lds_ratio() <= 0) return d0;
-  if (!ml_ready_) build_mfma_lds_tables();
+  ensure_tables(d0, d1);
   int T = d0 / kTileDms;
   const int T1 = (d1 - 1) / kTileDms + 1;
   // the MFMA kernel computes whole 32-DM tiles, the VALU kernels only the
@@ -359,7 +393,7 @@ int Dedisperser::mfma_lds_split(int d0, int d1) {
 
 void Dedisperser::run_mfma_lds(int d0, int d1, uint8_t* out, uint64_t out_stride, hipStream_t s) {
   const auto& g = fb_.geometry();
-  if (!ml_ready_) build_mfma_lds_tables();
+  ensure_tables(d0, d1);
   // whole tiles from the one holding d0; its DMs before d0 are not stored
   const int T0 = d0 / kTileDms, skip = d0 - T0 * kTileDms, nt = (d1 - T0 * kTileDms + kTileDms - 1) / kTileDms;
   kern::dedisperse_mfma_lds(fb_.data(), fb_.stride(), d_active_.data(), g.nactive, ml_steps_.data(),
@@ -423,7 +457,7 @@ void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispK
   }
   if (kind == DedispKernel::Mfma && g.nactive > 0) {
     // explicit MFMA: the LDS-fed kernel where every tile fits its window
-    if (!ml_ready_) build_mfma_lds_tables();
+    ensure_tables(d0, d1);
     bool fit = true;
     for (int T = d0 / kTileDms; T <= (d1 - 1) / kTileDms; ++T) fit = fit && ml_tile_ok_[static_cast<size_t>(T)];
     if (fit) {
@@ -435,7 +469,7 @@ void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispK
   if (kind == DedispKernel::Valu && g.nactive == 0) kind = DedispKernel::Direct;
   const int ndm = d1 - d0;
   if (kind == DedispKernel::Valu) {
-    if (!valu_ready_) build_valu_tables();
+    ensure_tables(d0, d1);
     int win = 0;
     for (int T = d0 / kTileDms; T <= (d1 - 1) / kTileDms; ++T) win = std::max(win, h_tile_win_[static_cast<size_t>(T)]);
     if (kern::dedisperse_lds_fits(g.nbits, g.nactive, win))

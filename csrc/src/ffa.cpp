@@ -271,7 +271,7 @@ FfaResult run_ffa_pipeline(const FfaCmdLineOptions& args) {
       PSOUP_HIP_CHECK(hipSetDevice(dev));
       Stream stream;
       DeviceFilterbank dfb(geom, stream.get());
-      dfb.load_packed_host(fb.data());
+      load_filterbank_fanout({&dfb}, {dev}, fb);
       Dedisperser dd(dfb, stream.get());
       FfaEngine eng(fp, geom.out_nsamps, stream.get());
       const uint64_t rs = Dedisperser::row_stride(geom.out_nsamps);

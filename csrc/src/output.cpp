@@ -5,7 +5,9 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
+#include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <ctime>
@@ -18,11 +20,16 @@ namespace psoup {
 namespace xml {
 
 namespace {
-template <class T>
-std::string stream_fmt(const T& v) {
-  std::ostringstream os;
-  os << std::setprecision(15) << v;
-  return os.str();
+// the digits `ostream << setprecision(15) << v` gives (%.15g; integers as
+// they are), without a stream per value
+std::string num_fmt(const char* f, ...) __attribute__((format(printf, 1, 2)));
+std::string num_fmt(const char* f, ...) {
+  char buf[64];
+  va_list ap;
+  va_start(ap, f);
+  const int n = std::vsnprintf(buf, sizeof(buf), f, ap);
+  va_end(ap);
+  return std::string(buf, static_cast<size_t>(std::max(0, std::min(n, static_cast<int>(sizeof(buf)) - 1))));
 }
 
 std::string escape(const std::string& s) {
@@ -38,34 +45,46 @@ std::string escape(const std::string& s) {
 }
 }  // namespace
 
-std::string fmt(double v) { return stream_fmt(v); }
-std::string fmt(float v) { return stream_fmt(v); }
-std::string fmt(int v) { return stream_fmt(v); }
-std::string fmt(unsigned v) { return stream_fmt(v); }
-std::string fmt(long v) { return stream_fmt(v); }
-std::string fmt(long long v) { return stream_fmt(v); }
-std::string fmt(unsigned long v) { return stream_fmt(v); }
-std::string fmt(unsigned long long v) { return stream_fmt(v); }
+std::string fmt(double v) { return num_fmt("%.15g", v); }
+std::string fmt(float v) { return num_fmt("%.15g", static_cast<double>(v)); }
+std::string fmt(int v) { return num_fmt("%d", v); }
+std::string fmt(unsigned v) { return num_fmt("%u", v); }
+std::string fmt(long v) { return num_fmt("%ld", v); }
+std::string fmt(long long v) { return num_fmt("%lld", v); }
+std::string fmt(unsigned long v) { return num_fmt("%lu", v); }
+std::string fmt(unsigned long long v) { return num_fmt("%llu", v); }
 std::string fmt(bool v) { return v ? "1" : "0"; }
 std::string fmt(const std::string& v) { return escape(v); }
 std::string fmt(const char* v) { return escape(v ? std::string(v) : std::string()); }
 
-std::string Element::to_string(bool header, int level) const {
-  std::ostringstream xmls;
-  if (header) xmls << "<?xml version='1.0' encoding='ISO-8859-1'?>\n";
-  for (int i = 0; i < level; ++i) xmls << "  ";
-  xmls << "<" << name_;
-  for (const auto& kv : attributes_) xmls << " " << kv.first << "=" << kv.second;
-  xmls << ">";
-  if (children_.empty()) {
-    xmls << text_;
-  } else {
-    xmls << "\n";
-    for (const auto& c : children_) xmls << c.to_string(false, level + 1);
-    for (int i = 0; i < level; ++i) xmls << "  ";
+void Element::write(std::string& o, int level) const {
+  o.append(2 * static_cast<size_t>(level), ' ');
+  o += '<';
+  o += name_;
+  for (const auto& kv : attributes_) {
+    o += ' ';
+    o += kv.first;
+    o += '=';
+    o += kv.second;
   }
-  xmls << "</" << name_ << ">\n";
-  return xmls.str();
+  o += '>';
+  if (children_.empty()) {
+    o += text_;
+  } else {
+    o += '\n';
+    for (const auto& c : children_) c.write(o, level + 1);
+    o.append(2 * static_cast<size_t>(level), ' ');
+  }
+  o += "</";
+  o += name_;
+  o += ">\n";
+}
+
+std::string Element::to_string(bool header, int level) const {
+  std::string o;
+  if (header) o = "<?xml version='1.0' encoding='ISO-8859-1'?>\n";
+  write(o, level);
+  return o;
 }
 
 }  // namespace xml
@@ -194,6 +213,8 @@ void OverviewWriter::add_gpu_info(const std::vector<int>& device_ids) {
 
 void OverviewWriter::add_candidates(const CandidateList& cands, const std::map<unsigned, long>& byte_map) {
   xml::Element e("candidates");
+  std::vector<int> nassoc(cands.size());  // (tree walks, on several threads)
+  parallel_each(cands.size(), 8, [&](size_t i) { nassoc[i] = cands[i].count_assoc(); });
   for (size_t i = 0; i < cands.size(); ++i) {
     const Candidate& c = cands[i];
     xml::Element x("candidate");
@@ -209,7 +230,7 @@ void OverviewWriter::add_candidates(const CandidateList& cands, const std::map<u
     x.append(xml::Element("is_physical", c.is_physical));
     x.append(xml::Element("ddm_count_ratio", c.ddm_count_ratio));
     x.append(xml::Element("ddm_snr_ratio", c.ddm_snr_ratio));
-    x.append(xml::Element("nassoc", c.count_assoc()));
+    x.append(xml::Element("nassoc", nassoc[i]));
     auto it = byte_map.find(static_cast<unsigned>(i));
     x.append(xml::Element("byte_offset", it == byte_map.end() ? 0L : it->second));
     e.append(x);
@@ -264,25 +285,43 @@ bool CandidateFileWriter::write_binary(const CandidateList& cands, const std::st
     return false;
   }
   byte_mapping.clear();
-  std::vector<CandidatePOD> dets;
-  for (size_t i = 0; i < cands.size(); ++i) {
-    const Candidate& c = cands[i];
-    byte_mapping[static_cast<unsigned>(i)] = std::ftell(fo);
-    if (!c.fold.empty()) {
-      std::fwrite("FOLD", 1, 4, fo);
-      int32_t nb = c.nbins, ni = c.nints;
-      std::fwrite(&nb, sizeof(int32_t), 1, fo);
-      std::fwrite(&ni, sizeof(int32_t), 1, fo);
-      std::fwrite(c.fold.data(), sizeof(float), static_cast<size_t>(nb) * ni, fo);
+  // each candidate's record (fold, then its association tree flattened) built
+  // on several threads -- config 4's 1000 candidates carry ~1.2M associated
+  // ones (42 MB), whose tree walk cost more than the write -- then written in
+  // order
+  const size_t n = cands.size();
+  std::vector<std::string> rec(n);
+  parallel_each(n, 8, [&](size_t i) {
+    thread_local std::vector<CandidatePOD> dets;
+    {
+      const Candidate& c = cands[i];
+      dets.clear();
+      c.collect_candidates(dets);
+      const int32_t ndets = static_cast<int32_t>(dets.size());
+      const size_t nf = c.fold.empty() ? 0 : static_cast<size_t>(c.nbins) * c.nints;
+      std::string& r = rec[i];
+      r.reserve((nf ? 12 + 4 * nf : 0) + 4 + dets.size() * sizeof(CandidatePOD));
+      if (nf) {
+        const int32_t nb = c.nbins, ni = c.nints;
+        r.append("FOLD", 4);
+        r.append(reinterpret_cast<const char*>(&nb), 4);
+        r.append(reinterpret_cast<const char*>(&ni), 4);
+        r.append(reinterpret_cast<const char*>(c.fold.data()), 4 * nf);
+      }
+      r.append(reinterpret_cast<const char*>(&ndets), 4);
+      r.append(reinterpret_cast<const char*>(dets.data()), dets.size() * sizeof(CandidatePOD));
     }
-    dets.clear();
-    c.collect_candidates(dets);
-    int32_t ndets = static_cast<int32_t>(dets.size());
-    std::fwrite(&ndets, sizeof(int32_t), 1, fo);
-    std::fwrite(dets.data(), sizeof(CandidatePOD), dets.size(), fo);
+  });
+  long off = std::ftell(fo);
+  bool ok = true;
+  for (size_t i = 0; i < n; ++i) {
+    byte_mapping[static_cast<unsigned>(i)] = off;
+    ok = ok && std::fwrite(rec[i].data(), 1, rec[i].size(), fo) == rec[i].size();
+    off += static_cast<long>(rec[i].size());
   }
-  std::fclose(fo);
-  return true;
+  ok = (std::fclose(fo) == 0) && ok;
+  if (!ok) perror(path.c_str());
+  return ok;
 }
 
 namespace {

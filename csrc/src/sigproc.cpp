@@ -9,7 +9,10 @@
 #include <cstring>
 #include <fstream>
 #include <iostream>
+#include <mutex>
 #include <sstream>
+#include <thread>
+#include <vector>
 
 #include "psoup/common.hpp"
 
@@ -204,7 +207,44 @@ Filterbank Filterbank::from_file(const std::string& filename) {
   });
   fb.data_ = static_cast<const uint8_t*>(map) + fb.hdr_.size;
   fb.data_bytes_ = want;
+  fb.path_ = filename;
+  fb.data_offset_ = static_cast<uint64_t>(fb.hdr_.size);
   return fb;
+}
+
+void Filterbank::read_data(uint64_t off, uint64_t n, uint8_t* dst, int nthreads) const {
+  PSOUP_CHECK(off + n <= data_bytes_, "read_data: past the data block");
+  if (path_.empty()) {
+    std::memcpy(dst, data_ + off, n);
+    return;
+  }
+  // pread from the page cache: ~3x the rate of copying out of the fresh
+  // mapping (whose first touch faults every page in), more with threads
+  int fd = ::open(path_.c_str(), O_RDONLY);
+  if (fd < 0) PSOUP_THROW("cannot open " << path_);
+  std::exception_ptr err;
+  std::mutex mu;
+  auto part = [&](uint64_t a, uint64_t b) {
+    try {
+      while (a < b) {
+        const ssize_t r = ::pread(fd, dst + a, static_cast<size_t>(b - a), static_cast<off_t>(data_offset_ + off + a));
+        if (r <= 0) PSOUP_THROW("read failed on " << path_);
+        a += static_cast<uint64_t>(r);
+      }
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!err) err = std::current_exception();
+    }
+  };
+  const int nt = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(static_cast<uint64_t>(std::max(1, nthreads)),
+                                                                          n >> 21)));  // >= 2 MB each
+  const uint64_t step = (n + nt - 1) / nt;
+  std::vector<std::thread> th;
+  for (int i = 1; i < nt; ++i) th.emplace_back(part, std::min(n, i * step), std::min(n, (i + 1) * step));
+  part(0, std::min(n, step));
+  for (auto& t : th) t.join();
+  ::close(fd);
+  if (err) std::rethrow_exception(err);
 }
 
 Filterbank Filterbank::from_memory(const SigprocHeader& hdr, std::vector<uint8_t> data) {

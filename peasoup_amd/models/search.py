@@ -94,10 +94,12 @@ class RankSearcher:
     """Per-rank search state: resident filterbank, dedisperser, engine."""
 
     def __init__(self, args, header: dict, packed: Optional[torch.Tensor], nsamps: int,
-                 killmask: Optional[Sequence[int]] = None, fft_mode: Optional[int] = None, resident: bool = True):
+                 killmask: Optional[Sequence[int]] = None, fft_mode: Optional[int] = None, resident: bool = True,
+                 warm: bool = True):
         """``resident=False``: no device filterbank / dedisperser (the
         time-sharded path hands DM trials over already dedispersed:
-        :meth:`search_rows`, ``fold(..., rows=...)``)."""
+        :meth:`search_rows`, ``fold(..., rows=...)``).  ``warm=False``: the
+        dedispersion plan tables wait for :meth:`warm` (a static shard's own)."""
         self.ctx = pdist.context()
         self.args = args
         self.header = dict(header)
@@ -125,7 +127,8 @@ class RankSearcher:
             if packed is not None:
                 self.load_packed(packed)
             self.dedisperser = _C.Dedisperser(self.dfb, self.stream)
-            self.dedisperser.warm()  # plan tables at setup, not at the first tile that needs them
+            if warm:
+                self.warm()
         self.kernel = {"auto": _C.DedispKernel.Auto, "mfma": _C.DedispKernel.Mfma, "valu": _C.DedispKernel.Valu,
                        "direct": _C.DedispKernel.Direct}[args.dedisp_kernel]
         self.row_stride = _C.Dedisperser.row_stride(self.geom.out_nsamps)
@@ -153,6 +156,12 @@ class RankSearcher:
             self.dfb.load_packed_device(packed.data_ptr())
         else:
             self.dfb.load_packed_host(packed.data_ptr())
+
+    def warm(self, d0: int = 0, d1: int = -1) -> None:
+        """Dedispersion plan tables for DMs [d0, d1) (default: the whole
+        list) at setup, not at the first tile that needs them."""
+        if self.dedisperser is not None:
+            self.dedisperser.warm(d0, d1)
 
     def accel_list(self, dm: float) -> List[float]:
         return self.accel_plan.generate(float(dm))
@@ -607,10 +616,11 @@ def load_packed_for_rank(infilename: str, ctx: pdist.DistContext, timers=None):
     if ctx.device.type == "cuda":
         packed = torch.empty(nbytes, dtype=torch.uint8, device=ctx.device)
         if ctx.is_root:
-            with warnings.catch_warnings():  # read-only mmap view, only copied to the device
-                warnings.simplefilter("ignore", UserWarning)
-                host = torch.from_numpy(fb.data())[:nbytes]
-            packed.copy_(host, non_blocking=False)
+            # threaded pread into pinned stages, copies overlapping the reads
+            # (a copy out of the fresh mapping faults every page in: ~0.15 s
+            # for config 4's 268 MB, ~10 ms this way)
+            torch.cuda.synchronize(ctx.device)
+            fb.upload(packed.data_ptr(), nbytes, torch.cuda.current_stream(ctx.device).cuda_stream)
         if ctx.distributed:
             pdist.broadcast_bytes(packed, nbytes)
     else:
@@ -672,10 +682,17 @@ def fold_owners(rs: RankSearcher, ctx) -> Dict[int, int]:
     return owner
 
 
-def run_search(args, write: bool = True) -> Optional[SearchResult]:
+def run_search(args, write: bool = True, as_rank: Optional[tuple] = None) -> Optional[SearchResult]:
     """Full distributed search (torchrun: one rank per GPU).  Returns the
-    result on rank 0 (None elsewhere)."""
+    result on rank 0 (None elsewhere).
+
+    ``as_rank=(W, r)`` (one process): rank r's whole share of a W-rank run --
+    setup for its static DM shard, its search, a merge of its own list -- so
+    one GPU can time every rank of a larger job (tools/baseline_configs.py
+    --as-rank)."""
     ctx = pdist.init()
+    if as_rank is not None:
+        assert ctx.world_size == 1 and 0 <= as_rank[1] < as_rank[0], as_rank
     timers = {k: Stopwatch() for k in ("reading", "dedispersion", "searching", "folding", "total")}
     timers["total"].start()
     # device start-up (context, allocator, kernel code objects) in "total"
@@ -695,15 +712,23 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     else:
         header, packed, nsamps = load_packed_for_rank(args.infilename, ctx, timers)
 
-    rs = RankSearcher(args, header, packed, nsamps, resident=not sharded)
+    rs = RankSearcher(args, header, packed, nsamps, resident=not sharded, warm=False)
     del packed
     ndm = len(rs.dm_list)
     weights = [len(rs.accel_list(d)) for d in rs.dm_list]
-    schedule = "time_sharded" if sharded else dm_schedule(args, ctx.world_size, ndm)
+    world = ctx.world_size if as_rank is None else as_rank[0]
+    schedule = "time_sharded" if sharded else "static" if as_rank else dm_schedule(args, world, ndm)
+    if schedule == "static":
+        # a static shard's plan tables only (dynamic ranks may claim any chunk)
+        shard = pdist.shard_range(ndm, world, ctx.rank if as_rank is None else as_rank[1], weights)
+        if len(shard):
+            rs.warm(shard.start, shard.stop)
+    elif not sharded:
+        rs.warm()
     rows = None
     row_first = 0
     if not sharded and args.npdmp > 0:
-        rs.keep_trials = keep_trials_fits(rs, ndm, ctx.world_size)
+        rs.keep_trials = keep_trials_fits(rs, ndm, world)
     if args.npdmp > 0 and _C.prev_power_of_two(rs.geom.out_nsamps) >= 1024:
         rs.fold_engine(njobs_hint=args.npdmp)  # folder buffers allocated with the rest of the setup
     pdist.barrier()
@@ -745,7 +770,6 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
         local = rs.search(blocks=blocks, claim=queue.claim, timers=timers)
         local_trials = sum(weights[d] for j in rs.blocks_done for d in range(*blocks[j]))
     else:
-        shard = pdist.shard_range(ndm, ctx.world_size, ctx.rank, weights)
         local = rs.search(shard, timers=timers)
         local_trials = sum(weights[i] for i in shard)
     torch.cuda.synchronize()
@@ -760,7 +784,7 @@ def run_search(args, write: bool = True) -> Optional[SearchResult]:
     all_stats = pdist.gather_bytes(json.dumps(rank_stats).encode(), dst=0)
 
     # ---- candidate gather (RCCL) + global distillation on rank 0
-    total_trials = sum(weights)
+    total_trials = sum(weights) if as_rank is None else local_trials
     if not ctx.distributed:
         # a world of one: the merge takes the rank's own list (no serialisation)
         cands = _C.merge_local(local, args, rs.header)

@@ -21,6 +21,19 @@ def test_tutorial_header_native_and_python(C):
     assert fb.cfreq() == pytest.approx(1475.12, abs=1e-3)
 
 
+def test_filterbank_threaded_pread_equals_mapping(C):
+    """The device upload's staging reads (pread on threads) return the mapped
+    data block byte for byte, at any offset and thread count."""
+    fb = C.Filterbank.from_file(TUTORIAL)
+    ref_ = np.array(fb.data())
+    for off, n, nt in ((0, fb.data_bytes, 4), (0, fb.data_bytes, 1), (12345, 2_100_001, 3), (fb.data_bytes - 7, 7, 4)):
+        out = np.zeros(n, dtype=np.uint8)
+        fb.read_into(off, n, out.ctypes.data, nt)
+        assert np.array_equal(out, ref_[off:off + n]), (off, n, nt)
+    with pytest.raises(Exception):
+        fb.read_into(fb.data_bytes - 2, 4, np.zeros(4, np.uint8).ctypes.data)
+
+
 def test_filterbank_roundtrip(C, tmp_path):
     rng = np.random.default_rng(0)
     for nbits in (1, 2, 4, 8):

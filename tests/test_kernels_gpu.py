@@ -126,6 +126,16 @@ def test_dedisperse_1024ch_hybrid_mfma_bit_exact(C):
     o = torch.zeros(len(lst) * stride, dtype=torch.uint8, device=dev)
     dd.run_list(lst, o.data_ptr(), stride)
     assert torch.equal(o.view(len(lst), stride)[:, : g.out_nsamps], ref_[lst])
+    # a static shard's own tables (warm(d0, d1)): its ranges are exact, and a
+    # range outside them rebuilds the whole list's and is exact too
+    for d0, d1, out_of in ((70, 150, (0, 40)), (200, ndm, (5, 70)), (13, 40, (250, ndm))):
+        sh = C.Dedisperser(dfb, s)
+        sh.warm(d0, d1)
+        for a, b in ((d0, d1), (d0 + 3, d1 - 1), out_of):
+            for k in (C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto):
+                o = torch.zeros((b - a) * stride, dtype=torch.uint8, device=dev)
+                sh.run(a, b, o.data_ptr(), stride, k)
+                assert torch.equal(o.view(b - a, stride)[:, : g.out_nsamps], ref_[a:b]), (d0, d1, a, b, k)
 
 
 def test_mfma_resident_plan_ranges_and_side_stream(C):

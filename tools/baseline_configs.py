@@ -17,6 +17,7 @@ series length (2 GB filterbank).
 
     python tools/baseline_configs.py --configs 1,2,3,4,5 [--ndm 2000] [--log2n 20]
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/baseline_configs.py --configs 4,5
+    python tools/baseline_configs.py --configs 4 --as-rank 8:0,3,7   # ranks of an 8-GPU run, one at a time
 """
 from __future__ import annotations
 
@@ -178,12 +179,12 @@ def _dm_end_for(ndm):
     return dm_end
 
 
-def config45(a, npdmp, cfg):
+def config45(a, npdmp, cfg, as_rank=None):
     from peasoup_amd.models.search import run_search
 
     ctx = pdist.init()
     path = _make_fb(a, ctx)
-    out = os.path.join(a.workdir, f"out_cfg{cfg}")
+    out = os.path.join(a.workdir, f"out_cfg{cfg}" + (f"_as{as_rank[0]}_{as_rank[1]}" if as_rank else ""))
     argv = ["peasoup", "-i", path, "-o", out, "--dm_end", f"{_dm_end_for(a.ndm):.3f}", "--acc_start", "-500",
             "--acc_end", "500", "-n", "3", "--npdmp", str(npdmp), "--limit", "1000"]
     ok, _, args = _C.parse_cmdline(argv)
@@ -203,9 +204,18 @@ def config45(a, npdmp, cfg):
                 "wall_s": round(wall, 3), "timers_s": {k: round(v, 3) for k, v in tr.get("timers_s", {}).items()},
                 "performance": tr.get("performance", {})}
     t0 = time.perf_counter()
-    res = run_search(args)
+    res = run_search(args, as_rank=as_rank)
     wall = time.perf_counter() - t0
     rec = None
+    if as_rank is not None:
+        st = res.rank_stats[0] if res.rank_stats else {}
+        return {"config": cfg, "as_rank": as_rank[1], "world": as_rank[0], "log2n": a.log2n,
+                "desc": f"rank {as_rank[1]} of a {as_rank[0]}-rank config-{cfg} run (static DM shard), on one GPU",
+                "dm_trials": st.get("dm_trials"), "accel_trials": res.accel_trials, "wall_s": round(wall, 3),
+                "timers_s": {k: round(v, 3) for k, v in res.timers.items()},
+                "total_minus_search_s": round(res.timers["total"] - st.get("search_s", 0.0), 3),
+                "search_s": round(st.get("search_s", 0.0), 3), "device_init_s": round(st.get("device_init_s", 0.0), 4),
+                "candidates": len(res.candidates)}
     if ctx.is_root:
         best = res.candidates[0] if res.candidates else None
         rec = {"config": cfg,
@@ -244,6 +254,9 @@ def main():
                     help="configs 4/5 data: the 64-pulsar sky (default) or one pulsar in noise (the round-2 data)")
     ap.add_argument("--out", default="")
     ap.add_argument("--native", action="store_true", help="configs 4/5 through bin/peasoup instead of Python")
+    ap.add_argument("--as-rank", default="", metavar="W:r[,r...]",
+                    help="configs 4/5: time ranks r of a W-rank run one after another on this GPU (setup included; "
+                         "an untimed run of the first rank warms the process)")
     a = ap.parse_args()
     os.makedirs(a.workdir, exist_ok=True)
     ctx = pdist.init()
@@ -251,6 +264,14 @@ def main():
         if c in (1, 2, 3):
             if ctx.is_root:
                 emit({1: config1, 2: config2, 3: config3}[c](a), a.out)
+        elif c in (4, 5) and a.as_rank:
+            w, _, rs_ = a.as_rank.partition(":")
+            ranks = [int(x) for x in rs_.split(",") if x != ""]
+            assert ctx.world_size == 1 and ranks, a.as_rank
+            first = config45(a, 0 if c == 4 else 128, c, (int(w), ranks[0]))
+            emit(dict(first, warmup=True), a.out)
+            for r in ranks:
+                emit(config45(a, 0 if c == 4 else 128, c, (int(w), r)), a.out)
         elif c in (4, 5):
             rec = config45(a, 0 if c == 4 else 128, c)
             if rec is not None:

@@ -24,3 +24,17 @@ for rep in range(3):
     out = _C.merge_candidate_blobs(blobs, args, hdr)
     print(json.dumps({"candidates_in": n_in, "out": len(out), "blob_mb": round(sum(map(len, blobs)) / 1e6, 2),
                       "merge_s": round(time.perf_counter() - t, 4)}))
+
+# the writers on the merged list (candidates.peasoup; overview.xml's candidate section)
+import tempfile  # noqa: E402
+
+out.truncate(max(0, args.limit))
+with tempfile.TemporaryDirectory() as td:
+    for rep in range(2):
+        t = time.perf_counter()
+        bm = _C.write_candidates_binary(td, out, "candidates.peasoup")
+        t1 = time.perf_counter()
+        _C.write_overview(os.path.join(td, "overview.xml"), args, hdr, [0.0], [0.0], [], out, bm, {}, {})
+        t2 = time.perf_counter()
+        print(json.dumps({"write_binary_s": round(t1 - t, 4), "overview_s": round(t2 - t1, 4),
+                          "bytes": os.path.getsize(os.path.join(td, "candidates.peasoup"))}))
