@@ -70,8 +70,8 @@ def parse():
                    help="peak-heavy data instead of pure noise: injected pulsars plus strong undispersed periodic "
                         "RFI (>= 1e4 threshold crossings per DM), to time the host clustering / distillation")
     p.add_argument("--serial-merge", action="store_true",
-                   help="run each step's candidate gather + global distillation before the next step starts "
-                        "(default: overlapped with the next step, as the pipeline's DM blocks are)")
+                   help="run each step's candidate gather + global distillation before the next step's "
+                        "candidates are collected (default: on a worker thread, overlapped)")
     p.add_argument("--as-rank", default="",
                    help="N:r[,r...] -- on one GPU, time rank r's shard of a world-N run (the DM list of N ranks, "
                         "shard [r*dms, (r+1)*dms)), one JSON line per r: checks that every rank's step costs the same")
@@ -198,24 +198,40 @@ def main() -> int:
         phase["gds"] += t4 - t3
         return out
 
-    def step():
+    # a step: the shard's DM blocks dedispersed + searched, its candidates
+    # merged.  Steps run back to back through the search pipeline, as a
+    # rank's DM chunks do in a run: step k+1's dedispersion and searches are
+    # in flight while step k's candidates are collected and handed to the
+    # merge (no idle GPU between steps).  Every step of a run_steps() call is
+    # issued and finished inside it.
+    tile = int(_C.Dedisperser.tile_dms)
+    step_blocks = rs.chunk_ranges(shard, max(tile, (a.dms_per_gpu + tile - 1) // tile * tile))
+
+    def run_steps(nsteps):
+        out, acc, got = [], _C.CandidateBag(), 0
         t = time.perf_counter()
-        local = rs.search(shard, chunk=a.dms_per_gpu)
-        phase["search"] += time.perf_counter() - t
-        return merger.submit(merge, local) if merger else merge(local)
+        for _, bag in rs.search_iter(blocks=step_blocks * nsteps):
+            acc.extend(bag)
+            got += 1
+            if got % len(step_blocks) == 0:
+                phase["search"] += time.perf_counter() - t
+                out.append(merger.submit(merge, acc) if merger else merge(acc))
+                acc = _C.CandidateBag()
+                t = time.perf_counter()
+        return out
 
     def finish(r):
         return r.result() if merger else r
 
-    for _ in range(a.warmup):
-        finish(step())
+    for r in run_steps(a.warmup):
+        finish(r)
     for e in rs.engines:
         e.reset_counters()
     phase.update(search=0.0, merge=0.0, ser=0.0, gather=0.0, gds=0.0)
     pdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    pending = [step() for _ in range(a.steps)]
+    pending = run_steps(a.steps)
     ncands = len(finish(pending[-1]))
     for r in pending:
         finish(r)
@@ -268,6 +284,7 @@ def main() -> int:
                 "search_s_per_step": round(phase["search"] / a.steps, 4),
                 "merge_s_per_step": round(phase["merge"] / a.steps, 4),
                 "merge_overlapped": not a.serial_merge,
+                "steps_pipelined": True,
                 "merge_split_s": {k: round(phase[k] / a.steps, 4) for k in ("ser", "gather", "gds")},
                 "candidate_blob_bytes": phase.get("blob_bytes", 0),
                 "accel_s_per_step": round(ctr.get("accel_s", 0) / a.steps, 4),

@@ -195,7 +195,21 @@ class RankSearcher:
     def search(self, dm_indices: Optional[Sequence[int]] = None, chunk: int = 32,
                timers: Optional[Dict[str, Stopwatch]] = None, progress=None,
                blocks: Optional[List[tuple]] = None, claim: Optional[Callable[[], Optional[int]]] = None) -> list:
-        """Dedisperse + search DM blocks.  Chunk k+1 is dedispersed on a side
+        """Dedisperse + search DM blocks (every block's candidates, in
+        processing order, as one CandidateBag): :meth:`search_iter` drained."""
+        cands = _C.CandidateBag()
+        for _, got in self.search_iter(dm_indices, chunk, timers, progress, blocks, claim):
+            cands.extend(got)
+        return cands
+
+    def search_iter(self, dm_indices: Optional[Sequence[int]] = None, chunk: int = 32,
+                    timers: Optional[Dict[str, Stopwatch]] = None, progress=None,
+                    blocks: Optional[List[tuple]] = None, claim: Optional[Callable[[], Optional[int]]] = None):
+        """Dedisperse + search DM blocks, yielding ``(block index, candidates)``
+        as each block is finalized -- while the next block's dedispersion and
+        searches are already in flight, so a consumer that merges or writes a
+        block's candidates keeps the GPU busy (bench.py's steps: one block
+        each, back to back, as a rank's DM chunks in a run).  Chunk k+1 is dedispersed on a side
         stream into the other half of a double buffer while chunk k is
         searched (the reference dedisperses the whole DM list up front,
         pipeline.cu:325-359); the search stream waits on an event, never the
@@ -222,7 +236,6 @@ class RankSearcher:
         # the candidates stay native (CandidateBag): no per-candidate Python
         # objects, no deep copies of association trees between the engine,
         # the spills and the merge
-        cands = _C.CandidateBag()
         t_dd = timers.get("dedispersion") if timers else None
         t_s = timers.get("searching") if timers else None
         ntrials = 0
@@ -310,10 +323,10 @@ class RankSearcher:
         # the engines' host workers when its batches have retired: it is
         # collected after the next block's searches are issued, so that host
         # tail overlaps GPU work (SearchEngine.search_prepared_many_async).
-        prev = None  # (ck, d0, d1, [(engine, jobs, handle)])
+        prev = None  # (j, ck, d0, d1, [(engine, jobs, handle)])
 
         def finalize(blk):
-            ck_, b0, b1, pend = blk
+            _, ck_, b0, b1, pend = blk
             per_dm: Dict[int, object] = {}
             for e_, jobs_, h_ in pend:
                 for (b, dm, d, accs), c in zip(jobs_, _C.collect_bags(e_, h_)):
@@ -323,7 +336,7 @@ class RankSearcher:
                 chunk_cands.extend(per_dm[d])
             if ck_:
                 _C.save_spill(ck_, ckey, chunk_cands)  # atomic; raises on a failed write
-            cands.extend(chunk_cands)
+            return chunk_cands
 
         while cur is not None:
             j, ck, resumed, inflight = cur
@@ -331,10 +344,12 @@ class RankSearcher:
             self.blocks_done.append(j)
             if resumed is not None:
                 if prev is not None:  # keep the block order of the candidate list
-                    finalize(prev)
+                    done = finalize(prev)
+                    pj = prev[0]
                     prev = None
+                    yield pj, done
                 # resume: same spill format as the native pipeline (keyed CandidatePOD trees)
-                cands.extend(resumed)
+                yield j, resumed
                 ntrials += sum(len(self.accel_list(self.dm_list[d])) for d in range(d0, d1))
                 if progress is not None:
                     progress(d1 - d0)
@@ -411,16 +426,18 @@ class RankSearcher:
                 ev.record(e.stream)
                 evs.append(ev)
             freed[k] = evs  # the double buffer's slot k is free once these retire
-            if prev is not None:
-                finalize(prev)
-            prev = (ck, d0, d1, pend)
+            done = finalize(prev) if prev is not None else None
+            pj = prev[0] if prev is not None else -1
+            prev = (j, ck, d0, d1, pend)
             if _BLOCK_TRACE:
                 with open(_BLOCK_TRACE, "a") as f:
                     f.write(json.dumps({"block": j, "t0": tb0, "pull_s": tb1 - tb0, "search_s": tb2 - tb1,
                                         "engines": eng_t, "tail_s": time.perf_counter() - tb2}) + "\n")
             cur = nxt
+            if done is not None:
+                yield pj, done  # (this block's searches and the next block's dedispersion are in flight)
         if prev is not None:
-            finalize(prev)
+            yield prev[0], finalize(prev)
         side.synchronize()
         for e in self.engines:
             _C.stream_synchronize(e.stream)
@@ -429,7 +446,6 @@ class RankSearcher:
         if t_dd and dd_events:
             t_dd.add(sum(a.elapsed_ms(b) for a, b in dd_events) * 1e-3)
         self.accel_trials = ntrials
-        return cands
 
     def search_rows(self, rows: torch.Tensor, dm_first: int, timers: Optional[Dict[str, Stopwatch]] = None) -> list:
         """Search DM trials already resident on the GPU: ``rows`` is uint8

@@ -335,6 +335,36 @@ def test_headline_shape_binary_pulsar_and_fft_modes(C):
         assert b.snr == pytest.approx(a.snr, rel=1e-4)
 
 
+def test_search_iter_blocks_back_to_back_equal_search(C):
+    """search_iter (the bench's back-to-back steps: the next block's
+    dedispersion and searches in flight while a block is collected) yields
+    each block's candidates as search() gives them, also for a block that
+    repeats (the same DM chunk searched again through the other buffer)."""
+    from peasoup_amd.models.search import RankSearcher
+    from peasoup_amd.utils import synthetic
+
+    nchans, tsamp, fch1, foff = 128, 64e-6, 1550.0, -400.0 / 128
+    psr = synthetic.PulsarSpec(period=0.0113, dm=30.0, duty=0.05, amplitude=0.08, accel=40.0)
+    n = 1 << 18
+    dms = C.generate_dm_list(0.0, 60.0, tsamp, 64.0, fch1, foff, nchans, 1.1)
+    nsamps = n + C.compute_max_delay(dms, C.generate_delay_table(nchans, tsamp, fch1, foff)) + 4096
+    hdr = synthetic.make_header(nchans=nchans, nbits=2, tsamp=tsamp, fch1=fch1, foff=foff, nsamples=nsamps)
+    packed = synthetic.generate_packed_torch(nsamps, hdr, [psr], seed=5, device="cuda")
+    ok, _, args = C.parse_cmdline(["peasoup", "-i", "synthetic", "--dm_end", "60", "--acc_start", "-50",
+                                   "--acc_end", "50", "-n", "3", "--fft_size", str(n)])
+    assert ok
+    rs = RankSearcher(args, hdr, packed, nsamps)
+    ndm = len(rs.dm_list)
+    assert ndm > 40
+    blocks = [(0, 32), (32, ndm), (0, 32), (8, 16)]
+    ref_ = {b: [(c.freq, c.dm_idx, c.acc, c.nh, c.snr) for c in rs.search(blocks=[b])] for b in set(blocks)}
+    got = list(rs.search_iter(blocks=blocks))
+    assert [j for j, _ in got] == list(range(len(blocks)))
+    for j, bag in got:
+        assert [(c.freq, c.dm_idx, c.acc, c.nh, c.snr) for c in bag] == ref_[blocks[j]], blocks[j]
+    assert any(len(v) for v in ref_.values())
+
+
 def test_peak_heavy_candidates_equal_across_clustering_paths(tmp_path):
     """RFI-heavy data (undispersed 50 Hz / 16.7 Hz pulse trains, hundreds of
     harmonics above threshold in every acceleration trial) through the native
