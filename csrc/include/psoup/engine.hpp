@@ -30,7 +30,10 @@
 
 namespace psoup {
 
-enum class DedispKernel { Auto = 0, Direct = 1, Mfma = 2, Valu = 3 };
+// Valu: the byte kernels (LDS-staged or global); Packed2: the 2-bit kernel
+// (nbits <= 2 only); Auto: LDS-fed MFMA on the narrow-spread leading tiles,
+// then Packed2 where the data allows, else Valu.
+enum class DedispKernel { Auto = 0, Direct = 1, Mfma = 2, Valu = 3, Packed2 = 4 };
 DedispKernel parse_dedisp_kernel(const std::string& s);
 
 // Geometry shared by every rank: DM list, delays, killmask, output length.
@@ -67,13 +70,19 @@ class DeviceFilterbank {
   hipStream_t stream() const { return stream_; }
   const int8_t* data() const { return chan_.data(); }
   uint64_t stride() const { return stride_; }
+  // narrow data (nbits <= 2): the rows again as 2-bit fields, 16 samples per
+  // dword (kern::pack2_rows), zero-padded past the int8 rows; else nullptr
+  const uint32_t* data2() const { return chan2_.size() ? chan2_.data() : nullptr; }
+  uint64_t stride2() const { return stride2_; }
   const DedispGeometry& geometry() const { return g_; }
 
  private:
+  void pack2(uint64_t t0, uint64_t ns, hipStream_t s);
   DedispGeometry g_;
   hipStream_t stream_;
-  uint64_t stride_;
+  uint64_t stride_, stride2_ = 0;
   DeviceBuffer<int8_t> chan_;
+  DeviceBuffer<uint32_t> chan2_;
 };
 
 // One host upload, then a device-to-device fan-out (SURVEY.md §2.7, §5.8
@@ -140,6 +149,7 @@ class Dedisperser {
   void build_tables(int t0, int t1);  // tiles [t0, t1)
   // offs: rows of DMs [e0, ...) covering tiles [t0, t1 + 1)
   void build_valu_tables(const std::vector<int32_t>& offs, int e0, int t0, int t1);
+  int max_spread(int d0, int d1) const;  // largest (offset - window start) over [d0, d1)'s tiles
   void upload_mfma_lds_tables(const kern::MfmaLdsPlan& plan);
   void run_mfma_lds(int d0, int d1, uint8_t* out, uint64_t out_stride, hipStream_t s);
   const DeviceFilterbank& fb_;

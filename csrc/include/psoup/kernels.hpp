@@ -126,6 +126,22 @@ void dedisperse_valu(const int8_t* chan_major, uint64_t chan_stride, const int32
 // rounded down to 16 and max_window = the largest (tile, channel) window
 // 1024 + (max offset - wmin) + 32 bytes.
 bool dedisperse_lds_fits(int nbits, int nactive, int max_window);
+// Packed 2-bit rows for dedisperse_2bit: dword j of row r = samples 16 j ..
+// 16 j + 15 of chan_major row r (values 0..3) at bits 2 (t & 15), for the
+// samples [t0, t0 + ns) (t0 a multiple of 16).
+void pack2_rows(const int8_t* chan_major, uint64_t chan_stride, int nrows, uint32_t* out, uint64_t stride2, uint64_t t0,
+                uint64_t ns, hipStream_t s);
+// Dedispersion of narrow data (nbits <= 2) from the packed 2-bit rows (VALU
+// nibble-lane sums, dedisperse.hip): bit-identical to dedisperse_direct.
+// max_spread: the largest (largest offset - window start) of the launch's
+// 32-DM tiles, in samples (window start: wmin, 16-sample aligned); max_offset:
+// the largest window start (rows are read to sample tiles * 2048 + max_offset
+// + the window).
+int dedisperse_2bit_window(int max_spread);  // staged dwords per channel
+bool dedisperse_2bit_fits(int nactive, int max_spread);
+void dedisperse_2bit(const uint32_t* x2, uint64_t stride2, const int32_t* d_active, int nactive, const int32_t* d_offT,
+                     int ldo, int d0, int ndm, const int32_t* d_wmin, int max_spread, int max_offset,
+                     uint64_t out_nsamps, uint8_t* out, uint64_t out_stride, float scale, hipStream_t s);
 void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_t* d_active, int nactive,
                     const int32_t* d_offT, int ldo, int d_base, int ndm, const int32_t* d_wmin, int max_window,
                     uint64_t out_nsamps, uint8_t* out, uint64_t out_stride, float scale, int nbits, int bias,
@@ -353,6 +369,8 @@ enum Fft4Flags : int {
   kFft4UniformTw = 65536,  // pass A: four-step twiddles as per-thread x workgroup-uniform (SGPR) factors
   kFft4OneX = 131072,      // pass A (tiled Y, column length 2048): 2 columns x 32 points per thread,
                            // one LDS exchange, compile-time twiddles inside the two local DFTs
+  kFft4PairY = 262144,     // the Stockham pass A (column lengths other than the one-exchange one) also
+                           // hands the fused spectrum pass row-pair Y (Y_p[k2/2][i][k2%2])
   kFft4StripInput = 1073741824,  // one-exchange pass A: the padded input in column strips (16 + 4 floats of
                                  // every row per strip, strips row-contiguous), so a wave's 16 rows are
                                  // one ~1.3 KiB contiguous range instead of 16 pieces 16 KiB apart

@@ -625,6 +625,173 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) d
   }
 }
 
+
+// ------------------------------------------------ packed 2-bit, VALU SWAR --
+// Narrow data (nbits <= 2: values 0..3) kept a second time as 2-bit fields,
+// 16 samples per dword (sample t of row c at bit 2 (t & 15) of dword t / 16):
+// a lane's 32 samples of one DM and channel are two dwords at a wave-uniform
+// bit shift (v_alignbit of three LDS dwords: 0.375 LDS bytes per sample
+// instead of the byte kernel's 2), added as nibble lanes (even / odd fields
+// masked apart: 4 adds per 32 samples), spilled to byte lanes every 4
+// channels (4 x 3 <= 15) and to 16-bit lanes every 64 (16 x 12 <= 255).
+// Workgroup: 4 waves x DPW DMs x 2048 samples; per channel the workgroup's
+// window (from the 32-DM tile's smallest offset, 64-sample aligned) is staged
+// in LDS, 8 channels per buffer, double-buffered.
+constexpr int k2bTs = 2048;    // samples per workgroup (64 lanes x 32)
+constexpr int k2bCpb = 8;      // channels per LDS buffer (32 threads each)
+constexpr int k2bWinDw = 384;  // largest staged window per channel (dwords = 16 samples)
+
+__global__ void __launch_bounds__(256) pack2_kernel(const int8_t* __restrict__ x, uint64_t stride,
+                                                    uint32_t* __restrict__ out, uint64_t stride2, uint64_t dw0,
+                                                    uint64_t ndw) {
+  const int8_t* row = x + static_cast<uint64_t>(blockIdx.y) * stride;
+  uint32_t* orow = out + static_cast<uint64_t>(blockIdx.y) * stride2;
+  for (uint64_t j = dw0 + static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x; j < dw0 + ndw;
+       j += static_cast<uint64_t>(gridDim.x) * 256) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(row + 16 * j);
+    uint32_t w = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t b = v[i];  // four samples, one per byte, each 0..3
+      const uint32_t p = (b & 3u) | ((b >> 6) & 0xCu) | ((b >> 12) & 0x30u) | ((b >> 18) & 0xC0u);
+      w |= p << (8 * i);
+    }
+    orow[j] = w;
+  }
+}
+
+template <int DPW>
+__global__ void __launch_bounds__(256) dedisperse_2bit_kernel(
+    const uint32_t* __restrict__ x2, uint64_t stride2, const int32_t* __restrict__ active, int nactive,
+    const int32_t* __restrict__ offT, int ldo, int d_base, int d_skip, int ndm, const int32_t* __restrict__ wmin,
+    int wvec, uint64_t out_nsamps, uint8_t* __restrict__ out, uint64_t out_stride, float scale) {
+  __shared__ __attribute__((aligned(16))) uint32_t win[2][k2bCpb * k2bWinDw];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int dm0 = static_cast<int>(blockIdx.x) * (4 * DPW) + wave * DPW;  // relative to d_base
+  const int tile = (d_base + static_cast<int>(blockIdx.x) * 4 * DPW) / 32;  // 4 DPW divides 32
+  const uint64_t tb = static_cast<uint64_t>(blockIdx.y) * k2bTs;
+  const int32_t* wm = wmin + static_cast<uint64_t>(tile) * nactive;
+  uint32_t a4[DPW][4], a8[DPW][8], a16[DPW][16];
+#pragma unroll
+  for (int j = 0; j < DPW; ++j) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) a4[j][m] = 0;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) a8[j][m] = 0;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) a16[j][m] = 0;
+  }
+  auto flush4 = [&]() {
+#pragma unroll
+    for (int j = 0; j < DPW; ++j)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        a8[j][2 * m] += a4[j][m] & 0x0F0F0F0Fu;
+        a8[j][2 * m + 1] += (a4[j][m] >> 4) & 0x0F0F0F0Fu;
+        a4[j][m] = 0;
+      }
+  };
+  auto flush8 = [&]() {
+#pragma unroll
+    for (int j = 0; j < DPW; ++j)
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        a16[j][2 * m] += a8[j][m] & 0x00FF00FFu;
+        a16[j][2 * m + 1] += (a8[j][m] >> 8) & 0x00FF00FFu;
+        a8[j][m] = 0;
+      }
+  };
+  // staging: thread (q = t / 32, e = t % 32) loads 16-byte vectors e, e + 32,
+  // e + 64 of channel q's window (wvec vectors: a launch-wide bound)
+  const int sq = threadIdx.x >> 5, se = threadIdx.x & 31;
+  u32x4 r[3];
+  auto gload = [&](int c0) {
+    const int ci = min(c0 + sq, nactive - 1);  // past the end: a harmless reload
+    const uint32_t* row = x2 + static_cast<uint64_t>(active[ci]) * stride2 + ((tb + (wm[ci] & ~63)) >> 4);
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (se + 32 * i < wvec) r[i] = *reinterpret_cast<const u32x4*>(row + 4 * (se + 32 * i));
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      if (se + 32 * i < wvec) *reinterpret_cast<u32x4*>(&win[buf][sq * k2bWinDw + 4 * (se + 32 * i)]) = r[i];
+  };
+  auto compute = [&](int ci, const uint32_t* wb) {
+    const int w0 = wm[ci] & ~63;
+    const int32_t* o = offT + static_cast<uint64_t>(ci) * ldo + d_base + dm0;
+    uint32_t d[DPW][3], sh[DPW];
+#pragma unroll
+    for (int j = 0; j < DPW; ++j) {
+      const int rel = o[j] - w0;  // >= 0, wave-uniform
+      sh[j] = 2u * static_cast<uint32_t>(rel & 15);
+      const uint32_t* src = wb + 2 * lane + (rel >> 4);
+      d[j][0] = src[0];
+      d[j][1] = src[1];
+      d[j][2] = src[2];
+    }
+#pragma unroll
+    for (int j = 0; j < DPW; ++j) {
+      const uint32_t u0 = __builtin_amdgcn_alignbit(d[j][1], d[j][0], sh[j]);
+      const uint32_t u1 = __builtin_amdgcn_alignbit(d[j][2], d[j][1], sh[j]);
+      a4[j][0] += u0 & 0x33333333u;
+      a4[j][1] += (u0 >> 2) & 0x33333333u;
+      a4[j][2] += u1 & 0x33333333u;
+      a4[j][3] += (u1 >> 2) & 0x33333333u;
+    }
+    if ((ci & 3) == 3) flush4();    // wave-uniform
+    if ((ci & 63) == 63) flush8();
+  };
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int c0 = 0, it = 0; c0 < nactive; c0 += k2bCpb, ++it) {
+    const int buf = it & 1;
+    if (c0 + k2bCpb < nactive) gload(c0 + k2bCpb);  // in flight during these channels' sums
+#pragma unroll 2
+    for (int q = 0; q < k2bCpb; ++q)
+      if (c0 + q < nactive) compute(c0 + q, &win[buf][q * k2bWinDw]);
+    if (c0 + k2bCpb < nactive) lstore(buf ^ 1);
+    __syncthreads();
+  }
+  flush4();
+  flush8();
+  const uint64_t t = tb + static_cast<uint64_t>(lane) * 32;
+  if (t >= out_nsamps) return;
+#pragma unroll
+  for (int j = 0; j < DPW; ++j) {
+    if (dm0 + j >= ndm) break;  // ndm counts from d_base
+    const int dd = dm0 + j - d_skip;
+    if (dd < 0) continue;
+    // sample s of word wi: a16[2 (4 wi + k) + ((s >> 2) & 1)] half s >> 3,
+    // k = 0, 2, 1, 3 for s & 3 = 0, 1, 2, 3 (even fields, then odd)
+    uint32_t ob[8];
+#pragma unroll
+    for (int wi = 0; wi < 2; ++wi)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {  // output dword g of the word: samples 4g .. 4g+3
+        uint32_t v = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int sidx = 4 * g + e;
+          constexpr int kk[4] = {0, 2, 1, 3};
+          const uint32_t h = a16[j][2 * (4 * wi + kk[e]) + ((sidx >> 2) & 1)];
+          const int sum = static_cast<int>((sidx >> 3) ? (h >> 16) : (h & 0xFFFFu));
+          v |= static_cast<uint32_t>(scale_out(sum, scale)) << (8 * e);
+        }
+        ob[4 * wi + g] = v;
+      }
+    uint8_t* orow = out + static_cast<uint64_t>(dd) * out_stride + t;
+    if (t + 32 <= out_nsamps) {
+      *reinterpret_cast<u32x4*>(orow) = u32x4{ob[0], ob[1], ob[2], ob[3]};
+      *reinterpret_cast<u32x4*>(orow + 16) = u32x4{ob[4], ob[5], ob[6], ob[7]};
+    } else {
+      for (uint64_t e = 0; t + e < out_nsamps; ++e) orow[e] = static_cast<uint8_t>(ob[e >> 2] >> (8 * (e & 3)));
+    }
+  }
+}
+
 }  // namespace
 
 void dedisperse_direct(const int8_t* chan_major, uint64_t chan_stride, int nchans, const int32_t* offsets,
@@ -930,6 +1097,46 @@ void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_
 #undef PSOUP_LDS_ONE
 #undef PSOUP_LDS_LAUNCH
   post_launch_check("dedisperse_lds_kernel", s);
+}
+
+
+void pack2_rows(const int8_t* chan_major, uint64_t chan_stride, int nrows, uint32_t* out, uint64_t stride2, uint64_t t0,
+                uint64_t ns, hipStream_t s) {
+  if (ns == 0 || nrows <= 0) return;
+  PSOUP_CHECK(t0 % 16 == 0 && (chan_stride & 15) == 0, "pack2_rows: alignment");
+  const uint64_t dw0 = t0 / 16, ndw = (ns + 15) / 16;
+  PSOUP_CHECK(16 * (dw0 + ndw) <= chan_stride && dw0 + ndw <= stride2, "pack2_rows: past the rows");
+  PSOUP_CHECK(nrows <= 65535, "pack2_rows: too many rows");
+  dim3 grid(static_cast<unsigned>(std::min<uint64_t>((ndw + 255) / 256, 1024)), static_cast<unsigned>(nrows));
+  pack2_kernel<<<grid, 256, 0, s>>>(chan_major, chan_stride, out, stride2, dw0, ndw);
+  post_launch_check("pack2_kernel", s);
+}
+
+int dedisperse_2bit_window(int max_spread) { return ((k2bTs + max_spread + 48 + 63) / 64 + 1) * 4; }
+bool dedisperse_2bit_fits(int nactive, int max_spread) {
+  return nactive <= 21845 && dedisperse_2bit_window(max_spread) <= k2bWinDw;
+}
+
+void dedisperse_2bit(const uint32_t* x2, uint64_t stride2, const int32_t* d_active, int nactive, const int32_t* d_offT,
+                     int ldo, int d0, int ndm, const int32_t* d_wmin, int max_spread, int max_offset,
+                     uint64_t out_nsamps, uint8_t* out, uint64_t out_stride, float scale, hipStream_t s) {
+  if (ndm <= 0 || out_nsamps == 0 || nactive <= 0) return;
+  PSOUP_CHECK(dedisperse_2bit_fits(nactive, max_spread), "dedisperse_2bit: window or sums too large");
+  PSOUP_CHECK((out_stride & 15) == 0 && d0 >= 0, "dedisperse_2bit: stride alignment");
+  const uint64_t ty = (out_nsamps + k2bTs - 1) / k2bTs;
+  PSOUP_CHECK(ty <= 65535, "dedisperse_2bit: series too long for the grid");
+  PSOUP_CHECK(16 * stride2 >= ty * k2bTs + static_cast<uint64_t>(max_offset) +
+                                   16ull * static_cast<uint64_t>(dedisperse_2bit_window(max_spread)) &&
+                  stride2 % 4 == 0,
+              "dedisperse_2bit: packed rows too short for the windows");
+  constexpr int DPW = 4;
+  const int d_base = d0 / (4 * DPW) * (4 * DPW), d_skip = d0 - d_base;
+  dim3 grid(static_cast<unsigned>((ndm + d_skip + 4 * DPW - 1) / (4 * DPW)), static_cast<unsigned>(ty));
+  PSOUP_CHECK(d_base + static_cast<int>(grid.x) * 4 * DPW <= ldo, "dedisperse_2bit: offset table too narrow");
+  dedisperse_2bit_kernel<DPW><<<grid, 256, 0, s>>>(x2, stride2, d_active, nactive, d_offT, ldo, d_base, d_skip,
+                                                   ndm + d_skip, d_wmin, dedisperse_2bit_window(max_spread) / 4,
+                                                   out_nsamps, out, out_stride, scale);
+  post_launch_check("dedisperse_2bit_kernel", s);
 }
 
 }  // namespace kern

@@ -342,6 +342,11 @@ __host__ __device__ inline bool onex_colpass(int n2, int f) {
   return (f & kFft4OneX) && (f & kFft4Blocked) && (f & kFft4TileY) && n2 == 2048;
 }
 __host__ __device__ inline bool strip_input(int n2, int f) { return (f & kFft4StripInput) && onex_colpass(n2, f); }
+// pass A writes row-pair Y for the fused spectrum pass: the one-exchange
+// kernel always can, the tiled-Y Stockham kernel with kFft4PairY
+__host__ __device__ inline bool pair_y_layout(int n2, int f) {
+  return onex_colpass(n2, f) || ((f & kFft4PairY) && (f & kFft4Blocked) && (f & kFft4TileY));
+}
 
 __global__ void __launch_bounds__(256) fft4_pad_strips_kernel(const float* __restrict__ in, uint64_t n,
                                                               float* __restrict__ out, uint32_t rowlen,
@@ -363,7 +368,8 @@ __global__ void __launch_bounds__(256) fft4_pad_strips_kernel(const float* __res
 // lane reads its rows' values as contiguous 16-byte vectors and eight lanes
 // cover 512 contiguous bytes.
 // bit 3 = tiled X: X_t[k2/8][k1/8][k2%8][k1%8] (read by r2c_interbin_normalise_tiled).
-constexpr int kModeBlocked = 1, kModeTileY = 4, kModeTileX = 8;
+// bit 4 = row-pair Y (pass A -> fused spectrum pass): Y_p[k2/2][i][k2%2].
+constexpr int kModeBlocked = 1, kModeTileY = 4, kModeTileX = 8, kModePairY = 16;
 
 // Pass A.  Logical block = column block * K + trial (trial fastest).
 template <int L, int CPT, int SUB, int MODE>
@@ -371,8 +377,9 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
     const float* __restrict__ in, const float* __restrict__ in_pad, uint64_t n, const double* __restrict__ afs, int K,
     float2* __restrict__ Y, Fft4Geom g, const float2* __restrict__ tab, int flags) {
   using C = Cfg<L, CPT, SUB>;
-  constexpr bool kBlocked = MODE & kModeBlocked, kTileY = MODE & kModeTileY;
+  constexpr bool kBlocked = MODE & kModeBlocked, kTileY = MODE & kModeTileY, kPairY = MODE & kModePairY;
   static_assert(!kTileY || (CPT == 8 && SUB == 1), "tiled Y: 8 transforms per thread");
+  static_assert(!kPairY || kTileY, "row-pair Y: the tiled-Y kernel shape");
   __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   constexpr int T = C::T;
   const int grp = threadIdx.x / T;
@@ -454,7 +461,13 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
       v[c][q] = cmul(v[c][q], w);
       w = cmul(w, step);
     }
-    if constexpr (kTileY) {
+    if constexpr (kPairY) {
+      // lanes k2, k2 + 1 write 16 contiguous bytes; the 8 columns of a lane
+      // fill one 128-byte line across the 8 stores (merged in L2)
+      float2* dst = yk + static_cast<uint64_t>(k2 >> 1) * (2 * N1) + 2 * c0 + (k2 & 1);
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) dst[2 * c] = v[c][q];
+    } else if constexpr (kTileY) {
       float2* dst = yk + static_cast<uint64_t>(c0) * g.n2 + (k2 >> 3) * 64 + (k2 & 7);
 #pragma unroll
       for (int c = 0; c < CPT; ++c) dst[c * 8] = v[c][q];
@@ -708,8 +721,9 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
     const float2* __restrict__ Y, float2* __restrict__ X, int K, Fft4Geom g, const float2* __restrict__ tab,
     int flags, uint32_t keep_oct) {
   using C = Cfg<L, CPT, SUB>;
-  constexpr bool kBlocked = MODE & kModeBlocked, kTileY = MODE & kModeTileY;
+  constexpr bool kBlocked = MODE & kModeBlocked, kTileY = MODE & kModeTileY, kPairY = MODE & kModePairY;
   static_assert(!kTileY || (CPT == 8 && SUB == 1), "tiled Y: 8 transforms per thread");
+  static_assert(!kPairY || kTileY, "row-pair Y: the tiled-Y kernel shape");
   __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
   constexpr int T = C::T;
   const int grp = threadIdx.x / T;
@@ -1023,7 +1037,7 @@ namespace {
 // fastest measured (tools/kbench.py, bench A/B); the strip input: pass A 15.9 -> 13.9 us/trial alone,
 // bench within noise (profiles/r3_strip)
 int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4TileY | kFft4TileX | kFft4PairXcd |
-                   kFft4GroupXcd | kFft4UniformTw | kFft4OneX | kFft4StripInput;
+                   kFft4GroupXcd | kFft4UniformTw | kFft4OneX | kFft4StripInput | kFft4PairY;
 }  // namespace
 
 void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& g, hipStream_t s, int count,
@@ -1105,7 +1119,7 @@ void fft4_rowpass_spectrum(const float2* Y, int K, const Fft4Geom& g, const floa
   const uint64_t nblocks = static_cast<uint64_t>(g.n2 / 8) * ((static_cast<uint64_t>(K) + 7) / 8 * 8);
   PSOUP_CHECK(nblocks < (1ull << 31), "fft4 spectrum pass: grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
-  PSOUP_CHECK(!g.ypair || fft4_pair_y(g), "fft4 spectrum pass: the row-pair Y layout needs the one-exchange pass A");
+  PSOUP_CHECK(!g.ypair || fft4_pair_y(g), "fft4 spectrum pass: pass A cannot write the row-pair Y layout");
   switch (g.n1) {
 #define PS_CASE(LL)                                                                                         \
   case LL:                                                                                                  \
@@ -1121,7 +1135,7 @@ void fft4_rowpass_spectrum(const float2* Y, int K, const Fft4Geom& g, const floa
   post_launch_check("fft4_rowpass_spectrum_kernel", s);
 }
 
-bool fft4_pair_y(const Fft4Geom& g) { return g.ok && onex_colpass(g.n2, g_fft4_flags); }
+bool fft4_pair_y(const Fft4Geom& g) { return g.ok && pair_y_layout(g.n2, g_fft4_flags); }
 
 void fft4_set_flags(int flags) {
   g_fft4_flags = flags;
@@ -1158,10 +1172,12 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 16 == 0, "fft4 colpass: grid");
   PSOUP_CHECK(!(f & kFft4GroupXcd) || (K & 7) != 0 || nblocks % 128 == 0, "fft4 colpass: group grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
-  PSOUP_CHECK(!g.ypair || onex_colpass(g.n2, f), "fft4 colpass: the row-pair Y layout needs the one-exchange pass A");
+  PSOUP_CHECK(!g.ypair || pair_y_layout(g.n2, f), "fft4 colpass: this pass A cannot write the row-pair Y layout");
   if (onex_colpass(g.n2, f))
     fft4_colpass_onex_kernel<2048, 64, 4><<<grid, OneX<2048, 64, 4>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g,
                                                                                     tables, f);
+  else if (g.ypair)
+    launch_colpass<8, 1, kModeBlocked | kModeTileY | kModePairY>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   else if ((f & kFft4Blocked) && (f & kFft4TileY))
     launch_colpass<8, 1, kModeBlocked | kModeTileY>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   else if ((f & kFft4Cpt8) && (f & kFft4Blocked))

@@ -479,48 +479,41 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
     const uint32_t i = r * kClThreads + t;
     if (i >= n || !(flag[kPad + i] & 1)) continue;
     const int xi = static_cast<int>(kidx[kPad + i]);
-    // positions after i below the target (sorted: a prefix of the window);
-    // fast path: a run of consecutive bins reaches the target exactly gap
-    // positions ahead
+    // positions after i below the target (sorted: a prefix of the next 31,
+    // at most gap - 1 <= 29 of them): fast path, a run of consecutive bins
+    // reaches the target exactly gap positions ahead; else a branchless
+    // binary search (5 LDS reads, not 32 compares; past n the pads read
+    // 0x7fffffff, never below a target)
+    const int tgt = xi + gap;
     uint32_t p;
-    if (i + gap < n && static_cast<int>(kidx[kPad + i + gap]) == xi + gap) {
+    if (i + gap < n && static_cast<int>(kidx[kPad + i + gap]) == tgt) {
       p = i + gap;
     } else {
-      const uint32_t a = (kPad + i + 1) & ~3u, sh = (kPad + i + 1) - a;
       uint32_t below = 0;
 #pragma unroll
-      for (int v = 0; v < 8; ++v) {
-        const uint4 xv = *reinterpret_cast<const uint4*>(kidx + a + 4 * v);
-        const uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t off = static_cast<uint32_t>(4 * v + e);
-          below += (off >= sh && static_cast<int>(xs[e]) < xi + gap) ? 1u : 0u;
-        }
-      }
+      for (uint32_t st = 16; st >= 1; st >>= 1)
+        if (static_cast<int>(kidx[kPad + i + below + st]) < tgt) below += st;
       p = i + 1 + below;
     }
     const uint32_t nx = p < n ? ((flag[kPad + p] & 1) ? p : jmp[p]) : n;
     // run start: no survivor within the gap before i; fast path: the
-    // previous position is a survivor within the gap
+    // previous position is a survivor within the gap.  Else k = the first
+    // position with idx > idx_i - gap (a binary search over the 32 before i;
+    // the pads before position 0 read as far below), and i starts a run iff
+    // the next survivor at or after k is i itself (a survivor's own entry:
+    // itself; a non-survivor's jump entry is never overwritten here)
     bool start = true;
     if (i > 0 && (flag[kPad + i - 1] & 1) && xi - static_cast<int>(kidx[kPad + i - 1]) < gap) {
       start = false;
     } else {
-      const uint32_t b = (kPad + i - 32) & ~3u;  // >= 0: kPad >= 36
+      const int lim = xi - gap;  // (pads: INT_MIN, at or below every limit)
+      uint32_t far = 0;          // positions of [i - 32, i) at or below idx_i - gap: a prefix
 #pragma unroll
-      for (int v = 0; v < 9; ++v) {
-        const uint4 xv = *reinterpret_cast<const uint4*>(kidx + b + 4 * v);
-        const uint32_t fw = *reinterpret_cast<const uint32_t*>(flag + b + 4 * v);
-        const uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t pos = b + static_cast<uint32_t>(4 * v + e);  // padded position
-          const bool before = pos < kPad + i;
-          const bool s1 = (fw >> (8 * e)) & 1u;
-          start = start && !(before && s1 && xi - static_cast<int>(xs[e]) < gap);
-        }
-      }
+      for (uint32_t st = 16; st >= 1; st >>= 1)
+        if (static_cast<int>(kidx[kPad + i - 32 + far + st - 1]) <= lim) far += st;
+      const uint32_t k = i - 32 + far + (static_cast<int>(kidx[kPad + i - 32 + far]) <= lim ? 1u : 0u);
+      const uint32_t ns = k >= i ? i : ((flag[kPad + k] & 1) ? k : static_cast<uint32_t>(jmp[k]));
+      start = ns >= i;
     }
     jmp[i] = static_cast<uint16_t>(nx);
     if (start) flag[kPad + i] = 5;

@@ -863,7 +863,8 @@ PYBIND11_MODULE(_C, m) {
       .value("Auto", DedispKernel::Auto)
       .value("Direct", DedispKernel::Direct)
       .value("Mfma", DedispKernel::Mfma)
-      .value("Valu", DedispKernel::Valu);
+      .value("Valu", DedispKernel::Valu)
+      .value("Packed2", DedispKernel::Packed2);
   py::class_<DedispGeometry>(m, "DedispGeometry")
       .def_static("make", [](const py::dict& hdr, uint64_t nsamps, const std::vector<float>& dms,
                              const std::vector<int>& kill) { return DedispGeometry::make(dict_to_header(hdr), nsamps, dms, kill); })

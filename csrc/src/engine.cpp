@@ -22,7 +22,8 @@ DedispKernel parse_dedisp_kernel(const std::string& s) {
   if (s == "direct") return DedispKernel::Direct;
   if (s == "mfma") return DedispKernel::Mfma;
   if (s == "valu") return DedispKernel::Valu;
-  PSOUP_THROW("unknown dedispersion kernel '" << s << "' (auto|direct|mfma|valu)");
+  if (s == "packed2") return DedispKernel::Packed2;
+  PSOUP_THROW("unknown dedispersion kernel '" << s << "' (auto|direct|mfma|valu|packed2)");
 }
 
 // ------------------------------------------------------------ geometry ------
@@ -66,10 +67,23 @@ DeviceFilterbank::DeviceFilterbank(const DedispGeometry& g, hipStream_t stream) 
   stride_ = (g_.nsamps + 1024 + 255) / 256 * 256;
   chan_.resize(stride_ * static_cast<uint64_t>(g_.nchans + 1));
   chan_.zero_async(stream_);
+  if (g_.nbits <= 2 && g_.bias == 0) {
+    // 2-bit rows: 6144 + 2048 samples of zeros past the int8 row length (a
+    // workgroup's staged window past its last sample)
+    stride2_ = (stride_ + 8192) / 64 * 4;
+    chan2_.resize(stride2_ * static_cast<uint64_t>(g_.nchans));
+    chan2_.zero_async(stream_);
+  }
+}
+
+void DeviceFilterbank::pack2(uint64_t t0, uint64_t ns, hipStream_t s) {
+  if (chan2_.size())
+    kern::pack2_rows(chan_.data(), stride_, g_.nchans, chan2_.data(), stride2_, t0, ns, s ? s : stream_);
 }
 
 void DeviceFilterbank::load_packed_device(const uint8_t* d_packed) {
   kern::unpack_transpose(d_packed, g_.nsamps, g_.nchans, g_.nbits, chan_.data(), stride_, g_.bias, stream_);
+  pack2(0, g_.nsamps, stream_);
 }
 
 void DeviceFilterbank::load_packed_host(const uint8_t* h_packed) {
@@ -92,6 +106,7 @@ void DeviceFilterbank::load_packed_host(const uint8_t* h_packed) {
     std::memcpy(stage[slot].data(), h_packed + t0 * bps, ns * bps);
     PSOUP_HIP_CHECK(hipMemcpyAsync(dstage[slot].data(), stage[slot].data(), ns * bps, hipMemcpyHostToDevice, stream_));
     kern::unpack_transpose(dstage[slot].data(), ns, g_.nchans, g_.nbits, chan_.data() + t0, stride_, g_.bias, stream_);
+    pack2(t0, ns, stream_);
     ev[slot].record(stream_);
     used[slot] = true;
     slot ^= 1;
@@ -103,6 +118,7 @@ void DeviceFilterbank::load_packed_host(const uint8_t* h_packed) {
 void DeviceFilterbank::unpack_chunk(const uint8_t* d_packed, uint64_t t0, uint64_t ns, hipStream_t s) {
   PSOUP_CHECK(t0 + ns <= g_.nsamps, "unpack_chunk: samples past the filterbank");
   kern::unpack_transpose(d_packed, ns, g_.nchans, g_.nbits, chan_.data() + t0, stride_, g_.bias, s ? s : stream_);
+  pack2(t0, ns, s);
 }
 
 void staged_upload(uint64_t bytes, uint64_t chunk, const HostReader& read, uint8_t* d_dst, hipStream_t s,
@@ -129,8 +145,9 @@ void staged_upload(uint64_t bytes, uint64_t chunk, const HostReader& read, uint8
     if (used[i]) staged[i].sync();
 }
 
-void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std::vector<int>& devices,
-                            const HostReader& read) {
+namespace {
+void fanout_impl(const std::vector<DeviceFilterbank*>& fbs, const std::vector<int>& devices, const HostReader& read,
+                 const uint8_t* h_direct) {
   PSOUP_CHECK(!fbs.empty() && fbs.size() == devices.size(), "load_filterbank_fanout: one device per filterbank");
   const DedispGeometry& g = fbs[0]->geometry();
   const uint64_t bps = static_cast<uint64_t>(g.nchans) * g.nbits / 8;  // bytes per sample
@@ -148,7 +165,7 @@ void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std
   PSOUP_HIP_CHECK(hipSetDevice(devices[0]));
   hipStream_t s0 = fbs[0]->stream();
   Event landed;
-  staged_upload(bytes, chunk * bps, read, packed[0].data(), s0, [&](uint64_t off, uint64_t nb) {
+  auto on_chunk = [&](uint64_t off, uint64_t nb) {
     const uint64_t t0 = off / bps, ns = nb / bps;
     landed.record(s0);
     fbs[0]->unpack_chunk(packed[0].data() + off, t0, ns);
@@ -160,7 +177,15 @@ void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std
       fbs[i]->unpack_chunk(packed[i].data() + off, t0, ns);
     }
     PSOUP_HIP_CHECK(hipSetDevice(devices[0]));
-  });
+  };
+  if (h_direct && bytes <= chunk * bps) {
+    // a file within one chunk goes up straight from its (mapped) pages:
+    // pinning a stage costs more than the copy (tutorial.fil: 3 MB)
+    PSOUP_HIP_CHECK(hipMemcpy(packed[0].data(), h_direct, bytes, hipMemcpyHostToDevice));
+    on_chunk(0, bytes);
+  } else {
+    staged_upload(bytes, chunk * bps, read, packed[0].data(), s0, on_chunk);
+  }
   for (size_t i = 0; i < n; ++i) {
     PSOUP_HIP_CHECK(hipSetDevice(devices[i]));
     PSOUP_HIP_CHECK(hipStreamSynchronize(fbs[i]->stream()));
@@ -173,16 +198,24 @@ void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std
   PSOUP_HIP_CHECK(hipSetDevice(prev));
 }
 
+}  // namespace
+
+void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std::vector<int>& devices,
+                            const HostReader& read) {
+  fanout_impl(fbs, devices, read, nullptr);
+}
+
 void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std::vector<int>& devices,
                             const uint8_t* h_packed) {
-  load_filterbank_fanout(fbs, devices,
-                         [h_packed](uint64_t off, uint64_t n, uint8_t* dst) { std::memcpy(dst, h_packed + off, n); });
+  fanout_impl(
+      fbs, devices, [h_packed](uint64_t off, uint64_t n, uint8_t* dst) { std::memcpy(dst, h_packed + off, n); },
+      h_packed);
 }
 
 void load_filterbank_fanout(const std::vector<DeviceFilterbank*>& fbs, const std::vector<int>& devices,
                             const Filterbank& fb) {
-  load_filterbank_fanout(fbs, devices,
-                         [&fb](uint64_t off, uint64_t n, uint8_t* dst) { fb.read_data(off, n, dst); });
+  fanout_impl(
+      fbs, devices, [&fb](uint64_t off, uint64_t n, uint8_t* dst) { fb.read_data(off, n, dst); }, fb.data());
 }
 
 Dedisperser::Dedisperser(const DeviceFilterbank& fb, hipStream_t stream) : fb_(fb), stream_(stream) {
@@ -322,6 +355,12 @@ void Dedisperser::build_valu_tables(const std::vector<int32_t>& offs, int e0, in
                             hipMemcpyHostToDevice));
 }
 
+int Dedisperser::max_spread(int d0, int d1) const {
+  int win = 0;
+  for (int T = d0 / kTileDms; T <= (d1 - 1) / kTileDms; ++T) win = std::max(win, h_tile_win_[static_cast<size_t>(T)]);
+  return std::max(0, win - 1056);  // h_tile_win_ = 1024 + (hi - w0) + 32
+}
+
 static double valu_ratio() {
   // MFMA steps per (tile, active channel) above which the VALU kernel is
   // faster (calibrated on MI355X with tools/dedisp_bench.py)
@@ -366,18 +405,29 @@ void Dedisperser::upload_mfma_lds_tables(const kern::MfmaLdsPlan& plan) {
   up(ml_wmin_, plan.wmin);
 }
 
-static double mfma_lds_ratio() {
+static double mfma_lds_ratio(bool packed2) {
   // LDS-fed MFMA steps per (tile, active channel) up to which a tile takes the
   // MFMA kernel in Auto (each step is 2 x 16-shift blocks of one-hot GEMM;
   // the VALU kernels cost the same per channel whatever the spread).
-  // Measured crossover on MI355X (profiles/r3_dedisp): ~2.35 steps/channel
+  // Measured crossover on MI355X vs the byte kernel (profiles/r3_dedisp):
+  // ~2.35 steps/channel; vs the 2-bit kernel: PSOUP_MFMA_LDS_RATIO_2BIT
+  // (tools/dedisp_bench.py sweeps it)
+  if (packed2) {
+    static const double r2 = [] {
+      const char* e = std::getenv("PSOUP_MFMA_LDS_RATIO_2BIT");
+      return e ? std::atof(e) : 2.3;
+    }();
+    return r2;
+  }
   return 2.3;
 }
 
 int Dedisperser::mfma_lds_split(int d0, int d1) {
   const auto& g = fb_.geometry();
-  if (g.nactive == 0 || mfma_lds_ratio() <= 0) return d0;
+  if (g.nactive == 0) return d0;
   ensure_tables(d0, d1);
+  const double ratio = mfma_lds_ratio(fb_.data2() != nullptr && kern::dedisperse_2bit_fits(g.nactive, max_spread(d0, d1)));
+  if (ratio <= 0) return d0;
   int T = d0 / kTileDms;
   const int T1 = (d1 - 1) / kTileDms + 1;
   // the MFMA kernel computes whole 32-DM tiles, the VALU kernels only the
@@ -386,7 +436,7 @@ int Dedisperser::mfma_lds_split(int d0, int d1) {
   // MFMA 9.7 ms vs VALU 4.9 ms per step at 2^23)
   auto tile_dms = [&](int t) { return std::min(d1, (t + 1) * kTileDms) - std::max(d0, t * kTileDms); };
   while (T < T1 && ml_tile_ok_[static_cast<size_t>(T)] &&
-         ml_tile_steps_[static_cast<size_t>(T)] <= mfma_lds_ratio() * g.nactive * tile_dms(T) / kTileDms)
+         ml_tile_steps_[static_cast<size_t>(T)] <= ratio * g.nactive * tile_dms(T) / kTileDms)
     ++T;
   return std::min(d1, T * kTileDms);
 }
@@ -451,7 +501,11 @@ void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispK
     const int split = mfma_lds_split(d0, d1);
     if (split > d0) {
       run_mfma_lds(d0, split, out, out_stride, s);
-      if (split < d1) run(split, d1, out + static_cast<uint64_t>(split - d0) * out_stride, out_stride, DedispKernel::Valu, s);
+      if (split < d1) {
+        const bool p2 = fb_.data2() && kern::dedisperse_2bit_fits(g.nactive, max_spread(split, d1));
+        run(split, d1, out + static_cast<uint64_t>(split - d0) * out_stride, out_stride,
+            p2 ? DedispKernel::Packed2 : DedispKernel::Valu, s);
+      }
       return;
     }
   }
@@ -465,9 +519,26 @@ void Dedisperser::run(int d0, int d1, uint8_t* out, uint64_t out_stride, DedispK
       return;
     }
   }
-  if (kind == DedispKernel::Auto) kind = choose(d0, d1);
-  if (kind == DedispKernel::Valu && g.nactive == 0) kind = DedispKernel::Direct;
+  if (kind == DedispKernel::Auto) {
+    // past the MFMA-LDS tiles: the 2-bit kernel where the data allows (it
+    // beats the global-load MFMA plan at any spread), else the byte / MFMA choice
+    ensure_tables(d0, d1);
+    kind = fb_.data2() && kern::dedisperse_2bit_fits(g.nactive, max_spread(d0, d1)) ? DedispKernel::Packed2
+                                                                                   : choose(d0, d1);
+  }
+  if ((kind == DedispKernel::Valu || kind == DedispKernel::Packed2) && g.nactive == 0) kind = DedispKernel::Direct;
   const int ndm = d1 - d0;
+  if (kind == DedispKernel::Packed2) {
+    PSOUP_CHECK(fb_.data2(), "packed2 dedispersion needs nbits <= 2 data");
+    ensure_tables(d0, d1);
+    const int spread = max_spread(d0, d1);
+    if (kern::dedisperse_2bit_fits(g.nactive, spread)) {
+      kern::dedisperse_2bit(fb_.data2(), fb_.stride2(), d_active_.data(), g.nactive, r_offT_.data(), ldo_, d0, ndm,
+                            r_wmin_.data(), spread, g.max_delay, g.out_nsamps, out, out_stride, g.out_scale, s);
+      return;
+    }
+    kind = DedispKernel::Valu;  // a window too wide for the 2-bit kernel's LDS
+  }
   if (kind == DedispKernel::Valu) {
     ensure_tables(d0, d1);
     int win = 0;
@@ -1035,6 +1106,27 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
     }
   } else {
     run(0, count, stream_);
+  }
+  if (const char* dump = std::getenv("PSOUP_DUMP_PEAKS")) {
+    // diagnostics (tools/expt/cluster_replay.py): the first batch's raw peak
+    // records with at least PSOUP_DUMP_PEAKS_MIN of them, for replaying the
+    // clustering kernels on real data
+    static std::atomic<bool> dumped{false};
+    const char* mn = std::getenv("PSOUP_DUMP_PEAKS_MIN");
+    uint32_t n = 0;
+    PSOUP_HIP_CHECK(hipMemcpyAsync(&n, s.d_count.data(), 4, hipMemcpyDeviceToHost, stream_));
+    PSOUP_HIP_CHECK(hipStreamSynchronize(stream_));
+    n = std::min(n, cap_);
+    if (n >= static_cast<uint32_t>(mn ? std::atoi(mn) : 1) && !dumped.exchange(true)) {
+      std::vector<kern::PeakRecord> h(n);
+      PSOUP_HIP_CHECK(hipMemcpy(h.data(), s.d_peaks.data(), n * sizeof(kern::PeakRecord), hipMemcpyDeviceToHost));
+      if (FILE* f = std::fopen(dump, "wb")) {
+        const uint32_t hdr[3] = {static_cast<uint32_t>(count) * 8, static_cast<uint32_t>(p_.min_gap), n};
+        std::fwrite(hdr, 4, 3, f);
+        std::fwrite(h.data(), sizeof(kern::PeakRecord), n, f);
+        std::fclose(f);
+      }
+    }
   }
   if (gpu_cluster_) {
     // cluster on the device: only cluster peaks (and the rare over-capacity

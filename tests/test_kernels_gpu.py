@@ -58,6 +58,8 @@ def test_dedisperse_direct_mfma_valu_bit_exact(C, nbits, nchans, kill):
     stride = C.Dedisperser.row_stride(g.out_nsamps)
     outs = {}
     kinds = (C.DedispKernel.Direct, C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto)
+    if nbits <= 2:  # the packed 2-bit kernel
+        kinds = kinds + (C.DedispKernel.Packed2,)
     for k in kinds:
         o = torch.zeros(ndm * stride, dtype=torch.uint8, device=dev)
         dd.run(0, ndm, o.data_ptr(), stride, k)
@@ -67,7 +69,7 @@ def test_dedisperse_direct_mfma_valu_bit_exact(C, nbits, nchans, kill):
     for k in kinds:
         assert np.array_equal(outs[k], exp), k
     # sub-range (DM offset inside a tile)
-    for k in (C.DedispKernel.Mfma, C.DedispKernel.Valu):
+    for k in kinds[1:]:
         o = torch.zeros(5 * stride, dtype=torch.uint8, device=dev)
         dd.run(3, 8, o.data_ptr(), stride, k)
         assert np.array_equal(o.view(5, stride)[:, : g.out_nsamps].cpu().numpy(), exp[3:8]), k
@@ -97,12 +99,13 @@ def test_dedisperse_1024ch_hybrid_mfma_bit_exact(C):
     assert dd.mfma_lds_split(0, 8) == 0  # an 8-DM partial tile: the VALU kernel (MFMA computes all 32 DMs)
     stride = C.Dedisperser.row_stride(g.out_nsamps)
     outs = {}
-    for k in (C.DedispKernel.Direct, C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto):
+    P2 = C.DedispKernel.Packed2
+    for k in (C.DedispKernel.Direct, C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto, P2):
         o = torch.zeros(ndm * stride, dtype=torch.uint8, device=dev)
         dd.run(0, ndm, o.data_ptr(), stride, k)
         outs[k] = o.view(ndm, stride)[:, : g.out_nsamps]
     ref_ = outs[C.DedispKernel.Direct]
-    for k in (C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto):
+    for k in (C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto, P2):
         assert torch.equal(outs[k], ref_), k
     # MFMA-LDS on the low-DM tiles alone, and a range starting inside the split
     o = torch.zeros(split * stride, dtype=torch.uint8, device=dev)
@@ -115,7 +118,7 @@ def test_dedisperse_1024ch_hybrid_mfma_bit_exact(C):
     # [8r, 8r + 8), static shards cut anywhere): every kernel, no per-call plan
     for d0, d1 in ((8, 16), (24, 32), (40, 48), (1, 9), (5, 70), (13, 40), (33, 97), (100, 101),
                    (split - 3, split + 37), (250, ndm)):
-        for k in (C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto):
+        for k in (C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto, P2):
             o = torch.zeros((d1 - d0 + 2) * stride, dtype=torch.uint8, device=dev)  # a guard row each side
             dd.run(d0, d1, o.data_ptr() + stride, stride, k)
             got = o.view(d1 - d0 + 2, stride)
@@ -132,10 +135,40 @@ def test_dedisperse_1024ch_hybrid_mfma_bit_exact(C):
         sh = C.Dedisperser(dfb, s)
         sh.warm(d0, d1)
         for a, b in ((d0, d1), (d0 + 3, d1 - 1), out_of):
-            for k in (C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto):
+            for k in (C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto, P2):
                 o = torch.zeros((b - a) * stride, dtype=torch.uint8, device=dev)
                 sh.run(a, b, o.data_ptr(), stride, k)
                 assert torch.equal(o.view(b - a, stride)[:, : g.out_nsamps], ref_[a:b]), (d0, d1, a, b, k)
+
+
+def test_dedisperse_packed2_high_dm_bit_exact(C):
+    """The 2-bit kernel at config-4 DMs up to ~2000 (wide per-tile spreads,
+    windows near its LDS bound), with killed channels: equal to the direct
+    kernel byte for byte, for whole tiles, unaligned ranges and Auto."""
+    rng = np.random.default_rng(41)
+    nchans, tsamp, fch1, foff = 1024, 64e-6, 1550.0, -400.0 / 1024
+    dms = C.generate_dm_list(0.0, 2200.0, tsamp, 64.0, fch1, foff, nchans, 1.1)
+    delays = C.generate_delay_table(nchans, tsamp, fch1, foff)
+    nsamps = (1 << 18) + 5000 + C.compute_max_delay(dms, delays)
+    hdr = synthetic.make_header(nchans=nchans, nbits=2, tsamp=tsamp, fch1=fch1, foff=foff, nsamples=nsamps)
+    killmask = [int(rng.random() > 0.03) for _ in range(nchans)]
+    g = C.DedispGeometry.make(hdr, nsamps, dms, killmask)
+    s = torch.cuda.current_stream().cuda_stream
+    dfb = C.DeviceFilterbank(g, s)
+    packed = torch.randint(0, 256, (nsamps * nchans * 2 // 8,), dtype=torch.uint8, device=dev)
+    dfb.load_packed_device(packed.data_ptr())
+    dd = C.Dedisperser(dfb, s)
+    ndm = len(dms)
+    stride = C.Dedisperser.row_stride(g.out_nsamps)
+    for d0, d1 in ((ndm - 64, ndm), (ndm // 2 + 5, ndm // 2 + 40), (700, 732), (0, 32)):
+        outs = {}
+        for k in (C.DedispKernel.Direct, C.DedispKernel.Packed2, C.DedispKernel.Auto):
+            o = torch.zeros((d1 - d0) * stride, dtype=torch.uint8, device=dev)
+            dd.run(d0, d1, o.data_ptr(), stride, k)
+            outs[k] = o.view(d1 - d0, stride)[:, : g.out_nsamps]
+        assert outs[C.DedispKernel.Direct].any()
+        for k in (C.DedispKernel.Packed2, C.DedispKernel.Auto):
+            assert torch.equal(outs[k], outs[C.DedispKernel.Direct]), (d0, d1, k)
 
 
 def test_mfma_resident_plan_ranges_and_side_stream(C):
@@ -317,11 +350,12 @@ def test_r2c_interbin_normalise_batch():
 
 
 # Every prefix of the kernel-shape chain (kernels.hpp Fft4Flags): None = the
-# default (1073954051 = 212227 | kFft4StripInput); 0 / 1 = natural layouts
-# (2 x 4 / 8 transforms per thread); 259 = blocked; 1299 = + tiled Y; 3331 =
-# + tiled X; 7427 = + paired XCD blocks; 15619 = + grouped XCD blocks; 81155 =
-# + uniform pass-A twiddles (the Stockham pass A); 212227 = + the one-exchange
-# pass A on the row-pitch input.
+# default (1074216195 = 212227 | kFft4StripInput | kFft4PairY); 0 / 1 =
+# natural layouts (2 x 4 / 8 transforms per thread); 259 = blocked; 1299 = +
+# tiled Y; 3331 = + tiled X; 7427 = + paired XCD blocks; 15619 = + grouped XCD
+# blocks; 81155 = + uniform pass-A twiddles (the Stockham pass A); 212227 = +
+# the one-exchange pass A on the row-pitch input.  (kFft4PairY only changes
+# the fused spectrum pass's input: tests/test_spectrum_gpu.py.)
 FFT4_FLAG_SETS = [None, 0, 1, 259, 1299, 3331, 7427, 15619, 81155, 212227]
 
 

@@ -44,10 +44,10 @@ def chunked_records(segs, rng):
     return np.concatenate(rows)
 
 
-def test_peak_cluster_matches_host_scan(C):
+@pytest.mark.parametrize("gap", [30, 5, 1])
+def test_peak_cluster_matches_host_scan(C, gap):
     K = C.kernels
-    rng = np.random.default_rng(3)
-    gap = 30
+    rng = np.random.default_rng(3 + gap)
     cap_seg = int(K.cluster_cap)
     sizes = [0, 1, 2, 31, 64, 65, 500, 4096, 4097, 5000, cap_seg, cap_seg + 1, 20000, 7, 0, 900, 12000, 3]
     segs = {}

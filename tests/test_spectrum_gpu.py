@@ -60,6 +60,12 @@ def test_spectrum_pass_matches_unfused(log2n):
 
     sh = C.kernels.spec_q_shift
     assert np.array_equal(Q.cpu().numpy()[:, sh:sh + M + 1], _q8_ref(Pn))
+    # the row-pair Y hand-over (both pass-A kernels) changes only the layout:
+    # the same bits as the tiled Y
+    assert g.ypair, "the default pass A hands over row-pair Y at every length"
+    Pt, Qt, gt = ops.fft4_spectrum_pass(x, accs, 64e-6, st, float(n), pair_y=False)
+    assert not gt.ypair
+    assert torch.equal(Pt, Pb) and torch.equal(Qt, Q)
 
 
 def test_spec_pblk_index_native_equals_python():

@@ -52,8 +52,10 @@ def main():
     ndm = len(dms)
     rs = _C.Dedisperser.row_stride(g.out_nsamps)
     T = _C.Dedisperser.tile_dms
-    bufs = {k: torch.empty(T * rs, dtype=torch.uint8, device="cuda") for k in ("m", "v")}
+    bufs = {k: torch.empty(T * rs, dtype=torch.uint8, device="cuda") for k in ("m", "v", "p")}
     kinds = {"m": _C.DedispKernel.Mfma, "v": _C.DedispKernel.Valu}
+    if a.nbits <= 2:
+        kinds["p"] = _C.DedispKernel.Packed2  # the 2-bit kernel
 
     def timed(k, d0, d1, reps):
         e0, e1 = _C.GpuEvent(True), _C.GpuEvent(True)
@@ -71,16 +73,18 @@ def main():
         d1 = min(ndm, d0 + T)
         tm = timed("m", d0, d1, a.reps)
         tv = timed("v", d0, d1, a.reps)
+        tp = timed("p", d0, d1, a.reps) if "p" in kinds else None
         s.synchronize()
         n = g.out_nsamps
-        same = bool(torch.equal(bufs["m"][: (d1 - d0) * rs].view(d1 - d0, rs)[:, :n],
-                                bufs["v"][: (d1 - d0) * rs].view(d1 - d0, rs)[:, :n]))
+        view = lambda k: bufs[k][: (d1 - d0) * rs].view(d1 - d0, rs)[:, :n]  # noqa: E731
+        same = bool(torch.equal(view("m"), view("v"))) and (tp is None or bool(torch.equal(view("m"), view("p"))))
         print(json.dumps({"d0": d0, "dm": round(dms[d0], 2), "mfma_ms": round(tm, 4), "valu_ms": round(tv, 4),
+                          "packed2_ms": round(tp, 4) if tp is not None else None,
                           "auto": "MfmaLds" if dd.mfma_lds_split(d0, d1) > d0 else str(dd.choose(d0, d1)).split(".")[-1],
                           "bit_exact": same,
                           "mfma_steps_per_chan": round(dd.mfma_steps_per_channel(d0, d1), 3)}), flush=True)
     tot = {}
-    for k in ("m", "v", "auto"):
+    for k in [x for x in ("m", "v", "p") if x in kinds] + ["auto"]:
         e0, e1 = _C.GpuEvent(True), _C.GpuEvent(True)
         e0.record(s.handle)
         for d0 in range(0, ndm, T):
@@ -103,14 +107,22 @@ def main():
     e1.record(s.handle)
     e1.synchronize()
     tot["valu_whole"] = round(e0.elapsed_ms(e1), 2)
+    if "p" in kinds:
+        e0.record(s.handle)
+        dd.run(0, ndm, whole.data_ptr(), rs, kinds["p"], s.handle)
+        e1.record(s.handle)
+        e1.synchronize()
+        tot["packed2_whole"] = round(e0.elapsed_ms(e1), 2)
     tot["split_dm"] = dd.mfma_lds_split(0, ndm)
     gsamp = ndm * g.out_nsamps * g.nactive / 1e9
     print(json.dumps({"ndm": ndm, "nchans": a.nchans, "nbits": a.nbits, "out_nsamps": g.out_nsamps,
-                      "total_ms": {"mfma": tot["m"], "valu": tot["v"], "auto": tot["auto"],
-                                   "auto_whole_list": tot["auto_whole"], "valu_whole_list": tot["valu_whole"]},
+                      "total_ms": {"mfma": tot["m"], "valu": tot["v"], "packed2": tot.get("p"), "auto": tot["auto"],
+                                   "auto_whole_list": tot["auto_whole"], "valu_whole_list": tot["valu_whole"],
+                                   "packed2_whole_list": tot.get("packed2_whole")},
                       "mfma_lds_split_dm_index": tot["split_dm"],
                       "G_chan_samples_per_s": {k: round(gsamp / (v * 1e-3), 1) for k, v in
-                                               (("mfma", tot["m"]), ("valu", tot["v"]), ("auto", tot["auto"]))}}))
+                                               (("mfma", tot["m"]), ("valu", tot["v"]), ("packed2", tot.get("p")),
+                                                ("auto", tot["auto"])) if v}}))
 
 
 if __name__ == "__main__":
