@@ -410,12 +410,13 @@ static double mfma_lds_ratio(bool packed2) {
   // MFMA kernel in Auto (each step is 2 x 16-shift blocks of one-hot GEMM;
   // the VALU kernels cost the same per channel whatever the spread).
   // Measured crossover on MI355X vs the byte kernel (profiles/r3_dedisp):
-  // ~2.35 steps/channel; vs the 2-bit kernel: PSOUP_MFMA_LDS_RATIO_2BIT
-  // (tools/dedisp_bench.py sweeps it)
+  // ~2.35 steps/channel; vs the 2-bit kernel none (1.11 vs 1.38 ms per
+  // 32-DM chunk at DM 0, 1024 ch x 2^20, profiles/r5_dedisp); override with
+  // PSOUP_MFMA_LDS_RATIO_2BIT
   if (packed2) {
     static const double r2 = [] {
       const char* e = std::getenv("PSOUP_MFMA_LDS_RATIO_2BIT");
-      return e ? std::atof(e) : 2.3;
+      return e ? std::atof(e) : 0.0;  // the 2-bit kernel won every 32-DM chunk of the config-4 list
     }();
     return r2;
   }
@@ -1116,8 +1117,7 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
     uint32_t n = 0;
     PSOUP_HIP_CHECK(hipMemcpyAsync(&n, s.d_count.data(), 4, hipMemcpyDeviceToHost, stream_));
     PSOUP_HIP_CHECK(hipStreamSynchronize(stream_));
-    n = std::min(n, cap_);
-    if (n >= static_cast<uint32_t>(mn ? std::atoi(mn) : 1) && !dumped.exchange(true)) {
+    if (n <= cap_ && n >= static_cast<uint32_t>(mn ? std::atoi(mn) : 1) && !dumped.exchange(true)) {
       std::vector<kern::PeakRecord> h(n);
       PSOUP_HIP_CHECK(hipMemcpy(h.data(), s.d_peaks.data(), n * sizeof(kern::PeakRecord), hipMemcpyDeviceToHost));
       if (FILE* f = std::fopen(dump, "wb")) {

@@ -75,31 +75,37 @@ def test_dedisperse_direct_mfma_valu_bit_exact(C, nbits, nchans, kill):
         assert np.array_equal(o.view(5, stride)[:, : g.out_nsamps].cpu().numpy(), exp[3:8]), k
 
 
-def test_dedisperse_1024ch_hybrid_mfma_bit_exact(C):
+@pytest.mark.parametrize("nbits", [2, 4])
+def test_dedisperse_1024ch_hybrid_mfma_bit_exact(C, nbits):
     """Config-4 geometry (1024 channels, 64 us, 1550 MHz - 400 MHz), 2^18
     output samples, 7 DM tiles from DM 0 to high DM: the LDS-fed one-hot MFMA
-    kernel (low-spread tiles), the VALU kernels and Auto's hybrid split all
-    equal the direct kernel byte for byte."""
+    kernel (low-spread tiles), the VALU kernels (byte and, for 2-bit data,
+    packed 2-bit) and Auto (4-bit data: the MFMA / VALU hybrid split; 2-bit:
+    the packed kernel throughout) all equal the direct kernel byte for byte."""
     rng = np.random.default_rng(21)
     nchans, tsamp, fch1, foff = 1024, 64e-6, 1550.0, -400.0 / 1024
     dms = C.generate_dm_list(0.0, 300.0, tsamp, 64.0, fch1, foff, nchans, 1.25)
     ndm = 320  # the first 10 tiles: ~2.1 -> 2.9 MFMA steps per channel (window-fitting to tile 10)
     delays = C.generate_delay_table(nchans, tsamp, fch1, foff)
     nsamps = (1 << 18) + C.compute_max_delay(dms, delays)
-    hdr = synthetic.make_header(nchans=nchans, nbits=2, tsamp=tsamp, fch1=fch1, foff=foff, nsamples=nsamps)
+    hdr = synthetic.make_header(nchans=nchans, nbits=nbits, tsamp=tsamp, fch1=fch1, foff=foff, nsamples=nsamps)
     killmask = [int(rng.random() > 0.05) for _ in range(nchans)]
     g = C.DedispGeometry.make(hdr, nsamps, dms, killmask)
     s = torch.cuda.current_stream().cuda_stream
     dfb = C.DeviceFilterbank(g, s)
-    packed = torch.randint(0, 256, (nsamps * nchans * 2 // 8,), dtype=torch.uint8, device=dev)
+    packed = torch.randint(0, 256, (nsamps * nchans * nbits // 8,), dtype=torch.uint8, device=dev)
     dfb.load_packed_device(packed.data_ptr())
     dd = C.Dedisperser(dfb, s)
     split = dd.mfma_lds_split(0, ndm)
-    assert 0 < split < ndm and split % 32 == 0, split  # both kernels run in Auto
+    if nbits == 4:
+        assert 0 < split < ndm and split % 32 == 0, split  # both kernels run in Auto
+    else:
+        assert split == 0, split  # the packed 2-bit kernel beats the MFMA one at every spread
+        split = 96  # (the LDS-fed MFMA kernel's leading tiles, run explicitly below)
     assert dd.mfma_lds_split(0, 8) == 0  # an 8-DM partial tile: the VALU kernel (MFMA computes all 32 DMs)
     stride = C.Dedisperser.row_stride(g.out_nsamps)
     outs = {}
-    P2 = C.DedispKernel.Packed2
+    P2 = C.DedispKernel.Packed2 if nbits == 2 else C.DedispKernel.Valu
     for k in (C.DedispKernel.Direct, C.DedispKernel.Mfma, C.DedispKernel.Valu, C.DedispKernel.Auto, P2):
         o = torch.zeros(ndm * stride, dtype=torch.uint8, device=dev)
         dd.run(0, ndm, o.data_ptr(), stride, k)
