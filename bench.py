@@ -72,6 +72,9 @@ def parse():
     p.add_argument("--serial-merge", action="store_true",
                    help="run each step's candidate gather + global distillation before the next step's "
                         "candidates are collected (default: on a worker thread, overlapped)")
+    p.add_argument("--serial-steps", action="store_true",
+                   help="each step a separate search() call (no overlap of a step's dedispersion and searches "
+                        "with the previous step's collection; A/B of the step pipeline)")
     p.add_argument("--as-rank", default="",
                    help="N:r[,r...] -- on one GPU, time rank r's shard of a world-N run (the DM list of N ranks, "
                         "shard [r*dms, (r+1)*dms)), one JSON line per r: checks that every rank's step costs the same")
@@ -210,6 +213,13 @@ def main() -> int:
     def run_steps(nsteps):
         out, acc, got = [], _C.CandidateBag(), 0
         t = time.perf_counter()
+        if a.serial_steps:
+            for _ in range(nsteps):
+                local = rs.search(blocks=step_blocks)
+                phase["search"] += time.perf_counter() - t
+                out.append(merger.submit(merge, local) if merger else merge(local))
+                t = time.perf_counter()
+            return out
         for _, bag in rs.search_iter(blocks=step_blocks * nsteps):
             acc.extend(bag)
             got += 1
@@ -284,7 +294,7 @@ def main() -> int:
                 "search_s_per_step": round(phase["search"] / a.steps, 4),
                 "merge_s_per_step": round(phase["merge"] / a.steps, 4),
                 "merge_overlapped": not a.serial_merge,
-                "steps_pipelined": True,
+                "steps_pipelined": not a.serial_steps,
                 "merge_split_s": {k: round(phase[k] / a.steps, 4) for k in ("ser", "gather", "gds")},
                 "candidate_blob_bytes": phase.get("blob_bytes", 0),
                 "accel_s_per_step": round(ctr.get("accel_s", 0) / a.steps, 4),

@@ -248,7 +248,12 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
   float* const ksnr = reinterpret_cast<float*>(kmem + CAP + 2 * kPad);
   uint2* const key = reinterpret_cast<uint2*>(kmem);  // radix keys (first idx, chunk)
   const int t = threadIdx.x;
-  const uint32_t seg = blockIdx.x;
+  // workgroups go round-robin over the 8 XCDs and the segment ids are trial
+  // x 8 + level, so blockIdx = segment would put every trial's level-h segment
+  // on XCD h (the big high levels of a peak-heavy batch on 2 of 8 XCDs): XCD
+  // x takes the contiguous eighth x of the segments instead (all levels)
+  const uint32_t nseg = gridDim.x;
+  const uint32_t seg = (nseg & 7u) == 0 ? (blockIdx.x & 7u) * (nseg >> 3) + (blockIdx.x >> 3) : blockIdx.x;
   const uint32_t n = segcnt[seg];                        // crossings
   const uint32_t m = segdcnt[seg], doff = segdoff[seg];  // chunks
   const uint4* dsc = desc + doff;
