@@ -1009,6 +1009,77 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
       return p[b];
     }
   };
+  // (levels <= 3 from P: two bin groups per round, all their 2 x 2^NLEV
+  // loads issued before the first sum -- one memory round trip per pair of
+  // groups on peak-heavy tiles, where most groups have candidates)
+  auto level_out = [&](const float (&sum)[NLEV + 1], int i, bool cand, bool (&pred)[NLEV + 1],
+                       float (&o)[NLEV + 1]) {
+#pragma unroll
+    for (int h = 0; h <= NLEV; ++h) {
+      if (h == 2)
+        o[h] = sum[h] * 0.5f;
+      else if (h == 4)
+        o[h] = sum[h] * 0.25f;
+      else
+        o[h] = h == 0 ? sum[0] : static_cast<float>(static_cast<double>(sum[h]) * c_level_scale[h]);
+      const bool in_range = inner | ((i >= hp.start[h]) & (i < hp.end[h]));
+      pred[h] = cand & in_range & (o[h] > thr);
+    }
+  };
+  if constexpr (!FROMX && NLEV <= 3 && BPT % 2 == 0) {
+    constexpr int NT = 1 << NLEV;  // terms per bin
+#pragma unroll 1
+    for (int u = 0; u < BPT; u += 2) {
+      const bool c0 = (cm >> u) & 1u, c1 = (cm >> (u + 1)) & 1u;
+      if (__ballot(c0 | c1) == 0ull) continue;
+      float tv[2][NT];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int i = i0 + (u + e) * 256;
+        const bool c = e ? c1 : c0;
+        // reference order: the fundamental, 1/2, then 3/4 before 1/4, then m/8 ascending
+        int b[NT];
+        b[0] = i;
+        if constexpr (NLEV >= 1) b[1] = (i + 1) >> 1;
+        if constexpr (NLEV >= 2) {
+          b[2] = (i * 3 + 2) >> 2;
+          b[3] = (i + 2) >> 2;
+        }
+        if constexpr (NLEV >= 3) {
+#pragma unroll
+          for (int m = 1; m < 8; m += 2) b[4 + m / 2] = (i * m + 4) >> 3;
+        }
+#pragma unroll
+        for (int q = 0; q < NT; ++q) tv[e][q] = c ? pv(b[q]) : 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int i = i0 + (u + e) * 256;
+        float sum[NLEV + 1];
+        float val = tv[e][0];
+        sum[0] = val;
+        if constexpr (NLEV >= 1) {
+          val += tv[e][1];
+          sum[1] = val;
+        }
+        if constexpr (NLEV >= 2) {
+          val += tv[e][2];
+          val += tv[e][3];
+          sum[2] = val;
+        }
+        if constexpr (NLEV >= 3) {
+#pragma unroll
+          for (int q = 4; q < 8; ++q) val += tv[e][q];
+          sum[3] = val;
+        }
+        bool pred[NLEV + 1];
+        float o[NLEV + 1];
+        level_out(sum, i, e ? c1 : c0, pred, o);
+        emit_levels<NLEV + 1>(pred, 0, NLEV, seg0, i, o, out, count, hp.capacity);
+      }
+    }
+    return;
+  }
 #pragma unroll 1
   for (int u = 0; u < BPT; ++u) {
     const bool cand = (cm >> u) & 1u;
