@@ -622,8 +622,15 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
   const uint32_t nn = static_cast<uint32_t>(n);
   float2* tws = lds + C::NBUF * C::BUF;
   static_assert(onex_g(L) == G, "one-exchange twiddle table shape");
-  for (int e = t; e < 8 * G; e += C::THREADS)  // rows c0 .. c0 + 7 of the ox table (first barrier: the exchange)
-    tws[(e / G) * (G + 1) + (e % G)] = tab[to.ox + static_cast<uint64_t>(c0) * G + e];
+  // rows c0 .. c0 + 7 of the ox table: loaded first, written to LDS only
+  // after the input loads are issued (a store here would wait for its load --
+  // a whole memory round trip -- before the first input load goes out);
+  // visible to every thread after the exchange's first barrier
+  static_assert((8 * G) % C::THREADS == 0, "ox rows per thread");
+  constexpr int kTw = 8 * G / C::THREADS;
+  float2 twv[kTw];
+#pragma unroll
+  for (int q = 0; q < kTw; ++q) twv[q] = tab[to.ox + static_cast<uint64_t>(c0) * G + t + q * C::THREADS];
   const float afl = static_cast<float>(af), sizef = static_cast<float>(n);
   // fp32 shift estimate: |af p (p - n)| <= |af| n^2 / 4 with < 2.4e-7 relative
   // error; exact float positions need n <= 2^24
@@ -685,6 +692,11 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
         }
       }
     }
+  }
+#pragma unroll
+  for (int q = 0; q < kTw; ++q) {
+    const int e = t + q * C::THREADS;
+    tws[(e / G) * (G + 1) + (e % G)] = twv[q];
   }
   const int rc = (lane >> 3) & 7;
   float2 u[C::NPAIR][G];
