@@ -277,6 +277,10 @@ struct SpecOut {
   const float* stats = nullptr;
   const uint32_t* tsrc = nullptr;
   float nscale = 1.f;
+  // bins [0, nbins) are written (whole 4-bin groups; 0: all M + 1): the
+  // search reads none above its highest bin (14% of the spectrum at 2^23 x
+  // 64 us, 1100 Hz), so the rest of P and Q is neither formed nor stored
+  uint32_t nbins = 0;
 };
 // Position of bin b (0 <= b <= M = n1 << log2_n2) in the blocked P: rows
 // r = b mod n2 in [1, n2/2] at ((2v) n1 + k1) 4 + j with v = (r-1)/4, j = (r-1)%4;

@@ -948,11 +948,17 @@ fft4_rowpass_spectrum_kernel(const float2* __restrict__ Y, int K, Fft4Geom g, co
   // values doubles the amplitude, so P = (amp2 - 2 mean) / (2 sigma) rounds
   // exactly as (amp - mean) / sigma.
   const float mean2 = 2.0f * mean, sigma2 = 2.0f * sigma, rsig2 = 0.5f * rsig;
+  const uint32_t nb = o.nbins ? o.nbins : M + 1;  // bins the search reads
 #pragma unroll
   for (int q = 0; q < kPts; ++q) {
     // (one iteration at a time: interleaving them raised the register peak into scratch spills)
     __builtin_amdgcn_sched_barrier(0);
     const uint32_t k1 = tt + q * T;
+    // forward bins n2 k1 + fr + 1 .. + 4, mirror bins M - n2 k1 - fr - 3 .. M - n2 k1 - fr:
+    // formed and stored only below nb (lanes of a wave share k1's high bits:
+    // whole waves skip)
+    const bool wf = n2 * k1 + fr + 1 < nb, wm = M - n2 * k1 - fr - 3 < nb;
+    if (!(wf | wm)) continue;
     const float2 hk = q == 0 ? ht : cmul(ht, make_float2(kCos16[q], -kSin16[q]));  // e^{-i pi k1 / L}
     float2 X[NP], Xm[NP];
 #pragma unroll
@@ -979,8 +985,8 @@ fft4_rowpass_spectrum_kernel(const float2* __restrict__ Y, int K, Fft4Geom g, co
       pp[j] = dev::div_rn(amp(X[j + 1], X[j]) - mean2, sigma2, rsig2);
       pm[j] = dev::div_rn(amp(Xm[j], Xm[j + 1]) - mean2, sigma2, rsig2);
     }
-    pk[2 * v * L + k1] = make_float4(pp[0], pp[1], pp[2], pp[3]);
-    pk[(2 * v + 1) * L + k1] = make_float4(pm[0], pm[1], pm[2], pm[3]);
+    if (wf) pk[2 * v * L + k1] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    if (wm) pk[(2 * v + 1) * L + k1] = make_float4(pm[0], pm[1], pm[2], pm[3]);
     // screening bytes (dev::q8): t = rint(4 p) + 127 -> t in [0, 253] as is,
     // >= 254 or NaN -> 254, <= -1 -> 255 (min first: NaN -> 254)
     auto qb = [](float p) {
@@ -989,8 +995,8 @@ fft4_rowpass_spectrum_kernel(const float2* __restrict__ Y, int K, Fft4Geom g, co
     };
     const uint32_t qa = qb(pp[0]) | (qb(pp[1]) << 8) | (qb(pp[2]) << 16) | (qb(pp[3]) << 24);
     const uint32_t qm = qb(pm[3]) | (qb(pm[2]) << 8) | (qb(pm[1]) << 16) | (qb(pm[0]) << 24);
-    *reinterpret_cast<uint32_t*>(qk + fr + 1 + n2 * k1) = qa;        // bins fr+1 .. fr+4 (+ n2 k1)
-    *reinterpret_cast<uint32_t*>(qk + (M - n2 * k1 - fr - 3)) = qm;  // bins M - n2 k1 - (fr+3 .. fr)
+    if (wf) *reinterpret_cast<uint32_t*>(qk + fr + 1 + n2 * k1) = qa;        // bins fr+1 .. fr+4 (+ n2 k1)
+    if (wm) *reinterpret_cast<uint32_t*>(qk + (M - n2 * k1 - fr - 3)) = qm;  // bins M - n2 k1 - (fr+3 .. fr)
     if (v == 0 && k1 == 0) {  // bin 0: X[-1] = 0 (bin_interbin)
       const float p0 = dev::div_rn(amp(X[0], make_float2(0.f, 0.f)) - mean2, sigma2, rsig2);
       o.P[static_cast<uint64_t>(k) * o.pstride + M] = p0;

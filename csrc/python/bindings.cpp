@@ -752,8 +752,9 @@ PYBIND11_MODULE(_C, m) {
   k.def(
       "fft4_rowpass_spectrum",
       [](uintptr_t Y, int K, const kern::Fft4Geom& g, uintptr_t tab, uintptr_t Pout, uint64_t pstride, uintptr_t q,
-         uint64_t qstride, uintptr_t stats, float nscale, uintptr_t s, uintptr_t tsrc) {
+         uint64_t qstride, uintptr_t stats, float nscale, uintptr_t s, uintptr_t tsrc, uint32_t nbins) {
         kern::SpecOut o;
+        o.nbins = nbins;
         o.P = P<float>(Pout);
         o.pstride = pstride;
         o.Q = P<uint8_t>(q);
@@ -764,7 +765,8 @@ PYBIND11_MODULE(_C, m) {
         kern::fft4_rowpass_spectrum(P<const float2>(Y), K, g, P<const float2>(tab), o, S(s));
       },
       py::arg("Y"), py::arg("K"), py::arg("g"), py::arg("tab"), py::arg("P"), py::arg("pstride"), py::arg("q"),
-      py::arg("qstride"), py::arg("stats"), py::arg("nscale"), py::arg("s"), py::arg("tsrc") = 0);
+      py::arg("qstride"), py::arg("stats"), py::arg("nscale"), py::arg("s"), py::arg("tsrc") = 0,
+      py::arg("nbins") = 0);
   k.attr("spec_q_shift") = kern::kSpecQShift;
   k.def("spec_pblk_index", &kern::spec_pblk_index);
   k.def("r2c_tiled_row_blocks", &kern::r2c_tiled_row_blocks);

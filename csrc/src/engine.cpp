@@ -1043,6 +1043,7 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
         so.stats = wstats_.data();
         so.tsrc = src;
         so.nscale = static_cast<float>(n_);
+        so.nbins = static_cast<uint32_t>(hi_);  // the harmonic sum reads no bin at or above hi_
         kern::fft4_rowpass_spectrum(Y, c, g, f4_tab_.data(), so, st);
         fx.pblk = 1;
         fx.qshift = kern::kSpecQShift;

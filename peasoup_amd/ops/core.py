@@ -290,7 +290,7 @@ def fft4_resample_interbin(x: torch.Tensor, accels: Sequence[float], tsamp: floa
 
 
 def fft4_spectrum_pass(x: torch.Tensor, accels: Sequence[float], tsamp: float, stats: torch.Tensor,
-                       nscale: float, pair_y: bool | None = None):
+                       nscale: float, pair_y: bool | None = None, nbins: int = 0):
     """The search hot path with the fused spectrum pass (the default engine
     path): fused resample + pass A, then pass B forming the normalised
     interbinned spectrum and its screening bytes directly
@@ -298,7 +298,8 @@ def fft4_spectrum_pass(x: torch.Tensor, accels: Sequence[float], tsamp: float, s
     in the blocked layout (``spec_unblock`` gives natural order), Q [K,
     qstride] uint8 with bin b at column ``spec_q_shift`` + b.  ``pair_y``:
     pass A hands over Y in row pairs (default: where ``fft4_pair_y`` allows,
-    as the search engine does)."""
+    as the search engine does).  ``nbins`` > 0: only bins below it are
+    written (whole 4-bin groups; the rest of Pb / Q keeps its zeros)."""
     _check(x, torch.float32, "x")
     n = x.numel()
     g = K.fft4_geometry(n // 2)
@@ -318,7 +319,7 @@ def fft4_spectrum_pass(x: torch.Tensor, accels: Sequence[float], tsamp: float, s
     Pb = torch.zeros((Kb, pst), dtype=torch.float32, device=x.device)
     Q = torch.zeros((Kb, qst), dtype=torch.uint8, device=x.device)
     K.fft4_rowpass_spectrum(Y.data_ptr(), Kb, g, tab.data_ptr(), Pb.data_ptr(), pst, Q.data_ptr(), qst,
-                            stats.data_ptr(), float(nscale), _s())
+                            stats.data_ptr(), float(nscale), _s(), 0, int(nbins))
     return Pb, Q, g
 
 

@@ -66,6 +66,15 @@ def test_spectrum_pass_matches_unfused(log2n):
     Pt, Qt, gt = ops.fft4_spectrum_pass(x, accs, 64e-6, st, float(n), pair_y=False)
     assert not gt.ypair
     assert torch.equal(Pt, Pb) and torch.equal(Qt, Q)
+    # only the searched bins (the engine passes its highest bin): those equal
+    # the full pass, nothing at or above the 4-bin group holding the bound
+    nb = int(0.14 * M) + 3
+    Ps, Qs, _ = ops.fft4_spectrum_pass(x, accs, 64e-6, st, float(n), nbins=nb)
+    Pns = ops.spec_unblock(Ps, g).cpu().numpy()
+    assert np.array_equal(Pns[:, :nb], Pn[:, :nb])
+    assert np.array_equal(Qs.cpu().numpy()[:, sh:sh + nb], Q.cpu().numpy()[:, sh:sh + nb])
+    hi_ = (nb + 3) // 4 * 4 + 4
+    assert not Pns[:, hi_:M].any() and not Qs.cpu().numpy()[:, sh + hi_:sh + M].any()
 
 
 def test_spec_pblk_index_native_equals_python():
