@@ -278,8 +278,10 @@ struct SpecOut {
   const uint32_t* tsrc = nullptr;
   float nscale = 1.f;
   // bins [0, nbins) are written (whole 4-bin groups; 0: all M + 1): the
-  // search reads none above its highest bin (14% of the spectrum at 2^23 x
-  // 64 us, 1100 Hz), so the rest of P and Q is neither formed nor stored
+  // search reads none at or above its highest harmonic bin (max_freq x
+  // 2^nlevels: below M only for few harmonics -- 1100 Hz at 2^23 x 64 us is
+  // 14% of the spectrum per harmonic doubling), so the rest of P and Q is
+  // neither formed nor stored
   uint32_t nbins = 0;
 };
 // Position of bin b (0 <= b <= M = n1 << log2_n2) in the blocked P: rows

@@ -66,7 +66,7 @@ def test_spectrum_pass_matches_unfused(log2n):
     Pt, Qt, gt = ops.fft4_spectrum_pass(x, accs, 64e-6, st, float(n), pair_y=False)
     assert not gt.ypair
     assert torch.equal(Pt, Pb) and torch.equal(Qt, Q)
-    # only the searched bins (the engine passes its highest bin): those equal
+    # only the searched bins (the engine passes its highest harmonic bin): those equal
     # the full pass, nothing at or above the 4-bin group holding the bound
     nb = int(0.14 * M) + 3
     Ps, Qs, _ = ops.fft4_spectrum_pass(x, accs, 64e-6, st, float(n), nbins=nb)
