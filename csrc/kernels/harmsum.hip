@@ -1250,7 +1250,9 @@ namespace {
 // recomputed from the spectrum X (unfused engines); bit 5: the fp32 3-level
 // kernel in two staging phases; bit 6: the engine's fused spectrum pass
 // (fft4_rowpass_spectrum: pass B writes P and Q, no X and no r2c pass);
-// bits 8-15: dynamic-LDS occupancy cap in KiB of the two-phase kernel.
+// bits 8-15: dynamic-LDS occupancy cap in KiB of the two-phase kernel;
+// bit 16: the screened kernel up to 3 levels with 16 bins per thread (a
+// 4096-bin tile: twice the staging per workgroup in flight).
 // Engines read bits 2, 3 and 6 when they are built.
 int g_harm_flags = 1 | 8 | 32 | 64 | (10 << 8);
 
@@ -1517,8 +1519,8 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
         src = 1;
       }
     }
-    auto oneq = [&](auto nl_c) {
-      constexpr int NL = decltype(nl_c)::value, BP = NL <= 3 ? 8 : 4;
+    auto oneq_bp = [&](auto nl_c, auto bp_c) {
+      constexpr int NL = decltype(nl_c)::value, BP = decltype(bp_c)::value;
       const int nt = ntiles_of(HarmTileQ<NL, BP>::B);
       PSOUP_CHECK(static_cast<int64_t>(nt) * K < (int64_t(1) << 31), "harmonic grid too large");
       const dim3 grid(static_cast<unsigned>(nt * K));
@@ -1531,6 +1533,18 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
       else
         harmonic_peaks_q8_kernel<NL, BP, 0><<<grid, 256, 0, s>>>(P, pstride, Q, qstride, lo, hi, hp, out, count, nt,
                                                                  xcd, lim, fxv);
+    };
+    // bins per thread: 8 up to 3 levels (16 with flag bit 16), else 4
+    auto oneq = [&](auto nl_c) {
+      constexpr int NL = decltype(nl_c)::value;
+      if constexpr (NL <= 3) {
+        if (g_harm_flags & 65536)
+          oneq_bp(nl_c, std::integral_constant<int, 16>{});
+        else
+          oneq_bp(nl_c, std::integral_constant<int, 8>{});
+      } else {
+        oneq_bp(nl_c, std::integral_constant<int, 4>{});
+      }
     };
     switch (hp.nlevels) {
       case 0: oneq(std::integral_constant<int, 0>{}); break;

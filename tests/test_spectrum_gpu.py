@@ -106,7 +106,15 @@ def test_screened_sum_on_blocked_spectrum(log2n, nlev, thresh):
     starts = [3, 5, 9, 17, 33, 65]
     ends = [M + 1, M - 7, M + 1, M - 100, M + 1, M + 1]
     a = ops.harmonic_peaks(Pn, nlev, starts, ends, thresh)
-    b = ops.harmonic_peaks(Pb, nlev, starts, ends, thresh, nbins=M + 1, Q=Q, pblk=g)
     ra = sorted(zip(*[t.tolist() for t in a]))
-    rb = sorted(zip(*[t.tolist() for t in b]))
-    assert ra == rb and len(ra) > 20, (len(ra), len(rb))
+    import peasoup_amd._C as C
+
+    old = C.kernels.harmonic_flags()
+    try:
+        for flags in (old, old ^ 65536):  # bit 16: the 16-bins-per-thread tile (up to 3 levels)
+            C.kernels.harmonic_set_flags(flags)
+            b = ops.harmonic_peaks(Pb, nlev, starts, ends, thresh, nbins=M + 1, Q=Q, pblk=g)
+            rb = sorted(zip(*[t.tolist() for t in b]))
+            assert ra == rb and len(ra) > 20, (flags, len(ra), len(rb))
+    finally:
+        C.kernels.harmonic_set_flags(old)
