@@ -1252,9 +1252,10 @@ namespace {
 // (fft4_rowpass_spectrum: pass B writes P and Q, no X and no r2c pass);
 // bits 8-15: dynamic-LDS occupancy cap in KiB of the two-phase kernel;
 // bit 16: the screened kernel up to 3 levels with 16 bins per thread (a
-// 4096-bin tile: twice the staging per workgroup in flight).
+// 4096-bin tile: twice the staging per workgroup in flight; bench +2.7% over
+// 8); bit 17: 32 bins per thread.
 // Engines read bits 2, 3 and 6 when they are built.
-int g_harm_flags = 1 | 8 | 32 | 64 | (10 << 8);
+int g_harm_flags = 1 | 8 | 32 | 64 | (10 << 8) | 65536;
 
 // Mixed-radix n = m p (p a power of two, m odd): gather of the m strided
 // columns, and the length-m combination with the twiddles W_n^(n1 k)
@@ -1538,7 +1539,9 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
     auto oneq = [&](auto nl_c) {
       constexpr int NL = decltype(nl_c)::value;
       if constexpr (NL <= 3) {
-        if (g_harm_flags & 65536)
+        if (g_harm_flags & 131072)
+          oneq_bp(nl_c, std::integral_constant<int, 32>{});
+        else if (g_harm_flags & 65536)
           oneq_bp(nl_c, std::integral_constant<int, 16>{});
         else
           oneq_bp(nl_c, std::integral_constant<int, 8>{});

@@ -50,8 +50,8 @@ def test_screened_harmonic_peaks_equal_exact(nlev, thresh):
     assert np.array_equal(Q.cpu().numpy()[:, :n], _q8_ref(P))
     old = C.kernels.harmonic_flags()
     try:
-        # bit 1: pre-threshold off (every bin takes the exact path); bit 16:
-        # 16 bins per thread (twice the tile) up to 3 levels
+        # bit 1: pre-threshold off (every bin takes the exact path); bit 16
+        # toggled: the other tile size up to 3 levels (8 / 16 bins per thread)
         for flags in (old, old | 2, old ^ 65536, (old ^ 65536) | 2):
             C.kernels.harmonic_set_flags(flags)
             a = _records(ops.harmonic_peaks(Pt, nlev, starts, ends, thresh))

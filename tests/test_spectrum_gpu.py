@@ -111,7 +111,7 @@ def test_screened_sum_on_blocked_spectrum(log2n, nlev, thresh):
 
     old = C.kernels.harmonic_flags()
     try:
-        for flags in (old, old ^ 65536):  # bit 16: the 16-bins-per-thread tile (up to 3 levels)
+        for flags in (old, old ^ 65536):  # bit 16 toggled: the other tile size (8 / 16 bins per thread, up to 3 levels)
             C.kernels.harmonic_set_flags(flags)
             b = ops.harmonic_peaks(Pb, nlev, starts, ends, thresh, nbins=M + 1, Q=Q, pblk=g)
             rb = sorted(zip(*[t.tolist() for t in b]))
