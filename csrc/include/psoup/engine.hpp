@@ -445,7 +445,7 @@ class SearchEngine {
   bool fromx_ = false;
   // harmonic flag 64 (default): pass B forms P_ (blocked) and Q_ itself
   // (kern::fft4_rowpass_spectrum); no spec_ and no r2c pass
-  bool fused_ = false, pnat_ = false;
+  bool fused_ = false;
   const float2* rt_ = nullptr;  // kern::r2c_twiddle_table(n_ / 2)
   uint64_t qst_ = 0;  // bytes per trial of Q_ (>= hi_, multiple of 64)
   DeviceBuffer<uint8_t> Q_;

@@ -269,7 +269,6 @@ void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const fl
 // Q[k*qstride + kSpecQShift + b].  Trial k normalises with stats + 4*tsrc[k]
 // (tsrc null: stats) scaled by nscale.
 constexpr int kSpecQShift = 15;
-constexpr int kSpecPShift = 3;  // natural P (SpecOut::pnat): bin b at row + 3 + b (16-byte aligned groups)
 struct SpecOut {
   float* P = nullptr;
   uint64_t pstride = 0;  // floats per trial, >= M + 1 (multiple of 4)
@@ -284,11 +283,6 @@ struct SpecOut {
   // 14% of the spectrum per harmonic doubling), so the rest of P and Q is
   // neither formed nor stored
   uint32_t nbins = 0;
-  // P in natural bin order (bin b at P[k*pstride + kSpecPShift + b], pstride
-  // >= M + 1 + kSpecPShift) instead of workgroup-blocked: every 4-bin group
-  // is one aligned 16-byte store; the exact sums of the screened harmonic
-  // sum then read 4x fewer lines per wave
-  int pnat = 0;
 };
 // Position of bin b (0 <= b <= M = n1 << log2_n2) in the blocked P: rows
 // r = b mod n2 in [1, n2/2] at ((2v) n1 + k1) 4 + j with v = (r-1)/4, j = (r-1)%4;
@@ -417,7 +411,7 @@ struct HarmParams {
 // screening bytes of bin b are at Q[k*qstride + fx->qshift + b].
 struct HarmFromX {
   int pblk = 0;
-  int qshift = 0;  // (with pblk = 0 and X = nullptr: P natural, Q rows shifted -- SpecOut::pnat)
+  int qshift = 0;
   const float2* X = nullptr;  // tiled pass-B spectra, trial k at X + k*xstride
   uint64_t xstride = 0;
   int log2_n2 = 0;

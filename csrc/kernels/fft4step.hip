@@ -931,7 +931,6 @@ fft4_rowpass_spectrum_kernel(const float2* __restrict__ Y, int K, Fft4Geom g, co
   for (int c = 0; c < NP; ++c) hr[c] = tab[to.hr + fr + c];
   const uint32_t M = static_cast<uint32_t>(L) * n2;
   float4* pk = reinterpret_cast<float4*>(o.P + static_cast<uint64_t>(k) * o.pstride);
-  float4* pn = pk;  // (natural layout: the same row, bins at kSpecPShift + b)
   uint8_t* qk = o.Q + static_cast<uint64_t>(k) * o.qstride + kSpecQShift;  // qk[b]: bin b
   // A fresh copy of t: without it the compiler keeps the load phase's per-q
   // indices alive across the FFT (spilled to scratch, and every reload then
@@ -986,15 +985,8 @@ fft4_rowpass_spectrum_kernel(const float2* __restrict__ Y, int K, Fft4Geom g, co
       pp[j] = dev::div_rn(amp(X[j + 1], X[j]) - mean2, sigma2, rsig2);
       pm[j] = dev::div_rn(amp(Xm[j], Xm[j + 1]) - mean2, sigma2, rsig2);
     }
-    if (o.pnat) {
-      // natural order, row shifted by kSpecPShift: bins fr+1 .. fr+4 (+ n2 k1)
-      // and M - n2 k1 - (fr+3 .. fr) are aligned 16-byte groups
-      if (wf) pn[(n2 * k1 + fr + 4) >> 2] = make_float4(pp[0], pp[1], pp[2], pp[3]);
-      if (wm) pn[(M - n2 * k1 - fr) >> 2] = make_float4(pm[3], pm[2], pm[1], pm[0]);
-    } else {
-      if (wf) pk[2 * v * L + k1] = make_float4(pp[0], pp[1], pp[2], pp[3]);
-      if (wm) pk[(2 * v + 1) * L + k1] = make_float4(pm[0], pm[1], pm[2], pm[3]);
-    }
+    if (wf) pk[2 * v * L + k1] = make_float4(pp[0], pp[1], pp[2], pp[3]);
+    if (wm) pk[(2 * v + 1) * L + k1] = make_float4(pm[0], pm[1], pm[2], pm[3]);
     // screening bytes (dev::q8): t = rint(4 p) + 127 -> t in [0, 253] as is,
     // >= 254 or NaN -> 254, <= -1 -> 255 (min first: NaN -> 254)
     auto qb = [](float p) {
@@ -1007,7 +999,7 @@ fft4_rowpass_spectrum_kernel(const float2* __restrict__ Y, int K, Fft4Geom g, co
     if (wm) *reinterpret_cast<uint32_t*>(qk + (M - n2 * k1 - fr - 3)) = qm;  // bins M - n2 k1 - (fr+3 .. fr)
     if (v == 0 && k1 == 0) {  // bin 0: X[-1] = 0 (bin_interbin)
       const float p0 = dev::div_rn(amp(X[0], make_float2(0.f, 0.f)) - mean2, sigma2, rsig2);
-      o.P[static_cast<uint64_t>(k) * o.pstride + (o.pnat ? kSpecPShift : M)] = p0;
+      o.P[static_cast<uint64_t>(k) * o.pstride + M] = p0;
       qk[0] = static_cast<uint8_t>(qb(p0));
     }
   }
@@ -1138,8 +1130,7 @@ void fft4_rowpass_spectrum(const float2* Y, int K, const Fft4Geom& g, const floa
   PSOUP_CHECK(M < (1ull << 31), "fft4 spectrum pass: spectrum too long for 32-bit bin indices");
   const int f = g_fft4_flags;
   PSOUP_CHECK((f & kFft4Blocked) && (f & kFft4TileY), "fft4 spectrum pass: needs the tiled Y layout");
-  PSOUP_CHECK(o.P && o.Q && o.stats && o.pstride >= M + 1 + (o.pnat ? kSpecPShift : 0) && o.pstride % 4 == 0 &&
-                  o.qstride >= M + 1 + kSpecQShift &&
+  PSOUP_CHECK(o.P && o.Q && o.stats && o.pstride >= M + 1 && o.pstride % 4 == 0 && o.qstride >= M + 1 + kSpecQShift &&
                   o.qstride % 16 == 0 && (reinterpret_cast<uintptr_t>(o.P) & 15) == 0 &&
                   (reinterpret_cast<uintptr_t>(o.Q) & 15) == 0 && (reinterpret_cast<uintptr_t>(Y) & 15) == 0,
               "fft4 spectrum pass: output layout");

@@ -1513,10 +1513,6 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
                         pstride >= M + 1,
                     "harmonic_peaks_batch: bad blocked spectrum");
         src = 2;
-      } else if (!fxv.X) {
-        // natural P (the caller passes the row start of bin 0), shifted Q
-        PSOUP_CHECK(P && pstride >= static_cast<uint64_t>(hi), "harmonic_peaks_batch: bad natural spectrum");
-        src = 0;
       } else {
         PSOUP_CHECK(fxv.X && fxv.rt && fxv.stats && fxv.n1 >= 16 && M < (uint64_t(1) << 31) &&
                         static_cast<uint64_t>(hi) <= M + 1,

@@ -752,10 +752,9 @@ PYBIND11_MODULE(_C, m) {
   k.def(
       "fft4_rowpass_spectrum",
       [](uintptr_t Y, int K, const kern::Fft4Geom& g, uintptr_t tab, uintptr_t Pout, uint64_t pstride, uintptr_t q,
-         uint64_t qstride, uintptr_t stats, float nscale, uintptr_t s, uintptr_t tsrc, uint32_t nbins, int pnat) {
+         uint64_t qstride, uintptr_t stats, float nscale, uintptr_t s, uintptr_t tsrc, uint32_t nbins) {
         kern::SpecOut o;
         o.nbins = nbins;
-        o.pnat = pnat;
         o.P = P<float>(Pout);
         o.pstride = pstride;
         o.Q = P<uint8_t>(q);
@@ -767,15 +766,14 @@ PYBIND11_MODULE(_C, m) {
       },
       py::arg("Y"), py::arg("K"), py::arg("g"), py::arg("tab"), py::arg("P"), py::arg("pstride"), py::arg("q"),
       py::arg("qstride"), py::arg("stats"), py::arg("nscale"), py::arg("s"), py::arg("tsrc") = 0,
-      py::arg("nbins") = 0, py::arg("pnat") = 0);
+      py::arg("nbins") = 0);
   k.attr("spec_q_shift") = kern::kSpecQShift;
-  k.attr("spec_p_shift") = kern::kSpecPShift;
   k.def("spec_pblk_index", &kern::spec_pblk_index);
   k.def("r2c_tiled_row_blocks", &kern::r2c_tiled_row_blocks);
   k.def("harmonic_peaks_batch", [](uintptr_t Pin, uint64_t nb, uint64_t pstride, int K, int nlevels,
                                    const std::vector<int>& start, const std::vector<int>& end, float thresh,
                                    uint32_t capacity, uintptr_t out, uintptr_t count, uintptr_t s, uintptr_t q,
-                                   uint64_t qstride, int pblk_log2_n2, uint32_t pblk_n1, int qshift, bool pnat) {
+                                   uint64_t qstride, int pblk_log2_n2, uint32_t pblk_n1, int qshift) {
     kern::HarmParams hp{};
     hp.nlevels = nlevels;
     for (int i = 0; i < 6; ++i) {
@@ -789,13 +787,12 @@ PYBIND11_MODULE(_C, m) {
     fx.log2_n2 = pblk_log2_n2;
     fx.n1 = pblk_n1;
     fx.qshift = qshift;
-    // pnat: P natural from Pin (bin 0's address), Q rows shifted by qshift
     kern::harmonic_peaks_batch(P<const float>(Pin), nb, pstride, K, hp, P<kern::PeakRecord>(out), P<uint32_t>(count),
-                               S(s), P<const uint8_t>(q), qstride, (pblk_n1 > 0 || pnat) ? &fx : nullptr);
+                               S(s), P<const uint8_t>(q), qstride, pblk_n1 > 0 ? &fx : nullptr);
   }, py::arg("P"), py::arg("nb"), py::arg("pstride"), py::arg("K"), py::arg("nlevels"), py::arg("start"),
      py::arg("end"), py::arg("thresh"), py::arg("capacity"), py::arg("out"), py::arg("count"), py::arg("s"),
      py::arg("q") = 0, py::arg("qstride") = 0, py::arg("pblk_log2_n2") = 0, py::arg("pblk_n1") = 0,
-     py::arg("qshift") = 0, py::arg("pnat") = false);
+     py::arg("qshift") = 0);
   k.def("peak_cluster_batch", [](uintptr_t peaks, uintptr_t count, uint32_t cap, uint32_t nseg, int gap,
                                  uintptr_t work, uintptr_t sorted, uintptr_t out, uintptr_t segtab, uintptr_t total,
                                  uintptr_t s) {

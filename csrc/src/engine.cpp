@@ -868,7 +868,6 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   q8_ = mode_ == 2 && kern::fft4_x_layout(f4_).tiled && !(kern::harmonic_flags() & 4);
   // the fused spectrum pass (harmonic flag 64) writes every bin 0..M of P (blocked) and Q
   fused_ = q8_ && (kern::harmonic_flags() & 64) && f4_.n2 >= 16 && f4_.n1 >= 128;
-  pnat_ = fused_ && (kern::harmonic_flags() & 262144);  // bit 18: P in natural order (SpecOut::pnat)
   fromx_ = q8_ && !fused_ && (kern::harmonic_flags() & 8);
   if (fused_) pst_ = (n_ / 2 + 1 + 63) / 64 * 64;
   qst_ = q8_ ? (pst_ + (fused_ ? kern::kSpecQShift : 0) + 63) / 64 * 64 : 0;
@@ -1045,18 +1044,15 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
         so.tsrc = src;
         so.nscale = static_cast<float>(n_);
         so.nbins = static_cast<uint32_t>(hi_);  // the harmonic sum reads no bin at or above hi_
-        so.pnat = pnat_ ? 1 : 0;
         kern::fft4_rowpass_spectrum(Y, c, g, f4_tab_.data(), so, st);
-        fx.pblk = pnat_ ? 0 : 1;
-        fx.X = nullptr;
+        fx.pblk = 1;
         fx.qshift = kern::kSpecQShift;
         fx.log2_n2 = ilog2(static_cast<uint64_t>(f4_.n2));
         fx.n1 = static_cast<uint32_t>(f4_.n1);
         RoctxRange r("Harmonic summing");
         kern::HarmParams hp = hp_;
         hp.trial_base = static_cast<uint32_t>(b);
-        kern::harmonic_peaks_batch(pnat_ ? P + kern::kSpecPShift : P, nb_, pst, c, hp, s.d_peaks.data(),
-                                   s.d_count.data(), st, Q, qst_, &fx);
+        kern::harmonic_peaks_batch(P, nb_, pst, c, hp, s.d_peaks.data(), s.d_count.data(), st, Q, qst_, &fx);
         return;
       }
       float2* X = spec_.data() + static_cast<uint64_t>(b) * xs_;

@@ -290,7 +290,7 @@ def fft4_resample_interbin(x: torch.Tensor, accels: Sequence[float], tsamp: floa
 
 
 def fft4_spectrum_pass(x: torch.Tensor, accels: Sequence[float], tsamp: float, stats: torch.Tensor,
-                       nscale: float, pair_y: bool | None = None, nbins: int = 0, pnat: bool = False):
+                       nscale: float, pair_y: bool | None = None, nbins: int = 0):
     """The search hot path with the fused spectrum pass (the default engine
     path): fused resample + pass A, then pass B forming the normalised
     interbinned spectrum and its screening bytes directly
@@ -299,8 +299,7 @@ def fft4_spectrum_pass(x: torch.Tensor, accels: Sequence[float], tsamp: float, s
     qstride] uint8 with bin b at column ``spec_q_shift`` + b.  ``pair_y``:
     pass A hands over Y in row pairs (default: where ``fft4_pair_y`` allows,
     as the search engine does).  ``nbins`` > 0: only bins below it are
-    written (whole 4-bin groups; the rest of Pb / Q keeps its zeros).
-    ``pnat``: P in natural order instead, bin b at column ``spec_p_shift`` + b."""
+    written (whole 4-bin groups; the rest of Pb / Q keeps its zeros)."""
     _check(x, torch.float32, "x")
     n = x.numel()
     g = K.fft4_geometry(n // 2)
@@ -315,12 +314,12 @@ def fft4_spectrum_pass(x: torch.Tensor, accels: Sequence[float], tsamp: float, s
     Y = torch.empty((Kb, g.ystride, 2), dtype=torch.float32, device=x.device)
     K.fft4_pad_input(x.data_ptr(), n, xp.data_ptr(), g, _s())
     K.fft4_resample_colpass(x.data_ptr(), xp.data_ptr(), n, af.data_ptr(), Kb, Y.data_ptr(), g, tab.data_ptr(), _s())
-    pst = (M + 1 + K.spec_p_shift + 63) // 64 * 64
+    pst = (M + 1 + 63) // 64 * 64
     qst = (M + 1 + K.spec_q_shift + 63) // 64 * 64
     Pb = torch.zeros((Kb, pst), dtype=torch.float32, device=x.device)
     Q = torch.zeros((Kb, qst), dtype=torch.uint8, device=x.device)
     K.fft4_rowpass_spectrum(Y.data_ptr(), Kb, g, tab.data_ptr(), Pb.data_ptr(), pst, Q.data_ptr(), qst,
-                            stats.data_ptr(), float(nscale), _s(), 0, int(nbins), int(bool(pnat)))
+                            stats.data_ptr(), float(nscale), _s(), 0, int(nbins))
     return Pb, Q, g
 
 
@@ -375,7 +374,7 @@ def quantize_q8(P: torch.Tensor) -> torch.Tensor:
 
 def harmonic_peaks(P: torch.Tensor, nlevels: int, starts: Sequence[int], ends: Sequence[int], thresh: float,
                    capacity: int = 1 << 20, nbins: int | None = None, Q: torch.Tensor | None = None,
-                   pblk=None, pnat: bool = False):
+                   pblk=None):
     """Fused harmonic sum + threshold: P [K, n] -> records (trial, level, idx, snr)
     as int64/float32 tensors sorted by (trial, level, idx) (the kernel's chunk
     descriptors, kernels.hpp kPeakChunk, are dropped).  ``nbins``: bins per
@@ -383,9 +382,7 @@ def harmonic_peaks(P: torch.Tensor, nlevels: int, starts: Sequence[int], ends: S
     P ([K, qstride] uint8, ``quantize_q8``) -- the screened kernel, same
     records.  ``pblk`` = the geometry ``g`` of ``fft4_spectrum_pass``: P is
     its blocked spectrum and Q its screening rows (bins shifted by
-    ``spec_q_shift``).  ``pnat``: P is the natural spectrum of
-    ``fft4_spectrum_pass(pnat=True)`` (bin b at column ``spec_p_shift`` + b of
-    the padded rows) with its shifted screening rows."""
+    ``spec_q_shift``)."""
     _check(P, torch.float32, "P")
     Kb, n = P.shape
     rec = torch.empty((capacity, 3), dtype=torch.int32, device=P.device)
@@ -395,19 +392,14 @@ def harmonic_peaks(P: torch.Tensor, nlevels: int, starts: Sequence[int], ends: S
         if Q.dtype != torch.uint8 or Q.shape[0] != Kb or not Q.is_contiguous():
             raise ValueError("Q must be a contiguous [K, qstride] uint8 tensor")
     extra = {}
-    base = P.data_ptr()
     if pblk is not None:
         extra = dict(pblk_log2_n2=pblk.log2_xrow, pblk_n1=pblk.n1, qshift=K.spec_q_shift)
-    elif pnat:
-        extra = dict(qshift=K.spec_q_shift, pnat=True)
-        base += 4 * K.spec_p_shift
-    K.harmonic_peaks_batch(base, nb, n, Kb, nlevels, list(starts), list(ends), float(thresh), capacity,
+    K.harmonic_peaks_batch(P.data_ptr(), nb, n, Kb, nlevels, list(starts), list(ends), float(thresh), capacity,
                            rec.data_ptr(), cnt.data_ptr(), _s(), 0 if Q is None else Q.data_ptr(),
                            0 if Q is None else Q.shape[1], **extra)
     c = int(cnt.item())
     if c > capacity:
-        return harmonic_peaks(P, nlevels, starts, ends, thresh, capacity=c + 1024, nbins=nbins, Q=Q, pblk=pblk,
-                              pnat=pnat)
+        return harmonic_peaks(P, nlevels, starts, ends, thresh, capacity=c + 1024, nbins=nbins, Q=Q, pblk=pblk)
     r = rec[:c]
     r = r[r[:, 0] >= 0]  # drop the chunk descriptors (seg field with kPeakChunk, bit 31, set)
     seg = r[:, 0].to(torch.int64)

@@ -89,8 +89,7 @@ def test_engine_screen_equals_exact():
     sum, without it (harmonic flag 4) and with the exact sums recomputed from
     the spectrum instead of a stored P (flag 8) gives identical candidates;
     the fused spectrum pass (flag 64, the default) the same candidates with
-    S/N equal to FFT rounding (its mirror bins come from another transform),
-    in either P layout (flag 262144) exactly the same."""
+    S/N equal to FFT rounding (its mirror bins come from another transform)."""
     import peasoup_amd._C as C
 
     rng = np.random.default_rng(5)
@@ -105,9 +104,8 @@ def test_engine_screen_equals_exact():
     old = C.kernels.harmonic_flags()
     unf = old & ~64
     try:
-        # P stored / screen off / bins recomputed / fused (default) / fused
-        # with the other P layout (bit 18: natural order <-> blocked)
-        for flags in (unf & ~8, unf | 4, unf | 8, old | 64, (old | 64) ^ 262144):
+        # P stored / screen off / bins recomputed / fused (default)
+        for flags in (unf & ~8, unf | 4, unf | 8, old | 64):
             C.kernels.harmonic_set_flags(flags)
             p = C.SearchParams()
             p.fft_size, p.tsamp, p.nharmonics = 1 << 21, 64e-6, 4
@@ -121,4 +119,3 @@ def test_engine_screen_equals_exact():
     ref = sorted(out[0], key=lambda r: (r[0], r[1], r[2], r[4]))
     assert [(r[0], r[1], r[2], r[4], r[5]) for r in fused] == [(r[0], r[1], r[2], r[4], r[5]) for r in ref]
     assert all(abs(a[3] - b[3]) <= 1e-4 * abs(b[3]) for a, b in zip(fused, ref))
-    assert out[4] == out[3]  # the P layout changes no value
