@@ -241,7 +241,6 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
   __shared__ uint16_t jmp[CAP > 2 * kCnt ? CAP : 2 * kCnt];  // sorted chunks, then next survivor / chain jumps
   __shared__ __attribute__((aligned(16))) uint8_t flag[CAP + 2 * kPad];  // at kPad + i: bit 0 survivor, 1 peak, 2 run start
   __shared__ uint32_t sc[kClThreads];
-  __shared__ uint32_t wcnt[kClThreads / 64];   // per wave: first survivor of the row
   __shared__ uint32_t rw[R * (kClThreads / 64)];  // per (row, wave): peak count, then its output offset
   __shared__ uint32_t base_s, lo_s, hi_s;
   uint32_t* const kidx = kmem;
@@ -454,24 +453,50 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
   }
   __syncthreads();
   if (CAP > kClSmall) cl_trace(3);
-  // ---- 3b. next survivor at or after every position: rows from the last, a
-  // row's waves from their ballots, the carry from the rows after it
-  uint32_t carry = n;
-  for (uint32_t r = nrow; r-- > 0;) {
+  // ---- 3b. next survivor at or after every position, with two barriers:
+  // the first survivor of every 64-position block (a wave's part of a row,
+  // block q = r kW + w covers positions 64 q ..), one wave's suffix minimum
+  // over the blocks, then each position from its own wave's ballot or the
+  // suffix of the blocks after its own
+  const uint32_t nblk = nrow * kW;
+  for (uint32_t r = 0; r < nrow; ++r) {
     const uint32_t i = r * kClThreads + t;
-    const bool sv = i < n && (flag[kPad + i] & 1);
-    const uint64_t mask = __ballot(sv);
-    if (lane == 0) wcnt[w] = mask ? r * kClThreads + w * 64 + static_cast<uint32_t>(__builtin_ctzll(mask)) : n;
-    __syncthreads();
-    uint32_t c = carry;
-    for (int v = static_cast<int>(kW) - 1; v > w; --v) c = wcnt[v] < n ? wcnt[v] : c;
-    const uint64_t ge = mask >> lane;
-    if (i < n) jmp[i] = static_cast<uint16_t>(ge ? i + static_cast<uint32_t>(__builtin_ctzll(ge)) : c);
-    uint32_t rowfirst = n;
-    for (uint32_t v = 0; v < kW; ++v) rowfirst = min(rowfirst, wcnt[v]);
-    carry = rowfirst < n ? rowfirst : carry;
-    __syncthreads();
+    const uint64_t mask = __ballot(i < n && (flag[kPad + i] & 1));
+    if (lane == 0) rw[r * kW + w] = mask ? r * kClThreads + w * 64 + static_cast<uint32_t>(__builtin_ctzll(mask)) : n;
   }
+  __syncthreads();
+  if (w == 0) {
+    constexpr uint32_t kPerB = (R * kW + 63) / 64;  // blocks per lane
+    uint32_t v[kPerB + 1];
+    v[kPerB] = n;
+#pragma unroll
+    for (int e = static_cast<int>(kPerB) - 1; e >= 0; --e) {
+      const uint32_t q = static_cast<uint32_t>(lane) * kPerB + static_cast<uint32_t>(e);
+      v[e] = min(q < nblk ? rw[q] : n, v[e + 1]);
+    }
+    uint32_t x = v[0];  // suffix minimum over the lanes from this one
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t y = __shfl_down(x, off, 64);
+      if (lane + off < 64) x = min(x, y);
+    }
+    uint32_t after = __shfl_down(x, 1, 64);  // the lanes after this one
+    if (lane == 63) after = n;
+#pragma unroll
+    for (uint32_t e = 0; e < kPerB; ++e) {
+      const uint32_t q = static_cast<uint32_t>(lane) * kPerB + e;
+      if (q < nblk) sc[q] = min(v[e], after);  // first survivor at or after block q
+    }
+  }
+  __syncthreads();
+  for (uint32_t r = 0; r < nrow; ++r) {
+    const uint32_t i = r * kClThreads + t;
+    const uint64_t ge = __ballot(i < n && (flag[kPad + i] & 1)) >> lane;
+    const uint32_t q = r * kW + w;
+    const uint32_t nxt = q + 1 < nblk ? sc[q + 1] : n;
+    if (i < n) jmp[i] = static_cast<uint16_t>(ge ? i + static_cast<uint32_t>(__builtin_ctzll(ge)) : nxt);
+  }
+  __syncthreads();
   if (CAP > kClSmall) cl_trace(4);
   // ---- 3c. next(i): the first survivor with idx >= idx_i + gap = the next
   // survivor from the first position not below that target; a survivor
