@@ -420,36 +420,38 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
   // order the survivors / peaks inside a row.
   const uint32_t nrow = (n + kClThreads - 1) / kClThreads;
   // ---- 3a. window test: survives iff no strictly larger crossing among the
-  // following positions within the gap (at most 29 of them)
+  // following positions within the gap (at most 29 of them).  The window's
+  // end p (the first position with idx >= idx_i + gap) comes first -- a run of
+  // consecutive bins reaches it exactly gap positions ahead, else a 5-step
+  // binary search (past n the pads read 0x7fffffff) -- so the 32 S/N values
+  // after i need one compare each, their bits masked to the window; p - i - 1
+  // (<= 29) is kept in flag bits 3..7 for 3c
   for (uint32_t r = 0; r < nrow; ++r) {
     const uint32_t i = r * kClThreads + t;
     if (i >= n) break;
-    const uint32_t a = (kPad + i + 1) & ~3u, sh = (kPad + i + 1) - a;  // aligned base, offset of i + 1 (0..3)
     const int xi = static_cast<int>(kidx[kPad + i]);
     const float si = ksnr[kPad + i];
-    bool keep = true;
+    const int tgt = xi + gap;
+    uint32_t cnt;  // window positions i + 1 .. i + cnt
+    if (i + gap < n && static_cast<int>(kidx[kPad + i + gap]) == tgt) {
+      cnt = static_cast<uint32_t>(gap) - 1;
+    } else {
+      cnt = 0;
 #pragma unroll
-    for (int hlf = 0; hlf < 2; ++hlf) {  // two halves of 16 positions: fewer live registers
-      uint4 xv[4];
-      float4 sv[4];
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        xv[v] = *reinterpret_cast<const uint4*>(kidx + a + 16 * hlf + 4 * v);
-        sv[v] = *reinterpret_cast<const float4*>(ksnr + a + 16 * hlf + 4 * v);
-      }
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const uint32_t xs[4] = {xv[v].x, xv[v].y, xv[v].z, xv[v].w};
-        const float ss[4] = {sv[v].x, sv[v].y, sv[v].z, sv[v].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const uint32_t off = static_cast<uint32_t>(16 * hlf + 4 * v + e);  // position a + off
-          const bool in = off >= sh && static_cast<int>(xs[e]) - xi < gap;
-          keep = keep && !(in && ss[e] > si);
-        }
-      }
+      for (uint32_t st = 16; st >= 1; st >>= 1)
+        if (static_cast<int>(kidx[kPad + i + cnt + st]) < tgt) cnt += st;
     }
-    flag[kPad + i] = keep ? 1 : 0;
+    const uint32_t a = (kPad + i + 1) & ~3u, sh = (kPad + i + 1) - a;  // aligned base, offset of i + 1 (0..3)
+    const uint32_t win = ((1u << cnt) - 1u) << sh;                     // bits of positions a + off in the window
+    uint32_t gt = 0;                                                   // bit off: S/N at a + off above si
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const float4 sv = *reinterpret_cast<const float4*>(ksnr + a + 4 * v);
+      const float ss[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) gt |= ss[e] > si ? (1u << (4 * v + e)) : 0u;
+    }
+    flag[kPad + i] = static_cast<uint8_t>(((gt & win) == 0 ? 1u : 0u) | (cnt << 3));
   }
   __syncthreads();
   if (CAP > kClSmall) cl_trace(3);
@@ -509,22 +511,8 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
     const uint32_t i = r * kClThreads + t;
     if (i >= n || !(flag[kPad + i] & 1)) continue;
     const int xi = static_cast<int>(kidx[kPad + i]);
-    // positions after i below the target (sorted: a prefix of the next 31,
-    // at most gap - 1 <= 29 of them): fast path, a run of consecutive bins
-    // reaches the target exactly gap positions ahead; else a branchless
-    // binary search (5 LDS reads, not 32 compares; past n the pads read
-    // 0x7fffffff, never below a target)
-    const int tgt = xi + gap;
-    uint32_t p;
-    if (i + gap < n && static_cast<int>(kidx[kPad + i + gap]) == tgt) {
-      p = i + gap;
-    } else {
-      uint32_t below = 0;
-#pragma unroll
-      for (uint32_t st = 16; st >= 1; st >>= 1)
-        if (static_cast<int>(kidx[kPad + i + below + st]) < tgt) below += st;
-      p = i + 1 + below;
-    }
+    // the first position with idx >= idx_i + gap (3a's window end)
+    const uint32_t p = i + 1 + (static_cast<uint32_t>(flag[kPad + i]) >> 3);
     const uint32_t nx = p < n ? ((flag[kPad + p] & 1) ? p : jmp[p]) : n;
     // run start: no survivor within the gap before i; fast path: the
     // previous position is a survivor within the gap.  Else k = the first
