@@ -1541,9 +1541,34 @@ std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(
         if (tot2 > 0)
           PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_hout.data(), s.d_hout.data(), tot2 * sizeof(uint2),
                                          hipMemcpyDeviceToHost, copy_stream_.get()));
+        // the host trials' cluster segments: one copy of their hull when
+        // there are more than a few (each copy is a blit launch; peak-heavy
+        // batches left ~40 trials x 4 levels to the host)
+        uint64_t lo = ~0ull, hi = 0;
+        int nseg_h = 0;
         for (int k = 0; k < b_count; ++k)
           if (ttab_[static_cast<size_t>(k)].y & kern::kHarmHost)
-            for (int h = 0; h <= nlev_; ++h) copy_seg(segtab_[static_cast<size_t>(k) * 8 + h]);
+            for (int h = 0; h <= nlev_; ++h) {
+              const uint2& e = segtab_[static_cast<size_t>(k) * 8 + h];
+              if (e.y & kern::kClusterRaw) {
+                copy_seg(e);
+              } else if (e.y > 0) {
+                lo = std::min<uint64_t>(lo, e.x);
+                hi = std::max<uint64_t>(hi, static_cast<uint64_t>(e.x) + e.y);
+                ++nseg_h;
+              }
+            }
+        if (nseg_h > 4) {
+          PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_clust.data() + lo, s.d_clust.data() + lo, (hi - lo) * sizeof(uint2),
+                                         hipMemcpyDeviceToHost, copy_stream_.get()));
+        } else if (nseg_h > 0) {
+          for (int k = 0; k < b_count; ++k)
+            if (ttab_[static_cast<size_t>(k)].y & kern::kHarmHost)
+              for (int h = 0; h <= nlev_; ++h) {
+                const uint2& e = segtab_[static_cast<size_t>(k) * 8 + h];
+                if (!(e.y & kern::kClusterRaw)) copy_seg(e);
+              }
+        }
       } else {
         const uint32_t tot = s.h_count[1];
         if (tot > 0)
