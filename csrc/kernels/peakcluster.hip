@@ -395,19 +395,10 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
     uint32_t dst = kPad + block_scan_excl<kClThreads>(sum, sc, nullptr);
     for (uint32_t p = p0; p < p1; ++p) {
       const uint4 d = dsc[jmp[p]];
-      // eight records in flight per round (a chunk holds ~40 on dense data:
-      // one load at a time left the gather latency-bound)
-      for (uint32_t c0 = 0; c0 < d.z; c0 += 8) {
-        PeakRecord rr[8];
-#pragma unroll
-        for (uint32_t u = 0; u < 8; ++u)
-          if (c0 + u < d.z) rr[u] = recs[d.y + c0 + u];
-#pragma unroll
-        for (uint32_t u = 0; u < 8; ++u)
-          if (c0 + u < d.z) {
-            kidx[dst + c0 + u] = static_cast<uint32_t>(rr[u].idx);
-            ksnr[dst + c0 + u] = rr[u].snr;
-          }
+      for (uint32_t c = 0; c < d.z; ++c) {
+        const PeakRecord r = recs[d.y + c];
+        kidx[dst + c] = static_cast<uint32_t>(r.idx);
+        ksnr[dst + c] = r.snr;
       }
       dst += d.z;
     }
