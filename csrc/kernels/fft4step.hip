@@ -581,7 +581,7 @@ __device__ __forceinline__ void onex_core(float2 (&va)[L / G], float2 (&vb)[L / 
   trace_event(4);
 }
 
-template <int L, int G, int R>
+template <int L, int G, int R, bool STRIPS>
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, OneX<L, G, R>::THREADS), amdgpu_waves_per_eu(2)))
 fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__ in_pad, uint64_t n,
                          const double* __restrict__ afs, int K, float2* __restrict__ Y, Fft4Geom g,
@@ -649,7 +649,7 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(padk), 0, 0x7fffffff, 0x00020000);
     const uint32_t rowmask = (1u << log2row) - 1u, pitch = static_cast<uint32_t>(g.inpitch);
-    const bool strips = flags & kFft4StripInput;  // (the host pads in strips exactly when this kernel runs)
+    constexpr bool strips = STRIPS;  // (the host pads in strips exactly when kFft4StripInput is set)
     const uint32_t nrows = static_cast<uint32_t>(L);
     uint32_t bad = 0;
     // Rows are loaded in the order dft<P> consumes them: its first radix-8
@@ -665,9 +665,11 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
       const float pa = static_cast<float>(p0), pb = pa + 3.0f;
       const float fa = afl * pa * (pa - sizef), fb = afl * pb * (pb - sizef);
       const float sa = rintf(fa), sb = rintf(fb);
-      const int64_t first = static_cast<int64_t>(p0) + static_cast<int>(sa);
-      const bool ok = sa == sb && fabsf(fa - sa) < 0.5f - band && fabsf(fb - sb) < 0.5f - band && first >= 0 &&
-                      first + 3 < static_cast<int64_t>(nn);
+      // (32-bit: p0 < 2^24 where the fast path can hold, |shift| << 2^30)
+      const int first = static_cast<int>(p0 + static_cast<uint32_t>(static_cast<int>(sa)));  // (wrapping add)
+      // (& not &&: the compiler turned the short circuit into a branch per row)
+      const bool ok = (sa == sb) & (fabsf(fa - sa) < 0.5f - band) & (fabsf(fb - sb) < 0.5f - band) & (first >= 0) &
+                      (first + 3 < static_cast<int>(nn));
       const uint32_t i = ok ? static_cast<uint32_t>(first) : p0;
       const uint32_t row = i >> log2row, ic = i & rowmask;
       const uint32_t off = strips ? ((ic >> 4) * nrows + row) * kStripW + (ic & 15u) : row * pitch + ic;
@@ -1191,9 +1193,14 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   PSOUP_CHECK(!(f & kFft4GroupXcd) || (K & 7) != 0 || nblocks % 128 == 0, "fft4 colpass: group grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
   PSOUP_CHECK(!g.ypair || pair_y_layout(g.n2, f), "fft4 colpass: this pass A cannot write the row-pair Y layout");
-  if (onex_colpass(g.n2, f))
-    fft4_colpass_onex_kernel<2048, 64, 4><<<grid, OneX<2048, 64, 4>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g,
-                                                                                    tables, f);
+  if (onex_colpass(g.n2, f)) {
+    if (f & kFft4StripInput)
+      fft4_colpass_onex_kernel<2048, 64, 4, true><<<grid, OneX<2048, 64, 4>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y,
+                                                                                            g, tables, f);
+    else
+      fft4_colpass_onex_kernel<2048, 64, 4, false><<<grid, OneX<2048, 64, 4>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y,
+                                                                                             g, tables, f);
+  }
   else if (g.ypair)
     launch_colpass<8, 1, kModeBlocked | kModeTileY | kModePairY>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   else if ((f & kFft4Blocked) && (f & kFft4TileY))
