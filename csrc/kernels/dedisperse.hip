@@ -1129,11 +1129,19 @@ void dedisperse_2bit(const uint32_t* x2, uint64_t stride2, const int32_t* d_acti
                                    16ull * static_cast<uint64_t>(dedisperse_2bit_window(max_spread)) &&
                   stride2 % 4 == 0,
               "dedisperse_2bit: packed rows too short for the windows");
-  constexpr int DPW = 4;
-  const int d_base = d0 / (4 * DPW) * (4 * DPW), d_skip = d0 - d_base;
-  dim3 grid(static_cast<unsigned>((ndm + d_skip + 4 * DPW - 1) / (4 * DPW)), static_cast<unsigned>(ty));
-  PSOUP_CHECK(d_base + static_cast<int>(grid.x) * 4 * DPW <= ldo, "dedisperse_2bit: offset table too narrow");
-  dedisperse_2bit_kernel<DPW><<<grid, 256, 0, s>>>(x2, stride2, d_active, nactive, d_offT, ldo, d_base, d_skip,
+  // DMs per wave: 4 (16-DM workgroups); a launch of <= 8 DMs from an 8-DM
+  // boundary (the headline bench's per-rank chunk) takes 8-DM workgroups
+  // instead of computing 8 DMs it does not store
+  const int dpw = (ndm <= 8 && (d0 % 8) + ndm <= 8) ? 2 : 4;
+  const int d_base = d0 / (4 * dpw) * (4 * dpw), d_skip = d0 - d_base;
+  dim3 grid(static_cast<unsigned>((ndm + d_skip + 4 * dpw - 1) / (4 * dpw)), static_cast<unsigned>(ty));
+  PSOUP_CHECK(d_base + static_cast<int>(grid.x) * 4 * dpw <= ldo, "dedisperse_2bit: offset table too narrow");
+  if (dpw == 2)
+    dedisperse_2bit_kernel<2><<<grid, 256, 0, s>>>(x2, stride2, d_active, nactive, d_offT, ldo, d_base, d_skip,
+                                                   ndm + d_skip, d_wmin, dedisperse_2bit_window(max_spread) / 4,
+                                                   out_nsamps, out, out_stride, scale);
+  else
+    dedisperse_2bit_kernel<4><<<grid, 256, 0, s>>>(x2, stride2, d_active, nactive, d_offT, ldo, d_base, d_skip,
                                                    ndm + d_skip, d_wmin, dedisperse_2bit_window(max_spread) / 4,
                                                    out_nsamps, out, out_stride, scale);
   post_launch_check("dedisperse_2bit_kernel", s);
