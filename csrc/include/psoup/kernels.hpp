@@ -377,8 +377,6 @@ enum Fft4Flags : int {
                            // one LDS exchange, compile-time twiddles inside the two local DFTs
   kFft4PairY = 262144,     // the Stockham pass A (column lengths other than the one-exchange one) also
                            // hands the fused spectrum pass row-pair Y (Y_p[k2/2][i][k2%2])
-  kFft4GroupXcd16 = 524288,  // one-exchange pass A with kFft4GroupXcd: 16 trials (not 8) x 2 column blocks
-                             // per XCD group (needs K % 16 == 0): each input line read from HBM half as often
   kFft4StripInput = 1073741824,  // one-exchange pass A: the padded input in column strips (16 + 4 floats of
                                  // every row per strip, strips row-contiguous), so a wave's 16 rows are
                                  // one ~1.3 KiB contiguous range instead of 16 pieces 16 KiB apart

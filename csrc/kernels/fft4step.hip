@@ -597,14 +597,7 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
   const uint32_t lb = logical_block(gridDim.x, !(flags & kFft4NoRemap));
   int k = static_cast<int>(lb % static_cast<uint32_t>(K));
   int c0 = static_cast<int>(lb / static_cast<uint32_t>(K)) * 8;
-  if ((flags & kFft4GroupXcd) && (flags & kFft4GroupXcd16) && (K & 15) == 0) {
-    // 16 trials x column blocks 2p, 2p+1 (32 workgroups) per XCD group
-    const uint32_t b = blockIdx.x;
-    const uint32_t Gp = ((b >> 8) << 3) | (b & 7u), wq = (b >> 3) & 31u;
-    const uint32_t kg = static_cast<uint32_t>(K) >> 4;
-    k = static_cast<int>(16 * (Gp % kg) + (wq & 15u));
-    c0 = static_cast<int>(2 * (Gp / kg) + (wq >> 4)) * 8;
-  } else if ((flags & kFft4GroupXcd) && (K & 7) == 0) {
+  if ((flags & kFft4GroupXcd) && (K & 7) == 0) {
     const uint32_t b = blockIdx.x;
     const uint32_t Gp = ((b >> 7) << 3) | (b & 7u), wq = (b >> 3) & 15u;
     const uint32_t kg = static_cast<uint32_t>(K) >> 3;
@@ -1198,8 +1191,6 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   const uint64_t nblocks = static_cast<uint64_t>(g.n1 / 8) * K;
   PSOUP_CHECK(nblocks < (1ull << 31) && nblocks % 16 == 0, "fft4 colpass: grid");
   PSOUP_CHECK(!(f & kFft4GroupXcd) || (K & 7) != 0 || nblocks % 128 == 0, "fft4 colpass: group grid");
-  PSOUP_CHECK(!(f & kFft4GroupXcd) || !(f & kFft4GroupXcd16) || (K & 15) != 0 || nblocks % 256 == 0,
-              "fft4 colpass: 16-trial group grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
   PSOUP_CHECK(!g.ypair || pair_y_layout(g.n2, f), "fft4 colpass: this pass A cannot write the row-pair Y layout");
   if (onex_colpass(g.n2, f)) {

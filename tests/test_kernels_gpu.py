@@ -376,26 +376,6 @@ def fft4_flags(request):
     C.kernels.fft4_set_flags(old)
 
 
-def test_fft4_group_xcd16_same_values():
-    """The 16-trial XCD grouping of the one-exchange pass A (kFft4GroupXcd16)
-    only reorders workgroups: at 2^23 with K = 32 trials the spectra equal
-    the 8-trial grouping's bit for bit."""
-    import peasoup_amd._C as C
-    from peasoup_amd import ops
-
-    x = torch.from_numpy(np.random.default_rng(5).standard_normal(1 << 23).astype(np.float32)).to(dev)
-    accs = [float(a) for a in np.linspace(-480.0, 480.0, 32)]
-    old = C.kernels.fft4_flags()
-    try:
-        out = []
-        for f in (old & ~524288, old | 524288):
-            C.kernels.fft4_set_flags(f)
-            out.append(ops.fft4_resample_spectrum(x, accs, 64e-6))
-    finally:
-        C.kernels.fft4_set_flags(old)
-    assert torch.equal(out[0], out[1])
-
-
 @pytest.mark.parametrize("log2n", [15, 17, 20, 23, 25])
 def test_fft4_resample_spectrum_matches_numpy(log2n, fft4_flags):
     """Fused resample + four-step FFT vs (bit-exact GPU resample) + numpy fp64 FFT."""
