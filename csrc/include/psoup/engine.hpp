@@ -184,18 +184,19 @@ struct SearchParams {
   int accel_batch = 0;          // 0 = auto
   int sub_batch = -1;           // fused-FFT trials per sub-batch on alternating streams (0 = off, -1 = auto)
   int host_threads = -1;        // host workers clustering/distilling peak-heavy batches (-1 = auto, 0/1 = serial)
-  // auto-batch HBM budget (512 trials of 2^23: 43 GB of intermediates on a
-  // 288 GB device; same-box sweep without sub-batches: K = 512 22.25k/22.17k,
-  // 256 21.98k/21.97k, 128 21.65k trials/s, profiles/r3_sub/), capped at 70%
-  // of the device's free memory shared among its engines
-  size_t batch_bytes = 48ull << 30;
+  // auto-batch HBM budget (1024 trials of 2^23: 56 GB of intermediates --
+  // Y, P, Q -- on a 288 GB device; same-box sweep of the round-5 bench: K =
+  // 1024 34.45k/34.38k, 1376 33.72k/33.61k, 768 33.80k/33.83k, 512
+  // 33.30k/33.38k trials/s, profiles/r5_batch/), capped at 70% of the
+  // device's free memory shared among its engines
+  size_t batch_bytes = 64ull << 30;
   // Engines sharing the device: the auto budget is also capped at 70% of the
   // device's free memory divided by this count.
   int engines_per_device = 1;
   // Auto batching of short trial lists: lists shorter than min_batches full
   // batches are cut into min_batches even batches (multiples of 8), but never
   // below the batch an eighth of the budget gives.
-  int min_batches = 8;
+  int min_batches = 4;
   // Compute streams the sub-batches of a batch rotate over (>= 2).
   int sub_streams = 2;
   int min_gap = 30;

@@ -612,7 +612,7 @@ def test_auto_short_list_balancing_matches_fixed_batch(C):
                 per = n * 4 + pst * 4 + (pst + C.kernels.spec_q_shift + 63) // 64 * 64
             else:
                 per = n * 4 + nb * 8 + nb * 4 + (nb + 63) // 64 * 64
-            p.accel_batch, p.batch_bytes = 0, 64 * per
+            p.accel_batch, p.batch_bytes, p.min_batches = 0, 64 * per, 8
         else:
             p.accel_batch, p.sub_batch = 24, 0
         eng = C.SearchEngine(p, s)
