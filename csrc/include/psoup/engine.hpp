@@ -197,6 +197,10 @@ struct SearchParams {
   // batches are cut into min_batches even batches (multiples of 8), but never
   // below the batch an eighth of the budget gives.
   int min_batches = 4;
+  // Threshold-crossing records in 2^peak_region_log2 regions with a counter
+  // each (kern::kPeakRegionStride) when the device clusters them: the
+  // reservation atomics of peak-heavy batches spread over that many lines.
+  int peak_region_log2 = 6;
   // Compute streams the sub-batches of a batch rotate over (>= 2).
   int sub_streams = 2;
   int min_gap = 30;
@@ -353,7 +357,9 @@ class SearchEngine {
  private:
   struct Slot {
     DeviceBuffer<kern::PeakRecord> d_peaks;
-    DeviceBuffer<uint32_t> d_count;  // [0] threshold crossings, [1] cluster peaks, [2] distilled candidates
+    // [0] threshold crossings, [1] cluster peaks, [2] distilled candidates;
+    // with record regions their counters from [kPeakRegionStride] (rcount)
+    DeviceBuffer<uint32_t> d_count;
     PinnedBuffer<kern::PeakRecord> h_peaks;
     PinnedBuffer<uint32_t> h_count;
     // GPU clustering (kern::peak_cluster_batch): segment work/table, the
@@ -368,6 +374,7 @@ class SearchEngine {
     std::unique_ptr<Event> done, copied;
     int first = 0, count = 0;
   };
+  uint32_t* rcount(Slot& s) { return s.d_count.data() + (rlog2_ ? kern::kPeakRegionStride : 0); }
   void ensure_batch_buffers(int k);
   FftPlan& batch_plan(int count);
   void launch_batch(Slot& s, int first, int count);
@@ -393,6 +400,7 @@ class SearchEngine {
   std::vector<uint2> segtab_;  // segment table snapshot of the batch being processed
   std::vector<uint2> ttab_;    // its per-trial distillation table
   bool gpu_cluster_ = true;  // env PSOUP_GPU_CLUSTER=0: cluster on the host (reference path)
+  int rlog2_ = 0;            // record regions (SearchParams::peak_region_log2; device clustering only)
   bool gpu_distill_ = true;  // env PSOUP_GPU_DISTILL=0: per-trial harmonic distillation on the host
   kern::HarmDistillParams hdp_{};
   // flat trial list of the current search_prepared_many call

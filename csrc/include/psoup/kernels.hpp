@@ -34,6 +34,14 @@ namespace kern {
 // preceded by a chunk descriptor {kPeakChunk | count << 16 | segment, first
 // idx, position of its first crossing (as the snr bits)}.
 constexpr uint32_t kPeakChunk = 0x80000000u;
+// Record regions (HarmParams::region_log2 = g > 0): `out` is cut into 2^g
+// regions of capacity >> g records; workgroup b emits into region
+// b & (2^g - 1), whose counter is count[region * kPeakRegionStride] (one
+// 128-byte line each).  Chunk positions stay absolute.  One counter took
+// every wave's reservation atomic in turn: ~11 ns each, 8.8 ms for the 777k
+// chunks of one peak-heavy 1024-trial batch; 64 counters 0.2 ms
+// (tools/expt/atomic_bench.hip, profiles/r5_regions/).
+constexpr uint32_t kPeakRegionStride = 32;
 struct PeakRecord {
   uint32_t seg;  // batch_item * 8 + level, or a chunk descriptor (kPeakChunk)
   int32_t idx;
@@ -391,8 +399,9 @@ struct HarmParams {
   int start[6];            // per level search range [start, end)
   int end[6];
   float thresh;
-  uint32_t capacity;       // PeakRecord capacity of `out`
+  uint32_t capacity;       // PeakRecord capacity of `out` (a multiple of 2^region_log2)
   uint32_t trial_base = 0; // added to the batch item of every record (sub-batch launches)
+  int region_log2 = 0;     // record regions (kPeakRegionStride): 0 = one counter, count[0]
 };
 // Fused incoherent harmonic sum + threshold + compaction: never writes the
 // summed spectra.  Records land unordered; count may exceed capacity (then
@@ -443,9 +452,15 @@ void quantize_q8(const float* P, uint64_t pstride, uint64_t n, int K, uint8_t* Q
 void peak_cluster_set_trace(unsigned long long* d_events);
 constexpr uint32_t kClusterCap = 14000;
 constexpr uint32_t kClusterRaw = 0x80000000u;
+// region_log2 > 0: the records in regions as harmonic_peaks_batch wrote them
+// (kPeakRegionStride; d_count = the region counters, cap >> region_log2 a
+// multiple of 4096).
 void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint32_t cap, uint32_t nseg, int gap,
                         uint32_t* d_work, uint2* d_sorted, uint2* d_out, uint2* d_segtab, uint32_t* d_total,
-                        hipStream_t s);
+                        hipStream_t s, int region_log2 = 0);
+// *d_total = the records held in the 2^region_log2 regions of d_rcount, or,
+// when one overflowed, 2^region_log2 x its count (more than cap).
+void peak_regions_total(const uint32_t* d_rcount, int region_log2, uint32_t cap, uint32_t* d_total, hipStream_t s);
 // Per-trial harmonic distillation on the device (harmdistill.hip;
 // distiller.hpp:63-108, HarmonicDistiller(tol, max_harm, keep_related=false,
 // fractional_harms=true) on the cluster peaks of every level of one trial).

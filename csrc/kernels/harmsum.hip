@@ -371,7 +371,7 @@ __global__ void __launch_bounds__(256) r2c_interbin_tiled_shfl_kernel(
 template <int NL>
 __device__ __forceinline__ void emit_levels(const bool (&pred)[NL], int h0, int h1, uint32_t seg0, int idx,
                                             const float (&snr)[NL], PeakRecord* __restrict__ out,
-                                            uint32_t* __restrict__ count, uint32_t capacity) {
+                                            uint32_t* __restrict__ count, const HarmParams& hp) {
   const int lane = threadIdx.x & 63;
   unsigned long long mask[NL];
   uint32_t tot = 0;
@@ -381,8 +381,13 @@ __device__ __forceinline__ void emit_levels(const bool (&pred)[NL], int h0, int 
     tot += mask[h] ? static_cast<uint32_t>(__popcll(mask[h])) + 1u : 0u;  // + its descriptor
   }
   if (tot == 0) return;
+  // the workgroup's record region (kPeakRegionStride): block-uniform
+  const uint32_t rg = blockIdx.x & ((1u << hp.region_log2) - 1u);
+  const uint32_t capacity = hp.capacity >> hp.region_log2;
+  const uint32_t pos0 = rg * capacity;
+  out += pos0;
   uint32_t base = 0;
-  if (lane == 0) base = atomicAdd(count, tot);
+  if (lane == 0) base = atomicAdd(count + rg * kPeakRegionStride, tot);
   base = __shfl(base, 0, 64);
   const unsigned long long lt = (lane == 0) ? 0ull : ((1ull << lane) - 1ull);
 #pragma unroll
@@ -392,9 +397,9 @@ __device__ __forceinline__ void emit_levels(const bool (&pred)[NL], int h0, int 
     const uint32_t first = base + 1u;  // the chunk's first crossing
     if (pred[h]) {
       const uint32_t below = static_cast<uint32_t>(__popcll(mask[h] & lt));
-      if (below == 0 && base < capacity)  // the chunk's lowest lane: the descriptor
+      if (below == 0 && base < capacity)  // the chunk's lowest lane: the descriptor (absolute position)
         out[base] = PeakRecord{kPeakChunk | (cnt << 16) | (seg0 + static_cast<uint32_t>(h)), idx,
-                               __uint_as_float(first)};
+                               __uint_as_float(pos0 + first)};
       const uint32_t pos = first + below;
       if (pos < capacity) out[pos] = PeakRecord{seg0 + static_cast<uint32_t>(h), idx, snr[h]};
     }
@@ -613,7 +618,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks_kernel(const float* __rest
       any = any | pred[h];
     }
     if (__ballot(any) == 0ull) continue;  // one ballot per bin group in the (usual) no-peak case
-    emit_levels<NLEV + 1>(pred, 0, NLEV, seg0, i, o, out, count, hp.capacity);
+    emit_levels<NLEV + 1>(pred, 0, NLEV, seg0, i, o, out, count, hp);
   }
 }
 
@@ -734,7 +739,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks2_kernel(const float* __res
       any = any | pred[h];
     }
     if (__ballot(any) == 0ull) return;
-    emit_levels<NLEV + 1>(pred, h0, h1, seg0, i, o, out, count, hp.capacity);
+    emit_levels<NLEV + 1>(pred, h0, h1, seg0, i, o, out, count, hp);
   };
   float run[Tl::BPT];  // running sum after level NLEV - 1
 #pragma unroll
@@ -1075,7 +1080,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
         bool pred[NLEV + 1];
         float o[NLEV + 1];
         level_out(sum, i, e ? c1 : c0, pred, o);
-        emit_levels<NLEV + 1>(pred, 0, NLEV, seg0, i, o, out, count, hp.capacity);
+        emit_levels<NLEV + 1>(pred, 0, NLEV, seg0, i, o, out, count, hp);
       }
     }
     return;
@@ -1151,7 +1156,7 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
         pred[h] = in_range & (o[h] > thr);
       }
     }
-    emit_levels<NLEV + 1>(pred, 0, NLEV, seg0, i, o, out, count, hp.capacity);
+    emit_levels<NLEV + 1>(pred, 0, NLEV, seg0, i, o, out, count, hp);
   }
 }
 
@@ -1467,6 +1472,8 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
   }
   PSOUP_CHECK(hi <= static_cast<int>(nbins), "search range beyond spectrum");
   PSOUP_CHECK((static_cast<uint64_t>(K) + hp.trial_base) * 8 <= 65536, "chunk descriptors hold 16-bit segments");
+  PSOUP_CHECK(hp.region_log2 >= 0 && hp.region_log2 <= 8 && hp.capacity % (1u << hp.region_log2) == 0,
+              "harmonic_peaks_batch: record regions must divide the capacity");
   if (hi <= lo) return;
   PSOUP_CHECK(static_cast<int64_t>(hi) * 32 < (int64_t(1) << 31), "spectrum too long for the int32 gather math");
   const int xcd = (g_harm_flags & 1) && (K % 8 == 0) ? 1 : 0;

@@ -75,16 +75,29 @@ __device__ __forceinline__ bool chunk_ok(const PeakRecord& r, uint32_t nseg, uin
          static_cast<uint64_t>(__float_as_uint(r.snr)) + chunk_count(r.seg) <= n;
 }
 
+// Where the records are (kernels.hpp kPeakRegionStride): 2^log2 regions of
+// capr records, region r's count at count[r * kPeakRegionStride] (log2 = 0:
+// one region, count[0], capr = the capacity).
+struct RecRegions {
+  const uint32_t* count;
+  uint32_t capr;
+  int log2;
+};
+// the end (absolute, exclusive) of the records held in the region of position i
+__device__ __forceinline__ uint32_t region_end(const RecRegions& g, uint32_t i) {
+  const uint32_t r = g.log2 ? i / g.capr : 0u;
+  return r * g.capr + min(g.count[r * kPeakRegionStride], g.capr);
+}
+
 // Per-segment chunk and crossing counts: each block counts its descriptors
 // in LDS and adds the non-zero counts to the global ones (one atomic per
 // block and segment).
-__global__ void __launch_bounds__(256) seg_hist_kernel(const PeakRecord* __restrict__ in,
-                                                       const uint32_t* __restrict__ count, uint32_t cap,
+__global__ void __launch_bounds__(256) seg_hist_kernel(const PeakRecord* __restrict__ in, RecRegions g,
                                                        uint32_t nseg, uint32_t* __restrict__ segcnt,
                                                        uint32_t* __restrict__ segdcnt) {
   __shared__ uint32_t lr[kSegLds], lc[kSegLds];
-  const uint32_t n = min(*count, cap);
   const uint32_t base = blockIdx.x * 256u * kRecPerThread;
+  const uint32_t n = region_end(g, base);  // blocks never straddle regions (capr % 4096 == 0)
   if (base >= n) return;
   for (uint32_t i = threadIdx.x; i < nseg; i += 256) lr[i] = lc[i] = 0;
   __syncthreads();
@@ -128,14 +141,13 @@ __global__ void __launch_bounds__(kClThreads) seg_scan_kernel(const uint32_t* __
 // Chunk descriptors grouped by segment as {first idx, position, count}: LDS
 // ranks within the block, one global atomic per (block, segment) reserves
 // the block's range of the segment.
-__global__ void __launch_bounds__(256) seg_scatter_kernel(const PeakRecord* __restrict__ in,
-                                                          const uint32_t* __restrict__ count, uint32_t cap,
+__global__ void __launch_bounds__(256) seg_scatter_kernel(const PeakRecord* __restrict__ in, RecRegions g,
                                                           uint32_t nseg, const uint32_t* __restrict__ segdoff,
                                                           uint32_t* __restrict__ cursor, uint4* __restrict__ out) {
   __shared__ uint32_t lc[kSegLds];
   __shared__ uint32_t lb[kSegLds];
-  const uint32_t n = min(*count, cap);
   const uint32_t base = blockIdx.x * 256u * kRecPerThread;
+  const uint32_t n = region_end(g, base);
   if (base >= n) return;
   for (uint32_t i = threadIdx.x; i < nseg; i += 256) lc[i] = 0;
   __syncthreads();
@@ -586,12 +598,14 @@ __global__ void __launch_bounds__(kClThreads) peak_cluster_kernel(const PeakReco
 }
 
 // Fallbacks for batches with more than kSegLds segments: one global atomic per descriptor.
-__global__ void __launch_bounds__(256) seg_hist_global_kernel(const PeakRecord* __restrict__ in,
-                                                              const uint32_t* __restrict__ count, uint32_t cap,
-                                                              uint32_t nseg, uint32_t* __restrict__ segcnt,
+__global__ void __launch_bounds__(256) seg_hist_global_kernel(const PeakRecord* __restrict__ in, RecRegions g,
+                                                              uint32_t cap, uint32_t nseg,
+                                                              uint32_t* __restrict__ segcnt,
                                                               uint32_t* __restrict__ segdcnt) {
-  const uint32_t n = min(*count, cap);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  const uint32_t lim = g.log2 ? cap : min(*g.count, cap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += gridDim.x * blockDim.x) {
+    const uint32_t n = region_end(g, i);
+    if (i >= n) continue;
     const PeakRecord r = in[i];
     if (chunk_ok(r, nseg, n)) {
       atomicAdd(&segdcnt[chunk_seg(r.seg)], 1u);
@@ -600,13 +614,15 @@ __global__ void __launch_bounds__(256) seg_hist_global_kernel(const PeakRecord* 
   }
 }
 
-__global__ void __launch_bounds__(256) seg_scatter_global_kernel(const PeakRecord* __restrict__ in,
-                                                                 const uint32_t* __restrict__ count, uint32_t cap,
-                                                                 uint32_t nseg, const uint32_t* __restrict__ segdoff,
+__global__ void __launch_bounds__(256) seg_scatter_global_kernel(const PeakRecord* __restrict__ in, RecRegions g,
+                                                                 uint32_t cap, uint32_t nseg,
+                                                                 const uint32_t* __restrict__ segdoff,
                                                                  uint32_t* __restrict__ cursor,
                                                                  uint4* __restrict__ out) {
-  const uint32_t n = min(*count, cap);
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  const uint32_t lim = g.log2 ? cap : min(*g.count, cap);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += gridDim.x * blockDim.x) {
+    const uint32_t n = region_end(g, i);
+    if (i >= n) continue;
     const PeakRecord r = in[i];
     if (!chunk_ok(r, nseg, n)) continue;
     const uint32_t sg = chunk_seg(r.seg);
@@ -615,7 +631,36 @@ __global__ void __launch_bounds__(256) seg_scatter_global_kernel(const PeakRecor
   }
 }
 
+// The regions' total into *total, or 2^log2 x the fullest region's count
+// when one overflowed (> the capacity: the engine's re-run with a larger
+// buffer then fits every region).
+__global__ void __launch_bounds__(64) peak_regions_total_kernel(const uint32_t* __restrict__ count, int log2,
+                                                                uint32_t capr, uint32_t* __restrict__ total) {
+  const uint32_t R = 1u << log2;
+  unsigned long long sum = 0;
+  uint32_t mx = 0;
+  for (uint32_t r = threadIdx.x; r < R; r += 64) {
+    const uint32_t c = count[r * kPeakRegionStride];
+    sum += c;
+    mx = max(mx, c);
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    sum += __shfl_xor(sum, off, 64);
+    mx = max(mx, __shfl_xor(mx, off, 64));
+  }
+  if (threadIdx.x == 0)
+    *total = mx > capr ? static_cast<uint32_t>(min(static_cast<unsigned long long>(mx) << log2, 0x80000000ull))
+                       : static_cast<uint32_t>(sum);
+}
+
 }  // namespace
+
+void peak_regions_total(const uint32_t* d_rcount, int region_log2, uint32_t cap, uint32_t* d_total, hipStream_t s) {
+  PSOUP_CHECK(region_log2 >= 0 && region_log2 <= 8 && cap % (1u << region_log2) == 0, "peak_regions_total: regions");
+  peak_regions_total_kernel<<<1, 64, 0, s>>>(d_rcount, region_log2, cap >> region_log2, d_total);
+  post_launch_check("peak_regions_total_kernel", s);
+}
 
 void peak_cluster_set_trace(unsigned long long* d_events) {
   PSOUP_HIP_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_cl_trace), &d_events, sizeof(d_events)));
@@ -623,8 +668,13 @@ void peak_cluster_set_trace(unsigned long long* d_events) {
 
 void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint32_t cap, uint32_t nseg, int gap,
                         uint32_t* d_work, uint2* d_sorted, uint2* d_out, uint2* d_segtab, uint32_t* d_total,
-                        hipStream_t s) {
+                        hipStream_t s, int region_log2) {
   if (nseg == 0) return;
+  PSOUP_CHECK(region_log2 >= 0 && region_log2 <= 8 &&
+                  (region_log2 == 0 || (cap >> region_log2) % (256u * kRecPerThread) == 0) &&
+                  cap % (1u << region_log2) == 0,
+              "peak_cluster_batch: record regions must be whole multiples of 4096 records");
+  const RecRegions rg{d_count, cap >> region_log2, region_log2};
   // the window phases read the 32 positions next to a crossing: gap - 1 <= 29
   // of them can lie within the gap (the reference's min_gap is 30)
   PSOUP_CHECK(gap >= 1 && gap <= 30, "peak_cluster_batch: gap must be in [1, 30]");
@@ -641,23 +691,23 @@ void peak_cluster_batch(const PeakRecord* d_peaks, const uint32_t* d_count, uint
   if (nseg <= static_cast<uint32_t>(kSegLds)) {
     const uint64_t per = 256ull * kRecPerThread;
     const unsigned g = static_cast<unsigned>(std::max<uint64_t>(1, (static_cast<uint64_t>(cap) + per - 1) / per));
-    seg_hist_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segcnt, segdcnt);
+    seg_hist_kernel<<<g, 256, 0, s>>>(d_peaks, rg, nseg, segcnt, segdcnt);
     post_launch_check("seg_hist_kernel", s);
     seg_scan_kernel<<<1, kClThreads, 0, s>>>(segcnt, nseg, segoff);
     post_launch_check("seg_scan_kernel", s);
     seg_scan_kernel<<<1, kClThreads, 0, s>>>(segdcnt, nseg, segdoff);
     post_launch_check("seg_scan_kernel", s);
-    seg_scatter_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segdoff, cursor, desc);
+    seg_scatter_kernel<<<g, 256, 0, s>>>(d_peaks, rg, nseg, segdoff, cursor, desc);
     post_launch_check("seg_scatter_kernel", s);
   } else {
     const unsigned g = dev::grid_for(cap, 256, 4096);
-    seg_hist_global_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segcnt, segdcnt);
+    seg_hist_global_kernel<<<g, 256, 0, s>>>(d_peaks, rg, cap, nseg, segcnt, segdcnt);
     post_launch_check("seg_hist_global_kernel", s);
     seg_scan_kernel<<<1, kClThreads, 0, s>>>(segcnt, nseg, segoff);
     post_launch_check("seg_scan_kernel", s);
     seg_scan_kernel<<<1, kClThreads, 0, s>>>(segdcnt, nseg, segdoff);
     post_launch_check("seg_scan_kernel", s);
-    seg_scatter_global_kernel<<<g, 256, 0, s>>>(d_peaks, d_count, cap, nseg, segdoff, cursor, desc);
+    seg_scatter_global_kernel<<<g, 256, 0, s>>>(d_peaks, rg, cap, nseg, segdoff, cursor, desc);
     post_launch_check("seg_scatter_global_kernel", s);
   }
   peak_cluster_kernel<kClSmall, kClThreads><<<nseg, kClThreads, 0, s>>>(

@@ -773,8 +773,9 @@ PYBIND11_MODULE(_C, m) {
   k.def("harmonic_peaks_batch", [](uintptr_t Pin, uint64_t nb, uint64_t pstride, int K, int nlevels,
                                    const std::vector<int>& start, const std::vector<int>& end, float thresh,
                                    uint32_t capacity, uintptr_t out, uintptr_t count, uintptr_t s, uintptr_t q,
-                                   uint64_t qstride, int pblk_log2_n2, uint32_t pblk_n1, int qshift) {
+                                   uint64_t qstride, int pblk_log2_n2, uint32_t pblk_n1, int qshift, int region_log2) {
     kern::HarmParams hp{};
+    hp.region_log2 = region_log2;
     hp.nlevels = nlevels;
     for (int i = 0; i < 6; ++i) {
       hp.start[i] = i < static_cast<int>(start.size()) ? start[i] : 0;
@@ -792,14 +793,19 @@ PYBIND11_MODULE(_C, m) {
   }, py::arg("P"), py::arg("nb"), py::arg("pstride"), py::arg("K"), py::arg("nlevels"), py::arg("start"),
      py::arg("end"), py::arg("thresh"), py::arg("capacity"), py::arg("out"), py::arg("count"), py::arg("s"),
      py::arg("q") = 0, py::arg("qstride") = 0, py::arg("pblk_log2_n2") = 0, py::arg("pblk_n1") = 0,
-     py::arg("qshift") = 0);
+     py::arg("qshift") = 0, py::arg("region_log2") = 0);
   k.def("peak_cluster_batch", [](uintptr_t peaks, uintptr_t count, uint32_t cap, uint32_t nseg, int gap,
                                  uintptr_t work, uintptr_t sorted, uintptr_t out, uintptr_t segtab, uintptr_t total,
-                                 uintptr_t s) {
+                                 uintptr_t s, int region_log2) {
     kern::peak_cluster_batch(P<const kern::PeakRecord>(peaks), P<const uint32_t>(count), cap, nseg, gap,
                              P<uint32_t>(work), P<uint2>(sorted), P<uint2>(out), P<uint2>(segtab), P<uint32_t>(total),
-                             S(s));
+                             S(s), region_log2);
+  }, py::arg("peaks"), py::arg("count"), py::arg("cap"), py::arg("nseg"), py::arg("gap"), py::arg("work"),
+     py::arg("sorted"), py::arg("out"), py::arg("segtab"), py::arg("total"), py::arg("s"), py::arg("region_log2") = 0);
+  k.def("peak_regions_total", [](uintptr_t rcount, int region_log2, uint32_t cap, uintptr_t total, uintptr_t s) {
+    kern::peak_regions_total(P<const uint32_t>(rcount), region_log2, cap, P<uint32_t>(total), S(s));
   });
+  k.attr("peak_region_stride") = kern::kPeakRegionStride;
   k.attr("cluster_cap") = kern::kClusterCap;
   k.def("harm_distill_batch", [](uintptr_t clust, uintptr_t segtab, int ntrials, int nlevels,
                                  const std::vector<double>& factor, float tol, float max_harm, uintptr_t out,
@@ -960,6 +966,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("batch_bytes", &SearchParams::batch_bytes)
       .def_readwrite("engines_per_device", &SearchParams::engines_per_device)
       .def_readwrite("min_batches", &SearchParams::min_batches)
+      .def_readwrite("peak_region_log2", &SearchParams::peak_region_log2)
       .def_readwrite("min_gap", &SearchParams::min_gap)
       .def_readwrite("fft_mode", &SearchParams::fft_mode);
   py::class_<SearchEngine::Pending, std::shared_ptr<SearchEngine::Pending>>(m, "PendingSearch");

@@ -914,14 +914,20 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     }
   }
   cap_ = static_cast<uint32_t>(std::max<uint64_t>(1u << 16, static_cast<uint64_t>(K_) * 4096));
+  if (const char* e = std::getenv("PSOUP_GPU_CLUSTER")) gpu_cluster_ = std::atoi(e) != 0;
+  gpu_cluster_ = gpu_cluster_ && p_.min_gap >= 1 && p_.min_gap <= 30;  // the device windows span 32 positions
+  // record regions (kern::kPeakRegionStride) where the device clusters the
+  // records; the host path and the peak dump read one contiguous run
+  if (const char* e = std::getenv("PSOUP_PEAK_REGION_LOG2")) p_.peak_region_log2 = std::atoi(e);
+  rlog2_ = gpu_cluster_ && !std::getenv("PSOUP_DUMP_PEAKS") ? std::clamp(p_.peak_region_log2, 0, 8) : 0;
+  hp_.region_log2 = rlog2_;
   for (auto& s : slots_) {
     s.done = std::make_unique<Event>();
     s.copied = std::make_unique<Event>();
-    s.d_count.resize(3);
+    // [0] records, [1] cluster peaks, [2] distilled candidates; region counters from [32]
+    s.d_count.resize(rlog2_ ? kern::kPeakRegionStride * ((1u << rlog2_) + 1) : 3);
     s.h_count.resize(3);
   }
-  if (const char* e = std::getenv("PSOUP_GPU_CLUSTER")) gpu_cluster_ = std::atoi(e) != 0;
-  gpu_cluster_ = gpu_cluster_ && p_.min_gap >= 1 && p_.min_gap <= 30;  // the device windows span 32 positions
   // per-trial harmonic distillation on the device: needs the device clusters,
   // the fast relation's tolerance range, and bins that fit the record's 29 bits
   if (const char* e = std::getenv("PSOUP_GPU_DISTILL")) gpu_distill_ = std::atoi(e) != 0;
@@ -948,7 +954,11 @@ SearchEngine::~SearchEngine() {
 }
 
 void SearchEngine::grow_capacity(uint32_t need) {
-  cap_ = std::max(cap_, need);
+  // regions of whole 4096-record blocks (the clustering's hist/scatter blocks)
+  const uint64_t q = rlog2_ ? uint64_t(4096) << rlog2_ : 1;
+  const uint64_t c = (std::max<uint64_t>(cap_, need) + q - 1) / q * q;
+  PSOUP_CHECK(c < (uint64_t(1) << 32), "peak record capacity beyond 32-bit positions");
+  cap_ = static_cast<uint32_t>(c);
   for (auto& s : slots_) {
     s.d_peaks.resize(cap_);
     if (gpu_cluster_) {
@@ -1012,7 +1022,9 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
   const uint64_t pst = pst_;
   const kern::Fft4XLayout xl =
       mode_ == 2 ? kern::fft4_x_layout(f4_) : kern::Fft4XLayout{ilog2(n_ / 2), n_ / 2, 8, 3, false};
-  PSOUP_HIP_CHECK(hipMemsetAsync(s.d_count.data(), 0, sizeof(uint32_t), stream_));
+  // the record counter(s): region r's at rcount(s)[r * kPeakRegionStride]
+  PSOUP_HIP_CHECK(hipMemsetAsync(rcount(s), 0, (rlog2_ ? kern::kPeakRegionStride << rlog2_ : 1) * sizeof(uint32_t),
+                                 stream_));
   // Trials [b, b + c) of the batch: spectrum, power spectrum, harmonic peaks.
   auto run = [&](int b, int c, hipStream_t st) {
     float* P = fromx_ ? nullptr : P_.data() + static_cast<uint64_t>(b) * pst;
@@ -1052,7 +1064,7 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
         RoctxRange r("Harmonic summing");
         kern::HarmParams hp = hp_;
         hp.trial_base = static_cast<uint32_t>(b);
-        kern::harmonic_peaks_batch(P, nb_, pst, c, hp, s.d_peaks.data(), s.d_count.data(), st, Q, qst_, &fx);
+        kern::harmonic_peaks_batch(P, nb_, pst, c, hp, s.d_peaks.data(), rcount(s), st, Q, qst_, &fx);
         return;
       }
       float2* X = spec_.data() + static_cast<uint64_t>(b) * xs_;
@@ -1089,7 +1101,7 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
     RoctxRange r("Harmonic summing");
     kern::HarmParams hp = hp_;
     hp.trial_base = static_cast<uint32_t>(b);
-    kern::harmonic_peaks_batch(P, nb_, pst, c, hp, s.d_peaks.data(), s.d_count.data(), st, Q, qst_,
+    kern::harmonic_peaks_batch(P, nb_, pst, c, hp, s.d_peaks.data(), rcount(s), st, Q, qst_,
                                fromx_ ? &fx : nullptr);
   };
   if (sub_ > 0 && count > sub_) {
@@ -1109,6 +1121,8 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
   } else {
     run(0, count, stream_);
   }
+  // d_count[0]: the records held (or, after a region overflowed, the capacity that fits)
+  if (rlog2_) kern::peak_regions_total(rcount(s), rlog2_, cap_, s.d_count.data(), stream_);
   if (const char* dump = std::getenv("PSOUP_DUMP_PEAKS")) {
     // diagnostics (tools/expt/cluster_replay.py): the first batch's raw peak
     // records with at least PSOUP_DUMP_PEAKS_MIN of them, for replaying the
@@ -1132,9 +1146,9 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
   if (gpu_cluster_) {
     // cluster on the device: only cluster peaks (and the rare over-capacity
     // segment's raw crossings) are copied out
-    kern::peak_cluster_batch(s.d_peaks.data(), s.d_count.data(), cap_, static_cast<uint32_t>(count) * 8, p_.min_gap,
+    kern::peak_cluster_batch(s.d_peaks.data(), rcount(s), cap_, static_cast<uint32_t>(count) * 8, p_.min_gap,
                              s.d_work.data(), s.d_sorted.data(), s.d_clust.data(), s.d_segtab.data(),
-                             s.d_count.data() + 1, stream_);
+                             s.d_count.data() + 1, stream_, rlog2_);
     PSOUP_HIP_CHECK(hipMemcpyAsync(s.h_segtab.data(), s.d_segtab.data(), 8ull * count * sizeof(uint2),
                                    hipMemcpyDeviceToHost, stream_));
     if (gpu_distill_) {

@@ -127,3 +127,88 @@ def test_engine_gpu_clustering_equals_host(C):
     assert cg["peaks"] == ch["peaks"]
     assert len(gpu) == len(host) and len(gpu) > 0
     assert gpu == host
+
+
+def _search_regions(C, trial, nsamps, accs, rlog2, min_snr):
+    p = C.SearchParams()
+    p.fft_size, p.tsamp, p.nharmonics, p.min_snr = 1 << 20, 64e-6, 4, min_snr
+    p.accel_batch, p.peak_region_log2 = 8, rlog2
+    eng = C.SearchEngine(p, torch.cuda.current_stream().cuda_stream)
+    c = eng.search_trial(trial.data_ptr(), nsamps, 10.0, 3, accs)
+    return [(x.dm_idx, x.acc, x.nh, x.snr, x.freq) for x in c], eng.counters()
+
+
+@pytest.mark.parametrize("min_snr", [6.0, 1.5])
+def test_engine_record_regions_equal_one_counter(C, min_snr):
+    """Threshold crossings in 64 record regions (SearchParams.peak_region_log2,
+    one reservation counter each) give the candidates of the single counter;
+    at S/N 1.5 the 8-trial batches overflow their regions (4096 records each)
+    and are recomputed with the capacity the fullest region asked for."""
+    rng = np.random.default_rng(9)
+    n = (1 << 20) + 512
+    t = np.arange(n) * 64e-6
+    x = rng.normal(128, 6, n)
+    for per, amp in ((0.00731, 30.0), (0.02, 60.0)):
+        ph = (t / per) % 1.0
+        x += amp * (np.minimum(ph, 1 - ph) < 0.015)
+    trial = torch.from_numpy(np.clip(np.rint(x), 0, 255).astype(np.uint8)).to(dev)
+    accs = [float(a) for a in np.linspace(-40, 40, 17)]
+    one, c1 = _search_regions(C, trial, n, accs, 0, min_snr)
+    reg, c6 = _search_regions(C, trial, n, accs, 6, min_snr)
+    assert c6["peaks"] == c1["peaks"] and c1["peaks"] > 50000, (c1, c6)
+    if min_snr < 4:
+        assert c6["overflows"] > 0, (c6["peaks"], c6["overflows"])
+    assert len(reg) == len(one) and len(one) > 0
+    assert reg == one
+
+
+def test_harmonic_regions_kernel_level(C):
+    """harmonic_peaks_batch with 8 record regions: every region's records are
+    whole chunks at absolute positions, the union equals the single-counter
+    records, and peak_regions_total reports the sum -- or, when a region
+    overflows, 8 x its count (more than the capacity)."""
+    from peasoup_amd import ops
+
+    K = C.kernels
+    rng = np.random.default_rng(12)
+    Kb, n = 16, 1 << 18
+    P = torch.from_numpy((rng.exponential(1.0, (Kb, n)) - 1.0).astype(np.float32)).to(dev)
+    starts, ends, thr = [3, 5, 9, 17], [n] * 4, 3.0
+    Q = ops.quantize_q8(P)
+    s = torch.cuda.current_stream().cuda_stream
+    ref = ops.harmonic_peaks(P, 3, starts, ends, thr, Q=Q, capacity=1 << 22)
+    nref = len(ref[0])
+    stride = int(K.peak_region_stride)
+    for cap, expect_overflow in ((8 * 4096 * 64, False), (8 * 256, True)):
+        rec = torch.zeros((cap, 3), dtype=torch.int32, device=dev)
+        cnt = torch.zeros(stride * 9, dtype=torch.int32, device=dev)
+        K.harmonic_peaks_batch(P.data_ptr(), n, n, Kb, 3, starts, ends, thr, cap, rec.data_ptr(),
+                               cnt.data_ptr() + 4 * stride, s, Q.data_ptr(), Q.shape[1], region_log2=3)
+        K.peak_regions_total(cnt.data_ptr() + 4 * stride, 3, cap, cnt.data_ptr(), s)
+        torch.cuda.synchronize()
+        c = cnt.cpu().numpy().view(np.uint32)
+        per = c[stride:stride * 9:stride]
+        capr = cap // 8
+        if expect_overflow:
+            assert per.max() > capr and int(c[0]) == 8 * int(per.max()) > cap
+            continue
+        assert per.max() <= capr and int(c[0]) == int(per.sum())
+        r = rec.cpu().numpy().view(np.uint32)
+        got = []
+        for g in range(8):
+            reg = r[g * capr:g * capr + per[g]]
+            i = 0
+            while i < len(reg):  # the region is a sequence of whole chunks
+                d = reg[i]
+                assert d[0] & 0x80000000
+                m = (d[0] >> 16) & 0x7F
+                assert int(d[2]) == g * capr + i + 1  # absolute position of its first crossing
+                body = reg[i + 1:i + 1 + m]
+                assert np.all(body[:, 0] == (d[0] & 0xFFFF))
+                got.extend(zip(body[:, 0].tolist(), body[:, 1].tolist(), body[:, 2].tolist()))
+                i += 1 + m
+        got.sort()
+        seg = (ref[0] * 8 + ref[1]).cpu().numpy()
+        exp = sorted(zip(seg.tolist(), ref[2].cpu().numpy().tolist(),
+                         ref[3].cpu().numpy().view(np.uint32).tolist()))
+        assert len(got) == nref and got == exp

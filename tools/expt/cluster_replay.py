@@ -28,7 +28,8 @@ def main():
     seg = recs[chunk, 0] & 0xFFFF
     cnt = (recs[chunk, 0] >> 16) & 0x7F
     per = np.bincount(seg, weights=cnt, minlength=nseg)
-    print(f"nseg {nseg} gap {gap} records {n} crossings {int(cnt.sum())}; segments > 4096: {(per > 4096).sum()}, "
+    print(f"nseg {nseg} gap {gap} records {n} chunks {int(chunk.sum())} crossings {int(cnt.sum())} "
+          f"({cnt.mean() if cnt.size else 0:.1f} per chunk); segments > 4096: {(per > 4096).sum()}, "
           f"> 14000: {(per > 14000).sum()}, max {int(per.max())}, mean of >4096: {per[per > 4096].mean() if (per > 4096).any() else 0:.0f}")
     dev = "cuda"
     cap = n + 100
