@@ -633,15 +633,21 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
   for (int q = 0; q < kTw; ++q) twv[q] = tab[to.ox + static_cast<uint64_t>(c0) * G + t + q * C::THREADS];
   const float afl = static_cast<float>(af), sizef = static_cast<float>(n);
   // fp32 shift estimate: |af p (p - n)| <= |af| n^2 / 4 with < 2.4e-7 relative
-  // error; exact float positions need n <= 2^24
-  const float band = n <= (1ull << 24) ? 6e-7f * fabsf(afl) * sizef * sizef * 0.25f + 1e-5f : 1.0f;
+  // error; exact float positions need n <= 2^24.  The row's other three
+  // samples p0 + e differ from it by |af e (2 p0 + e - n)| <= 3 |af| (n + 3)
+  // (~1.3e-3 at 2^23 and 500 m/s^2): a first estimate that far inside its
+  // rounding interval gives all four samples its shift -- one estimate per
+  // row, not one at each end.
+  const float band = n <= (1ull << 24) ? 6e-7f * fabsf(afl) * sizef * sizef * 0.25f + 1e-5f +
+                                             3.0003f * fabsf(afl) * (sizef + 3.0f)
+                                       : 1.0f;
 
   float2 va[P], vb[P];  // columns c0 + 2cp, c0 + 2cp + 1
   {
     // four consecutive resampled samples x[p0 .. p0+3] per row (resampleII):
-    // the shift rint(af p (p - n)) is estimated in fp32 at both ends; when
-    // both estimates are further than `band` (the fp32 error bound) from a
-    // rounding tie and equal, the samples share that shift and are one
+    // the shift rint(af p (p - n)) is estimated in fp32 at p0; when the
+    // estimate is further than `band` (the fp32 error bound plus the span's
+    // change) from a rounding tie, the samples share that shift and are one
     // 16-byte load of the padded input (32-bit buffer offsets); other rows
     // (rare: a shift step inside the four samples, a near-tie, a series edge)
     // are redone below with every index evaluated exactly in double
@@ -662,14 +668,13 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
       const uint32_t j = static_cast<uint32_t>(gg + G * m);
       const uint32_t col = static_cast<uint32_t>(c0 + 2 * cp);
       const uint32_t p0 = 2u * (static_cast<uint32_t>(N1) * j + col);
-      const float pa = static_cast<float>(p0), pb = pa + 3.0f;
-      const float fa = afl * pa * (pa - sizef), fb = afl * pb * (pb - sizef);
-      const float sa = rintf(fa), sb = rintf(fb);
+      const float pa = static_cast<float>(p0);
+      const float fa = afl * pa * (pa - sizef);
+      const float sa = rintf(fa);
       // (32-bit: p0 < 2^24 where the fast path can hold, |shift| << 2^30)
       const int first = static_cast<int>(p0 + static_cast<uint32_t>(static_cast<int>(sa)));  // (wrapping add)
       // (& not &&: the compiler turned the short circuit into a branch per row)
-      const bool ok = (sa == sb) & (fabsf(fa - sa) < 0.5f - band) & (fabsf(fb - sb) < 0.5f - band) & (first >= 0) &
-                      (first + 3 < static_cast<int>(nn));
+      const bool ok = (fabsf(fa - sa) < 0.5f - band) & (first >= 0) & (first + 3 < static_cast<int>(nn));
       const uint32_t i = ok ? static_cast<uint32_t>(first) : p0;
       const uint32_t row = i >> log2row, ic = i & rowmask;
       const uint32_t off = strips ? ((ic >> 4) * nrows + row) * kStripW + (ic & 15u) : row * pitch + ic;
