@@ -428,7 +428,16 @@ void sort_by_folded_snr(CandidateList& cands) {
 }
 
 // ------------------------------------------------------------ serialise ----
+// Two record forms.  The full one carries every field (folded candidates,
+// checkpoints); the compact one (magic "PSOD") only what a candidate has
+// before folding and scoring -- the DM, acceleration, harmonic, S/N and
+// frequency of each node and its association count -- 28 instead of 55 bytes
+// a node.  The multi-rank merge ships search-stage lists (peak-heavy ranks:
+// ~15 MB a step in the full form), so the compact form halves what is
+// gathered, and serialised and rebuilt on both ends.
 namespace {
+constexpr uint32_t kMagicFull = 0x50534F43u;     // "PSOC"
+constexpr uint32_t kMagicCompact = 0x50534F44u;  // "PSOD"
 #pragma pack(push, 1)
 struct NodeRec {
   float dm;
@@ -448,11 +457,41 @@ struct NodeRec {
   int32_t nfold;
   int32_t nassoc;
 };
+struct CompactRec {
+  float dm;
+  int32_t dm_idx;
+  float acc;
+  int32_t nh;
+  float snr;
+  float freq;
+  int32_t nassoc;
+};
 #pragma pack(pop)
 
 void put(std::vector<uint8_t>& out, const void* p, size_t n) {
   const uint8_t* b = static_cast<const uint8_t*>(p);
   out.insert(out.end(), b, b + n);
+}
+
+// no field beyond the compact record's set (bit patterns: -0.0 is not default)
+template <typename T>
+bool zero_bits(T v) {
+  unsigned char b[sizeof(T)];
+  std::memcpy(b, &v, sizeof(T));
+  for (unsigned char x : b)
+    if (x) return false;
+  return true;
+}
+bool search_stage(const Candidate& c) {
+  auto zero = [](float f) { return zero_bits(f); };
+  return zero(c.folded_snr) && zero_bits(c.opt_period) && !c.is_adjacent && !c.is_physical &&
+         zero(c.ddm_count_ratio) && zero(c.ddm_snr_ratio) && c.nbins == 0 && c.nints == 0 && c.fold.empty();
+}
+bool search_stage_tree(const Candidate& c) {
+  if (!search_stage(c)) return false;
+  for (const auto& a : c.assoc)
+    if (!search_stage_tree(a)) return false;
+  return true;
 }
 
 void ser_node(const Candidate& c, std::vector<uint8_t>& out) {
@@ -465,6 +504,18 @@ void ser_node(const Candidate& c, std::vector<uint8_t>& out) {
   for (const auto& a : c.assoc) ser_node(a, out);
 }
 
+void ser_compact(const Candidate& c, std::vector<uint8_t>& out) {
+  CompactRec r{c.dm, c.dm_idx, c.acc, c.nh, c.snr, c.freq, static_cast<int32_t>(c.assoc.size())};
+  put(out, &r, sizeof(r));
+  for (const auto& a : c.assoc) ser_compact(a, out);
+}
+
+size_t tree_nodes(const Candidate& c) {
+  size_t n = 1;
+  for (const auto& a : c.assoc) n += tree_nodes(a);
+  return n;
+}
+
 struct Reader {
   const uint8_t* p;
   size_t n, off = 0;
@@ -475,86 +526,78 @@ struct Reader {
   }
 };
 
+template <bool COMPACT>
 Candidate de_node(Reader& r, int depth) {
   PSOUP_CHECK(depth < 64, "candidate tree too deep");
-  NodeRec rec;
-  r.get(&rec, sizeof(rec));
-  Candidate c(rec.dm, rec.dm_idx, rec.acc, rec.nh, rec.snr, rec.freq);
-  c.folded_snr = rec.folded_snr;
-  c.opt_period = rec.opt_period;
-  c.is_adjacent = rec.is_adjacent != 0;
-  c.is_physical = rec.is_physical != 0;
-  c.ddm_count_ratio = rec.ddm_count_ratio;
-  c.ddm_snr_ratio = rec.ddm_snr_ratio;
-  c.nbins = rec.nbins;
-  c.nints = rec.nints;
-  PSOUP_CHECK(rec.nfold >= 0 && rec.nassoc >= 0, "corrupt candidate record");
-  if (rec.nfold > 0) {
-    c.fold.resize(static_cast<size_t>(rec.nfold));
-    r.get(c.fold.data(), c.fold.size() * sizeof(float));
+  if constexpr (COMPACT) {
+    CompactRec rec;
+    r.get(&rec, sizeof(rec));
+    PSOUP_CHECK(rec.nassoc >= 0, "corrupt candidate record");
+    Candidate c(rec.dm, rec.dm_idx, rec.acc, rec.nh, rec.snr, rec.freq);
+    c.assoc.reserve(static_cast<size_t>(rec.nassoc));
+    for (int i = 0; i < rec.nassoc; ++i) c.assoc.push_back(de_node<true>(r, depth + 1));
+    return c;
+  } else {
+    NodeRec rec;
+    r.get(&rec, sizeof(rec));
+    Candidate c(rec.dm, rec.dm_idx, rec.acc, rec.nh, rec.snr, rec.freq);
+    c.folded_snr = rec.folded_snr;
+    c.opt_period = rec.opt_period;
+    c.is_adjacent = rec.is_adjacent != 0;
+    c.is_physical = rec.is_physical != 0;
+    c.ddm_count_ratio = rec.ddm_count_ratio;
+    c.ddm_snr_ratio = rec.ddm_snr_ratio;
+    c.nbins = rec.nbins;
+    c.nints = rec.nints;
+    PSOUP_CHECK(rec.nfold >= 0 && rec.nassoc >= 0, "corrupt candidate record");
+    if (rec.nfold > 0) {
+      c.fold.resize(static_cast<size_t>(rec.nfold));
+      r.get(c.fold.data(), c.fold.size() * sizeof(float));
+    }
+    c.assoc.reserve(static_cast<size_t>(rec.nassoc));
+    for (int i = 0; i < rec.nassoc; ++i) c.assoc.push_back(de_node<false>(r, depth + 1));
+    return c;
   }
-  c.assoc.reserve(static_cast<size_t>(rec.nassoc));
-  for (int i = 0; i < rec.nassoc; ++i) c.assoc.push_back(de_node(r, depth + 1));
-  return c;
-}
-}  // namespace
-
-std::vector<uint8_t> serialize_candidates(const CandidateList& cands) {
-  std::vector<const Candidate*> p;
-  p.reserve(cands.size());
-  for (const auto& c : cands) p.push_back(&c);
-  return serialize_candidates(p);
 }
 
-std::vector<uint8_t> serialize_candidates(const std::vector<const Candidate*>& cands) {
-  std::vector<uint8_t> out;
-  uint32_t magic = 0x50534F43u;  // "PSOC"
-  int64_t n = static_cast<int64_t>(cands.size());
-  put(out, &magic, 4);
-  put(out, &n, 8);
-  for (const Candidate* c : cands) ser_node(*c, out);
-  return out;
-}
-
-namespace {
 // past one record and its subtree (headers only): the byte offsets of the
 // top-level records, so their subtrees can be rebuilt in parallel
+template <bool COMPACT>
 void skip_node(Reader& r, int depth) {
   PSOUP_CHECK(depth < 64, "candidate tree too deep");
-  NodeRec rec;
-  r.get(&rec, sizeof(rec));
-  PSOUP_CHECK(rec.nfold >= 0 && rec.nassoc >= 0, "corrupt candidate record");
-  PSOUP_CHECK(r.off + static_cast<size_t>(rec.nfold) * sizeof(float) <= r.n, "truncated candidate stream");
-  r.off += static_cast<size_t>(rec.nfold) * sizeof(float);
-  for (int i = 0; i < rec.nassoc; ++i) skip_node(r, depth + 1);
+  if constexpr (COMPACT) {
+    CompactRec rec;
+    r.get(&rec, sizeof(rec));
+    PSOUP_CHECK(rec.nassoc >= 0, "corrupt candidate record");
+    for (int i = 0; i < rec.nassoc; ++i) skip_node<true>(r, depth + 1);
+  } else {
+    NodeRec rec;
+    r.get(&rec, sizeof(rec));
+    PSOUP_CHECK(rec.nfold >= 0 && rec.nassoc >= 0, "corrupt candidate record");
+    PSOUP_CHECK(r.off + static_cast<size_t>(rec.nfold) * sizeof(float) <= r.n, "truncated candidate stream");
+    r.off += static_cast<size_t>(rec.nfold) * sizeof(float);
+    for (int i = 0; i < rec.nassoc; ++i) skip_node<false>(r, depth + 1);
+  }
 }
-}  // namespace
 
-void deserialize_candidates_into(const uint8_t* data, size_t nbytes, CandidateList& out) {
-  if (nbytes == 0) return;
-  Reader r{data, nbytes};
-  uint32_t magic = 0;
-  int64_t n = 0;
-  r.get(&magic, 4);
-  PSOUP_CHECK(magic == 0x50534F43u, "bad candidate stream magic");
-  r.get(&n, 8);
-  PSOUP_CHECK(n >= 0, "bad candidate count");
+template <bool COMPACT>
+void deserialize_body(const uint8_t* data, size_t nbytes, Reader& r, int64_t n, CandidateList& out) {
   const size_t base = out.size();
   // Large streams (a merge of 138k candidates carrying 1.6M associated ones:
   // ~100 MB) are rebuilt on several threads: one header-only pass finds each
   // top-level record, then contiguous ranges of records are deserialised in
   // parallel straight into their final positions.
   const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-  if (nbytes < (16u << 20) || hw == 1 || n < 1024) {
+  if (nbytes < (8u << 20) || hw == 1 || n < 1024) {
     out.reserve(base + static_cast<size_t>(n));
-    for (int64_t i = 0; i < n; ++i) out.push_back(de_node(r, 0));
+    for (int64_t i = 0; i < n; ++i) out.push_back(de_node<COMPACT>(r, 0));
     PSOUP_CHECK(r.off == nbytes, "trailing bytes after the candidate stream");
     return;
   }
   std::vector<size_t> at(static_cast<size_t>(n) + 1);
   for (int64_t i = 0; i < n; ++i) {
     at[static_cast<size_t>(i)] = r.off;
-    skip_node(r, 0);
+    skip_node<COMPACT>(r, 0);
   }
   at[static_cast<size_t>(n)] = r.off;
   PSOUP_CHECK(r.off == nbytes, "trailing bytes after the candidate stream");
@@ -571,7 +614,7 @@ void deserialize_candidates_into(const uint8_t* data, size_t nbytes, CandidateLi
                                 : static_cast<size_t>(std::lower_bound(at.begin(), at.end() - 1, hi) - at.begin());
         for (size_t i = i0; i < i1; ++i) {
           Reader rr{data, nbytes, at[i]};
-          out[base + i] = de_node(rr, 0);
+          out[base + i] = de_node<COMPACT>(rr, 0);
         }
       } catch (...) {
         err[t] = std::current_exception();
@@ -580,6 +623,51 @@ void deserialize_candidates_into(const uint8_t* data, size_t nbytes, CandidateLi
   for (auto& x : th) x.join();
   for (auto& e : err)
     if (e) std::rethrow_exception(e);
+}
+}  // namespace
+
+std::vector<uint8_t> serialize_candidates(const CandidateList& cands) {
+  std::vector<const Candidate*> p;
+  p.reserve(cands.size());
+  for (const auto& c : cands) p.push_back(&c);
+  return serialize_candidates(p);
+}
+
+std::vector<uint8_t> serialize_candidates(const std::vector<const Candidate*>& cands) {
+  std::vector<uint8_t> out;
+  bool compact = true;
+  size_t nodes = 0;
+  for (const Candidate* c : cands) {
+    if (compact && !search_stage_tree(*c)) compact = false;
+    nodes += tree_nodes(*c);
+  }
+  out.reserve(12 + nodes * (compact ? sizeof(CompactRec) : sizeof(NodeRec)));
+  const uint32_t magic = compact ? kMagicCompact : kMagicFull;
+  int64_t n = static_cast<int64_t>(cands.size());
+  put(out, &magic, 4);
+  put(out, &n, 8);
+  for (const Candidate* c : cands) {
+    if (compact)
+      ser_compact(*c, out);
+    else
+      ser_node(*c, out);
+  }
+  return out;
+}
+
+void deserialize_candidates_into(const uint8_t* data, size_t nbytes, CandidateList& out) {
+  if (nbytes == 0) return;
+  Reader r{data, nbytes};
+  uint32_t magic = 0;
+  int64_t n = 0;
+  r.get(&magic, 4);
+  PSOUP_CHECK(magic == kMagicFull || magic == kMagicCompact, "bad candidate stream magic");
+  r.get(&n, 8);
+  PSOUP_CHECK(n >= 0, "bad candidate count");
+  if (magic == kMagicCompact)
+    deserialize_body<true>(data, nbytes, r, n, out);
+  else
+    deserialize_body<false>(data, nbytes, r, n, out);
 }
 
 CandidateList deserialize_candidates(const uint8_t* data, size_t nbytes) {

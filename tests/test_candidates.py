@@ -229,3 +229,39 @@ def test_merge_candidate_blobs_equals_python_merge(C):
     exp = C.global_distill_and_score(cands, args, hdr)
     assert len(got) > 5
     assert C.serialize_candidates(got) == C.serialize_candidates(exp)
+
+
+def test_compact_serialisation_of_search_stage_lists(C):
+    """Lists of unfolded, unscored candidates use the 28-byte compact record
+    (magic PSOD) and round-trip field for field; any folded or scored node
+    switches the whole stream to the full form.  Streams over 8 MB rebuild on
+    several threads (both forms)."""
+    rng = random.Random(11)
+
+    def tree(depth):
+        c = C.Candidate(rng.uniform(0, 500), rng.randrange(0, 3000), rng.uniform(-500, 500), rng.randrange(0, 5),
+                        rng.uniform(6, 60), rng.uniform(0.1, 900))
+        if depth < 2:
+            c.assoc = [tree(depth + 1) for _ in range(rng.randrange(0, 4))]
+        return c
+
+    def nodes(c):
+        return 1 + sum(nodes(a) for a in c.assoc)
+
+    def fields(c):
+        return ((c.dm, c.dm_idx, c.acc, c.nh, c.snr, c.freq, c.folded_snr, c.opt_period, c.is_adjacent,
+                 c.is_physical, c.ddm_count_ratio, c.ddm_snr_ratio, c.nbins, c.nints, list(c.fold)),
+                [fields(a) for a in c.assoc])
+
+    for n in (50, 80000):  # the second one: a > 8 MB stream in both forms
+        lst = [tree(0) for _ in range(n)]
+        blob = C.serialize_candidates(lst)
+        assert blob[:4] == b"DOSP" and len(blob) == 12 + 28 * sum(map(nodes, lst))
+        back = C.deserialize_candidates(blob)
+        assert [fields(c) for c in back] == [fields(c) for c in lst]
+        lst[n // 2].assoc[0].folded_snr = 12.5 if lst[n // 2].assoc else 0.0
+        lst[n // 3].is_physical = True
+        full = C.serialize_candidates(lst)
+        assert full[:4] == b"COSP" and len(full) > len(blob)
+        back = C.deserialize_candidates(full)
+        assert [fields(c) for c in back] == [fields(c) for c in lst]
