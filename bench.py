@@ -166,7 +166,7 @@ def main() -> int:
     tot = torch.tensor([trials_per_step_local], dtype=torch.int64, device=dev)
     trials_per_step = int(pdist.all_reduce_sum(tot).item())
 
-    phase = {"search": 0.0, "merge": 0.0, "ser": 0.0, "gather": 0.0, "gds": 0.0}
+    phase = {"search": 0.0, "merge": 0.0, "ser": 0.0, "wait": 0.0, "gather": 0.0, "gds": 0.0}
     # Steps are pipelined like the production run's DM blocks: step k's
     # candidate gather + global distillation (one worker thread, so the
     # gather collectives stay in order) overlaps step k+1's dedispersion and
@@ -189,8 +189,12 @@ def main() -> int:
         else:
             blob = torch.from_numpy(_C.serialize_candidates_array(local))
             t2 = time.perf_counter()
-            bufs = pdist.gather_buffers(blob, dst=0)
+            tm = {}
+            bufs = pdist.gather_buffers(blob, dst=0, timing=tm)
             t3 = time.perf_counter()
+            # the size exchange is where a rank waits for the slowest peer to
+            # reach this step's merge (rank skew, not merge work)
+            phase["wait"] += tm.get("sizes_done", t2) - t2
             phase["blob_bytes"] = blob.numel()
             out = (_C.merge_candidate_buffers([(b.data_ptr(), b.numel()) for b in bufs], args, rs.header)
                    if ctx.is_root else _C.CandidateBag())
@@ -237,7 +241,7 @@ def main() -> int:
         finish(r)
     for e in rs.engines:
         e.reset_counters()
-    phase.update(search=0.0, merge=0.0, ser=0.0, gather=0.0, gds=0.0)
+    phase.update(search=0.0, merge=0.0, ser=0.0, wait=0.0, gather=0.0, gds=0.0)
     pdist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -293,9 +297,11 @@ def main() -> int:
                 # acceleration loop, then the candidate gather + global distillation
                 "search_s_per_step": round(phase["search"] / a.steps, 4),
                 "merge_s_per_step": round(phase["merge"] / a.steps, 4),
+                # the merge without the wait for the slowest rank at its first collective
+                "merge_work_s_per_step": round((phase["merge"] - phase["wait"]) / a.steps, 4),
                 "merge_overlapped": not a.serial_merge,
                 "steps_pipelined": not a.serial_steps,
-                "merge_split_s": {k: round(phase[k] / a.steps, 4) for k in ("ser", "gather", "gds")},
+                "merge_split_s": {k: round(phase[k] / a.steps, 4) for k in ("ser", "wait", "gather", "gds")},
                 "candidate_blob_bytes": phase.get("blob_bytes", 0),
                 "accel_s_per_step": round(ctr.get("accel_s", 0) / a.steps, 4),
                 "accel_distill_s_per_step": round(ctr.get("accd_s", 0) / a.steps, 4),

@@ -312,12 +312,14 @@ def gather_bytes(payload: bytes, dst: Optional[int] = 0) -> Optional[List[bytes]
     return [bytes(o[:s].cpu().numpy().tobytes()) for o, s in zip(outs, sizes_i)]
 
 
-def gather_buffers(payload: torch.Tensor, dst: int = 0) -> Optional[List[torch.Tensor]]:
+def gather_buffers(payload: torch.Tensor, dst: int = 0, timing: Optional[dict] = None) -> Optional[List[torch.Tensor]]:
     """Variable-length gather of host uint8 tensors to ``dst`` only (sizes
     all-gathered, then one padded ``dist.gather``; RCCL on GPUs): the list of
     every rank's buffer (host tensors, rank order) on ``dst``, None elsewhere.
     Unlike :func:`gather_bytes` nothing reaches the other ranks and no Python
-    ``bytes`` objects are made (candidate lists are tens of MB per rank)."""
+    ``bytes`` objects are made (candidate lists are tens of MB per rank).
+    ``timing``: gets ``"sizes_done"`` (perf_counter after the size exchange,
+    which is also where this rank waits for the slowest peer to arrive)."""
     ctx = context()
     assert payload.dtype == torch.uint8 and payload.dim() == 1
     if not ctx.distributed:
@@ -327,6 +329,8 @@ def gather_buffers(payload: torch.Tensor, dst: int = 0) -> Optional[List[torch.T
     sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(ctx.world_size)]
     dist.all_gather(sizes, n)
     sizes_i = [int(s.item()) for s in sizes]
+    if timing is not None:
+        timing["sizes_done"] = time.perf_counter()
     mx = max(1, max(sizes_i))
     buf = torch.zeros(mx, dtype=torch.uint8, device=dev)
     if payload.numel():

@@ -11,6 +11,6 @@ for w in 2 4; do
   for sig in "" "--peak-heavy"; do
     tag=w${w}${sig:+_signal}
     timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node $w --master-addr 127.0.0.1 --master-port $((29600 + w)) bench.py --gpus $w --steps 3 --warmup 1 $sig > $O/$tag.log 2>&1 || { echo FAIL_$tag; tail -20 $O/$tag.log; exit 1; }
-    grep '^{"metric"' $O/$tag.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['config']; print('$tag', d['value'], d['ms_per_step'], 'merge', c['merge_s_per_step'], c['merge_split_s'], 'blob', c['candidate_blob_bytes'])"
+    grep '^{"metric"' $O/$tag.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); c=d['config']; print('$tag', d['value'], d['ms_per_step'], 'merge', c['merge_s_per_step'], 'work', c['merge_work_s_per_step'], c['merge_split_s'], 'blob', c['candidate_blob_bytes'])"
   done
 done
