@@ -864,13 +864,13 @@ __device__ __forceinline__ float2 x_canon(const float2* __restrict__ z, uint32_t
 // recomputed from the tiled spectrum X (HarmFromX), 2: the blocked P of
 // fft4_rowpass_spectrum (spec_pblk_index).  Q rows start fx.qshift bytes
 // before bin 0 (staging chunks stay 16-byte aligned in memory).
+// (waves_per_eu(7): the register budget of 7 waves per SIMD; the allocator
+// then fits 64 VGPRs, 8 waves, where it took 80 unconstrained)
 template <int NLEV, int BPT, int SRC>
-__global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __restrict__ P, uint64_t pstride,
-                                                                const uint8_t* __restrict__ Q, uint64_t qstride,
-                                                                int lo, int hi, HarmParams hp,
-                                                                PeakRecord* __restrict__ out,
-                                                                uint32_t* __restrict__ count, int ntiles,
-                                                                int xcd_trials, HarmLim lim, HarmFromX fx) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7)))
+harmonic_peaks_q8_kernel(const float* __restrict__ P, uint64_t pstride, const uint8_t* __restrict__ Q,
+                         uint64_t qstride, int lo, int hi, HarmParams hp, PeakRecord* __restrict__ out,
+                         uint32_t* __restrict__ count, int ntiles, int xcd_trials, HarmLim lim, HarmFromX fx) {
   using Tl = HarmTileQ<NLEV, BPT>;
   constexpr int B = Tl::B;
   __shared__ __attribute__((aligned(16))) uint8_t lds[Tl::TOTAL];
@@ -892,10 +892,36 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
   const int b0 = lo + tile * B;
   const int last = hi - 1;
   int fund[BPT];
+  // Interior tiles (block-uniform b0 + B <= hi: every bin and every staged
+  // range below hi) load without clamps: one per-thread offset, the rest
+  // scalar bases and immediate offsets (the clamped forms took ~100 VALU of
+  // a wave's ~400).
+  const bool interior = b0 + B <= hi;
+  uint4 tmp[Tl::ITERS];
+  if (interior) {
+    const uint8_t* qf = q + (b0 + t);
 #pragma unroll
-  for (int u = 0; u < BPT; ++u) fund[u] = q[min(b0 + t + 256 * u, last)];
-  {
-    uint4 tmp[Tl::ITERS];
+    for (int u = 0; u < BPT; ++u) fund[u] = qf[256 * u];
+    // the row as a buffer resource (base in SGPRs): a range's uniform start
+    // goes in the scalar offset, the thread's 16 t in the vector one
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(q - qs), 0, 0x7fffffff, 0x00020000);
+    const uint32_t vo = 16u * static_cast<uint32_t>(t);
+    int it = 0;
+#pragma unroll
+    for (int h = 1; h <= NLEV; ++h) {
+#pragma unroll
+      for (int m = 1; m < (1 << h); m += 2) {
+        // byte offset of the range's first chunk from the row start (16-byte aligned, >= 0)
+        const int r0 = ((((b0 * m + (1 << (h - 1))) >> h) + qs) & ~15);
+#pragma unroll
+        for (int e = 0; e < (Tl::chunks(h, m) + 255) / 256; ++e, ++it)
+          tmp[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 4096u * e, r0, 0));
+      }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < BPT; ++u) fund[u] = q[min(b0 + t + 256 * u, last)];
     int it = 0;
 #pragma unroll
     for (int h = 1; h <= NLEV; ++h) {
@@ -907,7 +933,9 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
           tmp[it] = load_q16(q, r0 + 16 * (t + 256 * e), last);
       }
     }
-    it = 0;
+  }
+  {
+    int it = 0;
 #pragma unroll
     for (int h = 1; h <= NLEV; ++h) {
 #pragma unroll
@@ -986,8 +1014,13 @@ __global__ void __launch_bounds__(256) harmonic_peaks_q8_kernel(const float* __r
       cand = cand | (sq > lim.v[5]);
     }
 #undef PS_QTERM
-    cand = (cand | (mx >= 254)) & (i < hi);
+    cand = cand | (mx >= 254);
     cm |= cand ? (1u << u) : 0u;
+  }
+  if (b0 + B > hi) {  // the last tile (block-uniform): its bins at or past hi are not searched
+#pragma unroll
+    for (int u = 0; u < BPT; ++u)
+      if (i0 + u * 256 >= hi) cm &= ~(1u << u);
   }
   if (__ballot(cm != 0u) == 0ull) return;  // the usual no-peak case: the whole wave is done
   // exact sums, one bin group at a time (not unrolled: the exact path is rare)
