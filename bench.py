@@ -45,8 +45,8 @@ BASELINE_TRIALS_PER_S = 6.6  # 573 trials/s @2^17 scaled by N log N
 def parse():
     p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=3)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--log2n", type=int, default=23, help="FFT length = 2^log2n")
     p.add_argument("--nchans", type=int, default=1024)
     p.add_argument("--nbits", type=int, default=2)
