@@ -902,10 +902,9 @@ harmonic_peaks_q8_kernel(const float* __restrict__ P, uint64_t pstride, const ui
     const uint8_t* qf = q + (b0 + t);
 #pragma unroll
     for (int u = 0; u < BPT; ++u) fund[u] = qf[256 * u];
-    // the row as a buffer resource (base in SGPRs): a range's uniform start
-    // goes in the scalar offset, the thread's 16 t in the vector one
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(q - qs), 0, 0x7fffffff, 0x00020000);
+    // each range as a buffer resource built in SGPRs (base = its first chunk,
+    // num_records = the rest of the row: a load past the row returns zeros),
+    // the thread's 16 t as the vector offset
     const uint32_t vo = 16u * static_cast<uint32_t>(t);
     int it = 0;
 #pragma unroll
@@ -914,9 +913,13 @@ harmonic_peaks_q8_kernel(const float* __restrict__ P, uint64_t pstride, const ui
       for (int m = 1; m < (1 << h); m += 2) {
         // byte offset of the range's first chunk from the row start (16-byte aligned, >= 0)
         const int r0 = ((((b0 * m + (1 << (h - 1))) >> h) + qs) & ~15);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint8_t*>(q - qs + r0), 0, static_cast<int>(qstride) - r0, 0x00020000);
+        // (only the range's chunks: the threads past them would read up to 4 KiB beyond it)
 #pragma unroll
         for (int e = 0; e < (Tl::chunks(h, m) + 255) / 256; ++e, ++it)
-          tmp[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 4096u * e, r0, 0));
+          if (t + 256 * e < Tl::chunks(h, m))
+            tmp[it] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo + 4096u * e, 0, 0));
       }
     }
   } else {
