@@ -226,7 +226,7 @@ static std::vector<Spec> peasoup_specs(CmdLineOptions& a) {
       // MI355X-native extensions
       val_s("", "accel_convention", "Acceleration-plan unit convention: legacy (default, golden) | reference",
             a.accel_convention),
-      val_s("", "dedisp_kernel", "Dedispersion kernel: auto | mfma | valu | direct", a.dedisp_kernel),
+      val_s("", "dedisp_kernel", "Dedispersion kernel: auto | mfma | valu | direct | packed2", a.dedisp_kernel),
       val_n("", "accel_batch", "Acceleration trials per batched FFT (0 = auto)", a.accel_batch),
       val_n("", "engines_per_gpu",
             "Search engines per GPU, each on its own stream and host thread, dealt every N-th DM of a chunk "
@@ -324,7 +324,7 @@ bool parse_ffa_cmdline(FfaCmdLineOptions& a, const std::vector<std::string>& arg
       val_n("", "bins", "Base bins per period (periods span [bins, 2 bins)); 0 = from --min_dc", a.nbins),
       val_n("", "limit", "Upper limit on the number of candidates written", a.limit),
       val_n("", "cluster_tol", "Peak clustering tolerance in units of 1/T_obs", a.cluster_tol),
-      val_s("", "dedisp_kernel", "Dedispersion kernel: auto | mfma | valu | direct", a.dedisp_kernel),
+      val_s("", "dedisp_kernel", "Dedispersion kernel: auto | mfma | valu | direct | packed2", a.dedisp_kernel),
   };
   return run_parser(specs, argv, "Peasoup/FFAster extension - a GPU FFA pulsar search pipeline", nullptr, exit_now);
 }
