@@ -906,7 +906,7 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   }
   sub_ = mode_ != 2 ? 0 : p_.sub_batch >= 0 ? p_.sub_batch : sub_auto;
   if (sub_ >= K_) sub_ = 0;
-  {
+  if (sub_ > 0) {  // (only the sub-batch pipeline uses them: a stream is a hardware queue, ~3-7 ms to create)
     const int ns = std::max(2, p_.sub_streams);
     for (int i = 1; i < ns; ++i) {
       aux_.push_back(std::make_unique<Stream>());
