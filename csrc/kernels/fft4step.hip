@@ -992,8 +992,11 @@ fft4_rowpass_spectrum_kernel(const float2* __restrict__ Y, int K, Fft4Geom g, co
       pp[j] = dev::div_rn(amp(X[j + 1], X[j]) - mean2, sigma2, rsig2);
       pm[j] = dev::div_rn(amp(Xm[j], Xm[j + 1]) - mean2, sigma2, rsig2);
     }
-    if (wf) pk[2 * v * L + k1] = make_float4(pp[0], pp[1], pp[2], pp[3]);
-    if (wm) pk[(2 * v + 1) * L + k1] = make_float4(pm[0], pm[1], pm[2], pm[3]);
+    // (P streams out: only candidate bins are read back, much later; non-temporal
+    // stores leave L2 to the Q lines still being assembled and the Y reads)
+    if (wf) __builtin_nontemporal_store(f4v{pp[0], pp[1], pp[2], pp[3]}, reinterpret_cast<f4v*>(pk + 2 * v * L + k1));
+    if (wm)
+      __builtin_nontemporal_store(f4v{pm[0], pm[1], pm[2], pm[3]}, reinterpret_cast<f4v*>(pk + (2 * v + 1) * L + k1));
     // screening bytes (dev::q8): t = rint(4 p) + 127 -> t in [0, 253] as is,
     // >= 254 or NaN -> 254, <= -1 -> 255 (min first: NaN -> 254)
     auto qb = [](float p) {
