@@ -70,6 +70,7 @@ template <int CPT>
 using Vec = float2[CPT][kPts];
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned 16-byte load
 typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int lds_pad(int x) { return x + (x >> 3); }
 using namespace dreg;  // butterflies, packed complex arithmetic, dft<N> (dft_reg.hpp)
@@ -725,10 +726,13 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
     for (int k2 = 0; k2 < G; ++k2) {
       const float2 wv = k2 == 0 ? om : cmul(om, twr[k2]);
       const uint32_t kk = k1 + static_cast<uint32_t>(P * k2);
-      if (g.ypair)  // Y_p[kk/2][col][kk%2]: per wave instruction four whole 128-byte lines
-        yp[(kk >> 1) * (2 * static_cast<uint32_t>(N1)) + (kk & 1)] = cmul(u[p][k2], wv);
-      else
-        yk[(kk >> 3) * 64 + static_cast<uint32_t>(rc) * 8 + (kk & 7)] = cmul(u[p][k2], wv);
+      // (non-temporal: Y is read back only by the spectrum pass after the whole
+      // batch, far beyond the caches; L2 and the Infinity Cache are left to the
+      // input series every trial of a DM re-reads)
+      const float2 yv = cmul(u[p][k2], wv);
+      float2* dst = g.ypair ? yp + (kk >> 1) * (2 * static_cast<uint32_t>(N1)) + (kk & 1)  // Y_p[kk/2][col][kk%2]
+                            : yk + (kk >> 3) * 64 + static_cast<uint32_t>(rc) * 8 + (kk & 7);
+      __builtin_nontemporal_store(f2v{yv.x, yv.y}, reinterpret_cast<f2v*>(dst));
     }
   }
   trace_event(11);
