@@ -184,18 +184,21 @@ struct SearchParams {
   int accel_batch = 0;          // 0 = auto
   int sub_batch = -1;           // fused-FFT trials per sub-batch on alternating streams (0 = off, -1 = auto)
   int host_threads = -1;        // host workers clustering/distilling peak-heavy batches (-1 = auto, 0/1 = serial)
-  // auto-batch HBM budget (1024 trials of 2^23: 56 GB of intermediates --
-  // Y, P, Q -- on a 288 GB device; same-box sweep of the round-5 bench: K =
-  // 1024 34.45k/34.38k, 1376 33.72k/33.61k, 768 33.80k/33.83k, 512
-  // 33.30k/33.38k trials/s, profiles/r5_batch/), capped at 70% of the
-  // device's free memory shared among its engines
-  size_t batch_bytes = 64ull << 30;
+  // auto-batch HBM budget (2048 trials of 2^23: 112 GB of intermediates --
+  // Y, P, Q -- on a 288 GB device; same-box sweep of the round-5 bench with
+  // the non-temporal Y / P stores: K = 2048 36.23k/36.19k, 1536
+  // 36.15k/36.13k, 1024 35.81k/35.67k, 768 35.84k/35.89k trials/s,
+  // profiles/r5_batch/), capped at 70% of the device's free memory shared
+  // among its engines
+  size_t batch_bytes = 128ull << 30;
   // Engines sharing the device: the auto budget is also capped at 70% of the
   // device's free memory divided by this count.
   int engines_per_device = 1;
   // Auto batching of short trial lists: lists shorter than min_batches full
   // batches are cut into min_batches even batches (multiples of 8), but never
   // below the batch an eighth of the budget gives.
+  // (4: the bench's 8-DM lists of 5480 trials at 2^23 run as 4 x 1376; 3 x
+  // 1832 was 0.6% faster on noise but put peak-heavy data below 90% of it)
   int min_batches = 4;
   // Threshold-crossing records in 2^peak_region_log2 regions with a counter
   // each (kern::kPeakRegionStride) when the device clusters them: the

@@ -880,9 +880,9 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b > 0)
       budget = std::min(budget, free_b / 10 * 7 / static_cast<size_t>(std::max(1, p_.engines_per_device)));
     const size_t per = n_ * 4 + (fused_ ? 0 : nb_ * 8) + (fromx_ ? 0 : pst_ * 4) + qst_;  // Y/res + X/spec + P + Q per trial
-    // at most 1024 trials per batch from 2^23 samples up, 256 below (the
+    // at most 2048 trials per batch from 2^23 samples up, 256 below (the
     // shorter series were only measured up to 256)
-    const size_t kmax = n_ >= (uint64_t(1) << 23) ? 1024 : 256;
+    const size_t kmax = n_ >= (uint64_t(1) << 23) ? 2048 : 256;
     auto round_batch = [kmax](size_t k) {
       int K = static_cast<int>(std::min<size_t>(kmax, std::max<size_t>(1, k)));
       if (K >= 32) K = K / 16 * 16;  // halves stay multiples of 8 (XCD-grouped kernels)
@@ -890,7 +890,7 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
       return K;
     };
     K_ = p_.accel_batch > 0 ? p_.accel_batch : round_batch(budget / per);
-    k_small_ = std::min(K_, std::max(16, round_batch(budget / 8 / per)));  // 144 at 2^23
+    k_small_ = std::min(K_, std::max(16, round_batch(budget / 8 / per)));  // 304 at 2^23
   }
   // Auto: sub-batches on alternating streams, half a batch but at most 2^28
   // samples -- below 2^22 samples only.  At 2^23 they were +4-5% in round 1
@@ -1356,8 +1356,8 @@ int SearchEngine::batch_for(int ntr) const {
   // Short trial lists (one DM at 2^23: 685 trials) keep at least min_batches
   // (SearchParams::min_batches, default 4) batches in the two-slot pipeline so
   // host clustering still overlaps the GPU, but never fall below k_small_
-  // (the batch an eighth of the budget gives: 144 at 2^23 with the default
-  // 64 GiB, rounded like K_).
+  // (the batch an eighth of the budget gives: 304 at 2^23 with the default
+  // 128 GiB, rounded like K_).
   const int min_batches = std::max(1, p_.min_batches);
   if (p_.accel_batch <= 0 && ntr < min_batches * K_) {
     const int even = (ntr + min_batches - 1) / min_batches;
@@ -1480,8 +1480,8 @@ std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(
   // Short trial lists (one DM at 2^23: 685 trials) keep at least min_batches
   // (SearchParams::min_batches, default 4) batches in the two-slot pipeline so
   // host clustering still overlaps the GPU, but never fall below k_small_
-  // (the batch an eighth of the budget gives: 144 at 2^23 with the default
-  // 64 GiB, rounded like K_).
+  // (the batch an eighth of the budget gives: 304 at 2^23 with the default
+  // 128 GiB, rounded like K_).
   const int kc = batch_for(ntr);
   last_kc_ = kc;
   ensure_batch_buffers(std::min(kc, ntr));
