@@ -287,6 +287,8 @@ def main() -> int:
                 "dms_per_gpu": a.dms_per_gpu,
                 "accel_trials_per_dm": trials_per_step_local // a.dms_per_gpu,
                 "accel_batch": rs.engine.batch_size,
+                # the batch the last launch used (short lists are cut into min_batches even batches)
+                "accel_batch_used": rs.engine.last_batch,
                 "sub_batch": rs.engine.sub_batch,
                 "fft_mode": rs.engine.fft_mode,
                 "candidates_after_distill": ncands,
