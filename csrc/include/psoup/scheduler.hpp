@@ -215,7 +215,19 @@ class ChunkScheduler {
         if (prev.slot >= 0) finalize(dev, eng, prev);
         prev = std::move(cur);
       }
-      if (prev.slot >= 0 && !abort_.load()) finalize(dev, eng, prev);
+      if (prev.slot >= 0) {
+        if (!abort_.load()) {
+          finalize(dev, eng, prev);
+        } else {
+          // another thread failed: this engine's share of the previous chunk
+          // was issued whole, so finalize it too; the chunk is handed over
+          // (checkpointed) once every engine has, whichever of them fails
+          try {
+            finalize(dev, eng, prev);
+          } catch (...) {  // the first failure is the one reported
+          }
+        }
+      }
       if (!abort_.load()) ops_.engine_exit(dev, eng);
     } catch (...) {
       fail();

@@ -226,17 +226,20 @@ PYBIND11_MODULE(_C, m) {
           py::arg("off"), py::arg("n"), py::arg("dst"), py::arg("nthreads") = 4, py::call_guard<py::gil_scoped_release>())
       .def(
           "upload",
-          [](const Filterbank& fb, uintptr_t dptr, uint64_t nbytes, uintptr_t stream) {
-            // the data block -> device (threaded pread into two pinned 16 MB
-            // stages, copies overlapping the reads); returns when it landed
-            const uint64_t n = nbytes ? nbytes : fb.data_bytes();
-            PSOUP_CHECK(n <= fb.data_bytes(), "upload: more bytes than the data block");
+          [](const Filterbank& fb, uintptr_t dptr, uint64_t nbytes, uint64_t dst_bytes, uintptr_t stream) {
+            // the first nbytes of the data block -> a device buffer of
+            // dst_bytes (threaded pread into two pinned 16 MB stages, copies
+            // overlapping the reads); returns when it landed.  0 bytes: no-op
+            PSOUP_CHECK(nbytes <= fb.data_bytes(), "upload: more bytes than the data block");
+            PSOUP_CHECK(nbytes <= dst_bytes, "upload: more bytes than the destination holds");
+            if (nbytes == 0) return;
             auto s = reinterpret_cast<hipStream_t>(stream);
-            staged_upload(n, 16ull << 20, [&fb](uint64_t o, uint64_t k, uint8_t* d) { fb.read_data(o, k, d); },
+            staged_upload(nbytes, 16ull << 20, [&fb](uint64_t o, uint64_t k, uint8_t* d) { fb.read_data(o, k, d); },
                           P<uint8_t>(dptr), s);
             PSOUP_HIP_CHECK(hipStreamSynchronize(s));
           },
-          py::arg("dptr"), py::arg("nbytes") = 0, py::arg("stream") = 0, py::call_guard<py::gil_scoped_release>())
+          py::arg("dptr"), py::arg("nbytes"), py::arg("dst_bytes"), py::arg("stream") = 0,
+          py::call_guard<py::gil_scoped_release>())
       .def("data", [](const Filterbank& fb) {
         // zero-copy read-only view of the mmapped data block
         py::array_t<uint8_t> a({static_cast<py::ssize_t>(fb.data_bytes())}, {1}, fb.data(), py::cast(fb));

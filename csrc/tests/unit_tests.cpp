@@ -276,6 +276,7 @@ namespace {
 struct FakeRun {
   int ndev, neng, ndm, chunk;
   int fault_after = -1;  // issue() throws once this many DMs were issued
+  int fault_d0 = -1;     // prepare() (the feeder) throws on the chunk starting here
   bool racy = false;
   std::mutex mu;
   std::map<int, int> handed;                // DM -> times handed over
@@ -293,6 +294,7 @@ struct FakeRun {
     using Chunk = SchedChunk<int>;
     ops.prepare = [&](int dev, int k, Chunk& c) {
       nap(150);
+      if (c.d0 == fault_d0) throw std::runtime_error("fault injection");
       if (resumed_chunk(c.d0, chunk)) {  // a spill: results without any search
         c.resumed = true;
         for (int d = c.d0; d < c.d1; ++d) c.items.push_back(d);
@@ -359,6 +361,19 @@ void t_scheduler_fault_ends_every_thread() {
     } catch (const std::runtime_error&) {
     }
     CHECK(one.handed.count(0) == 1 && one.handed.count(19) == 1 && one.handed.count(20) == 0);
+    // three engines per device: the feeder fails preparing chunk [60, 70);
+    // the engines see the abort while waiting for it and must still finalize
+    // [50, 60), which every engine issued whole, so it is handed over once
+    for (int k = 0; k < 6; ++k) {
+      FakeRun three{1, 3, 100, 10};
+      three.fault_d0 = 60;
+      try {
+        three.run();
+      } catch (const std::runtime_error&) {
+      }
+      for (int d = 0; d < 60; ++d) CHECK(three.handed.count(d) == 1 && three.handed[d] == 1);
+      CHECK(three.handed.count(60) == 0);
+    }
   }
 }
 

@@ -21,6 +21,20 @@ except ImportError as exc:  # pragma: no cover - exercised only when unbuilt
 NativeError = _C.NativeError
 
 
+DEDISP_KERNELS = ("auto", "mfma", "valu", "direct", "packed2")
+
+
+def dedisp_kernel(name: str):
+    """``--dedisp_kernel`` name -> ``_C.DedispKernel`` (the one map every
+    driver uses; the names are the native parser's, cli.cpp)."""
+    table = {"auto": _C.DedispKernel.Auto, "mfma": _C.DedispKernel.Mfma, "valu": _C.DedispKernel.Valu,
+             "direct": _C.DedispKernel.Direct, "packed2": _C.DedispKernel.Packed2}
+    try:
+        return table[str(name).lower()]
+    except KeyError:
+        raise ValueError(f"unknown dedispersion kernel {name!r}; one of {', '.join(DEDISP_KERNELS)}") from None
+
+
 def native_library_path() -> str:
     """Filesystem path of the loaded native extension."""
     return _C.__file__

@@ -20,7 +20,7 @@ from typing import List, Optional
 
 import torch
 
-from .. import _C
+from .. import _C, dedisp_kernel
 from ..parallel import dist as pdist
 from ..utils.timing import Stopwatch
 from .search import load_packed_for_rank
@@ -65,8 +65,7 @@ class RankFfa:
             else:
                 self.dfb.load_packed_host(packed.data_ptr())
         self.dedisperser = _C.Dedisperser(self.dfb, self.stream)
-        self.kernel = {"auto": _C.DedispKernel.Auto, "mfma": _C.DedispKernel.Mfma, "valu": _C.DedispKernel.Valu,
-                       "direct": _C.DedispKernel.Direct}[args.dedisp_kernel]
+        self.kernel = dedisp_kernel(args.dedisp_kernel)
         self.params = _C.ffa_params_from(args, float(header["tsamp"]))
         self.engine = _C.FfaEngine(self.params, int(self.geom.out_nsamps), self.stream)
         self.row_stride = _C.Dedisperser.row_stride(self.geom.out_nsamps)

@@ -42,7 +42,7 @@ from typing import Callable, Dict, List, Optional, Sequence
 import numpy as np
 import torch
 
-from .. import _C
+from .. import _C, dedisp_kernel
 from ..parallel import dist as pdist
 from ..utils.timing import Stopwatch, roctx_range
 
@@ -129,8 +129,7 @@ class RankSearcher:
             self.dedisperser = _C.Dedisperser(self.dfb, self.stream)
             if warm:
                 self.warm()
-        self.kernel = {"auto": _C.DedispKernel.Auto, "mfma": _C.DedispKernel.Mfma, "valu": _C.DedispKernel.Valu,
-                       "direct": _C.DedispKernel.Direct}[args.dedisp_kernel]
+        self.kernel = dedisp_kernel(args.dedisp_kernel)
         self.row_stride = _C.Dedisperser.row_stride(self.geom.out_nsamps)
         self.accel_plan = _C.accel_plan_from_args(args, self.header)
         max_trials = max((len(self.accel_list(d)) for d in self.dm_list), default=0)
@@ -636,7 +635,9 @@ def load_packed_for_rank(infilename: str, ctx: pdist.DistContext, timers=None):
             # (a copy out of the fresh mapping faults every page in: ~0.15 s
             # for config 4's 268 MB, ~10 ms this way)
             torch.cuda.synchronize(ctx.device)
-            fb.upload(packed.data_ptr(), nbytes, torch.cuda.current_stream(ctx.device).cuda_stream)
+            if nbytes > fb.data_bytes:
+                raise ValueError(f"{infilename}: header promises {nbytes} data bytes, the file holds {fb.data_bytes}")
+            fb.upload(packed.data_ptr(), nbytes, packed.numel(), torch.cuda.current_stream(ctx.device).cuda_stream)
         if ctx.distributed:
             pdist.broadcast_bytes(packed, nbytes)
     else:

@@ -153,8 +153,8 @@ def reference_dedisperser(header: dict, dm_list: Sequence[float], killmask=None)
 
 def native_dedisperser(header: dict, dm_list: Sequence[float], killmask=None, kernel: str = "auto") -> DedispFn:
     """Dedispersion of the rank's (haloed) window on its GPU (kernel: auto |
-    mfma | valu | direct; bit-identical outputs)."""
-    from .. import _C
+    mfma | valu | direct | packed2; bit-identical outputs)."""
+    from .. import _C, dedisp_kernel
 
     def fn(packed: torch.Tensor, nin: int, nout: int) -> torch.Tensor:
         hdr = dict(header)
@@ -167,9 +167,7 @@ def native_dedisperser(header: dict, dm_list: Sequence[float], killmask=None, ke
         dd = _C.Dedisperser(dfb, stream)
         stride = _C.Dedisperser.row_stride(nout)
         out = torch.empty((len(dm_list), stride), dtype=torch.uint8, device=packed.device)
-        k = {"auto": _C.DedispKernel.Auto, "mfma": _C.DedispKernel.Mfma, "valu": _C.DedispKernel.Valu,
-             "direct": _C.DedispKernel.Direct}[kernel]
-        dd.run(0, len(dm_list), out.data_ptr(), stride, k)
+        dd.run(0, len(dm_list), out.data_ptr(), stride, dedisp_kernel(kernel))
         torch.cuda.current_stream().synchronize()
         return out[:, :nout]
 

@@ -94,14 +94,23 @@ def test_native_fold_from_kept_rows_equals_redispersed(tmp_path):
 
 
 def test_direct_and_mfma_dedispersion_give_identical_search(C, tmp_path):
+    """Every --dedisp_kernel choice, on the native CLI and on the Python
+    driver, writes the same candidate file."""
     outs = []
-    for k in ("direct", "mfma"):
+    common = ["--dm_end", "100", "-n", "3"]
+    for k in ("direct", "mfma", "packed2"):
         d = tmp_path / k
-        r = subprocess.run([os.path.join(REPO, "bin", "peasoup"), "-i", TUTORIAL, "-o", str(d), "--dedisp_kernel", k,
-                            "--dm_end", "100", "-n", "3"], capture_output=True, text=True, timeout=600)
+        r = subprocess.run([os.path.join(REPO, "bin", "peasoup"), "-i", TUTORIAL, "-o", str(d), "--dedisp_kernel", k]
+                           + common, capture_output=True, text=True, timeout=600)
         assert r.returncode == 0, r.stderr
         outs.append(open(d / "candidates.peasoup", "rb").read())
-    assert outs[0] == outs[1]
+    for k in ("packed2", "valu"):
+        d = tmp_path / f"py_{k}"
+        r = subprocess.run([sys.executable, "-m", "peasoup_amd", "-i", TUTORIAL, "-o", str(d), "--dedisp_kernel", k]
+                           + common, capture_output=True, text=True, timeout=600, cwd=REPO)
+        assert r.returncode == 0, r.stderr
+        outs.append(open(d / "candidates.peasoup", "rb").read())
+    assert all(o == outs[0] for o in outs[1:])
 
 
 def test_checkpoint_resume_and_fault_injection(tmp_path):
