@@ -37,6 +37,7 @@ class OverviewFile:
               ("ddm_snr_ratio", float), ("nassoc", int), ("byte_offset", int)]
 
     def __init__(self, path: str):
+        self.path = path
         text = open(path, "r", encoding="latin-1").read()
         try:
             self.root = ET.fromstring(text)
@@ -72,6 +73,35 @@ class OverviewFile:
             el = c.find(tag)
             d[tag] = typ(float(el.text)) if typ is int else typ(el.text)
         return d
+
+    @property
+    def header(self) -> Dict[str, str]:
+        """The <header_parameters> section (tag -> text)."""
+        return self.section("header_parameters")
+
+    def get_candidate_data(self, idx: int) -> "CandidateFileParser":
+        """Parser of the candidate file that holds record ``idx`` (the
+        reference opens ``candidates.peasoup`` in the working directory,
+        peasoup_tools.py:149-151; here the one beside this overview file).
+        Read record ``idx`` with ``.cand_from_offset(get_candidate(idx)["byte_offset"])``."""
+        import os
+
+        self.get_candidate(idx)  # (IndexError for a missing candidate, as the reference)
+        return CandidateFileParser(os.path.join(os.path.dirname(os.path.abspath(self.path)), "candidates.peasoup"))
+
+    def make_predictor(self, idx: int) -> str:
+        """Ephemeris-style predictor of candidate ``idx`` (SOURCE, PERIOD, DM,
+        ACC, RA, DEC), peasoup_tools.py:153-164.  The reference reads the
+        candidate fields as float32 before formatting; so does this."""
+        c = self._cands[idx]
+        f32 = lambda tag: float(np.float32(c.find(tag).text))  # noqa: E731
+        hdr = self.header
+        return "\n".join(("SOURCE: %s" % hdr.get("source_name", ""),
+                          "PERIOD: %.15f" % f32("period"),
+                          "DM: %.3f" % f32("dm"),
+                          "ACC: %.3f" % f32("acc"),
+                          "RA: %s" % radec_to_str(float(hdr.get("src_raj", "0") or 0)),
+                          "DEC: %s" % radec_to_str(float(hdr.get("src_dej", "0") or 0))))
 
     def as_array(self) -> np.ndarray:
         dt = [("cand_num", "i4")] + [(t, "f8" if ty is float else "i8") for t, ty in self.fields]

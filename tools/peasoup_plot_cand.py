@@ -1,51 +1,39 @@
 #!/usr/bin/env python3
-"""Plot one candidate (fold sub-integrations, profile, DM/acc hits) -- the
-reference's CandidatePlotter (tools/peasoup_tools.py) in Python 3.  Needs
-matplotlib; without it the panels are written as .npy arrays instead."""
+"""Candidate diagnostic plots of a peasoup output directory (the reference's
+CandidatePlotter, tools/peasoup_tools.py:167-412): profile, sub-integrations,
+sub-integration statistics, info table, DM / acceleration / S/N scatters of
+the associated hits, DM-acceleration map, every candidate in period-DM space.
+
+    peasoup_plot_cand.py OUTDIR [INDEX ...] [-o FILE] [--all N] [--predictor]
+"""
 import argparse
 import os
 import sys
 
-import numpy as np
-
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from peasoup_amd.utils.outputs import PeasoupOutput  # noqa: E402
+from peasoup_amd.utils.plotting import CandidatePlotter, plot_all  # noqa: E402
 
 
 def main() -> int:
-    p = argparse.ArgumentParser(description=__doc__)
+    p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("outdir")
-    p.add_argument("index", type=int)
-    p.add_argument("-o", "--output", default=None)
+    p.add_argument("index", type=int, nargs="*")
+    p.add_argument("-o", "--output", default=None, help="file name (one index only)")
+    p.add_argument("--all", type=int, default=0, help="plot the first N candidates as Cand%%04d.png")
+    p.add_argument("--predictor", action="store_true", help="print each candidate's predictor instead")
     a = p.parse_args()
-    out = PeasoupOutput(os.path.join(a.outdir, "overview.xml"), os.path.join(a.outdir, "candidates.peasoup"))
-    c = out.get_candidate(a.index)
-    base = a.output or os.path.join(a.outdir, f"cand_{a.index:04d}")
-    try:
-        import matplotlib
-
-        matplotlib.use("Agg")
-        import matplotlib.pyplot as plt
-    except ImportError:
-        if c.fold is not None:
-            np.save(base + "_fold.npy", c.fold)
-        np.save(base + "_hits.npy", c.hits)
-        print(f"matplotlib not available; wrote {base}_fold.npy / _hits.npy")
+    if a.all:
+        for f in plot_all(a.outdir, a.all):
+            print(f)
         return 0
-    fig, ax = plt.subplots(2, 2, figsize=(10, 8))
-    if c.fold is not None:
-        ax[0, 0].imshow(c.fold, aspect="auto", origin="lower")
-        ax[0, 0].set_title("sub-integrations")
-        ax[1, 0].plot(np.concatenate([c.fold.sum(0)] * 2))
-        ax[1, 0].set_title("profile")
-    ax[0, 1].scatter(c.hits["dm"], c.hits["snr"], s=6)
-    ax[0, 1].set_xlabel("DM")
-    ax[1, 1].scatter(c.hits["acc"], c.hits["snr"], s=6)
-    ax[1, 1].set_xlabel("acc (m/s^2)")
-    fig.suptitle(f"P={c.info['period']:.9f}s DM={c.info['dm']:.2f} S/N={c.info['snr']:.1f} fold S/N={c.info['folded_snr']:.1f}")
-    fig.savefig(base + ".png")
-    print(base + ".png")
+    pl = CandidatePlotter(a.outdir)
+    for i in a.index or [0]:
+        if a.predictor:
+            print(pl.overview.make_predictor(i))
+            continue
+        out = a.output if (a.output and len(a.index) <= 1) else os.path.join(a.outdir, "Cand%04d.png" % i)
+        print(pl.plot_cand(i, out))
     return 0
 
 
