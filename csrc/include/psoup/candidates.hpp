@@ -100,6 +100,16 @@ class AccelerationDistiller {
   bool keep_related_;
 };
 
+// Acceleration trials of one DM split over work units (SearchEngine::Job::
+// raw, possibly searched on several ranks): `all` holds the units' raw lists
+// (per-trial harmonic-distilled candidates, trial order within a unit),
+// slice[i] the unit slice of top-level candidate i.  Per DM the slices are
+// joined in slice (= acceleration plan) order and acceleration-distilled --
+// the list SearchEngine distils for an unsplit DM, so the result is the same
+// -- on `nthreads` threads; the output is ordered by DM index.
+CandidateList accel_distill_slices(CandidateList all, const std::vector<int>& slice, const AccelerationDistiller& d,
+                                   int nthreads);
+
 class DMDistiller {
  public:
   DMDistiller(float tol, bool keep_related) : tol_(tol), keep_related_(keep_related) {}

@@ -49,6 +49,9 @@ struct CmdLineOptions {
   std::string dm_schedule = "auto";         // multi-rank DM distribution: dynamic | static | auto (dynamic with
                                             // >= 2 ranks and >= 4 32-DM chunks per rank, else static; an
                                             // explicit dynamic also runs the queue on one rank)
+  int accel_slices = 0;                     // acceleration-trial slices per DM work unit of the multi-rank
+                                            // Python driver (0 = auto: split when the job has fewer than 4 DM
+                                            // chunks per rank; 1 = never)
   int sub_batch = -1;                       // -1 = auto
   int fft_mode = 2;                         // see SearchParams::fft_mode
   bool use_boundaries = false;              // honour --boundary_* (reference ignores them)

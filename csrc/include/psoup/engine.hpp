@@ -294,6 +294,10 @@ struct SearchCounters {
   double tail_s = 0;    // time collect() waited for the acceleration distillation
 };
 
+// The per-DM acceleration distiller a SearchEngine built from p applies
+// (pipeline_multi.cu:243: tobs = fft size x tsamp, freq_tol, keep related).
+AccelerationDistiller search_accel_distiller(const SearchParams& p);
+
 class SearchEngine {
  public:
   SearchEngine(const SearchParams& p, hipStream_t stream);
@@ -317,6 +321,12 @@ class SearchEngine {
     float dm;
     int dm_idx;
     std::vector<float> accs;
+    // raw: the job is one slice of the DM's acceleration trials (the trials
+    // of one DM split over work units, possibly on several ranks): its list
+    // is the per-trial harmonic-distilled candidates in trial order, and the
+    // acceleration distillation runs once the slices are joined in plan order
+    // (accel_distill_slices)
+    bool raw = false;
   };
   std::vector<CandidateList> search_prepared_many(const std::vector<Job>& jobs);
   // The same in two halves: search_prepared_many_async returns once every

@@ -385,6 +385,11 @@ enum Fft4Flags : int {
                            // one LDS exchange, compile-time twiddles inside the two local DFTs
   kFft4PairY = 262144,     // the Stockham pass A (column lengths other than the one-exchange one) also
                            // hands the fused spectrum pass row-pair Y (Y_p[k2/2][i][k2%2])
+  kFft4EarlyTw = 2097152,  // one-exchange pass A / fused spectrum pass: every twiddle and output constant
+                           // loaded before the data (pass A) or staged in LDS (spectrum pass stages), no
+                           // dependent global round trip after the loads
+  kFft4WideY = 8388608,    // one-exchange pass A, row-pair Y: lane pairs swap halves (DPP) so every lane
+                           // stores 16 bytes (half the store instructions)
   kFft4StripInput = 1073741824,  // one-exchange pass A: the padded input in column strips (16 + 4 floats of
                                  // every row per strip, strips row-contiguous), so a wave's 16 rows are
                                  // one ~1.3 KiB contiguous range instead of 16 pieces 16 KiB apart

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #include "psoup/common.hpp"
 #include "psoup/kernels.hpp"
@@ -13,6 +14,26 @@ namespace kern {
 namespace dev {
 
 constexpr int kWave = 64;
+
+// Workgroup-uniform read of read-only global memory through the constant
+// address space: a scalar load into SGPRs (s_load, lgkmcnt) that no earlier
+// store in the kernel can turn into a vector load and no vector-memory wait
+// orders behind the streaming loads.  The memory must not be written while
+// the kernel runs; idx must be uniform.
+template <class T>
+__device__ __forceinline__ T sload(const T* p, uint64_t idx) {
+  static_assert(std::is_arithmetic<T>::value, "sload: scalar types (float2: sload2)");
+#if __HIP_DEVICE_COMPILE__
+  typedef const __attribute__((address_space(4))) T* cptr;
+  return reinterpret_cast<cptr>(reinterpret_cast<uintptr_t>(p))[idx];
+#else
+  return p[idx];  // (the host pass of a device function: never run)
+#endif
+}
+__device__ __forceinline__ float2 sload2(const float2* p, uint64_t idx) {
+  const float* f = reinterpret_cast<const float*>(p);
+  return make_float2(sload(f, 2 * idx), sload(f, 2 * idx + 1));
+}
 
 // Memory-bound launches: enough blocks to fill 256 CUs x 8, grid-stride the rest.
 inline unsigned grid_for(uint64_t work_items, unsigned block, unsigned cap = 2048) {

@@ -78,8 +78,41 @@ using namespace dreg;  // butterflies, packed complex arithmetic, dft<N> (dft_re
 // One Stockham iteration's arithmetic (Govindaraju et al. formulation): for
 // virtual thread j' = t + b*T, points v[b + r*B] = data[j' + r*L/R] are
 // twiddled by W_{Ns R}^{r (j' mod Ns)} and transformed in place.
-template <int L, int CPT, int Ns, int R>
-__device__ __forceinline__ void stage_compute(Vec<CPT>& v, int t, const float2* __restrict__ twL) {
+// Where the Stockham stages read W_L^m.  Global: the length-L table.  LDS
+// (TwLds): the entries the stages of a length-L transform use -- every m <
+// D, and multiples of S in [D, L/2) -- staged once per workgroup, so no
+// stage waits on a global round trip after its exchange.
+struct TwGlobal {
+  const float2* __restrict__ p;
+  __device__ __forceinline__ float2 operator()(int m) const { return p[m]; }
+};
+template <int L>
+struct TwLds {
+  static constexpr int D = L <= 1024 ? L / 2 : 512;
+  static constexpr int S = L <= 1024 ? 1 : (L == 2048 ? 16 : 4);
+  static constexpr int N = D + (L / 2 - D) / S;  // staged entries
+  __host__ __device__ static constexpr int slot(int m) { return m < D ? m : D + (m - D) / S; }
+  __host__ __device__ static constexpr int index(int e) { return e < D ? e : D + (e - D) * S; }
+  // every twiddle index stage_compute reads for this L is staged
+  static constexpr bool covers() {
+    for (int ns = 1; ns < L; ns *= 8) {
+      const int r = L / ns >= 8 ? 8 : L / ns;
+      if (ns == 1) continue;
+      const int scale = L / (ns * r);
+      for (int jm = 0; jm < ns; ++jm) {
+        const int a = jm * scale, b = 4 * jm * scale;
+        if (a >= L / 2 || (a >= D && (a - D) % S != 0)) return false;
+        if (r == 8 && (b >= L / 2 || (b >= D && (b - D) % S != 0))) return false;
+      }
+    }
+    return true;
+  }
+  const float2* __restrict__ p;
+  __device__ __forceinline__ float2 operator()(int m) const { return p[slot(m)]; }
+};
+
+template <int L, int CPT, int Ns, int R, class TW>
+__device__ __forceinline__ void stage_compute(Vec<CPT>& v, int t, const TW& twL) {
   constexpr int T = L / kPts, B = kPts / R;
 #pragma unroll
   for (int b = 0; b < B; ++b) {
@@ -89,13 +122,13 @@ __device__ __forceinline__ void stage_compute(Vec<CPT>& v, int t, const float2* 
       // W^{r jm scale}, r < R: two table reads (w1, w4) and short products
       // (at most two multiplications deep) instead of R-1 table reads
       float2 w[R];
-      w[1] = twL[jm * scale];
+      w[1] = twL(jm * scale);
       if constexpr (R >= 4) {
         w[2] = cmul(w[1], w[1]);
         w[3] = cmul(w[2], w[1]);
       }
       if constexpr (R == 8) {
-        w[4] = twL[4 * jm * scale];
+        w[4] = twL(4 * jm * scale);
         w[5] = cmul(w[4], w[1]);
         w[6] = cmul(w[4], w[2]);
         w[7] = cmul(w[4], w[3]);
@@ -165,9 +198,8 @@ __device__ __forceinline__ void trace_event(int ev) {
   if (tr != nullptr && threadIdx.x == 0) tr[blockIdx.x * kTraceEvents + ev] = __builtin_readcyclecounter();
 }
 
-template <int L, int CPT, int CG, int Ns>
-__device__ __forceinline__ void fft_stages(Vec<CPT>& v, float* __restrict__ lds, int t,
-                                           const float2* __restrict__ twL, int ev = 2) {
+template <int L, int CPT, int CG, int Ns, class TW>
+__device__ __forceinline__ void fft_stages(Vec<CPT>& v, float* __restrict__ lds, int t, const TW& twL, int ev = 2) {
   constexpr int R = (L / Ns >= 8) ? 8 : L / Ns;
   stage_compute<L, CPT, Ns, R>(v, t, twL);
   trace_event(ev);
@@ -176,6 +208,11 @@ __device__ __forceinline__ void fft_stages(Vec<CPT>& v, float* __restrict__ lds,
     trace_event(ev + 1);
     fft_stages<L, CPT, CG, Ns * R>(v, lds, t, twL, ev + 2);
   }
+}
+template <int L, int CPT, int CG, int Ns>
+__device__ __forceinline__ void fft_stages(Vec<CPT>& v, float* __restrict__ lds, int t,
+                                           const float2* __restrict__ twL, int ev = 2) {
+  fft_stages<L, CPT, CG, Ns>(v, lds, t, TwGlobal{twL}, ev);
 }
 
 // S consecutive resampled samples x[p0 .. p0+S-1] (resampleII indices,
@@ -526,27 +563,37 @@ struct OneX {
 // The part both one-exchange passes share: P-point DFTs of the thread's two
 // transforms, W_L^{g k1} (twL: the length-L table), the exchange, G-point
 // DFTs of the thread's pairs (u[p][k2] = X[k1 + P k2] of pair p).
-template <int L, int G, int R>
+// W_L^{g k1}, k1 = 8 a + b, as (W_L^{8 g a}) (W_L^{g b}): the factors from the length-L table
+template <int L, int P>
+__device__ __forceinline__ void onex_wl(const float2* __restrict__ twL, int gg, float2 (&pb)[8], float2 (&pa)[P / 8]) {
+  pb[0] = make_float2(1.f, 0.f);
+#pragma unroll
+  for (int b = 1; b < 8; ++b) pb[b] = twL[(gg * b) & (L - 1)];
+  pa[0] = make_float2(1.f, 0.f);
+#pragma unroll
+  for (int a = 1; a < P / 8; ++a) pa[a] = twL[(gg * 8 * a) & (L - 1)];
+}
+
+// EARLY: pb / pa were loaded by the caller before the data loads (their
+// round trip hidden behind the data's); else they are loaded here, after
+// the DFTs, and the wave waits for them
+template <int L, int G, int R, bool EARLY>
 __device__ __forceinline__ void onex_core(float2 (&va)[L / G], float2 (&vb)[L / G], float2 (&u)[2 * (L / G) / G][G],
-                                          float2* __restrict__ lds, const float2* __restrict__ twL, int t) {
+                                          float2* __restrict__ lds, const float2* __restrict__ twL, int t,
+                                          float2 (&pb)[8], float2 (&pa)[L / G / 8]) {
   using C = OneX<L, G, R>;
   constexpr int P = C::P;
   const int lane = t & 63, w = t >> 6, cp = t & 3, gg = t >> 2, rc = (lane >> 3) & 7;
   dft<P>(va);
   dft<P>(vb);
   {
-    // W_L^{g k1}, k1 = 8 a + b: (W_L^{8 g a}) (W_L^{g b}) from the length-L table
-    float2 pb[8];
-    pb[0] = make_float2(1.f, 0.f);
-#pragma unroll
-    for (int b = 1; b < 8; ++b) pb[b] = twL[(gg * b) & (L - 1)];
+    if constexpr (!EARLY) onex_wl<L, P>(twL, gg, pb, pa);
 #pragma unroll
     for (int a = 0; a < P / 8; ++a) {
-      const float2 pa = a == 0 ? make_float2(1.f, 0.f) : twL[(gg * 8 * a) & (L - 1)];
 #pragma unroll
       for (int b = 0; b < 8; ++b) {
         if (a == 0 && b == 0) continue;
-        const float2 wv = a == 0 ? pb[b] : cmul(pa, pb[b]);
+        const float2 wv = a == 0 ? pb[b] : cmul(pa[a], pb[b]);
         va[8 * a + b] = cmul(va[8 * a + b], wv);
         vb[8 * a + b] = cmul(vb[8 * a + b], wv);
       }
@@ -582,7 +629,7 @@ __device__ __forceinline__ void onex_core(float2 (&va)[L / G], float2 (&vb)[L / 
   trace_event(4);
 }
 
-template <int L, int G, int R, bool STRIPS>
+template <int L, int G, int R, bool STRIPS, bool EARLY, bool WIDE = false>
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, OneX<L, G, R>::THREADS), amdgpu_waves_per_eu(2)))
 fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__ in_pad, uint64_t n,
                          const double* __restrict__ afs, int K, float2* __restrict__ Y, Fft4Geom g,
@@ -629,6 +676,20 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
   // visible to every thread after the exchange's first barrier
   static_assert((8 * G) % C::THREADS == 0, "ox rows per thread");
   constexpr int kTw = 8 * G / C::THREADS;
+  const int rc = (lane >> 3) & 7;
+  const uint32_t mask = static_cast<uint32_t>(N1) * L - 1;
+  const uint32_t col = static_cast<uint32_t>(c0 + rc);
+  float2 pb[8], pa[P / 8], om_hi = make_float2(1.f, 0.f), om_lo = om_hi;
+  if constexpr (EARLY) {
+    // every table value the thread needs after its data loads (the W_L
+    // factors of the P-point DFT outputs, the two factors of the four-step
+    // twiddle W_M^{col k1}), issued first: the data loads' round trip covers
+    // theirs, and nothing waits on a dependent load after the exchange
+    onex_wl<L, P>(tab + to.n2, gg, pb, pa);
+    const uint32_t a0 = (col * static_cast<uint32_t>(8 * w + (lane & 7))) & mask;  // (NPAIR == 1: k1 of pair 0)
+    om_hi = tab[to.hi + (a0 >> kSplit)];
+    om_lo = tab[to.lo + (a0 & ((1u << kSplit) - 1))];
+  }
   float2 twv[kTw];
 #pragma unroll
   for (int q = 0; q < kTw; ++q) twv[q] = tab[to.ox + static_cast<uint64_t>(c0) * G + t + q * C::THREADS];
@@ -706,25 +767,20 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
     const int e = t + q * C::THREADS;
     tws[(e / G) * (G + 1) + (e % G)] = twv[q];
   }
-  const int rc = (lane >> 3) & 7;
   float2 u[C::NPAIR][G];
-  onex_core<L, G, R>(va, vb, u, lds, tab + to.n2, t);
+  onex_core<L, G, R, EARLY>(va, vb, u, lds, tab + to.n2, t, pb, pa);
 
   // four-step twiddle W_M^{col k}, k = k1 + P k2: W_M^{col k1} (table pair)
   // times W_M^{col P k2} (the staged ox rows); tiled store
   // Y_t[c0 / 8][k / 8][c][k % 8] (one 512-byte block per wave and k2)
-  const uint32_t mask = static_cast<uint32_t>(N1) * L - 1;
-  const uint32_t col = static_cast<uint32_t>(c0 + rc);
   float2* yk = Y + static_cast<uint64_t>(k) * g.ystride + static_cast<uint64_t>(c0) * L;
   float2* yp = Y + static_cast<uint64_t>(k) * g.ystride + 2 * col;
   const float2* twr = tws + rc * (G + 1);
 #pragma unroll
   for (int p = 0; p < C::NPAIR; ++p) {
     const uint32_t k1 = static_cast<uint32_t>(8 * (w + C::NW * p) + (lane & 7));
-    const float2 om = twiddle_M((col * k1) & mask, tab + to.lo, tab + to.hi);
-#pragma unroll
-    for (int k2 = 0; k2 < G; ++k2) {
-      const float2 wv = k2 == 0 ? om : cmul(om, twr[k2]);
+    const float2 om = EARLY && p == 0 ? cmul(om_hi, om_lo) : twiddle_M((col * k1) & mask, tab + to.lo, tab + to.hi);
+    auto put = [&](int k2, float2 wv) {
       const uint32_t kk = k1 + static_cast<uint32_t>(P * k2);
       // (non-temporal: Y is read back only by the spectrum pass after the whole
       // batch, far beyond the caches; L2 and the Infinity Cache are left to the
@@ -733,6 +789,50 @@ fft4_colpass_onex_kernel(const float* __restrict__ in, const float* __restrict__
       float2* dst = g.ypair ? yp + (kk >> 1) * (2 * static_cast<uint32_t>(N1)) + (kk & 1)  // Y_p[kk/2][col][kk%2]
                             : yk + (kk >> 3) * 64 + static_cast<uint32_t>(rc) * 8 + (kk & 7);
       __builtin_nontemporal_store(f2v{yv.x, yv.y}, reinterpret_cast<f2v*>(dst));
+    };
+    if constexpr (EARLY && WIDE) {
+      // row-pair Y (g.ypair): lanes k1 (even) and k1 + 1 of a column write the
+      // two halves of one 16-byte Y_p[kk/2][col] pair.  For each pair of k2
+      // values (a, b) the even lane hands its b value to the odd lane and
+      // takes the odd lane's a value (one DPP swap of adjacent lanes): the
+      // even lane stores {own a, partner a}, the odd lane {partner b, own b}
+      // -- one 16-byte store per lane per two k2, the same bytes and lines.
+      const bool odd = lane & 1;
+#pragma unroll
+      for (int k0 = 0; k0 < G; k0 += 8) {
+        float2 tw8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) tw8[e] = twr[k0 + e];
+#pragma unroll
+        for (int e = 0; e < 8; e += 2) {
+          const int a = k0 + e, b = a + 1;
+          const float2 ya = cmul(u[p][a], a == 0 ? om : cmul(om, tw8[e]));
+          const float2 yb = cmul(u[p][b], cmul(om, tw8[e + 1]));
+          const float2 snd = odd ? ya : yb;
+          // quad_perm [1, 0, 3, 2]: lane i reads lane i ^ 1
+          const float2 rcv = make_float2(
+              __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(snd.x), 0xB1, 0xF, 0xF, false)),
+              __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(snd.y), 0xB1, 0xF, 0xF, false)));
+          const float2 lo = odd ? rcv : ya, hi = odd ? yb : rcv;
+          const uint32_t kk = (odd ? k1 - 1 : k1) + static_cast<uint32_t>(P * (odd ? b : a));  // even
+          float2* dst = yp + (kk >> 1) * (2 * static_cast<uint32_t>(N1));
+          __builtin_nontemporal_store(f4v{lo.x, lo.y, hi.x, hi.y}, reinterpret_cast<f4v*>(dst));
+        }
+      }
+    } else if constexpr (EARLY) {
+      // the staged ox values eight at a time: their LDS reads issued together,
+      // one wait per eight stores instead of one per store
+#pragma unroll
+      for (int k0 = 0; k0 < G; k0 += 8) {
+        float2 tw8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) tw8[e] = twr[k0 + e];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) put(k0 + e, k0 + e == 0 ? om : cmul(om, tw8[e]));
+      }
+    } else {
+#pragma unroll
+      for (int k2 = 0; k2 < G; ++k2) put(k2, k2 == 0 ? om : cmul(om, twr[k2]));
     }
   }
   trace_event(11);
@@ -855,14 +955,30 @@ __constant__ constexpr float kCos16[8] = {1.f, 0.92387953251128676f, 0.707106781
 __constant__ constexpr float kSin16[8] = {0.f, 0.38268343236508977f, 0.70710678118654752f, 0.92387953251128676f,
                                           1.f, 0.92387953251128676f, 0.70710678118654752f, 0.38268343236508977f};
 
-template <int L, bool PAIRY>
+// EARLY (kFft4EarlyTw): the stage twiddles staged in LDS (TwLds) and the
+// output phase's constants (statistics, r2c twiddle factors) loaded with the
+// Y rows, so no dependent global round trip follows the loads.
+template <int L>
+struct SpecLds {
+  static constexpr int EX = Cfg<L, 2 * kSpecNp, 1>::LDS_FLOATS;  // exchange buffer (floats)
+  static constexpr int TW = 2 * TwLds<L>::N;                      // staged stage twiddles
+  static constexpr int HT = 2 * (L / kPts);                       // e^{-i pi t / L}, one per thread
+  // two workgroups per CU (163840 bytes): the per-thread factors join only where they fit
+  static constexpr bool HT_LDS = (EX + TW + HT) * 4 * 2 <= 163840;
+  static constexpr int TOTAL = EX + TW + (HT_LDS ? HT : 0);
+  static_assert((EX + TW) * 4 * 2 <= 163840, "spectrum pass LDS: two workgroups per CU");
+};
+
+template <int L, bool PAIRY, bool EARLY>
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, 2 * kSpecNp, 1>::THREADS),
                                amdgpu_waves_per_eu(2)))
 fft4_rowpass_spectrum_kernel(const float2* __restrict__ Y, int K, Fft4Geom g, const float2* __restrict__ tab,
                              SpecOut o) {
   constexpr int NP = kSpecNp, CPT = 2 * NP;
   using C = Cfg<L, CPT, 1>;
-  __shared__ __attribute__((aligned(16))) float lds[C::LDS_FLOATS];
+  using SL = SpecLds<L>;
+  static_assert(!EARLY || TwLds<L>::covers(), "staged twiddles cover every stage");
+  __shared__ __attribute__((aligned(16))) float lds[EARLY ? SL::TOTAL : C::LDS_FLOATS];
   constexpr int T = C::T;
   const int t = threadIdx.x;
   // block order: XCD x (blockIdx % 8) runs trials x, x+8, ..., each trial's
@@ -882,6 +998,21 @@ fft4_rowpass_spectrum_kernel(const float2* __restrict__ Y, int K, Fft4Geom g, co
   // W^{i} = W^{t} e^{-2 pi i q / 8} for i = t + q T (T = L / 8): one table
   // value per thread, the rest compile-time constants
   const float2 wt = tab[to.n1 + t];
+  // EARLY: the staged table entries and this thread's e^{-i pi t / L} ahead
+  // of the Y rows, the workgroup's statistics and r2c factors (scalar)
+  // right behind them: all needed only after the FFT or its first exchange
+  constexpr int kTwq = (TwLds<L>::N + T - 1) / T;
+  float2 twq[EARLY ? kTwq : 1], ht_early = make_float2(1.f, 0.f);
+  float mean_e = 0.f, sigma_e = 1.f;
+  float2 hr_early[NP];
+  if constexpr (EARLY) {
+#pragma unroll
+    for (int q = 0; q < kTwq; ++q) {
+      const int e = t + q * T;
+      twq[q] = e < TwLds<L>::N ? tab[to.n1 + TwLds<L>::index(e)] : make_float2(0.f, 0.f);
+    }
+    if constexpr (SL::HT_LDS) ht_early = tab[to.hk + t];
+  }
   Vec<CPT> x;
 #pragma unroll
   for (int q = 0; q < kPts; ++q) {
@@ -917,8 +1048,26 @@ fft4_rowpass_spectrum_kernel(const float2* __restrict__ Y, int K, Fft4Geom g, co
     x[7][q] = make_float2(b1.x, b1.y);
     x[6][q] = make_float2(b1.z, b1.w);
   }
+  if constexpr (EARLY) {
+    // (uniform values by scalar loads: in SGPRs, waited for by lgkmcnt)
+    const uint32_t ts = o.tsrc ? dev::sload(o.tsrc, static_cast<uint64_t>(k)) : 0u;
+    mean_e = dev::sload(o.stats, 4 * static_cast<uint64_t>(ts));
+    sigma_e = dev::sload(o.stats, 4 * static_cast<uint64_t>(ts) + 2);
+#pragma unroll
+    for (int c = 0; c < NP; ++c) hr_early[c] = dev::sload2(tab, to.hr + fr + c);
+  }
   // (every load is issued before the first use of a loaded value)
   __builtin_amdgcn_sched_barrier(0);
+  float2* tw_lds = reinterpret_cast<float2*>(lds + C::LDS_FLOATS);
+  float2* ht_lds = reinterpret_cast<float2*>(lds + C::LDS_FLOATS + SL::TW);
+  if constexpr (EARLY) {
+    // (visible to every thread after the first exchange's barrier; stage 0
+    // reads no twiddle)
+#pragma unroll
+    for (int q = 0; q < kTwq; ++q)
+      if (t + q * T < TwLds<L>::N) tw_lds[t + q * T] = twq[q];
+    if constexpr (SL::HT_LDS) ht_lds[t] = ht_early;
+  }
 #pragma unroll
   for (int q = 0; q < kPts; ++q) {
     // mirror channels: conj(u_r) = W^{i} conj(Y_{n2-r}) (pair-row 0: conj(Y_0))
@@ -930,16 +1079,27 @@ fft4_rowpass_spectrum_kernel(const float2* __restrict__ Y, int K, Fft4Geom g, co
     }
   }
   trace_event(1);
-  fft_stages<L, CPT, C::CG, 1>(x, lds, t, tab + to.n1);
+  if constexpr (EARLY)
+    fft_stages<L, CPT, C::CG, 1>(x, lds, t, TwLds<L>{tw_lds});
+  else
+    fft_stages<L, CPT, C::CG, 1>(x, lds, t, tab + to.n1);
   trace_event(9);
 
-  const float* st = o.stats + (o.tsrc ? 4 * static_cast<uint64_t>(o.tsrc[k]) : 0);
-  const float mean = st[0] * o.nscale;
-  const float sigma = st[2] * o.nscale;
-  const float rsig = 1.0f / sigma;  // per bin dev::div_rn: IEEE division
-  float2 hr[NP];                    // e^{-i pi r / M}, r = 4v .. 4v+4 (workgroup-uniform)
+  float mean, sigma;
+  float2 hr[NP];  // e^{-i pi r / M}, r = 4v .. 4v+4 (workgroup-uniform)
+  if constexpr (EARLY) {
+    mean = mean_e * o.nscale;
+    sigma = sigma_e * o.nscale;
 #pragma unroll
-  for (int c = 0; c < NP; ++c) hr[c] = tab[to.hr + fr + c];
+    for (int c = 0; c < NP; ++c) hr[c] = hr_early[c];
+  } else {
+    const float* st = o.stats + (o.tsrc ? 4 * static_cast<uint64_t>(o.tsrc[k]) : 0);
+    mean = st[0] * o.nscale;
+    sigma = st[2] * o.nscale;
+#pragma unroll
+    for (int c = 0; c < NP; ++c) hr[c] = tab[to.hr + fr + c];
+  }
+  const float rsig = 1.0f / sigma;  // per bin dev::div_rn: IEEE division
   const uint32_t M = static_cast<uint32_t>(L) * n2;
   float4* pk = reinterpret_cast<float4*>(o.P + static_cast<uint64_t>(k) * o.pstride);
   uint8_t* qk = o.Q + static_cast<uint64_t>(k) * o.qstride + kSpecQShift;  // qk[b]: bin b
@@ -950,7 +1110,7 @@ fft4_rowpass_spectrum_kernel(const float2* __restrict__ Y, int K, Fft4Geom g, co
   uint32_t tt = static_cast<uint32_t>(t);
   asm volatile("" : "+v"(tt));
   // e^{-i pi k1 / L} = e^{-i pi t / L} e^{-i pi q / 8} (k1 = t + q T), formed per q
-  float2 ht = tab[to.hk + tt];
+  float2 ht = EARLY && SL::HT_LDS ? ht_lds[tt] : tab[to.hk + tt];
   asm volatile("" : "+v"(ht.x), "+v"(ht.y));
   // Scaled forms (all factors exact powers of two): with e = z + w and
   // d = z - w (w = conj Z[M-k], as the mirror channel holds it), 2 X[k] =
@@ -1069,7 +1229,8 @@ namespace {
 // fastest measured (tools/kbench.py, bench A/B); the strip input: pass A 15.9 -> 13.9 us/trial alone,
 // bench within noise (profiles/r3_strip)
 int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4TileY | kFft4TileX | kFft4PairXcd |
-                   kFft4GroupXcd | kFft4UniformTw | kFft4OneX | kFft4StripInput | kFft4PairY;
+                   kFft4GroupXcd | kFft4UniformTw | kFft4OneX | kFft4StripInput | kFft4PairY | kFft4EarlyTw |
+                   kFft4WideY;
 }  // namespace
 
 void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& g, hipStream_t s, int count,
@@ -1155,10 +1316,15 @@ void fft4_rowpass_spectrum(const float2* Y, int K, const Fft4Geom& g, const floa
   switch (g.n1) {
 #define PS_CASE(LL)                                                                                         \
   case LL:                                                                                                  \
-    if (g.ypair)                                                                                            \
-      fft4_rowpass_spectrum_kernel<LL, true><<<grid, Cfg<LL, 2 * kSpecNp, 1>::THREADS, 0, s>>>(Y, K, g, tables, o); \
+    if (g.ypair && (f & kFft4EarlyTw))                                                                      \
+      fft4_rowpass_spectrum_kernel<LL, true, true><<<grid, Cfg<LL, 2 * kSpecNp, 1>::THREADS, 0, s>>>(Y, K, g, tables, \
+                                                                                                  o);             \
+    else if (g.ypair)                                                                                       \
+      fft4_rowpass_spectrum_kernel<LL, true, false><<<grid, Cfg<LL, 2 * kSpecNp, 1>::THREADS, 0, s>>>(Y, K, g,       \
+                                                                                                   tables, o);    \
     else                                                                                                    \
-      fft4_rowpass_spectrum_kernel<LL, false><<<grid, Cfg<LL, 2 * kSpecNp, 1>::THREADS, 0, s>>>(Y, K, g, tables, o); \
+      fft4_rowpass_spectrum_kernel<LL, false, false><<<grid, Cfg<LL, 2 * kSpecNp, 1>::THREADS, 0, s>>>(Y, K, g,      \
+                                                                                                    tables, o);   \
     break;
     PS_CASE(128) PS_CASE(256) PS_CASE(512) PS_CASE(1024) PS_CASE(2048) PS_CASE(4096)
 #undef PS_CASE
@@ -1206,12 +1372,16 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   const dim3 grid(static_cast<unsigned>(nblocks));
   PSOUP_CHECK(!g.ypair || pair_y_layout(g.n2, f), "fft4 colpass: this pass A cannot write the row-pair Y layout");
   if (onex_colpass(g.n2, f)) {
-    if (f & kFft4StripInput)
-      fft4_colpass_onex_kernel<2048, 64, 4, true><<<grid, OneX<2048, 64, 4>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y,
-                                                                                            g, tables, f);
+    constexpr int TH = OneX<2048, 64, 4>::THREADS;
+    if ((f & kFft4StripInput) && (f & kFft4EarlyTw) && (f & kFft4WideY) && g.ypair)
+      fft4_colpass_onex_kernel<2048, 64, 4, true, true, true><<<grid, TH, 0, s>>>(in, in_pad, n, af, K, Y, g, tables,
+                                                                                  f);
+    else if ((f & kFft4StripInput) && (f & kFft4EarlyTw))
+      fft4_colpass_onex_kernel<2048, 64, 4, true, true><<<grid, TH, 0, s>>>(in, in_pad, n, af, K, Y, g, tables, f);
+    else if (f & kFft4StripInput)
+      fft4_colpass_onex_kernel<2048, 64, 4, true, false><<<grid, TH, 0, s>>>(in, in_pad, n, af, K, Y, g, tables, f);
     else
-      fft4_colpass_onex_kernel<2048, 64, 4, false><<<grid, OneX<2048, 64, 4>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y,
-                                                                                             g, tables, f);
+      fft4_colpass_onex_kernel<2048, 64, 4, false, false><<<grid, TH, 0, s>>>(in, in_pad, n, af, K, Y, g, tables, f);
   }
   else if (g.ypair)
     launch_colpass<8, 1, kModeBlocked | kModeTileY | kModePairY>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);

@@ -381,6 +381,13 @@ PYBIND11_MODULE(_C, m) {
            py::arg("fractional_harms") = true)
       .def("distill", &HarmonicDistiller::distill)
       .def("distill_reference", &HarmonicDistiller::distill_reference);
+  m.def("accel_distill_slices",
+        [](CandidateList all, const std::vector<int>& slices, float tobs, float tol, int nthreads) {
+          return accel_distill_slices(std::move(all), slices, AccelerationDistiller(tobs, tol, true), nthreads);
+        },
+        py::arg("cands"), py::arg("slices"), py::arg("tobs"), py::arg("tol"), py::arg("nthreads") = 4,
+        py::call_guard<py::gil_scoped_release>(),
+        "join each DM's acceleration slices in slice order and acceleration-distil them (keep related)");
   py::class_<AccelerationDistiller>(m, "AccelerationDistiller")
       .def(py::init<float, float, bool>(), py::arg("tobs"), py::arg("tol"), py::arg("keep_related"))
       .def("distill", &AccelerationDistiller::distill)
@@ -483,6 +490,48 @@ PYBIND11_MODULE(_C, m) {
     }
     return out;
   });
+  // The merge when DMs' acceleration trials were split over work units
+  // (--accel_slices): every buffer holds raw slice lists, slices[i] their
+  // per-candidate slice indices (int32, (address, count) of host memory);
+  // the slices of each DM are joined in plan order and acceleration-distilled
+  // (accel_distill_slices), then the usual global distillation and scoring.
+  m.def("merge_split_buffers", [](const std::vector<std::pair<uintptr_t, size_t>>& bufs,
+                                  const std::vector<std::pair<uintptr_t, size_t>>& slices, const CmdLineOptions& args,
+                                  const py::dict& hdr, int nthreads) {
+    PSOUP_CHECK(bufs.size() == slices.size(), "merge_split_buffers: one slice array per buffer");
+    SearchSetup s = make_search_setup(args, dict_to_header(hdr));
+    auto out = std::make_shared<CandidateBag>();
+    {
+      py::gil_scoped_release nogil;
+      CandidateList all;
+      std::vector<int> sl;
+      for (size_t i = 0; i < bufs.size(); ++i) {
+        const size_t before = all.size();
+        deserialize_candidates_into(reinterpret_cast<const uint8_t*>(bufs[i].first), bufs[i].second, all);
+        PSOUP_CHECK(all.size() - before == slices[i].second, "merge_split_buffers: slice count mismatch");
+        const int32_t* si = reinterpret_cast<const int32_t*>(slices[i].first);
+        sl.insert(sl.end(), si, si + slices[i].second);
+      }
+      all = accel_distill_slices(std::move(all), sl, search_accel_distiller(s.search), nthreads);
+      stable_sort_by_dm_idx(all);
+      out->c = global_distill_and_score(std::move(all), args, s);
+    }
+    return out;
+  }, py::arg("bufs"), py::arg("slices"), py::arg("args"), py::arg("header"), py::arg("nthreads") = 8);
+  m.def("merge_split_local", [](CandidateBag& local, const std::vector<int>& slices, const CmdLineOptions& args,
+                                const py::dict& hdr, int nthreads) {
+    SearchSetup s = make_search_setup(args, dict_to_header(hdr));
+    auto out = std::make_shared<CandidateBag>();
+    {
+      py::gil_scoped_release nogil;
+      CandidateList all = std::move(local.c);
+      local.c.clear();
+      all = accel_distill_slices(std::move(all), slices, search_accel_distiller(s.search), nthreads);
+      stable_sort_by_dm_idx(all);
+      out->c = global_distill_and_score(std::move(all), args, s);
+    }
+    return out;
+  }, py::arg("local"), py::arg("slices"), py::arg("args"), py::arg("header"), py::arg("nthreads") = 8);
   // serialised into a uint8 numpy array that owns the bytes (torch.from_numpy
   // takes it without a copy)
   m.def("serialize_candidates_array", [](const CandidateBag& b) {
@@ -551,6 +600,7 @@ PYBIND11_MODULE(_C, m) {
       .def_readwrite("accel_batch", &CmdLineOptions::accel_batch)
       .def_readwrite("engines_per_gpu", &CmdLineOptions::engines_per_gpu)
       .def_readwrite("dm_schedule", &CmdLineOptions::dm_schedule)
+      .def_readwrite("accel_slices", &CmdLineOptions::accel_slices)
       .def_readwrite("sub_batch", &CmdLineOptions::sub_batch)
       .def_readwrite("fft_mode", &CmdLineOptions::fft_mode)
       .def_readwrite("use_boundaries", &CmdLineOptions::use_boundaries)
@@ -996,6 +1046,17 @@ PYBIND11_MODULE(_C, m) {
         return e.search_prepared_many(js);
       }, py::arg("jobs"), py::call_guard<py::gil_scoped_release>(),
          "jobs: [(prepared index, dm, dm_idx, accs)] -> one candidate list per job")
+      .def("search_prepared_many_async",
+           [](SearchEngine& e, const std::vector<std::tuple<int, float, int, std::vector<float>, bool>>& jobs) {
+             std::vector<SearchEngine::Job> js;
+             js.reserve(jobs.size());
+             for (const auto& j : jobs)
+               js.push_back(SearchEngine::Job{std::get<0>(j), std::get<1>(j), std::get<2>(j), std::get<3>(j),
+                                              std::get<4>(j)});
+             return e.search_prepared_many_async(js);
+           }, py::arg("jobs"), py::call_guard<py::gil_scoped_release>(),
+           "jobs: [(prepared index, dm, dm_idx, accs, raw)]; raw: an acceleration slice, its per-trial "
+           "harmonic-distilled list returned undistilled (accel_distill_slices joins the slices)")
       .def("search_prepared_many_async", [](SearchEngine& e, const std::vector<std::tuple<int, float, int, std::vector<float>>>& jobs) {
         std::vector<SearchEngine::Job> js;
         js.reserve(jobs.size());

@@ -1,10 +1,12 @@
 #include "psoup/candidates.hpp"
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -419,6 +421,52 @@ void stable_sort_by_dm_idx(CandidateList& c) {
   // std::stable_sort's permutation depends on the comparison outcomes alone
   std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return c[a].dm_idx < c[b].dm_idx; });
   apply_order(c, order);
+}
+
+CandidateList accel_distill_slices(CandidateList all, const std::vector<int>& slice, const AccelerationDistiller& d,
+                                   int nthreads) {
+  PSOUP_CHECK(slice.size() == all.size(), "accel_distill_slices: one slice index per candidate");
+  // (dm_idx, slice) order, stable: a slice's candidates keep their trial order
+  std::vector<uint32_t> order(all.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = static_cast<uint32_t>(i);
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+    return all[a].dm_idx != all[b].dm_idx ? all[a].dm_idx < all[b].dm_idx : slice[a] < slice[b];
+  });
+  apply_order(all, order);
+  std::vector<std::pair<size_t, size_t>> runs;  // one DM each
+  for (size_t i = 0; i < all.size();) {
+    size_t j = i + 1;
+    while (j < all.size() && all[j].dm_idx == all[i].dm_idx) ++j;
+    runs.emplace_back(i, j);
+    i = j;
+  }
+  std::vector<CandidateList> out(runs.size());
+  std::atomic<size_t> next{0};
+  std::exception_ptr err;
+  std::mutex err_mu;
+  auto work = [&] {
+    try {
+      for (size_t r; (r = next.fetch_add(1)) < runs.size();) {
+        CandidateList one(std::make_move_iterator(all.begin() + static_cast<std::ptrdiff_t>(runs[r].first)),
+                          std::make_move_iterator(all.begin() + static_cast<std::ptrdiff_t>(runs[r].second)));
+        out[r] = d.distill(std::move(one));
+      }
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(err_mu);
+      if (!err) err = std::current_exception();
+      next.store(runs.size());
+    }
+  };
+  const int nt = std::max(1, std::min<int>(nthreads, static_cast<int>(runs.size())));
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+  if (err) std::rethrow_exception(err);
+  CandidateList res;
+  for (auto& l : out)
+    for (auto& c : l) res.push_back(std::move(c));
+  return res;
 }
 
 void sort_by_folded_snr(CandidateList& cands) {

@@ -237,6 +237,10 @@ static std::vector<Spec> peasoup_specs(CmdLineOptions& a) {
             "from a shared first-come queue, like the reference's DMDispenser; static = contiguous shards balanced "
             "by acceleration-trial count; auto = dynamic when the list has >= 4 chunks per rank",
             a.dm_schedule),
+      val_n("", "accel_slices",
+            "Multi-rank Python driver: acceleration-trial slices per DM work unit, so DMs with many trials "
+            "spread over the ranks (0 = auto: split when the job has fewer than 4 DM chunks per rank; 1 = never)",
+            a.accel_slices),
       val_n("", "sub_batch", "Fused-FFT trials per sub-batch on two alternating streams (0 = off, -1 = auto)",
             a.sub_batch),
       val_n("", "fft_mode", "Accel-trial FFT: 2 = fused resample + four-step FFT (default), 1 = rocFFT C2C(N/2), 0 = rocFFT R2C",

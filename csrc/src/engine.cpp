@@ -805,11 +805,15 @@ static int ilog2(uint64_t v) {
   return l;
 }
 
+AccelerationDistiller search_accel_distiller(const SearchParams& p) {
+  return AccelerationDistiller(static_cast<float>(static_cast<float>(p.fft_size) * p.tsamp), p.freq_tol, true);
+}
+
 SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     : p_(p),
       stream_(stream),
       harm_(p.freq_tol, static_cast<float>(p.max_harm), false, true),
-      accd_(static_cast<float>(static_cast<float>(p.fft_size) * p.tsamp), p.freq_tol, true) {
+      accd_(search_accel_distiller(p)) {
   PSOUP_CHECK(p_.fft_size >= 250, "fft_size too small");
   n_ = p_.fft_size;
   nb_ = n_ / 2 + 1;
@@ -1406,8 +1410,8 @@ std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(
   if (mode_ != 2 && njobs > 1) {
     // the rocFFT paths resample one series per batch: one job at a time
     for (int j = 0; j < njobs; ++j) {
-      const Job& jb = jobs[static_cast<size_t>(j)];
-      pd->out[static_cast<size_t>(j)] = search_prepared(jb.b, jb.dm, jb.dm_idx, jb.accs);
+      const std::vector<Job> one(1, jobs[static_cast<size_t>(j)]);
+      pd->out[static_cast<size_t>(j)] = std::move(search_prepared_many(one)[0]);
     }
     return pd;
   }
@@ -1454,6 +1458,10 @@ std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(
   auto send_done = [&](int processed) {
     while (jobs_sent < njobs && job_end[static_cast<size_t>(jobs_sent)] <= processed) {
       const int j = jobs_sent++;
+      if (jobs[static_cast<size_t>(j)].raw) {  // a slice: distilled once the slices are joined
+        pd->out[static_cast<size_t>(j)] = std::move(pd->by_job[static_cast<size_t>(j)]);
+        continue;
+      }
       {
         std::lock_guard<std::mutex> lk(pd->mu);
         pd->remaining++;

@@ -197,8 +197,15 @@ class RankSearcher:
         """Dedisperse + search DM blocks (every block's candidates, in
         processing order, as one CandidateBag): :meth:`search_iter` drained."""
         cands = _C.CandidateBag()
-        for _, got in self.search_iter(dm_indices, chunk, timers, progress, blocks, claim):
+        slices: List[int] = []
+        split = blocks is not None and any(len(b) > 2 and b[3] > 1 for b in blocks)
+        for j, got in self.search_iter(dm_indices, chunk, timers, progress, blocks, claim):
+            if split:
+                slices.extend([int(blocks[j][2]) if len(blocks[j]) > 2 else 0] * len(got))
             cands.extend(got)
+        # acceleration-sliced units (blocks of (d0, d1, s, S)): their lists are
+        # raw, and the merge joins a DM's slices (merge_split_*) by these indices
+        self.raw_slices = slices if split else None
         return cands
 
     def search_iter(self, dm_indices: Optional[Sequence[int]] = None, chunk: int = 32,
@@ -217,7 +224,9 @@ class RankSearcher:
         of the search loop.
 
         The blocks are ``dm_indices`` cut into ``chunk``-aligned pieces, or
-        ``blocks`` as given; with ``claim`` (a callable returning the next
+        ``blocks`` as given: ``(d0, d1)``, or ``(d0, d1, s, S)`` for slice s
+        of S of every DM's acceleration trials (contiguous in plan order; the
+        block's lists are then raw, :func:`accel_units`); with ``claim`` (a callable returning the next
         block index or None, e.g. ``pdist.WorkQueue.claim``) the blocks are
         taken first-come from a queue shared with the other ranks -- one block
         ahead, so the next block's dedispersion still overlaps this one's
@@ -228,7 +237,7 @@ class RankSearcher:
         if blocks is None:
             blocks = self.chunk_ranges(dm_indices, chunk)
         blocks = [tuple(b) for b in blocks]
-        width = max((d1 - d0 for d0, d1 in blocks), default=0)
+        width = max((b[1] - b[0] for b in blocks), default=0)
         if claim is None:
             order = iter(range(len(blocks)))
             claim = lambda: next(order, None)  # noqa: E731
@@ -267,8 +276,10 @@ class RankSearcher:
             j = claim()
             if j is None:
                 return None
-            d0, d1 = blocks[j]
+            d0, d1 = blocks[j][:2]
             ck = _C.spill_path(ckdir, d0, d1) if ckdir else ""
+            if ck and len(blocks[j]) > 2 and blocks[j][3] > 1:
+                ck += ".slice%dof%d" % (blocks[j][2], blocks[j][3])  # (a slice's raw list)
             if ck:
                 status, got = _C.load_spill_bag(ck, ckey)
                 if status == "loaded":
@@ -328,8 +339,8 @@ class RankSearcher:
             _, ck_, b0, b1, pend = blk
             per_dm: Dict[int, object] = {}
             for e_, jobs_, h_ in pend:
-                for (b, dm, d, accs), c in zip(jobs_, _C.collect_bags(e_, h_)):
-                    per_dm[d] = c
+                for job, c in zip(jobs_, _C.collect_bags(e_, h_)):
+                    per_dm[job[2]] = c
             chunk_cands = _C.CandidateBag()
             for d in range(b0, b1):
                 chunk_cands.extend(per_dm[d])
@@ -337,9 +348,18 @@ class RankSearcher:
                 _C.save_spill(ck_, ckey, chunk_cands)  # atomic; raises on a failed write
             return chunk_cands
 
+        def trials_of(d, blk):
+            """DM d's acceleration trials in unit ``blk`` (all, or its slice)."""
+            accs = self.accel_list(self.dm_list[d])
+            if len(blk) > 2 and blk[3] > 1:
+                s_, S_ = blk[2], blk[3]
+                accs = accs[s_ * len(accs) // S_:(s_ + 1) * len(accs) // S_]
+            return accs
+
         while cur is not None:
             j, ck, resumed, inflight = cur
-            d0, d1 = blocks[j]
+            d0, d1 = blocks[j][:2]
+            raw = len(blocks[j]) > 2 and blocks[j][3] > 1
             self.blocks_done.append(j)
             if resumed is not None:
                 if prev is not None:  # keep the block order of the candidate list
@@ -349,7 +369,7 @@ class RankSearcher:
                     yield pj, done
                 # resume: same spill format as the native pipeline (keyed CandidatePOD trees)
                 yield j, resumed
-                ntrials += sum(len(self.accel_list(self.dm_list[d])) for d in range(d0, d1))
+                ntrials += sum(len(trials_of(d, blocks[j])) for d in range(d0, d1))
                 if progress is not None:
                     progress(d1 - d0)
                 cur = pull()
@@ -383,14 +403,14 @@ class RankSearcher:
                     e.prepare(buf.data_ptr() + (part[0] - d0) * self.row_stride, step * self.row_stride,
                               self.geom.out_nsamps, len(part))
                     te1 = time.perf_counter()
-                    jobs = [(b, self.dm_list[d], d, self.accel_list(self.dm_list[d])) for b, d in enumerate(part)]
+                    jobs = [(b, self.dm_list[d], d, trials_of(d, blocks[j]), raw) for b, d in enumerate(part)]
                     # one flat trial list over the part's DMs (batches span DM boundaries)
                     h = e.search_prepared_many_async(jobs)
                     if _BLOCK_TRACE:
                         eng_t.setdefault(dms[0] - d0, []).append((te0 - tb1, te1 - te0, time.perf_counter() - te1))
                     with lock:
                         pend.append((e, jobs, h))
-                        for (b, dm, d, accs) in jobs:
+                        for (b, dm, d, accs, _) in jobs:
                             ntrials += len(accs)
                             if progress is not None:
                                 progress(1)
@@ -670,6 +690,51 @@ def dm_schedule(args, world_size: int, ndm: Optional[int] = None) -> str:
     return s
 
 
+MIN_SLICE_TRIALS = 64  # auto slicing keeps at least this many acceleration trials per DM and unit
+
+
+def accel_slices(args, world: int, nblocks: int, max_trials: int) -> int:
+    """Slices per DM of the acceleration trials (``--accel_slices``; 0 =
+    auto).  A job with fewer DM chunks than 4 per rank (a single DM at 2^23,
+    a short DM list on 8 GPUs) would leave ranks idle or finish on a few:
+    auto cuts every DM's trial list into S contiguous slices so that the
+    (chunk, slice) units number at least 4 per rank, with at least
+    MIN_SLICE_TRIALS trials per slice.  One rank: no slicing."""
+    v = int(getattr(args, "accel_slices", 0) or 0)
+    if v > 0:
+        return v
+    if world <= 1 or nblocks <= 0 or nblocks >= 4 * world:
+        return 1
+    want = -(-4 * world // nblocks)
+    cap = max(1, min(want, max_trials // MIN_SLICE_TRIALS))
+    # prefer a unit count the ranks divide evenly (1 DM on 8 ranks: 8 slices,
+    # not 10) unless that gives up more than half the slices
+    for s_ in range(cap, 0, -1):
+        if (nblocks * s_) % world == 0:
+            return s_ if 2 * s_ >= cap else cap
+    return cap
+
+
+def accel_units(blocks: List[tuple], S: int) -> List[tuple]:
+    """Work units: every DM block, or (d0, d1, s, S) for each of its S
+    acceleration slices (block-major, so ranks claiming in turn take the
+    slices of one block)."""
+    if S <= 1:
+        return [tuple(b[:2]) for b in blocks]
+    return [(b[0], b[1], s_, S) for b in blocks for s_ in range(S)]
+
+
+def unit_weight(rs: "RankSearcher", unit: tuple) -> int:
+    """Acceleration trials a work unit searches."""
+    tot = 0
+    for d in range(unit[0], unit[1]):
+        n = len(rs.accel_list(rs.dm_list[d]))
+        if len(unit) > 2 and unit[3] > 1:
+            n = (unit[2] + 1) * n // unit[3] - unit[2] * n // unit[3]
+        tot += n
+    return tot
+
+
 def keep_trials_fits(rs: RankSearcher, ndm: int, world: int) -> bool:
     """Keep every searched DM row in HBM for the fold stage when this rank's
     share (with 2x slack for dynamic-schedule imbalance) fits in a quarter of
@@ -734,8 +799,22 @@ def run_search(args, write: bool = True, as_rank: Optional[tuple] = None) -> Opt
     ndm = len(rs.dm_list)
     weights = [len(rs.accel_list(d)) for d in rs.dm_list]
     world = ctx.world_size if as_rank is None else as_rank[0]
-    schedule = "time_sharded" if sharded else "static" if as_rank else dm_schedule(args, world, ndm)
-    if schedule == "static":
+    # work units: 32-DM chunks, each cut into S acceleration slices when the
+    # job has too few chunks for the ranks (accel_slices)
+    nslices = 1 if sharded else accel_slices(args, world, -(-ndm // DYNAMIC_CHUNK), max(weights, default=0))
+    units = accel_units(rs.chunk_ranges(range(ndm), DYNAMIC_CHUNK), nslices) if nslices > 1 else None
+    if units is not None:
+        schedule = "static" if as_rank else dm_schedule(args, world, len(units) * DYNAMIC_CHUNK)
+    else:
+        schedule = "time_sharded" if sharded else "static" if as_rank else dm_schedule(args, world, ndm)
+    my_units = None
+    if schedule == "static" and units is not None:
+        uw = [unit_weight(rs, u) for u in units]
+        us = pdist.shard_range(len(units), world, ctx.rank if as_rank is None else as_rank[1], uw)
+        my_units = [units[i] for i in us]
+        if my_units:
+            rs.warm(my_units[0][0], my_units[-1][1])
+    elif schedule == "static":
         # a static shard's plan tables only (dynamic ranks may claim any chunk)
         shard = pdist.shard_range(ndm, world, ctx.rank if as_rank is None else as_rank[1], weights)
         if len(shard):
@@ -780,12 +859,16 @@ def run_search(args, write: bool = True, as_rank: Optional[tuple] = None) -> Opt
         local = rs.search_rows(rows, shard.start, timers)
         local_trials = sum(weights[i] for i in shard)
     elif schedule == "dynamic":
-        # DMDispenser across processes: every rank claims 32-DM chunks of the
-        # whole list from one shared first-come queue (pipeline_multi.cu:33-81)
-        blocks = rs.chunk_ranges(range(ndm), DYNAMIC_CHUNK)
+        # DMDispenser across processes: every rank claims 32-DM chunks (or
+        # their acceleration slices) of the whole list from one shared
+        # first-come queue (pipeline_multi.cu:33-81)
+        blocks = units if units is not None else rs.chunk_ranges(range(ndm), DYNAMIC_CHUNK)
         queue = pdist.WorkQueue("dm_chunks", len(blocks))
         local = rs.search(blocks=blocks, claim=queue.claim, timers=timers)
-        local_trials = sum(weights[d] for j in rs.blocks_done for d in range(*blocks[j]))
+        local_trials = sum(unit_weight(rs, blocks[j]) for j in rs.blocks_done)
+    elif my_units is not None:
+        local = rs.search(blocks=my_units, timers=timers)
+        local_trials = sum(unit_weight(rs, u) for u in my_units)
     else:
         local = rs.search(shard, timers=timers)
         local_trials = sum(weights[i] for i in shard)
@@ -793,7 +876,7 @@ def run_search(args, write: bool = True, as_rank: Optional[tuple] = None) -> Opt
     search_wall = time.perf_counter() - t0
     rank_stats = rs.counters()
     rank_stats.update({"rank": ctx.rank, "search_s": search_wall, "accel_trials_planned": local_trials,
-                       "device_init_s": device_init_s,
+                       "device_init_s": device_init_s, "accel_slices": nslices,
                        "dm_schedule": schedule, "dm_blocks": len(rs.blocks_done),
                        "fft_mode": rs.engine.fft_mode, "accel_batch": rs.engine.batch_size,
                        "sub_batch": rs.engine.sub_batch,
@@ -802,17 +885,35 @@ def run_search(args, write: bool = True, as_rank: Optional[tuple] = None) -> Opt
 
     # ---- candidate gather (RCCL) + global distillation on rank 0
     total_trials = sum(weights) if as_rank is None else local_trials
+    raw_slices = getattr(rs, "raw_slices", None) if nslices > 1 else None
+    if nslices > 1 and raw_slices is None:
+        raw_slices = []  # (a rank that searched no unit)
     if not ctx.distributed:
         # a world of one: the merge takes the rank's own list (no serialisation)
-        cands = _C.merge_local(local, args, rs.header)
+        if raw_slices is not None:
+            cands = _C.merge_split_local(local, raw_slices, args, rs.header)
+        else:
+            cands = _C.merge_local(local, args, rs.header)
     else:
         # every rank's list to rank 0 only (RCCL gather of raw buffers), merged
-        # there: rank order, stable by DM index, global distillation, scoring
+        # there: rank order, stable by DM index, global distillation, scoring.
+        # Acceleration-sliced units: their raw lists and slice indices, each
+        # DM's slices joined in plan order and acceleration-distilled on rank 0
+        # first (the list an unsplit DM's engine distils: identical output)
         bufs = pdist.gather_buffers(torch.from_numpy(_C.serialize_candidates_array(local)), dst=0)
+        sbufs = None
+        if raw_slices is not None:
+            sl = np.asarray(raw_slices, dtype=np.int32)
+            sbufs = pdist.gather_buffers(torch.from_numpy(sl.view(np.uint8)), dst=0)
         del local
-        cands = (_C.merge_candidate_buffers([(b.data_ptr(), b.numel()) for b in bufs], args, rs.header)
-                 if ctx.is_root else None)
-        del bufs
+        if not ctx.is_root:
+            cands = None
+        elif sbufs is not None:
+            cands = _C.merge_split_buffers([(b.data_ptr(), b.numel()) for b in bufs],
+                                           [(b.data_ptr(), b.numel() // 4) for b in sbufs], args, rs.header)
+        else:
+            cands = _C.merge_candidate_buffers([(b.data_ptr(), b.numel()) for b in bufs], args, rs.header)
+        del bufs, sbufs
         if args.npdmp > 0:
             # the fold stage needs the top candidates' frequency, acceleration
             # and DM row on every rank (not their association trees)

@@ -265,3 +265,42 @@ def test_compact_serialisation_of_search_stage_lists(C):
         assert full[:4] == b"COSP" and len(full) > len(blob)
         back = C.deserialize_candidates(full)
         assert [fields(c) for c in back] == [fields(c) for c in lst]
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_accel_distill_slices_equals_whole_dm_distillation(C, seed):
+    """Acceleration trials split into slices searched by different ranks
+    (search.accel_units): joined per DM in slice order and acceleration-
+    distilled (C.accel_distill_slices), the result equals distilling each
+    DM's whole trial-ordered list -- whatever order the ranks' lists arrive in."""
+    import random
+
+    rng = random.Random(seed)
+    tobs, tol = 42.0, 1e-4
+    per_dm = {}
+    for d in (3, 7, 8):
+        lst = []
+        for trial in range(40):  # plan order; each trial a few harmonic-distilled candidates
+            acc = -5.0 + 0.25 * trial
+            for _ in range(rng.randrange(0, 4)):
+                f = rng.choice([4.0, 8.0, 12.5]) * (1 + rng.uniform(-2e-4, 2e-4))
+                lst.append(C.Candidate(10.0 + d, d, acc, rng.randrange(0, 4), rng.uniform(6, 60), f))
+        per_dm[d] = lst
+    expect = []
+    for d in sorted(per_dm):
+        expect += C.AccelerationDistiller(tobs, tol, True).distill(list(per_dm[d]))
+    S = 5
+    units = []  # (rank-claimed unit, its candidates, slice index)
+    for d, lst in per_dm.items():
+        n = len(lst)
+        for s in range(S):
+            units.append((lst[s * n // S:(s + 1) * n // S], s))
+    rng.shuffle(units)  # ranks return their units in any order
+    cands, slices = [], []
+    for lst, s in units:
+        cands += lst
+        slices += [s] * len(lst)
+    got = C.accel_distill_slices(cands, slices, tobs, tol, 3)
+    key = lambda c: (c.dm_idx, c.acc, c.nh, c.snr, c.freq, len(c.assoc))  # noqa: E731
+    assert [key(c) for c in got] == [key(c) for c in expect]
+    assert [[key(a) for a in c.assoc] for c in got] == [[key(a) for a in c.assoc] for c in expect]

@@ -134,6 +134,71 @@ def test_multi_rank_search_equals_single_rank(tmp_path, world, schedule):
         assert sum(d["dm_blocks"] for d in devs) == 2
 
 
+def _run_ranks(tmp_path, script, world, out, extra_env=None):
+    port = _free_port()
+    f = tmp_path / "run.py"
+    f.write_text(script)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), **(extra_env or {}))
+    procs = []
+    for r in range(world):
+        e = dict(env, RANK=str(r), LOCAL_RANK="0")
+        procs.append(subprocess.Popen([sys.executable, str(f), str(out)], env=e, stdout=subprocess.PIPE,
+                                      stderr=subprocess.PIPE, text=True))
+    for p in procs:
+        _, err = p.communicate(timeout=600)
+        assert p.returncode == 0, err[-3000:]
+
+
+@pytest.mark.parametrize("world,schedule,slices", [(2, "static", "0"), (4, "static", "0"), (2, "dynamic", "3"),
+                                                    (4, "dynamic", "0")])
+def test_one_dm_job_acceleration_sliced_over_ranks(tmp_path, world, schedule, slices):
+    """A 1-DM job (one 32-DM chunk) on 2 and 4 ranks: the DM's acceleration
+    trials are cut into slices that the ranks search (static shards or the
+    shared queue); the per-trial harmonic-distilled slice lists are joined in
+    plan order on rank 0 and acceleration-distilled there, so the candidate
+    file is byte-identical to one rank's unsliced search."""
+    common = ("'-i',%r,'--dm_start','30','--dm_end','30','--acc_start','-20','--acc_end','20',"
+              "'--accel_convention','reference','-n','3','--npdmp','3'" % (TUTORIAL,))
+    script = (
+        "import os,sys; sys.path.insert(0, %r)\n"
+        "from peasoup_amd.parallel import dist as pdist\n"
+        "pdist.init(backend='gloo')\n"
+        "from peasoup_amd import _C\n"
+        "from peasoup_amd.models import search as S\n"
+        "S.MIN_SLICE_TRIALS = 4\n"
+        "ok,_,a=_C.parse_cmdline(['peasoup',%s,'-o',sys.argv[1],'--dm_schedule',%r,'--accel_slices',%r,"
+        "'--trace_json',sys.argv[1]+'.json'])\n"
+        "S.run_search(a)\n"
+        "pdist.shutdown()\n" % (REPO, common, schedule, slices))
+    _run_ranks(tmp_path, script, world, tmp_path / "dist")
+    single = (
+        "import sys; sys.path.insert(0, %r)\n"
+        "from peasoup_amd import _C\n"
+        "from peasoup_amd.models.search import run_search\n"
+        "ok,_,a=_C.parse_cmdline(['peasoup',%s,'-o',sys.argv[1]])\n"
+        "res = run_search(a)\n"
+        "print('NTRIALS', res.accel_trials)\n" % (REPO, common))
+    f1 = tmp_path / "single.py"
+    f1.write_text(single)
+    r = subprocess.run([sys.executable, str(f1), str(tmp_path / "single")],
+                       env=dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0"), capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    ntrials = int(r.stdout.split("NTRIALS")[1].split()[0])
+    assert ntrials >= 16
+    a = open(tmp_path / "dist" / "candidates.peasoup", "rb").read()
+    b = open(tmp_path / "single" / "candidates.peasoup", "rb").read()
+    assert len(b) > 0 and a == b
+    import json
+
+    devs = json.load(open(str(tmp_path / "dist") + ".json"))["devices"]
+    nsl = devs[0]["accel_slices"]
+    assert nsl == (int(slices) if slices != "0" else 4 * world) and all(d["accel_slices"] == nsl for d in devs)
+    # every trial searched exactly once over the ranks; more than one rank did work
+    assert sum(d["accel_trials_planned"] for d in devs) == ntrials
+    assert sum(1 for d in devs if d["accel_trials_planned"] > 0) >= 2
+
+
 def test_dynamic_schedule_four_ranks_many_chunks(tmp_path):
     """The mode 8-GPU config 4 uses: four ranks claim first-come 32-DM chunks
     from the shared queue, with 18 chunks (>= 4 per rank) on a 572-DM list;

@@ -133,6 +133,48 @@ def config3(a):
             "best_period_s": (1.0 / best.freq) if best else None, "best_snr": best.snr if best else None}
 
 
+def config3_pipeline(a, as_rank=None):
+    """Config 3 through the distributed driver (run_search): a 64-channel
+    2-bit filterbank with one accelerated pulsar, searched at one DM, 2^23
+    points, +-500 m/s^2, 8 harmonics.  Under torchrun (or --as-rank W:r) the
+    DM's 685 acceleration trials are cut into slices the ranks share
+    (search.accel_slices); one rank searches them all."""
+    from peasoup_amd.models.search import run_search
+
+    ctx = pdist.init()
+    n = 1 << 23
+    path = os.path.join(a.workdir, "cfg3_1dm.fil")
+    if ctx.is_root and not os.path.exists(path):
+        gpu_filterbank(path, n + 8192, 64, TSAMP, FCH1, -6.25, period=0.0123456, dm=50.0, duty=0.05, amp=0.3,
+                       seed=3)
+    pdist.barrier()
+    out = os.path.join(a.workdir, "out_cfg3" + (f"_as{as_rank[0]}_{as_rank[1]}" if as_rank else ""))
+    argv = ["peasoup", "-i", path, "-o", out, "--dm_start", "50", "--dm_end", "50", "--acc_start", "-500",
+            "--acc_end", "500", "-n", "3", "--npdmp", "0", "--limit", "1000"]
+    ok, _, args = _C.parse_cmdline(argv)
+    assert ok
+    t0 = time.perf_counter()
+    res = run_search(args, as_rank=as_rank)
+    wall = time.perf_counter() - t0
+    if not ctx.is_root:
+        return None
+    st = res.rank_stats[0] if res.rank_stats else {}
+    rec = {"config": 3, "driver": "run_search", "log2n": 23, "wall_s": round(wall, 3),
+           "accel_trials": res.accel_trials, "accel_slices": st.get("accel_slices"),
+           "search_s": round(st.get("search_s", 0.0), 4),
+           "timers_s": {k: round(v, 4) for k, v in res.timers.items()}, "candidates": len(res.candidates)}
+    if as_rank is not None:
+        rec.update({"as_rank": as_rank[1], "world": as_rank[0],
+                    "desc": f"rank {as_rank[1]} of a {as_rank[0]}-rank config-3 run (its acceleration slices)"})
+    else:
+        rec.update({"ranks": ctx.world_size, "desc": "1 DM, 2^23 samples, +-500 m/s^2, 8 harmonics, run_search",
+                    "trials_per_s": round(res.accel_trials / st["search_s"], 1) if st.get("search_s") else None})
+        if res.candidates:
+            b = res.candidates[0]
+            rec["best"] = {"period_s": 1.0 / b.freq, "acc": b.acc, "snr": b.snr}
+    return rec
+
+
 def config5_pulsars(n: int = 64, seed: int = 5):
     """The config-5 sky: n pulsars with incommensurate periods (2 ms - 1 s,
     log-uniform), DMs over the searched range, accelerations within +-100
@@ -261,9 +303,23 @@ def main():
     os.makedirs(a.workdir, exist_ok=True)
     ctx = pdist.init()
     for c in [int(x) for x in a.configs.split(",")]:
-        if c in (1, 2, 3):
+        if c == 3 and a.as_rank:
+            w, _, rs_ = a.as_rank.partition(":")
+            ranks = [int(x) for x in rs_.split(",") if x != ""]
+            assert ctx.world_size == 1 and ranks, a.as_rank
+            emit(dict(config3_pipeline(a), warmup=True), a.out)  # (and the one-rank reference)
+            emit(config3_pipeline(a), a.out)
+            for r in ranks:
+                emit(config3_pipeline(a, (int(w), r)), a.out)
+        elif c == 3:
             if ctx.is_root:
-                emit({1: config1, 2: config2, 3: config3}[c](a), a.out)
+                emit(config3(a), a.out)  # the engine alone
+            rec = config3_pipeline(a)  # the driver (all ranks under torchrun)
+            if rec is not None:
+                emit(rec, a.out)
+        elif c in (1, 2):
+            if ctx.is_root:
+                emit({1: config1, 2: config2}[c](a), a.out)
         elif c in (4, 5) and a.as_rank:
             w, _, rs_ = a.as_rank.partition(":")
             ranks = [int(x) for x in rs_.split(",") if x != ""]
