@@ -61,7 +61,7 @@ def parse():
                    help="trials per sub-batch on two alternating streams (0 = off, -1 = auto: off from 2^22 samples, else half a batch, at most 2^28 samples)")
     p.add_argument("--fft-mode", type=int, default=2,
                    help="2: fused resample + four-step FFT; 1: rocFFT C2C(N/2) + fused r2c post; 0: rocFFT R2C")
-    p.add_argument("--dedisp-kernel", default="auto", choices=["auto", "mfma", "valu", "direct"])
+    p.add_argument("--dedisp-kernel", default="auto", choices=["auto", "mfma", "valu", "direct", "packed2"])
     p.add_argument("--fft4-flags", type=int, default=-1, help="fused-FFT kernel variant flags (tuning; -1 = default)")
     p.add_argument("--harm-flags", type=int, default=-1,
                    help="harmonic-sum / tiled-r2c kernel variant flags (tuning; -1 = default)")

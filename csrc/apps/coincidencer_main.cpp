@@ -2,8 +2,10 @@
 // (src/coincidencer.cpp:46-215).  Each beam is dedispersed at DM 0,
 // whitened and normalised; a time sample / Fourier bin is masked when it
 // exceeds --thresh in at least --beam_thresh beams.  Beams are spread over
-// the visible GPUs; per-GPU uint8 indicator counts are summed on device 0.
+// the visible GPUs; per-GPU uint8 indicator counts are summed on device 0
+// (peer copies + kernels) and thresholded there.
 #include <algorithm>
+#include <memory>
 #include <iostream>
 #include <mutex>
 #include <thread>
@@ -39,7 +41,12 @@ int main(int argc, char** argv) {
     const float tsamp = static_cast<float>(fbs[0].tsamp());
     const uint64_t nb = size / 2 + 1;
     const int ngpu = std::max(1, std::min(device_count(), nfiles));
-    std::vector<std::vector<uint8_t>> tcounts(static_cast<size_t>(ngpu)), scounts(static_cast<size_t>(ngpu));
+    // per device: its stream and the uint8 beam counts of its beams
+    struct DevCounts {
+      std::unique_ptr<Stream> st;
+      DeviceBuffer<uint8_t> tc, sc;
+    };
+    std::vector<DevCounts> dc(static_cast<size_t>(ngpu));
     std::vector<std::thread> th;
     std::exception_ptr err;
     std::mutex mu;
@@ -47,8 +54,13 @@ int main(int argc, char** argv) {
       th.emplace_back([&, dev] {
         try {
           PSOUP_HIP_CHECK(hipSetDevice(dev));
-          Stream st;
-          DeviceBuffer<uint8_t> tc(size), sc(nb);
+          DevCounts& d = dc[static_cast<size_t>(dev)];
+          d.st = std::make_unique<Stream>();
+          Stream& st = *d.st;
+          d.tc.resize(size);
+          d.sc.resize(nb);
+          DeviceBuffer<uint8_t>& tc = d.tc;
+          DeviceBuffer<uint8_t>& sc = d.sc;
           tc.zero_async(st.get());
           sc.zero_async(st.get());
           for (int b = dev; b < nfiles; b += ngpu) {
@@ -66,10 +78,6 @@ int main(int argc, char** argv) {
             kern::count_above(bp.spectrum.data(), nb, args.threshold, sc.data(), st.get());
             PSOUP_HIP_CHECK(hipStreamSynchronize(st.get()));
           }
-          tcounts[dev].resize(size);
-          scounts[dev].resize(nb);
-          PSOUP_HIP_CHECK(hipMemcpy(tcounts[dev].data(), tc.data(), size, hipMemcpyDeviceToHost));
-          PSOUP_HIP_CHECK(hipMemcpy(scounts[dev].data(), sc.data(), nb, hipMemcpyDeviceToHost));
         } catch (...) {
           std::lock_guard<std::mutex> lk(mu);
           if (!err) err = std::current_exception();
@@ -79,17 +87,29 @@ int main(int argc, char** argv) {
     for (auto& t : th) t.join();
     if (err) std::rethrow_exception(err);
     if (args.verbose) log_info("Performing cross beam coincidence matching");
+    // every device's counts summed on device 0 (peer copies over xGMI where
+    // the pair allows), thresholded there into the two masks
+    PSOUP_HIP_CHECK(hipSetDevice(0));
+    hipStream_t s0 = dc[0].st->get();
+    DeviceBuffer<uint8_t> stage_t, stage_s;
+    if (ngpu > 1) {
+      stage_t.resize(size);
+      stage_s.resize(nb);
+    }
+    for (int d = 1; d < ngpu; ++d) {
+      enable_peer_access(0, d);
+      PSOUP_HIP_CHECK(hipMemcpyPeerAsync(stage_t.data(), 0, dc[static_cast<size_t>(d)].tc.data(), d, size, s0));
+      kern::add_counts(stage_t.data(), size, dc[0].tc.data(), s0);
+      PSOUP_HIP_CHECK(hipMemcpyPeerAsync(stage_s.data(), 0, dc[static_cast<size_t>(d)].sc.data(), d, nb, s0));
+      kern::add_counts(stage_s.data(), nb, dc[0].sc.data(), s0);
+    }
+    DeviceBuffer<float> d_samp(size), d_spec(nb);
+    kern::coincidence_mask(dc[0].tc.data(), size, args.beam_threshold, d_samp.data(), s0);
+    kern::coincidence_mask(dc[0].sc.data(), nb, args.beam_threshold, d_spec.data(), s0);
     std::vector<float> samp_mask(size), spec_mask(nb);
-    for (uint64_t i = 0; i < size; ++i) {
-      int c = 0;
-      for (int d = 0; d < ngpu; ++d) c += tcounts[d][i];
-      samp_mask[i] = static_cast<float>(c < args.beam_threshold);
-    }
-    for (uint64_t i = 0; i < nb; ++i) {
-      int c = 0;
-      for (int d = 0; d < ngpu; ++d) c += scounts[d][i];
-      spec_mask[i] = static_cast<float>(c < args.beam_threshold);
-    }
+    PSOUP_HIP_CHECK(hipMemcpyAsync(samp_mask.data(), d_samp.data(), size * sizeof(float), hipMemcpyDeviceToHost, s0));
+    PSOUP_HIP_CHECK(hipMemcpyAsync(spec_mask.data(), d_spec.data(), nb * sizeof(float), hipMemcpyDeviceToHost, s0));
+    PSOUP_HIP_CHECK(hipStreamSynchronize(s0));
     const float bin_width = static_cast<float>(1.0 / static_cast<float>(size * tsamp));
     write_samp_mask(samp_mask, args.samp_outfilename);
     write_birdie_list(spec_mask, bin_width, args.spec_outfilename);

@@ -302,6 +302,9 @@ struct DeviceInfo {
   size_t total_mem = 0;
 };
 int device_count();
+// Lets `device` read and write `peer`'s memory directly over xGMI (hipDeviceEnablePeerAccess,
+// idempotent); false where the pair cannot (the copies then stage through the host) or is one device.
+bool enable_peer_access(int device, int peer);
 DeviceInfo device_info(int device);
 int runtime_version();
 int driver_version();

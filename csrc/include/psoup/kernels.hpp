@@ -526,6 +526,8 @@ void fold_optimise(const float* folds, int nfold, const float2* shift_table, flo
 void count_above(const float* x, uint64_t n, float thresh, uint8_t* counts, hipStream_t s);
 // mask[i] = counts[i] < beam_thresh
 void coincidence_mask(const uint8_t* counts, uint64_t n, int beam_thresh, float* mask, hipStream_t s);
+// acc[i] += a[i] (uint8 beam counts of two devices' beams)
+void add_counts(const uint8_t* a, uint64_t n, uint8_t* acc, hipStream_t s);
 
 // ------------------------------------------------------------- correlation --
 void conjugate(float2* x, uint64_t n, hipStream_t s);

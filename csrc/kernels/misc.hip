@@ -21,6 +21,13 @@ __global__ void __launch_bounds__(256) count_above_kernel(const float* __restric
     counts[i] = static_cast<uint8_t>(counts[i] + (x[i] > thresh ? 1 : 0));
 }
 
+__global__ void __launch_bounds__(256) add_counts_kernel(const uint8_t* __restrict__ a, uint64_t n,
+                                                         uint8_t* __restrict__ acc) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < n; i += stride)
+    acc[i] = static_cast<uint8_t>(acc[i] + a[i]);
+}
+
 __global__ void __launch_bounds__(256) coincidence_mask_kernel(const uint8_t* __restrict__ counts, uint64_t n,
                                                                int beam_thresh, float* __restrict__ mask) {
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
@@ -53,6 +60,11 @@ __global__ void __launch_bounds__(256) cmul_kernel(const float2* __restrict__ x,
 }
 
 }  // namespace
+
+void add_counts(const uint8_t* a, uint64_t n, uint8_t* acc, hipStream_t s) {
+  add_counts_kernel<<<dev::grid_for(n, 256), 256, 0, s>>>(a, n, acc);
+  post_launch_check("add_counts_kernel", s);
+}
 
 void count_above(const float* x, uint64_t n, float thresh, uint8_t* counts, hipStream_t s) {
   count_above_kernel<<<dev::grid_for(n, 256), 256, 0, s>>>(x, n, thresh, counts);

@@ -128,6 +128,23 @@ int device_count() {
   return n;
 }
 
+bool enable_peer_access(int device, int peer) {
+  if (device == peer) return false;
+  int can = 0;
+  if (hipDeviceCanAccessPeer(&can, device, peer) != hipSuccess || !can) return false;
+  int prev = 0;
+  PSOUP_HIP_CHECK(hipGetDevice(&prev));
+  PSOUP_HIP_CHECK(hipSetDevice(device));
+  const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+  PSOUP_HIP_CHECK(hipSetDevice(prev));
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();  // (clear the sticky status of the benign error)
+    return true;
+  }
+  PSOUP_HIP_CHECK(e);
+  return true;
+}
+
 DeviceInfo device_info(int device) {
   hipDeviceProp_t p;
   PSOUP_HIP_CHECK(hipGetDeviceProperties(&p, device));

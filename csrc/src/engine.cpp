@@ -156,6 +156,10 @@ void fanout_impl(const std::vector<DeviceFilterbank*>& fbs, const std::vector<in
   int prev = 0;
   PSOUP_HIP_CHECK(hipGetDevice(&prev));
   const size_t n = fbs.size();
+  // device i pulls each chunk from the first device: with peer access the
+  // copy reads device 0's memory straight over xGMI instead of staging it
+  // through host memory
+  for (size_t i = 1; i < n; ++i) enable_peer_access(devices[i], devices[0]);
   // the packed bytes on every device (transient: freed on return)
   std::vector<DeviceBuffer<uint8_t>> packed(n);
   for (size_t i = 0; i < n; ++i) {

@@ -181,6 +181,8 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
       init_s = std::max(init_s, warm_device());
     }
     res.performance["device_init_s"] = init_s;
+    const char* dl = std::getenv("HIP_ENABLE_DEFERRED_LOADING");
+    res.performance["code_objects_deferred"] = dl && std::atoi(dl) == 0 ? 0 : 1;
   }
   mark("device_init");
   log_verbose("Using " + std::to_string(ngpu) + " GPU(s); " + std::to_string(setup.dm_list.size()) + " DM trials; fft " +

@@ -392,18 +392,20 @@ def shard_range(n: int, world: int, rank: int, weights: Optional[Sequence[float]
     w = [float(x) for x in weights]
     assert len(w) == n
     total = sum(w)
-    cuts = [0]
+    if total <= 0:
+        return shard_range(n, world, rank)
+    # item i goes to the shard its weight's midpoint falls in: contiguous,
+    # and n equal items on n ranks are one each (a greedy cut at the first
+    # item that reaches a rank's quota handed 86 + 85 trials to rank 0 and
+    # none to rank 7 for 8 acceleration slices of 685 trials)
+    owner = []
     acc = 0.0
-    k = 1
-    for i, x in enumerate(w):
+    for x in w:
+        owner.append(min(world - 1, int((acc + 0.5 * x) * world / total)))
         acc += x
-        while k < world and acc >= total * k / world:
-            cuts.append(i + 1)
-            k += 1
-    while len(cuts) < world:
-        cuts.append(n)
-    cuts.append(n)
-    return range(cuts[rank], cuts[rank + 1])
+    lo = next((i for i, o in enumerate(owner) if o >= rank), n)
+    hi = next((i for i, o in enumerate(owner) if o > rank), n)
+    return range(lo, hi)
 
 
 _QUEUE_SEQ: dict = {}
