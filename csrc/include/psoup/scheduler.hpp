@@ -7,9 +7,9 @@
 // every Worker thread pulls single DM trials from (src/pipeline_multi.cu:
 // 33-81, 209-243).  Here, per device:
 //   * one feeder thread pulls DM chunks [d0, d1) from the queue shared by all
-//     devices (one atomic add), prepares each into one of two slots (the
-//     dedispersion of the next chunk overlaps the search of this one; or a
-//     checkpoint spill is loaded: a "resumed" chunk) and publishes it;
+//     devices (one atomic add), prepares each into one of kSchedSlots slots
+//     (the dedispersion of the next chunk overlaps the search of this one; or
+//     a checkpoint spill is loaded: a "resumed" chunk) and publishes it;
 //   * neng engine threads take every published chunk in order, issue their
 //     share of its searches (Ops::issue) and only then finalize the previous
 //     chunk (Ops::collect), so each chunk's host tail overlaps the next
@@ -41,6 +41,13 @@
 #include <vector>
 
 namespace psoup {
+
+// Chunk slots per device: with three, the feeder prepares chunk k + 1 (its
+// dedispersion on the GPU beside chunk k's search) while chunk k - 1 is still
+// being collected and handed over; with two it had to wait for that hand-over,
+// which comes after chunk k's searches were issued, and the next chunk's
+// dedispersion then ran alone on the GPU.
+constexpr int kSchedSlots = 3;
 
 template <class Item>
 struct SchedChunk {
@@ -96,7 +103,7 @@ class ChunkScheduler {
   struct Dev {
     std::mutex mu;
     std::condition_variable cv;
-    Chunk pub[2];
+    Chunk pub[kSchedSlots];
     long published = 0;
     bool done = false;
   };
@@ -139,7 +146,7 @@ class ChunkScheduler {
           dv.published++;
         }
         dv.cv.notify_all();
-        k ^= 1;
+        k = (k + 1) % kSchedSlots;
       }
     } catch (...) {
       fail();
@@ -195,7 +202,7 @@ class ChunkScheduler {
           if (abort_.load() || dv.published <= g) break;
         }
         Issued cur;
-        cur.slot = static_cast<int>(g & 1);
+        cur.slot = static_cast<int>(g % kSchedSlots);
         const Chunk& c = dv.pub[cur.slot];
         if (!c.resumed) {
           try {

@@ -702,29 +702,53 @@ __global__ void __launch_bounds__(256) dedisperse_2bit_kernel(
         a8[j][m] = 0;
       }
   };
-  // staging: thread (q = t / 32, e = t % 32) loads 16-byte vectors e, e + 32,
-  // e + 64 of channel q's window (wvec vectors: a launch-wide bound)
+  // Staging, per group of k2bCpb channels, one group ahead (double buffer):
+  // thread (q = t / 32, e = t % 32) loads 16-byte vectors e, e + 32, e + 64
+  // of channel q's window (wvec vectors: a launch-wide bound); threads t <
+  // k2bCpb * 4 DPW also write one entry of the group's rel table (a DM
+  // offset minus the channel's window start: the compute reads it from LDS,
+  // uniform).  The indices behind those loads -- the window channel's row
+  // (active) and start (wmin), the rel entry's offset and window start --
+  // are loaded a further group ahead and parked in LDS with the windows, so
+  // no global load waits on another issued in the same group (one dependent
+  // round trip per 8 channels was most of the kernel at 2^20).
+  constexpr int kRel = k2bCpb * 4 * DPW;  // rel entries per group
+  static_assert(kRel <= 256, "one rel entry per thread");
+  __shared__ int rel_l[2][kRel];
+  __shared__ int4 idx_l[2][256];
   const int sq = threadIdx.x >> 5, se = threadIdx.x & 31;
-  u32x4 r[3];
-  auto gload = [&](int c0) {
+  const int rq = static_cast<int>(threadIdx.x) / (4 * DPW), rk = static_cast<int>(threadIdx.x) % (4 * DPW);
+  const bool rthread = static_cast<int>(threadIdx.x) < kRel;
+  auto iload = [&](int c0) {  // {row, window start, rel offset, rel window start} of group c0
     const int ci = min(c0 + sq, nactive - 1);  // past the end: a harmless reload
-    const uint32_t* row = x2 + static_cast<uint64_t>(active[ci]) * stride2 + ((tb + (wm[ci] & ~63)) >> 4);
+    int4 v = make_int4(active[ci], wm[ci], 0, 0);
+    if (rthread) {
+      const int cr = min(c0 + rq, nactive - 1);
+      v.z = offT[static_cast<uint64_t>(cr) * ldo + d_base + static_cast<int>(blockIdx.x) * 4 * DPW + rk];
+      v.w = wm[cr];
+    }
+    return v;
+  };
+  u32x4 r[3];
+  int relv = 0;
+  auto gload = [&](const int4 ix) {
+    const uint32_t* row = x2 + static_cast<uint64_t>(ix.x) * stride2 + ((tb + (ix.y & ~63)) >> 4);
 #pragma unroll
     for (int i = 0; i < 3; ++i)
       if (se + 32 * i < wvec) r[i] = *reinterpret_cast<const u32x4*>(row + 4 * (se + 32 * i));
+    relv = ix.z - (ix.w & ~63);  // >= 0
   };
   auto lstore = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < 3; ++i)
       if (se + 32 * i < wvec) *reinterpret_cast<u32x4*>(&win[buf][sq * k2bWinDw + 4 * (se + 32 * i)]) = r[i];
+    if (rthread) rel_l[buf][threadIdx.x] = relv;
   };
-  auto compute = [&](int ci, const uint32_t* wb) {
-    const int w0 = wm[ci] & ~63;
-    const int32_t* o = offT + static_cast<uint64_t>(ci) * ldo + d_base + dm0;
+  auto compute = [&](int ci, int q, const uint32_t* wb, const int* rl) {
     uint32_t d[DPW][3], sh[DPW];
 #pragma unroll
     for (int j = 0; j < DPW; ++j) {
-      const int rel = o[j] - w0;  // >= 0, wave-uniform
+      const int rel = rl[q * 4 * DPW + wave * DPW + j];  // >= 0, wave-uniform (an LDS broadcast)
       sh[j] = 2u * static_cast<uint32_t>(rel & 15);
       const uint32_t* src = wb + 2 * lane + (rel >> 4);
       d[j][0] = src[0];
@@ -743,16 +767,23 @@ __global__ void __launch_bounds__(256) dedisperse_2bit_kernel(
     if ((ci & 3) == 3) flush4();    // wave-uniform
     if ((ci & 63) == 63) flush8();
   };
-  gload(0);
+  gload(iload(0));
+  if (k2bCpb < nactive) idx_l[1][threadIdx.x] = iload(k2bCpb);  // group 1's indices
   lstore(0);
   __syncthreads();
   for (int c0 = 0, it = 0; c0 < nactive; c0 += k2bCpb, ++it) {
     const int buf = it & 1;
-    if (c0 + k2bCpb < nactive) gload(c0 + k2bCpb);  // in flight during these channels' sums
+    const bool more = c0 + k2bCpb < nactive, more2 = c0 + 2 * k2bCpb < nactive;
+    int4 nx = make_int4(0, 0, 0, 0);
+    if (more) {
+      gload(idx_l[buf ^ 1][threadIdx.x]);       // group + 1's windows, in flight during the sums
+      if (more2) nx = iload(c0 + 2 * k2bCpb);  // group + 2's indices
+    }
 #pragma unroll 2
     for (int q = 0; q < k2bCpb; ++q)
-      if (c0 + q < nactive) compute(c0 + q, &win[buf][q * k2bWinDw]);
-    if (c0 + k2bCpb < nactive) lstore(buf ^ 1);
+      if (c0 + q < nactive) compute(c0 + q, q, &win[buf][q * k2bWinDw], rel_l[buf]);
+    if (more) lstore(buf ^ 1);
+    if (more2) idx_l[buf][threadIdx.x] = nx;  // (group + 2 uses buffer `buf` again)
     __syncthreads();
   }
   flush4();

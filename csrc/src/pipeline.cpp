@@ -339,11 +339,13 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   struct DevSched {
     std::atomic<int> processed{0};
     std::unique_ptr<Stream> dstream;
-    std::unique_ptr<DeviceBuffer<uint8_t>> trials[2];
-    Event ready[2] = {Event(true), Event(true)}, began[2] = {Event(true), Event(true)};
-    std::vector<std::unique_ptr<Event>> freed[2];
-    bool used[2] = {false, false};
-    const uint8_t* rows[2] = {nullptr, nullptr};  // the slot's dedispersed rows (row d at rows + (d - d0) * rstride)
+    static_assert(kSchedSlots == 3, "one initialiser per slot below");
+    std::unique_ptr<DeviceBuffer<uint8_t>> trials[kSchedSlots];
+    Event ready[kSchedSlots] = {Event(true), Event(true), Event(true)},
+          began[kSchedSlots] = {Event(true), Event(true), Event(true)};
+    std::vector<std::unique_ptr<Event>> freed[kSchedSlots];
+    bool used[kSchedSlots] = {};
+    const uint8_t* rows[kSchedSlots] = {};  // the slot's dedispersed rows (row d at rows + (d - d0) * rstride)
     double dd_ms = 0.0;
     std::vector<Stopwatch> search_w;  // per engine
   };
@@ -376,7 +378,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     PSOUP_HIP_CHECK(hipSetDevice(hip_dev(d)));
     auto sc = std::make_unique<DevSched>();
     sc->dstream = std::make_unique<Stream>();
-    for (int k = 0; k < 2; ++k) {
+    for (int k = 0; k < kSchedSlots; ++k) {
       if (!keep) sc->trials[k] = std::make_unique<DeviceBuffer<uint8_t>>(rstride * static_cast<uint64_t>(sh.chunk));
       for (int e = 0; e < neng; ++e) sc->freed[k].push_back(std::make_unique<Event>());
     }

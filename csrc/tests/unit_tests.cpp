@@ -289,7 +289,7 @@ struct FakeRun {
   }
   static bool resumed_chunk(int d0, int chunk) { return (d0 / chunk) % 5 == 3; }
   void run() {
-    slot_of.assign(static_cast<size_t>(ndev) * 2, {-1, -1, 0, 0});
+    slot_of.assign(static_cast<size_t>(ndev) * kSchedSlots, {-1, -1, 0, 0});
     SchedFns<int, std::vector<int>> ops;
     using Chunk = SchedChunk<int>;
     ops.prepare = [&](int dev, int k, Chunk& c) {
@@ -300,13 +300,13 @@ struct FakeRun {
         for (int d = c.d0; d < c.d1; ++d) c.items.push_back(d);
         return;
       }
-      auto& sl = slot_of[static_cast<size_t>(dev) * 2 + k];
+      auto& sl = slot_of[static_cast<size_t>(dev) * kSchedSlots + k];
       sl[0] = c.d0;  // "dedisperse" into the slot
       sl[1] = c.d1;
       sl[2]++;
     };
     ops.issue = [&](int dev, int eng, int k, const Chunk& c) {
-      const auto& sl = slot_of[static_cast<size_t>(dev) * 2 + k];
+      const auto& sl = slot_of[static_cast<size_t>(dev) * kSchedSlots + k];
       if (sl[0] != c.d0 || sl[1] != c.d1) throw std::runtime_error("slot refilled under a reading engine");
       std::vector<int> mine;
       for (int d = c.d0 + eng; d < c.d1; d += neng) mine.push_back(d);

@@ -36,12 +36,13 @@ def report(name, ev, names=NAMES):
 
 def main():
     flags = int(sys.argv[1]) if len(sys.argv) > 1 else -1  # fft4 flag set (-1: the default)
+    log2n = int(sys.argv[2]) if len(sys.argv) > 2 else 23
     if flags >= 0:
         K_.fft4_set_flags(flags)
     dev = torch.device("cuda")
-    n = 1 << 23
+    n = 1 << log2n
     M = n // 2
-    K = 32
+    K = 32 if log2n <= 23 else 8
     s = torch.cuda.current_stream().cuda_stream
     g = K_.fft4_geometry(M)
     g.ypair = K_.fft4_pair_y(g)  # pass A hands the spectrum pass row-pair Y (the engine's fused path)
