@@ -250,14 +250,45 @@ struct Fft4Geom {
   // Y in row pairs, Y_p[k2/2][i][k2%2], instead of 8x8 tiles (only where
   // fft4_pair_y(g) holds; read by fft4_rowpass_spectrum alone)
   bool ypair = false;
+  // every trial is a plain FFT (af = 0: the whitener's forward and inverse
+  // transforms): the one-exchange pass A reads the padded input in column
+  // strips; the Stockham pass A can read the sources below directly
+  bool zero_shift = false;
+  // zero_shift, Stockham pass A only (fft4_direct_source(g)): read trial k's
+  // series straight from its source instead of in_pad --
+  //   u8: 8-bit rows at u8 + src * src_stride, sample i < u8_nvalid as is,
+  //       then the row mean u8sum[src] / u8_nvalid up to n (the whitener's
+  //       forward input: no f32 copy, no pad kernel);
+  //   c2r: half spectra X (M + 1 bins at c2r + src * src_stride), turned into
+  //       the C2R pre-processed series on the fly (fft4_c2r_pre's arithmetic,
+  //       bit for bit: the whitener's inverse)
+  const uint8_t* u8 = nullptr;
+  const unsigned long long* u8sum = nullptr;
+  uint64_t u8_nvalid = 0;
+  const float2* c2r = nullptr;
+  uint64_t src_stride = 0;
+  //   f32_direct: the unpadded series in + src * in_tstride itself (no pad copy);
+  //   strips_direct: in_pad in column strips (fft4_pad_input_u8's layout)
+  bool f32_direct = false, strips_direct = false;
 };
 Fft4Geom fft4_geometry(uint64_t M);
+// Pass A of g can take the u8 / c2r direct sources (a zero-shift geometry
+// whose column pass is the Stockham kernel).
+bool fft4_direct_source(const Fft4Geom& g);
+// fft4_pad_input writes g's padded input in column strips (fft4_pad_input_u8 needs it)
+bool fft4_strip_layout(const Fft4Geom& g);
 // Twiddle tables (upload once per plan): see fft4step.hip for the layout.
 std::vector<float2> fft4_tables(const Fft4Geom& g);
 // Padded copy of the (whitened) input series read by pass A; insize floats.
 // count > 1: series b at in + b*in_stride -> in_pad + b*g.insize.
 void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& g, hipStream_t s, int count = 1,
                     uint64_t in_stride = 0);
+// The same padded copy straight from 8-bit dedispersed rows (strip layouts
+// only: fft4_strip_layout(g), or a direct-source geometry's strips_direct): sample i < nvalid is in[i], then
+// the row mean (sum[b] / nvalid) up to n, zeros beyond -- u8_to_f32_pad and
+// fft4_pad_input in one pass.  count rows at in + b * in_stride.
+void fft4_pad_input_u8(const uint8_t* in, uint64_t nvalid, uint64_t n, const unsigned long long* sum, float* in_pad,
+                       const Fft4Geom& g, hipStream_t s, int count, uint64_t in_stride);
 // Pass A: Y[k][k2][i] = W_M^{i k2} sum_j z_k[n1 j + i] W_n2^{j k2}, where
 // z_k[m] = x_k[2m] + i x_k[2m+1] and x_k = resampleII(in, af[k]); n = 2M.
 void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
@@ -390,6 +421,13 @@ enum Fft4Flags : int {
                            // dependent global round trip after the loads
   kFft4WideY = 8388608,    // one-exchange pass A, row-pair Y: lane pairs swap halves (DPP) so every lane
                            // stores 16 bytes (half the store instructions)
+  kFft4WhitenStrips = 16777216,  // whitener (plain FFTs, Fft4Geom::zero_shift): the one-exchange pass A reads
+                                 // the 8-bit rows staged into strips; the Stockham pass A reads its inverse
+                                 // input straight from the half spectra (C2R pre-processing fused) and
+  kFft4WhitenU8 = 33554432,      // its forward input straight from the 8-bit rows,
+  kFft4WhitenF32 = 67108864,     // or the unpadded f32 copy (neither: the 8-bit rows staged into strips).
+                                 // 2^20 bench A/B (gpurun_out whiten6d/e): strips / u8 / f32 all +1.5-2% over
+                                 // the f32 copy + pad path, within noise of each other; u8 moves the fewest bytes
   kFft4StripInput = 1073741824,  // one-exchange pass A: the padded input in column strips (16 + 4 floats of
                                  // every row per strip, strips row-contiguous), so a wave's 16 rows are
                                  // one ~1.3 KiB contiguous range instead of 16 pieces 16 KiB apart

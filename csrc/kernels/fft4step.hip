@@ -380,24 +380,111 @@ __host__ __device__ inline bool onex_colpass(int n2, int f) {
   return (f & kFft4OneX) && (f & kFft4Blocked) && (f & kFft4TileY) && n2 == 2048;
 }
 __host__ __device__ inline bool strip_input(int n2, int f) { return (f & kFft4StripInput) && onex_colpass(n2, f); }
+// the padded input of g is in strips: the one-exchange pass A reads them
+// (always for the whitener's zero-shift transforms)
+inline bool strip_layout(const Fft4Geom& g, int f) {
+  return strip_input(g.n2, f) || (g.zero_shift && onex_colpass(g.n2, f));
+}
 // pass A writes row-pair Y for the fused spectrum pass: the one-exchange
 // kernel always can, the tiled-Y Stockham kernel with kFft4PairY
 __host__ __device__ inline bool pair_y_layout(int n2, int f) {
   return onex_colpass(n2, f) || ((f & kFft4PairY) && (f & kFft4Blocked) && (f & kFft4TileY));
 }
 
+// Strip-layout copies, one thread per strip row (b, j): out[(b N2 + j) 20 +
+// e] = x[j rowlen + 16 b + e], e < 20, where x is the series (float, or
+// 8-bit with the row mean past nvalid) and zero past n.  Consecutive lanes
+// take consecutive rows of a strip, so a wave's stores are one contiguous
+// 5 KiB range; its loads hit 64 rows at once and the other strips of those
+// rows (the neighbouring waves) read the same lines out of L2.  The source
+// span of a strip row starts at a multiple of 16 elements: with an aligned
+// row base it is a 16-byte vector load sequence.
+__device__ __forceinline__ void store_strip_row(float* __restrict__ o, const float (&x)[kStripW]) {
+  f4v* d = reinterpret_cast<f4v*>(o);
+#pragma unroll
+  for (int u = 0; u < kStripW / 4; ++u) d[u] = f4v{x[4 * u], x[4 * u + 1], x[4 * u + 2], x[4 * u + 3]};
+}
+
+// 8-bit rows -> strips through LDS: a workgroup stages R consecutive rows
+// (coalesced 16-byte loads; row pitch rowlen + 16 bytes, so the strip-row
+// reads below spread over the banks) plus the head of the next row (the last
+// strip's 4-float tail), then writes R rows of every strip: per strip one
+// contiguous 80 R-byte range.  Samples past nvalid are the row mean, past n
+// zero (as u8_to_f32_pad + fft4_pad_input).
+constexpr int kStripLdsBytes = 32768;
+__global__ void __launch_bounds__(256) fft4_strips_u8_kernel(const uint8_t* __restrict__ in, uint64_t nvalid, uint64_t n,
+                                                             const unsigned long long* __restrict__ sum,
+                                                             float* __restrict__ out, uint32_t rowlen, uint32_t nrows,
+                                                             int log2_r, uint64_t in_stride, uint64_t out_stride) {
+  __shared__ __attribute__((aligned(16))) uint8_t st[kStripLdsBytes + 16 * 17 + 16];
+  in += blockIdx.y * in_stride;
+  out += blockIdx.y * out_stride;
+  const uint32_t R = 1u << log2_r, pitch = rowlen + 16, j0 = blockIdx.x * R;
+  const float mean = nvalid ? static_cast<float>(static_cast<double>(sum[blockIdx.y]) / static_cast<double>(nvalid))
+                            : 0.f;
+  // stage rows j0 .. j0 + R - 1 whole and the first 16 bytes of row j0 + R
+  const uint32_t c16 = rowlen >> 4, nchunks = R * c16 + 1;
+  for (uint32_t i = threadIdx.x; i < nchunks; i += blockDim.x) {
+    const uint32_t r = i / c16, c = i - r * c16;
+    const uint64_t s0 = static_cast<uint64_t>(j0 + r) * rowlen + 16u * c;
+    uint4 w = make_uint4(0u, 0u, 0u, 0u);
+    if (s0 + 16 <= nvalid) {
+      w = *reinterpret_cast<const uint4*>(in + s0);
+    } else if (s0 < nvalid) {
+      uint32_t wd[4] = {0u, 0u, 0u, 0u};
+      for (uint32_t e = 0; e < 16 && s0 + e < nvalid; ++e) wd[e >> 2] |= static_cast<uint32_t>(in[s0 + e]) << (8 * (e & 3));
+      w = make_uint4(wd[0], wd[1], wd[2], wd[3]);
+    }
+    *reinterpret_cast<uint4*>(st + r * pitch + 16u * c) = w;
+  }
+  __syncthreads();
+  const uint32_t nstrips = rowlen >> 4, total = nstrips << log2_r;
+  for (uint32_t u = threadIdx.x; u < total; u += blockDim.x) {
+    const uint32_t b = u >> log2_r, jj = u & (R - 1u);
+    const uint4 w = *reinterpret_cast<const uint4*>(st + jj * pitch + 16u * b);
+    const uint32_t tail = 16u * b + 16u < rowlen ? *reinterpret_cast<const uint32_t*>(st + jj * pitch + 16u * b + 16u)
+                                                 : *reinterpret_cast<const uint32_t*>(st + (jj + 1u) * pitch);
+    const uint32_t wd[5] = {w.x, w.y, w.z, w.w, tail};
+    const uint64_t s0 = static_cast<uint64_t>(j0 + jj) * rowlen + 16u * b;
+    float x[kStripW];
+    if (s0 + kStripW <= nvalid) {
+#pragma unroll
+      for (int e = 0; e < kStripW; ++e) x[e] = static_cast<float>((wd[e >> 2] >> (8 * (e & 3))) & 255u);
+    } else {
+#pragma unroll
+      for (int e = 0; e < kStripW; ++e)
+        x[e] = s0 + e < nvalid ? static_cast<float>((wd[e >> 2] >> (8 * (e & 3))) & 255u) : (s0 + e < n ? mean : 0.f);
+    }
+    store_strip_row(out + (static_cast<uint64_t>(b) * nrows + j0 + jj) * kStripW, x);
+  }
+}
+
 __global__ void __launch_bounds__(256) fft4_pad_strips_kernel(const float* __restrict__ in, uint64_t n,
                                                               float* __restrict__ out, uint32_t rowlen,
-                                                              uint32_t nrows, uint32_t total, uint64_t in_stride,
-                                                              uint64_t out_stride) {
+                                                              int log2_nrows, uint32_t nstriprows, uint64_t in_stride,
+                                                              uint64_t out_stride, bool aligned) {
   in += blockIdx.y * in_stride;
   out += blockIdx.y * out_stride;
   const uint32_t stride = gridDim.x * blockDim.x;
-  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < total; u += stride) {
-    const uint32_t rest = u / kStripW, e = u - rest * kStripW;
-    const uint32_t b = rest / nrows, j = rest - b * nrows;
-    const uint64_t src = static_cast<uint64_t>(j) * rowlen + 16u * b + e;
-    out[u] = src < n ? in[src] : 0.f;
+  for (uint32_t u = blockIdx.x * blockDim.x + threadIdx.x; u < nstriprows; u += stride) {
+    const uint32_t b = u >> log2_nrows, j = u & ((1u << log2_nrows) - 1u);
+    const uint64_t s0 = static_cast<uint64_t>(j) * rowlen + 16u * b;
+    float x[kStripW];
+    if (aligned && s0 + kStripW <= n) {
+      const f4v* src = reinterpret_cast<const f4v*>(in + s0);
+#pragma unroll
+      for (int u4 = 0; u4 < kStripW / 4; ++u4) {
+        const f4v w = src[u4];
+        x[4 * u4] = w.x;
+        x[4 * u4 + 1] = w.y;
+        x[4 * u4 + 2] = w.z;
+        x[4 * u4 + 3] = w.w;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < kStripW; ++e) x[e] = s0 + e < n ? in[s0 + e] : 0.f;
+    }
+    store_strip_row(out + static_cast<uint64_t>(u) * kStripW, x);
   }
 }
 
@@ -409,8 +496,14 @@ __global__ void __launch_bounds__(256) fft4_pad_strips_kernel(const float* __res
 // bit 4 = row-pair Y (pass A -> fused spectrum pass): Y_p[k2/2][i][k2%2].
 constexpr int kModeBlocked = 1, kModeTileY = 4, kModeTileX = 8, kModePairY = 16;
 
+// Pass A input sources: the padded series, resampled per trial (in_pad), or
+// for the whitener's plain FFTs (Fft4Geom::u8 / c2r) the 8-bit rows or the
+// half spectra themselves.  Separate instantiations, so the search's kernel
+// keeps its registers.
+constexpr int kSrcPad = 0, kSrcU8 = 1, kSrcC2R = 2, kSrcF32 = 3, kSrcStrips = 4;
+
 // Pass A.  Logical block = column block * K + trial (trial fastest).
-template <int L, int CPT, int SUB, int MODE>
+template <int L, int CPT, int SUB, int MODE, int SRC = kSrcPad>
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::THREADS), amdgpu_waves_per_eu(2))) fft4_colpass_kernel(
     const float* __restrict__ in, const float* __restrict__ in_pad, uint64_t n, const double* __restrict__ afs, int K,
     float2* __restrict__ Y, Fft4Geom g, const float2* __restrict__ tab, int flags) {
@@ -450,15 +543,119 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
       static_cast<uint32_t>(g.tsrc ? g.tsrc[k] : static_cast<uint64_t>(k)));
   const double size = static_cast<double>(n);
   Vec<CPT> v;
+  if constexpr (SRC == kSrcU8) {
+    // the whitener's forward input straight from the 8-bit row: row j's
+    // columns c0 .. c0+CPT-1 are 2 CPT consecutive bytes (one 16-byte load)
+    static_assert(CPT == 8 || CPT == 4, "8-bit rows: 16- or 8-byte loads");
+    const uint8_t* row = g.u8 + src * g.src_stride;
+    const uint64_t nvalid = g.u8_nvalid;
+    const float mean = nvalid ? static_cast<float>(static_cast<double>(g.u8sum[src]) / static_cast<double>(nvalid))
+                              : 0.f;
 #pragma unroll
-  for (int q = 0; q < kPts; ++q) {
-    const uint64_t j = t + q * T;
-    float x[2 * CPT];
-    load_resampled<2 * CPT>(in + src * g.in_tstride, in_pad + src * g.pad_tstride, static_cast<uint32_t>(n), log2row,
-                            static_cast<uint32_t>(g.inpitch), af, size,
-                            2u * (static_cast<uint32_t>(N1) * static_cast<uint32_t>(j) + static_cast<uint32_t>(c0)), x);
+    for (int q = 0; q < kPts; ++q) {
+      const uint64_t s0 = 2 * (static_cast<uint64_t>(N1) * (t + q * T) + c0);
+      float x[2 * CPT];
+      if (s0 + 2 * CPT <= nvalid) {
+        uint32_t wd[CPT / 2];
+        if constexpr (CPT == 8) {
+          const uint4 w = *reinterpret_cast<const uint4*>(row + s0);
+          wd[0] = w.x, wd[1] = w.y, wd[2] = w.z, wd[3] = w.w;
+        } else {
+          const uint2 w = *reinterpret_cast<const uint2*>(row + s0);
+          wd[0] = w.x, wd[1] = w.y;
+        }
 #pragma unroll
-    for (int c = 0; c < CPT; ++c) v[c][q] = make_float2(x[2 * c], x[2 * c + 1]);
+        for (int e = 0; e < 2 * CPT; ++e) x[e] = static_cast<float>((wd[e >> 2] >> (8 * (e & 3))) & 255u);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 2 * CPT; ++e) x[e] = s0 + e < nvalid ? static_cast<float>(row[s0 + e]) : (s0 + e < n ? mean : 0.f);
+      }
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) v[c][q] = make_float2(x[2 * c], x[2 * c + 1]);
+    }
+  } else if constexpr (SRC == kSrcStrips) {
+    // the padded input in column strips (fft4_pad_input_u8): row j's columns
+    // c0 .. c0+CPT-1 are 2 CPT consecutive floats of strip 2 c0 / 16, and a
+    // wave's consecutive rows are consecutive 80-byte strip rows
+    static_assert((2 * CPT) % 4 == 0 && 2 * CPT <= 16, "strip reads");
+    const float* sp = in_pad + src * g.pad_tstride + (static_cast<uint64_t>((2 * c0) >> 4) * L) * kStripW + ((2 * c0) & 15);
+#pragma unroll
+    for (int q = 0; q < kPts; ++q) {
+      const f4u* p4 = reinterpret_cast<const f4u*>(sp + static_cast<uint64_t>(t + q * T) * kStripW);
+#pragma unroll
+      for (int u = 0; u < CPT / 2; ++u) {
+        const f4u w = p4[u];
+        v[2 * u][q] = make_float2(w.x, w.y);
+        v[2 * u + 1][q] = make_float2(w.z, w.w);
+      }
+    }
+  } else if constexpr (SRC == kSrcF32) {
+    // plain FFT of an unpadded series: row j's columns are 2 CPT consecutive
+    // floats (no resampling, so no padded copy and no window)
+    const float* row = in + src * g.in_tstride;
+#pragma unroll
+    for (int q = 0; q < kPts; ++q) {
+      const f4v* p4 = reinterpret_cast<const f4v*>(row + 2 * (static_cast<uint64_t>(N1) * (t + q * T) + c0));
+#pragma unroll
+      for (int u = 0; u < CPT / 2; ++u) {
+        const f4v w = p4[u];
+        v[2 * u][q] = make_float2(w.x, w.y);
+        v[2 * u + 1][q] = make_float2(w.z, w.w);
+      }
+    }
+  } else if constexpr (SRC == kSrcC2R) {
+    // the whitener's inverse input from the half spectrum: z[m] = e + i W^m d,
+    // conjugated, e = X[m] + conj X[M-m], d = X[m] - conj X[M-m] (fft4_c2r_pre)
+    const float2* X = g.c2r + src * g.src_stride;
+    const uint32_t M = static_cast<uint32_t>(N1) * L;
+    const float invM = 1.0f / static_cast<float>(M);
+    // one row at a time: X[m0 .. m0+CPT) and X[M-m0-CPT+1 .. M-m0] as 16-byte
+    // loads (dword-aligned: the spectra are M + 1 bins apart)
+    static_assert(CPT % 2 == 0, "c2r: pairs of bins per load");
+    float2 a[1][CPT], b[1][CPT];
+    auto load_row = [&](int q, int) {
+      const uint32_t m0 = static_cast<uint32_t>(N1) * (t + q * T) + c0;
+      const f4u* pa = reinterpret_cast<const f4u*>(X + m0);
+      const f4u* pb = reinterpret_cast<const f4u*>(X + (M - m0 - (CPT - 1)));
+#pragma unroll
+      for (int u = 0; u < CPT / 2; ++u) {
+        const f4u wa = pa[u], wb = pb[u];
+        a[0][2 * u] = make_float2(wa.x, wa.y);
+        a[0][2 * u + 1] = make_float2(wa.z, wa.w);
+        // pb[u] holds X[M-m0-(CPT-1)+2u], X[M-m0-(CPT-2)+2u]: columns CPT-1-2u, CPT-2-2u
+        b[0][CPT - 1 - 2 * u] = make_float2(wb.x, wb.y);
+        b[0][CPT - 2 - 2 * u] = make_float2(wb.z, wb.w);
+      }
+    };
+#pragma unroll
+    for (int q = 0; q < kPts; ++q) {
+      load_row(q, 0);
+      const uint32_t m0 = static_cast<uint32_t>(N1) * (t + q * T) + c0;
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) {
+        const uint32_t m = m0 + c;
+        const float2 av = a[0][c], bv = b[0][c];
+        const float ex = av.x + bv.x, ey = av.y - bv.y;
+        const float dx = av.x - bv.x, dy = av.y + bv.y;
+        float sn, cs;
+        sincospif(static_cast<float>(m) * invM, &sn, &cs);
+        const float wx = cs * dx - sn * dy, wy = cs * dy + sn * dx;
+        v[c][q] = make_float2(ex - wy, -(ey + wx));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < kPts; ++q) {
+      const uint64_t j = t + q * T;
+      float x[2 * CPT];
+      load_resampled<2 * CPT>(in + src * g.in_tstride, in_pad + src * g.pad_tstride, static_cast<uint32_t>(n),
+                              log2row, static_cast<uint32_t>(g.inpitch), af, size,
+                              2u * (static_cast<uint32_t>(N1) * static_cast<uint32_t>(j) + static_cast<uint32_t>(c0)),
+                              x);
+#pragma unroll
+      for (int c = 0; c < CPT; ++c) v[c][q] = make_float2(x[2 * c], x[2 * c + 1]);
+    }
   }
   trace_event(1);
   fft_stages<L, CPT, C::CG, 1>(v, lds + grp * C::GROUP_FLOATS, t, tab + to.n2);
@@ -1230,19 +1427,43 @@ namespace {
 // bench within noise (profiles/r3_strip)
 int g_fft4_flags = kFft4Cpt8 | kFft4NoRemap | kFft4Blocked | kFft4TileY | kFft4TileX | kFft4PairXcd |
                    kFft4GroupXcd | kFft4UniformTw | kFft4OneX | kFft4StripInput | kFft4PairY | kFft4EarlyTw |
-                   kFft4WideY;
+                   kFft4WideY | kFft4WhitenStrips | kFft4WhitenU8;
 }  // namespace
+
+void fft4_pad_input_u8(const uint8_t* in, uint64_t nvalid, uint64_t n, const unsigned long long* sum, float* in_pad,
+                       const Fft4Geom& g, hipStream_t s, int count, uint64_t in_stride) {
+  PSOUP_CHECK(count >= 1 && count <= 65535, "fft4_pad_input_u8: bad count");
+  PSOUP_CHECK(strip_layout(g, g_fft4_flags) || fft4_direct_source(g), "fft4_pad_input_u8: strip layouts only");
+  PSOUP_CHECK(n == 2ull * g.n1 * g.n2 && nvalid <= n, "fft4_pad_input_u8: length");
+  const uint32_t rowlen = 2u * static_cast<uint32_t>(g.n1);
+  PSOUP_CHECK(rowlen % 16 == 0 && rowlen <= static_cast<uint32_t>(kStripLdsBytes) && strip_floats(g.n1, g.n2) <= g.insize &&
+                  g.insize % 4 == 0 && (reinterpret_cast<uintptr_t>(in_pad) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (count == 1 || in_stride % 16 == 0),
+              "fft4_pad_input_u8: strip layout size / alignment");
+  int log2_r = 0;  // rows per workgroup: the staged rows fill kStripLdsBytes, at most 16
+  while (log2_r < 4 && (rowlen << (log2_r + 1)) <= static_cast<uint32_t>(kStripLdsBytes) &&
+         (g.n2 >> (log2_r + 1)) >= 1)
+    ++log2_r;
+  PSOUP_CHECK(g.n2 % (1 << log2_r) == 0, "fft4_pad_input_u8: rows per workgroup");
+  const dim3 grid(static_cast<unsigned>(g.n2 >> log2_r), static_cast<unsigned>(count));
+  fft4_strips_u8_kernel<<<grid, 256, 0, s>>>(in, nvalid, n, sum, in_pad, rowlen, static_cast<uint32_t>(g.n2), log2_r,
+                                             in_stride, g.insize);
+  post_launch_check("fft4_strips_u8_kernel", s);
+}
 
 void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& g, hipStream_t s, int count,
                     uint64_t in_stride) {
   PSOUP_CHECK(count >= 1 && count <= 65535, "fft4_pad_input: bad count");
-  if (strip_input(g.n2, g_fft4_flags)) {
-    const uint64_t total = strip_floats(g.n1, g.n2);
-    PSOUP_CHECK(total < (1ull << 32) && total <= g.insize, "fft4_pad_input: strip layout size");
-    const dim3 grid(dev::grid_for(total, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
+  if (strip_layout(g, g_fft4_flags)) {
+    const uint64_t rows = strip_floats(g.n1, g.n2) / kStripW;
+    PSOUP_CHECK(rows < (1ull << 32) && rows * kStripW <= g.insize && g.insize % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(in_pad) & 15) == 0,
+                "fft4_pad_input: strip layout size / alignment");
+    const bool aligned = (reinterpret_cast<uintptr_t>(in) & 15) == 0 && (count == 1 || in_stride % 4 == 0);
+    const dim3 grid(dev::grid_for(rows, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
     fft4_pad_strips_kernel<<<grid, 256, 0, s>>>(in, n, in_pad, 2u * static_cast<uint32_t>(g.n1),
-                                                static_cast<uint32_t>(g.n2), static_cast<uint32_t>(total), in_stride,
-                                                g.insize);
+                                                __builtin_ctz(static_cast<unsigned>(g.n2)), static_cast<uint32_t>(rows),
+                                                in_stride, g.insize, aligned);
     post_launch_check("fft4_pad_strips_kernel", s);
     return;
   }
@@ -1266,14 +1487,14 @@ void fft4_pad_input(const float* in, uint64_t n, float* in_pad, const Fft4Geom& 
 
 namespace {
 
-template <int CPT, int SUB, int MODE>
+template <int CPT, int SUB, int MODE, int SRC = kSrcPad>
 void launch_colpass(const float* in, const float* in_pad, uint64_t n, const double* af, int K, float2* Y,
                     const Fft4Geom& g, const float2* tables, dim3 grid, int flags, hipStream_t s) {
   switch (g.n2) {
-#define PS_CASE(LL)                                                                                          \
-  case LL:                                                                                                   \
-    fft4_colpass_kernel<LL, CPT, SUB, MODE><<<grid, Cfg<LL, CPT, SUB>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, g, \
-                                                                                       tables, flags);       \
+#define PS_CASE(LL)                                                                                         \
+  case LL:                                                                                                  \
+    fft4_colpass_kernel<LL, CPT, SUB, MODE, SRC><<<grid, Cfg<LL, CPT, SUB>::THREADS, 0, s>>>(in, in_pad, n, af, K, Y, \
+                                                                                            g, tables, flags); \
     break;
     PS_CASE(128) PS_CASE(256) PS_CASE(512) PS_CASE(1024) PS_CASE(2048) PS_CASE(4096)
 #undef PS_CASE
@@ -1334,6 +1555,11 @@ void fft4_rowpass_spectrum(const float2* Y, int K, const Fft4Geom& g, const floa
 }
 
 bool fft4_pair_y(const Fft4Geom& g) { return g.ok && pair_y_layout(g.n2, g_fft4_flags); }
+bool fft4_direct_source(const Fft4Geom& g) {
+  const int f = g_fft4_flags;
+  return g.ok && g.zero_shift && !g.ypair && !onex_colpass(g.n2, f) && (f & kFft4Blocked) && (f & kFft4TileY);
+}
+bool fft4_strip_layout(const Fft4Geom& g) { return g.ok && strip_layout(g, g_fft4_flags); }
 
 void fft4_set_flags(int flags) {
   g_fft4_flags = flags;
@@ -1371,14 +1597,33 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   PSOUP_CHECK(!(f & kFft4GroupXcd) || (K & 7) != 0 || nblocks % 128 == 0, "fft4 colpass: group grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
   PSOUP_CHECK(!g.ypair || pair_y_layout(g.n2, f), "fft4 colpass: this pass A cannot write the row-pair Y layout");
-  if (onex_colpass(g.n2, f)) {
+  if (g.u8 || g.c2r || g.f32_direct || g.strips_direct) {
+    PSOUP_CHECK(fft4_direct_source(g) && (!!g.u8 + !!g.c2r + g.f32_direct + g.strips_direct) == 1,
+                "fft4 colpass: direct sources need a zero-shift Stockham pass A");
+    PSOUP_CHECK(!g.f32_direct || ((reinterpret_cast<uintptr_t>(in) & 15) == 0 && (K == 1 || g.in_tstride % 4 == 0)),
+                "fft4 colpass: f32 source alignment");
+    PSOUP_CHECK(!g.u8 || (g.u8sum && g.u8_nvalid <= n && (reinterpret_cast<uintptr_t>(g.u8) & 15) == 0 &&
+                          (K == 1 || g.src_stride % 16 == 0)),
+                "fft4 colpass: 8-bit source layout");
+    PSOUP_CHECK(!g.c2r || (K == 1 || g.src_stride >= n / 2 + 1), "fft4 colpass: spectrum source layout");
+  }
+  if (g.strips_direct)
+    launch_colpass<8, 1, kModeBlocked | kModeTileY, kSrcStrips>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  else if (g.f32_direct)
+    launch_colpass<8, 1, kModeBlocked | kModeTileY, kSrcF32>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  else if (g.u8)
+    launch_colpass<8, 1, kModeBlocked | kModeTileY, kSrcU8>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  else if (g.c2r)
+    launch_colpass<8, 1, kModeBlocked | kModeTileY, kSrcC2R>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  else if (onex_colpass(g.n2, f)) {
     constexpr int TH = OneX<2048, 64, 4>::THREADS;
-    if ((f & kFft4StripInput) && (f & kFft4EarlyTw) && (f & kFft4WideY) && g.ypair)
+    const bool strips = strip_layout(g, f);
+    if (strips && (f & kFft4EarlyTw) && (f & kFft4WideY) && g.ypair)
       fft4_colpass_onex_kernel<2048, 64, 4, true, true, true><<<grid, TH, 0, s>>>(in, in_pad, n, af, K, Y, g, tables,
                                                                                   f);
-    else if ((f & kFft4StripInput) && (f & kFft4EarlyTw))
+    else if (strips && (f & kFft4EarlyTw))
       fft4_colpass_onex_kernel<2048, 64, 4, true, true><<<grid, TH, 0, s>>>(in, in_pad, n, af, K, Y, g, tables, f);
-    else if (f & kFft4StripInput)
+    else if (strips)
       fft4_colpass_onex_kernel<2048, 64, 4, true, false><<<grid, TH, 0, s>>>(in, in_pad, n, af, K, Y, g, tables, f);
     else
       fft4_colpass_onex_kernel<2048, 64, 4, false, false><<<grid, TH, 0, s>>>(in, in_pad, n, af, K, Y, g, tables, f);

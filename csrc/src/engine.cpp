@@ -582,6 +582,7 @@ Whitener::Whitener(uint64_t n, float tsamp, hipStream_t stream, bool allow_fft4)
   const uint64_t nb = nbins();
   if (allow_fft4 && n % 2 == 0) {
     g4_ = kern::fft4_geometry(n / 2);
+    g4_.zero_shift = (kern::fft4_flags() & kern::kFft4WhitenStrips) != 0;  // plain FFTs: strip-layout pass A
     // single-transform grids of both passes need n1/8 % 16 == 0 and n2/8 % 8 == 0
     f4_ = g4_.ok && g4_.n1 >= 128 && g4_.n2 >= 64;
   }
@@ -604,6 +605,7 @@ Whitener::Whitener(uint64_t n, float tsamp, hipStream_t stream, bool allow_fft4)
     const uint64_t m = n / p;
     if (m >= 3 && m <= 255) {
       gm_ = kern::fft4_geometry(p);
+      gm_.zero_shift = (kern::fft4_flags() & kern::kFft4WhitenStrips) != 0;
       mixed_ = gm_.ok && gm_.n1 >= 128 && gm_.n2 >= 64;
     }
     if (mixed_) {
@@ -756,12 +758,33 @@ void Whitener::whiten_batch(const uint8_t* d_trials, uint64_t row_stride, uint64
   const uint64_t nvalid = std::min(nsamps, n_);
   const kern::XLayoutArgs L = kern::xlayout_args(g4_, kern::fft4_x_layout(g4_));
   kern::u8_sum(d_trials, nvalid, bsum_.data(), stream_, count, row_stride);
-  kern::u8_to_f32_pad(d_trials, nvalid, d_out, n_, bsum_.data(), stream_, count, row_stride, out_stride);
-  // forward: K = count transforms, trial b reading series b
+  // forward: K = count transforms, trial b reading series b, the 8-bit rows
+  // converted (mean-padded) straight into pass A's strip layout; d_out is
+  // first written by the inverse
   kern::Fft4Geom g = g4_;
   g.in_tstride = out_stride;
   g.pad_tstride = g4_.insize;
-  kern::fft4_pad_input(d_out, n_, in4_.data(), g4_, stream_, count, out_stride);
+  const bool direct = kern::fft4_direct_source(g4_);
+  const bool u8_aligned = (reinterpret_cast<uintptr_t>(d_trials) & 15) == 0 && (count == 1 || row_stride % 16 == 0);
+  if (direct && u8_aligned && (kern::fft4_flags() & kern::kFft4WhitenU8)) {
+    g.u8 = d_trials;  // pass A reads the 8-bit rows themselves
+    g.u8sum = bsum_.data();
+    g.u8_nvalid = nvalid;
+    g.src_stride = row_stride;
+  } else if (direct && u8_aligned && !(kern::fft4_flags() & kern::kFft4WhitenF32)) {
+    // 8-bit rows -> column strips, which pass A reads with contiguous wave loads
+    kern::fft4_pad_input_u8(d_trials, nvalid, n_, bsum_.data(), in4_.data(), g4_, stream_, count, row_stride);
+    g.strips_direct = true;
+  } else if (direct && out_stride % 4 == 0 && (reinterpret_cast<uintptr_t>(d_out) & 15) == 0) {
+    // pass A reads the f32 copy itself (no padded copy)
+    kern::u8_to_f32_pad(d_trials, nvalid, d_out, n_, bsum_.data(), stream_, count, row_stride, out_stride);
+    g.f32_direct = true;
+  } else if (kern::fft4_strip_layout(g4_) && u8_aligned) {
+    kern::fft4_pad_input_u8(d_trials, nvalid, n_, bsum_.data(), in4_.data(), g4_, stream_, count, row_stride);
+  } else {
+    kern::u8_to_f32_pad(d_trials, nvalid, d_out, n_, bsum_.data(), stream_, count, row_stride, out_stride);
+    kern::fft4_pad_input(d_out, n_, in4_.data(), g4_, stream_, count, out_stride);
+  }
   kern::fft4_resample_colpass(d_out, in4_.data(), n_, af0_.data(), count, y4_.data(), g, tab4_.data(), stream_);
   kern::fft4_rowpass(y4_.data(), x4_.data(), count, g4_, tab4_.data(), stream_);
   kern::fft4_r2c_half(x4_.data(), M, L, bspec_.data(), stream_, count, g4_.xstride, nb);
@@ -777,11 +800,18 @@ void Whitener::whiten_batch(const uint8_t* d_trials, uint64_t row_stride, uint64
                        std::max<uint64_t>(1, n125), pos5, pos25, d_zapmask, stream_, count, nb, ms);
     kern::interbin_stats(bspec_.data(), nb, nullptr, partials_.data(), 1024, d_stats, stream_, count, nb);
   }
-  // inverse
-  kern::fft4_c2r_pre(bspec_.data(), M, tmp4_.data(), stream_, count, nb, M);
+  // inverse (direct: pass A applies the C2R pre-processing to the spectra as it reads them)
   const float* t = reinterpret_cast<const float*>(tmp4_.data());
   g.in_tstride = n_;
-  kern::fft4_pad_input(t, n_, in4_.data(), g4_, stream_, count, n_);
+  g.u8 = nullptr;
+  g.f32_direct = g.strips_direct = false;
+  if (direct) {
+    g.c2r = bspec_.data();
+    g.src_stride = nb;
+  } else {
+    kern::fft4_c2r_pre(bspec_.data(), M, tmp4_.data(), stream_, count, nb, M);
+    kern::fft4_pad_input(t, n_, in4_.data(), g4_, stream_, count, n_);
+  }
   kern::fft4_resample_colpass(t, in4_.data(), n_, af0_.data(), count, y4_.data(), g, tab4_.data(), stream_);
   kern::fft4_rowpass(y4_.data(), x4_.data(), count, g4_, tab4_.data(), stream_);
   kern::fft4_c2r_post(x4_.data(), M, L, d_out, stream_, count, g4_.xstride, out_stride);

@@ -711,6 +711,49 @@ def test_batched_whitening_matches_single_trial(C):
         assert len(single) > 0
 
 
+@pytest.mark.parametrize("log2n", [18, 20, 23])
+def test_whitening_direct_sources_equal_padded_path(C, log2n):
+    """kFft4WhitenStrips, forward: the batched whitener's pass A reads the
+    8-bit rows staged into column strips (or the 8-bit rows themselves,
+    kFft4WhitenU8, or the unpadded f32 rows, kFft4WhitenF32); inverse: the
+    half spectra with the C2R pre-processing applied on the fly.  At column
+    length 2048 the one-exchange pass A reads the strips.  All give
+    bit-identical whitened series to the f32 copy + pad + c2r_pre kernels
+    (rows shorter than n: the mean-padded tail)."""
+    WS, U8, F32 = 16777216, 33554432, 67108864
+    rng = np.random.default_rng(log2n)
+    n, count = 1 << log2n, 3
+    nsamps = n - 1000
+    rs = n + 64
+    rows = torch.from_numpy(rng.integers(90, 170, (count, rs), dtype=np.uint8)).to(dev)
+    p = C.SearchParams()
+    p.fft_size, p.tsamp, p.nharmonics = n, 64e-6, 3
+    s = torch.cuda.current_stream().cuda_stream
+    f0 = C.kernels.fft4_flags()
+    assert f0 & WS
+    out = {}
+    try:
+        for f in (f0 & ~WS, f0 & ~(U8 | F32), (f0 & ~F32) | U8, (f0 & ~U8) | F32):
+            C.kernels.fft4_set_flags(f)
+            e = C.SearchEngine(p, s)
+            e.prepare(rows.data_ptr(), rs, nsamps, count)
+            ws = []
+            for b in range(count):
+                e.search_prepared(b, 5.0, b, [0.0])
+                w = torch.empty(n, dtype=torch.float32, device=dev)
+                e.copy_whitened(w.data_ptr())
+                ws.append(w)
+            torch.cuda.synchronize()
+            out[f] = ws
+            del e
+    finally:
+        C.kernels.fft4_set_flags(f0)
+    for b in range(count):
+        for f in (f0 & ~(U8 | F32), (f0 & ~F32) | U8, (f0 & ~U8) | F32):
+            assert torch.equal(out[f][b], out[f0 & ~WS][b]), (b, f)
+        assert out[f0 & ~WS][b].abs().max() > 0
+
+
 def test_flat_multi_dm_batches_match_per_dm_search(C):
     """search_prepared_many: the trials of several DMs concatenated and cut
     into K-trial batches across DM boundaries (per-trial series index and

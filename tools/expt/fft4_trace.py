@@ -42,7 +42,7 @@ def main():
     dev = torch.device("cuda")
     n = 1 << log2n
     M = n // 2
-    K = 32 if log2n <= 23 else 8
+    K = int(sys.argv[3]) if len(sys.argv) > 3 else (32 if log2n <= 23 else 8)
     s = torch.cuda.current_stream().cuda_stream
     g = K_.fft4_geometry(M)
     g.ypair = K_.fft4_pair_y(g)  # pass A hands the spectrum pass row-pair Y (the engine's fused path)
@@ -75,8 +75,15 @@ def main():
         fn()
         torch.cuda.synchronize()
         K_.fft4_set_trace(0)
-        onex = name == "colpass" and (K_.fft4_flags() & 131072) != 0
+        onex = name == "colpass" and (K_.fft4_flags() & 131072) != 0 and g.n2 == 2048
         report(name, tr.view(nblk, 12).cpu().numpy(), ONEX_NAMES if onex else NAMES)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"   {name}: {1e3 * e0.elapsed_time(e1) / 10 / K:.2f} us per trial (K = {K}, untraced)")
 
 
 if __name__ == "__main__":
