@@ -165,6 +165,8 @@ def config3_pipeline(a, as_rank=None):
            "timers_s": {k: round(v, 4) for k, v in res.timers.items()}, "candidates": len(res.candidates)}
     if as_rank is not None:
         rec.update({"as_rank": as_rank[1], "world": as_rank[0],
+                    "rank_stats": {k: (round(v, 4) if isinstance(v, float) else v) for k, v in st.items()
+                                   if isinstance(v, (int, float))},
                     "desc": f"rank {as_rank[1]} of a {as_rank[0]}-rank config-3 run (its acceleration slices)"})
     else:
         rec.update({"ranks": ctx.world_size, "desc": "1 DM, 2^23 samples, +-500 m/s^2, 8 harmonics, run_search",
