@@ -426,7 +426,7 @@ enum Fft4Flags : int {
                                  // input straight from the half spectra (C2R pre-processing fused) and
   kFft4WhitenU8 = 33554432,      // its forward input straight from the 8-bit rows,
   kFft4WhitenF32 = 67108864,     // or the unpadded f32 copy (neither: the 8-bit rows staged into strips).
-                                 // 2^20 bench A/B (gpurun_out whiten6d/e): strips / u8 / f32 all +1.5-2% over
+                                 // 2^20 bench A/B (profiles/r6_whiten): strips / u8 / f32 all +1.5-2% over
                                  // the f32 copy + pad path, within noise of each other; u8 moves the fewest bytes
   kFft4StripInput = 1073741824,  // one-exchange pass A: the padded input in column strips (16 + 4 floats of
                                  // every row per strip, strips row-contiguous), so a wave's 16 rows are

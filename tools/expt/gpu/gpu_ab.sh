@@ -1,5 +1,5 @@
 #!/bin/bash
-# A/B of bench.py over fft4 flag sets, interleaved repeats: tools/gpu_ab.sh REPS flagsA flagsB ...
+# A/B of bench.py over fft4 flag sets, interleaved repeats: tools/expt/gpu/gpu_ab.sh REPS flagsA flagsB ...
 set -o pipefail
 mkdir -p gpurun_out
 reps=$1; shift

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-6 A/B on one box: numerics tests of the fused FFT passes, per-kernel
 # times (kbench) and the trace of both flag sets, then the bench with each
-# flag set (ABAB).  tools/gpu_ab6.sh OUT OLD_FLAGS NEW_FLAGS [test files]
+# flag set (ABAB).  tools/expt/gpu/gpu_ab6.sh OUT OLD_FLAGS NEW_FLAGS [test files]
 set -o pipefail
 O=gpurun_out/${1:-ab6}; A=$2; B=$3; shift 3
 mkdir -p $O

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Same-box A/B of bench.py over option sets, interleaved repeats:
-#   tools/gpu_ab_args.sh REPS "--dedisp-kernel auto" "--dedisp-kernel mfma" ...
+#   tools/expt/gpu/gpu_ab_args.sh REPS "--dedisp-kernel auto" "--dedisp-kernel mfma" ...
 set -o pipefail
 mkdir -p gpurun_out
 reps=$1; shift

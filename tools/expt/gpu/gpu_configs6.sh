@@ -25,7 +25,7 @@ done
 step config 4 as ranks 0,3,7 of 8
 timeout -k 10 400 python3 tools/baseline_configs.py --configs 4 --as-rank 8:0,3,7 --workdir $W --out $O/c4_as8.jsonl > $O/c4_as8.log 2>&1 || { tail -20 $O/c4_as8.log; exit 1; }
 step golden command
-bash tools/gpu_golden.sh ${1:-configs6}/golden > $O/golden.log 2>&1 || { tail -20 $O/golden.log; exit 1; }
+bash tools/expt/gpu/gpu_golden.sh ${1:-configs6}/golden > $O/golden.log 2>&1 || { tail -20 $O/golden.log; exit 1; }
 for l in 20 21 22; do
   step bench 2^$l
   timeout -k 10 300 python3 bench.py --log2n $l --dms-per-gpu 32 --steps 10 --warmup 2 > $O/bench_$l.log 2>&1 || { tail -10 $O/bench_$l.log; exit 1; }

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Long series: kernel tables of one bench step at 2^25 and 2^26 (one DM per
-# step) and the config-3 rank rehearsal.  tools/gpu_long6.sh OUT
+# step) and the config-3 rank rehearsal.  tools/expt/gpu/gpu_long6.sh OUT
 set -o pipefail
 O=gpurun_out/${1:-long6}
 mkdir -p $O /tmp/cfgwork

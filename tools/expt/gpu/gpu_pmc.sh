@@ -1,6 +1,6 @@
 #!/bin/bash
 # PMC counters (separate passes, kernel-trace only) for the hot kernels.
-# usage: tools/gpu_pmc.sh [outdir-name] [extra bench args...]
+# usage: tools/expt/gpu/gpu_pmc.sh [outdir-name] [extra bench args...]
 set -o pipefail
 name=${1:-pmc}; shift || true
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null

@@ -6,4 +6,4 @@ timeout -k 10 300 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --t
 tail -1 gpurun_out/pytest_k.log
 timeout -k 10 300 python tools/kbench.py --K 32 --flags 0 > gpurun_out/kbench.log 2>&1 || { echo KBENCH_FAIL; tail -30 gpurun_out/kbench.log; exit 1; }
 grep -E "harmonic|tiled|torch" gpurun_out/kbench.log
-bash tools/gpu_pmc.sh pmc --sub-batch 0 --dms-per-gpu 2 && python3 tools/pmc_summary.py gpurun_out/pmc/*/p_counter_collection.csv --match fft4,r2c_inter,harmonic_peaks
+bash tools/expt/gpu/gpu_pmc.sh pmc --sub-batch 0 --dms-per-gpu 2 && python3 tools/pmc_summary.py gpurun_out/pmc/*/p_counter_collection.csv --match fft4,r2c_inter,harmonic_peaks

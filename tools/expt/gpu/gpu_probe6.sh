@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 probes: the config-3 rank rehearsal and the bench at long series.
-#   tools/gpu_probe6.sh OUT [bench log2n values...]
+#   tools/expt/gpu/gpu_probe6.sh OUT [bench log2n values...]
 set -o pipefail
 O=gpurun_out/${1:-probe6}; shift
 mkdir -p $O /tmp/cfgwork

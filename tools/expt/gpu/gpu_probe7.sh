@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-6 probes: 2^20 step kernel table, 2^25 fused-pass phase traces,
-# native vs Python config 4 (3 runs each).   tools/gpu_probe7.sh OUT
+# native vs Python config 4 (3 runs each).   tools/expt/gpu/gpu_probe7.sh OUT
 set -o pipefail
 O=gpurun_out/${1:-probe7}
 mkdir -p $O /tmp/cfgwork

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel-trace + stats of the headline bench (1 GPU).
-# usage: tools/gpu_prof.sh [outdir-name] [extra bench args...]
+# usage: tools/expt/gpu/gpu_prof.sh [outdir-name] [extra bench args...]
 set -o pipefail
 name=${1:-prof}; shift || true
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null

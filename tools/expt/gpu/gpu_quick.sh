@@ -1,7 +1,7 @@
 #!/bin/bash
 # Quick check after a kernel change: the given GPU test files (default: the
 # spectrum / screen / kernel numerics), kernel microbenchmarks, two noise and
-# one peak-heavy bench.  tools/gpu_quick.sh OUTNAME [test files...]
+# one peak-heavy bench.  tools/expt/gpu/gpu_quick.sh OUTNAME [test files...]
 set -o pipefail
 O=gpurun_out/${1:-quick}; shift
 mkdir -p $O

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Hashed peak-record regions: clustering / screen / distillation / pipeline
 # tests, config 3 as ranks 0/3/7 of 8 with default regions and one region,
-# config 4, and the headline bench.   tools/gpu_region6.sh OUT
+# config 4, and the headline bench.   tools/expt/gpu/gpu_region6.sh OUT
 set -o pipefail
 O=gpurun_out/${1:-region6}
 mkdir -p $O

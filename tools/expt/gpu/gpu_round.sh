@@ -8,4 +8,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -1 gpurun_out/smoke.log
 timeout -k 10 400 python bench.py "$@" > gpurun_out/bench.log 2>&1 || { echo BENCH_FAIL; tail -30 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
-bash tools/gpu_prof.sh prof "$@"
+bash tools/expt/gpu/gpu_prof.sh prof "$@"

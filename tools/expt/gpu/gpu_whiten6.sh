@@ -1,7 +1,7 @@
 #!/bin/bash
 # Whitening strip path: numerics tests, the isolated whitening cost, a
 # same-box A/B of the whitener's strip path (kFft4WhitenStrips) on the 2^20
-# bench, and a kernel profile of the new default.   tools/gpu_whiten6.sh OUT
+# bench, and a kernel profile of the new default.   tools/expt/gpu/gpu_whiten6.sh OUT
 set -o pipefail
 O=gpurun_out/${1:-whiten6}
 A=1084701955; B=1101479171; C=1168588035; D=1135033603

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Headline scaling curve on ONE node: bench.py at 1/2/4/8 ranks (one rank per
 # GPU under torch.distributed.run, RCCL over xGMI), one JSON line per N.
-#   tools/scale8.sh [steps] [warmup] [extra bench.py args...]
+#   tools/expt/gpu/scale8.sh [steps] [warmup] [extra bench.py args...]
 # Needs >= 8 visible MI355X for the N = 8 point (smaller N run regardless).
 set -o pipefail
 STEPS=${1:-10}; WARM=${2:-2}; shift 2 2>/dev/null
