@@ -360,6 +360,7 @@ class SearchEngine {
   int last_batch() const { return last_kc_; }  // batch size of the last search_prepared_many call
   int sub_batch() const { return sub_; }
   int fft_mode() const { return mode_; }
+  bool rows_ext() const { return rows_ext_; }  // fft_mode 2 with rocFFT rows (fft4_geometry_rows)
   hipStream_t stream() const { return stream_; }
   float tobs() const { return tobs_; }
   // Debug access to the whitened series / interbin stats of the last searched trial.
@@ -474,6 +475,8 @@ class SearchEngine {
   DeviceBuffer<double> af_;
   std::vector<double> af_host_;
   std::map<int, std::unique_ptr<FftPlan>> plans_;
+  bool rows_ext_ = false;                // f4_ from fft4_geometry_rows: rocFFT over the rows
+  std::unique_ptr<FftPlan> rows_plan_;  // (created on the first batch)
   Slot slots_[2];
   SearchCounters ctr_;
   HarmonicDistiller harm_;

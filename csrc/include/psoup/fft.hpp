@@ -18,9 +18,10 @@ enum class FftType { R2C, C2R, C2C_FWD, C2C_INV };
 
 class FftPlan {
  public:
-  // in_dist / out_dist: element distance between batch members (0 = packed).
+  // in_dist / out_dist: element distance between batch members (0 = packed);
+  // in_stride / out_stride: element distance within one transform.
   FftPlan(FftType type, uint64_t n, uint64_t batch = 1, uint64_t in_dist = 0, uint64_t out_dist = 0,
-          bool inplace = false);
+          bool inplace = false, uint64_t in_stride = 1, uint64_t out_stride = 1);
   ~FftPlan();
   FftPlan(const FftPlan&) = delete;
   FftPlan& operator=(const FftPlan&) = delete;

@@ -212,6 +212,14 @@ void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride,
                                   uint64_t blk_pitch, int log2_blk, float* P, uint64_t pstride, int K,
                                   uint64_t nbins_out, const float* stats, float nscale, hipStream_t s,
                                   const uint32_t* tsrc = nullptr);
+// The same from a row-major half spectrum Z[k2 * zp + k1] = FFT_M(z)[k2 + n2 k1]
+// (n2 = 2^log2_n2 rows of n1, e.g. rocFFT's row pass of the long-series
+// four-step FFT): LDS-tiled transpose, P in natural bin order; Q (optional):
+// the screening bytes dev::q8(P) of the same bins (natural, qstride per trial).
+void r2c_interbin_normalise_rows(const float2* Z, uint64_t zp, uint64_t zstride, int log2_n2, uint64_t n1, float* P,
+                                 uint64_t pstride, int K, uint64_t nbins_out, const float* stats, float nscale,
+                                 hipStream_t s, const uint32_t* tsrc = nullptr, uint8_t* Q = nullptr,
+                                 uint64_t qstride = 0);
 
 // Same output from the 8x8-tiled spectrum of fft4 pass B (kFft4TileX):
 // bin k = k2 + n2*k1 at X[k2/8][k1/8][k2%8][k1%8]; 64-byte loads per thread.
@@ -270,8 +278,16 @@ struct Fft4Geom {
   //   f32_direct: the unpadded series in + src * in_tstride itself (no pad copy);
   //   strips_direct: in_pad in column strips (fft4_pad_input_u8's layout)
   bool f32_direct = false, strips_direct = false;
+  // fft4_geometry_rows: rows longer than the fused passes take (n1 >= 8192)
+  // are transformed outside (rocFFT); pass A writes natural Y rows
+  // Y[k2 * ypitch + i] for it
+  bool rows_ext = false;
 };
 Fft4Geom fft4_geometry(uint64_t M);
+// Series of 2^26 points and more: columns of 4096 through the fused
+// resample + Stockham pass A, rows of n1 = M / 4096 for an external FFT
+// (ok = false below M = 2^25 or at M >= 2^31).
+Fft4Geom fft4_geometry_rows(uint64_t M);
 // Pass A of g can take the u8 / c2r direct sources (a zero-shift geometry
 // whose column pass is the Stockham kernel).
 bool fft4_direct_source(const Fft4Geom& g);

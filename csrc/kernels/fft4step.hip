@@ -1401,6 +1401,24 @@ Fft4Geom fft4_geometry(uint64_t M) {
   return g;
 }
 
+Fft4Geom fft4_geometry_rows(uint64_t M) {
+  Fft4Geom g;
+  constexpr int kCol = 4096;  // the longest column the Stockham pass A takes
+  if (M == 0 || (M & (M - 1)) != 0 || M < uint64_t(2) * kCol * kCol || M >= (uint64_t(1) << 31)) return g;
+  g.n2 = kCol;
+  g.n1 = static_cast<int>(M / kCol);
+  g.rows_ext = true;
+  g.ypitch = static_cast<uint64_t>(g.n1) + 8;  // natural Y rows: the row FFT's input, pitch off a power of two
+  g.ystride = g.ypitch * g.n2;
+  g.xpitch = static_cast<uint64_t>(g.n1) + 8;  // the row FFT's output rows (r2c_interbin_normalise_rows)
+  g.xstride = g.xpitch * g.n2;
+  g.log2_xrow = __builtin_ctz(static_cast<unsigned>(kCol));
+  g.inpitch = 2 * static_cast<uint64_t>(g.n1) + 32;
+  g.insize = g.inpitch * g.n2;
+  g.ok = true;
+  return g;
+}
+
 std::vector<float2> fft4_tables(const Fft4Geom& g) {
   const TableOffsets o = table_offsets(g.n1, g.n2);
   const double M = static_cast<double>(g.n1) * g.n2;
@@ -1521,7 +1539,7 @@ void launch_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const 
 
 void fft4_rowpass_spectrum(const float2* Y, int K, const Fft4Geom& g, const float2* tables, const SpecOut& o,
                            hipStream_t s) {
-  PSOUP_CHECK(g.ok && K >= 1 && g.n2 >= 16 && g.n1 >= 128, "fft4 spectrum pass: bad geometry");
+  PSOUP_CHECK(g.ok && K >= 1 && g.n2 >= 16 && g.n1 >= 128 && !g.rows_ext, "fft4 spectrum pass: bad geometry");
   const uint64_t M = static_cast<uint64_t>(g.n1) * g.n2;
   PSOUP_CHECK(M < (1ull << 31), "fft4 spectrum pass: spectrum too long for 32-bit bin indices");
   const int f = g_fft4_flags;
@@ -1597,6 +1615,8 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
   PSOUP_CHECK(!(f & kFft4GroupXcd) || (K & 7) != 0 || nblocks % 128 == 0, "fft4 colpass: group grid");
   const dim3 grid(static_cast<unsigned>(nblocks));
   PSOUP_CHECK(!g.ypair || pair_y_layout(g.n2, f), "fft4 colpass: this pass A cannot write the row-pair Y layout");
+  PSOUP_CHECK(!g.rows_ext || !(g.u8 || g.c2r || g.f32_direct || g.strips_direct || g.ypair || g.zero_shift),
+              "fft4 colpass: the external-row geometry takes the padded input and writes natural Y");
   if (g.u8 || g.c2r || g.f32_direct || g.strips_direct) {
     PSOUP_CHECK(fft4_direct_source(g) && (!!g.u8 + !!g.c2r + g.f32_direct + g.strips_direct) == 1,
                 "fft4 colpass: direct sources need a zero-shift Stockham pass A");
@@ -1607,7 +1627,9 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
                 "fft4 colpass: 8-bit source layout");
     PSOUP_CHECK(!g.c2r || (K == 1 || g.src_stride >= n / 2 + 1), "fft4 colpass: spectrum source layout");
   }
-  if (g.strips_direct)
+  if (g.rows_ext)  // natural Y rows for the external row FFT
+    launch_colpass<8, 1, 0>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
+  else if (g.strips_direct)
     launch_colpass<8, 1, kModeBlocked | kModeTileY, kSrcStrips>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
   else if (g.f32_direct)
     launch_colpass<8, 1, kModeBlocked | kModeTileY, kSrcF32>(in, in_pad, n, af, K, Y, g, tables, grid, f, s);
@@ -1643,7 +1665,7 @@ void fft4_resample_colpass(const float* in, const float* in_pad, uint64_t n, con
 
 void fft4_rowpass(const float2* Y, float2* X, int K, const Fft4Geom& g, const float2* tables, hipStream_t s,
                   uint64_t nbins_out) {
-  PSOUP_CHECK(g.ok && K >= 1, "fft4 rowpass: bad geometry");
+  PSOUP_CHECK(g.ok && K >= 1 && !g.rows_ext, "fft4 rowpass: bad geometry");
   PSOUP_CHECK((reinterpret_cast<uintptr_t>(X) & 63) == 0, "fft4 rowpass: X alignment");
   const int f = g_fft4_flags;
   const uint64_t nblocks = static_cast<uint64_t>(g.n2 / 8) * K;

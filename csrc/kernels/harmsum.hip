@@ -149,6 +149,155 @@ __global__ void __launch_bounds__(256) r2c_interbin_normalise_batch_kernel(
   }
 }
 
+// The same from a row-major half spectrum Zr[k2 * zp + k1] = Z[k2 + n2 k1]
+// (the rocFFT row pass of the long-series four-step FFT writes each row's
+// transform contiguously): a workgroup takes a tile of 32 k2 x 64 k1 with
+// k1 < n1/2, loads rows r0 - 1 .. r0 + 32 of it and the mirror rows (each
+// wave instruction one contiguous 512-byte row piece), forms X[k] and
+// X[M - k] of every loaded bin into LDS, and writes P[k] (32 consecutive k
+// per k1) and P[M - k] -- the transpose happens in LDS, every global access
+// is a whole row piece.  Bins k < M/2 and their mirrors (M/2, M]; bin M/2 by
+// block (0, 0).
+// (128 rows: one workgroup writes whole 128-byte Q lines and 512-byte P
+// runs; 32 rows x 64 columns wrote 32-byte Q pieces, +37 us per 2^26 trial)
+constexpr int kRowsTr = 128, kRowsTc = 16;
+constexpr int kRowsN = kRowsTr + 3;                        // loaded rows: k2 = r0 - 1 .. r0 + kRowsTr + 1
+constexpr int kRowsPer = 256 / kRowsTc;                    // rows per load pass
+constexpr int kRowsLd = (kRowsN + kRowsPer - 1) / kRowsPer;  // loaded rows per thread
+__global__ void __launch_bounds__(256) r2c_interbin_normalise_rows_kernel(
+    const float2* __restrict__ Z, uint64_t zp, uint64_t zstride, int log2_n2, uint64_t n1, float* __restrict__ P,
+    uint64_t pstride, uint64_t nbins_out, const float* __restrict__ stats, float nscale,
+    const uint32_t* __restrict__ tsrc, uint8_t* __restrict__ Q, uint64_t qstride) {
+  __shared__ float2 XA[kRowsN][kRowsTc + 1];  // X[kb(rr, cc)] (+1: conflict-free column reads)
+  __shared__ float2 XD[kRowsN][kRowsTc + 1];  // X[M - kb(rr, cc)]
+  const int kk = blockIdx.y;
+  const int t = threadIdx.x;
+  const uint64_t n2 = uint64_t(1) << log2_n2, M = n1 << log2_n2, half = M / 2;
+  const uint64_t ntr = n2 / kRowsTr;
+  const uint64_t r0 = (blockIdx.x % ntr) * kRowsTr, c0 = (blockIdx.x / ntr) * kRowsTc;
+  const float2* z = Z + static_cast<uint64_t>(kk) * zstride;
+  float* p = P + static_cast<uint64_t>(kk) * pstride;
+  uint8_t* q = Q ? Q + static_cast<uint64_t>(kk) * qstride : nullptr;
+  if (tsrc) stats += 4 * tsrc[kk];
+  const float mean = stats[0] * nscale;
+  const float sigma = stats[2] * nscale;
+  const float rsig = 1.0f / sigma;
+  const float invM = 1.0f / static_cast<float>(M);
+  // Forward bins k2 in [r0, r0 + 32), mirror bins M - k for k2 in (r0, r0 + 32]
+  // (so both come in aligned groups of four); workgroup-uniform skip
+  const bool fwd_any = r0 + n2 * c0 < nbins_out;
+  const bool mir_any = M - (r0 + kRowsTr) - n2 * (c0 + kRowsTc - 1) < nbins_out;
+  if (fwd_any || mir_any) {
+    // bin of row rr (0 .. 34), column cc: kb = r0 - 1 + rr + n2 (c0 + cc) (-1: X[-1] = 0).
+    // Every pair's two loads issued before any is used.
+    const int cc = t & (kRowsTc - 1);
+    float2 za[kRowsLd], zb[kRowsLd];
+#pragma unroll
+    for (int i = 0; i < kRowsLd; ++i) {
+      const int rr = t / kRowsTc + kRowsPer * i;
+      const int64_t kb = static_cast<int64_t>(r0) - 1 + rr + static_cast<int64_t>(n2 * (c0 + cc));
+      za[i] = zb[i] = make_float2(0.f, 0.f);
+      if (rr < kRowsN && kb >= 0) {
+        const uint64_t k = static_cast<uint64_t>(kb), mk = (M - k) & (M - 1);
+        za[i] = z[(k & (n2 - 1)) * zp + (k >> log2_n2)];
+        zb[i] = z[(mk & (n2 - 1)) * zp + (mk >> log2_n2)];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < kRowsLd; ++i) {
+      const int rr = t / kRowsTc + kRowsPer * i;
+      if (rr < kRowsN) {
+        const int64_t kb = static_cast<int64_t>(r0) - 1 + rr + static_cast<int64_t>(n2 * (c0 + cc));
+        float2 xa = make_float2(0.f, 0.f), xd = make_float2(0.f, 0.f);
+        if (kb >= 0) {
+          float sn, cs;
+          sincospif(-static_cast<float>(kb) * invM, &sn, &cs);
+          xa = r2c_combine(za[i], zb[i], cs, sn);
+          xd = r2c_combine(zb[i], za[i], -cs, sn);  // angle -pi (M-k)/M = -pi + pi k/M
+        }
+        XA[rr][cc] = xa;
+        XD[rr][cc] = xd;
+      }
+    }
+    __syncthreads();
+    // Thread (g = t % 32, column c = t / 32 (+ 8)): four consecutive bins per
+    // side as one 16-byte P store and one 4-byte Q store (32 lanes: 512
+    // contiguous bytes of P, one 128-byte Q line).  Forward: k2 = r0 + 4g ..
+    // +3 (rows 4g+1 .. 4g+4, neighbour the row above); mirror: j = M - k for
+    // k2 = r0 + 4g + 4 .. +1 (rows 4g+5 .. 4g+2, neighbour X[M - k - 1] the
+    // row below), ascending j.
+    const int g = t & (kRowsTr / 4 - 1);
+    auto q8x4 = [](const float (&v)[4]) {
+      return static_cast<uint32_t>(dev::q8(v[0])) | (static_cast<uint32_t>(dev::q8(v[1])) << 8) |
+             (static_cast<uint32_t>(dev::q8(v[2])) << 16) | (static_cast<uint32_t>(dev::q8(v[3])) << 24);
+    };
+#pragma unroll
+    for (int h = 0; h < kRowsTc / (256 / (kRowsTr / 4)); ++h) {
+      const int c = t / (kRowsTr / 4) + (256 / (kRowsTr / 4)) * h;
+      const uint64_t kc = n2 * (c0 + c);
+      const uint64_t k = r0 + 4 * g + kc;  // first forward bin (multiple of 4)
+      if (k < nbins_out) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          v[e] = dev::div_rn(dev::interbin(XA[4 * g + 1 + e][c], XA[4 * g + e][c]) - mean, sigma, rsig);
+        if (k + 4 <= nbins_out) {
+          *reinterpret_cast<float4*>(p + k) = make_float4(v[0], v[1], v[2], v[3]);
+          if (q) *reinterpret_cast<uint32_t*>(q + k) = q8x4(v);
+        } else {
+          for (int e = 0; e < 4 && k + e < nbins_out; ++e) {
+            p[k + e] = v[e];
+            if (q) q[k + e] = dev::q8(v[e]);
+          }
+        }
+      }
+      // first mirror bin (a multiple of 4, >= M/2: bin M/2 itself is written
+      // once, below, so a group starting there stores its other three alone)
+      const uint64_t j = M - (r0 + 4 * g + 4 + kc);
+      if (j < nbins_out && j + 3 > half) {
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)  // bin j + e = M - (k2 = r0 + 4g + 4 - e)
+          v[e] = dev::div_rn(dev::interbin(XD[4 * g + 5 - e][c], XD[4 * g + 6 - e][c]) - mean, sigma, rsig);
+        if (j > half && j + 4 <= nbins_out) {
+          *reinterpret_cast<float4*>(p + j) = make_float4(v[0], v[1], v[2], v[3]);
+          if (q) *reinterpret_cast<uint32_t*>(q + j) = q8x4(v);
+        } else {
+          for (int e = 0; e < 4 && j + e < nbins_out; ++e) {
+            if (j + e <= half) continue;
+            p[j + e] = v[e];
+            if (q) q[j + e] = dev::q8(v[e]);
+          }
+        }
+      }
+    }
+  }
+  if (blockIdx.x == 0 && t == 0) {
+    // bin M/2 (k2 = 0, k1 = n1/2: its own mirror) and bin M (the mirror of 0)
+    auto zat = [&](uint64_t k) { return z[(k & (n2 - 1)) * zp + (k >> log2_n2)]; };
+    auto xk = [&](uint64_t k) {
+      float sn, cs;
+      sincospif(-static_cast<float>(k) * invM, &sn, &cs);
+      return r2c_combine(zat(k), zat((M - k) & (M - 1)), cs, sn);
+    };
+    if (half < nbins_out) {
+      const float v = dev::div_rn(dev::interbin(xk(half), xk(half - 1)) - mean, sigma, rsig);
+      p[half] = v;
+      if (q) q[half] = dev::q8(v);
+    }
+    if (M < nbins_out) {
+      // X[M] = combine(Z[0], Z[0], -1, 0); its neighbour X[M - 1] = mirror of bin 1
+      const float2 z0 = zat(0), z1 = zat(1), zm1 = zat(M - 1);
+      float sn, cs;
+      sincospif(-invM, &sn, &cs);
+      const float v = dev::div_rn(dev::interbin(r2c_combine(z0, z0, -1.0f, 0.0f), r2c_combine(zm1, z1, -cs, sn)) - mean,
+                                  sigma, rsig);
+      p[M] = v;
+      if (q) q[M] = dev::q8(v);
+    }
+  }
+}
+
 // Tiled spectrum layout written by fft4 pass B (kFft4TileX):
 // bin k = k2 + n2*k1 at X_t[k2/8][k1/8][k2%8][k1%8]; a (k2-octet, k1-octet)
 // pair is one contiguous 512-byte chunk.
@@ -1372,6 +1521,26 @@ void r2c_interbin_normalise_batch(const float2* Z, uint64_t M, uint64_t zstride,
   r2c_interbin_normalise_batch_kernel<<<grid, 256, 0, s>>>(Z, M, zstride, log2_row, row_pitch, blk_pitch, log2_blk, P,
                                                            pstride, nbins_out, stats, nscale, tsrc);
   post_launch_check("r2c_interbin_normalise_batch_kernel", s);
+}
+
+void r2c_interbin_normalise_rows(const float2* Z, uint64_t zp, uint64_t zstride, int log2_n2, uint64_t n1, float* P,
+                                 uint64_t pstride, int K, uint64_t nbins_out, const float* stats, float nscale,
+                                 hipStream_t s, const uint32_t* tsrc, uint8_t* Q, uint64_t qstride) {
+  PSOUP_CHECK(K >= 1 && K <= 65535, "bad batch");
+  PSOUP_CHECK((uint64_t(1) << log2_n2) >= kRowsTr && n1 >= 2 * kRowsTc && (n1 & (n1 - 1)) == 0 && zp >= n1,
+              "r2c rows: layout");
+  PSOUP_CHECK(pstride % 4 == 0 && (reinterpret_cast<uintptr_t>(P) & 15) == 0 && (!Q || qstride % 4 == 0) &&
+                  (reinterpret_cast<uintptr_t>(Q) & 3) == 0,
+              "r2c rows: P / Q alignment");
+  const uint64_t M = n1 << log2_n2;
+  PSOUP_CHECK(M < (uint64_t(1) << 31) && nbins_out <= M + 1, "r2c rows: length");
+  if (nbins_out == 0) return;
+  const uint64_t tiles = ((uint64_t(1) << log2_n2) / kRowsTr) * (n1 / 2 / kRowsTc);
+  PSOUP_CHECK(tiles < (uint64_t(1) << 31), "r2c rows: grid");
+  const dim3 grid(static_cast<unsigned>(tiles), static_cast<unsigned>(K));
+  r2c_interbin_normalise_rows_kernel<<<grid, 256, 0, s>>>(Z, zp, zstride, log2_n2, n1, P, pstride, nbins_out, stats,
+                                                          nscale, tsrc, Q, qstride);
+  post_launch_check("r2c_interbin_normalise_rows_kernel", s);
 }
 
 const float2* r2c_twiddle_table(uint64_t M) {

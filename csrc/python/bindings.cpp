@@ -746,6 +746,16 @@ PYBIND11_MODULE(_C, m) {
     kern::r2c_interbin_normalise_batch(P<const float2>(Z), M, zstride, log2_row, row_pitch, blk_pitch, log2_blk,
                                        P<float>(Pout), pstride, K, nbo, P<const float>(stats), nscale, S(s));
   });
+  k.def(
+      "r2c_interbin_normalise_rows",
+      [](uintptr_t Z, uint64_t zp, uint64_t zstride, int log2_n2, uint64_t n1, uintptr_t Pout, uint64_t pstride, int K,
+         uint64_t nbo, uintptr_t stats, float nscale, uintptr_t s, uintptr_t q, uint64_t qstride) {
+        kern::r2c_interbin_normalise_rows(P<const float2>(Z), zp, zstride, log2_n2, n1, P<float>(Pout), pstride, K,
+                                          nbo, P<const float>(stats), nscale, S(s), nullptr, P<uint8_t>(q), qstride);
+      },
+      py::arg("Z"), py::arg("zp"), py::arg("zstride"), py::arg("log2_n2"), py::arg("n1"), py::arg("P"),
+      py::arg("pstride"), py::arg("K"), py::arg("nbo"), py::arg("stats"), py::arg("nscale"), py::arg("s"),
+      py::arg("q") = 0, py::arg("qstride") = 0);
   k.def("fft4_x_layout", [](const kern::Fft4Geom& g) {
     kern::Fft4XLayout l = kern::fft4_x_layout(g);
     return py::make_tuple(l.log2_row, l.row_pitch, l.blk_pitch, l.log2_blk, l.tiled);
@@ -774,9 +784,11 @@ PYBIND11_MODULE(_C, m) {
       .def_readonly("log2_xrow", &kern::Fft4Geom::log2_xrow)
       .def_readonly("inpitch", &kern::Fft4Geom::inpitch)
       .def_readonly("insize", &kern::Fft4Geom::insize)
-      .def_readwrite("ypair", &kern::Fft4Geom::ypair);
+      .def_readwrite("ypair", &kern::Fft4Geom::ypair)
+      .def_readonly("rows_ext", &kern::Fft4Geom::rows_ext);
   k.def("fft4_pair_y", &kern::fft4_pair_y);
   k.def("fft4_geometry", &kern::fft4_geometry);
+  k.def("fft4_geometry_rows", &kern::fft4_geometry_rows);
   k.def("fft4_set_flags", &kern::fft4_set_flags);
   k.def("peak_cluster_set_trace",
         [](uintptr_t p) { kern::peak_cluster_set_trace(reinterpret_cast<unsigned long long*>(p)); });
@@ -914,8 +926,9 @@ PYBIND11_MODULE(_C, m) {
       .value("C2C_FWD", FftType::C2C_FWD)
       .value("C2C_INV", FftType::C2C_INV);
   py::class_<FftPlan>(m, "FftPlan")
-      .def(py::init<FftType, uint64_t, uint64_t, uint64_t, uint64_t, bool>(), py::arg("type"), py::arg("n"),
-           py::arg("batch") = 1, py::arg("in_dist") = 0, py::arg("out_dist") = 0, py::arg("inplace") = false)
+      .def(py::init<FftType, uint64_t, uint64_t, uint64_t, uint64_t, bool, uint64_t, uint64_t>(), py::arg("type"),
+           py::arg("n"), py::arg("batch") = 1, py::arg("in_dist") = 0, py::arg("out_dist") = 0,
+           py::arg("inplace") = false, py::arg("in_stride") = 1, py::arg("out_stride") = 1)
       .def("execute", [](FftPlan& p, uintptr_t in, uintptr_t out, uintptr_t s) { p.execute(P<void>(in), P<void>(out), S(s)); })
       .def_property_readonly("work_bytes", &FftPlan::work_bytes);
 
@@ -1071,6 +1084,7 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("last_batch", &SearchEngine::last_batch)
       .def_property_readonly("sub_batch", &SearchEngine::sub_batch)
       .def_property_readonly("fft_mode", &SearchEngine::fft_mode)
+      .def_property_readonly("rows_ext", &SearchEngine::rows_ext)
       .def_property_readonly("stream", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.stream()); })
       .def_property_readonly("tobs", &SearchEngine::tobs)
       .def_property_readonly("whitened_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.whitened()); })

@@ -868,6 +868,14 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   wstats_.resize(4 * static_cast<uint64_t>(max_prep_));
   mode_ = (n_ % 2 == 0) ? std::min(std::max(p_.fft_mode, 0), 2) : 0;
   if (mode_ == 2) f4_ = kern::fft4_geometry(n_ / 2);
+  if (mode_ == 2 && !f4_.ok) {
+    // rows too long for the fused passes (2^26 and up): fused resample +
+    // pass A over columns of 4096, rocFFT over the rows, then a transposing
+    // r2c + interbin + normalise (PSOUP_ROWS_EXT=0: the plain rocFFT path)
+    const char* re = std::getenv("PSOUP_ROWS_EXT");
+    if (!(re && std::atoi(re) == 0)) f4_ = kern::fft4_geometry_rows(n_ / 2);
+    rows_ext_ = f4_.ok;
+  }
   if (mode_ == 2 && !f4_.ok) mode_ = 1;
   if (mode_ == 2) {
     auto tab = kern::fft4_tables(f4_);
@@ -903,13 +911,16 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   // harmonic sum reads its blocked layout at 2.1x the cost,
   // profiles/r3_fused/SUMMARY.md.)
   pst_ = std::max<uint64_t>(1, static_cast<uint64_t>(hi_));
-  q8_ = mode_ == 2 && kern::fft4_x_layout(f4_).tiled && !(kern::harmonic_flags() & 4);
+  // screened harmonic sum on the bytes the r2c kernel writes (the tiled fused
+  // layouts, or the transposing r2c of the external-row path)
+  q8_ = mode_ == 2 && (rows_ext_ || kern::fft4_x_layout(f4_).tiled) && !(kern::harmonic_flags() & 4);
   // the fused spectrum pass (harmonic flag 64) writes every bin 0..M of P (blocked) and Q
-  fused_ = q8_ && (kern::harmonic_flags() & 64) && f4_.n2 >= 16 && f4_.n1 >= 128;
-  fromx_ = q8_ && !fused_ && (kern::harmonic_flags() & 8);
+  fused_ = q8_ && !rows_ext_ && (kern::harmonic_flags() & 64) && f4_.n2 >= 16 && f4_.n1 >= 128;
+  fromx_ = q8_ && !fused_ && !rows_ext_ && (kern::harmonic_flags() & 8);
   if (fused_) pst_ = (n_ / 2 + 1 + 63) / 64 * 64;
+  if (rows_ext_) pst_ = (pst_ + 63) / 64 * 64;  // 16-byte P / 4-byte Q groups
   qst_ = q8_ ? (pst_ + (fused_ ? kern::kSpecQShift : 0) + 63) / 64 * 64 : 0;
-  if (mode_ == 2) rt_ = kern::r2c_twiddle_table(n_ / 2);
+  if (mode_ == 2 && !rows_ext_) rt_ = kern::r2c_twiddle_table(n_ / 2);
   // batch size
   {
     // auto budget: capped by the device's free memory shared among its engines
@@ -1059,8 +1070,8 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
   s.first = first;
   s.count = count;
   const uint64_t pst = pst_;
-  const kern::Fft4XLayout xl =
-      mode_ == 2 ? kern::fft4_x_layout(f4_) : kern::Fft4XLayout{ilog2(n_ / 2), n_ / 2, 8, 3, false};
+  const kern::Fft4XLayout xl = mode_ == 2 && !rows_ext_ ? kern::fft4_x_layout(f4_)
+                                                        : kern::Fft4XLayout{ilog2(n_ / 2), n_ / 2, 8, 3, false};
   // the record counter(s): region r's at rcount(s)[r * kPeakRegionStride]
   PSOUP_HIP_CHECK(hipMemsetAsync(rcount(s), 0, (rlog2_ ? kern::kPeakRegionStride << rlog2_ : 1) * sizeof(uint32_t),
                                  stream_));
@@ -1068,7 +1079,7 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
   auto run = [&](int b, int c, hipStream_t st) {
     float* P = fromx_ ? nullptr : P_.data() + static_cast<uint64_t>(b) * pst;
     // (the kernel flags can change after construction: Q only where the tiled r2c writes it)
-    uint8_t* Q = q8_ && mode_ == 2 && xl.tiled ? Q_.data() + static_cast<uint64_t>(b) * qst_ : nullptr;
+    uint8_t* Q = q8_ && mode_ == 2 && (xl.tiled || rows_ext_) ? Q_.data() + static_cast<uint64_t>(b) * qst_ : nullptr;
     PSOUP_CHECK(!fromx_ || Q, "fft4 kernel flags changed under an engine that recomputes spectra from X");
     kern::HarmFromX fx;
     if (mode_ == 2) {
@@ -1107,6 +1118,25 @@ void SearchEngine::launch_batch(Slot& s, int first, int count) {
         return;
       }
       float2* X = spec_.data() + static_cast<uint64_t>(b) * xs_;
+      if (rows_ext_) {
+        // the rows (n1 >= 8192 points, contiguous in Y) by rocFFT, each row's
+        // transform written contiguously (4.3 TB/s at 2^26; a natural-order
+        // output stride ran at 1.0: tools/expt/rows_probe.py), then the
+        // transposing r2c + interbin + normalise
+        if (!rows_plan_)
+          rows_plan_ = std::make_unique<FftPlan>(FftType::C2C_FWD, static_cast<uint64_t>(f4_.n1),
+                                                 static_cast<uint64_t>(f4_.n2), f4_.ypitch, f4_.xpitch);
+        for (int i = 0; i < c; ++i)
+          rows_plan_->execute(Y + static_cast<uint64_t>(i) * f4_.ystride, X + static_cast<uint64_t>(i) * xs_, st);
+        kern::r2c_interbin_normalise_rows(X, f4_.xpitch, xs_, ilog2(static_cast<uint64_t>(f4_.n2)),
+                                          static_cast<uint64_t>(f4_.n1), P, pst, c, static_cast<uint64_t>(hi_),
+                                          wstats_.data(), static_cast<float>(n_), st, src, Q, qst_);
+        RoctxRange r("Harmonic summing");
+        kern::HarmParams hp = hp_;
+        hp.trial_base = static_cast<uint32_t>(b);
+        kern::harmonic_peaks_batch(P, nb_, pst, c, hp, s.d_peaks.data(), rcount(s), st, Q, qst_, nullptr);
+        return;
+      }
       kern::fft4_rowpass(Y, X, c, f4_, f4_tab_.data(), st, static_cast<uint64_t>(hi_));
       if (xl.tiled) {
         kern::r2c_interbin_normalise_tiled(X, f4_.n1, f4_.n2, xs_, P, pst, c, static_cast<uint64_t>(hi_),

@@ -16,9 +16,10 @@ void fft_global_setup() {
   std::call_once(once, [] { PSOUP_ROCFFT_CHECK(rocfft_setup()); });
 }
 
-FftPlan::FftPlan(FftType type, uint64_t n, uint64_t batch, uint64_t in_dist, uint64_t out_dist, bool inplace)
+FftPlan::FftPlan(FftType type, uint64_t n, uint64_t batch, uint64_t in_dist, uint64_t out_dist, bool inplace,
+                 uint64_t in_stride, uint64_t out_stride)
     : type_(type), n_(n), batch_(batch), inplace_(inplace) {
-  PSOUP_CHECK(n >= 1 && batch >= 1, "bad FFT size");
+  PSOUP_CHECK(n >= 1 && batch >= 1 && in_stride >= 1 && out_stride >= 1, "bad FFT size");
   fft_global_setup();
   rocfft_transform_type tt;
   rocfft_array_type ain, aout;
@@ -58,10 +59,10 @@ FftPlan::FftPlan(FftType type, uint64_t n, uint64_t batch, uint64_t in_dist, uin
   }
   rocfft_plan_description desc = nullptr;
   PSOUP_ROCFFT_CHECK(rocfft_plan_description_create(&desc));
-  size_t stride1 = 1;
+  size_t istride = static_cast<size_t>(in_stride), ostride = static_cast<size_t>(out_stride);
   size_t lengths[1] = {static_cast<size_t>(n)};
-  rocfft_status st = rocfft_plan_description_set_data_layout(desc, ain, aout, nullptr, nullptr, 1, &stride1,
-                                                             static_cast<size_t>(in_dist), 1, &stride1,
+  rocfft_status st = rocfft_plan_description_set_data_layout(desc, ain, aout, nullptr, nullptr, 1, &istride,
+                                                             static_cast<size_t>(in_dist), 1, &ostride,
                                                              static_cast<size_t>(out_dist));
   if (st != rocfft_status_success) {
     rocfft_plan_description_destroy(desc);

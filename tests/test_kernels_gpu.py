@@ -355,6 +355,78 @@ def test_r2c_interbin_normalise_batch():
         assert np.allclose(P[k], exp, rtol=1e-4, atol=2e-3), np.abs(P[k] - exp).max()
 
 
+def test_r2c_interbin_normalise_rows_matches_numpy(C):
+    """The transposing post-processing of the long-series path: a row-major
+    half spectrum Z'[k2][k1] = Z[k2 + n2 k1] (row pitch n1 + 8) in, natural
+    P out, vs numpy rfft + interbin (every bin 0 .. M, bins M/2 and M
+    included)."""
+    rng = np.random.default_rng(11)
+    n2, n1 = 128, 256
+    M = n1 * n2
+    n = 2 * M
+    K = 2
+    x = rng.standard_normal((K, n)).astype(np.float32)
+    zp = n1 + 8
+    Zr = np.zeros((K, n2, zp), dtype=np.complex64)
+    for k in range(K):
+        z = np.fft.fft(x[k, 0::2].astype(np.float64) + 1j * x[k, 1::2].astype(np.float64))
+        Zr[k, :, :n1] = z.reshape(n1, n2).T.astype(np.complex64)  # Z'[k2][k1] = Z[k2 + n2 k1]
+    Zd = torch.from_numpy(Zr.view(np.float32).reshape(-1)).to(dev)
+    st = torch.tensor([1.5, 2.0, 0.75, 0.0], dtype=torch.float32, device=dev)
+    pst = M + 1 + 7
+    P = torch.zeros(K * pst, device=dev)
+    qst = (M + 1 + 63) // 64 * 64
+    Q = torch.zeros(K * qst, dtype=torch.uint8, device=dev)
+    s = torch.cuda.current_stream().cuda_stream
+    C.kernels.r2c_interbin_normalise_rows(Zd.data_ptr(), zp, n2 * zp, 7, n1, P.data_ptr(), pst, K, M + 1,
+                                          st.data_ptr(), 1.0, s, Q.data_ptr(), qst)
+    torch.cuda.synchronize()
+    Pn = P.cpu().numpy().reshape(K, pst)
+    Qn = Q.cpu().numpy().reshape(K, qst)[:, : M + 1]
+    q_exp = (np.clip(np.rint(Pn[:, : M + 1] * 4.0) + 127.0, -1, 254).astype(np.int64) & 0xFF).astype(np.uint8)
+    assert np.array_equal(Qn, q_exp)  # the screening bytes dev::q8 of every P
+    for k in range(K):
+        X = np.fft.rfft(x[k].astype(np.float64))
+        exp = (ref.interbin(X.astype(np.complex64)) - 1.5) / 0.75
+        assert np.allclose(Pn[k, : M + 1], exp, rtol=1e-4, atol=2e-3), np.abs(Pn[k, : M + 1] - exp).max()
+    g = C.kernels.fft4_geometry_rows(1 << 25)
+    assert g.ok and g.rows_ext and (g.n1, g.n2) == (8192, 4096)
+    assert not C.kernels.fft4_geometry_rows(1 << 24).ok
+
+
+def test_long_series_external_rows_match_rocfft_path(C):
+    """2^26 points (rows of 8192: beyond the fused passes): the fused resample
+    + pass A over columns of 4096, rocFFT over the rows and the transposing
+    r2c (fft4_geometry_rows) find the candidates of the plain rocFFT path
+    (fft_mode 1: resample kernel + N/2-point C2C), S/N within 1e-4."""
+    n = 1 << 26
+    g = torch.Generator(device=dev)
+    g.manual_seed(26)
+    t = torch.arange(n, device=dev, dtype=torch.float64) * 64e-6
+    pulse = ((t / 0.0173) % 1.0) < 0.03
+    x = 128 + 10 * torch.randn(n, device=dev, generator=g) + 6 * pulse.float()
+    row = torch.clamp(torch.round(x), 0, 255).to(torch.uint8)
+    del t, pulse, x
+    s = torch.cuda.current_stream().cuda_stream
+    accs = [-2.0, 0.0, 3.0]
+    out = {}
+    for mode in (2, 1):
+        p = C.SearchParams()
+        p.fft_size, p.tsamp, p.nharmonics, p.fft_mode = n, 64e-6, 3, mode
+        e = C.SearchEngine(p, s)
+        assert e.fft_mode == mode and e.rows_ext == (mode == 2)
+        cands = e.search_trial(row.data_ptr(), n, 10.0, 0, accs)
+        torch.cuda.synchronize()
+        out[mode] = sorted(cands, key=lambda c: -c.snr)
+        del e
+    a, b = out[2], out[1]
+    assert len(a) > 0 and abs(len(a) - len(b)) <= max(2, len(b) // 20), (len(a), len(b))
+    for ca, cb in zip(a[:10], b[:10]):
+        assert (round(ca.freq, 6), ca.nh, ca.acc) == (round(cb.freq, 6), cb.nh, cb.acc)
+        assert abs(ca.snr - cb.snr) <= 1e-4 * abs(cb.snr) + 1e-3, (ca.snr, cb.snr)
+    assert abs(1.0 / a[0].freq - 0.0173) < 1e-3 or any(abs(1.0 / c.freq - 0.0173) < 1e-4 for c in a[:5])
+
+
 # Every prefix of the kernel-shape chain (kernels.hpp Fft4Flags): None = the
 # default (1074216195 = 212227 | kFft4StripInput | kFft4PairY); 0 / 1 =
 # natural layouts (2 x 4 / 8 transforms per thread); 259 = blocked; 1299 = +
