@@ -319,6 +319,37 @@ __device__ __forceinline__ void store_row(float2* __restrict__ dst, const Vec<CP
   for (int c = 0; c < CPT; c += 2) d[c / 2] = f4v{v[c][q].x, v[c][q].y, v[c + 1][q].x, v[c + 1][q].y};
 }
 
+// 4 x 4 transpose of 16-byte pieces within each lane quad: afterwards lane
+// j holds at [r] what lane r of its quad held at [j].  Two exchange stages
+// (partners j ^ 1, then j ^ 2) with DPP quad permutes, no LDS.
+template <int CTRL>
+__device__ __forceinline__ f4v dpp4(const f4v& x) {
+  return f4v{__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x.x), CTRL, 0xF, 0xF, false)),
+             __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x.y), CTRL, 0xF, 0xF, false)),
+             __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x.z), CTRL, 0xF, 0xF, false)),
+             __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x.w), CTRL, 0xF, 0xF, false))};
+}
+__device__ __forceinline__ void quad_transpose(f4v (&a)[4], int j) {
+  // stage 1 (bit 0 of row and piece): keep a[i] where i & 1 == j & 1, else the partner's a[i ^ 1]
+  {
+    const f4v p0 = dpp4<0xB1>(a[1]), p1 = dpp4<0xB1>(a[0]), p2 = dpp4<0xB1>(a[3]), p3 = dpp4<0xB1>(a[2]);
+    const bool odd = j & 1;
+    a[0] = odd ? p0 : a[0];
+    a[1] = odd ? a[1] : p1;
+    a[2] = odd ? p2 : a[2];
+    a[3] = odd ? a[3] : p3;
+  }
+  // stage 2 (bit 1): keep a[i] where i & 2 == j & 2, else the partner's a[i ^ 2]
+  {
+    const f4v p0 = dpp4<0x4E>(a[2]), p1 = dpp4<0x4E>(a[3]), p2 = dpp4<0x4E>(a[0]), p3 = dpp4<0x4E>(a[1]);
+    const bool hi = j & 2;
+    a[0] = hi ? p0 : a[0];
+    a[1] = hi ? p1 : a[1];
+    a[2] = hi ? a[2] : p2;
+    a[3] = hi ? a[3] : p3;
+  }
+}
+
 // XCD-aware block order (remap = true): logical block
 // b' = (b % 8) * (nblocks / 8) + b / 8, so each XCD's share of the grid is one
 // contiguous logical range (nblocks is a multiple of 8).
@@ -706,6 +737,21 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, Cfg<L, CPT, SUB>::
       float2* dst = yk + static_cast<uint64_t>(c0) * g.n2 + (k2 >> 3) * 64 + (k2 & 7);
 #pragma unroll
       for (int c = 0; c < CPT; ++c) dst[c * 8] = v[c][q];
+    } else if constexpr (!kBlocked && CPT == 8) {
+      // natural Y[k2][i] (the external row FFT's input): the four lanes of a
+      // quad hold rows k2 .. k2+3 (8 columns each); a 4 x 4 transpose of
+      // their 16-byte pieces (two DPP xor exchanges) lets each store
+      // instruction write 64 contiguous bytes per row through four lanes,
+      // instead of 16 bytes in 64 different rows
+      const int j = static_cast<int>(threadIdx.x & 3u);
+      f4v a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] = f4v{v[2 * u][q].x, v[2 * u][q].y, v[2 * u + 1][q].x, v[2 * u + 1][q].y};
+      quad_transpose(a, j);
+      const uint64_t kb = static_cast<uint64_t>(k2 - j);  // the quad's first row
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        *reinterpret_cast<f4v*>(yk + (kb + r) * g.ypitch + c0 + 2 * j) = a[r];
     } else {
       // blocked: Y_b[c0/8][k2][c] (each lane 64 contiguous bytes); else Y[k2][i] at pitch ypitch
       float2* dst = kBlocked ? yk + static_cast<uint64_t>(c0) * g.n2 + k2 * CPT
