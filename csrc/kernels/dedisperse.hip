@@ -1155,11 +1155,21 @@ void dedisperse_2bit(const uint32_t* x2, uint64_t stride2, const int32_t* d_acti
   PSOUP_CHECK(dedisperse_2bit_fits(nactive, max_spread), "dedisperse_2bit: window or sums too large");
   PSOUP_CHECK((out_stride & 15) == 0 && d0 >= 0, "dedisperse_2bit: stride alignment");
   const uint64_t ty = (out_nsamps + k2bTs - 1) / k2bTs;
-  PSOUP_CHECK(ty <= 65535, "dedisperse_2bit: series too long for the grid");
   PSOUP_CHECK(16 * stride2 >= ty * k2bTs + static_cast<uint64_t>(max_offset) +
                                    16ull * static_cast<uint64_t>(dedisperse_2bit_window(max_spread)) &&
                   stride2 % 4 == 0,
               "dedisperse_2bit: packed rows too short for the windows");
+  if (ty > 65535) {
+    // longer than one grid (2^26 samples and up): consecutive time ranges of
+    // 65535 tiles, input and output shifted by the same number of samples
+    constexpr uint64_t kSpan = 65535ull * k2bTs;
+    static_assert(k2bTs % 64 == 0, "shifted packed rows stay 16-byte aligned");
+    for (uint64_t t0 = 0; t0 < out_nsamps; t0 += kSpan) {
+      dedisperse_2bit(x2 + t0 / 16, stride2, d_active, nactive, d_offT, ldo, d0, ndm, d_wmin, max_spread, max_offset,
+                      std::min(kSpan, out_nsamps - t0), out + t0, out_stride, scale, s);
+    }
+    return;
+  }
   // DMs per wave: 4 (16-DM workgroups); a launch of <= 8 DMs from an 8-DM
   // boundary (the headline bench's per-rank chunk) takes 8-DM workgroups
   // instead of computing 8 DMs it does not store

@@ -1684,7 +1684,9 @@ void harmonic_peaks_batch(const float* P, uint64_t nbins, uint64_t pstride, int 
   PSOUP_CHECK(hp.region_log2 >= 0 && hp.region_log2 <= 8 && hp.capacity % (1u << hp.region_log2) == 0,
               "harmonic_peaks_batch: record regions must divide the capacity");
   if (hi <= lo) return;
-  PSOUP_CHECK(static_cast<int64_t>(hi) * 32 < (int64_t(1) << 31), "spectrum too long for the int32 gather math");
+  // the gathers of level h read bin (i m + 2^(h-1)) >> h, m < 2^h: int32 up to
+  // hi 2^nlevels (2^27-point series: 2^26 bins x 8 at 3 levels)
+  PSOUP_CHECK(static_cast<int64_t>(hi) << hp.nlevels < (int64_t(1) << 31), "spectrum too long for the int32 gather math");
   const int xcd = (g_harm_flags & 1) && (K % 8 == 0) ? 1 : 0;
   // bits 8-15: dynamic LDS occupancy cap, measured for (and applied to) the
   // two-phase 3-level kernel only (the other kernels keep their full occupancy)
