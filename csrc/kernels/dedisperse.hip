@@ -1053,7 +1053,14 @@ void dedisperse_mfma_lds(const int8_t* chan_major, uint64_t chan_stride, const i
               "dedisperse_mfma_lds: bad tile range");
   PSOUP_CHECK((chan_stride & 15) == 0, "dedisperse_mfma_lds: stride alignment");
   const uint64_t ty = (out_nsamps + kMlTs - 1) / kMlTs;
-  PSOUP_CHECK(ty <= 65535, "dedisperse_mfma_lds: series too long for the grid");
+  if (ty > 65535) {  // beyond one grid: consecutive shifted time ranges (as dedisperse_2bit)
+    constexpr uint64_t kSpan = 65535ull * kMlTs;
+    for (uint64_t t0 = 0; t0 < out_nsamps; t0 += kSpan)
+      dedisperse_mfma_lds(chan_major + t0, chan_stride, d_active, nactive, d_steps, d_relo, d_ginfo, ngroups, d_wmin,
+                          ntiles, ndm, std::min(kSpan, out_nsamps - t0), out + t0, out_stride, scale, bias_total, s,
+                          d_skip);
+    return;
+  }
   dim3 grid(static_cast<unsigned>(ntiles), static_cast<unsigned>(ty));
   dedisperse_mfma_lds_kernel<kMfmaLdsGroup><<<grid, 256, 0, s>>>(
       chan_major, chan_stride, d_active, nactive, reinterpret_cast<const uint32_t*>(d_steps), d_relo,
@@ -1076,7 +1083,13 @@ void dedisperse_lds(const int8_t* chan_major, uint64_t chan_stride, const int32_
   PSOUP_CHECK(dedisperse_lds_fits(nbits, nactive, max_window), "dedisperse_lds: window or sums too large");
   PSOUP_CHECK((chan_stride & 15) == 0 && (out_stride & 15) == 0, "dedisperse_lds: stride alignment");
   const uint64_t ty = (out_nsamps + 1023) / 1024;
-  PSOUP_CHECK(ty <= 65535, "dedisperse_lds: series too long for the grid");
+  if (ty > 65535) {  // beyond one grid: consecutive shifted time ranges (as dedisperse_2bit)
+    constexpr uint64_t kSpan = 65535ull * 1024;
+    for (uint64_t t0 = 0; t0 < out_nsamps; t0 += kSpan)
+      dedisperse_lds(chan_major + t0, chan_stride, d_active, nactive, d_offT, ldo, d0, ndm, d_wmin, max_window,
+                     std::min(kSpan, out_nsamps - t0), out + t0, out_stride, scale, nbits, bias, s);
+    return;
+  }
   // DMs per wave: a launch of <= 8 DMs (the headline bench's per-rank chunk)
   // fills 8-DM workgroups instead of half-empty 16-DM ones; otherwise 4
   // (config-4 DM list: 141 ms vs 173 ms at 8).  Two-pass windows (> 4096

@@ -177,35 +177,40 @@ def test_dedisperse_packed2_high_dm_bit_exact(C):
             assert torch.equal(outs[k], outs[C.DedispKernel.Direct]), (d0, d1, k)
 
 
-def test_dedisperse_packed2_beyond_one_grid_bit_exact(C):
-    """A series longer than one launch of the 2-bit kernel (65535 time tiles
-    of 2048 samples: 2^27-sample observations) runs as consecutive shifted
-    ranges: equal to the direct kernel byte for byte, across the seam."""
+@pytest.mark.parametrize("nbits", [2, 8])
+def test_dedisperse_beyond_one_grid_bit_exact(C, nbits):
+    """A series longer than one launch (65535 time tiles: 2048 samples for the
+    2-bit kernel, 1024 for the byte-VALU and MFMA kernels -- 2^27-sample
+    observations) runs as consecutive shifted ranges: equal to the direct
+    kernel byte for byte, across the seam."""
     nchans, tsamp, fch1, foff = 16, 64e-6, 1550.0, -400.0 / 16
     dms = C.generate_dm_list(0.0, 60.0, tsamp, 64.0, fch1, foff, nchans, 1.1)[:8]
     delays = C.generate_delay_table(nchans, tsamp, fch1, foff)
-    nsamps = 65535 * 2048 + 70000 + C.compute_max_delay(dms, delays)
-    hdr = synthetic.make_header(nchans=nchans, nbits=2, tsamp=tsamp, fch1=fch1, foff=foff, nsamples=nsamps)
+    tile = 2048 if nbits == 2 else 1024
+    nsamps = 65535 * tile + 70000 + C.compute_max_delay(dms, delays)
+    hdr = synthetic.make_header(nchans=nchans, nbits=nbits, tsamp=tsamp, fch1=fch1, foff=foff, nsamples=nsamps)
     g = C.DedispGeometry.make(hdr, nsamps, dms, [1] * nchans)
     s = torch.cuda.current_stream().cuda_stream
     dfb = C.DeviceFilterbank(g, s)
     gen = torch.Generator(device=dev)
     gen.manual_seed(27)
-    packed = torch.randint(0, 256, (nsamps * nchans * 2 // 8,), dtype=torch.uint8, device=dev, generator=gen)
+    packed = torch.randint(0, 256, (nsamps * nchans * nbits // 8,), dtype=torch.uint8, device=dev, generator=gen)
     dfb.load_packed_device(packed.data_ptr())
     del packed
     dd = C.Dedisperser(dfb, s)
     stride = C.Dedisperser.row_stride(g.out_nsamps)
-    assert g.out_nsamps > 65535 * 2048
+    assert g.out_nsamps > 65535 * tile
+    kinds = (C.DedispKernel.Packed2,) if nbits == 2 else (C.DedispKernel.Valu, C.DedispKernel.Mfma)
     outs = {}
-    for k in (C.DedispKernel.Direct, C.DedispKernel.Packed2):
+    for k in (C.DedispKernel.Direct,) + kinds:
         o = torch.zeros(len(dms) * stride, dtype=torch.uint8, device=dev)
         dd.run(0, len(dms), o.data_ptr(), stride, k)
         outs[k] = o.view(len(dms), stride)[:, : g.out_nsamps]
     torch.cuda.synchronize()
-    seam = 65535 * 2048
+    seam = 65535 * tile
     assert outs[C.DedispKernel.Direct][:, seam - 4096: seam + 4096].any()
-    assert torch.equal(outs[C.DedispKernel.Packed2], outs[C.DedispKernel.Direct])
+    for k in kinds:
+        assert torch.equal(outs[k], outs[C.DedispKernel.Direct]), k
 
 
 def test_mfma_resident_plan_ranges_and_side_stream(C):

@@ -6,7 +6,7 @@ set -o pipefail
 O=gpurun_out/${1:-long8}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_kernels_gpu.py -k "beyond_one_grid or rows or packed2" > $O/t.log 2>&1 || { tail -40 $O/t.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread tests/test_kernels_gpu.py -k "beyond_one_grid or rows or packed2 or dedisp" > $O/t.log 2>&1 || { tail -40 $O/t.log; exit 1; }
 tail -1 $O/t.log
 timeout -k 10 500 python -u bench.py --log2n 26 --dms-per-gpu 1 --steps 2 --warmup 1 > $O/b26.log 2>&1 || { tail -20 $O/b26.log; exit 1; }
 grep '^{"metric"' $O/b26.log > $O/b26.json; grep -o '"value": [0-9.]*' $O/b26.json
