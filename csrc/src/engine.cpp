@@ -995,7 +995,9 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
   if (ht > 1) pool_ = std::make_unique<HostPool>(ht - 1);
   // acceleration distillation of each DM as its last batch retires, on two
   // workers of their own (none: synchronous, in the calling thread)
-  accq_ = std::make_unique<TaskQueue>(ht > 1 ? 2 : 0);
+  int aw = ht > 1 ? 2 : 0;
+  if (const char* e = std::getenv("PSOUP_ACCD_THREADS")) aw = std::max(0, std::atoi(e));
+  accq_ = std::make_unique<TaskQueue>(aw);
 }
 
 SearchEngine::~SearchEngine() {

@@ -7,9 +7,12 @@ import sys
 
 def get(d, path):
     for k in path.split("."):
-        if not isinstance(d, dict):
+        if isinstance(d, list) and k.isdigit() and int(k) < len(d):
+            d = d[int(k)]
+        elif isinstance(d, dict):
+            d = d.get(k)
+        else:
             return None
-        d = d.get(k)
     return d
 
 
