@@ -478,7 +478,11 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     }
     {
       std::lock_guard<std::mutex> lk(sh.mu);
-      for (auto& x : p.items) sh.cands.push_back(x);
+      // moved, not copied (the chunk's list is cleared after the hand-over):
+      // a copy duplicated every association tree under the lock
+      const size_t need = sh.cands.size() + p.items.size();
+      if (need > sh.cands.capacity()) sh.cands.reserve(std::max(need, 2 * sh.cands.capacity()));
+      for (auto& x : p.items) sh.cands.push_back(std::move(x));
     }
     const int done = sh.done_dms.fetch_add(p.d1 - p.d0) + (p.d1 - p.d0);
     if (sh.progress) sh.progress->set(static_cast<double>(done) / sh.ndm);
