@@ -138,3 +138,44 @@ def test_dada_header_and_channel_extraction(C, tmp_path):
     arr = dada.extract_channel(path, channel=2, size=100, offset=10, pol=1)
     assert arr.shape == (nant, 200)
     assert np.array_equal(arr[1].reshape(100, 2), payload[10:110, 1, 2, 1, :])
+
+
+def test_fft4_geometries_for_every_series_length(C):
+    """Host-side FFT plan choice (no device needed): the fused four-step
+    geometry up to 2^25 points (rows and columns of at most 4096), the
+    external-row geometry from 2^26 (columns of 4096 through the fused pass
+    A, rows of 8192 / 16384 for rocFFT, natural Y rows with an off-power-of-two
+    pitch), neither for lengths that are not powers of two."""
+    K = C.kernels
+    for log2n in range(15, 26):
+        g = K.fft4_geometry(1 << (log2n - 1))
+        assert g.ok and not g.rows_ext and g.n1 * g.n2 == 1 << (log2n - 1) and max(g.n1, g.n2) <= 4096
+        assert not K.fft4_geometry_rows(1 << (log2n - 1)).ok
+    for log2n, n1 in ((26, 8192), (27, 16384)):
+        M = 1 << (log2n - 1)
+        assert not K.fft4_geometry(M).ok
+        g = K.fft4_geometry_rows(M)
+        assert g.ok and g.rows_ext and (g.n1, g.n2) == (n1, 4096)
+        assert g.ypitch == n1 + 8 and g.ystride == g.ypitch * 4096 and g.insize >= 2 * M
+    assert not K.fft4_geometry(3 << 20).ok and not K.fft4_geometry_rows(3 << 24).ok
+
+
+def test_static_chunk_sizes():
+    """Long static shards take 64-DM blocks (fewer engine calls, each of which
+    waits for its last batch), short ones and the override keep the 32-DM tile."""
+    import os
+
+    from peasoup_amd.models.search import DYNAMIC_CHUNK, static_chunk
+
+    old = os.environ.pop("PSOUP_STATIC_CHUNK", None)
+    try:
+        assert static_chunk(2026) == 2 * DYNAMIC_CHUNK
+        assert static_chunk(8 * DYNAMIC_CHUNK - 1) == DYNAMIC_CHUNK
+        os.environ["PSOUP_STATIC_CHUNK"] = "100"
+        assert static_chunk(2026) == 96
+        os.environ["PSOUP_STATIC_CHUNK"] = "8"
+        assert static_chunk(2026) == DYNAMIC_CHUNK
+    finally:
+        os.environ.pop("PSOUP_STATIC_CHUNK", None)
+        if old is not None:
+            os.environ["PSOUP_STATIC_CHUNK"] = old
