@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <functional>
+#include <deque>
 #include <map>
 #include <memory>
 #include <string>
@@ -309,7 +310,7 @@ class SearchEngine {
   // Batched front end: whiten `count` (<= max_prepare()) trials at d_trials +
   // b*row_stride in one batch, then search each with search_prepared(b, ...).
   // search_trial = prepare(trial, 0, nsamps, 1) + search_prepared(0, ...).
-  void prepare(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count);
+  void prepare(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count, int first = 0);
   CandidateList search_prepared(int b, float dm, int dm_idx, const std::vector<float>& accs);
   // Several prepared DMs at once: their acceleration trials are concatenated
   // and cut into batches of K regardless of DM boundaries (a batch's trials
@@ -342,15 +343,33 @@ class SearchEngine {
     std::condition_variable cv;
     int remaining = 0;   // acceleration distillation tasks not yet finished
     std::exception_ptr err;
-    double accel_s = 0;  // host wall time of the call until it returned
+    double accel_s = 0;  // host wall time of the launch and the finish
+    // launch / finish state
+    std::vector<Job> jobs;
+    std::vector<int> job_end;  // flat index one past each job's last trial
+    int jobs_sent = 0, next = 0, kc = 0, ntr = 0;
+    std::deque<int> inflight;  // slots with a batch in flight
+    bool open = false;         // launched, not yet finished
+    Stopwatch sw;
+    double launch_s = 0;
   };
   std::shared_ptr<Pending> search_prepared_many_async(const std::vector<Job>& jobs);
+  // search_prepared_many_async in two halves: search_launch returns once the
+  // first (up to two) batches are issued; the caller may then issue other GPU
+  // work on the engine's stream (the next DM block's whitening, into the other
+  // half of the prepared slots: prepare(..., first)) before search_finish
+  // waits for the batches, issues the rest and processes every peak.  One
+  // launch at a time (search_finish before the next launch).
+  std::shared_ptr<Pending> search_launch(const std::vector<Job>& jobs);
+  void search_finish(const std::shared_ptr<Pending>& p);
   std::vector<CandidateList> collect(const std::shared_ptr<Pending>& p);
   int max_prepare() const { return max_prep_; }
   // Allocate up front what prepare(count) and search_prepared_many over
   // `trials` trials would grow on first use (a growth mid-search frees the
   // old buffer: hipFree waits for the whole device, every engine's stream)
-  void reserve(int count, int trials);
+  // two: room for a second half of prepared slots [max_prepare, 2 max_prepare)
+  // (prepare(..., first = max_prepare) while the first half is searched)
+  void reserve(int count, int trials, bool two = false);
   // the acceleration batch search_prepared_many uses for a flat list of ntr trials
   int batch_for(int ntr) const;
   const SearchParams& params() const { return p_; }
@@ -475,6 +494,10 @@ class SearchEngine {
   DeviceBuffer<double> af_;
   std::vector<double> af_host_;
   std::map<int, std::unique_ptr<FftPlan>> plans_;
+  bool open_ = false;   // a search_launch awaits its search_finish
+  int slot_next_ = 0;   // the batch slot the next launch issues into first
+  void issue_batch(Pending& pd, int slot);
+  void send_done(const std::shared_ptr<Pending>& pd, int processed);
   bool rows_ext_ = false;                // f4_ from fft4_geometry_rows: rocFFT over the rows
   std::unique_ptr<FftPlan> rows_plan_;  // (created on the first batch)
   Slot slots_[2];

@@ -1047,11 +1047,11 @@ PYBIND11_MODULE(_C, m) {
                               const std::vector<float>& accs) {
         return e.search_trial(P<const uint8_t>(trial), nsamps, dm, dm_idx, accs);
       }, py::call_guard<py::gil_scoped_release>())
-      .def("prepare", [](SearchEngine& e, uintptr_t trials, uint64_t row_stride, uint64_t nsamps, int count) {
-        e.prepare(P<const uint8_t>(trials), row_stride, nsamps, count);
-      }, py::arg("trials"), py::arg("row_stride"), py::arg("nsamps"), py::arg("count"),
-         py::call_guard<py::gil_scoped_release>())
-      .def("reserve", &SearchEngine::reserve, py::arg("count"), py::arg("trials"),
+      .def("prepare", [](SearchEngine& e, uintptr_t trials, uint64_t row_stride, uint64_t nsamps, int count,
+                         int first) { e.prepare(P<const uint8_t>(trials), row_stride, nsamps, count, first); },
+           py::arg("trials"), py::arg("row_stride"), py::arg("nsamps"), py::arg("count"), py::arg("first") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("reserve", &SearchEngine::reserve, py::arg("count"), py::arg("trials"), py::arg("two") = false,
            py::call_guard<py::gil_scoped_release>())
       .def("batch_for", &SearchEngine::batch_for, py::arg("ntr"))
       .def("search_prepared", [](SearchEngine& e, int b, float dm, int dm_idx, const std::vector<float>& accs) {
@@ -1083,6 +1083,19 @@ PYBIND11_MODULE(_C, m) {
       }, py::arg("jobs"), py::call_guard<py::gil_scoped_release>(),
          "as search_prepared_many, returning once the batches have retired; collect(handle) waits for the "
          "per-DM acceleration distillation still running on the engine's workers")
+      .def("search_launch",
+           [](SearchEngine& e, const std::vector<std::tuple<int, float, int, std::vector<float>, bool>>& jobs) {
+             std::vector<SearchEngine::Job> js;
+             js.reserve(jobs.size());
+             for (const auto& j : jobs)
+               js.push_back(SearchEngine::Job{std::get<0>(j), std::get<1>(j), std::get<2>(j), std::get<3>(j),
+                                              std::get<4>(j)});
+             return e.search_launch(js);
+           }, py::arg("jobs"), py::call_guard<py::gil_scoped_release>(),
+           "search_prepared_many_async's first half: issues the first batches and returns (search_finish next)")
+      .def("search_finish", &SearchEngine::search_finish, py::arg("handle"),
+           py::call_guard<py::gil_scoped_release>(),
+           "waits for a launched search's batches, issues the rest, processes the peaks (then collect)")
       .def("collect", &SearchEngine::collect, py::arg("handle"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("max_prepare", &SearchEngine::max_prepare)
       .def_property_readonly("batch_size", &SearchEngine::batch_size)

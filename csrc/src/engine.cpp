@@ -865,7 +865,7 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     max_prep_ = per ? static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(64, (3ull << 30) / per))) : 1;
   }
   tim_.resize(n_);
-  wstats_.resize(4 * static_cast<uint64_t>(max_prep_));
+  wstats_.resize(8 * static_cast<uint64_t>(max_prep_));  // two halves of prepared slots
   mode_ = (n_ % 2 == 0) ? std::min(std::max(p_.fft_mode, 0), 2) : 0;
   if (mode_ == 2) f4_ = kern::fft4_geometry(n_ / 2);
   if (mode_ == 2 && !f4_.ok) {
@@ -1396,19 +1396,28 @@ void SearchEngine::build_trials(int first, int count, size_t work,
   ctr_.host_distilled += static_cast<uint64_t>(count) - on_gpu.load();
 }
 
-void SearchEngine::prepare(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count) {
+void SearchEngine::prepare(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count, int first) {
   PSOUP_CHECK(count >= 1 && count <= max_prep_, "prepare: count " << count << " outside [1, " << max_prep_ << "]");
+  PSOUP_CHECK(first == 0 || first == max_prep_, "prepare: first slot " << first << " (0 or max_prepare)");
   RoctxRange r("Whitening");
-  // the previous batch's searches have retired (search_prepared waits on every
-  // acceleration batch), so the buffers may be rewritten
-  tim_.resize(n_ * static_cast<uint64_t>(count));
-  wh_->whiten_batch(d_trials, row_stride, nsamps, count, tim_.data(), n_, zap_ ? zapmask_.data() : nullptr,
-                    wstats_.data(), p_.boundary_5_freq, p_.boundary_25_freq);
-  if (mode_ == 2) {
-    f4_in_.resize(f4_.insize * static_cast<uint64_t>(count));
-    kern::fft4_pad_input(tim_.data(), n_, f4_in_.data(), f4_, stream_, count, n_);
+  // first == 0: the previous searches have retired (search_prepared waits on
+  // every acceleration batch), so the buffers may be rewritten (and grown);
+  // first == max_prepare: the other half of a reserve(.., two = true) layout,
+  // written while the first half's search may still be in flight (the
+  // kernels run after it in stream order; nothing is reallocated)
+  const uint64_t end = static_cast<uint64_t>(first) + static_cast<uint64_t>(count);
+  if (first == 0) {  // grow only: a reserve(.., two = true) keeps its second half
+    if (tim_.size() < n_ * end) tim_.resize(n_ * end);
+    if (mode_ == 2 && f4_in_.size() < f4_.insize * end) f4_in_.resize(f4_.insize * end);
   }
-  prepared_ = count;
+  PSOUP_CHECK(tim_.size() >= n_ * end && (mode_ != 2 || f4_in_.size() >= f4_.insize * end),
+              "prepare: the second half of the prepared slots needs reserve(count, trials, true)");
+  float* tim = tim_.data() + static_cast<uint64_t>(first) * n_;
+  wh_->whiten_batch(d_trials, row_stride, nsamps, count, tim, n_, zap_ ? zapmask_.data() : nullptr,
+                    wstats_.data() + 4 * static_cast<uint64_t>(first), p_.boundary_5_freq, p_.boundary_25_freq);
+  if (mode_ == 2)
+    kern::fft4_pad_input(tim, n_, f4_in_.data() + static_cast<uint64_t>(first) * f4_.insize, f4_, stream_, count, n_);
+  prepared_ = static_cast<int>(end);
 }
 
 CandidateList SearchEngine::search_trial(const uint8_t* d_trial, uint64_t nsamps, float dm, int dm_idx,
@@ -1437,11 +1446,12 @@ int SearchEngine::batch_for(int ntr) const {
   return K_;
 }
 
-void SearchEngine::reserve(int count, int trials) {
+void SearchEngine::reserve(int count, int trials, bool two) {
   count = std::max(1, std::min(count, max_prep_));
-  tim_.resize(n_ * static_cast<uint64_t>(count));
+  const uint64_t slots = two ? 2 * static_cast<uint64_t>(max_prep_) : static_cast<uint64_t>(count);
+  if (tim_.size() < n_ * slots) tim_.resize(n_ * slots);  // grow only
   wh_->reserve_batch(count);
-  if (mode_ == 2) f4_in_.resize(f4_.insize * static_cast<uint64_t>(count));
+  if (mode_ == 2 && f4_in_.size() < f4_.insize * slots) f4_in_.resize(f4_.insize * slots);
   if (trials > 0) ensure_batch_buffers(std::min(batch_for(trials), trials));
 }
 
@@ -1463,11 +1473,49 @@ std::vector<CandidateList> SearchEngine::collect(const std::shared_ptr<Pending>&
 }
 
 std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(const std::vector<Job>& jobs) {
+  auto pd = search_launch(jobs);
+  search_finish(pd);
+  return pd;
+}
+
+void SearchEngine::send_done(const std::shared_ptr<Pending>& pd, int processed) {
+  const int njobs = static_cast<int>(pd->jobs.size());
+  while (pd->jobs_sent < njobs && pd->job_end[static_cast<size_t>(pd->jobs_sent)] <= processed) {
+    const int j = pd->jobs_sent++;
+    if (pd->jobs[static_cast<size_t>(j)].raw) {  // a slice: distilled once the slices are joined
+      pd->out[static_cast<size_t>(j)] = std::move(pd->by_job[static_cast<size_t>(j)]);
+      continue;
+    }
+    {
+      std::lock_guard<std::mutex> lk(pd->mu);
+      pd->remaining++;
+    }
+    accq_->submit([this, j, pd] {
+      Stopwatch w;
+      w.start();
+      std::exception_ptr err;
+      try {
+        pd->out[static_cast<size_t>(j)] = accd_.distill(std::move(pd->by_job[static_cast<size_t>(j)]));
+      } catch (...) {
+        err = std::current_exception();
+      }
+      w.stop();
+      std::lock_guard<std::mutex> lk(pd->mu);
+      pd->accd_t[static_cast<size_t>(j)] = w.get_time();
+      if (err && !pd->err) pd->err = err;
+      if (--pd->remaining == 0) pd->cv.notify_all();
+    });
+  }
+}
+
+std::shared_ptr<SearchEngine::Pending> SearchEngine::search_launch(const std::vector<Job>& jobs_in) {
+  PSOUP_CHECK(!open_, "search_launch: the previous launch has not been finished (search_finish)");
   RoctxRange dm_range("DM-Loop");
-  Stopwatch sw;
-  sw.start();
-  const int njobs = static_cast<int>(jobs.size());
   auto pd = std::make_shared<Pending>();
+  pd->sw.start();
+  pd->jobs = jobs_in;  // owned: the batches are processed after this call returns
+  const std::vector<Job>& jobs = pd->jobs;
+  const int njobs = static_cast<int>(jobs.size());
   pd->out.resize(static_cast<size_t>(njobs));
   pd->by_job.resize(static_cast<size_t>(njobs));
   pd->accd_t.assign(static_cast<size_t>(njobs), 0.0);
@@ -1503,7 +1551,7 @@ std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(
   cur_stats_ = wstats_.data() + 4 * static_cast<uint64_t>(j0.b);
   const int ntr = static_cast<int>(flat_acc_.size());
   if (ntr == 0) return pd;
-  jobs_ = &jobs;
+  jobs_ = &pd->jobs;
   // previous batches have all retired (their events were waited on), so the
   // device copies of the trial tables may be rewritten
   af_.resize(af_host_.size());
@@ -1518,40 +1566,13 @@ std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(
   // while the GPU runs the next batches; the tasks own their data through
   // the Pending record, so the last DMs' distillation may outlive this call
   // (collect() waits for it).
-  std::vector<int> job_end(static_cast<size_t>(njobs));
-  for (int j = 0, e = 0; j < njobs; ++j) job_end[static_cast<size_t>(j)] = e += static_cast<int>(jobs[static_cast<size_t>(j)].accs.size());
-  int jobs_sent = 0;
-  auto send_done = [&](int processed) {
-    while (jobs_sent < njobs && job_end[static_cast<size_t>(jobs_sent)] <= processed) {
-      const int j = jobs_sent++;
-      if (jobs[static_cast<size_t>(j)].raw) {  // a slice: distilled once the slices are joined
-        pd->out[static_cast<size_t>(j)] = std::move(pd->by_job[static_cast<size_t>(j)]);
-        continue;
-      }
-      {
-        std::lock_guard<std::mutex> lk(pd->mu);
-        pd->remaining++;
-      }
-      accq_->submit([this, j, pd] {
-        Stopwatch w;
-        w.start();
-        std::exception_ptr err;
-        try {
-          pd->out[static_cast<size_t>(j)] = accd_.distill(std::move(pd->by_job[static_cast<size_t>(j)]));
-        } catch (...) {
-          err = std::current_exception();
-        }
-        w.stop();
-        std::lock_guard<std::mutex> lk(pd->mu);
-        pd->accd_t[static_cast<size_t>(j)] = w.get_time();
-        if (err && !pd->err) pd->err = err;
-        if (--pd->remaining == 0) pd->cv.notify_all();
-      });
-    }
-  };
-  send_done(0);
-  std::deque<int> inflight;  // slot indices
-  int next = 0, slot = 0;
+  pd->job_end.resize(static_cast<size_t>(njobs));
+  for (int j = 0, e = 0; j < njobs; ++j)
+    pd->job_end[static_cast<size_t>(j)] = e += static_cast<int>(jobs[static_cast<size_t>(j)].accs.size());
+  send_done(pd, 0);
+  std::deque<int>& inflight = pd->inflight;  // slot indices
+  int& next = pd->next;
+  int slot = slot_next_;
   // Short trial lists (one DM at 2^23: 685 trials) keep at least min_batches
   // (SearchParams::min_batches, default 4) batches in the two-slot pipeline so
   // host clustering still overlaps the GPU, but never fall below k_small_
@@ -1559,17 +1580,41 @@ std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(
   // 128 GiB, rounded like K_).
   const int kc = batch_for(ntr);
   last_kc_ = kc;
+  pd->kc = kc;
+  pd->ntr = ntr;
   ensure_batch_buffers(std::min(kc, ntr));
-  auto issue = [&](int sl) {
-    const int c = std::min(kc, ntr - next);
-    launch_batch(slots_[sl], next, c);
-    inflight.push_back(sl);
-    next += c;
-  };
   while (inflight.size() < 2 && next < ntr) {
-    issue(slot);
+    issue_batch(*pd, slot);
     slot ^= 1;
   }
+  slot_next_ = slot;
+  pd->open = true;
+  open_ = true;
+  pd->launch_s = pd->sw.get_time();
+  return pd;
+}
+
+void SearchEngine::issue_batch(Pending& pd, int sl) {
+  const int c = std::min(pd.kc, pd.ntr - pd.next);
+  launch_batch(slots_[sl], pd.next, c);
+  pd.inflight.push_back(sl);
+  pd.next += c;
+}
+
+void SearchEngine::search_finish(const std::shared_ptr<Pending>& pd) {
+  if (!pd->open) {  // nothing deferred (an empty list, or the rocFFT paths' job-by-job search)
+    pd->accel_s = pd->sw.get_time();
+    return;
+  }
+  pd->open = false;
+  open_ = false;
+  Stopwatch fsw;
+  fsw.start();
+  RoctxRange acc_range("Acceleration-Loop");
+  std::vector<CandidateList>& by_job = pd->by_job;
+  std::deque<int>& inflight = pd->inflight;
+  const int ntr = pd->ntr;
+  jobs_ = &pd->jobs;
   Stopwatch host;
   while (!inflight.empty()) {
     const int sl = inflight.front();
@@ -1674,7 +1719,7 @@ std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(
     s.copied->record(copy_stream_.get());
     // the next batch that reuses this slot must wait for the copy-out
     PSOUP_HIP_CHECK(hipStreamWaitEvent(stream_, s.copied->get(), 0));
-    if (next < ntr) issue(sl);
+    if (pd->next < ntr) issue_batch(*pd, sl);
     s.copied->sync();
     host.start();
     if (gpu_cluster_) {
@@ -1685,14 +1730,13 @@ std::shared_ptr<SearchEngine::Pending> SearchEngine::search_prepared_many_async(
     }
     host.stop();
     ctr_.accel_trials += static_cast<uint64_t>(b_count);
-    send_done(b_first + b_count);
+    send_done(pd, b_first + b_count);
   }
   ctr_.host_s += host.get_time();
-  send_done(ntr);
+  send_done(pd, ntr);
   jobs_ = nullptr;
-  sw.stop();
-  pd->accel_s = sw.get_time();
-  return pd;
+  fsw.stop();
+  pd->accel_s = pd->launch_s + fsw.get_time();
 }
 
 // ---------------------------------------------------------------- folding ---

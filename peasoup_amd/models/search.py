@@ -318,14 +318,23 @@ class RankSearcher:
 
         dd_events = []
         lock = threading.Lock()
-        if self.engines and width > getattr(self, "_reserved_width", 0):
+        # Block pipeline (one engine, blocks of at most max_prepare DMs): block
+        # k's searches are launched, block k+1 is whitened into the other half
+        # of the prepared slots behind them on the engine's stream, and only
+        # then does the host wait for block k's batches and process their
+        # peaks -- the GPU runs k+1's whitening through that host time
+        pipelined = (len(self.engines) == 1 and 0 < width <= self.engine.max_prepare
+                     and os.environ.get("PSOUP_BLOCK_PIPELINE", "1") != "0")
+        if self.engines and (width > getattr(self, "_reserved_width", 0)
+                             or (pipelined and not getattr(self, "_reserved_two", False))):
             # whitening / batch buffers sized before the timer (growing one
             # mid-search frees the old buffer, which waits for the whole device)
             ne = len(self.engines)
             per_e = max(1, min(self.engine.max_prepare, -(-width // ne)))
             for e in self.engines:
-                e.reserve(per_e, per_e * self.max_trials)
+                e.reserve(per_e, per_e * self.max_trials, pipelined)
             self._reserved_width = width
+            self._reserved_two = getattr(self, "_reserved_two", False) or pipelined
         cur = pull()  # the first block's dedispersion is issued before the search timer starts
         if t_s:
             t_s.start()
@@ -356,6 +365,92 @@ class RankSearcher:
                 accs = accs[s_ * len(accs) // S_:(s_ + 1) * len(accs) // S_]
             return accs
 
+        half = [0]
+
+        def prep(blk):
+            """Whiten a freshly dedispersed block into the next half of the
+            prepared slots; returns its first slot (None: nothing to prepare)."""
+            nonlocal processed
+            if blk is None or blk[3] is None:
+                return None
+            j_, _, _, (k_, buf_, ready_, start_) = blk
+            b0_, b1_ = blocks[j_][:2]
+            e_ = self.engine
+            first = half[0] * e_.max_prepare
+            half[0] ^= 1
+            ready_.wait(e_.stream)
+            dd_events.append((start_, ready_))
+            with lock:
+                if 0 <= fault_after < processed + (b1_ - b0_):
+                    raise RuntimeError(f"fault injection: rank {self.ctx.rank} aborting after {processed} DM trials")
+                processed += b1_ - b0_
+            e_.prepare(buf_.data_ptr(), self.row_stride, self.geom.out_nsamps, b1_ - b0_, first)
+            ev = _C.GpuEvent()
+            ev.record(e_.stream)
+            freed[k_] = [ev]  # the dedispersion buffer is read by the whitening alone
+            return first
+
+        cur_first = prep(cur) if pipelined else None
+        while pipelined and cur is not None:
+            j, ck, resumed, inflight = cur
+            d0, d1 = blocks[j][:2]
+            raw = len(blocks[j]) > 2 and blocks[j][3] > 1
+            self.blocks_done.append(j)
+            if resumed is not None:
+                if prev is not None:
+                    done = finalize(prev)
+                    pj = prev[0]
+                    prev = None
+                    yield pj, done
+                yield j, resumed
+                ntrials += sum(len(trials_of(d, blocks[j])) for d in range(d0, d1))
+                if progress is not None:
+                    progress(d1 - d0)
+                cur = pull()
+                cur_first = prep(cur)
+                continue
+            e = self.engine
+            nxt = pull()  # its dedispersion overlaps this block's search
+            jobs = [(cur_first + i, self.dm_list[d], d, trials_of(d, blocks[j]), raw)
+                    for i, d in enumerate(range(d0, d1))]
+            def fail_closing(extra=None):
+                # the blocks searched whole are collected and spilled before a
+                # failure propagates, so a resume does not redo them
+                for blk in (prev, extra):
+                    if blk is not None:
+                        try:
+                            finalize(blk)
+                        except Exception:  # the original failure is the one to report
+                            pass
+
+            try:
+                h = e.search_launch(jobs)
+            except BaseException:
+                fail_closing()
+                raise
+            perr = None
+            try:
+                nxt_first = prep(nxt)  # behind this block's first batches on the engine's stream
+            except BaseException as x:  # (this block is still finished and spilled first)
+                perr = x
+            try:
+                e.search_finish(h)
+            except BaseException:
+                fail_closing()
+                raise
+            if perr is not None:
+                fail_closing((j, ck, d0, d1, [(e, jobs, h)]))
+                raise perr
+            for (_, _, _, accs, _) in jobs:
+                ntrials += len(accs)
+                if progress is not None:
+                    progress(1)
+            done = finalize(prev) if prev is not None else None
+            pj = prev[0] if prev is not None else -1
+            prev = (j, ck, d0, d1, [(e, jobs, h)])
+            cur, cur_first = nxt, nxt_first
+            if done is not None:
+                yield pj, done
         while cur is not None:
             j, ck, resumed, inflight = cur
             d0, d1 = blocks[j][:2]

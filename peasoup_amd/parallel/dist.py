@@ -171,6 +171,38 @@ def peer_failure() -> Optional[str]:
     return None
 
 
+def _peer_aware(fn):
+    """A collective that breaks because a peer exited (gloo: "connection
+    closed by peer") reports the peer's published failure, as the watchdog
+    would a moment later, instead of the broken transport: the peer's record
+    is waited for a few heartbeats before the original error is re-raised."""
+    import functools
+
+    @functools.wraps(fn)
+    def wrapped(*args, **kwargs):
+        try:
+            return fn(*args, **kwargs)
+        except Exception:
+            ctx = _CTX
+            if ctx is None or not ctx.distributed:
+                raise
+            period = float(os.environ.get("PSOUP_HEARTBEAT_S", "1.0"))
+            deadline = time.monotonic() + max(1.0, 4 * period)
+            while time.monotonic() < deadline:
+                msg = peer_failure()
+                if msg is not None:
+                    if _WATCHDOG is not None:
+                        _WATCHDOG.stop.set()
+                        _WATCHDOG._abort(f"peer failure: {msg}")
+                    sys.stderr.write(f"[rank {ctx.rank}] aborting: peer failure: {msg}\n")
+                    sys.stderr.flush()
+                    os._exit(3)
+                time.sleep(0.05)
+            raise
+
+    return wrapped
+
+
 def init(backend: Optional[str] = None, timeout_s: Optional[float] = None) -> DistContext:
     """Initialise (or return) the process group from torchrun-style env vars.
 
@@ -250,6 +282,7 @@ def shutdown() -> None:
     _CTX = None
 
 
+@_peer_aware
 def barrier() -> None:
     ctx = context()
     if ctx.distributed:
@@ -263,6 +296,7 @@ def _comm_device(ctx: DistContext) -> torch.device:
     return ctx.device if ctx.backend == "nccl" else torch.device("cpu")
 
 
+@_peer_aware
 def broadcast_bytes(buf: Optional[torch.Tensor], nbytes: int, src: int = 0) -> torch.Tensor:
     """Broadcast a uint8 buffer of ``nbytes`` from ``src`` (RCCL over xGMI on GPUs).
 
@@ -289,6 +323,7 @@ def broadcast_bytes(buf: Optional[torch.Tensor], nbytes: int, src: int = 0) -> t
     return buf
 
 
+@_peer_aware
 def gather_bytes(payload: bytes, dst: Optional[int] = 0) -> Optional[List[bytes]]:
     """Variable-length gather of byte strings (all_gather of sizes, then of a
     padded uint8 tensor).  Returns the list on ``dst`` (all ranks if dst is
@@ -312,6 +347,7 @@ def gather_bytes(payload: bytes, dst: Optional[int] = 0) -> Optional[List[bytes]
     return [bytes(o[:s].cpu().numpy().tobytes()) for o, s in zip(outs, sizes_i)]
 
 
+@_peer_aware
 def gather_buffers(payload: torch.Tensor, dst: int = 0, timing: Optional[dict] = None) -> Optional[List[torch.Tensor]]:
     """Variable-length gather of host uint8 tensors to ``dst`` only (sizes
     all-gathered, then one padded ``dist.gather``; RCCL on GPUs): the list of
@@ -342,6 +378,7 @@ def gather_buffers(payload: torch.Tensor, dst: int = 0, timing: Optional[dict] =
     return [o[:s].cpu() for o, s in zip(outs, sizes_i)]
 
 
+@_peer_aware
 def broadcast_object_bytes(payload: Optional[bytes], src: int = 0) -> bytes:
     """Broadcast a byte string of unknown length from ``src``."""
     ctx = context()
@@ -358,6 +395,7 @@ def broadcast_object_bytes(payload: Optional[bytes], src: int = 0) -> bytes:
     return bytes(buf[:size].cpu().numpy().tobytes())
 
 
+@_peer_aware
 def all_reduce_sum(t: torch.Tensor) -> torch.Tensor:
     """In-place sum across ranks (RCCL ring/tree all-reduce over xGMI)."""
     ctx = context()
@@ -371,6 +409,7 @@ def all_reduce_sum(t: torch.Tensor) -> torch.Tensor:
     return t
 
 
+@_peer_aware
 def all_reduce_max_float(x: float) -> float:
     ctx = context()
     if not ctx.distributed:
