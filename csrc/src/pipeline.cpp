@@ -200,7 +200,14 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   sh.setup = &setup;
   sh.fb = &fb;
   sh.ndm = static_cast<int>(setup.dm_list.size());
-  sh.chunk = std::max(1, std::min(32, sh.ndm / (4 * ngpu) + 1));
+  // DMs per chunk: 32, or 64 for lists of at least 8 x 64 DMs per GPU (an
+  // engine's chunk ends with a wait for its last batch and the peaks' host
+  // processing before the next chunk is issued: fewer, larger chunks leave
+  // the GPU idle less often -- as the Python driver's static blocks); the
+  // PSOUP_CHUNK_DMS environment variable overrides
+  int cmax = sh.ndm / ngpu >= 8 * 64 ? 64 : 32;
+  if (const char* e = std::getenv("PSOUP_CHUNK_DMS")) cmax = std::max(1, std::atoi(e));
+  sh.chunk = std::max(1, std::min(cmax, sh.ndm / (4 * ngpu) + 1));
   sh.dedisp_s.assign(static_cast<size_t>(ngpu), 0.0);
   sh.dev_stats.assign(static_cast<size_t>(ngpu), {});
   sh.search_s.assign(static_cast<size_t>(ngpu), 0.0);
