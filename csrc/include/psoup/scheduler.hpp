@@ -24,7 +24,15 @@
 //   using Token = ...;  // what issue() hands to collect() (default-constructible)
 //   void bind(int dev);                         // first call of every scheduler thread (device binding)
 //   void prepare(int dev, int slot, Chunk& c);  // fills c.resumed (and c.items when resumed)
-//   Token issue(int dev, int engine, int slot, const Chunk& c);  // not called for resumed chunks
+//   Token issue(int dev, int engine, int slot, const Chunk& c,   // not called for resumed chunks
+//               int next_slot, const std::function<const Chunk*()>& next);
+//       next(): waits until the feeder has published the following chunk
+//       and returns it (nullptr: there is none, it is resumed, or the run
+//       aborts).  Its slot stays valid until this engine finalizes it, so
+//       issue() may start on it (whiten it ahead).  The wait cannot deadlock:
+//       that chunk needs the slot of chunk g - 2, which every engine has
+//       finalized once it is issuing chunk g - 1 or later, so the slowest
+//       engine's wait is always satisfiable.
 //   void collect(int dev, int engine, Token& t, std::vector<Item>& out);
 //   void handover(int dev, int slot, Chunk& c);  // c.items: every engine's results
 //   void engine_exit(int dev, int engine);       // an engine thread's last call (not after a failure)
@@ -65,7 +73,7 @@ struct SchedFns {
   using Chunk = SchedChunk<Item>;
   std::function<void(int)> bind = [](int) {};
   std::function<void(int, int, Chunk&)> prepare;
-  std::function<Token(int, int, int, const Chunk&)> issue;
+  std::function<Token(int, int, int, const Chunk&, int, const std::function<const Chunk*()>&)> issue;
   std::function<void(int, int, Token&, std::vector<Item>&)> collect;
   std::function<void(int, int, Chunk&)> handover;
   std::function<void(int, int)> engine_exit = [](int, int) {};
@@ -205,8 +213,17 @@ class ChunkScheduler {
         cur.slot = static_cast<int>(g % kSchedSlots);
         const Chunk& c = dv.pub[cur.slot];
         if (!c.resumed) {
+          // the next chunk, once the feeder has published it: its slot is
+          // not refilled before this engine has finalized it
+          const int ns = static_cast<int>((g + 1) % kSchedSlots);
+          const std::function<const Chunk*()> nx = [&, g, ns]() -> const Chunk* {
+            std::unique_lock<std::mutex> lk(dv.mu);
+            dv.cv.wait(lk, [&] { return dv.published > g + 1 || dv.done || abort_.load(); });
+            if (abort_.load() || dv.published <= g + 1 || dv.pub[ns].resumed) return nullptr;
+            return &dv.pub[ns];
+          };
           try {
-            cur.token = ops_.issue(dev, eng, cur.slot, c);
+            cur.token = ops_.issue(dev, eng, cur.slot, c, ns, nx);
           } catch (...) {
             // the previous chunk was issued whole: finalize it (its checkpoint
             // spill) before the failure propagates, so a resume skips it

@@ -863,6 +863,8 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     // whitening batch: up to 3 GB of per-trial whitening state (>= 1 trial)
     const uint64_t per = wh_->batch_bytes_per_trial() + n_ * 4 + (p_.fft_mode == 2 ? n_ * 4 + 4096 : 0);
     max_prep_ = per ? static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(64, (3ull << 30) / per))) : 1;
+    // PSOUP_MAX_PREPARE lowers it (tests: chunks of several whitening groups)
+    if (const char* e = std::getenv("PSOUP_MAX_PREPARE")) max_prep_ = std::clamp(std::atoi(e), 1, max_prep_);
   }
   tim_.resize(n_);
   wstats_.resize(8 * static_cast<uint64_t>(max_prep_));  // two halves of prepared slots

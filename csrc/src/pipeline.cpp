@@ -15,6 +15,7 @@
 #include <mutex>
 #include <sstream>
 #include <thread>
+#include <tuple>
 
 #include "psoup/checkpoint.hpp"
 #include "psoup/output.hpp"
@@ -240,6 +241,10 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   }
   res.performance["engines_per_gpu"] = neng;
   setup.search.engines_per_device = neng;  // the auto batch budget is shared among them
+  // block pipeline (ops.issue below): two halves of prepared slots per engine
+  const char* pipe_env = std::getenv("PSOUP_BLOCK_PIPELINE");
+  const bool pipelined = pipe_env == nullptr || std::atoi(pipe_env) != 0;
+  res.performance["block_pipeline"] = pipelined ? 1 : 0;
 
   // phase 1: resident filterbank per device: one host upload to the first
   // device and a chunk-pipelined device-to-device fan-out to the others
@@ -282,7 +287,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
             if (e > 0) ds.estreams.push_back(std::make_unique<Stream>());
             ds.engines.push_back(std::make_unique<SearchEngine>(
                 setup.search, e > 0 ? ds.estreams.back()->get() : ds.stream->get()));
-            ds.engines.back()->reserve(ds.engines.back()->max_prepare(), 0);
+            ds.engines.back()->reserve(ds.engines.back()->max_prepare(), 0, pipelined);
           }
           const double t_eng = wl.get_time();
           if (args.npdmp > 0 && prev_power_of_two(geom.out_nsamps) >= 1024) {
@@ -336,6 +341,22 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
   res.performance["setup_engines_host_s"] = setup_eng;
   res.performance["setup_fold_host_s"] = setup_fold;
   t_search.start();
+  // PSOUP_SCHED_TRACE=<file>: the scheduler's host events as CSV (ms, thread,
+  // event, chunk d0) -- where the feeder and the engines wait
+  struct SchedTrace {
+    std::mutex mu;
+    std::vector<std::tuple<double, int, const char*, int>> ev;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    bool on = false;
+    void add(int who, const char* what, int d0) {
+      if (!on) return;
+      const double t = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      std::lock_guard<std::mutex> lk(mu);
+      ev.emplace_back(t, who, what, d0);
+    }
+  } strace;
+  const char* strace_path = std::getenv("PSOUP_SCHED_TRACE");
+  strace.on = strace_path != nullptr;
   // phase 2, per device: a feeder thread dedisperses DM chunks (one ahead,
   // double-buffered, on its own stream) and publishes them; each of the
   // device's neng engine threads searches every neng-th DM row of each chunk
@@ -355,6 +376,15 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     const uint8_t* rows[kSchedSlots] = {};  // the slot's dedispersed rows (row d at rows + (d - d0) * rstride)
     double dd_ms = 0.0;
     std::vector<Stopwatch> search_w;  // per engine
+    // per engine: the next chunk's first rows whitened ahead (into the other
+    // half of the prepared slots while this chunk's last batches run)
+    struct Ahead {
+      int d0 = -1;  // the chunk they belong to (-1: none)
+      int first = 0;
+      int half = 0;  // the half the next prepare writes
+      std::exception_ptr err;  // a failure whitening ahead, reported by the next issue
+    };
+    std::vector<Ahead> ahead;
   };
   std::vector<std::unique_ptr<DevSched>> scheds;
   const uint64_t rstride = Dedisperser::row_stride(geom.out_nsamps);
@@ -391,6 +421,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     }
     if (keep) kept[static_cast<size_t>(d)] = std::make_unique<DeviceBuffer<uint8_t>>(rstride * static_cast<uint64_t>(sh.ndm));
     sc->search_w.resize(static_cast<size_t>(neng));
+    sc->ahead.resize(static_cast<size_t>(neng));
     sh.dev_stats[static_cast<size_t>(d)]["kept_trials"] = keep ? 1.0 : 0.0;
     scheds.push_back(std::move(sc));
   }
@@ -414,6 +445,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
       log_info("checkpoint spill " + ck + " is " + spill_status_name(st) + "; recomputing DMs [" +
                std::to_string(p.d0) + "," + std::to_string(p.d1) + ")");
     p.items.clear();
+    strace.add(-1 - dev, "prep0", p.d0);
     uint8_t* rows = keep ? kept[static_cast<size_t>(dev)]->data() + static_cast<uint64_t>(p.d0) * rstride
                          : sc.trials[k]->data();
     if (sc.used[k] && !keep)
@@ -423,41 +455,102 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     sc.ready[k].record(dst);
     sc.used[k] = true;
     sc.rows[k] = rows;
+    strace.add(-1 - dev, "prep1", p.d0);
     if (keep)
       for (int d = p.d0; d < p.d1; ++d) row_owner[static_cast<size_t>(d)] = dev;
   };
   // A chunk's searches are issued (search_prepared_many_async) and the
   // previous chunk is collected only after them, so its acceleration
   // distillation on the engine's host workers overlaps this chunk's GPU work
-  // (the Python driver's RankSearcher does the same).
-  ops.issue = [&](int dev, int slot, int k, const Chunk& p) {
+  // (the Python driver's RankSearcher does the same).  Block pipeline: the
+  // last group of a chunk is issued in two halves (search_launch /
+  // search_finish) with the next chunk's first rows -- when the feeder has
+  // published it -- whitened in between into the other half of the prepared
+  // slots, so that whitening runs behind this chunk's first batches instead
+  // of after its last peaks were processed (Python: RankSearcher.search_iter's
+  // prep; PSOUP_BLOCK_PIPELINE=0 turns it off in both).
+  ops.issue = [&](int dev, int slot, int k, const Chunk& p, int kn,
+                  const std::function<const Chunk*()>& peek_next) {
     DevSched& sc = *scheds[static_cast<size_t>(dev)];
+    DevSched::Ahead& ah = sc.ahead[static_cast<size_t>(slot)];
+    if (ah.err) {  // whitening this chunk ahead failed (the previous chunk was finished first)
+      std::exception_ptr e = ah.err;
+      ah.err = nullptr;
+      std::rethrow_exception(e);
+    }
     SearchEngine& engine = *devs[static_cast<size_t>(dev)].engines[static_cast<size_t>(slot)];
     hipStream_t st = engine.stream();
     Stopwatch& ws = sc.search_w[static_cast<size_t>(slot)];
-    std::vector<Pending> pend;
-    PSOUP_HIP_CHECK(hipStreamWaitEvent(st, sc.ready[k].get(), 0));
-    ws.start();
-    std::vector<int> rows;
-    for (int d = p.d0 + slot; d < p.d1; d += neng) rows.push_back(d);
-    for (size_t r0 = 0; r0 < rows.size(); r0 += static_cast<size_t>(engine.max_prepare())) {
-      const int cnt = static_cast<int>(std::min(rows.size() - r0, static_cast<size_t>(engine.max_prepare())));
+    const int mp = engine.max_prepare();
+    const int who = dev * 64 + slot;
+    strace.add(who, "issue0", p.d0);
+    auto rows_of = [&](const Chunk& c) {
+      std::vector<int> r;
+      for (int d = c.d0 + slot; d < c.d1; d += neng) r.push_back(d);
+      return r;
+    };
+    // whiten rows rr[r0, r0 + cnt) of chunk c (slot kk) into the next half
+    auto whiten = [&](int kk, const Chunk& c, const std::vector<int>& rr, size_t r0, int cnt) {
       const int before = sc.processed.fetch_add(cnt);
       if (args.fault_after_dms >= 0 && before + cnt > args.fault_after_dms)
         PSOUP_THROW("fault injection: device " << dev << " aborting after " << before << " DM trials");
-      engine.prepare(sc.rows[k] + static_cast<uint64_t>(rows[r0] - p.d0) * rstride,
-                     static_cast<uint64_t>(neng) * rstride, geom.out_nsamps, cnt);
+      const int first = ah.half * mp;
+      engine.prepare(sc.rows[kk] + static_cast<uint64_t>(rr[r0] - c.d0) * rstride,
+                     static_cast<uint64_t>(neng) * rstride, geom.out_nsamps, cnt, first);
+      if (pipelined) ah.half ^= 1;  // (else every group is whitened into the first half)
+      return first;
+    };
+    std::vector<Pending> pend;
+    PSOUP_HIP_CHECK(hipStreamWaitEvent(st, sc.ready[k].get(), 0));
+    ws.start();
+    const std::vector<int> rows = rows_of(p);
+    for (size_t r0 = 0; r0 < rows.size(); r0 += static_cast<size_t>(mp)) {
+      const int cnt = static_cast<int>(std::min(rows.size() - r0, static_cast<size_t>(mp)));
+      int first;
+      if (r0 == 0 && ah.d0 == p.d0) {
+        first = ah.first;  // whitened ahead, during the previous chunk
+      } else {
+        first = whiten(k, p, rows, r0, cnt);
+      }
+      ah.d0 = -1;
       std::vector<SearchEngine::Job> jobs;
       for (int i = 0; i < cnt; ++i) {
         const int d = rows[r0 + static_cast<size_t>(i)];
         const float dm = setup.dm_list[static_cast<size_t>(d)];
-        jobs.push_back(SearchEngine::Job{i, dm, d, setup.accel_plan.generate(dm)});
+        jobs.push_back(SearchEngine::Job{first + i, dm, d, setup.accel_plan.generate(dm)});
         log_verbose("Searching " + std::to_string(jobs.back().accs.size()) + " acceleration trials for DM " +
                     std::to_string(dm));
         sh.accel_trials += jobs.back().accs.size();
       }
-      // one flat trial list over these DMs (batches span DM boundaries)
-      pend.push_back(engine.search_prepared_many_async(jobs));
+      if (!pipelined || r0 + static_cast<size_t>(mp) < rows.size()) {
+        // one flat trial list over these DMs (batches span DM boundaries)
+        pend.push_back(engine.search_prepared_many_async(jobs));
+        continue;
+      }
+      strace.add(who, "launch0", p.d0);
+      auto h = engine.search_launch(jobs);
+      try {
+        // (waits for the feeder to publish it: this chunk's first batches
+        // are already queued on the GPU)
+        strace.add(who, "peek0", p.d0);
+        const Chunk* next = peek_next();
+        strace.add(who, "peek1", next != nullptr ? next->d0 : -1);
+        const std::vector<int> nrows = next != nullptr ? rows_of(*next) : std::vector<int>();
+        if (!nrows.empty()) {
+          PSOUP_HIP_CHECK(hipStreamWaitEvent(st, sc.ready[kn].get(), 0));
+          ah.first = whiten(kn, *next, nrows, 0, static_cast<int>(std::min(nrows.size(), static_cast<size_t>(mp))));
+          ah.d0 = next->d0;
+          strace.add(who, "ahead1", next->d0);
+        }
+      } catch (...) {
+        // this chunk is still finished (and, once collected, checkpointed)
+        // before the failure is reported, by the next chunk's issue
+        ah.err = std::current_exception();
+        ah.d0 = -1;
+      }
+      engine.search_finish(h);
+      strace.add(who, "finish1", p.d0);
+      pend.push_back(h);
     }
     ws.stop();
     sc.freed[k][static_cast<size_t>(slot)]->record(st);
@@ -468,9 +561,11 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     SearchEngine& engine = *devs[static_cast<size_t>(dev)].engines[static_cast<size_t>(slot)];
     Stopwatch& ws = sc.search_w[static_cast<size_t>(slot)];
     ws.start();
+    strace.add(dev * 64 + slot, "coll0", -1);
     for (auto& h : pend)
       for (auto& c : engine.collect(h))
         for (auto& x : c) out.push_back(std::move(x));
+    strace.add(dev * 64 + slot, "coll1", -1);
     ws.stop();
   };
   ops.handover = [&](int dev, int k, Chunk& p) {
@@ -491,6 +586,7 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
       if (need > sh.cands.capacity()) sh.cands.reserve(std::max(need, 2 * sh.cands.capacity()));
       for (auto& x : p.items) sh.cands.push_back(std::move(x));
     }
+    strace.add(-1 - dev, "hand1", p.d0);
     const int done = sh.done_dms.fetch_add(p.d1 - p.d0) + (p.d1 - p.d0);
     if (sh.progress) sh.progress->set(static_cast<double>(done) / sh.ndm);
   };
@@ -524,6 +620,12 @@ PipelineResult run_pipeline(const CmdLineOptions& args) {
     } catch (...) {
       sh.error = std::current_exception();
     }
+  }
+  if (strace.on) {
+    std::ofstream f(strace_path);
+    f << "# t0_ns " << std::chrono::duration_cast<std::chrono::nanoseconds>(strace.t0.time_since_epoch()).count()
+      << " (steady_clock)\nms,thread,event,d0\n";
+    for (const auto& [t, who, what, d0] : strace.ev) f << t << ',' << who << ',' << what << ',' << d0 << '\n';
   }
   for (int d = 0; d < ngpu; ++d) {
     PSOUP_HIP_CHECK(hipSetDevice(hip_dev(d)));

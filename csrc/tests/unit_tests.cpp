@@ -305,7 +305,7 @@ struct FakeRun {
       sl[1] = c.d1;
       sl[2]++;
     };
-    ops.issue = [&](int dev, int eng, int k, const Chunk& c) {
+    ops.issue = [&](int dev, int eng, int k, const Chunk& c, int kn, const std::function<const Chunk*()>& peek) {
       const auto& sl = slot_of[static_cast<size_t>(dev) * kSchedSlots + k];
       if (sl[0] != c.d0 || sl[1] != c.d1) throw std::runtime_error("slot refilled under a reading engine");
       std::vector<int> mine;
@@ -313,6 +313,16 @@ struct FakeRun {
       if (fault_after >= 0 && issued.fetch_add(static_cast<int>(mine.size())) > fault_after)
         throw std::runtime_error("fault injection");
       nap(200);
+      const Chunk* next = peek();
+      if (next != nullptr) {
+        // "whiten the next chunk ahead": its slot holds it, and keeps it
+        // while this engine reads it
+        const auto& sn = slot_of[static_cast<size_t>(dev) * kSchedSlots + kn];
+        if (next->resumed || next->d0 <= c.d0 || sn[0] != next->d0 || sn[1] != next->d1)
+          throw std::runtime_error("look-ahead chunk is not the published next chunk");
+        nap(100);
+        if (sn[0] != next->d0 || sn[1] != next->d1) throw std::runtime_error("slot refilled under a reading engine");
+      }
       return mine;
     };
     ops.collect = [&](int, int, std::vector<int>& t, std::vector<int>& out) {

@@ -271,6 +271,28 @@ def test_engines_per_gpu_do_not_change_results(tmp_path):
     assert outs[2] == outs[3]
 
 
+def test_native_block_pipeline_does_not_change_results(tmp_path):
+    """bin/peasoup's block pipeline (each chunk's last whitening group searched
+    in two halves, with the next chunk's first rows whitened in between into
+    the other half of the prepared slots) writes the candidate file of the
+    unpipelined run: 1 and 3 engines, chunks of one and of several whitening
+    groups (PSOUP_MAX_PREPARE)."""
+    exe = os.path.join(REPO, "bin", "peasoup")
+    outs = {}
+    for pipe, eng, maxp in (("0", "1", "64"), ("1", "1", "64"), ("1", "1", "3"), ("1", "3", "2"), ("0", "3", "2")):
+        d = tmp_path / f"p{pipe}e{eng}m{maxp}"
+        env = dict(os.environ, PSOUP_BLOCK_PIPELINE=pipe, PSOUP_CHUNK_DMS="7", PSOUP_MAX_PREPARE=maxp)
+        r = subprocess.run([exe, "-i", TUTORIAL, "-o", str(d), "--engines_per_gpu", eng, "--trace_json",
+                            str(d) + ".json"] + GOLDEN_ARGS, capture_output=True, text=True, timeout=600, env=env)
+        assert r.returncode == 0, r.stderr
+        outs[(pipe, eng, maxp)] = (d / "candidates.peasoup").read_bytes()
+        import json
+
+        assert json.load(open(str(d) + ".json"))["performance"]["block_pipeline"] == int(pipe)
+    vals = list(outs.values())
+    assert all(v == vals[0] for v in vals[1:])
+
+
 def test_native_oversubscribed_device_workers_match_one(tmp_path):
     """PSOUP_OVERSUBSCRIBE=1: `peasoup -t 4` runs four device workers (feeder +
     engine threads, one filterbank upload fanned out device to device, DM queue, fold

@@ -246,7 +246,7 @@ def config45(a, npdmp, cfg, as_rank=None):
         tr = json.load(open(trace))
         return {"config": cfg, "desc": "native bin/peasoup, same data and options", "log2n": a.log2n,
                 "wall_s": round(wall, 3), "timers_s": {k: round(v, 3) for k, v in tr.get("timers_s", {}).items()},
-                "performance": tr.get("performance", {})}
+                "performance": tr.get("performance", {}), "argv": argv[1:]}
     t0 = time.perf_counter()
     res = run_search(args, as_rank=as_rank)
     wall = time.perf_counter() - t0
