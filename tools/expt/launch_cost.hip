@@ -28,6 +28,13 @@ __global__ void spin_kernel(unsigned long long ticks, int* out) {
   if (threadIdx.x == 0 && blockIdx.x == 0) out[0] = 1;
 }
 
+// memory-bound: streams n floats (HBM traffic while the host launches)
+__global__ void copy_kernel(const float4* __restrict__ a, float4* __restrict__ b, size_t n) {
+  for (size_t i = blockIdx.x * static_cast<size_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<size_t>(gridDim.x) * blockDim.x)
+    b[i] = a[i];
+}
+
 __global__ void tiny_kernel(int* out, int v) {
   if (threadIdx.x == 0) out[blockIdx.x] = v;
 }
@@ -121,6 +128,29 @@ int main() {
   CK(hipStreamWaitEvent(A, join, 0));
   hipLaunchKernelGGL(tiny_kernel, dim3(1), dim3(64), 0, A, buf, 0);
   report("join, one launch, then launches", launches(A, buf));
+  CK(hipDeviceSynchronize());
+  // every CU busy: many spinning workgroups on B, launches on A
+  hipLaunchKernelGGL(spin_kernel, dim3(8192), dim3(256), 0, B, ticks, buf);
+  report("all CUs busy with spinning workgroups on another stream", launches(A, buf));
+  CK(hipDeviceSynchronize());
+  // HBM saturated: 2 GiB copies on B (about 0.5 ms each), launches on A
+  const size_t n4 = (size_t(1) << 31) / 16;
+  float4 *x = nullptr, *y = nullptr;
+  CK(hipMalloc(&x, n4 * 16));
+  CK(hipMalloc(&y, n4 * 16));
+  for (int i = 0; i < 20; ++i) hipLaunchKernelGGL(copy_kernel, dim3(4096), dim3(256), 0, B, x, y, n4);
+  report("HBM-bound copies running on another stream", launches(A, buf));
+  for (int i = 0; i < 20; ++i) hipLaunchKernelGGL(copy_kernel, dim3(4096), dim3(256), 0, A, x, y, n4);
+  report("HBM-bound copies queued on the same stream", launches(A, buf));
+  CK(hipDeviceSynchronize());
+  // the engine's pattern: copies on A and B, then A joins B, then launches
+  for (int i = 0; i < 10; ++i) {
+    hipLaunchKernelGGL(copy_kernel, dim3(4096), dim3(256), 0, A, x, y, n4);
+    hipLaunchKernelGGL(copy_kernel, dim3(4096), dim3(256), 0, B, x, y, n4);
+  }
+  CK(hipEventRecord(join, B));
+  CK(hipStreamWaitEvent(A, join, 0));
+  report("HBM-bound copies on both, A joined B, then launches on A", launches(A, buf));
   CK(hipDeviceSynchronize());
   std::printf("DONE\n");
   return 0;
