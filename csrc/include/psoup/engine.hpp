@@ -229,9 +229,14 @@ class Whitener {
   // at d_trials + b*row_stride -> d_out + b*out_stride, its interbin stats
   // {mean, rms, std} at d_stats + 4b.  The forward and inverse transforms run
   // as one K = count four-step FFT each (rocFFT per trial without fft4).
-  void whiten_batch(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count, float* d_out,
+  // With pad_out (and its geometry pad_g), the whitened series may instead be
+  // written straight into pass A's padded row input, trial b at pad_out +
+  // b*pad_stride (fft4_c2r_post_pad); the return value says whether it was,
+  // in which case d_out is left unwritten.
+  bool whiten_batch(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count, float* d_out,
                     uint64_t out_stride, const uint32_t* d_zapmask, float* d_stats, float boundary5,
-                    float boundary25);
+                    float boundary25, float* pad_out = nullptr, const kern::Fft4Geom* pad_g = nullptr,
+                    uint64_t pad_stride = 0);
   // device bytes whiten_batch holds per trial of its largest batch
   uint64_t batch_bytes_per_trial() const;
   // Unnormalised N-point R2C (n/2+1 bins) and C2R, as rocFFT's.
@@ -384,6 +389,9 @@ class SearchEngine {
   float tobs() const { return tobs_; }
   // Debug access to the whitened series / interbin stats of the last searched trial.
   const float* whitened() const { return cur_tim_; }
+  // The current search's whitened series (n floats) into dst, from the
+  // padded input when prepare() wrote only that (blocking copy).
+  void copy_whitened(float* dst) const;
   const float* trial_stats() const { return cur_stats_; }
   const Whitener& whitener() const { return *wh_; }
 
@@ -467,6 +475,8 @@ class SearchEngine {
   int prepared_ = 0, max_prep_ = 1;
   const float* cur_tim_ = nullptr;  // trial being searched
   const float* cur_pad_ = nullptr;
+  bool pad_direct_ = true;   // whiten into the padded input directly (PSOUP_WHITEN_PAD_DIRECT=0: no)
+  bool pad_only_ = false;    // the last prepare() wrote the padded input only (tim_ unwritten)
   const float* cur_stats_ = nullptr;
   DeviceBuffer<uint32_t> zapmask_;
   bool zap_ = false;

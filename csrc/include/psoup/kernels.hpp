@@ -404,6 +404,13 @@ void fft4_c2r_pre(const float2* X, uint64_t M, float2* out, hipStream_t s, int c
 // x[2m] + i x[2m+1] = conj(Z[m]) (Z in layout L): the N-point unnormalised C2R.
 void fft4_c2r_post(const float2* Z, uint64_t M, const XLayoutArgs& L, float* x, hipStream_t s, int count = 1,
                    uint64_t zstride = 0, uint64_t ostride = 0);
+// The same inverse written straight into the search pass A's padded row input
+// (fft4_pad_input's layout: rows of 2 gs.n1 floats at pitch gs.inpitch, each
+// row's pad holding the next row's head, trial b at xpad + b * pstride).
+// Returns false, writing nothing, where the layouts do not allow it (the
+// strip layout, the external-row geometry, an untiled spectrum).
+bool fft4_c2r_post_pad(const float2* Z, uint64_t M, const XLayoutArgs& L, float* xpad, const Fft4Geom& gs,
+                       hipStream_t s, int count, uint64_t zstride, uint64_t pstride);
 // Mixed-radix (n = m p, p a power of two, m odd) transforms on the four-step
 // passes, for series whose length is not a power of two (the multi-beam
 // coincidencer transforms the whole DM-0 series): z[n1][n2] = s(n1 + m n2),

@@ -280,7 +280,9 @@ __device__ __forceinline__ void load_resampled(const float* __restrict__ in, con
     for (int e = 0; e < S; ++e) x[e] = e < hi ? w[e + 1] : (up ? w[e + 2] : w[e]);
   } else {
 #pragma unroll
-    for (int i = 0; i < S; ++i) x[i] = in[dev::accel_index_ii32(af, size, p0 + static_cast<uint32_t>(i), n - 1)];
+    // (from the padded copy: the engine may whiten straight into it and
+    // leave the unpadded series unwritten, fft4_c2r_post_pad)
+    for (int i = 0; i < S; ++i) x[i] = in_pad[addr(dev::accel_index_ii32(af, size, p0 + static_cast<uint32_t>(i), n - 1))];
   }
 }
 

@@ -402,6 +402,39 @@ __global__ void __launch_bounds__(256) c2r_post_tiled_kernel(const float2* __res
   }
 }
 
+// The same inverse written straight into the search pass A's padded input
+// (fft4_pad_input's row layout, which it replaces): natural float2 m = j R + r
+// (R = 2^log2_r float2 per row) goes to row j at r, a row's first `head`
+// float2 also to the previous row's pad (a padded row holds the next row's
+// head), and the last row's pad is zero -- the bytes fft4_pad_input writes.
+__global__ void __launch_bounds__(256) c2r_post_tiled_pad_kernel(const float2* __restrict__ Z, int log2_n2,
+                                                                 uint64_t n1, uint64_t zstride,
+                                                                 float2* __restrict__ xp, uint64_t pstride,
+                                                                 int log2_r, uint32_t pitch, uint32_t head,
+                                                                 uint32_t nrows) {
+  const uint64_t n2 = uint64_t(1) << log2_n2;
+  const float2* z = Z + static_cast<uint64_t>(blockIdx.z) * zstride;
+  float2* o = xp + static_cast<uint64_t>(blockIdx.z) * pstride;
+  const uint64_t g0 = static_cast<uint64_t>(blockIdx.y) * 8;
+  const uint64_t k2 = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+  const uint32_t rlen = 1u << log2_r, rmask = rlen - 1u;
+  auto put = [&](uint64_t m, float2 v) {
+    const uint32_t j = static_cast<uint32_t>(m >> log2_r), r = static_cast<uint32_t>(m) & rmask;
+    o[static_cast<uint64_t>(j) * pitch + r] = v;
+    if (r < head) {
+      if (j > 0) o[static_cast<uint64_t>(j - 1) * pitch + rlen + r] = v;
+      else o[static_cast<uint64_t>(nrows - 1) * pitch + rlen + r] = make_float2(0.f, 0.f);
+    }
+  };
+  const float4* sa = reinterpret_cast<const float4*>(z + (k2 >> 3) * (8 * n1) + (g0 >> 3) * 64 + (k2 & 7) * 8);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float4 a = sa[u];
+    put((g0 + 2 * u) * n2 + k2, make_float2(a.x, -a.y));
+    put((g0 + 2 * u + 1) * n2 + k2, make_float2(a.z, -a.w));
+  }
+}
+
 // The search's r2c + interbin + normalise on that tile.  Interbin
 // neighbours come by cross-lane shuffles: lane l's left neighbour X[k-1] is
 // lane l-1's ascending bin and its mirror neighbour X[M-(k+1)] is lane l+1's
@@ -1651,6 +1684,27 @@ void fft4_c2r_post(const float2* Z, uint64_t M, const XLayoutArgs& L, float* x, 
   const dim3 grid(dev::grid_for(M, 256, count > 1 ? 1024 : 4096), static_cast<unsigned>(count));
   c2r_post_kernel<<<grid, 256, 0, s>>>(Z, M, L, reinterpret_cast<float2*>(x), zstride, ostride / 2);
   post_launch_check("c2r_post_kernel", s);
+}
+
+bool fft4_c2r_post_pad(const float2* Z, uint64_t M, const XLayoutArgs& L, float* xpad, const Fft4Geom& gs,
+                       hipStream_t s, int count, uint64_t zstride, uint64_t pstride) {
+  const uint64_t n1 = L.n1, n2 = L.tiled ? (uint64_t(1) << L.log2_row) : 0;
+  const uint64_t rlen = static_cast<uint64_t>(gs.n1), rows = static_cast<uint64_t>(gs.n2);
+  const bool ok = L.tiled && n1 >= 8 && n2 >= 256 && n1 * n2 == M && (reinterpret_cast<uintptr_t>(Z) & 15) == 0 &&
+                  zstride % 2 == 0 && !fft4_strip_layout(gs) && !gs.rows_ext && rlen * rows == M &&
+                  (rlen & (rlen - 1)) == 0 && gs.inpitch % 2 == 0 && gs.inpitch >= 2 * rlen &&
+                  (gs.inpitch - 2 * rlen) / 2 <= rlen && rows * gs.inpitch <= gs.insize && pstride % 2 == 0 &&
+                  (reinterpret_cast<uintptr_t>(xpad) & 7) == 0 && gs.insize < (1ull << 32);
+  if (!ok) return false;
+  PSOUP_CHECK(count >= 1 && count <= 65535, "c2r_post_pad: bad count");
+  const dim3 grid(static_cast<unsigned>(n2 / 256), static_cast<unsigned>(n1 / 8), static_cast<unsigned>(count));
+  c2r_post_tiled_pad_kernel<<<grid, 256, 0, s>>>(Z, L.log2_row, n1, zstride, reinterpret_cast<float2*>(xpad),
+                                                 pstride / 2, __builtin_ctzll(rlen),
+                                                 static_cast<uint32_t>(gs.inpitch / 2),
+                                                 static_cast<uint32_t>((gs.inpitch - 2 * rlen) / 2),
+                                                 static_cast<uint32_t>(rows));
+  post_launch_check("c2r_post_tiled_pad_kernel", s);
+  return true;
 }
 
 void harmonic_set_flags(int flags) {

@@ -1105,11 +1105,8 @@ PYBIND11_MODULE(_C, m) {
       .def_property_readonly("rows_ext", &SearchEngine::rows_ext)
       .def_property_readonly("stream", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.stream()); })
       .def_property_readonly("tobs", &SearchEngine::tobs)
-      .def_property_readonly("whitened_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.whitened()); })
       .def_property_readonly("stats_address", [](const SearchEngine& e) { return reinterpret_cast<uintptr_t>(e.trial_stats()); })
-      .def("copy_whitened", [](const SearchEngine& e, uintptr_t dst) {
-        PSOUP_HIP_CHECK(hipMemcpy(P<void>(dst), e.whitened(), e.params().fft_size * sizeof(float), hipMemcpyDeviceToDevice));
-      })
+      .def("copy_whitened", [](const SearchEngine& e, uintptr_t dst) { e.copy_whitened(P<float>(dst)); })
       .def("copy_stats", [](const SearchEngine& e, uintptr_t dst) {
         PSOUP_HIP_CHECK(hipMemcpy(P<void>(dst), e.trial_stats(), 3 * sizeof(float), hipMemcpyDeviceToDevice));
       })

@@ -739,9 +739,9 @@ void Whitener::ensure_batch(int count) {
   bcap_ = count;
 }
 
-void Whitener::whiten_batch(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count, float* d_out,
+bool Whitener::whiten_batch(const uint8_t* d_trials, uint64_t row_stride, uint64_t nsamps, int count, float* d_out,
                             uint64_t out_stride, const uint32_t* d_zapmask, float* d_stats, float boundary5,
-                            float boundary25) {
+                            float boundary25, float* pad_out, const kern::Fft4Geom* pad_g, uint64_t pad_stride) {
   PSOUP_CHECK(count >= 1, "whiten_batch: empty batch");
   if (!f4_) {
     for (int b = 0; b < count; ++b) {
@@ -751,7 +751,7 @@ void Whitener::whiten_batch(const uint8_t* d_trials, uint64_t row_stride, uint64
       dered_stats(fser_.data(), d_zapmask, d_stats + 4 * b, boundary5, boundary25);
       inverse(fser_.data(), x);
     }
-    return;
+    return false;
   }
   ensure_batch(count);
   const uint64_t M = n_ / 2, nb = nbins();
@@ -814,7 +814,11 @@ void Whitener::whiten_batch(const uint8_t* d_trials, uint64_t row_stride, uint64
   }
   kern::fft4_resample_colpass(t, in4_.data(), n_, af0_.data(), count, y4_.data(), g, tab4_.data(), stream_);
   kern::fft4_rowpass(y4_.data(), x4_.data(), count, g4_, tab4_.data(), stream_);
+  if (pad_out && pad_g && kern::fft4_c2r_post_pad(x4_.data(), M, L, pad_out, *pad_g, stream_, count, g4_.xstride,
+                                                  pad_stride))
+    return true;
   kern::fft4_c2r_post(x4_.data(), M, L, d_out, stream_, count, g4_.xstride, out_stride);
+  return false;
 }
 
 std::vector<uint32_t> build_zap_mask(const std::vector<float>& freqs, const std::vector<float>& widths,
@@ -879,6 +883,7 @@ SearchEngine::SearchEngine(const SearchParams& p, hipStream_t stream)
     rows_ext_ = f4_.ok;
   }
   if (mode_ == 2 && !f4_.ok) mode_ = 1;
+  if (const char* pd = std::getenv("PSOUP_WHITEN_PAD_DIRECT")) pad_direct_ = std::atoi(pd) != 0;
   if (mode_ == 2) {
     auto tab = kern::fft4_tables(f4_);
     f4_tab_.resize(tab.size());
@@ -1415,11 +1420,25 @@ void SearchEngine::prepare(const uint8_t* d_trials, uint64_t row_stride, uint64_
   PSOUP_CHECK(tim_.size() >= n_ * end && (mode_ != 2 || f4_in_.size() >= f4_.insize * end),
               "prepare: the second half of the prepared slots needs reserve(count, trials, true)");
   float* tim = tim_.data() + static_cast<uint64_t>(first) * n_;
-  wh_->whiten_batch(d_trials, row_stride, nsamps, count, tim, n_, zap_ ? zapmask_.data() : nullptr,
-                    wstats_.data() + 4 * static_cast<uint64_t>(first), p_.boundary_5_freq, p_.boundary_25_freq);
-  if (mode_ == 2)
-    kern::fft4_pad_input(tim, n_, f4_in_.data() + static_cast<uint64_t>(first) * f4_.insize, f4_, stream_, count, n_);
+  float* pad = mode_ == 2 ? f4_in_.data() + static_cast<uint64_t>(first) * f4_.insize : nullptr;
+  // the padded rows of pass A's input written by the whitener's last kernel
+  // (no unpadded copy and no pad kernel) where the layouts allow it
+  pad_only_ = wh_->whiten_batch(d_trials, row_stride, nsamps, count, tim, n_, zap_ ? zapmask_.data() : nullptr,
+                                wstats_.data() + 4 * static_cast<uint64_t>(first), p_.boundary_5_freq,
+                                p_.boundary_25_freq, pad_direct_ ? pad : nullptr, &f4_, f4_.insize);
+  if (mode_ == 2 && !pad_only_) kern::fft4_pad_input(tim, n_, pad, f4_, stream_, count, n_);
   prepared_ = static_cast<int>(end);
+}
+
+void SearchEngine::copy_whitened(float* dst) const {
+  if (!pad_only_) {
+    PSOUP_HIP_CHECK(hipMemcpy(dst, cur_tim_, n_ * sizeof(float), hipMemcpyDeviceToDevice));
+    return;
+  }
+  // rows of 2 n1 floats at pitch inpitch
+  const uint64_t row = 2 * static_cast<uint64_t>(f4_.n1);
+  PSOUP_HIP_CHECK(hipMemcpy2D(dst, row * sizeof(float), cur_pad_, f4_.inpitch * sizeof(float), row * sizeof(float),
+                              static_cast<size_t>(f4_.n2), hipMemcpyDeviceToDevice));
 }
 
 CandidateList SearchEngine::search_trial(const uint8_t* d_trial, uint64_t nsamps, float dm, int dm_idx,

@@ -862,6 +862,43 @@ def test_whitening_direct_sources_equal_padded_path(C, log2n):
         assert out[f0 & ~WS][b].abs().max() > 0
 
 
+@pytest.mark.parametrize("log2n", [20, 21])
+def test_whitening_into_padded_input_equals_pad_kernel(C, monkeypatch, log2n):
+    """fft4_c2r_post_pad: the whitener's inverse writes pass A's padded row
+    input directly (no unpadded series, no pad kernel), and pass A's
+    off-band fallback reads the padded copy.  The whitened series and every
+    candidate of an accelerated search equal PSOUP_WHITEN_PAD_DIRECT=0's
+    (unpadded series + fft4_pad_input) bit for bit."""
+    rng = np.random.default_rng(log2n)
+    n, count = 1 << log2n, 3
+    nsamps = n - 700
+    rs = n + 64
+    t = np.arange(nsamps) * 64e-6
+    rows = np.zeros((count, rs), dtype=np.uint8)
+    for b in range(count):
+        x = rng.normal(128, 10, nsamps) + 30 * (((t / (0.0123 * (1 + 0.1 * b))) % 1.0) < 0.04)
+        rows[b, :nsamps] = np.clip(np.rint(x), 0, 255).astype(np.uint8)
+    d = torch.from_numpy(rows).to(dev)
+    p = C.SearchParams()
+    p.fft_size, p.tsamp, p.nharmonics = n, 64e-6, 3
+    s = torch.cuda.current_stream().cuda_stream
+    accs = list(np.linspace(-300, 300, 23))
+    key = lambda c: (c.dm_idx, c.freq, c.acc, c.nh, c.snr)  # noqa: E731
+    res = {}
+    for direct in ("0", "1"):
+        monkeypatch.setenv("PSOUP_WHITEN_PAD_DIRECT", direct)
+        e = C.SearchEngine(p, s)
+        e.prepare(d.data_ptr(), rs, nsamps, count)
+        many = e.search_prepared_many([(b, 5.0 + b, b, accs) for b in range(count)])
+        w = torch.empty(n, dtype=torch.float32, device=dev)
+        e.copy_whitened(w.data_ptr())  # the current search's first series
+        torch.cuda.synchronize()
+        res[direct] = ([sorted(map(key, many[b])) for b in range(count)], w)
+        del e
+    assert res["0"][0] == res["1"][0] and sum(len(c) for c in res["1"][0]) > 0
+    assert torch.equal(res["0"][1], res["1"][1]) and res["1"][1].abs().max() > 0
+
+
 def test_flat_multi_dm_batches_match_per_dm_search(C):
     """search_prepared_many: the trials of several DMs concatenated and cut
     into K-trial batches across DM boundaries (per-trial series index and
