@@ -267,6 +267,7 @@ class Whitener {
   // complex FFTs on the four-step passes + a length-mm_ combination
   // (kern::mixed_*), so no length needs rocFFT's runtime-compiled kernels
   bool mixed_ = false;
+  bool fused_stats_ = true;  // deredden + interbin stats in one pass (PSOUP_WHITEN_FUSED_STATS=0: two kernels)
   uint32_t mm_ = 1;
   uint64_t mp_ = 0;
   kern::Fft4Geom gm_;

@@ -188,6 +188,13 @@ void deredden_zap(float2* X, uint64_t nbins, const float* m5, uint64_t n5, const
 // partials + 2*npartials*b, stats at stats + 4*b
 void interbin_stats(const float2* X, uint64_t nbins, float* P, double* partials, int npartials, float* stats,
                     hipStream_t s, int batch = 1, uint64_t xstride = 0);
+// deredden_zap + interbin_stats (P == nullptr) in one pass, out of place:
+// item b's X (stride xstride) -> out (stride ostride), the statistics
+// bit-identical to the two-kernel sequence's.
+void deredden_zap_stats(const float2* X, float2* out, uint64_t nbins, const float* m5, uint64_t n5, const float* m25,
+                        uint64_t n25, const float* m125, uint64_t n125, int64_t pos5, int64_t pos25,
+                        const uint32_t* zapmask, double* partials, int npartials, float* stats, hipStream_t s,
+                        int batch, uint64_t xstride, uint64_t ostride, uint64_t mstride);
 
 // ------------------------------------------------------------- resampling ---
 // out[k][i] = in[clamp(rint(i + i*af_k*(i - n)))], af_k = acc_k*tsamp/(2c)

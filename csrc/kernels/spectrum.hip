@@ -157,6 +157,55 @@ __global__ void __launch_bounds__(256) interbin_moments_kernel(const float2* __r
   }
 }
 
+// deredden_zap and interbin_moments in one pass, out of place: item b's
+// spectrum X -> out (dereddened, zapped), with the interbin partial sums of
+// out over the same grid and loop order as interbin_moments_kernel (so the
+// statistics are bit-identical).  The left neighbour is dereddened again from
+// X rather than read back from out, which other workgroups write.
+__global__ void __launch_bounds__(256) deredden_zap_moments_kernel(
+    const float2* __restrict__ X, float2* __restrict__ out, uint64_t nbins, const float* __restrict__ m5, uint64_t n5,
+    float step5, const float* __restrict__ m25, uint64_t n25, float step25, const float* __restrict__ m125,
+    uint64_t n125, float step125, int64_t pos5, int64_t pos25, const uint32_t* __restrict__ zapmask, uint64_t xstride,
+    uint64_t ostride, uint64_t mstride, double* __restrict__ partials, int pstride) {
+  __shared__ double scratch[4];
+  X += blockIdx.y * xstride;
+  out += blockIdx.y * ostride;
+  m5 += blockIdx.y * mstride;
+  m25 += blockIdx.y * mstride;
+  m125 += blockIdx.y * mstride;
+  partials += static_cast<uint64_t>(blockIdx.y) * pstride;
+  auto dz = [&](uint64_t k) {  // deredden_zap_kernel's value of bin k
+    float2 x;
+    if (k < 5) {
+      x = make_float2(0.f, 0.f);
+    } else {
+      float med;
+      if (static_cast<int64_t>(k) >= pos25) med = stretch_at(m125, n125, step125, k);
+      else if (static_cast<int64_t>(k) >= pos5) med = stretch_at(m25, n25, step25, k);
+      else med = stretch_at(m5, n5, step5, k);
+      x = dev::cdiv_real(X[k], med);
+    }
+    if (zapmask && ((zapmask[k >> 5] >> (k & 31)) & 1u)) x = make_float2(1.f, 0.f);
+    return x;
+  };
+  double s = 0.0, s2 = 0.0;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = blockIdx.x * static_cast<uint64_t>(blockDim.x) + threadIdx.x; i < nbins; i += stride) {
+    const float2 x = dz(i);
+    out[i] = x;
+    const float2 xl = i > 0 ? dz(i - 1) : make_float2(0.f, 0.f);
+    const float v = dev::interbin(x, xl);
+    s += v;
+    s2 += static_cast<double>(v) * v;
+  }
+  s = dev::block_sum(s, scratch);
+  s2 = dev::block_sum(s2, scratch);
+  if (threadIdx.x == 0) {
+    partials[2 * blockIdx.x] = s;
+    partials[2 * blockIdx.x + 1] = s2;
+  }
+}
+
 float stretch_step(uint64_t in_count, uint64_t out_count) {
   if (out_count <= 1 || in_count == 0) return 0.f;
   return static_cast<float>(in_count - 1) / static_cast<float>(out_count - 1);
@@ -229,6 +278,22 @@ void interbin_stats(const float2* X, uint64_t nbins, float* P, double* partials,
   interbin_moments_kernel<<<dim3(gx, static_cast<unsigned>(batch)), 256, 0, s>>>(X, nbins, P, partials, xstride,
                                                                                  2 * npartials);
   post_launch_check("interbin_moments_kernel", s);
+  stats_finalize_kernel<<<static_cast<unsigned>(batch), 256, 0, s>>>(partials, static_cast<int>(gx), nbins, stats,
+                                                                      2 * npartials);
+  post_launch_check("stats_finalize_kernel", s);
+}
+
+void deredden_zap_stats(const float2* X, float2* out, uint64_t nbins, const float* m5, uint64_t n5, const float* m25,
+                        uint64_t n25, const float* m125, uint64_t n125, int64_t pos5, int64_t pos25,
+                        const uint32_t* zapmask, double* partials, int npartials, float* stats, hipStream_t s,
+                        int batch, uint64_t xstride, uint64_t ostride, uint64_t mstride) {
+  PSOUP_CHECK(n5 >= 1 && n25 >= 1 && n125 >= 1, "running median needs >= 125 bins");
+  PSOUP_CHECK(batch >= 1 && batch <= 65535 && X != out, "deredden_zap_stats: bad batch / in place");
+  const unsigned gx = dev::grid_for(nbins, 256, static_cast<unsigned>(npartials));  // as interbin_stats
+  deredden_zap_moments_kernel<<<dim3(gx, static_cast<unsigned>(batch)), 256, 0, s>>>(
+      X, out, nbins, m5, n5, stretch_step(n5, nbins), m25, n25, stretch_step(n25, nbins), m125, n125,
+      stretch_step(n125, nbins), pos5, pos25, zapmask, xstride, ostride, mstride, partials, 2 * npartials);
+  post_launch_check("deredden_zap_moments_kernel", s);
   stats_finalize_kernel<<<static_cast<unsigned>(batch), 256, 0, s>>>(partials, static_cast<int>(gx), nbins, stats,
                                                                       2 * npartials);
   post_launch_check("stats_finalize_kernel", s);

@@ -586,6 +586,7 @@ Whitener::Whitener(uint64_t n, float tsamp, hipStream_t stream, bool allow_fft4)
     // single-transform grids of both passes need n1/8 % 16 == 0 and n2/8 % 8 == 0
     f4_ = g4_.ok && g4_.n1 >= 128 && g4_.n2 >= 64;
   }
+  if (const char* fs = std::getenv("PSOUP_WHITEN_FUSED_STATS")) fused_stats_ = std::atoi(fs) != 0;
   fser_.resize(nb);
   m5_.resize(nb / 5);
   m25_.resize(std::max<uint64_t>(1, nb / 5 / 5));
@@ -796,20 +797,32 @@ bool Whitener::whiten_batch(const uint8_t* d_trials, uint64_t row_stride, uint64
     kern::median5(m25_.data(), n25, m125_.data(), stream_, count, ms, ms);
     const int64_t pos5 = static_cast<int64_t>(static_cast<int>(boundary5 / bin_width_));
     const int64_t pos25 = static_cast<int64_t>(static_cast<int>(boundary25 / bin_width_));
-    kern::deredden_zap(bspec_.data(), nb, m5_.data(), n5, m25_.data(), std::max<uint64_t>(1, n25), m125_.data(),
-                       std::max<uint64_t>(1, n125), pos5, pos25, d_zapmask, stream_, count, nb, ms);
-    kern::interbin_stats(bspec_.data(), nb, nullptr, partials_.data(), 1024, d_stats, stream_, count, nb);
+    PSOUP_CHECK(!fused_stats_ || g4_.xstride >= nb, "whiten_batch: X stride below the spectrum length");
+    if (fused_stats_) {
+      // one pass, out of place into x4_ (free after the r2c until the
+      // inverse's pass B; xstride >= nb): its statistics equal the two
+      // kernels' bit for bit
+      kern::deredden_zap_stats(bspec_.data(), x4_.data(), nb, m5_.data(), n5, m25_.data(),
+                               std::max<uint64_t>(1, n25), m125_.data(), std::max<uint64_t>(1, n125), pos5, pos25,
+                               d_zapmask, partials_.data(), 1024, d_stats, stream_, count, nb, g4_.xstride, ms);
+    } else {
+      kern::deredden_zap(bspec_.data(), nb, m5_.data(), n5, m25_.data(), std::max<uint64_t>(1, n25), m125_.data(),
+                         std::max<uint64_t>(1, n125), pos5, pos25, d_zapmask, stream_, count, nb, ms);
+      kern::interbin_stats(bspec_.data(), nb, nullptr, partials_.data(), 1024, d_stats, stream_, count, nb);
+    }
   }
   // inverse (direct: pass A applies the C2R pre-processing to the spectra as it reads them)
+  const float2* wspec = fused_stats_ ? x4_.data() : bspec_.data();
+  const uint64_t wstride = fused_stats_ ? g4_.xstride : nb;
   const float* t = reinterpret_cast<const float*>(tmp4_.data());
   g.in_tstride = n_;
   g.u8 = nullptr;
   g.f32_direct = g.strips_direct = false;
   if (direct) {
-    g.c2r = bspec_.data();
-    g.src_stride = nb;
+    g.c2r = wspec;
+    g.src_stride = wstride;
   } else {
-    kern::fft4_c2r_pre(bspec_.data(), M, tmp4_.data(), stream_, count, nb, M);
+    kern::fft4_c2r_pre(wspec, M, tmp4_.data(), stream_, count, wstride, M);
     kern::fft4_pad_input(t, n_, in4_.data(), g4_, stream_, count, n_);
   }
   kern::fft4_resample_colpass(t, in4_.data(), n_, af0_.data(), count, y4_.data(), g, tab4_.data(), stream_);

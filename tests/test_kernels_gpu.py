@@ -862,13 +862,16 @@ def test_whitening_direct_sources_equal_padded_path(C, log2n):
         assert out[f0 & ~WS][b].abs().max() > 0
 
 
-@pytest.mark.parametrize("log2n", [20, 21])
+@pytest.mark.parametrize("log2n", [20, 21, 23])
 def test_whitening_into_padded_input_equals_pad_kernel(C, monkeypatch, log2n):
     """fft4_c2r_post_pad: the whitener's inverse writes pass A's padded row
     input directly (no unpadded series, no pad kernel), and pass A's
-    off-band fallback reads the padded copy.  The whitened series and every
-    candidate of an accelerated search equal PSOUP_WHITEN_PAD_DIRECT=0's
-    (unpadded series + fft4_pad_input) bit for bit."""
+    off-band fallback reads the padded copy; deredden_zap_stats: dereddening
+    and the interbin statistics in one out-of-place pass.  The whitened
+    series and every candidate of an accelerated search equal those of the
+    two-kernel sequences (PSOUP_WHITEN_PAD_DIRECT=0,
+    PSOUP_WHITEN_FUSED_STATS=0) bit for bit (2^23: the strip layout keeps
+    the pad kernel)."""
     rng = np.random.default_rng(log2n)
     n, count = 1 << log2n, 3
     nsamps = n - 700
@@ -885,8 +888,9 @@ def test_whitening_into_padded_input_equals_pad_kernel(C, monkeypatch, log2n):
     accs = list(np.linspace(-300, 300, 23))
     key = lambda c: (c.dm_idx, c.freq, c.acc, c.nh, c.snr)  # noqa: E731
     res = {}
-    for direct in ("0", "1"):
-        monkeypatch.setenv("PSOUP_WHITEN_PAD_DIRECT", direct)
+    for direct in ("00", "10", "11"):
+        monkeypatch.setenv("PSOUP_WHITEN_PAD_DIRECT", direct[0])
+        monkeypatch.setenv("PSOUP_WHITEN_FUSED_STATS", direct[1])
         e = C.SearchEngine(p, s)
         e.prepare(d.data_ptr(), rs, nsamps, count)
         many = e.search_prepared_many([(b, 5.0 + b, b, accs) for b in range(count)])
@@ -895,8 +899,9 @@ def test_whitening_into_padded_input_equals_pad_kernel(C, monkeypatch, log2n):
         torch.cuda.synchronize()
         res[direct] = ([sorted(map(key, many[b])) for b in range(count)], w)
         del e
-    assert res["0"][0] == res["1"][0] and sum(len(c) for c in res["1"][0]) > 0
-    assert torch.equal(res["0"][1], res["1"][1]) and res["1"][1].abs().max() > 0
+    for v in ("10", "11"):
+        assert res["00"][0] == res[v][0] and sum(len(c) for c in res[v][0]) > 0, v
+        assert torch.equal(res["00"][1], res[v][1]) and res[v][1].abs().max() > 0, v
 
 
 def test_flat_multi_dm_batches_match_per_dm_search(C):
